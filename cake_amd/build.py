@@ -1,0 +1,124 @@
+"""Native build driver: HIP kernels (gfx950) and the C++ host runtime.
+
+Everything is compiled in-tree into ``cake_amd/lib/`` so the shared objects
+travel with the repository snapshot to the GPU box:
+
+* ``libcake_kernels.so`` — every ``csrc/kernels/*.hip`` file, ``hipcc
+  --offload-arch=gfx950``; plain C ABI (``extern "C" cake_*``) driven from
+  :mod:`cake_amd.ops.hip` through ctypes with torch's current HIP stream, so
+  the launches are capturable in hipGraphs.
+* ``libcake_runtime.so`` — ``csrc/runtime/*.cpp`` (topology parser, wire codec,
+  safetensors mmap reader/writer, framed TCP transport), C ABI.
+* ``cake-split-model`` — native executable (``csrc/tools/split_model.cpp``).
+
+Object files are cached under ``build/`` keyed on mtimes of the source and the
+shared headers, so re-running is cheap.
+
+Usage: ``python -m cake_amd.build [--force] [-j N]``
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+CSRC = PKG / "csrc"
+LIB = PKG / "lib"
+BUILD = PKG.parent / "build" / "native"
+ARCH = os.environ.get("CAKE_OFFLOAD_ARCH", "gfx950")
+
+HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+CXX = shutil.which("g++") or "c++"
+
+KERNEL_LIB = LIB / "libcake_kernels.so"
+RUNTIME_LIB = LIB / "libcake_runtime.so"
+SPLIT_TOOL = LIB / "cake-split-model"
+
+
+def _newer(src: Path, deps: list[Path], out: Path) -> bool:
+    if not out.exists():
+        return True
+    t = out.stat().st_mtime
+    return any(p.stat().st_mtime > t for p in [src, *deps] if p.exists())
+
+
+def _run(cmd: list[str]) -> None:
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"command failed ({r.returncode}): {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+
+
+def _compile_hip(src: Path, force: bool) -> Path:
+    out = BUILD / "kernels" / (src.stem + ".o")
+    out.parent.mkdir(parents=True, exist_ok=True)
+    headers = sorted((CSRC / "kernels").glob("*.h"))
+    if force or _newer(src, headers, out):
+        _run([HIPCC, "-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC",
+              "-Wno-unused-result", "-munsafe-fp-atomics", "-c", str(src), "-o", str(out)])
+    return out
+
+
+def _compile_cpp(src: Path, force: bool, extra: list[str] | None = None) -> Path:
+    out = BUILD / "runtime" / (src.stem + ".o")
+    out.parent.mkdir(parents=True, exist_ok=True)
+    headers = sorted((CSRC / "runtime").glob("*.h"))
+    if force or _newer(src, headers, out):
+        _run([CXX, "-O2", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
+              *(extra or []), "-c", str(src), "-o", str(out)])
+    return out
+
+
+def build_kernels(force: bool = False, jobs: int = 8) -> Path:
+    srcs = sorted((CSRC / "kernels").glob("*.hip"))
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(lambda s: _compile_hip(s, force), srcs))
+    LIB.mkdir(parents=True, exist_ok=True)
+    if force or any(_newer(o, [], KERNEL_LIB) for o in objs):
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs),
+              "-o", str(KERNEL_LIB)])
+    return KERNEL_LIB
+
+
+def build_runtime(force: bool = False, jobs: int = 8) -> Path | None:
+    rt_dir = CSRC / "runtime"
+    srcs = sorted(rt_dir.glob("*.cpp"))
+    if not srcs:
+        return None
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(lambda s: _compile_cpp(s, force), srcs))
+    LIB.mkdir(parents=True, exist_ok=True)
+    if force or any(_newer(o, [], RUNTIME_LIB) for o in objs):
+        _run([CXX, "-shared", "-fPIC", *map(str, objs), "-o", str(RUNTIME_LIB), "-lpthread"])
+    tool = CSRC / "tools" / "split_model.cpp"
+    if tool.exists():
+        if force or _newer(tool, [*objs], SPLIT_TOOL):
+            _run([CXX, "-O2", "-std=c++17", f"-I{rt_dir}", str(tool), *map(str, objs),
+                  "-o", str(SPLIT_TOOL), "-lpthread"])
+    return RUNTIME_LIB
+
+
+def build_all(force: bool = False, jobs: int = 8) -> None:
+    build_kernels(force, jobs)
+    build_runtime(force, jobs)
+
+
+def main(argv: list[str] | None = None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", "--jobs", type=int, default=min(8, os.cpu_count() or 4))
+    ap.add_argument("--only", choices=["kernels", "runtime"], default=None)
+    a = ap.parse_args(argv)
+    if a.only in (None, "kernels"):
+        print("built", build_kernels(a.force, a.jobs))
+    if a.only in (None, "runtime"):
+        print("built", build_runtime(a.force, a.jobs))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

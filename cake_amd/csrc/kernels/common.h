@@ -1,0 +1,104 @@
+// Shared device helpers for the cake_amd CDNA4 (gfx950) kernels.
+//
+// Conventions used by every kernel in this directory:
+//   * wave64: lane = threadIdx.x & 63, wave = threadIdx.x >> 6.
+//   * 16-bit storage types are carried as raw uint16 bit patterns (bf16 or f16,
+//     selected by the DT template parameter) and widened to f32 in registers.
+//     All accumulation is f32.
+//   * Every exported entry point is `extern "C"`, takes raw device pointers and a
+//     hipStream_t, and returns a hipError_t as int, so the launches are captured
+//     unchanged inside hipGraphs (the Python side passes torch's current stream).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define CAKE_API extern "C" __attribute__((visibility("default")))
+
+namespace cake {
+
+enum DType : int { kBF16 = 0, kF16 = 1, kF32 = 2 };
+
+__device__ __forceinline__ float bf16_to_f32(uint16_t h) {
+  return __uint_as_float(((uint32_t)h) << 16);
+}
+
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);  // NaN
+  u += 0x7fffu + ((u >> 16) & 1u);  // round to nearest even
+  return (uint16_t)(u >> 16);
+}
+
+__device__ __forceinline__ float f16_to_f32(uint16_t h) {
+  _Float16 v;
+  __builtin_memcpy(&v, &h, 2);
+  return (float)v;
+}
+
+__device__ __forceinline__ uint16_t f32_to_f16(float f) {
+  _Float16 v = (_Float16)f;
+  uint16_t h;
+  __builtin_memcpy(&h, &v, 2);
+  return h;
+}
+
+template <int DT>
+__device__ __forceinline__ float to_f32(uint16_t h) {
+  if constexpr (DT == kBF16) return bf16_to_f32(h);
+  else return f16_to_f32(h);
+}
+
+template <int DT>
+__device__ __forceinline__ uint16_t from_f32(float f) {
+  if constexpr (DT == kBF16) return f32_to_bf16(f);
+  else return f32_to_f16(f);
+}
+
+// Unpack 8 packed 16-bit values (one 16-byte load) into f32.
+template <int DT>
+__device__ __forceinline__ void unpack8(const uint4 v, float* o) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    o[2 * i] = to_f32<DT>((uint16_t)(w[i] & 0xffffu));
+    o[2 * i + 1] = to_f32<DT>((uint16_t)(w[i] >> 16));
+  }
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+  return v;
+}
+
+// Block-wide sum for blockDim.x <= 1024; `red` must hold >= 16 floats.
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nw = (blockDim.x + 63) >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) red[wave] = v;
+  __syncthreads();
+  float t = 0.f;
+  for (int i = 0; i < nw; ++i) t += red[i];
+  return t;
+}
+
+// Streaming (read-once) 16-byte load: weights in batch-1 decode are touched by
+// exactly one wave, so keep them from displacing reusable lines.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ld_nt16(const uint4* p) {
+  const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+__device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
+
+}  // namespace cake

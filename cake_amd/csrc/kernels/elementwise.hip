@@ -1,0 +1,169 @@
+// Row-wise and elementwise kernels: embedding gather, RMSNorm, RoPE + KV-cache
+// write for multi-token (prefill) steps, SwiGLU, residual add.
+//
+// Reference ops replaced:
+//   K01 embedding index_select   cake-core/src/models/llama3/llama.rs:74
+//   K02 RmsNorm                  cake-core/src/models/llama3/transformer.rs:60,68
+//   K05 rope (non-interleaved)   cake-core/src/models/llama3/attention.rs:25-35
+//   K06 kv cat                   cake-core/src/models/llama3/cache.rs:93-122
+//   K15 silu * up                cake-core/src/models/llama3/mlp.rs:16
+// Decode never uses these (the GEMV prologues/epilogues fuse them); prefill
+// runs GEMMs on MFMA and uses these for the glue.
+#include "common.h"
+
+namespace cake {
+
+template <int DT>
+__global__ void embed_kernel(const uint16_t* __restrict__ table, const int* __restrict__ tok,
+                             int H, float* __restrict__ out) {
+  const int t = blockIdx.x;
+  const uint16_t* row = table + (size_t)tok[t] * H;
+  float* o = out + (size_t)t * H;
+  for (int i = threadIdx.x * 8; i < H; i += blockDim.x * 8) {
+    float f[8];
+    unpack8<DT>(*reinterpret_cast<const uint4*>(row + i), f);
+    *reinterpret_cast<float4*>(o + i) = make_float4(f[0], f[1], f[2], f[3]);
+    *reinterpret_cast<float4*>(o + i + 4) = make_float4(f[4], f[5], f[6], f[7]);
+  }
+}
+
+// out[t] = x[t] * rsqrt(mean(x[t]^2) + eps) * w  (x f32, out 16-bit)
+template <int DT>
+__global__ __launch_bounds__(256) void rmsnorm_kernel(const float* __restrict__ x,
+                                                      const uint16_t* __restrict__ w,
+                                                      float eps, int H,
+                                                      uint16_t* __restrict__ out) {
+  __shared__ float red[16];
+  const float* xr = x + (size_t)blockIdx.x * H;
+  float ss = 0.f;
+  for (int i = threadIdx.x * 4; i < H; i += blockDim.x * 4) {
+    const float4 v = *reinterpret_cast<const float4*>(xr + i);
+    ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  }
+  ss = block_sum(ss, red);
+  const float r = rsqrtf(ss / (float)H + eps);
+  uint16_t* o = out + (size_t)blockIdx.x * H;
+  for (int i = threadIdx.x * 4; i < H; i += blockDim.x * 4) {
+    const float4 v = *reinterpret_cast<const float4*>(xr + i);
+    const uint2 wv = *reinterpret_cast<const uint2*>(w + i);
+    uint2 ov;
+    ov.x = (uint32_t)from_f32<DT>(v.x * r * to_f32<DT>((uint16_t)(wv.x & 0xffff))) |
+           ((uint32_t)from_f32<DT>(v.y * r * to_f32<DT>((uint16_t)(wv.x >> 16))) << 16);
+    ov.y = (uint32_t)from_f32<DT>(v.z * r * to_f32<DT>((uint16_t)(wv.y & 0xffff))) |
+           ((uint32_t)from_f32<DT>(v.w * r * to_f32<DT>((uint16_t)(wv.y >> 16))) << 16);
+    *reinterpret_cast<uint2*>(o + i) = ov;
+  }
+}
+
+// Prefill RoPE: q [T, nh*hd] roped in place; k roped and v copied into the
+// cache rows pos0+t of [nkv][S][hd].
+template <int DT>
+__global__ void rope_kv_kernel(uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
+                               const uint16_t* __restrict__ v, int nh, int nkv, int hd,
+                               const float* __restrict__ inv_freq, int pos0, int S,
+                               uint16_t* __restrict__ kc, uint16_t* __restrict__ vc) {
+  const int t = blockIdx.x, pos = pos0 + t, half = hd >> 1;
+  const int nq = nh * half, nk = nkv * half;
+  for (int p = threadIdx.x; p < nq + 2 * nk; p += blockDim.x) {
+    if (p < nq + nk) {
+      const bool isq = p < nq;
+      const int pp = isq ? p : p - nq;
+      const int head = pp / half, i = pp - head * half;
+      float s, c;
+      sincosf((float)pos * inv_freq[i], &s, &c);
+      const uint16_t* src = isq ? q + (size_t)t * nh * hd : k + (size_t)t * nkv * hd;
+      const float a = to_f32<DT>(src[head * hd + i]);
+      const float b = to_f32<DT>(src[head * hd + i + half]);
+      const uint16_t oa = from_f32<DT>(a * c - b * s), ob = from_f32<DT>(a * s + b * c);
+      if (isq) {
+        q[(size_t)t * nh * hd + head * hd + i] = oa;
+        q[(size_t)t * nh * hd + head * hd + i + half] = ob;
+      } else {
+        const size_t off = ((size_t)head * S + pos) * hd + i;
+        kc[off] = oa;
+        kc[off + half] = ob;
+      }
+    } else {
+      const int pp = p - nq - nk;
+      const int head = pp / half, i = pp - head * half;
+      const size_t off = ((size_t)head * S + pos) * hd + i;
+      const uint16_t* src = v + (size_t)t * nkv * hd + head * hd;
+      vc[off] = src[i];
+      vc[off + half] = src[i + half];
+    }
+  }
+}
+
+// act = silu(g) * u   (16-bit in/out), gu = [T, 2, I] packed or separate.
+template <int DT>
+__global__ void silu_mul_kernel(const uint16_t* __restrict__ g, const uint16_t* __restrict__ u,
+                                size_t n, uint16_t* __restrict__ out) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x)
+    out[i] = from_f32<DT>(silu(to_f32<DT>(g[i])) * to_f32<DT>(u[i]));
+}
+
+// resid (f32) += y (16-bit)
+template <int DT>
+__global__ void add_resid_kernel(float* __restrict__ resid, const uint16_t* __restrict__ y,
+                                 size_t n) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x)
+    resid[i] += to_f32<DT>(y[i]);
+}
+
+}  // namespace cake
+
+using namespace cake;
+
+#define DISPATCH_DT(dt, ...)                       \
+  do {                                             \
+    if ((dt) == kBF16) { constexpr int DT = kBF16; __VA_ARGS__; } \
+    else if ((dt) == kF16) { constexpr int DT = kF16; __VA_ARGS__; } \
+    else return (int)hipErrorInvalidValue;         \
+  } while (0)
+
+static inline int ew_grid(size_t n) {
+  size_t g = (n + 255) / 256;
+  return (int)(g < 4096 ? g : 4096);
+}
+
+CAKE_API int cake_embed(int dt, const void* table, const int* tok, int T, int H, float* out,
+                        hipStream_t st) {
+  if (H % 8) return (int)hipErrorInvalidValue;
+  DISPATCH_DT(dt, hipLaunchKernelGGL((embed_kernel<DT>), dim3(T), dim3(256), 0, st,
+                                     (const uint16_t*)table, tok, H, out));
+  return (int)hipGetLastError();
+}
+
+CAKE_API int cake_rmsnorm(int dt, const float* x, const void* w, float eps, int T, int H,
+                          void* out, hipStream_t st) {
+  if (H % 4) return (int)hipErrorInvalidValue;
+  DISPATCH_DT(dt, hipLaunchKernelGGL((rmsnorm_kernel<DT>), dim3(T), dim3(256), 0, st, x,
+                                     (const uint16_t*)w, eps, H, (uint16_t*)out));
+  return (int)hipGetLastError();
+}
+
+CAKE_API int cake_rope_kv(int dt, void* q, const void* k, const void* v, int T, int nh,
+                          int nkv, int hd, const float* inv_freq, int pos0, int S, void* kc,
+                          void* vc, hipStream_t st) {
+  DISPATCH_DT(dt, hipLaunchKernelGGL((rope_kv_kernel<DT>), dim3(T), dim3(256), 0, st,
+                                     (uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, nh,
+                                     nkv, hd, inv_freq, pos0, S, (uint16_t*)kc,
+                                     (uint16_t*)vc));
+  return (int)hipGetLastError();
+}
+
+CAKE_API int cake_silu_mul(int dt, const void* g, const void* u, size_t n, void* out,
+                           hipStream_t st) {
+  DISPATCH_DT(dt, hipLaunchKernelGGL((silu_mul_kernel<DT>), dim3(ew_grid(n)), dim3(256), 0, st,
+                                     (const uint16_t*)g, (const uint16_t*)u, n,
+                                     (uint16_t*)out));
+  return (int)hipGetLastError();
+}
+
+CAKE_API int cake_add_resid(int dt, float* resid, const void* y, size_t n, hipStream_t st) {
+  DISPATCH_DT(dt, hipLaunchKernelGGL((add_resid_kernel<DT>), dim3(ew_grid(n)), dim3(256), 0,
+                                     st, resid, (const uint16_t*)y, n));
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,323 @@
+// Batch-1 decode projections: bandwidth-bound GEMV with fused prologues/epilogues.
+//
+// Replaces the reference's per-layer chain of candle ops for one decode token
+// (SURVEY §2.4.1 K02 rms_norm, K03 Linear, K04 head-major copy, K05 rope,
+// K06 kv cat, K14 residual add, K15 silu*mul, K17 logits cast), i.e.
+//   cake-core/src/models/llama3/transformer.rs:51-73 (block forward),
+//   cake-core/src/models/llama3/attention.rs:49-83 (q/k/v proj + rope),
+//   cake-core/src/models/llama3/mlp.rs:15-18 (SwiGLU),
+//   cake-core/src/models/llama3/llama.rs:119-137 (ln_f + lm_head -> f32).
+//
+// Design (MI355X-first):
+//   * Weights stay in HF [out, in] row-major layout; every weight byte is read
+//     exactly once per token with 16-byte non-temporal loads.
+//   * One wave64 computes a PAIR of output rows so that the pair needs no
+//     cross-wave communication in its epilogue:
+//       - QKV:    rows (i, i + d/2) of one head -> RoPE rotation in registers,
+//                 q written f32, k/v written straight into the preallocated
+//                 KV cache slot [kvh][pos][d] (no cat, no transpose kernel).
+//       - SwiGLU: gate row j and up row j -> act[j] = silu(g) * u.
+//       - Resid:  rows (2p, 2p+1) -> residual stream += W x (in place, f32).
+//       - F32:    rows (2p, 2p+1) -> f32 output (lm_head logits).
+//   * RMSNorm is a block prologue: the f32 residual row is normalised into LDS
+//     once per workgroup (4 waves), so no separate norm launch exists.
+//   * The token position is read from device memory so the launches replay
+//     unchanged inside a hipGraph.
+#include "common.h"
+
+namespace cake {
+
+constexpr int kGemvThreads = 256;  // 4 waves
+constexpr int kGemvWaves = kGemvThreads / 64;
+constexpr int kGemvMaxBlocks = 1024;
+
+// ---------------------------------------------------------------------------
+// x staging (prologues)
+// ---------------------------------------------------------------------------
+
+// Normalise a f32 row into LDS:  xs[i] = x[i] * rsqrt(mean(x^2) + eps) * w[i].
+template <int DT>
+__device__ __forceinline__ void stage_rmsnorm(const float* __restrict__ x,
+                                              const uint16_t* __restrict__ w,
+                                              float eps, int K, float* xs) {
+  __shared__ float red[16];
+  float ss = 0.f;
+  for (int i = threadIdx.x * 4; i < K; i += kGemvThreads * 4) {
+    const float4 v = *reinterpret_cast<const float4*>(x + i);
+    *reinterpret_cast<float4*>(xs + i) = v;
+    ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  }
+  ss = block_sum(ss, red);
+  const float r = rsqrtf(ss / (float)K + eps);
+  for (int i = threadIdx.x * 4; i < K; i += kGemvThreads * 4) {
+    float4 v = *reinterpret_cast<float4*>(xs + i);
+    const uint2 wv = *reinterpret_cast<const uint2*>(w + i);
+    v.x *= r * to_f32<DT>((uint16_t)(wv.x & 0xffff));
+    v.y *= r * to_f32<DT>((uint16_t)(wv.x >> 16));
+    v.z *= r * to_f32<DT>((uint16_t)(wv.y & 0xffff));
+    v.w *= r * to_f32<DT>((uint16_t)(wv.y >> 16));
+    *reinterpret_cast<float4*>(xs + i) = v;
+  }
+  __syncthreads();
+}
+
+// Copy a 16-bit activation row into LDS (kept 16-bit: 70B down_proj has K=28672).
+__device__ __forceinline__ void stage_plain16(const uint16_t* __restrict__ x, int K,
+                                              uint16_t* xs) {
+  for (int i = threadIdx.x * 8; i < K; i += kGemvThreads * 8)
+    *reinterpret_cast<uint4*>(xs + i) = *reinterpret_cast<const uint4*>(x + i);
+  __syncthreads();
+}
+
+template <int DT, bool XF32>
+__device__ __forceinline__ void load_x8(const void* xs, int chunk, float* o) {
+  if constexpr (XF32) {
+    const float4* p = reinterpret_cast<const float4*>(xs) + chunk * 2;
+    const float4 a = p[0], b = p[1];
+    o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w;
+    o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+  } else {
+    unpack8<DT>(reinterpret_cast<const uint4*>(xs)[chunk], o);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// core: one wave, two rows, dot with the staged x.  U = 16-byte chunks per row
+// in flight per lane per iteration (2*U loads outstanding).
+// ---------------------------------------------------------------------------
+template <int DT, bool XF32, int U>
+__device__ __forceinline__ void dot_pair(const uint16_t* __restrict__ wa,
+                                         const uint16_t* __restrict__ wb,
+                                         const void* xs, int K, float& da, float& db) {
+  const int lane = threadIdx.x & 63;
+  const int nch = K >> 3;  // 16-byte chunks per row
+  const uint4* a4 = reinterpret_cast<const uint4*>(wa);
+  const uint4* b4 = reinterpret_cast<const uint4*>(wb);
+  float acc_a = 0.f, acc_b = 0.f;
+  const int full = (nch / (64 * U)) * (64 * U);
+  for (int c0 = 0; c0 < full; c0 += 64 * U) {
+    uint4 va[U], vb[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      va[u] = ld_nt16(a4 + c0 + u * 64 + lane);
+      vb[u] = ld_nt16(b4 + c0 + u * 64 + lane);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float xv[8], fa[8], fb[8];
+      load_x8<DT, XF32>(xs, c0 + u * 64 + lane, xv);
+      unpack8<DT>(va[u], fa);
+      unpack8<DT>(vb[u], fb);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        acc_a = fmaf(fa[e], xv[e], acc_a);
+        acc_b = fmaf(fb[e], xv[e], acc_b);
+      }
+    }
+  }
+  for (int c = full + lane; c < nch; c += 64) {  // tail (small test shapes only)
+    float xv[8], fa[8], fb[8];
+    load_x8<DT, XF32>(xs, c, xv);
+    unpack8<DT>(a4[c], fa);
+    unpack8<DT>(b4[c], fb);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      acc_a = fmaf(fa[e], xv[e], acc_a);
+      acc_b = fmaf(fb[e], xv[e], acc_b);
+    }
+  }
+  da = wave_sum(acc_a);
+  db = wave_sum(acc_b);
+}
+
+// ---------------------------------------------------------------------------
+// QKV + RoPE + KV-cache write
+// ---------------------------------------------------------------------------
+struct QkvArgs {
+  const float* resid;      // [K] f32
+  const uint16_t* norm_w;  // [K]
+  float eps;
+  const uint16_t* wq;  // [nh*hd, K]
+  const uint16_t* wk;  // [nkv*hd, K]
+  const uint16_t* wv;  // [nkv*hd, K]
+  int K, nh, nkv, hd;
+  const float* inv_freq;  // [hd/2]
+  const int* pos;         // device scalar: position of this token
+  float* q_out;           // [nh*hd] f32 (roped)
+  uint16_t* kcache;       // [nkv][S][hd] (this layer)
+  uint16_t* vcache;
+  int S;
+};
+
+template <int DT, int U>
+__global__ __launch_bounds__(kGemvThreads) void qkv_rope_kernel(QkvArgs a) {
+  extern __shared__ float xs[];
+  stage_rmsnorm<DT>(a.resid, a.norm_w, a.eps, a.K, xs);
+  const int half = a.hd >> 1;
+  const int npairs = (a.nh + 2 * a.nkv) * half;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int pos = *a.pos;
+  for (int p = blockIdx.x * kGemvWaves + wave; p < npairs; p += gridDim.x * kGemvWaves) {
+    const int slot = p / half, i = p - slot * half;
+    const uint16_t* base;
+    int kind, head;  // 0=q 1=k 2=v
+    if (slot < a.nh) { kind = 0; head = slot; base = a.wq; }
+    else if (slot < a.nh + a.nkv) { kind = 1; head = slot - a.nh; base = a.wk; }
+    else { kind = 2; head = slot - a.nh - a.nkv; base = a.wv; }
+    const size_t ra = (size_t)head * a.hd + i;
+    float da, db;
+    dot_pair<DT, true, U>(base + ra * a.K, base + (ra + half) * a.K, xs, a.K, da, db);
+    if (lane == 0) {
+      float oa = da, ob = db;
+      if (kind < 2) {
+        float s, c;
+        sincosf((float)pos * a.inv_freq[i], &s, &c);
+        oa = da * c - db * s;
+        ob = da * s + db * c;
+      }
+      if (kind == 0) {
+        a.q_out[ra] = oa;
+        a.q_out[ra + half] = ob;
+      } else {
+        uint16_t* cache = kind == 1 ? a.kcache : a.vcache;
+        const size_t off = ((size_t)head * a.S + pos) * a.hd + i;
+        cache[off] = from_f32<DT>(oa);
+        cache[off + half] = from_f32<DT>(ob);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// RMSNorm + gate/up + SiLU*mul
+// ---------------------------------------------------------------------------
+template <int DT, int U>
+__global__ __launch_bounds__(kGemvThreads) void swiglu_kernel(
+    const float* __restrict__ resid, const uint16_t* __restrict__ norm_w, float eps,
+    const uint16_t* __restrict__ wg, const uint16_t* __restrict__ wu, int K, int I,
+    uint16_t* __restrict__ act) {
+  extern __shared__ float xs[];
+  stage_rmsnorm<DT>(resid, norm_w, eps, K, xs);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int j = blockIdx.x * kGemvWaves + wave; j < I; j += gridDim.x * kGemvWaves) {
+    float g, u;
+    dot_pair<DT, true, U>(wg + (size_t)j * K, wu + (size_t)j * K, xs, K, g, u);
+    if (lane == 0) act[j] = from_f32<DT>(silu(g) * u);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// out (+)= W x   with 16-bit x: o_proj / down_proj (accumulate into the f32
+// residual stream) — or plain f32 output.
+// ---------------------------------------------------------------------------
+template <int DT, int U, bool ACCUM>
+__global__ __launch_bounds__(kGemvThreads) void gemv_x16_kernel(
+    const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, int K, int N,
+    float* __restrict__ out) {
+  extern __shared__ float smem[];
+  uint16_t* xs = reinterpret_cast<uint16_t*>(smem);
+  stage_plain16(x, K, xs);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int npairs = (N + 1) >> 1;
+  for (int p = blockIdx.x * kGemvWaves + wave; p < npairs; p += gridDim.x * kGemvWaves) {
+    const int ra = 2 * p, rb = min(2 * p + 1, N - 1);
+    float da, db;
+    dot_pair<DT, false, U>(w + (size_t)ra * K, w + (size_t)rb * K, xs, K, da, db);
+    if (lane == 0) {
+      if (ACCUM) out[ra] += da; else out[ra] = da;
+      if (2 * p + 1 < N) { if (ACCUM) out[rb] += db; else out[rb] = db; }
+    }
+  }
+}
+
+// RMSNorm(f32 row) then f32 output: the lm_head.
+template <int DT, int U>
+__global__ __launch_bounds__(kGemvThreads) void gemv_norm_f32_kernel(
+    const float* __restrict__ resid, const uint16_t* __restrict__ norm_w, float eps,
+    const uint16_t* __restrict__ w, int K, int N, float* __restrict__ out) {
+  extern __shared__ float xs[];
+  stage_rmsnorm<DT>(resid, norm_w, eps, K, xs);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int npairs = (N + 1) >> 1;
+  for (int p = blockIdx.x * kGemvWaves + wave; p < npairs; p += gridDim.x * kGemvWaves) {
+    const int ra = 2 * p, rb = min(2 * p + 1, N - 1);
+    float da, db;
+    dot_pair<DT, true, U>(w + (size_t)ra * K, w + (size_t)rb * K, xs, K, da, db);
+    if (lane == 0) {
+      out[ra] = da;
+      if (2 * p + 1 < N) out[rb] = db;
+    }
+  }
+}
+
+static inline int grid_for(int npairs) {
+  int g = (npairs + kGemvWaves - 1) / kGemvWaves;
+  return g < kGemvMaxBlocks ? g : kGemvMaxBlocks;
+}
+
+}  // namespace cake
+
+using namespace cake;
+
+#define DISPATCH_DT(dt, ...)                       \
+  do {                                             \
+    if ((dt) == kBF16) { constexpr int DT = kBF16; __VA_ARGS__; } \
+    else if ((dt) == kF16) { constexpr int DT = kF16; __VA_ARGS__; } \
+    else return (int)hipErrorInvalidValue;         \
+  } while (0)
+
+CAKE_API int cake_qkv_rope(int dt, const float* resid, const void* norm_w, float eps,
+                           const void* wq, const void* wk, const void* wv, int K, int nh,
+                           int nkv, int hd, const float* inv_freq, const int* pos,
+                           float* q_out, void* kcache, void* vcache, int S,
+                           hipStream_t st) {
+  if (K % 8 || hd % 2) return (int)hipErrorInvalidValue;
+  QkvArgs a{resid, (const uint16_t*)norm_w, eps, (const uint16_t*)wq,
+            (const uint16_t*)wk, (const uint16_t*)wv, K, nh, nkv, hd, inv_freq, pos,
+            q_out, (uint16_t*)kcache, (uint16_t*)vcache, S};
+  const int npairs = (nh + 2 * nkv) * (hd / 2);
+  const size_t lds = (size_t)K * sizeof(float);
+  DISPATCH_DT(dt, hipLaunchKernelGGL((qkv_rope_kernel<DT, 4>), dim3(grid_for(npairs)),
+                                     dim3(kGemvThreads), lds, st, a));
+  return (int)hipGetLastError();
+}
+
+CAKE_API int cake_swiglu(int dt, const float* resid, const void* norm_w, float eps,
+                         const void* wg, const void* wu, int K, int I, void* act,
+                         hipStream_t st) {
+  if (K % 8) return (int)hipErrorInvalidValue;
+  const size_t lds = (size_t)K * sizeof(float);
+  DISPATCH_DT(dt, hipLaunchKernelGGL((swiglu_kernel<DT, 4>), dim3(grid_for(I)),
+                                     dim3(kGemvThreads), lds, st, resid,
+                                     (const uint16_t*)norm_w, eps, (const uint16_t*)wg,
+                                     (const uint16_t*)wu, K, I, (uint16_t*)act));
+  return (int)hipGetLastError();
+}
+
+CAKE_API int cake_gemv_x16(int dt, const void* x, const void* w, int K, int N, float* out,
+                           int accumulate, hipStream_t st) {
+  if (K % 8) return (int)hipErrorInvalidValue;
+  const size_t lds = (size_t)K * 2;
+  const int g = grid_for((N + 1) / 2);
+  if (accumulate) {
+    DISPATCH_DT(dt, hipLaunchKernelGGL((gemv_x16_kernel<DT, 4, true>), dim3(g),
+                                       dim3(kGemvThreads), lds, st, (const uint16_t*)x,
+                                       (const uint16_t*)w, K, N, out));
+  } else {
+    DISPATCH_DT(dt, hipLaunchKernelGGL((gemv_x16_kernel<DT, 4, false>), dim3(g),
+                                       dim3(kGemvThreads), lds, st, (const uint16_t*)x,
+                                       (const uint16_t*)w, K, N, out));
+  }
+  return (int)hipGetLastError();
+}
+
+CAKE_API int cake_gemv_norm_f32(int dt, const float* resid, const void* norm_w, float eps,
+                                const void* w, int K, int N, float* out, hipStream_t st) {
+  if (K % 8) return (int)hipErrorInvalidValue;
+  const size_t lds = (size_t)K * sizeof(float);
+  DISPATCH_DT(dt, hipLaunchKernelGGL((gemv_norm_f32_kernel<DT, 4>),
+                                     dim3(grid_for((N + 1) / 2)), dim3(kGemvThreads), lds,
+                                     st, resid, (const uint16_t*)norm_w, eps,
+                                     (const uint16_t*)w, K, N, out));
+  return (int)hipGetLastError();
+}

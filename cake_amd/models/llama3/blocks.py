@@ -1,0 +1,218 @@
+"""Transformer-block execution: a rank's local layers + their KV cache.
+
+A :class:`LayerStack` is the MI355X-native counterpart of the reference's
+per-layer ``Transformer`` forwarders (cake-core/src/models/llama3/transformer.rs)
+plus the KV part of ``Cache`` (cache.rs:93-135).  Both the master (layers not
+assigned to any worker) and each worker own one.
+
+Two execution backends share the same weights and cache layout:
+
+* ``hip``   — gfx950 kernels (:mod:`cake_amd.ops.hip`).  Decode (T=1) runs five
+  fused launches per layer with the position read from device memory, so a
+  whole token step is hipGraph-capturable; prefill (T>1) runs the projections
+  as MFMA GEMMs (``torch.matmul`` → hipBLASLt) plus our RoPE/KV-write,
+  causal-attention, SwiGLU and residual kernels.
+* ``torch`` — the Appendix-D reference math in PyTorch (CPU mode ``--cpu``,
+  f32 dtype, and the oracle in tests).
+
+KV cache: one preallocated ``[n_local, nkv, max_seq, hd]`` K and V tensor per
+session (SURVEY Appendix E Q2 — no ``Tensor::cat`` growth).  Sessions isolate
+concurrent masters on one worker (worker.rs:52-72) and are reset explicitly
+(fixes Appendix E Q7).
+"""
+from __future__ import annotations
+
+import math
+from collections import OrderedDict
+
+import torch
+
+from ...ops import reference as R
+from .config import LlamaConfig
+from .weights import BlockWeights
+
+
+class KVCache:
+    def __init__(self, n_layers: int, cfg: LlamaConfig, max_seq: int, device, dtype):
+        shape = (n_layers, cfg.num_key_value_heads, max_seq, cfg.head_dim)
+        self.k = torch.zeros(shape, device=device, dtype=dtype)
+        self.v = torch.zeros(shape, device=device, dtype=dtype)
+        self.max_seq = max_seq
+        self.length = 0  # number of valid positions (host bookkeeping)
+
+    def clear(self) -> None:
+        self.length = 0
+
+
+class DecodeBuffers:
+    """Device-resident state of a batch-1 decode step (graph-stable addresses)."""
+
+    def __init__(self, cfg: LlamaConfig, max_seq: int, device, dtype, with_head: bool):
+        H, I, hd, nh = cfg.hidden_size, cfg.intermediate_size, cfg.head_dim, cfg.num_attention_heads
+        f32, i32 = torch.float32, torch.int32
+        self.resid = torch.zeros(H, device=device, dtype=f32)
+        self.q = torch.zeros(nh * hd, device=device, dtype=f32)
+        self.attn_out = torch.zeros(nh * hd, device=device, dtype=dtype)
+        self.act = torch.zeros(I, device=device, dtype=dtype)
+        nsplit = (max_seq + 63) // 64
+        self.part = torch.zeros(nh * nsplit * (hd + 2), device=device, dtype=f32)
+        self.pos = torch.zeros(1, device=device, dtype=i32)
+        if with_head:
+            self.logits = torch.zeros(cfg.vocab_size, device=device, dtype=f32)
+            self.tok = torch.zeros(1, device=device, dtype=i32)
+            self.hist = torch.zeros(max_seq, device=device, dtype=i32)
+            self.hist_len = torch.zeros(1, device=device, dtype=i32)
+            self.slot = torch.zeros(1, device=device, dtype=torch.int64)
+
+
+class LayerStack:
+    def __init__(self, cfg: LlamaConfig, weights: dict[int, BlockWeights], device, dtype,
+                 max_seq: int, backend: str, max_sessions: int = 8):
+        if backend not in ("hip", "torch"):
+            raise ValueError(f"unknown backend {backend}")
+        if backend == "hip" and dtype not in (torch.bfloat16, torch.float16):
+            raise ValueError("hip backend needs bf16/f16 weights (use torch backend for f32)")
+        self.cfg = cfg
+        self.weights = dict(sorted(weights.items()))
+        self.slot_of = {li: i for i, li in enumerate(self.weights)}
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.max_seq = max_seq
+        self.backend = backend
+        self.max_sessions = max_sessions
+        self.inv_freq = R.inv_freq(cfg.head_dim, cfg.rope_theta, cfg.rope_scaling).to(self.device)
+        self.scale = 1.0 / math.sqrt(cfg.head_dim)
+        self._sessions: OrderedDict[int, KVCache] = OrderedDict()
+        self._decode_bufs: DecodeBuffers | None = None
+        self._hostpos_bufs: DecodeBuffers | None = None
+
+    # ------------------------------------------------------------------ sessions
+    def cache(self, session: int = 0) -> KVCache:
+        kv = self._sessions.get(session)
+        if kv is None:
+            while len(self._sessions) >= self.max_sessions:
+                self._sessions.popitem(last=False)
+            kv = KVCache(len(self.weights), self.cfg, self.max_seq, self.device, self.dtype)
+            self._sessions[session] = kv
+        else:
+            self._sessions.move_to_end(session)
+        return kv
+
+    def reset(self, session: int | None = None) -> None:
+        if session is None:
+            for kv in self._sessions.values():
+                kv.clear()
+        elif session in self._sessions:
+            self._sessions[session].clear()
+
+    def drop(self, session: int) -> None:
+        self._sessions.pop(session, None)
+
+    @property
+    def layer_ids(self) -> list[int]:
+        return list(self.weights)
+
+    def decode_buffers(self, with_head: bool = False) -> DecodeBuffers:
+        if self._decode_bufs is None or (with_head and not hasattr(self._decode_bufs, "logits")):
+            self._decode_bufs = DecodeBuffers(self.cfg, self.max_seq, self.device, self.dtype,
+                                              with_head)
+        return self._decode_bufs
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, hidden: torch.Tensor, layers: list[int], pos0: int,
+                session: int = 0) -> torch.Tensor:
+        """Run `layers` (in order) over hidden [T, H] f32 at positions pos0.., in place."""
+        if hidden.dtype != torch.float32 or hidden.dim() != 2:
+            raise ValueError("hidden must be f32 [T, H]")
+        T = hidden.shape[0]
+        kv = self.cache(session)
+        if pos0 + T > self.max_seq:
+            raise ValueError(f"sequence length {pos0 + T} exceeds max_seq {self.max_seq}")
+        for li in layers:
+            w = self.weights[li]
+            s = self.slot_of[li]
+            if self.backend == "hip":
+                if T == 1:
+                    self._decode_hip_hostpos(hidden, w, kv.k[s], kv.v[s], pos0)
+                else:
+                    self._prefill_hip(hidden, w, kv.k[s], kv.v[s], pos0)
+            else:
+                self._block_torch(hidden, w, kv.k[s], kv.v[s], pos0)
+        kv.length = max(kv.length, pos0 + T)
+        return hidden
+
+    def decode_step(self, bufs: DecodeBuffers, layers: list[int], session: int = 0) -> None:
+        """Graph-capturable T=1 step over bufs.resid at device position bufs.pos (hip only)."""
+        from ...ops import hip as K
+        kv = self.cache(session)
+        cfg = self.cfg
+        for li in layers:
+            w = self.weights[li]
+            s = self.slot_of[li]
+            kc, vc = kv.k[s], kv.v[s]
+            K.qkv_rope(bufs.resid, w.ln1, cfg.rms_norm_eps, w.wq, w.wk, w.wv, self.inv_freq,
+                       bufs.pos, bufs.q, kc, vc)
+            K.attn_decode(bufs.q, kc, vc, bufs.pos, self.scale, bufs.part, bufs.attn_out)
+            K.gemv(bufs.attn_out, w.wo, bufs.resid, accumulate=True)
+            K.swiglu(bufs.resid, w.ln2, cfg.rms_norm_eps, w.wg, w.wu, bufs.act)
+            K.gemv(bufs.act, w.wd, bufs.resid, accumulate=True)
+
+    # ------------------------------------------------------------------ hip paths
+    def _decode_hip_hostpos(self, hidden, w, kc, vc, pos0):
+        if self._hostpos_bufs is None:
+            self._hostpos_bufs = DecodeBuffers(self.cfg, self.max_seq, self.device, self.dtype,
+                                               with_head=False)
+        bufs = self._hostpos_bufs
+        bufs.pos.fill_(pos0)
+        bufs.resid.copy_(hidden[0])
+        from ...ops import hip as K
+        cfg = self.cfg
+        K.qkv_rope(bufs.resid, w.ln1, cfg.rms_norm_eps, w.wq, w.wk, w.wv, self.inv_freq,
+                   bufs.pos, bufs.q, kc, vc)
+        K.attn_decode(bufs.q, kc, vc, bufs.pos, self.scale, bufs.part, bufs.attn_out)
+        K.gemv(bufs.attn_out, w.wo, bufs.resid, accumulate=True)
+        K.swiglu(bufs.resid, w.ln2, cfg.rms_norm_eps, w.wg, w.wu, bufs.act)
+        K.gemv(bufs.act, w.wd, bufs.resid, accumulate=True)
+        hidden[0].copy_(bufs.resid)
+
+    def _prefill_hip(self, hidden, w, kc, vc, pos0):
+        from ...ops import hip as K
+        cfg = self.cfg
+        T, H = hidden.shape
+        x = torch.empty((T, H), device=hidden.device, dtype=self.dtype)
+        K.rmsnorm(hidden, w.ln1, cfg.rms_norm_eps, x)
+        q = torch.matmul(x, w.wq.t())
+        k = torch.matmul(x, w.wk.t())
+        v = torch.matmul(x, w.wv.t())
+        K.rope_kv(q, k, v, self.inv_freq, pos0, kc, vc)
+        att = torch.empty_like(q)
+        K.attn_prefill(q, kc, vc, pos0, self.scale, att)
+        K.add_resid(hidden, torch.matmul(att, w.wo.t()))
+        K.rmsnorm(hidden, w.ln2, cfg.rms_norm_eps, x)
+        g = torch.matmul(x, w.wg.t())
+        u = torch.matmul(x, w.wu.t())
+        K.silu_mul(g, u, g)
+        K.add_resid(hidden, torch.matmul(g, w.wd.t()))
+
+    # ------------------------------------------------------------------ torch path
+    def _block_torch(self, hidden, w, kc, vc, pos0):
+        cfg = self.cfg
+        T = hidden.shape[0]
+        nh, nkv, hd = cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim
+        dt = self.dtype
+        positions = torch.arange(pos0, pos0 + T, device=hidden.device)
+        x = R.rms_norm(hidden, w.ln1, cfg.rms_norm_eps).to(dt)
+        q = (x @ w.wq.t()).view(T, nh, hd)
+        k = (x @ w.wk.t()).view(T, nkv, hd)
+        v = (x @ w.wv.t()).view(T, nkv, hd)
+        q = R.rope(q, positions, self.inv_freq).to(dt)
+        k = R.rope(k, positions, self.inv_freq).to(dt)
+        kc[:, pos0:pos0 + T] = k.transpose(0, 1)
+        vc[:, pos0:pos0 + T] = v.to(dt).transpose(0, 1)
+        Tk = pos0 + T
+        att = R.attention(q, kc[:, :Tk].transpose(0, 1), vc[:, :Tk].transpose(0, 1), pos0)
+        att = att.to(dt).reshape(T, nh * hd)
+        hidden += (att @ w.wo.t()).float()
+        x2 = R.rms_norm(hidden, w.ln2, cfg.rms_norm_eps).to(dt)
+        act = R.silu_mul(x2 @ w.wg.t(), x2 @ w.wu.t()).to(dt)
+        hidden += (act @ w.wd.t()).float()

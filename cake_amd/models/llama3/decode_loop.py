@@ -1,0 +1,102 @@
+"""Host side of the device decode loop (one step of host/GPU overlap).
+
+The GPU graph for step k+1 only needs the token chosen by step k, which the
+graph itself leaves in device memory — so the host enqueues step k+1 *before*
+it reads token k back (4 bytes through a pinned ring).  EOS detection lags by
+one step (the extra speculative step is discarded).  Per-token latency comes
+from device events recorded after every step: the reference only logs an
+aggregate rate (cake-core/src/cake/master.rs:93-121); BASELINE asks for p50.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+from typing import Callable
+
+import torch
+
+from .model import DeviceDecoder
+
+
+@dataclass
+class DecodeStats:
+    tokens: list[int] = field(default_factory=list)
+    step_ms: list[float] = field(default_factory=list)   # device time per token
+    wall_s: float = 0.0
+
+    def percentile(self, q: float) -> float:
+        if not self.step_ms:
+            return float("nan")
+        xs = sorted(self.step_ms)
+        k = min(len(xs) - 1, max(0, int(round(q / 100.0 * (len(xs) - 1)))))
+        return xs[k]
+
+
+def run_decode(dec: DeviceDecoder, n_steps: int, eos_ids: set[int] | None = None,
+               on_token: Callable[[int], None] | None = None,
+               sampler: Callable[[torch.Tensor], int] | None = None) -> DecodeStats:
+    """Run up to n_steps decode steps; stop at EOS (unless eos_ids is None)."""
+    st = DecodeStats()
+    if n_steps <= 0:
+        return st
+    dev = dec.bufs.tok.device
+    if sampler is not None:
+        # sampled mode: the host draws each token, so no lookahead is possible
+        t0 = time.perf_counter()
+        prev_ev = torch.cuda.Event(enable_timing=True)
+        prev_ev.record()
+        for _ in range(n_steps):
+            dec.launch()
+            tok = sampler(dec.logits())
+            dec.push(tok)
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            ev.synchronize()
+            st.step_ms.append(prev_ev.elapsed_time(ev))
+            prev_ev = ev
+            st.tokens.append(tok)
+            if on_token:
+                on_token(tok)
+            if eos_ids and tok in eos_ids:
+                break
+        st.wall_s = time.perf_counter() - t0
+        return st
+
+    ring = torch.empty(2, dtype=torch.int32, pin_memory=True)
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    start_ev = torch.cuda.Event(enable_timing=True)
+    start_ev.record()
+    prev_done = start_ev
+    t0 = time.perf_counter()
+    pending = None  # (slot, event)
+    issued = 0
+    stop = False
+    while not stop:
+        cur = None
+        if issued < n_steps:
+            slot = issued & 1
+            dec.launch()
+            ring[slot:slot + 1].copy_(dec.bufs.tok, non_blocking=True)
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            cur = (slot, ev)
+            issued += 1
+        if pending is not None:
+            slot, ev = pending
+            ev.synchronize()
+            st.step_ms.append(prev_done.elapsed_time(ev))
+            prev_done = ev
+            tok = int(ring[slot].item())
+            st.tokens.append(tok)
+            if on_token:
+                on_token(tok)
+            if eos_ids and tok in eos_ids:
+                stop = True
+        pending = cur
+        if pending is None:
+            stop = True
+    if pending is not None:
+        pending[1].synchronize()
+    st.wall_s = time.perf_counter() - t0
+    del dev, evs
+    return st

@@ -1,0 +1,226 @@
+"""Master-side Llama-3 model: embedding → placed blocks → ln_f → lm_head.
+
+Counterpart of ``LLama::forward`` (cake-core/src/models/llama3/llama.rs:72-138).
+Blocks are placed per the topology: a layer named on a worker is reached
+through a remote :class:`~cake_amd.parallel.forwarder.Forwarder`; every other
+layer runs in this process's :class:`LayerStack`.  Consecutive layers with the
+same owner form one *run* and cost one hop (contiguous-block batching,
+llama.rs:95-114) — planned once at load time by :func:`plan_runs`.
+
+For the all-local HIP case, :class:`DeviceDecoder` captures the whole decode
+step (embedding, 32/80 layers, ln_f + lm_head, repeat penalty, argmax, next
+token/position bookkeeping) into ONE hipGraph; the host reads 4 bytes per token,
+one step behind the GPU.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import torch
+
+from ...ops import reference as R
+from .blocks import DecodeBuffers, LayerStack
+from .config import LlamaConfig
+from .weights import HeadWeights, layer_name
+
+
+@dataclass
+class Run:
+    ident: str                 # "local" or the worker identity
+    layers: list[int]
+    forwarder: object | None = None   # parallel.forwarder.Forwarder for remote runs
+
+    @property
+    def local(self) -> bool:
+        return self.ident == "local"
+
+
+def plan_runs(num_layers: int, remote: dict[int, object]) -> list[Run]:
+    """Group consecutive layers with equal owner identity (llama.rs:95-114)."""
+    runs: list[Run] = []
+    for li in range(num_layers):
+        fwd = remote.get(li)
+        ident = "local" if fwd is None else fwd.ident()
+        if runs and runs[-1].ident == ident:
+            runs[-1].layers.append(li)
+        else:
+            runs.append(Run(ident=ident, layers=[li], forwarder=fwd))
+    return runs
+
+
+class LlamaModel:
+    def __init__(self, cfg: LlamaConfig, head: HeadWeights, stack: LayerStack,
+                 remote: dict[int, object] | None = None):
+        self.cfg = cfg
+        self.head = head
+        self.stack = stack
+        self.remote = dict(remote or {})
+        self.runs = plan_runs(cfg.num_hidden_layers, self.remote)
+        missing = [li for r in self.runs if r.local for li in r.layers if li not in stack.weights]
+        if missing:
+            raise ValueError(f"local layers without weights: {missing[:8]}")
+        self.device = stack.device
+        self.dtype = stack.dtype
+        self.backend = stack.backend
+        self.session = 0
+
+    @property
+    def all_local(self) -> bool:
+        return all(r.local for r in self.runs)
+
+    # ------------------------------------------------------------------ generic path
+    def embed(self, tokens: list[int]) -> torch.Tensor:
+        ids = torch.tensor(tokens, dtype=torch.int32, device=self.device)
+        if self.backend == "hip":
+            from ...ops import hip as K
+            out = torch.empty((len(tokens), self.cfg.hidden_size), device=self.device,
+                              dtype=torch.float32)
+            K.embed(self.head.embed, ids, out)
+            return out
+        return self.head.embed[ids.long()].float()
+
+    def forward_hidden(self, hidden: torch.Tensor, pos0: int) -> torch.Tensor:
+        for run in self.runs:
+            if run.local:
+                self.stack.forward(hidden, run.layers, pos0, self.session)
+            else:
+                batch = [(layer_name(li), pos0, li) for li in run.layers]
+                hidden = run.forwarder.forward_batch(hidden, batch, self.session)
+                if hidden.device != self.device:
+                    hidden = hidden.to(self.device)
+                hidden = hidden.float().contiguous()
+        return hidden
+
+    def head_logits(self, last: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        """ln_f + lm_head on one f32 row -> f32 logits (llama.rs:119-137)."""
+        if self.backend == "hip":
+            from ...ops import hip as K
+            if out is None:
+                out = torch.empty(self.cfg.vocab_size, device=self.device, dtype=torch.float32)
+            K.norm_gemv_f32(last.contiguous(), self.head.norm, self.cfg.rms_norm_eps,
+                            self.head.lm_head, out)
+            return out
+        x = R.rms_norm(last, self.head.norm, self.cfg.rms_norm_eps).to(self.dtype)
+        return (x @ self.head.lm_head.t()).float()
+
+    def forward(self, tokens: list[int], pos0: int) -> torch.Tensor:
+        """Logits (f32 [V]) of the last of `tokens`, fed at positions pos0.."""
+        h = self.embed(tokens)
+        h = self.forward_hidden(h, pos0)
+        return self.head_logits(h[-1])
+
+    def reset(self) -> None:
+        self.stack.reset(self.session)
+        for run in self.runs:
+            if not run.local and hasattr(run.forwarder, "reset"):
+                run.forwarder.reset(self.session)
+
+
+@dataclass
+class _Pending:
+    event: torch.cuda.Event
+    host: torch.Tensor
+    t_issue: float = 0.0
+    extra: dict = field(default_factory=dict)
+
+
+class DeviceDecoder:
+    """Whole-step hipGraph decoder for an all-local model on the HIP backend.
+
+    Device state (DecodeBuffers): tok, pos, hist, hist_len, slot.  A step:
+    embed(tok) → layers(pos) → ln_f/lm_head → [repeat penalty] → argmax →
+    finalize (tok ← argmax, hist.append, pos += 1).  For temperature > 0 the
+    graph stops after the penalty and the host sampler pushes the token.
+    """
+
+    def __init__(self, model: LlamaModel, repeat_penalty: float = 1.0, repeat_last_n: int = 128,
+                 greedy: bool = True, use_graph: bool = True):
+        if model.backend != "hip" or not model.all_local:
+            raise ValueError("DeviceDecoder needs an all-local model on the hip backend")
+        self.m = model
+        self.penalty = float(repeat_penalty)
+        self.last_n = int(repeat_last_n)
+        self.greedy = greedy
+        self.use_graph = use_graph
+        self.bufs: DecodeBuffers = model.stack.decode_buffers(with_head=True)
+        self.graph: torch.cuda.CUDAGraph | None = None
+        self._layers = list(range(model.cfg.num_hidden_layers))
+
+    # the captured body
+    def _step_body(self) -> None:
+        from ...ops import hip as K
+        b, m = self.bufs, self.m
+        K.embed(m.head.embed, b.tok, b.resid)
+        m.stack.decode_step(b, self._layers, m.session)
+        K.norm_gemv_f32(b.resid, m.head.norm, m.cfg.rms_norm_eps, m.head.lm_head, b.logits)
+        if self.penalty != 1.0:
+            K.repeat_penalty(b.logits, b.hist, b.hist_len, self.last_n, self.penalty)
+        if self.greedy:
+            K.argmax(b.logits, b.slot)
+            K.finalize_token(b.slot, b.tok, b.hist, b.hist_len, b.pos)
+
+    def capture(self) -> None:
+        if not self.use_graph or self.graph is not None:
+            return
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        # warm the kernels once outside capture on scratch state, then restore
+        saved = [t.clone() for t in (self.bufs.tok, self.bufs.pos, self.bufs.hist_len)]
+        hist = self.bufs.hist.clone()
+        with torch.cuda.stream(s):
+            self._step_body()
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        for t, v in zip((self.bufs.tok, self.bufs.pos, self.bufs.hist_len), saved):
+            t.copy_(v)
+        self.bufs.hist.copy_(hist)
+        self.bufs.slot.zero_()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._step_body()
+        self.graph = g
+        torch.cuda.synchronize()
+
+    def start(self, prompt: list[int]) -> int:
+        """Prefill `prompt` at position 0 and select the first token (returned)."""
+        m, b = self.m, self.bufs
+        T = len(prompt)
+        if T + 1 > m.stack.max_seq:
+            raise ValueError("prompt longer than max_seq")
+        m.stack.reset(m.session)
+        h = m.embed(prompt)
+        h = m.forward_hidden(h, 0)
+        ids = torch.tensor(prompt, dtype=torch.int32)
+        b.hist[:T].copy_(ids.to(m.device))
+        b.hist_len.fill_(T)
+        b.pos.fill_(T - 1)
+        b.slot.zero_()
+        m.head_logits(h[-1], out=b.logits)
+        return self._select_first()
+
+    def _select_first(self) -> int:
+        from ...ops import hip as K
+        b = self.bufs
+        if self.penalty != 1.0:
+            K.repeat_penalty(b.logits, b.hist, b.hist_len, self.last_n, self.penalty)
+        if self.greedy:
+            K.argmax(b.logits, b.slot)
+            K.finalize_token(b.slot, b.tok, b.hist, b.hist_len, b.pos)
+            return int(b.tok.item())
+        raise RuntimeError("sampled mode: caller pushes the first token")
+
+    def push(self, token: int) -> None:
+        from ...ops import hip as K
+        b = self.bufs
+        src = torch.tensor([token], dtype=torch.int32, device=self.m.device)
+        K.push_token(src, b.tok, b.hist, b.hist_len, b.pos)
+
+    def launch(self) -> None:
+        """Enqueue one decode step (async)."""
+        if self.graph is not None:
+            self.graph.replay()
+        else:
+            self._step_body()
+
+    def logits(self) -> torch.Tensor:
+        return self.bufs.logits

@@ -1,0 +1,86 @@
+"""ctypes binding of ``libcake_kernels.so`` (the gfx950 HIP kernels).
+
+The library exposes a plain C ABI; each entry point takes raw device pointers
+plus the HIP stream to launch on.  We pass torch's *current* stream so that a
+``torch.cuda.graph`` capture records our launches like any torch op.
+
+On a machine with a GPU the library is mandatory: :func:`kernels` raises if it
+is missing rather than silently falling back to PyTorch ops.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+from pathlib import Path
+
+_LIB_PATH = Path(__file__).resolve().parent.parent / "lib" / "libcake_kernels.so"
+_lock = threading.Lock()
+_lib = None
+
+P = C.c_void_p
+I = C.c_int
+F = C.c_float
+Z = C.c_size_t
+
+# name -> argtypes (all return int hipError_t)
+_SIGS = {
+    "cake_qkv_rope": [I, P, P, F, P, P, P, I, I, I, I, P, P, P, P, P, I, P],
+    "cake_swiglu": [I, P, P, F, P, P, I, I, P, P],
+    "cake_gemv_x16": [I, P, P, I, I, P, I, P],
+    "cake_gemv_norm_f32": [I, P, P, F, P, I, I, P, P],
+    "cake_attn_decode": [I, P, P, P, P, I, I, I, I, F, P, P, P],
+    "cake_attn_prefill": [I, P, P, P, I, I, I, I, I, I, F, P, P],
+    "cake_embed": [I, P, P, I, I, P, P],
+    "cake_rmsnorm": [I, P, P, F, I, I, P, P],
+    "cake_rope_kv": [I, P, P, P, I, I, I, I, P, I, I, P, P, P],
+    "cake_silu_mul": [I, P, P, Z, P, P],
+    "cake_add_resid": [I, P, P, Z, P],
+    "cake_repeat_penalty": [P, P, P, I, F, P],
+    "cake_argmax": [P, I, P, P],
+    "cake_finalize_token": [P, P, P, P, P, I, P],
+    "cake_push_token": [P, P, P, P, P, I, P],
+}
+
+
+class KernelError(RuntimeError):
+    pass
+
+
+def lib_path() -> Path:
+    return Path(os.environ.get("CAKE_KERNEL_LIB", _LIB_PATH))
+
+
+def kernels():
+    """Load (once) and return the kernel library; raise if it is unavailable."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            import torch  # noqa: F401  (HIP runtime must be loaded by torch first)
+
+            path = lib_path()
+            if not path.exists():
+                raise KernelError(
+                    f"{path} not built; run `python -m cake_amd.build` (hipcc gfx950)")
+            lib = C.CDLL(str(path), mode=C.RTLD_GLOBAL)
+            for name, argtypes in _SIGS.items():
+                fn = getattr(lib, name)
+                fn.argtypes = argtypes
+                fn.restype = C.c_int
+            _lib = lib
+    return _lib
+
+
+def available() -> bool:
+    try:
+        kernels()
+        return True
+    except (KernelError, OSError):
+        return False
+
+
+def check(rc: int, name: str) -> None:
+    if rc != 0:
+        raise KernelError(f"{name} failed with hipError {rc}")

@@ -1,0 +1,196 @@
+"""Numerics of the gfx950 HIP kernels vs the plain-PyTorch f32 reference."""
+import math
+
+import pytest
+import torch
+
+from cake_amd.ops import reference as R
+
+pytestmark = pytest.mark.gpu
+
+DTYPES = [torch.bfloat16, torch.float16]
+
+
+def _tol(dt):
+    return dict(atol=3e-2, rtol=3e-2) if dt == torch.bfloat16 else dict(atol=1e-2, rtol=1e-2)
+
+
+def _rand(*shape, dt=torch.float32, std=1.0, dev="cuda"):
+    return (torch.randn(*shape, device=dev) * std).to(dt)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("K,N", [(4096, 4096), (256, 6), (1024, 14336 // 4), (14336, 512)])
+def test_gemv_accumulate(cuda, dt, K, N):
+    from cake_amd.ops import hip as K_
+    torch.manual_seed(0)
+    x = _rand(K, dt=dt)
+    w = _rand(N, K, dt=dt, std=0.02)
+    out = torch.randn(N, device=cuda)
+    ref = out + (w.float() @ x.float())
+    K_.gemv(x, w, out, accumulate=True)
+    torch.testing.assert_close(out, ref, atol=2e-3 * math.sqrt(K / 256), rtol=1e-3)
+    out2 = torch.empty(N, device=cuda)
+    K_.gemv(x, w, out2, accumulate=False)
+    torch.testing.assert_close(out2, w.float() @ x.float(), atol=2e-3 * math.sqrt(K / 256), rtol=1e-3)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("K,N", [(4096, 128256), (256, 512), (512, 7)])
+def test_norm_gemv_f32(cuda, dt, K, N):
+    from cake_amd.ops import hip as K_
+    torch.manual_seed(1)
+    resid = torch.randn(K, device=cuda) * 3
+    nw = (1 + 0.1 * torch.randn(K, device=cuda)).to(dt)
+    w = _rand(N, K, dt=dt, std=0.02)
+    out = torch.empty(N, device=cuda)
+    K_.norm_gemv_f32(resid, nw, 1e-5, w, out)
+    ref = w.float() @ R.rms_norm(resid, nw, 1e-5)
+    torch.testing.assert_close(out, ref, atol=3e-3, rtol=1e-3)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("K,I", [(4096, 14336), (256, 512)])
+def test_swiglu(cuda, dt, K, I):
+    from cake_amd.ops import hip as K_
+    torch.manual_seed(2)
+    resid = torch.randn(K, device=cuda)
+    nw = (1 + 0.1 * torch.randn(K, device=cuda)).to(dt)
+    wg = _rand(I, K, dt=dt, std=0.05)
+    wu = _rand(I, K, dt=dt, std=0.05)
+    act = torch.empty(I, device=cuda, dtype=dt)
+    K_.swiglu(resid, nw, 1e-5, wg, wu, act)
+    x = R.rms_norm(resid, nw, 1e-5)
+    ref = R.silu_mul(wg.float() @ x, wu.float() @ x)
+    torch.testing.assert_close(act.float(), ref, **_tol(dt))
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("H,nh,nkv,hd,pos", [(4096, 32, 8, 128, 0), (4096, 32, 8, 128, 777),
+                                             (256, 4, 1, 64, 5), (1024, 8, 8, 128, 4095)])
+def test_qkv_rope(cuda, dt, H, nh, nkv, hd, pos):
+    from cake_amd.ops import hip as K_
+    torch.manual_seed(3)
+    S = 4096
+    resid = torch.randn(H, device=cuda)
+    nw = (1 + 0.1 * torch.randn(H, device=cuda)).to(dt)
+    wq, wk, wv = (_rand(n * hd, H, dt=dt, std=0.05) for n in (nh, nkv, nkv))
+    invf = R.inv_freq(hd, 500000.0).to(cuda)
+    kc = torch.zeros(nkv, S, hd, device=cuda, dtype=dt)
+    vc = torch.zeros_like(kc)
+    q = torch.empty(nh * hd, device=cuda)
+    p = torch.tensor([pos], dtype=torch.int32, device=cuda)
+    K_.qkv_rope(resid, nw, 1e-5, wq, wk, wv, invf, p, q, kc, vc)
+    x = R.rms_norm(resid, nw, 1e-5)
+    posv = torch.tensor([pos], device=cuda)
+    qr = R.rope((wq.float() @ x).view(1, nh, hd), posv, invf).view(-1)
+    kr = R.rope((wk.float() @ x).view(1, nkv, hd), posv, invf).view(nkv, hd)
+    vr = (wv.float() @ x).view(nkv, hd)
+    torch.testing.assert_close(q, qr, atol=2e-3, rtol=2e-3)
+    torch.testing.assert_close(kc[:, pos].float(), kr, **_tol(dt))
+    torch.testing.assert_close(vc[:, pos].float(), vr, **_tol(dt))
+    assert kc[:, :pos].abs().sum() == 0 and kc[:, pos + 1:].abs().sum() == 0
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("nh,nkv,hd,pos", [(32, 8, 128, 0), (32, 8, 128, 63), (32, 8, 128, 64),
+                                           (32, 8, 128, 1000), (64, 8, 128, 300),
+                                           (4, 1, 64, 17), (8, 8, 64, 200)])
+def test_attn_decode(cuda, dt, nh, nkv, hd, pos):
+    from cake_amd.ops import hip as K_
+    torch.manual_seed(4)
+    S = 2048
+    kc = _rand(nkv, S, hd, dt=dt)
+    vc = _rand(nkv, S, hd, dt=dt)
+    q = torch.randn(nh * hd, device=cuda)
+    p = torch.tensor([pos], dtype=torch.int32, device=cuda)
+    part = torch.empty(K_.attn_workspace_numel(nh, hd, S), device=cuda)
+    out = torch.empty(nh * hd, device=cuda, dtype=dt)
+    K_.attn_decode(q, kc, vc, p, 1 / math.sqrt(hd), part, out)
+    Tk = pos + 1
+    ref = R.attention(q.view(1, nh, hd), kc[:, :Tk].transpose(0, 1), vc[:, :Tk].transpose(0, 1),
+                      pos).reshape(-1)
+    torch.testing.assert_close(out.float(), ref, **_tol(dt))
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("T,pos0,nh,nkv,hd", [(7, 0, 32, 8, 128), (70, 0, 4, 1, 64),
+                                              (33, 100, 32, 8, 128), (1, 5, 8, 8, 64)])
+def test_rope_kv_and_prefill_attention(cuda, dt, T, pos0, nh, nkv, hd):
+    from cake_amd.ops import hip as K_
+    torch.manual_seed(5)
+    S = 512
+    kc = _rand(nkv, S, hd, dt=dt)
+    vc = _rand(nkv, S, hd, dt=dt)
+    q = _rand(T, nh * hd, dt=dt)
+    k = _rand(T, nkv * hd, dt=dt)
+    v = _rand(T, nkv * hd, dt=dt)
+    invf = R.inv_freq(hd, 500000.0).to(cuda)
+    positions = torch.arange(pos0, pos0 + T, device=cuda)
+    qr = R.rope(q.view(T, nh, hd), positions, invf)
+    kr = R.rope(k.view(T, nkv, hd), positions, invf)
+    q_in = q.clone()
+    K_.rope_kv(q_in, k, v, invf, pos0, kc, vc)
+    torch.testing.assert_close(q_in.float().view(T, nh, hd), qr, **_tol(dt))
+    torch.testing.assert_close(kc[:, pos0:pos0 + T].float().transpose(0, 1), kr, **_tol(dt))
+    torch.testing.assert_close(vc[:, pos0:pos0 + T].transpose(0, 1).reshape(T, -1), v)
+    out = torch.empty_like(q_in)
+    K_.attn_prefill(q_in, kc, vc, pos0, 1 / math.sqrt(hd), out)
+    Tk = pos0 + T
+    ref = R.attention(q_in.view(T, nh, hd), kc[:, :Tk].transpose(0, 1), vc[:, :Tk].transpose(0, 1),
+                      pos0)
+    torch.testing.assert_close(out.float().view(T, nh, hd), ref, **_tol(dt))
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+def test_embed_rmsnorm_silu_add(cuda, dt):
+    from cake_amd.ops import hip as K_
+    torch.manual_seed(6)
+    V, H, T = 1000, 4096, 5
+    table = _rand(V, H, dt=dt)
+    tok = torch.tensor([3, 999, 0, 17, 3], dtype=torch.int32, device=cuda)
+    out = torch.empty(T, H, device=cuda)
+    K_.embed(table, tok, out)
+    torch.testing.assert_close(out, table[tok.long()].float())
+    w = (1 + 0.1 * torch.randn(H, device=cuda)).to(dt)
+    xn = torch.empty(T, H, device=cuda, dtype=dt)
+    K_.rmsnorm(out, w, 1e-5, xn)
+    torch.testing.assert_close(xn.float(), R.rms_norm(out, w, 1e-5), **_tol(dt))
+    g, u = _rand(T, 300, dt=dt), _rand(T, 300, dt=dt)
+    act = torch.empty_like(g)
+    K_.silu_mul(g, u, act)
+    torch.testing.assert_close(act.float(), R.silu_mul(g, u), **_tol(dt))
+    resid = torch.randn(T, 300, device=cuda)
+    ref = resid + act.float()
+    K_.add_resid(resid, act)
+    torch.testing.assert_close(resid, ref)
+
+
+def test_penalty_argmax_finalize(cuda):
+    from cake_amd.ops import hip as K_
+    torch.manual_seed(7)
+    V = 128256
+    logits = torch.randn(V, device=cuda)
+    hist_list = [5, 9, 5, 100, 7, 9, 120000]
+    hist = torch.zeros(64, dtype=torch.int32, device=cuda)
+    hist[:len(hist_list)] = torch.tensor(hist_list, dtype=torch.int32)
+    hist_len = torch.tensor([len(hist_list)], dtype=torch.int32, device=cuda)
+    logits[9] = 50.0
+    logits[5] = -3.0
+    ref = R.apply_repeat_penalty(logits, 1.3, hist_list[-4:])
+    K_.repeat_penalty(logits, hist, hist_len, 4, 1.3)
+    torch.testing.assert_close(logits, ref)
+    slot = torch.zeros(1, dtype=torch.int64, device=cuda)
+    K_.argmax(logits, slot)
+    tok = torch.zeros(1, dtype=torch.int32, device=cuda)
+    pos = torch.tensor([10], dtype=torch.int32, device=cuda)
+    K_.finalize_token(slot, tok, hist, hist_len, pos)
+    expect = int(torch.argmax(ref))
+    assert int(tok) == expect
+    assert int(hist_len) == len(hist_list) + 1 and int(hist[len(hist_list)]) == expect
+    assert int(pos) == 11 and int(slot) == 0
+    # ties resolve to the smallest index
+    logits.fill_(1.0)
+    K_.argmax(logits, slot)
+    K_.finalize_token(slot, tok, hist, hist_len, pos)
+    assert int(tok) == 0
