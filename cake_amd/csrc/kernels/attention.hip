@@ -13,9 +13,9 @@
 //     repeat_kv is never materialised.
 //   * Decode is flash-decoding: grid (nkv, S/64) — each workgroup owns 64 keys
 //     (one per lane), computes a local softmax and P·V in f32, and writes
-//     (max, sum, o[hd]) partials; a combine kernel merges the splits.  The
-//     grid is sized for max_seq so the launch is hipGraph-replayable; blocks
-//     past the live length exit immediately.
+//     (max, sum, o[hd]) partials; the last-arriving split merges them (one
+//     launch per layer).  The grid is sized for max_seq so the launch is
+//     hipGraph-replayable; blocks past the live length exit immediately.
 //   * Prefill: one wave per (query row, head) with an online softmax over
 //     64-key tiles; the causal limit is offset-aware (pos0 + t), which fixes the
 //     reference's index_pos==0-only mask and enables
@@ -29,93 +29,135 @@ constexpr int kKeysPerSplit = 64;
 // ---------------------------------------------------------------------------
 // decode
 // ---------------------------------------------------------------------------
-template <int DT, int HD>
-__global__ void attn_decode_kernel(const float* __restrict__ q,
-                                   const uint16_t* __restrict__ kc,
-                                   const uint16_t* __restrict__ vc,
-                                   const int* __restrict__ pos_ptr, int S, int nkv,
-                                   int n_rep, float scale, float* __restrict__ part,
-                                   int nsplit) {
-  constexpr int DPL = HD / 64;  // output dims per lane
-  __shared__ float qs[8 * HD];  // n_rep <= 8
+// One workgroup = (kv head g, 64-key split s), NREP waves (one per query head
+// of the GQA group).  K/V rows of the split are staged into LDS with coalesced
+// 16-byte loads (K rows padded by 16 B so the per-lane row reads are
+// conflict-free), scores/softmax/P·V run from LDS, and the split's
+// (max, sum, o[HD]) partial goes to a workspace.  The LAST split to finish
+// (agent-scope release/acquire ticket per kv head) merges all partials and
+// writes the head outputs, so no separate combine launch exists; a
+// single-split context (Tk <= 64) writes its output directly.
+template <int DT, int HD, int NREP>
+__global__ __launch_bounds__(64 * NREP) void attn_decode_kernel(
+    const float* __restrict__ q, const uint16_t* __restrict__ kc,
+    const uint16_t* __restrict__ vc, const int* __restrict__ pos_ptr, int S, float scale,
+    float* __restrict__ part, int nsplit, unsigned int* __restrict__ tickets,
+    uint16_t* __restrict__ out) {
+  constexpr int DPL = HD / 64;         // output dims per lane
+  constexpr int KROW = HD + 8;         // padded K row (elements)
+  constexpr int CPR = HD / 8;          // 16-byte chunks per row
+  constexpr int NT = 64 * NREP;
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[kKeysPerSplit * KROW];
+  __shared__ __attribute__((aligned(16))) uint16_t Vs[kKeysPerSplit * HD];
+  __shared__ __attribute__((aligned(16))) float qs[NREP * HD];
+  __shared__ float ps[NREP * kKeysPerSplit];
+  __shared__ unsigned int last_flag;
+
   const int g = blockIdx.x, s = blockIdx.y;
   const int Tk = *pos_ptr + 1;
   const int k0 = s * kKeysPerSplit;
   if (k0 >= Tk) return;
   const int kn = min(kKeysPerSplit, Tk - k0);
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int h = g * n_rep + wave;
-  for (int i = threadIdx.x; i < n_rep * HD; i += blockDim.x) qs[i] = q[g * n_rep * HD + i];
-  __syncthreads();
+  const int ns = (Tk + kKeysPerSplit - 1) / kKeysPerSplit;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int h = g * NREP + wave;
 
-  const uint16_t* kbase = kc + ((size_t)g * S + k0) * HD;
-  const uint16_t* vbase = vc + ((size_t)g * S + k0) * HD;
-  const float* qh = qs + wave * HD;
+  const uint4* kg = reinterpret_cast<const uint4*>(kc + ((size_t)g * S + k0) * HD);
+  const uint4* vg = reinterpret_cast<const uint4*>(vc + ((size_t)g * S + k0) * HD);
+  for (int i = tid; i < kn * CPR; i += NT) {
+    const int r = i / CPR, c = i - r * CPR;
+    *reinterpret_cast<uint4*>(Ks + r * KROW + c * 8) = kg[i];
+    reinterpret_cast<uint4*>(Vs)[i] = vg[i];
+  }
+  for (int i = tid; i < NREP * HD; i += NT) qs[i] = q[(size_t)g * NREP * HD + i];
+  __syncthreads();
 
   // scores: lane j <-> key k0 + j
   float sc = -INFINITY;
   if (lane < kn) {
-    const uint4* kr = reinterpret_cast<const uint4*>(kbase + (size_t)lane * HD);
+    const uint16_t* kr = Ks + lane * KROW;
+    const float* qh = qs + wave * HD;
     float acc = 0.f;
 #pragma unroll
-    for (int c = 0; c < HD / 8; ++c) {
+    for (int c = 0; c < CPR; ++c) {
       float kf[8];
-      unpack8<DT>(kr[c], kf);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) acc = fmaf(qh[c * 8 + e], kf[e], acc);
+      unpack8<DT>(*reinterpret_cast<const uint4*>(kr + c * 8), kf);
+      const float4 qa = *reinterpret_cast<const float4*>(qh + c * 8);
+      const float4 qb = *reinterpret_cast<const float4*>(qh + c * 8 + 4);
+      acc = fmaf(qa.x, kf[0], acc); acc = fmaf(qa.y, kf[1], acc);
+      acc = fmaf(qa.z, kf[2], acc); acc = fmaf(qa.w, kf[3], acc);
+      acc = fmaf(qb.x, kf[4], acc); acc = fmaf(qb.y, kf[5], acc);
+      acc = fmaf(qb.z, kf[6], acc); acc = fmaf(qb.w, kf[7], acc);
     }
     sc = acc * scale;
   }
   const float m = wave_max(sc);
   const float p = lane < kn ? __expf(sc - m) : 0.f;
   const float l = wave_sum(p);
+  ps[wave * kKeysPerSplit + lane] = p;
+  __syncthreads();
 
-  // o[d] = sum_j p_j v_j[d]; lane owns dims lane*DPL .. +DPL
   float o[DPL];
 #pragma unroll
   for (int d = 0; d < DPL; ++d) o[d] = 0.f;
+  const float* pw = ps + wave * kKeysPerSplit;
+#pragma unroll 8
   for (int j = 0; j < kn; ++j) {
-    const float pj = __shfl(p, j, 64);
-    const uint16_t* vr = vbase + (size_t)j * HD + lane * DPL;
-    if constexpr (DPL == 2) {
-      const uint32_t w = *reinterpret_cast<const uint32_t*>(vr);
-      o[0] = fmaf(pj, to_f32<DT>((uint16_t)(w & 0xffff)), o[0]);
-      o[1] = fmaf(pj, to_f32<DT>((uint16_t)(w >> 16)), o[1]);
-    } else {
+    const float pj = pw[j];
+    const uint16_t* vr = Vs + j * HD + lane * DPL;
 #pragma unroll
-      for (int d = 0; d < DPL; ++d) o[d] = fmaf(pj, to_f32<DT>(vr[d]), o[d]);
-    }
+    for (int d = 0; d < DPL; ++d) o[d] = fmaf(pj, to_f32<DT>(vr[d]), o[d]);
   }
+
+  if (ns == 1) {  // whole context in this split: finish here
+    const float inv = 1.f / l;
+#pragma unroll
+    for (int d = 0; d < DPL; ++d) out[(size_t)h * HD + lane * DPL + d] = from_f32<DT>(o[d] * inv);
+    return;
+  }
+
   float* dst = part + ((size_t)h * nsplit + s) * (HD + 2);
   if (lane == 0) { dst[0] = m; dst[1] = l; }
 #pragma unroll
   for (int d = 0; d < DPL; ++d) dst[2 + lane * DPL + d] = o[d];
-}
 
-template <int DT, int HD>
-__global__ void attn_combine_kernel(const float* __restrict__ part,
-                                    const int* __restrict__ pos_ptr, int nsplit,
-                                    uint16_t* __restrict__ out) {
-  constexpr int DPL = HD / 64;
-  const int h = blockIdx.x, lane = threadIdx.x;
-  const int Tk = *pos_ptr + 1;
-  const int ns = (Tk + kKeysPerSplit - 1) / kKeysPerSplit;
+  // publish: stores -> vmcnt(0) -> barrier -> release(agent) -> ticket
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned int t =
+        __hip_atomic_fetch_add(&tickets[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned int last = (t == (unsigned int)(ns - 1)) ? 1u : 0u;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      tickets[g] = 0u;  // re-arm for the next launch
+    }
+    last_flag = last;
+  }
+  __syncthreads();
+  if (!last_flag) return;
+
+  // combine all ns partials of this wave's head
   const float* src = part + (size_t)h * nsplit * (HD + 2);
   float M = -INFINITY;
-  for (int s = 0; s < ns; ++s) M = fmaxf(M, src[s * (HD + 2)]);
-  float L = 0.f, o[DPL];
+  for (int t = 0; t < ns; ++t) M = fmaxf(M, src[t * (HD + 2)]);
+  float L = 0.f, acc[DPL];
 #pragma unroll
-  for (int d = 0; d < DPL; ++d) o[d] = 0.f;
-  for (int s = 0; s < ns; ++s) {
-    const float* ps = src + s * (HD + 2);
-    const float w = __expf(ps[0] - M);
-    L = fmaf(w, ps[1], L);
+  for (int d = 0; d < DPL; ++d) acc[d] = 0.f;
+#pragma unroll 4
+  for (int t = 0; t < ns; ++t) {
+    const float* pt = src + t * (HD + 2);
+    const float w = __expf(pt[0] - M);
+    L = fmaf(w, pt[1], L);
 #pragma unroll
-    for (int d = 0; d < DPL; ++d) o[d] = fmaf(w, ps[2 + lane * DPL + d], o[d]);
+    for (int d = 0; d < DPL; ++d) acc[d] = fmaf(w, pt[2 + lane * DPL + d], acc[d]);
   }
   const float inv = 1.f / L;
 #pragma unroll
-  for (int d = 0; d < DPL; ++d) out[(size_t)h * HD + lane * DPL + d] = from_f32<DT>(o[d] * inv);
+  for (int d = 0; d < DPL; ++d) out[(size_t)h * HD + lane * DPL + d] = from_f32<DT>(acc[d] * inv);
 }
 
 // ---------------------------------------------------------------------------
@@ -195,21 +237,37 @@ using namespace cake;
     else return (int)hipErrorInvalidValue;                                        \
   } while (0)
 
-// part: workspace [nh][nsplit][hd+2] f32, nsplit = ceil(S / 64)
+// part: workspace [nh][nsplit][hd+2] f32, nsplit = ceil(S / 64);
+// tickets: [nkv] u32, zero-initialised once (the kernel re-arms them).
+template <int DT, int HD>
+static int launch_decode(int n_rep, dim3 grid, hipStream_t st, const float* q, const void* kc,
+                         const void* vc, const int* pos, int S, float scale, float* part,
+                         int nsplit, unsigned int* tickets, void* out) {
+#define CAKE_DEC(NR)                                                                         \
+  hipLaunchKernelGGL((attn_decode_kernel<DT, HD, NR>), grid, dim3(64 * NR), 0, st, q,        \
+                     (const uint16_t*)kc, (const uint16_t*)vc, pos, S, scale, part, nsplit,  \
+                     tickets, (uint16_t*)out)
+  switch (n_rep) {
+    case 1: CAKE_DEC(1); break;
+    case 2: CAKE_DEC(2); break;
+    case 4: CAKE_DEC(4); break;
+    case 8: CAKE_DEC(8); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef CAKE_DEC
+  return (int)hipGetLastError();
+}
+
 CAKE_API int cake_attn_decode(int dt, const float* q, const void* kc, const void* vc,
                               const int* pos, int S, int nh, int nkv, int hd, float scale,
-                              float* part, void* out, hipStream_t st) {
+                              float* part, unsigned int* tickets, void* out, hipStream_t st) {
   const int n_rep = nh / nkv;
   if (nh % nkv || n_rep > 8) return (int)hipErrorInvalidValue;
   const int nsplit = (S + kKeysPerSplit - 1) / kKeysPerSplit;
-  DISPATCH_DT_HD(dt, hd, {
-    hipLaunchKernelGGL((attn_decode_kernel<DT, HD>), dim3(nkv, nsplit), dim3(64 * n_rep), 0,
-                       st, q, (const uint16_t*)kc, (const uint16_t*)vc, pos, S, nkv, n_rep,
-                       scale, part, nsplit);
-    hipLaunchKernelGGL((attn_combine_kernel<DT, HD>), dim3(nh), dim3(64), 0, st, part, pos,
-                       nsplit, (uint16_t*)out);
-  });
-  return (int)hipGetLastError();
+  const dim3 grid(nkv, nsplit);
+  DISPATCH_DT_HD(dt, hd, return (launch_decode<DT, HD>(n_rep, grid, st, q, kc, vc, pos, S, scale,
+                                                       part, nsplit, tickets, out)));
+  return (int)hipErrorInvalidValue;
 }
 
 CAKE_API int cake_attn_prefill(int dt, const void* q, const void* kc, const void* vc,

@@ -84,36 +84,74 @@ __device__ __forceinline__ void load_x8(const void* xs, int chunk, float* o) {
 // ---------------------------------------------------------------------------
 // core: one wave, two rows, dot with the staged x.  U = 16-byte chunks per row
 // in flight per lane per iteration (2*U loads outstanding).
+//
+// The first batch of a wave's first row pair is issued BEFORE the x prologue
+// (rmsnorm / x staging) so HBM latency overlaps the prologue (PairPrefetch).
 // ---------------------------------------------------------------------------
+template <int U>
+struct PairPrefetch {
+  uint4 va[U], vb[U];
+  bool valid = false;
+};
+
+template <int U>
+__device__ __forceinline__ void prefetch_pair(const uint16_t* wa, const uint16_t* wb, int K,
+                                              PairPrefetch<U>& pf) {
+  const int lane = threadIdx.x & 63;
+  if ((K >> 3) < 64 * U) return;  // too short for a full batch: no prefetch
+  const uint4* a4 = reinterpret_cast<const uint4*>(wa);
+  const uint4* b4 = reinterpret_cast<const uint4*>(wb);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    pf.va[u] = ld_nt16(a4 + u * 64 + lane);
+    pf.vb[u] = ld_nt16(b4 + u * 64 + lane);
+  }
+  pf.valid = true;
+}
+
+template <int DT, bool XF32, int U>
+__device__ __forceinline__ void consume_batch(const void* xs, int c0, const uint4 (&va)[U],
+                                              const uint4 (&vb)[U], float& acc_a, float& acc_b) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    float xv[8], fa[8], fb[8];
+    load_x8<DT, XF32>(xs, c0 + u * 64 + lane, xv);
+    unpack8<DT>(va[u], fa);
+    unpack8<DT>(vb[u], fb);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      acc_a = fmaf(fa[e], xv[e], acc_a);
+      acc_b = fmaf(fb[e], xv[e], acc_b);
+    }
+  }
+}
+
 template <int DT, bool XF32, int U>
 __device__ __forceinline__ void dot_pair(const uint16_t* __restrict__ wa,
                                          const uint16_t* __restrict__ wb,
-                                         const void* xs, int K, float& da, float& db) {
+                                         const void* xs, int K, float& da, float& db,
+                                         PairPrefetch<U>* pf = nullptr) {
   const int lane = threadIdx.x & 63;
   const int nch = K >> 3;  // 16-byte chunks per row
   const uint4* a4 = reinterpret_cast<const uint4*>(wa);
   const uint4* b4 = reinterpret_cast<const uint4*>(wb);
   float acc_a = 0.f, acc_b = 0.f;
   const int full = (nch / (64 * U)) * (64 * U);
-  for (int c0 = 0; c0 < full; c0 += 64 * U) {
+  int c0 = 0;
+  if (pf && pf->valid) {
+    consume_batch<DT, XF32, U>(xs, 0, pf->va, pf->vb, acc_a, acc_b);
+    pf->valid = false;
+    c0 = 64 * U;
+  }
+  for (; c0 < full; c0 += 64 * U) {
     uint4 va[U], vb[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       va[u] = ld_nt16(a4 + c0 + u * 64 + lane);
       vb[u] = ld_nt16(b4 + c0 + u * 64 + lane);
     }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      float xv[8], fa[8], fb[8];
-      load_x8<DT, XF32>(xs, c0 + u * 64 + lane, xv);
-      unpack8<DT>(va[u], fa);
-      unpack8<DT>(vb[u], fb);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        acc_a = fmaf(fa[e], xv[e], acc_a);
-        acc_b = fmaf(fb[e], xv[e], acc_b);
-      }
-    }
+    consume_batch<DT, XF32, U>(xs, c0, va, vb, acc_a, acc_b);
   }
   for (int c = full + lane; c < nch; c += 64) {  // tail (small test shapes only)
     float xv[8], fa[8], fb[8];
@@ -149,24 +187,44 @@ struct QkvArgs {
   int S;
 };
 
-template <int DT, int U>
+struct QkvRow {
+  const uint16_t* base;
+  int kind, head, i;  // kind 0=q 1=k 2=v
+  size_t ra;
+};
+
+__device__ __forceinline__ QkvRow qkv_row(const QkvArgs& a, int p) {
+  const int half = a.hd >> 1;
+  const int slot = p / half;
+  QkvRow r;
+  r.i = p - slot * half;
+  if (slot < a.nh) { r.kind = 0; r.head = slot; r.base = a.wq; }
+  else if (slot < a.nh + a.nkv) { r.kind = 1; r.head = slot - a.nh; r.base = a.wk; }
+  else { r.kind = 2; r.head = slot - a.nh - a.nkv; r.base = a.wv; }
+  r.ra = (size_t)r.head * a.hd + r.i;
+  return r;
+}
+
+template <int DT, int U, bool PF>
 __global__ __launch_bounds__(kGemvThreads) void qkv_rope_kernel(QkvArgs a) {
   extern __shared__ float xs[];
-  stage_rmsnorm<DT>(a.resid, a.norm_w, a.eps, a.K, xs);
   const int half = a.hd >> 1;
   const int npairs = (a.nh + 2 * a.nkv) * half;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int p0 = blockIdx.x * kGemvWaves + wave;
+  PairPrefetch<U> pf;
+  if (PF && p0 < npairs) {
+    const QkvRow r = qkv_row(a, p0);
+    prefetch_pair<U>(r.base + r.ra * a.K, r.base + (r.ra + half) * a.K, a.K, pf);
+  }
+  stage_rmsnorm<DT>(a.resid, a.norm_w, a.eps, a.K, xs);
   const int pos = *a.pos;
-  for (int p = blockIdx.x * kGemvWaves + wave; p < npairs; p += gridDim.x * kGemvWaves) {
-    const int slot = p / half, i = p - slot * half;
-    const uint16_t* base;
-    int kind, head;  // 0=q 1=k 2=v
-    if (slot < a.nh) { kind = 0; head = slot; base = a.wq; }
-    else if (slot < a.nh + a.nkv) { kind = 1; head = slot - a.nh; base = a.wk; }
-    else { kind = 2; head = slot - a.nh - a.nkv; base = a.wv; }
-    const size_t ra = (size_t)head * a.hd + i;
+  for (int p = p0; p < npairs; p += gridDim.x * kGemvWaves) {
+    const QkvRow r = qkv_row(a, p);
+    const int kind = r.kind, head = r.head, i = r.i;
+    const size_t ra = r.ra;
     float da, db;
-    dot_pair<DT, true, U>(base + ra * a.K, base + (ra + half) * a.K, xs, a.K, da, db);
+    dot_pair<DT, true, U>(r.base + ra * a.K, r.base + (ra + half) * a.K, xs, a.K, da, db, &pf);
     if (lane == 0) {
       float oa = da, ob = db;
       if (kind < 2) {
@@ -191,17 +249,20 @@ __global__ __launch_bounds__(kGemvThreads) void qkv_rope_kernel(QkvArgs a) {
 // ---------------------------------------------------------------------------
 // RMSNorm + gate/up + SiLU*mul
 // ---------------------------------------------------------------------------
-template <int DT, int U>
+template <int DT, int U, bool PF>
 __global__ __launch_bounds__(kGemvThreads) void swiglu_kernel(
     const float* __restrict__ resid, const uint16_t* __restrict__ norm_w, float eps,
     const uint16_t* __restrict__ wg, const uint16_t* __restrict__ wu, int K, int I,
     uint16_t* __restrict__ act) {
   extern __shared__ float xs[];
-  stage_rmsnorm<DT>(resid, norm_w, eps, K, xs);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (int j = blockIdx.x * kGemvWaves + wave; j < I; j += gridDim.x * kGemvWaves) {
+  const int j0 = blockIdx.x * kGemvWaves + wave;
+  PairPrefetch<U> pf;
+  if (PF && j0 < I) prefetch_pair<U>(wg + (size_t)j0 * K, wu + (size_t)j0 * K, K, pf);
+  stage_rmsnorm<DT>(resid, norm_w, eps, K, xs);
+  for (int j = j0; j < I; j += gridDim.x * kGemvWaves) {
     float g, u;
-    dot_pair<DT, true, U>(wg + (size_t)j * K, wu + (size_t)j * K, xs, K, g, u);
+    dot_pair<DT, true, U>(wg + (size_t)j * K, wu + (size_t)j * K, xs, K, g, u, &pf);
     if (lane == 0) act[j] = from_f32<DT>(silu(g) * u);
   }
 }
@@ -210,19 +271,23 @@ __global__ __launch_bounds__(kGemvThreads) void swiglu_kernel(
 // out (+)= W x   with 16-bit x: o_proj / down_proj (accumulate into the f32
 // residual stream) — or plain f32 output.
 // ---------------------------------------------------------------------------
-template <int DT, int U, bool ACCUM>
+template <int DT, int U, bool PF, bool ACCUM>
 __global__ __launch_bounds__(kGemvThreads) void gemv_x16_kernel(
     const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, int K, int N,
     float* __restrict__ out) {
   extern __shared__ float smem[];
   uint16_t* xs = reinterpret_cast<uint16_t*>(smem);
-  stage_plain16(x, K, xs);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int npairs = (N + 1) >> 1;
-  for (int p = blockIdx.x * kGemvWaves + wave; p < npairs; p += gridDim.x * kGemvWaves) {
+  const int p0 = blockIdx.x * kGemvWaves + wave;
+  PairPrefetch<U> pf;
+  if (PF && p0 < npairs)
+    prefetch_pair<U>(w + (size_t)(2 * p0) * K, w + (size_t)min(2 * p0 + 1, N - 1) * K, K, pf);
+  stage_plain16(x, K, xs);
+  for (int p = p0; p < npairs; p += gridDim.x * kGemvWaves) {
     const int ra = 2 * p, rb = min(2 * p + 1, N - 1);
     float da, db;
-    dot_pair<DT, false, U>(w + (size_t)ra * K, w + (size_t)rb * K, xs, K, da, db);
+    dot_pair<DT, false, U>(w + (size_t)ra * K, w + (size_t)rb * K, xs, K, da, db, &pf);
     if (lane == 0) {
       if (ACCUM) out[ra] += da; else out[ra] = da;
       if (2 * p + 1 < N) { if (ACCUM) out[rb] += db; else out[rb] = db; }
@@ -231,18 +296,22 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_x16_kernel(
 }
 
 // RMSNorm(f32 row) then f32 output: the lm_head.
-template <int DT, int U>
+template <int DT, int U, bool PF>
 __global__ __launch_bounds__(kGemvThreads) void gemv_norm_f32_kernel(
     const float* __restrict__ resid, const uint16_t* __restrict__ norm_w, float eps,
     const uint16_t* __restrict__ w, int K, int N, float* __restrict__ out) {
   extern __shared__ float xs[];
-  stage_rmsnorm<DT>(resid, norm_w, eps, K, xs);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int npairs = (N + 1) >> 1;
-  for (int p = blockIdx.x * kGemvWaves + wave; p < npairs; p += gridDim.x * kGemvWaves) {
+  const int p0 = blockIdx.x * kGemvWaves + wave;
+  PairPrefetch<U> pf;
+  if (PF && p0 < npairs)
+    prefetch_pair<U>(w + (size_t)(2 * p0) * K, w + (size_t)min(2 * p0 + 1, N - 1) * K, K, pf);
+  stage_rmsnorm<DT>(resid, norm_w, eps, K, xs);
+  for (int p = p0; p < npairs; p += gridDim.x * kGemvWaves) {
     const int ra = 2 * p, rb = min(2 * p + 1, N - 1);
     float da, db;
-    dot_pair<DT, true, U>(w + (size_t)ra * K, w + (size_t)rb * K, xs, K, da, db);
+    dot_pair<DT, true, U>(w + (size_t)ra * K, w + (size_t)rb * K, xs, K, da, db, &pf);
     if (lane == 0) {
       out[ra] = da;
       if (2 * p + 1 < N) out[rb] = db;
@@ -250,9 +319,17 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_norm_f32_kernel(
   }
 }
 
-static inline int grid_for(int npairs) {
+// Launch geometry per kernel kind (tunable at run time; defaults from the
+// rocprofv3-measured sweep in profiles/): U = chunks in flight per row,
+// PF = prefetch the first weight batch before the x prologue, MB = grid cap.
+struct GemvTune { int U, PF, MB; };
+enum GemvKind { kQkv = 0, kSwiglu = 1, kX16 = 2, kNormF32 = 3, kNumKinds = 4 };
+// measured: profiles/r1_gemv_tune_8b.txt (lm_head 7.0 TB/s at 256 blocks)
+static GemvTune g_tune[kNumKinds] = {{8, 0, 1024}, {2, 0, 512}, {4, 0, 1024}, {4, 0, 256}};
+
+static inline int grid_for(int npairs, int max_blocks) {
   int g = (npairs + kGemvWaves - 1) / kGemvWaves;
-  return g < kGemvMaxBlocks ? g : kGemvMaxBlocks;
+  return g < max_blocks ? g : max_blocks;
 }
 
 }  // namespace cake
@@ -266,6 +343,22 @@ using namespace cake;
     else return (int)hipErrorInvalidValue;         \
   } while (0)
 
+// Expand BODY for the run-time (U, PF) choice.
+#define DISPATCH_TUNE(t, ...)                                                        \
+  do {                                                                               \
+    if ((t).U == 2 && !(t).PF) { constexpr int U = 2; constexpr bool PF = false; __VA_ARGS__; } \
+    else if ((t).U == 8 && !(t).PF) { constexpr int U = 8; constexpr bool PF = false; __VA_ARGS__; } \
+    else if ((t).U == 4 && (t).PF) { constexpr int U = 4; constexpr bool PF = true; __VA_ARGS__; } \
+    else { constexpr int U = 4; constexpr bool PF = false; __VA_ARGS__; }            \
+  } while (0)
+
+CAKE_API int cake_gemv_set_tuning(int kind, int U, int prefetch, int max_blocks) {
+  if (kind < 0 || kind >= kNumKinds || (U != 2 && U != 4 && U != 8) || max_blocks < 1)
+    return (int)hipErrorInvalidValue;
+  g_tune[kind] = GemvTune{U, prefetch ? 1 : 0, max_blocks};
+  return 0;
+}
+
 CAKE_API int cake_qkv_rope(int dt, const float* resid, const void* norm_w, float eps,
                            const void* wq, const void* wk, const void* wv, int K, int nh,
                            int nkv, int hd, const float* inv_freq, const int* pos,
@@ -277,8 +370,10 @@ CAKE_API int cake_qkv_rope(int dt, const float* resid, const void* norm_w, float
             q_out, (uint16_t*)kcache, (uint16_t*)vcache, S};
   const int npairs = (nh + 2 * nkv) * (hd / 2);
   const size_t lds = (size_t)K * sizeof(float);
-  DISPATCH_DT(dt, hipLaunchKernelGGL((qkv_rope_kernel<DT, 4>), dim3(grid_for(npairs)),
-                                     dim3(kGemvThreads), lds, st, a));
+  const GemvTune t = g_tune[kQkv];
+  DISPATCH_DT(dt, DISPATCH_TUNE(t, hipLaunchKernelGGL((qkv_rope_kernel<DT, U, PF>),
+                                                      dim3(grid_for(npairs, t.MB)),
+                                                      dim3(kGemvThreads), lds, st, a)));
   return (int)hipGetLastError();
 }
 
@@ -287,10 +382,12 @@ CAKE_API int cake_swiglu(int dt, const float* resid, const void* norm_w, float e
                          hipStream_t st) {
   if (K % 8) return (int)hipErrorInvalidValue;
   const size_t lds = (size_t)K * sizeof(float);
-  DISPATCH_DT(dt, hipLaunchKernelGGL((swiglu_kernel<DT, 4>), dim3(grid_for(I)),
-                                     dim3(kGemvThreads), lds, st, resid,
-                                     (const uint16_t*)norm_w, eps, (const uint16_t*)wg,
-                                     (const uint16_t*)wu, K, I, (uint16_t*)act));
+  const GemvTune t = g_tune[kSwiglu];
+  DISPATCH_DT(dt, DISPATCH_TUNE(t, hipLaunchKernelGGL((swiglu_kernel<DT, U, PF>),
+                                                      dim3(grid_for(I, t.MB)), dim3(kGemvThreads),
+                                                      lds, st, resid, (const uint16_t*)norm_w, eps,
+                                                      (const uint16_t*)wg, (const uint16_t*)wu, K,
+                                                      I, (uint16_t*)act)));
   return (int)hipGetLastError();
 }
 
@@ -298,15 +395,18 @@ CAKE_API int cake_gemv_x16(int dt, const void* x, const void* w, int K, int N, f
                            int accumulate, hipStream_t st) {
   if (K % 8) return (int)hipErrorInvalidValue;
   const size_t lds = (size_t)K * 2;
-  const int g = grid_for((N + 1) / 2);
+  const GemvTune t = g_tune[kX16];
+  const int g = grid_for((N + 1) / 2, t.MB);
   if (accumulate) {
-    DISPATCH_DT(dt, hipLaunchKernelGGL((gemv_x16_kernel<DT, 4, true>), dim3(g),
-                                       dim3(kGemvThreads), lds, st, (const uint16_t*)x,
-                                       (const uint16_t*)w, K, N, out));
+    DISPATCH_DT(dt, DISPATCH_TUNE(t, hipLaunchKernelGGL((gemv_x16_kernel<DT, U, PF, true>),
+                                                        dim3(g), dim3(kGemvThreads), lds, st,
+                                                        (const uint16_t*)x, (const uint16_t*)w, K,
+                                                        N, out)));
   } else {
-    DISPATCH_DT(dt, hipLaunchKernelGGL((gemv_x16_kernel<DT, 4, false>), dim3(g),
-                                       dim3(kGemvThreads), lds, st, (const uint16_t*)x,
-                                       (const uint16_t*)w, K, N, out));
+    DISPATCH_DT(dt, DISPATCH_TUNE(t, hipLaunchKernelGGL((gemv_x16_kernel<DT, U, PF, false>),
+                                                        dim3(g), dim3(kGemvThreads), lds, st,
+                                                        (const uint16_t*)x, (const uint16_t*)w, K,
+                                                        N, out)));
   }
   return (int)hipGetLastError();
 }
@@ -315,9 +415,11 @@ CAKE_API int cake_gemv_norm_f32(int dt, const float* resid, const void* norm_w, 
                                 const void* w, int K, int N, float* out, hipStream_t st) {
   if (K % 8) return (int)hipErrorInvalidValue;
   const size_t lds = (size_t)K * sizeof(float);
-  DISPATCH_DT(dt, hipLaunchKernelGGL((gemv_norm_f32_kernel<DT, 4>),
-                                     dim3(grid_for((N + 1) / 2)), dim3(kGemvThreads), lds,
-                                     st, resid, (const uint16_t*)norm_w, eps,
-                                     (const uint16_t*)w, K, N, out));
+  const GemvTune t = g_tune[kNormF32];
+  DISPATCH_DT(dt, DISPATCH_TUNE(t, hipLaunchKernelGGL((gemv_norm_f32_kernel<DT, U, PF>),
+                                                      dim3(grid_for((N + 1) / 2, t.MB)),
+                                                      dim3(kGemvThreads), lds, st, resid,
+                                                      (const uint16_t*)norm_w, eps,
+                                                      (const uint16_t*)w, K, N, out)));
   return (int)hipGetLastError();
 }

@@ -56,6 +56,7 @@ class DecodeBuffers:
         self.act = torch.zeros(I, device=device, dtype=dtype)
         nsplit = (max_seq + 63) // 64
         self.part = torch.zeros(nh * nsplit * (hd + 2), device=device, dtype=f32)
+        self.tickets = torch.zeros(cfg.num_key_value_heads, device=device, dtype=i32)
         self.pos = torch.zeros(1, device=device, dtype=i32)
         if with_head:
             self.logits = torch.zeros(cfg.vocab_size, device=device, dtype=f32)
@@ -152,7 +153,8 @@ class LayerStack:
             kc, vc = kv.k[s], kv.v[s]
             K.qkv_rope(bufs.resid, w.ln1, cfg.rms_norm_eps, w.wq, w.wk, w.wv, self.inv_freq,
                        bufs.pos, bufs.q, kc, vc)
-            K.attn_decode(bufs.q, kc, vc, bufs.pos, self.scale, bufs.part, bufs.attn_out)
+            K.attn_decode(bufs.q, kc, vc, bufs.pos, self.scale, bufs.part, bufs.tickets,
+                          bufs.attn_out)
             K.gemv(bufs.attn_out, w.wo, bufs.resid, accumulate=True)
             K.swiglu(bufs.resid, w.ln2, cfg.rms_norm_eps, w.wg, w.wu, bufs.act)
             K.gemv(bufs.act, w.wd, bufs.resid, accumulate=True)
@@ -169,7 +171,8 @@ class LayerStack:
         cfg = self.cfg
         K.qkv_rope(bufs.resid, w.ln1, cfg.rms_norm_eps, w.wq, w.wk, w.wv, self.inv_freq,
                    bufs.pos, bufs.q, kc, vc)
-        K.attn_decode(bufs.q, kc, vc, bufs.pos, self.scale, bufs.part, bufs.attn_out)
+        K.attn_decode(bufs.q, kc, vc, bufs.pos, self.scale, bufs.part, bufs.tickets,
+                          bufs.attn_out)
         K.gemv(bufs.attn_out, w.wo, bufs.resid, accumulate=True)
         K.swiglu(bufs.resid, w.ln2, cfg.rms_norm_eps, w.wg, w.wu, bufs.act)
         K.gemv(bufs.act, w.wd, bufs.resid, accumulate=True)

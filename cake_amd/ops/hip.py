@@ -109,8 +109,12 @@ def norm_gemv_f32(resid, norm_w, eps, w, out):
                                        _p(out), _stream()), "gemv_norm_f32")
 
 
-def attn_decode(q, kcache, vcache, pos, scale, part, out):
-    """Split-K GQA decode attention for the token at device position `pos`."""
+def attn_decode(q, kcache, vcache, pos, scale, part, tickets, out):
+    """Split-K GQA decode attention for the token at device position `pos`.
+
+    part: f32 workspace (:func:`attn_workspace_numel`); tickets: int32 [nkv],
+    zero-initialised once and re-armed by the kernel itself.
+    """
     nkv, S, hd = kcache.shape
     nh = q.numel() // hd
     nsplit = (S + 63) // 64
@@ -120,10 +124,12 @@ def attn_decode(q, kcache, vcache, pos, scale, part, out):
     _req(pos, "pos", dtype=torch.int32, numel=1)
     _req(part, "part", dtype=torch.float32, numel=nh * nsplit * (hd + 2))
     _req(out, "out", dtype=kcache.dtype, numel=nh * hd)
-    if hd not in (64, 128) or nh % nkv or nh // nkv > 8:
+    _req(tickets, "tickets", dtype=torch.int32, numel=nkv)
+    if hd not in (64, 128) or nh % nkv or (nh // nkv) not in (1, 2, 4, 8):
         raise ValueError(f"unsupported attention shape nh={nh} nkv={nkv} hd={hd}")
     check(kernels().cake_attn_decode(_dt(kcache), _p(q), _p(kcache), _p(vcache), _p(pos), S, nh,
-                                     nkv, hd, float(scale), _p(part), _p(out), _stream()),
+                                     nkv, hd, float(scale), _p(part), _p(tickets), _p(out),
+                                     _stream()),
           "attn_decode")
 
 
@@ -231,3 +237,12 @@ def push_token(src, tok, hist, hist_len, pos):
         _req(t, n, dtype=torch.int32)
     check(kernels().cake_push_token(_p(src), _p(tok), _p(hist), _p(hist_len), _p(pos),
                                     hist.numel(), _stream()), "push_token")
+
+
+GEMV_KINDS = {"qkv": 0, "swiglu": 1, "x16": 2, "norm_f32": 3}
+
+
+def set_gemv_tuning(kind: str, U: int = 4, prefetch: bool = False, max_blocks: int = 1024) -> None:
+    """Select the decode-GEMV launch geometry for one kernel kind (see gemv.hip)."""
+    check(kernels().cake_gemv_set_tuning(GEMV_KINDS[kind], int(U), int(prefetch), int(max_blocks)),
+          "gemv_set_tuning")

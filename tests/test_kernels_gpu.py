@@ -106,7 +106,11 @@ def test_attn_decode(cuda, dt, nh, nkv, hd, pos):
     p = torch.tensor([pos], dtype=torch.int32, device=cuda)
     part = torch.empty(K_.attn_workspace_numel(nh, hd, S), device=cuda)
     out = torch.empty(nh * hd, device=cuda, dtype=dt)
-    K_.attn_decode(q, kc, vc, p, 1 / math.sqrt(hd), part, out)
+    tickets = torch.zeros(nkv, dtype=torch.int32, device=cuda)
+    for _ in range(2):  # second call checks the tickets were re-armed
+        out.zero_()
+        K_.attn_decode(q, kc, vc, p, 1 / math.sqrt(hd), part, tickets, out)
+        assert int(tickets.abs().sum()) == 0
     Tk = pos + 1
     ref = R.attention(q.view(1, nh, hd), kc[:, :Tk].transpose(0, 1), vc[:, :Tk].transpose(0, 1),
                       pos).reshape(-1)
