@@ -44,6 +44,9 @@ def _args(argv=None):
     ap.add_argument("--repeat-penalty", type=float, default=1.1)
     ap.add_argument("--repeat-last-n", type=int, default=128)
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--streams", type=int, default=0,
+                    help="N>1: concurrent sequences in the pipeline (default = N; 1 = cake's "
+                         "single-sequence pipeline)")
     return ap.parse_args(argv)
 
 
@@ -66,9 +69,10 @@ def _emit(a, value, ms, p50, p99, n, extra):
         "data": "synthetic (random-init weights, synthetic prompt ids, EOS ignored)",
         "config": {"model": {"llama3-8b": "Llama-3-8B", "llama3-70b": "Llama-3-70B",
                              "tiny": "tiny"}[a.model],
-                   "global_batch": 1, "seq_len": a.prompt_len + a.warmup + a.steps,
+                   "global_batch": extra.get("streams", 1), "seq_len": a.prompt_len + a.warmup + a.steps,
                    "prompt_len": a.prompt_len,
-                   "parallelism": "single" if n == 1 else f"pp{n} (layer-sharded, RCCL p2p)",
+                   "parallelism": "single" if n == 1 else
+                   f"pp{n} (layer-sharded, RCCL p2p, {extra.get('streams', 1)} streams)",
                    "decode": "greedy, repeat_penalty %.2f last_n %d" % (a.repeat_penalty,
                                                                         a.repeat_last_n)},
     }

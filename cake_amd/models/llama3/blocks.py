@@ -47,17 +47,18 @@ class KVCache:
 class DecodeBuffers:
     """Device-resident state of a batch-1 decode step (graph-stable addresses)."""
 
-    def __init__(self, cfg: LlamaConfig, max_seq: int, device, dtype, with_head: bool):
+    def __init__(self, cfg: LlamaConfig, max_seq: int, device, dtype, with_head: bool,
+                 resid: torch.Tensor | None = None, pos: torch.Tensor | None = None):
         H, I, hd, nh = cfg.hidden_size, cfg.intermediate_size, cfg.head_dim, cfg.num_attention_heads
         f32, i32 = torch.float32, torch.int32
-        self.resid = torch.zeros(H, device=device, dtype=f32)
+        self.resid = torch.zeros(H, device=device, dtype=f32) if resid is None else resid
         self.q = torch.zeros(nh * hd, device=device, dtype=f32)
         self.attn_out = torch.zeros(nh * hd, device=device, dtype=dtype)
         self.act = torch.zeros(I, device=device, dtype=dtype)
         nsplit = (max_seq + 63) // 64
         self.part = torch.zeros(nh * nsplit * (hd + 2), device=device, dtype=f32)
         self.tickets = torch.zeros(cfg.num_key_value_heads, device=device, dtype=i32)
-        self.pos = torch.zeros(1, device=device, dtype=i32)
+        self.pos = torch.zeros(1, device=device, dtype=i32) if pos is None else pos
         if with_head:
             self.logits = torch.zeros(cfg.vocab_size, device=device, dtype=f32)
             self.tok = torch.zeros(1, device=device, dtype=i32)

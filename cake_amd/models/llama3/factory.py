@@ -30,7 +30,7 @@ def default_backend(device: torch.device, dtype: torch.dtype) -> str:
 
 
 def random_stack(cfg: LlamaConfig, layers: list[int], device, dtype, max_seq: int = MAX_SEQ_LEN,
-                 backend: str | None = None, seed: int = 0) -> LayerStack:
+                 backend: str | None = None, seed: int = 0, max_sessions: int = 8) -> LayerStack:
     device = torch.device(device)
     gen = torch.Generator(device=device)
     gen.manual_seed(seed)
@@ -38,7 +38,15 @@ def random_stack(cfg: LlamaConfig, layers: list[int], device, dtype, max_seq: in
     for li in layers:
         gen.manual_seed(seed * 1000003 + li)
         weights[li] = BlockWeights.random(cfg, device, dtype, gen)
-    return LayerStack(cfg, weights, device, dtype, max_seq, backend or default_backend(device, dtype))
+    return LayerStack(cfg, weights, device, dtype, max_seq, backend or default_backend(device, dtype),
+                      max_sessions=max_sessions)
+
+
+def random_head(cfg: LlamaConfig, device, dtype, seed: int = 0) -> HeadWeights:
+    device = torch.device(device)
+    gen = torch.Generator(device=device)
+    gen.manual_seed(seed * 7919 + 17)
+    return HeadWeights.random(cfg, device, dtype, gen)
 
 
 def random_model(cfg: LlamaConfig | str, device, dtype, max_seq: int = MAX_SEQ_LEN,
@@ -50,10 +58,7 @@ def random_model(cfg: LlamaConfig | str, device, dtype, max_seq: int = MAX_SEQ_L
     if local_layers is None:
         local_layers = [li for li in range(cfg.num_hidden_layers) if li not in (remote or {})]
     stack = random_stack(cfg, local_layers, device, dtype, max_seq, backend, seed)
-    gen = torch.Generator(device=device)
-    gen.manual_seed(seed * 7919 + 17)
-    head = HeadWeights.random(cfg, device, dtype, gen)
-    return LlamaModel(cfg, head, stack, remote)
+    return LlamaModel(cfg, random_head(cfg, device, dtype, seed), stack, remote)
 
 
 def load_stack(model_dir: str | Path, cfg: LlamaConfig, layers: list[int], device, dtype,

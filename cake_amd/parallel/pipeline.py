@@ -1,0 +1,364 @@
+"""Layer-sharded decode pipeline over RCCL point-to-point (one process per GPU).
+
+This is the MI355X data plane for cake's master → worker → master hop
+(cake-core/src/models/llama3/llama.rs:95-114 and client.rs:116-124, which send a
+``Batch{x, [(layer, index_pos, block_idx)]}`` frame over TCP and copy the
+tensor device→host→device on both ends, proto/message.rs:22-38).  Here:
+
+* The placement is a list of *runs* (consecutive layers with one owner rank,
+  i.e. contiguous-block batching); rank 0 is the master (embedding, ln_f,
+  lm_head, sampling) and may own runs too.
+* A hop is ONE device-to-device RCCL send/recv of a message
+  ``[hidden (H f32) | header (16 x int32)]`` — header word 0 is the position,
+  word 1 the stream (sequence) id — so the receiving rank's hipGraph reads
+  the position straight out of the received buffer: no host round trip, no
+  descriptor message for decode.  Prefill (T>1) sends an int32 header, then
+  the [T, H] block.
+* ``streams`` independent sequences can be in flight: while rank r runs
+  stream s, rank r-1 already runs stream s+1 (the reference's global API lock
+  allows one).  With streams = 1 it is exactly cake's sequential pipeline.
+* Backends: ``hip`` (graph per stream per run, RCCL via torch.distributed
+  backend "nccl") or ``torch`` (eager reference math; gloo on CPU for tests).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+from ..models.llama3.blocks import DecodeBuffers, LayerStack
+from ..models.llama3.config import LlamaConfig
+from ..models.llama3.weights import HeadWeights
+from ..ops import reference as R
+
+HDR = 16          # int32 header words appended to each hop message
+H_POS, H_STREAM, H_T, H_FLAGS = 0, 1, 2, 3
+FLAG_RESET = 1
+
+
+def shard_layers(num_layers: int, world: int) -> list[list[int]]:
+    """Contiguous near-equal shards (rank r gets layers [a_r, b_r))."""
+    base, extra = divmod(num_layers, world)
+    out, start = [], 0
+    for r in range(world):
+        n = base + (1 if r < extra else 0)
+        out.append(list(range(start, start + n)))
+        start += n
+    return out
+
+
+@dataclass
+class PipeRun:
+    owner: int
+    layers: list[int]
+
+
+def plan_from_owners(owners: list[int]) -> list[PipeRun]:
+    """owners[l] = rank executing layer l -> runs of consecutive equal owners."""
+    runs: list[PipeRun] = []
+    for li, r in enumerate(owners):
+        if runs and runs[-1].owner == r:
+            runs[-1].layers.append(li)
+        else:
+            runs.append(PipeRun(r, [li]))
+    return runs
+
+
+class _Stream:
+    """Per-sequence device state on one rank."""
+
+    def __init__(self, eng: "PipelineEngine", sid: int):
+        H = eng.cfg.hidden_size
+        self.sid = sid
+        self.msg = torch.zeros(H + HDR, device=eng.device, dtype=torch.float32)
+        self.resid = self.msg[:H]
+        self.hdr = self.msg[H:].view(torch.int32)
+        self.bufs = DecodeBuffers(eng.cfg, eng.stack.max_seq, eng.device, eng.stack.dtype,
+                                  with_head=eng.is_master, resid=self.resid,
+                                  pos=self.hdr[H_POS:H_POS + 1])
+        self.graphs: dict[str, torch.cuda.CUDAGraph] = {}
+        self.send_work = None
+        self.host_tokens: list[int] = []   # torch backend bookkeeping (master)
+        self.host_pos = 0
+
+
+class PipelineEngine:
+    def __init__(self, cfg: LlamaConfig, stack: LayerStack, owners: list[int], rank: int,
+                 world: int, streams: int = 1, head: HeadWeights | None = None,
+                 repeat_penalty: float = 1.0, repeat_last_n: int = 128, use_graph: bool = True,
+                 group=None):
+        self.cfg, self.stack, self.rank, self.world = cfg, stack, rank, world
+        self.device = stack.device
+        self.is_master = rank == 0
+        self.head = head
+        if self.is_master and head is None:
+            raise ValueError("rank 0 (master) needs the head weights")
+        self.runs = plan_from_owners(owners)
+        self.my_runs = [j for j, r in enumerate(self.runs) if r.owner == rank]
+        for j in self.my_runs:
+            missing = [li for li in self.runs[j].layers if li not in stack.weights]
+            if missing:
+                raise ValueError(f"rank {rank} lacks weights for layers {missing}")
+        self.penalty, self.last_n = float(repeat_penalty), int(repeat_last_n)
+        self.hip = stack.backend == "hip"
+        self.use_graph = use_graph and self.hip
+        self.group = group
+        if stack.max_sessions < streams:
+            stack.max_sessions = streams
+        self.streams = [_Stream(self, s) for s in range(streams)]
+
+    # ------------------------------------------------------------------ hop helpers
+    def _prev(self, j: int) -> int:
+        return self.runs[j - 1].owner if j > 0 else 0
+
+    def _next(self, j: int) -> int:
+        return self.runs[j + 1].owner if j + 1 < len(self.runs) else 0
+
+    def _first_dst(self) -> int:
+        """Rank the master sends a freshly embedded token to."""
+        return self.runs[0].owner if self.runs[0].owner != 0 else self._next(0)
+
+    def _final_src(self) -> int:
+        """Rank the master receives the finished hidden state from."""
+        last = len(self.runs) - 1
+        if self.runs[last].owner != 0:
+            return self.runs[last].owner
+        return self.runs[last - 1].owner if last > 0 else 0
+
+    def _send(self, t: torch.Tensor, dst: int):
+        return dist.isend(t, dst, group=self.group)
+
+    def _recv(self, t: torch.Tensor, src: int) -> None:
+        dist.irecv(t, src, group=self.group).wait()
+
+    @staticmethod
+    def _wait(work) -> None:
+        if work is not None:
+            work.wait()
+
+    # ------------------------------------------------------------------ master head ops
+    def _embed(self, tokens, out: torch.Tensor) -> None:
+        if self.hip:
+            from ..ops import hip as K
+            K.embed(self.head.embed, tokens, out)
+        else:
+            out.copy_(self.head.embed[tokens.long()].float().view_as(out))
+
+    def _logits(self, row: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        if self.hip:
+            from ..ops import hip as K
+            if out is None:
+                out = torch.empty(self.cfg.vocab_size, device=self.device)
+            K.norm_gemv_f32(row, self.head.norm, self.cfg.rms_norm_eps, self.head.lm_head, out)
+            return out
+        x = R.rms_norm(row, self.head.norm, self.cfg.rms_norm_eps).to(self.stack.dtype)
+        return (x @ self.head.lm_head.t()).float()
+
+    def _select_host(self, st: _Stream, logits: torch.Tensor) -> int:
+        if self.penalty != 1.0:
+            logits = R.apply_repeat_penalty(logits, self.penalty, st.host_tokens[-self.last_n:])
+        return int(torch.argmax(logits))
+
+    def _select_device(self, st: _Stream) -> None:
+        from ..ops import hip as K
+        b = st.bufs
+        if self.penalty != 1.0:
+            K.repeat_penalty(b.logits, b.hist, b.hist_len, self.last_n, self.penalty)
+        K.argmax(b.logits, b.slot)
+        K.finalize_token(b.slot, b.tok, b.hist, b.hist_len, b.pos)
+
+    # ------------------------------------------------------------------ prefill
+    def prefill(self, sid: int, prompt: list[int] | None = None) -> int | None:
+        """Prefill one stream through the pipeline.  Master passes the prompt and
+        gets the first generated token; workers pass nothing."""
+        st = self.streams[sid]
+        H = self.cfg.hidden_size
+        self.stack.reset(sid)
+        if self.is_master:
+            T = len(prompt)
+            ids = torch.tensor(prompt, dtype=torch.int32, device=self.device)
+            h = torch.empty((T, H), device=self.device, dtype=torch.float32)
+            self._embed(ids, h)
+        h_runs = self.runs
+        hdr = torch.zeros(HDR, dtype=torch.int32, device=self.device)
+        if self.is_master and self.runs[0].owner != 0:
+            hdr[H_POS], hdr[H_STREAM], hdr[H_T] = 0, sid, T
+            self._wait(self._send(hdr, self.runs[0].owner))
+            self._wait(self._send(h, self.runs[0].owner))
+        for j, run in enumerate(h_runs):
+            if run.owner != self.rank:
+                continue
+            if not (self.is_master and j == 0):
+                self._recv(hdr, self._prev(j))
+                T = int(hdr[H_T].item())
+                h = torch.empty((T, H), device=self.device, dtype=torch.float32)
+                self._recv(h, self._prev(j))
+            self.stack.forward(h, run.layers, 0, session=sid)
+            nxt = self._next(j)
+            if nxt != self.rank:
+                hdr[H_POS], hdr[H_STREAM], hdr[H_T] = 0, sid, T
+                self._wait(self._send(hdr, nxt))
+                self._wait(self._send(h, nxt))
+        if not self.is_master:
+            return None
+        if self.runs[-1].owner != 0:
+            self._recv(hdr, self._final_src())
+            h = torch.empty((int(hdr[H_T].item()), H), device=self.device, dtype=torch.float32)
+            self._recv(h, self._final_src())
+        T = len(prompt)
+        if self.hip:
+            b = st.bufs
+            b.hist[:T].copy_(ids)
+            b.hist_len.fill_(T)
+            b.pos.fill_(T - 1)
+            b.slot.zero_()
+            self._logits(h[-1].contiguous(), b.logits)
+            self._select_device(st)
+            return int(b.tok.item())
+        st.host_tokens = list(prompt)
+        tok = self._select_host(st, self._logits(h[-1]))
+        st.host_tokens.append(tok)
+        st.host_pos = T
+        st.hdr[H_POS] = T
+        return tok
+
+    # ------------------------------------------------------------------ decode bodies
+    def _body_first(self, st: _Stream) -> None:
+        """Master: embed the stream's token (+ its run 0 layers if it owns run 0)."""
+        if self.hip:
+            from ..ops import hip as K
+            K.embed(self.head.embed, st.bufs.tok, st.resid)
+            if self.runs[0].owner == 0:
+                self.stack.decode_step(st.bufs, self.runs[0].layers, st.sid)
+        else:
+            tok = torch.tensor([st.host_tokens[-1]], dtype=torch.int32, device=self.device)
+            self._embed(tok, st.resid.view(1, -1))
+            if self.runs[0].owner == 0:
+                self.stack.forward(st.resid.view(1, -1), self.runs[0].layers, st.host_pos, st.sid)
+
+    def _body_run(self, st: _Stream, j: int) -> None:
+        if self.hip:
+            self.stack.decode_step(st.bufs, self.runs[j].layers, st.sid)
+        else:
+            pos = int(st.hdr[H_POS].item())
+            self.stack.forward(st.resid.view(1, -1), self.runs[j].layers, pos, st.sid)
+
+    def _body_last(self, st: _Stream) -> None:
+        """Master: (its last run if it owns it) + ln_f/lm_head + token selection."""
+        last = len(self.runs) - 1
+        if self.hip:
+            if self.runs[last].owner == 0 and last > 0:
+                self.stack.decode_step(st.bufs, self.runs[last].layers, st.sid)
+            from ..ops import hip as K
+            K.norm_gemv_f32(st.resid, self.head.norm, self.cfg.rms_norm_eps, self.head.lm_head,
+                            st.bufs.logits)
+            self._select_device(st)
+        else:
+            if self.runs[last].owner == 0 and last > 0:
+                self.stack.forward(st.resid.view(1, -1), self.runs[last].layers, st.host_pos,
+                                   st.sid)
+            tok = self._select_host(st, self._logits(st.resid))
+            st.host_tokens.append(tok)
+            st.host_pos += 1
+            st.hdr[H_POS] = st.host_pos
+
+    def _replay(self, st: _Stream, key: str, fn) -> None:
+        if not self.use_graph:
+            fn()
+            return
+        g = st.graphs.get(key)
+        if g is None:
+            raise RuntimeError("capture() first")
+        g.replay()
+
+    def capture(self) -> None:
+        """Capture one hipGraph per (stream, body) — RCCL hops stay outside."""
+        if not self.use_graph:
+            return
+        for st in self.streams:
+            bodies = self._bodies(st)
+            for key, fn in bodies.items():
+                # warm-up on a scratch copy of the state the body mutates; the
+                # warm-up writes K/V at a scratch position (last cache row) so
+                # the prefilled rows are untouched
+                saved = st.msg.clone()
+                st.hdr[H_POS] = self.stack.max_seq - 1
+                keep = None
+                if self.is_master:
+                    b = st.bufs
+                    keep = [t.clone() for t in (b.tok, b.hist, b.hist_len, b.slot)]
+                s = torch.cuda.Stream()
+                s.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(s):
+                    fn()
+                torch.cuda.current_stream().wait_stream(s)
+                torch.cuda.synchronize()
+                st.msg.copy_(saved)
+                if keep is not None:
+                    for t, v in zip((b.tok, b.hist, b.hist_len, b.slot), keep):
+                        t.copy_(v)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    fn()
+                st.graphs[key] = g
+        torch.cuda.synchronize()
+
+    def _bodies(self, st: _Stream) -> dict:
+        out = {}
+        if self.is_master:
+            out["first"] = lambda st=st: self._body_first(st)
+            out["last"] = lambda st=st: self._body_last(st)
+        for j in self.my_runs:
+            if self.is_master and (j == 0 or j == len(self.runs) - 1):
+                continue
+            out[f"run{j}"] = lambda st=st, j=j: self._body_run(st, j)
+        return out
+
+    # ------------------------------------------------------------------ decode loop
+    def decode(self, rounds: int) -> None:
+        """Every stream generates `rounds` tokens (ignoring EOS)."""
+        single = self.world == 1 or all(r.owner == 0 for r in self.runs)
+        for k in range(rounds):
+            for st in self.streams:
+                if self.is_master:
+                    if single:
+                        self._replay(st, "first", lambda: self._body_first(st))
+                        self._replay(st, "last", lambda: self._body_last(st))
+                        continue
+                    self._wait(st.send_work)
+                    if k > 0:
+                        self._recv(st.msg, self._final_src())
+                        self._replay(st, "last", lambda: self._body_last(st))
+                    self._replay(st, "first", lambda: self._body_first(st))
+                    st.send_work = self._send(st.msg, self._first_dst())
+                self._worker_runs(st)
+        if self.is_master and not single:
+            for st in self.streams:
+                self._wait(st.send_work)
+                st.send_work = None
+                self._recv(st.msg, self._final_src())
+                self._replay(st, "last", lambda: self._body_last(st))
+
+    def _worker_runs(self, st: _Stream) -> None:
+        last = len(self.runs) - 1
+        for j in self.my_runs:
+            if self.is_master and (j == 0 or j == last):
+                continue
+            self._wait(st.send_work)
+            self._recv(st.msg, self._prev(j))
+            self._replay(st, f"run{j}", lambda j=j: self._body_run(st, j))
+            st.send_work = self._send(st.msg, self._next(j))
+
+    def flush(self) -> None:
+        for st in self.streams:
+            self._wait(st.send_work)
+            st.send_work = None
+
+    def tokens(self, sid: int) -> list[int]:
+        """Master: full token history (prompt + generated) of a stream."""
+        st = self.streams[sid]
+        if self.hip:
+            n = int(st.bufs.hist_len.item())
+            return st.bufs.hist[:n].tolist()
+        return list(st.host_tokens)

@@ -62,3 +62,32 @@ def test_device_decoder_matches_host_loop(cuda, use_graph):
     st = run_decode(dec, 11)
     assert [first] + st.tokens == host
     assert len(st.step_ms) == 11 and all(x > 0 for x in st.step_ms)
+
+
+def test_pipeline_engine_single_rank_streams(cuda):
+    """The RCCL pipeline's graph bodies (world=1, 2 streams) == DeviceDecoder per stream."""
+    from cake_amd.models.llama3.decode_loop import run_decode
+    from cake_amd.models.llama3.factory import random_head, random_stack
+    from cake_amd.models.llama3.model import DeviceDecoder
+    from cake_amd.parallel.pipeline import PipelineEngine
+
+    cfg = preset("llama3-8b", num_hidden_layers=3, vocab_size=2048, intermediate_size=1024,
+                 hidden_size=512, num_attention_heads=4, num_key_value_heads=1)
+    prompts = [[5, 6, 7, 8, 9], [100, 3, 3, 12]]
+    expect = []
+    model = random_model(cfg, "cuda:0", torch.bfloat16, max_seq=256, seed=3)
+    for p in prompts:
+        dec = DeviceDecoder(model, repeat_penalty=1.1, repeat_last_n=16, greedy=True)
+        first = dec.start(p)
+        dec.capture()
+        expect.append(p + [first] + run_decode(dec, 9).tokens)
+    stack = random_stack(cfg, list(range(3)), "cuda:0", torch.bfloat16, max_seq=256, seed=3)
+    eng = PipelineEngine(cfg, stack, [0, 0, 0], 0, 1, streams=2,
+                         head=random_head(cfg, "cuda:0", torch.bfloat16, seed=3),
+                         repeat_penalty=1.1, repeat_last_n=16)
+    for s, p in enumerate(prompts):
+        eng.prefill(s, p)
+    eng.capture()
+    eng.decode(9)
+    torch.cuda.synchronize()
+    assert [eng.tokens(0), eng.tokens(1)] == expect
