@@ -44,6 +44,9 @@ def _args(argv=None):
     ap.add_argument("--repeat-penalty", type=float, default=1.1)
     ap.add_argument("--repeat-last-n", type=int, default=128)
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="N>1 transport: nccl (= RCCL over xGMI) or host-staged gloo (tests)")
+    ap.add_argument("--dump-tokens", default=None, help="write generated token ids (JSON)")
     ap.add_argument("--streams", type=int, default=0,
                     help="N>1: concurrent sequences in the pipeline (default = N; 1 = cake's "
                          "single-sequence pipeline)")
@@ -109,6 +112,9 @@ def bench_single(a) -> None:
     st = run_decode(dec, a.steps)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    if a.dump_tokens:
+        with open(a.dump_tokens, "w") as f:
+            json.dump([dec.bufs.hist[:int(dec.bufs.hist_len.item())].tolist()], f)
     _emit(a, a.steps / dt, dt * 1e3 / a.steps, st.percentile(50), st.percentile(99), 1,
           {"ttft_ms_prefill": round(ttft, 3), "graph": not a.no_graph})
 

@@ -104,6 +104,8 @@ class PipelineEngine:
         self.hip = stack.backend == "hip"
         self.use_graph = use_graph and self.hip
         self.group = group
+        # gloo with device tensors (1-GPU multi-process tests): stage via the host
+        self.staged = dist.is_initialized() and dist.get_backend(group) == "gloo"
         if stack.max_sessions < streams:
             stack.max_sessions = streams
         self.streams = [_Stream(self, s) for s in range(streams)]
@@ -127,9 +129,17 @@ class PipelineEngine:
         return self.runs[last - 1].owner if last > 0 else 0
 
     def _send(self, t: torch.Tensor, dst: int):
+        if self.staged and t.is_cuda:
+            host = t.to("cpu")          # gloo moves host memory only: stage through the host
+            return dist.isend(host, dst, group=self.group)
         return dist.isend(t, dst, group=self.group)
 
     def _recv(self, t: torch.Tensor, src: int) -> None:
+        if self.staged and t.is_cuda:
+            host = torch.empty(t.shape, dtype=t.dtype)
+            dist.irecv(host, src, group=self.group).wait()
+            t.copy_(host)
+            return
         dist.irecv(t, src, group=self.group).wait()
 
     @staticmethod

@@ -20,7 +20,11 @@ def bench_pipeline(a, emit) -> None:
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    backend = getattr(a, "dist_backend", "nccl")
+    if backend == "nccl":
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    else:  # gloo: host-staged hops (lets N ranks share one GPU in tests)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     cfg = preset(a.model)
     dtype = parse_dtype(a.dtype)
     shards = shard_layers(cfg.num_hidden_layers, world)
@@ -54,9 +58,13 @@ def bench_pipeline(a, emit) -> None:
     torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
-    dt = torch.tensor([time.perf_counter() - t0], device=dev)
+    dt = torch.tensor([time.perf_counter() - t0], device=dev if backend == "nccl" else "cpu")
     dist.all_reduce(dt, op=dist.ReduceOp.MAX)
     dt = float(dt.item())
+    if rank == 0 and getattr(a, "dump_tokens", None):
+        import json
+        with open(a.dump_tokens, "w") as f:
+            json.dump([eng.tokens(s) for s in range(streams)], f)
     if rank == 0:
         ms_round = dt * 1e3 / a.steps
         emit(a, streams * a.steps / dt, ms_round, ms_round, ms_round, world,
