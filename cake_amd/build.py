@@ -69,9 +69,19 @@ def _compile_cpp(src: Path, force: bool, extra: list[str] | None = None) -> Path
     headers = sorted((CSRC / "runtime").glob("*.h"))
     if force or _newer(src, headers, out):
         _run([CXX, "-O2", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
-              *(extra or []), "-c", str(src), "-o", str(out)])
+              "-fvisibility=hidden", *(extra or []), "-c", str(src), "-o", str(out)])
     return out
 
+
+def _py_ext_flags() -> tuple[list[str], str]:
+    import sysconfig
+
+    import pybind11
+    inc = [f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}"]
+    return inc, sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+
+
+PY_EXT = LIB / "_cake_runtime"  # + EXT_SUFFIX
 
 def build_kernels(force: bool = False, jobs: int = 8) -> Path:
     srcs = sorted((CSRC / "kernels").glob("*.hip"))
@@ -84,22 +94,28 @@ def build_kernels(force: bool = False, jobs: int = 8) -> Path:
     return KERNEL_LIB
 
 
-def build_runtime(force: bool = False, jobs: int = 8) -> Path | None:
-    rt_dir = CSRC / "runtime"
-    srcs = sorted(rt_dir.glob("*.cpp"))
-    if not srcs:
-        return None
+def build_runtime(force: bool = False, jobs: int = 8) -> Path:
+    """C++ host runtime: pybind11 module, C-ABI library and the split-model tool."""
+    rt = CSRC / "runtime"
+    core_srcs = [rt / f"{n}.cpp" for n in ("json", "topology", "proto", "net", "safetensors")]
+    inc, ext = _py_ext_flags()
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        objs = list(ex.map(lambda s: _compile_cpp(s, force), srcs))
+        core = list(ex.map(lambda s: _compile_cpp(s, force), core_srcs))
+        capi_f = ex.submit(_compile_cpp, rt / "capi.cpp", force)
+        bind_f = ex.submit(_compile_cpp, rt / "bindings.cpp", force, inc)
+        capi, bind = capi_f.result(), bind_f.result()
     LIB.mkdir(parents=True, exist_ok=True)
-    if force or any(_newer(o, [], RUNTIME_LIB) for o in objs):
-        _run([CXX, "-shared", "-fPIC", *map(str, objs), "-o", str(RUNTIME_LIB), "-lpthread"])
+    pyext = PY_EXT.with_name(PY_EXT.name + ext)
+    if force or any(_newer(o, [], pyext) for o in [*core, bind]):
+        _run([CXX, "-shared", "-fPIC", *map(str, core), str(bind), "-o", str(pyext), "-lpthread"])
+    if force or any(_newer(o, [], RUNTIME_LIB) for o in [*core, capi]):
+        _run([CXX, "-shared", "-fPIC", *map(str, core), str(capi), "-o", str(RUNTIME_LIB),
+              "-lpthread"])
     tool = CSRC / "tools" / "split_model.cpp"
-    if tool.exists():
-        if force or _newer(tool, [*objs], SPLIT_TOOL):
-            _run([CXX, "-O2", "-std=c++17", f"-I{rt_dir}", str(tool), *map(str, objs),
-                  "-o", str(SPLIT_TOOL), "-lpthread"])
-    return RUNTIME_LIB
+    if force or _newer(tool, [*core, *sorted(rt.glob("*.h"))], SPLIT_TOOL):
+        _run([CXX, "-O2", "-std=c++17", f"-I{rt}", str(tool), *map(str, core), "-o",
+              str(SPLIT_TOOL), "-lpthread"])
+    return pyext
 
 
 def build_all(force: bool = False, jobs: int = 8) -> None:

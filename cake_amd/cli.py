@@ -1,0 +1,103 @@
+"""cake-cli: one entry point, master or worker mode (cake-cli/src/main.rs:8-63).
+
+Flag names and defaults follow cake-core/src/lib.rs:21-200;
+the image-generation flags double as the JSON keys of the image API.
+MI355X additions: ``--max-seq-len``, ``--no-graph``, ``--trace FILE``,
+``--log-level``.
+
+    python -m cake_amd.cli --model DIR --topology topology.yml --prompt "..."
+    python -m cake_amd.cli --mode worker --name w1 --model DIR --topology t.yml --address 0.0.0.0:10128
+    python -m cake_amd.cli --model DIR --api 0.0.0.0:8080
+"""
+from __future__ import annotations
+
+import argparse
+import logging
+import os
+import sys
+
+SD_VERSIONS = ["v1-5", "v2-1", "xl", "turbo"]
+
+
+def _bool(s: str) -> bool:
+    return str(s).lower() in ("1", "true", "yes", "on")
+
+
+def build_parser() -> argparse.ArgumentParser:
+    ap = argparse.ArgumentParser(prog="cake-cli", description="MI355X-native distributed inference")
+    a = ap.add_argument
+    a("--device", type=int, default=0, help="GPU ordinal")
+    a("--mode", choices=["master", "worker"], default="master")
+    a("--name", default=None, help="worker name (must be in the topology)")
+    a("--address", default="127.0.0.1:10128", help="worker bind address")
+    a("--api", default=None, help="serve the REST API on this address instead of one CLI generation")
+    a("--model", default="./cake-data/Meta-Llama-3-8B/")
+    a("--topology", default="./cake-data/topology.yml")
+    a("--prompt", default="The sky is blue because ")
+    a("--system-prompt", default="You are a helpful AI assistant.")
+    a("--seed", type=int, default=299792458)
+    a("-n", "--sample-len", type=int, default=100)
+    a("--temperature", type=float, default=1.0)
+    a("--top-p", type=float, default=None)
+    a("--top-k", type=int, default=None)
+    a("--repeat-penalty", type=float, default=1.1)
+    a("--repeat-last-n", type=int, default=128)
+    a("--dtype", default=None, help="f16 (default), bf16 or f32")
+    a("--cpu", action="store_true")
+    a("--model-type", choices=["text-model", "image-model"], default="text-model")
+    # SD args (lib.rs:90-127)
+    a("--sd-tokenizer", default=None)
+    a("--sd-tokenizer-2", default=None)
+    a("--sd-version", choices=SD_VERSIONS, default="v1-5")
+    a("--sd-use-f16", type=_bool, default=True)
+    a("--sd-width", type=int, default=None)
+    a("--sd-height", type=int, default=None)
+    a("--sd-sliced-attention-size", type=int, default=None)
+    a("--sd-clip", default=None)
+    a("--sd-clip2", default=None)
+    a("--sd-vae", default=None)
+    a("--sd-unet", default=None)
+    a("--sd-use-flash-attention", action="store_true")
+    # image generation args (lib.rs:129-200)
+    a("--sd-image-prompt", default="A very realistic photo of a rusty robot walking on a sandy beach")
+    a("--sd-uncond-prompt", default="")
+    a("--sd-tracing", action="store_true")
+    a("--sd-n-steps", type=int, default=None)
+    a("--sd-num-samples", type=int, default=1)
+    a("--sd-bsize", type=int, default=1)
+    a("--sd-intermediary-images", type=int, default=0)
+    a("--sd-guidance-scale", type=float, default=None)
+    a("--sd-img2img", default=None)
+    a("--sd-img2img-strength", type=float, default=0.8)
+    a("--sd-seed", type=int, default=None)
+    # MI355X-native extras
+    a("--max-seq-len", type=int, default=4096)
+    a("--no-graph", action="store_true", help="disable hipGraph capture of the decode step")
+    a("--trace", default=None, help="write a chrome-trace JSON of the run")
+    a("--log-level", default=os.environ.get("CAKE_LOG", "info"))
+    return ap
+
+
+def setup_logging(level: str) -> None:
+    # RUST_LOG default "info,tokenizers=error,actix_server=warn" (cake-cli/src/main.rs:14-22)
+    logging.basicConfig(level=getattr(logging, level.upper(), logging.INFO),
+                        format="[%(asctime)s %(levelname)s] %(message)s", datefmt="%H:%M:%S")
+    logging.getLogger("uvicorn.access").setLevel(logging.WARNING)
+
+
+def main(argv: list[str] | None = None) -> int:
+    args = build_parser().parse_args(argv)
+    setup_logging(args.log_level)
+    from .context import Context
+    ctx = Context.from_args(args)
+    if args.mode == "worker":
+        from .parallel.worker import Worker
+        Worker(ctx).run()
+        return 0
+    from .master import Master
+    Master(ctx).run()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,103 @@
+"""Master role (cake-core/src/cake/master.rs).
+
+Loads the text or image generator for ``--model-type``; either serves the REST
+API (``--api``) or runs ONE generation from the CLI flags: text streamed to
+stdout, images written to ``images/image_{b}_{step}.png`` (the directory is
+created — Appendix E Q15).  Text statistics use the reference formula:
+tokens/s = (generated - 1) / time since the first token (master.rs:93-121,
+guarded for a single token — Q13) plus p50/p99 per-token latency and TTFT.
+"""
+from __future__ import annotations
+
+import logging
+import sys
+import time
+from pathlib import Path
+from typing import Callable
+
+from .context import Context, rss_mib
+from .models.chat import Message
+
+log = logging.getLogger("cake.master")
+
+
+class Master:
+    def __init__(self, ctx: Context, llm=None, sd=None):
+        self.ctx = ctx
+        self.llm = llm
+        self.sd = sd
+        self.last_stats: dict = {}
+        if llm is None and sd is None:
+            if ctx.model_type == "text-model":
+                from .models.llama3.generator import LLamaGenerator
+                self.llm = LLamaGenerator.load(ctx)
+            else:
+                from .models.sd.pipeline import SDGenerator
+                self.sd = SDGenerator.load(ctx)
+        log.info("model loaded - mem=%.1f MiB", rss_mib())
+
+    def run(self) -> None:
+        a = self.ctx.args
+        if getattr(a, "api", None):
+            from .api.server import start
+            start(self, a.api)
+            return
+        if self.llm is not None:
+            self.llm.add_message(Message.system(a.system_prompt))
+            self.llm.add_message(Message.user(a.prompt))
+
+            def out(s: str) -> None:
+                sys.stdout.write(s)
+                sys.stdout.flush()
+            self.generate_text(out)
+            sys.stdout.write("\n")
+        else:
+            from .models.sd.args import ImageGenerationArgs
+            Path("images").mkdir(exist_ok=True)
+            step = [0]
+
+            def save(images) -> None:
+                for b, img in enumerate(images):
+                    p = f"images/image_{b}_{step[0]}.png"
+                    img.save(p)
+                    log.info("saved %s", p)
+                step[0] += 1
+            self.generate_image(ImageGenerationArgs.from_cli(a), save)
+
+    def reset(self) -> None:
+        if self.llm is not None:
+            self.llm.reset()
+
+    def generate_text(self, stream: Callable[[str], None], max_tokens: int | None = None) -> dict:
+        n = max_tokens if max_tokens is not None else self.ctx.args.sample_len
+        llm = self.llm
+        t_start = time.perf_counter()
+        times: list[float] = []
+
+        def on_token(tok) -> None:
+            times.append(time.perf_counter())
+            if not tok.is_end_of_stream:
+                stream(str(tok))
+
+        llm.stream(n, on_token)
+        generated = llm.generated_tokens()
+        stats = {"generated": generated}
+        if times:
+            stats["ttft_ms"] = (times[0] - t_start) * 1e3
+        if len(times) > 1:
+            dt = times[-1] - times[0]
+            stats["tokens_per_sec"] = (len(times) - 1) / dt if dt > 0 else float("inf")
+            lat = sorted((b - a) * 1e3 for a, b in zip(times, times[1:]))
+            dev = getattr(llm, "last_stats", None)
+            if dev is not None and dev.step_ms:  # device-timed steps when available
+                lat = sorted(dev.step_ms)
+            stats["p50_ms"] = lat[len(lat) // 2]
+            stats["p99_ms"] = lat[min(len(lat) - 1, int(round(0.99 * (len(lat) - 1))))]
+        log.info("%d tokens generated (%.2f token/s) p50=%.2fms p99=%.2fms ttft=%.1fms - mem=%.1f MiB",
+                 generated, stats.get("tokens_per_sec", 0.0), stats.get("p50_ms", 0.0),
+                 stats.get("p99_ms", 0.0), stats.get("ttft_ms", 0.0), rss_mib())
+        self.last_stats = stats
+        return stats
+
+    def generate_image(self, args, callback) -> None:
+        self.sd.generate_image(args, callback)

@@ -33,6 +33,14 @@ BLOCK_TENSORS = (
 )
 
 
+def _materialize(t: torch.Tensor, device, dtype) -> torch.Tensor:
+    """Own copy on `device` (never a view of a read-only checkpoint mapping)."""
+    out = t.to(device=device, dtype=dtype)
+    if out.data_ptr() == t.data_ptr():
+        out = out.clone()
+    return out.contiguous()
+
+
 def layer_name(i: int) -> str:
     return f"model.layers.{i}"
 
@@ -60,7 +68,7 @@ class BlockWeights:
             t = get(f"{prefix}.{suffix}")
             if tuple(t.shape) != shapes[key]:
                 raise ValueError(f"{prefix}.{suffix}: shape {tuple(t.shape)} != {shapes[key]}")
-            out[key] = t.to(device=device, dtype=dtype).contiguous()
+            out[key] = _materialize(t, device, dtype)
         return cls(**out)
 
     @classmethod
@@ -95,14 +103,14 @@ class HeadWeights:
 
     @classmethod
     def load(cls, get: Getter, cfg: LlamaConfig, device, dtype) -> "HeadWeights":
-        emb = get("model.embed_tokens.weight").to(device=device, dtype=dtype).contiguous()
+        emb = _materialize(get("model.embed_tokens.weight"), device, dtype)
         try:
-            head = get("lm_head.weight").to(device=device, dtype=dtype).contiguous()
+            head = _materialize(get("lm_head.weight"), device, dtype)
         except KeyError:
             if not cfg.tie_word_embeddings:
                 raise
             head = emb
-        norm = get("model.norm.weight").to(device=device, dtype=dtype).contiguous()
+        norm = _materialize(get("model.norm.weight"), device, dtype)
         return cls(embed=emb, norm=norm, lm_head=head)
 
     @classmethod

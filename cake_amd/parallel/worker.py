@@ -1,0 +1,203 @@
+"""Worker role: serve placed layers / model components over the framed TCP protocol.
+
+Reference: cake-core/src/cake/worker.rs.
+* Resolve ``--name`` in the topology; an unknown name serves the FIRST node
+  with a loud warning (worker.rs:90-104, Appendix E Q12).
+* Load only the owned units (text: ``model.layers.N`` blocks into one
+  :class:`LayerStack`; image: clip/clip2/vae/unet — worker.rs:110-125).
+* Accept many masters; each connection gets its own KV session while weights
+  are shared (worker.rs:52-72, 290-303).  Per connection: ``Hello`` →
+  ``WorkerInfo`` (latency = ms spent reading Hello), then ``SingleOp``/``Batch``
+  → run the ops in order → ``Tensor`` (worker.rs:177-287).
+* Every 5 messages log ops/s and read/write bandwidth (worker.rs:18-19,271-282).
+* Extensions: ``Reset`` clears the session KV, ``Ping``→``Pong``, failures
+  are returned as ``Error`` instead of aborting the process (Appendix E Q6),
+  and ``CAKE_FAULT_INJECT=drop_after=N`` drops a connection after N ops (tests).
+"""
+from __future__ import annotations
+
+import itertools
+import logging
+import os
+import platform
+import threading
+import time
+
+import torch
+
+from . import proto as P
+
+log = logging.getLogger("cake.worker")
+NUM_OPS_TO_STATS = 5
+
+
+def _layer_index(name: str) -> int:
+    prefix = "model.layers."
+    if not name.startswith(prefix):
+        raise ValueError(f"not a transformer block: {name}")
+    return int(name[len(prefix):])
+
+
+class Worker:
+    def __init__(self, ctx):
+        self.ctx = ctx
+        topo = ctx.topology
+        node = topo.get(ctx.name) if ctx.name else None
+        if node is None:
+            if not topo.nodes:
+                raise ValueError("topology has no workers")
+            node = topo.nodes[0]
+            log.warning("worker name %r not found in topology, serving the FIRST node %r",
+                        ctx.name, node.name)
+        self.node = node
+        self.text = ctx.model_type == "text-model"
+        self.compute_lock = threading.Lock()
+        self._sessions = itertools.count(1)
+        self.stack = None
+        self.units = {}
+        if self.text:
+            from ..models.llama3.config import LlamaConfig
+            from ..models.llama3.factory import load_stack
+            cfg = LlamaConfig.from_path(ctx.model_path)
+            layers = sorted(_layer_index(l) for l in node.layers if l.startswith("model.layers."))
+            self.stack = load_stack(ctx.model_path, cfg, layers, ctx.device, ctx.dtype,
+                                    max_seq=ctx.max_seq_len)
+            self.stack.max_sessions = 64
+            log.info("loaded %d blocks on %s (%s)", len(layers), ctx.device, ctx.dtype)
+        else:
+            from ..models.sd.shardable import load_sd_units
+            self.units = load_sd_units(ctx, node.layers)
+        host, _, port = ctx.address.rpartition(":")
+        from ..utils.native import runtime
+        self._rt = runtime()
+        self.listen_fd = self._rt.tcp_listen(host or "0.0.0.0", int(port))
+        self.port = self._rt.tcp_local_port(self.listen_fd)
+        self._stop = threading.Event()
+        fi = os.environ.get("CAKE_FAULT_INJECT", "")
+        self.drop_after = int(fi.split("=")[1]) if fi.startswith("drop_after=") else 0
+        log.info("worker %s listening on %s:%d", node.name, host, self.port)
+
+    # ------------------------------------------------------------------ info
+    def info(self, latency_ms: int) -> dict:
+        dev = self.ctx.device
+        return {"version": P.PROTO_VERSION,
+                "dtype": P.CANDLE_DTYPES.get(self.ctx.dtype, str(self.ctx.dtype)),
+                "os": platform.system().lower(), "arch": platform.machine(),
+                "device": "rocm" if dev.type == "cuda" else "cpu",
+                "device_idx": int(dev.index or 0), "latency": int(latency_ms)}
+
+    # ------------------------------------------------------------------ serving
+    def run(self) -> None:
+        while not self._stop.is_set():
+            try:
+                fd, peer = self._rt.tcp_accept(self.listen_fd)
+            except RuntimeError:
+                if self._stop.is_set():
+                    break
+                raise
+            t = threading.Thread(target=self._serve, args=(P.Connection(fd, peer),), daemon=True)
+            t.start()
+
+    def serve_in_thread(self) -> threading.Thread:
+        t = threading.Thread(target=self.run, daemon=True)
+        t.start()
+        return t
+
+    def stop(self) -> None:
+        self._stop.set()
+        self._rt.tcp_close(self.listen_fd)
+
+    def _serve(self, conn: P.Connection) -> None:
+        session = next(self._sessions)
+        log.info("[%s] connected (session %d)", conn.peer, session)
+        n_ops = 0
+        try:
+            t0 = time.perf_counter()
+            msg, _ = conn.recv()
+            latency = int((time.perf_counter() - t0) * 1000)
+            if msg["type"] != P.HELLO:
+                conn.send({"type": P.ERROR, "error": "expected Hello"})
+                return
+            conn.send({"type": P.WORKER_INFO, "info": self.info(latency)})
+            stats_t, stats_ops, stats_in, stats_out, stats_msgs = time.perf_counter(), 0, 0, 0, 0
+            while True:
+                try:
+                    msg, body = conn.recv()
+                except RuntimeError:
+                    break  # peer closed: end this connection silently (worker.rs:208)
+                kind = msg["type"]
+                if kind == P.PING:
+                    conn.send({"type": P.PONG})
+                    continue
+                if kind == P.RESET:
+                    self._reset(session)
+                    conn.send({"type": P.PONG})
+                    continue
+                if kind not in (P.SINGLE_OP, P.BATCH):
+                    conn.send({"type": P.ERROR, "error": f"unexpected message type {kind}"})
+                    continue
+                ops = ([(msg["layer_name"], msg["index_pos"], msg["block_idx"])]
+                       if kind == P.SINGLE_OP else msg["batch"])
+                try:
+                    x = P.tensor_from_payload(msg, body)
+                    y = self._run_ops(x, ops, session)
+                    conn.send({"type": P.TENSOR}, y)
+                except Exception as e:  # noqa: BLE001
+                    log.error("[%s] op failed: %s", conn.peer, e)
+                    conn.send({"type": P.ERROR, "error": str(e)})
+                n_ops += len(ops)
+                stats_ops += len(ops)
+                stats_msgs += 1
+                if self.drop_after and n_ops >= self.drop_after:
+                    log.warning("fault injection: dropping connection after %d ops", n_ops)
+                    break
+                if stats_msgs % NUM_OPS_TO_STATS == 0:
+                    dt = time.perf_counter() - stats_t
+                    din, dout = conn.bytes_in - stats_in, conn.bytes_out - stats_out
+                    log.info("%s | ops=%.1f/s read=%.1f KB/s write=%.1f KB/s", self.node.name,
+                             stats_ops / dt, din / dt / 1e3, dout / dt / 1e3)
+                    stats_t, stats_ops = time.perf_counter(), 0
+                    stats_in, stats_out = conn.bytes_in, conn.bytes_out
+        finally:
+            self._drop_session(session)
+            conn.close()
+            log.info("[%s] disconnected", conn.peer)
+
+    def _reset(self, session: int) -> None:
+        if self.stack is not None:
+            with self.compute_lock:
+                self.stack.reset(session)
+
+    def _drop_session(self, session: int) -> None:
+        if self.stack is not None:
+            with self.compute_lock:
+                self.stack.drop(session)
+
+    def _run_ops(self, x: torch.Tensor, ops, session: int) -> torch.Tensor:
+        if self.text:
+            shape = x.shape
+            h = x.to(self.ctx.device).float().reshape(-1, shape[-1]).contiguous()
+            i = 0
+            with self.compute_lock:
+                while i < len(ops):  # consecutive ops at one position -> one stack call
+                    pos = int(ops[i][1])
+                    j = i
+                    layers = []
+                    while j < len(ops) and int(ops[j][1]) == pos:
+                        li = _layer_index(ops[j][0])
+                        if li not in self.stack.weights:
+                            raise ValueError(f"layer {ops[j][0]} is not served by {self.node.name}")
+                        layers.append(li)
+                        j += 1
+                    self.stack.forward(h, layers, pos, session)
+                    i = j
+                if h.is_cuda:
+                    torch.cuda.synchronize()
+            return h.reshape(shape)
+        with self.compute_lock:
+            for name, _, _ in ops:
+                unit = self.units.get(name)
+                if unit is None:
+                    raise ValueError(f"{name} is not served by {self.node.name}")
+                x = unit.forward_packed(x)
+            return x
