@@ -37,15 +37,29 @@ H_POS, H_STREAM, H_T, H_FLAGS = 0, 1, 2, 3
 FLAG_RESET = 1
 
 
-def shard_layers(num_layers: int, world: int) -> list[list[int]]:
-    """Contiguous near-equal shards (rank r gets layers [a_r, b_r))."""
-    base, extra = divmod(num_layers, world)
+def shard_layers(num_layers: int, world: int, head_cost: float = 0.0) -> list[list[int]]:
+    """Contiguous shards (rank r gets layers [a_r, b_r)) balancing per-rank work.
+
+    ``head_cost`` is the master's extra work (embedding + ln_f + lm_head +
+    sampling) in units of one transformer block; rank 0 then gets that many
+    fewer blocks.  With head_cost = 0 this is a near-equal split.
+    """
+    if world == 1:
+        return [list(range(num_layers))]
+    total = num_layers + head_cost
     out, start = [], 0
     for r in range(world):
-        n = base + (1 if r < extra else 0)
-        out.append(list(range(start, start + n)))
-        start += n
+        # cumulative target boundary after rank r (in block units incl. the head)
+        end = round((r + 1) * total / world - head_cost) if r < world - 1 else num_layers
+        end = max(start + (1 if num_layers - start >= world - r else 0), min(end, num_layers - (world - 1 - r)))
+        out.append(list(range(start, end)))
+        start = end
     return out
+
+
+def head_cost_in_layers(cfg) -> float:
+    """lm_head bytes relative to one block's weight bytes (decode is bandwidth-bound)."""
+    return (cfg.vocab_size * cfg.hidden_size * 2) / cfg.layer_bytes(2)
 
 
 @dataclass

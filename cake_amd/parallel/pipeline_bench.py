@@ -10,7 +10,7 @@ import torch.distributed as dist
 
 from ..models.llama3.config import preset
 from ..models.llama3.factory import parse_dtype, random_head, random_stack
-from .pipeline import PipelineEngine, shard_layers
+from .pipeline import PipelineEngine, head_cost_in_layers, shard_layers
 
 
 def bench_pipeline(a, emit) -> None:
@@ -27,7 +27,7 @@ def bench_pipeline(a, emit) -> None:
         dist.init_process_group("gloo", rank=rank, world_size=world)
     cfg = preset(a.model)
     dtype = parse_dtype(a.dtype)
-    shards = shard_layers(cfg.num_hidden_layers, world)
+    shards = shard_layers(cfg.num_hidden_layers, world, head_cost_in_layers(cfg))
     owners = [r for r, sh in enumerate(shards) for _ in sh]
     streams = a.streams if a.streams > 0 else world
     t0 = time.time()

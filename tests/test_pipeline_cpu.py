@@ -76,7 +76,12 @@ def _run(world, owners, streams):
 
 
 def test_plan_and_shards():
-    assert shard_layers(32, 3) == [list(range(0, 11)), list(range(11, 22)), list(range(22, 32))]
+    for L, w, hc in ((32, 3, 0.0), (32, 8, 2.4), (80, 8, 1.2), (5, 5, 10.0), (7, 2, 0.0)):
+        sh = shard_layers(L, w, hc)
+        assert [li for s in sh for li in s] == list(range(L)) and all(sh)
+        loads = [len(s) + (hc if r == 0 else 0) for r, s in enumerate(sh)]
+        if L >= 2 * w and hc < L / w:
+            assert max(loads) - min(loads) <= 1.5
     runs = plan_from_owners([0, 0, 1, 1, 1, 0, 2])
     assert [(r.owner, r.layers) for r in runs] == [(0, [0, 1]), (1, [2, 3, 4]), (0, [5]), (2, [6])]
 
