@@ -1,0 +1,210 @@
+// Stable Diffusion normalisation / activation kernels (NCHW activations).
+//
+// Reference ops (candle-transformers stable_diffusion via cake's UNet/VAE/CLIP
+// forwarders):
+//   K31/K33 GroupNorm(32) [+ SiLU] in every ResnetBlock2D and the attention
+//           blocks' group_norm,
+//   K34     LayerNorm in the BasicTransformerBlock / CLIP encoder,
+//   K36     GEGLU feed-forward gate (candle: x * gelu_tanh(gate)).
+// GroupNorm is two launches so the reduction spreads over the whole chip even
+// at batch 2 (B*32 groups would fill only a quarter of the 256 CUs):
+//   1. stats:  grid (B*G, S) — each workgroup folds a slice of one group into a
+//              Welford (count, mean, M2) partial;
+//   2. apply:  grid over the tensor — each workgroup merges its group's S
+//              partials (Chan's formula) once, then normalises + affine
+//              (+ SiLU) with 16-byte accesses.
+#include "common.h"
+
+namespace cake {
+
+constexpr int kGnSplit = 16;
+
+__device__ __forceinline__ void welford_merge(float& n, float& mean, float& m2, float nb,
+                                              float meanb, float m2b) {
+  if (nb == 0.f) return;
+  const float nt = n + nb;
+  const float d = meanb - mean;
+  mean += d * (nb / nt);
+  m2 += m2b + d * d * (n * nb / nt);
+  n = nt;
+}
+
+template <int DT>
+__global__ __launch_bounds__(256) void gn_stats_kernel(const uint16_t* __restrict__ x,
+                                                       long long group_elems,
+                                                       float* __restrict__ part) {
+  const int bg = blockIdx.x, s = blockIdx.y;
+  const long long per = (group_elems + kGnSplit - 1) / kGnSplit;
+  const long long beg = s * per, end = min(group_elems, beg + per);
+  const uint16_t* base = x + (long long)bg * group_elems;
+  float n = 0.f, mean = 0.f, m2 = 0.f;
+  for (long long i = beg + threadIdx.x; i < end; i += blockDim.x) {
+    const float v = to_f32<DT>(base[i]);
+    n += 1.f;
+    const float d = v - mean;
+    mean += d / n;
+    m2 += d * (v - mean);
+  }
+  // wave then block merge
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const float nb = __shfl_xor(n, off, 64), mb = __shfl_xor(mean, off, 64),
+                qb = __shfl_xor(m2, off, 64);
+    welford_merge(n, mean, m2, nb, mb, qb);
+  }
+  __shared__ float red[4][3];
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { red[w][0] = n; red[w][1] = mean; red[w][2] = m2; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < 4; ++i) welford_merge(n, mean, m2, red[i][0], red[i][1], red[i][2]);
+    float* p = part + ((long long)bg * kGnSplit + s) * 3;
+    p[0] = n; p[1] = mean; p[2] = m2;
+  }
+}
+
+// x, y: [B, C, HW]; gamma/beta [C]
+template <int DT, bool SILU>
+__global__ __launch_bounds__(256) void gn_apply_kernel(const uint16_t* __restrict__ x,
+                                                       const uint16_t* __restrict__ gamma,
+                                                       const uint16_t* __restrict__ beta,
+                                                       const float* __restrict__ part, int C,
+                                                       int G, long long HW, float eps,
+                                                       uint16_t* __restrict__ y) {
+  // one workgroup covers a contiguous 8*256-element chunk inside ONE group
+  const long long group_elems = (long long)(C / G) * HW;
+  const long long chunks_per_group = (group_elems + 2047) / 2048;
+  const long long bg = blockIdx.x / chunks_per_group;
+  const long long chunk = blockIdx.x - bg * chunks_per_group;
+  __shared__ float stat[2];
+  if (threadIdx.x == 0) {
+    float n = 0.f, mean = 0.f, m2 = 0.f;
+    const float* p = part + bg * kGnSplit * 3;
+    for (int s = 0; s < kGnSplit; ++s) welford_merge(n, mean, m2, p[3 * s], p[3 * s + 1], p[3 * s + 2]);
+    stat[0] = mean;
+    stat[1] = rsqrtf(m2 / n + eps);
+  }
+  __syncthreads();
+  const float mean = stat[0], rstd = stat[1];
+  const int g = (int)(bg % G);
+  const long long base = bg * group_elems;
+  const long long i0 = chunk * 2048 + threadIdx.x * 8;
+  if (i0 >= group_elems) return;
+  const bool vec = (HW % 8 == 0) && (i0 + 8 <= group_elems);
+  if (vec) {
+    float f[8];
+    unpack8<DT>(*reinterpret_cast<const uint4*>(x + base + i0), f);
+    const int c = g * (C / G) + (int)(i0 / HW);  // 8 elements never straddle a channel
+    const float ga = to_f32<DT>(gamma[c]) * rstd, be = to_f32<DT>(beta[c]);
+    uint16_t o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float v = (f[e] - mean) * ga + be;
+      if (SILU) v = silu(v);
+      o[e] = from_f32<DT>(v);
+    }
+    *reinterpret_cast<uint4*>(y + base + i0) = *reinterpret_cast<uint4*>(o);
+  } else {
+    for (long long i = i0; i < min(i0 + 8, group_elems); ++i) {
+      const int c = g * (C / G) + (int)(i / HW);
+      float v = (to_f32<DT>(x[base + i]) - mean) * rstd * to_f32<DT>(gamma[c]) + to_f32<DT>(beta[c]);
+      if (SILU) v = silu(v);
+      y[base + i] = from_f32<DT>(v);
+    }
+  }
+}
+
+// LayerNorm over the last dim (rows of C)
+template <int DT>
+__global__ __launch_bounds__(256) void layernorm_kernel(const uint16_t* __restrict__ x,
+                                                        const uint16_t* __restrict__ gamma,
+                                                        const uint16_t* __restrict__ beta, int C,
+                                                        float eps, uint16_t* __restrict__ y) {
+  __shared__ float red[16];
+  const uint16_t* xr = x + (long long)blockIdx.x * C;
+  uint16_t* yr = y + (long long)blockIdx.x * C;
+  float s = 0.f;
+  for (int i = threadIdx.x; i < C; i += blockDim.x) s += to_f32<DT>(xr[i]);
+  const float mean = block_sum(s, red) / (float)C;
+  float q = 0.f;
+  for (int i = threadIdx.x; i < C; i += blockDim.x) {
+    const float d = to_f32<DT>(xr[i]) - mean;
+    q += d * d;
+  }
+  const float rstd = rsqrtf(block_sum(q, red) / (float)C + eps);
+  for (int i = threadIdx.x; i < C; i += blockDim.x)
+    yr[i] = from_f32<DT>((to_f32<DT>(xr[i]) - mean) * rstd * to_f32<DT>(gamma[i]) +
+                         to_f32<DT>(beta[i]));
+}
+
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float k = 0.7978845608028654f;  // sqrt(2/pi)
+  return 0.5f * x * (1.f + tanhf(k * (x + 0.044715f * x * x * x)));
+}
+
+// h [rows, 2F] -> out [rows, F] = h[:, :F] * gelu_tanh(h[:, F:])
+template <int DT>
+__global__ void geglu_kernel(const uint16_t* __restrict__ h, long long rows, int F,
+                             uint16_t* __restrict__ out) {
+  const long long n = rows * F;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long r = i / F;
+    const int c = (int)(i - r * F);
+    const float a = to_f32<DT>(h[r * 2 * F + c]), g = to_f32<DT>(h[r * 2 * F + F + c]);
+    out[i] = from_f32<DT>(a * gelu_tanh(g));
+  }
+}
+
+}  // namespace cake
+
+using namespace cake;
+
+#define DISPATCH_DT(dt, ...)                       \
+  do {                                             \
+    if ((dt) == kBF16) { constexpr int DT = kBF16; __VA_ARGS__; } \
+    else if ((dt) == kF16) { constexpr int DT = kF16; __VA_ARGS__; } \
+    else return (int)hipErrorInvalidValue;         \
+  } while (0)
+
+// part: workspace of B*G*16*3 floats
+CAKE_API int cake_groupnorm(int dt, const void* x, const void* gamma, const void* beta, int B,
+                            int C, long long HW, int G, float eps, int silu_act, float* part,
+                            void* y, hipStream_t st) {
+  if (C % G) return (int)hipErrorInvalidValue;
+  const long long ge = (long long)(C / G) * HW;
+  const long long chunks = (ge + 2047) / 2048;
+  const long long nblk = (long long)B * G * chunks;
+  if (nblk > 0x7fffffffLL) return (int)hipErrorInvalidValue;
+  DISPATCH_DT(dt, {
+    hipLaunchKernelGGL((gn_stats_kernel<DT>), dim3(B * G, kGnSplit), dim3(256), 0, st,
+                       (const uint16_t*)x, ge, part);
+    if (silu_act)
+      hipLaunchKernelGGL((gn_apply_kernel<DT, true>), dim3((unsigned)nblk), dim3(256), 0, st,
+                         (const uint16_t*)x, (const uint16_t*)gamma, (const uint16_t*)beta, part, C,
+                         G, HW, eps, (uint16_t*)y);
+    else
+      hipLaunchKernelGGL((gn_apply_kernel<DT, false>), dim3((unsigned)nblk), dim3(256), 0, st,
+                         (const uint16_t*)x, (const uint16_t*)gamma, (const uint16_t*)beta, part, C,
+                         G, HW, eps, (uint16_t*)y);
+  });
+  return (int)hipGetLastError();
+}
+
+CAKE_API int cake_layernorm(int dt, const void* x, const void* gamma, const void* beta,
+                            long long rows, int C, float eps, void* y, hipStream_t st) {
+  if (rows > 0x7fffffffLL) return (int)hipErrorInvalidValue;
+  DISPATCH_DT(dt, hipLaunchKernelGGL((layernorm_kernel<DT>), dim3((unsigned)rows), dim3(256), 0,
+                                     st, (const uint16_t*)x, (const uint16_t*)gamma,
+                                     (const uint16_t*)beta, C, eps, (uint16_t*)y));
+  return (int)hipGetLastError();
+}
+
+CAKE_API int cake_geglu(int dt, const void* h, long long rows, int F, void* out, hipStream_t st) {
+  long long n = rows * F;
+  long long g = (n + 255) / 256;
+  if (g > 8192) g = 8192;
+  DISPATCH_DT(dt, hipLaunchKernelGGL((geglu_kernel<DT>), dim3((unsigned)g), dim3(256), 0, st,
+                                     (const uint16_t*)h, rows, F, (uint16_t*)out));
+  return (int)hipGetLastError();
+}

@@ -190,7 +190,10 @@ class LayerStack:
         v = torch.matmul(x, w.wv.t())
         K.rope_kv(q, k, v, self.inv_freq, pos0, kc, vc)
         att = torch.empty_like(q)
-        K.attn_prefill(q, kc, vc, pos0, self.scale, att)
+        nh, hd = cfg.num_attention_heads, cfg.head_dim
+        Tk = pos0 + T
+        K.flash_attn(q.view(1, T, nh, hd).transpose(1, 2), kc[None, :, :Tk], vc[None, :, :Tk],
+                     att.view(1, T, nh, hd).transpose(1, 2), self.scale, causal=True, pos0=pos0)
         K.add_resid(hidden, torch.matmul(att, w.wo.t()))
         K.rmsnorm(hidden, w.ln2, cfg.rms_norm_eps, x)
         g = torch.matmul(x, w.wg.t())

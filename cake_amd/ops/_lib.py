@@ -85,3 +85,10 @@ def available() -> bool:
 def check(rc: int, name: str) -> None:
     if rc != 0:
         raise KernelError(f"{name} failed with hipError {rc}")
+
+_SIGS.update({
+    "cake_flash_attn": [I, P, P, P, P, I, I, I, I, I, I, P, F, I, I, P],
+    "cake_groupnorm": [I, P, P, P, I, I, C.c_longlong, I, F, I, P, P, P],
+    "cake_layernorm": [I, P, P, P, C.c_longlong, I, F, P, P],
+    "cake_geglu": [I, P, C.c_longlong, I, P, P],
+})

@@ -246,3 +246,69 @@ def set_gemv_tuning(kind: str, U: int = 4, prefetch: bool = False, max_blocks: i
     """Select the decode-GEMV launch geometry for one kernel kind (see gemv.hip)."""
     check(kernels().cake_gemv_set_tuning(GEMV_KINDS[kind], int(U), int(prefetch), int(max_blocks)),
           "gemv_set_tuning")
+
+
+# ---------------------------------------------------------------------------
+# MFMA flash attention + SD normalisation kernels
+# ---------------------------------------------------------------------------
+
+def flash_attn(q, k, v, out, scale: float, causal: bool = False, pos0: int = 0):
+    """out = softmax(q kᵀ * scale [+causal mask]) v on MFMA.
+
+    All four are 4-D *views* [B, H|Hkv, rows, D] with unit stride on D (any
+    batch/head/row strides — e.g. [B, N, H, D] projections viewed as
+    .transpose(1, 2), or a KV cache [Hkv, S, D][None]).  GQA when
+    Hkv < H.  Causal: query row i sits at absolute position pos0 + i.
+    """
+    import ctypes
+    B, H, N, D = q.shape
+    Bk, Hkv, M, Dk = k.shape
+    if v.shape != k.shape or Dk != D or Bk != B or tuple(out.shape) != (B, H, N, D):
+        raise ValueError(f"flash_attn shapes q{tuple(q.shape)} k{tuple(k.shape)} "
+                         f"v{tuple(v.shape)} o{tuple(out.shape)}")
+    if H % Hkv or D > 256:
+        raise ValueError("flash_attn: H % Hkv != 0 or D > 256")
+    for t, n in ((q, "q"), (k, "k"), (v, "v"), (out, "out")):
+        if not t.is_cuda or t.dtype != q.dtype or t.stride(3) != 1:
+            raise ValueError(f"flash_attn: {n} must be a unit-stride-D device tensor of {q.dtype}")
+        if (t.data_ptr() % 16) or (D % 8 == 0 and any(s % 8 for s in t.stride()[:3])):
+            raise ValueError(f"flash_attn: {n} not 16-byte aligned for vector loads")
+    st = [s for t in (q, k, v, out) for s in t.stride()[:3]]
+    arr = (ctypes.c_longlong * 12)(*st)
+    check(kernels().cake_flash_attn(_dt(q), _p(q), _p(k), _p(v), _p(out), B, H, Hkv, N, M, D,
+                                    ctypes.cast(arr, ctypes.c_void_p), float(scale), int(causal),
+                                    int(pos0), _stream()), "flash_attn")
+
+
+def group_norm(x, gamma, beta, groups: int, eps: float, silu: bool, out):
+    """GroupNorm over NCHW (contiguous) [+ fused SiLU]."""
+    B, C = x.shape[:2]
+    HW = x.numel() // (B * C)
+    _req(x, "x")
+    _req(gamma, "gamma", dtype=x.dtype, shape=(C,))
+    _req(beta, "beta", dtype=x.dtype, shape=(C,))
+    _req(out, "out", dtype=x.dtype, shape=x.shape)
+    if C % groups:
+        raise ValueError("C % groups != 0")
+    part = torch.empty(B * groups * 16 * 3, device=x.device, dtype=torch.float32)
+    check(kernels().cake_groupnorm(_dt(x), _p(x), _p(gamma), _p(beta), B, C, HW, groups,
+                                   float(eps), int(silu), _p(part), _p(out), _stream()),
+          "groupnorm")
+
+
+def layer_norm(x, gamma, beta, eps: float, out):
+    C = x.shape[-1]
+    _req(x, "x")
+    _req(gamma, "gamma", dtype=x.dtype, shape=(C,))
+    _req(beta, "beta", dtype=x.dtype, shape=(C,))
+    _req(out, "out", dtype=x.dtype, shape=x.shape)
+    check(kernels().cake_layernorm(_dt(x), _p(x), _p(gamma), _p(beta), x.numel() // C, C,
+                                   float(eps), _p(out), _stream()), "layernorm")
+
+
+def geglu(h, out):
+    F = h.shape[-1] // 2
+    _req(h, "h")
+    _req(out, "out", dtype=h.dtype, numel=h.numel() // 2)
+    check(kernels().cake_geglu(_dt(h), _p(h), h.numel() // (2 * F), F, _p(out), _stream()),
+          "geglu")
