@@ -1,0 +1,136 @@
+"""SD shardable units (cake-core/src/models/sd/{sd_shardable,unet,vae,clip}.rs).
+
+Every component — ``clip``, ``clip2``, ``vae``, ``unet`` — is a unit with the
+reference's packed single-tensor interface so it can run locally or on a
+worker (SingleOp with ``layer_name`` = component name):
+* clip/clip2: token ids [1, 77] -> last hidden state [1, 77, D];
+* unet: pack([latents, text_embeddings, t]) -> noise prediction;
+* vae: pack([direction, x]) -> encode(x).sample() if direction == 1.0 else decode(x).
+"""
+from __future__ import annotations
+
+import json
+import logging
+from pathlib import Path
+
+import torch
+
+from .clip import ClipTextTransformer
+from .config import SDConfig, get_config, tiny_config
+from .unet import UNet2DConditionModel
+from .util import pack_tensors, unpack_tensors
+from .vae import AutoencoderKL
+from .weights import load_component, random_component, resolve
+
+log = logging.getLogger("cake.sd")
+SD_COMPONENTS = ("clip", "clip2", "vae", "unet")
+
+
+def sd_config_for(ctx) -> SDConfig:
+    a = ctx.args
+    meta = Path(ctx.model_path) / "cake_sd.json"
+    tiny = meta.exists() and json.loads(meta.read_text()).get("tiny", False)
+    if tiny:
+        cfg = tiny_config(a.sd_version)
+        if a.sd_height:
+            cfg.height = a.sd_height
+        if a.sd_width:
+            cfg.width = a.sd_width
+        cfg.unet.sliced_attention_size = a.sd_sliced_attention_size
+        return cfg
+    return get_config(a.sd_version, a.sd_height, a.sd_width, a.sd_sliced_attention_size)
+
+
+class SDUnit:
+    def __init__(self, name: str, cfg: SDConfig, weights: dict[str, torch.Tensor], device, dtype):
+        self.name, self.cfg, self.w, self.device, self.dtype = name, cfg, weights, device, dtype
+        if name == "unet":
+            self.model = UNet2DConditionModel(cfg.unet)
+        elif name == "vae":
+            self.model = AutoencoderKL(cfg.vae)
+        else:
+            self.model = ClipTextTransformer(cfg.clip if name == "clip" else cfg.clip2, weights)
+        self.generator = torch.Generator(device="cpu")
+
+    def layer_name(self) -> str:
+        return self.name
+
+    def ident(self) -> str:
+        return "local"
+
+    @torch.no_grad()
+    def forward_packed(self, x: torch.Tensor) -> torch.Tensor:
+        if self.name in ("clip", "clip2"):
+            return self.model.forward(x.to(self.device))
+        parts = unpack_tensors(x.to(self.device))
+        if self.name == "unet":
+            lat, emb, t = parts
+            return self.model.forward(self.w, lat.to(self.dtype), float(t.reshape(-1)[0]),
+                                      emb.to(self.dtype))
+        direction, inp = parts
+        inp = inp.to(self.dtype)
+        if float(direction.reshape(-1)[0]) == 1.0:
+            return self.model.encode(self.w, inp, self.generator)
+        return self.model.decode(self.w, inp)
+
+    # pipeline-facing helpers (same packing as the reference, unet.rs:81-100, vae.rs:87-108)
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return self.forward_packed(x)
+
+
+class RemoteSDUnit:
+    """A component served by a worker: SingleOp(layer_name=component, x=packed)."""
+
+    def __init__(self, client, name: str):
+        self.client, self.name = client, name
+
+    def layer_name(self) -> str:
+        return self.name
+
+    def ident(self) -> str:
+        return self.client.ident()
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return self.client.forward_named(self.name, x)
+
+
+def unet_forward_unpacked(unit, latents, text_embeddings, timestep: int, device) -> torch.Tensor:
+    t = torch.tensor([float(timestep)], device=device)
+    return unit.forward(pack_tensors([latents, text_embeddings, t], device))
+
+
+def vae_encode(unit, image, device) -> torch.Tensor:
+    return unit.forward(pack_tensors([torch.tensor([1.0], device=device), image], device))
+
+
+def vae_decode(unit, latents, device) -> torch.Tensor:
+    return unit.forward(pack_tensors([torch.tensor([0.0], device=device), latents], device))
+
+
+def load_unit(name: str, ctx, cfg: SDConfig | None = None) -> SDUnit:
+    a = ctx.args
+    cfg = cfg or sd_config_for(ctx)
+    override = {"unet": a.sd_unet, "vae": a.sd_vae, "clip": a.sd_clip, "clip2": a.sd_clip2}[name]
+    if name == "clip2" and cfg.clip2 is None:
+        raise ValueError(f"sd version {cfg.version} has no clip2")
+    try:
+        path = resolve(name, override, cfg.version, a.sd_use_f16, ctx.model_path)
+        w = load_component(name, path, cfg, ctx.device, ctx.dtype)
+        log.info("loaded %s from %s", name, path)
+    except FileNotFoundError:
+        if not getattr(a, "sd_random_init", False):
+            raise
+        log.warning("%s: no weights found, using random init", name)
+        w = random_component(name, cfg, ctx.device, ctx.dtype)
+    return SDUnit(name, cfg, w, ctx.device, ctx.dtype)
+
+
+def load_sd_units(ctx, layers: list[str]) -> dict[str, SDUnit]:
+    """Worker side (sd_shardable.rs:29-45): build each named component."""
+    cfg = sd_config_for(ctx)
+    units = {}
+    for name in layers:
+        if name not in SD_COMPONENTS:
+            raise ValueError(f"unknown SD component {name!r} (clip, clip2, vae, unet)")
+        units[name] = load_unit(name, ctx, cfg)
+    return units

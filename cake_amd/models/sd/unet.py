@@ -1,0 +1,281 @@
+"""UNet2DConditionModel (diffusers layout; candle ``build_unet`` in the reference,
+cake-core/src/models/sd/unet.rs:67-79).
+
+Structure: conv_in → timestep embedding (sinusoidal, flip_sin_to_cos) →
+down blocks [ResnetBlock2D (+ Transformer2DModel)]* (+ stride-2 conv) →
+mid block (resnet, transformer, resnet) → up blocks with skip concatenation
+(+ nearest-2x upsample conv) → GroupNorm/SiLU/conv_out.  SDXL's added
+text-time conditioning is NOT used (cake passes only encoder_hidden_states,
+unet.rs:54), matching the reference.
+
+Each module is built once from the config and knows both its parameter
+shapes (for random init / checkpoint validation) and its forward.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from . import ops
+from .config import UNetConfig
+
+
+class Module:
+    def params(self) -> dict[str, tuple]:
+        raise NotImplementedError
+
+
+class Conv(Module):
+    def __init__(self, name, cin, cout, k=3, stride=1, padding=None, bias=True):
+        self.name, self.cin, self.cout, self.k, self.stride = name, cin, cout, k, stride
+        self.padding = (k // 2) if padding is None else padding
+        self.bias = bias
+
+    def params(self):
+        p = {f"{self.name}.weight": (self.cout, self.cin, self.k, self.k)}
+        if self.bias:
+            p[f"{self.name}.bias"] = (self.cout,)
+        return p
+
+    def __call__(self, W, x):
+        return ops.conv2d(x, W[f"{self.name}.weight"], W.get(f"{self.name}.bias"), self.stride,
+                          self.padding)
+
+
+class Linear(Module):
+    def __init__(self, name, cin, cout, bias=True):
+        self.name, self.cin, self.cout, self.bias = name, cin, cout, bias
+
+    def params(self):
+        p = {f"{self.name}.weight": (self.cout, self.cin)}
+        if self.bias:
+            p[f"{self.name}.bias"] = (self.cout,)
+        return p
+
+    def __call__(self, W, x):
+        return ops.linear(x, W[f"{self.name}.weight"], W.get(f"{self.name}.bias"))
+
+
+class Norm(Module):
+    def __init__(self, name, c):
+        self.name, self.c = name, c
+
+    def params(self):
+        return {f"{self.name}.weight": (self.c,), f"{self.name}.bias": (self.c,)}
+
+
+class ResnetBlock2D(Module):
+    def __init__(self, name, cin, cout, temb_dim, groups, eps):
+        self.name, self.cin, self.cout, self.groups, self.eps = name, cin, cout, groups, eps
+        self.norm1 = Norm(f"{name}.norm1", cin)
+        self.conv1 = Conv(f"{name}.conv1", cin, cout)
+        self.temb = Linear(f"{name}.time_emb_proj", temb_dim, cout) if temb_dim else None
+        self.norm2 = Norm(f"{name}.norm2", cout)
+        self.conv2 = Conv(f"{name}.conv2", cout, cout)
+        self.short = Conv(f"{name}.conv_shortcut", cin, cout, k=1, padding=0) if cin != cout else None
+
+    def params(self):
+        p = {}
+        for m in (self.norm1, self.conv1, self.temb, self.norm2, self.conv2, self.short):
+            if m is not None:
+                p.update(m.params())
+        return p
+
+    def __call__(self, W, x, temb=None):
+        h = ops.group_norm(x, W[f"{self.name}.norm1.weight"], W[f"{self.name}.norm1.bias"],
+                           self.groups, self.eps, silu=True)
+        h = self.conv1(W, h)
+        if self.temb is not None and temb is not None:
+            h = h + self.temb(W, F.silu(temb))[:, :, None, None]
+        h = ops.group_norm(h, W[f"{self.name}.norm2.weight"], W[f"{self.name}.norm2.bias"],
+                           self.groups, self.eps, silu=True)
+        h = self.conv2(W, h)
+        return (self.short(W, x) if self.short is not None else x) + h
+
+
+class Attention(Module):
+    """diffusers Attention: to_q/to_k/to_v (no bias), to_out.0 (bias)."""
+
+    def __init__(self, name, dim, ctx_dim, heads, sliced=None):
+        self.name, self.heads, self.sliced = name, heads, sliced
+        self.q = Linear(f"{name}.to_q", dim, dim, bias=False)
+        self.k = Linear(f"{name}.to_k", ctx_dim, dim, bias=False)
+        self.v = Linear(f"{name}.to_v", ctx_dim, dim, bias=False)
+        self.o = Linear(f"{name}.to_out.0", dim, dim)
+
+    def params(self):
+        p = {}
+        for m in (self.q, self.k, self.v, self.o):
+            p.update(m.params())
+        return p
+
+    def __call__(self, W, x, ctx=None):
+        c = x if ctx is None else ctx
+        a = ops.attention(self.q(W, x), self.k(W, c), self.v(W, c), self.heads, sliced=self.sliced)
+        return self.o(W, a)
+
+
+class BasicTransformerBlock(Module):
+    def __init__(self, name, dim, ctx_dim, heads, sliced):
+        self.name = name
+        self.n1, self.n2, self.n3 = (Norm(f"{name}.norm{i}", dim) for i in (1, 2, 3))
+        self.attn1 = Attention(f"{name}.attn1", dim, dim, heads, sliced)
+        self.attn2 = Attention(f"{name}.attn2", dim, ctx_dim, heads, sliced)
+        self.ff_in = Linear(f"{name}.ff.net.0.proj", dim, dim * 8)  # GEGLU: 2 x 4*dim
+        self.ff_out = Linear(f"{name}.ff.net.2", dim * 4, dim)
+
+    def params(self):
+        p = {}
+        for m in (self.n1, self.n2, self.n3, self.attn1, self.attn2, self.ff_in, self.ff_out):
+            p.update(m.params())
+        return p
+
+    def __call__(self, W, x, ctx):
+        n = self.name
+        x = x + self.attn1(W, ops.layer_norm(x, W[f"{n}.norm1.weight"], W[f"{n}.norm1.bias"], 1e-5))
+        x = x + self.attn2(W, ops.layer_norm(x, W[f"{n}.norm2.weight"], W[f"{n}.norm2.bias"], 1e-5),
+                           ctx)
+        h = ops.layer_norm(x, W[f"{n}.norm3.weight"], W[f"{n}.norm3.bias"], 1e-5)
+        return x + self.ff_out(W, ops.geglu(self.ff_in(W, h)))
+
+
+class Transformer2DModel(Module):
+    """SpatialTransformer: GroupNorm → proj_in → blocks → proj_out → + residual."""
+
+    def __init__(self, name, ch, ctx_dim, heads, layers, linear_proj, groups, sliced):
+        self.name, self.ch, self.groups, self.linear = name, ch, groups, linear_proj
+        self.norm = Norm(f"{name}.norm", ch)
+        mk = (lambda n: Linear(n, ch, ch)) if linear_proj else (lambda n: Conv(n, ch, ch, 1, 1, 0))
+        self.proj_in, self.proj_out = mk(f"{name}.proj_in"), mk(f"{name}.proj_out")
+        self.blocks = [BasicTransformerBlock(f"{name}.transformer_blocks.{i}", ch, ctx_dim, heads,
+                                             sliced) for i in range(layers)]
+
+    def params(self):
+        p = {}
+        for m in (self.norm, self.proj_in, self.proj_out, *self.blocks):
+            p.update(m.params())
+        return p
+
+    def __call__(self, W, x, ctx):
+        B, C, H, Wd = x.shape
+        h = ops.group_norm(x, W[f"{self.name}.norm.weight"], W[f"{self.name}.norm.bias"],
+                           self.groups, 1e-6)
+        if self.linear:
+            h = self.proj_in(W, h.permute(0, 2, 3, 1).reshape(B, H * Wd, C))
+        else:
+            h = self.proj_in(W, h).permute(0, 2, 3, 1).reshape(B, H * Wd, C)
+        for blk in self.blocks:
+            h = blk(W, h, ctx)
+        if self.linear:
+            h = self.proj_out(W, h).reshape(B, H, Wd, C).permute(0, 3, 1, 2)
+        else:
+            h = self.proj_out(W, h.reshape(B, H, Wd, C).permute(0, 3, 1, 2).contiguous())
+        return h.contiguous() + x
+
+
+def timestep_embedding(t: torch.Tensor, dim: int, flip_sin_to_cos: bool, shift: float) -> torch.Tensor:
+    half = dim // 2
+    exponent = -math.log(10000.0) * torch.arange(half, dtype=torch.float32, device=t.device) / (half - shift)
+    emb = t.float()[:, None] * torch.exp(exponent)[None]
+    emb = torch.cat([torch.sin(emb), torch.cos(emb)], -1)
+    if flip_sin_to_cos:
+        emb = torch.cat([emb[:, half:], emb[:, :half]], -1)
+    return emb
+
+
+class UNet2DConditionModel(Module):
+    def __init__(self, cfg: UNetConfig):
+        self.cfg = cfg
+        chans = [b.out_channels for b in cfg.blocks]
+        G, eps, ctx, lin, sl = (cfg.norm_num_groups, cfg.norm_eps, cfg.cross_attention_dim,
+                                cfg.use_linear_projection, cfg.sliced_attention_size)
+        temb = chans[0] * 4
+        self.temb_dim = temb
+        self.conv_in = Conv("conv_in", cfg.in_channels, chans[0])
+        self.t1 = Linear("time_embedding.linear_1", chans[0], temb)
+        self.t2 = Linear("time_embedding.linear_2", temb, temb)
+        self.down = []
+        cout = chans[0]
+        for i, b in enumerate(cfg.blocks):
+            cin, cout = cout, b.out_channels
+            final = i == len(cfg.blocks) - 1
+            res, att = [], []
+            for j in range(cfg.layers_per_block):
+                res.append(ResnetBlock2D(f"down_blocks.{i}.resnets.{j}", cin if j == 0 else cout,
+                                         cout, temb, G, eps))
+                if b.cross_attn:
+                    att.append(Transformer2DModel(f"down_blocks.{i}.attentions.{j}", cout, ctx,
+                                                  b.heads, b.transformer_layers, lin, G, sl))
+            ds = None if final else Conv(f"down_blocks.{i}.downsamplers.0.conv", cout, cout, 3, 2, 1)
+            self.down.append((res, att, ds))
+        mid = cfg.blocks[-1]
+        cm = chans[-1]
+        self.mid_res = [ResnetBlock2D(f"mid_block.resnets.{j}", cm, cm, temb, G, eps) for j in (0, 1)]
+        self.mid_att = Transformer2DModel("mid_block.attentions.0", cm, ctx, mid.heads,
+                                          mid.transformer_layers, lin, G, sl)
+        self.up = []
+        rev = list(reversed(chans))
+        rblocks = list(reversed(cfg.blocks))
+        out_ch = rev[0]
+        for i, b in enumerate(rblocks):
+            prev_out, out_ch = out_ch, rev[i]
+            in_ch = rev[min(i + 1, len(chans) - 1)]
+            final = i == len(chans) - 1
+            res, att = [], []
+            n = cfg.layers_per_block + 1
+            for j in range(n):
+                skip = in_ch if j == n - 1 else out_ch
+                rin = prev_out if j == 0 else out_ch
+                res.append(ResnetBlock2D(f"up_blocks.{i}.resnets.{j}", rin + skip, out_ch, temb, G, eps))
+                if b.cross_attn:
+                    att.append(Transformer2DModel(f"up_blocks.{i}.attentions.{j}", out_ch, ctx,
+                                                  b.heads, b.transformer_layers, lin, G, sl))
+            us = None if final else Conv(f"up_blocks.{i}.upsamplers.0.conv", out_ch, out_ch)
+            self.up.append((res, att, us))
+        self.norm_out = Norm("conv_norm_out", chans[0])
+        self.conv_out = Conv("conv_out", chans[0], cfg.out_channels)
+
+    def params(self) -> dict[str, tuple]:
+        p = {}
+        mods = [self.conv_in, self.t1, self.t2, *self.mid_res, self.mid_att, self.norm_out,
+                self.conv_out]
+        for res, att, s in self.down + self.up:
+            mods += res + att + ([s] if s else [])
+        for m in mods:
+            p.update(m.params())
+        return p
+
+    def forward(self, W, sample: torch.Tensor, timestep: float, ctx: torch.Tensor) -> torch.Tensor:
+        cfg = self.cfg
+        B = sample.shape[0]
+        dt = sample.dtype
+        t = torch.full((B,), float(timestep), device=sample.device)
+        emb = timestep_embedding(t, cfg.blocks[0].out_channels, cfg.flip_sin_to_cos,
+                                 cfg.freq_shift).to(dt)
+        emb = self.t2(W, F.silu(self.t1(W, emb)))
+        x = self.conv_in(W, sample)
+        skips = [x]
+        for res, att, ds in self.down:
+            for j, r in enumerate(res):
+                x = r(W, x, emb)
+                if att:
+                    x = att[j](W, x, ctx)
+                skips.append(x)
+            if ds is not None:
+                x = ds(W, x)
+                skips.append(x)
+        x = self.mid_res[0](W, x, emb)
+        x = self.mid_att(W, x, ctx)
+        x = self.mid_res[1](W, x, emb)
+        for res, att, us in self.up:
+            for j, r in enumerate(res):
+                x = r(W, torch.cat([x, skips.pop()], 1), emb)
+                if att:
+                    x = att[j](W, x, ctx)
+            if us is not None:
+                x = us(W, F.interpolate(x, scale_factor=2.0, mode="nearest"))
+        x = ops.group_norm(x, W["conv_norm_out.weight"], W["conv_norm_out.bias"],
+                           cfg.norm_num_groups, cfg.norm_eps, silu=True)
+        return self.conv_out(W, x)
