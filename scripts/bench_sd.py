@@ -1,0 +1,48 @@
+"""Seconds per diffusion step (UNet round trip incl. CFG batch doubling), random-init weights.
+
+The reference logs "step i/n done, {dt}s" (cake-core/src/models/sd/sd.rs:506-507);
+this measures the same quantity for a full-size UNet on one MI355X."""
+import argparse
+import json
+import sys
+import os
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from cake_amd.models.sd.config import get_config  # noqa: E402
+from cake_amd.models.sd.unet import UNet2DConditionModel  # noqa: E402
+from cake_amd.models.sd.weights import random_component  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--version", default="v1-5")
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--dtype", default="f16")
+    a = ap.parse_args()
+    dt = torch.float16 if a.dtype == "f16" else torch.bfloat16
+    cfg = get_config(a.version)
+    dev = torch.device("cuda:0")
+    w = random_component("unet", cfg, dev, dt)
+    unet = UNet2DConditionModel(cfg.unet)
+    B = 2  # classifier-free guidance doubles the batch
+    x = torch.randn(B, 4, cfg.height // 8, cfg.width // 8, device=dev, dtype=dt)
+    ctx = torch.randn(B, 77, cfg.unet.cross_attention_dim, device=dev, dtype=dt)
+    with torch.no_grad():
+        for _ in range(2):
+            unet.forward(w, x, 500, ctx)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(a.steps):
+            unet.forward(w, x, 999 - i, ctx)
+        torch.cuda.synchronize()
+    dt_step = (time.perf_counter() - t0) / a.steps
+    print(json.dumps({"metric": "sd_unet_seconds_per_step", "version": a.version,
+                      "resolution": f"{cfg.width}x{cfg.height}", "batch": B, "dtype": a.dtype,
+                      "value": round(dt_step, 4), "unit": "s/step"}))
+
+
+if __name__ == "__main__":
+    main()
