@@ -100,8 +100,10 @@ def bench_single(a) -> None:
                         greedy=True, use_graph=not a.no_graph)
     g = torch.Generator().manual_seed(1234)
     prompt = torch.randint(0, model.cfg.vocab_size, (a.prompt_len,), generator=g).tolist()
+    dec.start(prompt)  # cold: first-call library/module setup
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
-    dec.start(prompt)
+    dec.start(prompt)  # warm TTFT (prefill + first token), reported separately from tok/s
     torch.cuda.synchronize()
     ttft = (time.perf_counter() - t0) * 1e3
     dec.capture()
