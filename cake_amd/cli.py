@@ -73,7 +73,8 @@ def build_parser() -> argparse.ArgumentParser:
     # MI355X-native extras
     a("--max-seq-len", type=int, default=4096)
     a("--no-graph", action="store_true", help="disable hipGraph capture of the decode step")
-    a("--trace", default=None, help="write a chrome-trace JSON of the run")
+    a("--trace", default=None, help="write a chrome-trace JSON of each text generation")
+    a("--metrics", default=None, help="append one JSON line of stats per generation")
     a("--log-level", default=os.environ.get("CAKE_LOG", "info"))
     return ap
 

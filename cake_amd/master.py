@@ -93,11 +93,27 @@ class Master:
                 lat = sorted(dev.step_ms)
             stats["p50_ms"] = lat[len(lat) // 2]
             stats["p99_ms"] = lat[min(len(lat) - 1, int(round(0.99 * (len(lat) - 1))))]
+        self._export(stats, t_start, times)
         log.info("%d tokens generated (%.2f token/s) p50=%.2fms p99=%.2fms ttft=%.1fms - mem=%.1f MiB",
                  generated, stats.get("tokens_per_sec", 0.0), stats.get("p50_ms", 0.0),
                  stats.get("p99_ms", 0.0), stats.get("ttft_ms", 0.0), rss_mib())
         self.last_stats = stats
         return stats
+
+    def _export(self, stats: dict, t_start: float, times: list[float]) -> None:
+        a = self.ctx.args
+        if getattr(a, "metrics", None):
+            import json
+            with open(a.metrics, "a") as f:
+                f.write(json.dumps({"ts": time.time(), "kind": "text", **stats}) + "\n")
+        if getattr(a, "trace", None) and times:
+            from .utils.trace import ChromeTrace
+            tr = ChromeTrace()
+            tr.t0 = t_start
+            tr.add("prefill+first token", t_start, times[0])
+            for i, (x, y) in enumerate(zip(times, times[1:])):
+                tr.add(f"token {i + 1}", x, y)
+            tr.save(a.trace)
 
     def generate_image(self, args, callback) -> None:
         self.sd.generate_image(args, callback)
