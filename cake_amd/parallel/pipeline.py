@@ -120,6 +120,15 @@ class PipelineEngine:
         self.group = group
         # gloo with device tensors (1-GPU multi-process tests): stage via the host
         self.staged = dist.is_initialized() and dist.get_backend(group) == "gloo"
+        # Hops toward a higher rank and toward a lower rank use two different
+        # communicators (own RCCL comm + stream each), so two ranks exchanging in
+        # both directions never serialise a send behind a recv on one stream —
+        # the schedule is deadlock-free even with rendezvous (unbuffered) sends.
+        self.g_up = self.g_down = group
+        if dist.is_initialized() and world > 1:
+            ranks = list(range(world))
+            self.g_up = dist.new_group(ranks)
+            self.g_down = dist.new_group(ranks)
         if stack.max_sessions < streams:
             stack.max_sessions = streams
         self.streams = [_Stream(self, s) for s in range(streams)]
@@ -143,18 +152,20 @@ class PipelineEngine:
         return self.runs[last - 1].owner if last > 0 else 0
 
     def _send(self, t: torch.Tensor, dst: int):
+        g = self.g_up if dst > self.rank else self.g_down
         if self.staged and t.is_cuda:
             host = t.to("cpu")          # gloo moves host memory only: stage through the host
-            return dist.isend(host, dst, group=self.group)
-        return dist.isend(t, dst, group=self.group)
+            return dist.isend(host, dst, group=g)
+        return dist.isend(t, dst, group=g)
 
     def _recv(self, t: torch.Tensor, src: int) -> None:
+        g = self.g_up if src < self.rank else self.g_down
         if self.staged and t.is_cuda:
             host = torch.empty(t.shape, dtype=t.dtype)
-            dist.irecv(host, src, group=self.group).wait()
+            dist.irecv(host, src, group=g).wait()
             t.copy_(host)
             return
-        dist.irecv(t, src, group=self.group).wait()
+        dist.irecv(t, src, group=g).wait()
 
     @staticmethod
     def _wait(work) -> None:
