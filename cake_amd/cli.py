@@ -71,6 +71,8 @@ def build_parser() -> argparse.ArgumentParser:
     a("--sd-img2img-strength", type=float, default=0.8)
     a("--sd-seed", type=int, default=None)
     # MI355X-native extras
+    a("--transport", choices=["tcp", "rccl"], default="tcp",
+      help="rccl: torchrun one rank per GPU, rank 0 master, rank i serves topology node i")
     a("--max-seq-len", type=int, default=4096)
     a("--no-graph", action="store_true", help="disable hipGraph capture of the decode step")
     a("--trace", default=None, help="write a chrome-trace JSON of each text generation")
@@ -91,6 +93,10 @@ def main(argv: list[str] | None = None) -> int:
     setup_logging(args.log_level)
     from .context import Context
     ctx = Context.from_args(args)
+    if args.transport == "rccl":
+        from .parallel.rccl_roles import run_rccl
+        run_rccl(ctx)
+        return 0
     if args.mode == "worker":
         from .parallel.worker import Worker
         Worker(ctx).run()

@@ -82,90 +82,94 @@ __device__ __forceinline__ void load_x8(const void* xs, int chunk, float* o) {
 }
 
 // ---------------------------------------------------------------------------
-// core: one wave, two rows, dot with the staged x.  U = 16-byte chunks per row
-// in flight per lane per iteration (2*U loads outstanding).
-//
-// The first batch of a wave's first row pair is issued BEFORE the x prologue
-// (rmsnorm / x staging) so HBM latency overlaps the prologue (PairPrefetch).
+// core: one wave computes dot products of a PAIR of weight rows with the x row
+// staged in LDS.  U = 16-byte chunks per row in flight per lane per iteration
+// (2*U loads outstanding).  PFC = chunks per row per lane of the wave's FIRST
+// pair issued before the x prologue (RMSNorm / staging) so the HBM stream
+// overlaps it; for K = 4096 PFC = 8 is the whole pair (64 VGPRs).  All
+// register arrays are indexed by compile-time constants (no scratch).
 // ---------------------------------------------------------------------------
-template <int U>
-struct PairPrefetch {
-  uint4 va[U], vb[U];
-  bool valid = false;
-};
-
-template <int U>
-__device__ __forceinline__ void prefetch_pair(const uint16_t* wa, const uint16_t* wb, int K,
-                                              PairPrefetch<U>& pf) {
-  const int lane = threadIdx.x & 63;
-  if ((K >> 3) < 64 * U) return;  // too short for a full batch: no prefetch
-  const uint4* a4 = reinterpret_cast<const uint4*>(wa);
-  const uint4* b4 = reinterpret_cast<const uint4*>(wb);
+template <int DT, bool XF32>
+__device__ __forceinline__ void fma_chunk(const void* xs, int chunk, const uint4 va,
+                                          const uint4 vb, float& acc_a, float& acc_b) {
+  float xv[8], fa[8], fb[8];
+  load_x8<DT, XF32>(xs, chunk, xv);
+  unpack8<DT>(va, fa);
+  unpack8<DT>(vb, fb);
 #pragma unroll
-  for (int u = 0; u < U; ++u) {
-    pf.va[u] = ld_nt16(a4 + u * 64 + lane);
-    pf.vb[u] = ld_nt16(b4 + u * 64 + lane);
-  }
-  pf.valid = true;
-}
-
-template <int DT, bool XF32, int U>
-__device__ __forceinline__ void consume_batch(const void* xs, int c0, const uint4 (&va)[U],
-                                              const uint4 (&vb)[U], float& acc_a, float& acc_b) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    float xv[8], fa[8], fb[8];
-    load_x8<DT, XF32>(xs, c0 + u * 64 + lane, xv);
-    unpack8<DT>(va[u], fa);
-    unpack8<DT>(vb[u], fb);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      acc_a = fmaf(fa[e], xv[e], acc_a);
-      acc_b = fmaf(fb[e], xv[e], acc_b);
-    }
+  for (int e = 0; e < 8; ++e) {
+    acc_a = fmaf(fa[e], xv[e], acc_a);
+    acc_b = fmaf(fb[e], xv[e], acc_b);
   }
 }
 
+// accumulate chunks [c_start, nch) of rows wa, wb
 template <int DT, bool XF32, int U>
-__device__ __forceinline__ void dot_pair(const uint16_t* __restrict__ wa,
-                                         const uint16_t* __restrict__ wb,
-                                         const void* xs, int K, float& da, float& db,
-                                         PairPrefetch<U>* pf = nullptr) {
+__device__ __forceinline__ void dot_range(const uint16_t* __restrict__ wa,
+                                          const uint16_t* __restrict__ wb, const void* xs,
+                                          int nch, int c_start, float& acc_a, float& acc_b) {
   const int lane = threadIdx.x & 63;
-  const int nch = K >> 3;  // 16-byte chunks per row
   const uint4* a4 = reinterpret_cast<const uint4*>(wa);
   const uint4* b4 = reinterpret_cast<const uint4*>(wb);
-  float acc_a = 0.f, acc_b = 0.f;
-  const int full = (nch / (64 * U)) * (64 * U);
-  int c0 = 0;
-  if (pf && pf->valid) {
-    consume_batch<DT, XF32, U>(xs, 0, pf->va, pf->vb, acc_a, acc_b);
-    pf->valid = false;
-    c0 = 64 * U;
-  }
-  for (; c0 < full; c0 += 64 * U) {
+  const int full = c_start + ((nch - c_start) / (64 * U)) * (64 * U);
+  for (int c0 = c_start; c0 < full; c0 += 64 * U) {
     uint4 va[U], vb[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       va[u] = ld_nt16(a4 + c0 + u * 64 + lane);
       vb[u] = ld_nt16(b4 + c0 + u * 64 + lane);
     }
-    consume_batch<DT, XF32, U>(xs, c0, va, vb, acc_a, acc_b);
-  }
-  for (int c = full + lane; c < nch; c += 64) {  // tail (small test shapes only)
-    float xv[8], fa[8], fb[8];
-    load_x8<DT, XF32>(xs, c, xv);
-    unpack8<DT>(a4[c], fa);
-    unpack8<DT>(b4[c], fb);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      acc_a = fmaf(fa[e], xv[e], acc_a);
-      acc_b = fmaf(fb[e], xv[e], acc_b);
+    for (int u = 0; u < U; ++u) fma_chunk<DT, XF32>(xs, c0 + u * 64 + lane, va[u], vb[u], acc_a, acc_b);
+  }
+  for (int c = full + lane; c < nch; c += 64) fma_chunk<DT, XF32>(xs, c, a4[c], b4[c], acc_a, acc_b);
+}
+
+template <int N> struct Regs { uint4 a[N], b[N]; };
+template <> struct Regs<0> { uint4 a[1], b[1]; };
+
+// issue the first PFC chunks of (wa, wb)
+template <int PFC>
+__device__ __forceinline__ void prefetch_rows(const uint16_t* wa, const uint16_t* wb, Regs<PFC>& r) {
+  if constexpr (PFC > 0) {
+    const int lane = threadIdx.x & 63;
+    const uint4* a4 = reinterpret_cast<const uint4*>(wa);
+    const uint4* b4 = reinterpret_cast<const uint4*>(wb);
+#pragma unroll
+    for (int c = 0; c < PFC; ++c) {
+      r.a[c] = ld_nt16(a4 + c * 64 + lane);
+      r.b[c] = ld_nt16(b4 + c * 64 + lane);
     }
   }
-  da = wave_sum(acc_a);
-  db = wave_sum(acc_b);
+}
+
+// Walk the wave's pairs p0, p0+stride, ...: map(p, wa, wb) gives the rows,
+// epi(p, da, db) consumes the two dot products (full wave sums).
+template <int DT, bool XF32, int U, int PFC, class Map, class Epi>
+__device__ __forceinline__ void run_pairs(const Map& map, const Epi& epi, const void* xs, int K,
+                                          int npairs, int p0, int stride, const Regs<PFC>& pre) {
+  const int nch = K >> 3;
+  int p = p0;
+  if constexpr (PFC > 0) {
+    if (p < npairs) {
+      const uint16_t *wa, *wb;
+      map(p, wa, wb);
+      const int lane = threadIdx.x & 63;
+      float aa = 0.f, ab = 0.f;
+#pragma unroll
+      for (int c = 0; c < PFC; ++c) fma_chunk<DT, XF32>(xs, c * 64 + lane, pre.a[c], pre.b[c], aa, ab);
+      dot_range<DT, XF32, U>(wa, wb, xs, nch, PFC * 64, aa, ab);
+      epi(p, wave_sum(aa), wave_sum(ab));
+      p += stride;
+    }
+  }
+  for (; p < npairs; p += stride) {
+    const uint16_t *wa, *wb;
+    map(p, wa, wb);
+    float aa = 0.f, ab = 0.f;
+    dot_range<DT, XF32, U>(wa, wb, xs, nch, 0, aa, ab);
+    epi(p, wave_sum(aa), wave_sum(ab));
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -205,51 +209,53 @@ __device__ __forceinline__ QkvRow qkv_row(const QkvArgs& a, int p) {
   return r;
 }
 
-template <int DT, int U, bool PF>
+template <int DT, int U, int PFC>
 __global__ __launch_bounds__(kGemvThreads) void qkv_rope_kernel(QkvArgs a) {
   extern __shared__ float xs[];
   const int half = a.hd >> 1;
   const int npairs = (a.nh + 2 * a.nkv) * half;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int p0 = blockIdx.x * kGemvWaves + wave;
-  PairPrefetch<U> pf;
-  if (PF && p0 < npairs) {
-    const QkvRow r = qkv_row(a, p0);
-    prefetch_pair<U>(r.base + r.ra * a.K, r.base + (r.ra + half) * a.K, a.K, pf);
+  auto map = [&](int p, const uint16_t*& wa, const uint16_t*& wb) {
+    const QkvRow r = qkv_row(a, p);
+    wa = r.base + r.ra * a.K;
+    wb = r.base + (r.ra + half) * a.K;
+  };
+  Regs<PFC> pre;
+  if (PFC > 0 && p0 < npairs) {
+    const uint16_t *wa, *wb;
+    map(p0, wa, wb);
+    prefetch_rows<PFC>(wa, wb, pre);
   }
   stage_rmsnorm<DT>(a.resid, a.norm_w, a.eps, a.K, xs);
   const int pos = *a.pos;
-  for (int p = p0; p < npairs; p += gridDim.x * kGemvWaves) {
+  auto epi = [&](int p, float da, float db) {
+    if (lane != 0) return;
     const QkvRow r = qkv_row(a, p);
-    const int kind = r.kind, head = r.head, i = r.i;
-    const size_t ra = r.ra;
-    float da, db;
-    dot_pair<DT, true, U>(r.base + ra * a.K, r.base + (ra + half) * a.K, xs, a.K, da, db, &pf);
-    if (lane == 0) {
-      float oa = da, ob = db;
-      if (kind < 2) {
-        float s, c;
-        sincosf((float)pos * a.inv_freq[i], &s, &c);
-        oa = da * c - db * s;
-        ob = da * s + db * c;
-      }
-      if (kind == 0) {
-        a.q_out[ra] = oa;
-        a.q_out[ra + half] = ob;
-      } else {
-        uint16_t* cache = kind == 1 ? a.kcache : a.vcache;
-        const size_t off = ((size_t)head * a.S + pos) * a.hd + i;
-        cache[off] = from_f32<DT>(oa);
-        cache[off + half] = from_f32<DT>(ob);
-      }
+    float oa = da, ob = db;
+    if (r.kind < 2) {
+      float s, c;
+      sincosf((float)pos * a.inv_freq[r.i], &s, &c);
+      oa = da * c - db * s;
+      ob = da * s + db * c;
     }
-  }
+    if (r.kind == 0) {
+      a.q_out[r.ra] = oa;
+      a.q_out[r.ra + half] = ob;
+    } else {
+      uint16_t* cache = r.kind == 1 ? a.kcache : a.vcache;
+      const size_t off = ((size_t)r.head * a.S + pos) * a.hd + r.i;
+      cache[off] = from_f32<DT>(oa);
+      cache[off + half] = from_f32<DT>(ob);
+    }
+  };
+  run_pairs<DT, true, U, PFC>(map, epi, xs, a.K, npairs, p0, gridDim.x * kGemvWaves, pre);
 }
 
 // ---------------------------------------------------------------------------
 // RMSNorm + gate/up + SiLU*mul
 // ---------------------------------------------------------------------------
-template <int DT, int U, bool PF>
+template <int DT, int U, int PFC>
 __global__ __launch_bounds__(kGemvThreads) void swiglu_kernel(
     const float* __restrict__ resid, const uint16_t* __restrict__ norm_w, float eps,
     const uint16_t* __restrict__ wg, const uint16_t* __restrict__ wu, int K, int I,
@@ -257,21 +263,24 @@ __global__ __launch_bounds__(kGemvThreads) void swiglu_kernel(
   extern __shared__ float xs[];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int j0 = blockIdx.x * kGemvWaves + wave;
-  PairPrefetch<U> pf;
-  if (PF && j0 < I) prefetch_pair<U>(wg + (size_t)j0 * K, wu + (size_t)j0 * K, K, pf);
+  auto map = [&](int j, const uint16_t*& wa, const uint16_t*& wb) {
+    wa = wg + (size_t)j * K;
+    wb = wu + (size_t)j * K;
+  };
+  Regs<PFC> pre;
+  if (PFC > 0 && j0 < I) prefetch_rows<PFC>(wg + (size_t)j0 * K, wu + (size_t)j0 * K, pre);
   stage_rmsnorm<DT>(resid, norm_w, eps, K, xs);
-  for (int j = j0; j < I; j += gridDim.x * kGemvWaves) {
-    float g, u;
-    dot_pair<DT, true, U>(wg + (size_t)j * K, wu + (size_t)j * K, xs, K, g, u, &pf);
+  auto epi = [&](int j, float g, float u) {
     if (lane == 0) act[j] = from_f32<DT>(silu(g) * u);
-  }
+  };
+  run_pairs<DT, true, U, PFC>(map, epi, xs, K, I, j0, gridDim.x * kGemvWaves, pre);
 }
 
 // ---------------------------------------------------------------------------
 // out (+)= W x   with 16-bit x: o_proj / down_proj (accumulate into the f32
 // residual stream) — or plain f32 output.
 // ---------------------------------------------------------------------------
-template <int DT, int U, bool PF, bool ACCUM>
+template <int DT, int U, int PFC, bool ACCUM>
 __global__ __launch_bounds__(kGemvThreads) void gemv_x16_kernel(
     const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, int K, int N,
     float* __restrict__ out) {
@@ -280,23 +289,28 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_x16_kernel(
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int npairs = (N + 1) >> 1;
   const int p0 = blockIdx.x * kGemvWaves + wave;
-  PairPrefetch<U> pf;
-  if (PF && p0 < npairs)
-    prefetch_pair<U>(w + (size_t)(2 * p0) * K, w + (size_t)min(2 * p0 + 1, N - 1) * K, K, pf);
-  stage_plain16(x, K, xs);
-  for (int p = p0; p < npairs; p += gridDim.x * kGemvWaves) {
-    const int ra = 2 * p, rb = min(2 * p + 1, N - 1);
-    float da, db;
-    dot_pair<DT, false, U>(w + (size_t)ra * K, w + (size_t)rb * K, xs, K, da, db, &pf);
-    if (lane == 0) {
-      if (ACCUM) out[ra] += da; else out[ra] = da;
-      if (2 * p + 1 < N) { if (ACCUM) out[rb] += db; else out[rb] = db; }
-    }
+  auto map = [&](int p, const uint16_t*& wa, const uint16_t*& wb) {
+    wa = w + (size_t)(2 * p) * K;
+    wb = w + (size_t)min(2 * p + 1, N - 1) * K;
+  };
+  Regs<PFC> pre;
+  if (PFC > 0 && p0 < npairs) {
+    const uint16_t *wa, *wb;
+    map(p0, wa, wb);
+    prefetch_rows<PFC>(wa, wb, pre);
   }
+  stage_plain16(x, K, xs);
+  auto epi = [&](int p, float da, float db) {
+    if (lane != 0) return;
+    const int ra = 2 * p, rb = 2 * p + 1;
+    if (ACCUM) out[ra] += da; else out[ra] = da;
+    if (rb < N) { if (ACCUM) out[rb] += db; else out[rb] = db; }
+  };
+  run_pairs<DT, false, U, PFC>(map, epi, xs, K, npairs, p0, gridDim.x * kGemvWaves, pre);
 }
 
 // RMSNorm(f32 row) then f32 output: the lm_head.
-template <int DT, int U, bool PF>
+template <int DT, int U, int PFC>
 __global__ __launch_bounds__(kGemvThreads) void gemv_norm_f32_kernel(
     const float* __restrict__ resid, const uint16_t* __restrict__ norm_w, float eps,
     const uint16_t* __restrict__ w, int K, int N, float* __restrict__ out) {
@@ -304,19 +318,23 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_norm_f32_kernel(
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int npairs = (N + 1) >> 1;
   const int p0 = blockIdx.x * kGemvWaves + wave;
-  PairPrefetch<U> pf;
-  if (PF && p0 < npairs)
-    prefetch_pair<U>(w + (size_t)(2 * p0) * K, w + (size_t)min(2 * p0 + 1, N - 1) * K, K, pf);
-  stage_rmsnorm<DT>(resid, norm_w, eps, K, xs);
-  for (int p = p0; p < npairs; p += gridDim.x * kGemvWaves) {
-    const int ra = 2 * p, rb = min(2 * p + 1, N - 1);
-    float da, db;
-    dot_pair<DT, true, U>(w + (size_t)ra * K, w + (size_t)rb * K, xs, K, da, db, &pf);
-    if (lane == 0) {
-      out[ra] = da;
-      if (2 * p + 1 < N) out[rb] = db;
-    }
+  auto map = [&](int p, const uint16_t*& wa, const uint16_t*& wb) {
+    wa = w + (size_t)(2 * p) * K;
+    wb = w + (size_t)min(2 * p + 1, N - 1) * K;
+  };
+  Regs<PFC> pre;
+  if (PFC > 0 && p0 < npairs) {
+    const uint16_t *wa, *wb;
+    map(p0, wa, wb);
+    prefetch_rows<PFC>(wa, wb, pre);
   }
+  stage_rmsnorm<DT>(resid, norm_w, eps, K, xs);
+  auto epi = [&](int p, float da, float db) {
+    if (lane != 0) return;
+    out[2 * p] = da;
+    if (2 * p + 1 < N) out[2 * p + 1] = db;
+  };
+  run_pairs<DT, true, U, PFC>(map, epi, xs, K, npairs, p0, gridDim.x * kGemvWaves, pre);
 }
 
 // Launch geometry per kernel kind (tunable at run time; defaults from the
@@ -324,7 +342,7 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_norm_f32_kernel(
 // PF = prefetch the first weight batch before the x prologue, MB = grid cap.
 struct GemvTune { int U, PF, MB; };
 enum GemvKind { kQkv = 0, kSwiglu = 1, kX16 = 2, kNormF32 = 3, kNumKinds = 4 };
-// measured: profiles/r1_gemv_tune_8b.txt (lm_head 7.0 TB/s at 256 blocks)
+// measured: profiles/r1_gemv_tune_8b*.txt (lm_head 7.0 TB/s at 256 blocks)
 static GemvTune g_tune[kNumKinds] = {{8, 0, 1024}, {2, 0, 512}, {4, 0, 1024}, {4, 0, 256}};
 
 static inline int grid_for(int npairs, int max_blocks) {
@@ -343,19 +361,25 @@ using namespace cake;
     else return (int)hipErrorInvalidValue;         \
   } while (0)
 
-// Expand BODY for the run-time (U, PF) choice.
-#define DISPATCH_TUNE(t, ...)                                                        \
+// Expand BODY for the run-time (U, PFC) choice; PFC falls back to 0 when a
+// row is shorter than PFC*64 chunks (small test shapes).
+#define CAKE_TUNE_U(PFCV, ...)                                                       \
+  if (t.U == 2) { constexpr int U = 2; constexpr int PF = PFCV; __VA_ARGS__; }       \
+  else if (t.U == 8) { constexpr int U = 8; constexpr int PF = PFCV; __VA_ARGS__; }  \
+  else { constexpr int U = 4; constexpr int PF = PFCV; __VA_ARGS__; }
+#define DISPATCH_TUNE(t, K, ...)                                                     \
   do {                                                                               \
-    if ((t).U == 2 && !(t).PF) { constexpr int U = 2; constexpr bool PF = false; __VA_ARGS__; } \
-    else if ((t).U == 8 && !(t).PF) { constexpr int U = 8; constexpr bool PF = false; __VA_ARGS__; } \
-    else if ((t).U == 4 && (t).PF) { constexpr int U = 4; constexpr bool PF = true; __VA_ARGS__; } \
-    else { constexpr int U = 4; constexpr bool PF = false; __VA_ARGS__; }            \
+    const int pfc_ = ((K) / 8 >= 64 * (t).PF) ? (t).PF : 0;                          \
+    if (pfc_ == 8) { CAKE_TUNE_U(8, __VA_ARGS__) }                                   \
+    else if (pfc_ == 4) { CAKE_TUNE_U(4, __VA_ARGS__) }                              \
+    else { CAKE_TUNE_U(0, __VA_ARGS__) }                                             \
   } while (0)
 
 CAKE_API int cake_gemv_set_tuning(int kind, int U, int prefetch, int max_blocks) {
-  if (kind < 0 || kind >= kNumKinds || (U != 2 && U != 4 && U != 8) || max_blocks < 1)
+  if (kind < 0 || kind >= kNumKinds || (U != 2 && U != 4 && U != 8) || max_blocks < 1 ||
+      (prefetch != 0 && prefetch != 4 && prefetch != 8))
     return (int)hipErrorInvalidValue;
-  g_tune[kind] = GemvTune{U, prefetch ? 1 : 0, max_blocks};
+  g_tune[kind] = GemvTune{U, prefetch, max_blocks};
   return 0;
 }
 
@@ -371,7 +395,7 @@ CAKE_API int cake_qkv_rope(int dt, const float* resid, const void* norm_w, float
   const int npairs = (nh + 2 * nkv) * (hd / 2);
   const size_t lds = (size_t)K * sizeof(float);
   const GemvTune t = g_tune[kQkv];
-  DISPATCH_DT(dt, DISPATCH_TUNE(t, hipLaunchKernelGGL((qkv_rope_kernel<DT, U, PF>),
+  DISPATCH_DT(dt, DISPATCH_TUNE(t, K, hipLaunchKernelGGL((qkv_rope_kernel<DT, U, PF>),
                                                       dim3(grid_for(npairs, t.MB)),
                                                       dim3(kGemvThreads), lds, st, a)));
   return (int)hipGetLastError();
@@ -383,7 +407,7 @@ CAKE_API int cake_swiglu(int dt, const float* resid, const void* norm_w, float e
   if (K % 8) return (int)hipErrorInvalidValue;
   const size_t lds = (size_t)K * sizeof(float);
   const GemvTune t = g_tune[kSwiglu];
-  DISPATCH_DT(dt, DISPATCH_TUNE(t, hipLaunchKernelGGL((swiglu_kernel<DT, U, PF>),
+  DISPATCH_DT(dt, DISPATCH_TUNE(t, K, hipLaunchKernelGGL((swiglu_kernel<DT, U, PF>),
                                                       dim3(grid_for(I, t.MB)), dim3(kGemvThreads),
                                                       lds, st, resid, (const uint16_t*)norm_w, eps,
                                                       (const uint16_t*)wg, (const uint16_t*)wu, K,
@@ -398,12 +422,12 @@ CAKE_API int cake_gemv_x16(int dt, const void* x, const void* w, int K, int N, f
   const GemvTune t = g_tune[kX16];
   const int g = grid_for((N + 1) / 2, t.MB);
   if (accumulate) {
-    DISPATCH_DT(dt, DISPATCH_TUNE(t, hipLaunchKernelGGL((gemv_x16_kernel<DT, U, PF, true>),
+    DISPATCH_DT(dt, DISPATCH_TUNE(t, K, hipLaunchKernelGGL((gemv_x16_kernel<DT, U, PF, true>),
                                                         dim3(g), dim3(kGemvThreads), lds, st,
                                                         (const uint16_t*)x, (const uint16_t*)w, K,
                                                         N, out)));
   } else {
-    DISPATCH_DT(dt, DISPATCH_TUNE(t, hipLaunchKernelGGL((gemv_x16_kernel<DT, U, PF, false>),
+    DISPATCH_DT(dt, DISPATCH_TUNE(t, K, hipLaunchKernelGGL((gemv_x16_kernel<DT, U, PF, false>),
                                                         dim3(g), dim3(kGemvThreads), lds, st,
                                                         (const uint16_t*)x, (const uint16_t*)w, K,
                                                         N, out)));
@@ -416,7 +440,7 @@ CAKE_API int cake_gemv_norm_f32(int dt, const float* resid, const void* norm_w, 
   if (K % 8) return (int)hipErrorInvalidValue;
   const size_t lds = (size_t)K * sizeof(float);
   const GemvTune t = g_tune[kNormF32];
-  DISPATCH_DT(dt, DISPATCH_TUNE(t, hipLaunchKernelGGL((gemv_norm_f32_kernel<DT, U, PF>),
+  DISPATCH_DT(dt, DISPATCH_TUNE(t, K, hipLaunchKernelGGL((gemv_norm_f32_kernel<DT, U, PF>),
                                                       dim3(grid_for((N + 1) / 2, t.MB)),
                                                       dim3(kGemvThreads), lds, st, resid,
                                                       (const uint16_t*)norm_w, eps,

@@ -242,7 +242,7 @@ def push_token(src, tok, hist, hist_len, pos):
 GEMV_KINDS = {"qkv": 0, "swiglu": 1, "x16": 2, "norm_f32": 3}
 
 
-def set_gemv_tuning(kind: str, U: int = 4, prefetch: bool = False, max_blocks: int = 1024) -> None:
+def set_gemv_tuning(kind: str, U: int = 4, prefetch: int = 0, max_blocks: int = 1024) -> None:
     """Select the decode-GEMV launch geometry for one kernel kind (see gemv.hip)."""
     check(kernels().cake_gemv_set_tuning(GEMV_KINDS[kind], int(U), int(prefetch), int(max_blocks)),
           "gemv_set_tuning")

@@ -34,7 +34,7 @@ from ..ops import reference as R
 
 HDR = 16          # int32 header words appended to each hop message
 H_POS, H_STREAM, H_T, H_FLAGS = 0, 1, 2, 3
-FLAG_RESET = 1
+FLAG_RESET, FLAG_PREFILL, FLAG_STOP = 1, 2, 4
 
 
 def shard_layers(num_layers: int, world: int, head_cost: float = 0.0) -> list[list[int]]:
@@ -115,6 +115,7 @@ class PipelineEngine:
             if missing:
                 raise ValueError(f"rank {rank} lacks weights for layers {missing}")
         self.penalty, self.last_n = float(repeat_penalty), int(repeat_last_n)
+        self.sampler = None  # host sampler (temperature > 0); None = greedy on device
         self.hip = stack.backend == "hip"
         self.use_graph = use_graph and self.hip
         self.group = group
@@ -193,15 +194,28 @@ class PipelineEngine:
     def _select_host(self, st: _Stream, logits: torch.Tensor) -> int:
         if self.penalty != 1.0:
             logits = R.apply_repeat_penalty(logits, self.penalty, st.host_tokens[-self.last_n:])
+        if self.sampler is not None:
+            return int(self.sampler(logits))
         return int(torch.argmax(logits))
 
     def _select_device(self, st: _Stream) -> None:
+        """Penalty (+ argmax + next-token bookkeeping when greedy) on the device."""
         from ..ops import hip as K
         b = st.bufs
         if self.penalty != 1.0:
             K.repeat_penalty(b.logits, b.hist, b.hist_len, self.last_n, self.penalty)
-        K.argmax(b.logits, b.slot)
-        K.finalize_token(b.slot, b.tok, b.hist, b.hist_len, b.pos)
+        if self.sampler is None:
+            K.argmax(b.logits, b.slot)
+            K.finalize_token(b.slot, b.tok, b.hist, b.hist_len, b.pos)
+
+    def _host_sample_device(self, st: _Stream) -> int:
+        """Sampled decoding on the hip path: draw on the host, push to the device state."""
+        from ..ops import hip as K
+        tok = int(self.sampler(st.bufs.logits))
+        src = torch.tensor([tok], dtype=torch.int32, device=self.device)
+        b = st.bufs
+        K.push_token(src, b.tok, b.hist, b.hist_len, b.pos)
+        return tok
 
     # ------------------------------------------------------------------ prefill
     def prefill(self, sid: int, prompt: list[int] | None = None) -> int | None:
@@ -210,37 +224,40 @@ class PipelineEngine:
         st = self.streams[sid]
         H = self.cfg.hidden_size
         self.stack.reset(sid)
+        # control header travels in the stream's hop message (flags = PREFILL|RESET)
+        hdr = st.hdr
         if self.is_master:
             T = len(prompt)
             ids = torch.tensor(prompt, dtype=torch.int32, device=self.device)
             h = torch.empty((T, H), device=self.device, dtype=torch.float32)
             self._embed(ids, h)
-        h_runs = self.runs
-        hdr = torch.zeros(HDR, dtype=torch.int32, device=self.device)
-        if self.is_master and self.runs[0].owner != 0:
-            hdr[H_POS], hdr[H_STREAM], hdr[H_T] = 0, sid, T
-            self._wait(self._send(hdr, self.runs[0].owner))
-            self._wait(self._send(h, self.runs[0].owner))
-        for j, run in enumerate(h_runs):
+            self._wait(st.send_work)
+            st.send_work = None
+            hdr[H_POS], hdr[H_STREAM], hdr[H_T], hdr[H_FLAGS] = 0, sid, T, FLAG_PREFILL | FLAG_RESET
+            if self.runs[0].owner != 0:
+                self._wait(self._send(st.msg, self.runs[0].owner))
+                self._wait(self._send(h, self.runs[0].owner))
+        for j, run in enumerate(self.runs):
             if run.owner != self.rank:
                 continue
-            if not (self.is_master and j == 0):
-                self._recv(hdr, self._prev(j))
-                T = int(hdr[H_T].item())
-                h = torch.empty((T, H), device=self.device, dtype=torch.float32)
-                self._recv(h, self._prev(j))
-            self.stack.forward(h, run.layers, 0, session=sid)
-            nxt = self._next(j)
-            if nxt != self.rank:
-                hdr[H_POS], hdr[H_STREAM], hdr[H_T] = 0, sid, T
-                self._wait(self._send(hdr, nxt))
-                self._wait(self._send(h, nxt))
+            if self.is_master and j == 0:
+                self.stack.forward(h, run.layers, 0, session=sid)
+                nxt = self._next(j)
+                if nxt != self.rank:
+                    self._wait(self._send(st.msg, nxt))
+                    self._wait(self._send(h, nxt))
+                continue
+            self._wait(st.send_work)
+            st.send_work = None
+            self._recv(st.msg, self._prev(j))
+            h = self._prefill_run(st, j)
         if not self.is_master:
             return None
         if self.runs[-1].owner != 0:
-            self._recv(hdr, self._final_src())
+            self._recv(st.msg, self._final_src())
             h = torch.empty((int(hdr[H_T].item()), H), device=self.device, dtype=torch.float32)
             self._recv(h, self._final_src())
+        hdr[H_FLAGS] = 0
         T = len(prompt)
         if self.hip:
             b = st.bufs
@@ -250,6 +267,8 @@ class PipelineEngine:
             b.slot.zero_()
             self._logits(h[-1].contiguous(), b.logits)
             self._select_device(st)
+            if self.sampler is not None:
+                return self._host_sample_device(st)
             return int(b.tok.item())
         st.host_tokens = list(prompt)
         tok = self._select_host(st, self._logits(h[-1]))
@@ -257,6 +276,87 @@ class PipelineEngine:
         st.host_pos = T
         st.hdr[H_POS] = T
         return tok
+
+    def _prefill_run(self, st: _Stream, j: int) -> torch.Tensor:
+        """Worker side of one prefill hop: the control message is already in st.msg."""
+        H = self.cfg.hidden_size
+        T, pos0, sid = int(st.hdr[H_T].item()), int(st.hdr[H_POS].item()), int(st.hdr[H_STREAM].item())
+        h = torch.empty((T, H), device=self.device, dtype=torch.float32)
+        self._recv(h, self._prev(j))
+        if int(st.hdr[H_FLAGS].item()) & FLAG_RESET:
+            self.stack.reset(sid)
+        self.stack.forward(h, self.runs[j].layers, pos0, session=sid)
+        nxt = self._next(j)
+        if nxt != self.rank:
+            self._wait(self._send(st.msg, nxt))
+            self._wait(self._send(h, nxt))
+        return h
+
+    # ------------------------------------------------------------------ serving (message-driven)
+    def serve(self) -> None:
+        """Worker loop for interactive use (CLI/API master on rank 0, one stream):
+        every hop starts with the stream's message; its header says PREFILL (a
+        [T, H] block follows), STOP (forward it and return) or decode."""
+        if self.is_master:
+            raise RuntimeError("serve() is the worker loop")
+        st = self.streams[0]
+        runs = [j for j in self.my_runs]
+        while True:
+            stopped = False
+            for j in runs:
+                self._wait(st.send_work)
+                st.send_work = None
+                self._recv(st.msg, self._prev(j))
+                flags = int(st.hdr[H_FLAGS].item())
+                if flags & FLAG_STOP:
+                    self._wait(self._send(st.msg, self._next(j)))
+                    stopped = True
+                    continue
+                if flags & FLAG_PREFILL:
+                    self._prefill_run(st, j)
+                    continue
+                self._replay(st, f"run{j}", lambda j=j: self._body_run(st, j))
+                st.send_work = self._send(st.msg, self._next(j))
+            if stopped:
+                self.flush()
+                return
+
+    def step(self, sid: int = 0) -> int:
+        """Master: one decode step of one stream; returns the new token id."""
+        st = self.streams[sid]
+        single = self.world == 1 or all(r.owner == 0 for r in self.runs)
+        self._wait(st.send_work)
+        st.send_work = None
+        st.hdr[H_FLAGS] = 0
+        self._replay(st, "first", lambda: self._body_first(st))
+        if not single:
+            self._wait(self._send(st.msg, self._first_dst()))
+            self._worker_runs(st)
+            self._wait(st.send_work)
+            st.send_work = None
+            self._recv(st.msg, self._final_src())
+        self._replay(st, "last", lambda: self._body_last(st))
+        if self.hip:
+            if self.sampler is not None:
+                return self._host_sample_device(st)
+            return int(st.bufs.tok.item())
+        return st.host_tokens[-1]
+
+    def shutdown(self) -> None:
+        """Master: send STOP along the chain and wait for it to come back."""
+        if not self.is_master or self.world == 1 or all(r.owner == 0 for r in self.runs):
+            return
+        st = self.streams[0]
+        self._wait(st.send_work)
+        st.send_work = None
+        st.hdr[H_FLAGS] = FLAG_STOP
+        self._wait(self._send(st.msg, self._first_dst()))
+        for j in self.my_runs:   # master-owned middle runs see STOP too
+            if j in (0, len(self.runs) - 1):
+                continue
+            self._recv(st.msg, self._prev(j))
+            self._wait(self._send(st.msg, self._next(j)))
+        self._recv(st.msg, self._final_src())
 
     # ------------------------------------------------------------------ decode bodies
     def _body_first(self, st: _Stream) -> None:

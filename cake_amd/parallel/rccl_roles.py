@@ -1,0 +1,150 @@
+"""Master/worker roles over RCCL (``--transport rccl``, launched with torchrun).
+
+One process per GPU of a node: rank 0 is the master (tokenizer, embedding,
+ln_f, lm_head, sampling, CLI or REST API, plus every layer no worker owns);
+rank i >= 1 serves the i-th node of ``topology.yml`` (file order).  Hidden
+states hop device-to-device with RCCL p2p (``parallel/pipeline.py``) instead of
+cake's TCP frames; each rank loads only the tensors it owns from the
+checkpoint (or a split-model bundle).
+
+    torchrun --nproc-per-node 4 --master-addr 127.0.0.1 -m cake_amd.cli \\
+        --transport rccl --model M --topology topology.yml --api 0.0.0.0:8080
+"""
+from __future__ import annotations
+
+import logging
+import os
+
+import torch
+import torch.distributed as dist
+
+from ..models.base import TextGenerator, Token
+from ..models.chat import History
+from ..models.sampling import LogitsProcessor
+from .pipeline import PipelineEngine
+
+log = logging.getLogger("cake.rccl")
+
+
+def owners_from_topology(topology, num_layers: int, world: int) -> list[int]:
+    owners = [0] * num_layers
+    if len(topology.nodes) > world - 1:
+        raise ValueError(f"topology has {len(topology.nodes)} workers but only {world - 1} "
+                         "worker ranks were launched")
+    for i, node in enumerate(topology.nodes):
+        for name in node.layers:
+            if name.startswith("model.layers."):
+                li = int(name.split(".")[-1])
+                if 0 <= li < num_layers:
+                    owners[li] = i + 1
+    return owners
+
+
+class PipelineLLM(TextGenerator):
+    """TextGenerator over the RCCL pipeline (master rank)."""
+    MODEL_NAME = "llama3"
+
+    def __init__(self, engine: PipelineEngine, tokenizer, eos_ids, sampling):
+        self.eng, self.tokenizer, self.eos_ids, self.sampling = engine, tokenizer, set(eos_ids), sampling
+        self.history = History()
+        self.tokens: list[int] = []
+        self.generated = 0
+        if not sampling.greedy:
+            lp = LogitsProcessor(sampling)
+            engine.sampler = lp.sample
+        self.last_stats = None
+
+    @classmethod
+    def load(cls, ctx):  # built by run_rccl (needs the engine)
+        raise NotImplementedError("PipelineLLM is constructed by run_rccl")
+
+    def add_message(self, message) -> None:
+        self.history.append(message)
+
+    def reset(self) -> None:
+        self.history.clear()
+        self.tokens.clear()
+        self.generated = 0
+
+    def generated_tokens(self) -> int:
+        return self.generated
+
+    def next_token(self, index: int) -> Token:
+        if self.generated == 0:
+            self.tokens = self.tokenizer.encode(self.history.encode_dialog_to_prompt(),
+                                                add_special_tokens=False).ids
+            tid = self.eng.prefill(0, self.tokens)
+        else:
+            tid = self.eng.step(0)
+        self.generated += 1
+        self.tokens.append(tid)
+        text = self.tokenizer.decode([tid], skip_special_tokens=False)
+        return Token(tid, text, tid in self.eos_ids)
+
+    def stream(self, max_tokens, on_token, stop_at_eos=True):
+        out = []
+        for i in range(max_tokens):
+            t = self.next_token(i)
+            out.append(t)
+            on_token(t)
+            if t.is_end_of_stream and stop_at_eos:
+                break
+        return out
+
+
+def run_rccl(ctx) -> None:
+    from ..models.llama3.config import LlamaConfig
+    from ..models.llama3.factory import load_stack
+    from ..models.llama3.generator import load_tokenizer
+    from ..models.llama3.weights import HeadWeights
+    from ..utils.safetensors_io import ShardedCheckpoint
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if ctx.device.type == "cuda":
+        local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(local)
+        ctx.device = torch.device("cuda", local)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=ctx.device)
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cfg = LlamaConfig.from_path(ctx.model_path)
+        owners = owners_from_topology(ctx.topology, cfg.num_hidden_layers, world)
+        mine = [li for li, r in enumerate(owners) if r == rank]
+        stack = load_stack(ctx.model_path, cfg, mine, ctx.device, ctx.dtype, ctx.max_seq_len)
+        head = None
+        if rank == 0:
+            head = HeadWeights.load(ShardedCheckpoint(ctx.model_path).get, cfg, ctx.device, ctx.dtype)
+        s = ctx.sampling
+        eng = PipelineEngine(cfg, stack, owners, rank, world, streams=1, head=head,
+                             repeat_penalty=s.repeat_penalty, repeat_last_n=s.repeat_last_n,
+                             use_graph=not ctx.no_graph)
+        log.info("rank %d/%d owns layers %s", rank, world, mine[:3] + (["..."] if len(mine) > 3 else []))
+        if eng.use_graph:
+            # the worker graphs read the position from the received header; a
+            # dummy prefill gives every graph valid state to capture against
+            if rank == 0:
+                eng.prefill(0, [cfg.bos_token_id or 0])
+            else:
+                _serve_one_prefill(eng)
+            eng.capture()
+        if rank == 0:
+            from ..master import Master
+            tok, eos = load_tokenizer(ctx.model_path, cfg.eos_token_id)
+            master = Master(ctx, llm=PipelineLLM(eng, tok, eos, s))
+            try:
+                master.run()
+            finally:
+                eng.shutdown()
+        else:
+            eng.serve()
+    finally:
+        dist.destroy_process_group()
+
+
+def _serve_one_prefill(eng: PipelineEngine) -> None:
+    st = eng.streams[0]
+    for j in eng.my_runs:
+        eng._recv(st.msg, eng._prev(j))
+        eng._prefill_run(st, j)

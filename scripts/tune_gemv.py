@@ -102,8 +102,7 @@ def main():
         H, I, nh, nkv, hd, V = 4096, 14336, 32, 8, 128, 128256
     else:
         H, I, nh, nkv, hd, V = 8192, 28672, 64, 8, 128, 128256
-    configs = [(U, pf, mb) for U, pf, mb in itertools.product((2, 4, 8), (False, True), (256, 512, 1024, 2048, 4096))
-               if not (pf and U != 4)]
+    configs = list(itertools.product((2, 4, 8), (0, 4, 8), (256, 512, 1024, 2048)))
     results = {}
     for kind in a.kinds.split(","):
         copies, fn, per = make_case(kind, H, I, nh, nkv, hd, V, dt, dev)
@@ -118,7 +117,7 @@ def main():
         for med, mn, c in rows[:8]:
             print(f"  U={c[0]} pf={int(c[1])} mb={c[2]:5d}  median {med:8.2f} us  min {mn:8.2f} us  "
                   f"{per / med / 1e6:6.2f} TB/s")
-        base = statistics.median(times[(4, False, 1024)])
+        base = statistics.median(times[(4, 0, 1024)])
         print(f"  default U=4 pf=0 mb=1024: {base:.2f} us  {per / base / 1e6:.2f} TB/s")
         results[kind] = [{"U": c[0], "pf": c[1], "mb": c[2], "median_us": med, "min_us": mn}
                          for med, mn, c in rows]
