@@ -97,7 +97,8 @@ def build_kernels(force: bool = False, jobs: int = 8) -> Path:
 def build_runtime(force: bool = False, jobs: int = 8) -> Path:
     """C++ host runtime: pybind11 module, C-ABI library and the split-model tool."""
     rt = CSRC / "runtime"
-    core_srcs = [rt / f"{n}.cpp" for n in ("json", "topology", "proto", "net", "safetensors")]
+    core_srcs = [rt / f"{n}.cpp" for n in ("json", "topology", "proto", "net", "safetensors",
+                                            "server")]
     inc, ext = _py_ext_flags()
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         core = list(ex.map(lambda s: _compile_cpp(s, force), core_srcs))

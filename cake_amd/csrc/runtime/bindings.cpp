@@ -8,6 +8,7 @@
 #include "net.h"
 #include "proto.h"
 #include "safetensors.h"
+#include "server.h"
 #include "topology.h"
 
 namespace py = pybind11;
@@ -215,6 +216,73 @@ PYBIND11_MODULE(_cake_runtime, mod) {
     write_safetensors(path, out, metadata);
   }, py::arg("path"), py::arg("tensors"), py::arg("metadata") = std::map<std::string, std::string>{});
   mod.def("load_weight_map", &load_weight_map);
+
+  // ---------------------------------------------------------------- worker server
+  py::class_<WorkerServer>(mod, "WorkerServer")
+      .def(py::init([](const std::string& host, int port, const py::dict& i, const std::string& name) {
+             WorkerInfo info;
+             info.version = i["version"].cast<std::string>();
+             info.dtype = i["dtype"].cast<std::string>();
+             info.os = i["os"].cast<std::string>();
+             info.arch = i["arch"].cast<std::string>();
+             info.device = i["device"].cast<std::string>();
+             info.device_idx = i["device_idx"].cast<uint64_t>();
+             py::gil_scoped_release nogil;
+             return new WorkerServer(host, port, info, name);
+           }),
+           py::arg("host"), py::arg("port"), py::arg("info"), py::arg("name"))
+      .def_property_readonly("port", &WorkerServer::port)
+      .def("serve", [](WorkerServer& s) {
+        py::gil_scoped_release nogil;
+        s.serve();
+      })
+      .def("stop", &WorkerServer::stop)
+      .def("set_drop_after", &WorkerServer::set_drop_after)
+      .def("set_stats_every", &WorkerServer::set_stats_every)
+      .def("set_compute", [](WorkerServer& s, py::function fn) {
+        // fn(session, ops[(name, pos, idx)], dtype, shape, memoryview) -> (dtype, shape, bytes)
+        auto holder = std::make_shared<py::function>(std::move(fn));
+        s.set_compute([holder](uint64_t session, const std::vector<BatchItem>& ops,
+                               const RawTensor& x) -> OpResult {
+          py::gil_scoped_acquire gil;
+          OpResult r;
+          try {
+            py::list pops;
+            for (const auto& o : ops) pops.append(py::make_tuple(o.layer_name, o.index_pos, o.block_idx));
+            auto mv = py::memoryview::from_memory(const_cast<uint8_t*>(x.data), (ssize_t)x.nbytes, true);
+            py::tuple out = (*holder)(session, pops, x.dtype, x.shape, mv);
+            r.dtype = out[0].cast<std::string>();
+            r.shape = out[1].cast<std::vector<uint64_t>>();
+            r.data = out[2].cast<std::string>();
+          } catch (py::error_already_set& e) {
+            r.error = e.what();
+          }
+          return r;
+        });
+      })
+      .def("set_reset", [](WorkerServer& s, py::function fn) {
+        auto holder = std::make_shared<py::function>(std::move(fn));
+        s.set_reset([holder](uint64_t session) { py::gil_scoped_acquire g; (*holder)(session); });
+      })
+      .def("set_drop", [](WorkerServer& s, py::function fn) {
+        auto holder = std::make_shared<py::function>(std::move(fn));
+        s.set_drop([holder](uint64_t session) { py::gil_scoped_acquire g; (*holder)(session); });
+      })
+      .def("set_log", [](WorkerServer& s, py::function fn) {
+        auto holder = std::make_shared<py::function>(std::move(fn));
+        s.set_log([holder](const std::string& m) { py::gil_scoped_acquire g; (*holder)(m); });
+      })
+      .def("stats", [](const WorkerServer& s) {
+        const ServerStats& st = s.stats();
+        py::dict d;
+        d["connections"] = st.connections.load();
+        d["messages"] = st.messages.load();
+        d["ops"] = st.ops.load();
+        d["bytes_in"] = st.bytes_in.load();
+        d["bytes_out"] = st.bytes_out.load();
+        d["errors"] = st.errors.load();
+        return d;
+      });
   mod.def("json_roundtrip", [](const std::string& s, int indent) { return Json::parse(s).dump(indent); },
           py::arg("text"), py::arg("indent") = -1);
 }

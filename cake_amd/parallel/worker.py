@@ -16,7 +16,6 @@ Reference: cake-core/src/cake/worker.rs.
 """
 from __future__ import annotations
 
-import itertools
 import logging
 import os
 import platform
@@ -52,7 +51,6 @@ class Worker:
         self.node = node
         self.text = ctx.model_type == "text-model"
         self.compute_lock = threading.Lock()
-        self._sessions = itertools.count(1)
         self.stack = None
         self.units = {}
         if self.text:
@@ -69,12 +67,16 @@ class Worker:
             self.units = load_sd_units(ctx, node.layers)
         host, _, port = ctx.address.rpartition(":")
         from ..utils.native import runtime
-        self._rt = runtime()
-        self.listen_fd = self._rt.tcp_listen(host or "0.0.0.0", int(port))
-        self.port = self._rt.tcp_local_port(self.listen_fd)
-        self._stop = threading.Event()
+        self.server = runtime().WorkerServer(host or "0.0.0.0", int(port), self.info(0), node.name)
+        self.port = self.server.port
         fi = os.environ.get("CAKE_FAULT_INJECT", "")
-        self.drop_after = int(fi.split("=")[1]) if fi.startswith("drop_after=") else 0
+        if fi.startswith("drop_after="):
+            self.server.set_drop_after(int(fi.split("=")[1]))
+        self.server.set_stats_every(NUM_OPS_TO_STATS)
+        self.server.set_compute(self._compute)
+        self.server.set_reset(self._reset)
+        self.server.set_drop(self._drop_session)
+        self.server.set_log(lambda m: log.info("%s", m))
         log.info("worker %s listening on %s:%d", node.name, host, self.port)
 
     # ------------------------------------------------------------------ info
@@ -88,15 +90,8 @@ class Worker:
 
     # ------------------------------------------------------------------ serving
     def run(self) -> None:
-        while not self._stop.is_set():
-            try:
-                fd, peer = self._rt.tcp_accept(self.listen_fd)
-            except RuntimeError:
-                if self._stop.is_set():
-                    break
-                raise
-            t = threading.Thread(target=self._serve, args=(P.Connection(fd, peer),), daemon=True)
-            t.start()
+        """Blocking accept loop (native: csrc/runtime/server.cpp)."""
+        self.server.serve()
 
     def serve_in_thread(self) -> threading.Thread:
         t = threading.Thread(target=self.run, daemon=True)
@@ -104,64 +99,18 @@ class Worker:
         return t
 
     def stop(self) -> None:
-        self._stop.set()
-        self._rt.tcp_close(self.listen_fd)
+        self.server.stop()
 
-    def _serve(self, conn: P.Connection) -> None:
-        session = next(self._sessions)
-        log.info("[%s] connected (session %d)", conn.peer, session)
-        n_ops = 0
-        try:
-            t0 = time.perf_counter()
-            msg, _ = conn.recv()
-            latency = int((time.perf_counter() - t0) * 1000)
-            if msg["type"] != P.HELLO:
-                conn.send({"type": P.ERROR, "error": "expected Hello"})
-                return
-            conn.send({"type": P.WORKER_INFO, "info": self.info(latency)})
-            stats_t, stats_ops, stats_in, stats_out, stats_msgs = time.perf_counter(), 0, 0, 0, 0
-            while True:
-                try:
-                    msg, body = conn.recv()
-                except RuntimeError:
-                    break  # peer closed: end this connection silently (worker.rs:208)
-                kind = msg["type"]
-                if kind == P.PING:
-                    conn.send({"type": P.PONG})
-                    continue
-                if kind == P.RESET:
-                    self._reset(session)
-                    conn.send({"type": P.PONG})
-                    continue
-                if kind not in (P.SINGLE_OP, P.BATCH):
-                    conn.send({"type": P.ERROR, "error": f"unexpected message type {kind}"})
-                    continue
-                ops = ([(msg["layer_name"], msg["index_pos"], msg["block_idx"])]
-                       if kind == P.SINGLE_OP else msg["batch"])
-                try:
-                    x = P.tensor_from_payload(msg, body)
-                    y = self._run_ops(x, ops, session)
-                    conn.send({"type": P.TENSOR}, y)
-                except Exception as e:  # noqa: BLE001
-                    log.error("[%s] op failed: %s", conn.peer, e)
-                    conn.send({"type": P.ERROR, "error": str(e)})
-                n_ops += len(ops)
-                stats_ops += len(ops)
-                stats_msgs += 1
-                if self.drop_after and n_ops >= self.drop_after:
-                    log.warning("fault injection: dropping connection after %d ops", n_ops)
-                    break
-                if stats_msgs % NUM_OPS_TO_STATS == 0:
-                    dt = time.perf_counter() - stats_t
-                    din, dout = conn.bytes_in - stats_in, conn.bytes_out - stats_out
-                    log.info("%s | ops=%.1f/s read=%.1f KB/s write=%.1f KB/s", self.node.name,
-                             stats_ops / dt, din / dt / 1e3, dout / dt / 1e3)
-                    stats_t, stats_ops = time.perf_counter(), 0
-                    stats_in, stats_out = conn.bytes_in, conn.bytes_out
-        finally:
-            self._drop_session(session)
-            conn.close()
-            log.info("[%s] disconnected", conn.peer)
+    def stats(self) -> dict:
+        return self.server.stats()
+
+    def _compute(self, session: int, ops, dtype: str, shape, data) -> tuple:
+        """Native-server callback: run `ops` on the payload, return (dtype, shape, bytes)."""
+        x = P.tensor_from_payload({"dtype": dtype, "shape": list(shape), "offset": 0,
+                                   "nbytes": len(data)}, bytes(data))
+        y = self._run_ops(x, ops, session)
+        name, shp, buf = P.tensor_payload(y)
+        return name, shp, buf.tobytes()
 
     def _reset(self, session: int) -> None:
         if self.stack is not None:

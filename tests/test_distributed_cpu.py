@@ -101,3 +101,19 @@ def test_unknown_worker_name_serves_first_node(ckpt, tmp_path):
         assert w.node.name == "a" and w.stack.layer_ids == [0]
     finally:
         w.stop()
+
+
+def test_fault_injection_and_native_stats(ckpt, tmp_path, monkeypatch):
+    monkeypatch.setenv("CAKE_FAULT_INJECT", "drop_after=2")
+    w = _start_worker(ckpt, tmp_path, "wf", ["model.layers.0"])
+    try:
+        c = Client("cpu", f"127.0.0.1:{w.port}", "model.layers.0")
+        x = torch.randn(1, 1, 256)
+        c.forward_mut(x, 0, 0)
+        c.forward_mut(x, 1, 0)           # 2nd op: the worker then drops the connection
+        with pytest.raises(Exception):
+            c.forward_mut(x, 2, 0)
+        st = w.stats()
+        assert st["ops"] == 2 and st["connections"] == 1 and st["bytes_in"] > 0
+    finally:
+        w.stop()
