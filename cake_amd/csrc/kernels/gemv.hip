@@ -189,6 +189,7 @@ struct QkvArgs {
   uint16_t* kcache;       // [nkv][S][hd] (this layer)
   uint16_t* vcache;
   int S;
+  unsigned int* rearm;  // optional: zeroed by block 0 (fused attention done-counter)
 };
 
 struct QkvRow {
@@ -227,6 +228,7 @@ __global__ __launch_bounds__(kGemvThreads) void qkv_rope_kernel(QkvArgs a) {
     map(p0, wa, wb);
     prefetch_rows<PFC>(wa, wb, pre);
   }
+  if (a.rearm != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *a.rearm = 0u;
   stage_rmsnorm<DT>(a.resid, a.norm_w, a.eps, a.K, xs);
   const int pos = *a.pos;
   auto epi = [&](int p, float da, float db) {
@@ -387,11 +389,11 @@ CAKE_API int cake_qkv_rope(int dt, const float* resid, const void* norm_w, float
                            const void* wq, const void* wk, const void* wv, int K, int nh,
                            int nkv, int hd, const float* inv_freq, const int* pos,
                            float* q_out, void* kcache, void* vcache, int S,
-                           hipStream_t st) {
+                           unsigned int* rearm, hipStream_t st) {
   if (K % 8 || hd % 2) return (int)hipErrorInvalidValue;
   QkvArgs a{resid, (const uint16_t*)norm_w, eps, (const uint16_t*)wq,
             (const uint16_t*)wk, (const uint16_t*)wv, K, nh, nkv, hd, inv_freq, pos,
-            q_out, (uint16_t*)kcache, (uint16_t*)vcache, S};
+            q_out, (uint16_t*)kcache, (uint16_t*)vcache, S, rearm};
   const int npairs = (nh + 2 * nkv) * (hd / 2);
   const size_t lds = (size_t)K * sizeof(float);
   const GemvTune t = g_tune[kQkv];

@@ -58,6 +58,8 @@ class DecodeBuffers:
         nsplit = (max_seq + 63) // 64
         self.part = torch.zeros(nh * nsplit * (hd + 2), device=device, dtype=f32)
         self.tickets = torch.zeros(cfg.num_key_value_heads, device=device, dtype=i32)
+        self.ctl = torch.zeros(3, device=device, dtype=i32)   # fused attn+o_proj counters
+        self.err = torch.zeros(1, device=device, dtype=i32)
         self.pos = torch.zeros(1, device=device, dtype=i32) if pos is None else pos
         if with_head:
             self.logits = torch.zeros(cfg.vocab_size, device=device, dtype=f32)
@@ -87,6 +89,18 @@ class LayerStack:
         self._sessions: OrderedDict[int, KVCache] = OrderedDict()
         self._decode_bufs: DecodeBuffers | None = None
         self._hostpos_bufs: DecodeBuffers | None = None
+        # fused attention + o_proj decode kernel (decode_fused.hip), opt-in with
+        # CAKE_FUSED=1 (2 = without weight prefetch).  Measured slower than the
+        # two-kernel path on MI355X (profiles/r1_fused_ao_sweep.txt), so off by default.
+        import os
+        from ...ops.hip import attn_oproj_supported
+        mode = os.environ.get("CAKE_FUSED", "0")
+        self.fused_prefetch = mode != "2"
+        self.fused_grid = int(os.environ.get("CAKE_AO_GRID", "0")) or None
+        self.fused_sleep = int(os.environ.get("CAKE_AO_SLEEP", "1"))
+        self.fused_ao = (backend == "hip" and mode != "0" and
+                         attn_oproj_supported(cfg.num_attention_heads, cfg.num_key_value_heads,
+                                              cfg.head_dim, cfg.hidden_size))
 
     # ------------------------------------------------------------------ sessions
     def cache(self, session: int = 0) -> KVCache:
@@ -153,10 +167,16 @@ class LayerStack:
             s = self.slot_of[li]
             kc, vc = kv.k[s], kv.v[s]
             K.qkv_rope(bufs.resid, w.ln1, cfg.rms_norm_eps, w.wq, w.wk, w.wv, self.inv_freq,
-                       bufs.pos, bufs.q, kc, vc)
-            K.attn_decode(bufs.q, kc, vc, bufs.pos, self.scale, bufs.part, bufs.tickets,
-                          bufs.attn_out)
-            K.gemv(bufs.attn_out, w.wo, bufs.resid, accumulate=True)
+                       bufs.pos, bufs.q, kc, vc, rearm=bufs.ctl if self.fused_ao else None)
+            if self.fused_ao:
+                K.attn_oproj(bufs.q, kc, vc, bufs.pos, self.scale, bufs.part, bufs.tickets,
+                             bufs.ctl, bufs.attn_out, w.wo, bufs.resid, bufs.err,
+                             prefetch=self.fused_prefetch, grid=self.fused_grid,
+                             sleep=self.fused_sleep)
+            else:
+                K.attn_decode(bufs.q, kc, vc, bufs.pos, self.scale, bufs.part, bufs.tickets,
+                              bufs.attn_out)
+                K.gemv(bufs.attn_out, w.wo, bufs.resid, accumulate=True)
             K.swiglu(bufs.resid, w.ln2, cfg.rms_norm_eps, w.wg, w.wu, bufs.act)
             K.gemv(bufs.act, w.wd, bufs.resid, accumulate=True)
 

@@ -25,7 +25,7 @@ Z = C.c_size_t
 
 # name -> argtypes (all return int hipError_t)
 _SIGS = {
-    "cake_qkv_rope": [I, P, P, F, P, P, P, I, I, I, I, P, P, P, P, P, I, P],
+    "cake_qkv_rope": [I, P, P, F, P, P, P, I, I, I, I, P, P, P, P, P, I, P, P],
     "cake_swiglu": [I, P, P, F, P, P, I, I, P, P],
     "cake_gemv_x16": [I, P, P, I, I, P, I, P],
     "cake_gemv_norm_f32": [I, P, P, F, P, I, I, P, P],
@@ -91,4 +91,8 @@ _SIGS.update({
     "cake_groupnorm": [I, P, P, P, I, I, C.c_longlong, I, F, I, P, P, P],
     "cake_layernorm": [I, P, P, P, C.c_longlong, I, F, P, P],
     "cake_geglu": [I, P, C.c_longlong, I, P, P],
+})
+
+_SIGS.update({
+    "cake_attn_oproj": [I, P, P, P, P, I, I, I, I, F, P, P, P, P, P, I, P, P, I, I, I, P],
 })

@@ -46,7 +46,7 @@ def _req(t: torch.Tensor, name: str, *, dtype=None, numel=None, shape=None) -> N
 # decode (batch 1) fused projections
 # ---------------------------------------------------------------------------
 
-def qkv_rope(resid, norm_w, eps, wq, wk, wv, inv_freq, pos, q_out, kcache, vcache):
+def qkv_rope(resid, norm_w, eps, wq, wk, wv, inv_freq, pos, q_out, kcache, vcache, rearm=None):
     """rmsnorm(resid) -> q/k/v GEMV -> RoPE(pos) -> q_out f32, k/v into cache[:, pos].
 
     kcache/vcache: [nkv, S, hd] (one layer). pos: int32 device scalar.
@@ -69,7 +69,9 @@ def qkv_rope(resid, norm_w, eps, wq, wk, wv, inv_freq, pos, q_out, kcache, vcach
         raise ValueError("hidden size must be a multiple of 8")
     check(kernels().cake_qkv_rope(_dt(wq), _p(resid), _p(norm_w), float(eps), _p(wq), _p(wk),
                                   _p(wv), K, nh, nkv, hd, _p(inv_freq), _p(pos), _p(q_out),
-                                  _p(kcache), _p(vcache), S, _stream()), "qkv_rope")
+                                  _p(kcache), _p(vcache), S,
+                                  None if rearm is None else rearm[1:].data_ptr(), _stream()),
+          "qkv_rope")
 
 
 def swiglu(resid, norm_w, eps, wg, wu, act):
@@ -312,3 +314,38 @@ def geglu(h, out):
     _req(out, "out", dtype=h.dtype, numel=h.numel() // 2)
     check(kernels().cake_geglu(_dt(h), _p(h), h.numel() // (2 * F), F, _p(out), _stream()),
           "geglu")
+
+
+def attn_oproj_supported(nh: int, nkv: int, hd: int, H: int) -> bool:
+    return hd == 128 and nh % nkv == 0 and nh // nkv in (4, 8) and 4096 <= nh * hd <= 8192
+
+
+def attn_oproj(q, kcache, vcache, pos, scale, part, tickets, ctl, attn_out, wo, resid, err,
+               prefetch: bool = True, grid: int | None = None, sleep: int = 1):
+    """Fused decode attention + o_proj + residual (decode_fused.hip).
+
+    ctl: int32[3] (ctl[1] must be 0 at launch: qkv_rope(rearm=ctl) zeroes it); err: int32[1].
+    """
+    nkv, S, hd = kcache.shape
+    nh = q.numel() // hd
+    N, K = wo.shape
+    if not attn_oproj_supported(nh, nkv, hd, N) or K != nh * hd:
+        raise ValueError(f"attn_oproj: unsupported shape nh={nh} nkv={nkv} hd={hd} wo={tuple(wo.shape)}")
+    _req(q, "q", dtype=torch.float32)
+    _req(kcache, "kcache")
+    _req(vcache, "vcache", dtype=kcache.dtype, shape=kcache.shape)
+    _req(pos, "pos", dtype=torch.int32, numel=1)
+    _req(part, "part", dtype=torch.float32, numel=nh * ((S + 63) // 64) * (hd + 2))
+    _req(tickets, "tickets", dtype=torch.int32, numel=nkv)
+    _req(ctl, "ctl", dtype=torch.int32, numel=3)
+    _req(attn_out, "attn_out", dtype=kcache.dtype, numel=nh * hd)
+    _req(wo, "wo", dtype=kcache.dtype)
+    _req(resid, "resid", dtype=torch.float32, numel=N)
+    _req(err, "err", dtype=torch.int32, numel=1)
+    if grid is None:
+        grid = max(1, ((N + 1) // 2 + 3) // 4)
+    check(kernels().cake_attn_oproj(_dt(kcache), _p(q), _p(kcache), _p(vcache), _p(pos), S, nh,
+                                    nkv, hd, float(scale), _p(part), _p(tickets), _p(ctl),
+                                    _p(attn_out), _p(wo), N, _p(resid), _p(err), int(grid),
+                                    int(prefetch), int(sleep), _stream()),
+          "attn_oproj")

@@ -198,3 +198,37 @@ def test_penalty_argmax_finalize(cuda):
     K_.argmax(logits, slot)
     K_.finalize_token(slot, tok, hist, hist_len, pos)
     assert int(tok) == 0
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("nh,nkv,H", [(32, 8, 4096), (64, 8, 8192)])
+def test_attn_oproj_fused_matches_unfused(cuda, dt, nh, nkv, H):
+    """decode_fused.hip == attn_decode + gemv(accumulate), over several positions and
+    back-to-back launches, including multi-split contexts.  The done-counter is
+    re-armed before each launch (the QKV kernel does this in the decode step)."""
+    from cake_amd.ops import hip as K_
+    torch.manual_seed(8)
+    hd, S = 128, 1024
+    kc = _rand(nkv, S, hd, dt=dt)
+    vc = _rand(nkv, S, hd, dt=dt)
+    wo = _rand(H, nh * hd, dt=dt, std=0.02)
+    part = torch.empty(K_.attn_workspace_numel(nh, hd, S), device=cuda)
+    tickets = torch.zeros(nkv, dtype=torch.int32, device=cuda)
+    ctl = torch.zeros(3, dtype=torch.int32, device=cuda)
+    err = torch.zeros(1, dtype=torch.int32, device=cuda)
+    for pos in (0, 63, 64, 200, 1023):
+        q = torch.randn(nh * hd, device=cuda)
+        p = torch.tensor([pos], dtype=torch.int32, device=cuda)
+        r0 = torch.randn(H, device=cuda)
+        ref_att = torch.empty(nh * hd, device=cuda, dtype=dt)
+        K_.attn_decode(q, kc, vc, p, 1 / math.sqrt(hd), part, tickets, ref_att)
+        ref = r0.clone()
+        K_.gemv(ref_att, wo, ref, accumulate=True)
+        out = r0.clone()
+        att = torch.empty(nh * hd, device=cuda, dtype=dt)
+        ctl.zero_()
+        K_.attn_oproj(q, kc, vc, p, 1 / math.sqrt(hd), part, tickets, ctl, att, wo, out, err)
+        torch.cuda.synchronize()
+        assert int(err) == 0 and int(ctl[1]) == nkv and int(tickets.abs().sum()) == 0
+        torch.testing.assert_close(att.float(), ref_att.float())
+        torch.testing.assert_close(out, ref, atol=2e-3, rtol=1e-3)
