@@ -15,6 +15,8 @@
 //              (+ SiLU) with 16-byte accesses.
 #include "common.h"
 
+#include <algorithm>
+
 namespace cake {
 
 constexpr int kGnSplit = 16;
@@ -156,6 +158,133 @@ __global__ void geglu_kernel(const uint16_t* __restrict__ h, long long rows, int
   }
 }
 
+// ---------------------------------------------------------------------------
+// GroupNorm on channels-last activations x [N, HW, C] (the layout the MFMA
+// convolutions and the transformer blocks share, so no NCHW<->NHWC copies).
+// 1. stats: grid (S, N), block (C/8 channel vectors) x (pixel lanes).  Every
+//    thread owns 8 fixed channels (<= 2 groups) and accumulates sum / sum^2 in
+//    f64 over its pixels; the block folds them per group and writes a f64
+//    partial.  The last block of image n (agent-scope ticket, CDNA guide
+//    Guideline 16) folds the S partials into (mean, rstd) per group and
+//    re-arms the ticket, so the launch replays unchanged in a hipGraph.
+// 2. apply: per-channel scale/shift for image n in LDS, then one fma (+SiLU)
+//    per element with 16-byte accesses.
+// ---------------------------------------------------------------------------
+constexpr int kGnMaxC = 4096;
+
+template <int DT>
+__global__ __launch_bounds__(512) void gn_nhwc_stats_kernel(const uint16_t* __restrict__ x, int HW,
+                                                            int C, int G, double* __restrict__ part,
+                                                            unsigned int* __restrict__ tickets,
+                                                            float* __restrict__ stats) {
+  const int Tx = C >> 3, Ty = blockDim.x / Tx;
+  const int cv = threadIdx.x % Tx, py = threadIdx.x / Tx;
+  const int n = blockIdx.y, S = gridDim.x, sp = blockIdx.x;
+  const int Cg = C / G;
+  const int g0 = (cv * 8) / Cg;
+  const int per = (HW + S - 1) / S, p0 = sp * per, p1 = min(HW, p0 + per);
+  double s0 = 0.0, q0 = 0.0, s1 = 0.0, q1 = 0.0;
+  if (py < Ty) {
+    const uint16_t* base = x + ((size_t)n * HW) * C + cv * 8;
+    for (int p = p0 + py; p < p1; p += Ty) {
+      float f[8];
+      unpack8<DT>(*reinterpret_cast<const uint4*>(base + (size_t)p * C), f);
+      float a0 = 0.f, b0 = 0.f, a1 = 0.f, b1 = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        if ((cv * 8 + e) / Cg == g0) { a0 += f[e]; b0 += f[e] * f[e]; }
+        else { a1 += f[e]; b1 += f[e] * f[e]; }
+      }
+      s0 += a0; q0 += b0; s1 += a1; q1 += b1;
+    }
+  }
+  __shared__ double red[512 * 4];
+  __shared__ int last;
+  red[threadIdx.x * 4 + 0] = s0; red[threadIdx.x * 4 + 1] = q0;
+  red[threadIdx.x * 4 + 2] = s1; red[threadIdx.x * 4 + 3] = q1;
+  __syncthreads();
+  double* pn = part + ((size_t)n * S + sp) * G * 2;
+  for (int g = threadIdx.x; g < G; g += blockDim.x) {
+    double ts = 0.0, tq = 0.0;
+    const int vlo = (g * Cg) / 8, vhi = ((g + 1) * Cg - 1) / 8;
+    for (int v = vlo; v <= vhi; ++v) {
+      const int slot = ((v * 8) / Cg == g) ? 0 : 2;
+      for (int y = 0; y < Ty; ++y) {
+        ts += red[(y * Tx + v) * 4 + slot];
+        tq += red[(y * Tx + v) * 4 + slot + 1];
+      }
+    }
+    pn[2 * g] = ts;
+    pn[2 * g + 1] = tq;
+  }
+  // publish partial; the last block of image n folds all S of them
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned prev = __hip_atomic_fetch_add(&tickets[n], 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+    last = prev == (unsigned)(S - 1);
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      tickets[n] = 0u;
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  const double cnt = (double)HW * Cg;
+  for (int g = threadIdx.x; g < G; g += blockDim.x) {
+    double ts = 0.0, tq = 0.0;
+    for (int k = 0; k < S; ++k) {
+      const double* q = part + ((size_t)n * S + k) * G * 2;
+      ts += __builtin_nontemporal_load(q + 2 * g);
+      tq += __builtin_nontemporal_load(q + 2 * g + 1);
+    }
+    const double mean = ts / cnt;
+    const double var = fmax(tq / cnt - mean * mean, 0.0);
+    stats[((size_t)n * G + g) * 2] = (float)mean;
+    stats[((size_t)n * G + g) * 2 + 1] = (float)var;
+  }
+}
+
+template <int DT, bool SILU>
+__global__ __launch_bounds__(256) void gn_nhwc_apply_kernel(const uint16_t* __restrict__ x,
+                                                            const uint16_t* __restrict__ gamma,
+                                                            const uint16_t* __restrict__ beta,
+                                                            const float* __restrict__ stats,
+                                                            int HW, int C, int G, float eps,
+                                                            uint16_t* __restrict__ y) {
+  __shared__ float sc[kGnMaxC], sh[kGnMaxC];
+  const int n = blockIdx.y, Cg = C / G;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const int g = c / Cg;
+    const float mean = stats[((size_t)n * G + g) * 2];
+    const float rstd = rsqrtf(stats[((size_t)n * G + g) * 2 + 1] + eps);
+    const float a = rstd * to_f32<DT>(gamma[c]);
+    sc[c] = a;
+    sh[c] = to_f32<DT>(beta[c]) - mean * a;
+  }
+  __syncthreads();
+  const size_t nv = (size_t)HW * (C >> 3);
+  const size_t base = (size_t)n * HW * C;
+  for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv;
+       v += (size_t)gridDim.x * blockDim.x) {
+    const int c0 = (int)(v % (C >> 3)) * 8;
+    float f[8];
+    unpack8<DT>(*reinterpret_cast<const uint4*>(x + base + v * 8), f);
+    uint16_t o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float t = fmaf(f[e], sc[c0 + e], sh[c0 + e]);
+      if (SILU) t = silu(t);
+      o[e] = from_f32<DT>(t);
+    }
+    *reinterpret_cast<uint4*>(y + base + v * 8) = *reinterpret_cast<uint4*>(o);
+  }
+}
+
 }  // namespace cake
 
 using namespace cake;
@@ -206,5 +335,36 @@ CAKE_API int cake_geglu(int dt, const void* h, long long rows, int F, void* out,
   if (g > 8192) g = 8192;
   DISPATCH_DT(dt, hipLaunchKernelGGL((geglu_kernel<DT>), dim3((unsigned)g), dim3(256), 0, st,
                                      (const uint16_t*)h, rows, F, (uint16_t*)out));
+  return (int)hipGetLastError();
+}
+
+// Channels-last GroupNorm.  part: N*S*G*2 f64 (S = cake_groupnorm_nhwc_splits),
+// tickets: N u32 zeroed once (re-armed by the kernel), stats: N*G*2 f32.
+CAKE_API int cake_groupnorm_nhwc_splits(int HW) { return HW < 64 ? HW : 64; }
+
+CAKE_API int cake_groupnorm_nhwc(int dt, const void* x, const void* gamma, const void* beta, int N,
+                                 int HW, int C, int G, float eps, int silu_act, double* part,
+                                 unsigned int* tickets, float* stats, void* y, hipStream_t st) {
+  if (C % G || C % 8 || C > kGnMaxC || C / 8 > 512 || N <= 0 || HW <= 0 || (C / G) < 1)
+    return (int)hipErrorInvalidValue;
+  // every 8-channel vector must span at most two groups
+  if ((C / G) < 8 && 8 % (C / G)) return (int)hipErrorInvalidValue;
+  if ((C / G) < 4) return (int)hipErrorInvalidValue;
+  const int Tx = C / 8, Ty = Tx >= 512 ? 1 : 512 / Tx;
+  const int S = cake_groupnorm_nhwc_splits(HW);
+  const size_t nv = (size_t)HW * (C / 8);
+  const unsigned ab = (unsigned)std::min<size_t>((nv + 255) / 256, 1024);
+  DISPATCH_DT(dt, {
+    hipLaunchKernelGGL((gn_nhwc_stats_kernel<DT>), dim3(S, N), dim3(Tx * Ty), 0, st,
+                       (const uint16_t*)x, HW, C, G, part, tickets, stats);
+    if (silu_act)
+      hipLaunchKernelGGL((gn_nhwc_apply_kernel<DT, true>), dim3(ab, N), dim3(256), 0, st,
+                         (const uint16_t*)x, (const uint16_t*)gamma, (const uint16_t*)beta, stats,
+                         HW, C, G, eps, (uint16_t*)y);
+    else
+      hipLaunchKernelGGL((gn_nhwc_apply_kernel<DT, false>), dim3(ab, N), dim3(256), 0, st,
+                         (const uint16_t*)x, (const uint16_t*)gamma, (const uint16_t*)beta, stats,
+                         HW, C, G, eps, (uint16_t*)y);
+  });
   return (int)hipGetLastError();
 }

@@ -1,15 +1,80 @@
 """SD op dispatch: gfx950 HIP kernels on the device path, PyTorch on CPU / f32.
 
-GroupNorm(+SiLU), LayerNorm, multi-head attention (MFMA flash attention) and
-GEGLU run as our kernels; convolutions go to MIOpen and the
-plain linears to hipBLASLt (library GEMMs) through torch.
+On the device path the UNet and VAE run channels-last (NHWC): convolutions are
+our MFMA implicit-GEMM kernels (conv2d.hip, per-shape autotuned, time-embedding
+bias and residual fused into the epilogue, nearest-2x upsample fused into the
+operand addressing), GroupNorm(+SiLU) is the channels-last kernel, and the
+SpatialTransformer consumes [B, HW, C] views with no permutes.  LayerNorm,
+multi-head attention (MFMA flash attention) and GEGLU are our kernels too
+(SURVEY K31-K36); the plain linears go to hipBLASLt (library GEMMs) through
+torch.  The CPU / f32 path is plain NCHW PyTorch.
 """
 from __future__ import annotations
 
 import math
+import os
+import threading
+from contextlib import contextmanager
 
 import torch
 import torch.nn.functional as F
+
+_state = threading.local()
+
+
+def nhwc() -> bool:
+    """True while a channels-last forward is running on this thread."""
+    return getattr(_state, "nhwc", False)
+
+
+@contextmanager
+def layout_nhwc(on: bool):
+    prev = nhwc()
+    _state.nhwc = on
+    try:
+        yield
+    finally:
+        _state.nhwc = prev
+
+
+def want_nhwc(x: torch.Tensor) -> bool:
+    return _hip(x) and os.environ.get("CAKE_SD_NHWC", "1") != "0"
+
+
+def cdim() -> int:
+    return -1 if nhwc() else 1
+
+
+def to_internal(x: torch.Tensor) -> torch.Tensor:
+    """NCHW module input -> the active layout."""
+    return x.permute(0, 2, 3, 1).contiguous() if nhwc() else x
+
+
+def to_external(x: torch.Tensor) -> torch.Tensor:
+    """Active layout -> NCHW module output."""
+    return x.permute(0, 3, 1, 2).contiguous() if nhwc() else x
+
+
+def pad_hw_end(x: torch.Tensor) -> torch.Tensor:
+    """Zero-pad one row at the bottom and one column at the right."""
+    return F.pad(x, (0, 0, 0, 1, 0, 1)) if nhwc() else F.pad(x, (0, 1, 0, 1))
+
+
+def tokens(x: torch.Tensor) -> torch.Tensor:
+    """Feature map -> [B, HW, C] tokens."""
+    if nhwc():
+        B, H, W, C = x.shape
+        return x.reshape(B, H * W, C)
+    B, C, H, W = x.shape
+    return x.permute(0, 2, 3, 1).reshape(B, H * W, C)
+
+
+def untokens(t: torch.Tensor, like: torch.Tensor) -> torch.Tensor:
+    """[B, HW, C] tokens -> feature map shaped like `like`."""
+    if nhwc():
+        return t.reshape(like.shape)
+    B, C, H, W = like.shape
+    return t.reshape(B, H, W, C).permute(0, 3, 1, 2).contiguous()
 
 
 def _hip(x: torch.Tensor) -> bool:
@@ -17,6 +82,16 @@ def _hip(x: torch.Tensor) -> bool:
 
 
 def group_norm(x, w, b, groups: int, eps: float, silu: bool = False):
+    if nhwc():
+        from ...ops import hip as K
+        if _hip(x) and K.group_norm_nhwc_supported(x.shape[-1], groups):
+            x = x.contiguous()
+            y = torch.empty_like(x)
+            K.group_norm_nhwc(x, w, b, groups, eps, silu, y)
+            return y
+        y = F.group_norm(x.float().permute(0, 3, 1, 2), groups, w.float(), b.float(), eps)
+        y = F.silu(y) if silu else y
+        return y.permute(0, 2, 3, 1).to(x.dtype).contiguous()
     if _hip(x):
         from ...ops import hip as K
         x = x.contiguous()
@@ -82,3 +157,42 @@ def linear(x, w, b=None):
 
 def conv2d(x, w, b=None, stride: int = 1, padding: int = 1):
     return F.conv2d(x, w, b, stride=stride, padding=padding)
+
+
+def conv(W, name: str, x, stride: int = 1, padding: int = 1, up: bool = False, bias2=None,
+         resid=None):
+    """Convolution `name` of W on x in the active layout.
+
+    up: nearest-2x upsample x first; bias2 [B, OC]: per-sample additive bias
+    (ResnetBlock2D time embedding); resid: added to the output (block residual).
+    """
+    w, b = W[f"{name}.weight"], W.get(f"{name}.bias")
+    if nhwc():
+        from ...ops import hip as K
+        OC, IC = w.shape[:2]
+        if _hip(x) and K.conv_supported(IC, OC, stride, up):
+            from ...ops import conv as C
+            key = f"{name}.weight@nhwc"
+            wp = W.get(key)
+            if wp is None or wp.dtype != x.dtype:
+                wp = W[key] = w.to(x.dtype).permute(0, 2, 3, 1).contiguous()
+            return C.conv2d(x.contiguous(), wp, b, stride=stride, pad=padding, up=up,
+                            bias2=None if bias2 is None else bias2.float().contiguous(),
+                            resid=None if resid is None else resid.contiguous())
+        xn = x.permute(0, 3, 1, 2)  # channels_last view: MIOpen's NHWC kernels
+        if up:
+            xn = F.interpolate(xn, scale_factor=2.0, mode="nearest")
+        y = F.conv2d(xn, w, b, stride=stride, padding=padding).permute(0, 2, 3, 1)
+        if bias2 is not None:
+            y = y + bias2[:, None, None, :].to(y.dtype)
+        if resid is not None:
+            y = y + resid
+        return y.contiguous()
+    if up:
+        x = F.interpolate(x, scale_factor=2.0, mode="nearest")
+    y = conv2d(x, w, b, stride, padding)
+    if bias2 is not None:
+        y = y + bias2[:, :, None, None].to(y.dtype)
+    if resid is not None:
+        y = y + resid
+    return y

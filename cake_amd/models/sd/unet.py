@@ -39,9 +39,9 @@ class Conv(Module):
             p[f"{self.name}.bias"] = (self.cout,)
         return p
 
-    def __call__(self, W, x):
-        return ops.conv2d(x, W[f"{self.name}.weight"], W.get(f"{self.name}.bias"), self.stride,
-                          self.padding)
+    def __call__(self, W, x, up=False, bias2=None, resid=None):
+        return ops.conv(W, self.name, x, self.stride, self.padding, up=up, bias2=bias2,
+                        resid=resid)
 
 
 class Linear(Module):
@@ -86,13 +86,12 @@ class ResnetBlock2D(Module):
     def __call__(self, W, x, temb=None):
         h = ops.group_norm(x, W[f"{self.name}.norm1.weight"], W[f"{self.name}.norm1.bias"],
                            self.groups, self.eps, silu=True)
-        h = self.conv1(W, h)
-        if self.temb is not None and temb is not None:
-            h = h + self.temb(W, F.silu(temb))[:, :, None, None]
+        tb = self.temb(W, F.silu(temb)) if self.temb is not None and temb is not None else None
+        h = self.conv1(W, h, bias2=tb)  # time embedding fused as a per-sample bias
         h = ops.group_norm(h, W[f"{self.name}.norm2.weight"], W[f"{self.name}.norm2.bias"],
                            self.groups, self.eps, silu=True)
-        h = self.conv2(W, h)
-        return (self.short(W, x) if self.short is not None else x) + h
+        short = self.short(W, x) if self.short is not None else x
+        return self.conv2(W, h, resid=short)  # residual fused into the epilogue
 
 
 class Attention(Module):
@@ -159,20 +158,22 @@ class Transformer2DModel(Module):
         return p
 
     def __call__(self, W, x, ctx):
-        B, C, H, Wd = x.shape
         h = ops.group_norm(x, W[f"{self.name}.norm.weight"], W[f"{self.name}.norm.bias"],
                            self.groups, 1e-6)
-        if self.linear:
-            h = self.proj_in(W, h.permute(0, 2, 3, 1).reshape(B, H * Wd, C))
-        else:
-            h = self.proj_in(W, h).permute(0, 2, 3, 1).reshape(B, H * Wd, C)
+        # proj_in / proj_out are per-pixel linears (1x1 convs in SD1.x): run them
+        # on [B, HW, C] tokens, which is a free view in the channels-last layout
+        h = _token_linear(W, self.proj_in.name, ops.tokens(h))
         for blk in self.blocks:
             h = blk(W, h, ctx)
-        if self.linear:
-            h = self.proj_out(W, h).reshape(B, H, Wd, C).permute(0, 3, 1, 2)
-        else:
-            h = self.proj_out(W, h.reshape(B, H, Wd, C).permute(0, 3, 1, 2).contiguous())
-        return h.contiguous() + x
+        h = _token_linear(W, self.proj_out.name, h)
+        return ops.untokens(h, x) + x
+
+
+def _token_linear(W, name, t):
+    w = W[f"{name}.weight"]
+    if w.dim() == 4:
+        w = w[:, :, 0, 0]
+    return ops.linear(t, w, W.get(f"{name}.bias"))
 
 
 def timestep_embedding(t: torch.Tensor, dim: int, flip_sin_to_cos: bool, shift: float) -> torch.Tensor:
@@ -251,10 +252,18 @@ class UNet2DConditionModel(Module):
         cfg = self.cfg
         B = sample.shape[0]
         dt = sample.dtype
-        t = torch.full((B,), float(timestep), device=sample.device)
+        if isinstance(timestep, torch.Tensor):  # device scalar: replayable in a hipGraph
+            t = timestep.to(sample.device, torch.float32).reshape(-1).expand(B)
+        else:
+            t = torch.full((B,), float(timestep), device=sample.device)
         emb = timestep_embedding(t, cfg.blocks[0].out_channels, cfg.flip_sin_to_cos,
                                  cfg.freq_shift).to(dt)
         emb = self.t2(W, F.silu(self.t1(W, emb)))
+        with ops.layout_nhwc(ops.want_nhwc(sample)):
+            return ops.to_external(self._body(W, ops.to_internal(sample), emb, ctx))
+
+    def _body(self, W, sample, emb, ctx):
+        cfg = self.cfg
         x = self.conv_in(W, sample)
         skips = [x]
         for res, att, ds in self.down:
@@ -271,11 +280,11 @@ class UNet2DConditionModel(Module):
         x = self.mid_res[1](W, x, emb)
         for res, att, us in self.up:
             for j, r in enumerate(res):
-                x = r(W, torch.cat([x, skips.pop()], 1), emb)
+                x = r(W, torch.cat([x, skips.pop()], ops.cdim()), emb)
                 if att:
                     x = att[j](W, x, ctx)
             if us is not None:
-                x = us(W, F.interpolate(x, scale_factor=2.0, mode="nearest"))
+                x = us(W, x, up=True)  # nearest-2x upsample fused into the conv
         x = ops.group_norm(x, W["conv_norm_out.weight"], W["conv_norm_out.bias"],
                            cfg.norm_num_groups, cfg.norm_eps, silu=True)
         return self.conv_out(W, x)

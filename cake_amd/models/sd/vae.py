@@ -12,7 +12,6 @@ Accepts both current (to_q/to_k/to_v/to_out.0) and legacy
 from __future__ import annotations
 
 import torch
-import torch.nn.functional as F
 
 from . import ops
 from .config import VAEConfig
@@ -49,13 +48,11 @@ class VAEAttention(Module):
         return p
 
     def __call__(self, W, x):
-        B, C, H, Wd = x.shape
         h = ops.group_norm(x, W[f"{self.name}.group_norm.weight"], W[f"{self.name}.group_norm.bias"],
                            self.groups, 1e-6)
-        h = h.reshape(B, C, H * Wd).transpose(1, 2)
+        h = ops.tokens(h)
         a = ops.attention(self.q(W, h), self.k(W, h), self.v(W, h), 1)
-        o = self.o(W, a).transpose(1, 2).reshape(B, C, H, Wd)
-        return o + x
+        return ops.untokens(self.o(W, a), x) + x
 
 
 class AutoencoderKL(Module):
@@ -111,25 +108,33 @@ class AutoencoderKL(Module):
 
     def encode(self, W, x: torch.Tensor, generator: torch.Generator | None = None) -> torch.Tensor:
         """image [B,3,H,W] in [-1,1] -> latent sample [B,4,H/8,W/8] (unscaled)."""
+        with ops.layout_nhwc(ops.want_nhwc(x)):
+            moments = ops.to_external(self._encode(W, ops.to_internal(x))).float()
+        mean, logvar = moments.chunk(2, 1)
+        logvar = logvar.clamp(-30.0, 20.0)
+        eps = torch.randn(mean.shape, generator=generator, device="cpu").to(mean.device)
+        return (mean + torch.exp(0.5 * logvar) * eps).to(x.dtype)
+
+    def _encode(self, W, x):
         G = self.cfg.norm_num_groups
         h = self.e_in(W, x)
         for res, ds in self.e_down:
             for r in res:
                 h = r(W, h)
             if ds is not None:
-                h = ds(W, F.pad(h, (0, 1, 0, 1)))
+                h = ds(W, ops.pad_hw_end(h))
         h = self.e_mid[0](W, h)
         h = self.e_att(W, h)
         h = self.e_mid[1](W, h)
         h = ops.group_norm(h, W["encoder.conv_norm_out.weight"], W["encoder.conv_norm_out.bias"],
                            G, 1e-6, silu=True)
-        moments = self.quant(W, self.e_out(W, h)).float()
-        mean, logvar = moments.chunk(2, 1)
-        logvar = logvar.clamp(-30.0, 20.0)
-        eps = torch.randn(mean.shape, generator=generator, device="cpu").to(mean.device)
-        return (mean + torch.exp(0.5 * logvar) * eps).to(x.dtype)
+        return self.quant(W, self.e_out(W, h))
 
     def decode(self, W, z: torch.Tensor) -> torch.Tensor:
+        with ops.layout_nhwc(ops.want_nhwc(z)):
+            return ops.to_external(self._decode(W, ops.to_internal(z)))
+
+    def _decode(self, W, z):
         G = self.cfg.norm_num_groups
         h = self.d_in(W, self.post_quant(W, z))
         h = self.d_mid[0](W, h)
@@ -139,7 +144,7 @@ class AutoencoderKL(Module):
             for r in res:
                 h = r(W, h)
             if us is not None:
-                h = us(W, F.interpolate(h, scale_factor=2.0, mode="nearest"))
+                h = us(W, h, up=True)
         h = ops.group_norm(h, W["decoder.conv_norm_out.weight"], W["decoder.conv_norm_out.bias"],
                            G, 1e-6, silu=True)
         return self.d_out(W, h)

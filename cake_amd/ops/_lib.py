@@ -89,8 +89,11 @@ def check(rc: int, name: str) -> None:
 _SIGS.update({
     "cake_flash_attn": [I, P, P, P, P, I, I, I, I, I, I, P, F, I, I, P],
     "cake_groupnorm": [I, P, P, P, I, I, C.c_longlong, I, F, I, P, P, P],
+    "cake_groupnorm_nhwc": [I, P, P, P, I, I, I, I, F, I, P, P, P, P, P],
+    "cake_groupnorm_nhwc_splits": [I],
     "cake_layernorm": [I, P, P, P, C.c_longlong, I, F, P, P],
     "cake_geglu": [I, P, C.c_longlong, I, P, P],
+    "cake_conv2d_nhwc": [I, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, P],
 })
 
 _SIGS.update({

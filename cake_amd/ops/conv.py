@@ -1,0 +1,76 @@
+"""Per-shape autotuning front end for the MFMA implicit-GEMM convolution (conv2d.hip).
+
+The UNet / VAE run a fixed set of convolution shapes, so the first call of each
+shape times every applicable kernel variant (tile shape x LDS staging x split-K
+x halo) and caches the winner -- the role cudnn/MIOpen "find" plays for the
+reference's candle conv2d.  Calls made while a hipGraph is being
+captured never tune (they use the cached choice or the static planner), so run
+one eager warmup step before capturing.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from . import hip as K
+
+_cache: dict[tuple, tuple[int, int]] = {}
+_AUTOTUNE = os.environ.get("CAKE_CONV_AUTOTUNE", "1") != "0"
+
+
+def _candidates(stride: int, k: int, splits_ok: bool):
+    c = []
+    if stride == 1 and k > 1:
+        c += [(8, 1), (9, 1), (10, 1), (11, 1), (12, 1), (13, 1)]
+    for cfg in (4, 5, 6, 7, 0, 1, 2, 3):
+        for sp in ((1, 2, 4, 8) if splits_ok else (1,)):
+            c.append((cfg, sp))
+    return c
+
+
+def _time(fn, iters=3) -> float:
+    fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e)
+
+
+def conv2d(x, w, bias=None, *, stride: int = 1, pad: int = 1, up: bool = False, bias2=None,
+           resid=None):
+    """NHWC conv with the tuned kernel variant for this shape (see conv2d_nhwc)."""
+    N, H, W, IC = x.shape
+    OC, KH, KW, _ = w.shape
+    key = (x.dtype, N, H, W, IC, OC, KH, KW, stride, pad, bool(up), bias2 is not None,
+           resid is not None)
+    choice = _cache.get(key)
+    if choice is None:
+        capturing = torch.cuda.is_current_stream_capturing()
+        if _AUTOTUNE and not capturing:
+            best = None
+            for cfg, sp in _candidates(stride, KH * KW, True):
+                f = (lambda c=cfg, s=sp: K.conv2d_nhwc(x, w, bias, stride=stride, pad=pad, up=up,
+                                                       bias2=bias2, resid=resid, cfg=c, splits=s))
+                try:
+                    t = _time(f)
+                except (ValueError, RuntimeError):
+                    continue
+                if best is None or t < best[0]:
+                    best = (t, cfg, sp)
+            choice = (best[1], best[2])
+        else:
+            VH, VW = H << int(up), W << int(up)
+            OH, OW = (VH + 2 * pad - KH) // stride + 1, (VW + 2 * pad - KW) // stride + 1
+            choice = K.conv_plan(N * OH * OW, OC, KH * KW * IC // 64)
+        _cache[key] = choice
+    return K.conv2d_nhwc(x, w, bias, stride=stride, pad=pad, up=up, bias2=bias2, resid=resid,
+                         cfg=choice[0], splits=choice[1])
+
+
+def tuned() -> dict:
+    """Shape -> (cfg, splits) choices made so far (for logs / profiles)."""
+    return dict(_cache)

@@ -298,6 +298,36 @@ def group_norm(x, gamma, beta, groups: int, eps: float, silu: bool, out):
           "groupnorm")
 
 
+_gn_tickets: dict = {}
+
+
+def group_norm_nhwc_supported(C: int, groups: int) -> bool:
+    cg = C // groups
+    return C % groups == 0 and C % 8 == 0 and C <= 4096 and cg >= 4 and (cg >= 8 or 8 % cg == 0)
+
+
+def group_norm_nhwc(x, gamma, beta, groups: int, eps: float, silu: bool, out):
+    """GroupNorm over channels-last x [N, ..., C] (contiguous) [+ fused SiLU]."""
+    N, C = x.shape[0], x.shape[-1]
+    HW = x.numel() // (N * C)
+    _req(x, "x")
+    _req(gamma, "gamma", dtype=x.dtype, shape=(C,))
+    _req(beta, "beta", dtype=x.dtype, shape=(C,))
+    _req(out, "out", dtype=x.dtype, shape=x.shape)
+    if not group_norm_nhwc_supported(C, groups):
+        raise ValueError(f"group_norm_nhwc: unsupported C={C} groups={groups}")
+    S = kernels().cake_groupnorm_nhwc_splits(HW)
+    t = _gn_tickets.get(x.device)
+    if t is None or t.numel() < N:
+        t = _gn_tickets[x.device] = torch.zeros(max(N, 64), device=x.device, dtype=torch.int32)
+    part = torch.empty(N * S * groups * 2, device=x.device, dtype=torch.float64)
+    stats = torch.empty(N * groups * 2, device=x.device, dtype=torch.float32)
+    check(kernels().cake_groupnorm_nhwc(_dt(x), _p(x), _p(gamma), _p(beta), N, HW, C, groups,
+                                        float(eps), int(silu), _p(part), _p(t), _p(stats),
+                                        _p(out), _stream()),
+          "groupnorm_nhwc")
+
+
 def layer_norm(x, gamma, beta, eps: float, out):
     C = x.shape[-1]
     _req(x, "x")
@@ -314,6 +344,108 @@ def geglu(h, out):
     _req(out, "out", dtype=h.dtype, numel=h.numel() // 2)
     check(kernels().cake_geglu(_dt(h), _p(h), h.numel() // (2 * F), F, _p(out), _stream()),
           "geglu")
+
+
+# ---------------------------------------------------------------------------
+# implicit-GEMM convolution (conv2d.hip), NHWC activations
+# ---------------------------------------------------------------------------
+
+# cfg ids 0-3: register-staged LDS tiles; 4-7: the same tiles staged by LDS-DMA
+_CONV_TILES = ((128, 128), (64, 128), (128, 64), (64, 64)) * 2  # (oc, pixel) tile per cfg
+_CONV_SLOTS = (2, 3, 3, 5) * 2        # resident workgroups per CU (VGPR/LDS bound)
+_CONV_EFF = (1.0, 0.8, 0.8, 0.6) * 2  # relative MFMA efficiency of the tile shapes
+_CONV_CFGS = (0, 1, 2, 3)             # planner candidates
+_NUM_CUS = 256
+_zero_lines: dict = {}
+
+
+def _zeros16(dev) -> torch.Tensor:
+    z = _zero_lines.get(dev)
+    if z is None:
+        z = _zero_lines[dev] = torch.zeros(64, dtype=torch.int32, device=dev)
+    return z
+
+
+def conv_supported(IC: int, OC: int, stride: int = 1, up: bool = False) -> bool:
+    return IC % 64 == 0 and OC % 4 == 0 and not (up and stride != 1)
+
+
+_HALO_TILES = {256: ((16, 16), (8, 32), (32, 8)),
+               128: ((8, 16), (16, 8), (10, 12), (12, 10)), 64: ((8, 8), (4, 16), (16, 4))}
+
+
+def halo_tile(OH: int, OW: int, bn: int) -> tuple[int, int]:
+    """Spatial output tile (th, tw), th*tw <= bn, with the least padded area."""
+    return min(_HALO_TILES[bn], key=lambda t: (-(-OH // t[0]) * t[0] * -(-OW // t[1]) * t[1],
+                                                -t[1]))
+
+
+def conv_plan(P: int, OC: int, ksteps: int) -> tuple[int, int]:
+    """(tile cfg, split-K) minimising a waves-of-tiles cost model."""
+    best = None
+    for cfg in _CONV_CFGS:
+        bm, bn = _CONV_TILES[cfg]
+        tiles = -(-OC // bm) * -(-P // bn)
+        for splits in (1, 2, 4, 8):
+            if splits > 1 and (ksteps // splits < 4 or tiles * splits > 2 * _NUM_CUS * _CONV_SLOTS[cfg]):
+                continue
+            waves = -(-tiles * splits // (_NUM_CUS * _CONV_SLOTS[cfg]))
+            cost = waves * _CONV_SLOTS[cfg] * bm * bn * (-(-ksteps // splits)) / _CONV_EFF[cfg]
+            cost += (splits > 1) * P * OC * splits * 0.05  # slab round trip + finalize launch
+            if best is None or cost < best[0]:
+                best = (cost, cfg, splits)
+    return best[1], best[2]
+
+
+def conv2d_nhwc(x, w, bias=None, *, stride: int = 1, pad: int = 1, up: bool = False,
+                bias2=None, resid=None, out=None, cfg: int | None = None,
+                splits: int | None = None, tile: tuple[int, int] | None = None):
+    """NHWC conv: x [N,H,W,IC], w packed [OC,KH,KW,IC] -> [N,OH,OW,OC].
+
+    bias [OC]; bias2 [N,OC] f32 (per-sample additive, e.g. time embedding);
+    resid [N,OH,OW,OC] added in the epilogue; up = nearest-2x upsample of x first.
+    """
+    N, H, W, IC = x.shape
+    OC, KH, KW, IC2 = w.shape
+    if IC2 != IC or not conv_supported(IC, OC, stride, up):
+        raise ValueError(f"conv2d_nhwc: unsupported IC={IC} OC={OC} w={tuple(w.shape)}")
+    VH, VW = H << int(up), W << int(up)
+    OH, OW = (VH + 2 * pad - KH) // stride + 1, (VW + 2 * pad - KW) // stride + 1
+    _req(x, "x")
+    _req(w, "w", dtype=x.dtype)
+    if bias is not None:
+        _req(bias, "bias", dtype=x.dtype, numel=OC)
+    if bias2 is not None:
+        _req(bias2, "bias2", dtype=torch.float32, shape=(N, OC))
+    if resid is not None:
+        _req(resid, "resid", dtype=x.dtype, shape=(N, OH, OW, OC))
+    if out is None:
+        out = torch.empty(N, OH, OW, OC, device=x.device, dtype=x.dtype)
+    _req(out, "out", dtype=x.dtype, shape=(N, OH, OW, OC))
+    P, ksteps = N * OH * OW, KH * KW * IC // 64
+    if cfg is None or splits is None:
+        c0, s0 = conv_plan(P, OC, ksteps)
+        cfg = c0 if cfg is None else cfg
+        splits = s0 if splits is None else splits
+    th = tw = 0
+    if cfg >= 8:  # halo kernels: stride 1, no split-K
+        if stride != 1:
+            raise ValueError("conv2d_nhwc: halo tiles need stride 1")
+        splits = 1
+        th, tw = tile or halo_tile(OH, OW, 256 if cfg >= 12 else 128 if cfg < 10 else 64)
+    splits = max(1, min(splits, ksteps))
+    kps = -(-ksteps // splits)
+    splits = -(-ksteps // kps)
+    ws = torch.empty(splits * P * OC, device=x.device, dtype=torch.float32) if splits > 1 else None
+    check(kernels().cake_conv2d_nhwc(_dt(x), _p(x), _p(w), None if bias is None else _p(bias),
+                                     None if bias2 is None else _p(bias2),
+                                     None if resid is None else _p(resid), _p(out),
+                                     None if ws is None else _p(ws), _p(_zeros16(x.device)),
+                                     N, H, W, IC, OC, KH, KW,
+                                     stride, pad, int(up), int(cfg), int(splits), th, tw,
+                                     _stream()),
+          "conv2d_nhwc")
+    return out
 
 
 def attn_oproj_supported(nh: int, nkv: int, hd: int, H: int) -> bool:

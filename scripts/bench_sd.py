@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--version", default="v1-5")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--dtype", default="f16")
+    ap.add_argument("--graph", action="store_true", help="replay the UNet step as one hipGraph")
     a = ap.parse_args()
     dt = torch.float16 if a.dtype == "f16" else torch.bfloat16
     cfg = get_config(a.version)
@@ -30,18 +31,28 @@ def main():
     B = 2  # classifier-free guidance doubles the batch
     x = torch.randn(B, 4, cfg.height // 8, cfg.width // 8, device=dev, dtype=dt)
     ctx = torch.randn(B, 77, cfg.unet.cross_attention_dim, device=dev, dtype=dt)
+    tbuf = torch.zeros((), device=dev)
     with torch.no_grad():
-        for _ in range(2):
-            unet.forward(w, x, 500, ctx)
+        for _ in range(2):  # warmup: conv autotuning, packed weights, workspaces
+            unet.forward(w, x, tbuf, ctx)
+        torch.cuda.synchronize()
+        step = lambda: unet.forward(w, x, tbuf, ctx)  # noqa: E731
+        if a.graph:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                unet.forward(w, x, tbuf, ctx)
+            step = g.replay
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for i in range(a.steps):
-            unet.forward(w, x, 999 - i, ctx)
+            tbuf.fill_(999 - i)
+            step()
         torch.cuda.synchronize()
     dt_step = (time.perf_counter() - t0) / a.steps
     print(json.dumps({"metric": "sd_unet_seconds_per_step", "version": a.version,
                       "resolution": f"{cfg.width}x{cfg.height}", "batch": B, "dtype": a.dtype,
-                      "value": round(dt_step, 4), "unit": "s/step"}))
+                      "value": round(dt_step, 4), "unit": "s/step", "graph": a.graph,
+                      "nhwc": os.environ.get("CAKE_SD_NHWC", "1") != "0"}))
 
 
 if __name__ == "__main__":

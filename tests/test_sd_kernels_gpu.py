@@ -97,3 +97,103 @@ def test_layer_norm_and_geglu(cuda, dt):
     a, gate = h.float().chunk(2, -1)
     torch.testing.assert_close(o.float(), a * torch.nn.functional.gelu(gate, approximate="tanh"),
                                **_tol(dt))
+
+
+def _ref_conv(x, w, b, stride, pad, up, bias2=None, resid=None):
+    """x NHWC, w [OC,IC,KH,KW] -> NHWC, f32."""
+    xc = x.float().permute(0, 3, 1, 2)
+    if up:
+        xc = torch.nn.functional.interpolate(xc, scale_factor=2.0, mode="nearest")
+    y = torch.nn.functional.conv2d(xc, w.float(), None if b is None else b.float(), stride=stride,
+                                   padding=pad).permute(0, 2, 3, 1)
+    if bias2 is not None:
+        y = y + bias2[:, None, None, :]
+    if resid is not None:
+        y = y + resid.float()
+    return y
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("N,H,W,IC,OC,k,stride,up", [
+    (2, 16, 16, 64, 128, 3, 1, False),
+    (2, 9, 7, 128, 320, 3, 1, False),    # ragged pixels, OC not a tile multiple
+    (1, 16, 16, 64, 64, 3, 2, False),    # downsampler (stride 2)
+    (1, 15, 17, 64, 64, 3, 2, False),    # stride 2, odd sizes
+    (2, 8, 8, 64, 128, 3, 1, True),      # upsampler (nearest 2x fused)
+    (2, 12, 12, 192, 64, 1, 1, False),   # 1x1 shortcut
+    (1, 8, 8, 320, 4, 3, 1, False),      # conv_out-like OC=4
+])
+@pytest.mark.parametrize("cfg,splits", [(None, None), (0, 1), (3, 1), (1, 3), (2, 2),
+                                        (4, 1), (5, 2), (6, 1), (7, 3),
+                                        (8, 1), (9, 1), (10, 1), (11, 1), (12, 1), (13, 1)])
+def test_conv2d_nhwc(cuda, dt, N, H, W, IC, OC, k, stride, up, cfg, splits):
+    from cake_amd.ops import hip as K
+    if cfg is not None and cfg >= 8 and stride != 1:
+        pytest.skip("halo kernels are stride-1 only")
+    torch.manual_seed(5)
+    x = torch.randn(N, H, W, IC, device=cuda).to(dt)
+    w = (torch.randn(OC, IC, k, k, device=cuda) / math.sqrt(IC * k * k)).to(dt)
+    b = torch.randn(OC, device=cuda).to(dt)
+    pad = k // 2
+    wp = w.permute(0, 2, 3, 1).contiguous()
+    y = K.conv2d_nhwc(x, wp, b, stride=stride, pad=pad, up=up, cfg=cfg, splits=splits)
+    ref = _ref_conv(x, w, b, stride, pad, up)
+    assert y.shape == ref.shape
+    torch.testing.assert_close(y.float(), ref, **_tol(dt))
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("splits", [1, 4])
+@pytest.mark.parametrize("cfg", [0, 6, 8, 11, 12])
+def test_conv2d_nhwc_fused_epilogue(cuda, dt, splits, cfg):
+    """bias + per-sample f32 bias (time embedding) + residual, as ResnetBlock2D uses them."""
+    from cake_amd.ops import hip as K
+    torch.manual_seed(6)
+    N, H, W, IC, OC = 2, 10, 12, 128, 192
+    x = torch.randn(N, H, W, IC, device=cuda).to(dt)
+    w = (torch.randn(OC, IC, 3, 3, device=cuda) / math.sqrt(IC * 9)).to(dt)
+    b = torch.randn(OC, device=cuda).to(dt)
+    b2 = torch.randn(N, OC, device=cuda)
+    r = torch.randn(N, H, W, OC, device=cuda).to(dt)
+    y = K.conv2d_nhwc(x, w.permute(0, 2, 3, 1).contiguous(), b, bias2=b2, resid=r,
+                      cfg=cfg, splits=splits)
+    torch.testing.assert_close(y.float(), _ref_conv(x, w, b, 1, 1, False, b2, r), **_tol(dt))
+
+
+@pytest.mark.parametrize("cfg,tile", [(8, (8, 16)), (8, (16, 8)), (8, (10, 12)), (8, (12, 10)),
+                                      (12, (16, 16)), (12, (8, 32)), (13, (32, 8))])
+def test_conv2d_halo_tiles(cuda, cfg, tile):
+    """Every spatial tile shape of the halo kernel, with partial edge tiles."""
+    from cake_amd.ops import hip as K
+    torch.manual_seed(7)
+    dt = torch.bfloat16
+    x = torch.randn(2, 21, 19, 128, device=cuda).to(dt)
+    w = (torch.randn(192, 128, 3, 3, device=cuda) / math.sqrt(128 * 9)).to(dt)
+    b = torch.randn(192, device=cuda).to(dt)
+    y = K.conv2d_nhwc(x, w.permute(0, 2, 3, 1).contiguous(), b, cfg=cfg, tile=tile)
+    torch.testing.assert_close(y.float(), _ref_conv(x, w, b, 1, 1, False), **_tol(dt))
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("N,H,W,C,G", [
+    (2, 16, 16, 320, 32),    # Cg = 10: 8-channel vectors straddle groups
+    (2, 8, 8, 2560, 32),     # concat width (Cg = 80), > 256 channel vectors
+    (1, 32, 24, 128, 32),    # VAE (Cg = 4)
+    (2, 5, 7, 640, 32),      # ragged spatial size
+    (1, 64, 64, 256, 32),    # Cg = 8, many pixels
+])
+@pytest.mark.parametrize("silu", [False, True])
+def test_group_norm_nhwc(cuda, dt, N, H, W, C, G, silu):
+    from cake_amd.ops import hip as K
+    torch.manual_seed(11)
+    x = (torch.randn(N, H, W, C, device=cuda) * 3 + 2).to(dt)
+    g = (1 + 0.1 * torch.randn(C, device=cuda)).to(dt)
+    b = (0.1 * torch.randn(C, device=cuda)).to(dt)
+    y = torch.empty_like(x)
+    for _ in range(2):  # second call checks the re-armed tickets
+        K.group_norm_nhwc(x, g, b, G, 1e-5, silu, y)
+    ref = torch.nn.functional.group_norm(x.float().permute(0, 3, 1, 2), G, g.float(), b.float(),
+                                         1e-5)
+    if silu:
+        ref = torch.nn.functional.silu(ref)
+    torch.testing.assert_close(y.float(), ref.permute(0, 2, 3, 1), **_tol(dt))
