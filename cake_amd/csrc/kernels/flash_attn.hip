@@ -22,6 +22,8 @@
 // DP = head dim padded to a multiple of 32 (zero-filled, never stored).
 #include "common.h"
 
+#include <cstdlib>
+
 namespace cake {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -220,12 +222,260 @@ __global__ __launch_bounds__(256) void flash_fwd_kernel(FlashArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// v2: 32x32x16 MFMA, swapped QKᵀ, P straight from the accumulators.
+//
+// Workgroup = 4 waves x 32 query rows; key tiles of 64 (two 32-key subtiles).
+// Per wave and tile:
+//   Sᵀ[key][q] = K·Qᵀ            (A = K rows from LDS, B = Q rows in registers)
+//     -> lane (q = lane&31, half h) holds the scores of its query row for
+//        keys (r&3) + 8(r>>2) + 4h: the row max is 31 in-lane fmax + ONE
+//        cross-half shuffle, the row sum stays lane-partial until the end.
+//   Oᵀ[d][q] += Vᵀ·Pᵀ            (B = the Sᵀ accumulator registers packed to
+//        16-bit: an accumulator tile is the next MFMA's B operand when the
+//        product sums over its rows; CDNA guide §3.  A = Vᵀ rows from LDS,
+//        in the matching permuted key order: two 8-byte reads per fragment)
+// K is staged row-major with a 16-byte XOR swizzle (conflict-free
+// ds_read_b128), V transposed (row stride 68 elements: conflict-free
+// ds_read_b64), both double-buffered; the next tile's global loads are issued
+// before the MFMAs and written to LDS after them (issue-early / write-late).
+// DP = head dim padded to 64 or 128.
+// ---------------------------------------------------------------------------
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+template <int DT>
+__device__ __forceinline__ f32x16 mfma32(const uint4 a, const uint4 b, f32x16 c) {
+  if constexpr (DT == kBF16) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
+                                                   __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+  } else {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a),
+                                                  __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+  }
+}
+
+template <int DP>
+__device__ __forceinline__ int k_swz(int row, int chunk) {
+  // 16-byte chunk position inside a K row (conflict-free ds_read_b128 for the
+  // 16-lane groups {0-3,12-15,20-27}, ...; MI355X_MICROARCH §LDS)
+  if constexpr (DP == 64) return chunk ^ ((row >> 1) & 7);
+  else return chunk ^ (row & 15);
+}
+
+__device__ __forceinline__ uint32_t pack2(uint16_t lo, uint16_t hi) {
+  return (uint32_t)lo | ((uint32_t)hi << 16);
+}
+
+constexpr int kV2Rows = 128, kVTS = 68;
+
+template <int DT, int DP>
+__global__ __launch_bounds__(256, 2) void flash2_fwd_kernel(FlashArgs a) {
+  constexpr int KS = DP / 16;   // QKᵀ k-steps
+  constexpr int NCH = DP / 8;   // 16-byte chunks per K/V row
+  constexpr int DTL = DP / 32;  // Oᵀ tiles
+  constexpr int NPR = NCH / 8;  // key pairs x chunks per thread per tile (32*NCH/256)
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * 64 * DP + 2 * DP * kVTS];
+  uint16_t* const Kb = smem;
+  uint16_t* const Vb = smem + 2 * 64 * DP;
+
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int l32 = lane & 31, h = lane >> 5;
+  const int mblk = blockIdx.x * kV2Rows;
+  const int qrow = mblk + wave * 32 + l32;
+  const int hq = blockIdx.y, b = blockIdx.z;
+  const int hk = hq / (a.H / a.Hkv);
+  const uint16_t* qb = a.q + b * a.q_sb + hq * a.q_sh;
+  const uint16_t* kb = a.k + b * a.k_sb + hk * a.k_sh;
+  const uint16_t* vb = a.v + b * a.v_sb + hk * a.v_sh;
+
+  // Q as the B operand: lane holds Q[qrow][16ks + 8h .. +8]
+  uint4 qf[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    const int d0 = 16 * ks + 8 * h;
+    qf[ks] = (qrow < a.N && d0 < a.D)
+                 ? *reinterpret_cast<const uint4*>(qb + (long long)qrow * a.q_sn + d0)
+                 : make_uint4(0, 0, 0, 0);
+  }
+
+  f32x16 o[DTL];
+#pragma unroll
+  for (int t = 0; t < DTL; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[t][r] = 0.f;
+  float m = -INFINITY, l = 0.f;
+  const int qpos = qrow + a.pos0;
+
+  int kend = a.M;
+  if (a.causal) kend = min(kend, a.pos0 + mblk + kV2Rows);
+  const int ntiles = (kend + 63) / 64;
+
+  // staging: pair pi -> keys 2*(pi / NCH) + {0,1}, chunk pi % NCH
+  uint4 kr[NPR][2], vr[NPR][2];
+  auto gload = [&](int j) {
+#pragma unroll
+    for (int i = 0; i < NPR; ++i) {
+      const int pi = tid + 256 * i, kp = pi / NCH, c = pi - kp * NCH;
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int key = j * 64 + 2 * kp + e;
+        const bool ok = key < a.M && c * 8 < a.D;
+        kr[i][e] = ok ? *reinterpret_cast<const uint4*>(kb + (long long)key * a.k_sn + c * 8)
+                      : make_uint4(0, 0, 0, 0);
+        vr[i][e] = ok ? *reinterpret_cast<const uint4*>(vb + (long long)key * a.v_sn + c * 8)
+                      : make_uint4(0, 0, 0, 0);
+      }
+    }
+  };
+  auto sstore = [&](int buf) {
+    uint16_t* Ks = Kb + buf * 64 * DP;
+    uint16_t* Vt = Vb + buf * DP * kVTS;
+#pragma unroll
+    for (int i = 0; i < NPR; ++i) {
+      const int pi = tid + 256 * i, kp = pi / NCH, c = pi - kp * NCH;
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int row = 2 * kp + e;
+        *reinterpret_cast<uint4*>(Ks + row * DP + k_swz<DP>(row, c) * 8) = kr[i][e];
+      }
+      const uint16_t* v0 = reinterpret_cast<const uint16_t*>(&vr[i][0]);
+      const uint16_t* v1 = reinterpret_cast<const uint16_t*>(&vr[i][1]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        *reinterpret_cast<uint32_t*>(Vt + (c * 8 + e) * kVTS + 2 * kp) = pack2(v0[e], v1[e]);
+    }
+  };
+
+  if (ntiles > 0) {
+    gload(0);
+    sstore(0);
+  }
+  __syncthreads();
+  for (int j = 0; j < ntiles; ++j) {
+    const int buf = j & 1;
+    const bool more = j + 1 < ntiles;
+    if (more) gload(j + 1);
+    const uint16_t* Ks = Kb + buf * 64 * DP;
+    const uint16_t* Vt = Vb + buf * DP * kVTS;
+
+    // ---- Sᵀ = K Qᵀ over two 32-key subtiles
+    f32x16 s[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s[t][r] = 0.f;
+      const int row = 32 * t + l32;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const uint4 kf =
+            *reinterpret_cast<const uint4*>(Ks + row * DP + k_swz<DP>(row, 2 * ks + h) * 8);
+        s[t] = mfma32<DT>(kf, qf[ks], s[t]);
+      }
+    }
+
+    // ---- mask + online softmax (exp2 domain); the row spans lanes l, l^32
+    float mt = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = j * 64 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h;
+        float x = s[t][r] * a.scale_log2;
+        if (key >= a.M || (a.causal && key > qpos)) x = -INFINITY;
+        s[t][r] = x;
+        mt = fmaxf(mt, x);
+      }
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    const float mn = fmaxf(m, mt);
+    const float alpha = mn == -INFINITY ? 1.f : __builtin_amdgcn_exp2f(m - mn);
+    float rs = 0.f;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = mn == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(s[t][r] - mn);
+        s[t][r] = p;
+        rs += p;
+      }
+    l = l * alpha + rs;
+    m = mn;
+#pragma unroll
+    for (int t = 0; t < DTL; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
+
+    // ---- Oᵀ += Vᵀ Pᵀ: k-step (t, s2) covers keys 32t + 16s2 + {8(j>>2) + 4h + (j&3)}
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        uint4 pf;
+        pf.x = pack2(from_f32<DT>(s[t][8 * s2 + 0]), from_f32<DT>(s[t][8 * s2 + 1]));
+        pf.y = pack2(from_f32<DT>(s[t][8 * s2 + 2]), from_f32<DT>(s[t][8 * s2 + 3]));
+        pf.z = pack2(from_f32<DT>(s[t][8 * s2 + 4]), from_f32<DT>(s[t][8 * s2 + 5]));
+        pf.w = pack2(from_f32<DT>(s[t][8 * s2 + 6]), from_f32<DT>(s[t][8 * s2 + 7]));
+        const int k0 = 32 * t + 16 * s2 + 4 * h;
+#pragma unroll
+        for (int dt = 0; dt < DTL; ++dt) {
+          const uint16_t* vrow = Vt + (32 * dt + l32) * kVTS + k0;
+          const uint2 lo = *reinterpret_cast<const uint2*>(vrow);
+          const uint2 hi = *reinterpret_cast<const uint2*>(vrow + 8);
+          o[dt] = mfma32<DT>(make_uint4(lo.x, lo.y, hi.x, hi.y), pf, o[dt]);
+        }
+      }
+    if (more) sstore(buf ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: O[q][d] = Oᵀ[d][q] / l  (d = 32dt + 8g + 4h + i)
+  const float lt = l + __shfl_xor(l, 32, 64);
+  const float inv = lt > 0.f ? 1.f / lt : 0.f;
+  if (qrow < a.N) {
+    uint16_t* orow = a.o + b * a.o_sb + hq * a.o_sh + (long long)qrow * a.o_sn;
+#pragma unroll
+    for (int dt = 0; dt < DTL; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = 32 * dt + 8 * g + 4 * h;
+        if (d < a.D) {
+          uint2 st;
+          st.x = pack2(from_f32<DT>(o[dt][4 * g + 0] * inv), from_f32<DT>(o[dt][4 * g + 1] * inv));
+          st.y = pack2(from_f32<DT>(o[dt][4 * g + 2] * inv), from_f32<DT>(o[dt][4 * g + 3] * inv));
+          *reinterpret_cast<uint2*>(orow + d) = st;
+        }
+      }
+  }
+}
+
 }  // namespace cake
 
 using namespace cake;
 
+static int g_flash_impl = -1;  // -1: from CAKE_FLASH_IMPL (default 2)
+
+static int flash_impl() {
+  if (g_flash_impl < 0) {
+    const char* e = getenv("CAKE_FLASH_IMPL");
+    g_flash_impl = e ? atoi(e) : 2;
+  }
+  return g_flash_impl;
+}
+
 template <int DT>
 static int launch_flash(const FlashArgs& a, hipStream_t st) {
+  // v2 needs 16-byte rows (D % 8 == 0, 8-byte aligned strides) and D <= 128
+  auto al = [](const void* p, int n) { return ((uintptr_t)p % n) == 0; };
+  const bool v2 = flash_impl() >= 2 && a.D % 8 == 0 && a.D <= 128 && a.q_sn % 8 == 0 &&
+                  a.k_sn % 8 == 0 && a.v_sn % 8 == 0 && a.o_sn % 4 == 0 && a.q_sb % 8 == 0 &&
+                  a.q_sh % 8 == 0 && a.k_sb % 8 == 0 && a.k_sh % 8 == 0 && a.v_sb % 8 == 0 &&
+                  a.v_sh % 8 == 0 && a.o_sb % 4 == 0 && a.o_sh % 4 == 0 && al(a.q, 16) &&
+                  al(a.k, 16) && al(a.v, 16) && al(a.o, 8);
+  if (v2) {
+    const dim3 g2((a.N + kV2Rows - 1) / kV2Rows, a.H, a.B);
+    if (a.D <= 64) hipLaunchKernelGGL((flash2_fwd_kernel<DT, 64>), g2, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((flash2_fwd_kernel<DT, 128>), g2, dim3(256), 0, st, a);
+    return (int)hipGetLastError();
+  }
   const dim3 grid((a.N + kBM - 1) / kBM, a.H, a.B);
   const int dp = ((a.D + 31) / 32) * 32;
 #define CAKE_FL(P) \
@@ -243,6 +493,9 @@ static int launch_flash(const FlashArgs& a, hipStream_t st) {
 #undef CAKE_FL
   return (int)hipGetLastError();
 }
+
+// 1 = the 16-row 16x16x32 kernel, 2 = the 32x32x16 swapped-QKᵀ kernel (when shapes allow)
+CAKE_API void cake_flash_set_impl(int v) { g_flash_impl = v; }
 
 // strides in ELEMENTS: s[0]=batch, s[1]=head, s[2]=row for q, k, v, o (12 values)
 CAKE_API int cake_flash_attn(int dt, const void* q, const void* k, const void* v, void* o, int B,

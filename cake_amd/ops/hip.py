@@ -254,6 +254,11 @@ def set_gemv_tuning(kind: str, U: int = 4, prefetch: int = 0, max_blocks: int = 
 # MFMA flash attention + SD normalisation kernels
 # ---------------------------------------------------------------------------
 
+def flash_set_impl(v: int) -> None:
+    """1 = 16-row 16x16x32 kernel, 2 = 32x32x16 swapped-QKᵀ kernel (default where shapes allow)."""
+    kernels().cake_flash_set_impl(int(v))
+
+
 def flash_attn(q, k, v, out, scale: float, causal: bool = False, pos0: int = 0):
     """out = softmax(q kᵀ * scale [+causal mask]) v on MFMA.
 

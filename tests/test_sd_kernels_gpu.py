@@ -36,7 +36,8 @@ def _ref_attn(q, k, v, scale, causal, pos0):
     (1, 32, 8, 50, 150, 128, True, 100),         # chunked prefill (offset causal)
     (1, 12, 12, 77, 77, 64, True, 0),            # CLIP causal
 ])
-def test_flash_attn(cuda, dt, B, H, Hkv, N, M, D, causal, pos0):
+@pytest.mark.parametrize("impl", [1, 2])
+def test_flash_attn(cuda, dt, B, H, Hkv, N, M, D, causal, pos0, impl):
     from cake_amd.ops import hip as K
     torch.manual_seed(0)
     # projection-style layouts: [B, rows, heads, D] viewed as [B, heads, rows, D]
@@ -45,13 +46,19 @@ def test_flash_attn(cuda, dt, B, H, Hkv, N, M, D, causal, pos0):
     v = torch.randn(B, M, Hkv, D, device=cuda).to(dt).transpose(1, 2)
     out = torch.empty(B, N, H, D, device=cuda, dtype=dt).transpose(1, 2)
     scale = 1 / math.sqrt(D)
-    K.flash_attn(q, k, v, out, scale, causal, pos0)
+    K.flash_set_impl(impl)
+    try:
+        K.flash_attn(q, k, v, out, scale, causal, pos0)
+    finally:
+        K.flash_set_impl(2)
     torch.testing.assert_close(out.float(), _ref_attn(q, k, v, scale, causal, pos0), **_tol(dt))
 
 
-def test_flash_attn_softmax_rescale_branch(cuda):
+@pytest.mark.parametrize("impl", [1, 2])
+def test_flash_attn_softmax_rescale_branch(cuda, impl):
     """A late key tile with a much larger score forces the online-softmax rescale."""
     from cake_amd.ops import hip as K
+    K.flash_set_impl(impl)
     dt = torch.bfloat16
     q = torch.randn(1, 1, 64, 64, device=cuda).to(dt)
     k = torch.randn(1, 1, 256, 64, device=cuda)
@@ -60,6 +67,7 @@ def test_flash_attn_softmax_rescale_branch(cuda):
     v = torch.randn(1, 1, 256, 64, device=cuda).to(dt)
     out = torch.empty_like(q)
     K.flash_attn(q, k, v, out, 0.125)
+    K.flash_set_impl(2)
     torch.testing.assert_close(out.float(), _ref_attn(q, k, v, 0.125, False, 0), **_tol(dt))
 
 
