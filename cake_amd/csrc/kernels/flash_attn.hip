@@ -266,21 +266,35 @@ __device__ __forceinline__ uint32_t pack2(uint16_t lo, uint16_t hi) {
   return (uint32_t)lo | ((uint32_t)hi << 16);
 }
 
-constexpr int kV2Rows = 128, kVTS = 68;
+// two f32 -> packed 16-bit pair (RNE; hipcc emits v_cvt_pk_bf16_f32 on gfx950)
+template <int DT>
+__device__ __forceinline__ uint32_t cvt_pk(float lo, float hi) {
+  if constexpr (DT == kBF16) {
+    const __bf16 a = (__bf16)lo, b = (__bf16)hi;
+    return (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
+  } else {
+    const _Float16 a = (_Float16)lo, b = (_Float16)hi;
+    return (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
+  }
+}
 
-template <int DT, int DP>
-__global__ __launch_bounds__(256, 2) void flash2_fwd_kernel(FlashArgs a) {
+constexpr int kVTS = 68;
+
+template <int DT, int DP, int NW>
+__global__ __launch_bounds__(64 * NW, 2) void flash2_fwd_kernel(FlashArgs a) {
   constexpr int KS = DP / 16;   // QKᵀ k-steps
   constexpr int NCH = DP / 8;   // 16-byte chunks per K/V row
   constexpr int DTL = DP / 32;  // Oᵀ tiles
-  constexpr int NPR = NCH / 8;  // key pairs x chunks per thread per tile (32*NCH/256)
+  constexpr int NT = 64 * NW;   // threads
+  constexpr int NPR = 32 * NCH / NT;  // (key pair, chunk) items per thread per tile
+  static_assert(NPR * NT == 32 * NCH, "staging must divide evenly");
   __shared__ __attribute__((aligned(16))) uint16_t smem[2 * 64 * DP + 2 * DP * kVTS];
   uint16_t* const Kb = smem;
   uint16_t* const Vb = smem + 2 * 64 * DP;
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int l32 = lane & 31, h = lane >> 5;
-  const int mblk = blockIdx.x * kV2Rows;
+  const int mblk = blockIdx.x * (32 * NW);
   const int qrow = mblk + wave * 32 + l32;
   const int hq = blockIdx.y, b = blockIdx.z;
   const int hk = hq / (a.H / a.Hkv);
@@ -305,9 +319,10 @@ __global__ __launch_bounds__(256, 2) void flash2_fwd_kernel(FlashArgs a) {
     for (int r = 0; r < 16; ++r) o[t][r] = 0.f;
   float m = -INFINITY, l = 0.f;
   const int qpos = qrow + a.pos0;
+  const int qmin = mblk + wave * 32 + a.pos0;  // smallest query position of this wave
 
   int kend = a.M;
-  if (a.causal) kend = min(kend, a.pos0 + mblk + kV2Rows);
+  if (a.causal) kend = min(kend, a.pos0 + mblk + 32 * NW);
   const int ntiles = (kend + 63) / 64;
 
   // staging: pair pi -> keys 2*(pi / NCH) + {0,1}, chunk pi % NCH
@@ -315,7 +330,7 @@ __global__ __launch_bounds__(256, 2) void flash2_fwd_kernel(FlashArgs a) {
   auto gload = [&](int j) {
 #pragma unroll
     for (int i = 0; i < NPR; ++i) {
-      const int pi = tid + 256 * i, kp = pi / NCH, c = pi - kp * NCH;
+      const int pi = tid + NT * i, kp = pi / NCH, c = pi - kp * NCH;
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
         const int key = j * 64 + 2 * kp + e;
@@ -332,7 +347,7 @@ __global__ __launch_bounds__(256, 2) void flash2_fwd_kernel(FlashArgs a) {
     uint16_t* Vt = Vb + buf * DP * kVTS;
 #pragma unroll
     for (int i = 0; i < NPR; ++i) {
-      const int pi = tid + 256 * i, kp = pi / NCH, c = pi - kp * NCH;
+      const int pi = tid + NT * i, kp = pi / NCH, c = pi - kp * NCH;
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
         const int row = 2 * kp + e;
@@ -373,36 +388,42 @@ __global__ __launch_bounds__(256, 2) void flash2_fwd_kernel(FlashArgs a) {
       }
     }
 
-    // ---- mask + online softmax (exp2 domain); the row spans lanes l, l^32
+    // ---- online softmax; the row spans lanes l, l^32.  Scores stay raw (the
+    // scale is folded into one fma per exp2); masking only on boundary tiles.
+    const bool edge = j * 64 + 64 > a.M || (a.causal && j * 64 + 63 > qmin);
+    if (edge) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = j * 64 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h;
+          if (key >= a.M || (a.causal && key > qpos)) s[t][r] = -INFINITY;
+        }
+    }
     float mt = -INFINITY;
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = j * 64 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h;
-        float x = s[t][r] * a.scale_log2;
-        if (key >= a.M || (a.causal && key > qpos)) x = -INFINITY;
-        s[t][r] = x;
-        mt = fmaxf(mt, x);
-      }
+      for (int r = 0; r < 16; ++r) mt = fmaxf(mt, s[t][r]);
     mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-    const float mn = fmaxf(m, mt);
-    const float alpha = mn == -INFINITY ? 1.f : __builtin_amdgcn_exp2f(m - mn);
+    const float mn = fmaxf(m, mt);           // raw-score units
+    const float mc = mn == -INFINITY ? 0.f : mn * a.scale_log2;
+    const float alpha = __builtin_amdgcn_exp2f(m * a.scale_log2 - mc);  // m = -inf -> 0
     float rs = 0.f;
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float p = mn == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(s[t][r] - mn);
+        const float p = __builtin_amdgcn_exp2f(fmaf(s[t][r], a.scale_log2, -mc));
         s[t][r] = p;
         rs += p;
       }
     l = l * alpha + rs;
-    m = mn;
 #pragma unroll
     for (int t = 0; t < DTL; ++t)
 #pragma unroll
       for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
+    m = mn;
 
     // ---- Oᵀ += Vᵀ Pᵀ: k-step (t, s2) covers keys 32t + 16s2 + {8(j>>2) + 4h + (j&3)}
 #pragma unroll
@@ -410,10 +431,10 @@ __global__ __launch_bounds__(256, 2) void flash2_fwd_kernel(FlashArgs a) {
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
         uint4 pf;
-        pf.x = pack2(from_f32<DT>(s[t][8 * s2 + 0]), from_f32<DT>(s[t][8 * s2 + 1]));
-        pf.y = pack2(from_f32<DT>(s[t][8 * s2 + 2]), from_f32<DT>(s[t][8 * s2 + 3]));
-        pf.z = pack2(from_f32<DT>(s[t][8 * s2 + 4]), from_f32<DT>(s[t][8 * s2 + 5]));
-        pf.w = pack2(from_f32<DT>(s[t][8 * s2 + 6]), from_f32<DT>(s[t][8 * s2 + 7]));
+        pf.x = cvt_pk<DT>(s[t][8 * s2 + 0], s[t][8 * s2 + 1]);
+        pf.y = cvt_pk<DT>(s[t][8 * s2 + 2], s[t][8 * s2 + 3]);
+        pf.z = cvt_pk<DT>(s[t][8 * s2 + 4], s[t][8 * s2 + 5]);
+        pf.w = cvt_pk<DT>(s[t][8 * s2 + 6], s[t][8 * s2 + 7]);
         const int k0 = 32 * t + 16 * s2 + 4 * h;
 #pragma unroll
         for (int dt = 0; dt < DTL; ++dt) {
@@ -471,9 +492,19 @@ static int launch_flash(const FlashArgs& a, hipStream_t st) {
                   a.v_sh % 8 == 0 && a.o_sb % 4 == 0 && a.o_sh % 4 == 0 && al(a.q, 16) &&
                   al(a.k, 16) && al(a.v, 16) && al(a.o, 8);
   if (v2) {
-    const dim3 g2((a.N + kV2Rows - 1) / kV2Rows, a.H, a.B);
-    if (a.D <= 64) hipLaunchKernelGGL((flash2_fwd_kernel<DT, 64>), g2, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((flash2_fwd_kernel<DT, 128>), g2, dim3(256), 0, st, a);
+    // rows per workgroup: 128 (4 waves); smaller only for tiny grids (measured:
+    // 4-wave workgroups win even at 128 workgroups on 256 CUs)
+    int nw = 4;
+    const int nw_min = a.D <= 64 ? 1 : 2;  // DP=128 staging registers need >= 2 waves
+    while (nw > nw_min && (long long)((a.N + 32 * nw - 1) / (32 * nw)) * a.H * a.B < 32) nw >>= 1;
+    const dim3 g2((a.N + 32 * nw - 1) / (32 * nw), a.H, a.B);
+#define CAKE_FL2(P, W) hipLaunchKernelGGL((flash2_fwd_kernel<DT, P, W>), g2, dim3(64 * W), 0, st, a)
+    if (a.D <= 64) {
+      if (nw == 4) CAKE_FL2(64, 4); else if (nw == 2) CAKE_FL2(64, 2); else CAKE_FL2(64, 1);
+    } else {
+      if (nw == 4) CAKE_FL2(128, 4); else CAKE_FL2(128, 2);
+    }
+#undef CAKE_FL2
     return (int)hipGetLastError();
   }
   const dim3 grid((a.N + kBM - 1) / kBM, a.H, a.B);

@@ -35,6 +35,8 @@ def _ref_attn(q, k, v, scale, causal, pos0):
     (1, 32, 8, 77, 77, 128, True, 0),            # Llama prefill, GQA 4:1
     (1, 32, 8, 50, 150, 128, True, 100),         # chunked prefill (offset causal)
     (1, 12, 12, 77, 77, 64, True, 0),            # CLIP causal
+    (2, 16, 16, 4096, 256, 64, False, 0),        # large grid: 4-wave workgroups, DP 64
+    (1, 32, 8, 2048, 2048, 128, True, 0),        # large grid: 4-wave workgroups, DP 128
 ])
 @pytest.mark.parametrize("impl", [1, 2])
 def test_flash_attn(cuda, dt, B, H, Hkv, N, M, D, causal, pos0, impl):
