@@ -158,6 +158,79 @@ __global__ void geglu_kernel(const uint16_t* __restrict__ h, long long rows, int
   }
 }
 
+// LayerNorm, one wave per row, 16-byte accesses, the row held in registers
+// (exact two-pass mean / variance from one read).  C % 8 == 0, C <= 512*CPL.
+template <int DT, int CPL>
+__global__ __launch_bounds__(256) void layernorm_wave_kernel(const uint16_t* __restrict__ x,
+                                                             const uint16_t* __restrict__ gamma,
+                                                             const uint16_t* __restrict__ beta,
+                                                             long long rows, int C, float eps,
+                                                             uint16_t* __restrict__ y) {
+  const int lane = threadIdx.x & 63;
+  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int nch = C >> 3;
+  const uint16_t* xr = x + row * C;
+  float v[CPL][8];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nch) {
+      unpack8<DT>(*reinterpret_cast<const uint4*>(xr + c * 8), v[i]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += v[i][e];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[i][e] = 0.f;
+    }
+  }
+  const float mean = wave_sum(s) / (float)C;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < CPL; ++i)
+    if (lane + 64 * i < nch)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float d = v[i][e] - mean;
+        q += d * d;
+      }
+  const float rstd = rsqrtf(wave_sum(q) / (float)C + eps);
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) {
+    const int c = lane + 64 * i;
+    if (c >= nch) continue;
+    float g[8], b[8];
+    unpack8<DT>(*reinterpret_cast<const uint4*>(gamma + c * 8), g);
+    unpack8<DT>(*reinterpret_cast<const uint4*>(beta + c * 8), b);
+    uint16_t o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = from_f32<DT>((v[i][e] - mean) * rstd * g[e] + b[e]);
+    *reinterpret_cast<uint4*>(y + row * C + c * 8) = *reinterpret_cast<uint4*>(o);
+  }
+}
+
+// GEGLU with 16-byte accesses: F % 8 == 0
+template <int DT>
+__global__ __launch_bounds__(256) void geglu_vec_kernel(const uint16_t* __restrict__ h,
+                                                        long long rows, int F,
+                                                        uint16_t* __restrict__ out) {
+  const int fv = F >> 3;
+  const long long n = rows * fv;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long r = i / fv;
+    const int c = (int)(i - r * fv) * 8;
+    float a[8], g[8];
+    unpack8<DT>(*reinterpret_cast<const uint4*>(h + r * 2 * F + c), a);
+    unpack8<DT>(*reinterpret_cast<const uint4*>(h + r * 2 * F + F + c), g);
+    uint16_t o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = from_f32<DT>(a[e] * gelu_tanh(g[e]));
+    *reinterpret_cast<uint4*>(out + r * F + c) = *reinterpret_cast<uint4*>(o);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // GroupNorm on channels-last activations x [N, HW, C] (the layout the MFMA
 // convolutions and the transformer blocks share, so no NCHW<->NHWC copies).
@@ -323,6 +396,23 @@ CAKE_API int cake_groupnorm(int dt, const void* x, const void* gamma, const void
 CAKE_API int cake_layernorm(int dt, const void* x, const void* gamma, const void* beta,
                             long long rows, int C, float eps, void* y, hipStream_t st) {
   if (rows > 0x7fffffffLL) return (int)hipErrorInvalidValue;
+  const bool al = ((uintptr_t)x | (uintptr_t)y | (uintptr_t)gamma | (uintptr_t)beta) % 16 == 0;
+  if (C % 8 == 0 && C <= 2048 && al) {
+    const unsigned g = (unsigned)((rows + 3) / 4);
+    if (C <= 512)
+      DISPATCH_DT(dt, hipLaunchKernelGGL((layernorm_wave_kernel<DT, 1>), dim3(g), dim3(256), 0, st,
+                                         (const uint16_t*)x, (const uint16_t*)gamma,
+                                         (const uint16_t*)beta, rows, C, eps, (uint16_t*)y));
+    else if (C <= 1024)
+      DISPATCH_DT(dt, hipLaunchKernelGGL((layernorm_wave_kernel<DT, 2>), dim3(g), dim3(256), 0, st,
+                                         (const uint16_t*)x, (const uint16_t*)gamma,
+                                         (const uint16_t*)beta, rows, C, eps, (uint16_t*)y));
+    else
+      DISPATCH_DT(dt, hipLaunchKernelGGL((layernorm_wave_kernel<DT, 4>), dim3(g), dim3(256), 0, st,
+                                         (const uint16_t*)x, (const uint16_t*)gamma,
+                                         (const uint16_t*)beta, rows, C, eps, (uint16_t*)y));
+    return (int)hipGetLastError();
+  }
   DISPATCH_DT(dt, hipLaunchKernelGGL((layernorm_kernel<DT>), dim3((unsigned)rows), dim3(256), 0,
                                      st, (const uint16_t*)x, (const uint16_t*)gamma,
                                      (const uint16_t*)beta, C, eps, (uint16_t*)y));
@@ -330,6 +420,14 @@ CAKE_API int cake_layernorm(int dt, const void* x, const void* gamma, const void
 }
 
 CAKE_API int cake_geglu(int dt, const void* h, long long rows, int F, void* out, hipStream_t st) {
+  const bool al = ((uintptr_t)h | (uintptr_t)out) % 16 == 0;
+  if (F % 8 == 0 && al) {
+    const long long n = rows * (F / 8);
+    const long long g = std::min<long long>((n + 255) / 256, 16384);
+    DISPATCH_DT(dt, hipLaunchKernelGGL((geglu_vec_kernel<DT>), dim3((unsigned)g), dim3(256), 0, st,
+                                       (const uint16_t*)h, rows, F, (uint16_t*)out));
+    return (int)hipGetLastError();
+  }
   long long n = rows * F;
   long long g = (n + 255) / 256;
   if (g > 8192) g = 8192;
@@ -340,7 +438,10 @@ CAKE_API int cake_geglu(int dt, const void* h, long long rows, int F, void* out,
 
 // Channels-last GroupNorm.  part: N*S*G*2 f64 (S = cake_groupnorm_nhwc_splits),
 // tickets: N u32 zeroed once (re-armed by the kernel), stats: N*G*2 f32.
-CAKE_API int cake_groupnorm_nhwc_splits(int HW) { return HW < 64 ? HW : 64; }
+CAKE_API int cake_groupnorm_nhwc_splits(int HW) {
+  const int s = HW / 16;  // >= 16 pixels per workgroup, <= 256 partials per image
+  return s < 1 ? 1 : (s > 256 ? 256 : s);
+}
 
 CAKE_API int cake_groupnorm_nhwc(int dt, const void* x, const void* gamma, const void* beta, int N,
                                  int HW, int C, int G, float eps, int silu_act, double* part,

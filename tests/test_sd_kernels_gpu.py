@@ -91,18 +91,19 @@ def test_group_norm(cuda, dt, shape, G, silu):
 
 
 @pytest.mark.parametrize("dt", DTYPES)
-def test_layer_norm_and_geglu(cuda, dt):
+@pytest.mark.parametrize("C", [768, 320, 1280, 2048, 100])  # wave kernel (1/2/4 chunks), fallback
+def test_layer_norm_and_geglu(cuda, dt, C):
     from cake_amd.ops import hip as K
     torch.manual_seed(2)
-    x = torch.randn(2, 77, 768, device=cuda).to(dt)
-    g = (1 + 0.1 * torch.randn(768, device=cuda)).to(dt)
-    b = (0.1 * torch.randn(768, device=cuda)).to(dt)
+    x = (torch.randn(2, 77, C, device=cuda) * 2 + 3).to(dt)
+    g = (1 + 0.1 * torch.randn(C, device=cuda)).to(dt)
+    b = (0.1 * torch.randn(C, device=cuda)).to(dt)
     y = torch.empty_like(x)
     K.layer_norm(x, g, b, 1e-5, y)
-    ref = torch.nn.functional.layer_norm(x.float(), (768,), g.float(), b.float(), 1e-5)
+    ref = torch.nn.functional.layer_norm(x.float(), (C,), g.float(), b.float(), 1e-5)
     torch.testing.assert_close(y.float(), ref, **_tol(dt))
-    h = torch.randn(2, 50, 2 * 1280, device=cuda).to(dt)
-    o = torch.empty(2, 50, 1280, device=cuda, dtype=dt)
+    h = torch.randn(2, 50, 2 * C, device=cuda).to(dt)
+    o = torch.empty(2, 50, C, device=cuda, dtype=dt)
     K.geglu(h, o)
     a, gate = h.float().chunk(2, -1)
     torch.testing.assert_close(o.float(), a * torch.nn.functional.gelu(gate, approximate="tanh"),
