@@ -307,14 +307,29 @@ __global__ __launch_bounds__(512) void gn_nhwc_stats_kernel(const uint16_t* __re
   }
   __syncthreads();
   if (!last) return;
-  const double cnt = (double)HW * Cg;
-  for (int g = threadIdx.x; g < G; g += blockDim.x) {
+  // fold the S partials with every thread: (group, slice) lanes, then LDS
+  const int nthr = blockDim.x, lpg = nthr / G;
+  {
+    const int g = threadIdx.x % G, sl = threadIdx.x / G;
     double ts = 0.0, tq = 0.0;
-    for (int k = 0; k < S; ++k) {
-      const double* q = part + ((size_t)n * S + k) * G * 2;
-      ts += __builtin_nontemporal_load(q + 2 * g);
-      tq += __builtin_nontemporal_load(q + 2 * g + 1);
+    if (sl < lpg)
+      for (int k = sl; k < S; k += lpg) {
+        const double* q = part + ((size_t)n * S + k) * G * 2;
+        ts += __builtin_nontemporal_load(q + 2 * g);
+        tq += __builtin_nontemporal_load(q + 2 * g + 1);
+      }
+    red[threadIdx.x * 2] = ts;
+    red[threadIdx.x * 2 + 1] = tq;
+  }
+  __syncthreads();
+  if (threadIdx.x < G) {
+    const int g = threadIdx.x;
+    double ts = 0.0, tq = 0.0;
+    for (int sl = 0; sl < lpg; ++sl) {
+      ts += red[(sl * G + g) * 2];
+      tq += red[(sl * G + g) * 2 + 1];
     }
+    const double cnt = (double)HW * Cg;
     const double mean = ts / cnt;
     const double var = fmax(tq / cnt - mean * mean, 0.0);
     stats[((size_t)n * G + g) * 2] = (float)mean;
@@ -446,7 +461,7 @@ CAKE_API int cake_groupnorm_nhwc_splits(int HW) {
 CAKE_API int cake_groupnorm_nhwc(int dt, const void* x, const void* gamma, const void* beta, int N,
                                  int HW, int C, int G, float eps, int silu_act, double* part,
                                  unsigned int* tickets, float* stats, void* y, hipStream_t st) {
-  if (C % G || C % 8 || C > kGnMaxC || C / 8 > 512 || N <= 0 || HW <= 0 || (C / G) < 1)
+  if (C % G || C % 8 || C > kGnMaxC || C / 8 > 512 || N <= 0 || HW <= 0 || (C / G) < 1 || G > 256)
     return (int)hipErrorInvalidValue;
   // every 8-channel vector must span at most two groups
   if ((C / G) < 8 && 8 % (C / G)) return (int)hipErrorInvalidValue;

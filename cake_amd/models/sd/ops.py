@@ -120,11 +120,15 @@ def attention(q, k, v, heads: int, causal: bool = False, sliced: int | None = No
     scale = 1.0 / math.sqrt(D)
     if _hip(q) and D <= 256:
         from ...ops import hip as K
-        q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
-        out = torch.empty_like(q)
-        K.flash_attn(q.view(B, N, heads, D).transpose(1, 2), k.view(B, M, heads, D).transpose(1, 2),
-                     v.view(B, M, heads, D).transpose(1, 2), out.view(B, N, heads, D).transpose(1, 2),
-                     scale, causal)
+
+        def heads4(t, rows):  # [B, rows, C] (any row stride, unit channel stride) -> [B, h, rows, D]
+            if t.stride(-1) != 1 or t.data_ptr() % 16 or any(st % 8 for st in t.stride()[:2]):
+                t = t.contiguous()
+            return t.view(B, rows, heads, D).transpose(1, 2)
+
+        out = torch.empty(B, N, C, device=q.device, dtype=q.dtype)
+        K.flash_attn(heads4(q, N), heads4(k, M), heads4(v, M),
+                     out.view(B, N, heads, D).transpose(1, 2), scale, causal)
         return out
     qh = q.view(B, N, heads, D).transpose(1, 2).float()
     kh = k.view(B, M, heads, D).transpose(1, 2).float()

@@ -51,6 +51,18 @@ class SDUnit:
         else:
             self.model = ClipTextTransformer(cfg.clip if name == "clip" else cfg.clip2, weights)
         self.generator = torch.Generator(device="cpu")
+        self._ctx = None  # (text embedding, cross-attention k/v cache) of the current generation
+
+    def _kv_cache(self, emb: torch.Tensor) -> dict:
+        """Cross-attention k/v of a text embedding are reused while it does not change
+        (every step of one generation sends the same embedding)."""
+        if self._ctx is not None:
+            ref, cache = self._ctx
+            if ref.shape == emb.shape and ref.dtype == emb.dtype and torch.equal(ref, emb):
+                return cache
+        cache: dict = {}
+        self._ctx = (emb.clone(), cache)
+        return cache
 
     def layer_name(self) -> str:
         return self.name
@@ -65,8 +77,9 @@ class SDUnit:
         parts = unpack_tensors(x.to(self.device))
         if self.name == "unet":
             lat, emb, t = parts
-            return self.model.forward(self.w, lat.to(self.dtype), float(t.reshape(-1)[0]),
-                                      emb.to(self.dtype))
+            emb = emb.to(self.dtype)
+            return self.model.forward(self.w, lat.to(self.dtype), float(t.reshape(-1)[0]), emb,
+                                      kv_cache=self._kv_cache(emb))
         direction, inp = parts
         inp = inp.to(self.dtype)
         if float(direction.reshape(-1)[0]) == 1.0:

@@ -110,9 +110,29 @@ class Attention(Module):
             p.update(m.params())
         return p
 
-    def __call__(self, W, x, ctx=None):
-        c = x if ctx is None else ctx
-        a = ops.attention(self.q(W, x), self.k(W, c), self.v(W, c), self.heads, sliced=self.sliced)
+    def _fused(self, W, names):
+        key = f"{self.name}.{'+'.join(names)}@fused"
+        w = W.get(key)
+        if w is None:
+            w = W[key] = torch.cat([W[f"{self.name}.{n}.weight"] for n in names], 0)
+        return w
+
+    def __call__(self, W, x, ctx=None, kv_cache=None):
+        C = self.q.cout
+        if ctx is None:  # self-attention: one GEMM for q, k and v
+            qkv = ops.linear(x, self._fused(W, ("to_q", "to_k", "to_v")))
+            q, k, v = qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:]
+        else:
+            # cross-attention: k/v depend only on the text context, which is fixed
+            # for a whole generation -> computed once per context (kv_cache)
+            q = self.q(W, x)
+            kv = kv_cache.get(self.name) if kv_cache is not None else None
+            if kv is None:
+                kv = ops.linear(ctx, self._fused(W, ("to_k", "to_v")))
+                if kv_cache is not None:
+                    kv_cache[self.name] = kv
+            k, v = kv[..., :C], kv[..., C:]
+        a = ops.attention(q, k, v, self.heads, sliced=self.sliced)
         return self.o(W, a)
 
 
@@ -131,11 +151,11 @@ class BasicTransformerBlock(Module):
             p.update(m.params())
         return p
 
-    def __call__(self, W, x, ctx):
+    def __call__(self, W, x, ctx, kv_cache=None):
         n = self.name
         x = x + self.attn1(W, ops.layer_norm(x, W[f"{n}.norm1.weight"], W[f"{n}.norm1.bias"], 1e-5))
         x = x + self.attn2(W, ops.layer_norm(x, W[f"{n}.norm2.weight"], W[f"{n}.norm2.bias"], 1e-5),
-                           ctx)
+                           ctx, kv_cache)
         h = ops.layer_norm(x, W[f"{n}.norm3.weight"], W[f"{n}.norm3.bias"], 1e-5)
         return x + self.ff_out(W, ops.geglu(self.ff_in(W, h)))
 
@@ -157,14 +177,14 @@ class Transformer2DModel(Module):
             p.update(m.params())
         return p
 
-    def __call__(self, W, x, ctx):
+    def __call__(self, W, x, ctx, kv_cache=None):
         h = ops.group_norm(x, W[f"{self.name}.norm.weight"], W[f"{self.name}.norm.bias"],
                            self.groups, 1e-6)
         # proj_in / proj_out are per-pixel linears (1x1 convs in SD1.x): run them
         # on [B, HW, C] tokens, which is a free view in the channels-last layout
         h = _token_linear(W, self.proj_in.name, ops.tokens(h))
         for blk in self.blocks:
-            h = blk(W, h, ctx)
+            h = blk(W, h, ctx, kv_cache)
         h = _token_linear(W, self.proj_out.name, h)
         return ops.untokens(h, x) + x
 
@@ -248,7 +268,10 @@ class UNet2DConditionModel(Module):
             p.update(m.params())
         return p
 
-    def forward(self, W, sample: torch.Tensor, timestep: float, ctx: torch.Tensor) -> torch.Tensor:
+    def forward(self, W, sample: torch.Tensor, timestep: float, ctx: torch.Tensor,
+                kv_cache: dict | None = None) -> torch.Tensor:
+        """kv_cache: optional dict reused across the steps of ONE generation (fixed ctx);
+        holds the cross-attention k/v projections of the context."""
         cfg = self.cfg
         B = sample.shape[0]
         dt = sample.dtype
@@ -260,9 +283,9 @@ class UNet2DConditionModel(Module):
                                  cfg.freq_shift).to(dt)
         emb = self.t2(W, F.silu(self.t1(W, emb)))
         with ops.layout_nhwc(ops.want_nhwc(sample)):
-            return ops.to_external(self._body(W, ops.to_internal(sample), emb, ctx))
+            return ops.to_external(self._body(W, ops.to_internal(sample), emb, ctx, kv_cache))
 
-    def _body(self, W, sample, emb, ctx):
+    def _body(self, W, sample, emb, ctx, kv_cache):
         cfg = self.cfg
         x = self.conv_in(W, sample)
         skips = [x]
@@ -270,19 +293,19 @@ class UNet2DConditionModel(Module):
             for j, r in enumerate(res):
                 x = r(W, x, emb)
                 if att:
-                    x = att[j](W, x, ctx)
+                    x = att[j](W, x, ctx, kv_cache)
                 skips.append(x)
             if ds is not None:
                 x = ds(W, x)
                 skips.append(x)
         x = self.mid_res[0](W, x, emb)
-        x = self.mid_att(W, x, ctx)
+        x = self.mid_att(W, x, ctx, kv_cache)
         x = self.mid_res[1](W, x, emb)
         for res, att, us in self.up:
             for j, r in enumerate(res):
                 x = r(W, torch.cat([x, skips.pop()], ops.cdim()), emb)
                 if att:
-                    x = att[j](W, x, ctx)
+                    x = att[j](W, x, ctx, kv_cache)
             if us is not None:
                 x = us(W, x, up=True)  # nearest-2x upsample fused into the conv
         x = ops.group_norm(x, W["conv_norm_out.weight"], W["conv_norm_out.bias"],

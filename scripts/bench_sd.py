@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--dtype", default="f16")
     ap.add_argument("--graph", action="store_true", help="replay the UNet step as one hipGraph")
+    ap.add_argument("--no-kv-cache", dest="kv_cache", action="store_false",
+                    help="recompute the cross-attention k/v of the text context every step")
     a = ap.parse_args()
     dt = torch.float16 if a.dtype == "f16" else torch.bfloat16
     cfg = get_config(a.version)
@@ -32,15 +34,16 @@ def main():
     x = torch.randn(B, 4, cfg.height // 8, cfg.width // 8, device=dev, dtype=dt)
     ctx = torch.randn(B, 77, cfg.unet.cross_attention_dim, device=dev, dtype=dt)
     tbuf = torch.zeros((), device=dev)
+    kv = {} if a.kv_cache else None  # cross-attn k/v of the (fixed) text context, as the pipeline
     with torch.no_grad():
         for _ in range(2):  # warmup: conv autotuning, packed weights, workspaces
-            unet.forward(w, x, tbuf, ctx)
+            unet.forward(w, x, tbuf, ctx, kv)
         torch.cuda.synchronize()
-        step = lambda: unet.forward(w, x, tbuf, ctx)  # noqa: E731
+        step = lambda: unet.forward(w, x, tbuf, ctx, kv)  # noqa: E731
         if a.graph:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                unet.forward(w, x, tbuf, ctx)
+                unet.forward(w, x, tbuf, ctx, kv)
             step = g.replay
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -52,6 +55,7 @@ def main():
     print(json.dumps({"metric": "sd_unet_seconds_per_step", "version": a.version,
                       "resolution": f"{cfg.width}x{cfg.height}", "batch": B, "dtype": a.dtype,
                       "value": round(dt_step, 4), "unit": "s/step", "graph": a.graph,
+                      "ctx_kv_cache": a.kv_cache,
                       "nhwc": os.environ.get("CAKE_SD_NHWC", "1") != "0"}))
 
 

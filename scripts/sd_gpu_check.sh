@@ -10,6 +10,7 @@ if [[ $r -ne 0 ]]; then exit $r; fi
 for v in ${VERSIONS:-v1-5 xl}; do
   CAKE_SD_NHWC=0 timeout -k 10 300 python scripts/bench_sd.py --version $v --steps 10 >> gpurun_out/sd_steps.jsonl 2>>gpurun_out/sd_steps.err || exit 1
   timeout -k 10 300 python scripts/bench_sd.py --version $v --steps 10 >> gpurun_out/sd_steps.jsonl 2>>gpurun_out/sd_steps.err || exit 1
+  timeout -k 10 300 python scripts/bench_sd.py --version $v --steps 10 --graph --no-kv-cache >> gpurun_out/sd_steps.jsonl 2>>gpurun_out/sd_steps.err || exit 1
   timeout -k 10 300 python scripts/bench_sd.py --version $v --steps 10 --graph >> gpurun_out/sd_steps.jsonl 2>>gpurun_out/sd_steps.err || exit 1
 done
 cat gpurun_out/sd_steps.jsonl
