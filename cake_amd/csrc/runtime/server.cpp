@@ -143,11 +143,13 @@ void WorkerServer::handle(int fd, std::string peer, uint64_t session) {
         st_out += nb;
         stats_.bytes_out += nb;
         ++msgs;
-        if (drop_after_ && n_ops >= drop_after_) {
+        const uint64_t drop_after = drop_after_.load(std::memory_order_relaxed);
+        const int stats_every = stats_every_.load(std::memory_order_relaxed);
+        if (drop_after && n_ops >= drop_after) {
           log("fault injection: dropping connection after " + std::to_string(n_ops) + " ops");
           break;
         }
-        if (stats_every_ > 0 && msgs % stats_every_ == 0) {
+        if (stats_every > 0 && msgs % (uint64_t)stats_every == 0) {
           const double dt = std::chrono::duration<double>(clock::now() - st_t).count();
           char buf[256];
           std::snprintf(buf, sizeof buf, "%s | ops=%.1f/s read=%.1f KB/s write=%.1f KB/s",

@@ -45,12 +45,14 @@ class WorkerServer {
   WorkerServer(const std::string& host, int port, WorkerInfo info, std::string name);
   ~WorkerServer();
   int port() const { return port_; }
+  // callbacks: set before serve() (connection threads read them unsynchronised)
   void set_compute(ComputeFn f) { compute_ = std::move(f); }
   void set_reset(SessionFn f) { reset_ = std::move(f); }
   void set_drop(SessionFn f) { drop_ = std::move(f); }
   void set_log(LogFn f) { log_ = std::move(f); }
-  void set_drop_after(uint64_t n) { drop_after_ = n; }
-  void set_stats_every(int n) { stats_every_ = n; }
+  // knobs: safe to change while serving
+  void set_drop_after(uint64_t n) { drop_after_.store(n, std::memory_order_relaxed); }
+  void set_stats_every(int n) { stats_every_.store(n, std::memory_order_relaxed); }
   // blocking accept loop (returns after stop())
   void serve();
   void stop();
@@ -67,8 +69,8 @@ class WorkerServer {
   ComputeFn compute_;
   SessionFn reset_, drop_;
   LogFn log_;
-  uint64_t drop_after_ = 0;
-  int stats_every_ = 5;
+  std::atomic<uint64_t> drop_after_{0};
+  std::atomic<int> stats_every_{5};
   std::atomic<bool> stop_{false};
   std::atomic<uint64_t> next_session_{1};
   std::mutex threads_mu_;
