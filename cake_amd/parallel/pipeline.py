@@ -32,6 +32,19 @@ from ..models.llama3.config import LlamaConfig
 from ..models.llama3.weights import HeadWeights
 from ..ops import reference as R
 
+
+def init_process_group(backend: str, rank: int, world: int, device=None) -> None:
+    """torch.distributed init with a bounded collective timeout (CAKE_DIST_TIMEOUT s,
+    default 600) and asynchronous error handling, so a dead peer surfaces as an
+    error on the other ranks instead of a hang."""
+    import datetime
+    import os
+    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+    timeout = datetime.timedelta(seconds=float(os.environ.get("CAKE_DIST_TIMEOUT", "600")))
+    kw = {"device_id": device} if backend == "nccl" and device is not None else {}
+    dist.init_process_group(backend, rank=rank, world_size=world, timeout=timeout, **kw)
+
+
 HDR = 16          # int32 header words appended to each hop message
 H_POS, H_STREAM, H_T, H_FLAGS = 0, 1, 2, 3
 FLAG_RESET, FLAG_PREFILL, FLAG_STOP = 1, 2, 4

@@ -10,7 +10,7 @@ import torch.distributed as dist
 
 from ..models.llama3.config import preset
 from ..models.llama3.factory import parse_dtype, random_head, random_stack
-from .pipeline import PipelineEngine, head_cost_in_layers, shard_layers
+from .pipeline import PipelineEngine, head_cost_in_layers, init_process_group, shard_layers
 
 
 def bench_pipeline(a, emit) -> None:
@@ -22,9 +22,9 @@ def bench_pipeline(a, emit) -> None:
     dev = torch.device("cuda", local)
     backend = getattr(a, "dist_backend", "nccl")
     if backend == "nccl":
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        init_process_group("nccl", rank, world, dev)
     else:  # gloo: host-staged hops (lets N ranks share one GPU in tests)
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        init_process_group("gloo", rank, world)
     cfg = preset(a.model)
     dtype = parse_dtype(a.dtype)
     shards = shard_layers(cfg.num_hidden_layers, world, head_cost_in_layers(cfg))

@@ -21,7 +21,7 @@ import torch.distributed as dist
 from ..models.base import TextGenerator, Token
 from ..models.chat import History
 from ..models.sampling import LogitsProcessor
-from .pipeline import PipelineEngine
+from .pipeline import PipelineEngine, init_process_group
 
 log = logging.getLogger("cake.rccl")
 
@@ -105,9 +105,9 @@ def run_rccl(ctx) -> None:
         local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
         ctx.device = torch.device("cuda", local)
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=ctx.device)
+        init_process_group("nccl", rank, world, ctx.device)
     else:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        init_process_group("gloo", rank, world)
     try:
         cfg = LlamaConfig.from_path(ctx.model_path)
         owners = owners_from_topology(ctx.topology, cfg.num_hidden_layers, world)
