@@ -87,6 +87,7 @@ def bench_single(a) -> None:
     from cake_amd.models.llama3.decode_loop import run_decode
     from cake_amd.models.llama3.factory import parse_dtype, random_model
     from cake_amd.models.llama3.model import DeviceDecoder
+    from cake_amd.context import hbm_mib
 
     torch.cuda.set_device(0)
     dtype = parse_dtype(a.dtype)
@@ -118,7 +119,7 @@ def bench_single(a) -> None:
         with open(a.dump_tokens, "w") as f:
             json.dump([dec.bufs.hist[:int(dec.bufs.hist_len.item())].tolist()], f)
     _emit(a, a.steps / dt, dt * 1e3 / a.steps, st.percentile(50), st.percentile(99), 1,
-          {"ttft_ms_prefill": round(ttft, 3), "graph": not a.no_graph})
+          {"ttft_ms_prefill": round(ttft, 3), "graph": not a.no_graph, **hbm_mib()})
 
 
 def main(argv=None) -> int:

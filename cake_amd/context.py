@@ -68,6 +68,19 @@ class Context:
                    no_graph=getattr(args, "no_graph", False))
 
 
+def hbm_mib(device=None) -> dict:
+    """HBM of this rank's GPU: torch-allocated now / peak and device-wide used (MiB)."""
+    import torch
+    if not torch.cuda.is_available():
+        return {}
+    dev = torch.cuda.current_device() if device is None else device
+    free, total = torch.cuda.mem_get_info(dev)
+    return {"hbm_alloc_mib": round(torch.cuda.memory_allocated(dev) / 2**20, 1),
+            "hbm_peak_mib": round(torch.cuda.max_memory_allocated(dev) / 2**20, 1),
+            "hbm_used_mib": round((total - free) / 2**20, 1),
+            "hbm_total_mib": round(total / 2**20, 1)}
+
+
 def rss_mib() -> float:
     try:
         with open(f"/proc/{os.getpid()}/status") as f:

@@ -15,7 +15,7 @@ import time
 from pathlib import Path
 from typing import Callable
 
-from .context import Context, rss_mib
+from .context import Context, hbm_mib, rss_mib
 from .models.chat import Message
 
 log = logging.getLogger("cake.master")
@@ -105,7 +105,8 @@ class Master:
         if getattr(a, "metrics", None):
             import json
             with open(a.metrics, "a") as f:
-                f.write(json.dumps({"ts": time.time(), "kind": "text", **stats}) + "\n")
+                f.write(json.dumps({"ts": time.time(), "kind": "text", **stats,
+                                    "rss_mib": round(rss_mib(), 1), **hbm_mib()}) + "\n")
         if getattr(a, "trace", None) and times:
             from .utils.trace import ChromeTrace
             tr = ChromeTrace()

@@ -61,6 +61,9 @@ def bench_pipeline(a, emit) -> None:
     dt = torch.tensor([time.perf_counter() - t0], device=dev if backend == "nccl" else "cpu")
     dist.all_reduce(dt, op=dist.ReduceOp.MAX)
     dt = float(dt.item())
+    hbm = torch.tensor([torch.cuda.max_memory_allocated(dev) / 2**20],
+                       device=dev if backend == "nccl" else "cpu")
+    dist.all_reduce(hbm, op=dist.ReduceOp.MAX)
     if rank == 0 and getattr(a, "dump_tokens", None):
         import json
         with open(a.dump_tokens, "w") as f:
@@ -70,6 +73,7 @@ def bench_pipeline(a, emit) -> None:
         emit(a, streams * a.steps / dt, ms_round, ms_round, ms_round, world,
              {"streams": streams, "per_stream_tokens_per_sec": round(a.steps / dt, 3),
               "note": "per-token latency = decode round time (one token per stream per round)",
+              "hbm_peak_mib_max_rank": round(float(hbm.item()), 1),
               "scaling": "weak" if streams == world else "strong"})
     dist.barrier()
     dist.destroy_process_group()
