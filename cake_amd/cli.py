@@ -71,8 +71,9 @@ def build_parser() -> argparse.ArgumentParser:
     a("--sd-img2img-strength", type=float, default=0.8)
     a("--sd-seed", type=int, default=None)
     # MI355X-native extras
-    a("--transport", choices=["tcp", "rccl"], default="tcp",
-      help="rccl: torchrun one rank per GPU, rank 0 master, rank i serves topology node i")
+    a("--transport", choices=["tcp", "rccl", "loopback"], default="tcp",
+      help="rccl: torchrun one rank per GPU, rank 0 master, rank i serves topology node i; "
+           "loopback: every topology node served in-process (wire protocol over 127.0.0.1)")
     a("--max-seq-len", type=int, default=4096)
     a("--no-graph", action="store_true", help="disable hipGraph capture of the decode step")
     a("--trace", default=None, help="write a chrome-trace JSON of each text generation")
@@ -101,8 +102,17 @@ def main(argv: list[str] | None = None) -> int:
         from .parallel.worker import Worker
         Worker(ctx).run()
         return 0
+    workers = []
+    if args.transport == "loopback":
+        from .parallel.loopback import start_loopback_workers
+        workers = start_loopback_workers(ctx)
     from .master import Master
-    Master(ctx).run()
+    try:
+        Master(ctx).run()
+    finally:
+        if workers:
+            from .parallel.loopback import stop_loopback_workers
+            stop_loopback_workers(workers)
     return 0
 
 

@@ -117,3 +117,21 @@ def test_fault_injection_and_native_stats(ckpt, tmp_path, monkeypatch):
         assert st["ops"] == 2 and st["connections"] == 1 and st["bytes_in"] > 0
     finally:
         w.stop()
+
+
+def test_loopback_transport_matches_local(ckpt, tmp_path):
+    """--transport loopback: every topology node served in-process over the wire protocol
+    reproduces the all-local greedy stream."""
+    from cake_amd.parallel.loopback import start_loopback_workers, stop_loopback_workers
+    local = _generate(_ctx(ckpt, tmp_path / "none.yml"), ["hello"], n=8)
+    topo = tmp_path / "loop.yml"
+    topo.write_text("a:\n  host: 'unused:1'\n  layers:\n    - model.layers.0-1\n"
+                    "b:\n  host: 'unused:2'\n  layers:\n    - model.layers.3\n")
+    ctx = _ctx(ckpt, topo, "--transport", "loopback")
+    workers = start_loopback_workers(ctx)
+    try:
+        assert all(n.host.startswith("127.0.0.1:") for n in ctx.topology.nodes)
+        assert _generate(ctx, ["hello"], n=8) == local
+        assert sum(w.stats()["ops"] for w in workers) > 0
+    finally:
+        stop_loopback_workers(workers)
