@@ -59,7 +59,8 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const float* __restrict__ 
 // cache rows pos0+t of [nkv][S][hd].
 template <int DT>
 __global__ void rope_kv_kernel(uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
-                               const uint16_t* __restrict__ v, int nh, int nkv, int hd,
+                               const uint16_t* __restrict__ v, int ldq, int ld, int nh, int nkv,
+                               int hd,
                                const float* __restrict__ inv_freq, int pos0, int S,
                                uint16_t* __restrict__ kc, uint16_t* __restrict__ vc) {
   const int t = blockIdx.x, pos = pos0 + t, half = hd >> 1;
@@ -71,13 +72,13 @@ __global__ void rope_kv_kernel(uint16_t* __restrict__ q, const uint16_t* __restr
       const int head = pp / half, i = pp - head * half;
       float s, c;
       sincosf((float)pos * inv_freq[i], &s, &c);
-      const uint16_t* src = isq ? q + (size_t)t * nh * hd : k + (size_t)t * nkv * hd;
+      const uint16_t* src = isq ? q + (size_t)t * ldq : k + (size_t)t * ld;
       const float a = to_f32<DT>(src[head * hd + i]);
       const float b = to_f32<DT>(src[head * hd + i + half]);
       const uint16_t oa = from_f32<DT>(a * c - b * s), ob = from_f32<DT>(a * s + b * c);
       if (isq) {
-        q[(size_t)t * nh * hd + head * hd + i] = oa;
-        q[(size_t)t * nh * hd + head * hd + i + half] = ob;
+        q[(size_t)t * ldq + head * hd + i] = oa;
+        q[(size_t)t * ldq + head * hd + i + half] = ob;
       } else {
         const size_t off = ((size_t)head * S + pos) * hd + i;
         kc[off] = oa;
@@ -87,7 +88,7 @@ __global__ void rope_kv_kernel(uint16_t* __restrict__ q, const uint16_t* __restr
       const int pp = p - nq - nk;
       const int head = pp / half, i = pp - head * half;
       const size_t off = ((size_t)head * S + pos) * hd + i;
-      const uint16_t* src = v + (size_t)t * nkv * hd + head * hd;
+      const uint16_t* src = v + (size_t)t * ld + head * hd;
       vc[off] = src[i];
       vc[off + half] = src[i + half];
     }
@@ -101,6 +102,43 @@ __global__ void silu_mul_kernel(const uint16_t* __restrict__ g, const uint16_t* 
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (size_t)gridDim.x * blockDim.x)
     out[i] = from_f32<DT>(silu(to_f32<DT>(g[i])) * to_f32<DT>(u[i]));
+}
+
+// out[t][i] = silu(gu[t][i]) * gu[t][I + i]  (fused gate|up GEMM output), 8 per thread
+template <int DT>
+__global__ void silu_mul_rows_kernel(const uint16_t* __restrict__ gu, size_t T, int I,
+                                     uint16_t* __restrict__ out) {
+  const int iv = I >> 3;
+  const size_t n = T * iv;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const size_t t = i / iv;
+    const int c = (int)(i - t * iv) * 8;
+    float g[8], u[8];
+    unpack8<DT>(*reinterpret_cast<const uint4*>(gu + t * 2 * I + c), g);
+    unpack8<DT>(*reinterpret_cast<const uint4*>(gu + t * 2 * I + I + c), u);
+    uint16_t o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = from_f32<DT>(silu(g[e]) * u[e]);
+    *reinterpret_cast<uint4*>(out + t * I + c) = *reinterpret_cast<uint4*>(o);
+  }
+}
+
+// resid (f32) += y (16-bit), 8 per thread
+template <int DT>
+__global__ void add_resid8_kernel(float* __restrict__ resid, const uint16_t* __restrict__ y,
+                                  size_t n8) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8;
+       i += (size_t)gridDim.x * blockDim.x) {
+    float f[8];
+    unpack8<DT>(*reinterpret_cast<const uint4*>(y + i * 8), f);
+    float4* r = reinterpret_cast<float4*>(resid + i * 8);
+    float4 a = r[0], b = r[1];
+    a.x += f[0]; a.y += f[1]; a.z += f[2]; a.w += f[3];
+    b.x += f[4]; b.y += f[5]; b.z += f[6]; b.w += f[7];
+    r[0] = a;
+    r[1] = b;
+  }
 }
 
 // resid (f32) += y (16-bit)
@@ -144,11 +182,13 @@ CAKE_API int cake_rmsnorm(int dt, const float* x, const void* w, float eps, int 
   return (int)hipGetLastError();
 }
 
-CAKE_API int cake_rope_kv(int dt, void* q, const void* k, const void* v, int T, int nh,
+// q rows are `ldq` elements apart, k / v rows `ld` apart (separate tensors, or
+// column slices of one fused [T, (nh + 2 nkv) hd] projection output)
+CAKE_API int cake_rope_kv(int dt, void* q, const void* k, const void* v, int ldq, int ld, int T, int nh,
                           int nkv, int hd, const float* inv_freq, int pos0, int S, void* kc,
                           void* vc, hipStream_t st) {
   DISPATCH_DT(dt, hipLaunchKernelGGL((rope_kv_kernel<DT>), dim3(T), dim3(256), 0, st,
-                                     (uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, nh,
+                                     (uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, ldq, ld, nh,
                                      nkv, hd, inv_freq, pos0, S, (uint16_t*)kc,
                                      (uint16_t*)vc));
   return (int)hipGetLastError();
@@ -162,7 +202,21 @@ CAKE_API int cake_silu_mul(int dt, const void* g, const void* u, size_t n, void*
   return (int)hipGetLastError();
 }
 
+CAKE_API int cake_silu_mul_rows(int dt, const void* gu, size_t T, int I, void* out,
+                                hipStream_t st) {
+  if (I % 8 || ((uintptr_t)gu | (uintptr_t)out) % 16) return (int)hipErrorInvalidValue;
+  DISPATCH_DT(dt, hipLaunchKernelGGL((silu_mul_rows_kernel<DT>), dim3(ew_grid(T * I / 8)),
+                                     dim3(256), 0, st, (const uint16_t*)gu, T, I,
+                                     (uint16_t*)out));
+  return (int)hipGetLastError();
+}
+
 CAKE_API int cake_add_resid(int dt, float* resid, const void* y, size_t n, hipStream_t st) {
+  if (n % 8 == 0 && ((uintptr_t)resid % 32 == 0) && ((uintptr_t)y % 16 == 0)) {
+    DISPATCH_DT(dt, hipLaunchKernelGGL((add_resid8_kernel<DT>), dim3(ew_grid(n / 8)), dim3(256),
+                                       0, st, resid, (const uint16_t*)y, n / 8));
+    return (int)hipGetLastError();
+  }
   DISPATCH_DT(dt, hipLaunchKernelGGL((add_resid_kernel<DT>), dim3(ew_grid(n)), dim3(256), 0,
                                      st, resid, (const uint16_t*)y, n));
   return (int)hipGetLastError();

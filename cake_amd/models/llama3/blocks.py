@@ -205,21 +205,21 @@ class LayerStack:
         T, H = hidden.shape
         x = torch.empty((T, H), device=hidden.device, dtype=self.dtype)
         K.rmsnorm(hidden, w.ln1, cfg.rms_norm_eps, x)
-        q = torch.matmul(x, w.wq.t())
-        k = torch.matmul(x, w.wk.t())
-        v = torch.matmul(x, w.wv.t())
+        nh, nkv, hd = cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim
+        nq, nk = nh * hd, nkv * hd
+        qkv = torch.matmul(x, w.wqkv.t())  # one GEMM for q|k|v
+        q, k, v = qkv[:, :nq], qkv[:, nq:nq + nk], qkv[:, nq + nk:]
         K.rope_kv(q, k, v, self.inv_freq, pos0, kc, vc)
-        att = torch.empty_like(q)
-        nh, hd = cfg.num_attention_heads, cfg.head_dim
+        att = torch.empty((T, nq), device=hidden.device, dtype=self.dtype)
         Tk = pos0 + T
         K.flash_attn(q.view(1, T, nh, hd).transpose(1, 2), kc[None, :, :Tk], vc[None, :, :Tk],
                      att.view(1, T, nh, hd).transpose(1, 2), self.scale, causal=True, pos0=pos0)
         K.add_resid(hidden, torch.matmul(att, w.wo.t()))
         K.rmsnorm(hidden, w.ln2, cfg.rms_norm_eps, x)
-        g = torch.matmul(x, w.wg.t())
-        u = torch.matmul(x, w.wu.t())
-        K.silu_mul(g, u, g)
-        K.add_resid(hidden, torch.matmul(g, w.wd.t()))
+        gu = torch.matmul(x, w.wgu.t())  # one GEMM for gate|up
+        act = torch.empty((T, cfg.intermediate_size), device=hidden.device, dtype=self.dtype)
+        K.silu_mul_rows(gu, act)
+        K.add_resid(hidden, torch.matmul(act, w.wd.t()))
 
     # ------------------------------------------------------------------ torch path
     def _block_torch(self, hidden, w, kc, vc, pos0):

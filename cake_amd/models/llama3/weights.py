@@ -57,6 +57,16 @@ class BlockWeights:
     wu: torch.Tensor
     wd: torch.Tensor
 
+    def __post_init__(self):
+        # q|k|v and gate|up live in one allocation each: prefill runs ONE GEMM per
+        # group, and wq/wk/wv/wg/wu stay (contiguous row-slice) views for decode.
+        nq, nk, ni = self.wq.shape[0], self.wk.shape[0], self.wg.shape[0]
+        self.wqkv = torch.cat([self.wq, self.wk, self.wv], 0)
+        self.wq, self.wk, self.wv = (self.wqkv[:nq], self.wqkv[nq:nq + nk],
+                                     self.wqkv[nq + nk:])
+        self.wgu = torch.cat([self.wg, self.wu], 0)
+        self.wg, self.wu = self.wgu[:ni], self.wgu[ni:]
+
     @classmethod
     def load(cls, get: Getter, prefix: str, cfg: LlamaConfig, device, dtype) -> "BlockWeights":
         H, I, hd = cfg.hidden_size, cfg.intermediate_size, cfg.head_dim
@@ -91,7 +101,8 @@ class BlockWeights:
                    wo=lin(H, nh * hd), ln2=norm(), wg=lin(I, H), wu=lin(I, H), wd=lin(H, I))
 
     def state_dict(self, prefix: str) -> dict[str, torch.Tensor]:
-        return {f"{prefix}.{suffix}": getattr(self, key) for key, suffix in BLOCK_TENSORS}
+        # clones: the fused views share storage, which safetensors refuses to save
+        return {f"{prefix}.{suffix}": getattr(self, key).clone() for key, suffix in BLOCK_TENSORS}
 
 
 @dataclass

@@ -33,8 +33,9 @@ _SIGS = {
     "cake_attn_prefill": [I, P, P, P, I, I, I, I, I, I, F, P, P],
     "cake_embed": [I, P, P, I, I, P, P],
     "cake_rmsnorm": [I, P, P, F, I, I, P, P],
-    "cake_rope_kv": [I, P, P, P, I, I, I, I, P, I, I, P, P, P],
+    "cake_rope_kv": [I, P, P, P, I, I, I, I, I, I, P, I, I, P, P, P],
     "cake_silu_mul": [I, P, P, Z, P, P],
+    "cake_silu_mul_rows": [I, P, Z, I, P, P],
     "cake_add_resid": [I, P, P, Z, P],
     "cake_repeat_penalty": [P, P, P, I, F, P],
     "cake_argmax": [P, I, P, P],

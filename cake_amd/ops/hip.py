@@ -161,20 +161,33 @@ def rmsnorm(x, w, eps, out):
           "rmsnorm")
 
 
+def _rows(t: torch.Tensor, name: str, cols: int, T: int, dtype) -> int:
+    """Validate a [T, cols] row-strided view (unit column stride); return its row stride."""
+    if not t.is_cuda or t.dtype != dtype or t.dim() != 2 or tuple(t.shape) != (T, cols) \
+            or t.stride(1) != 1:
+        raise ValueError(f"{name}: expected a [{T}, {cols}] {dtype} device view with unit "
+                         f"column stride, got {tuple(t.shape)} {t.dtype} strides {t.stride()}")
+    return t.stride(0)
+
+
 def rope_kv(q, k, v, inv_freq, pos0: int, kcache, vcache):
-    """q [T, nh*hd] roped in place; k roped / v copied into cache rows pos0..pos0+T-1."""
+    """q [T, nh*hd] roped in place; k roped / v copied into cache rows pos0..pos0+T-1.
+
+    q, k, v may be column slices of one fused [T, (nh + 2 nkv) hd] projection
+    or separate contiguous tensors (k and v share a row stride)."""
     nkv, S, hd = kcache.shape
     T = q.shape[0]
     nh = q.shape[1] // hd
     if pos0 < 0 or pos0 + T > S:
         raise ValueError(f"positions {pos0}..{pos0 + T} exceed cache length {S}")
-    _req(q, "q", dtype=kcache.dtype)
-    _req(k, "k", dtype=kcache.dtype, shape=(T, nkv * hd))
-    _req(v, "v", dtype=kcache.dtype, shape=(T, nkv * hd))
+    ldq = _rows(q, "q", nh * hd, T, kcache.dtype)
+    ld = _rows(k, "k", nkv * hd, T, kcache.dtype)
+    if _rows(v, "v", nkv * hd, T, kcache.dtype) != ld and T > 1:
+        raise ValueError("rope_kv: k and v need the same row stride")
     _req(inv_freq, "inv_freq", dtype=torch.float32, shape=(hd // 2,))
     _req(kcache, "kcache")
     _req(vcache, "vcache", shape=kcache.shape)
-    check(kernels().cake_rope_kv(_dt(q), _p(q), _p(k), _p(v), T, nh, nkv, hd, _p(inv_freq),
+    check(kernels().cake_rope_kv(_dt(q), _p(q), _p(k), _p(v), ldq, ld, T, nh, nkv, hd, _p(inv_freq),
                                  int(pos0), S, _p(kcache), _p(vcache), _stream()), "rope_kv")
 
 
@@ -199,6 +212,15 @@ def silu_mul(g, u, out):
     _req(out, "out", dtype=g.dtype, shape=g.shape)
     check(kernels().cake_silu_mul(_dt(g), _p(g), _p(u), g.numel(), _p(out), _stream()),
           "silu_mul")
+
+
+def silu_mul_rows(gu, out):
+    """out [T, I] = silu(gu[:, :I]) * gu[:, I:]  (fused gate|up projection output)."""
+    T, I2 = gu.shape
+    _req(gu, "gu")
+    _req(out, "out", dtype=gu.dtype, shape=(T, I2 // 2))
+    check(kernels().cake_silu_mul_rows(_dt(gu), _p(gu), T, I2 // 2, _p(out), _stream()),
+          "silu_mul_rows")
 
 
 def add_resid(resid, y):

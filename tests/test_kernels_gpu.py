@@ -232,3 +232,31 @@ def test_attn_oproj_fused_matches_unfused(cuda, dt, nh, nkv, H):
         assert int(err) == 0 and int(ctl[1]) == nkv and int(tickets.abs().sum()) == 0
         torch.testing.assert_close(att.float(), ref_att.float())
         torch.testing.assert_close(out, ref, atol=2e-3, rtol=1e-3)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+def test_rope_kv_fused_qkv_and_silu_mul_rows(cuda, dt):
+    """Prefill layouts: q/k/v as column slices of one fused projection; gate|up fused."""
+    from cake_amd.ops import hip as K_
+    torch.manual_seed(9)
+    T, nh, nkv, hd, S, pos0 = 37, 32, 8, 128, 256, 11
+    qkv = _rand(T, (nh + 2 * nkv) * hd, dt=dt)
+    nq, nk = nh * hd, nkv * hd
+    q, k, v = qkv[:, :nq], qkv[:, nq:nq + nk], qkv[:, nq + nk:]
+    kc = torch.zeros(nkv, S, hd, device=cuda, dtype=dt)
+    vc = torch.zeros_like(kc)
+    invf = R.inv_freq(hd, 500000.0).to(cuda)
+    positions = torch.arange(pos0, pos0 + T, device=cuda)
+    qr = R.rope(q.reshape(T, nh, hd), positions, invf)
+    kr = R.rope(k.reshape(T, nkv, hd), positions, invf)
+    v_ref = v.clone()
+    K_.rope_kv(q, k, v, invf, pos0, kc, vc)
+    torch.testing.assert_close(q.float().reshape(T, nh, hd), qr, **_tol(dt))
+    torch.testing.assert_close(kc[:, pos0:pos0 + T].float().transpose(0, 1), kr, **_tol(dt))
+    torch.testing.assert_close(vc[:, pos0:pos0 + T].transpose(0, 1).reshape(T, -1), v_ref)
+    I = 1024
+    gu = _rand(T, 2 * I, dt=dt)
+    act = torch.empty(T, I, device=cuda, dtype=dt)
+    K_.silu_mul_rows(gu, act)
+    ref = torch.nn.functional.silu(gu[:, :I].float()) * gu[:, I:].float()
+    torch.testing.assert_close(act.float(), ref, **_tol(dt))
