@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import json
 import logging
+import os
 from pathlib import Path
 
 import torch
@@ -52,6 +53,9 @@ class SDUnit:
             self.model = ClipTextTransformer(cfg.clip if name == "clip" else cfg.clip2, weights)
         self.generator = torch.Generator(device="cpu")
         self._ctx = None  # (text embedding, cross-attention k/v cache) of the current generation
+        self._graphs: dict = {}  # UNet step hipGraphs per input shape
+        self.use_graph = (name == "unet" and torch.device(device).type == "cuda"
+                          and os.environ.get("CAKE_SD_GRAPH", "1") != "0")
 
     def _kv_cache(self, emb: torch.Tensor) -> dict:
         """Cross-attention k/v of a text embedding are reused while it does not change
@@ -63,6 +67,32 @@ class SDUnit:
         cache: dict = {}
         self._ctx = (emb.clone(), cache)
         return cache
+
+    def _unet_graph(self, lat: torch.Tensor, emb: torch.Tensor, t: float) -> torch.Tensor:
+        """One UNet step as a hipGraph replay (captured on first use of a shape after one
+        eager warm-up step that autotunes the convolutions).  The cross-attention
+        k/v cache is refreshed in place when the text embedding changes."""
+        from .unet import refresh_kv_cache
+        key = (tuple(lat.shape), tuple(emb.shape), lat.dtype)
+        st = self._graphs.get(key)
+        if st is None:
+            st = {"lat": lat.clone(), "emb": emb.clone(), "kv": {},
+                  "t": torch.full((), t, device=lat.device, dtype=torch.float32)}
+            self.model.forward(self.w, st["lat"], st["t"], st["emb"], kv_cache=st["kv"])
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                st["out"] = self.model.forward(self.w, st["lat"], st["t"], st["emb"],
+                                               kv_cache=st["kv"])
+            st["graph"] = g
+            self._graphs[key] = st
+        elif not torch.equal(st["emb"], emb):
+            st["emb"].copy_(emb)
+            refresh_kv_cache(st["kv"], st["emb"])
+        st["lat"].copy_(lat)
+        st["t"].fill_(t)
+        st["graph"].replay()
+        return st["out"].clone()
 
     def layer_name(self) -> str:
         return self.name
@@ -78,6 +108,8 @@ class SDUnit:
         if self.name == "unet":
             lat, emb, t = parts
             emb = emb.to(self.dtype)
+            if self.use_graph:
+                return self._unet_graph(lat.to(self.dtype), emb, float(t.reshape(-1)[0]))
             return self.model.forward(self.w, lat.to(self.dtype), float(t.reshape(-1)[0]), emb,
                                       kv_cache=self._kv_cache(emb))
         direction, inp = parts
@@ -96,6 +128,32 @@ class RemoteSDUnit:
 
     def __init__(self, client, name: str):
         self.client, self.name = client, name
+
+    def _unet_graph(self, lat: torch.Tensor, emb: torch.Tensor, t: float) -> torch.Tensor:
+        """One UNet step as a hipGraph replay (captured on first use of a shape after one
+        eager warm-up step that autotunes the convolutions).  The cross-attention
+        k/v cache is refreshed in place when the text embedding changes."""
+        from .unet import refresh_kv_cache
+        key = (tuple(lat.shape), tuple(emb.shape), lat.dtype)
+        st = self._graphs.get(key)
+        if st is None:
+            st = {"lat": lat.clone(), "emb": emb.clone(), "kv": {},
+                  "t": torch.full((), t, device=lat.device, dtype=torch.float32)}
+            self.model.forward(self.w, st["lat"], st["t"], st["emb"], kv_cache=st["kv"])
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                st["out"] = self.model.forward(self.w, st["lat"], st["t"], st["emb"],
+                                               kv_cache=st["kv"])
+            st["graph"] = g
+            self._graphs[key] = st
+        elif not torch.equal(st["emb"], emb):
+            st["emb"].copy_(emb)
+            refresh_kv_cache(st["kv"], st["emb"])
+        st["lat"].copy_(lat)
+        st["t"].fill_(t)
+        st["graph"].replay()
+        return st["out"].clone()
 
     def layer_name(self) -> str:
         return self.name

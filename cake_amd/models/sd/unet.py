@@ -128,9 +128,11 @@ class Attention(Module):
             q = self.q(W, x)
             kv = kv_cache.get(self.name) if kv_cache is not None else None
             if kv is None:
-                kv = ops.linear(ctx, self._fused(W, ("to_k", "to_v")))
+                wkv = self._fused(W, ("to_k", "to_v"))
+                kv = ops.linear(ctx, wkv)
                 if kv_cache is not None:
                     kv_cache[self.name] = kv
+                    kv_cache[f"{self.name}@w"] = wkv
             k, v = kv[..., :C], kv[..., C:]
         a = ops.attention(q, k, v, self.heads, sliced=self.sliced)
         return self.o(W, a)
@@ -187,6 +189,14 @@ class Transformer2DModel(Module):
             h = blk(W, h, ctx, kv_cache)
         h = _token_linear(W, self.proj_out.name, h)
         return ops.untokens(h, x) + x
+
+
+def refresh_kv_cache(kv_cache: dict, ctx: torch.Tensor) -> None:
+    """Recompute a cross-attention k/v cache IN PLACE for a new text context (the
+    tensors may be baked into a captured hipGraph)."""
+    for name, kv in kv_cache.items():
+        if not name.endswith("@w"):
+            torch.matmul(ctx, kv_cache[f"{name}@w"].t(), out=kv)
 
 
 def _token_linear(W, name, t):

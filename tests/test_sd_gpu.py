@@ -73,3 +73,30 @@ def test_unet_vae_channels_last_kernels_gpu_vs_cpu(cuda):
     g = torch.Generator().manual_seed(0)
     out = vae.encode({k: v.to(cuda, dt) for k, v in wv.items()}, img.to(cuda, dt), g)
     torch.testing.assert_close(out.float().cpu(), ref, atol=6e-2, rtol=6e-2)
+
+
+def test_unet_unit_graph_replay_matches_eager(cuda):
+    """SDUnit replays the UNet step as a hipGraph; a new text embedding refreshes the
+    cached cross-attention k/v in place; outputs equal the eager forward."""
+    import dataclasses
+    from cake_amd.models.sd.config import UNetBlock
+    from cake_amd.models.sd.shardable import SDUnit
+    from cake_amd.models.sd.util import pack_tensors
+    base = tiny_config("v1-5")
+    ucfg = dataclasses.replace(base.unet, blocks=[UNetBlock(64, True, 2), UNetBlock(128, False, 4)],
+                               cross_attention_dim=64, norm_num_groups=8)
+    cfg = dataclasses.replace(base, unet=ucfg)
+    dt = torch.bfloat16
+    w = {k: v.to(cuda, dt) for k, v in random_component("unet", cfg, "cpu", torch.float32).items()}
+    unit = SDUnit("unet", cfg, w, cuda, dt)
+    assert unit.use_graph
+    lat = torch.randn(2, 4, 16, 16, device=cuda).to(dt)
+    e1 = torch.randn(2, 77, 64, device=cuda).to(dt)
+    e2 = torch.randn(2, 77, 64, device=cuda).to(dt)
+    eager = UNet2DConditionModel(cfg.unet)
+    for emb, t in ((e1, 500.0), (e1, 300.0), (e2, 500.0), (e1, 100.0)):
+        got = unit.forward(pack_tensors([lat, emb, torch.tensor([t], device=cuda)], cuda))
+        with torch.no_grad():
+            ref = eager.forward(w, lat, t, emb)
+        torch.testing.assert_close(got.float(), ref.float(), atol=3e-2, rtol=3e-2)
+    assert len(unit._graphs) == 1
