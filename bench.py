@@ -44,6 +44,9 @@ def _args(argv=None):
     ap.add_argument("--repeat-penalty", type=float, default=1.1)
     ap.add_argument("--repeat-last-n", type=int, default=128)
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--steps-per-graph", type=int, default=1,
+                    help="greedy decode steps captured per graph launch (per-token latency "
+                         "is then measured at that granularity)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="N>1 transport: nccl (= RCCL over xGMI) or host-staged gloo (tests)")
     ap.add_argument("--dump-tokens", default=None, help="write generated token ids (JSON)")
@@ -98,7 +101,7 @@ def bench_single(a) -> None:
     print(f"[bench] model {a.model} random-init in {load_s:.1f}s, "
           f"HBM {torch.cuda.memory_allocated() / 2**30:.1f} GiB", file=sys.stderr, flush=True)
     dec = DeviceDecoder(model, repeat_penalty=a.repeat_penalty, repeat_last_n=a.repeat_last_n,
-                        greedy=True, use_graph=not a.no_graph)
+                        greedy=True, use_graph=not a.no_graph, steps_per_graph=a.steps_per_graph)
     g = torch.Generator().manual_seed(1234)
     prompt = torch.randint(0, model.cfg.vocab_size, (a.prompt_len,), generator=g).tolist()
     dec.start(prompt)  # cold: first-call library/module setup
@@ -119,7 +122,8 @@ def bench_single(a) -> None:
         with open(a.dump_tokens, "w") as f:
             json.dump([dec.bufs.hist[:int(dec.bufs.hist_len.item())].tolist()], f)
     _emit(a, a.steps / dt, dt * 1e3 / a.steps, st.percentile(50), st.percentile(99), 1,
-          {"ttft_ms_prefill": round(ttft, 3), "graph": not a.no_graph, **hbm_mib()})
+          {"ttft_ms_prefill": round(ttft, 3), "graph": not a.no_graph,
+           "steps_per_graph": dec.k, **hbm_mib()})
 
 
 def main(argv=None) -> int:

@@ -62,41 +62,48 @@ def run_decode(dec: DeviceDecoder, n_steps: int, eos_ids: set[int] | None = None
         st.wall_s = time.perf_counter() - t0
         return st
 
-    ring = torch.empty(2, dtype=torch.int32, pin_memory=True)
-    evs = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    # greedy: every launch runs dec.k steps; their tokens are the next k entries of
+    # the device history, copied to a pinned ring one launch behind
+    k = dec.k
+    base = int(dec.bufs.hist_len.item())
+    ring = torch.empty(2 * k, dtype=torch.int32, pin_memory=True)
     start_ev = torch.cuda.Event(enable_timing=True)
     start_ev.record()
     prev_done = start_ev
     t0 = time.perf_counter()
-    pending = None  # (slot, event)
+    pending = None  # (slot, event, n_tokens)
     issued = 0
     stop = False
     while not stop:
         cur = None
-        if issued < n_steps:
-            slot = issued & 1
+        if issued < n_steps and base + issued + k <= dec.bufs.hist.numel():
+            slot = (issued // k) & 1
             dec.launch()
-            ring[slot:slot + 1].copy_(dec.bufs.tok, non_blocking=True)
+            lo = base + issued
+            ring[slot * k:slot * k + k].copy_(dec.bufs.hist[lo:lo + k], non_blocking=True)
             ev = torch.cuda.Event(enable_timing=True)
             ev.record()
-            cur = (slot, ev)
-            issued += 1
+            cur = (slot, ev, min(k, n_steps - issued))
+            issued += k
         if pending is not None:
-            slot, ev = pending
+            slot, ev, n = pending
             ev.synchronize()
-            st.step_ms.append(prev_done.elapsed_time(ev))
+            dt = prev_done.elapsed_time(ev) / k  # device time per token of this launch
             prev_done = ev
-            tok = int(ring[slot].item())
-            st.tokens.append(tok)
-            if on_token:
-                on_token(tok)
-            if eos_ids and tok in eos_ids:
-                stop = True
+            for i in range(n):
+                tok = int(ring[slot * k + i].item())
+                st.step_ms.append(dt)
+                st.tokens.append(tok)
+                if on_token:
+                    on_token(tok)
+                if eos_ids and tok in eos_ids:
+                    stop = True
+                    break
         pending = cur
         if pending is None:
             stop = True
     if pending is not None:
         pending[1].synchronize()
     st.wall_s = time.perf_counter() - t0
-    del dev, evs
+    del dev
     return st

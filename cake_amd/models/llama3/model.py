@@ -134,9 +134,12 @@ class DeviceDecoder:
     """
 
     def __init__(self, model: LlamaModel, repeat_penalty: float = 1.0, repeat_last_n: int = 128,
-                 greedy: bool = True, use_graph: bool = True):
+                 greedy: bool = True, use_graph: bool = True, steps_per_graph: int = 1):
         if model.backend != "hip" or not model.all_local:
             raise ValueError("DeviceDecoder needs an all-local model on the hip backend")
+        # greedy decode needs no host input between steps, so several steps can
+        # share one graph launch (fewer host round trips); sampled mode is 1
+        self.k = max(1, int(steps_per_graph)) if greedy and use_graph else 1
         self.m = model
         self.penalty = float(repeat_penalty)
         self.last_n = int(repeat_last_n)
@@ -177,7 +180,8 @@ class DeviceDecoder:
         self.bufs.slot.zero_()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            self._step_body()
+            for _ in range(self.k):
+                self._step_body()
         self.graph = g
         torch.cuda.synchronize()
 
@@ -216,7 +220,7 @@ class DeviceDecoder:
         K.push_token(src, b.tok, b.hist, b.hist_len, b.pos)
 
     def launch(self) -> None:
-        """Enqueue one decode step (async)."""
+        """Enqueue `self.k` decode steps (one graph replay; async)."""
         if self.graph is not None:
             self.graph.replay()
         else:

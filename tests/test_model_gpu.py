@@ -36,7 +36,8 @@ def test_prefill_and_decode_logits_match_reference(cuda, dt, name):
 
 
 @pytest.mark.parametrize("use_graph", [False, True])
-def test_device_decoder_matches_host_loop(cuda, use_graph):
+@pytest.mark.parametrize("k", [1, 4])
+def test_device_decoder_matches_host_loop(cuda, use_graph, k):
     from cake_amd.models.llama3.decode_loop import run_decode
     from cake_amd.models.llama3.model import DeviceDecoder
     from cake_amd.ops import reference as R
@@ -56,10 +57,10 @@ def test_device_decoder_matches_host_loop(cuda, use_graph):
         toks.append(t)
         logits = model.forward([t], len(toks) - 1)
     dec = DeviceDecoder(model, repeat_penalty=1.1, repeat_last_n=16, greedy=True,
-                        use_graph=use_graph)
+                        use_graph=use_graph, steps_per_graph=k)
     first = dec.start(prompt)
     dec.capture()
-    st = run_decode(dec, 11)
+    st = run_decode(dec, 11)  # 11 is not a multiple of k: the last launch overshoots
     assert [first] + st.tokens == host
     assert len(st.step_ms) == 11 and all(x > 0 for x in st.step_ms)
 
