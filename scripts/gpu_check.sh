@@ -8,7 +8,7 @@ export HSA_ENABLE_IPC_MODE_LEGACY=0
 STEPS=${STEPS:-tests,bench,prof}
 rc=0
 if [[ $STEPS == *tests* ]]; then
-  timeout -k 10 ${TEST_TIMEOUT:-420} python -m pytest ${TESTS:-tests} -x -q -m gpu > gpurun_out/pytest.log 2>&1
+  timeout -k 10 ${TEST_TIMEOUT:-420} python -u -m pytest ${TESTS:-tests} -x -v -m gpu --timeout 120 --timeout-method thread > gpurun_out/pytest.log 2>&1
   rc=$?
   tail -5 gpurun_out/pytest.log
   if [[ $rc -ne 0 && $rc -ne 1 ]]; then echo "pytest rc=$rc -> stop"; exit $rc; fi
