@@ -69,6 +69,83 @@ class DecodeBuffers:
             self.slot = torch.zeros(1, device=device, dtype=torch.int64)
 
 
+class MegaPlan:
+    """Persistent decode megakernel (decode_mega.hip) over a run of local layers.
+
+    Holds the device layer table (weight + KV pointers of one session) and the
+    megakernel's exchange buffers.  One launch runs every layer of the run
+    (and, for the master's all-local case, ln_f + lm_head into the logits).
+    """
+
+    def __init__(self, stack: "LayerStack", layers: list[int]):
+        from ...ops import hip as K
+        cfg = stack.cfg
+        self.stack = stack
+        self.layers = list(layers)
+        self.grid = K.mega_grid()
+        nh, nkv, hd, H = (cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim,
+                          cfg.hidden_size)
+        self.KS = K.mega_ks(H, nh, nkv, hd, self.grid)
+        dev = stack.device
+        self.ws = K.mega_workspace(H, cfg.intermediate_size, nh, nkv, hd, self.KS, dev)
+        self.launch_ctr = torch.ones(1, device=dev, dtype=torch.int32)
+        self.err = torch.zeros(1, device=dev, dtype=torch.int32)
+        self._table = None
+        self._table_key = None
+        self.trace = None  # set to an int64 [4 * (5L + 1)] tensor to record phase timestamps
+
+    @staticmethod
+    def supported(cfg: LlamaConfig) -> bool:
+        from ...ops import hip as K
+        return K.mega_supported(cfg.hidden_size, cfg.intermediate_size, cfg.num_attention_heads,
+                                cfg.num_key_value_heads, cfg.head_dim, cfg.vocab_size)
+
+    def table(self, session: int) -> torch.Tensor:
+        kv = self.stack.cache(session)
+        key = (id(kv), kv.k.data_ptr())
+        if self._table is None or self._table_key != key:
+            rows = []
+            for li in self.layers:
+                w = self.stack.weights[li]
+                s = self.stack.slot_of[li]
+                rows.append([w.ln1.data_ptr(), w.wqkv.data_ptr(), w.wo.data_ptr(),
+                             w.ln2.data_ptr(), w.wg.data_ptr(), w.wu.data_ptr(),
+                             w.wd.data_ptr(), kv.k[s].data_ptr(), kv.v[s].data_ptr()])
+            self._table = torch.tensor(rows, dtype=torch.int64).to(self.stack.device)
+            self._table_key = key
+        return self._table
+
+    def launch(self, bufs: "DecodeBuffers", session: int = 0, head=None, logits=None) -> None:
+        """Run the layers on bufs.resid at device position bufs.pos (graph-capturable).
+
+        head = (norm_f, lm_head): also ln_f + lm_head into `logits` (bufs.resid is then
+        left unchanged: the final hidden state only exists on chip).
+        """
+        from ...ops import hip as K
+        cfg, st = self.stack.cfg, self.stack
+        tab = self.table(session)
+        K.decode_mega(tab, len(self.layers),
+                      (cfg.hidden_size, cfg.intermediate_size, cfg.num_attention_heads,
+                       cfg.num_key_value_heads, cfg.head_dim),
+                      st.max_seq, self.KS, cfg.rms_norm_eps, st.scale, st.inv_freq, bufs.pos,
+                      bufs.resid, self.ws, bufs.part, self.launch_ctr, self.err,
+                      st.dtype, norm_f=None if head is None else head[0],
+                      lm_head=None if head is None else head[1], logits=logits,
+                      grid=self.grid, trace=self.trace)
+
+    def check(self) -> None:
+        if int(self.err.item()) != 0:
+            raise RuntimeError("decode megakernel: grid barrier timed out (not all workgroups "
+                               "co-resident?); set CAKE_MEGA=0")
+
+
+def mega_enabled() -> bool:
+    """Opt-in (CAKE_MEGA=1): measured slower than the multi-kernel hipGraph on MI355X
+    (8B: 257 vs 331 tok/s, profiles/r1_mega_decode_trace.json) — see decode_mega.hip."""
+    import os
+    return os.environ.get("CAKE_MEGA", "0") == "1"
+
+
 class LayerStack:
     def __init__(self, cfg: LlamaConfig, weights: dict[int, BlockWeights], device, dtype,
                  max_seq: int, backend: str, max_sessions: int = 8):

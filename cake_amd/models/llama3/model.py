@@ -19,7 +19,7 @@ from dataclasses import dataclass, field
 import torch
 
 from ...ops import reference as R
-from .blocks import DecodeBuffers, LayerStack
+from .blocks import DecodeBuffers, LayerStack, MegaPlan, mega_enabled
 from .config import LlamaConfig
 from .weights import HeadWeights, layer_name
 
@@ -148,14 +148,21 @@ class DeviceDecoder:
         self.bufs: DecodeBuffers = model.stack.decode_buffers(with_head=True)
         self.graph: torch.cuda.CUDAGraph | None = None
         self._layers = list(range(model.cfg.num_hidden_layers))
+        # the whole step's layers + lm_head as ONE persistent launch (decode_mega.hip)
+        self.mega: MegaPlan | None = None
+        if mega_enabled() and MegaPlan.supported(model.cfg):
+            self.mega = MegaPlan(model.stack, self._layers)
 
     # the captured body
     def _step_body(self) -> None:
         from ...ops import hip as K
         b, m = self.bufs, self.m
         K.embed(m.head.embed, b.tok, b.resid)
-        m.stack.decode_step(b, self._layers, m.session)
-        K.norm_gemv_f32(b.resid, m.head.norm, m.cfg.rms_norm_eps, m.head.lm_head, b.logits)
+        if self.mega is not None:
+            self.mega.launch(b, m.session, head=(m.head.norm, m.head.lm_head), logits=b.logits)
+        else:
+            m.stack.decode_step(b, self._layers, m.session)
+            K.norm_gemv_f32(b.resid, m.head.norm, m.cfg.rms_norm_eps, m.head.lm_head, b.logits)
         if self.penalty != 1.0:
             K.repeat_penalty(b.logits, b.hist, b.hist_len, self.last_n, self.penalty)
         if self.greedy:
@@ -174,6 +181,8 @@ class DeviceDecoder:
             self._step_body()
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
+        if self.mega is not None:
+            self.mega.check()
         for t, v in zip((self.bufs.tok, self.bufs.pos, self.bufs.hist_len), saved):
             t.copy_(v)
         self.bufs.hist.copy_(hist)

@@ -101,3 +101,11 @@ _SIGS.update({
 _SIGS.update({
     "cake_attn_oproj": [I, P, P, P, P, I, I, I, I, F, P, P, P, P, P, I, P, P, I, I, I, P],
 })
+
+_SIGS.update({
+    "cake_mega_grid": [],
+    "cake_mega_supported": [I, I, I, I, I, I],
+    "cake_mega_ks": [I, I, I, I, I],
+    "cake_decode_mega": [I, P, I, I, I, I, I, I, I, I, F, F, P, P, P, P, P, P, P, P, P, P, P,
+                         P, P, P, I, P, I, C.c_double, P, P],
+})

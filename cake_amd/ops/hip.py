@@ -508,3 +508,77 @@ def attn_oproj(q, kcache, vcache, pos, scale, part, tickets, ctl, attn_out, wo, 
                                     _p(attn_out), _p(wo), N, _p(resid), _p(err), int(grid),
                                     int(prefetch), int(sleep), _stream()),
           "attn_oproj")
+
+
+# ---------------------------------------------------------------------------
+# persistent decode megakernel (decode_mega.hip)
+# ---------------------------------------------------------------------------
+
+def mega_supported(H: int, I: int, nh: int, nkv: int, hd: int, V: int = 2) -> bool:
+    return bool(kernels().cake_mega_supported(H, I, nh, nkv, hd, V))
+
+
+def mega_grid() -> int:
+    """Workgroups of one launch = CUs of the current device (one per CU)."""
+    return int(kernels().cake_mega_grid())
+
+
+def mega_ks(H: int, nh: int, nkv: int, hd: int, grid: int = 0) -> int:
+    return int(kernels().cake_mega_ks(H, nh, nkv, hd, grid))
+
+
+def decode_mega(layer_table, L: int, cfg_dims: tuple, S: int, KS: int, eps: float, scale: float,
+                inv_freq, pos, resid, ws: dict, attn_part, launch_ctr, err, dtype,
+                norm_f=None, lm_head=None, logits=None, grid: int = 0, timeout_s: float = 0.25,
+                trace=None):
+    """All `L` decode layers (+ optional ln_f/lm_head -> logits) in one launch.
+
+    layer_table: int64 device tensor [L, 9] of pointers (ln1, wqkv, wo, ln2, wg, wu, wd,
+    kcache, vcache).  ws: the tagged exchange buffers (see :func:`mega_workspace`).
+    launch_ctr (int32 [1]) is advanced by the kernel; err (int32 [1]) is set to 1 if a
+    dependency wait timed out (the launch then exits without hanging).
+    """
+    H, I, nh, nkv, hd = cfg_dims
+    nq, nk = nh * hd, nkv * hd
+    f32, i32 = torch.float32, torch.int32
+    _req(layer_table, "layer_table", dtype=torch.int64, shape=(L, 9))
+    _req(inv_freq, "inv_freq", dtype=f32, shape=(hd // 2,))
+    _req(pos, "pos", dtype=i32, numel=1)
+    _req(resid, "resid", dtype=f32, numel=H)
+    _req(ws["yo"], "yo_t", dtype=torch.int64, numel=H)
+    _req(ws["yd"], "yd_t", dtype=torch.int64, numel=H)
+    _req(ws["qkv"], "qkv_t", dtype=torch.int64, numel=KS * (nq + 2 * nk))
+    _req(ws["attn"], "attn_t", dtype=i32, numel=nq)
+    _req(ws["act"], "act_t", dtype=i32, numel=I)
+    _req(attn_part, "attn_part", dtype=f32, numel=nh * ((S + 63) // 64) * (hd + 2))
+    _req(ws["tickets"], "tickets", dtype=i32, numel=nh)
+    _req(launch_ctr, "launch_ctr", dtype=i32, numel=1)
+    _req(err, "err", dtype=i32, numel=1)
+    V = 0
+    if lm_head is not None:
+        V = lm_head.shape[0]
+        _req(lm_head, "lm_head", dtype=dtype, shape=(V, H))
+        _req(norm_f, "norm_f", dtype=dtype, shape=(H,))
+        _req(logits, "logits", dtype=f32, numel=V)
+    if trace is not None:
+        _req(trace, "trace", dtype=torch.int64, numel=8 * (5 * L + 1) * (grid or mega_grid()))
+    if not mega_supported(H, I, nh, nkv, hd, V if V else 2):
+        raise ValueError(f"decode_mega: unsupported shape H={H} I={I} nh={nh} nkv={nkv} hd={hd}")
+    check(kernels().cake_decode_mega(
+        _DT[dtype], _p(layer_table), L, H, I, nh, nkv, hd, S, KS, float(eps), float(scale),
+        _p(inv_freq), _p(pos), _p(resid), _p(ws["yo"]), _p(ws["yd"]), _p(ws["qkv"]),
+        _p(ws["attn"]), _p(ws["act"]), _p(attn_part), _p(ws["tickets"]), _p(launch_ctr), _p(err),
+        _p(norm_f), _p(lm_head), V, _p(logits), int(grid), float(timeout_s), _p(trace),
+        _stream()), "decode_mega")
+
+
+def mega_workspace(H: int, I: int, nh: int, nkv: int, hd: int, KS: int, device) -> dict:
+    """Tagged exchange buffers of the megakernel (zero = no valid tag)."""
+    i64, i32 = torch.int64, torch.int32
+    R = (nh + 2 * nkv) * hd
+    return {"yo": torch.zeros(H, dtype=i64, device=device),
+            "yd": torch.zeros(H, dtype=i64, device=device),
+            "qkv": torch.zeros(KS * R, dtype=i64, device=device),
+            "attn": torch.zeros(nh * hd, dtype=i32, device=device),
+            "act": torch.zeros(I, dtype=i32, device=device),
+            "tickets": torch.zeros(nh, dtype=i32, device=device)}
