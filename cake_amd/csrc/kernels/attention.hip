@@ -26,6 +26,32 @@ namespace cake {
 
 constexpr int kKeysPerSplit = 64;
 
+// Decode attention moves a few hundred KB while HBM sits idle for ~5 us; extra
+// workgroups appended to its grid (blockIdx.y >= nsplit) read the o_proj
+// weights that the next launch needs, with ordinary (allocating) loads, so they
+// land in the memory-side Infinity Cache (MALL, 256 MB) and the GEMV reads them
+// from there.  Read-only: the loaded words are folded into a register that an
+// empty volatile asm consumes, which keeps the loads alive without any store.
+template <int NT>
+__device__ __forceinline__ void prefetch_blocks(const uint4* __restrict__ p, size_t nchunks,
+                                                int b, int nb) {
+  const size_t per = (nchunks + nb - 1) / nb;
+  const size_t lo = (size_t)b * per;
+  const size_t hi = lo + per < nchunks ? lo + per : nchunks;
+  unsigned int acc = 0u;
+  constexpr int UN = 8;
+  size_t i = lo + threadIdx.x;
+  for (; i + (UN - 1) * NT < hi; i += UN * NT) {
+    uint4 v[UN];
+#pragma unroll
+    for (int u = 0; u < UN; ++u) v[u] = p[i + u * NT];
+#pragma unroll
+    for (int u = 0; u < UN; ++u) acc ^= v[u].x ^ v[u].w;
+  }
+  for (; i < hi; i += NT) { const uint4 v = p[i]; acc ^= v.x ^ v.w; }
+  asm volatile("" ::"v"(acc));
+}
+
 // ---------------------------------------------------------------------------
 // decode
 // ---------------------------------------------------------------------------
@@ -42,7 +68,7 @@ __global__ __launch_bounds__(64 * NREP) void attn_decode_kernel(
     const float* __restrict__ q, const uint16_t* __restrict__ kc,
     const uint16_t* __restrict__ vc, const int* __restrict__ pos_ptr, int S, float scale,
     float* __restrict__ part, int nsplit, unsigned int* __restrict__ tickets,
-    uint16_t* __restrict__ out) {
+    uint16_t* __restrict__ out, const uint4* __restrict__ pf, size_t pf_chunks) {
   constexpr int DPL = HD / 64;         // output dims per lane
   constexpr int KROW = HD + 8;         // padded K row (elements)
   constexpr int CPR = HD / 8;          // 16-byte chunks per row
@@ -54,6 +80,11 @@ __global__ __launch_bounds__(64 * NREP) void attn_decode_kernel(
   __shared__ unsigned int last_flag;
 
   const int g = blockIdx.x, s = blockIdx.y;
+  if (s >= nsplit) {  // Infinity-Cache warm-up of the next GEMV's weights (see header)
+    prefetch_blocks<64 * NREP>(pf, pf_chunks, (s - nsplit) * gridDim.x + g,
+                               (gridDim.y - nsplit) * gridDim.x);
+    return;
+  }
   const int Tk = *pos_ptr + 1;
   const int k0 = s * kKeysPerSplit;
   if (k0 >= Tk) return;
@@ -242,11 +273,12 @@ using namespace cake;
 template <int DT, int HD>
 static int launch_decode(int n_rep, dim3 grid, hipStream_t st, const float* q, const void* kc,
                          const void* vc, const int* pos, int S, float scale, float* part,
-                         int nsplit, unsigned int* tickets, void* out) {
+                         int nsplit, unsigned int* tickets, void* out, const void* pf,
+                         size_t pf_chunks) {
 #define CAKE_DEC(NR)                                                                         \
   hipLaunchKernelGGL((attn_decode_kernel<DT, HD, NR>), grid, dim3(64 * NR), 0, st, q,        \
                      (const uint16_t*)kc, (const uint16_t*)vc, pos, S, scale, part, nsplit,  \
-                     tickets, (uint16_t*)out)
+                     tickets, (uint16_t*)out, (const uint4*)pf, pf_chunks)
   switch (n_rep) {
     case 1: CAKE_DEC(1); break;
     case 2: CAKE_DEC(2); break;
@@ -258,16 +290,28 @@ static int launch_decode(int n_rep, dim3 grid, hipStream_t st, const float* q, c
   return (int)hipGetLastError();
 }
 
+// pf/pf_bytes/pf_rows: optional read-only weight range to warm into the
+// Infinity Cache with pf_rows extra grid rows (nkv workgroups each).
+CAKE_API int cake_attn_decode_pf(int dt, const float* q, const void* kc, const void* vc,
+                                 const int* pos, int S, int nh, int nkv, int hd, float scale,
+                                 float* part, unsigned int* tickets, void* out, const void* pf,
+                                 size_t pf_bytes, int pf_rows, hipStream_t st) {
+  const int n_rep = nh / nkv;
+  if (nh % nkv || n_rep > 8 || pf_bytes % 16 || pf_rows < 0) return (int)hipErrorInvalidValue;
+  if (pf == nullptr || pf_bytes == 0) pf_rows = 0;
+  const int nsplit = (S + kKeysPerSplit - 1) / kKeysPerSplit;
+  const dim3 grid(nkv, nsplit + pf_rows);
+  DISPATCH_DT_HD(dt, hd, return (launch_decode<DT, HD>(n_rep, grid, st, q, kc, vc, pos, S, scale,
+                                                       part, nsplit, tickets, out, pf,
+                                                       pf_bytes / 16)));
+  return (int)hipErrorInvalidValue;
+}
+
 CAKE_API int cake_attn_decode(int dt, const float* q, const void* kc, const void* vc,
                               const int* pos, int S, int nh, int nkv, int hd, float scale,
                               float* part, unsigned int* tickets, void* out, hipStream_t st) {
-  const int n_rep = nh / nkv;
-  if (nh % nkv || n_rep > 8) return (int)hipErrorInvalidValue;
-  const int nsplit = (S + kKeysPerSplit - 1) / kKeysPerSplit;
-  const dim3 grid(nkv, nsplit);
-  DISPATCH_DT_HD(dt, hd, return (launch_decode<DT, HD>(n_rep, grid, st, q, kc, vc, pos, S, scale,
-                                                       part, nsplit, tickets, out)));
-  return (int)hipErrorInvalidValue;
+  return cake_attn_decode_pf(dt, q, kc, vc, pos, S, nh, nkv, hd, scale, part, tickets, out,
+                             nullptr, 0, 0, st);
 }
 
 CAKE_API int cake_attn_prefill(int dt, const void* q, const void* kc, const void* vc,

@@ -175,6 +175,9 @@ class LayerStack:
         self.fused_prefetch = mode != "2"
         self.fused_grid = int(os.environ.get("CAKE_AO_GRID", "0")) or None
         self.fused_sleep = int(os.environ.get("CAKE_AO_SLEEP", "1"))
+        # decode attention warms the o_proj weights into the Infinity Cache with
+        # CAKE_ATTN_PF_ROWS extra grid rows (0 = off)
+        self.attn_pf_rows = int(os.environ.get("CAKE_ATTN_PF_ROWS", "0"))
         self.fused_ao = (backend == "hip" and mode != "0" and
                          attn_oproj_supported(cfg.num_attention_heads, cfg.num_key_value_heads,
                                               cfg.head_dim, cfg.hidden_size))
@@ -252,7 +255,7 @@ class LayerStack:
                              sleep=self.fused_sleep)
             else:
                 K.attn_decode(bufs.q, kc, vc, bufs.pos, self.scale, bufs.part, bufs.tickets,
-                              bufs.attn_out)
+                              bufs.attn_out, prefetch=w.wo, prefetch_rows=self.attn_pf_rows)
                 K.gemv(bufs.attn_out, w.wo, bufs.resid, accumulate=True)
             K.swiglu(bufs.resid, w.ln2, cfg.rms_norm_eps, w.wg, w.wu, bufs.act)
             K.gemv(bufs.act, w.wd, bufs.resid, accumulate=True)

@@ -30,6 +30,7 @@ _SIGS = {
     "cake_gemv_x16": [I, P, P, I, I, P, I, P],
     "cake_gemv_norm_f32": [I, P, P, F, P, I, I, P, P],
     "cake_attn_decode": [I, P, P, P, P, I, I, I, I, F, P, P, P, P],
+    "cake_attn_decode_pf": [I, P, P, P, P, I, I, I, I, F, P, P, P, P, Z, I, P],
     "cake_attn_prefill": [I, P, P, P, I, I, I, I, I, I, F, P, P],
     "cake_embed": [I, P, P, I, I, P, P],
     "cake_rmsnorm": [I, P, P, F, I, I, P, P],

@@ -111,11 +111,14 @@ def norm_gemv_f32(resid, norm_w, eps, w, out):
                                        _p(out), _stream()), "gemv_norm_f32")
 
 
-def attn_decode(q, kcache, vcache, pos, scale, part, tickets, out):
+def attn_decode(q, kcache, vcache, pos, scale, part, tickets, out, prefetch=None,
+                prefetch_rows=0):
     """Split-K GQA decode attention for the token at device position `pos`.
 
     part: f32 workspace (:func:`attn_workspace_numel`); tickets: int32 [nkv],
-    zero-initialised once and re-armed by the kernel itself.
+    zero-initialised once and re-armed by the kernel itself.  prefetch: optional
+    contiguous tensor (the next GEMV's weights) that `prefetch_rows` extra grid
+    rows read into the Infinity Cache while the attention runs (read-only).
     """
     nkv, S, hd = kcache.shape
     nh = q.numel() // hd
@@ -129,6 +132,16 @@ def attn_decode(q, kcache, vcache, pos, scale, part, tickets, out):
     _req(tickets, "tickets", dtype=torch.int32, numel=nkv)
     if hd not in (64, 128) or nh % nkv or (nh // nkv) not in (1, 2, 4, 8):
         raise ValueError(f"unsupported attention shape nh={nh} nkv={nkv} hd={hd}")
+    if prefetch is not None and prefetch_rows > 0:
+        _req(prefetch, "prefetch")
+        nbytes = prefetch.numel() * prefetch.element_size()
+        nbytes -= nbytes % 16
+        check(kernels().cake_attn_decode_pf(_dt(kcache), _p(q), _p(kcache), _p(vcache), _p(pos),
+                                            S, nh, nkv, hd, float(scale), _p(part), _p(tickets),
+                                            _p(out), _p(prefetch), nbytes, int(prefetch_rows),
+                                            _stream()),
+              "attn_decode_pf")
+        return
     check(kernels().cake_attn_decode(_dt(kcache), _p(q), _p(kcache), _p(vcache), _p(pos), S, nh,
                                      nkv, hd, float(scale), _p(part), _p(tickets), _p(out),
                                      _stream()),

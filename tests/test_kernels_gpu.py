@@ -115,6 +115,15 @@ def test_attn_decode(cuda, dt, nh, nkv, hd, pos):
     ref = R.attention(q.view(1, nh, hd), kc[:, :Tk].transpose(0, 1), vc[:, :Tk].transpose(0, 1),
                       pos).reshape(-1)
     torch.testing.assert_close(out.float(), ref, **_tol(dt))
+    # Infinity-Cache warm-up rows: read-only, same output, weights untouched
+    wo = _rand(nh * hd, 1000, dt=dt)
+    wo_before = wo.clone()
+    out_pf = torch.zeros_like(out)
+    K_.attn_decode(q, kc, vc, p, 1 / math.sqrt(hd), part, tickets, out_pf, prefetch=wo,
+                   prefetch_rows=7)
+    assert int(tickets.abs().sum()) == 0
+    torch.testing.assert_close(out_pf, out, rtol=0, atol=0)
+    assert torch.equal(wo, wo_before)
 
 
 @pytest.mark.parametrize("dt", DTYPES)
