@@ -58,6 +58,7 @@ class DecodeBuffers:
         nsplit = (max_seq + 63) // 64
         self.part = torch.zeros(nh * nsplit * (hd + 2), device=device, dtype=f32)
         self.tickets = torch.zeros(cfg.num_key_value_heads, device=device, dtype=i32)
+        self.done = torch.zeros(cfg.num_key_value_heads, device=device, dtype=i32)  # qkv_attn
         self.ctl = torch.zeros(3, device=device, dtype=i32)   # fused attn+o_proj counters
         self.err = torch.zeros(1, device=device, dtype=i32)
         self.pos = torch.zeros(1, device=device, dtype=i32) if pos is None else pos
@@ -178,6 +179,10 @@ class LayerStack:
         # decode attention warms the o_proj weights into the Infinity Cache with
         # CAKE_ATTN_PF_ROWS extra grid rows (0 = off)
         self.attn_pf_rows = int(os.environ.get("CAKE_ATTN_PF_ROWS", "0"))
+        # decode graphs for positions < qkv_attn_max_t fold attention into the QKV
+        # launch (one workgroup per kv head does it); 0 disables.  Opt-in: measured
+        # slower at every context length (profiles/r1_qkv_attn_sweep.txt)
+        self.qkv_attn_max_t = int(os.environ.get("CAKE_QKV_ATTN_MAX_T", "0"))
         self.fused_ao = (backend == "hip" and mode != "0" and
                          attn_oproj_supported(cfg.num_attention_heads, cfg.num_key_value_heads,
                                               cfg.head_dim, cfg.hidden_size))
@@ -237,15 +242,35 @@ class LayerStack:
         kv.length = max(kv.length, pos0 + T)
         return hidden
 
-    def decode_step(self, bufs: DecodeBuffers, layers: list[int], session: int = 0) -> None:
-        """Graph-capturable T=1 step over bufs.resid at device position bufs.pos (hip only)."""
+    def qkv_attn_ok(self) -> bool:
+        """Whether the one-launch QKV+attention kernel (short contexts) applies."""
+        from ...ops.hip import qkv_attn_supported
+        c = self.cfg
+        return (self.backend == "hip" and not self.fused_ao and self.qkv_attn_max_t > 0 and
+                qkv_attn_supported(c.num_attention_heads, c.num_key_value_heads, c.head_dim))
+
+    def decode_step(self, bufs: DecodeBuffers, layers: list[int], session: int = 0,
+                    short_ctx: bool = False) -> None:
+        """Graph-capturable T=1 step over bufs.resid at device position bufs.pos (hip only).
+
+        short_ctx: the caller guarantees pos < qkv_attn_max_t for every replay, so
+        each layer's attention runs as the tail of its QKV launch (qkv_attn).
+        """
         from ...ops import hip as K
         kv = self.cache(session)
         cfg = self.cfg
+        fuse_qa = short_ctx and self.qkv_attn_ok()
         for li in layers:
             w = self.weights[li]
             s = self.slot_of[li]
             kc, vc = kv.k[s], kv.v[s]
+            if fuse_qa:
+                K.qkv_attn(bufs.resid, w.ln1, cfg.rms_norm_eps, w.wq, w.wk, w.wv, self.inv_freq,
+                           bufs.pos, bufs.q, kc, vc, bufs.done, bufs.attn_out, self.scale)
+                K.gemv(bufs.attn_out, w.wo, bufs.resid, accumulate=True)
+                K.swiglu(bufs.resid, w.ln2, cfg.rms_norm_eps, w.wg, w.wu, bufs.act)
+                K.gemv(bufs.act, w.wd, bufs.resid, accumulate=True)
+                continue
             K.qkv_rope(bufs.resid, w.ln1, cfg.rms_norm_eps, w.wq, w.wk, w.wv, self.inv_freq,
                        bufs.pos, bufs.q, kc, vc, rearm=bufs.ctl if self.fused_ao else None)
             if self.fused_ao:

@@ -147,21 +147,30 @@ class DeviceDecoder:
         self.use_graph = use_graph
         self.bufs: DecodeBuffers = model.stack.decode_buffers(with_head=True)
         self.graph: torch.cuda.CUDAGraph | None = None
+        # short-context variant: attention folded into each layer's QKV launch,
+        # replayed while every position of the launch is < qkv_attn_max_t
+        self.graph_short: torch.cuda.CUDAGraph | None = None
+        self.host_pos = 0  # device position of the next step (tracked on the host)
         self._layers = list(range(model.cfg.num_hidden_layers))
         # the whole step's layers + lm_head as ONE persistent launch (decode_mega.hip)
         self.mega: MegaPlan | None = None
         if mega_enabled() and MegaPlan.supported(model.cfg):
             self.mega = MegaPlan(model.stack, self._layers)
+        self.short_ok = self.mega is None and model.stack.qkv_attn_ok()
+
+    def _short(self) -> bool:
+        """All positions of the next launch are short enough for qkv_attn."""
+        return self.short_ok and self.host_pos + self.k <= self.m.stack.qkv_attn_max_t
 
     # the captured body
-    def _step_body(self) -> None:
+    def _step_body(self, short: bool = False) -> None:
         from ...ops import hip as K
         b, m = self.bufs, self.m
         K.embed(m.head.embed, b.tok, b.resid)
         if self.mega is not None:
             self.mega.launch(b, m.session, head=(m.head.norm, m.head.lm_head), logits=b.logits)
         else:
-            m.stack.decode_step(b, self._layers, m.session)
+            m.stack.decode_step(b, self._layers, m.session, short_ctx=short)
             K.norm_gemv_f32(b.resid, m.head.norm, m.cfg.rms_norm_eps, m.head.lm_head, b.logits)
         if self.penalty != 1.0:
             K.repeat_penalty(b.logits, b.hist, b.hist_len, self.last_n, self.penalty)
@@ -177,8 +186,10 @@ class DeviceDecoder:
         # warm the kernels once outside capture on scratch state, then restore
         saved = [t.clone() for t in (self.bufs.tok, self.bufs.pos, self.bufs.hist_len)]
         hist = self.bufs.hist.clone()
+        variants = [False, True] if self.short_ok else [False]
         with torch.cuda.stream(s):
-            self._step_body()
+            for short in variants:
+                self._step_body(short)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         if self.mega is not None:
@@ -187,11 +198,15 @@ class DeviceDecoder:
             t.copy_(v)
         self.bufs.hist.copy_(hist)
         self.bufs.slot.zero_()
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            for _ in range(self.k):
-                self._step_body()
-        self.graph = g
+        for short in variants:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for _ in range(self.k):
+                    self._step_body(short)
+            if short:
+                self.graph_short = g
+            else:
+                self.graph = g
         torch.cuda.synchronize()
 
     def start(self, prompt: list[int]) -> int:
@@ -209,6 +224,7 @@ class DeviceDecoder:
         b.pos.fill_(T - 1)
         b.slot.zero_()
         m.head_logits(h[-1], out=b.logits)
+        self.host_pos = T - 1
         return self._select_first()
 
     def _select_first(self) -> int:
@@ -219,6 +235,7 @@ class DeviceDecoder:
         if self.greedy:
             K.argmax(b.logits, b.slot)
             K.finalize_token(b.slot, b.tok, b.hist, b.hist_len, b.pos)
+            self.host_pos += 1
             return int(b.tok.item())
         raise RuntimeError("sampled mode: caller pushes the first token")
 
@@ -227,13 +244,17 @@ class DeviceDecoder:
         b = self.bufs
         src = torch.tensor([token], dtype=torch.int32, device=self.m.device)
         K.push_token(src, b.tok, b.hist, b.hist_len, b.pos)
+        self.host_pos += 1
 
     def launch(self) -> None:
         """Enqueue `self.k` decode steps (one graph replay; async)."""
+        short = self._short()
         if self.graph is not None:
-            self.graph.replay()
+            (self.graph_short if short and self.graph_short is not None else self.graph).replay()
         else:
-            self._step_body()
+            self._step_body(short)
+        if self.greedy:  # greedy steps advance pos on the device; sampled ones via push()
+            self.host_pos += self.k
 
     def logits(self) -> torch.Tensor:
         return self.bufs.logits

@@ -26,6 +26,7 @@ Z = C.c_size_t
 # name -> argtypes (all return int hipError_t)
 _SIGS = {
     "cake_qkv_rope": [I, P, P, F, P, P, P, I, I, I, I, P, P, P, P, P, I, P, P],
+    "cake_qkv_attn": [I, P, P, F, P, P, P, I, I, I, I, P, P, P, P, P, I, P, P, F, P],
     "cake_swiglu": [I, P, P, F, P, P, I, I, P, P],
     "cake_gemv_x16": [I, P, P, I, I, P, I, P],
     "cake_gemv_norm_f32": [I, P, P, F, P, I, I, P, P],

@@ -74,6 +74,43 @@ def qkv_rope(resid, norm_w, eps, wq, wk, wv, inv_freq, pos, q_out, kcache, vcach
           "qkv_rope")
 
 
+def qkv_attn_supported(nh: int, nkv: int, hd: int) -> bool:
+    return hd in (64, 128) and nkv > 0 and nh % nkv == 0 and (nh // nkv) in (1, 2, 4, 8)
+
+
+def qkv_attn(resid, norm_w, eps, wq, wk, wv, inv_freq, pos, q_out, kcache, vcache, done,
+             attn_out, scale):
+    """qkv_rope + the decode attention of the token at `pos`, in one launch.
+
+    The last workgroup of each GQA group runs that group's attention over
+    positions [0, pos] (see gemv.hip qkv_attn_kernel).  done: int32 [nkv],
+    zero-initialised once (re-armed by the kernel); attn_out: [nh*hd] 16-bit.
+    """
+    K = resid.numel()
+    nkv, S, hd = kcache.shape
+    nh = wq.shape[0] // hd
+    dt = wq.dtype
+    _req(resid, "resid", dtype=torch.float32)
+    _req(norm_w, "norm_w", dtype=dt, shape=(K,))
+    _req(wq, "wq", dtype=dt, shape=(nh * hd, K))
+    _req(wk, "wk", dtype=dt, shape=(nkv * hd, K))
+    _req(wv, "wv", dtype=dt, shape=(nkv * hd, K))
+    _req(inv_freq, "inv_freq", dtype=torch.float32, shape=(hd // 2,))
+    _req(pos, "pos", dtype=torch.int32, numel=1)
+    _req(q_out, "q_out", dtype=torch.float32, numel=nh * hd)
+    _req(kcache, "kcache", dtype=dt)
+    _req(vcache, "vcache", dtype=dt, shape=kcache.shape)
+    _req(done, "done", dtype=torch.int32, numel=nkv)
+    _req(attn_out, "attn_out", dtype=dt, numel=nh * hd)
+    if K % 8 or not qkv_attn_supported(nh, nkv, hd):
+        raise ValueError(f"qkv_attn: unsupported shape K={K} nh={nh} nkv={nkv} hd={hd}")
+    check(kernels().cake_qkv_attn(_dt(wq), _p(resid), _p(norm_w), float(eps), _p(wq), _p(wk),
+                                  _p(wv), K, nh, nkv, hd, _p(inv_freq), _p(pos), _p(q_out),
+                                  _p(kcache), _p(vcache), S, _p(done), _p(attn_out),
+                                  float(scale), _stream()),
+          "qkv_attn")
+
+
 def swiglu(resid, norm_w, eps, wg, wu, act):
     """act = silu(rmsnorm(resid) @ wg.T) * (rmsnorm(resid) @ wu.T)   (batch 1)."""
     K = resid.numel()

@@ -93,6 +93,41 @@ def test_qkv_rope(cuda, dt, H, nh, nkv, hd, pos):
 
 
 @pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("H,nh,nkv,hd,pos", [(4096, 32, 8, 128, 0), (4096, 32, 8, 128, 63),
+                                             (4096, 32, 8, 128, 64), (4096, 32, 8, 128, 300),
+                                             (8192, 64, 8, 128, 100), (1024, 16, 16, 64, 70),
+                                             (1024, 8, 4, 64, 130), (512, 4, 1, 128, 9)])
+def test_qkv_attn(cuda, dt, H, nh, nkv, hd, pos):
+    """One-launch QKV+RoPE+KV write+attention == qkv_rope then the f32 attention reference."""
+    from cake_amd.ops import hip as K_
+    torch.manual_seed(7)
+    S = 512
+    resid = torch.randn(H, device=cuda)
+    nw = (1 + 0.1 * torch.randn(H, device=cuda)).to(dt)
+    wq, wk, wv = (_rand(n * hd, H, dt=dt, std=0.05) for n in (nh, nkv, nkv))
+    invf = R.inv_freq(hd, 500000.0).to(cuda)
+    kc = _rand(nkv, S, hd, dt=dt)  # history rows [0, pos) are arbitrary
+    vc = _rand(nkv, S, hd, dt=dt)
+    kc2, vc2 = kc.clone(), vc.clone()
+    p = torch.tensor([pos], dtype=torch.int32, device=cuda)
+    q, q2 = torch.empty(nh * hd, device=cuda), torch.empty(nh * hd, device=cuda)
+    done = torch.zeros(nkv, dtype=torch.int32, device=cuda)
+    out = torch.zeros(nh * hd, device=cuda, dtype=dt)
+    scale = 1 / math.sqrt(hd)
+    for _ in range(2):  # second launch checks the done counters were re-armed
+        out.zero_()
+        K_.qkv_attn(resid, nw, 1e-5, wq, wk, wv, invf, p, q, kc, vc, done, out, scale)
+        assert int(done.abs().sum()) == 0
+    K_.qkv_rope(resid, nw, 1e-5, wq, wk, wv, invf, p, q2, kc2, vc2)
+    torch.testing.assert_close(q, q2, rtol=0, atol=0)
+    assert torch.equal(kc, kc2) and torch.equal(vc, vc2)
+    Tk = pos + 1
+    ref = R.attention(q2.view(1, nh, hd), kc2[:, :Tk].transpose(0, 1).float(),
+                      vc2[:, :Tk].transpose(0, 1).float(), pos).reshape(-1)
+    torch.testing.assert_close(out.float(), ref, **_tol(dt))
+
+
+@pytest.mark.parametrize("dt", DTYPES)
 @pytest.mark.parametrize("nh,nkv,hd,pos", [(32, 8, 128, 0), (32, 8, 128, 63), (32, 8, 128, 64),
                                            (32, 8, 128, 1000), (64, 8, 128, 300),
                                            (4, 1, 64, 17), (8, 8, 64, 200)])
