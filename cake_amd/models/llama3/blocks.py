@@ -141,8 +141,10 @@ class MegaPlan:
 
 
 def mega_enabled() -> bool:
-    """Opt-in (CAKE_MEGA=1): measured slower than the multi-kernel hipGraph on MI355X
-    (8B: 257 vs 331 tok/s, profiles/r1_mega_decode_trace.json) — see decode_mega.hip."""
+    """Opt-in (CAKE_MEGA=1), experimental: measured slower than the multi-kernel
+    hipGraph on MI355X (8B: 257 vs 331 tok/s) — see decode_mega.hip — and one
+    intermittent numerics mismatch was observed in its GPU tests
+    (tests/test_mega_gpu.py); not for production use."""
     import os
     return os.environ.get("CAKE_MEGA", "0") == "1"
 
