@@ -101,4 +101,15 @@ __device__ __forceinline__ uint4 ld_nt16(const uint4* p) {
 
 __device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
 
+// LDS-DMA (global_load_lds) operand types and an s_waitcnt immediate that
+// constrains only the vector-memory counter (gfx9 encoding).
+typedef const __attribute__((address_space(1))) void* gptr_t;
+typedef __attribute__((address_space(3))) void* lptr_t;
+constexpr int vm_wait(int n) { return (n & 0xF) | ((n >> 4) << 14) | (0x7 << 4) | (0xF << 8); }
+
+// 16 bytes global -> LDS; the LDS destination of lane l is lds_wave_base + 16 l.
+__device__ __forceinline__ void glds16(const void* g, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((gptr_t)g, (lptr_t)lds_wave_base, 16, 0, 0);
+}
+
 }  // namespace cake

@@ -215,8 +215,6 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
   }
 }
 
-// s_waitcnt with only the vector-memory counter constrained (gfx9 encoding)
-constexpr int vm_wait(int n) { return (n & 0xF) | ((n >> 4) << 14) | (0x7 << 4) | (0xF << 8); }
 
 // Same GEMM with LDS-DMA staging (global_load_lds_dwordx4): no VGPR round trip
 // and no ds_write pass.  The LDS image stays lane-linear per wave instruction
@@ -269,8 +267,6 @@ __global__ __launch_bounds__(256, 2) void conv_glds_kernel(ConvArgs a) {
       pbase[i] = a.x;
     }
   }
-  typedef const __attribute__((address_space(1))) void* gptr_t;
-  typedef __attribute__((address_space(3))) void* lptr_t;
   auto issue = [&](int s, int buf) {
     const int tap = s / cpt, icb = (s - tap * cpt) << 6;
     const int ky = tap / a.KW, kx = tap - ky * a.KW;
@@ -408,8 +404,6 @@ __global__ __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) void conv_halo_kernel(
         hoff[i] = (((long long)n * a.H + (vy >> a.up)) * a.W + (vx >> a.up)) * a.IC + lch * 8;
     }
   }
-  typedef const __attribute__((address_space(1))) void* gptr_t;
-  typedef __attribute__((address_space(3))) void* lptr_t;
   auto issue_w = [&](int s, int buf) {
     const int chunk = s / taps, tap = s - chunk * taps;
     const size_t koff = (size_t)tap * a.IC + chunk * kCBK;

@@ -189,12 +189,6 @@ struct QkvArgs {
   uint16_t* kcache;       // [nkv][S][hd] (this layer)
   uint16_t* vcache;
   int S;
-  unsigned int* rearm;  // optional: zeroed by block 0 (fused attention done-counter)
-  // attention tail (qkv_attn_kernel only): per-kv-group done counters [nkv]
-  // (zero-initialised once, re-armed by the kernel) and the head outputs
-  unsigned int* done;
-  uint16_t* attn_out;  // [nh*hd]
-  float scale;
 };
 
 struct QkvRow {
@@ -233,7 +227,6 @@ __global__ __launch_bounds__(kGemvThreads) void qkv_rope_kernel(QkvArgs a) {
     map(p0, wa, wb);
     prefetch_rows<PFC>(wa, wb, pre);
   }
-  if (a.rearm != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *a.rearm = 0u;
   stage_rmsnorm<DT>(a.resid, a.norm_w, a.eps, a.K, xs);
   const int pos = *a.pos;
   auto epi = [&](int p, float da, float db) {
@@ -257,182 +250,6 @@ __global__ __launch_bounds__(kGemvThreads) void qkv_rope_kernel(QkvArgs a) {
     }
   };
   run_pairs<DT, true, U, PFC>(map, epi, xs, a.K, npairs, p0, gridDim.x * kGemvWaves, pre);
-}
-
-// ---------------------------------------------------------------------------
-// QKV + RoPE + KV write + decode attention in ONE launch (short contexts).
-//
-// A separate attention launch costs ~6 us per layer in the decode graph, most of
-// it fixed launch/drain latency (attention moves < 1 MB at short context).  Here
-// the grid has exactly one pair per wave, so a workgroup's 4 pairs belong to one
-// q/k/v head and hence to one GQA group g.  Each workgroup, after its epilogue
-// stores, bumps done[g] (agent-scope release); the LAST of the group's
-// (nrep + 2) * hd / 8 workgroups acquires and runs the whole group's attention
-// (nrep query heads over Tk keys, 64-key chunks staged through LDS, online
-// softmax in f32) and writes attn_out — the work the attention launch did, minus
-// its launch.  The tail is one workgroup per kv head, so the host uses this
-// kernel only while Tk is short (DeviceDecoder picks the graph by position).
-// ---------------------------------------------------------------------------
-template <int DT, int HD, int HPW>
-__device__ __forceinline__ void group_attention_tail(const QkvArgs& a, int g, int Tk, float* lds) {
-  constexpr int DPL = HD / 64;
-  constexpr int KROW = HD + 8;
-  constexpr int CPR = HD / 8;
-  const int nrep = a.nh / a.nkv;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  uint16_t* Ks = reinterpret_cast<uint16_t*>(lds);                // [64][KROW]
-  uint16_t* Vs = Ks + 64 * KROW;                                  // [64][HD]
-  float* qs = reinterpret_cast<float*>(Vs + 64 * HD);             // [nrep][HD]
-  float* ps = qs + nrep * HD;                                     // [nrep][64]
-  for (int i = tid; i < nrep * HD; i += kGemvThreads) qs[i] = a.q_out[(size_t)g * nrep * HD + i];
-  float m[HPW], l[HPW], o[HPW][DPL];
-#pragma unroll
-  for (int i = 0; i < HPW; ++i) {
-    m[i] = -INFINITY; l[i] = 0.f;
-#pragma unroll
-    for (int d = 0; d < DPL; ++d) o[i][d] = 0.f;
-  }
-  const uint4* kg = reinterpret_cast<const uint4*>(a.kcache + (size_t)g * a.S * HD);
-  const uint4* vg = reinterpret_cast<const uint4*>(a.vcache + (size_t)g * a.S * HD);
-  for (int k0 = 0; k0 < Tk; k0 += 64) {
-    const int kn = min(64, Tk - k0);
-    __syncthreads();  // previous chunk consumed (and qs staged on the first pass)
-    for (int i = tid; i < kn * CPR; i += kGemvThreads) {
-      const int r = i / CPR, c = i - r * CPR;
-      *reinterpret_cast<uint4*>(Ks + r * KROW + c * 8) = kg[(size_t)k0 * CPR + i];
-      reinterpret_cast<uint4*>(Vs)[i] = vg[(size_t)k0 * CPR + i];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < HPW; ++i) {
-      const int hh = wave + i * kGemvWaves;
-      if (hh >= nrep) break;  // wave-uniform
-      float sc = -INFINITY;
-      if (lane < kn) {
-        const uint16_t* kr = Ks + lane * KROW;
-        const float* qh = qs + hh * HD;
-        float acc = 0.f;
-#pragma unroll
-        for (int c = 0; c < CPR; ++c) {
-          float kf[8];
-          unpack8<DT>(*reinterpret_cast<const uint4*>(kr + c * 8), kf);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) acc = fmaf(qh[c * 8 + e], kf[e], acc);
-        }
-        sc = acc * a.scale;
-      }
-      const float mn = fmaxf(m[i], wave_max(sc));
-      const float alpha = __expf(m[i] - mn);  // 0 on the first chunk (m = -inf)
-      const float pj = lane < kn ? __expf(sc - mn) : 0.f;
-      l[i] = l[i] * alpha + wave_sum(pj);
-      m[i] = mn;
-      float* pw = ps + hh * 64;
-      pw[lane] = pj;
-      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's p row is in LDS
-      __builtin_amdgcn_wave_barrier();
-#pragma unroll
-      for (int d = 0; d < DPL; ++d) o[i][d] *= alpha;
-#pragma unroll 8
-      for (int j = 0; j < kn; ++j) {
-        const float w = pw[j];
-        const uint16_t* vr = Vs + j * HD + lane * DPL;
-#pragma unroll
-        for (int d = 0; d < DPL; ++d) o[i][d] = fmaf(w, to_f32<DT>(vr[d]), o[i][d]);
-      }
-      __builtin_amdgcn_wave_barrier();  // p row reads done before the next head reuses it
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < HPW; ++i) {
-    const int hh = wave + i * kGemvWaves;
-    if (hh >= nrep) break;
-    const float inv = 1.f / l[i];
-    uint16_t* dst = a.attn_out + ((size_t)g * nrep + hh) * HD + lane * DPL;
-#pragma unroll
-    for (int d = 0; d < DPL; ++d) dst[d] = from_f32<DT>(o[i][d] * inv);
-  }
-}
-
-template <int DT, int U, int PFC>
-__global__ __launch_bounds__(kGemvThreads) void qkv_attn_kernel(QkvArgs a) {
-  extern __shared__ float xs[];
-  __shared__ unsigned int last_flag;
-  const int half = a.hd >> 1;
-  const int npairs = (a.nh + 2 * a.nkv) * half;  // == gridDim.x * kGemvWaves (host-checked)
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int p0 = blockIdx.x * kGemvWaves + wave;
-  auto map = [&](int p, const uint16_t*& wa, const uint16_t*& wb) {
-    const QkvRow r = qkv_row(a, p);
-    wa = r.base + r.ra * a.K;
-    wb = r.base + (r.ra + half) * a.K;
-  };
-  Regs<PFC> pre;
-  if (PFC > 0) {
-    const uint16_t *wa, *wb;
-    map(p0, wa, wb);
-    prefetch_rows<PFC>(wa, wb, pre);
-  }
-  stage_rmsnorm<DT>(a.resid, a.norm_w, a.eps, a.K, xs);
-  const int pos = *a.pos;
-  auto epi = [&](int p, float da, float db) {
-    if (lane != 0) return;
-    const QkvRow r = qkv_row(a, p);
-    float oa = da, ob = db;
-    if (r.kind < 2) {
-      float s, c;
-      sincosf((float)pos * a.inv_freq[r.i], &s, &c);
-      oa = da * c - db * s;
-      ob = da * s + db * c;
-    }
-    if (r.kind == 0) {
-      a.q_out[r.ra] = oa;
-      a.q_out[r.ra + half] = ob;
-    } else {
-      uint16_t* cache = r.kind == 1 ? a.kcache : a.vcache;
-      const size_t off = ((size_t)r.head * a.S + pos) * a.hd + r.i;
-      cache[off] = from_f32<DT>(oa);
-      cache[off + half] = from_f32<DT>(ob);
-    }
-  };
-  run_pairs<DT, true, U, PFC>(map, epi, xs, a.K, npairs, p0, npairs, pre);
-
-  // which GQA group this workgroup's head belongs to
-  const int nrep = a.nh / a.nkv;
-  const int slot = (blockIdx.x * kGemvWaves) / half;
-  const int g = slot < a.nh ? slot / nrep : (slot < a.nh + a.nkv ? slot - a.nh : slot - a.nh - a.nkv);
-  const unsigned int nblk = (unsigned int)((nrep + 2) * half / kGemvWaves);
-  // publish: epilogue stores -> vmcnt(0) -> barrier -> release(agent) -> ticket
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned int t =
-        __hip_atomic_fetch_add(&a.done[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned int last = (t == nblk - 1) ? 1u : 0u;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      a.done[g] = 0u;  // re-arm for the next launch
-    }
-    last_flag = last;
-  }
-  __syncthreads();
-  if (!last_flag) return;
-  const int Tk = pos + 1;
-  if (a.hd == 128) {
-    if (nrep > kGemvWaves) group_attention_tail<DT, 128, 2>(a, g, Tk, xs);
-    else group_attention_tail<DT, 128, 1>(a, g, Tk, xs);
-  } else {
-    if (nrep > kGemvWaves) group_attention_tail<DT, 64, 2>(a, g, Tk, xs);
-    else group_attention_tail<DT, 64, 1>(a, g, Tk, xs);
-  }
-}
-
-// LDS bytes the attention tail needs (Ks padded + Vs + qs + ps), in floats
-static inline size_t qkv_attn_tail_lds(int hd, int nrep) {
-  return (size_t)64 * (hd + 8) * 2 + (size_t)64 * hd * 2 + (size_t)nrep * hd * 4 +
-         (size_t)nrep * 64 * 4;
 }
 
 // ---------------------------------------------------------------------------
@@ -570,41 +387,16 @@ CAKE_API int cake_qkv_rope(int dt, const float* resid, const void* norm_w, float
                            const void* wq, const void* wk, const void* wv, int K, int nh,
                            int nkv, int hd, const float* inv_freq, const int* pos,
                            float* q_out, void* kcache, void* vcache, int S,
-                           unsigned int* rearm, hipStream_t st) {
+                           hipStream_t st) {
   if (K % 8 || hd % 2) return (int)hipErrorInvalidValue;
   QkvArgs a{resid, (const uint16_t*)norm_w, eps, (const uint16_t*)wq,
             (const uint16_t*)wk, (const uint16_t*)wv, K, nh, nkv, hd, inv_freq, pos,
-            q_out, (uint16_t*)kcache, (uint16_t*)vcache, S, rearm};
+            q_out, (uint16_t*)kcache, (uint16_t*)vcache, S};
   const int npairs = (nh + 2 * nkv) * (hd / 2);
   const size_t lds = (size_t)K * sizeof(float);
   const GemvTune t = g_tune[kQkv];
   DISPATCH_DT(dt, DISPATCH_TUNE(t, K, hipLaunchKernelGGL((qkv_rope_kernel<DT, U, PF>),
                                                       dim3(grid_for(npairs, t.MB)),
-                                                      dim3(kGemvThreads), lds, st, a)));
-  return (int)hipGetLastError();
-}
-
-// qkv_rope + decode attention (see qkv_attn_kernel).  done: u32 [nkv] zeroed
-// once; attn_out: [nh*hd] 16-bit.  hd in {64, 128}, nh/nkv in {1, 2, 4, 8}.
-CAKE_API int cake_qkv_attn(int dt, const float* resid, const void* norm_w, float eps,
-                           const void* wq, const void* wk, const void* wv, int K, int nh,
-                           int nkv, int hd, const float* inv_freq, const int* pos,
-                           float* q_out, void* kcache, void* vcache, int S,
-                           unsigned int* done, void* attn_out, float scale, hipStream_t st) {
-  if (K % 8 || (hd != 64 && hd != 128) || nkv <= 0 || nh % nkv) return (int)hipErrorInvalidValue;
-  const int nrep = nh / nkv;
-  if (nrep != 1 && nrep != 2 && nrep != 4 && nrep != 8) return (int)hipErrorInvalidValue;
-  QkvArgs a{resid, (const uint16_t*)norm_w, eps, (const uint16_t*)wq,
-            (const uint16_t*)wk, (const uint16_t*)wv, K, nh, nkv, hd, inv_freq, pos,
-            q_out, (uint16_t*)kcache, (uint16_t*)vcache, S, nullptr,
-            done, (uint16_t*)attn_out, scale};
-  const int npairs = (nh + 2 * nkv) * (hd / 2);  // hd/2 % 4 == 0: one head per workgroup
-  size_t lds = (size_t)K * sizeof(float);
-  const size_t tail = qkv_attn_tail_lds(hd, nrep);
-  if (tail > lds) lds = tail;
-  const GemvTune t = g_tune[kQkv];
-  DISPATCH_DT(dt, DISPATCH_TUNE(t, K, hipLaunchKernelGGL((qkv_attn_kernel<DT, U, PF>),
-                                                      dim3(npairs / kGemvWaves),
                                                       dim3(kGemvThreads), lds, st, a)));
   return (int)hipGetLastError();
 }

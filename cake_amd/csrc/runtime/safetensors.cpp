@@ -46,16 +46,28 @@ SafeTensorsFile::SafeTensorsFile(const std::string& path) : path_(path) {
     TensorView v;
     v.name = kv.first;
     v.dtype = kv.second.get("dtype").as_string();
+    // every header integer is validated before use: negative values and
+    // overflowing products are rejected (a crafted header must not produce a
+    // view outside the mapping)
+    const auto bad = [&](const char* what) {
+      return std::runtime_error(path + ": tensor " + v.name + " " + what);
+    };
     uint64_t numel = 1;
     for (const auto& d : kv.second.get("shape").items()) {
-      v.shape.push_back((uint64_t)d.as_int());
-      numel *= (uint64_t)d.as_int();
+      const int64_t dim = d.as_int();
+      if (dim < 0) throw bad("has a negative dimension");
+      if (dim != 0 && numel > UINT64_MAX / (uint64_t)dim) throw bad("shape overflows");
+      v.shape.push_back((uint64_t)dim);
+      numel *= (uint64_t)dim;
     }
     const auto& off = kv.second.get("data_offsets");
-    const uint64_t b = (uint64_t)off.at(0).as_int(), e = (uint64_t)off.at(1).as_int();
-    if (e < b || data0 + e > size_) throw std::runtime_error(path + ": tensor " + v.name + " out of bounds");
-    if (e - b != numel * dtype_size(v.dtype))
-      throw std::runtime_error(path + ": tensor " + v.name + " size mismatch");
+    const int64_t bi = off.at(0).as_int(), ei = off.at(1).as_int();
+    if (bi < 0 || ei < 0) throw bad("has negative data offsets");
+    const uint64_t b = (uint64_t)bi, e = (uint64_t)ei;
+    if (e < b || e > size_ - data0) throw bad("out of bounds");
+    const uint64_t es = dtype_size(v.dtype);
+    if (es != 0 && numel > UINT64_MAX / es) throw bad("byte size overflows");
+    if (e - b != numel * es) throw bad("size mismatch");
     v.offset = data0 + b;
     v.data = base_ + v.offset;
     v.nbytes = e - b;

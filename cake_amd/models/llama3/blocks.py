@@ -55,12 +55,8 @@ class DecodeBuffers:
         self.q = torch.zeros(nh * hd, device=device, dtype=f32)
         self.attn_out = torch.zeros(nh * hd, device=device, dtype=dtype)
         self.act = torch.zeros(I, device=device, dtype=dtype)
-        nsplit = (max_seq + 63) // 64
-        self.part = torch.zeros(nh * nsplit * (hd + 2), device=device, dtype=f32)
+        self.part = torch.zeros(nh * 64 * (hd + 2), device=device, dtype=f32)  # <= 64 splits
         self.tickets = torch.zeros(cfg.num_key_value_heads, device=device, dtype=i32)
-        self.done = torch.zeros(cfg.num_key_value_heads, device=device, dtype=i32)  # qkv_attn
-        self.ctl = torch.zeros(3, device=device, dtype=i32)   # fused attn+o_proj counters
-        self.err = torch.zeros(1, device=device, dtype=i32)
         self.pos = torch.zeros(1, device=device, dtype=i32) if pos is None else pos
         if with_head:
             self.logits = torch.zeros(cfg.vocab_size, device=device, dtype=f32)
@@ -68,85 +64,6 @@ class DecodeBuffers:
             self.hist = torch.zeros(max_seq, device=device, dtype=i32)
             self.hist_len = torch.zeros(1, device=device, dtype=i32)
             self.slot = torch.zeros(1, device=device, dtype=torch.int64)
-
-
-class MegaPlan:
-    """Persistent decode megakernel (decode_mega.hip) over a run of local layers.
-
-    Holds the device layer table (weight + KV pointers of one session) and the
-    megakernel's exchange buffers.  One launch runs every layer of the run
-    (and, for the master's all-local case, ln_f + lm_head into the logits).
-    """
-
-    def __init__(self, stack: "LayerStack", layers: list[int]):
-        from ...ops import hip as K
-        cfg = stack.cfg
-        self.stack = stack
-        self.layers = list(layers)
-        self.grid = K.mega_grid()
-        nh, nkv, hd, H = (cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim,
-                          cfg.hidden_size)
-        self.KS = K.mega_ks(H, nh, nkv, hd, self.grid)
-        dev = stack.device
-        self.ws = K.mega_workspace(H, cfg.intermediate_size, nh, nkv, hd, self.KS, dev)
-        self.launch_ctr = torch.ones(1, device=dev, dtype=torch.int32)
-        self.err = torch.zeros(1, device=dev, dtype=torch.int32)
-        self._table = None
-        self._table_key = None
-        self.trace = None  # set to an int64 [4 * (5L + 1)] tensor to record phase timestamps
-
-    @staticmethod
-    def supported(cfg: LlamaConfig) -> bool:
-        from ...ops import hip as K
-        return K.mega_supported(cfg.hidden_size, cfg.intermediate_size, cfg.num_attention_heads,
-                                cfg.num_key_value_heads, cfg.head_dim, cfg.vocab_size)
-
-    def table(self, session: int) -> torch.Tensor:
-        kv = self.stack.cache(session)
-        key = (id(kv), kv.k.data_ptr())
-        if self._table is None or self._table_key != key:
-            rows = []
-            for li in self.layers:
-                w = self.stack.weights[li]
-                s = self.stack.slot_of[li]
-                rows.append([w.ln1.data_ptr(), w.wqkv.data_ptr(), w.wo.data_ptr(),
-                             w.ln2.data_ptr(), w.wg.data_ptr(), w.wu.data_ptr(),
-                             w.wd.data_ptr(), kv.k[s].data_ptr(), kv.v[s].data_ptr()])
-            self._table = torch.tensor(rows, dtype=torch.int64).to(self.stack.device)
-            self._table_key = key
-        return self._table
-
-    def launch(self, bufs: "DecodeBuffers", session: int = 0, head=None, logits=None) -> None:
-        """Run the layers on bufs.resid at device position bufs.pos (graph-capturable).
-
-        head = (norm_f, lm_head): also ln_f + lm_head into `logits` (bufs.resid is then
-        left unchanged: the final hidden state only exists on chip).
-        """
-        from ...ops import hip as K
-        cfg, st = self.stack.cfg, self.stack
-        tab = self.table(session)
-        K.decode_mega(tab, len(self.layers),
-                      (cfg.hidden_size, cfg.intermediate_size, cfg.num_attention_heads,
-                       cfg.num_key_value_heads, cfg.head_dim),
-                      st.max_seq, self.KS, cfg.rms_norm_eps, st.scale, st.inv_freq, bufs.pos,
-                      bufs.resid, self.ws, bufs.part, self.launch_ctr, self.err,
-                      st.dtype, norm_f=None if head is None else head[0],
-                      lm_head=None if head is None else head[1], logits=logits,
-                      grid=self.grid, trace=self.trace)
-
-    def check(self) -> None:
-        if int(self.err.item()) != 0:
-            raise RuntimeError("decode megakernel: grid barrier timed out (not all workgroups "
-                               "co-resident?); set CAKE_MEGA=0")
-
-
-def mega_enabled() -> bool:
-    """Opt-in (CAKE_MEGA=1), experimental: measured slower than the multi-kernel
-    hipGraph on MI355X (8B: 257 vs 331 tok/s) — see decode_mega.hip — and one
-    intermittent numerics mismatch was observed in its GPU tests
-    (tests/test_mega_gpu.py); not for production use."""
-    import os
-    return os.environ.get("CAKE_MEGA", "0") == "1"
 
 
 class LayerStack:
@@ -169,25 +86,6 @@ class LayerStack:
         self._sessions: OrderedDict[int, KVCache] = OrderedDict()
         self._decode_bufs: DecodeBuffers | None = None
         self._hostpos_bufs: DecodeBuffers | None = None
-        # fused attention + o_proj decode kernel (decode_fused.hip), opt-in with
-        # CAKE_FUSED=1 (2 = without weight prefetch).  Measured slower than the
-        # two-kernel path on MI355X (profiles/r1_fused_ao_sweep.txt), so off by default.
-        import os
-        from ...ops.hip import attn_oproj_supported
-        mode = os.environ.get("CAKE_FUSED", "0")
-        self.fused_prefetch = mode != "2"
-        self.fused_grid = int(os.environ.get("CAKE_AO_GRID", "0")) or None
-        self.fused_sleep = int(os.environ.get("CAKE_AO_SLEEP", "1"))
-        # decode attention warms the o_proj weights into the Infinity Cache with
-        # CAKE_ATTN_PF_ROWS extra grid rows (0 = off)
-        self.attn_pf_rows = int(os.environ.get("CAKE_ATTN_PF_ROWS", "0"))
-        # decode graphs for positions < qkv_attn_max_t fold attention into the QKV
-        # launch (one workgroup per kv head does it); 0 disables.  Opt-in: measured
-        # slower at every context length (profiles/r1_qkv_attn_sweep.txt)
-        self.qkv_attn_max_t = int(os.environ.get("CAKE_QKV_ATTN_MAX_T", "0"))
-        self.fused_ao = (backend == "hip" and mode != "0" and
-                         attn_oproj_supported(cfg.num_attention_heads, cfg.num_key_value_heads,
-                                              cfg.head_dim, cfg.hidden_size))
 
     # ------------------------------------------------------------------ sessions
     def cache(self, session: int = 0) -> KVCache:
@@ -244,46 +142,22 @@ class LayerStack:
         kv.length = max(kv.length, pos0 + T)
         return hidden
 
-    def qkv_attn_ok(self) -> bool:
-        """Whether the one-launch QKV+attention kernel (short contexts) applies."""
-        from ...ops.hip import qkv_attn_supported
-        c = self.cfg
-        return (self.backend == "hip" and not self.fused_ao and self.qkv_attn_max_t > 0 and
-                qkv_attn_supported(c.num_attention_heads, c.num_key_value_heads, c.head_dim))
-
-    def decode_step(self, bufs: DecodeBuffers, layers: list[int], session: int = 0,
-                    short_ctx: bool = False) -> None:
-        """Graph-capturable T=1 step over bufs.resid at device position bufs.pos (hip only).
-
-        short_ctx: the caller guarantees pos < qkv_attn_max_t for every replay, so
-        each layer's attention runs as the tail of its QKV launch (qkv_attn).
-        """
+    def decode_step(self, bufs: DecodeBuffers, layers: list[int], session: int = 0) -> None:
+        """Graph-capturable T=1 step over bufs.resid at device position bufs.pos (hip only):
+        five launches per layer (QKV+RoPE+KV write, attention, o_proj+residual,
+        norm+gate/up+SwiGLU, down_proj+residual)."""
         from ...ops import hip as K
         kv = self.cache(session)
         cfg = self.cfg
-        fuse_qa = short_ctx and self.qkv_attn_ok()
         for li in layers:
             w = self.weights[li]
             s = self.slot_of[li]
             kc, vc = kv.k[s], kv.v[s]
-            if fuse_qa:
-                K.qkv_attn(bufs.resid, w.ln1, cfg.rms_norm_eps, w.wq, w.wk, w.wv, self.inv_freq,
-                           bufs.pos, bufs.q, kc, vc, bufs.done, bufs.attn_out, self.scale)
-                K.gemv(bufs.attn_out, w.wo, bufs.resid, accumulate=True)
-                K.swiglu(bufs.resid, w.ln2, cfg.rms_norm_eps, w.wg, w.wu, bufs.act)
-                K.gemv(bufs.act, w.wd, bufs.resid, accumulate=True)
-                continue
             K.qkv_rope(bufs.resid, w.ln1, cfg.rms_norm_eps, w.wq, w.wk, w.wv, self.inv_freq,
-                       bufs.pos, bufs.q, kc, vc, rearm=bufs.ctl if self.fused_ao else None)
-            if self.fused_ao:
-                K.attn_oproj(bufs.q, kc, vc, bufs.pos, self.scale, bufs.part, bufs.tickets,
-                             bufs.ctl, bufs.attn_out, w.wo, bufs.resid, bufs.err,
-                             prefetch=self.fused_prefetch, grid=self.fused_grid,
-                             sleep=self.fused_sleep)
-            else:
-                K.attn_decode(bufs.q, kc, vc, bufs.pos, self.scale, bufs.part, bufs.tickets,
-                              bufs.attn_out, prefetch=w.wo, prefetch_rows=self.attn_pf_rows)
-                K.gemv(bufs.attn_out, w.wo, bufs.resid, accumulate=True)
+                       bufs.pos, bufs.q, kc, vc)
+            K.attn_decode(bufs.q, kc, vc, bufs.pos, self.scale, bufs.part, bufs.tickets,
+                          bufs.attn_out)
+            K.gemv(bufs.attn_out, w.wo, bufs.resid, accumulate=True)
             K.swiglu(bufs.resid, w.ln2, cfg.rms_norm_eps, w.wg, w.wu, bufs.act)
             K.gemv(bufs.act, w.wd, bufs.resid, accumulate=True)
 

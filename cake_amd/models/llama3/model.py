@@ -19,7 +19,7 @@ from dataclasses import dataclass, field
 import torch
 
 from ...ops import reference as R
-from .blocks import DecodeBuffers, LayerStack, MegaPlan, mega_enabled
+from .blocks import DecodeBuffers, LayerStack
 from .config import LlamaConfig
 from .weights import HeadWeights, layer_name
 
@@ -147,31 +147,16 @@ class DeviceDecoder:
         self.use_graph = use_graph
         self.bufs: DecodeBuffers = model.stack.decode_buffers(with_head=True)
         self.graph: torch.cuda.CUDAGraph | None = None
-        # short-context variant: attention folded into each layer's QKV launch,
-        # replayed while every position of the launch is < qkv_attn_max_t
-        self.graph_short: torch.cuda.CUDAGraph | None = None
         self.host_pos = 0  # device position of the next step (tracked on the host)
         self._layers = list(range(model.cfg.num_hidden_layers))
-        # the whole step's layers + lm_head as ONE persistent launch (decode_mega.hip)
-        self.mega: MegaPlan | None = None
-        if mega_enabled() and MegaPlan.supported(model.cfg):
-            self.mega = MegaPlan(model.stack, self._layers)
-        self.short_ok = self.mega is None and model.stack.qkv_attn_ok()
-
-    def _short(self) -> bool:
-        """All positions of the next launch are short enough for qkv_attn."""
-        return self.short_ok and self.host_pos + self.k <= self.m.stack.qkv_attn_max_t
 
     # the captured body
-    def _step_body(self, short: bool = False) -> None:
+    def _step_body(self) -> None:
         from ...ops import hip as K
         b, m = self.bufs, self.m
         K.embed(m.head.embed, b.tok, b.resid)
-        if self.mega is not None:
-            self.mega.launch(b, m.session, head=(m.head.norm, m.head.lm_head), logits=b.logits)
-        else:
-            m.stack.decode_step(b, self._layers, m.session, short_ctx=short)
-            K.norm_gemv_f32(b.resid, m.head.norm, m.cfg.rms_norm_eps, m.head.lm_head, b.logits)
+        m.stack.decode_step(b, self._layers, m.session)
+        K.norm_gemv_f32(b.resid, m.head.norm, m.cfg.rms_norm_eps, m.head.lm_head, b.logits)
         if self.penalty != 1.0:
             K.repeat_penalty(b.logits, b.hist, b.hist_len, self.last_n, self.penalty)
         if self.greedy:
@@ -186,27 +171,19 @@ class DeviceDecoder:
         # warm the kernels once outside capture on scratch state, then restore
         saved = [t.clone() for t in (self.bufs.tok, self.bufs.pos, self.bufs.hist_len)]
         hist = self.bufs.hist.clone()
-        variants = [False, True] if self.short_ok else [False]
         with torch.cuda.stream(s):
-            for short in variants:
-                self._step_body(short)
+            self._step_body()
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
-        if self.mega is not None:
-            self.mega.check()
         for t, v in zip((self.bufs.tok, self.bufs.pos, self.bufs.hist_len), saved):
             t.copy_(v)
         self.bufs.hist.copy_(hist)
         self.bufs.slot.zero_()
-        for short in variants:
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                for _ in range(self.k):
-                    self._step_body(short)
-            if short:
-                self.graph_short = g
-            else:
-                self.graph = g
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(self.k):
+                self._step_body()
+        self.graph = g
         torch.cuda.synchronize()
 
     def start(self, prompt: list[int]) -> int:
@@ -248,11 +225,10 @@ class DeviceDecoder:
 
     def launch(self) -> None:
         """Enqueue `self.k` decode steps (one graph replay; async)."""
-        short = self._short()
         if self.graph is not None:
-            (self.graph_short if short and self.graph_short is not None else self.graph).replay()
+            self.graph.replay()
         else:
-            self._step_body(short)
+            self._step_body()
         if self.greedy:  # greedy steps advance pos on the device; sampled ones via push()
             self.host_pos += self.k
 

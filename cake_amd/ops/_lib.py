@@ -25,14 +25,12 @@ Z = C.c_size_t
 
 # name -> argtypes (all return int hipError_t)
 _SIGS = {
-    "cake_qkv_rope": [I, P, P, F, P, P, P, I, I, I, I, P, P, P, P, P, I, P, P],
-    "cake_qkv_attn": [I, P, P, F, P, P, P, I, I, I, I, P, P, P, P, P, I, P, P, F, P],
+    "cake_qkv_rope": [I, P, P, F, P, P, P, I, I, I, I, P, P, P, P, P, I, P],
     "cake_swiglu": [I, P, P, F, P, P, I, I, P, P],
     "cake_gemv_x16": [I, P, P, I, I, P, I, P],
     "cake_gemv_norm_f32": [I, P, P, F, P, I, I, P, P],
     "cake_attn_decode": [I, P, P, P, P, I, I, I, I, F, P, P, P, P],
-    "cake_attn_decode_pf": [I, P, P, P, P, I, I, I, I, F, P, P, P, P, Z, I, P],
-    "cake_attn_prefill": [I, P, P, P, I, I, I, I, I, I, F, P, P],
+    "cake_attn_set_min_keys": [I],
     "cake_embed": [I, P, P, I, I, P, P],
     "cake_rmsnorm": [I, P, P, F, I, I, P, P],
     "cake_rope_kv": [I, P, P, P, I, I, I, I, I, I, P, I, I, P, P, P],
@@ -98,16 +96,4 @@ _SIGS.update({
     "cake_layernorm": [I, P, P, P, C.c_longlong, I, F, P, P],
     "cake_geglu": [I, P, C.c_longlong, I, P, P],
     "cake_conv2d_nhwc": [I, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, P],
-})
-
-_SIGS.update({
-    "cake_attn_oproj": [I, P, P, P, P, I, I, I, I, F, P, P, P, P, P, I, P, P, I, I, I, P],
-})
-
-_SIGS.update({
-    "cake_mega_grid": [],
-    "cake_mega_supported": [I, I, I, I, I, I],
-    "cake_mega_ks": [I, I, I, I, I],
-    "cake_decode_mega": [I, P, I, I, I, I, I, I, I, I, F, F, P, P, P, P, P, P, P, P, P, P, P,
-                         P, P, P, I, P, I, C.c_double, P, P],
 })

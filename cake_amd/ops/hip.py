@@ -46,7 +46,7 @@ def _req(t: torch.Tensor, name: str, *, dtype=None, numel=None, shape=None) -> N
 # decode (batch 1) fused projections
 # ---------------------------------------------------------------------------
 
-def qkv_rope(resid, norm_w, eps, wq, wk, wv, inv_freq, pos, q_out, kcache, vcache, rearm=None):
+def qkv_rope(resid, norm_w, eps, wq, wk, wv, inv_freq, pos, q_out, kcache, vcache):
     """rmsnorm(resid) -> q/k/v GEMV -> RoPE(pos) -> q_out f32, k/v into cache[:, pos].
 
     kcache/vcache: [nkv, S, hd] (one layer). pos: int32 device scalar.
@@ -69,46 +69,8 @@ def qkv_rope(resid, norm_w, eps, wq, wk, wv, inv_freq, pos, q_out, kcache, vcach
         raise ValueError("hidden size must be a multiple of 8")
     check(kernels().cake_qkv_rope(_dt(wq), _p(resid), _p(norm_w), float(eps), _p(wq), _p(wk),
                                   _p(wv), K, nh, nkv, hd, _p(inv_freq), _p(pos), _p(q_out),
-                                  _p(kcache), _p(vcache), S,
-                                  None if rearm is None else rearm[1:].data_ptr(), _stream()),
+                                  _p(kcache), _p(vcache), S, _stream()),
           "qkv_rope")
-
-
-def qkv_attn_supported(nh: int, nkv: int, hd: int) -> bool:
-    return hd in (64, 128) and nkv > 0 and nh % nkv == 0 and (nh // nkv) in (1, 2, 4, 8)
-
-
-def qkv_attn(resid, norm_w, eps, wq, wk, wv, inv_freq, pos, q_out, kcache, vcache, done,
-             attn_out, scale):
-    """qkv_rope + the decode attention of the token at `pos`, in one launch.
-
-    The last workgroup of each GQA group runs that group's attention over
-    positions [0, pos] (see gemv.hip qkv_attn_kernel).  done: int32 [nkv],
-    zero-initialised once (re-armed by the kernel); attn_out: [nh*hd] 16-bit.
-    """
-    K = resid.numel()
-    nkv, S, hd = kcache.shape
-    nh = wq.shape[0] // hd
-    dt = wq.dtype
-    _req(resid, "resid", dtype=torch.float32)
-    _req(norm_w, "norm_w", dtype=dt, shape=(K,))
-    _req(wq, "wq", dtype=dt, shape=(nh * hd, K))
-    _req(wk, "wk", dtype=dt, shape=(nkv * hd, K))
-    _req(wv, "wv", dtype=dt, shape=(nkv * hd, K))
-    _req(inv_freq, "inv_freq", dtype=torch.float32, shape=(hd // 2,))
-    _req(pos, "pos", dtype=torch.int32, numel=1)
-    _req(q_out, "q_out", dtype=torch.float32, numel=nh * hd)
-    _req(kcache, "kcache", dtype=dt)
-    _req(vcache, "vcache", dtype=dt, shape=kcache.shape)
-    _req(done, "done", dtype=torch.int32, numel=nkv)
-    _req(attn_out, "attn_out", dtype=dt, numel=nh * hd)
-    if K % 8 or not qkv_attn_supported(nh, nkv, hd):
-        raise ValueError(f"qkv_attn: unsupported shape K={K} nh={nh} nkv={nkv} hd={hd}")
-    check(kernels().cake_qkv_attn(_dt(wq), _p(resid), _p(norm_w), float(eps), _p(wq), _p(wk),
-                                  _p(wv), K, nh, nkv, hd, _p(inv_freq), _p(pos), _p(q_out),
-                                  _p(kcache), _p(vcache), S, _p(done), _p(attn_out),
-                                  float(scale), _stream()),
-          "qkv_attn")
 
 
 def swiglu(resid, norm_w, eps, wg, wu, act):
@@ -148,37 +110,25 @@ def norm_gemv_f32(resid, norm_w, eps, w, out):
                                        _p(out), _stream()), "gemv_norm_f32")
 
 
-def attn_decode(q, kcache, vcache, pos, scale, part, tickets, out, prefetch=None,
-                prefetch_rows=0):
+def attn_decode(q, kcache, vcache, pos, scale, part, tickets, out):
     """Split-K GQA decode attention for the token at device position `pos`.
 
-    part: f32 workspace (:func:`attn_workspace_numel`); tickets: int32 [nkv],
-    zero-initialised once and re-armed by the kernel itself.  prefetch: optional
-    contiguous tensor (the next GEMV's weights) that `prefetch_rows` extra grid
-    rows read into the Infinity Cache while the attention runs (read-only).
+    The split count is derived on the device from the live length, so one
+    captured launch serves every position.  part: f32 workspace
+    (:func:`attn_workspace_numel`); tickets: int32 [nkv], zero-initialised once
+    and re-armed by the kernel itself.
     """
     nkv, S, hd = kcache.shape
     nh = q.numel() // hd
-    nsplit = (S + 63) // 64
     _req(q, "q", dtype=torch.float32)
     _req(kcache, "kcache")
     _req(vcache, "vcache", dtype=kcache.dtype, shape=kcache.shape)
     _req(pos, "pos", dtype=torch.int32, numel=1)
-    _req(part, "part", dtype=torch.float32, numel=nh * nsplit * (hd + 2))
+    _req(part, "part", dtype=torch.float32, numel=attn_workspace_numel(nh, hd, S))
     _req(out, "out", dtype=kcache.dtype, numel=nh * hd)
     _req(tickets, "tickets", dtype=torch.int32, numel=nkv)
     if hd not in (64, 128) or nh % nkv or (nh // nkv) not in (1, 2, 4, 8):
         raise ValueError(f"unsupported attention shape nh={nh} nkv={nkv} hd={hd}")
-    if prefetch is not None and prefetch_rows > 0:
-        _req(prefetch, "prefetch")
-        nbytes = prefetch.numel() * prefetch.element_size()
-        nbytes -= nbytes % 16
-        check(kernels().cake_attn_decode_pf(_dt(kcache), _p(q), _p(kcache), _p(vcache), _p(pos),
-                                            S, nh, nkv, hd, float(scale), _p(part), _p(tickets),
-                                            _p(out), _p(prefetch), nbytes, int(prefetch_rows),
-                                            _stream()),
-              "attn_decode_pf")
-        return
     check(kernels().cake_attn_decode(_dt(kcache), _p(q), _p(kcache), _p(vcache), _p(pos), S, nh,
                                      nkv, hd, float(scale), _p(part), _p(tickets), _p(out),
                                      _stream()),
@@ -186,7 +136,14 @@ def attn_decode(q, kcache, vcache, pos, scale, part, tickets, out, prefetch=None
 
 
 def attn_workspace_numel(nh: int, hd: int, S: int) -> int:
-    return nh * ((S + 63) // 64) * (hd + 2)
+    """Partials of at most 64 splits per head (attention.hip kMaxSplit)."""
+    del S
+    return nh * 64 * (hd + 2)
+
+
+def attn_set_min_keys(n: int) -> None:
+    """Minimum keys per decode-attention split (multiple of 64; default 64)."""
+    check(kernels().cake_attn_set_min_keys(int(n)), "attn_set_min_keys")
 
 
 # ---------------------------------------------------------------------------
@@ -239,21 +196,6 @@ def rope_kv(q, k, v, inv_freq, pos0: int, kcache, vcache):
     _req(vcache, "vcache", shape=kcache.shape)
     check(kernels().cake_rope_kv(_dt(q), _p(q), _p(k), _p(v), ldq, ld, T, nh, nkv, hd, _p(inv_freq),
                                  int(pos0), S, _p(kcache), _p(vcache), _stream()), "rope_kv")
-
-
-def attn_prefill(q, kcache, vcache, pos0: int, scale: float, out):
-    nkv, S, hd = kcache.shape
-    T = q.shape[0]
-    nh = q.shape[1] // hd
-    if pos0 < 0 or pos0 + T > S:
-        raise ValueError("positions exceed cache length")
-    if hd not in (64, 128) or nh % nkv:
-        raise ValueError(f"unsupported attention shape nh={nh} nkv={nkv} hd={hd}")
-    _req(q, "q", dtype=kcache.dtype)
-    _req(out, "out", dtype=kcache.dtype, shape=q.shape)
-    check(kernels().cake_attn_prefill(_dt(q), _p(q), _p(kcache), _p(vcache), int(pos0), T, S,
-                                      nh, nkv, hd, float(scale), _p(out), _stream()),
-          "attn_prefill")
 
 
 def silu_mul(g, u, out):
@@ -523,112 +465,3 @@ def conv2d_nhwc(x, w, bias=None, *, stride: int = 1, pad: int = 1, up: bool = Fa
                                      _stream()),
           "conv2d_nhwc")
     return out
-
-
-def attn_oproj_supported(nh: int, nkv: int, hd: int, H: int) -> bool:
-    return hd == 128 and nh % nkv == 0 and nh // nkv in (4, 8) and 4096 <= nh * hd <= 8192
-
-
-def attn_oproj(q, kcache, vcache, pos, scale, part, tickets, ctl, attn_out, wo, resid, err,
-               prefetch: bool = True, grid: int | None = None, sleep: int = 1):
-    """Fused decode attention + o_proj + residual (decode_fused.hip).
-
-    ctl: int32[3] (ctl[1] must be 0 at launch: qkv_rope(rearm=ctl) zeroes it); err: int32[1].
-    """
-    nkv, S, hd = kcache.shape
-    nh = q.numel() // hd
-    N, K = wo.shape
-    if not attn_oproj_supported(nh, nkv, hd, N) or K != nh * hd:
-        raise ValueError(f"attn_oproj: unsupported shape nh={nh} nkv={nkv} hd={hd} wo={tuple(wo.shape)}")
-    _req(q, "q", dtype=torch.float32)
-    _req(kcache, "kcache")
-    _req(vcache, "vcache", dtype=kcache.dtype, shape=kcache.shape)
-    _req(pos, "pos", dtype=torch.int32, numel=1)
-    _req(part, "part", dtype=torch.float32, numel=nh * ((S + 63) // 64) * (hd + 2))
-    _req(tickets, "tickets", dtype=torch.int32, numel=nkv)
-    _req(ctl, "ctl", dtype=torch.int32, numel=3)
-    _req(attn_out, "attn_out", dtype=kcache.dtype, numel=nh * hd)
-    _req(wo, "wo", dtype=kcache.dtype)
-    _req(resid, "resid", dtype=torch.float32, numel=N)
-    _req(err, "err", dtype=torch.int32, numel=1)
-    if grid is None:
-        grid = max(1, ((N + 1) // 2 + 3) // 4)
-    check(kernels().cake_attn_oproj(_dt(kcache), _p(q), _p(kcache), _p(vcache), _p(pos), S, nh,
-                                    nkv, hd, float(scale), _p(part), _p(tickets), _p(ctl),
-                                    _p(attn_out), _p(wo), N, _p(resid), _p(err), int(grid),
-                                    int(prefetch), int(sleep), _stream()),
-          "attn_oproj")
-
-
-# ---------------------------------------------------------------------------
-# persistent decode megakernel (decode_mega.hip)
-# ---------------------------------------------------------------------------
-
-def mega_supported(H: int, I: int, nh: int, nkv: int, hd: int, V: int = 2) -> bool:
-    return bool(kernels().cake_mega_supported(H, I, nh, nkv, hd, V))
-
-
-def mega_grid() -> int:
-    """Workgroups of one launch = CUs of the current device (one per CU)."""
-    return int(kernels().cake_mega_grid())
-
-
-def mega_ks(H: int, nh: int, nkv: int, hd: int, grid: int = 0) -> int:
-    return int(kernels().cake_mega_ks(H, nh, nkv, hd, grid))
-
-
-def decode_mega(layer_table, L: int, cfg_dims: tuple, S: int, KS: int, eps: float, scale: float,
-                inv_freq, pos, resid, ws: dict, attn_part, launch_ctr, err, dtype,
-                norm_f=None, lm_head=None, logits=None, grid: int = 0, timeout_s: float = 0.25,
-                trace=None):
-    """All `L` decode layers (+ optional ln_f/lm_head -> logits) in one launch.
-
-    layer_table: int64 device tensor [L, 9] of pointers (ln1, wqkv, wo, ln2, wg, wu, wd,
-    kcache, vcache).  ws: the tagged exchange buffers (see :func:`mega_workspace`).
-    launch_ctr (int32 [1]) is advanced by the kernel; err (int32 [1]) is set to 1 if a
-    dependency wait timed out (the launch then exits without hanging).
-    """
-    H, I, nh, nkv, hd = cfg_dims
-    nq, nk = nh * hd, nkv * hd
-    f32, i32 = torch.float32, torch.int32
-    _req(layer_table, "layer_table", dtype=torch.int64, shape=(L, 9))
-    _req(inv_freq, "inv_freq", dtype=f32, shape=(hd // 2,))
-    _req(pos, "pos", dtype=i32, numel=1)
-    _req(resid, "resid", dtype=f32, numel=H)
-    _req(ws["yo"], "yo_t", dtype=torch.int64, numel=H)
-    _req(ws["yd"], "yd_t", dtype=torch.int64, numel=H)
-    _req(ws["qkv"], "qkv_t", dtype=torch.int64, numel=KS * (nq + 2 * nk))
-    _req(ws["attn"], "attn_t", dtype=i32, numel=nq)
-    _req(ws["act"], "act_t", dtype=i32, numel=I)
-    _req(attn_part, "attn_part", dtype=f32, numel=nh * ((S + 63) // 64) * (hd + 2))
-    _req(ws["tickets"], "tickets", dtype=i32, numel=nh)
-    _req(launch_ctr, "launch_ctr", dtype=i32, numel=1)
-    _req(err, "err", dtype=i32, numel=1)
-    V = 0
-    if lm_head is not None:
-        V = lm_head.shape[0]
-        _req(lm_head, "lm_head", dtype=dtype, shape=(V, H))
-        _req(norm_f, "norm_f", dtype=dtype, shape=(H,))
-        _req(logits, "logits", dtype=f32, numel=V)
-    if trace is not None:
-        _req(trace, "trace", dtype=torch.int64, numel=8 * (5 * L + 1) * (grid or mega_grid()))
-    if not mega_supported(H, I, nh, nkv, hd, V if V else 2):
-        raise ValueError(f"decode_mega: unsupported shape H={H} I={I} nh={nh} nkv={nkv} hd={hd}")
-    check(kernels().cake_decode_mega(
-        _DT[dtype], _p(layer_table), L, H, I, nh, nkv, hd, S, KS, float(eps), float(scale),
-        _p(inv_freq), _p(pos), _p(resid), _p(ws["yo"]), _p(ws["yd"]), _p(ws["qkv"]),
-        _p(ws["attn"]), _p(ws["act"]), _p(attn_part), _p(ws["tickets"]), _p(launch_ctr), _p(err),
-        _p(norm_f), _p(lm_head), V, _p(logits), int(grid), float(timeout_s), _p(trace),
-        _stream()), "decode_mega")
-
-
-def mega_workspace(H: int, I: int, nh: int, nkv: int, hd: int, KS: int, device) -> dict:
-    """Tagged exchange buffers of the megakernel (zero = no valid tag)."""
-    i64, i32 = torch.int64, torch.int32
-    R = (nh + 2 * nkv) * hd
-    return {"yo": torch.zeros(H, dtype=i64, device=device),
-            "yd": torch.zeros(H, dtype=i64, device=device),
-            "qkv": torch.zeros(KS * R, dtype=i64, device=device),
-            "attn": torch.zeros(nh * hd, dtype=i32, device=device),
-            "act": torch.zeros(I, dtype=i32, device=device),
-            "tickets": torch.zeros(nh, dtype=i32, device=device)}

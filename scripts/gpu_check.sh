@@ -18,6 +18,17 @@ if [[ $STEPS == *bench* ]]; then
   b=$?; cat gpurun_out/bench.json; tail -3 gpurun_out/bench.err
   if [[ $b -ne 0 ]]; then echo "bench rc=$b -> stop"; exit $b; fi
 fi
+if [[ $STEPS == *extra* ]]; then
+  # EXTRA_BENCH="args one;args two": further bench configurations, one line each
+  IFS=';' read -ra XB <<< "${EXTRA_BENCH:-}"
+  i=0
+  for args in "${XB[@]}"; do
+    i=$((i+1))
+    timeout -k 10 ${BENCH_TIMEOUT:-300} python bench.py $args > gpurun_out/bench_x$i.json 2> gpurun_out/bench_x$i.err
+    b=$?; echo "[$args]"; cat gpurun_out/bench_x$i.json; tail -2 gpurun_out/bench_x$i.err
+    if [[ $b -ne 0 ]]; then echo "bench rc=$b -> stop"; exit $b; fi
+  done
+fi
 if [[ $STEPS == *prof* ]]; then
   cd /tmp && export TMPDIR=/tmp
   timeout -k 10 ${PROF_TIMEOUT:-300} rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 32 --warmup 4 ${BENCH_ARGS:-} > "$GRAFT_REPO_ROOT/gpurun_out/prof.log" 2>&1

@@ -93,48 +93,17 @@ def test_qkv_rope(cuda, dt, H, nh, nkv, hd, pos):
 
 
 @pytest.mark.parametrize("dt", DTYPES)
-@pytest.mark.parametrize("H,nh,nkv,hd,pos", [(4096, 32, 8, 128, 0), (4096, 32, 8, 128, 63),
-                                             (4096, 32, 8, 128, 64), (4096, 32, 8, 128, 300),
-                                             (8192, 64, 8, 128, 100), (1024, 16, 16, 64, 70),
-                                             (1024, 8, 4, 64, 130), (512, 4, 1, 128, 9)])
-def test_qkv_attn(cuda, dt, H, nh, nkv, hd, pos):
-    """One-launch QKV+RoPE+KV write+attention == qkv_rope then the f32 attention reference."""
-    from cake_amd.ops import hip as K_
-    torch.manual_seed(7)
-    S = 512
-    resid = torch.randn(H, device=cuda)
-    nw = (1 + 0.1 * torch.randn(H, device=cuda)).to(dt)
-    wq, wk, wv = (_rand(n * hd, H, dt=dt, std=0.05) for n in (nh, nkv, nkv))
-    invf = R.inv_freq(hd, 500000.0).to(cuda)
-    kc = _rand(nkv, S, hd, dt=dt)  # history rows [0, pos) are arbitrary
-    vc = _rand(nkv, S, hd, dt=dt)
-    kc2, vc2 = kc.clone(), vc.clone()
-    p = torch.tensor([pos], dtype=torch.int32, device=cuda)
-    q, q2 = torch.empty(nh * hd, device=cuda), torch.empty(nh * hd, device=cuda)
-    done = torch.zeros(nkv, dtype=torch.int32, device=cuda)
-    out = torch.zeros(nh * hd, device=cuda, dtype=dt)
-    scale = 1 / math.sqrt(hd)
-    for _ in range(2):  # second launch checks the done counters were re-armed
-        out.zero_()
-        K_.qkv_attn(resid, nw, 1e-5, wq, wk, wv, invf, p, q, kc, vc, done, out, scale)
-        assert int(done.abs().sum()) == 0
-    K_.qkv_rope(resid, nw, 1e-5, wq, wk, wv, invf, p, q2, kc2, vc2)
-    torch.testing.assert_close(q, q2, rtol=0, atol=0)
-    assert torch.equal(kc, kc2) and torch.equal(vc, vc2)
-    Tk = pos + 1
-    ref = R.attention(q2.view(1, nh, hd), kc2[:, :Tk].transpose(0, 1).float(),
-                      vc2[:, :Tk].transpose(0, 1).float(), pos).reshape(-1)
-    torch.testing.assert_close(out.float(), ref, **_tol(dt))
-
-
-@pytest.mark.parametrize("dt", DTYPES)
-@pytest.mark.parametrize("nh,nkv,hd,pos", [(32, 8, 128, 0), (32, 8, 128, 63), (32, 8, 128, 64),
-                                           (32, 8, 128, 1000), (64, 8, 128, 300),
-                                           (4, 1, 64, 17), (8, 8, 64, 200)])
-def test_attn_decode(cuda, dt, nh, nkv, hd, pos):
+@pytest.mark.parametrize("nh,nkv,hd,pos,S", [(32, 8, 128, 0, 2048), (32, 8, 128, 63, 2048),
+                                             (32, 8, 128, 64, 2048), (32, 8, 128, 1000, 2048),
+                                             (32, 8, 128, 2047, 2048), (64, 8, 128, 300, 2048),
+                                             (4, 1, 64, 17, 2048), (8, 8, 64, 200, 2048),
+                                             (16, 4, 128, 70, 100), (32, 8, 128, 8190, 8192)])
+@pytest.mark.parametrize("min_keys", [64, 256])
+def test_attn_decode(cuda, dt, nh, nkv, hd, pos, S, min_keys):
+    """Split-K decode attention (split count derived on device from pos) vs f32 attention;
+    S not a multiple of 64, more than 64 splits' worth of keys (S = 8192: 128-key splits)."""
     from cake_amd.ops import hip as K_
     torch.manual_seed(4)
-    S = 2048
     kc = _rand(nkv, S, hd, dt=dt)
     vc = _rand(nkv, S, hd, dt=dt)
     q = torch.randn(nh * hd, device=cuda)
@@ -142,23 +111,18 @@ def test_attn_decode(cuda, dt, nh, nkv, hd, pos):
     part = torch.empty(K_.attn_workspace_numel(nh, hd, S), device=cuda)
     out = torch.empty(nh * hd, device=cuda, dtype=dt)
     tickets = torch.zeros(nkv, dtype=torch.int32, device=cuda)
-    for _ in range(2):  # second call checks the tickets were re-armed
-        out.zero_()
-        K_.attn_decode(q, kc, vc, p, 1 / math.sqrt(hd), part, tickets, out)
-        assert int(tickets.abs().sum()) == 0
+    K_.attn_set_min_keys(min_keys)
+    try:
+        for _ in range(2):  # second call checks the tickets were re-armed
+            out.zero_()
+            K_.attn_decode(q, kc, vc, p, 1 / math.sqrt(hd), part, tickets, out)
+            assert int(tickets.abs().sum()) == 0
+    finally:
+        K_.attn_set_min_keys(64)
     Tk = pos + 1
     ref = R.attention(q.view(1, nh, hd), kc[:, :Tk].transpose(0, 1), vc[:, :Tk].transpose(0, 1),
                       pos).reshape(-1)
     torch.testing.assert_close(out.float(), ref, **_tol(dt))
-    # Infinity-Cache warm-up rows: read-only, same output, weights untouched
-    wo = _rand(nh * hd, 1000, dt=dt)
-    wo_before = wo.clone()
-    out_pf = torch.zeros_like(out)
-    K_.attn_decode(q, kc, vc, p, 1 / math.sqrt(hd), part, tickets, out_pf, prefetch=wo,
-                   prefetch_rows=7)
-    assert int(tickets.abs().sum()) == 0
-    torch.testing.assert_close(out_pf, out, rtol=0, atol=0)
-    assert torch.equal(wo, wo_before)
 
 
 @pytest.mark.parametrize("dt", DTYPES)
@@ -183,8 +147,9 @@ def test_rope_kv_and_prefill_attention(cuda, dt, T, pos0, nh, nkv, hd):
     torch.testing.assert_close(kc[:, pos0:pos0 + T].float().transpose(0, 1), kr, **_tol(dt))
     torch.testing.assert_close(vc[:, pos0:pos0 + T].transpose(0, 1).reshape(T, -1), v)
     out = torch.empty_like(q_in)
-    K_.attn_prefill(q_in, kc, vc, pos0, 1 / math.sqrt(hd), out)
     Tk = pos0 + T
+    K_.flash_attn(q_in.view(1, T, nh, hd).transpose(1, 2), kc[None, :, :Tk], vc[None, :, :Tk],
+                  out.view(1, T, nh, hd).transpose(1, 2), 1 / math.sqrt(hd), causal=True, pos0=pos0)
     ref = R.attention(q_in.view(T, nh, hd), kc[:, :Tk].transpose(0, 1), vc[:, :Tk].transpose(0, 1),
                       pos0)
     torch.testing.assert_close(out.float().view(T, nh, hd), ref, **_tol(dt))
@@ -242,40 +207,6 @@ def test_penalty_argmax_finalize(cuda):
     K_.argmax(logits, slot)
     K_.finalize_token(slot, tok, hist, hist_len, pos)
     assert int(tok) == 0
-
-
-@pytest.mark.parametrize("dt", DTYPES)
-@pytest.mark.parametrize("nh,nkv,H", [(32, 8, 4096), (64, 8, 8192)])
-def test_attn_oproj_fused_matches_unfused(cuda, dt, nh, nkv, H):
-    """decode_fused.hip == attn_decode + gemv(accumulate), over several positions and
-    back-to-back launches, including multi-split contexts.  The done-counter is
-    re-armed before each launch (the QKV kernel does this in the decode step)."""
-    from cake_amd.ops import hip as K_
-    torch.manual_seed(8)
-    hd, S = 128, 1024
-    kc = _rand(nkv, S, hd, dt=dt)
-    vc = _rand(nkv, S, hd, dt=dt)
-    wo = _rand(H, nh * hd, dt=dt, std=0.02)
-    part = torch.empty(K_.attn_workspace_numel(nh, hd, S), device=cuda)
-    tickets = torch.zeros(nkv, dtype=torch.int32, device=cuda)
-    ctl = torch.zeros(3, dtype=torch.int32, device=cuda)
-    err = torch.zeros(1, dtype=torch.int32, device=cuda)
-    for pos in (0, 63, 64, 200, 1023):
-        q = torch.randn(nh * hd, device=cuda)
-        p = torch.tensor([pos], dtype=torch.int32, device=cuda)
-        r0 = torch.randn(H, device=cuda)
-        ref_att = torch.empty(nh * hd, device=cuda, dtype=dt)
-        K_.attn_decode(q, kc, vc, p, 1 / math.sqrt(hd), part, tickets, ref_att)
-        ref = r0.clone()
-        K_.gemv(ref_att, wo, ref, accumulate=True)
-        out = r0.clone()
-        att = torch.empty(nh * hd, device=cuda, dtype=dt)
-        ctl.zero_()
-        K_.attn_oproj(q, kc, vc, p, 1 / math.sqrt(hd), part, tickets, ctl, att, wo, out, err)
-        torch.cuda.synchronize()
-        assert int(err) == 0 and int(ctl[1]) == nkv and int(tickets.abs().sum()) == 0
-        torch.testing.assert_close(att.float(), ref_att.float())
-        torch.testing.assert_close(out, ref, atol=2e-3, rtol=1e-3)
 
 
 @pytest.mark.parametrize("dt", DTYPES)

@@ -119,3 +119,21 @@ def test_split_model_tool(tmp_path):
         assert (b / "model" / "config.json").exists()
         t = Topology.from_path(str(b / "topology.yml"))
         assert t.names() == [w]
+
+
+@pytest.mark.parametrize("entry", [
+    {"dtype": "F32", "shape": [2], "data_offsets": [-8, 0]},          # negative begin
+    {"dtype": "F32", "shape": [2], "data_offsets": [0, -8]},          # negative end
+    {"dtype": "F32", "shape": [-2], "data_offsets": [0, 8]},          # negative dim
+    {"dtype": "F32", "shape": [2**62, 8], "data_offsets": [0, 8]},    # numel overflow
+    {"dtype": "F32", "shape": [4], "data_offsets": [0, 1 << 40]},     # past the mapping
+])
+def test_safetensors_rejects_malformed_headers(tmp_path, entry):
+    """The native mmap reader validates header integers before forming a view."""
+    import struct
+    from cake_amd.utils.native import runtime
+    hdr = json.dumps({"t": entry}).encode()
+    p = tmp_path / "bad.safetensors"
+    p.write_bytes(struct.pack("<Q", len(hdr)) + hdr + b"\0" * 16)
+    with pytest.raises(Exception):
+        runtime().SafeTensorsFile(str(p))
