@@ -19,9 +19,17 @@ tensor device→host→device on both ends, proto/message.rs:22-38).  Here:
   allows one).  With streams = 1 it is exactly cake's sequential pipeline.
 * Backends: ``hip`` (graph per stream per run, RCCL via torch.distributed
   backend "nccl") or ``torch`` (eager reference math; gloo on CPU for tests).
+* Decode hops (``hop``): ``"dist"`` — host-issued torch.distributed p2p
+  between graph replays (RCCL over xGMI, or host-staged gloo); ``"ipc"`` —
+  device-side peer stores into the next rank's inbox (parallel/hop.py,
+  csrc/kernels/hop.hip), captured INSIDE each rank's decode graph, so a rank's
+  whole token (receive -> its layers -> send) is one replay and no host is on
+  the critical path.  Prefill always uses the dist path.
 """
 from __future__ import annotations
 
+import os
+import sys
 from dataclasses import dataclass
 
 import torch
@@ -114,7 +122,8 @@ class PipelineEngine:
     def __init__(self, cfg: LlamaConfig, stack: LayerStack, owners: list[int], rank: int,
                  world: int, streams: int = 1, head: HeadWeights | None = None,
                  repeat_penalty: float = 1.0, repeat_last_n: int = 128, use_graph: bool = True,
-                 group=None):
+                 group=None, hop: str = "dist", hop_bf16: bool = False,
+                 steps_per_graph: int = 1):
         self.cfg, self.stack, self.rank, self.world = cfg, stack, rank, world
         self.device = stack.device
         self.is_master = rank == 0
@@ -146,6 +155,15 @@ class PipelineEngine:
         if stack.max_sessions < streams:
             stack.max_sessions = streams
         self.streams = [_Stream(self, s) for s in range(streams)]
+        if hop not in ("dist", "ipc"):
+            raise ValueError(f"unknown hop transport {hop}")
+        self.hop = "dist"
+        self.hop_bf16 = bool(hop_bf16)
+        self.k = max(1, int(steps_per_graph))
+        self._skip_hops = False
+        self._events: list = []
+        if hop == "ipc" and world > 1 and self.use_graph and dist.is_initialized():
+            self._setup_ipc()  # (ipc hops need the hip backend with graphs: else dist)
 
     # ------------------------------------------------------------------ hop helpers
     def _prev(self, j: int) -> int:
@@ -164,6 +182,230 @@ class PipelineEngine:
         if self.runs[last].owner != 0:
             return self.runs[last].owner
         return self.runs[last - 1].owner if last > 0 else 0
+
+    # ------------------------------------------------------------------ ipc hops
+    # Stage k of a token: 0 = head (master: embed), 1..R = run k-1, R+1 = tail
+    # (master: ln_f, lm_head, token selection).  A hop precedes stage k when its
+    # owner differs from stage k-1's.
+    def _stage_owner(self, k: int) -> int:
+        R = len(self.runs)
+        return 0 if k == 0 or k == R + 1 else self.runs[k - 1].owner
+
+    def _recv_point(self, k: int) -> bool:
+        return k > 0 and self._stage_owner(k) != self._stage_owner(k - 1)
+
+    def _setup_ipc(self) -> None:
+        """Allocate this rank's inboxes, exchange IPC handles, map the peers' inboxes,
+        then prove every link with one tagged message (fall back to dist hops on
+        any failure, agreed by all ranks)."""
+        from . import hop as HP
+        H = self.cfg.hidden_size
+        R = len(self.runs)
+        self._H = H
+        words = HP.hop_words(H, HDR, self.hop_bf16)
+        n_st = len(self.streams)
+        ok = 1
+        self.inbox, self.peer = {}, {}
+        try:
+            mine = {}
+            for st in self.streams:
+                for k in range(1, R + 2):
+                    if self._recv_point(k) and self._stage_owner(k) == self.rank:
+                        ib = HP.Inbox(words)
+                        self.inbox[(st.sid, k)] = ib
+                        mine[(st.sid, k)] = ib.handle()
+        except Exception as e:  # noqa: BLE001  (reported, then agreed on below)
+            print(f"[pipeline] rank {self.rank}: inbox setup failed: {e}", file=sys.stderr, flush=True)
+            ok, mine = 0, {}
+        allh = [None] * self.world
+        dist.all_gather_object(allh, mine)
+        try:
+            if ok:
+                for st in self.streams:
+                    for k in range(1, R + 2):
+                        if self._recv_point(k) and self._stage_owner(k - 1) == self.rank:
+                            owner = self._stage_owner(k)
+                            self.peer[(st.sid, k)] = HP.PeerInbox(allh[owner][(st.sid, k)])
+        except Exception as e:  # noqa: BLE001
+            print(f"[pipeline] rank {self.rank}: ipc open failed: {e}", file=sys.stderr, flush=True)
+            ok = 0
+        # per (stream, stage) sequence counters (sender side and receiver side) + error word
+        self._seq = torch.zeros(2 * n_st * (R + 2), dtype=torch.int32, device=self.device)
+        self._err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        if ok:
+            ok = int(self._ipc_selftest())
+        flag = torch.tensor([ok], dtype=torch.int32,
+                            device=self.device if dist.get_backend(self.group) == "nccl" else "cpu")
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
+        if int(flag.item()) == 1:
+            self.hop = "ipc"
+            return
+        if self.rank == 0:
+            print("[pipeline] ipc hops unavailable on some rank: using dist hops", file=sys.stderr, flush=True)
+        for t in list(self.peer.values()) + list(self.inbox.values()):
+            t.close()
+        self.inbox, self.peer = {}, {}
+
+    def _seq_t(self, sid: int, k: int, side: int) -> torch.Tensor:
+        R = len(self.runs)
+        i = (side * len(self.streams) + sid) * (R + 2) + k
+        return self._seq[i:i + 1]
+
+    def _ipc_send(self, st: "_Stream", k: int) -> None:
+        from . import hop as HP
+        HP.send(st.msg, self._H, HDR, self.hop_bf16, self.peer[(st.sid, k)],
+                self._seq_t(st.sid, k, 0))
+
+    def _ipc_recv(self, st: "_Stream", k: int, timeout_s: float | None = None) -> None:
+        from . import hop as HP
+        HP.recv(self.inbox[(st.sid, k)], st.msg, self._H, HDR, self.hop_bf16,
+                self._seq_t(st.sid, k, 1), self._err, timeout_s)
+
+    def _ipc_selftest(self) -> bool:
+        """One tagged message over every link (a known pattern, short timeout);
+        the message buffers and sequence counters are restored afterwards."""
+        R = len(self.runs)
+        saved = [st.msg.clone() for st in self.streams]
+        try:
+            for st in self.streams:
+                pat = torch.arange(st.msg.numel(), device=self.device, dtype=torch.float32)
+                pat = pat * 0.25 + 1000 * self.rank + st.sid
+                for k in range(1, R + 2):
+                    if not self._recv_point(k):
+                        continue
+                    src, dst = self._stage_owner(k - 1), self._stage_owner(k)
+                    if src == dst:
+                        continue
+                    if src == self.rank:
+                        st.msg.copy_(pat)
+                        self._ipc_send(st, k)
+                    if dst == self.rank:
+                        self._ipc_recv(st, k, timeout_s=20.0)
+                        torch.cuda.synchronize(self.device)
+                        exp = (torch.arange(st.msg.numel(), device=self.device,
+                                            dtype=torch.float32) * 0.25 + 1000 * src + st.sid)
+                        H = self._H
+                        got_h, exp_h = st.msg[:H], exp[:H]
+                        if self.hop_bf16:
+                            exp_h = exp_h.to(torch.bfloat16).float()
+                        if int(self._err.item()) != 0 or not torch.equal(got_h, exp_h) or \
+                                not torch.equal(st.msg[H:].view(torch.int32),
+                                                exp[H:].view(torch.int32)):
+                            print(f"[pipeline] rank {self.rank}: ipc self-test mismatch on "
+                                  f"stage {k}", file=sys.stderr, flush=True)
+                            return False
+                    torch.cuda.synchronize(self.device)
+            return True
+        except Exception as e:  # noqa: BLE001
+            print(f"[pipeline] rank {self.rank}: ipc self-test failed: {e}", file=sys.stderr, flush=True)
+            return False
+        finally:
+            torch.cuda.synchronize(self.device)
+            for st, v in zip(self.streams, saved):
+                st.msg.copy_(v)
+            self._err.zero_()
+
+    def _ipc_stages(self) -> list[int]:
+        return [k for k in range(len(self.runs) + 2) if self._stage_owner(k) == self.rank]
+
+    def _ipc_stage_body(self, st: "_Stream", k: int) -> None:
+        """Stage k of one token for stream st on this rank (graph-capturable)."""
+        from ..ops import hip as K
+        R = len(self.runs)
+        if self._recv_point(k) and not self._skip_hops:
+            self._ipc_recv(st, k)
+        if k == 0:
+            K.embed(self.head.embed, st.bufs.tok, st.resid)
+        elif k == R + 1:
+            K.norm_gemv_f32(st.resid, self.head.norm, self.cfg.rms_norm_eps, self.head.lm_head,
+                            st.bufs.logits)
+            self._select_device(st)
+        else:
+            self.stack.decode_step(st.bufs, self.runs[k - 1].layers, st.sid)
+        if k < R + 1 and self._recv_point(k + 1) and not self._skip_hops:
+            self._ipc_send(st, k + 1)
+
+    def _ipc_token_body(self, st: "_Stream") -> None:
+        for k in self._ipc_stages():
+            self._ipc_stage_body(st, k)
+
+    def check_hops(self) -> None:
+        """Raise if any device-side receive timed out (a peer stopped sending)."""
+        if self.hop == "ipc" and int(self._err.item()) != 0:
+            raise RuntimeError(f"rank {self.rank}: a pipeline hop timed out "
+                               f"(CAKE_HOP_TIMEOUT={os.environ.get('CAKE_HOP_TIMEOUT', '60')} s)")
+
+    def measure_hop_us(self, iters: int = 100) -> float | None:
+        """One-way latency of a decode hop between ranks 0 and 1 (ping-pong; µs).
+        All ranks call it; ranks >= 2 only join the barriers.  None if world == 1."""
+        if self.world < 2:
+            return None
+        H = self.cfg.hidden_size
+        msg = torch.zeros(H + HDR, device=self.device, dtype=torch.float32)
+        reps = 10
+        if self.hop == "ipc":
+            from . import hop as HP
+            words = HP.hop_words(H, HDR, self.hop_bf16)
+            ib = HP.Inbox(words) if self.rank in (0, 1) else None
+            allh = [None] * self.world
+            dist.all_gather_object(allh, ib.handle() if ib is not None else None)
+            peer = HP.PeerInbox(allh[1 - self.rank]) if self.rank in (0, 1) else None
+            seq = torch.zeros(2, dtype=torch.int32, device=self.device)
+            err = torch.zeros(1, dtype=torch.int32, device=self.device)
+
+            def body():
+                for _ in range(iters):
+                    if self.rank == 0:
+                        HP.send(msg, H, HDR, self.hop_bf16, peer, seq[0:1])
+                        HP.recv(ib, msg, H, HDR, self.hop_bf16, seq[1:2], err)
+                    else:
+                        HP.recv(ib, msg, H, HDR, self.hop_bf16, seq[1:2], err)
+                        HP.send(msg, H, HDR, self.hop_bf16, peer, seq[0:1])
+            g = None
+            if self.rank in (0, 1):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    body()
+            dist.barrier(group=self.group)
+            torch.cuda.synchronize(self.device)
+            t = None
+            if g is not None:
+                g.replay()  # warm
+                torch.cuda.synchronize(self.device)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(reps):
+                    g.replay()
+                e1.record()
+                e1.synchronize()
+                t = e0.elapsed_time(e1) * 1e3 / (reps * iters * 2)
+                if int(err.item()) != 0:
+                    t = None
+            torch.cuda.synchronize(self.device)
+            dist.barrier(group=self.group)
+            if peer is not None:
+                peer.close()
+            dist.barrier(group=self.group)
+            if ib is not None:
+                ib.close()
+            return t
+        # host-issued dist p2p ping-pong
+        import time
+        dist.barrier(group=self.group)
+        t0 = time.perf_counter()
+        n = iters * 2
+        for _ in range(n // 2):
+            if self.rank == 0:
+                self._wait(self._send(msg, 1))
+                self._recv(msg, 1)
+            elif self.rank == 1:
+                self._recv(msg, 0)
+                self._wait(self._send(msg, 0))
+        if msg.is_cuda:
+            torch.cuda.synchronize(self.device)
+        dt = (time.perf_counter() - t0) * 1e6 / n
+        dist.barrier(group=self.group)
+        return dt if self.rank in (0, 1) else None
 
     def _send(self, t: torch.Tensor, dst: int):
         g = self.g_up if dst > self.rank else self.g_down
@@ -421,8 +663,14 @@ class PipelineEngine:
         g.replay()
 
     def capture(self) -> None:
-        """Capture one hipGraph per (stream, body) — RCCL hops stay outside."""
+        """Capture one hipGraph per (stream, body) — RCCL hops stay outside.  With ipc
+        hops the receives/sends are inside the graphs: one graph per stream holding
+        this rank's stages of `k` consecutive tokens (streams = 1), or one per
+        (stream, stage) replayed stage-major so streams overlap (streams > 1)."""
         if not self.use_graph:
+            return
+        if self.hop == "ipc":
+            self._capture_ipc()
             return
         for st in self.streams:
             bodies = self._bodies(st)
@@ -452,6 +700,77 @@ class PipelineEngine:
                 st.graphs[key] = g
         torch.cuda.synchronize()
 
+    def _capture_ipc(self) -> None:
+        bodies = {}
+        for st in self.streams:
+            if len(self.streams) == 1:
+                bodies[(st.sid, "tok")] = (st, lambda st=st: [self._ipc_token_body(st)
+                                                              for _ in range(self.k)])
+            else:
+                for k in self._ipc_stages():
+                    bodies[(st.sid, k)] = (st, lambda st=st, k=k: self._ipc_stage_body(st, k))
+        # warm-up outside capture WITHOUT hops (a receive would wait on a peer that
+        # is not sending), on scratch state that is restored afterwards
+        self._skip_hops = True
+        try:
+            for key, (st, fn) in bodies.items():
+                saved = st.msg.clone()
+                st.hdr[H_POS] = self.stack.max_seq - 1
+                keep = None
+                if self.is_master:
+                    b = st.bufs
+                    keep = [t.clone() for t in (b.tok, b.hist, b.hist_len, b.slot)]
+                s = torch.cuda.Stream()
+                s.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(s):
+                    if len(self.streams) == 1:
+                        self._ipc_token_body(st)
+                    else:
+                        fn()
+                torch.cuda.current_stream().wait_stream(s)
+                torch.cuda.synchronize()
+                st.msg.copy_(saved)
+                if keep is not None:
+                    for t, v in zip((b.tok, b.hist, b.hist_len, b.slot), keep):
+                        t.copy_(v)
+        finally:
+            self._skip_hops = False
+        for key, (st, fn) in bodies.items():
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                fn()
+            st.graphs[key] = g
+        torch.cuda.synchronize()
+
+    def _decode_ipc(self, rounds: int) -> None:
+        """Every rank enqueues its graphs for `rounds` tokens; the hops synchronise
+        the ranks on the device.  The master records one event per replay."""
+        if len(self.streams) == 1:
+            st = self.streams[0]
+            g = st.graphs[(st.sid, "tok")]
+            for _ in range(-(-rounds // self.k)):
+                g.replay()
+                if self.is_master:
+                    ev = torch.cuda.Event(enable_timing=True)
+                    ev.record()
+                    self._events.append(ev)
+            return
+        stages = self._ipc_stages()
+        for _ in range(rounds):
+            for k in stages:
+                for st in self.streams:
+                    st.graphs[(st.sid, k)].replay()
+            if self.is_master:
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record()
+                self._events.append(ev)
+
+    def step_times_ms(self) -> list[float]:
+        """Master: per-replay device intervals recorded by the last ipc decode()
+        (per token when streams = 1 and k = 1; otherwise per round / per k tokens)."""
+        ev = self._events
+        return [a.elapsed_time(b) for a, b in zip(ev, ev[1:])]
+
     def _bodies(self, st: _Stream) -> dict:
         out = {}
         if self.is_master:
@@ -466,8 +785,27 @@ class PipelineEngine:
     # ------------------------------------------------------------------ decode loop
     def decode(self, rounds: int) -> None:
         """Every stream generates `rounds` tokens (ignoring EOS)."""
+        if self.hop == "ipc":
+            self._events = []
+            if self.is_master:
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record()
+                self._events.append(ev)
+            self._decode_ipc(rounds)
+            return
         single = self.world == 1 or all(r.owner == 0 for r in self.runs)
+        self._events = []
+        timed = self.is_master and self.hip
+
+        def mark():
+            if timed:
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record()
+                self._events.append(ev)
+        mark()
         for k in range(rounds):
+            if k > 0:
+                mark()
             for st in self.streams:
                 if self.is_master:
                     if single:
@@ -487,6 +825,7 @@ class PipelineEngine:
                 st.send_work = None
                 self._recv(st.msg, self._final_src())
                 self._replay(st, "last", lambda: self._body_last(st))
+        mark()
 
     def _worker_runs(self, st: _Stream) -> None:
         last = len(self.runs) - 1

@@ -1,0 +1,47 @@
+"""bench.py contract on CPU: self-launched N>1 ranks (no torchrun), fail-fast on a dead rank.
+
+The driver runs ``bench.py --gpus N`` (torchrun or bare); without WORLD_SIZE in the
+environment bench.py spawns the ranks itself.  --cpu runs the reference math with gloo
+so the launch / aggregation / equivalence plumbing is covered without a GPU."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ARGS = ["--cpu", "--model", "tiny", "--steps", "5", "--warmup", "2", "--prompt-len", "9",
+        "--max-seq", "64"]
+
+
+def _run(extra, env=None, timeout=240):
+    e = dict(os.environ)
+    e.pop("WORLD_SIZE", None)
+    e.update(env or {})
+    return subprocess.run([sys.executable, "bench.py", *ARGS, *extra], cwd=ROOT,
+                          capture_output=True, text=True, timeout=timeout, env=e)
+
+
+def _json(r):
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout + r.stderr[-2000:]
+    return json.loads(lines[0])
+
+
+def test_self_launch_matches_single(tmp_path):
+    r1 = _run(["--dump-tokens", str(tmp_path / "a.json")])
+    assert r1.returncode == 0, r1.stderr[-2000:]
+    r2 = _run(["--gpus", "3", "--dump-tokens", str(tmp_path / "b.json")])
+    assert r2.returncode == 0, r2.stderr[-2000:]
+    j = _json(r2)
+    assert j["n_gpus"] == 3 and j["steps"] == 5 and j["warmup"] == 2 and j["value"] > 0
+    assert j["config"]["global_batch"] == 1 and j["scaling"] == "strong"
+    assert j["hops_per_token"] == 3 and j["hop_us"] > 0
+    a = json.loads((tmp_path / "a.json").read_text())
+    b = json.loads((tmp_path / "b.json").read_text())
+    assert a[0] == b[0]          # layer sharding does not change the token stream
+
+
+def test_self_launch_fails_fast_when_a_rank_dies():
+    r = _run(["--gpus", "3"], env={"CAKE_BENCH_FAIL_RANK": "2"}, timeout=120)
+    assert r.returncode != 0
+    assert "stopping the others" in r.stderr

@@ -1,6 +1,7 @@
-"""Multi-process pipeline on ONE GPU (host-staged gloo hops; RCCL refuses duplicate GPUs).
+"""Multi-process pipeline on ONE GPU (RCCL refuses duplicate GPUs, so control/prefill use
+gloo; decode hops are the device-side ipc stores or host-staged gloo p2p).
 
-Runs bench.py under torchrun with 2 and 3 ranks sharing cuda:0 and checks that the
+Runs bench.py self-launched with 2 and 3 ranks sharing cuda:0 and checks that the
 generated token ids equal the single-rank run (equivalence invariant)."""
 import json
 import os
@@ -13,28 +14,44 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _bench(tmp_path, n, streams, name):
+def _bench(tmp_path, n, streams, name, hop="dist", hop_dtype="f32", k=1):
     out = tmp_path / f"{name}.json"
     args = ["bench.py", "--model", "tiny", "--steps", "12", "--warmup", "3", "--prompt-len", "9",
             "--max-seq", "256", "--dump-tokens", str(out)]
-    if n == 1:
-        cmd = [sys.executable] + args
-    else:
-        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
-               f"--nproc-per-node={n}", "--master-addr=127.0.0.1", f"--master-port={29600 + n}",
-               ] + args + ["--gpus", str(n), "--dist-backend", "gloo", "--streams", str(streams)]
-    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
-    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240, env=env)
+    if n > 1:
+        args += ["--gpus", str(n), "--dist-backend", "gloo", "--streams", str(streams),
+                 "--hop", hop, "--hop-dtype", hop_dtype, "--steps-per-graph", str(k),
+                 "--launch-timeout", "200"]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", CAKE_HOP_TIMEOUT="30")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable] + args, cwd=ROOT, capture_output=True, text=True,
+                       timeout=240, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
     return json.loads(line), json.loads(out.read_text())
 
 
-def test_pipeline_multirank_matches_single(cuda, tmp_path):
+def test_pipeline_multirank_dist_hops_match_single(cuda, tmp_path):
     _, single = _bench(tmp_path, 1, 1, "single")
     m2, pp2 = _bench(tmp_path, 2, 1, "pp2")
     assert pp2[0] == single[0]
-    assert m2["n_gpus"] == 2 and m2["value"] > 0
+    assert m2["n_gpus"] == 2 and m2["value"] > 0 and m2["hop"] == "dist"
     m3, pp3 = _bench(tmp_path, 3, 2, "pp3")
     assert pp3[0] == single[0]          # stream 0 uses the same prompt as the single run
     assert len(pp3) == 2 and len(pp3[1]) == len(pp3[0])
+
+
+def test_pipeline_ipc_hops_in_graph_match_single(cuda, tmp_path):
+    """Device-side hops captured in every rank's graph: exact with f32 payloads, also
+    several tokens per graph (k = 4, 12 steps) and two concurrent streams."""
+    _, single = _bench(tmp_path, 1, 1, "single")
+    m2, pp2 = _bench(tmp_path, 2, 1, "ipc2", hop="ipc")
+    assert m2["hop"] == "ipc", m2
+    assert pp2[0] == single[0]
+    assert m2["hop_us"] is not None and m2["hop_us"] > 0
+    m3, pp3 = _bench(tmp_path, 3, 1, "ipc3k", hop="ipc", k=4)
+    assert m3["hop"] == "ipc" and pp3[0] == single[0]
+    m4, pp4 = _bench(tmp_path, 2, 2, "ipc2s", hop="ipc")
+    assert m4["hop"] == "ipc" and pp4[0] == single[0] and len(pp4) == 2
+    m5, pp5 = _bench(tmp_path, 2, 1, "ipc2bf", hop="ipc", hop_dtype="bf16")
+    assert m5["hop"] == "ipc-bf16" and len(pp5[0]) == len(single[0])
