@@ -101,6 +101,28 @@ __device__ __forceinline__ uint4 ld_nt16(const uint4* p) {
 
 __device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
 
+// MFMA operand / accumulator vectors (16x16x32: 8 x 16-bit per lane, 4 f32 acc)
+typedef __bf16 cbf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 cf16x8 __attribute__((ext_vector_type(8)));
+typedef float cf32x4 __attribute__((ext_vector_type(4)));
+
+// D = A(16x32) B(32x16) + C; lane l holds A[l&15][8(l>>4)..+8] and B[8(l>>4)..+8][l&15]
+// (16-byte k-contiguous fragments), D[4(l>>4)+e][l&15] in element e.
+template <int DT>
+__device__ __forceinline__ cf32x4 cmfma(const uint4 a, const uint4 b, cf32x4 c) {
+  if constexpr (DT == kBF16)
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(cbf16x8, a),
+                                                   __builtin_bit_cast(cbf16x8, b), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(cf16x8, a),
+                                                  __builtin_bit_cast(cf16x8, b), c, 0, 0, 0);
+}
+
+// LDS byte offset of a __shared__ pointer (for inline-asm ds_* operands)
+__device__ __forceinline__ uint32_t lds_off(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
 // LDS-DMA (global_load_lds) operand types and an s_waitcnt immediate that
 // constrains only the vector-memory counter (gfx9 encoding).
 typedef const __attribute__((address_space(1))) void* gptr_t;

@@ -30,10 +30,6 @@
 
 namespace cake {
 
-typedef __bf16 cbf16x8 __attribute__((ext_vector_type(8)));
-typedef _Float16 cf16x8 __attribute__((ext_vector_type(8)));
-typedef float cf32x4 __attribute__((ext_vector_type(4)));
-
 constexpr int kCBK = 64;  // k per step (one tap x 64 input channels)
 
 struct ConvArgs {
@@ -49,15 +45,6 @@ struct ConvArgs {
   int P, ksteps, ks_per_split, tiles_m, tiles_n;
 };
 
-template <int DT>
-__device__ __forceinline__ cf32x4 cmfma(const uint4 a, const uint4 b, cf32x4 c) {
-  if constexpr (DT == kBF16)
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(cbf16x8, a),
-                                                   __builtin_bit_cast(cbf16x8, b), c, 0, 0, 0);
-  else
-    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(cf16x8, a),
-                                                  __builtin_bit_cast(cf16x8, b), c, 0, 0, 0);
-}
 
 // element offset of (row, 16-byte chunk) in a [rows][64] swizzled tile
 __device__ __forceinline__ int swz(int row, int chunk) { return (row * 8 + (chunk ^ (row & 7))) * 8; }

@@ -1,0 +1,479 @@
+// MFMA GEMM for every T > 1 linear layer: y = x W^T (+ fused epilogue).
+//
+// Replaces the reference's candle Linear -> cuBLAS gemm for the Llama prefill
+// projections (cake-core/src/models/llama3/attention.rs:49-60 q/k/v, :120 o;
+// mlp.rs:14-18 gate/up/down) and every Stable Diffusion / CLIP linear
+// (candle-transformers stable_diffusion attention/FF/proj layers reached from
+// cake-core/src/models/sd/{unet,vae,clip}.rs), SURVEY K03 / K34-K36 / K40.
+//
+//   A = x [M][K] (activations, row stride lda), B = W [N][K] (HF weight layout,
+//   row stride ldb): both operands are k-contiguous, so every MFMA fragment is
+//   one 16-byte LDS read.  f32 accumulation on v_mfma_f32_16x16x32_{bf16,f16}.
+//
+// Structure (gfx950):
+//   * Workgroup tile BM x BN x 64, 256 threads = WM x WN waves, per-wave tile
+//     (BM/WM) x (BN/WN) as FM x FN 16x16 MFMA tiles.
+//   * Operands staged global -> LDS by LDS-DMA (global_load_lds_dwordx4, no
+//     VGPR round trip) into two buffers; the DMA of k-step t+2 is in flight
+//     while step t computes.  The 128-byte rows are XOR-swizzled in 16-byte
+//     slots (slot ^= (row >> 1) & 7) on the SOURCE address (the DMA writes
+//     lane-linear), which makes the fragment ds_read_b128 conflict-free.
+//   * Fragment reads are inline-asm ds_read_b128 with an explicit lgkmcnt wait:
+//     hipcc cannot see them, so it does not drain the in-flight DMA (vmcnt(0))
+//     in front of them, which it does for compiler-visible LDS reads of a
+//     buffer a DMA may write.  Waits on the DMA are counted (vmcnt(N)) and the
+//     barriers are raw s_barrier (MI355X guide: "Pipelining across barriers").
+//   * XCD-aware grouped tile order: round-robin block -> XCD dealing is undone
+//     so each XCD's blocks cover a compact group of tiles (shared A rows / W
+//     rows hit that XCD's L2).
+//   * Split-K (grid.y) for grids smaller than the chip: f32 partial slabs and
+//     a second kernel that reduces them and applies the epilogue.
+//   * Epilogues (C staged through LDS per 16-row strip, 16-32 byte vector
+//     stores): plain store (+bias), f32 residual accumulate (Llama o/down
+//     proj: resid += y), 16-bit add (+bias, +residual: SD proj_out), SwiGLU
+//     (silu(gate) * up from the fused gate|up weight) and GEGLU
+//     (h * gelu_tanh(gate), SD FeedForward).  For the gated forms the B rows
+//     are read in a virtual order that interleaves 16-row blocks of the two
+//     halves, so gate and up of one feature land in the same lane.
+#include "common.h"
+
+namespace cake {
+
+constexpr int kGBK = 64;  // k per step (128-byte rows)
+
+enum GemmEpi : int {
+  kEpiStore = 0,   // C16 = acc (+ bias)
+  kEpiResid32 = 1, // R32 += acc (+ bias)
+  kEpiAdd16 = 2,   // C16 = acc (+ bias) + R16
+  kEpiSwiglu = 3,  // C16[:, f] = silu(acc_gate) * acc_up
+  kEpiGeglu = 4,   // C16[:, f] = acc_h * gelu_tanh(acc_gate)
+  kEpiPartial = 5, // W32[split] = acc (split-K slab, virtual column order)
+};
+
+struct GemmArgs {
+  const uint16_t* a;     // [M][lda]
+  const uint16_t* b;     // [Nw][ldb] weight rows
+  uint16_t* c;           // [M][ldc] 16-bit output
+  const uint16_t* bias;  // [N] or null
+  float* r32;            // [M][ldr] f32 residual (kEpiResid32)
+  const uint16_t* r16;   // [M][ldr] 16-bit residual (kEpiAdd16)
+  float* ws;             // [splits][M][Nv] f32 slabs (kEpiPartial)
+  const uint16_t* zeros; // >= 16 zero bytes (DMA source for out-of-range rows / k)
+  long long lda, ldb, ldc, ldr;
+  int M, N, K;           // N = output columns (features); Nv = virtual B rows
+  int Nv, half;          // gated: Nv = 2 * half, half = N
+  int gated;             // B row order interleaves 16-row blocks of two halves
+  int tiles_m, tiles_n, kps;  // k elements per split
+};
+
+// virtual B row -> weight row (gated: [16 gate rows | 16 up rows] per 32-row block)
+__device__ __forceinline__ int wrow(const GemmArgs& g, int v) {
+  if (!g.gated) return v;
+  const int blk = v >> 5, w = v & 31;
+  return w < 16 ? blk * 16 + w : g.half + blk * 16 + (w - 16);
+}
+
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
+  return 0.5f * x * (1.f + tanhf(u));
+}
+
+__device__ __forceinline__ uint4 ds_read16(uint32_t addr) {
+  uint4 v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr));
+  return v;
+}
+
+template <int DT, int BM, int BN, int WM, int WN, int NS, int EPI>
+__global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(GemmArgs g) {
+  constexpr int NT = 64 * WM * WN;
+  constexpr int NWAVE = WM * WN;
+  constexpr int WTM = BM / WM, WTN = BN / WN;  // per-wave tile
+  constexpr int FM = WTM / 16, FN = WTN / 16;
+  constexpr int ROWS = BM + BN;                // 128-byte rows per k-step
+  constexpr int IPW = ROWS / 8 / NWAVE;        // DMA wave-instructions per wave per k-step
+  constexpr int BUF = ROWS * 128;              // bytes per LDS buffer
+  static_assert(ROWS % (8 * NWAVE) == 0 && BM % 16 == 0 && BN % 32 == 0, "tile geometry");
+  static_assert(WTM % 16 == 0 && WTN % 32 == 0, "wave tile geometry");
+  constexpr int STG_LD = WTN + 4;              // epilogue staging row stride (floats)
+  constexpr int STG = 16 * STG_LD * 4;         // bytes per wave
+  constexpr int LDS_BYTES = (NS * BUF > NWAVE * STG) ? NS * BUF : NWAVE * STG;
+  static_assert(NS == 2 || NS == 3, "LDS stages");
+  __shared__ __attribute__((aligned(16))) uint8_t smem[LDS_BYTES];
+
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wr = wave / WN, wc = wave % WN;
+
+  // ---- XCD-aware grouped tile order --------------------------------------
+  const int ntiles = g.tiles_m * g.tiles_n;
+  const int bid = blockIdx.x;
+  int id;
+  {
+    const int q = ntiles / 8, r = ntiles % 8, x = bid % 8, i = bid / 8;
+    id = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;  // bijective undealing
+  }
+  constexpr int GROUP = 8;
+  const int per_group = GROUP * g.tiles_n;
+  const int grp = id / per_group;
+  const int first_m = grp * GROUP;
+  const int gm = min(GROUP, g.tiles_m - first_m);
+  const int tm = first_m + (id % per_group) % gm;
+  const int tn = (id % per_group) / gm;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int split = blockIdx.y;
+  const int kb = split * g.kps, ke = min(g.K, kb + g.kps);
+  const int nk = (ke - kb + kGBK - 1) / kGBK;
+
+  // ---- DMA sources of this lane (fixed rows; k advances) -----------------
+  const uint16_t* src[IPW];
+  bool is_a[IPW];
+  int chunk[IPW];
+#pragma unroll
+  for (int i = 0; i < IPW; ++i) {
+    const int t = (wave * IPW + i) * 8 + (lane >> 3);  // tile row (A rows, then B rows)
+    const int slot = lane & 7;
+    chunk[i] = slot ^ ((t >> 1) & 7);
+    if (t < BM) {
+      const int m = m0 + t;
+      src[i] = m < g.M ? g.a + (size_t)m * g.lda : nullptr;
+      is_a[i] = true;
+    } else {
+      const int v = n0 + (t - BM);
+      src[i] = v < g.Nv ? g.b + (size_t)wrow(g, v) * g.ldb : nullptr;
+      is_a[i] = false;
+    }
+  }
+  (void)is_a;
+  const uint32_t lds0 = lds_off(smem);
+  auto stage = [&](int step, int buf) {
+    const int k0 = kb + step * kGBK;
+#pragma unroll
+    for (int i = 0; i < IPW; ++i) {
+      const int k = k0 + chunk[i] * 8;
+      const uint16_t* p = (src[i] != nullptr && k < ke) ? src[i] + k : g.zeros;
+      glds16(p, smem + buf * BUF + (wave * IPW + i) * 1024);
+    }
+  };
+
+  // ---- fragment addresses: row (lane & 15) of a 16-row group, slot swizzled
+  const int swz = (lane & 15) >> 1;
+  const uint32_t lrow = (uint32_t)(lane & 15) * 128;
+  const uint32_t off0 = (uint32_t)((((lane >> 4)) ^ swz) * 16);      // k 0..31
+  const uint32_t off1 = (uint32_t)(((4 + (lane >> 4)) ^ swz) * 16);  // k 32..63
+  const uint32_t a_base = lds0 + (uint32_t)(wr * WTM) * 128 + lrow;
+  const uint32_t b_base = lds0 + (uint32_t)(BM + wc * WTN) * 128 + lrow;
+
+  cf32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = cf32x4{0.f, 0.f, 0.f, 0.f};
+
+  // One barrier per k-step.  At the top of step t every wave waits for its own
+  // DMA of step t (counted vmcnt: with 3 stages the DMA of t+1 stays in flight)
+  // and the barrier then publishes every wave's; the same barrier proves every
+  // wave finished reading step t-1's buffer (its reads completed before its
+  // MFMAs), so the DMA issued right after it may overwrite that buffer: step t+1
+  // (2 stages) or t+2 (3 stages).  Within a step the k 32..63 fragment reads
+  // overlap the k 0..31 MFMAs.
+  if (nk > 0) stage(0, 0);
+  if (NS == 3 && nk > 1) stage(1, 1);
+  int buf = 0;
+  for (int t = 0; t < nk; ++t) {
+    if (NS == 3 && t + 1 < nk) __builtin_amdgcn_s_waitcnt(vm_wait(IPW));
+    else __builtin_amdgcn_s_waitcnt(vm_wait(0));
+    asm volatile("s_barrier" ::: "memory");
+    if (t + NS - 1 < nk) {
+      int nb = buf + NS - 1;
+      nb = nb >= NS ? nb - NS : nb;
+      stage(t + NS - 1, nb);
+    }
+    uint4 af[FM][2], bfr[FN][2];
+    const uint32_t ab = a_base + buf * BUF, bb = b_base + buf * BUF;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) af[i][0] = ds_read16(ab + i * 16 * 128 + off0);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) bfr[j][0] = ds_read16(bb + j * 16 * 128 + off0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < FM; ++i) af[i][1] = ds_read16(ab + i * 16 * 128 + off1);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) bfr[j][1] = ds_read16(bb + j * 16 * 128 + off1);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = cmfma<DT>(af[i][0], bfr[j][0], acc[i][j]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = cmfma<DT>(af[i][1], bfr[j][1], acc[i][j]);
+    buf = buf + 1 == NS ? 0 : buf + 1;
+  }
+
+  // ---- epilogue: 16-row strips staged through this wave's LDS slice --------
+  __builtin_amdgcn_s_waitcnt(vm_wait(0));
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  float* stg = reinterpret_cast<float*>(smem + wave * STG);
+  const int row_m0 = m0 + wr * WTM;
+  const int vcol0 = n0 + wc * WTN;  // first virtual column of this wave
+  constexpr bool GATED = (EPI == kEpiSwiglu || EPI == kEpiGeglu);
+  constexpr int OUTC = GATED ? WTN / 2 : WTN;  // output columns of this wave
+  constexpr int CPL = OUTC / 4;                // columns per lane (4 lanes per row)
+  const int er = lane >> 2, ec = (lane & 3) * CPL;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        stg[((lane >> 4) * 4 + e) * STG_LD + j * 16 + (lane & 15)] = acc[i][j][e];
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    const int m = row_m0 + i * 16 + er;
+    if (m < g.M) {
+      const float* srow = stg + er * STG_LD;
+      if constexpr (EPI == kEpiPartial) {
+        float* dst = g.ws + ((size_t)split * g.M + m) * g.Nv;
+#pragma unroll
+        for (int c = 0; c < CPL; c += 4) {
+          const int n = vcol0 + ec + c;
+          const float4 v = *reinterpret_cast<const float4*>(srow + ec + c);
+          if (n + 3 < g.Nv) *reinterpret_cast<float4*>(dst + n) = v;
+          else {
+            const float vv[4] = {v.x, v.y, v.z, v.w};
+            for (int q = 0; q < 4; ++q) if (n + q < g.Nv) dst[n + q] = vv[q];
+          }
+        }
+      } else if constexpr (GATED) {
+        // output column f of this lane: virtual cols (32-block b): gate at 32b + c, up at 32b + 16 + c
+        const int f0 = vcol0 / 2 + ec;  // vcol0 is a multiple of 32
+        uint16_t outv[CPL];
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+          const int lc = ec + c;                           // output col within the wave
+          const int vc = (lc >> 4) * 32 + (lc & 15);       // gate's staged column
+          float a = srow[vc], b = srow[vc + 16];
+          if (g.bias != nullptr && f0 + c < g.N) {
+            a += to_f32<DT>(g.bias[f0 + c]);
+            b += to_f32<DT>(g.bias[g.half + f0 + c]);
+          }
+          float y;
+          if constexpr (EPI == kEpiSwiglu) y = silu(a) * b;
+          else y = a * gelu_tanh(b);
+          outv[c] = from_f32<DT>(y);
+        }
+        uint16_t* dst = g.c + (size_t)m * g.ldc;
+        if (CPL % 8 == 0 && f0 + CPL <= g.N && ((g.ldc | f0) & 7) == 0) {
+#pragma unroll
+          for (int c = 0; c + 7 < CPL; c += 8)
+            *reinterpret_cast<uint4*>(dst + f0 + c) = *reinterpret_cast<const uint4*>(outv + c);
+        } else {
+          for (int c = 0; c < CPL; ++c) if (f0 + c < g.N) dst[f0 + c] = outv[c];
+        }
+      } else {
+        const int n0c = vcol0 + ec;
+        float v[CPL];
+#pragma unroll
+        for (int c = 0; c < CPL; c += 4) {
+          const float4 t4 = *reinterpret_cast<const float4*>(srow + ec + c);
+          v[c] = t4.x; v[c + 1] = t4.y; v[c + 2] = t4.z; v[c + 3] = t4.w;
+        }
+        const bool full = n0c + CPL <= g.N;
+        if (g.bias != nullptr) {
+#pragma unroll
+          for (int c = 0; c < CPL; ++c)
+            if (full || n0c + c < g.N) v[c] += to_f32<DT>(g.bias[n0c + c]);
+        }
+        if constexpr (EPI == kEpiResid32) {
+          float* r = g.r32 + (size_t)m * g.ldr + n0c;
+          if (full && ((g.ldr | n0c) & 3) == 0) {
+#pragma unroll
+            for (int c = 0; c < CPL; c += 4) {
+              float4 o = *reinterpret_cast<float4*>(r + c);
+              o.x += v[c]; o.y += v[c + 1]; o.z += v[c + 2]; o.w += v[c + 3];
+              *reinterpret_cast<float4*>(r + c) = o;
+            }
+          } else {
+            for (int c = 0; c < CPL; ++c) if (n0c + c < g.N) r[c] += v[c];
+          }
+        } else {
+          if constexpr (EPI == kEpiAdd16) {
+            const uint16_t* r = g.r16 + (size_t)m * g.ldr + n0c;
+#pragma unroll
+            for (int c = 0; c < CPL; ++c)
+              if (full || n0c + c < g.N) v[c] += to_f32<DT>(r[c]);
+          }
+          uint16_t outv[CPL];
+#pragma unroll
+          for (int c = 0; c < CPL; ++c) outv[c] = from_f32<DT>(v[c]);
+          uint16_t* dst = g.c + (size_t)m * g.ldc + n0c;
+          if (CPL % 8 == 0 && full && ((g.ldc | n0c) & 7) == 0) {
+#pragma unroll
+            for (int c = 0; c + 7 < CPL; c += 8)
+              *reinterpret_cast<uint4*>(dst + c) = *reinterpret_cast<const uint4*>(outv + c);
+          } else {
+            for (int c = 0; c < CPL; ++c) if (n0c + c < g.N) dst[c] = outv[c];
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // strip consumed before the next one overwrites it
+  }
+}
+
+// Split-K finalize: out = epilogue(sum over splits of the slabs).  One thread
+// per 4 output columns of one row.
+template <int DT, int EPI>
+__global__ __launch_bounds__(256) void gemm_splitk_finalize(GemmArgs g, int splits) {
+  const int m = blockIdx.y;
+  const int f = (blockIdx.x * 256 + threadIdx.x) * 4;
+  if (f >= g.N) return;
+  const size_t slab = (size_t)g.M * g.Nv;
+  float v[4] = {0.f, 0.f, 0.f, 0.f}, u[4] = {0.f, 0.f, 0.f, 0.f};
+  constexpr bool GATED = (EPI == kEpiSwiglu || EPI == kEpiGeglu);
+  for (int s = 0; s < splits; ++s) {
+    const float* row = g.ws + s * slab + (size_t)m * g.Nv;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int fq = f + q;
+      if (fq >= g.N) break;
+      if constexpr (GATED) {
+        const int vc = (fq >> 4) * 32 + (fq & 15);
+        v[q] += row[vc];
+        u[q] += row[vc + 16];
+      } else {
+        v[q] += row[fq];
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int fq = f + q;
+    if (fq >= g.N) break;
+    float y;
+    if constexpr (GATED) {
+      if (g.bias != nullptr) {
+        v[q] += to_f32<DT>(g.bias[fq]);
+        u[q] += to_f32<DT>(g.bias[g.half + fq]);
+      }
+    }
+    if constexpr (EPI == kEpiSwiglu) y = silu(v[q]) * u[q];
+    else if constexpr (EPI == kEpiGeglu) y = v[q] * gelu_tanh(u[q]);
+    else {
+      y = v[q] + (g.bias != nullptr ? to_f32<DT>(g.bias[fq]) : 0.f);
+      if constexpr (EPI == kEpiAdd16) y += to_f32<DT>(g.r16[(size_t)m * g.ldr + fq]);
+    }
+    if constexpr (EPI == kEpiResid32) g.r32[(size_t)m * g.ldr + fq] += y;
+    else g.c[(size_t)m * g.ldc + fq] = from_f32<DT>(y);
+  }
+}
+
+}  // namespace cake
+
+using namespace cake;
+
+// tile configurations (BM, BN, WM, WN, LDS stages)
+#define CAKE_GEMM_CFGS(X)  \
+  X(0, 128, 128, 2, 2, 2)  \
+  X(1, 64, 128, 1, 4, 2)   \
+  X(2, 256, 128, 2, 2, 3)  \
+  X(3, 128, 256, 2, 2, 3)  \
+  X(4, 64, 64, 2, 2, 2)    \
+  X(5, 256, 256, 2, 4, 2)  \
+  X(6, 256, 128, 4, 2, 3)  \
+  X(7, 128, 128, 2, 2, 3)
+
+static inline void cfg_dims(int cfg, int& bm, int& bn) {
+#define X(id, BM, BN, WM, WN, NS) if (cfg == id) { bm = BM; bn = BN; return; }
+  CAKE_GEMM_CFGS(X)
+#undef X
+  bm = bn = 0;
+}
+
+CAKE_API int cake_gemm_tile(int cfg, int* bm, int* bn) {
+  cfg_dims(cfg, *bm, *bn);
+  return *bm > 0 ? 0 : (int)hipErrorInvalidValue;
+}
+
+template <int DT, int EPI>
+static int launch_gemm(int cfg, dim3 grid, hipStream_t st, const GemmArgs& g) {
+#define X(id, BM, BN, WM, WN, NS)                                                            \
+  if (cfg == id) {                                                                           \
+    hipLaunchKernelGGL((gemm_kernel<DT, BM, BN, WM, WN, NS, EPI>), grid, dim3(64 * WM * WN), 0, \
+                       st, g);                                                               \
+    return (int)hipGetLastError();                                                          \
+  }
+  CAKE_GEMM_CFGS(X)
+#undef X
+  return (int)hipErrorInvalidValue;
+}
+
+template <int DT>
+static int dispatch_epi(int epi, int cfg, dim3 grid, hipStream_t st, const GemmArgs& g) {
+  switch (epi) {
+    case kEpiStore: return launch_gemm<DT, kEpiStore>(cfg, grid, st, g);
+    case kEpiResid32: return launch_gemm<DT, kEpiResid32>(cfg, grid, st, g);
+    case kEpiAdd16: return launch_gemm<DT, kEpiAdd16>(cfg, grid, st, g);
+    case kEpiSwiglu: return launch_gemm<DT, kEpiSwiglu>(cfg, grid, st, g);
+    case kEpiGeglu: return launch_gemm<DT, kEpiGeglu>(cfg, grid, st, g);
+    case kEpiPartial: return launch_gemm<DT, kEpiPartial>(cfg, grid, st, g);
+  }
+  return (int)hipErrorInvalidValue;
+}
+
+template <int DT>
+static int dispatch_finalize(int epi, dim3 grid, hipStream_t st, const GemmArgs& g, int splits) {
+  switch (epi) {
+#define F(E) case E: hipLaunchKernelGGL((gemm_splitk_finalize<DT, E>), grid, dim3(256), 0, st, g, splits); break;
+    F(kEpiStore) F(kEpiResid32) F(kEpiAdd16) F(kEpiSwiglu) F(kEpiGeglu)
+#undef F
+    default: return (int)hipErrorInvalidValue;
+  }
+  return (int)hipGetLastError();
+}
+
+// y = epilogue(x W^T).  N = output features (gated: W has 2N rows, gate rows
+// [0, N), up/gate-2 rows [N, 2N)).  splits > 1 needs ws = splits * M * Nv f32.
+// Requirements (host-checked in ops/gemm.py): K % 8 == 0, lda/ldb % 8 == 0,
+// 16-byte aligned operand bases, gated => N % 16 == 0.
+CAKE_API int cake_gemm(int dt, int epi, int cfg, int splits, const void* a, long long lda,
+                       const void* b, long long ldb, void* c, long long ldc, const void* bias,
+                       void* resid, long long ldr, float* ws, const void* zeros, int M, int N,
+                       int K, hipStream_t st) {
+  int bm, bn;
+  cfg_dims(cfg, bm, bn);
+  if (bm == 0 || M <= 0 || N <= 0 || K <= 0 || K % 8 || lda % 8 || ldb % 8 || splits < 1)
+    return (int)hipErrorInvalidValue;
+  const bool gated = (epi == kEpiSwiglu || epi == kEpiGeglu);
+  if (gated && N % 16) return (int)hipErrorInvalidValue;
+  GemmArgs g{};
+  g.a = (const uint16_t*)a; g.b = (const uint16_t*)b; g.c = (uint16_t*)c;
+  g.bias = (const uint16_t*)bias;
+  g.r32 = (epi == kEpiResid32) ? (float*)resid : nullptr;
+  g.r16 = (epi == kEpiAdd16) ? (const uint16_t*)resid : nullptr;
+  g.ws = ws; g.zeros = (const uint16_t*)zeros;
+  g.lda = lda; g.ldb = ldb; g.ldc = ldc; g.ldr = ldr;
+  g.M = M; g.N = N; g.K = K;
+  g.gated = gated ? 1 : 0;
+  g.half = N;
+  g.Nv = gated ? 2 * N : N;
+  g.tiles_m = (M + bm - 1) / bm;
+  g.tiles_n = (g.Nv + bn - 1) / bn;
+  int kps = (K + splits - 1) / splits;
+  kps = (kps + kGBK - 1) / kGBK * kGBK;
+  splits = (K + kps - 1) / kps;
+  g.kps = kps;
+  const dim3 grid(g.tiles_m * g.tiles_n, splits);
+  const int kernel_epi = splits > 1 ? (int)kEpiPartial : epi;
+  if (splits > 1 && ws == nullptr) return (int)hipErrorInvalidValue;
+  int rc = (dt == kBF16) ? dispatch_epi<kBF16>(kernel_epi, cfg, grid, st, g)
+         : (dt == kF16) ? dispatch_epi<kF16>(kernel_epi, cfg, grid, st, g)
+                        : (int)hipErrorInvalidValue;
+  if (rc != 0 || splits == 1) return rc;
+  const dim3 fgrid((N + 1023) / 1024, M);
+  return (dt == kBF16) ? dispatch_finalize<kBF16>(epi, fgrid, st, g, splits)
+                       : dispatch_finalize<kF16>(epi, fgrid, st, g, splits);
+}

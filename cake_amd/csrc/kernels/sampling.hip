@@ -80,9 +80,206 @@ __global__ void push_token_kernel(const int* __restrict__ src, int* __restrict__
   *pos += 1;
 }
 
+// ---------------------------------------------------------------------------
+// Sampled decoding on the device (temperature / top-k / top-p / multinomial).
+//
+// candle's LogitsProcessor (llama.rs:34-48, 323-326) draws from
+// softmax(logits / T), optionally restricted to the top-k tokens and/or the
+// smallest top-probability prefix whose mass reaches p, with a seeded host RNG.
+// Here the draw is the Gumbel-max identity: argmax_i(l_i / T + G_i) with
+// G_i = -log(-log(U_i)) is distributed exactly as softmax(l / T), and the same
+// argmax restricted to a set S is the renormalised draw over S.  U_i comes from
+// a counter-based Philox4x32-10 keyed by the 64-bit seed with counter
+// (token index i, step = history length), so a replayed graph draws a fresh,
+// reproducible variate every step with no RNG state.  top-k / top-p reduce to
+// one threshold on the (order-preserving) logit key, found by radix select in
+// one workgroup; the draw itself is the multi-workgroup argmax of the greedy
+// path (same slot + finalize kernels).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t philox_u32(uint32_t c0, uint32_t c1, uint32_t k0,
+                                               uint32_t k1) {
+  uint32_t c2 = 0u, c3 = 0u;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+    const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+    const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c1 = lo1;
+    c3 = lo0;
+    c0 = n0;
+    c2 = n2;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c0;
+}
+
+__device__ __forceinline__ float gumbel(uint32_t bits) {
+  const float u = (float)(bits >> 8) * 5.9604644775390625e-08f + 2.98023223876953125e-08f;
+  return -__logf(-__logf(u));  // u in (0, 1)
+}
+
+__global__ __launch_bounds__(256) void gumbel_argmax_kernel(
+    const float* __restrict__ logits, int V, float inv_t, uint32_t k0, uint32_t k1,
+    const int* __restrict__ step_ptr, const unsigned int* __restrict__ thr,
+    unsigned long long* __restrict__ slot) {
+  __shared__ unsigned long long red[4];
+  const uint32_t step = (uint32_t)*step_ptr;
+  const unsigned int lim = thr != nullptr ? *thr : 0u;
+  unsigned long long best = 0;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < V; i += gridDim.x * blockDim.x) {
+    const float l = logits[i];
+    if (ordered(l) < lim) continue;
+    const float v = l * inv_t + gumbel(philox_u32((uint32_t)i, step, k0, k1));
+    const unsigned long long key =
+        ((unsigned long long)ordered(v) << 32) | (0xffffffffu - (unsigned int)i);
+    best = key > best ? key : best;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const unsigned long long o = __shfl_xor(best, off, 64);
+    best = o > best ? o : best;
+  }
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = best;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 4; ++w) best = red[w] > best ? red[w] : best;
+    atomicMax(slot, best);
+  }
+}
+
+constexpr int kSelThreads = 1024;
+
+// Block-wide max / sum (1024 threads = 16 waves).
+__device__ __forceinline__ float sel_max(float v, float* red) {
+  v = wave_max(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  float r = red[0];
+  for (int w = 1; w < kSelThreads / 64; ++w) r = fmaxf(r, red[w]);
+  return r;
+}
+
+// Threshold key: tokens with ordered(logit) >= *thr_out form the sampling set
+// (top-k, then top-p within it).  One workgroup; each radix level is one pass
+// over the logits (L2-resident right after the lm_head).
+__global__ __launch_bounds__(kSelThreads) void sample_threshold_kernel(
+    const float* __restrict__ logits, int V, float inv_t, int top_k, float top_p,
+    unsigned int* __restrict__ thr_out) {
+  __shared__ unsigned int cnt[256];
+  __shared__ float mass[256];
+  __shared__ float red[kSelThreads / 64];
+  __shared__ unsigned int sel[2];
+  const int tid = threadIdx.x;
+  unsigned int kthr = 0u;
+  if (top_k > 0 && top_k < V) {
+    unsigned int prefix = 0u, pmask = 0u;
+    int k = top_k;
+    for (int shift = 24; shift >= 0; shift -= 8) {
+      for (int b = tid; b < 256; b += kSelThreads) cnt[b] = 0u;
+      __syncthreads();
+      for (int i = tid; i < V; i += kSelThreads) {
+        const unsigned int key = ordered(logits[i]);
+        if ((key & pmask) == prefix) atomicAdd(&cnt[(key >> shift) & 255u], 1u);
+      }
+      __syncthreads();
+      if (tid == 0) {
+        int cum = 0, b = 255;
+        for (; b > 0; --b) {
+          if (cum + (int)cnt[b] >= k) break;
+          cum += (int)cnt[b];
+        }
+        sel[0] = (unsigned int)b;
+        sel[1] = (unsigned int)(k - cum);
+      }
+      __syncthreads();
+      prefix |= sel[0] << shift;
+      pmask |= 255u << shift;
+      k = (int)sel[1];
+      __syncthreads();
+    }
+    kthr = prefix;  // key of the k-th largest logit
+  }
+  unsigned int pthr = 0u;
+  if (top_p > 0.f && top_p < 1.f) {
+    float m = -INFINITY;
+    for (int i = tid; i < V; i += kSelThreads) {
+      const float l = logits[i];
+      if (ordered(l) >= kthr) m = fmaxf(m, l);
+    }
+    m = sel_max(m, red);
+    float z = 0.f;
+    for (int i = tid; i < V; i += kSelThreads) {
+      const float l = logits[i];
+      if (ordered(l) >= kthr) z += __expf((l - m) * inv_t);
+    }
+    z = wave_sum(z);
+    __syncthreads();
+    if ((tid & 63) == 0) red[tid >> 6] = z;
+    __syncthreads();
+    float Z = 0.f;
+    for (int w = 0; w < kSelThreads / 64; ++w) Z += red[w];
+    float target = top_p * Z, before = 0.f;
+    unsigned int prefix = 0u, pmask = 0u;
+    for (int shift = 24; shift >= 0; shift -= 8) {
+      for (int b = tid; b < 256; b += kSelThreads) mass[b] = 0.f;
+      __syncthreads();
+      for (int i = tid; i < V; i += kSelThreads) {
+        const float l = logits[i];
+        const unsigned int key = ordered(l);
+        if (key >= kthr && (key & pmask) == prefix)
+          atomicAdd(&mass[(key >> shift) & 255u], __expf((l - m) * inv_t));
+      }
+      __syncthreads();
+      if (tid == 0) {
+        // descending bins: the first whose inclusive mass reaches the target holds
+        // the last kept token (element J); rounding: fall back to the lowest non-empty bin
+        int b = 255, last_nz = -1;
+        float cum = before;
+        for (; b >= 0; --b) {
+          if (mass[b] > 0.f) last_nz = b;
+          if (mass[b] > 0.f && cum + mass[b] >= target) break;
+          cum += mass[b];
+        }
+        if (b < 0) { b = last_nz < 0 ? 0 : last_nz; cum -= (last_nz < 0 ? 0.f : mass[b]); }
+        sel[0] = (unsigned int)b;
+        red[0] = cum;
+      }
+      __syncthreads();
+      prefix |= sel[0] << shift;
+      pmask |= 255u << shift;
+      before = red[0];
+      __syncthreads();
+    }
+    pthr = prefix;
+  }
+  if (tid == 0) *thr_out = kthr > pthr ? kthr : pthr;
+}
+
 }  // namespace cake
 
 using namespace cake;
+
+CAKE_API int cake_sample_threshold(const float* logits, int V, float temperature, int top_k,
+                                   float top_p, unsigned int* thr, hipStream_t st) {
+  if (V <= 0 || !(temperature > 0.f)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(sample_threshold_kernel, dim3(1), dim3(kSelThreads), 0, st, logits, V,
+                     1.f / temperature, top_k, top_p, thr);
+  return (int)hipGetLastError();
+}
+
+CAKE_API int cake_gumbel_argmax(const float* logits, int V, float temperature,
+                                unsigned long long seed, const int* step, const unsigned int* thr,
+                                unsigned long long* slot, hipStream_t st) {
+  if (V <= 0 || !(temperature > 0.f)) return (int)hipErrorInvalidValue;
+  int g = (V + 255) / 256;
+  if (g > 512) g = 512;
+  hipLaunchKernelGGL(gumbel_argmax_kernel, dim3(g), dim3(256), 0, st, logits, V,
+                     1.f / temperature, (uint32_t)(seed & 0xffffffffull), (uint32_t)(seed >> 32),
+                     step, thr, slot);
+  return (int)hipGetLastError();
+}
 
 CAKE_API int cake_repeat_penalty(float* logits, const int* hist, const int* hist_len,
                                  int last_n, float penalty, hipStream_t st) {

@@ -10,8 +10,8 @@ Two execution backends share the same weights and cache layout:
 * ``hip``   — gfx950 kernels (:mod:`cake_amd.ops.hip`).  Decode (T=1) runs five
   fused launches per layer with the position read from device memory, so a
   whole token step is hipGraph-capturable; prefill (T>1) runs the projections
-  as MFMA GEMMs (``torch.matmul`` → hipBLASLt) plus our RoPE/KV-write,
-  causal-attention, SwiGLU and residual kernels.
+  on our MFMA GEMM (gemm.hip; residual / SwiGLU in its epilogues) plus the
+  RoPE/KV-write and MFMA flash-attention kernels.
 * ``torch`` — the Appendix-D reference math in PyTorch (CPU mode ``--cpu``,
   f32 dtype, and the oracle in tests).
 
@@ -64,6 +64,7 @@ class DecodeBuffers:
             self.hist = torch.zeros(max_seq, device=device, dtype=i32)
             self.hist_len = torch.zeros(1, device=device, dtype=i32)
             self.slot = torch.zeros(1, device=device, dtype=torch.int64)
+            self.thr = torch.zeros(1, device=device, dtype=torch.int32)  # top-k/p threshold
 
 
 class LayerStack:
@@ -181,6 +182,10 @@ class LayerStack:
         hidden[0].copy_(bufs.resid)
 
     def _prefill_hip(self, hidden, w, kc, vc, pos0):
+        """T > 1 block on MFMA GEMMs (gemm.hip) with fused epilogues: q|k|v in one
+        GEMM, o_proj and down_proj accumulate into the f32 residual stream, the
+        gate|up GEMM applies SwiGLU in its epilogue."""
+        from ...ops import gemm as G
         from ...ops import hip as K
         cfg = self.cfg
         T, H = hidden.shape
@@ -188,19 +193,17 @@ class LayerStack:
         K.rmsnorm(hidden, w.ln1, cfg.rms_norm_eps, x)
         nh, nkv, hd = cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim
         nq, nk = nh * hd, nkv * hd
-        qkv = torch.matmul(x, w.wqkv.t())  # one GEMM for q|k|v
+        qkv = G.linear(x, w.wqkv)  # one GEMM for q|k|v
         q, k, v = qkv[:, :nq], qkv[:, nq:nq + nk], qkv[:, nq + nk:]
         K.rope_kv(q, k, v, self.inv_freq, pos0, kc, vc)
         att = torch.empty((T, nq), device=hidden.device, dtype=self.dtype)
         Tk = pos0 + T
         K.flash_attn(q.view(1, T, nh, hd).transpose(1, 2), kc[None, :, :Tk], vc[None, :, :Tk],
                      att.view(1, T, nh, hd).transpose(1, 2), self.scale, causal=True, pos0=pos0)
-        K.add_resid(hidden, torch.matmul(att, w.wo.t()))
+        G.linear(att, w.wo, epi="resid32", resid=hidden)      # hidden += att @ wo^T
         K.rmsnorm(hidden, w.ln2, cfg.rms_norm_eps, x)
-        gu = torch.matmul(x, w.wgu.t())  # one GEMM for gate|up
-        act = torch.empty((T, cfg.intermediate_size), device=hidden.device, dtype=self.dtype)
-        K.silu_mul_rows(gu, act)
-        K.add_resid(hidden, torch.matmul(act, w.wd.t()))
+        act = G.linear(x, w.wgu, epi="swiglu")                # silu(x wg^T) * (x wu^T)
+        G.linear(act, w.wd, epi="resid32", resid=hidden)      # hidden += act @ wd^T
 
     # ------------------------------------------------------------------ torch path
     def _block_torch(self, hidden, w, kc, vc, pos0):

@@ -12,10 +12,13 @@
   ``is_end_of_stream`` when the id is an EOS id (config ``eos_token_id``
   scalar or list — Appendix E Q8 — else the ``</s>`` token).
 
-Fast path: when every block is local on the HIP backend and decoding is
-greedy, the whole step (layers + lm_head + penalty + argmax) is one hipGraph
+Fast path: when every block is local on the HIP backend, the whole step
+(layers + lm_head + penalty + argmax, or the seeded temperature / top-k /
+top-p draw — the reference's default is temperature 1.0) is one hipGraph
 replay (:class:`DeviceDecoder`) and :meth:`stream` overlaps the host token
-read-back with the next step.
+read-back with the next step.  The device RNG is Philox keyed by the seed
+(sampled ids are reproducible per seed but differ from Rust's StdRng stream:
+"parity unpinned").
 """
 from __future__ import annotations
 
@@ -103,7 +106,7 @@ class LLamaGenerator(TextGenerator):
         self.index_pos = 0
 
     def _fast_path(self) -> bool:
-        return (self.model.backend == "hip" and self.model.all_local and self.sampling.greedy)
+        return self.model.backend == "hip" and self.model.all_local
 
     def next_token(self, index: int) -> Token:
         if self.generated == 0:
@@ -129,7 +132,7 @@ class LLamaGenerator(TextGenerator):
         if self._dec is None:
             self._dec = DeviceDecoder(self.model, repeat_penalty=self.sampling.repeat_penalty,
                                       repeat_last_n=self.sampling.repeat_last_n, greedy=True,
-                                      use_graph=self._use_graph)
+                                      use_graph=self._use_graph, sampling=self.sampling)
         return self._dec
 
     def _next_token_device(self, index: int) -> Token:

@@ -128,17 +128,24 @@ class DeviceDecoder:
     """Whole-step hipGraph decoder for an all-local model on the HIP backend.
 
     Device state (DecodeBuffers): tok, pos, hist, hist_len, slot.  A step:
-    embed(tok) → layers(pos) → ln_f/lm_head → [repeat penalty] → argmax →
-    finalize (tok ← argmax, hist.append, pos += 1).  For temperature > 0 the
-    graph stops after the penalty and the host sampler pushes the token.
+    embed(tok) → layers(pos) → ln_f/lm_head → [repeat penalty] → token
+    selection → finalize (tok ← selected, hist.append, pos += 1).  Selection is
+    argmax (greedy) or, with ``sampling`` (temperature > 0), a seeded device draw
+    (top-k / top-p threshold + Gumbel-max, sampling.hip) — both inside the graph.
+    ``greedy=False`` without ``sampling`` keeps the host-sampler mode: the graph
+    stops after the penalty and the caller pushes the token.
     """
 
     def __init__(self, model: LlamaModel, repeat_penalty: float = 1.0, repeat_last_n: int = 128,
-                 greedy: bool = True, use_graph: bool = True, steps_per_graph: int = 1):
+                 greedy: bool = True, use_graph: bool = True, steps_per_graph: int = 1,
+                 sampling=None):
         if model.backend != "hip" or not model.all_local:
             raise ValueError("DeviceDecoder needs an all-local model on the hip backend")
-        # greedy decode needs no host input between steps, so several steps can
-        # share one graph launch (fewer host round trips); sampled mode is 1
+        self.sampling = sampling if sampling is not None and not sampling.greedy else None
+        if self.sampling is not None:
+            greedy = True  # token chosen on the device: no host input between steps
+        # device-selected decode needs no host input between steps, so several steps
+        # can share one graph launch (fewer host round trips); host-sampled mode is 1
         self.k = max(1, int(steps_per_graph)) if greedy and use_graph else 1
         self.m = model
         self.penalty = float(repeat_penalty)
@@ -160,8 +167,8 @@ class DeviceDecoder:
         if self.penalty != 1.0:
             K.repeat_penalty(b.logits, b.hist, b.hist_len, self.last_n, self.penalty)
         if self.greedy:
-            K.argmax(b.logits, b.slot)
-            K.finalize_token(b.slot, b.tok, b.hist, b.hist_len, b.pos)
+            K.select_token(b.logits, b.slot, b.hist, b.hist_len, b.tok, b.pos, self.sampling,
+                           b.thr)
 
     def capture(self) -> None:
         if not self.use_graph or self.graph is not None:
@@ -210,8 +217,8 @@ class DeviceDecoder:
         if self.penalty != 1.0:
             K.repeat_penalty(b.logits, b.hist, b.hist_len, self.last_n, self.penalty)
         if self.greedy:
-            K.argmax(b.logits, b.slot)
-            K.finalize_token(b.slot, b.tok, b.hist, b.hist_len, b.pos)
+            K.select_token(b.logits, b.slot, b.hist, b.hist_len, b.tok, b.pos, self.sampling,
+                           b.thr)
             self.host_pos += 1
             return int(b.tok.item())
         raise RuntimeError("sampled mode: caller pushes the first token")

@@ -6,8 +6,9 @@ bias and residual fused into the epilogue, nearest-2x upsample fused into the
 operand addressing), GroupNorm(+SiLU) is the channels-last kernel, and the
 SpatialTransformer consumes [B, HW, C] views with no permutes.  LayerNorm,
 multi-head attention (MFMA flash attention) and GEGLU are our kernels too
-(SURVEY K31-K36); the plain linears go to hipBLASLt (library GEMMs) through
-torch.  The CPU / f32 path is plain NCHW PyTorch.
+(SURVEY K31-K36); every linear is the MFMA GEMM (gemm.hip) with bias, block
+residual and GEGLU fused in its epilogue.  The CPU / f32 path is plain NCHW
+PyTorch.
 """
 from __future__ import annotations
 
@@ -155,8 +156,31 @@ def geglu(h):
     return (a * F.gelu(g, approximate="tanh")).to(h.dtype)
 
 
-def linear(x, w, b=None):
-    return F.linear(x, w, b)
+def _gemm_ok(x, w) -> bool:
+    return _hip(x) and w.dtype == x.dtype and x.shape[-1] % 8 == 0 and w.stride(-1) == 1 \
+        and w.stride(0) % 8 == 0
+
+
+def linear(x, w, b=None, resid=None, gated: str | None = None):
+    """y = x w^T (+ b) on the MFMA GEMM (gemm.hip), with fused epilogues:
+    resid -> y + resid (block residual); gated="geglu" -> GEGLU over the two halves
+    of w's rows (diffusers FeedForward proj, bias included)."""
+    if _gemm_ok(x, w):
+        from ...ops import gemm as G
+        if gated is not None:
+            return G.linear(x, w, b, epi=gated)
+        if resid is not None:
+            return G.linear(x, w, b, epi="add16", resid=resid.contiguous())
+        return G.linear(x, w, b)
+    y = F.linear(x, w, b)
+    if gated == "geglu":
+        a, g = y.float().chunk(2, -1)
+        y = (a * F.gelu(g, approximate="tanh")).to(x.dtype)
+    elif gated is not None:
+        raise ValueError(gated)
+    if resid is not None:
+        y = y + resid
+    return y
 
 
 def conv2d(x, w, b=None, stride: int = 1, padding: int = 1):

@@ -54,8 +54,9 @@ class Linear(Module):
             p[f"{self.name}.bias"] = (self.cout,)
         return p
 
-    def __call__(self, W, x):
-        return ops.linear(x, W[f"{self.name}.weight"], W.get(f"{self.name}.bias"))
+    def __call__(self, W, x, resid=None, gated=None):
+        return ops.linear(x, W[f"{self.name}.weight"], W.get(f"{self.name}.bias"), resid=resid,
+                          gated=gated)
 
 
 class Norm(Module):
@@ -117,7 +118,7 @@ class Attention(Module):
             w = W[key] = torch.cat([W[f"{self.name}.{n}.weight"] for n in names], 0)
         return w
 
-    def __call__(self, W, x, ctx=None, kv_cache=None):
+    def __call__(self, W, x, ctx=None, kv_cache=None, resid=None):
         C = self.q.cout
         if ctx is None:  # self-attention: one GEMM for q, k and v
             qkv = ops.linear(x, self._fused(W, ("to_q", "to_k", "to_v")))
@@ -135,7 +136,7 @@ class Attention(Module):
                     kv_cache[f"{self.name}@w"] = wkv
             k, v = kv[..., :C], kv[..., C:]
         a = ops.attention(q, k, v, self.heads, sliced=self.sliced)
-        return self.o(W, a)
+        return self.o(W, a, resid=resid)  # + residual in the GEMM epilogue
 
 
 class BasicTransformerBlock(Module):
@@ -155,11 +156,13 @@ class BasicTransformerBlock(Module):
 
     def __call__(self, W, x, ctx, kv_cache=None):
         n = self.name
-        x = x + self.attn1(W, ops.layer_norm(x, W[f"{n}.norm1.weight"], W[f"{n}.norm1.bias"], 1e-5))
-        x = x + self.attn2(W, ops.layer_norm(x, W[f"{n}.norm2.weight"], W[f"{n}.norm2.bias"], 1e-5),
-                           ctx, kv_cache)
+        x = self.attn1(W, ops.layer_norm(x, W[f"{n}.norm1.weight"], W[f"{n}.norm1.bias"], 1e-5),
+                       resid=x)
+        x = self.attn2(W, ops.layer_norm(x, W[f"{n}.norm2.weight"], W[f"{n}.norm2.bias"], 1e-5),
+                       ctx, kv_cache, resid=x)
         h = ops.layer_norm(x, W[f"{n}.norm3.weight"], W[f"{n}.norm3.bias"], 1e-5)
-        return x + self.ff_out(W, ops.geglu(self.ff_in(W, h)))
+        # GEGLU fused into the FF input projection, residual into the output projection
+        return self.ff_out(W, self.ff_in(W, h, gated="geglu"), resid=x)
 
 
 class Transformer2DModel(Module):
@@ -187,6 +190,8 @@ class Transformer2DModel(Module):
         h = _token_linear(W, self.proj_in.name, ops.tokens(h))
         for blk in self.blocks:
             h = blk(W, h, ctx, kv_cache)
+        if ops.nhwc():  # channels-last: the residual is a free token view of x
+            return ops.untokens(_token_linear(W, self.proj_out.name, h, resid=ops.tokens(x)), x)
         h = _token_linear(W, self.proj_out.name, h)
         return ops.untokens(h, x) + x
 
@@ -196,14 +201,19 @@ def refresh_kv_cache(kv_cache: dict, ctx: torch.Tensor) -> None:
     tensors may be baked into a captured hipGraph)."""
     for name, kv in kv_cache.items():
         if not name.endswith("@w"):
-            torch.matmul(ctx, kv_cache[f"{name}@w"].t(), out=kv)
+            w = kv_cache[f"{name}@w"]
+            if ops._gemm_ok(ctx, w):
+                from ...ops import gemm as G
+                G.linear(ctx, w, out=kv)
+            else:
+                torch.matmul(ctx, w.t(), out=kv)
 
 
-def _token_linear(W, name, t):
+def _token_linear(W, name, t, resid=None):
     w = W[f"{name}.weight"]
     if w.dim() == 4:
         w = w[:, :, 0, 0]
-    return ops.linear(t, w, W.get(f"{name}.bias"))
+    return ops.linear(t, w, W.get(f"{name}.bias"), resid=resid)
 
 
 def timestep_embedding(t: torch.Tensor, dim: int, flip_sin_to_cos: bool, shift: float) -> torch.Tensor:

@@ -1,0 +1,192 @@
+"""Host side of the MFMA GEMM (csrc/kernels/gemm.hip): y = x W^T + fused epilogue.
+
+Every T > 1 linear on the device path goes through :func:`linear`: Llama prefill
+q|k|v, o (+residual), gate|up (+SwiGLU), down (+residual); every SD UNet / VAE /
+CLIP projection (+bias, +residual, +GEGLU).  Shapes and strides are validated
+on the host before launch; there is no library fallback.
+
+Tile choice: a cost model over the kernel's tile configurations (waves of
+tiles x per-tile work, split-K when the grid is smaller than the chip), with an
+optional measured override table (:func:`set_plan`, filled by
+scripts/tune_gemm.py on the GPU box).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from ._lib import check, kernels
+
+EPI = {"store": 0, "resid32": 1, "add16": 2, "swiglu": 3, "geglu": 4}
+_DT = {torch.bfloat16: 0, torch.float16: 1}
+# (BM, BN) of the kernel's tile configurations (gemm.hip CAKE_GEMM_CFGS)
+CFG_TILES = {0: (128, 128), 1: (64, 128), 2: (256, 128), 3: (128, 256), 4: (64, 64)}
+_SLOTS = {0: 2, 1: 2, 2: 1, 3: 1, 4: 4}   # resident workgroups per CU (LDS / VGPR bound)
+_EFF = {0: 1.0, 1: 0.8, 2: 1.1, 3: 1.1, 4: 0.55}  # relative MFMA efficiency per tile
+NUM_CUS = 256
+_bound = False
+_plans: dict = {}
+_ws: dict = {}
+_zeros: dict = {}
+
+
+def _lib():
+    global _bound
+    lib = kernels()
+    if not _bound:
+        P, I, L = C.c_void_p, C.c_int, C.c_longlong
+        lib.cake_gemm.argtypes = [I, I, I, I, P, L, P, L, P, L, P, P, L, P, P, I, I, I, P]
+        lib.cake_gemm.restype = I
+        _bound = True
+    return lib
+
+
+def _zeros16(dev) -> torch.Tensor:
+    z = _zeros.get(dev)
+    if z is None:
+        z = _zeros[dev] = torch.zeros(64, dtype=torch.int32, device=dev)
+    return z
+
+
+_ws_keep: list = []
+
+
+def _workspace(dev, numel: int) -> torch.Tensor:
+    """Split-K slabs.  Superseded buffers are kept alive: a captured hipGraph may
+    still point at them."""
+    w = _ws.get(dev)
+    if w is None or w.numel() < numel:
+        if w is not None:
+            _ws_keep.append(w)
+        w = _ws[dev] = torch.empty(max(numel, 1 << 20), dtype=torch.float32, device=dev)
+    return w
+
+
+def set_plan(M: int, N: int, K: int, epi: str, cfg: int, splits: int) -> None:
+    """Pin the tile configuration / split-K of one shape (measured tuning)."""
+    _plans[(M, N, K, epi)] = (cfg, splits)
+
+
+def plan(M: int, Nv: int, K: int, epi: str = "store") -> tuple[int, int]:
+    """(cfg, splits) for an M x Nv x K problem (Nv = weight rows read)."""
+    p = _plans.get((M, Nv, K, epi))
+    if p is not None:
+        return p
+    best = None
+    ksteps = -(-K // 64)
+    cands = (1, 4) if M <= 64 else (0, 2, 3, 1)
+    for cfg in cands:
+        bm, bn = CFG_TILES[cfg]
+        tiles = -(-M // bm) * -(-Nv // bn)
+        for splits in (1, 2, 4, 8, 16):
+            if splits > 1 and (ksteps // splits < 4 or tiles * splits > 2 * NUM_CUS * _SLOTS[cfg]):
+                continue
+            waves = -(-tiles * splits // (NUM_CUS * _SLOTS[cfg]))
+            cost = waves * _SLOTS[cfg] * bm * bn * (-(-ksteps // splits)) / _EFF[cfg]
+            cost += (splits > 1) * M * Nv * splits * 0.1   # slab round trip + finalize
+            if best is None or cost < best[0]:
+                best = (cost, cfg, splits)
+    return best[1], best[2]
+
+
+def _rows_view(t: torch.Tensor, name: str) -> tuple[torch.Tensor, int]:
+    """[..., C] tensor with unit column stride -> ([R, C] VIEW of it, row stride)."""
+    if t.dim() < 2:
+        t = t.view(1, -1)
+    if t.stride(-1) != 1:
+        raise ValueError(f"{name}: needs unit column stride")
+    if t.dim() > 2:
+        try:
+            t2 = t.view(-1, t.shape[-1])   # never a copy: outputs are written through it
+        except RuntimeError:
+            raise ValueError(f"{name}: leading dims do not flatten to one row stride") from None
+    else:
+        t2 = t
+    if t2.dim() == 2 and t2.shape[0] > 1 and t2.stride(0) < t2.shape[1]:
+        raise ValueError(f"{name}: overlapping rows")
+    return t2, (t2.stride(0) if t2.shape[0] > 1 else t2.shape[1])
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, *,
+           epi: str = "store", out: torch.Tensor | None = None,
+           resid: torch.Tensor | None = None, cfg: int | None = None,
+           splits: int | None = None) -> torch.Tensor:
+    """y = epilogue(x @ w.T) on MFMA.
+
+    x [..., K] (16-bit, unit column stride, any row stride that is a multiple of
+    8); w [N, K] ([2F, K] for the gated epilogues: rows [0, F) gate/h, [F, 2F)
+    up/gate).  Epilogues:
+      store   -> out [..., N] = y (+ bias)
+      resid32 -> resid (f32 [..., N]) += y (+ bias); returns resid
+      add16   -> out = y (+ bias) + resid (16-bit [..., N])
+      swiglu  -> out [..., F] = silu(y_gate) * y_up
+      geglu   -> out [..., F] = (y_h + b_h) * gelu_tanh(y_gate + b_gate)
+    """
+    if epi not in EPI:
+        raise ValueError(f"unknown epilogue {epi}")
+    if not (x.is_cuda and w.is_cuda) or x.dtype not in _DT or w.dtype != x.dtype:
+        raise TypeError("gemm.linear: 16-bit device tensors of one dtype expected")
+    lead = x.shape[:-1]
+    K = x.shape[-1]
+    if x.dim() > 2 and x.stride(-1) == 1:
+        try:
+            x.view(-1, K)
+        except RuntimeError:
+            x = x.contiguous()
+    x2, lda = _rows_view(x, "x")
+    M = x2.shape[0]
+    if w.dim() != 2 or w.shape[1] != K or w.stride(1) != 1:
+        raise ValueError(f"gemm.linear: weight {tuple(w.shape)} does not match K={K}")
+    ldb = w.stride(0)
+    gated = epi in ("swiglu", "geglu")
+    Nv = w.shape[0]
+    if gated and Nv % 32:
+        raise ValueError("gated epilogue needs 2F weight rows with F % 16 == 0")
+    N = Nv // 2 if gated else Nv
+    if K % 8 or lda % 8 or ldb % 8 or x2.data_ptr() % 16 or w.data_ptr() % 16:
+        raise ValueError("gemm.linear: K, row strides must be multiples of 8 and bases 16-byte "
+                         "aligned")
+    if bias is not None:
+        if not (bias.is_cuda and bias.dtype == x.dtype and bias.is_contiguous()
+                and bias.numel() == Nv):
+            raise ValueError(f"gemm.linear: bias must be a contiguous {x.dtype} [{Nv}] tensor")
+    ldr = 0
+    rptr = None
+    if epi == "resid32":
+        if resid is None or resid.dtype != torch.float32 or not resid.is_cuda:
+            raise ValueError("resid32 needs an f32 device residual")
+        r2, ldr = _rows_view(resid, "resid")
+        if tuple(r2.shape) != (M, N):
+            raise ValueError(f"resid shape {tuple(resid.shape)} != {(M, N)}")
+        rptr = r2.data_ptr()
+    elif epi == "add16":
+        if resid is None or resid.dtype != x.dtype or not resid.is_cuda:
+            raise ValueError("add16 needs a 16-bit device residual")
+        r2, ldr = _rows_view(resid, "resid")
+        if tuple(r2.shape) != (M, N):
+            raise ValueError(f"resid shape {tuple(resid.shape)} != {(M, N)}")
+        rptr = r2.data_ptr()
+    if epi == "resid32":
+        out2, ldc, cptr = None, 0, None
+    else:
+        if out is None:
+            out = torch.empty(*lead, N, device=x.device, dtype=x.dtype)
+        if out.dtype != x.dtype or not out.is_cuda:
+            raise ValueError("out dtype/device mismatch")
+        out2, ldc = _rows_view(out, "out")
+        if tuple(out2.shape) != (M, N):
+            raise ValueError(f"out shape {tuple(out.shape)} != {(M, N)}")
+        cptr = out2.data_ptr()
+    if M == 0:
+        return resid if epi == "resid32" else out
+    c0, s0 = plan(M, Nv, K, epi)
+    cfg = c0 if cfg is None else cfg
+    splits = s0 if splits is None else max(1, int(splits))
+    ws = _workspace(x.device, splits * M * Nv) if splits > 1 else None
+    check(_lib().cake_gemm(_DT[x.dtype], EPI[epi], int(cfg), int(splits), x2.data_ptr(), lda,
+                           w.data_ptr(), ldb, cptr, ldc,
+                           None if bias is None else bias.data_ptr(), rptr, ldr,
+                           None if ws is None else ws.data_ptr(), _zeros16(x.device).data_ptr(),
+                           M, N, K, torch.cuda.current_stream().cuda_stream), "gemm")
+    return resid if epi == "resid32" else out

@@ -240,6 +240,43 @@ def argmax(logits, slot):
     check(kernels().cake_argmax(_p(logits), logits.numel(), _p(slot), _stream()), "argmax")
 
 
+def sample_threshold(logits, temperature: float, top_k: int | None, top_p: float | None, thr):
+    """thr (int32[1]) <- order key of the least logit in the top-k / top-p set."""
+    _req(logits, "logits", dtype=torch.float32)
+    _req(thr, "thr", dtype=torch.int32, numel=1)
+    check(kernels().cake_sample_threshold(_p(logits), logits.numel(), float(temperature),
+                                          int(top_k or 0), float(top_p or 0.0), _p(thr),
+                                          _stream()), "sample_threshold")
+
+
+def gumbel_argmax(logits, temperature: float, seed: int, step, slot, thr=None):
+    """slot <- argmax_i(logits_i / T + Gumbel_i) over logits keys >= thr: one draw from
+    softmax(logits / T) restricted to the set (Philox(seed; i, *step) variates)."""
+    _req(logits, "logits", dtype=torch.float32)
+    _req(step, "step", dtype=torch.int32, numel=1)
+    _req(slot, "slot", dtype=torch.int64, numel=1)
+    if thr is not None:
+        _req(thr, "thr", dtype=torch.int32, numel=1)
+    check(kernels().cake_gumbel_argmax(_p(logits), logits.numel(), float(temperature),
+                                       int(seed) & 0xFFFFFFFFFFFFFFFF, _p(step), _p(thr),
+                                       _p(slot), _stream()), "gumbel_argmax")
+
+
+def select_token(logits, slot, hist, hist_len, tok, pos, sampling=None, thr=None):
+    """Device token selection of one decode step: argmax (greedy) or a seeded draw
+    (temperature / top-k / top-p), then the step finalizer (tok, history, pos)."""
+    if sampling is None or sampling.greedy:
+        argmax(logits, slot)
+    else:
+        restrict = (sampling.top_k is not None and sampling.top_k > 0) or \
+            (sampling.top_p is not None and 0.0 < sampling.top_p < 1.0)
+        if restrict:
+            sample_threshold(logits, sampling.temperature, sampling.top_k, sampling.top_p, thr)
+        gumbel_argmax(logits, sampling.temperature, sampling.seed, hist_len, slot,
+                      thr if restrict else None)
+    finalize_token(slot, tok, hist, hist_len, pos)
+
+
 def finalize_token(slot, tok, hist, hist_len, pos):
     for t, n in ((tok, "tok"), (hist, "hist"), (hist_len, "hist_len"), (pos, "pos")):
         _req(t, n, dtype=torch.int32)

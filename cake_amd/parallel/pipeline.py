@@ -137,7 +137,8 @@ class PipelineEngine:
             if missing:
                 raise ValueError(f"rank {rank} lacks weights for layers {missing}")
         self.penalty, self.last_n = float(repeat_penalty), int(repeat_last_n)
-        self.sampler = None  # host sampler (temperature > 0); None = greedy on device
+        self.sampler = None   # host sampler (torch backend); None = selection on the device
+        self.sampling = None  # SamplingConfig for the device draw (temperature > 0)
         self.hip = stack.backend == "hip"
         self.use_graph = use_graph and self.hip
         self.group = group
@@ -454,14 +455,15 @@ class PipelineEngine:
         return int(torch.argmax(logits))
 
     def _select_device(self, st: _Stream) -> None:
-        """Penalty (+ argmax + next-token bookkeeping when greedy) on the device."""
+        """Penalty + token selection (argmax, or the seeded device draw when
+        ``self.sampling`` is set) + next-token bookkeeping, on the device."""
         from ..ops import hip as K
         b = st.bufs
         if self.penalty != 1.0:
             K.repeat_penalty(b.logits, b.hist, b.hist_len, self.last_n, self.penalty)
         if self.sampler is None:
-            K.argmax(b.logits, b.slot)
-            K.finalize_token(b.slot, b.tok, b.hist, b.hist_len, b.pos)
+            K.select_token(b.logits, b.slot, b.hist, b.hist_len, b.tok, b.pos, self.sampling,
+                           b.thr)
 
     def _host_sample_device(self, st: _Stream) -> int:
         """Sampled decoding on the hip path: draw on the host, push to the device state."""

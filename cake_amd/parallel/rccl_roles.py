@@ -50,8 +50,10 @@ class PipelineLLM(TextGenerator):
         self.tokens: list[int] = []
         self.generated = 0
         if not sampling.greedy:
-            lp = LogitsProcessor(sampling)
-            engine.sampler = lp.sample
+            if engine.hip:   # seeded temperature / top-k / top-p draw inside the graph
+                engine.sampling = sampling
+            else:
+                engine.sampler = LogitsProcessor(sampling).sample
         self.last_stats = None
 
     @classmethod

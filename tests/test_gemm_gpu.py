@@ -1,0 +1,118 @@
+"""MFMA GEMM (gemm.hip) vs a plain-PyTorch f32 reference, every epilogue and tile config,
+split-K, ragged M/N edges, strided inputs, and the Llama-3 8B/70B + SDXL shapes."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DTYPES = [torch.bfloat16, torch.float16]
+
+
+def _r(*shape, dt, std=1.0):
+    return (torch.randn(*shape, device="cuda") * std).to(dt)
+
+
+def _ref(x, w, b=None):
+    y = x.float() @ w.float().t()
+    return y if b is None else y + b.float()
+
+
+def _close(got, ref, K):
+    # bf16/f16 output rounding + f32 accumulation-order differences
+    tol = 2e-2 * max(1.0, float(ref.abs().max()))
+    torch.testing.assert_close(got.float(), ref, atol=tol, rtol=2e-2)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("M,N,K,splits", [(128, 256, 256, 1), (77, 200, 320, 1),
+                                          (300, 520, 1024, 3), (1, 64, 64, 1),
+                                          (513, 136, 648, 2)])
+def test_gemm_store_configs(cuda, dt, cfg, M, N, K, splits):
+    from cake_amd.ops import gemm as G
+    torch.manual_seed(M + N + K)
+    x, w, b = _r(M, K, dt=dt), _r(N, K, dt=dt, std=K ** -0.5), _r(N, dt=dt)
+    y = G.linear(x, w, b, cfg=cfg, splits=splits)
+    _close(y, _ref(x, w, b), K)
+    y2 = G.linear(x, w, cfg=cfg, splits=splits)
+    _close(y2, _ref(x, w), K)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("splits", [1, 4])
+def test_gemm_resid32_and_add16(cuda, dt, splits):
+    from cake_amd.ops import gemm as G
+    torch.manual_seed(1)
+    M, N, K = 200, 4096, 1024
+    x, w = _r(M, K, dt=dt), _r(N, K, dt=dt, std=K ** -0.5)
+    r = torch.randn(M, N, device="cuda")
+    ref = r + _ref(x, w)
+    G.linear(x, w, epi="resid32", resid=r, splits=splits)
+    torch.testing.assert_close(r, ref, atol=3e-2, rtol=1e-2)
+    b, r16 = _r(N, dt=dt), _r(M, N, dt=dt)
+    y = G.linear(x, w, b, epi="add16", resid=r16, splits=splits)
+    _close(y, _ref(x, w, b) + r16.float(), K)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("M,Fh,K,splits", [(37, 512, 512, 1), (130, 1024, 1024, 2),
+                                          (257, 48, 320, 1)])
+def test_gemm_gated(cuda, dt, M, Fh, K, splits):
+    from cake_amd.ops import gemm as G
+    torch.manual_seed(2)
+    x, w = _r(M, K, dt=dt), _r(2 * Fh, K, dt=dt, std=K ** -0.5)
+    y = _ref(x, w)
+    g = G.linear(x, w, epi="swiglu", splits=splits)
+    _close(g, F.silu(y[:, :Fh]) * y[:, Fh:], K)
+    b = _r(2 * Fh, dt=dt)
+    yb = _ref(x, w, b)
+    h = G.linear(x, w, b, epi="geglu", splits=splits)
+    _close(h, yb[:, :Fh] * F.gelu(yb[:, Fh:], approximate="tanh"), K)
+
+
+def test_gemm_strided_views(cuda):
+    """q|k|v column slices as inputs, 3-D token tensors, an output written into a view."""
+    from cake_amd.ops import gemm as G
+    dt = torch.bfloat16
+    torch.manual_seed(3)
+    qkv = _r(2, 50, 3 * 320, dt=dt)
+    q = qkv[..., :320]
+    w = _r(640, 320, dt=dt, std=320 ** -0.5)
+    _close(G.linear(q, w), _ref(q.reshape(-1, 320), w).view(2, 50, 640), 320)
+    out = torch.zeros(100, 2 * 640, device="cuda", dtype=dt)
+    G.linear(q.reshape(100, 320), w, out=out[:, 640:])
+    assert out[:, :640].abs().sum() == 0
+    _close(out[:, 640:], _ref(q.reshape(100, 320), w), 320)
+
+
+@pytest.mark.parametrize("name,M,N,K,epi", [
+    ("8b_qkv", 512, 6144, 4096, "store"), ("8b_o", 512, 4096, 4096, "resid32"),
+    ("8b_gateup", 512, 14336, 4096, "swiglu"), ("8b_down", 512, 4096, 14336, "resid32"),
+    ("8b_qkv_t32", 32, 6144, 4096, "store"), ("70b_qkv", 256, 10240, 8192, "store"),
+    ("70b_down", 128, 8192, 28672, "resid32"),
+    ("sdxl_ff_in", 2048, 5120, 640, "geglu"), ("sdxl_ff_out", 2048, 640, 2560, "add16"),
+    ("sdxl_qkv_1280", 2048, 3840, 1280, "store"), ("clip_fc1", 77, 3072, 768, "store")])
+def test_gemm_model_shapes(cuda, name, M, N, K, epi):
+    from cake_amd.ops import gemm as G
+    dt = torch.bfloat16
+    torch.manual_seed(4)
+    x = _r(M, K, dt=dt)
+    if epi in ("swiglu", "geglu"):
+        w = _r(2 * N, K, dt=dt, std=K ** -0.5)
+        y = _ref(x, w)
+        ref = (F.silu(y[:, :N]) * y[:, N:]) if epi == "swiglu" else \
+            y[:, :N] * F.gelu(y[:, N:], approximate="tanh")
+        _close(G.linear(x, w, epi=epi), ref, K)
+        return
+    w = _r(N, K, dt=dt, std=K ** -0.5)
+    if epi == "resid32":
+        r = torch.randn(M, N, device="cuda")
+        ref = r + _ref(x, w)
+        G.linear(x, w, epi=epi, resid=r)
+        torch.testing.assert_close(r, ref, atol=3e-2, rtol=1e-2)
+    elif epi == "add16":
+        r16 = _r(M, N, dt=dt)
+        _close(G.linear(x, w, epi=epi, resid=r16), _ref(x, w) + r16.float(), K)
+    else:
+        _close(G.linear(x, w), _ref(x, w), K)
