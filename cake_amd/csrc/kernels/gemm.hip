@@ -169,48 +169,61 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(GemmArgs g) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = cf32x4{0.f, 0.f, 0.f, 0.f};
 
-  // One barrier per k-step.  At the top of step t every wave waits for its own
-  // DMA of step t (counted vmcnt: with 3 stages the DMA of t+1 stays in flight)
-  // and the barrier then publishes every wave's; the same barrier proves every
-  // wave finished reading step t-1's buffer (its reads completed before its
-  // MFMAs), so the DMA issued right after it may overwrite that buffer: step t+1
-  // (2 stages) or t+2 (3 stages).  Within a step the k 32..63 fragment reads
-  // overlap the k 0..31 MFMAs.
+  // One barrier per k-step, placed between the k 0..31 and k 32..63 halves so
+  // that LDS latency never sits in front of the MFMAs:
+  //   [kk1 reads of t] [kk0 MFMAs of t] wait | vmcnt(DMA t+1) barrier
+  //   [DMA t+NS into t's buffer] [kk0 reads of t+1] [kk1 MFMAs of t] wait
+  // The barrier publishes every wave's DMA of step t+1 and proves every wave
+  // finished reading step t's buffer (its kk1 reads completed before it), so
+  // the DMA issued right after it may overwrite that buffer.
+  uint4 af0[FM], bf0[FN], af1[FM], bf1[FN];
   if (nk > 0) stage(0, 0);
   if (NS == 3 && nk > 1) stage(1, 1);
-  int buf = 0;
-  for (int t = 0; t < nk; ++t) {
-    if (NS == 3 && t + 1 < nk) __builtin_amdgcn_s_waitcnt(vm_wait(IPW));
+  if (nk > 0) {
+    if (NS == 3 && nk > 1) __builtin_amdgcn_s_waitcnt(vm_wait(IPW));
     else __builtin_amdgcn_s_waitcnt(vm_wait(0));
     asm volatile("s_barrier" ::: "memory");
-    if (t + NS - 1 < nk) {
-      int nb = buf + NS - 1;
-      nb = nb >= NS ? nb - NS : nb;
-      stage(t + NS - 1, nb);
-    }
-    uint4 af[FM][2], bfr[FN][2];
+    if (NS - 1 < nk) stage(NS - 1, NS - 1);
+#pragma unroll
+    for (int i = 0; i < FM; ++i) af0[i] = ds_read16(a_base + i * 16 * 128 + off0);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) bf0[j] = ds_read16(b_base + j * 16 * 128 + off0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  int buf = 0;
+  for (int t = 0; t < nk; ++t) {
     const uint32_t ab = a_base + buf * BUF, bb = b_base + buf * BUF;
 #pragma unroll
-    for (int i = 0; i < FM; ++i) af[i][0] = ds_read16(ab + i * 16 * 128 + off0);
+    for (int i = 0; i < FM; ++i) af1[i] = ds_read16(ab + i * 16 * 128 + off1);
 #pragma unroll
-    for (int j = 0; j < FN; ++j) bfr[j][0] = ds_read16(bb + j * 16 * 128 + off0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int i = 0; i < FM; ++i) af[i][1] = ds_read16(ab + i * 16 * 128 + off1);
-#pragma unroll
-    for (int j = 0; j < FN; ++j) bfr[j][1] = ds_read16(bb + j * 16 * 128 + off1);
+    for (int j = 0; j < FN; ++j) bf1[j] = ds_read16(bb + j * 16 * 128 + off1);
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = cmfma<DT>(af[i][0], bfr[j][0], acc[i][j]);
+      for (int j = 0; j < FN; ++j) acc[i][j] = cmfma<DT>(af0[i], bf0[j], acc[i][j]);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
+    const int nbuf = buf + 1 == NS ? 0 : buf + 1;
+    if (t + 1 < nk) {
+      // DMAs still allowed in flight: step t+2's (3 stages, issued last iteration)
+      if (NS == 3 && t + 2 < nk) __builtin_amdgcn_s_waitcnt(vm_wait(IPW));
+      else __builtin_amdgcn_s_waitcnt(vm_wait(0));
+      asm volatile("s_barrier" ::: "memory");
+      if (t + NS < nk) stage(t + NS, buf);
+      const uint32_t na = a_base + nbuf * BUF, nb = b_base + nbuf * BUF;
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af0[i] = ds_read16(na + i * 16 * 128 + off0);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bf0[j] = ds_read16(nb + j * 16 * 128 + off0);
+    }
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = cmfma<DT>(af[i][1], bfr[j][1], acc[i][j]);
-    buf = buf + 1 == NS ? 0 : buf + 1;
+      for (int j = 0; j < FN; ++j) acc[i][j] = cmfma<DT>(af1[i], bf1[j], acc[i][j]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    buf = nbuf;
   }
 
   // ---- epilogue: 16-row strips staged through this wave's LDS slice --------
