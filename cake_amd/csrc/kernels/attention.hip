@@ -24,29 +24,30 @@ namespace cake {
 // ---------------------------------------------------------------------------
 // decode (flash-decoding, split-K over the live context)
 // ---------------------------------------------------------------------------
-// Grid (nkv, maxsplit), 4 waves per workgroup.  A workgroup = (kv head g,
-// split s) and computes all NREP query heads of the GQA group, so every K/V
-// byte is read from HBM once per token.  The live length Tk = pos + 1 is read
-// on the device (the launch is graph-replayed at every position) and cut into
-// 64-key chunks; a split owns `cps` consecutive chunks (cps = max(min_chunks,
-// ceil(chunks / maxsplit))), its 4 waves take one chunk each (looping when
-// cps > 4).  A chunk is ONE round trip: every load is issued before the first
-// use — K rows by LDS-DMA into this wave's LDS slice (16-byte slots XOR-
-// swizzled on the source address so the row-per-lane ds_read_b128 is
-// conflict-free), V rows straight to registers (lane = two head dims), q once
-// per workgroup.  Per wave: lane j scores key j for each head, online softmax
+// Grid (nkv, maxsplit).  One workgroup = (kv head g, split s) and runs all
+// NREP query heads of the GQA group (one wave each), so every K/V byte is read
+// from HBM once per token.  The number of live splits is derived ON DEVICE from
+// the live length Tk = pos + 1 (the launch is graph-replayed at every
+// position): ns = min(maxsplit, ceil(Tk / min_keys)); each split owns a
+// contiguous range of whole 64-key chunks.  Chunks are streamed
+// global -> registers (every load of the next chunk is issued before the
+// current chunk is computed) -> LDS (K rows padded 16 B: conflict-free
+// row-per-lane ds_read_b128).  Per wave: lane j scores key j, online softmax
 // in base 2 (scale * log2 e folded into q), P·V with lanes over head dims.
-// The waves merge in LDS; with one split (short contexts: Tk <= 64 * min_chunks)
-// that is the output, with no further hand-off.
 //
-// Splits publish (m, l, o[HD]) with write-through (sc1) stores, drain
+// Combine: splits publish (m, l, o[HD]) with write-through (sc1) stores, drain
 // (vmcnt 0), barrier, then one relaxed agent-scope ticket add per workgroup;
 // the workgroup whose add returns ns - 1 reads every partial with sc1 loads
-// (MI355X_MICROARCH "Valid forms", row 1) and writes the head outputs.
-constexpr int kChunk = 64;         // keys per wave chunk (one per lane)
-constexpr int kMaxSplit = 64;      // splits per kv head (partials merged lane-parallel)
-constexpr int kAttnWaves = 4;
-static int g_attn_min_chunks = 4;  // min chunks per split (tunable)
+// (MI355X_MICROARCH "Valid forms", row 1) and writes the head outputs.  ns == 1
+// (short contexts) writes the output directly.
+constexpr int kChunk = 64;        // keys per LDS chunk (one per lane)
+constexpr int kMaxSplit = 64;     // splits per kv head (partials merged lane-parallel)
+static int g_attn_min_keys = 64;  // min keys per split (tunable)
+
+template <int NREP> struct AttnGeom {
+  static constexpr int NW = NREP < 4 ? 4 : NREP;  // waves (>= 4 so loads stay wide)
+  static constexpr int NT = 64 * NW;
+};
 
 __device__ __forceinline__ void st_sc1(float* p, float v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -56,197 +57,152 @@ __device__ __forceinline__ float ld_sc1(const float* p) {
 }
 
 template <int DT, int HD, int NREP>
-__global__ __launch_bounds__(64 * kAttnWaves) void attn_decode_kernel(
+__global__ __launch_bounds__(AttnGeom<NREP>::NT) void attn_decode_kernel(
     const float* __restrict__ q, const uint16_t* __restrict__ kc,
     const uint16_t* __restrict__ vc, const int* __restrict__ pos_ptr, int S, float scale_log2,
     float* __restrict__ part, unsigned int* __restrict__ tickets, uint16_t* __restrict__ out,
-    int min_chunks) {
-  constexpr int NW = kAttnWaves, NT = 64 * NW;
-  constexpr int DPL = HD / 64;              // head dims per lane (P·V)
-  constexpr int CPR = HD / 8;               // 16-byte pieces per K row
-  constexpr int KIPW = kChunk * CPR / 64;   // K LDS-DMA wave-instructions per chunk
-  constexpr int KBYTES = kChunk * HD * 2;   // one wave's K slice
-  constexpr int HPW = (NREP + NW - 1) / NW; // heads merged per wave
-  // one LDS array: [NW][K chunk] 16-bit | q [NREP][HD] f32 | p [NW][NREP][64] |
-  // merge [NW][NREP][HD + 2] | flag
-  constexpr int OFF_Q = NW * KBYTES;
-  constexpr int OFF_P = OFF_Q + NREP * HD * 4;
-  constexpr int OFF_M = OFF_P + NW * NREP * kChunk * 4;
-  constexpr int OFF_F = OFF_M + NW * NREP * (HD + 2) * 4;
-  __shared__ __attribute__((aligned(16))) uint8_t smem[OFF_F + 16];
-  float* qs = reinterpret_cast<float*>(smem + OFF_Q);
-  float* ps = reinterpret_cast<float*>(smem + OFF_P);
-  float* ms = reinterpret_cast<float*>(smem + OFF_M);
-  unsigned int& last_flag = *reinterpret_cast<unsigned int*>(smem + OFF_F);
+    int min_keys) {
+  constexpr int NT = AttnGeom<NREP>::NT;
+  constexpr int NW = AttnGeom<NREP>::NW;
+  constexpr int DPL = HD / 64;              // output dims per lane
+  constexpr int CPR = HD / 8;               // 16-byte pieces per row
+  constexpr int PIECES = kChunk * CPR;      // pieces per chunk (each of K and V)
+  constexpr int IPW = PIECES / 64 / NW;     // LDS-DMA wave-instructions per wave (each of K, V)
+  static_assert(IPW >= 1 && PIECES % (64 * NW) == 0, "chunk/wave geometry");
+  // one LDS array (LDS-DMA pipelines need it: MI355X guide, GEMM item 4a):
+  // [2 buffers][K chunk | V chunk] 16-bit, then q (f32, pre-scaled), then p rows
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * 2 * PIECES * 8 + NREP * HD * 2 +
+                                                        NREP * kChunk * 2 + 2];
+  float* qs = reinterpret_cast<float*>(smem + 2 * 2 * PIECES * 8);
+  float* ps = qs + NREP * HD;
+  unsigned int& last_flag = *reinterpret_cast<unsigned int*>(ps + NREP * kChunk);
 
   const int g = blockIdx.x, s = blockIdx.y;
   const int Tk = *pos_ptr + 1;
-  const int C = (Tk + kChunk - 1) / kChunk;
-  int cps = (C + (int)gridDim.y - 1) / (int)gridDim.y;
-  cps = cps > min_chunks ? cps : min_chunks;
-  const int ns = (C + cps - 1) / cps;
+  int ns = (Tk + min_keys - 1) / min_keys;
+  if (ns > (int)gridDim.y) ns = gridDim.y;
+  int kps = (Tk + ns - 1) / ns;
+  kps = (kps + kChunk - 1) / kChunk * kChunk;
+  ns = (Tk + kps - 1) / kps;
   if (s >= ns) return;
-  const int c_end = min(C, (s + 1) * cps);
+  const int kb = s * kps, ke = min(Tk, kb + kps);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+
+
   const uint16_t* kg = kc + (size_t)g * S * HD;
   const uint16_t* vg = vc + (size_t)g * S * HD;
-  uint8_t* kslice = smem + wave * KBYTES;
-
-  float m[NREP], l[NREP], o[NREP][DPL];
+  // Stage chunk [c0, c0 + 64) into buffer b.  LDS piece P (row P / CPR, slot
+  // P % CPR) of K holds key piece slot ^ (row % CPR): an XOR swizzle applied on
+  // the SOURCE address (the DMA writes lane-linear), so the row-per-lane
+  // ds_read_b128 of the scores is conflict-free.  V stays linear.  Rows past
+  // the live end re-read the last live row (never outside the cache).
+  auto stage = [&](int c0, int b) {
+    const int last = ke - 1 - c0;
+    uint16_t* kd = smem + b * 2 * PIECES * 8;
+    uint16_t* vd = kd + PIECES * 8;
 #pragma unroll
-  for (int h = 0; h < NREP; ++h) {
-    m[h] = -INFINITY;
-    l[h] = 0.f;
-#pragma unroll
-    for (int d = 0; d < DPL; ++d) o[h][d] = 0.f;
-  }
-  bool first = true;
-  for (int c = s * cps + wave; c < c_end || first; c += NW) {
-    const bool active = c < c_end;
-    const int k0 = c * kChunk;
-    const int kn = active ? min(kChunk, Tk - k0) : 0;
-    // ---- issue every load of this chunk (one round trip).  V first: with the
-    // LDS-DMA issued last hipcc keeps all of them in flight (K DMA first made it
-    // drain vmcnt(0) before the 16th DMA) --------------------------------------
-    uint32_t vr[kChunk][1];
-    if (active) {
-#pragma unroll
-      for (int r = 0; r < kChunk; ++r) {
-        const int rr = r < kn ? r : kn - 1;
-        if constexpr (DPL == 2)
-          vr[r][0] = *reinterpret_cast<const uint32_t*>(vg + (size_t)(k0 + rr) * HD + lane * 2);
-        else
-          vr[r][0] = (uint32_t)vg[(size_t)(k0 + rr) * HD + lane];
-      }
-#pragma unroll
-      for (int i = 0; i < KIPW; ++i) {
-        const int P = i * 64 + lane;              // LDS slot (row P / CPR, piece P % CPR)
-        const int r = P / CPR, pc = P % CPR;
-        const int rr = r < kn ? r : kn - 1;       // never past the live rows
-        glds16(kg + (size_t)(k0 + rr) * HD + ((pc ^ (r % CPR)) * 8), kslice + i * 1024);
-      }
+    for (int i = 0; i < IPW; ++i) {
+      const int P = (wave * IPW + i) * 64 + lane;
+      const int r = P / CPR, c = P % CPR;
+      const int rr = r < last ? r : last;
+      glds16(kg + (size_t)(c0 + rr) * HD + (c ^ (r % CPR)) * 8, kd + (wave * IPW + i) * 64 * 8);
+      glds16(vg + (size_t)(c0 + rr) * HD + c * 8, vd + (wave * IPW + i) * 64 * 8);
     }
-    if (first) {  // q of the whole GQA group, pre-scaled (loads overlap the chunk's)
-      for (int i = tid; i < NREP * HD; i += NT) qs[i] = q[(size_t)g * NREP * HD + i] * scale_log2;
-      __builtin_amdgcn_s_waitcnt(vm_wait(0));
-      __syncthreads();
-      first = false;
+  };
+
+  float m = -INFINITY, l = 0.f, o[DPL];
+#pragma unroll
+  for (int d = 0; d < DPL; ++d) o[d] = 0.f;
+  stage(kb, 0);
+  // q after the first chunk's DMA: one round trip covers both (hipcc drains the
+  // DMA together with the q loads before the LDS stores below)
+  for (int i = tid; i < NREP * HD; i += NT) qs[i] = q[(size_t)g * NREP * HD + i] * scale_log2;
+  __syncthreads();
+  int buf = 0;
+  for (int c0 = kb; c0 < ke; c0 += kChunk, buf ^= 1) {
+    const int kn = min(kChunk, ke - c0);
+    if (c0 + kChunk < ke) {  // next chunk streams while this one computes
+      stage(c0 + kChunk, buf ^ 1);
+      __builtin_amdgcn_s_waitcnt(vm_wait(2 * IPW));
     } else {
       __builtin_amdgcn_s_waitcnt(vm_wait(0));
-      __builtin_amdgcn_wave_barrier();
     }
-    if (!active) break;
-    // ---- scores: lane j <-> key k0 + j, all heads ------------------------
-    float sc[NREP];
+    __builtin_amdgcn_s_barrier();  // every wave's DMA for this chunk has landed
+    const uint16_t* Ks = smem + buf * 2 * PIECES * 8;
+    const uint16_t* Vs = Ks + PIECES * 8;
+    if (wave < NREP) {
+      float sc = -INFINITY;
+      if (lane < kn) {
+        const uint16_t* kr = Ks + lane * HD;
+        const float* qh = qs + wave * HD;
+        float acc = 0.f;
 #pragma unroll
-    for (int h = 0; h < NREP; ++h) sc[h] = 0.f;
-    const uint8_t* krow = kslice + lane * HD * 2;
-#pragma unroll
-    for (int pc = 0; pc < CPR; ++pc) {
-      float kf[8];
-      unpack8<DT>(*reinterpret_cast<const uint4*>(krow + ((pc ^ (lane % CPR)) * 16)), kf);
-#pragma unroll
-      for (int h = 0; h < NREP; ++h) {
-        const float4 qa = *reinterpret_cast<const float4*>(qs + h * HD + pc * 8);
-        const float4 qb = *reinterpret_cast<const float4*>(qs + h * HD + pc * 8 + 4);
-        float a = sc[h];
-        a = fmaf(qa.x, kf[0], a); a = fmaf(qa.y, kf[1], a);
-        a = fmaf(qa.z, kf[2], a); a = fmaf(qa.w, kf[3], a);
-        a = fmaf(qb.x, kf[4], a); a = fmaf(qb.y, kf[5], a);
-        a = fmaf(qb.z, kf[6], a); a = fmaf(qb.w, kf[7], a);
-        sc[h] = a;
+        for (int c = 0; c < CPR; ++c) {
+          float kf[8];
+          unpack8<DT>(*reinterpret_cast<const uint4*>(kr + ((c ^ (lane % CPR)) * 8)), kf);
+          const float4 qa = *reinterpret_cast<const float4*>(qh + c * 8);
+          const float4 qb = *reinterpret_cast<const float4*>(qh + c * 8 + 4);
+          acc = fmaf(qa.x, kf[0], acc); acc = fmaf(qa.y, kf[1], acc);
+          acc = fmaf(qa.z, kf[2], acc); acc = fmaf(qa.w, kf[3], acc);
+          acc = fmaf(qb.x, kf[4], acc); acc = fmaf(qb.y, kf[5], acc);
+          acc = fmaf(qb.z, kf[6], acc); acc = fmaf(qb.w, kf[7], acc);
+        }
+        sc = acc;
       }
-    }
-    float* pw = ps + wave * NREP * kChunk;
+      const float mn = fmaxf(m, wave_max(sc));
+      const float alpha = exp2f(m - mn);  // 0 on the first chunk (m = -inf)
+      const float p = lane < kn ? exp2f(sc - mn) : 0.f;
+      l = l * alpha + wave_sum(p);
+      m = mn;
+      float* pw = ps + wave * kChunk;
+      pw[lane] = p;
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's p row is in LDS
+      __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int h = 0; h < NREP; ++h) {
-      const float sv = lane < kn ? sc[h] : -INFINITY;
-      const float mn = fmaxf(m[h], wave_max(sv));
-      const float alpha = exp2f(m[h] - mn);  // 0 on the first chunk (m = -inf)
-      const float p = lane < kn ? exp2f(sv - mn) : 0.f;
-      l[h] = l[h] * alpha + wave_sum(p);
-      m[h] = mn;
-#pragma unroll
-      for (int d = 0; d < DPL; ++d) o[h][d] *= alpha;
-      pw[h * kChunk + lane] = p;
-    }
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's p rows are in LDS
-    __builtin_amdgcn_wave_barrier();
-    // ---- P·V: lanes over head dims, V rows from registers ----------------
-#pragma unroll
-    for (int r0 = 0; r0 < kChunk; r0 += 4) {
-#pragma unroll
-      for (int h = 0; h < NREP; ++h) {
-        const float4 p4 = *reinterpret_cast<const float4*>(pw + h * kChunk + r0);
+      for (int d = 0; d < DPL; ++d) o[d] *= alpha;
+      const int kn4 = kn & ~3;
+      for (int j = 0; j < kn4; j += 4) {
+        const float4 p4 = *reinterpret_cast<const float4*>(pw + j);
         const float pj[4] = {p4.x, p4.y, p4.z, p4.w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
+          const uint16_t* vr = Vs + (j + e) * HD + lane * DPL;
           if constexpr (DPL == 2) {
-            const uint32_t w2 = vr[r0 + e][0];
-            o[h][0] = fmaf(pj[e], to_f32<DT>((uint16_t)(w2 & 0xffffu)), o[h][0]);
-            o[h][1] = fmaf(pj[e], to_f32<DT>((uint16_t)(w2 >> 16)), o[h][1]);
+            const uint32_t w2 = *reinterpret_cast<const uint32_t*>(vr);
+            o[0] = fmaf(pj[e], to_f32<DT>((uint16_t)(w2 & 0xffffu)), o[0]);
+            o[1] = fmaf(pj[e], to_f32<DT>((uint16_t)(w2 >> 16)), o[1]);
           } else {
-            o[h][0] = fmaf(pj[e], to_f32<DT>((uint16_t)vr[r0 + e][0]), o[h][0]);
+#pragma unroll
+            for (int d = 0; d < DPL; ++d) o[d] = fmaf(pj[e], to_f32<DT>(vr[d]), o[d]);
           }
         }
       }
+      for (int j = kn4; j < kn; ++j) {
+        const uint16_t* vr = Vs + j * HD + lane * DPL;
+#pragma unroll
+        for (int d = 0; d < DPL; ++d) o[d] = fmaf(pw[j], to_f32<DT>(vr[d]), o[d]);
+      }
     }
-    __builtin_amdgcn_wave_barrier();  // p rows read before the next chunk rewrites them
+    // every wave is done with this buffer before the next iteration restages it
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
 
-  // ---- merge the waves of this split in LDS -------------------------------
-#pragma unroll
-  for (int h = 0; h < NREP; ++h) {
-    float* mw = ms + (wave * NREP + h) * (HD + 2);
-    if (lane == 0) { mw[0] = m[h]; mw[1] = l[h]; }
-#pragma unroll
-    for (int d = 0; d < DPL; ++d) mw[2 + lane * DPL + d] = o[h][d];
-  }
-  __syncthreads();
-  float hm[HPW], hl[HPW], ho[HPW][DPL];
-#pragma unroll
-  for (int i = 0; i < HPW; ++i) {
-    const int h = wave + i * NW;
-    hm[i] = -INFINITY; hl[i] = 0.f;
-#pragma unroll
-    for (int d = 0; d < DPL; ++d) ho[i][d] = 0.f;
-    if (h >= NREP) continue;
-    float M = -INFINITY;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) M = fmaxf(M, ms[(w * NREP + h) * (HD + 2)]);
-    float L = 0.f;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) {
-      const float* mw = ms + (w * NREP + h) * (HD + 2);
-      const float sc = mw[0] == -INFINITY ? 0.f : exp2f(mw[0] - M);
-      L = fmaf(sc, mw[1], L);
-#pragma unroll
-      for (int d = 0; d < DPL; ++d) ho[i][d] = fmaf(sc, mw[2 + lane * DPL + d], ho[i][d]);
-    }
-    hm[i] = M; hl[i] = L;
-  }
+  const int h = g * NREP + wave;
   if (ns == 1) {  // the whole context in this split: finish here
+    if (wave < NREP) {
+      const float inv = 1.f / l;
 #pragma unroll
-    for (int i = 0; i < HPW; ++i) {
-      const int h = wave + i * NW;
-      if (h >= NREP) continue;
-      const float inv = 1.f / hl[i];
-#pragma unroll
-      for (int d = 0; d < DPL; ++d)
-        out[((size_t)g * NREP + h) * HD + lane * DPL + d] = from_f32<DT>(ho[i][d] * inv);
+      for (int d = 0; d < DPL; ++d) out[(size_t)h * HD + lane * DPL + d] = from_f32<DT>(o[d] * inv);
     }
     return;
   }
 
-  // ---- publish the split's partial: write-through stores -> drain -> ticket
+  // publish the partial: write-through stores -> drain -> barrier -> ticket
+  if (wave < NREP) {
+    float* dst = part + ((size_t)h * kMaxSplit + s) * (HD + 2);
+    if (lane == 0) { st_sc1(dst, m); st_sc1(dst + 1, l); }
 #pragma unroll
-  for (int i = 0; i < HPW; ++i) {
-    const int h = wave + i * NW;
-    if (h >= NREP) continue;
-    float* dst = part + (((size_t)g * NREP + h) * kMaxSplit + s) * (HD + 2);
-    if (lane == 0) { st_sc1(dst, hm[i]); st_sc1(dst + 1, hl[i]); }
-#pragma unroll
-    for (int d = 0; d < DPL; ++d) st_sc1(dst + 2 + lane * DPL + d, ho[i][d]);
+    for (int d = 0; d < DPL; ++d) st_sc1(dst + 2 + lane * DPL + d, o[d]);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -258,41 +214,32 @@ __global__ __launch_bounds__(64 * kAttnWaves) void attn_decode_kernel(
     last_flag = last;
   }
   __syncthreads();
-  if (!last_flag) return;
+  if (!last_flag || wave >= NREP) return;
 
-  // ---- merge the ns <= 64 split partials: lane t owns split t's (m, l) ----
+  // merge the ns <= 64 partials of this wave's head: lane t owns split t's (m, l)
+  const float* src = part + (size_t)h * kMaxSplit * (HD + 2);
+  const float mt = lane < ns ? ld_sc1(src + lane * (HD + 2)) : -INFINITY;
+  const float lt = lane < ns ? ld_sc1(src + lane * (HD + 2) + 1) : 0.f;
+  const float M = wave_max(mt);
+  const float wt = lane < ns ? exp2f(mt - M) : 0.f;
+  const float L = wave_sum(wt * lt);
+  float* pw = ps + wave * kChunk;
+  pw[lane] = wt;
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+  float acc[DPL];
 #pragma unroll
-  for (int i = 0; i < HPW; ++i) {
-    const int h = wave + i * NW;
-    if (h >= NREP) continue;
-    const float* src = part + ((size_t)g * NREP + h) * kMaxSplit * (HD + 2);
-    const float mt = lane < ns ? ld_sc1(src + lane * (HD + 2)) : -INFINITY;
-    const float lt = lane < ns ? ld_sc1(src + lane * (HD + 2) + 1) : 0.f;
-    const float M = wave_max(mt);
-    const float wt = lane < ns ? exp2f(mt - M) : 0.f;
-    const float L = wave_sum(wt * lt);
-    float acc[DPL];
+  for (int d = 0; d < DPL; ++d) acc[d] = 0.f;
+#pragma unroll 8
+  for (int t = 0; t < ns; ++t) {
+    const float w = pw[t];
+    const float* pt = src + t * (HD + 2) + 2 + lane * DPL;
 #pragma unroll
-    for (int d = 0; d < DPL; ++d) acc[d] = 0.f;
-    for (int t0 = 0; t0 < ns; t0 += 8) {
-      float vals[8][DPL];
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-#pragma unroll
-        for (int d = 0; d < DPL; ++d)
-          vals[u][d] = t0 + u < ns ? ld_sc1(src + (t0 + u) * (HD + 2) + 2 + lane * DPL + d) : 0.f;
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const float w = __shfl(wt, (t0 + u) & 63, 64);
-#pragma unroll
-        for (int d = 0; d < DPL; ++d) acc[d] = fmaf(w, vals[u][d], acc[d]);
-      }
-    }
-    const float inv = 1.f / L;
-#pragma unroll
-    for (int d = 0; d < DPL; ++d)
-      out[((size_t)g * NREP + h) * HD + lane * DPL + d] = from_f32<DT>(acc[d] * inv);
+    for (int d = 0; d < DPL; ++d) acc[d] = fmaf(w, ld_sc1(pt + d), acc[d]);
   }
+  const float inv = 1.f / L;
+#pragma unroll
+  for (int d = 0; d < DPL; ++d) out[(size_t)h * HD + lane * DPL + d] = from_f32<DT>(acc[d] * inv);
 }
 
 }  // namespace cake
@@ -317,7 +264,7 @@ static inline int attn_max_split(int S) {
 
 CAKE_API int cake_attn_set_min_keys(int min_keys) {
   if (min_keys < kChunk || min_keys % kChunk) return (int)hipErrorInvalidValue;
-  g_attn_min_chunks = min_keys / kChunk;
+  g_attn_min_keys = min_keys;
   return 0;
 }
 
@@ -326,9 +273,9 @@ static int launch_decode(int n_rep, dim3 grid, hipStream_t st, const float* q, c
                          const void* vc, const int* pos, int S, float sl2, float* part,
                          unsigned int* tickets, void* out) {
 #define CAKE_DEC(NR)                                                                          \
-  hipLaunchKernelGGL((attn_decode_kernel<DT, HD, NR>), grid, dim3(64 * kAttnWaves), 0, st, q,  \
+  hipLaunchKernelGGL((attn_decode_kernel<DT, HD, NR>), grid, dim3(AttnGeom<NR>::NT), 0, st, q, \
                      (const uint16_t*)kc, (const uint16_t*)vc, pos, S, sl2, part, tickets,    \
-                     (uint16_t*)out, g_attn_min_chunks)
+                     (uint16_t*)out, g_attn_min_keys)
   switch (n_rep) {
     case 1: CAKE_DEC(1); break;
     case 2: CAKE_DEC(2); break;

@@ -131,6 +131,15 @@ def attention(q, k, v, heads: int, causal: bool = False, sliced: int | None = No
         K.flash_attn(heads4(q, N), heads4(k, M), heads4(v, M),
                      out.view(B, N, heads, D).transpose(1, 2), scale, causal)
         return out
+    if _hip(q) and D == 512 and heads == 1:  # VAE mid-block: flash kernel for head dim 512
+        from ...ops import hip as K
+
+        def rows(t):
+            return t if (t.stride(-1) == 1 and t.data_ptr() % 16 == 0 and t.stride(1) % 8 == 0) \
+                else t.contiguous()
+        out = torch.empty(B, N, C, device=q.device, dtype=q.dtype)
+        K.attn512(rows(q), rows(k), rows(v), out, scale)
+        return out
     qh = q.view(B, N, heads, D).transpose(1, 2).float()
     kh = k.view(B, M, heads, D).transpose(1, 2).float()
     vh = v.view(B, M, heads, D).transpose(1, 2).float()

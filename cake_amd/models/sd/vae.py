@@ -4,8 +4,10 @@ cake-core/src/models/sd/vae.rs).
 encode: encoder → quant_conv → (mean, logvar) → mean + exp(logvar/2)·ε
 decode: post_quant_conv → decoder (mid-block single-head attention, resnets,
 nearest-2x upsampling) → RGB in [-1, 1].
-The mid-block attention has one head of dim C (512): it runs on the MFMA
-flash kernel when C <= 256 and through the PyTorch path otherwise.
+The mid-block attention has one head of dim C (512): q|k|v is one fused GEMM,
+the attention is the head-dim-512 MFMA flash kernel (attn512.hip; the
+generic flash kernel for C <= 256), and the output projection adds the block
+residual in its GEMM epilogue.
 Accepts both current (to_q/to_k/to_v/to_out.0) and legacy
 (query/key/value/proj_attn) attention weight names.
 """
@@ -51,7 +53,16 @@ class VAEAttention(Module):
         h = ops.group_norm(x, W[f"{self.name}.group_norm.weight"], W[f"{self.name}.group_norm.bias"],
                            self.groups, 1e-6)
         h = ops.tokens(h)
-        a = ops.attention(self.q(W, h), self.k(W, h), self.v(W, h), 1)
+        C = self.q.cout
+        key = f"{self.name}.qkv@fused"
+        if key not in W:
+            W[key] = torch.cat([W[f"{self.name}.{n}.weight"] for n in ("to_q", "to_k", "to_v")], 0)
+            W[key + ".bias"] = torch.cat([W[f"{self.name}.{n}.bias"]
+                                          for n in ("to_q", "to_k", "to_v")], 0)
+        qkv = ops.linear(h, W[key], W[key + ".bias"])  # one GEMM for q|k|v
+        a = ops.attention(qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:], 1)
+        if ops.nhwc():  # residual fused into the output projection's epilogue
+            return ops.untokens(self.o(W, a, resid=ops.tokens(x)), x)
         return ops.untokens(self.o(W, a), x) + x
 
 

@@ -43,6 +43,9 @@ _SIGS = {
     "cake_push_token": [P, P, P, P, P, I, P],
     "cake_gemv_set_tuning": [I, I, I, I],
     "cake_sample_threshold": [P, I, F, I, F, P, P],
+    "cake_attn512": [I, P, P, P, P, I, I, I, C.c_longlong, C.c_longlong, C.c_longlong,
+                     C.c_longlong, C.c_longlong, C.c_longlong, C.c_longlong, C.c_longlong, F, P,
+                     P],
     "cake_gumbel_argmax": [P, I, F, C.c_ulonglong, P, P, P, P],
 }
 

@@ -338,6 +338,29 @@ def flash_attn(q, k, v, out, scale: float, causal: bool = False, pos0: int = 0):
                                     int(pos0), _stream()), "flash_attn")
 
 
+_zero16: dict = {}
+
+
+def attn512(q, k, v, out, scale: float):
+    """Single-head attention with head dim 512 (VAE mid-block): q/out [B, N, 512],
+    k/v [B, M, 512] 16-bit views with unit column stride (attn512.hip)."""
+    B, N, D = q.shape
+    Bk, M, Dk = k.shape
+    if D != 512 or Dk != 512 or Bk != B or v.shape != k.shape or tuple(out.shape) != (B, N, D):
+        raise ValueError(f"attn512 shapes q{tuple(q.shape)} k{tuple(k.shape)} v{tuple(v.shape)}")
+    for t, n in ((q, "q"), (k, "k"), (v, "v"), (out, "out")):
+        if not t.is_cuda or t.dtype != q.dtype or t.stride(2) != 1 or t.data_ptr() % 16 or \
+                t.stride(1) % 8:
+            raise ValueError(f"attn512: {n} must be a 16-byte aligned unit-stride {q.dtype} view")
+    z = _zero16.get(q.device)
+    if z is None:
+        z = _zero16[q.device] = torch.zeros(64, dtype=torch.int32, device=q.device)
+    check(kernels().cake_attn512(_dt(q), _p(q), _p(k), _p(v), _p(out), B, N, M, q.stride(1),
+                                 k.stride(1), v.stride(1), out.stride(1), q.stride(0),
+                                 k.stride(0), v.stride(0), out.stride(0), float(scale), _p(z),
+                                 _stream()), "attn512")
+
+
 def group_norm(x, gamma, beta, groups: int, eps: float, silu: bool, out):
     """GroupNorm over NCHW (contiguous) [+ fused SiLU]."""
     B, C = x.shape[:2]

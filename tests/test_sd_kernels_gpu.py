@@ -208,3 +208,24 @@ def test_group_norm_nhwc(cuda, dt, N, H, W, C, G, silu):
     if silu:
         ref = torch.nn.functional.silu(ref)
     torch.testing.assert_close(y.float(), ref.permute(0, 2, 3, 1), **_tol(dt))
+
+
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("B,N,M", [(1, 4096, 4096), (2, 1000, 777), (1, 16384, 16384), (1, 70, 33)])
+def test_attn512_vs_fp32(cuda, dt, B, N, M):
+    """Head-dim-512 flash attention (VAE mid-block) vs the f32 softmax reference."""
+    import math
+    from cake_amd.ops import hip as K
+    torch.manual_seed(N + M)
+    q = (torch.randn(B, N, 512, device=cuda) * 0.5).to(dt)
+    k = (torch.randn(B, M, 512, device=cuda) * 0.5).to(dt)
+    v = torch.randn(B, M, 512, device=cuda).to(dt)
+    out = torch.empty(B, N, 512, device=cuda, dtype=dt)
+    scale = 1 / math.sqrt(512)
+    K.attn512(q, k, v, out, scale)
+    ref = torch.empty(B, N, 512, device=cuda)
+    for b in range(B):
+        for s0 in range(0, N, 4096):  # bounded f32 score slabs
+            sc = (q[b, s0:s0 + 4096].float() @ k[b].float().t()) * scale
+            ref[b, s0:s0 + 4096] = torch.softmax(sc, -1) @ v[b].float()
+    torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
