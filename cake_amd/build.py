@@ -10,6 +10,9 @@ travel with the repository snapshot to the GPU box:
 * ``libcake_runtime.so`` — ``csrc/runtime/*.cpp`` (topology parser, wire codec,
   safetensors mmap reader/writer, framed TCP transport), C ABI.
 * ``cake-split-model`` — native executable (``csrc/tools/split_model.cpp``).
+* ``cake-cli`` — the native entry point (``csrc/tools/cake_cli.cpp``): flags,
+  validation and topology natively, compute runtime embedded in-process
+  (libpython); ``libcake_runtime.so``'s ``cake_start_worker`` embeds the same way.
 
 Object files are cached under ``build/`` keyed on mtimes of the source and the
 shared headers, so re-running is cheap.
@@ -38,6 +41,7 @@ CXX = shutil.which("g++") or "c++"
 KERNEL_LIB = LIB / "libcake_kernels.so"
 RUNTIME_LIB = LIB / "libcake_runtime.so"
 SPLIT_TOOL = LIB / "cake-split-model"
+CLI_TOOL = LIB / "cake-cli"
 
 
 def _newer(src: Path, deps: list[Path], out: Path) -> bool:
@@ -94,28 +98,43 @@ def build_kernels(force: bool = False, jobs: int = 8) -> Path:
     return KERNEL_LIB
 
 
+def _embed_flags() -> tuple[list[str], list[str]]:
+    """Compile / link flags to embed libpython (python3-config --embed equivalent)."""
+    import sysconfig
+    inc = [f"-I{sysconfig.get_paths()['include']}"]
+    ver = sysconfig.get_config_var("LDVERSION") or sysconfig.get_python_version()
+    libdir = sysconfig.get_config_var("LIBDIR") or "/usr/lib"
+    return inc, [f"-L{libdir}", f"-lpython{ver}", "-ldl", "-lm", "-lpthread"]
+
+
 def build_runtime(force: bool = False, jobs: int = 8) -> Path:
-    """C++ host runtime: pybind11 module, C-ABI library and the split-model tool."""
+    """C++ host runtime: pybind11 module, C-ABI library, split-model tool and cake-cli."""
     rt = CSRC / "runtime"
     core_srcs = [rt / f"{n}.cpp" for n in ("json", "topology", "proto", "net", "safetensors",
                                             "server")]
     inc, ext = _py_ext_flags()
+    einc, elink = _embed_flags()
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         core = list(ex.map(lambda s: _compile_cpp(s, force), core_srcs))
         capi_f = ex.submit(_compile_cpp, rt / "capi.cpp", force)
         bind_f = ex.submit(_compile_cpp, rt / "bindings.cpp", force, inc)
-        capi, bind = capi_f.result(), bind_f.result()
+        emb_f = ex.submit(_compile_cpp, rt / "embed.cpp", force, einc)
+        capi, bind, emb = capi_f.result(), bind_f.result(), emb_f.result()
     LIB.mkdir(parents=True, exist_ok=True)
     pyext = PY_EXT.with_name(PY_EXT.name + ext)
     if force or any(_newer(o, [], pyext) for o in [*core, bind]):
         _run([CXX, "-shared", "-fPIC", *map(str, core), str(bind), "-o", str(pyext), "-lpthread"])
-    if force or any(_newer(o, [], RUNTIME_LIB) for o in [*core, capi]):
-        _run([CXX, "-shared", "-fPIC", *map(str, core), str(capi), "-o", str(RUNTIME_LIB),
-              "-lpthread"])
+    if force or any(_newer(o, [], RUNTIME_LIB) for o in [*core, capi, emb]):
+        _run([CXX, "-shared", "-fPIC", *map(str, core), str(capi), str(emb), "-o",
+              str(RUNTIME_LIB), *elink])
     tool = CSRC / "tools" / "split_model.cpp"
     if force or _newer(tool, [*core, *sorted(rt.glob("*.h"))], SPLIT_TOOL):
         _run([CXX, "-O2", "-std=c++17", f"-I{rt}", str(tool), *map(str, core), "-o",
               str(SPLIT_TOOL), "-lpthread"])
+    cli = CSRC / "tools" / "cake_cli.cpp"
+    if force or _newer(cli, [*core, emb, *sorted(rt.glob("*.h"))], CLI_TOOL):
+        _run([CXX, "-O2", "-std=c++17", f"-I{rt}", str(cli), *map(str, core), str(emb), "-o",
+              str(CLI_TOOL), *elink])
     return pyext
 
 

@@ -5,9 +5,14 @@ the image-generation flags double as the JSON keys of the image API.
 MI355X additions: ``--max-seq-len``, ``--no-graph``, ``--trace FILE``,
 ``--log-level``.
 
-    python -m cake_amd.cli --model DIR --topology topology.yml --prompt "..."
-    python -m cake_amd.cli --mode worker --name w1 --model DIR --topology t.yml --address 0.0.0.0:10128
-    python -m cake_amd.cli --model DIR --api 0.0.0.0:8080
+    cake_amd/lib/cake-cli --model DIR --topology topology.yml --prompt "..."
+    cake_amd/lib/cake-cli --mode worker --name w1 --model DIR --topology t.yml --address 0.0.0.0:10128
+    cake_amd/lib/cake-cli --model DIR --api 0.0.0.0:8080
+
+``cake-cli`` is the native executable (csrc/tools/cake_cli.cpp): it parses and
+validates these flags and resolves the topology natively, then runs the role
+with the compute runtime embedded in-process (:func:`run_parsed`).  ``python -m
+cake_amd.cli`` takes the same flags (development entry).
 """
 from __future__ import annotations
 
@@ -89,8 +94,24 @@ def setup_logging(level: str) -> None:
     logging.getLogger("uvicorn.access").setLevel(logging.WARNING)
 
 
+def run_parsed(opts: dict) -> int:
+    """Entry point of the native cake-cli / cake_start_worker (csrc/tools/cake_cli.cpp,
+    csrc/runtime/capi.cpp): the flags were parsed and validated natively; ``opts``
+    maps argparse dests to typed values.  Unknown keys are rejected."""
+    ap = build_parser()
+    args = ap.parse_args([])
+    for k, v in opts.items():
+        if not hasattr(args, k):
+            raise ValueError(f"unknown option {k!r}")
+        setattr(args, k, v)
+    return _run(args)
+
+
 def main(argv: list[str] | None = None) -> int:
-    args = build_parser().parse_args(argv)
+    return _run(build_parser().parse_args(argv))
+
+
+def _run(args) -> int:
     setup_logging(args.log_level)
     from .context import Context
     ctx = Context.from_args(args)

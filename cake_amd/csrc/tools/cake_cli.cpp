@@ -1,0 +1,210 @@
+// cake-cli: the native entry point (master or worker), cake-cli/src/main.rs:8-63.
+//
+// Flags, defaults and choices follow cake-core/src/lib.rs:21-200 (SURVEY
+// Appendix B) plus the MI355X extras; they are parsed and validated here
+// (unknown flags, bad numbers, bad choices and a missing worker topology are
+// rejected before any runtime starts; --help prints the table).  The topology
+// is resolved with the native parser: a worker whose --name is not in the file
+// serves the FIRST node (worker.rs:90-104), with a warning.  Then the process
+// runs its role: the tensor compute (PyTorch-ROCm + the gfx950 HIP kernels) in
+// an interpreter embedded in THIS process (embed.cpp), the worker's TCP
+// control plane on the native WorkerServer.
+#include <unistd.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <iostream>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "embed.h"
+#include "topology.h"
+
+using cake::PyArg;
+
+namespace {
+
+struct Flag {
+  const char* name;     // --name
+  const char* dest;     // argparse dest
+  PyArg::Kind kind;
+  const char* def;      // nullptr -> None
+  const char* choices;  // "a|b|c" or nullptr
+  bool is_switch;       // store_true
+  const char* help;
+};
+
+const Flag kFlags[] = {
+    {"--device", "device", PyArg::kInt, "0", nullptr, false, "GPU ordinal"},
+    {"--mode", "mode", PyArg::kStr, "master", "master|worker", false, "role"},
+    {"--name", "name", PyArg::kStr, nullptr, nullptr, false, "worker name (must be in the topology)"},
+    {"--address", "address", PyArg::kStr, "127.0.0.1:10128", nullptr, false, "worker bind address"},
+    {"--api", "api", PyArg::kStr, nullptr, nullptr, false,
+     "serve the REST API on this address instead of one CLI generation"},
+    {"--model", "model", PyArg::kStr, "./cake-data/Meta-Llama-3-8B/", nullptr, false, "model dir"},
+    {"--topology", "topology", PyArg::kStr, "./cake-data/topology.yml", nullptr, false, "topology"},
+    {"--prompt", "prompt", PyArg::kStr, "The sky is blue because ", nullptr, false, "prompt"},
+    {"--system-prompt", "system_prompt", PyArg::kStr, "You are a helpful AI assistant.", nullptr,
+     false, "system prompt"},
+    {"--seed", "seed", PyArg::kInt, "299792458", nullptr, false, "sampling seed"},
+    {"--sample-len", "sample_len", PyArg::kInt, "100", nullptr, false, "tokens to generate (-n)"},
+    {"--temperature", "temperature", PyArg::kFloat, "1.0", nullptr, false, "<= 0: greedy"},
+    {"--top-p", "top_p", PyArg::kFloat, nullptr, nullptr, false, "nucleus cutoff"},
+    {"--top-k", "top_k", PyArg::kInt, nullptr, nullptr, false, "top-k cutoff"},
+    {"--repeat-penalty", "repeat_penalty", PyArg::kFloat, "1.1", nullptr, false, "1 = off"},
+    {"--repeat-last-n", "repeat_last_n", PyArg::kInt, "128", nullptr, false, "penalty window"},
+    {"--dtype", "dtype", PyArg::kStr, nullptr, "f16|bf16|f32", false, "f16 (default), bf16, f32"},
+    {"--cpu", "cpu", PyArg::kBool, "0", nullptr, true, "run on the CPU"},
+    {"--model-type", "model_type", PyArg::kStr, "text-model", "text-model|image-model", false,
+     "text or image model"},
+    {"--sd-tokenizer", "sd_tokenizer", PyArg::kStr, nullptr, nullptr, false, ""},
+    {"--sd-tokenizer-2", "sd_tokenizer_2", PyArg::kStr, nullptr, nullptr, false, ""},
+    {"--sd-version", "sd_version", PyArg::kStr, "v1-5", "v1-5|v2-1|xl|turbo", false, ""},
+    {"--sd-use-f16", "sd_use_f16", PyArg::kBool, "1", "true|false|1|0|yes|no|on|off", false, ""},
+    {"--sd-width", "sd_width", PyArg::kInt, nullptr, nullptr, false, ""},
+    {"--sd-height", "sd_height", PyArg::kInt, nullptr, nullptr, false, ""},
+    {"--sd-sliced-attention-size", "sd_sliced_attention_size", PyArg::kInt, nullptr, nullptr, false,
+     ""},
+    {"--sd-clip", "sd_clip", PyArg::kStr, nullptr, nullptr, false, ""},
+    {"--sd-clip2", "sd_clip2", PyArg::kStr, nullptr, nullptr, false, ""},
+    {"--sd-vae", "sd_vae", PyArg::kStr, nullptr, nullptr, false, ""},
+    {"--sd-unet", "sd_unet", PyArg::kStr, nullptr, nullptr, false, ""},
+    {"--sd-use-flash-attention", "sd_use_flash_attention", PyArg::kBool, "0", nullptr, true, ""},
+    {"--sd-image-prompt", "sd_image_prompt", PyArg::kStr,
+     "A very realistic photo of a rusty robot walking on a sandy beach", nullptr, false, ""},
+    {"--sd-uncond-prompt", "sd_uncond_prompt", PyArg::kStr, "", nullptr, false, ""},
+    {"--sd-tracing", "sd_tracing", PyArg::kBool, "0", nullptr, true, ""},
+    {"--sd-n-steps", "sd_n_steps", PyArg::kInt, nullptr, nullptr, false, ""},
+    {"--sd-num-samples", "sd_num_samples", PyArg::kInt, "1", nullptr, false, ""},
+    {"--sd-bsize", "sd_bsize", PyArg::kInt, "1", nullptr, false, ""},
+    {"--sd-intermediary-images", "sd_intermediary_images", PyArg::kInt, "0", nullptr, false, ""},
+    {"--sd-guidance-scale", "sd_guidance_scale", PyArg::kFloat, nullptr, nullptr, false, ""},
+    {"--sd-img2img", "sd_img2img", PyArg::kStr, nullptr, nullptr, false, ""},
+    {"--sd-img2img-strength", "sd_img2img_strength", PyArg::kFloat, "0.8", nullptr, false, ""},
+    {"--sd-seed", "sd_seed", PyArg::kInt, nullptr, nullptr, false, ""},
+    {"--transport", "transport", PyArg::kStr, "tcp", "tcp|rccl|loopback", false,
+     "tcp, rccl (one rank per GPU) or loopback"},
+    {"--max-seq-len", "max_seq_len", PyArg::kInt, "4096", nullptr, false, "KV cache length"},
+    {"--no-graph", "no_graph", PyArg::kBool, "0", nullptr, true, "disable hipGraph decode"},
+    {"--trace", "trace", PyArg::kStr, nullptr, nullptr, false, "chrome-trace JSON per generation"},
+    {"--metrics", "metrics", PyArg::kStr, nullptr, nullptr, false, "append JSON stats lines"},
+    {"--log-level", "log_level", PyArg::kStr, "info", "debug|info|warning|error", false, ""},
+};
+
+const Flag* find_flag(const std::string& n) {
+  if (n == "-n") return find_flag("--sample-len");
+  for (const auto& f : kFlags)
+    if (n == f.name) return &f;
+  return nullptr;
+}
+
+void usage() {
+  std::printf("usage: cake-cli [flags]   (MI355X-native distributed inference)\n\n");
+  for (const auto& f : kFlags) {
+    std::printf("  %-28s %s", f.name, f.help);
+    if (f.def && !f.is_switch) std::printf(" [default: %s]", f.def);
+    if (f.choices) std::printf(" {%s}", f.choices);
+    std::printf("\n");
+  }
+}
+
+bool valid_number(const std::string& s, PyArg::Kind k) {
+  if (s.empty()) return false;
+  char* end = nullptr;
+  if (k == PyArg::kInt) std::strtoll(s.c_str(), &end, 10);
+  else std::strtod(s.c_str(), &end);
+  return end && *end == '\0';
+}
+
+bool in_choices(const std::string& v, const char* choices) {
+  std::string c = choices;
+  size_t a = 0;
+  while (a <= c.size()) {
+    const size_t b = c.find('|', a);
+    if (c.substr(a, b == std::string::npos ? std::string::npos : b - a) == v) return true;
+    if (b == std::string::npos) break;
+    a = b + 1;
+  }
+  return false;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  cake::PyArgs opts;
+  for (const auto& f : kFlags) {
+    PyArg a;
+    if (f.def == nullptr) a.kind = PyArg::kNone;
+    else { a.kind = f.kind; a.value = f.def; }
+    opts[f.dest] = a;
+  }
+  if (const char* lv = std::getenv("CAKE_LOG")) opts["log_level"] = PyArg{PyArg::kStr, lv};
+  for (int i = 1; i < argc; ++i) {
+    std::string arg = argv[i];
+    if (arg == "-h" || arg == "--help") { usage(); return 0; }
+    std::string val;
+    bool has_val = false;
+    const auto eq = arg.find('=');
+    if (arg.rfind("--", 0) == 0 && eq != std::string::npos) {
+      val = arg.substr(eq + 1);
+      arg = arg.substr(0, eq);
+      has_val = true;
+    }
+    const Flag* f = find_flag(arg);
+    if (!f) { std::fprintf(stderr, "cake-cli: unknown flag %s (see --help)\n", arg.c_str()); return 2; }
+    if (f->is_switch) {
+      if (has_val) { std::fprintf(stderr, "cake-cli: %s takes no value\n", f->name); return 2; }
+      opts[f->dest] = PyArg{PyArg::kBool, "1"};
+      continue;
+    }
+    if (!has_val) {
+      if (i + 1 >= argc) { std::fprintf(stderr, "cake-cli: %s needs a value\n", f->name); return 2; }
+      val = argv[++i];
+    }
+    if ((f->kind == PyArg::kInt || f->kind == PyArg::kFloat) && !valid_number(val, f->kind)) {
+      std::fprintf(stderr, "cake-cli: %s: invalid number '%s'\n", f->name, val.c_str());
+      return 2;
+    }
+    if (f->choices && !in_choices(val, f->choices)) {
+      std::fprintf(stderr, "cake-cli: %s: '%s' not in {%s}\n", f->name, val.c_str(), f->choices);
+      return 2;
+    }
+    if (f->kind == PyArg::kBool) {  // --sd-use-f16 true|false
+      opts[f->dest] = PyArg{PyArg::kBool, (val == "true" || val == "1" || val == "yes" ||
+                                           val == "on") ? "1" : "0"};
+      continue;
+    }
+    opts[f->dest] = PyArg{f->kind, val};
+  }
+  // ---- topology (native parser): validate placement before any runtime starts
+  const bool text = opts["model_type"].value == "text-model";
+  const std::string topo_path = opts["topology"].value;
+  const bool worker = opts["mode"].value == "worker";
+  if (access(topo_path.c_str(), R_OK) == 0) {
+    try {
+      const cake::Topology topo = cake::Topology::from_path(topo_path, text);
+      size_t layers = 0;
+      for (const auto& n : topo.nodes) layers += n.layers.size();
+      std::fprintf(stderr, "[cake-cli] topology %s: %zu node(s), %zu placed unit(s)\n",
+                   topo_path.c_str(), topo.nodes.size(), layers);
+      if (worker) {
+        if (topo.nodes.empty()) { std::fprintf(stderr, "cake-cli: topology has no workers\n"); return 2; }
+        const PyArg& nm = opts["name"];
+        if (nm.kind == PyArg::kNone || !topo.find(nm.value))
+          std::fprintf(stderr, "[cake-cli] worker name %s not in the topology: serving the FIRST "
+                       "node '%s'\n", nm.kind == PyArg::kNone ? "(none)" : nm.value.c_str(),
+                       topo.nodes[0].name.c_str());
+      }
+    } catch (const std::exception& e) {
+      std::fprintf(stderr, "cake-cli: bad topology %s: %s\n", topo_path.c_str(), e.what());
+      return 2;
+    }
+  } else if (worker) {
+    std::fprintf(stderr, "cake-cli: worker mode needs a topology (%s not found)\n",
+                 topo_path.c_str());
+    return 2;
+  }
+  return cake::run_embedded(opts);
+}
