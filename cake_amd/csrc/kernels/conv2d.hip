@@ -43,6 +43,7 @@ struct ConvArgs {
   const uint16_t* zeros;  // >= 16 zero bytes (LDS-DMA source for padding)
   int N, H, W, IC, OC, OH, OW, KH, KW, stride, pad, up;
   int P, ksteps, ks_per_split, tiles_m, tiles_n;
+  int bias2_ld;           // row stride of bias2 (elements; OC when packed)
 };
 
 
@@ -59,7 +60,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, int oc, int p, 
   }
   if (a.bias2) {
     const int n = p / (a.OH * a.OW);
-    const float4 b = *reinterpret_cast<const float4*>(a.bias2 + (size_t)n * a.OC + oc);
+    const float4 b = *reinterpret_cast<const float4*>(a.bias2 + (size_t)n * a.bias2_ld + oc);
     r[0] += b.x; r[1] += b.y; r[2] += b.z; r[3] += b.w;
   }
   const size_t o = (size_t)p * a.OC + oc;
@@ -509,8 +510,9 @@ CAKE_API int cake_conv2d_nhwc(int dt, const void* x, const void* w, const void* 
                               const void* zeros,
                               int N, int H, int W, int IC, int OC, int KH, int KW, int stride,
                               int pad, int up, int cfg, int splits, int th, int tw,
-                              hipStream_t st) {
+                              int bias2_ld, hipStream_t st) {
   if (IC % 64 || OC % 4 || N <= 0 || stride <= 0 || KH <= 0 || KW <= 0 || splits <= 0 ||
+      (bias2 && bias2_ld > 0 && (bias2_ld % 4 || bias2_ld < OC)) ||
       (up && stride != 1) || cfg < 0 || cfg > 13 || (splits > 1 && !ws) || (cfg > 3 && !zeros))
     return (int)hipErrorInvalidValue;
   const int VH = H << up, VW = W << up;
@@ -527,6 +529,7 @@ CAKE_API int cake_conv2d_nhwc(int dt, const void* x, const void* w, const void* 
                (const uint16_t*)resid, (uint16_t*)out, nullptr, (const uint16_t*)zeros, N, H, W,
                IC, OC, OH, OW, KH, KW, 1, pad, up, N * OH * OW, KH * KW * (IC / 64), 0,
                (OC + bm - 1) / bm, N * ty * tx};
+    a.bias2_ld = bias2_ld > 0 ? bias2_ld : OC;
     const dim3 grid(a.tiles_m * a.tiles_n);
 #define CAKE_HALO(DTV)                                                                                     \
     switch (cfg) {                                                                                         \
@@ -548,6 +551,7 @@ CAKE_API int cake_conv2d_nhwc(int dt, const void* x, const void* w, const void* 
   ConvArgs a{(const uint16_t*)x, (const uint16_t*)w, (const uint16_t*)bias, bias2,
              (const uint16_t*)resid, (uint16_t*)out, ws, (const uint16_t*)zeros, N, H, W, IC, OC, OH, OW, KH, KW,
              stride, pad, up, N * OH * OW, KH * KW * (IC / 64), 0, 0, 0};
+  a.bias2_ld = bias2_ld > 0 ? bias2_ld : OC;
   a.tiles_m = (OC + BMs[cfg] - 1) / BMs[cfg];
   a.tiles_n = (a.P + BNs[cfg] - 1) / BNs[cfg];
   splits = splits > a.ksteps ? a.ksteps : splits;

@@ -48,6 +48,8 @@ enum GemmEpi : int {
   kEpiSwiglu = 3,  // C16[:, f] = silu(acc_gate) * acc_up
   kEpiGeglu = 4,   // C16[:, f] = acc_h * gelu_tanh(acc_gate)
   kEpiPartial = 5, // W32[split] = acc (split-K slab, virtual column order)
+  kEpiStore32 = 6, // R32 = acc (+ bias)              (f32 output, e.g. conv time biases)
+  kEpiSilu = 7,    // C16 = silu(acc (+ bias))        (time-embedding MLP)
 };
 
 struct GemmArgs {
@@ -300,17 +302,19 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(GemmArgs g) {
           for (int c = 0; c < CPL; ++c)
             if (full || n0c + c < g.N) v[c] += to_f32<DT>(g.bias[n0c + c]);
         }
-        if constexpr (EPI == kEpiResid32) {
+        if constexpr (EPI == kEpiResid32 || EPI == kEpiStore32) {
+          constexpr bool ADD = EPI == kEpiResid32;
           float* r = g.r32 + (size_t)m * g.ldr + n0c;
           if (full && ((g.ldr | n0c) & 3) == 0) {
 #pragma unroll
             for (int c = 0; c < CPL; c += 4) {
-              float4 o = *reinterpret_cast<float4*>(r + c);
+              float4 o = ADD ? *reinterpret_cast<float4*>(r + c) : make_float4(0.f, 0.f, 0.f, 0.f);
               o.x += v[c]; o.y += v[c + 1]; o.z += v[c + 2]; o.w += v[c + 3];
               *reinterpret_cast<float4*>(r + c) = o;
             }
           } else {
-            for (int c = 0; c < CPL; ++c) if (n0c + c < g.N) r[c] += v[c];
+            for (int c = 0; c < CPL; ++c)
+              if (n0c + c < g.N) r[c] = ADD ? r[c] + v[c] : v[c];
           }
         } else {
           if constexpr (EPI == kEpiAdd16) {
@@ -318,6 +322,10 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(GemmArgs g) {
 #pragma unroll
             for (int c = 0; c < CPL; ++c)
               if (full || n0c + c < g.N) v[c] += to_f32<DT>(r[c]);
+          }
+          if constexpr (EPI == kEpiSilu) {
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) v[c] = silu(v[c]);
           }
           uint16_t outv[CPL];
 #pragma unroll
@@ -378,8 +386,10 @@ __global__ __launch_bounds__(256) void gemm_splitk_finalize(GemmArgs g, int spli
     else {
       y = v[q] + (g.bias != nullptr ? to_f32<DT>(g.bias[fq]) : 0.f);
       if constexpr (EPI == kEpiAdd16) y += to_f32<DT>(g.r16[(size_t)m * g.ldr + fq]);
+      if constexpr (EPI == kEpiSilu) y = silu(y);
     }
     if constexpr (EPI == kEpiResid32) g.r32[(size_t)m * g.ldr + fq] += y;
+    else if constexpr (EPI == kEpiStore32) g.r32[(size_t)m * g.ldr + fq] = y;
     else g.c[(size_t)m * g.ldc + fq] = from_f32<DT>(y);
   }
 }
@@ -433,6 +443,8 @@ static int dispatch_epi(int epi, int cfg, dim3 grid, hipStream_t st, const GemmA
     case kEpiSwiglu: return launch_gemm<DT, kEpiSwiglu>(cfg, grid, st, g);
     case kEpiGeglu: return launch_gemm<DT, kEpiGeglu>(cfg, grid, st, g);
     case kEpiPartial: return launch_gemm<DT, kEpiPartial>(cfg, grid, st, g);
+    case kEpiStore32: return launch_gemm<DT, kEpiStore32>(cfg, grid, st, g);
+    case kEpiSilu: return launch_gemm<DT, kEpiSilu>(cfg, grid, st, g);
   }
   return (int)hipErrorInvalidValue;
 }
@@ -441,7 +453,8 @@ template <int DT>
 static int dispatch_finalize(int epi, dim3 grid, hipStream_t st, const GemmArgs& g, int splits) {
   switch (epi) {
 #define F(E) case E: hipLaunchKernelGGL((gemm_splitk_finalize<DT, E>), grid, dim3(256), 0, st, g, splits); break;
-    F(kEpiStore) F(kEpiResid32) F(kEpiAdd16) F(kEpiSwiglu) F(kEpiGeglu)
+    F(kEpiStore) F(kEpiResid32) F(kEpiAdd16) F(kEpiSwiglu) F(kEpiGeglu) F(kEpiStore32)
+    F(kEpiSilu)
 #undef F
     default: return (int)hipErrorInvalidValue;
   }
@@ -465,7 +478,7 @@ CAKE_API int cake_gemm(int dt, int epi, int cfg, int splits, const void* a, long
   GemmArgs g{};
   g.a = (const uint16_t*)a; g.b = (const uint16_t*)b; g.c = (uint16_t*)c;
   g.bias = (const uint16_t*)bias;
-  g.r32 = (epi == kEpiResid32) ? (float*)resid : nullptr;
+  g.r32 = (epi == kEpiResid32 || epi == kEpiStore32) ? (float*)resid : nullptr;
   g.r16 = (epi == kEpiAdd16) ? (const uint16_t*)resid : nullptr;
   g.ws = ws; g.zeros = (const uint16_t*)zeros;
   g.lda = lda; g.ldb = ldb; g.ldc = ldc; g.ldr = ldr;

@@ -214,7 +214,8 @@ def conv(W, name: str, x, stride: int = 1, padding: int = 1, up: bool = False, b
             if wp is None or wp.dtype != x.dtype:
                 wp = W[key] = w.to(x.dtype).permute(0, 2, 3, 1).contiguous()
             return C.conv2d(x.contiguous(), wp, b, stride=stride, pad=padding, up=up,
-                            bias2=None if bias2 is None else bias2.float().contiguous(),
+                            bias2=None if bias2 is None else
+                            (bias2 if bias2.dtype == torch.float32 else bias2.float()),
                             resid=None if resid is None else resid.contiguous())
         xn = x.permute(0, 3, 1, 2)  # channels_last view: MIOpen's NHWC kernels
         if up:

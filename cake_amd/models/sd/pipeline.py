@@ -50,13 +50,16 @@ def image_preprocess(path: str) -> torch.Tensor:
 
 
 def to_images(decoded: torch.Tensor) -> list:
+    """[B, 3, H, W] in [-1, 1] -> 8-bit RGB PIL images (sd.rs:544-547): on the device
+    path one kernel (sd_small.hip to_rgb8) writes u8 HWC, then one D2H copy."""
     from PIL import Image
-    x = ((decoded.float() / 2 + 0.5).clamp(0, 1) * 255).to(torch.uint8).cpu()
-    out = []
-    for b in range(x.shape[0]):
-        hwc = x[b].permute(1, 2, 0).contiguous().numpy()
-        out.append(Image.fromarray(hwc, "RGB"))
-    return out
+    if decoded.is_cuda and decoded.dtype in (torch.float16, torch.bfloat16):
+        from ...ops import hip as K
+        x = K.to_rgb8(decoded.contiguous()).cpu()
+    else:
+        x = ((decoded.float() / 2 + 0.5).clamp(0, 1) * 255).to(torch.uint8).permute(0, 2, 3, 1)
+        x = x.contiguous().cpu()
+    return [Image.fromarray(x[b].numpy(), "RGB") for b in range(x.shape[0])]
 
 
 class SDGenerator(ImageGenerator):
@@ -131,6 +134,40 @@ class SDGenerator(ImageGenerator):
             emb = torch.cat([u.to(self.device), emb.to(self.device)], 0)
         return emb.to(device=self.device, dtype=self.dtype)
 
+    def _fused_steps(self) -> bool:
+        import os
+
+        from .shardable import SDUnit
+        return (isinstance(self.unet, SDUnit) and torch.device(self.device).type == "cuda"
+                and self.dtype in (torch.float16, torch.bfloat16)
+                and os.environ.get("CAKE_SD_FUSED_STEP", "1") != "0")
+
+    def _steps_eager(self, args, sched, ts, t_start, latents, text_emb, guidance, use_guide, gen,
+                     trace, n_steps, callback):
+        """One UNet round trip per step (remote UNet / CPU): the reference's loop."""
+        for i, t in enumerate(ts):
+            if i < t_start:
+                continue
+            t0 = time.perf_counter()
+            with ChromeTrace.span(trace, f"step {i + 1}"):
+                inp = torch.cat([latents, latents], 0) if use_guide else latents
+                inp = sched.scale_model_input(inp, t)
+                with ChromeTrace.span(trace, "unet"):
+                    pred = unet_forward_unpacked(self.unet, inp.to(self.dtype), text_emb, t,
+                                                 self.device).float()
+                if use_guide:
+                    u, c = pred.chunk(2, 0)
+                    pred = u + (c - u) * guidance
+                latents = sched.step(pred, t, latents, gen)
+            if self.device.type == "cuda":
+                torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            self.last_step_s.append(dt)
+            log.info("step %d/%d done, %.2fs", i + 1, n_steps, dt)
+            if args.intermediary_images and i % args.intermediary_images == 0:
+                callback(self.split_images(latents))
+        return latents
+
     # ------------------------------------------------------------------ images
     def split_images(self, latents: torch.Tensor) -> list:
         dec = vae_decode(self.vae, (latents / self.cfg.vae_scale).to(self.dtype), self.device)
@@ -174,27 +211,25 @@ class SDGenerator(ImageGenerator):
                 shape = (args.bsize, 4, cfg.height // 8, cfg.width // 8)
                 latents = torch.randn(shape, generator=gen).to(self.device) * sched.init_noise_sigma
             latents = latents.float()
-            for i, t in enumerate(ts):
-                if i < t_start:
-                    continue
-                t0 = time.perf_counter()
-                with ChromeTrace.span(trace, f"step {i + 1}"):
-                    inp = torch.cat([latents, latents], 0) if use_guide else latents
-                    inp = sched.scale_model_input(inp, t)
-                    with ChromeTrace.span(trace, "unet"):
-                        pred = unet_forward_unpacked(self.unet, inp.to(self.dtype), text_emb, t,
-                                                     self.device).float()
-                    if use_guide:
-                        u, c = pred.chunk(2, 0)
-                        pred = u + (c - u) * guidance
-                    latents = sched.step(pred, t, latents, gen)
-                if self.device.type == "cuda":
-                    torch.cuda.synchronize()
-                dt = time.perf_counter() - t0
-                self.last_step_s.append(dt)
-                log.info("step %d/%d done, %.2fs", i + 1, n_steps, dt)
-                if args.intermediary_images and i % args.intermediary_images == 0:
-                    callback(self.split_images(latents))
+            if self._fused_steps() and t_start < len(ts):
+                # local UNet on the GPU: each step is one graph replay (device timestep,
+                # UNet, CFG + scheduler update + next input; SDUnit.denoise)
+                steps = ts[t_start:]
+                seed = int(torch.randint(0, 2 ** 62, (1,), generator=gen).item())
+
+                def on_step(k, x, first=t_start):
+                    i = first + k
+                    if args.intermediary_images and i % args.intermediary_images == 0:
+                        callback(self.split_images(x))
+                with ChromeTrace.span(trace, f"denoise {len(steps)} steps"):
+                    latents, dts = self.unet.denoise(latents, text_emb, sched, steps, guidance,
+                                                     use_guide, seed, on_step)
+                for k, dt in enumerate(dts):
+                    self.last_step_s.append(dt)
+                    log.info("step %d/%d done, %.2fs", t_start + k + 1, n_steps, dt)
+            else:
+                latents = self._steps_eager(args, sched, ts, t_start, latents, text_emb,
+                                            guidance, use_guide, gen, trace, n_steps, callback)
             log.debug("Generating the final image for sample %d/%d.", idx + 1, args.num_samples)
             with ChromeTrace.span(trace, "vae_decode"):
                 callback(self.split_images(latents))

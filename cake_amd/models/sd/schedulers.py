@@ -1,8 +1,12 @@
 """Diffusion schedulers (the reference uses candle's DDIM and Euler-ancestral,
 cake-core/src/models/sd/sd.rs:429-431,442,476,504).
 
-Both operate on f32 latents with host-side coefficients; the elementwise
-update is a handful of fused torch ops (bandwidth-trivial next to the UNet).
+Both operate on f32 latents with host-side coefficients.  The device path
+(``step_coefs`` + sd_small.hip ``sched_step``) writes every step's update as
+``prev = A x + B eps + N z`` with the next step's input scale S, so the
+CFG combine, the update and the next UNet input are one kernel whose
+coefficients come from a device table (the denoise step replays as a graph);
+the torch methods below are the CPU path and the reference math.
 """
 from __future__ import annotations
 
@@ -58,6 +62,23 @@ class DDIMScheduler:
         a = float(self.acp[t])
         return math.sqrt(a) * original.float() + math.sqrt(1.0 - a) * noise.float()
 
+    def input_scale(self, timestep: int) -> float:
+        return 1.0
+
+    def step_coefs(self, timestep: int, next_timestep: int | None) -> tuple:
+        """(A, B, N, S_next): prev = A x + B eps (+ N z); S_next scales the next input."""
+        t = timestep if timestep < len(self.acp) else timestep - 1
+        prev = t - self.step_ratio
+        a_t = float(self.acp[t])
+        a_p = float(self.acp[prev]) if prev >= 0 else self.final_acp
+        if self.cfg.prediction_type == "epsilon":
+            A = math.sqrt(a_p / a_t)
+            B = math.sqrt(1.0 - a_p) - math.sqrt(a_p * (1.0 - a_t) / a_t)
+        else:  # v_prediction
+            A = math.sqrt(a_p * a_t) + math.sqrt((1.0 - a_p) * (1.0 - a_t))
+            B = math.sqrt((1.0 - a_p) * a_t) - math.sqrt(a_p * (1.0 - a_t))
+        return (A, B, 0.0, 1.0)
+
 
 class EulerAncestralScheduler:
     """Euler-ancestral (SDXL-Turbo), epsilon prediction."""
@@ -106,6 +127,18 @@ class EulerAncestralScheduler:
     def add_noise(self, original: torch.Tensor, noise: torch.Tensor, timestep: int) -> torch.Tensor:
         s = float(self.sigmas[self._index.get(timestep, 0)])
         return original.float() + noise.float() * s
+
+    def input_scale(self, timestep: int) -> float:
+        s = float(self.sigmas[self._index[timestep]])
+        return 1.0 / math.sqrt(s * s + 1)
+
+    def step_coefs(self, timestep: int, next_timestep: int | None) -> tuple:
+        i = self._index[timestep]
+        s_from, s_to = float(self.sigmas[i]), float(self.sigmas[i + 1])
+        s_up = math.sqrt(max(0.0, s_to ** 2 * (s_from ** 2 - s_to ** 2) / s_from ** 2))
+        s_down = math.sqrt(max(0.0, s_to ** 2 - s_up ** 2))
+        S = self.input_scale(next_timestep) if next_timestep is not None else 1.0
+        return (1.0, s_down - s_from, s_up, S)
 
 
 def build_scheduler(cfg: SchedulerConfig, steps: int):

@@ -94,6 +94,75 @@ class SDUnit:
         st["graph"].replay()
         return st["out"].clone()
 
+    @torch.no_grad()
+    def denoise(self, x: torch.Tensor, emb: torch.Tensor, sched, ts: list[int],
+                guidance: float, use_guide: bool, seed: int, on_step=None) -> tuple:
+        """Every diffusion step of ``ts`` on this local UNet, each step ONE hipGraph
+        replay: time biases from the device timestep table -> UNet -> CFG combine +
+        scheduler update + next UNet input (sd_small.hip) -> step += 1.  The first
+        step runs eagerly (conv autotuning, cross-attention k/v) and the graph is
+        captured from the second on; graphs are kept per shape / step count, their
+        buffers refilled for a new generation.  on_step(i, x) runs between steps
+        (intermediary images).  Returns (latents f32, per-step seconds)."""
+        from ...ops import hip as K
+        from .unet import refresh_kv_cache
+        dev = self.device
+        n = len(ts)
+        x = x.to(dev, torch.float32).contiguous()
+        emb = emb.to(dev, self.dtype).contiguous()
+        B2 = x.shape[0] * (2 if use_guide else 1)
+        key = ("denoise", tuple(x.shape), tuple(emb.shape), bool(use_guide), n, float(guidance))
+        st = self._graphs.get(key)
+        coef = torch.tensor([sched.step_coefs(t, ts[i + 1] if i + 1 < n else None)
+                             for i, t in enumerate(ts)], dtype=torch.float32)
+        ttab = torch.tensor([float(t) for t in ts], dtype=torch.float32)
+        if st is None:
+            st = {"x": x.clone(), "emb": emb.clone(), "kv": {}, "graph": None,
+                  "t": ttab.to(dev), "coef": coef.to(dev),
+                  "step": torch.zeros(1, dtype=torch.int32, device=dev),
+                  "seed": torch.zeros(1, dtype=torch.int64, device=dev),
+                  "inp": torch.empty((B2,) + tuple(x.shape[1:]), device=dev, dtype=self.dtype)}
+            self._graphs[key] = st
+        else:
+            st["x"].copy_(x)
+            st["t"].copy_(ttab)
+            st["coef"].copy_(coef)
+            st["step"].zero_()
+            if not torch.equal(st["emb"], emb):
+                st["emb"].copy_(emb)
+                refresh_kv_cache(st["kv"], st["emb"])
+        st["seed"].fill_(int(seed) & 0x7FFFFFFFFFFFFFFF)
+        K.scale_copy(st["x"], sched.input_scale(ts[0]), use_guide, st["inp"])
+
+        def body():
+            pred = self.model.forward(self.w, st["inp"], st["t"], st["emb"], kv_cache=st["kv"],
+                                      t_index=st["step"])
+            K.sched_step(st["x"], pred, use_guide, guidance, st["coef"], st["step"],
+                         st["seed"], next_in=st["inp"])
+            K.step_advance(st["step"])
+        times = []
+        for i in range(n):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            if st["graph"] is not None and self.use_graph:
+                st["graph"].replay()
+            elif i == 0 or not self.use_graph:
+                body()
+            else:
+                g = torch.cuda.CUDAGraph()
+                # capture only records; the step is then replayed for real (guidance is
+                # part of the key's graph: a new guidance value recaptures)
+                with torch.cuda.graph(g):
+                    body()
+                st["graph"] = g
+                g.replay()
+            e1.record()
+            e1.synchronize()
+            times.append(e0.elapsed_time(e1) / 1e3)
+            if on_step is not None:
+                on_step(i, st["x"])
+        return st["x"].clone(), times
+
     def layer_name(self) -> str:
         return self.name
 
@@ -128,32 +197,6 @@ class RemoteSDUnit:
 
     def __init__(self, client, name: str):
         self.client, self.name = client, name
-
-    def _unet_graph(self, lat: torch.Tensor, emb: torch.Tensor, t: float) -> torch.Tensor:
-        """One UNet step as a hipGraph replay (captured on first use of a shape after one
-        eager warm-up step that autotunes the convolutions).  The cross-attention
-        k/v cache is refreshed in place when the text embedding changes."""
-        from .unet import refresh_kv_cache
-        key = (tuple(lat.shape), tuple(emb.shape), lat.dtype)
-        st = self._graphs.get(key)
-        if st is None:
-            st = {"lat": lat.clone(), "emb": emb.clone(), "kv": {},
-                  "t": torch.full((), t, device=lat.device, dtype=torch.float32)}
-            self.model.forward(self.w, st["lat"], st["t"], st["emb"], kv_cache=st["kv"])
-            torch.cuda.synchronize()
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                st["out"] = self.model.forward(self.w, st["lat"], st["t"], st["emb"],
-                                               kv_cache=st["kv"])
-            st["graph"] = g
-            self._graphs[key] = st
-        elif not torch.equal(st["emb"], emb):
-            st["emb"].copy_(emb)
-            refresh_kv_cache(st["kv"], st["emb"])
-        st["lat"].copy_(lat)
-        st["t"].fill_(t)
-        st["graph"].replay()
-        return st["out"].clone()
 
     def layer_name(self) -> str:
         return self.name

@@ -84,10 +84,14 @@ class ResnetBlock2D(Module):
                 p.update(m.params())
         return p
 
-    def __call__(self, W, x, temb=None):
+    def __call__(self, W, x, temb=None, tb=None):
+        """temb: the time embedding (the block projects silu(temb) itself), or tb: this
+        block's precomputed time bias [B, C_out] f32 (the UNet batches every block's
+        projection into one GEMM)."""
         h = ops.group_norm(x, W[f"{self.name}.norm1.weight"], W[f"{self.name}.norm1.bias"],
                            self.groups, self.eps, silu=True)
-        tb = self.temb(W, F.silu(temb)) if self.temb is not None and temb is not None else None
+        if tb is None and self.temb is not None and temb is not None:
+            tb = self.temb(W, F.silu(temb))
         h = self.conv1(W, h, bias2=tb)  # time embedding fused as a per-sample bias
         h = ops.group_norm(h, W[f"{self.name}.norm2.weight"], W[f"{self.name}.norm2.bias"],
                            self.groups, self.eps, silu=True)
@@ -288,42 +292,95 @@ class UNet2DConditionModel(Module):
             p.update(m.params())
         return p
 
-    def forward(self, W, sample: torch.Tensor, timestep: float, ctx: torch.Tensor,
-                kv_cache: dict | None = None) -> torch.Tensor:
-        """kv_cache: optional dict reused across the steps of ONE generation (fixed ctx);
-        holds the cross-attention k/v projections of the context."""
-        cfg = self.cfg
-        B = sample.shape[0]
-        dt = sample.dtype
-        if isinstance(timestep, torch.Tensor):  # device scalar: replayable in a hipGraph
-            t = timestep.to(sample.device, torch.float32).reshape(-1).expand(B)
-        else:
-            t = torch.full((B,), float(timestep), device=sample.device)
-        emb = timestep_embedding(t, cfg.blocks[0].out_channels, cfg.flip_sin_to_cos,
-                                 cfg.freq_shift).to(dt)
-        emb = self.t2(W, F.silu(self.t1(W, emb)))
-        with ops.layout_nhwc(ops.want_nhwc(sample)):
-            return ops.to_external(self._body(W, ops.to_internal(sample), emb, ctx, kv_cache))
+    def resnets(self) -> list:
+        out = []
+        for res, _, _ in self.down:
+            out += res
+        out += self.mid_res
+        for res, _, _ in self.up:
+            out += res
+        return out
 
-    def _body(self, W, sample, emb, ctx, kv_cache):
+    def _temb_all(self, W):
+        """Every ResnetBlock2D's time_emb_proj stacked into ONE weight [sum C, temb]
+        (+ bias): the per-step time biases of the whole UNet are one GEMM."""
+        key = "@temb_all"
+        if key not in W:
+            blocks = [r for r in self.resnets() if r.temb is not None]
+            W[key] = torch.cat([W[f"{r.temb.name}.weight"] for r in blocks], 0).contiguous()
+            W[key + ".bias"] = torch.cat([W[f"{r.temb.name}.bias"] for r in blocks], 0)
+            offs, o = {}, 0
+            for r in blocks:
+                offs[r.name] = (o, r.temb.cout)
+                o += r.temb.cout
+            W[key + ".offs"] = offs
+        return W[key], W[key + ".bias"], W[key + ".offs"]
+
+    def time_biases(self, W, timestep, B: int, dtype, device, t_index=None) -> dict:
+        """{resnet name: time bias [B, C] f32} for this step.
+
+        timestep: a float, a device scalar, or a device table indexed on the device by
+        t_index (int32 [1]) — the last two replay unchanged in a hipGraph across steps.
+        Device path: sinusoidal-embedding kernel -> linear_1 (+SiLU) -> linear_2 (+SiLU)
+        -> one GEMM for every block's time_emb_proj (f32 out)."""
+        cfg = self.cfg
+        C0 = cfg.blocks[0].out_channels
+        wall, ball, offs = self._temb_all(W)
+        hip = torch.device(device).type == "cuda" and dtype in (torch.float16, torch.bfloat16)
+        if hip:
+            from ...ops import gemm as G
+            from ...ops import hip as K
+            if isinstance(timestep, torch.Tensor):
+                tt = timestep.to(device, torch.float32).reshape(-1).contiguous()
+            else:
+                tt = torch.full((1,), float(timestep), device=device)
+            emb = torch.empty(B, C0, device=device, dtype=dtype)
+            K.timestep_embed(tt, t_index, B, C0, cfg.flip_sin_to_cos, cfg.freq_shift, emb)
+            h = G.linear(emb, W[f"{self.t1.name}.weight"], W[f"{self.t1.name}.bias"], epi="silu")
+            st = G.linear(h, W[f"{self.t2.name}.weight"], W[f"{self.t2.name}.bias"], epi="silu")
+            tb = torch.empty(B, wall.shape[0], device=device, dtype=torch.float32)
+            G.linear(st, wall, ball, epi="store32", resid=tb)
+        else:
+            if isinstance(timestep, torch.Tensor):
+                tv = timestep.reshape(-1)
+                tv = tv[int(t_index.item())] if t_index is not None else tv[0]
+                t = tv.to(device, torch.float32).expand(B)
+            else:
+                t = torch.full((B,), float(timestep), device=device)
+            emb = timestep_embedding(t, C0, cfg.flip_sin_to_cos, cfg.freq_shift).to(dtype)
+            st = F.silu(self.t2(W, F.silu(self.t1(W, emb))))
+            tb = F.linear(st, wall, ball).float()
+        return {name: tb[:, o:o + c] for name, (o, c) in offs.items()}
+
+    def forward(self, W, sample: torch.Tensor, timestep, ctx: torch.Tensor,
+                kv_cache: dict | None = None, t_index=None) -> torch.Tensor:
+        """kv_cache: optional dict reused across the steps of ONE generation (fixed ctx);
+        holds the cross-attention k/v projections of the context.  timestep: float, device
+        scalar, or device table + t_index (see :meth:`time_biases`)."""
+        tbs = self.time_biases(W, timestep, sample.shape[0], sample.dtype, sample.device,
+                               t_index)
+        with ops.layout_nhwc(ops.want_nhwc(sample)):
+            return ops.to_external(self._body(W, ops.to_internal(sample), tbs, ctx, kv_cache))
+
+    def _body(self, W, sample, tbs, ctx, kv_cache):
         cfg = self.cfg
         x = self.conv_in(W, sample)
         skips = [x]
         for res, att, ds in self.down:
             for j, r in enumerate(res):
-                x = r(W, x, emb)
+                x = r(W, x, tb=tbs[r.name])
                 if att:
                     x = att[j](W, x, ctx, kv_cache)
                 skips.append(x)
             if ds is not None:
                 x = ds(W, x)
                 skips.append(x)
-        x = self.mid_res[0](W, x, emb)
+        x = self.mid_res[0](W, x, tb=tbs[self.mid_res[0].name])
         x = self.mid_att(W, x, ctx, kv_cache)
-        x = self.mid_res[1](W, x, emb)
+        x = self.mid_res[1](W, x, tb=tbs[self.mid_res[1].name])
         for res, att, us in self.up:
             for j, r in enumerate(res):
-                x = r(W, torch.cat([x, skips.pop()], ops.cdim()), emb)
+                x = r(W, torch.cat([x, skips.pop()], ops.cdim()), tb=tbs[r.name])
                 if att:
                     x = att[j](W, x, ctx, kv_cache)
             if us is not None:

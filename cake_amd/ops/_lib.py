@@ -43,6 +43,11 @@ _SIGS = {
     "cake_push_token": [P, P, P, P, P, I, P],
     "cake_gemv_set_tuning": [I, I, I, I],
     "cake_sample_threshold": [P, I, F, I, F, P, P],
+    "cake_timestep_embed": [I, P, P, I, I, I, F, I, P, P],
+    "cake_sched_step": [I, P, P, C.c_longlong, I, F, P, P, P, P, P],
+    "cake_step_advance": [P, P],
+    "cake_scale_copy": [I, P, C.c_longlong, F, I, P, P],
+    "cake_to_rgb8": [I, P, I, I, I, I, P, P],
     "cake_attn512": [I, P, P, P, P, I, I, I, C.c_longlong, C.c_longlong, C.c_longlong,
                      C.c_longlong, C.c_longlong, C.c_longlong, C.c_longlong, C.c_longlong, F, P,
                      P],
@@ -100,5 +105,5 @@ _SIGS.update({
     "cake_groupnorm_nhwc_splits": [I],
     "cake_layernorm": [I, P, P, P, C.c_longlong, I, F, P, P],
     "cake_geglu": [I, P, C.c_longlong, I, P, P],
-    "cake_conv2d_nhwc": [I, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, P],
+    "cake_conv2d_nhwc": [I, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, P],
 })

@@ -18,7 +18,7 @@ import torch
 
 from ._lib import check, kernels
 
-EPI = {"store": 0, "resid32": 1, "add16": 2, "swiglu": 3, "geglu": 4}
+EPI = {"store": 0, "resid32": 1, "add16": 2, "swiglu": 3, "geglu": 4, "store32": 6, "silu": 7}
 _DT = {torch.bfloat16: 0, torch.float16: 1}
 # (BM, BN) of the kernel's tile configurations (gemm.hip CAKE_GEMM_CFGS)
 CFG_TILES = {0: (128, 128), 1: (64, 128), 2: (256, 128), 3: (128, 256), 4: (64, 64),
@@ -125,6 +125,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, *
       add16   -> out = y (+ bias) + resid (16-bit [..., N])
       swiglu  -> out [..., F] = silu(y_gate) * y_up
       geglu   -> out [..., F] = (y_h + b_h) * gelu_tanh(y_gate + b_gate)
+      store32 -> resid (f32 [..., N], any row stride) = y (+ bias); returns resid
+      silu    -> out = silu(y (+ bias))
     """
     if epi not in EPI:
         raise ValueError(f"unknown epilogue {epi}")
@@ -156,9 +158,9 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, *
             raise ValueError(f"gemm.linear: bias must be a contiguous {x.dtype} [{Nv}] tensor")
     ldr = 0
     rptr = None
-    if epi == "resid32":
+    if epi in ("resid32", "store32"):
         if resid is None or resid.dtype != torch.float32 or not resid.is_cuda:
-            raise ValueError("resid32 needs an f32 device residual")
+            raise ValueError(f"{epi} needs an f32 device output/residual")
         r2, ldr = _rows_view(resid, "resid")
         if tuple(r2.shape) != (M, N):
             raise ValueError(f"resid shape {tuple(resid.shape)} != {(M, N)}")
@@ -170,7 +172,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, *
         if tuple(r2.shape) != (M, N):
             raise ValueError(f"resid shape {tuple(resid.shape)} != {(M, N)}")
         rptr = r2.data_ptr()
-    if epi == "resid32":
+    if epi in ("resid32", "store32"):
         out2, ldc, cptr = None, 0, None
     else:
         if out is None:
@@ -181,8 +183,9 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, *
         if tuple(out2.shape) != (M, N):
             raise ValueError(f"out shape {tuple(out.shape)} != {(M, N)}")
         cptr = out2.data_ptr()
+    f32_out = epi in ("resid32", "store32")
     if M == 0:
-        return resid if epi == "resid32" else out
+        return resid if f32_out else out
     c0, s0 = plan(M, Nv, K, epi)
     cfg = c0 if cfg is None else cfg
     splits = s0 if splits is None else max(1, int(splits))
@@ -192,4 +195,4 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, *
                            None if bias is None else bias.data_ptr(), rptr, ldr,
                            None if ws is None else ws.data_ptr(), _zeros16(x.device).data_ptr(),
                            M, N, K, torch.cuda.current_stream().cuda_stream), "gemm")
-    return resid if epi == "resid32" else out
+    return resid if f32_out else out

@@ -494,8 +494,13 @@ def conv2d_nhwc(x, w, bias=None, *, stride: int = 1, pad: int = 1, up: bool = Fa
     _req(w, "w", dtype=x.dtype)
     if bias is not None:
         _req(bias, "bias", dtype=x.dtype, numel=OC)
-    if bias2 is not None:
-        _req(bias2, "bias2", dtype=torch.float32, shape=(N, OC))
+    bias2_ld = 0
+    if bias2 is not None:  # [N, OC] f32, rows may be strided (one slice of a batched projection)
+        if not (bias2.is_cuda and bias2.dtype == torch.float32 and tuple(bias2.shape) == (N, OC)
+                and bias2.stride(1) == 1 and bias2.stride(0) % 4 == 0 and bias2.data_ptr() % 16 == 0):
+            raise ValueError(f"bias2: expected an f32 [{N}, {OC}] device view with unit column "
+                             f"stride and 16-byte aligned rows")
+        bias2_ld = bias2.stride(0) if N > 1 else OC
     if resid is not None:
         _req(resid, "resid", dtype=x.dtype, shape=(N, OH, OW, OC))
     if out is None:
@@ -522,6 +527,73 @@ def conv2d_nhwc(x, w, bias=None, *, stride: int = 1, pad: int = 1, up: bool = Fa
                                      None if ws is None else _p(ws), _p(_zeros16(x.device)),
                                      N, H, W, IC, OC, KH, KW,
                                      stride, pad, int(up), int(cfg), int(splits), th, tw,
-                                     _stream()),
+                                     int(bias2_ld), _stream()),
           "conv2d_nhwc")
+    return out
+
+
+# ---------------------------------------------------------------------------
+# Stable Diffusion step glue (sd_small.hip)
+# ---------------------------------------------------------------------------
+
+def timestep_embed(t_table, step, B: int, dim: int, flip: bool, shift: float, out):
+    """out [B, dim] (16-bit or f32) = sinusoidal embedding of t_table[*step] (step may be
+    None: t_table[0]); both read on the device, so the launch replays across steps."""
+    _req(t_table, "t_table", dtype=torch.float32)
+    if step is not None:
+        _req(step, "step", dtype=torch.int32, numel=1)
+    _req(out, "out", numel=B * dim)
+    out16 = out.dtype in _DT
+    if not out16 and out.dtype != torch.float32:
+        raise TypeError("timestep_embed: out must be 16-bit or f32")
+    check(kernels().cake_timestep_embed(_DT.get(out.dtype, 0), _p(t_table), _p(step), B, dim,
+                                        int(flip), float(shift), int(out16), _p(out), _stream()),
+          "timestep_embed")
+
+
+def sched_step(x, pred, cfg: bool, guidance: float, coef, step, seed, next_in=None):
+    """x (f32 latents) <- A x + B eps + N z  with eps the CFG-combined UNet prediction
+    and (A, B, N, S) = coef[*step]; next_in (16-bit) <- S * x (duplicated for CFG).
+    seed: int64 device scalar keying the Philox noise (read on the device)."""
+    n = x.numel()
+    _req(x, "x", dtype=torch.float32)
+    _req(pred, "pred", numel=n * (2 if cfg else 1))
+    _req(coef, "coef", dtype=torch.float32)
+    _req(step, "step", dtype=torch.int32, numel=1)
+    if coef.dim() != 2 or coef.shape[1] != 4:
+        raise ValueError("coef must be [steps, 4]")
+    if next_in is not None:
+        _req(next_in, "next_in", dtype=pred.dtype, numel=n * (2 if cfg else 1))
+    _req(seed, "seed", dtype=torch.int64, numel=1)
+    check(kernels().cake_sched_step(_dt(pred), _p(x), _p(pred), n, int(cfg), float(guidance),
+                                    _p(coef), _p(step), _p(seed), _p(next_in), _stream()),
+          "sched_step")
+
+
+def step_advance(step):
+    _req(step, "step", dtype=torch.int32, numel=1)
+    check(kernels().cake_step_advance(_p(step), _stream()), "step_advance")
+
+
+def scale_copy(x, scale: float, dup: bool, out):
+    """out (16-bit) <- scale * x (f32), written twice back to back when dup (CFG batch)."""
+    n = x.numel()
+    _req(x, "x", dtype=torch.float32)
+    _req(out, "out", numel=n * (2 if dup else 1))
+    check(kernels().cake_scale_copy(_dt(out), _p(x), n, float(scale), int(dup), _p(out),
+                                    _stream()), "scale_copy")
+
+
+def to_rgb8(img, nhwc: bool = False) -> torch.Tensor:
+    """Decoded image (16-bit, [B,3,H,W] or [B,H,W,3] when nhwc) -> u8 [B,H,W,3]."""
+    _req(img, "img")
+    if nhwc:
+        B, H, W, C = img.shape
+    else:
+        B, C, H, W = img.shape
+    if C != 3:
+        raise ValueError("to_rgb8: 3 channels expected")
+    out = torch.empty(B, H, W, 3, device=img.device, dtype=torch.uint8)
+    check(kernels().cake_to_rgb8(_dt(img), _p(img), B, H, W, int(nhwc), _p(out), _stream()),
+          "to_rgb8")
     return out

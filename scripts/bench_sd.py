@@ -22,6 +22,9 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--dtype", default="f16")
     ap.add_argument("--graph", action="store_true", help="replay the UNet step as one hipGraph")
+    ap.add_argument("--denoise", action="store_true",
+                    help="whole diffusion loop through SDUnit.denoise: device timestep, UNet, "
+                         "CFG + scheduler update in one graph replay per step")
     ap.add_argument("--no-kv-cache", dest="kv_cache", action="store_false",
                     help="recompute the cross-attention k/v of the text context every step")
     a = ap.parse_args()
@@ -33,6 +36,8 @@ def main():
     B = 2  # classifier-free guidance doubles the batch
     x = torch.randn(B, 4, cfg.height // 8, cfg.width // 8, device=dev, dtype=dt)
     ctx = torch.randn(B, 77, cfg.unet.cross_attention_dim, device=dev, dtype=dt)
+    if a.denoise:
+        return bench_denoise(a, cfg, w, dev, dt, ctx)
     tbuf = torch.zeros((), device=dev)
     kv = {} if a.kv_cache else None  # cross-attn k/v of the (fixed) text context, as the pipeline
     with torch.no_grad():
@@ -56,6 +61,28 @@ def main():
                       "resolution": f"{cfg.width}x{cfg.height}", "batch": B, "dtype": a.dtype,
                       "value": round(dt_step, 4), "unit": "s/step", "graph": a.graph,
                       "ctx_kv_cache": a.kv_cache,
+                      "nhwc": os.environ.get("CAKE_SD_NHWC", "1") != "0"}))
+
+
+def bench_denoise(a, cfg, w, dev, dt, ctx):
+    from cake_amd.models.sd.schedulers import build_scheduler
+    from cake_amd.models.sd.shardable import SDUnit
+    unit = SDUnit("unet", cfg, w, dev, dt)
+    sched = build_scheduler(cfg.scheduler, a.steps + 2)
+    ts = sched.timesteps()
+    lat = torch.randn(1, 4, cfg.height // 8, cfg.width // 8, device=dev) * sched.init_noise_sigma
+    with torch.no_grad():
+        unit.denoise(lat, ctx, sched, ts, 7.5, True, 1)  # step 0 eager, capture, replays
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        _, per = unit.denoise(lat, ctx, sched, ts, 7.5, True, 2)
+        torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / len(ts)
+    print(json.dumps({"metric": "sd_unet_seconds_per_step", "version": a.version,
+                      "resolution": f"{cfg.width}x{cfg.height}", "batch": 2, "dtype": a.dtype,
+                      "value": round(wall, 4), "unit": "s/step", "graph": True, "denoise": True,
+                      "scheduler": cfg.scheduler.kind, "steps": len(ts),
+                      "per_step_s": [round(x, 4) for x in per],
                       "nhwc": os.environ.get("CAKE_SD_NHWC", "1") != "0"}))
 
 

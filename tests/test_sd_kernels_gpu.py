@@ -229,3 +229,79 @@ def test_attn512_vs_fp32(cuda, dt, B, N, M):
             sc = (q[b, s0:s0 + 4096].float() @ k[b].float().t()) * scale
             ref[b, s0:s0 + 4096] = torch.softmax(sc, -1) @ v[b].float()
     torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("dim,flip,shift", [(320, True, 0.0), (256, False, 1.0)])
+def test_timestep_embed_vs_torch(cuda, dt, dim, flip, shift):
+    """sd_small.hip timestep_embed (device table + device step) vs the torch embedding."""
+    from cake_amd.models.sd.unet import timestep_embedding
+    from cake_amd.ops import hip as K
+    table = torch.tensor([999.0, 761.0, 21.0], device=cuda)
+    step = torch.tensor([1], device=cuda, dtype=torch.int32)
+    out = torch.empty(2, dim, device=cuda, dtype=dt)
+    K.timestep_embed(table, step, 2, dim, flip, shift, out)
+    ref = timestep_embedding(torch.tensor([761.0, 761.0]), dim, flip, shift)
+    tol = dict(atol=1e-3, rtol=1e-3) if dt == torch.float32 else _tol(dt)
+    torch.testing.assert_close(out.float().cpu(), ref, **tol)
+
+
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("cfg", [True, False])
+def test_sched_step_deterministic_vs_torch(cuda, dt, cfg):
+    """CFG combine + DDIM-style update (N = 0) + next input == the torch expression."""
+    from cake_amd.ops import hip as K
+    n = 4 * 32 * 32
+    x = torch.randn(n, device=cuda)
+    pred = torch.randn((2 if cfg else 1) * n, device=cuda).to(dt)
+    coef = torch.tensor([[0.9, -0.3, 0.0, 0.5], [1.1, 0.2, 0.0, 2.0]], device=cuda)
+    step = torch.tensor([1], device=cuda, dtype=torch.int32)
+    seed = torch.tensor([7], device=cuda, dtype=torch.int64)
+    nxt = torch.empty_like(pred)
+    x0 = x.clone()
+    K.sched_step(x, pred, cfg, 7.5, coef, step, seed, next_in=nxt)
+    e = pred.float()
+    if cfg:
+        u, c = e[:n], e[n:]
+        e = u + 7.5 * (c - u)
+    ref = 1.1 * x0 + 0.2 * e
+    torch.testing.assert_close(x, ref, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(nxt[:n].float(), (2.0 * ref).to(dt).float(), atol=0, rtol=0)
+    if cfg:
+        assert torch.equal(nxt[:n], nxt[n:])
+    K.step_advance(step)
+    assert int(step.item()) == 2
+
+
+def test_sched_step_noise_is_standard_normal(cuda):
+    """Euler-ancestral noise term: N(0, 1) per element, fresh per step, keyed by the seed."""
+    from cake_amd.ops import hip as K
+    n = 1 << 20
+    pred = torch.zeros(n, device=cuda, dtype=torch.bfloat16)
+    coef = torch.tensor([[0.0, 0.0, 1.0, 1.0]] * 2, device=cuda)
+    seed = torch.tensor([12345], device=cuda, dtype=torch.int64)
+    draws = []
+    for s in (0, 1, 0):
+        x = torch.zeros(n, device=cuda)
+        K.sched_step(x, pred, False, 1.0, coef, torch.tensor([s], device=cuda, dtype=torch.int32),
+                     seed)
+        draws.append(x)
+    z = draws[0]
+    assert abs(float(z.mean())) < 5e-3 and abs(float(z.std()) - 1.0) < 5e-3
+    assert abs(float(((z > 1.96).float().mean())) - 0.025) < 2e-3
+    assert torch.equal(draws[0], draws[2])  # same (seed, step) -> same noise
+    assert abs(float((draws[0] * draws[1]).mean())) < 5e-3  # steps independent
+    seed.fill_(54321)
+    x = torch.zeros(n, device=cuda)
+    K.sched_step(x, pred, False, 1.0, coef, torch.tensor([0], device=cuda, dtype=torch.int32), seed)
+    assert abs(float((x * z).mean())) < 5e-3
+
+
+@pytest.mark.parametrize("nhwc", [False, True])
+def test_to_rgb8_vs_torch(cuda, nhwc):
+    from cake_amd.ops import hip as K
+    img = (torch.rand(2, 3, 40, 24, device=cuda) * 2.4 - 1.2).half()
+    src = img.permute(0, 2, 3, 1).contiguous() if nhwc else img
+    got = K.to_rgb8(src, nhwc=nhwc)
+    ref = ((img.float() / 2 + 0.5).clamp(0, 1) * 255).to(torch.uint8).permute(0, 2, 3, 1)
+    assert torch.equal(got, ref)
