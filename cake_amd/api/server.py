@@ -5,7 +5,10 @@
   choices: [{index: 0, message: {role, content}}]}`` (text.rs:16-52,54-96).
   One request at a time (the reference's global write lock, text.rs:67):
   reset → add messages → generate.  Superset (Appendix E Q4/Q5): honours
-  ``max_tokens`` and ``stream`` (server-sent events), adds a ``usage`` block
+  ``max_tokens``, ``stream`` (server-sent events) and per-request
+  ``temperature`` / ``top_p`` / ``top_k`` / ``seed`` (the server's CLI values
+  when absent; on the device path they are read by the decode graph from device
+  memory, no recapture), adds a ``usage`` block
   and lowercase ``role`` (``CAKE_API_REFERENCE_ROLES=1`` restores the
   capitalised reference serialisation).
 * ``POST /api/v1/image`` — body ``{"image_args": {...sd-* keys...}}``,
@@ -30,6 +33,34 @@ def _reference_roles() -> bool:
     return os.environ.get("CAKE_API_REFERENCE_ROLES", "0") == "1"
 
 
+def request_sampling(body: dict, default):
+    """SamplingConfig of one chat request: the server default with the request's
+    temperature / top_p / top_k / seed.  ValueError on an invalid value."""
+    import dataclasses
+    over = {}
+    if body.get("temperature") is not None:
+        t = float(body["temperature"])
+        if not t >= 0.0:
+            raise ValueError("temperature must be >= 0")
+        over["temperature"] = t
+    if body.get("top_p") is not None:
+        p = float(body["top_p"])
+        if not 0.0 < p <= 1.0:
+            raise ValueError("top_p must be in (0, 1]")
+        over["top_p"] = None if p >= 1.0 else p
+    if body.get("top_k") is not None:
+        k = body["top_k"]
+        if isinstance(k, bool) or not isinstance(k, int) or k < 0:
+            raise ValueError("top_k must be a non-negative integer")
+        over["top_k"] = k or None
+    if body.get("seed") is not None:
+        sd = body["seed"]
+        if isinstance(sd, bool) or not isinstance(sd, int):
+            raise ValueError("seed must be an integer")
+        over["seed"] = sd & 0xFFFFFFFFFFFFFFFF
+    return dataclasses.replace(default, **over)
+
+
 def create_app(master):
     from fastapi import FastAPI, Request
     from fastapi.responses import JSONResponse, PlainTextResponse, StreamingResponse
@@ -51,6 +82,13 @@ def create_app(master):
         except (KeyError, TypeError, ValueError) as e:
             return JSONResponse({"error": f"bad request: {e}"}, status_code=400)
         max_tokens = body.get("max_tokens")
+        default = getattr(master.ctx, "sampling", None)
+        sampling = None
+        if default is not None and hasattr(master.llm, "set_sampling"):
+            try:
+                sampling = request_sampling(body, default)
+            except (TypeError, ValueError) as e:
+                return JSONResponse({"error": f"bad request: {e}"}, status_code=400)
         model_name = master.llm.MODEL_NAME
         rid, created = str(uuid.uuid4()), int(time.time())
         role = "Assistant" if _reference_roles() else "assistant"
@@ -58,6 +96,10 @@ def create_app(master):
         def run(sink):
             with lock:
                 master.reset()
+                # a new configuration, or an explicit seed (restart its stream)
+                if sampling is not None and (body.get("seed") is not None or
+                                             sampling != getattr(master.llm, "sampling", None)):
+                    master.llm.set_sampling(sampling)
                 for m in messages:
                     master.llm.add_message(m)
                 return master.generate_text(sink, max_tokens=max_tokens)

@@ -119,18 +119,37 @@ __device__ __forceinline__ float gumbel(uint32_t bits) {
   return -__logf(-__logf(u));  // u in (0, 1)
 }
 
+// Per-request sampling parameters read on the device (the API's temperature /
+// top_k / top_p / seed change without recapturing the decode graph).
+// temperature <= 0 selects greedy argmax.
+struct SampleParams {
+  float temperature;
+  int top_k;
+  float top_p;
+  uint32_t seed_lo, seed_hi;
+  uint32_t pad[3];
+};
+
+// params != nullptr overrides (inv_t, k0, k1); inv_t == 0 -> plain argmax (greedy)
 __global__ __launch_bounds__(256) void gumbel_argmax_kernel(
     const float* __restrict__ logits, int V, float inv_t, uint32_t k0, uint32_t k1,
     const int* __restrict__ step_ptr, const unsigned int* __restrict__ thr,
-    unsigned long long* __restrict__ slot) {
+    const SampleParams* __restrict__ params, unsigned long long* __restrict__ slot) {
   __shared__ unsigned long long red[4];
+  if (params != nullptr) {
+    const float t = params->temperature;
+    inv_t = t > 0.f ? 1.f / t : 0.f;
+    k0 = params->seed_lo;
+    k1 = params->seed_hi;
+  }
+  const bool greedy = !(inv_t > 0.f);
   const uint32_t step = (uint32_t)*step_ptr;
   const unsigned int lim = thr != nullptr ? *thr : 0u;
   unsigned long long best = 0;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < V; i += gridDim.x * blockDim.x) {
     const float l = logits[i];
     if (ordered(l) < lim) continue;
-    const float v = l * inv_t + gumbel(philox_u32((uint32_t)i, step, k0, k1));
+    const float v = greedy ? l : l * inv_t + gumbel(philox_u32((uint32_t)i, step, k0, k1));
     const unsigned long long key =
         ((unsigned long long)ordered(v) << 32) | (0xffffffffu - (unsigned int)i);
     best = key > best ? key : best;
@@ -166,12 +185,22 @@ __device__ __forceinline__ float sel_max(float v, float* red) {
 // over the logits (L2-resident right after the lm_head).
 __global__ __launch_bounds__(kSelThreads) void sample_threshold_kernel(
     const float* __restrict__ logits, int V, float inv_t, int top_k, float top_p,
-    unsigned int* __restrict__ thr_out) {
+    const SampleParams* __restrict__ params, unsigned int* __restrict__ thr_out) {
   __shared__ unsigned int cnt[256];
   __shared__ float mass[256];
   __shared__ float red[kSelThreads / 64];
   __shared__ unsigned int sel[2];
   const int tid = threadIdx.x;
+  if (params != nullptr) {
+    const float t = params->temperature;
+    if (!(t > 0.f)) {  // greedy: no restriction
+      if (tid == 0) *thr_out = 0u;
+      return;
+    }
+    inv_t = 1.f / t;
+    top_k = params->top_k;
+    top_p = params->top_p;
+  }
   unsigned int kthr = 0u;
   if (top_k > 0 && top_k < V) {
     unsigned int prefix = 0u, pmask = 0u;
@@ -265,7 +294,22 @@ CAKE_API int cake_sample_threshold(const float* logits, int V, float temperature
                                    float top_p, unsigned int* thr, hipStream_t st) {
   if (V <= 0 || !(temperature > 0.f)) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(sample_threshold_kernel, dim3(1), dim3(kSelThreads), 0, st, logits, V,
-                     1.f / temperature, top_k, top_p, thr);
+                     1.f / temperature, top_k, top_p, (const SampleParams*)nullptr, thr);
+  return (int)hipGetLastError();
+}
+
+// Device-parameter selection (SampleParams in device memory): threshold (a no-op
+// write of 0 when greedy / unrestricted) then the Gumbel (or plain) argmax.
+CAKE_API int cake_select_dev(const float* logits, int V, const void* params, const int* step,
+                             unsigned int* thr, unsigned long long* slot, hipStream_t st) {
+  if (V <= 0 || params == nullptr || thr == nullptr) return (int)hipErrorInvalidValue;
+  const SampleParams* p = (const SampleParams*)params;
+  hipLaunchKernelGGL(sample_threshold_kernel, dim3(1), dim3(kSelThreads), 0, st, logits, V, 1.f,
+                     0, 0.f, p, thr);
+  int g = (V + 255) / 256;
+  if (g > 512) g = 512;
+  hipLaunchKernelGGL(gumbel_argmax_kernel, dim3(g), dim3(256), 0, st, logits, V, 1.f, 0u, 0u,
+                     step, (const unsigned int*)thr, p, slot);
   return (int)hipGetLastError();
 }
 
@@ -277,7 +321,7 @@ CAKE_API int cake_gumbel_argmax(const float* logits, int V, float temperature,
   if (g > 512) g = 512;
   hipLaunchKernelGGL(gumbel_argmax_kernel, dim3(g), dim3(256), 0, st, logits, V,
                      1.f / temperature, (uint32_t)(seed & 0xffffffffull), (uint32_t)(seed >> 32),
-                     step, thr, slot);
+                     step, thr, (const SampleParams*)nullptr, slot);
   return (int)hipGetLastError();
 }
 

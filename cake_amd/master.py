@@ -104,9 +104,17 @@ class Master:
         a = self.ctx.args
         if getattr(a, "metrics", None):
             import json
+            extra = {}
+            fn = getattr(self.llm, "metrics", None)
+            if callable(fn):
+                try:
+                    extra = fn()
+                except Exception as e:  # noqa: BLE001  (metrics never fail a generation)
+                    log.warning("metrics: %s", e)
             with open(a.metrics, "a") as f:
                 f.write(json.dumps({"ts": time.time(), "kind": "text", **stats,
-                                    "rss_mib": round(rss_mib(), 1), **hbm_mib()}) + "\n")
+                                    "rss_mib": round(rss_mib(), 1), **hbm_mib(),
+                                    **extra}) + "\n")
         if getattr(a, "trace", None) and times:
             from .utils.trace import ChromeTrace
             tr = ChromeTrace()

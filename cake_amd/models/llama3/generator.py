@@ -63,6 +63,7 @@ class LLamaGenerator(TextGenerator):
         self.index_pos = 0
         self._dec: DeviceDecoder | None = None
         self._use_graph = use_graph
+        self._per_request = False
         self.last_stats = None
 
     # ------------------------------------------------------------------ factory
@@ -89,6 +90,23 @@ class LLamaGenerator(TextGenerator):
 
     def generated_tokens(self) -> int:
         return self.generated
+
+    def metrics(self) -> dict:
+        """Extra fields for the --metrics sink: per-layer decode kernel ms (device path)."""
+        if self._dec is None or not self._fast_path():
+            return {}
+        ms = self._dec.profile_layers()
+        return {"layer_ms": [round(x, 4) for x in ms], "layers_ms_total": round(sum(ms), 3)}
+
+    def set_sampling(self, sampling: SamplingConfig) -> None:
+        """Sampling configuration of the next generation (API per-request temperature /
+        top_k / top_p).  On the device path the decode graph reads it from device
+        memory, so switching costs no recapture after the first switch."""
+        self.sampling = sampling
+        self.logits_processor = LogitsProcessor(sampling)
+        self._per_request = True
+        if self._dec is not None:
+            self._dec.set_sampling(sampling)
 
     def _decode(self, tid: int) -> str | None:
         try:
@@ -133,6 +151,8 @@ class LLamaGenerator(TextGenerator):
             self._dec = DeviceDecoder(self.model, repeat_penalty=self.sampling.repeat_penalty,
                                       repeat_last_n=self.sampling.repeat_last_n, greedy=True,
                                       use_graph=self._use_graph, sampling=self.sampling)
+            if self._per_request:
+                self._dec.set_sampling(self.sampling)
         return self._dec
 
     def _next_token_device(self, index: int) -> Token:

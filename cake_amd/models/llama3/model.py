@@ -153,6 +153,7 @@ class DeviceDecoder:
         self.greedy = greedy
         self.use_graph = use_graph
         self.bufs: DecodeBuffers = model.stack.decode_buffers(with_head=True)
+        self.params: torch.Tensor | None = None  # device SampleParams (set_sampling)
         self.graph: torch.cuda.CUDAGraph | None = None
         self.host_pos = 0  # device position of the next step (tracked on the host)
         self._layers = list(range(model.cfg.num_hidden_layers))
@@ -168,7 +169,50 @@ class DeviceDecoder:
             K.repeat_penalty(b.logits, b.hist, b.hist_len, self.last_n, self.penalty)
         if self.greedy:
             K.select_token(b.logits, b.slot, b.hist, b.hist_len, b.tok, b.pos, self.sampling,
-                           b.thr)
+                           b.thr, params=self.params)
+
+    def set_sampling(self, sampling) -> None:
+        """Per-request sampling configuration (None / temperature <= 0 = greedy).  The
+        first call switches the selection to a device parameter block (one recapture);
+        later calls only rewrite that block, so the captured graph is reused."""
+        from ...ops import hip as K
+        if self.params is None:
+            self.params = torch.zeros(K.SAMPLE_PARAMS_WORDS, dtype=torch.int32,
+                                      device=self.m.device)
+            self.graph = None
+            self.greedy = True
+        self.sampling = sampling if sampling is not None and not sampling.greedy else None
+        self.params.copy_(K.pack_sample_params(sampling))
+
+    def profile_layers(self, reps: int = 3) -> list[float]:
+        """Per-layer decode kernel time (ms): each layer's five launches
+        captured as its own small graph and replayed between timing events, at the
+        current device position (the K/V row it writes is the next step's, which that
+        step rewrites).  Run between generations (--metrics)."""
+        from ...ops import hip as K
+        b, m = self.bufs, self.m
+        if getattr(self, "_layer_graphs", None) is None:
+            K.embed(m.head.embed, b.tok, b.resid)
+            torch.cuda.synchronize()
+            gs = []
+            for li in self._layers:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    m.stack.decode_step(b, [li], m.session)
+                gs.append(g)
+            self._layer_graphs = gs
+        K.embed(m.head.embed, b.tok, b.resid)
+        out = [0.0] * len(self._layer_graphs)
+        for _ in range(reps):
+            evs = [torch.cuda.Event(enable_timing=True) for _ in range(len(out) + 1)]
+            evs[0].record()
+            for i, g in enumerate(self._layer_graphs):
+                g.replay()
+                evs[i + 1].record()
+            evs[-1].synchronize()
+            for i in range(len(out)):
+                out[i] += evs[i].elapsed_time(evs[i + 1]) / reps
+        return out
 
     def capture(self) -> None:
         if not self.use_graph or self.graph is not None:
@@ -218,7 +262,7 @@ class DeviceDecoder:
             K.repeat_penalty(b.logits, b.hist, b.hist_len, self.last_n, self.penalty)
         if self.greedy:
             K.select_token(b.logits, b.slot, b.hist, b.hist_len, b.tok, b.pos, self.sampling,
-                           b.thr)
+                           b.thr, params=self.params)
             self.host_pos += 1
             return int(b.tok.item())
         raise RuntimeError("sampled mode: caller pushes the first token")

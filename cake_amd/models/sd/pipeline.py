@@ -222,8 +222,9 @@ class SDGenerator(ImageGenerator):
                     if args.intermediary_images and i % args.intermediary_images == 0:
                         callback(self.split_images(x))
                 with ChromeTrace.span(trace, f"denoise {len(steps)} steps"):
-                    latents, dts = self.unet.denoise(latents, text_emb, sched, steps, guidance,
-                                                     use_guide, seed, on_step)
+                    latents, dts = self.unet.denoise(
+                        latents, text_emb, sched, steps, guidance, use_guide, seed,
+                        on_step if args.intermediary_images else None)
                 for k, dt in enumerate(dts):
                     self.last_step_s.append(dt)
                     log.info("step %d/%d done, %.2fs", t_start + k + 1, n_steps, dt)

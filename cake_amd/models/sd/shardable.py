@@ -140,7 +140,7 @@ class SDUnit:
             K.sched_step(st["x"], pred, use_guide, guidance, st["coef"], st["step"],
                          st["seed"], next_in=st["inp"])
             K.step_advance(st["step"])
-        times = []
+        evs = []
         for i in range(n):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -157,10 +157,14 @@ class SDUnit:
                 st["graph"] = g
                 g.replay()
             e1.record()
-            e1.synchronize()
-            times.append(e0.elapsed_time(e1) / 1e3)
-            if on_step is not None:
+            evs.append((e0, e1))
+            if on_step is not None:  # intermediary images: the host needs this step's x
+                e1.synchronize()
                 on_step(i, st["x"])
+        # no host sync between steps otherwise: the next replay is enqueued while the
+        # current one runs (a large graph's launch is not free)
+        torch.cuda.synchronize()
+        times = [a.elapsed_time(b) / 1e3 for a, b in evs]
         return st["x"].clone(), times
 
     def layer_name(self) -> str:

@@ -305,16 +305,17 @@ class UNet2DConditionModel(Module):
         """Every ResnetBlock2D's time_emb_proj stacked into ONE weight [sum C, temb]
         (+ bias): the per-step time biases of the whole UNet are one GEMM."""
         key = "@temb_all"
+        blocks = [r for r in self.resnets() if r.temb is not None]
         if key not in W:
-            blocks = [r for r in self.resnets() if r.temb is not None]
             W[key] = torch.cat([W[f"{r.temb.name}.weight"] for r in blocks], 0).contiguous()
             W[key + ".bias"] = torch.cat([W[f"{r.temb.name}.bias"] for r in blocks], 0)
+        if getattr(self, "_temb_offs", None) is None:
             offs, o = {}, 0
             for r in blocks:
                 offs[r.name] = (o, r.temb.cout)
                 o += r.temb.cout
-            W[key + ".offs"] = offs
-        return W[key], W[key + ".bias"], W[key + ".offs"]
+            self._temb_offs = offs
+        return W[key], W[key + ".bias"], self._temb_offs
 
     def time_biases(self, W, timestep, B: int, dtype, device, t_index=None) -> dict:
         """{resnet name: time bias [B, C] f32} for this step.

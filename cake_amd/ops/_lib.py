@@ -52,6 +52,7 @@ _SIGS = {
                      C.c_longlong, C.c_longlong, C.c_longlong, C.c_longlong, C.c_longlong, F, P,
                      P],
     "cake_gumbel_argmax": [P, I, F, C.c_ulonglong, P, P, P, P],
+    "cake_select_dev": [P, I, P, P, P, P, P],
 }
 
 

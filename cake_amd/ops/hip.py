@@ -262,10 +262,39 @@ def gumbel_argmax(logits, temperature: float, seed: int, step, slot, thr=None):
                                        _p(slot), _stream()), "gumbel_argmax")
 
 
-def select_token(logits, slot, hist, hist_len, tok, pos, sampling=None, thr=None):
-    """Device token selection of one decode step: argmax (greedy) or a seeded draw
-    (temperature / top-k / top-p), then the step finalizer (tok, history, pos)."""
+SAMPLE_PARAMS_WORDS = 8
+
+
+def sample_params_tensor(sampling, device) -> torch.Tensor:
+    """Pack a SamplingConfig (None = greedy) into the 32-byte device SampleParams."""
+    return pack_sample_params(sampling).to(device)
+
+
+def pack_sample_params(sampling) -> torch.Tensor:
+    import struct
     if sampling is None or sampling.greedy:
+        t, k, p, seed = 0.0, 0, 0.0, 0
+    else:
+        t = float(sampling.temperature)
+        k = int(sampling.top_k) if sampling.top_k else 0
+        p = float(sampling.top_p) if sampling.top_p is not None else 0.0
+        seed = int(sampling.seed) & 0xFFFFFFFFFFFFFFFF
+    raw = struct.pack("<fif2I3I", t, k, p, seed & 0xFFFFFFFF, seed >> 32, 0, 0, 0)
+    return torch.frombuffer(bytearray(raw), dtype=torch.int32).clone()
+
+
+def select_token(logits, slot, hist, hist_len, tok, pos, sampling=None, thr=None, params=None):
+    """Device token selection of one decode step: argmax (greedy) or a seeded draw
+    (temperature / top-k / top-p), then the step finalizer (tok, history, pos).
+    params (int32[8] device SampleParams): the sampling configuration is read on the
+    device instead (temperature <= 0 = greedy), so it can change between graph replays."""
+    if params is not None:
+        _req(params, "params", dtype=torch.int32, numel=SAMPLE_PARAMS_WORDS)
+        _req(thr, "thr", numel=1)
+        _req(hist_len, "hist_len", dtype=torch.int32)
+        check(kernels().cake_select_dev(_p(logits), logits.numel(), _p(params), _p(hist_len),
+                                        _p(thr), _p(slot), _stream()), "select_dev")
+    elif sampling is None or sampling.greedy:
         argmax(logits, slot)
     else:
         restrict = (sampling.top_k is not None and sampling.top_k > 0) or \

@@ -139,6 +139,7 @@ class PipelineEngine:
         self.penalty, self.last_n = float(repeat_penalty), int(repeat_last_n)
         self.sampler = None   # host sampler (torch backend); None = selection on the device
         self.sampling = None  # SamplingConfig for the device draw (temperature > 0)
+        self.sample_params = None  # device SampleParams (set_sampling): per-request config
         self.hip = stack.backend == "hip"
         self.use_graph = use_graph and self.hip
         self.group = group
@@ -463,7 +464,28 @@ class PipelineEngine:
             K.repeat_penalty(b.logits, b.hist, b.hist_len, self.last_n, self.penalty)
         if self.sampler is None:
             K.select_token(b.logits, b.slot, b.hist, b.hist_len, b.tok, b.pos, self.sampling,
-                           b.thr)
+                           b.thr, params=self.sample_params)
+
+    def set_sampling(self, sampling) -> None:
+        """Per-request sampling (API temperature / top_k / top_p; None or temperature
+        <= 0 = greedy).  hip: the selection reads a device parameter block, so the
+        captured graphs stay valid; call once before capture() to switch to it."""
+        if not self.is_master:
+            return
+        if not self.hip:
+            from ..models.sampling import LogitsProcessor
+            self.sampler = None if sampling is None or sampling.greedy else \
+                LogitsProcessor(sampling).sample
+            return
+        from ..ops import hip as K
+        if self.sample_params is None:
+            if any(st.graphs for st in self.streams):
+                raise RuntimeError("set_sampling: call before capture()")
+            self.sample_params = torch.zeros(K.SAMPLE_PARAMS_WORDS, dtype=torch.int32,
+                                             device=self.device)
+        self.sampler = None
+        self.sampling = sampling if sampling is not None and not sampling.greedy else None
+        self.sample_params.copy_(K.pack_sample_params(sampling))
 
     def _host_sample_device(self, st: _Stream) -> int:
         """Sampled decoding on the hip path: draw on the host, push to the device state."""

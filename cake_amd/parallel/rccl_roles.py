@@ -57,8 +57,25 @@ class PipelineLLM(TextGenerator):
         self.last_stats = None
 
     @classmethod
-    def load(cls, ctx):  # built by run_rccl (needs the engine)
-        raise NotImplementedError("PipelineLLM is constructed by run_rccl")
+    def load(cls, ctx):
+        """Master-rank generator of an already running RCCL job (run_rccl builds the
+        engine collectively on every rank first; ``ctx.engine`` is that engine)."""
+        from ..models.llama3.generator import load_tokenizer
+        eng = getattr(ctx, "engine", None)
+        if eng is None or not eng.is_master:
+            raise RuntimeError("PipelineLLM.load needs ctx.engine: the master rank's "
+                               "PipelineEngine (see run_rccl)")
+        tok, eos = load_tokenizer(ctx.model_path, eng.cfg.eos_token_id)
+        return cls(eng, tok, eos, ctx.sampling)
+
+    def metrics(self) -> dict:
+        """--metrics fields of the pipeline: hop latency measured at start-up
+        (µs, device-timed ping-pong), hops per token, and every rank's HBM."""
+        return dict(getattr(self.eng, "metrics", {}) or {})
+
+    def set_sampling(self, sampling) -> None:
+        self.sampling = sampling
+        self.eng.set_sampling(sampling)
 
     def add_message(self, message) -> None:
         self.history.append(message)
@@ -123,6 +140,8 @@ def run_rccl(ctx) -> None:
                              repeat_penalty=s.repeat_penalty, repeat_last_n=s.repeat_last_n,
                              use_graph=not ctx.no_graph)
         log.info("rank %d/%d owns layers %s", rank, world, mine[:3] + (["..."] if len(mine) > 3 else []))
+        if rank == 0 and eng.hip:
+            eng.set_sampling(s)  # device-read parameters: per-request API sampling
         if eng.use_graph:
             # the worker graphs read the position from the received header; a
             # dummy prefill gives every graph valid state to capture against
@@ -131,10 +150,11 @@ def run_rccl(ctx) -> None:
             else:
                 _serve_one_prefill(eng)
             eng.capture()
+        _startup_metrics(eng, ctx, rank, world, len(mine))
         if rank == 0:
             from ..master import Master
-            tok, eos = load_tokenizer(ctx.model_path, cfg.eos_token_id)
-            master = Master(ctx, llm=PipelineLLM(eng, tok, eos, s))
+            ctx.engine = eng
+            master = Master(ctx, llm=PipelineLLM.load(ctx))
             try:
                 master.run()
             finally:
@@ -143,6 +163,24 @@ def run_rccl(ctx) -> None:
             eng.serve()
     finally:
         dist.destroy_process_group()
+
+
+def _startup_metrics(eng: PipelineEngine, ctx, rank: int, world: int, n_layers: int) -> None:
+    """Collective, once: per-hop latency (rank 0 <-> 1 ping-pong over the configured
+    transport) and each rank's HBM / layer count, kept on the master's engine."""
+    from ..context import hbm_mib
+    hop_us = eng.measure_hop_us() if world > 1 else None
+    mine = {"rank": rank, "layers": n_layers,
+            **(hbm_mib(ctx.device) if ctx.device.type == "cuda" else {})}
+    ranks = [None] * world
+    dist.all_gather_object(ranks, mine)
+    hops = sum(1 for k in range(1, len(eng.runs) + 2) if eng._recv_point(k))
+    eng.metrics = {"hop_us": None if hop_us is None else round(hop_us, 2),
+                   "hops_per_token": hops, "rank_hbm": ranks}
+    if rank == 0:
+        log.info("pipeline: %d hops/token, hop %s us; per-rank HBM %s", hops,
+                 "n/a" if hop_us is None else f"{hop_us:.1f}",
+                 [r.get("hbm_used_mib") for r in ranks])
 
 
 def _serve_one_prefill(eng: PipelineEngine) -> None:

@@ -51,3 +51,34 @@ def test_streaming_and_404(client):
     assert r.status_code == 404 and r.text == "nope"
     r = client.post("/api/v1/image", json={"image_args": {}})
     assert r.status_code == 400
+
+
+def test_per_request_sampling(client):
+    """temperature / top_p / top_k / seed per request (SURVEY Appendix E Q5 superset):
+    a seeded sampled request is reproducible, invalid values are rejected, and a
+    request without them returns to the server's (greedy) configuration."""
+    msgs = [{"role": "user", "content": "hello"}]
+    greedy = client.post("/api/v1/chat/completions", json={"messages": msgs}).json()
+    req = {"messages": msgs, "temperature": 1.5, "top_k": 50, "top_p": 0.95, "seed": 7}
+    a = client.post("/api/v1/chat/completions", json=req)
+    b = client.post("/api/v1/chat/completions", json=req)
+    assert a.status_code == 200
+    assert a.json()["choices"][0]["message"]["content"] == b.json()["choices"][0]["message"]["content"]
+    outs = {client.post("/api/v1/chat/completions", json=dict(req, seed=s)).json()
+            ["choices"][0]["message"]["content"] for s in range(6)}
+    assert len(outs) > 1  # the draw depends on the seed
+    back = client.post("/api/v1/chat/completions", json={"messages": msgs}).json()
+    assert back["choices"][0]["message"]["content"] == greedy["choices"][0]["message"]["content"]
+    for bad in ({"temperature": -1}, {"top_p": 0}, {"top_p": 1.5}, {"top_k": -3}, {"top_k": 1.5},
+                {"seed": "x"}):
+        r = client.post("/api/v1/chat/completions", json=dict(messages=msgs, **bad))
+        assert r.status_code == 400, bad
+
+
+def test_request_sampling_merge():
+    from cake_amd.api.server import request_sampling
+    from cake_amd.models.sampling import SamplingConfig
+    d = SamplingConfig(temperature=0.0, top_k=None, top_p=None, seed=1)
+    s = request_sampling({"temperature": 0.7, "top_p": 1.0, "top_k": 0}, d)
+    assert s.temperature == 0.7 and s.top_p is None and s.top_k is None and s.seed == 1
+    assert request_sampling({}, d) == d

@@ -92,3 +92,23 @@ def test_pipeline_engine_single_rank_streams(cuda):
     eng.decode(9)
     torch.cuda.synchronize()
     assert [eng.tokens(0), eng.tokens(1)] == expect
+
+
+def test_profile_layers_per_layer_ms(cuda):
+    """Per-layer decode kernel ms for the --metrics sink (one small graph per layer)."""
+    from cake_amd.models.llama3.config import preset
+    from cake_amd.models.llama3.decode_loop import run_decode
+    from cake_amd.models.llama3.factory import random_model
+    from cake_amd.models.llama3.model import DeviceDecoder
+    cfg = preset("llama3-8b", num_hidden_layers=3, vocab_size=4096, intermediate_size=1024,
+                 hidden_size=512, num_attention_heads=4, num_key_value_heads=1)
+    model = random_model(cfg, "cuda:0", torch.bfloat16, max_seq=128, seed=1)
+    dec = DeviceDecoder(model)
+    first = dec.start([1, 2, 3])
+    dec.capture()
+    toks = [first] + run_decode(dec, 6).tokens
+    ms = dec.profile_layers()
+    assert len(ms) == 3 and all(0 < x < 5 for x in ms)
+    # decoding again from the same prompt is unaffected by the profiling replays
+    first = dec.start([1, 2, 3])
+    assert [first] + run_decode(dec, 6).tokens == toks

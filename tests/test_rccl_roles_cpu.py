@@ -29,7 +29,16 @@ def test_rccl_roles_match_local(tmp_path):
     assert local.returncode == 0, local.stderr[-2000:]
     dist = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=3",
                  "--master-addr=127.0.0.1", "--master-port=29571", "-m", "cake_amd.cli",
-                 "--transport", "rccl", "--topology", str(topo), *common])
+                 "--transport", "rccl", "--topology", str(topo), "--metrics",
+                 str(tmp_path / "m.jsonl"), *common])
     assert dist.returncode == 0, dist.stderr[-3000:]
     text = local.stdout.strip()
     assert text and text in dist.stdout
+    # metrics sink: hop latency, hops per token and every rank's entry
+    import json
+    rec = json.loads((tmp_path / "m.jsonl").read_text().splitlines()[-1])
+    assert rec["kind"] == "text" and rec["generated"] == 10
+    assert rec["hop_us"] is not None and rec["hop_us"] > 0
+    assert rec["hops_per_token"] == 3
+    assert [r["rank"] for r in rec["rank_hbm"]] == [0, 1, 2]
+    assert [r["layers"] for r in rec["rank_hbm"]] == [1, 2, 1]

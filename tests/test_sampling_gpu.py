@@ -104,3 +104,37 @@ def test_seed_determinism_and_decoder(cuda):
     assert len(set(a)) > 3  # a real draw, not argmax repeated
     d = gen(7, T=0.5, k=5, p=0.9)
     assert len(d) == 25
+
+
+def test_device_params_match_static_and_switch_without_recapture(cuda):
+    """set_sampling (API per-request config): the decode graph reads the sampling
+    parameters from device memory — same tokens as the launch-argument path, greedy
+    (temperature 0) equals argmax, and later switches reuse the captured graph."""
+    from cake_amd.models.llama3.config import preset
+    from cake_amd.models.llama3.decode_loop import run_decode
+    from cake_amd.models.llama3.factory import random_model
+    from cake_amd.models.llama3.model import DeviceDecoder
+    from cake_amd.models.sampling import SamplingConfig
+    cfg = preset("llama3-8b", num_hidden_layers=2, vocab_size=4096, intermediate_size=1024,
+                 hidden_size=512, num_attention_heads=4, num_key_value_heads=1)
+    model = random_model(cfg, "cuda:0", torch.bfloat16, max_seq=256, seed=5)
+    prompt = [5, 6, 7, 8, 9]
+
+    def run(dec, n=20):
+        first = dec.start(prompt)
+        dec.capture()
+        return [first] + run_decode(dec, n).tokens
+
+    s1 = SamplingConfig(temperature=0.8, top_k=40, top_p=0.9, seed=3)
+    g0 = SamplingConfig(temperature=0.0)
+    static_s = run(DeviceDecoder(model, repeat_penalty=1.1, repeat_last_n=16, sampling=s1))
+    static_g = run(DeviceDecoder(model, repeat_penalty=1.1, repeat_last_n=16))
+    dyn = DeviceDecoder(model, repeat_penalty=1.1, repeat_last_n=16)
+    dyn.set_sampling(s1)
+    assert run(dyn) == static_s
+    graph = dyn.graph
+    dyn.set_sampling(g0)
+    assert run(dyn) == static_g
+    dyn.set_sampling(s1)
+    assert run(dyn) == static_s
+    assert dyn.graph is graph  # captured once
