@@ -86,7 +86,7 @@ __device__ __forceinline__ uint4 ds_read16(uint32_t addr) {
   return v;
 }
 
-template <int DT, int BM, int BN, int WM, int WN, int NS, int EPI>
+template <int DT, int BM, int BN, int WM, int WN, int NS, int EPI, int PR>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(GemmArgs g) {
   constexpr int NT = 64 * WM * WN;
   constexpr int NWAVE = WM * WN;
@@ -200,10 +200,12 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(GemmArgs g) {
     for (int i = 0; i < FM; ++i) af1[i] = ds_read16(ab + i * 16 * 128 + off1);
 #pragma unroll
     for (int j = 0; j < FN; ++j) bf1[j] = ds_read16(bb + j * 16 * 128 + off1);
+    if (PR) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j) acc[i][j] = cmfma<DT>(af0[i], bf0[j], acc[i][j]);
+    if (PR) __builtin_amdgcn_s_setprio(0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     const int nbuf = buf + 1 == NS ? 0 : buf + 1;
@@ -219,10 +221,12 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(GemmArgs g) {
 #pragma unroll
       for (int j = 0; j < FN; ++j) bf0[j] = ds_read16(nb + j * 16 * 128 + off0);
     }
+    if (PR) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j) acc[i][j] = cmfma<DT>(af1[i], bf1[j], acc[i][j]);
+    if (PR) __builtin_amdgcn_s_setprio(0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     buf = nbuf;
@@ -398,19 +402,22 @@ __global__ __launch_bounds__(256) void gemm_splitk_finalize(GemmArgs g, int spli
 
 using namespace cake;
 
-// tile configurations (BM, BN, WM, WN, LDS stages)
-#define CAKE_GEMM_CFGS(X)  \
-  X(0, 128, 128, 2, 2, 2)  \
-  X(1, 64, 128, 1, 4, 2)   \
-  X(2, 256, 128, 2, 2, 3)  \
-  X(3, 128, 256, 2, 2, 3)  \
-  X(4, 64, 64, 2, 2, 2)    \
-  X(5, 256, 256, 2, 4, 2)  \
-  X(6, 256, 128, 4, 2, 3)  \
-  X(7, 128, 128, 2, 2, 3)
+// tile configurations (BM, BN, WM, WN, LDS stages, s_setprio around the MFMA clusters)
+#define CAKE_GEMM_CFGS(X)    \
+  X(0, 128, 128, 2, 2, 2, 0) \
+  X(1, 64, 128, 1, 4, 2, 0)  \
+  X(2, 256, 128, 2, 2, 3, 0) \
+  X(3, 128, 256, 2, 2, 3, 0) \
+  X(4, 64, 64, 2, 2, 2, 0)   \
+  X(5, 256, 256, 2, 4, 2, 0) \
+  X(6, 256, 128, 4, 2, 3, 0) \
+  X(7, 128, 128, 2, 2, 3, 0) \
+  X(8, 256, 256, 2, 4, 2, 1) \
+  X(9, 256, 128, 4, 2, 3, 1) \
+  X(10, 128, 128, 2, 2, 2, 1)
 
 static inline void cfg_dims(int cfg, int& bm, int& bn) {
-#define X(id, BM, BN, WM, WN, NS) if (cfg == id) { bm = BM; bn = BN; return; }
+#define X(id, BM, BN, WM, WN, NS, PR) if (cfg == id) { bm = BM; bn = BN; return; }
   CAKE_GEMM_CFGS(X)
 #undef X
   bm = bn = 0;
@@ -423,10 +430,10 @@ CAKE_API int cake_gemm_tile(int cfg, int* bm, int* bn) {
 
 template <int DT, int EPI>
 static int launch_gemm(int cfg, dim3 grid, hipStream_t st, const GemmArgs& g) {
-#define X(id, BM, BN, WM, WN, NS)                                                            \
+#define X(id, BM, BN, WM, WN, NS, PR)                                                        \
   if (cfg == id) {                                                                           \
-    hipLaunchKernelGGL((gemm_kernel<DT, BM, BN, WM, WN, NS, EPI>), grid, dim3(64 * WM * WN), 0, \
-                       st, g);                                                               \
+    hipLaunchKernelGGL((gemm_kernel<DT, BM, BN, WM, WN, NS, EPI, PR>), grid, dim3(64 * WM * WN), \
+                       0, st, g);                                                            \
     return (int)hipGetLastError();                                                          \
   }
   CAKE_GEMM_CFGS(X)

@@ -22,11 +22,13 @@ EPI = {"store": 0, "resid32": 1, "add16": 2, "swiglu": 3, "geglu": 4, "store32":
 _DT = {torch.bfloat16: 0, torch.float16: 1}
 # (BM, BN) of the kernel's tile configurations (gemm.hip CAKE_GEMM_CFGS)
 CFG_TILES = {0: (128, 128), 1: (64, 128), 2: (256, 128), 3: (128, 256), 4: (64, 64),
-             5: (256, 256), 6: (256, 128), 7: (128, 128)}
-_SLOTS = {0: 2, 1: 2, 2: 1, 3: 1, 4: 4, 5: 1, 6: 1, 7: 1}  # resident workgroups per CU
+             5: (256, 256), 6: (256, 128), 7: (128, 128), 8: (256, 256), 9: (256, 128),
+             10: (128, 128)}
+_SLOTS = {0: 2, 1: 2, 2: 1, 3: 1, 4: 4, 5: 1, 6: 1, 7: 1, 8: 1, 9: 1, 10: 2}  # WGs per CU
 # relative per-tile throughput (measured sweep, profiles/r2_gemm_sweep.jsonl: the
 # 128x128 two-stage tile wins nearly every model shape)
-_EFF = {0: 1.0, 1: 0.75, 2: 0.8, 3: 0.8, 4: 0.5, 5: 0.8, 6: 0.8, 7: 0.9}
+_EFF = {0: 1.0, 1: 0.75, 2: 0.8, 3: 0.8, 4: 0.5, 5: 0.8, 6: 0.8, 7: 0.9, 8: 0.8, 9: 0.8,
+        10: 1.0}
 NUM_CUS = 256
 _bound = False
 _plans: dict = {}

@@ -45,6 +45,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--sweep", action="store_true")
     ap.add_argument("--only", default=None)
+    ap.add_argument("--cfgs", default=None, help="comma list: time each cfg (splits 1)")
     a = ap.parse_args()
     dt = torch.bfloat16
     for name, M, N, K, epi in SHAPES:
@@ -100,6 +101,13 @@ def main():
                         best = (t, cfg, splits)
             rec["best"] = {"cfg": best[1], "splits": best[2], "ms": round(best[0], 4),
                            "tflops": round(flops / best[0] / 1e9, 1)}
+        if a.cfgs:
+            per = {}
+            for _ in range(3):
+                for cfg in [int(c) for c in a.cfgs.split(",")]:
+                    t = timeit(lambda: ours(cfg, 1), reps=10)
+                    per[cfg] = min(per.get(cfg, 1e9), t)
+            rec["per_cfg_tflops"] = {c: round(flops / t / 1e9, 1) for c, t in per.items()}
         print(json.dumps(rec), flush=True)
 
 
