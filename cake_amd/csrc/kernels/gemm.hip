@@ -80,14 +80,50 @@ __device__ __forceinline__ float gelu_tanh(float x) {
   return 0.5f * x * (1.f + tanhf(u));
 }
 
+// MFMA with the accumulator pinned to AGPRs (tied "+a" operand): for 128x128 wave
+// tiles (256 accumulator registers) hipcc's own allocation rotates the accumulators
+// through VGPR copies around every MFMA.  Chained MFMAs on one accumulator need no
+// wait states; the A/B fragments come from counted LDS reads.
+typedef unsigned cu32x4 __attribute__((ext_vector_type(4)));
+
+template <int DT>
+__device__ __forceinline__ void amfma(cf32x4& acc, const uint4& a, const uint4& b) {
+  const cu32x4 av = __builtin_bit_cast(cu32x4, a), bv = __builtin_bit_cast(cu32x4, b);
+  if constexpr (DT == kBF16)
+    asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(av), "v"(bv));
+  else
+    asm("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(acc) : "v"(av), "v"(bv));
+}
+
+// same, volatile: kept in program order among the loads it is interleaved with
+template <int DT>
+__device__ __forceinline__ void amfma_v(cf32x4& acc, const uint4& a, const uint4& b) {
+  const cu32x4 av = __builtin_bit_cast(cu32x4, a), bv = __builtin_bit_cast(cu32x4, b);
+  if constexpr (DT == kBF16)
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(av), "v"(bv));
+  else
+    asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(acc) : "v"(av), "v"(bv));
+}
+
+// acc = 0 in the AGPR file (0 x 0 + 0; the fresh zero VGPRs need 2 wait states)
+__device__ __forceinline__ void azero(cf32x4& acc) {
+  const cu32x4 z = {0u, 0u, 0u, 0u};
+  asm volatile("s_nop 1\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %1, 0" : "=a"(acc) : "v"(z));
+}
+
 __device__ __forceinline__ uint4 ds_read16(uint32_t addr) {
   uint4 v;
   asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr));
   return v;
 }
 
+// PR bit 0: s_setprio(1) around the MFMA clusters; bit 1: AGPR-pinned accumulators;
+// bit 2: interleaved schedule (needs bit 1)
 template <int DT, int BM, int BN, int WM, int WN, int NS, int EPI, int PR>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(GemmArgs g) {
+  constexpr bool AG = (PR & 2) != 0;
+  constexpr bool IL = (PR & 4) != 0;
+  static_assert(!IL || AG, "the interleaved schedule pins AGPR-accumulator MFMAs");
   constexpr int NT = 64 * WM * WN;
   constexpr int NWAVE = WM * WN;
   constexpr int WTM = BM / WM, WTN = BN / WN;  // per-wave tile
@@ -147,14 +183,14 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(GemmArgs g) {
   }
   (void)is_a;
   const uint32_t lds0 = lds_off(smem);
+  auto stage_one = [&](int step, int buf, int i) {
+    const int k = kb + step * kGBK + chunk[i] * 8;
+    const uint16_t* p = (src[i] != nullptr && k < ke) ? src[i] + k : g.zeros;
+    glds16(p, smem + buf * BUF + (wave * IPW + i) * 1024);
+  };
   auto stage = [&](int step, int buf) {
-    const int k0 = kb + step * kGBK;
 #pragma unroll
-    for (int i = 0; i < IPW; ++i) {
-      const int k = k0 + chunk[i] * 8;
-      const uint16_t* p = (src[i] != nullptr && k < ke) ? src[i] + k : g.zeros;
-      glds16(p, smem + buf * BUF + (wave * IPW + i) * 1024);
-    }
+    for (int i = 0; i < IPW; ++i) stage_one(step, buf, i);
   };
 
   // ---- fragment addresses: row (lane & 15) of a 16-row group, slot swizzled
@@ -166,10 +202,21 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(GemmArgs g) {
   const uint32_t b_base = lds0 + (uint32_t)(BM + wc * WTN) * 128 + lrow;
 
   cf32x4 acc[FM][FN];
+  if constexpr (AG) {
 #pragma unroll
-  for (int i = 0; i < FM; ++i)
+    for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = cf32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < FN; ++j) azero(acc[i][j]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = cf32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  auto mma = [&](cf32x4& c, const uint4& a, const uint4& b) {
+    if constexpr (AG) amfma<DT>(c, a, b);
+    else c = cmfma<DT>(a, b, c);
+  };
 
   // One barrier per k-step, placed between the k 0..31 and k 32..63 halves so
   // that LDS latency never sits in front of the MFMAs:
@@ -179,6 +226,65 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(GemmArgs g) {
   // finished reading step t's buffer (its kk1 reads completed before it), so
   // the DMA issued right after it may overwrite that buffer.
   uint4 af0[FM], bf0[FN], af1[FM], bf1[FN];
+  if constexpr (IL) {
+    // Same pipeline as below, with every LDS read and DMA issued BETWEEN the MFMAs
+    // (program order pinned: volatile MFMAs and reads) instead of in bursts in
+    // front of them, so the matrix pipe never idles while a wave issues its
+    // loads.  Every step issues exactly IPW DMAs (past the end: the zeros page
+    // into the consumed buffer) so the counted waits are the same every step.
+    constexpr int NM = FM * FN, NR = FM + FN, NL = IPW + NR;
+    if (nk > 0) {
+      stage(0, 0);
+      if (NS == 3) stage(1, 1);
+      __builtin_amdgcn_s_waitcnt(vm_wait(NS == 3 ? IPW : 0));
+      asm volatile("s_barrier" ::: "memory");
+      stage(NS - 1, NS - 1);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af0[i] = ds_read16(a_base + i * 16 * 128 + off0);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bf0[j] = ds_read16(b_base + j * 16 * 128 + off0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    int buf = 0;
+    for (int t = 0; t < nk; ++t) {
+      const uint32_t ab = a_base + buf * BUF, bb = b_base + buf * BUF;
+#pragma unroll
+      for (int m = 0; m < NM; ++m) {
+        amfma_v<DT>(acc[m / FN][m % FN], af0[m / FN], bf0[m % FN]);
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+          if ((r * NM) / NR != m) continue;
+          if (r < FM) af1[r] = ds_read16(ab + r * 16 * 128 + off1);
+          else bf1[r - FM] = ds_read16(bb + (r - FM) * 16 * 128 + off1);
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      const int nbuf = buf + 1 == NS ? 0 : buf + 1;
+      __builtin_amdgcn_s_waitcnt(vm_wait((NS - 2) * IPW));  // DMA of step t+1 landed
+      asm volatile("s_barrier" ::: "memory");
+      const uint32_t na = a_base + nbuf * BUF, nb = b_base + nbuf * BUF;
+#pragma unroll
+      for (int m = 0; m < NM; ++m) {
+        amfma_v<DT>(acc[m / FN][m % FN], af1[m / FN], bf1[m % FN]);
+#pragma unroll
+        for (int l = 0; l < NL; ++l) {
+          if ((l * NM) / NL != m) continue;
+          if (l < IPW) {
+            stage_one(t + NS, buf, l);
+          } else {
+            const int r = l - IPW;
+            if (r < FM) af0[r] = ds_read16(na + r * 16 * 128 + off0);
+            else bf0[r - FM] = ds_read16(nb + (r - FM) * 16 * 128 + off0);
+          }
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      buf = nbuf;
+    }
+  } else {
   if (nk > 0) stage(0, 0);
   if (NS == 3 && nk > 1) stage(1, 1);
   if (nk > 0) {
@@ -200,12 +306,12 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(GemmArgs g) {
     for (int i = 0; i < FM; ++i) af1[i] = ds_read16(ab + i * 16 * 128 + off1);
 #pragma unroll
     for (int j = 0; j < FN; ++j) bf1[j] = ds_read16(bb + j * 16 * 128 + off1);
-    if (PR) __builtin_amdgcn_s_setprio(1);
+    if (PR & 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = cmfma<DT>(af0[i], bf0[j], acc[i][j]);
-    if (PR) __builtin_amdgcn_s_setprio(0);
+      for (int j = 0; j < FN; ++j) mma(acc[i][j], af0[i], bf0[j]);
+    if (PR & 1) __builtin_amdgcn_s_setprio(0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     const int nbuf = buf + 1 == NS ? 0 : buf + 1;
@@ -221,18 +327,26 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(GemmArgs g) {
 #pragma unroll
       for (int j = 0; j < FN; ++j) bf0[j] = ds_read16(nb + j * 16 * 128 + off0);
     }
-    if (PR) __builtin_amdgcn_s_setprio(1);
+    if (PR & 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = cmfma<DT>(af1[i], bf1[j], acc[i][j]);
-    if (PR) __builtin_amdgcn_s_setprio(0);
+      for (int j = 0; j < FN; ++j) mma(acc[i][j], af1[i], bf1[j]);
+    if (PR & 1) __builtin_amdgcn_s_setprio(0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     buf = nbuf;
   }
+  }
 
   // ---- epilogue: 16-row strips staged through this wave's LDS slice --------
+  if constexpr (AG) {  // MFMA D -> VALU read: >= 12 wait states after the last MFMA
+#pragma unroll
+    for (int j = 0; j < FN; ++j) asm volatile("" : "+a"(acc[FM - 1][j]));
+    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+#pragma unroll
+    for (int j = 0; j < FN; ++j) asm volatile("" : "+a"(acc[FM - 1][j]));
+  }
   __builtin_amdgcn_s_waitcnt(vm_wait(0));
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   float* stg = reinterpret_cast<float*>(smem + wave * STG);
@@ -402,19 +516,25 @@ __global__ __launch_bounds__(256) void gemm_splitk_finalize(GemmArgs g, int spli
 
 using namespace cake;
 
-// tile configurations (BM, BN, WM, WN, LDS stages, s_setprio around the MFMA clusters)
+// tile configurations (BM, BN, WM, WN, LDS stages, PR flags).  Measured
+// (profiles/r2_gemm_sweep_agpr.jsonl): AGPR-pinned accumulators are +10-20 % on
+// the 4-wave tiles; the 8-wave 256x256 tile is faster with the compiler's own
+// accumulators (11); a 4-wave 256x256 tile (128x128 per wave) and s_setprio
+// measured slower / neutral and were dropped.
 #define CAKE_GEMM_CFGS(X)    \
-  X(0, 128, 128, 2, 2, 2, 0) \
-  X(1, 64, 128, 1, 4, 2, 0)  \
-  X(2, 256, 128, 2, 2, 3, 0) \
-  X(3, 128, 256, 2, 2, 3, 0) \
-  X(4, 64, 64, 2, 2, 2, 0)   \
-  X(5, 256, 256, 2, 4, 2, 0) \
-  X(6, 256, 128, 4, 2, 3, 0) \
-  X(7, 128, 128, 2, 2, 3, 0) \
-  X(8, 256, 256, 2, 4, 2, 1) \
-  X(9, 256, 128, 4, 2, 3, 1) \
-  X(10, 128, 128, 2, 2, 2, 1)
+  X(0, 128, 128, 2, 2, 2, 2) \
+  X(1, 64, 128, 1, 4, 2, 2)  \
+  X(2, 256, 128, 2, 2, 3, 2) \
+  X(3, 128, 256, 2, 2, 3, 2) \
+  X(4, 64, 64, 2, 2, 2, 2)   \
+  X(5, 256, 256, 2, 4, 2, 2) \
+  X(6, 256, 128, 4, 2, 3, 2) \
+  X(7, 128, 128, 2, 2, 3, 2) \
+  X(8, 128, 128, 2, 2, 2, 6) \
+  X(9, 256, 256, 2, 4, 2, 6) \
+  X(10, 64, 128, 1, 4, 2, 6) \
+  X(11, 256, 256, 2, 4, 2, 0) \
+  X(12, 256, 128, 4, 2, 3, 6)
 
 static inline void cfg_dims(int cfg, int& bm, int& bn) {
 #define X(id, BM, BN, WM, WN, NS, PR) if (cfg == id) { bm = BM; bn = BN; return; }
