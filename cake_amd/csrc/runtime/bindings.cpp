@@ -240,7 +240,8 @@ PYBIND11_MODULE(_cake_runtime, mod) {
       .def("set_drop_after", &WorkerServer::set_drop_after)
       .def("set_stats_every", &WorkerServer::set_stats_every)
       .def("set_compute", [](WorkerServer& s, py::function fn) {
-        // fn(session, ops[(name, pos, idx)], dtype, shape, memoryview) -> (dtype, shape, bytes)
+        // fn(session, ops[(name, pos, idx)], dtype, shape, memoryview) -> (dtype, shape, data)
+        // data: bytes or any contiguous buffer (copied once into the reply)
         auto holder = std::make_shared<py::function>(std::move(fn));
         s.set_compute([holder](uint64_t session, const std::vector<BatchItem>& ops,
                                const RawTensor& x) -> OpResult {
@@ -253,7 +254,13 @@ PYBIND11_MODULE(_cake_runtime, mod) {
             py::tuple out = (*holder)(session, pops, x.dtype, x.shape, mv);
             r.dtype = out[0].cast<std::string>();
             r.shape = out[1].cast<std::vector<uint64_t>>();
-            r.data = out[2].cast<std::string>();
+            py::object d = out[2];
+            if (py::isinstance<py::bytes>(d)) {
+              r.data = d.cast<std::string>();
+            } else {
+              py::buffer_info bi = d.cast<py::buffer>().request();
+              r.data.assign(static_cast<const char*>(bi.ptr), (size_t)(bi.size * bi.itemsize));
+            }
           } catch (py::error_already_set& e) {
             r.error = e.what();
           }

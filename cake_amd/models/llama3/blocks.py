@@ -87,13 +87,16 @@ class LayerStack:
         self._sessions: OrderedDict[int, KVCache] = OrderedDict()
         self._decode_bufs: DecodeBuffers | None = None
         self._hostpos_bufs: DecodeBuffers | None = None
+        self.step_graphs = False  # T = 1 forward() as graph replays (worker serving)
+        self._step_graph_cache: dict = {}
 
     # ------------------------------------------------------------------ sessions
     def cache(self, session: int = 0) -> KVCache:
         kv = self._sessions.get(session)
         if kv is None:
             while len(self._sessions) >= self.max_sessions:
-                self._sessions.popitem(last=False)
+                old, _ = self._sessions.popitem(last=False)
+                self._drop_step_graphs(old)  # their graphs point at the evicted cache
             kv = KVCache(len(self.weights), self.cfg, self.max_seq, self.device, self.dtype)
             self._sessions[session] = kv
         else:
@@ -109,6 +112,7 @@ class LayerStack:
 
     def drop(self, session: int) -> None:
         self._sessions.pop(session, None)
+        self._drop_step_graphs(session)
 
     @property
     def layer_ids(self) -> list[int]:
@@ -130,6 +134,10 @@ class LayerStack:
         kv = self.cache(session)
         if pos0 + T > self.max_seq:
             raise ValueError(f"sequence length {pos0 + T} exceeds max_seq {self.max_seq}")
+        if self.backend == "hip" and T == 1 and self.step_graphs and hidden.is_cuda:
+            self._decode_graph(hidden, layers, pos0, session)
+            kv.length = max(kv.length, pos0 + 1)
+            return hidden
         for li in layers:
             w = self.weights[li]
             s = self.slot_of[li]
@@ -163,6 +171,33 @@ class LayerStack:
             K.gemv(bufs.act, w.wd, bufs.resid, accumulate=True)
 
     # ------------------------------------------------------------------ hip paths
+    def _decode_graph(self, hidden, layers: list[int], pos0: int, session: int) -> None:
+        """T = 1 over a run of layers as ONE graph replay (worker serving path): the
+        first request of a (session, run) runs eagerly and captures the step; later
+        ones copy the hidden state and position in, replay, copy the state out."""
+        key = (session, tuple(layers))
+        ent = self._step_graph_cache.get(key)
+        if ent is None:
+            bufs = DecodeBuffers(self.cfg, self.max_seq, self.device, self.dtype, with_head=False)
+            bufs.pos.fill_(pos0)
+            bufs.resid.copy_(hidden[0])
+            self.decode_step(bufs, layers, session)
+            hidden[0].copy_(bufs.resid)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):  # records only
+                self.decode_step(bufs, layers, session)
+            self._step_graph_cache[key] = (g, bufs)
+            return
+        g, bufs = ent
+        bufs.pos.fill_(pos0)
+        bufs.resid.copy_(hidden[0])
+        g.replay()
+        hidden[0].copy_(bufs.resid)
+
+    def _drop_step_graphs(self, session: int) -> None:
+        for k in [k for k in self._step_graph_cache if k[0] == session]:
+            del self._step_graph_cache[k]
+
     def _decode_hip_hostpos(self, hidden, w, kc, vc, pos0):
         if self._hostpos_bufs is None:
             self._hostpos_bufs = DecodeBuffers(self.cfg, self.max_seq, self.device, self.dtype,

@@ -21,6 +21,7 @@ import os
 import platform
 import threading
 import time
+import warnings
 
 import torch
 
@@ -61,6 +62,8 @@ class Worker:
             self.stack = load_stack(ctx.model_path, cfg, layers, ctx.device, ctx.dtype,
                                     max_seq=ctx.max_seq_len)
             self.stack.max_sessions = 64
+            # T = 1 requests replay one captured graph per (session, layer run)
+            self.stack.step_graphs = os.environ.get("CAKE_WORKER_GRAPH", "1") != "0"
             log.info("loaded %d blocks on %s (%s)", len(layers), ctx.device, ctx.dtype)
         else:
             from ..models.sd.shardable import load_sd_units
@@ -105,12 +108,19 @@ class Worker:
         return self.server.stats()
 
     def _compute(self, session: int, ops, dtype: str, shape, data) -> tuple:
-        """Native-server callback: run `ops` on the payload, return (dtype, shape, bytes)."""
-        x = P.tensor_from_payload({"dtype": dtype, "shape": list(shape), "offset": 0,
-                                   "nbytes": len(data)}, bytes(data))
+        """Native-server callback: run `ops` on the payload, return (dtype, shape, data).
+
+        The request tensor is a zero-copy view of the native server's receive buffer
+        (copied once, straight to the device); the reply is one device-to-host copy
+        whose buffer the native server copies into the frame."""
+        with warnings.catch_warnings():  # the receive buffer is read-only; it is only read
+            warnings.simplefilter("ignore", UserWarning)
+            raw = torch.frombuffer(data, dtype=torch.uint8) if len(data) else \
+                torch.empty(0, dtype=torch.uint8)
+        x = raw.view(P.FROM_CANDLE[dtype]).reshape(list(shape))
         y = self._run_ops(x, ops, session)
         name, shp, buf = P.tensor_payload(y)
-        return name, shp, buf.tobytes()
+        return name, shp, buf
 
     def _reset(self, session: int) -> None:
         if self.stack is not None:
@@ -140,8 +150,6 @@ class Worker:
                         j += 1
                     self.stack.forward(h, layers, pos, session)
                     i = j
-                if h.is_cuda:
-                    torch.cuda.synchronize()
             return h.reshape(shape)
         with self.compute_lock:
             for name, _, _ in ops:

@@ -112,3 +112,33 @@ def test_profile_layers_per_layer_ms(cuda):
     # decoding again from the same prompt is unaffected by the profiling replays
     first = dec.start([1, 2, 3])
     assert [first] + run_decode(dec, 6).tokens == toks
+
+
+def test_worker_step_graphs_match_eager(cuda):
+    """Worker serving path: T = 1 forward() over a layer run replays one captured graph
+    per (session, run); outputs equal the eager launches, sessions stay independent,
+    and evicting a session drops its graphs."""
+    cfg = preset("llama3-8b", num_hidden_layers=4, vocab_size=512, intermediate_size=1024,
+                 hidden_size=512, num_attention_heads=4, num_key_value_heads=1)
+    m = random_model(cfg, "cuda:0", torch.bfloat16, max_seq=64, seed=3)
+    st = m.stack
+    torch.manual_seed(0)
+    xs = [torch.randn(1, 512, device=cuda) for _ in range(6)]
+
+    def run(graphs):
+        st.step_graphs = graphs
+        st.reset()
+        outs = []
+        for sess in (0, 1):
+            for p, x in enumerate(xs[:3] if sess == 0 else xs[3:]):
+                h = x.clone()
+                st.forward(h, [1, 2], p, session=sess)
+                outs.append(h)
+        return torch.stack(outs)
+    ref = run(False)
+    got = run(True)
+    torch.testing.assert_close(got, ref, atol=1e-3, rtol=1e-3)
+    assert {k[0] for k in st._step_graph_cache} == {0, 1}
+    st.drop(1)
+    assert {k[0] for k in st._step_graph_cache} == {0}
+    st.step_graphs = False
