@@ -12,7 +12,12 @@ timed region and exactly K decode steps are timed.
   behind the GPU.
 * N > 1 (one rank per GPU; launched by torchrun, or self-launched: with no
   WORLD_SIZE in the environment bench.py spawns the N ranks itself and only
-  relays rank 0's JSON line): the layers are sharded contiguously over the N
+  relays rank 0's JSON line), default ``--parallel tp``: every rank holds 1/N
+  of every layer (heads, MLP rows, vocabulary) and streams 1/N of the weights
+  per token; the two per-layer all-reduces and the argmax max are device-side
+  one-shot kernels over xGMI inside each rank's decode graph
+  (parallel/tensor_parallel.py).  ``--parallel pp``: the reference's layer
+  sharding — the layers are sharded contiguously over the N
   ranks as a cake topology would place them (rank 0 = master with
   embedding/lm_head + the first shard); the hidden state hops rank→rank as
   device-side peer stores over xGMI captured inside every rank's decode graph
@@ -41,7 +46,7 @@ def _args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=128)
     ap.add_argument("--warmup", type=int, default=16)
-    ap.add_argument("--model", default="llama3-8b", choices=["llama3-8b", "llama3-70b", "tiny"])
+    ap.add_argument("--model", default="llama3-8b", choices=["llama3-8b", "llama3-70b", "tiny", "tiny-kv2"])
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--prompt-len", type=int, default=32)
     ap.add_argument("--max-seq", type=int, default=4096)
@@ -57,6 +62,12 @@ def _args(argv=None):
     ap.add_argument("--streams", type=int, default=1,
                     help="N>1: concurrent sequences in the pipeline (1 = cake's single-sequence "
                          "pipeline, the headline; S > 1 = aggregate throughput of S sequences)")
+    ap.add_argument("--parallel", default="tp", choices=["tp", "pp"],
+                    help="N > 1: tp = tensor-parallel (every rank 1/N of every layer, default), "
+                         "pp = the reference's layer sharding (pipeline)")
+    ap.add_argument("--allreduce", default="ipc", choices=["ipc", "dist"],
+                    help="tp all-reduce: device-side one-shot kernels over xGMI, or "
+                         "torch.distributed")
     ap.add_argument("--hop", default="ipc", choices=["ipc", "dist"],
                     help="N>1 decode hop: device-side peer stores in the graph (ipc) or "
                          "host-issued torch.distributed p2p (dist)")
@@ -87,12 +98,14 @@ def _emit(a, value, ms, p50, p99, n, extra):
         "dtype": "f32" if getattr(a, "cpu", False) else a.dtype,
         "data": "synthetic (random-init weights, synthetic prompt ids, EOS ignored)",
         "config": {"model": {"llama3-8b": "Llama-3-8B", "llama3-70b": "Llama-3-70B",
-                             "tiny": "tiny"}[a.model],
+                             "tiny": "tiny", "tiny-kv2": "tiny-kv2"}[a.model],
                    "global_batch": extra.get("streams", 1), "seq_len": a.prompt_len + a.warmup + a.steps,
                    "prompt_len": a.prompt_len,
                    "parallelism": "single" if n == 1 else
-                   f"pp{n} (layer-sharded, {extra.get('hop', 'dist')} hops, "
-                   f"{extra.get('streams', 1)} stream(s))",
+                   (f"tp{n} (tensor-parallel, {extra.get('allreduce')} all-reduce)"
+                    if extra.get("parallel") == "tp" else
+                    f"pp{n} (layer-sharded, {extra.get('hop', 'dist')} hops, "
+                    f"{extra.get('streams', 1)} stream(s))"),
                    "decode": "greedy, repeat_penalty %.2f last_n %d" % (a.repeat_penalty,
                                                                         a.repeat_last_n)},
     }
@@ -238,8 +251,12 @@ def main(argv=None) -> int:
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return self_launch(a, argv)
     if world > 1 or a.gpus > 1:
-        from cake_amd.parallel.pipeline_bench import bench_pipeline
-        bench_pipeline(a, _emit)
+        if a.parallel == "tp":
+            from cake_amd.parallel.tp_bench import bench_tp
+            bench_tp(a, _emit)
+        else:
+            from cake_amd.parallel.pipeline_bench import bench_pipeline
+            bench_pipeline(a, _emit)
     elif a.cpu:
         bench_cpu_single(a)
     else:

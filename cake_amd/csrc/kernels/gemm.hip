@@ -517,24 +517,22 @@ __global__ __launch_bounds__(256) void gemm_splitk_finalize(GemmArgs g, int spli
 using namespace cake;
 
 // tile configurations (BM, BN, WM, WN, LDS stages, PR flags).  Measured
-// (profiles/r2_gemm_sweep_agpr.jsonl): AGPR-pinned accumulators are +10-20 % on
-// the 4-wave tiles; the 8-wave 256x256 tile is faster with the compiler's own
-// accumulators (11); a 4-wave 256x256 tile (128x128 per wave) and s_setprio
-// measured slower / neutral and were dropped.
+// (profiles/r2_gemm_sweep_agpr.jsonl, r2_gemm_sweep_il.jsonl): AGPR-pinned
+// accumulators +10-20 % on the 4-wave tiles, the interleaved schedule a further
+// +5-13 % on every tile (8-wave 256x256: 1144 -> 1286 TFLOP/s at 8192^3); 8 and 11
+// are the non-interleaved forms kept for A/B; a 4-wave 256x256 tile (128x128
+// per wave) and s_setprio measured slower / neutral and were dropped.
 #define CAKE_GEMM_CFGS(X)    \
-  X(0, 128, 128, 2, 2, 2, 2) \
-  X(1, 64, 128, 1, 4, 2, 2)  \
-  X(2, 256, 128, 2, 2, 3, 2) \
-  X(3, 128, 256, 2, 2, 3, 2) \
-  X(4, 64, 64, 2, 2, 2, 2)   \
-  X(5, 256, 256, 2, 4, 2, 2) \
-  X(6, 256, 128, 4, 2, 3, 2) \
-  X(7, 128, 128, 2, 2, 3, 2) \
-  X(8, 128, 128, 2, 2, 2, 6) \
-  X(9, 256, 256, 2, 4, 2, 6) \
-  X(10, 64, 128, 1, 4, 2, 6) \
-  X(11, 256, 256, 2, 4, 2, 0) \
-  X(12, 256, 128, 4, 2, 3, 6)
+  X(0, 128, 128, 2, 2, 2, 6) \
+  X(1, 64, 128, 1, 4, 2, 6)  \
+  X(2, 256, 128, 2, 2, 3, 6) \
+  X(3, 128, 256, 2, 2, 3, 6) \
+  X(4, 64, 64, 2, 2, 2, 6)   \
+  X(5, 256, 256, 2, 4, 2, 6) \
+  X(6, 256, 128, 4, 2, 3, 6) \
+  X(7, 128, 128, 2, 2, 3, 6) \
+  X(8, 128, 128, 2, 2, 2, 2) \
+  X(11, 256, 256, 2, 4, 2, 0)
 
 static inline void cfg_dims(int cfg, int& bm, int& bn) {
 #define X(id, BM, BN, WM, WN, NS, PR) if (cfg == id) { bm = BM; bn = BN; return; }

@@ -11,9 +11,11 @@
 
 namespace cake {
 
+// logits holds vocab entries [off, off + V) (tensor-parallel shard; off = 0, V = all
+// otherwise); history tokens outside the shard are skipped.
 __global__ void repeat_penalty_kernel(float* __restrict__ logits, const int* __restrict__ hist,
                                       const int* __restrict__ hist_len, int last_n,
-                                      float penalty) {
+                                      float penalty, int off, int V) {
   const int len = *hist_len;
   const int n = min(last_n, len);
   const int start = len - n;
@@ -21,9 +23,10 @@ __global__ void repeat_penalty_kernel(float* __restrict__ logits, const int* __r
     const int tok = hist[start + i];
     bool dup = false;
     for (int j = 0; j < i; ++j) dup |= (hist[start + j] == tok);
-    if (!dup) {
-      const float s = logits[tok];
-      logits[tok] = s >= 0.f ? s / penalty : s * penalty;
+    const int t = tok - off;
+    if (!dup && t >= 0 && t < V) {
+      const float s = logits[t];
+      logits[t] = s >= 0.f ? s / penalty : s * penalty;
     }
   }
 }
@@ -34,13 +37,15 @@ __device__ __forceinline__ unsigned int ordered(float f) {
 }
 
 // slot holds max over (ordered(value) << 32 | ~index): ties -> smallest index.
+// off: global vocab index of logits[0] (tensor-parallel shard)
 __global__ __launch_bounds__(256) void argmax_kernel(const float* __restrict__ logits, int V,
-                                                     unsigned long long* __restrict__ slot) {
+                                                     unsigned long long* __restrict__ slot,
+                                                     int off) {
   __shared__ unsigned long long red[4];
   unsigned long long best = 0;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < V; i += gridDim.x * blockDim.x) {
     const unsigned long long key =
-        ((unsigned long long)ordered(logits[i]) << 32) | (0xffffffffu - (unsigned int)i);
+        ((unsigned long long)ordered(logits[i]) << 32) | (0xffffffffu - (unsigned int)(i + off));
     best = key > best ? key : best;
   }
 #pragma unroll
@@ -134,7 +139,7 @@ struct SampleParams {
 __global__ __launch_bounds__(256) void gumbel_argmax_kernel(
     const float* __restrict__ logits, int V, float inv_t, uint32_t k0, uint32_t k1,
     const int* __restrict__ step_ptr, const unsigned int* __restrict__ thr,
-    const SampleParams* __restrict__ params, unsigned long long* __restrict__ slot) {
+    const SampleParams* __restrict__ params, unsigned long long* __restrict__ slot, int off) {
   __shared__ unsigned long long red[4];
   if (params != nullptr) {
     const float t = params->temperature;
@@ -149,9 +154,9 @@ __global__ __launch_bounds__(256) void gumbel_argmax_kernel(
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < V; i += gridDim.x * blockDim.x) {
     const float l = logits[i];
     if (ordered(l) < lim) continue;
-    const float v = greedy ? l : l * inv_t + gumbel(philox_u32((uint32_t)i, step, k0, k1));
-    const unsigned long long key =
-        ((unsigned long long)ordered(v) << 32) | (0xffffffffu - (unsigned int)i);
+    const uint32_t gi = (uint32_t)(i + off);  // global index: shard-independent draw
+    const float v = greedy ? l : l * inv_t + gumbel(philox_u32(gi, step, k0, k1));
+    const unsigned long long key = ((unsigned long long)ordered(v) << 32) | (0xffffffffu - gi);
     best = key > best ? key : best;
   }
 #pragma unroll
@@ -309,7 +314,7 @@ CAKE_API int cake_select_dev(const float* logits, int V, const void* params, con
   int g = (V + 255) / 256;
   if (g > 512) g = 512;
   hipLaunchKernelGGL(gumbel_argmax_kernel, dim3(g), dim3(256), 0, st, logits, V, 1.f, 0u, 0u,
-                     step, (const unsigned int*)thr, p, slot);
+                     step, (const unsigned int*)thr, p, slot, 0);
   return (int)hipGetLastError();
 }
 
@@ -321,14 +326,14 @@ CAKE_API int cake_gumbel_argmax(const float* logits, int V, float temperature,
   if (g > 512) g = 512;
   hipLaunchKernelGGL(gumbel_argmax_kernel, dim3(g), dim3(256), 0, st, logits, V,
                      1.f / temperature, (uint32_t)(seed & 0xffffffffull), (uint32_t)(seed >> 32),
-                     step, thr, (const SampleParams*)nullptr, slot);
+                     step, thr, (const SampleParams*)nullptr, slot, 0);
   return (int)hipGetLastError();
 }
 
 CAKE_API int cake_repeat_penalty(float* logits, const int* hist, const int* hist_len,
                                  int last_n, float penalty, hipStream_t st) {
   hipLaunchKernelGGL(repeat_penalty_kernel, dim3(1), dim3(256), 0, st, logits, hist, hist_len,
-                     last_n, penalty);
+                     last_n, penalty, 0, 0x7fffffff);
   return (int)hipGetLastError();
 }
 
@@ -336,7 +341,30 @@ CAKE_API int cake_argmax(const float* logits, int V, unsigned long long* slot,
                          hipStream_t st) {
   int g = (V + 255) / 256;
   if (g > 512) g = 512;
-  hipLaunchKernelGGL(argmax_kernel, dim3(g), dim3(256), 0, st, logits, V, slot);
+  hipLaunchKernelGGL(argmax_kernel, dim3(g), dim3(256), 0, st, logits, V, slot, 0);
+  return (int)hipGetLastError();
+}
+
+// Tensor-parallel vocab shard: logits = entries [off, off + V) of the vocabulary.
+// Penalty over the shard, then the shard's argmax key (global index) or, with
+// temperature > 0, its Gumbel-max key (Philox counter = global index, so the
+// all-reduced max equals the single-GPU draw).
+CAKE_API int cake_select_shard(float* logits, int V, int off, const int* hist, const int* hist_len,
+                               int last_n, float penalty, float temperature,
+                               unsigned long long seed, unsigned long long* slot, hipStream_t st) {
+  if (V <= 0 || off < 0) return (int)hipErrorInvalidValue;
+  if (penalty != 1.f)
+    hipLaunchKernelGGL(repeat_penalty_kernel, dim3(1), dim3(256), 0, st, logits, hist, hist_len,
+                       last_n, penalty, off, V);
+  int g = (V + 255) / 256;
+  if (g > 512) g = 512;
+  if (temperature > 0.f)
+    hipLaunchKernelGGL(gumbel_argmax_kernel, dim3(g), dim3(256), 0, st, logits, V,
+                       1.f / temperature, (uint32_t)(seed & 0xffffffffull), (uint32_t)(seed >> 32),
+                       hist_len, (const unsigned int*)nullptr, (const SampleParams*)nullptr, slot,
+                       off);
+  else
+    hipLaunchKernelGGL(argmax_kernel, dim3(g), dim3(256), 0, st, logits, V, slot, off);
   return (int)hipGetLastError();
 }
 

@@ -98,6 +98,11 @@ PRESETS: dict[str, dict] = {
                  num_attention_heads=4, num_key_value_heads=1, rms_norm_eps=1e-5,
                  rope_theta=500000.0, bos_token_id=1, eos_token_id=2,
                  max_position_embeddings=1024),
+    # tiny with 2 KV heads: tensor-parallel tests (TP degree must divide the KV heads)
+    "tiny-kv2": dict(hidden_size=256, intermediate_size=512, vocab_size=512, num_hidden_layers=2,
+                     num_attention_heads=4, num_key_value_heads=2, rms_norm_eps=1e-5,
+                     rope_theta=500000.0, bos_token_id=1, eos_token_id=2,
+                     max_position_embeddings=1024),
 }
 
 

@@ -7,6 +7,8 @@ the kernel library is missing, :func:`cake_amd.ops._lib.kernels` raises.
 """
 from __future__ import annotations
 
+import ctypes as C
+
 import torch
 
 from ._lib import check, kernels
@@ -304,6 +306,38 @@ def select_token(logits, slot, hist, hist_len, tok, pos, sampling=None, thr=None
         gumbel_argmax(logits, sampling.temperature, sampling.seed, hist_len, slot,
                       thr if restrict else None)
     finalize_token(slot, tok, hist, hist_len, pos)
+
+
+def select_shard(logits, off: int, hist, hist_len, last_n: int, penalty: float,
+                 temperature: float, seed: int, slot):
+    """Tensor-parallel vocab shard (global ids [off, off + len(logits))): repeat penalty
+    on the shard, then its argmax / Gumbel-max key into slot (all-reduce max next)."""
+    _req(logits, "logits", dtype=torch.float32)
+    _req(slot, "slot", dtype=torch.int64, numel=1)
+    check(kernels().cake_select_shard(_p(logits), logits.numel(), int(off), _p(hist),
+                                      _p(hist_len), int(last_n), float(penalty),
+                                      float(temperature or 0.0),
+                                      int(seed) & 0xFFFFFFFFFFFFFFFF, _p(slot), _stream()),
+          "select_shard")
+
+
+def ar_sum(partial, out, accumulate: bool, peers, inbox: int, seq, err, rank: int, world: int,
+           timeout_s: float):
+    """out (+)= all-reduce-sum of the f32 vector partial over the TP ranks (allreduce.hip).
+    peers: ctypes array of the peers' inbox pointers; inbox: this rank's inbox."""
+    _req(partial, "partial", dtype=torch.float32)
+    _req(out, "out", dtype=torch.float32, numel=partial.numel())
+    check(kernels().cake_ar_sum(_p(partial), _p(out), partial.numel(), int(bool(accumulate)),
+                                peers, C.c_void_p(inbox), _p(seq), _p(err), int(rank),
+                                int(world), float(timeout_s), _stream()), "ar_sum")
+
+
+def ar_max_key(slot, peers, inbox: int, seq, err, rank: int, world: int, timeout_s: float):
+    """slot (u64 argmax key) <- max over the TP ranks."""
+    _req(slot, "slot", dtype=torch.int64, numel=1)
+    check(kernels().cake_ar_max_key(_p(slot), peers, C.c_void_p(inbox), _p(seq), _p(err),
+                                    int(rank), int(world), float(timeout_s), _stream()),
+          "ar_max_key")
 
 
 def finalize_token(slot, tok, hist, hist_len, pos):

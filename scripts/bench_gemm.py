@@ -24,6 +24,9 @@ SHAPES = [  # name, M, N (output features), K, epi
     ("sdxl_qkv_4096tok", 8192, 1920, 640, "store"), ("sdxl_ff_in_4096tok", 8192, 5120, 640, "geglu"),
     ("sdxl_ff_out_4096tok", 8192, 640, 2560, "add16"), ("sdxl_qkv_1024tok", 2048, 3840, 1280, "store"),
     ("sdxl_ff_in_1024tok", 2048, 10240, 1280, "geglu"), ("sd15_qkv_4096tok", 8192, 960, 320, "store"),
+    ("sdxl_attn_out_1024tok", 2048, 1280, 1280, "add16"), ("sdxl_ff_out_1024tok", 2048, 1280, 5120, "add16"),
+    ("sdxl_attn_out_4096tok", 8192, 640, 640, "add16"), ("sdxl_q_1024tok", 2048, 1280, 1280, "store"),
+    ("sd15_ff_in_4096tok", 8192, 2560, 320, "geglu"), ("sd15_ff_out_4096tok", 8192, 320, 1280, "add16"),
     ("square_4096", 4096, 4096, 4096, "store"), ("square_8192", 8192, 8192, 8192, "store"),
 ]
 

@@ -30,7 +30,7 @@ def _json(r):
 def test_self_launch_matches_single(tmp_path):
     r1 = _run(["--dump-tokens", str(tmp_path / "a.json")])
     assert r1.returncode == 0, r1.stderr[-2000:]
-    r2 = _run(["--gpus", "3", "--dump-tokens", str(tmp_path / "b.json")])
+    r2 = _run(["--gpus", "3", "--parallel", "pp", "--dump-tokens", str(tmp_path / "b.json")])
     assert r2.returncode == 0, r2.stderr[-2000:]
     j = _json(r2)
     assert j["n_gpus"] == 3 and j["steps"] == 5 and j["warmup"] == 2 and j["value"] > 0
@@ -42,6 +42,18 @@ def test_self_launch_matches_single(tmp_path):
 
 
 def test_self_launch_fails_fast_when_a_rank_dies():
-    r = _run(["--gpus", "3"], env={"CAKE_BENCH_FAIL_RANK": "2"}, timeout=120)
+    r = _run(["--gpus", "3", "--parallel", "pp"], env={"CAKE_BENCH_FAIL_RANK": "2"}, timeout=120)
     assert r.returncode != 0
     assert "stopping the others" in r.stderr
+
+
+def test_self_launch_tensor_parallel(tmp_path):
+    """Default N > 1 mode: tensor-parallel ranks; same stream at TP 1 and TP 2 is covered
+    by tests/test_tp_cpu.py (here: the launch / JSON contract)."""
+    r = _run(["--gpus", "2", "--model", "tiny-kv2", "--dump-tokens", str(tmp_path / "t.json")])
+    assert r.returncode == 0, r.stderr[-2000:]
+    j = _json(r)
+    assert j["n_gpus"] == 2 and j["config"]["parallelism"].startswith("tp2")
+    assert j["allreduces_per_token"] == 2 * 2 + 1 and j["value"] > 0
+    toks = json.loads((tmp_path / "t.json").read_text())[0]
+    assert len(toks) == 9 + 1 + 2 + 5   # prompt + first token + warmup + timed steps
