@@ -79,6 +79,9 @@ def build_parser() -> argparse.ArgumentParser:
     a("--transport", choices=["tcp", "rccl", "loopback"], default="tcp",
       help="rccl: torchrun one rank per GPU, rank 0 master, rank i serves topology node i; "
            "loopback: every topology node served in-process (wire protocol over 127.0.0.1)")
+    a("--parallel", choices=["pp", "tp"], default="pp",
+      help="with --transport rccl: pp = the topology's layer sharding (reference), "
+           "tp = tensor parallel (every rank 1/N of every layer; topology layers ignored)")
     a("--max-seq-len", type=int, default=4096)
     a("--no-graph", action="store_true", help="disable hipGraph capture of the decode step")
     a("--trace", default=None, help="write a chrome-trace JSON of each text generation")

@@ -86,6 +86,8 @@ const Flag kFlags[] = {
     {"--sd-seed", "sd_seed", PyArg::kInt, nullptr, nullptr, false, ""},
     {"--transport", "transport", PyArg::kStr, "tcp", "tcp|rccl|loopback", false,
      "tcp, rccl (one rank per GPU) or loopback"},
+    {"--parallel", "parallel", PyArg::kStr, "pp", "pp|tp", false,
+     "rccl: pp = layer sharding (topology), tp = tensor parallel"},
     {"--max-seq-len", "max_seq_len", PyArg::kInt, "4096", nullptr, false, "KV cache length"},
     {"--no-graph", "no_graph", PyArg::kBool, "0", nullptr, true, "disable hipGraph decode"},
     {"--trace", "trace", PyArg::kStr, nullptr, nullptr, false, "chrome-trace JSON per generation"},

@@ -111,7 +111,144 @@ class PipelineLLM(TextGenerator):
         return out
 
 
+class TPLLM(TextGenerator):
+    """TextGenerator over the tensor-parallel engine (rank 0).  Every generation is a
+    broadcast command the other ranks execute in lock step (``_tp_follow``); all
+    ranks see the same tokens, so each detects EOS by itself."""
+    MODEL_NAME = "llama3"
+
+    def __init__(self, eng, tokenizer, eos_ids, sampling):
+        self.eng, self.tokenizer, self.eos_ids = eng, tokenizer, set(eos_ids)
+        self.sampling = sampling
+        self.history = History()
+        self.generated = 0
+        self.last_stats = None
+
+    @classmethod
+    def load(cls, ctx):
+        """Rank-0 generator of a running TP job (``ctx.engine``: its TPEngine)."""
+        from ..models.llama3.generator import load_tokenizer
+        eng = getattr(ctx, "engine", None)
+        if eng is None or eng.rank != 0:
+            raise RuntimeError("TPLLM.load needs ctx.engine: rank 0's TPEngine (see run_tp)")
+        tok, eos = load_tokenizer(ctx.model_path, eng.cfg.eos_token_id)
+        return cls(eng, tok, eos, ctx.sampling)
+
+    def add_message(self, message) -> None:
+        self.history.append(message)
+
+    def reset(self) -> None:
+        self.history.clear()
+        self.generated = 0
+
+    def generated_tokens(self) -> int:
+        return self.generated
+
+    def set_sampling(self, sampling) -> None:
+        if sampling.top_k or (sampling.top_p is not None and sampling.top_p < 1.0):
+            raise ValueError("tensor-parallel serving supports greedy / temperature sampling")
+        self.sampling = sampling
+
+    def next_token(self, index: int) -> Token:  # pragma: no cover - stream() drives it
+        raise NotImplementedError("use stream()")
+
+    def stream(self, max_tokens, on_token, stop_at_eos=True):
+        prompt = self.tokenizer.encode(self.history.encode_dialog_to_prompt(),
+                                       add_special_tokens=False).ids
+        s = self.sampling
+        cmd = {"op": "generate", "prompt": prompt, "max_tokens": int(max_tokens),
+               "eos": sorted(self.eos_ids) if stop_at_eos else [],
+               "temperature": 0.0 if s.greedy else float(s.temperature), "seed": int(s.seed)}
+        dist.broadcast_object_list([cmd], src=0)
+        out = []
+
+        def emit(tid):
+            self.generated += 1
+            t = Token(tid, self.tokenizer.decode([tid], skip_special_tokens=False),
+                      tid in self.eos_ids)
+            out.append(t)
+            on_token(t)
+        _tp_generate(self.eng, cmd, emit)
+        return out
+
+
+def _tp_generate(eng, cmd, emit=None) -> None:
+    """One generation on every rank (same command, same tokens)."""
+    temp, seed = float(cmd["temperature"]), int(cmd["seed"])
+    if (temp, seed) != (eng.temperature, eng.seed):
+        eng.temperature, eng.seed = temp, seed
+        eng.graph = None  # the selection is baked into the graph: recapture (all ranks)
+    n, eos = int(cmd["max_tokens"]), set(cmd["eos"])
+    if n <= 0:
+        return
+    tid = eng.prefill(cmd["prompt"])
+    eng.capture()
+    for i in range(n):
+        if i > 0:
+            tid = eng.step()
+        if emit is not None:
+            emit(tid)
+        if tid in eos:
+            break
+    eng.check()
+
+
+def _tp_follow(eng) -> None:
+    """Ranks >= 1 of a tensor-parallel job: execute rank 0's commands until "stop"."""
+    while True:
+        box = [None]
+        dist.broadcast_object_list(box, src=0)
+        cmd = box[0]
+        if cmd is None or cmd.get("op") == "stop":
+            return
+        _tp_generate(eng, cmd)
+
+
+def run_tp(ctx) -> None:
+    """``--transport rccl --parallel tp``: every rank loads 1/N of every layer (the
+    topology's layer placement does not apply); rank 0 runs the master / API."""
+    from ..models.llama3.config import LlamaConfig
+    from .tensor_parallel import AllReduce, TPEngine, check_tp, load_shards
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if ctx.device.type == "cuda":
+        local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(local)
+        ctx.device = torch.device("cuda", local)
+        init_process_group("nccl", rank, world, ctx.device)
+    else:
+        init_process_group("gloo", rank, world)
+    try:
+        cfg = LlamaConfig.from_path(ctx.model_path)
+        check_tp(cfg, world)
+        blocks, head = load_shards(ctx.model_path, cfg, rank, world, ctx.device, ctx.dtype)
+        comm = AllReduce(rank, world, ctx.device, cfg.hidden_size)
+        s = ctx.sampling
+        eng = TPEngine(cfg, blocks, head, rank, world, ctx.device, ctx.dtype, ctx.max_seq_len,
+                       comm, repeat_penalty=s.repeat_penalty, repeat_last_n=s.repeat_last_n,
+                       temperature=0.0 if s.greedy else s.temperature, seed=s.seed,
+                       use_graph=not ctx.no_graph)
+        log.info("rank %d/%d: tensor-parallel shard, all-reduce %s", rank, world, comm.mode)
+        if rank == 0:
+            from ..master import Master
+            ctx.engine = eng
+            llm = TPLLM.load(ctx)
+            llm.set_sampling(s)
+            try:
+                Master(ctx, llm=llm).run()
+            finally:
+                dist.broadcast_object_list([{"op": "stop"}], src=0)
+        else:
+            _tp_follow(eng)
+        comm.close()
+    finally:
+        dist.destroy_process_group()
+
+
 def run_rccl(ctx) -> None:
+    if getattr(ctx.args, "parallel", "pp") == "tp":
+        run_tp(ctx)
+        return
     from ..models.llama3.config import LlamaConfig
     from ..models.llama3.factory import load_stack
     from ..models.llama3.generator import load_tokenizer

@@ -126,7 +126,7 @@ def load_shards(model_path: str, cfg: LlamaConfig, rank: int, world: int, device
     ck = ShardedCheckpoint(model_path)
     blocks = {}
     for li in range(cfg.num_hidden_layers):
-        full = BlockWeights.load(ck.get, f"model.layers.{li}.", cfg, "cpu", dtype)
+        full = BlockWeights.load(ck.get, f"model.layers.{li}", cfg, "cpu", dtype)
         blocks[li] = shard_block(full, cfg, rank, world, device, dtype)
     hw = HeadWeights.load(ck.get, cfg, "cpu", dtype)
     return blocks, shard_head(hw.embed, hw.norm, hw.lm_head, rank, world, device, dtype)

@@ -42,3 +42,21 @@ def test_rccl_roles_match_local(tmp_path):
     assert rec["hops_per_token"] == 3
     assert [r["rank"] for r in rec["rank_hbm"]] == [0, 1, 2]
     assert [r["layers"] for r in rec["rank_hbm"]] == [1, 2, 1]
+
+
+def test_rccl_tensor_parallel_roles_match_local(tmp_path):
+    """--transport rccl --parallel tp: 2 ranks, each 1/2 of every layer (real checkpoint
+    slices), rank 0 the master; the CLI text equals the all-local generation."""
+    d = tmp_path / "m"
+    write_checkpoint(d, tiny_config(num_hidden_layers=3, num_key_value_heads=2), torch.float32)
+    (tmp_path / "empty.yml").write_text("{}\n")
+    common = ["--model", str(d), "--cpu", "-n", "10", "--temperature", "0", "--prompt", "hi there",
+              "--topology", str(tmp_path / "empty.yml")]
+    local = _run([sys.executable, "-m", "cake_amd.cli", *common])
+    assert local.returncode == 0, local.stderr[-2000:]
+    tp = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+               "--master-addr=127.0.0.1", "--master-port=29573", "-m", "cake_amd.cli",
+               "--transport", "rccl", "--parallel", "tp", *common])
+    assert tp.returncode == 0, tp.stderr[-3000:]
+    text = local.stdout.strip()
+    assert text and text in tp.stdout
