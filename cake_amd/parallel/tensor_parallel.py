@@ -363,7 +363,8 @@ class TPEngine:
         self.penalty, self.last_n = float(repeat_penalty), int(repeat_last_n)
         self.temperature, self.seed = float(temperature or 0.0), int(seed)
         self.hip = self.device.type == "cuda" and dtype in (torch.float16, torch.bfloat16)
-        self.use_graph = use_graph and self.hip
+        # the torch.distributed fallback issues host collectives: eager launches only
+        self.use_graph = use_graph and self.hip and (world == 1 or comm.mode == "ipc")
         H, hd = cfg.hidden_size, cfg.head_dim
         self.nq = cfg.num_attention_heads // world
         self.nkv = cfg.num_key_value_heads // world

@@ -5,7 +5,7 @@ set -u
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-timeout -k 10 900 python -u -m pytest tests/test_tp_gpu.py tests/test_gemm_gpu.py tests/test_model_gpu.py tests/test_sampling_gpu.py -x -q --timeout 300 --timeout-method thread > gpurun_out/r2h_pytest.log 2>&1
+timeout -k 10 900 python -u -m pytest tests/test_tp_gpu.py tests/test_gemm_gpu.py tests/test_model_gpu.py tests/test_sampling_gpu.py -x -v --timeout 170 --timeout-method thread > gpurun_out/r2h_pytest.log 2>&1
 rc=$?; tail -4 gpurun_out/r2h_pytest.log
 if [[ $rc -ne 0 ]]; then exit $rc; fi
 timeout -k 10 300 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || exit $?

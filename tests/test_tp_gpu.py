@@ -83,12 +83,17 @@ def test_tp2_matches_single_gpu(cuda, mode):
     for p in ps:
         p.start()
     got = {}
-    for _ in range(2):
-        r, used, toks, us = q.get(timeout=240)
-        got[r] = (used, toks, us)
-    for p in ps:
-        p.join(timeout=60)
-        assert p.exitcode == 0
+    try:
+        for _ in range(2):
+            r, used, toks, us = q.get(timeout=150)
+            got[r] = (used, toks, us)
+        for p in ps:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+    finally:
+        for p in ps:  # a failed rank leaves its peer blocked in a collective
+            if p.is_alive():
+                p.kill()
     assert got[0][1] == got[1][1]          # the ranks agree token for token
     assert got[0][0] == mode, got[0][0]    # the IPC self-test passed (no silent fallback)
     toks = got[0][1]
