@@ -250,7 +250,8 @@ def main(argv=None) -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return self_launch(a, argv)
-    if world > 1 or a.gpus > 1:
+    # under torchrun (WORLD_SIZE set) the distributed path runs even at N = 1
+    if world > 1 or a.gpus > 1 or "WORLD_SIZE" in os.environ:
         if a.parallel == "tp":
             from cake_amd.parallel.tp_bench import bench_tp
             bench_tp(a, _emit)

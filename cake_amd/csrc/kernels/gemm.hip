@@ -136,7 +136,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(GemmArgs g) {
   constexpr int STG_LD = WTN + 4;              // epilogue staging row stride (floats)
   constexpr int STG = 16 * STG_LD * 4;         // bytes per wave
   constexpr int LDS_BYTES = (NS * BUF > NWAVE * STG) ? NS * BUF : NWAVE * STG;
-  static_assert(NS == 2 || NS == 3, "LDS stages");
+  static_assert(NS == 2 || NS == 3 || (IL && NS == 4), "LDS stages");
   __shared__ __attribute__((aligned(16))) uint8_t smem[LDS_BYTES];
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -234,9 +234,9 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(GemmArgs g) {
     // into the consumed buffer) so the counted waits are the same every step.
     constexpr int NM = FM * FN, NR = FM + FN, NL = IPW + NR;
     if (nk > 0) {
-      stage(0, 0);
-      if (NS == 3) stage(1, 1);
-      __builtin_amdgcn_s_waitcnt(vm_wait(NS == 3 ? IPW : 0));
+#pragma unroll
+      for (int p = 0; p + 1 < NS; ++p) stage(p, p);
+      __builtin_amdgcn_s_waitcnt(vm_wait((NS - 2) * IPW));
       asm volatile("s_barrier" ::: "memory");
       stage(NS - 1, NS - 1);
 #pragma unroll
@@ -532,7 +532,9 @@ using namespace cake;
   X(6, 256, 128, 4, 2, 3, 6) \
   X(7, 128, 128, 2, 2, 3, 6) \
   X(8, 128, 128, 2, 2, 2, 2) \
-  X(11, 256, 256, 2, 4, 2, 0)
+  X(11, 256, 256, 2, 4, 2, 0) \
+  X(12, 64, 128, 1, 4, 3, 6) \
+  X(13, 64, 64, 2, 2, 4, 6)
 
 static inline void cfg_dims(int cfg, int& bm, int& bn) {
 #define X(id, BM, BN, WM, WN, NS, PR) if (cfg == id) { bm = BM; bn = BN; return; }

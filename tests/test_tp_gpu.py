@@ -104,3 +104,25 @@ def test_tp2_matches_single_gpu(cuda, mode):
     assert toks[:n] == ref[:n], (toks, ref)
     if mode == "ipc":
         assert got[0][2] is not None and got[0][2] > 0
+
+
+def test_bench_under_torchrun_uses_rccl(cuda, tmp_path):
+    """One rank under torchrun: the distributed bench path initialises the nccl (RCCL)
+    process group and runs its barrier / all-reduce (the 8-GPU scaling run's code path)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    env.pop("WORLD_SIZE", None)
+    for par in ("tp", "pp"):
+        r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                            "--nproc-per-node=1", "--master-addr=127.0.0.1",
+                            f"--master-port={_free_port()}", "bench.py", "--gpus", "1",
+                            "--model", "tiny-kv2", "--steps", "8", "--warmup", "2",
+                            "--parallel", par], cwd=root, capture_output=True, text=True,
+                           timeout=200, env=env)
+        assert r.returncode == 0, r.stderr[-3000:]
+        j = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+        assert j["n_gpus"] == 1 and j["value"] > 0
+        assert j["config"]["parallelism"].startswith(par + "1"), j["config"]
