@@ -101,7 +101,7 @@ def _emit(a, value, ms, p50, p99, n, extra):
                              "tiny": "tiny", "tiny-kv2": "tiny-kv2"}[a.model],
                    "global_batch": extra.get("streams", 1), "seq_len": a.prompt_len + a.warmup + a.steps,
                    "prompt_len": a.prompt_len,
-                   "parallelism": "single" if n == 1 else
+                   "parallelism": "single" if "parallel" not in extra else
                    (f"tp{n} (tensor-parallel, {extra.get('allreduce')} all-reduce)"
                     if extra.get("parallel") == "tp" else
                     f"pp{n} (layer-sharded, {extra.get('hop', 'dist')} hops, "

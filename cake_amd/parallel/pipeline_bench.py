@@ -111,7 +111,8 @@ def bench_pipeline(a, emit) -> None:
         per_tok = [x / k for x in step_ms] if step_ms else [dt * 1e3 / a.steps]
         emit(a, streams * a.steps / dt, dt * 1e3 / a.steps, _pct(per_tok, 50), _pct(per_tok, 99),
              world,
-             {"streams": streams, "per_stream_tokens_per_sec": round(a.steps / dt, 3),
+             {"parallel": "pp", "streams": streams,
+              "per_stream_tokens_per_sec": round(a.steps / dt, 3),
               "hop": eng.hop + ("-bf16" if eng.hop == "ipc" and eng.hop_bf16 else ""),
               "hop_us": None if hop_us is None else round(hop_us, 2),
               "hops_per_token": sum(1 for k in range(1, len(eng.runs) + 2) if eng._recv_point(k)),
