@@ -70,6 +70,37 @@ def _workspace(dev, numel: int) -> torch.Tensor:
     return w
 
 
+def _load_tuned() -> list:
+    """Measured best (cfg, split-K) per model shape (gemm_tuned.json, written by
+    scripts/gemm_tune_table.py from a bench_gemm.py --sweep on an MI355X)."""
+    import json
+    import os
+    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_tuned.json")
+    try:
+        with open(p) as f:
+            return [e for e in json.load(f)["entries"] if e["cfg"] in CFG_TILES]
+    except (OSError, ValueError, KeyError):
+        return []
+
+
+_TUNED = _load_tuned()
+
+
+def _tuned(M: int, Nv: int, K: int, epi: str):
+    """Exact measured shape, else the same (Nv, K, epilogue) measured at an M within 2x
+    (its tile config, without split-K)."""
+    near = None
+    for e in _TUNED:
+        if e["Nv"] != Nv or e["K"] != K or e["epi"] != epi:
+            continue
+        if e["M"] == M:
+            return e["cfg"], e["splits"]
+        r = max(M, e["M"]) / min(M, e["M"])
+        if r <= 2 and (near is None or r < near[0]):
+            near = (r, e["cfg"])
+    return (near[1], 1) if near else None
+
+
 def set_plan(M: int, N: int, K: int, epi: str, cfg: int, splits: int) -> None:
     """Pin the tile configuration / split-K of one shape (measured tuning)."""
     _plans[(M, N, K, epi)] = (cfg, splits)
@@ -79,6 +110,10 @@ def plan(M: int, Nv: int, K: int, epi: str = "store") -> tuple[int, int]:
     """(cfg, splits) for an M x Nv x K problem (Nv = weight rows read)."""
     p = _plans.get((M, Nv, K, epi))
     if p is not None:
+        return p
+    p = _tuned(M, Nv, K, epi)
+    if p is not None:
+        _plans[(M, Nv, K, epi)] = p
         return p
     best = None
     ksteps = -(-K // 64)
