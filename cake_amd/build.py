@@ -57,13 +57,20 @@ def _run(cmd: list[str]) -> None:
         raise RuntimeError(f"command failed ({r.returncode}): {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
 
 
+# per-file hipcc flags: the GEMM's compile-time-unrolled interleaved schedule needs its
+# lambdas fully inlined (below the default threshold the 128x128-per-wave tile keeps
+# closures in scratch memory)
+HIP_EXTRA = {"gemm": ["-mllvm", "-inline-threshold=100000"]}
+
+
 def _compile_hip(src: Path, force: bool) -> Path:
     out = BUILD / "kernels" / (src.stem + ".o")
     out.parent.mkdir(parents=True, exist_ok=True)
     headers = sorted((CSRC / "kernels").glob("*.h"))
     if force or _newer(src, headers, out):
         _run([HIPCC, "-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC",
-              "-Wno-unused-result", "-munsafe-fp-atomics", "-c", str(src), "-o", str(out)])
+              "-Wno-unused-result", "-munsafe-fp-atomics", *HIP_EXTRA.get(src.stem, []),
+              "-c", str(src), "-o", str(out)])
     return out
 
 

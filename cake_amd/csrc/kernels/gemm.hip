@@ -37,6 +37,8 @@
 //     halves, so gate and up of one feature land in the same lane.
 #include "common.h"
 
+#include <type_traits>
+
 namespace cake {
 
 constexpr int kGBK = 64;  // k per step (128-byte rows)
@@ -111,6 +113,27 @@ __device__ __forceinline__ void azero(cf32x4& acc) {
   asm volatile("s_nop 1\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %1, 0" : "=a"(acc) : "v"(z));
 }
 
+// Compile-time loop: f(std::integral_constant<int, I>) for I in [B, E) — the interleaved
+// schedule's indices must be constants however long the sweep (a #pragma unroll of a
+// 64 x 32 nest can stay rolled, sending the accumulators to scratch).
+template <int B, class F, int... Is>
+__device__ __forceinline__ void static_for_impl(F& f, std::integer_sequence<int, Is...>) {
+  (f(std::integral_constant<int, B + Is>{}), ...);  // flat expansion, no recursion
+}
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) static_for_impl<B>(f, std::make_integer_sequence<int, E - B>{});
+}
+
+// same with a compile-time byte offset in the instruction (one base VGPR per tile)
+template <int OFF>
+__device__ __forceinline__ uint4 ds_read16_off(uint32_t base) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset field is 16-bit");
+  uint4 v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(base), "i"(OFF));
+  return v;
+}
+
 __device__ __forceinline__ uint4 ds_read16(uint32_t addr) {
   uint4 v;
   asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr));
@@ -163,29 +186,39 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(GemmArgs g) {
   const int nk = (ke - kb + kGBK - 1) / kGBK;
 
   // ---- DMA sources of this lane (fixed rows; k advances) -----------------
-  const uint16_t* src[IPW];
-  bool is_a[IPW];
-  int chunk[IPW];
-#pragma unroll
-  for (int i = 0; i < IPW; ++i) {
-    const int t = (wave * IPW + i) * 8 + (lane >> 3);  // tile row (A rows, then B rows)
-    const int slot = lane & 7;
-    chunk[i] = slot ^ ((t >> 1) & 7);
+  // Precomputed per instruction, or (LAZY: many DMA instructions per wave, where the
+  // pointer array would crowd out the accumulators) recomputed at each issue.
+  constexpr bool LAZY = IL && IPW > 8;
+  constexpr int NSRC = LAZY ? 1 : IPW;
+  const uint16_t* src[NSRC];
+  int chunk[NSRC];
+  auto row_src = [&](int i, int& ch) __attribute__((always_inline)) -> const uint16_t* {
+    int t = (wave * IPW + i) * 8 + (lane >> 3);  // tile row (A rows, then B rows)
+    if constexpr (LAZY) asm volatile("" : "+v"(t));  // recompute per issue: no hoisting
+    ch = (lane & 7) ^ ((t >> 1) & 7);
     if (t < BM) {
       const int m = m0 + t;
-      src[i] = m < g.M ? g.a + (size_t)m * g.lda : nullptr;
-      is_a[i] = true;
-    } else {
-      const int v = n0 + (t - BM);
-      src[i] = v < g.Nv ? g.b + (size_t)wrow(g, v) * g.ldb : nullptr;
-      is_a[i] = false;
+      return m < g.M ? g.a + (size_t)m * g.lda : nullptr;
     }
+    const int v = n0 + (t - BM);
+    return v < g.Nv ? g.b + (size_t)wrow(g, v) * g.ldb : nullptr;
+  };
+  if constexpr (!LAZY) {
+#pragma unroll
+    for (int i = 0; i < IPW; ++i) src[i] = row_src(i, chunk[i]);
   }
-  (void)is_a;
   const uint32_t lds0 = lds_off(smem);
-  auto stage_one = [&](int step, int buf, int i) {
-    const int k = kb + step * kGBK + chunk[i] * 8;
-    const uint16_t* p = (src[i] != nullptr && k < ke) ? src[i] + k : g.zeros;
+  auto stage_one = [&](int step, int buf, int i) __attribute__((always_inline)) {
+    const uint16_t* s0;
+    int ch;
+    if constexpr (LAZY) {
+      s0 = row_src(i, ch);
+    } else {
+      s0 = src[i];
+      ch = chunk[i];
+    }
+    const int k = kb + step * kGBK + ch * 8;
+    const uint16_t* p = (s0 != nullptr && k < ke) ? s0 + k : g.zeros;
     glds16(p, smem + buf * BUF + (wave * IPW + i) * 1024);
   };
   auto stage = [&](int step, int buf) {
@@ -249,37 +282,38 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(GemmArgs g) {
     int buf = 0;
     for (int t = 0; t < nk; ++t) {
       const uint32_t ab = a_base + buf * BUF, bb = b_base + buf * BUF;
-#pragma unroll
-      for (int m = 0; m < NM; ++m) {
+      // load r goes after MFMA floor(r * NM / NR)
+      static_for<0, NM>([&](auto mi) __attribute__((always_inline)) {
+        constexpr int m = decltype(mi)::value;
         amfma_v<DT>(acc[m / FN][m % FN], af0[m / FN], bf0[m % FN]);
-#pragma unroll
-        for (int r = 0; r < NR; ++r) {
-          if ((r * NM) / NR != m) continue;
-          if (r < FM) af1[r] = ds_read16(ab + r * 16 * 128 + off1);
-          else bf1[r - FM] = ds_read16(bb + (r - FM) * 16 * 128 + off1);
-        }
-      }
+        static_for<(m * NR + NM - 1) / NM, ((m + 1) * NR + NM - 1) / NM>([&](auto ri)
+                                                                      __attribute__((always_inline)) {
+          constexpr int r = decltype(ri)::value;
+          if constexpr (r < FM) af1[r] = ds_read16_off<r * 16 * 128>(ab + off1);
+          else bf1[r - FM] = ds_read16_off<(r - FM) * 16 * 128>(bb + off1);
+        });
+      });
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
       const int nbuf = buf + 1 == NS ? 0 : buf + 1;
       __builtin_amdgcn_s_waitcnt(vm_wait((NS - 2) * IPW));  // DMA of step t+1 landed
       asm volatile("s_barrier" ::: "memory");
       const uint32_t na = a_base + nbuf * BUF, nb = b_base + nbuf * BUF;
-#pragma unroll
-      for (int m = 0; m < NM; ++m) {
+      static_for<0, NM>([&](auto mi) __attribute__((always_inline)) {
+        constexpr int m = decltype(mi)::value;
         amfma_v<DT>(acc[m / FN][m % FN], af1[m / FN], bf1[m % FN]);
-#pragma unroll
-        for (int l = 0; l < NL; ++l) {
-          if ((l * NM) / NL != m) continue;
-          if (l < IPW) {
+        static_for<(m * NL + NM - 1) / NM, ((m + 1) * NL + NM - 1) / NM>([&](auto li)
+                                                                      __attribute__((always_inline)) {
+          constexpr int l = decltype(li)::value;
+          if constexpr (l < IPW) {
             stage_one(t + NS, buf, l);
           } else {
-            const int r = l - IPW;
-            if (r < FM) af0[r] = ds_read16(na + r * 16 * 128 + off0);
-            else bf0[r - FM] = ds_read16(nb + (r - FM) * 16 * 128 + off0);
+            constexpr int r = l - IPW;
+            if constexpr (r < FM) af0[r] = ds_read16_off<r * 16 * 128>(na + off0);
+            else bf0[r - FM] = ds_read16_off<(r - FM) * 16 * 128>(nb + off0);
           }
-        }
-      }
+        });
+      });
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
       buf = nbuf;
@@ -534,7 +568,8 @@ using namespace cake;
   X(8, 128, 128, 2, 2, 2, 2) \
   X(11, 256, 256, 2, 4, 2, 0) \
   X(12, 64, 128, 1, 4, 3, 6) \
-  X(13, 64, 64, 2, 2, 4, 6)
+  X(13, 64, 64, 2, 2, 4, 6) \
+  X(14, 256, 256, 2, 2, 2, 6)
 
 static inline void cfg_dims(int cfg, int& bm, int& bn) {
 #define X(id, BM, BN, WM, WN, NS, PR) if (cfg == id) { bm = BM; bn = BN; return; }
