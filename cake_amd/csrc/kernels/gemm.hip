@@ -555,7 +555,8 @@ using namespace cake;
 // accumulators +10-20 % on the 4-wave tiles, the interleaved schedule a further
 // +5-13 % on every tile (8-wave 256x256: 1144 -> 1286 TFLOP/s at 8192^3); 8 and 11
 // are the non-interleaved forms kept for A/B; a 4-wave 256x256 tile (128x128
-// per wave) and s_setprio measured slower / neutral and were dropped.
+// per wave; with or without the interleaved schedule: 0.5x of tile 5) and s_setprio
+// measured slower / neutral and were dropped.
 #define CAKE_GEMM_CFGS(X)    \
   X(0, 128, 128, 2, 2, 2, 6) \
   X(1, 64, 128, 1, 4, 2, 6)  \
@@ -568,8 +569,7 @@ using namespace cake;
   X(8, 128, 128, 2, 2, 2, 2) \
   X(11, 256, 256, 2, 4, 2, 0) \
   X(12, 64, 128, 1, 4, 3, 6) \
-  X(13, 64, 64, 2, 2, 4, 6) \
-  X(14, 256, 256, 2, 2, 2, 6)
+  X(13, 64, 64, 2, 2, 4, 6)
 
 static inline void cfg_dims(int cfg, int& bm, int& bn) {
 #define X(id, BM, BN, WM, WN, NS, PR) if (cfg == id) { bm = BM; bn = BN; return; }
