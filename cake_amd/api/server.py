@@ -87,6 +87,9 @@ def create_app(master):
         if default is not None and hasattr(master.llm, "set_sampling"):
             try:
                 sampling = request_sampling(body, default)
+                check = getattr(master.llm, "check_sampling", None)
+                if check is not None:
+                    check(sampling)  # a generator may support only part of the space
             except (TypeError, ValueError) as e:
                 return JSONResponse({"error": f"bad request: {e}"}, status_code=400)
         model_name = master.llm.MODEL_NAME

@@ -144,9 +144,14 @@ class TPLLM(TextGenerator):
     def generated_tokens(self) -> int:
         return self.generated
 
-    def set_sampling(self, sampling) -> None:
+    @staticmethod
+    def check_sampling(sampling) -> None:
         if sampling.top_k or (sampling.top_p is not None and sampling.top_p < 1.0):
-            raise ValueError("tensor-parallel serving supports greedy / temperature sampling")
+            raise ValueError("tensor-parallel serving supports greedy / temperature sampling "
+                             "(top_k / top_p need the whole vocabulary on one rank)")
+
+    def set_sampling(self, sampling) -> None:
+        self.check_sampling(sampling)
         self.sampling = sampling
 
     def next_token(self, index: int) -> Token:  # pragma: no cover - stream() drives it

@@ -19,7 +19,8 @@ def _bench(tmp_path, n, streams, name, hop="dist", hop_dtype="f32", k=1):
     args = ["bench.py", "--model", "tiny", "--steps", "12", "--warmup", "3", "--prompt-len", "9",
             "--max-seq", "256", "--dump-tokens", str(out)]
     if n > 1:
-        args += ["--gpus", str(n), "--dist-backend", "gloo", "--streams", str(streams),
+        args += ["--gpus", str(n), "--parallel", "pp", "--dist-backend", "gloo",
+                 "--streams", str(streams),
                  "--hop", hop, "--hop-dtype", hop_dtype, "--steps-per-graph", str(k),
                  "--launch-timeout", "200"]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", CAKE_HOP_TIMEOUT="30")
