@@ -4,7 +4,7 @@ set -u
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 170 --timeout-method thread > gpurun_out/r2l_pytest.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -q -m gpu --timeout 170 --timeout-method thread > gpurun_out/r2l_pytest.log 2>&1
 rc=$?; tail -3 gpurun_out/r2l_pytest.log
 if [[ $rc -ne 0 && $rc -ne 1 ]]; then exit $rc; fi
 timeout -k 10 300 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || exit $?
