@@ -26,11 +26,12 @@
 // stream), and MAX of one 64-bit argmax key (vocab-sharded lm_head: the key is
 // (ordered logit << 32 | ~global index), so the max is the global argmax with
 // the smallest index on ties, exactly as the single-GPU argmax_kernel).
-#include "ar_push.h"
+#include "common.h"
 
 namespace cake {
 
 constexpr int kArThreads = 256;
+constexpr int kArMaxRanks = 8;
 
 struct ArArgs {
   unsigned long long* peer[kArMaxRanks];  // peers' inboxes (own slot unused)
@@ -69,15 +70,14 @@ __device__ __forceinline__ void ar_finish(const ArArgs& a, unsigned int tag) {
   }
 }
 
-// out[i] (+)= sum over ranks of partial[i], i < n.  PUSHED: the producing kernel
-// already stored this rank's words into the peers' inboxes (gemv.hip push epilogue).
-template <bool ACC, bool PUSHED>
+// out[i] (+)= sum over ranks of partial[i], i < n
+template <bool ACC>
 __global__ __launch_bounds__(kArThreads) void ar_sum_kernel(ArArgs a, const float* __restrict__ partial,
                                                             float* __restrict__ out) {
   const unsigned int tag = __hip_atomic_load(a.seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) + 1u;
   const size_t bank = (size_t)(tag & 1u) * a.world * a.n;
   const int i0 = blockIdx.x * kArThreads + threadIdx.x, stride = gridDim.x * kArThreads;
-  for (int i = i0; i < a.n && !PUSHED; i += stride) {
+  for (int i = i0; i < a.n; i += stride) {
     const unsigned long long g =
         (unsigned long long)__float_as_uint(partial[i]) | ((unsigned long long)tag << 32);
     for (int r = 0; r < a.world; ++r)
@@ -166,22 +166,18 @@ static int ar_args(ArArgs& a, void* const* peers, const void* inbox, unsigned in
 CAKE_API long long cake_ar_inbox_words(int world, int n) { return 2ll * world * n; }
 
 // out (+)= sum over ranks of partial (f32[n]); partial and out may alias when !accumulate.
-// pushed: the peers' inboxes already hold this rank's words (cake_gemv_x16_push).
-CAKE_API int cake_ar_sum(const float* partial, float* out, int n, int accumulate, int pushed,
-                         void* const* peers, const void* inbox, unsigned int* seq, int* err,
-                         int rank, int world, double timeout_s, hipStream_t st) {
+CAKE_API int cake_ar_sum(const float* partial, float* out, int n, int accumulate, void* const* peers,
+                         const void* inbox, unsigned int* seq, int* err, int rank, int world,
+                         double timeout_s, hipStream_t st) {
   ArArgs a;
   const int rc = ar_args(a, peers, inbox, seq, err, rank, world, n, timeout_s);
   if (rc) return rc;
   int g = (n + kArThreads - 1) / kArThreads;
   if (g > 64) g = 64;
-#define CAKE_AR_SUM(ACC, PU)                                                                    \
-  hipLaunchKernelGGL((ar_sum_kernel<ACC, PU>), dim3(g), dim3(kArThreads), 0, st, a, partial, out)
-  if (accumulate && pushed) CAKE_AR_SUM(true, true);
-  else if (accumulate) CAKE_AR_SUM(true, false);
-  else if (pushed) CAKE_AR_SUM(false, true);
-  else CAKE_AR_SUM(false, false);
-#undef CAKE_AR_SUM
+  if (accumulate)
+    hipLaunchKernelGGL((ar_sum_kernel<true>), dim3(g), dim3(kArThreads), 0, st, a, partial, out);
+  else
+    hipLaunchKernelGGL((ar_sum_kernel<false>), dim3(g), dim3(kArThreads), 0, st, a, partial, out);
   return (int)hipGetLastError();
 }
 

@@ -23,7 +23,7 @@
 //     once per workgroup (4 waves), so no separate norm launch exists.
 //   * The token position is read from device memory so the launches replay
 //     unchanged inside a hipGraph.
-#include "ar_push.h"
+#include "common.h"
 
 namespace cake {
 
@@ -280,15 +280,10 @@ __global__ __launch_bounds__(kGemvThreads) void swiglu_kernel(
 // out (+)= W x   with 16-bit x: o_proj / down_proj (accumulate into the f32
 // residual stream) — or plain f32 output.
 // ---------------------------------------------------------------------------
-// PUSH (tensor-parallel o_proj / down_proj partial sums): the epilogue also stores
-// each output word into every peer's all-reduce inbox (ar_push.h), so the following
-// all-reduce kernel only polls and sums (cake_ar_sum pushed = 1).
-template <int DT, int U, int PFC, bool ACCUM, bool PUSH = false>
+template <int DT, int U, int PFC, bool ACCUM>
 __global__ __launch_bounds__(kGemvThreads) void gemv_x16_kernel(
     const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, int K, int N,
-    float* __restrict__ out, ArPush push = ArPush{}) {
-  unsigned int tag = 0;
-  if constexpr (PUSH) tag = ar_next_tag(push.seq);
+    float* __restrict__ out) {
   extern __shared__ float smem[];
   uint16_t* xs = reinterpret_cast<uint16_t*>(smem);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -310,10 +305,6 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_x16_kernel(
     const int ra = 2 * p, rb = 2 * p + 1;
     if (ACCUM) out[ra] += da; else out[ra] = da;
     if (rb < N) { if (ACCUM) out[rb] += db; else out[rb] = db; }
-    if constexpr (PUSH) {
-      ar_push_word(push, tag, ra, da);
-      if (rb < N) ar_push_word(push, tag, rb, db);
-    }
   };
   run_pairs<DT, false, U, PFC>(map, epi, xs, K, npairs, p0, gridDim.x * kGemvWaves, pre);
 }
@@ -441,32 +432,6 @@ CAKE_API int cake_gemv_x16(int dt, const void* x, const void* w, int K, int N, f
                                                         (const uint16_t*)x, (const uint16_t*)w, K,
                                                         N, out)));
   }
-  return (int)hipGetLastError();
-}
-
-// out = w x (f32 partial, tensor-parallel row-parallel layer) and the same words pushed
-// into every peer's inbox of the all-reduce channel (peers / seq: cake_ar_sum's).
-CAKE_API int cake_gemv_x16_push(int dt, const void* x, const void* w, int K, int N, float* out,
-                                void* const* peers, const unsigned int* seq, int rank, int world,
-                                hipStream_t st) {
-  if (K % 8 || world < 1 || world > kArMaxRanks || rank < 0 || rank >= world || !seq)
-    return (int)hipErrorInvalidValue;
-  ArPush p{};
-  for (int r = 0; r < kArMaxRanks; ++r) {
-    p.peer[r] = (r < world && r != rank) ? (unsigned long long*)peers[r] : nullptr;
-    if (r < world && r != rank && p.peer[r] == nullptr) return (int)hipErrorInvalidValue;
-  }
-  p.seq = seq;
-  p.rank = rank;
-  p.world = world;
-  p.n = N;
-  const size_t lds = (size_t)K * 2;
-  const GemvTune t = g_tune[kX16];
-  const int g = grid_for((N + 1) / 2, t.MB);
-  DISPATCH_DT(dt, DISPATCH_TUNE(t, K, hipLaunchKernelGGL((gemv_x16_kernel<DT, U, PF, false, true>),
-                                                      dim3(g), dim3(kGemvThreads), lds, st,
-                                                      (const uint16_t*)x, (const uint16_t*)w, K,
-                                                      N, out, p)));
   return (int)hipGetLastError();
 }
 

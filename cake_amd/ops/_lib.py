@@ -54,8 +54,7 @@ _SIGS = {
     "cake_gumbel_argmax": [P, I, F, C.c_ulonglong, P, P, P, P],
     "cake_select_dev": [P, I, P, P, P, P, P],
     "cake_select_shard": [P, I, I, P, P, I, F, F, C.c_ulonglong, P, P],
-    "cake_ar_sum": [P, P, I, I, I, P, P, P, P, I, I, C.c_double, P],
-    "cake_gemv_x16_push": [I, P, P, I, I, P, P, P, I, I, P],
+    "cake_ar_sum": [P, P, I, I, P, P, P, P, I, I, C.c_double, P],
     "cake_ar_max_key": [P, P, P, P, P, I, I, C.c_double, P],
 }
 

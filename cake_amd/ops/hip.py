@@ -322,26 +322,14 @@ def select_shard(logits, off: int, hist, hist_len, last_n: int, penalty: float,
 
 
 def ar_sum(partial, out, accumulate: bool, peers, inbox: int, seq, err, rank: int, world: int,
-           timeout_s: float, pushed: bool = False):
+           timeout_s: float):
     """out (+)= all-reduce-sum of the f32 vector partial over the TP ranks (allreduce.hip).
-    peers: ctypes array of the peers' inbox pointers; inbox: this rank's inbox; pushed:
-    the producer already stored this rank's words in the peers' inboxes (gemv_push)."""
+    peers: ctypes array of the peers' inbox pointers; inbox: this rank's inbox."""
     _req(partial, "partial", dtype=torch.float32)
     _req(out, "out", dtype=torch.float32, numel=partial.numel())
     check(kernels().cake_ar_sum(_p(partial), _p(out), partial.numel(), int(bool(accumulate)),
-                                int(bool(pushed)), peers, C.c_void_p(inbox), _p(seq), _p(err),
-                                int(rank), int(world), float(timeout_s), _stream()), "ar_sum")
-
-
-def gemv_push(x, w, out, peers, seq, rank: int, world: int):
-    """out (f32) = w @ x, each word also pushed into every peer's all-reduce inbox (the
-    tensor-parallel o_proj / down_proj partial; follow with ar_sum(pushed=True))."""
-    N, K = w.shape
-    _req(w, "w")
-    _req(x, "x", dtype=w.dtype, numel=K)
-    _req(out, "out", dtype=torch.float32, numel=N)
-    check(kernels().cake_gemv_x16_push(_dt(w), _p(x), _p(w), K, N, _p(out), peers, _p(seq),
-                                       int(rank), int(world), _stream()), "gemv_x16_push")
+                                peers, C.c_void_p(inbox), _p(seq), _p(err), int(rank),
+                                int(world), float(timeout_s), _stream()), "ar_sum")
 
 
 def ar_max_key(slot, peers, inbox: int, seq, err, rank: int, world: int, timeout_s: float):

@@ -25,12 +25,15 @@ def main():
     ap.add_argument("--denoise", action="store_true",
                     help="whole diffusion loop through SDUnit.denoise: device timestep, UNet, "
                          "CFG + scheduler update in one graph replay per step")
+    ap.add_argument("--vae", action="store_true", help="time one VAE decode (batch 1) instead")
     ap.add_argument("--no-kv-cache", dest="kv_cache", action="store_false",
                     help="recompute the cross-attention k/v of the text context every step")
     a = ap.parse_args()
     dt = torch.float16 if a.dtype == "f16" else torch.bfloat16
     cfg = get_config(a.version)
     dev = torch.device("cuda:0")
+    if a.vae:
+        return bench_vae(a, cfg, dev, dt)
     w = random_component("unet", cfg, dev, dt)
     unet = UNet2DConditionModel(cfg.unet)
     B = 2  # classifier-free guidance doubles the batch
@@ -62,6 +65,27 @@ def main():
                       "value": round(dt_step, 4), "unit": "s/step", "graph": a.graph,
                       "ctx_kv_cache": a.kv_cache,
                       "nhwc": os.environ.get("CAKE_SD_NHWC", "1") != "0"}))
+
+
+def bench_vae(a, cfg, dev, dt):
+    """VAE decode of one latent (incl. the head-dim-512 mid-block attention)."""
+    from cake_amd.models.sd.vae import AutoencoderKL
+    w = random_component("vae", cfg, dev, dt)
+    vae = AutoencoderKL(cfg.vae)
+    z = torch.randn(1, 4, cfg.height // 8, cfg.width // 8, device=dev, dtype=dt)
+    with torch.no_grad():
+        for _ in range(2):
+            vae.decode(w, z)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        n = max(1, a.steps)
+        for _ in range(n):
+            vae.decode(w, z)
+        torch.cuda.synchronize()
+    dt_s = (time.perf_counter() - t0) / n
+    print(json.dumps({"metric": "sd_vae_decode_seconds", "version": a.version,
+                      "resolution": f"{cfg.width}x{cfg.height}", "batch": 1, "dtype": a.dtype,
+                      "value": round(dt_s, 4), "unit": "s"}))
 
 
 def bench_denoise(a, cfg, w, dev, dt, ctx):
