@@ -508,184 +508,6 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(GemmArgs g) {
   for (int i = 0; i < FM; ++i) epi_strip<DT, EPI, FN>(g, acc[i], stg, row_m0 + i * 16, vcol0, split, lane);
 }
 
-// ---------------------------------------------------------------------------
-// 256x256 "8-phase" tile (cdna_hip_programming.md §5 'The 256^2 8-phase template'):
-// 8 waves (2 M x 4 N), each owning a 128x64 output split in four 64x32
-// quadrants; the K loop runs 2 K-tiles (BK = 64) per iteration in 8 phases.
-// Every phase: read one register subtile (A rows of one M half: 8 ds_read_b128,
-// and/or B cols of one N half: 4), issue one half-tile (16 KiB) of LDS-DMA
-// prefetch, barrier, 16 MFMAs on one quadrant x K=64, barrier.  The two M wave
-// groups run one barrier apart (group 1 starts with an extra barrier), so one
-// group's MFMAs overlap the other's LDS reads; counted vmcnt(6) at phases 4 and
-// 8 keeps 3 half-tiles (1.5 K-tiles) of DMA in flight across barriers, and the
-// two LDS buffers are recycled by HALF-tile as soon as their last reader is past:
-//
-//   per K-tile (phases 1-4 read the even buffer, 5-8 the odd one):
-//     P1 read B(n0) + A(m0) -> quadrant (m0, n0)    P2 read B(n1) -> (m0, n1)
-//     P3 read A(m1)         -> (m1, n1)             P4 (no read)  -> (m1, n0)
-//   half-tile restage: B0 one phase after its read (its 4 reads are retired by
-//   lgkmcnt(8) before that phase's first barrier), A0 / B1 / A1 two phases after;
-//   K-tile 2i+2 -> even buffer in P2..P5, 2i+3 -> odd buffer in P6..P8 + next P1.
-// Each wave's 64 output columns are the two 32-column blocks wc*32 and 128 + wc*32
-// (and its 128 rows wr*64 and 128 + wr*64), so every quadrant of every wave lives
-// in one half-tile of A and one of B.
-template <int DT, int EPI>
-__global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
-  constexpr int HT = 128 * 128;   // bytes per half-tile (128 rows x 64 k x 2 B)
-  constexpr int BUF = 4 * HT;     // A0 A1 B0 B1
-  constexpr int STG = 16 * (32 + 4) * 4;
-  static_assert(8 * STG <= 2 * BUF, "epilogue staging fits the operand buffers");
-  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * BUF];
-
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int wr = wave >> 2, wc = wave & 3;
-  const int ntiles = g.tiles_m * g.tiles_n;
-  int id;
-  {
-    const int bid = blockIdx.x;
-    const int q = ntiles / 8, r = ntiles % 8, x = bid % 8, i = bid / 8;
-    id = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
-  }
-  constexpr int GROUP = 8;
-  const int per_group = GROUP * g.tiles_n;
-  const int first_m = (id / per_group) * GROUP;
-  const int gm = min(GROUP, g.tiles_m - first_m);
-  const int m0 = (first_m + (id % per_group) % gm) * 256, n0 = ((id % per_group) / gm) * 256;
-  const int split = blockIdx.y;
-  const int kb = split * g.kps, ke = min(g.K, kb + g.kps);
-  const int nk = (ke - kb + kGBK - 1) / kGBK;
-  const int iters = (nk + 1) / 2;
-
-  const uint32_t lds0 = lds_off(smem);
-  // half-tile h (0 A rows 0-127, 1 A rows 128-255, 2 B rows 0-127, 3 B rows 128-255) of
-  // K-tile kt into buffer buf: 2 LDS-DMA instructions per wave (8 rows x 128 B each)
-  auto stage_half = [&](int kt, int buf, int h) __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      int t = (wave * 2 + i) * 8 + (lane >> 3);  // row within the half-tile
-      asm volatile("" : "+v"(t));                // recomputed per issue (no hoisting)
-      const int ch = (lane & 7) ^ ((t >> 1) & 7);
-      const int k = kb + kt * kGBK + ch * 8;
-      const uint16_t* src = g.zeros;
-      if (h < 2) {
-        const int m = m0 + h * 128 + t;
-        if (m < g.M && k < ke) src = g.a + (size_t)m * g.lda + k;
-      } else {
-        const int v = n0 + (h - 2) * 128 + t;
-        if (v < g.Nv && k < ke) src = g.b + (size_t)wrow(g, v) * g.ldb + k;
-      }
-      glds16(src, smem + buf * BUF + h * HT + (wave * 2 + i) * 1024);
-    }
-  };
-
-  const int swz = (lane & 15) >> 1;
-  const uint32_t lrow = (uint32_t)(lane & 15) * 128;
-  const uint32_t off0 = (uint32_t)((((lane >> 4)) ^ swz) * 16);
-  const uint32_t off1 = (uint32_t)(((4 + (lane >> 4)) ^ swz) * 16);
-  // fragment bases: A rows (mh*128 + wr*64 + f*16), B rows (nh*128 + wc*32 + f*16)
-  const uint32_t a_base = lds0 + (uint32_t)(wr * 64) * 128 + lrow;
-  const uint32_t b_base = lds0 + 2 * HT + (uint32_t)(wc * 32) * 128 + lrow;
-
-  cf32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) azero(acc[i][j]);
-  uint4 fa[4][2], fb0[2][2], fb1[2][2];
-
-  auto read_a = [&](int buf, int mh) __attribute__((always_inline)) {
-    const uint32_t base = a_base + buf * BUF + mh * HT;
-    static_for<0, 4>([&](auto fi) __attribute__((always_inline)) {
-      constexpr int f = decltype(fi)::value;
-      fa[f][0] = ds_read16_off<f * 16 * 128>(base + off0);
-      fa[f][1] = ds_read16_off<f * 16 * 128>(base + off1);
-    });
-  };
-  auto read_b = [&](int buf, int nh, uint4 (&fb)[2][2]) __attribute__((always_inline)) {
-    const uint32_t base = b_base + buf * BUF + nh * HT;
-    static_for<0, 2>([&](auto fi) __attribute__((always_inline)) {
-      constexpr int f = decltype(fi)::value;
-      fb[f][0] = ds_read16_off<f * 16 * 128>(base + off0);
-      fb[f][1] = ds_read16_off<f * 16 * 128>(base + off1);
-    });
-  };
-  auto quadrant = [&](int mh, int nh, const uint4 (&fb)[2][2]) __attribute__((always_inline)) {
-    __builtin_amdgcn_s_setprio(1);
-    static_for<0, 4>([&](auto fi) __attribute__((always_inline)) {
-      constexpr int f = decltype(fi)::value;
-      static_for<0, 2>([&](auto gi) __attribute__((always_inline)) {
-        constexpr int gg = decltype(gi)::value;
-        amfma_v<DT>(acc[mh * 4 + f][nh * 2 + gg], fa[f][0], fb[gg][0]);
-        amfma_v<DT>(acc[mh * 4 + f][nh * 2 + gg], fa[f][1], fb[gg][1]);
-      });
-    });
-    __builtin_amdgcn_s_setprio(0);
-  };
-  auto bar = []() __attribute__((always_inline)) { asm volatile("s_barrier" ::: "memory"); };
-  auto mid = []() __attribute__((always_inline)) {  // between a phase's reads and its MFMAs
-    asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-  };
-
-  // prologue: K-tile 0 -> even buffer (complete), 3 half-tiles of K-tile 1 in flight
-  stage_half(0, 0, 2); stage_half(0, 0, 0); stage_half(0, 0, 3); stage_half(0, 0, 1);
-  stage_half(1, 1, 2); stage_half(1, 1, 0); stage_half(1, 1, 3);
-  __builtin_amdgcn_s_waitcnt(vm_wait(6));
-  bar();
-  if (wr == 1) bar();  // stagger the M wave groups by one barrier
-
-  for (int it = 0; it < iters; ++it) {
-    const int ke0 = 2 * it;
-    // ---- K-tile 2it from the even buffer
-    read_b(0, 0, fb0); __builtin_amdgcn_sched_barrier(0); read_a(0, 0);      // P1
-    stage_half(ke0 + 1, 1, 1);
-    asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
-    mid(); quadrant(0, 0, fb0); bar();
-    read_b(0, 1, fb1);                                                        // P2
-    stage_half(ke0 + 2, 0, 2);
-    mid(); quadrant(0, 1, fb1); bar();
-    read_a(0, 1);                                                             // P3
-    stage_half(ke0 + 2, 0, 0);
-    mid(); quadrant(1, 1, fb1); bar();
-    stage_half(ke0 + 2, 0, 3);                                                // P4
-    __builtin_amdgcn_s_waitcnt(vm_wait(6));  // K-tile 2it+1 landed (read from P5)
-    mid(); quadrant(1, 0, fb0); bar();
-    // ---- K-tile 2it+1 from the odd buffer
-    read_b(1, 0, fb0); __builtin_amdgcn_sched_barrier(0); read_a(1, 0);      // P5
-    stage_half(ke0 + 2, 0, 1);
-    asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
-    mid(); quadrant(0, 0, fb0); bar();
-    read_b(1, 1, fb1);                                                        // P6
-    stage_half(ke0 + 3, 1, 2);
-    mid(); quadrant(0, 1, fb1); bar();
-    read_a(1, 1);                                                             // P7
-    stage_half(ke0 + 3, 1, 0);
-    mid(); quadrant(1, 1, fb1); bar();
-    stage_half(ke0 + 3, 1, 3);                                                // P8
-    __builtin_amdgcn_s_waitcnt(vm_wait(6));  // K-tile 2it+2 landed (read from next P1)
-    mid(); quadrant(1, 0, fb0); bar();
-  }
-  if (wr == 0) bar();  // un-stagger: both groups have passed the same barrier count
-
-  // ---- epilogue (MFMA D -> VALU read wait states, drain the DMA, reuse LDS)
-#pragma unroll
-  for (int j = 0; j < 4; ++j) asm volatile("" : "+a"(acc[7][j]));
-  asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
-#pragma unroll
-  for (int j = 0; j < 4; ++j) asm volatile("" : "+a"(acc[7][j]));
-  __builtin_amdgcn_s_waitcnt(vm_wait(0));
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  float* stg = reinterpret_cast<float*>(smem + wave * STG);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int row = m0 + (i >> 2) * 128 + wr * 64 + (i & 3) * 16;
-    const cf32x4 t0[2] = {acc[i][0], acc[i][1]};
-    const cf32x4 t1[2] = {acc[i][2], acc[i][3]};
-    epi_strip<DT, EPI, 2>(g, t0, stg, row, n0 + wc * 32, split, lane);
-    epi_strip<DT, EPI, 2>(g, t1, stg, row, n0 + 128 + wc * 32, split, lane);
-  }
-}
-
 // Split-K finalize: out = epilogue(sum over splits of the slabs).  One thread
 // per 4 output columns of one row.
 template <int DT, int EPI>
@@ -744,8 +566,9 @@ using namespace cake;
 // accumulators +10-20 % on the 4-wave tiles, the interleaved schedule a further
 // +5-13 % on every tile (8-wave 256x256: 1144 -> 1286 TFLOP/s at 8192^3); 8 and 11
 // are the non-interleaved forms kept for A/B; a 4-wave 256x256 tile (128x128
-// per wave; with or without the interleaved schedule: 0.5x of tile 5) and s_setprio
-// measured slower / neutral and were dropped.
+// per wave; with or without the interleaved schedule: 0.5x of tile 5), an 8-phase
+// staggered-wave-group 256x256 tile (0.74x of tile 5, profiles/r2_gemm_8phase_rejected.jsonl)
+// and s_setprio measured slower / neutral and were dropped.
 #define CAKE_GEMM_CFGS(X)    \
   X(0, 128, 128, 2, 2, 2, 6) \
   X(1, 64, 128, 1, 4, 2, 6)  \
@@ -760,10 +583,7 @@ using namespace cake;
   X(12, 64, 128, 1, 4, 3, 6) \
   X(13, 64, 64, 2, 2, 4, 6)
 
-constexpr int kCfg8Phase = 14;  // 256x256 8-phase tile (gemm8p_kernel)
-
 static inline void cfg_dims(int cfg, int& bm, int& bn) {
-  if (cfg == kCfg8Phase) { bm = bn = 256; return; }
 #define X(id, BM, BN, WM, WN, NS, PR) if (cfg == id) { bm = BM; bn = BN; return; }
   CAKE_GEMM_CFGS(X)
 #undef X
@@ -777,10 +597,7 @@ CAKE_API int cake_gemm_tile(int cfg, int* bm, int* bn) {
 
 template <int DT, int EPI>
 static int launch_gemm(int cfg, dim3 grid, hipStream_t st, const GemmArgs& g) {
-  if (cfg == kCfg8Phase) {
-    hipLaunchKernelGGL((gemm8p_kernel<DT, EPI>), grid, dim3(512), 0, st, g);
-    return (int)hipGetLastError();
-  }
+
 #define X(id, BM, BN, WM, WN, NS, PR)                                                        \
   if (cfg == id) {                                                                           \
     hipLaunchKernelGGL((gemm_kernel<DT, BM, BN, WM, WN, NS, EPI, PR>), grid, dim3(64 * WM * WN), \

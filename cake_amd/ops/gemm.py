@@ -23,15 +23,14 @@ _DT = {torch.bfloat16: 0, torch.float16: 1}
 # (BM, BN) of the kernel's tile configurations (gemm.hip CAKE_GEMM_CFGS)
 CFG_TILES = {0: (128, 128), 1: (64, 128), 2: (256, 128), 3: (128, 256), 4: (64, 64),
              5: (256, 256), 6: (256, 128), 7: (128, 128), 8: (128, 128), 11: (256, 256),
-             12: (64, 128), 13: (64, 64), 14: (256, 256)}
-_SLOTS = {0: 2, 1: 2, 2: 1, 3: 1, 4: 4, 5: 1, 6: 1, 7: 1, 8: 2, 11: 1, 12: 2, 13: 2,
-          14: 1}  # WGs per CU
+             12: (64, 128), 13: (64, 64)}
+_SLOTS = {0: 2, 1: 2, 2: 1, 3: 1, 4: 4, 5: 1, 6: 1, 7: 1, 8: 2, 11: 1, 12: 2, 13: 2}  # WGs/CU
 # relative per-tile throughput (measured per-config sweep,
 # profiles/r2_gemm_sweep_agpr.jsonl): the AGPR-accumulator 128x128 tile (0) for most
 # shapes, the 8-wave 256x256 tile (11) where its tiles fill the chip, 64-wide tiles
 # (1, 4) for short M
 _EFF = {0: 1.0, 1: 0.8, 2: 0.8, 3: 0.8, 4: 0.7, 5: 1.2, 6: 0.95, 7: 0.9, 8: 0.9, 11: 1.1,
-        12: 0.8, 13: 0.7, 14: 1.2}
+        12: 0.8, 13: 0.7}
 NUM_CUS = 256
 _bound = False
 _plans: dict = {}
