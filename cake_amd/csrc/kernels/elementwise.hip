@@ -150,9 +150,41 @@ __global__ void add_resid_kernel(float* __restrict__ resid, const uint16_t* __re
     resid[i] += to_f32<DT>(y[i]);
 }
 
+// Streaming-read probe (scripts/decode_ceiling.py): reads n16 16-byte words
+// with the decode GEMVs' non-temporal loads, 8 per lane in flight, and does no
+// other work — the speed-of-light reference for a bandwidth-bound kernel of the
+// same byte count (the sink is written only on an impossible value).
+__global__ __launch_bounds__(256) void stream_read_kernel(const uint4* __restrict__ p, size_t n16,
+                                                          unsigned int* __restrict__ sink) {
+  constexpr int U = 8;
+  const size_t stride = (size_t)gridDim.x * 256;
+  size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  unsigned int acc = 0;
+  for (; i + (U - 1) * stride < n16; i += U * stride) {
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = ld_nt16(p + i + u * stride);
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+  }
+  for (; i < n16; i += stride) {
+    const uint4 v = ld_nt16(p + i);
+    acc ^= v.x ^ v.y ^ v.z ^ v.w;
+  }
+  if (acc == 0x9e3779b9u) sink[0] = acc;
+}
+
 }  // namespace cake
 
 using namespace cake;
+
+CAKE_API int cake_stream_read(const void* p, size_t bytes, int blocks, unsigned int* sink,
+                              hipStream_t st) {
+  if (bytes % 16 || blocks < 1 || ((uintptr_t)p % 16)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(stream_read_kernel, dim3(blocks), dim3(256), 0, st, (const uint4*)p,
+                     bytes / 16, sink);
+  return (int)hipGetLastError();
+}
 
 #define DISPATCH_DT(dt, ...)                       \
   do {                                             \

@@ -69,6 +69,64 @@ __device__ __forceinline__ void stage_plain16(const uint16_t* __restrict__ x, in
   __syncthreads();
 }
 
+// Split x prologues (NX > 0, used with a weight prefetch PFC > 0): the x loads
+// are issued FIRST, then the wave's first weight rows, then the x half is
+// finished.  Loads retire in order (vmcnt), so issuing the weights first — the
+// plain prologue order — made the norm wait for the whole weight batch; in this
+// order the norm waits only for x, and its reduction / LDS round trips overlap
+// the weight stream.  K = 1024 NX (RMSNorm, f32 row) or 2048 NX (16-bit row).
+template <int DT, int NX> struct NormPre {  // K <= 1024 NX, K % 4 == 0
+  float4 x[NX];
+  uint2 w[NX];
+  __device__ __forceinline__ void load(const float* __restrict__ xg, const uint16_t* __restrict__ wg,
+                                       int K) {
+#pragma unroll
+    for (int j = 0; j < NX; ++j) {
+      const int i = (j * kGemvThreads + threadIdx.x) * 4;
+      x[j] = i < K ? *reinterpret_cast<const float4*>(xg + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+      w[j] = i < K ? *reinterpret_cast<const uint2*>(wg + i) : make_uint2(0u, 0u);
+    }
+  }
+  __device__ __forceinline__ void finish(float eps, int K, float* xs) {
+    __shared__ float red[16];
+    float ss = 0.f;
+#pragma unroll
+    for (int j = 0; j < NX; ++j) ss += x[j].x * x[j].x + x[j].y * x[j].y + x[j].z * x[j].z + x[j].w * x[j].w;
+    ss = block_sum(ss, red);
+    const float r = rsqrtf(ss / (float)K + eps);
+#pragma unroll
+    for (int j = 0; j < NX; ++j) {
+      const int i = (j * kGemvThreads + threadIdx.x) * 4;
+      float4 v = x[j];
+      v.x *= r * to_f32<DT>((uint16_t)(w[j].x & 0xffff));
+      v.y *= r * to_f32<DT>((uint16_t)(w[j].x >> 16));
+      v.z *= r * to_f32<DT>((uint16_t)(w[j].y & 0xffff));
+      v.w *= r * to_f32<DT>((uint16_t)(w[j].y >> 16));
+      if (i < K) *reinterpret_cast<float4*>(xs + i) = v;
+    }
+    __syncthreads();
+  }
+};
+
+template <int NX> struct Plain16Pre {  // K <= 2048 NX, K % 8 == 0
+  uint4 v[NX];
+  __device__ __forceinline__ void load(const uint16_t* __restrict__ xg, int K) {
+#pragma unroll
+    for (int j = 0; j < NX; ++j) {
+      const int i = (j * kGemvThreads + threadIdx.x) * 8;
+      v[j] = i < K ? *reinterpret_cast<const uint4*>(xg + i) : make_uint4(0u, 0u, 0u, 0u);
+    }
+  }
+  __device__ __forceinline__ void finish(int K, uint16_t* xs) {
+#pragma unroll
+    for (int j = 0; j < NX; ++j) {
+      const int i = (j * kGemvThreads + threadIdx.x) * 8;
+      if (i < K) *reinterpret_cast<uint4*>(xs + i) = v[j];
+    }
+    __syncthreads();
+  }
+};
+
 template <int DT, bool XF32>
 __device__ __forceinline__ void load_x8(const void* xs, int chunk, float* o) {
   if constexpr (XF32) {
@@ -151,17 +209,20 @@ __device__ __forceinline__ void run_pairs(const Map& map, const Epi& epi, const 
   const int nch = K >> 3;
   int p = p0;
   if constexpr (PFC > 0) {
-    if (p < npairs) {
-      const uint16_t *wa, *wb;
-      map(p, wa, wb);
-      const int lane = threadIdx.x & 63;
-      float aa = 0.f, ab = 0.f;
+    // Unconditional (an idle wave works on a clamped pair and drops it): a use of
+    // the prefetched registers inside a branch lets the compiler sink the
+    // prefetch loads past the x prologue's barrier, serialising them again.
+    const uint16_t *wa, *wb;
+    map(p < npairs ? p : npairs - 1, wa, wb);
+    const int lane = threadIdx.x & 63;
+    float aa = 0.f, ab = 0.f;
 #pragma unroll
-      for (int c = 0; c < PFC; ++c) fma_chunk<DT, XF32>(xs, c * 64 + lane, pre.a[c], pre.b[c], aa, ab);
-      dot_range<DT, XF32, U>(wa, wb, xs, nch, PFC * 64, aa, ab);
-      epi(p, wave_sum(aa), wave_sum(ab));
-      p += stride;
-    }
+    for (int c = 0; c < PFC; ++c) fma_chunk<DT, XF32>(xs, c * 64 + lane, pre.a[c], pre.b[c], aa, ab);
+    dot_range<DT, XF32, U>(wa, wb, xs, nch, PFC * 64, aa, ab);
+    aa = wave_sum(aa);
+    ab = wave_sum(ab);
+    if (p < npairs) epi(p, aa, ab);
+    p += stride;
   }
   for (; p < npairs; p += stride) {
     const uint16_t *wa, *wb;
@@ -209,25 +270,39 @@ __device__ __forceinline__ QkvRow qkv_row(const QkvArgs& a, int p) {
   return r;
 }
 
-template <int DT, int U, int PFC>
+template <int DT, int U, int PFC, int NX>
 __global__ __launch_bounds__(kGemvThreads) void qkv_rope_kernel(QkvArgs a) {
   extern __shared__ float xs[];
   const int half = a.hd >> 1;
   const int npairs = (a.nh + 2 * a.nkv) * half;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int p0 = blockIdx.x * kGemvWaves + wave;
-  auto map = [&](int p, const uint16_t*& wa, const uint16_t*& wb) {
-    const QkvRow r = qkv_row(a, p);
-    wa = r.base + r.ra * a.K;
-    wb = r.base + (r.ra + half) * a.K;
+  // base selected by address arithmetic, not a pointer select: a select between
+  // kernel-argument fields becomes a memory load of the argument block, which
+  // would stand (in vmcnt order) in front of the split prologue's x loads
+  // (offsets from wq keep the global address space visible: no flat loads)
+  const uint16_t* wq = a.wq;
+  const ptrdiff_t dk = a.wk - a.wq, dv = a.wv - a.wq;
+  const int nh = a.nh, nqk = a.nh + a.nkv, hd = a.hd, K = a.K;
+  auto map = [=](int p, const uint16_t*& wa, const uint16_t*& wb) {
+    const int slot = p / half;
+    const bool isq = slot < nh, isk = !isq && slot < nqk;
+    const uint16_t* base = wq + (isq ? 0 : (isk ? dk : dv));
+    const int head = slot - (isq ? 0 : (isk ? nh : nqk));
+    const size_t ra = (size_t)head * hd + (p - slot * half);
+    wa = base + ra * K;
+    wb = base + (ra + half) * K;
   };
   Regs<PFC> pre;
-  if (PFC > 0 && p0 < npairs) {
-    const uint16_t *wa, *wb;
-    map(p0, wa, wb);
-    prefetch_rows<PFC>(wa, wb, pre);
-  }
-  stage_rmsnorm<DT>(a.resid, a.norm_w, a.eps, a.K, xs);
+  NormPre<DT, NX> xp;
+  const uint16_t *wa0, *wb0;  // rows first: their address math may load (kernarg select)
+  map(p0 < npairs ? p0 : npairs - 1, wa0, wb0);
+  if constexpr (NX > 0) xp.load(a.resid, a.norm_w, a.K);
+  __builtin_amdgcn_sched_barrier(0);  // x loads strictly before the weights (in-order vmcnt)
+  if (NX > 0 || (PFC > 0 && p0 < npairs)) prefetch_rows<PFC>(wa0, wb0, pre);  // NX: exact vmcnt
+  __builtin_amdgcn_sched_barrier(0);
+  if constexpr (NX > 0) xp.finish(a.eps, a.K, xs);
+  else stage_rmsnorm<DT>(a.resid, a.norm_w, a.eps, a.K, xs);
   const int pos = *a.pos;
   auto epi = [&](int p, float da, float db) {
     if (lane != 0) return;
@@ -255,7 +330,7 @@ __global__ __launch_bounds__(kGemvThreads) void qkv_rope_kernel(QkvArgs a) {
 // ---------------------------------------------------------------------------
 // RMSNorm + gate/up + SiLU*mul
 // ---------------------------------------------------------------------------
-template <int DT, int U, int PFC>
+template <int DT, int U, int PFC, int NX>
 __global__ __launch_bounds__(kGemvThreads) void swiglu_kernel(
     const float* __restrict__ resid, const uint16_t* __restrict__ norm_w, float eps,
     const uint16_t* __restrict__ wg, const uint16_t* __restrict__ wu, int K, int I,
@@ -268,8 +343,16 @@ __global__ __launch_bounds__(kGemvThreads) void swiglu_kernel(
     wb = wu + (size_t)j * K;
   };
   Regs<PFC> pre;
-  if (PFC > 0 && j0 < I) prefetch_rows<PFC>(wg + (size_t)j0 * K, wu + (size_t)j0 * K, pre);
-  stage_rmsnorm<DT>(resid, norm_w, eps, K, xs);
+  NormPre<DT, NX> xp;
+  const int jp = j0 < I ? j0 : I - 1;
+  const uint16_t *wa0 = wg + (size_t)jp * K, *wb0 = wu + (size_t)jp * K;
+  if constexpr (NX > 0) xp.load(resid, norm_w, K);
+  __builtin_amdgcn_sched_barrier(0);  // x loads strictly before the weights (in-order vmcnt)
+  // NX: unconditional (an idle wave re-reads the last row), so the vmcnt is exact
+  if (NX > 0 || (PFC > 0 && j0 < I)) prefetch_rows<PFC>(wa0, wb0, pre);
+  __builtin_amdgcn_sched_barrier(0);
+  if constexpr (NX > 0) xp.finish(eps, K, xs);
+  else stage_rmsnorm<DT>(resid, norm_w, eps, K, xs);
   auto epi = [&](int j, float g, float u) {
     if (lane == 0) act[j] = from_f32<DT>(silu(g) * u);
   };
@@ -280,7 +363,7 @@ __global__ __launch_bounds__(kGemvThreads) void swiglu_kernel(
 // out (+)= W x   with 16-bit x: o_proj / down_proj (accumulate into the f32
 // residual stream) — or plain f32 output.
 // ---------------------------------------------------------------------------
-template <int DT, int U, int PFC, bool ACCUM>
+template <int DT, int U, int PFC, int NX, bool ACCUM>
 __global__ __launch_bounds__(kGemvThreads) void gemv_x16_kernel(
     const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, int K, int N,
     float* __restrict__ out) {
@@ -294,12 +377,15 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_x16_kernel(
     wb = w + (size_t)min(2 * p + 1, N - 1) * K;
   };
   Regs<PFC> pre;
-  if (PFC > 0 && p0 < npairs) {
-    const uint16_t *wa, *wb;
-    map(p0, wa, wb);
-    prefetch_rows<PFC>(wa, wb, pre);
-  }
-  stage_plain16(x, K, xs);
+  Plain16Pre<NX> xp;
+  const uint16_t *wa0, *wb0;
+  map(p0 < npairs ? p0 : npairs - 1, wa0, wb0);
+  if constexpr (NX > 0) xp.load(x, K);
+  __builtin_amdgcn_sched_barrier(0);  // x loads strictly before the weights (in-order vmcnt)
+  if (NX > 0 || (PFC > 0 && p0 < npairs)) prefetch_rows<PFC>(wa0, wb0, pre);  // NX: exact vmcnt
+  __builtin_amdgcn_sched_barrier(0);
+  if constexpr (NX > 0) xp.finish(K, xs);
+  else stage_plain16(x, K, xs);
   auto epi = [&](int p, float da, float db) {
     if (lane != 0) return;
     const int ra = 2 * p, rb = 2 * p + 1;
@@ -310,7 +396,7 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_x16_kernel(
 }
 
 // RMSNorm(f32 row) then f32 output: the lm_head.
-template <int DT, int U, int PFC>
+template <int DT, int U, int PFC, int NX>
 __global__ __launch_bounds__(kGemvThreads) void gemv_norm_f32_kernel(
     const float* __restrict__ resid, const uint16_t* __restrict__ norm_w, float eps,
     const uint16_t* __restrict__ w, int K, int N, float* __restrict__ out) {
@@ -323,12 +409,15 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_norm_f32_kernel(
     wb = w + (size_t)min(2 * p + 1, N - 1) * K;
   };
   Regs<PFC> pre;
-  if (PFC > 0 && p0 < npairs) {
-    const uint16_t *wa, *wb;
-    map(p0, wa, wb);
-    prefetch_rows<PFC>(wa, wb, pre);
-  }
-  stage_rmsnorm<DT>(resid, norm_w, eps, K, xs);
+  NormPre<DT, NX> xp;
+  const uint16_t *wa0, *wb0;
+  map(p0 < npairs ? p0 : npairs - 1, wa0, wb0);
+  if constexpr (NX > 0) xp.load(resid, norm_w, K);
+  __builtin_amdgcn_sched_barrier(0);  // x loads strictly before the weights (in-order vmcnt)
+  if (NX > 0 || (PFC > 0 && p0 < npairs)) prefetch_rows<PFC>(wa0, wb0, pre);  // NX: exact vmcnt
+  __builtin_amdgcn_sched_barrier(0);
+  if constexpr (NX > 0) xp.finish(eps, K, xs);
+  else stage_rmsnorm<DT>(resid, norm_w, eps, K, xs);
   auto epi = [&](int p, float da, float db) {
     if (lane != 0) return;
     out[2 * p] = da;
@@ -342,8 +431,9 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_norm_f32_kernel(
 // PF = prefetch the first weight batch before the x prologue, MB = grid cap.
 struct GemvTune { int U, PF, MB; };
 enum GemvKind { kQkv = 0, kSwiglu = 1, kX16 = 2, kNormF32 = 3, kNumKinds = 4 };
-// measured: profiles/r1_gemv_tune_8b*.txt (lm_head 7.0 TB/s at 256 blocks)
-static GemvTune g_tune[kNumKinds] = {{8, 0, 1024}, {2, 0, 512}, {4, 0, 1024}, {4, 0, 256}};
+// measured in the decode graph (8B, tok/s): profiles/r2_gemv_split_prologue_sweep*.jsonl —
+// prefetching the first weight rows behind the split x prologue is +10% (323 -> 357)
+static GemvTune g_tune[kNumKinds] = {{4, 8, 1024}, {2, 4, 512}, {4, 4, 1024}, {4, 4, 256}};
 
 static inline int grid_for(int npairs, int max_blocks) {
   int g = (npairs + kGemvWaves - 1) / kGemvWaves;
@@ -367,6 +457,24 @@ using namespace cake;
   if (t.U == 2) { constexpr int U = 2; constexpr int PF = PFCV; __VA_ARGS__; }       \
   else if (t.U == 8) { constexpr int U = 8; constexpr int PF = PFCV; __VA_ARGS__; }  \
   else { constexpr int U = 4; constexpr int PF = PFCV; __VA_ARGS__; }
+// NX: split x prologue (only with a weight prefetch): RMSNorm rows K <= 1024 NX,
+// 16-bit rows K <= 2048 NX (guarded tails: the TP shards' K); larger K use the
+// plain prologue (NX = 0).
+#define CAKE_NX_NORM(K, ...)                                                         \
+  if constexpr (PF > 0) {                                                            \
+    if ((K) <= 4096) { constexpr int NX = 4; __VA_ARGS__; }                          \
+    else if ((K) <= 8192) { constexpr int NX = 8; __VA_ARGS__; }                     \
+    else { constexpr int NX = 0; __VA_ARGS__; }                                      \
+  } else { constexpr int NX = 0; __VA_ARGS__; }
+#define CAKE_NX_X16(K, ...)                                                          \
+  if constexpr (PF > 0) {                                                            \
+    if ((K) <= 2048) { constexpr int NX = 1; __VA_ARGS__; }                          \
+    else if ((K) <= 4096) { constexpr int NX = 2; __VA_ARGS__; }                     \
+    else if ((K) <= 8192) { constexpr int NX = 4; __VA_ARGS__; }                     \
+    else if ((K) <= 14336) { constexpr int NX = 7; __VA_ARGS__; }                    \
+    else if ((K) <= 28672) { constexpr int NX = 14; __VA_ARGS__; }                   \
+    else { constexpr int NX = 0; __VA_ARGS__; }                                      \
+  } else { constexpr int NX = 0; __VA_ARGS__; }
 #define DISPATCH_TUNE(t, K, ...)                                                     \
   do {                                                                               \
     const int pfc_ = ((K) / 8 >= 64 * (t).PF) ? (t).PF : 0;                          \
@@ -395,9 +503,9 @@ CAKE_API int cake_qkv_rope(int dt, const float* resid, const void* norm_w, float
   const int npairs = (nh + 2 * nkv) * (hd / 2);
   const size_t lds = (size_t)K * sizeof(float);
   const GemvTune t = g_tune[kQkv];
-  DISPATCH_DT(dt, DISPATCH_TUNE(t, K, hipLaunchKernelGGL((qkv_rope_kernel<DT, U, PF>),
+  DISPATCH_DT(dt, DISPATCH_TUNE(t, K, CAKE_NX_NORM(K, hipLaunchKernelGGL((qkv_rope_kernel<DT, U, PF, NX>),
                                                       dim3(grid_for(npairs, t.MB)),
-                                                      dim3(kGemvThreads), lds, st, a)));
+                                                      dim3(kGemvThreads), lds, st, a))));
   return (int)hipGetLastError();
 }
 
@@ -407,11 +515,11 @@ CAKE_API int cake_swiglu(int dt, const float* resid, const void* norm_w, float e
   if (K % 8) return (int)hipErrorInvalidValue;
   const size_t lds = (size_t)K * sizeof(float);
   const GemvTune t = g_tune[kSwiglu];
-  DISPATCH_DT(dt, DISPATCH_TUNE(t, K, hipLaunchKernelGGL((swiglu_kernel<DT, U, PF>),
+  DISPATCH_DT(dt, DISPATCH_TUNE(t, K, CAKE_NX_NORM(K, hipLaunchKernelGGL((swiglu_kernel<DT, U, PF, NX>),
                                                       dim3(grid_for(I, t.MB)), dim3(kGemvThreads),
                                                       lds, st, resid, (const uint16_t*)norm_w, eps,
                                                       (const uint16_t*)wg, (const uint16_t*)wu, K,
-                                                      I, (uint16_t*)act)));
+                                                      I, (uint16_t*)act))));
   return (int)hipGetLastError();
 }
 
@@ -422,15 +530,15 @@ CAKE_API int cake_gemv_x16(int dt, const void* x, const void* w, int K, int N, f
   const GemvTune t = g_tune[kX16];
   const int g = grid_for((N + 1) / 2, t.MB);
   if (accumulate) {
-    DISPATCH_DT(dt, DISPATCH_TUNE(t, K, hipLaunchKernelGGL((gemv_x16_kernel<DT, U, PF, true>),
+    DISPATCH_DT(dt, DISPATCH_TUNE(t, K, CAKE_NX_X16(K, hipLaunchKernelGGL((gemv_x16_kernel<DT, U, PF, NX, true>),
                                                         dim3(g), dim3(kGemvThreads), lds, st,
                                                         (const uint16_t*)x, (const uint16_t*)w, K,
-                                                        N, out)));
+                                                        N, out))));
   } else {
-    DISPATCH_DT(dt, DISPATCH_TUNE(t, K, hipLaunchKernelGGL((gemv_x16_kernel<DT, U, PF, false>),
+    DISPATCH_DT(dt, DISPATCH_TUNE(t, K, CAKE_NX_X16(K, hipLaunchKernelGGL((gemv_x16_kernel<DT, U, PF, NX, false>),
                                                         dim3(g), dim3(kGemvThreads), lds, st,
                                                         (const uint16_t*)x, (const uint16_t*)w, K,
-                                                        N, out)));
+                                                        N, out))));
   }
   return (int)hipGetLastError();
 }
@@ -440,10 +548,10 @@ CAKE_API int cake_gemv_norm_f32(int dt, const float* resid, const void* norm_w, 
   if (K % 8) return (int)hipErrorInvalidValue;
   const size_t lds = (size_t)K * sizeof(float);
   const GemvTune t = g_tune[kNormF32];
-  DISPATCH_DT(dt, DISPATCH_TUNE(t, K, hipLaunchKernelGGL((gemv_norm_f32_kernel<DT, U, PF>),
+  DISPATCH_DT(dt, DISPATCH_TUNE(t, K, CAKE_NX_NORM(K, hipLaunchKernelGGL((gemv_norm_f32_kernel<DT, U, PF, NX>),
                                                       dim3(grid_for((N + 1) / 2, t.MB)),
                                                       dim3(kGemvThreads), lds, st, resid,
                                                       (const uint16_t*)norm_w, eps,
-                                                      (const uint16_t*)w, K, N, out)));
+                                                      (const uint16_t*)w, K, N, out))));
   return (int)hipGetLastError();
 }

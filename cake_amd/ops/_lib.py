@@ -109,5 +109,6 @@ _SIGS.update({
     "cake_groupnorm_nhwc_splits": [I],
     "cake_layernorm": [I, P, P, P, C.c_longlong, I, F, P, P],
     "cake_geglu": [I, P, C.c_longlong, I, P, P],
+    "cake_stream_read": [P, Z, I, P, P],
     "cake_conv2d_nhwc": [I, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, P],
 })

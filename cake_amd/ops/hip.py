@@ -224,6 +224,15 @@ def add_resid(resid, y):
           "add_resid")
 
 
+def stream_read(buf, blocks, sink, nbytes=None):
+    """Bandwidth probe: read ``nbytes`` (default all) of ``buf`` and nothing else."""
+    _req(buf, "buf")
+    _req(sink, "sink", dtype=torch.int32)
+    n = buf.numel() * buf.element_size() if nbytes is None else int(nbytes)
+    check(kernels().cake_stream_read(_p(buf), n, int(blocks), _p(sink), _stream()),
+          "stream_read")
+
+
 # ---------------------------------------------------------------------------
 # token selection
 # ---------------------------------------------------------------------------
@@ -362,6 +371,7 @@ def set_gemv_tuning(kind: str, U: int = 4, prefetch: int = 0, max_blocks: int = 
     """Select the decode-GEMV launch geometry for one kernel kind (see gemv.hip)."""
     check(kernels().cake_gemv_set_tuning(GEMV_KINDS[kind], int(U), int(prefetch), int(max_blocks)),
           "gemv_set_tuning")
+
 
 
 # ---------------------------------------------------------------------------

@@ -13,16 +13,29 @@ from cake_amd.models.llama3.factory import random_model  # noqa: E402
 from cake_amd.models.llama3.model import DeviceDecoder  # noqa: E402
 from cake_amd.ops import hip as K  # noqa: E402
 
+# kind -> (U, prefetch, max_blocks); prefetch > 0 also selects the split x prologue
+# (gemv.hip NormPre / Plain16Pre) for the model's K
+DEFAULTS = {"qkv": (4, 8, 1024), "swiglu": (2, 4, 512), "x16": (4, 4, 1024),
+            "norm_f32": (4, 4, 256)}
+BEST = {"qkv": (4, 8, 1024), "swiglu": (2, 4, 512), "x16": (4, 4, 1024)}
 VARIANTS = {
     "default": {},
-    "qkv_pf4": {"qkv": (8, 4, 1024)},
-    "qkv_pf8": {"qkv": (8, 8, 1024)},
-    "qkv_u4pf8": {"qkv": (4, 8, 1024)},
-    "swiglu_pf4": {"swiglu": (2, 4, 512)},
-    "x16_pf4": {"x16": (4, 4, 1024)},
-    "all_pf4": {"qkv": (8, 4, 1024), "swiglu": (2, 4, 512), "x16": (4, 4, 1024)},
+    "best": BEST,
+    "best_head_pf4": {**BEST, "norm_f32": (4, 4, 256)},
+    "best_q2pf8": {**BEST, "qkv": (2, 8, 1024)},
+    "best_q8pf8": {**BEST, "qkv": (8, 8, 1024)},
+    "best_q4pf8_768": {**BEST, "qkv": (4, 8, 768)},
+    "best_sw256": {**BEST, "swiglu": (2, 4, 256)},
+    "best_sw1024": {**BEST, "swiglu": (2, 4, 1024)},
+    "best_sw4_1024": {**BEST, "swiglu": (4, 4, 1024)},
+    "best_x512": {**BEST, "x16": (4, 4, 512)},
+    "best_x2048": {**BEST, "x16": (4, 4, 2048)},
+    "best_x2pf4": {**BEST, "x16": (2, 4, 1024)},
+    "best_x8pf4": {**BEST, "x16": (8, 4, 1024)},
 }
-DEFAULTS = {"qkv": (8, 0, 1024), "swiglu": (2, 0, 512), "x16": (4, 0, 1024)}
+if os.environ.get("SWEEP_VARIANTS"):
+    VARIANTS = {k: v for k, v in VARIANTS.items()
+                if k in os.environ["SWEEP_VARIANTS"].split(",") or k == "default"}
 
 
 def main():

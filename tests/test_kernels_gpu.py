@@ -235,3 +235,66 @@ def test_rope_kv_fused_qkv_and_silu_mul_rows(cuda, dt):
     K_.silu_mul_rows(gu, act)
     ref = torch.nn.functional.silu(gu[:, :I].float()) * gu[:, I:].float()
     torch.testing.assert_close(act.float(), ref, **_tol(dt))
+
+GEMV_DEFAULTS = {"qkv": (4, 8, 1024), "swiglu": (2, 4, 512), "x16": (4, 4, 1024),
+                 "norm_f32": (4, 4, 256)}
+
+
+@pytest.fixture
+def gemv_tuning():
+    from cake_amd.ops import hip as K_
+    yield K_
+    for kind, (u, pf, mb) in GEMV_DEFAULTS.items():
+        K_.set_gemv_tuning(kind, U=u, prefetch=pf, max_blocks=mb)
+
+
+@pytest.mark.parametrize("U,pf", [(2, 4), (4, 4), (8, 8), (4, 8)])
+@pytest.mark.parametrize("mb", [3, 1024])
+def test_gemv_split_prologue(cuda, gemv_tuning, U, pf, mb):
+    """Weight prefetch with the split x prologue (x loads, then weights, then the norm /
+    staging): the model K values (4096 RMSNorm rows; 4096 / 14336 16-bit rows), idle
+    waves (N < waves) and many pairs per wave (grid cap 3)."""
+    K_ = gemv_tuning
+    for kind in GEMV_DEFAULTS:
+        K_.set_gemv_tuning(kind, U=U, prefetch=pf, max_blocks=mb)
+    torch.manual_seed(8)
+    dt = torch.bfloat16
+    # TP shard K values too: 3584 / 2048 take guarded split prologues, 1792 the plain one
+    for Kd, N in [(4096, 4096), (14336, 1030), (4096, 6), (3584, 257), (2048, 100), (1792, 64)]:
+        x = _rand(Kd, dt=dt)
+        w = _rand(N, Kd, dt=dt, std=0.02)
+        out = torch.randn(N, device=cuda)
+        ref = out + (w.float() @ x.float())
+        K_.gemv(x, w, out, accumulate=True)
+        torch.testing.assert_close(out, ref, atol=2e-3 * math.sqrt(Kd / 256), rtol=1e-3)
+    r3 = torch.randn(3072, device=cuda)
+    n3 = (1 + 0.1 * torch.randn(3072, device=cuda)).to(dt)
+    w3 = _rand(999, 3072, dt=dt, std=0.02)
+    o3 = torch.empty(999, device=cuda)
+    K_.norm_gemv_f32(r3, n3, 1e-5, w3, o3)
+    torch.testing.assert_close(o3, w3.float() @ R.rms_norm(r3, n3, 1e-5), atol=3e-3, rtol=1e-3)
+    resid = torch.randn(4096, device=cuda)
+    nw = (1 + 0.1 * torch.randn(4096, device=cuda)).to(dt)
+    xn = R.rms_norm(resid, nw, 1e-5)
+    w = _rand(3001, 4096, dt=dt, std=0.02)
+    out = torch.empty(3001, device=cuda)
+    K_.norm_gemv_f32(resid, nw, 1e-5, w, out)
+    torch.testing.assert_close(out, w.float() @ xn, atol=3e-3, rtol=1e-3)
+    wg, wu = _rand(1000, 4096, dt=dt, std=0.05), _rand(1000, 4096, dt=dt, std=0.05)
+    act = torch.empty(1000, device=cuda, dtype=dt)
+    K_.swiglu(resid, nw, 1e-5, wg, wu, act)
+    torch.testing.assert_close(act.float(), R.silu_mul(wg.float() @ xn, wu.float() @ xn), **_tol(dt))
+    nh, nkv, hd, pos = 32, 8, 128, 77
+    wq, wk, wv = (_rand(n * hd, 4096, dt=dt, std=0.05) for n in (nh, nkv, nkv))
+    invf = R.inv_freq(hd, 500000.0).to(cuda)
+    kc = torch.zeros(nkv, 128, hd, device=cuda, dtype=dt)
+    vc = torch.zeros_like(kc)
+    q = torch.empty(nh * hd, device=cuda)
+    K_.qkv_rope(resid, nw, 1e-5, wq, wk, wv, invf, torch.tensor([pos], dtype=torch.int32,
+                device=cuda), q, kc, vc)
+    posv = torch.tensor([pos], device=cuda)
+    torch.testing.assert_close(q, R.rope((wq.float() @ xn).view(1, nh, hd), posv, invf).view(-1),
+                               atol=2e-3, rtol=2e-3)
+    kr = R.rope((wk.float() @ xn).view(1, nkv, hd), posv, invf).view(nkv, hd)
+    torch.testing.assert_close(kc[:, pos].float(), kr, **_tol(dt))
+    torch.testing.assert_close(vc[:, pos].float(), (wv.float() @ xn).view(nkv, hd), **_tol(dt))

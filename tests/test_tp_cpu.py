@@ -16,6 +16,14 @@ from cake_amd.parallel.tensor_parallel import (AllReduce, TPEngine, check_tp, sh
 
 CFG = dict(num_hidden_layers=3, num_attention_heads=4, num_key_value_heads=2,
            intermediate_size=520, vocab_size=509)
+
+
+def _cfg(world):
+    # TP needs nkv % world == 0: widen the GQA geometry for 4 and 8 ranks (n_rep 2 kept)
+    if world > 2:
+        return preset("tiny", **dict(CFG, num_attention_heads=2 * world,
+                                     num_key_value_heads=world))
+    return preset("tiny", **CFG)
 PROMPT = [1, 5, 9, 33, 2, 7]
 STEPS = 8
 
@@ -28,8 +36,8 @@ def _free_port():
     return p
 
 
-def _reference_tokens(penalty=1.1, last_n=16):
-    cfg = preset("tiny", **CFG)
+def _reference_tokens(world, penalty=1.1, last_n=16):
+    cfg = _cfg(world)
     m = random_model(cfg, "cpu", torch.float32, max_seq=64, seed=3)
     toks = list(PROMPT)
     logits = m.forward(PROMPT, 0)
@@ -44,7 +52,7 @@ def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        cfg = preset("tiny", **CFG)
+        cfg = _cfg(world)
         m = random_model(cfg, "cpu", torch.float32, max_seq=64, seed=3)
         blocks = {li: shard_block(w, cfg, rank, world) for li, w in m.stack.weights.items()}
         head = shard_head(m.head.embed, m.head.norm, m.head.lm_head, rank, world)
@@ -59,9 +67,9 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [1, 2])
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
 def test_tp_matches_all_local(world):
-    ref = _reference_tokens()
+    ref = _reference_tokens(world)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()

@@ -19,10 +19,11 @@ def _free_port():
     return p
 
 
-def _cfg():
+def _cfg(world=2):
     from cake_amd.models.llama3.config import preset
+    # TP needs nkv % world == 0
     return preset("llama3-8b", num_hidden_layers=2, hidden_size=512, num_attention_heads=8,
-                  num_key_value_heads=2, intermediate_size=1024, vocab_size=1000)
+                  num_key_value_heads=max(2, world), intermediate_size=1024, vocab_size=1000)
 
 
 PROMPT = [3, 14, 15, 92, 65, 35, 89, 79]
@@ -38,7 +39,7 @@ def _worker(rank, world, port, mode, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         torch.cuda.set_device(0)
-        cfg = _cfg()
+        cfg = _cfg(world)
         m = random_model(cfg, "cuda:0", torch.bfloat16, max_seq=64, seed=5)
         blocks = {li: shard_block(w, cfg, rank, world) for li, w in m.stack.weights.items()}
         head = shard_head(m.head.embed, m.head.norm, m.head.lm_head, rank, world)
@@ -61,30 +62,32 @@ def _worker(rank, world, port, mode, q):
         dist.destroy_process_group()
 
 
-def _reference():
+def _reference(world):
     from cake_amd.models.llama3.decode_loop import run_decode
     from cake_amd.models.llama3.factory import random_model
     from cake_amd.models.llama3.model import DeviceDecoder
-    m = random_model(_cfg(), "cuda:0", torch.bfloat16, max_seq=64, seed=5)
+    m = random_model(_cfg(world), "cuda:0", torch.bfloat16, max_seq=64, seed=5)
     dec = DeviceDecoder(m, repeat_penalty=1.1, repeat_last_n=16)
     first = dec.start(PROMPT)
     dec.capture()
     return PROMPT + [first] + run_decode(dec, STEPS).tokens
 
 
-@pytest.mark.parametrize("mode", ["ipc", "dist"])
-def test_tp2_matches_single_gpu(cuda, mode):
+@pytest.mark.parametrize("mode,world", [("ipc", 2), ("dist", 2), ("ipc", 4)])
+def test_tp_matches_single_gpu(cuda, mode, world):
+    """world ranks share cuda:0 (a 4-rank run exercises the all-reduce kernels' bank /
+    peer indexing beyond a pair)."""
     import torch.multiprocessing as mp
-    ref = _reference()
+    ref = _reference(world)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, 2, port, mode, q)) for r in range(2)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, mode, q)) for r in range(world)]
     for p in ps:
         p.start()
     got = {}
     try:
-        for _ in range(2):
+        for _ in range(world):
             r, used, toks, us = q.get(timeout=150)
             got[r] = (used, toks, us)
         for p in ps:
@@ -94,7 +97,7 @@ def test_tp2_matches_single_gpu(cuda, mode):
         for p in ps:  # a failed rank leaves its peer blocked in a collective
             if p.is_alive():
                 p.kill()
-    assert got[0][1] == got[1][1]          # the ranks agree token for token
+    assert all(got[r][1] == got[0][1] for r in range(world))  # ranks agree token for token
     assert got[0][0] == mode, got[0][0]    # the IPC self-test passed (no silent fallback)
     toks = got[0][1]
     assert len(toks) == len(ref)
