@@ -31,7 +31,7 @@ namespace cake {
 // position): ns = min(maxsplit, ceil(Tk / min_keys)); each split owns a
 // contiguous range of whole 64-key chunks.  Chunks are streamed
 // global -> registers (every load of the next chunk is issued before the
-// current chunk is computed) -> LDS (K rows padded 16 B: conflict-free
+// current chunk is computed) -> LDS (K rows XOR-swizzled: conflict-free
 // row-per-lane ds_read_b128).  Per wave: lane j scores key j, online softmax
 // in base 2 (scale * log2 e folded into q), P·V with lanes over head dims.
 //
@@ -56,6 +56,39 @@ __device__ __forceinline__ float ld_sc1(const float* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Chunk [c0, c0 + 64) of one kv head, staged global -> registers -> LDS: piece P
+// (row P / CPR, slot P % CPR) of K lands at slot ^ (row % CPR) (the XOR swizzle
+// makes the row-per-lane ds_read_b128 of the scores conflict-free), V linear.
+// Rows past the live end re-read the last live row (never outside the cache).
+template <int HD, int NW, int IPW>
+__device__ __forceinline__ void kv_load(u32x4 (&rk)[IPW], u32x4 (&rv)[IPW], const uint16_t* kg,
+                                        const uint16_t* vg, int c0, int ke, int wave, int lane) {
+  constexpr int CPR = HD / 8;
+  const int last = ke - 1 - c0;
+#pragma unroll
+  for (int i = 0; i < IPW; ++i) {
+    const int P = (wave * IPW + i) * 64 + lane;
+    const int r = P / CPR, c = P % CPR;
+    const size_t src = (size_t)(c0 + (r < last ? r : last)) * HD + c * 8;
+    rk[i] = *reinterpret_cast<const u32x4*>(kg + src);
+    rv[i] = *reinterpret_cast<const u32x4*>(vg + src);
+  }
+}
+
+template <int HD, int IPW>
+__device__ __forceinline__ void kv_store(const u32x4 (&rk)[IPW], const u32x4 (&rv)[IPW],
+                                         uint16_t* kd, int wave, int lane) {
+  constexpr int CPR = HD / 8;
+  uint16_t* vd = kd + kChunk * HD;
+#pragma unroll
+  for (int i = 0; i < IPW; ++i) {
+    const int P = (wave * IPW + i) * 64 + lane;
+    const int r = P / CPR, c = P % CPR;
+    *reinterpret_cast<u32x4*>(kd + (r * CPR + (c ^ (r % CPR))) * 8) = rk[i];
+    *reinterpret_cast<u32x4*>(vd + P * 8) = rv[i];
+  }
+}
+
 template <int DT, int HD, int NREP>
 __global__ __launch_bounds__(AttnGeom<NREP>::NT) void attn_decode_kernel(
     const float* __restrict__ q, const uint16_t* __restrict__ kc,
@@ -67,7 +100,7 @@ __global__ __launch_bounds__(AttnGeom<NREP>::NT) void attn_decode_kernel(
   constexpr int DPL = HD / 64;              // output dims per lane
   constexpr int CPR = HD / 8;               // 16-byte pieces per row
   constexpr int PIECES = kChunk * CPR;      // pieces per chunk (each of K and V)
-  constexpr int IPW = PIECES / 64 / NW;     // LDS-DMA wave-instructions per wave (each of K, V)
+  constexpr int IPW = PIECES / 64 / NW;     // 16-byte pieces per thread per chunk (each of K, V)
   static_assert(IPW >= 1 && PIECES % (64 * NW) == 0, "chunk/wave geometry");
   // one LDS array (LDS-DMA pipelines need it: MI355X guide, GEMM item 4a):
   // [2 buffers][K chunk | V chunk] 16-bit, then q (f32, pre-scaled), then p rows
@@ -79,7 +112,11 @@ __global__ __launch_bounds__(AttnGeom<NREP>::NT) void attn_decode_kernel(
 
   const int g = blockIdx.x, s = blockIdx.y;
   const int Tk = *pos_ptr + 1;
-  int ns = (Tk + min_keys - 1) / min_keys;
+  // past 1024 keys two chunks per split: every extra chunk per split costs about
+  // one load round trip (~1.8 us), every extra split ~0.05-0.1 us of merge
+  // (profiles/r2_decode_attn_pv*.jsonl: 2048 keys 11.7 us in 17 splits vs 12.4 in 33)
+  const int keys = max(max(min_keys, Tk > 1024 ? 2 * kChunk : kChunk), (Tk + kMaxSplit - 1) / kMaxSplit);
+  int ns = (Tk + keys - 1) / keys;
   if (ns > (int)gridDim.y) ns = gridDim.y;
   int kps = (Tk + ns - 1) / ns;
   kps = (kps + kChunk - 1) / kChunk * kChunk;
@@ -91,43 +128,29 @@ __global__ __launch_bounds__(AttnGeom<NREP>::NT) void attn_decode_kernel(
 
   const uint16_t* kg = kc + (size_t)g * S * HD;
   const uint16_t* vg = vc + (size_t)g * S * HD;
-  // Stage chunk [c0, c0 + 64) into buffer b.  LDS piece P (row P / CPR, slot
-  // P % CPR) of K holds key piece slot ^ (row % CPR): an XOR swizzle applied on
-  // the SOURCE address (the DMA writes lane-linear), so the row-per-lane
-  // ds_read_b128 of the scores is conflict-free.  V stays linear.  Rows past
-  // the live end re-read the last live row (never outside the cache).
-  auto stage = [&](int c0, int b) {
-    const int last = ke - 1 - c0;
-    uint16_t* kd = smem + b * 2 * PIECES * 8;
-    uint16_t* vd = kd + PIECES * 8;
+  // The loads of the next chunk are issued before the current chunk is computed
+  // and stored to the other LDS buffer after it (register staging: the compiler's
+  // vmcnt covers exactly these loads, where an LDS-DMA stage made every LDS read
+  // wait for the in-flight DMA as well).
+  u32x4 rk[IPW], rv[IPW];
+  // P·V mapping: lane = key group kgi (keys kgi*VT .. +VT of the chunk) x dim
+  // group dg (dims dg*8 .. +8): one ds_read_b128 per key per lane, VT of them
+  // independent per chunk; the key groups' partial sums are only combined once,
+  // after the last chunk (the online-softmax rescale is the same for every lane)
+  constexpr int DG = HD / 8, KG = 64 / DG, VT = kChunk / KG;
+  const int dg = lane % DG, kgi = lane / DG;
+  float m = -INFINITY, l = 0.f, o[8];
 #pragma unroll
-    for (int i = 0; i < IPW; ++i) {
-      const int P = (wave * IPW + i) * 64 + lane;
-      const int r = P / CPR, c = P % CPR;
-      const int rr = r < last ? r : last;
-      glds16(kg + (size_t)(c0 + rr) * HD + (c ^ (r % CPR)) * 8, kd + (wave * IPW + i) * 64 * 8);
-      glds16(vg + (size_t)(c0 + rr) * HD + c * 8, vd + (wave * IPW + i) * 64 * 8);
-    }
-  };
-
-  float m = -INFINITY, l = 0.f, o[DPL];
-#pragma unroll
-  for (int d = 0; d < DPL; ++d) o[d] = 0.f;
-  stage(kb, 0);
-  // q after the first chunk's DMA: one round trip covers both (hipcc drains the
-  // DMA together with the q loads before the LDS stores below)
+  for (int d = 0; d < 8; ++d) o[d] = 0.f;
   for (int i = tid; i < NREP * HD; i += NT) qs[i] = q[(size_t)g * NREP * HD + i] * scale_log2;
+  kv_load<HD, NW, IPW>(rk, rv, kg, vg, kb, ke, wave, lane);
+  kv_store<HD, IPW>(rk, rv, smem, wave, lane);
   __syncthreads();
   int buf = 0;
   for (int c0 = kb; c0 < ke; c0 += kChunk, buf ^= 1) {
     const int kn = min(kChunk, ke - c0);
-    if (c0 + kChunk < ke) {  // next chunk streams while this one computes
-      stage(c0 + kChunk, buf ^ 1);
-      __builtin_amdgcn_s_waitcnt(vm_wait(2 * IPW));
-    } else {
-      __builtin_amdgcn_s_waitcnt(vm_wait(0));
-    }
-    __builtin_amdgcn_s_barrier();  // every wave's DMA for this chunk has landed
+    const bool more = c0 + kChunk < ke;
+    if (more) kv_load<HD, NW, IPW>(rk, rv, kg, vg, c0 + kChunk, ke, wave, lane);  // in flight
     const uint16_t* Ks = smem + buf * 2 * PIECES * 8;
     const uint16_t* Vs = Ks + PIECES * 8;
     if (wave < NREP) {
@@ -159,40 +182,42 @@ __global__ __launch_bounds__(AttnGeom<NREP>::NT) void attn_decode_kernel(
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's p row is in LDS
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
-      for (int d = 0; d < DPL; ++d) o[d] *= alpha;
-      const int kn4 = kn & ~3;
-      for (int j = 0; j < kn4; j += 4) {
-        const float4 p4 = *reinterpret_cast<const float4*>(pw + j);
-        const float pj[4] = {p4.x, p4.y, p4.z, p4.w};
+      for (int d = 0; d < 8; ++d) o[d] *= alpha;
+      // keys past kn have p = 0 and V rows re-read from the live range (finite)
+      float pv[VT];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const uint16_t* vr = Vs + (j + e) * HD + lane * DPL;
-          if constexpr (DPL == 2) {
-            const uint32_t w2 = *reinterpret_cast<const uint32_t*>(vr);
-            o[0] = fmaf(pj[e], to_f32<DT>((uint16_t)(w2 & 0xffffu)), o[0]);
-            o[1] = fmaf(pj[e], to_f32<DT>((uint16_t)(w2 >> 16)), o[1]);
-          } else {
-#pragma unroll
-            for (int d = 0; d < DPL; ++d) o[d] = fmaf(pj[e], to_f32<DT>(vr[d]), o[d]);
-          }
-        }
+      for (int t = 0; t < VT; t += 4) {
+        const float4 p4 = *reinterpret_cast<const float4*>(pw + kgi * VT + t);
+        pv[t] = p4.x; pv[t + 1] = p4.y; pv[t + 2] = p4.z; pv[t + 3] = p4.w;
       }
-      for (int j = kn4; j < kn; ++j) {
-        const uint16_t* vr = Vs + j * HD + lane * DPL;
+      const uint16_t* vcol = Vs + (size_t)kgi * VT * HD + dg * 8;
 #pragma unroll
-        for (int d = 0; d < DPL; ++d) o[d] = fmaf(pw[j], to_f32<DT>(vr[d]), o[d]);
+      for (int t = 0; t < VT; ++t) {
+        float vf[8];
+        unpack8<DT>(*reinterpret_cast<const uint4*>(vcol + t * HD), vf);
+#pragma unroll
+        for (int d = 0; d < 8; ++d) o[d] = fmaf(pv[t], vf[d], o[d]);
       }
     }
-    // every wave is done with this buffer before the next iteration restages it
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    // (that buffer was released by the previous barrier)
+    if (more) kv_store<HD, IPW>(rk, rv, smem + (buf ^ 1) * 2 * kChunk * HD, wave, lane);
+    __syncthreads();           // next chunk visible; this buffer free for reuse
   }
 
+  // combine the key groups: afterwards every lane of dim group dg holds its 8 sums
+#pragma unroll
+  for (int off = DG; off < 64; off <<= 1) {
+#pragma unroll
+    for (int d = 0; d < 8; ++d) o[d] += __shfl_xor(o[d], off, 64);
+  }
   const int h = g * NREP + wave;
   if (ns == 1) {  // the whole context in this split: finish here
-    if (wave < NREP) {
+    if (wave < NREP && kgi == 0) {
       const float inv = 1.f / l;
+      uint16_t ob[8];
 #pragma unroll
-      for (int d = 0; d < DPL; ++d) out[(size_t)h * HD + lane * DPL + d] = from_f32<DT>(o[d] * inv);
+      for (int d = 0; d < 8; ++d) ob[d] = from_f32<DT>(o[d] * inv);
+      *reinterpret_cast<uint4*>(out + (size_t)h * HD + dg * 8) = *reinterpret_cast<const uint4*>(ob);
     }
     return;
   }
@@ -201,8 +226,10 @@ __global__ __launch_bounds__(AttnGeom<NREP>::NT) void attn_decode_kernel(
   if (wave < NREP) {
     float* dst = part + ((size_t)h * kMaxSplit + s) * (HD + 2);
     if (lane == 0) { st_sc1(dst, m); st_sc1(dst + 1, l); }
+    if (kgi == 0) {
 #pragma unroll
-    for (int d = 0; d < DPL; ++d) st_sc1(dst + 2 + lane * DPL + d, o[d]);
+      for (int d = 0; d < 8; ++d) st_sc1(dst + 2 + dg * 8 + d, o[d]);
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -230,12 +257,22 @@ __global__ __launch_bounds__(AttnGeom<NREP>::NT) void attn_decode_kernel(
   float acc[DPL];
 #pragma unroll
   for (int d = 0; d < DPL; ++d) acc[d] = 0.f;
-#pragma unroll 8
-  for (int t = 0; t < ns; ++t) {
-    const float w = pw[t];
-    const float* pt = src + t * (HD + 2) + 2 + lane * DPL;
+  // 16 partials' loads in flight per round trip (ns <= 64: at most 4 rounds)
+  for (int t0 = 0; t0 < ns; t0 += 16) {
+    float v[16][DPL];
 #pragma unroll
-    for (int d = 0; d < DPL; ++d) acc[d] = fmaf(w, ld_sc1(pt + d), acc[d]);
+    for (int u = 0; u < 16; ++u) {
+      const int t = t0 + u < ns ? t0 + u : ns - 1;
+      const float* pt = src + t * (HD + 2) + 2 + lane * DPL;
+#pragma unroll
+      for (int d = 0; d < DPL; ++d) v[u][d] = ld_sc1(pt + d);
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const float w = t0 + u < ns ? pw[t0 + u] : 0.f;
+#pragma unroll
+      for (int d = 0; d < DPL; ++d) acc[d] = fmaf(w, v[u][d], acc[d]);
+    }
   }
   const float inv = 1.f / L;
 #pragma unroll

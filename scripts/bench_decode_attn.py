@@ -23,12 +23,12 @@ def main():
         tickets = torch.zeros(nkv, dtype=torch.int32, device=dev)
         out = torch.empty(nh * hd, device=dev, dtype=dt)
         pos = torch.zeros(1, dtype=torch.int32, device=dev)
-        for Tk in (176, 512, 1024, 2048, 4096, 8192):
+        for Tk in (55, 176, 512, 1024, 2048, 4096, 8192):
             if Tk > S or (S == 8192 and Tk < 4096):
                 continue
             pos.fill_(Tk - 1)
             rec = {"S": S, "Tk": Tk}
-            for mk in (64, 128, 256):
+            for mk in (64, 128, 256, 512):
                 K.attn_set_min_keys(mk)
                 K.attn_decode(q, kc, vc, pos, 1 / math.sqrt(hd), part, tickets, out)
                 g = torch.cuda.CUDAGraph()
