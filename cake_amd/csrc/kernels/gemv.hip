@@ -300,6 +300,10 @@ __global__ __launch_bounds__(kGemvThreads) void qkv_rope_kernel(QkvArgs a) {
   if constexpr (NX > 0) xp.load(a.resid, a.norm_w, a.K);
   __builtin_amdgcn_sched_barrier(0);  // x loads strictly before the weights (in-order vmcnt)
   if (NX > 0 || (PFC > 0 && p0 < npairs)) prefetch_rows<PFC>(wa0, wb0, pre);  // NX: exact vmcnt
+  // the RoPE frequency of the wave's first pair, requested now: loaded in the
+  // epilogue it was one more memory round trip at the end of every wave
+  const int pc = p0 < npairs ? p0 : npairs - 1;
+  const float f0 = a.inv_freq[pc - (pc / half) * half];
   __builtin_amdgcn_sched_barrier(0);
   if constexpr (NX > 0) xp.finish(a.eps, a.K, xs);
   else stage_rmsnorm<DT>(a.resid, a.norm_w, a.eps, a.K, xs);
@@ -310,7 +314,7 @@ __global__ __launch_bounds__(kGemvThreads) void qkv_rope_kernel(QkvArgs a) {
     float oa = da, ob = db;
     if (r.kind < 2) {
       float s, c;
-      sincosf((float)pos * a.inv_freq[r.i], &s, &c);
+      sincosf((float)pos * (p == p0 ? f0 : a.inv_freq[r.i]), &s, &c);
       oa = da * c - db * s;
       ob = da * s + db * c;
     }
@@ -383,14 +387,23 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_x16_kernel(
   if constexpr (NX > 0) xp.load(x, K);
   __builtin_amdgcn_sched_barrier(0);  // x loads strictly before the weights (in-order vmcnt)
   if (NX > 0 || (PFC > 0 && p0 < npairs)) prefetch_rows<PFC>(wa0, wb0, pre);  // NX: exact vmcnt
+  // ACCUM: the residual words of the wave's first pair, requested now (read in
+  // the epilogue they were one more memory round trip at the end of every wave;
+  // no other wave of this launch writes them)
+  float r0a = 0.f, r0b = 0.f;
+  if constexpr (ACCUM) {
+    const int pc = p0 < npairs ? p0 : npairs - 1;
+    r0a = out[2 * pc];
+    r0b = out[min(2 * pc + 1, N - 1)];
+  }
   __builtin_amdgcn_sched_barrier(0);
   if constexpr (NX > 0) xp.finish(K, xs);
   else stage_plain16(x, K, xs);
   auto epi = [&](int p, float da, float db) {
     if (lane != 0) return;
     const int ra = 2 * p, rb = 2 * p + 1;
-    if (ACCUM) out[ra] += da; else out[ra] = da;
-    if (rb < N) { if (ACCUM) out[rb] += db; else out[rb] = db; }
+    if (ACCUM) out[ra] = da + (p == p0 ? r0a : out[ra]); else out[ra] = da;
+    if (rb < N) { if (ACCUM) out[rb] = db + (p == p0 ? r0b : out[rb]); else out[rb] = db; }
   };
   run_pairs<DT, false, U, PFC>(map, epi, xs, K, npairs, p0, gridDim.x * kGemvWaves, pre);
 }
@@ -555,3 +568,4 @@ CAKE_API int cake_gemv_norm_f32(int dt, const float* resid, const void* norm_w, 
                                                       (const uint16_t*)w, K, N, out))));
   return (int)hipGetLastError();
 }
+

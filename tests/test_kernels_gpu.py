@@ -125,6 +125,30 @@ def test_attn_decode(cuda, dt, nh, nkv, hd, pos, S, min_keys):
     torch.testing.assert_close(out.float(), ref, **_tol(dt))
 
 
+@pytest.mark.parametrize("pos", [0, 5, 63, 64, 130])
+def test_attn_decode_dead_rows_nan(cuda, pos):
+    """Cache rows past the live length hold NaN: split 0 loads its first chunk before
+    the length is known, so those rows must never reach the output."""
+    from cake_amd.ops import hip as K_
+    torch.manual_seed(5)
+    nh, nkv, hd, S = 32, 8, 128, 512
+    kc = _rand(nkv, S, hd, dt=torch.bfloat16)
+    vc = _rand(nkv, S, hd, dt=torch.bfloat16)
+    kc[:, pos + 1:] = float("nan")
+    vc[:, pos + 1:] = float("nan")
+    q = torch.randn(nh * hd, device=cuda)
+    p = torch.tensor([pos], dtype=torch.int32, device=cuda)
+    part = torch.empty(K_.attn_workspace_numel(nh, hd, S), device=cuda)
+    out = torch.empty(nh * hd, device=cuda, dtype=torch.bfloat16)
+    tickets = torch.zeros(nkv, dtype=torch.int32, device=cuda)
+    K_.attn_decode(q, kc, vc, p, 1 / math.sqrt(hd), part, tickets, out)
+    Tk = pos + 1
+    ref = R.attention(q.view(1, nh, hd), kc[:, :Tk].transpose(0, 1), vc[:, :Tk].transpose(0, 1),
+                      pos).reshape(-1)
+    assert torch.isfinite(out.float()).all()
+    torch.testing.assert_close(out.float(), ref, **_tol(torch.bfloat16))
+
+
 @pytest.mark.parametrize("dt", DTYPES)
 @pytest.mark.parametrize("T,pos0,nh,nkv,hd", [(7, 0, 32, 8, 128), (70, 0, 4, 1, 64),
                                               (33, 100, 32, 8, 128), (1, 5, 8, 8, 64)])
