@@ -156,6 +156,7 @@ __device__ __forceinline__ void attn_decode_block(const AttnDecArgs& a, int g, i
   // independent per chunk; the key groups' partial sums are only combined once,
   // after the last chunk (the online-softmax rescale is the same for every lane)
   constexpr int DG = HD / 8, KG = 64 / DG, VT = kChunk / KG;
+  static_assert(DG == 8 || DG == 16, "key-group combine covers hd 64 and 128");
   const int dg = lane % DG, kgi = lane / DG;
   float m = -INFINITY, l = 0.f, o[8];
 #pragma unroll
@@ -261,9 +262,9 @@ __device__ __forceinline__ void attn_decode_block(const AttnDecArgs& a, int g, i
 
   // combine the key groups: afterwards every lane of dim group dg holds its 8 sums
 #pragma unroll
-  for (int off = DG; off < 64; off <<= 1) {
-#pragma unroll
-    for (int d = 0; d < 8; ++d) o[d] += __shfl_xor(o[d], off, 64);
+  for (int d = 0; d < 8; ++d) {
+    if constexpr (DG <= 8) o[d] = xor_add<8>(o[d]);
+    o[d] = xor_add<32>(xor_add<16>(o[d]));
   }
   const int h = g * NREP + wave;
   if (ns == 1) {  // the whole context in this split: finish here

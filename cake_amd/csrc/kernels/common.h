@@ -66,16 +66,54 @@ __device__ __forceinline__ void unpack8(const uint4 v, float* o) {
   }
 }
 
+// Wave-wide butterfly reductions without LDS: DPP (quad_perm xor 1 / xor 2,
+// row_half_mirror, row_mirror) inside each 16-lane row, then the gfx950 lane-swap
+// instructions across rows (v_permlane16_swap: rows 0|1 and 2|3; v_permlane32_swap:
+// halves).  Every lane ends with the same bits.  (The __shfl_xor form was six
+// dependent ds_bpermute round trips per reduction.)
+template <int CTRL> __device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL,
+                                                               0xF, 0xF, false));
+}
+constexpr int kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppHalfMirror = 0x141, kDppMirror = 0x140;
+
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
+  v += dpp_f<kDppXor1>(v);
+  v += dpp_f<kDppXor2>(v);
+  v += dpp_f<kDppHalfMirror>(v);
+  v += dpp_f<kDppMirror>(v);
+  const int b = __builtin_bit_cast(int, v);
+  const auto p = __builtin_amdgcn_permlane16_swap(b, b, false, false);
+  v = __builtin_bit_cast(float, (int)p[0]) + __builtin_bit_cast(float, (int)p[1]);
+  const int c = __builtin_bit_cast(int, v);
+  const auto q = __builtin_amdgcn_permlane32_swap(c, c, false, false);
+  return __builtin_bit_cast(float, (int)q[0]) + __builtin_bit_cast(float, (int)q[1]);
 }
 
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
-  return v;
+  v = fmaxf(v, dpp_f<kDppXor1>(v));
+  v = fmaxf(v, dpp_f<kDppXor2>(v));
+  v = fmaxf(v, dpp_f<kDppHalfMirror>(v));
+  v = fmaxf(v, dpp_f<kDppMirror>(v));
+  const int b = __builtin_bit_cast(int, v);
+  const auto p = __builtin_amdgcn_permlane16_swap(b, b, false, false);
+  v = fmaxf(__builtin_bit_cast(float, (int)p[0]), __builtin_bit_cast(float, (int)p[1]));
+  const int c = __builtin_bit_cast(int, v);
+  const auto q = __builtin_amdgcn_permlane32_swap(c, c, false, false);
+  return fmaxf(__builtin_bit_cast(float, (int)q[0]), __builtin_bit_cast(float, (int)q[1]));
+}
+
+// v + v[lane ^ OFF] (same bits in both lanes of a pair), OFF in {8, 16, 32}.
+template <int OFF> __device__ __forceinline__ float xor_add(float v) {
+  static_assert(OFF == 8 || OFF == 16 || OFF == 32, "xor_add offset");
+  if constexpr (OFF == 8) {
+    return v + dpp_f<0x128>(v);  // row_ror:8 == lane ^ 8 inside a 16-lane row
+  } else {
+    const int b = __builtin_bit_cast(int, v);
+    const auto p = OFF == 16 ? __builtin_amdgcn_permlane16_swap(b, b, false, false)
+                             : __builtin_amdgcn_permlane32_swap(b, b, false, false);
+    return __builtin_bit_cast(float, (int)p[0]) + __builtin_bit_cast(float, (int)p[1]);
+  }
 }
 
 // Block-wide sum for blockDim.x <= 1024; `red` must hold >= 16 floats.

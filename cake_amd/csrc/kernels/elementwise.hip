@@ -253,3 +253,20 @@ CAKE_API int cake_add_resid(int dt, float* resid, const void* y, size_t n, hipSt
                                      st, resid, (const uint16_t*)y, n));
   return (int)hipGetLastError();
 }
+
+// Test hook for the wave reductions of common.h (one wave): out[0:64] wave_sum,
+// [64:128] wave_max, [128:192] x + x[l^8], [192:256] x + x[l^16], [256:320] x + x[l^32].
+__global__ __launch_bounds__(64) void wave_reduce_probe_kernel(const float* x, float* out) {
+  const int l = threadIdx.x;
+  const float v = x[l];
+  out[l] = wave_sum(v);
+  out[64 + l] = wave_max(v);
+  out[128 + l] = xor_add<8>(v);
+  out[192 + l] = xor_add<16>(v);
+  out[256 + l] = xor_add<32>(v);
+}
+
+CAKE_API int cake_wave_reduce_probe(const float* x, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(wave_reduce_probe_kernel, dim3(1), dim3(64), 0, st, x, out);
+  return (int)hipGetLastError();
+}

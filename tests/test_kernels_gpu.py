@@ -125,6 +125,23 @@ def test_attn_decode(cuda, dt, nh, nkv, hd, pos, S, min_keys):
     torch.testing.assert_close(out.float(), ref, **_tol(dt))
 
 
+def test_wave_reductions(cuda):
+    """DPP / permlane-swap wave reductions (common.h) against torch, every lane."""
+    from cake_amd.ops._lib import check, kernels
+    torch.manual_seed(8)
+    x = torch.randn(64, device=cuda)
+    out = torch.empty(320, device=cuda)
+    check(kernels().cake_wave_reduce_probe(x.data_ptr(), out.data_ptr(),
+                                           torch.cuda.current_stream().cuda_stream), "probe")
+    torch.cuda.synchronize()
+    idx = torch.arange(64, device=cuda)
+    torch.testing.assert_close(out[:64], x.sum().expand(64), atol=1e-5, rtol=1e-5)
+    assert torch.equal(out[64:128], x.max().expand(64))
+    assert out[:64].unique().numel() == 1  # identical bits in every lane
+    for k, off in enumerate((8, 16, 32)):
+        torch.testing.assert_close(out[128 + 64 * k:192 + 64 * k], x + x[idx ^ off])
+
+
 @pytest.mark.parametrize("pos", [0, 5, 63, 64, 130])
 def test_attn_decode_dead_rows_nan(cuda, pos):
     """Cache rows past the live length hold NaN: split 0 loads its first chunk before
