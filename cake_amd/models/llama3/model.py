@@ -155,6 +155,8 @@ class DeviceDecoder:
         self.bufs: DecodeBuffers = model.stack.decode_buffers(with_head=True)
         self.params: torch.Tensor | None = None  # device SampleParams (set_sampling)
         self.graph: torch.cuda.CUDAGraph | None = None
+        # one graph per attention split cap (position buckets), see capture()
+        self.graphs: dict[int, torch.cuda.CUDAGraph] = {}
         self.host_pos = 0  # device position of the next step (tracked on the host)
         self._layers = list(range(model.cfg.num_hidden_layers))
 
@@ -180,6 +182,7 @@ class DeviceDecoder:
             self.params = torch.zeros(K.SAMPLE_PARAMS_WORDS, dtype=torch.int32,
                                       device=self.m.device)
             self.graph = None
+            self.graphs = {}
             self.greedy = True
         self.sampling = sampling if sampling is not None and not sampling.greedy else None
         self.params.copy_(K.pack_sample_params(sampling))
@@ -230,12 +233,29 @@ class DeviceDecoder:
             t.copy_(v)
         self.bufs.hist.copy_(hist)
         self.bufs.slot.zero_()
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            for _ in range(self.k):
-                self._step_body()
-        self.graph = g
+        # Position buckets: the decode-attention grid is sized by its split cap, and
+        # a max_seq-sized grid's idle workgroups cost every layer (8B, max_seq 4096:
+        # 353 -> 368 tok/s at short context).  One graph per cap; launch() replays
+        # the smallest whose cap covers the live length.
+        from ...ops import hip as K
+        full = K.attn_max_split(self.m.stack.max_seq)
+        self.graphs = {}
+        for cap in sorted({min(c, full) for c in (8, 16, 32, 64)}):
+            g = torch.cuda.CUDAGraph()
+            with K.attn_split_cap(cap), torch.cuda.graph(g):
+                for _ in range(self.k):
+                    self._step_body()
+            self.graphs[cap] = g
+        self.graph = self.graphs[max(self.graphs)]
         torch.cuda.synchronize()
+
+    def _graph_for(self, tk: int) -> torch.cuda.CUDAGraph:
+        from ...ops import hip as K
+        need = K.attn_splits(tk)
+        for cap in sorted(self.graphs):
+            if cap >= need:
+                return self.graphs[cap]
+        return self.graph
 
     def start(self, prompt: list[int]) -> int:
         """Prefill `prompt` at position 0 and select the first token (returned)."""
@@ -277,7 +297,8 @@ class DeviceDecoder:
     def launch(self) -> None:
         """Enqueue `self.k` decode steps (one graph replay; async)."""
         if self.graph is not None:
-            self.graph.replay()
+            # live length of the last step of this replay (+1: sampled mode pushes)
+            self._graph_for(self.host_pos + self.k + 1).replay()
         else:
             self._step_body()
         if self.greedy:  # greedy steps advance pos on the device; sampled ones via push()

@@ -31,6 +31,7 @@ _SIGS = {
     "cake_gemv_norm_f32": [I, P, P, F, P, I, I, P, P],
     "cake_attn_decode": [I, P, P, P, P, I, I, I, I, F, P, P, P, P],
     "cake_attn_set_min_keys": [I],
+    "cake_attn_set_split_cap": [I],
     "cake_wave_reduce_probe": [P, P, P],
     "cake_embed": [I, P, P, I, I, P, P],
     "cake_rmsnorm": [I, P, P, F, I, I, P, P],

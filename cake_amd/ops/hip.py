@@ -143,9 +143,42 @@ def attn_workspace_numel(nh: int, hd: int, S: int) -> int:
     return nh * 64 * (hd + 2)
 
 
+_ATTN_MIN_KEYS = [64]
+
+
 def attn_set_min_keys(n: int) -> None:
     """Minimum keys per decode-attention split (multiple of 64; default 64)."""
     check(kernels().cake_attn_set_min_keys(int(n)), "attn_set_min_keys")
+    _ATTN_MIN_KEYS[0] = int(n)
+
+
+def attn_max_split(S: int) -> int:
+    """Splits per kv head of a max_seq = S launch (attention.hip attn_max_split)."""
+    return min((S + 63) // 64, 64)
+
+
+def attn_splits(Tk: int) -> int:
+    """Splits the decode-attention kernel uses at live length Tk with no cap (the
+    device-side policy of attn_core.h, mirrored for choosing a capped graph)."""
+    keys = max(_ATTN_MIN_KEYS[0], 128 if Tk > 1024 else 64, -(-Tk // 64))
+    return -(-Tk // keys)
+
+
+class attn_split_cap:
+    """Context manager: decode-attention launches (and graph captures) inside it use at
+    most `cap` splits per kv head (correct at any live length; fastest where
+    attn_splits(Tk) <= cap)."""
+
+    def __init__(self, cap: int):
+        self.cap = int(cap)
+
+    def __enter__(self):
+        check(kernels().cake_attn_set_split_cap(self.cap), "attn_set_split_cap")
+        return self
+
+    def __exit__(self, *exc):
+        check(kernels().cake_attn_set_split_cap(0), "attn_set_split_cap")
+        return False
 
 
 # ---------------------------------------------------------------------------

@@ -32,6 +32,13 @@ VARIANTS = {
     "best_x2048": {**BEST, "x16": (4, 4, 2048)},
     "best_x2pf4": {**BEST, "x16": (2, 4, 1024)},
     "best_x8pf4": {**BEST, "x16": (8, 4, 1024)},
+    "best_sw2pf8": {**BEST, "swiglu": (2, 8, 512)},
+    "best_sw4pf8": {**BEST, "swiglu": (4, 8, 512)},
+    "best_sw2pf4_768": {**BEST, "swiglu": (2, 4, 768)},
+    "best_sw2pf8_1024": {**BEST, "swiglu": (2, 8, 1024)},
+    "best_x4pf8": {**BEST, "x16": (4, 8, 1024)},
+    "best_x2pf8": {**BEST, "x16": (2, 8, 1024)},
+    "best_q4pf4": {**BEST, "qkv": (4, 4, 1024)},
 }
 if os.environ.get("SWEEP_VARIANTS"):
     VARIANTS = {k: v for k, v in VARIANTS.items()

@@ -65,6 +65,37 @@ def test_device_decoder_matches_host_loop(cuda, use_graph, k):
     assert len(st.step_ms) == 11 and all(x > 0 for x in st.step_ms)
 
 
+def test_device_decoder_crosses_split_buckets(cuda):
+    """Graphs captured per attention split cap: a generation whose live length crosses
+    the 512-key bucket edge (cap 8 -> 16) matches the host loop token for token."""
+    from cake_amd.models.llama3.decode_loop import run_decode
+    from cake_amd.models.llama3.model import DeviceDecoder
+    from cake_amd.ops import hip as K
+    from cake_amd.ops import reference as R
+
+    cfg = preset("llama3-8b", num_hidden_layers=2, vocab_size=2048, intermediate_size=1024,
+                 hidden_size=512, num_attention_heads=8, num_key_value_heads=2)
+    model = random_model(cfg, "cuda:0", torch.bfloat16, max_seq=4096, seed=4)
+    g = torch.Generator().manual_seed(9)
+    prompt = torch.randint(0, 2048, (503,), generator=g).tolist()
+    toks = list(prompt)
+    logits = model.forward(prompt, 0)
+    host = []
+    for _ in range(16):
+        t = int(torch.argmax(R.apply_repeat_penalty(logits, 1.1, toks[-16:])))
+        host.append(t)
+        toks.append(t)
+        logits = model.forward([t], len(toks) - 1)
+    dec = DeviceDecoder(model, repeat_penalty=1.1, repeat_last_n=16, greedy=True)
+    first = dec.start(prompt)
+    dec.capture()
+    assert sorted(dec.graphs) == [8, 16, 32, 64]
+    assert dec._graph_for(500) is dec.graphs[8] and dec._graph_for(600) is dec.graphs[16]
+    assert K.attn_splits(4096) == 32 and K.attn_splits(8000) == 63
+    st = run_decode(dec, 15)
+    assert [first] + st.tokens == host
+
+
 def test_pipeline_engine_single_rank_streams(cuda):
     """The RCCL pipeline's graph bodies (world=1, 2 streams) == DeviceDecoder per stream."""
     from cake_amd.models.llama3.decode_loop import run_decode
