@@ -519,17 +519,29 @@ class TPEngine:
         torch.cuda.synchronize(self.device)
         for t, v in zip((b.tok, b.pos, b.hist_len, b.hist, b.slot), saved):
             t.copy_(v)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self._step_body()
-        self.graph = g
+        # one graph per attention split cap (position buckets, as DeviceDecoder.capture);
+        # every rank picks the same one from the same host position
+        from ..ops import hip as K
+        full = K.attn_max_split(self.max_seq)
+        self.graphs = {}
+        for cap in sorted({min(c, full) for c in (8, 16, 32, 64)}):
+            g = torch.cuda.CUDAGraph()
+            with K.attn_split_cap(cap), torch.cuda.graph(g):
+                self._step_body()
+            self.graphs[cap] = g
+        self.graph = self.graphs[max(self.graphs)]
         torch.cuda.synchronize(self.device)
+
+    def _graph_for(self, tk: int):
+        from ..ops import hip as K
+        need = K.attn_splits(tk)
+        return next((self.graphs[c] for c in sorted(self.graphs) if c >= need), self.graph)
 
     def launch(self) -> None:
         """Enqueue one decode step (async on the HIP path)."""
         if self.hip:
             if self.graph is not None:
-                self.graph.replay()
+                self._graph_for(self.host_pos + 2).replay()
             else:
                 self._step_body()
         else:
