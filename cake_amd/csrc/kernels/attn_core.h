@@ -26,7 +26,7 @@
 // (Rejected after measuring: attention and o_proj as one launch whose o_proj
 // blocks stream their weights while attention runs and wait on an agent-scope
 // counter — 17.3 us vs 5.5 + 7.2 us for the two launches, the attention loads
-// queue behind the weight stream; profiles/r2_attn_oproj_fused_rejected.json.)
+// queue behind the weight stream; profiles/r2_decode_rejected_experiments.jsonl.)
 #pragma once
 #include "common.h"
 
