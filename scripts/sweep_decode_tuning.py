@@ -39,6 +39,13 @@ VARIANTS = {
     "best_x4pf8": {**BEST, "x16": (4, 8, 1024)},
     "best_x2pf8": {**BEST, "x16": (2, 8, 1024)},
     "best_q4pf4": {**BEST, "qkv": (4, 4, 1024)},
+    "best_q2pf4": {**BEST, "qkv": (2, 4, 1024)},
+    "best_sw2pf4_1024": {**BEST, "swiglu": (2, 4, 1024)},
+    "best_x2pf4_512": {**BEST, "x16": (2, 4, 512)},
+    "best_x4pf4_512": {**BEST, "x16": (4, 4, 512)},
+    "best_x4pf0": {**BEST, "x16": (4, 0, 1024)},
+    "best_head_u2": {**BEST, "norm_f32": (2, 4, 256)},
+    "best_head_512": {**BEST, "norm_f32": (4, 4, 512)},
 }
 if os.environ.get("SWEEP_VARIANTS"):
     VARIANTS = {k: v for k, v in VARIANTS.items()
@@ -46,7 +53,9 @@ if os.environ.get("SWEEP_VARIANTS"):
 
 
 def main():
-    m = random_model("llama3-8b", "cuda:0", torch.bfloat16, max_seq=1024)
+    model = os.environ.get("SWEEP_MODEL", "llama3-8b")
+    m = random_model(model, "cuda:0", torch.bfloat16, max_seq=1024)
+    steps = int(os.environ.get("SWEEP_STEPS", "96"))
     prompt = list(range(100, 132))
     res = {k: [] for k in VARIANTS}
     for rnd in range(3):
@@ -59,9 +68,9 @@ def main():
             run_decode(dec, 8)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            run_decode(dec, 96)
+            run_decode(dec, steps)
             torch.cuda.synchronize()
-            res[name].append(96 / (time.perf_counter() - t0))
+            res[name].append(steps / (time.perf_counter() - t0))
             del dec
     for name, v in res.items():
         print(json.dumps({"variant": name, "tok_s": [round(x, 1) for x in v],
