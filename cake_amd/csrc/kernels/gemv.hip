@@ -528,8 +528,11 @@ CAKE_API int cake_swiglu(int dt, const float* resid, const void* norm_w, float e
   if (K % 8) return (int)hipErrorInvalidValue;
   const size_t lds = (size_t)K * sizeof(float);
   const GemvTune t = g_tune[kSwiglu];
+  // at least one block per 28 rows (7 row pairs per wave): 70B's I = 28672 runs 1024
+  // blocks (+0.7 %, profiles/r2_decode_gemv_tuning_70b.jsonl), 8B's 14336 the tuned 512
+  const int mb = t.MB > (I + 27) / 28 ? t.MB : (I + 27) / 28;
   DISPATCH_DT(dt, DISPATCH_TUNE(t, K, CAKE_NX_NORM(K, hipLaunchKernelGGL((swiglu_kernel<DT, U, PF, NX>),
-                                                      dim3(grid_for(I, t.MB)), dim3(kGemvThreads),
+                                                      dim3(grid_for(I, mb)), dim3(kGemvThreads),
                                                       lds, st, resid, (const uint16_t*)norm_w, eps,
                                                       (const uint16_t*)wg, (const uint16_t*)wu, K,
                                                       I, (uint16_t*)act))));
