@@ -43,6 +43,7 @@ struct FlashArgs {
   float scale_log2;  // softmax scale * log2(e)
   int causal;
   int pos0;          // absolute position of query row 0 (keys start at 0)
+  int pair;          // v2 causal: workgroup x runs q tiles x and n-1-x (equal work)
 };
 
 constexpr int kBM = 64, kBN = 64, kKP = 8;  // rows, keys, LDS row pad (elements)
@@ -294,9 +295,17 @@ __global__ __launch_bounds__(64 * NW, 2) void flash2_fwd_kernel(FlashArgs a) {
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int l32 = lane & 31, h = lane >> 5;
-  const int mblk = blockIdx.x * (32 * NW);
-  const int qrow = mblk + wave * 32 + l32;
   const int hq = blockIdx.y, b = blockIdx.z;
+  // Causal load balance: q tile x costs ~x key tiles, so with a grid that fills the
+  // chip once, the last tiles' workgroups set the kernel time at ~2x the mean.
+  // Paired, workgroup x runs tiles x and n-1-x back to back (n+1 tiles' work each).
+  const int nqt = (a.N + 32 * NW - 1) / (32 * NW);
+  const int bx = blockIdx.x;
+  const int npass = (a.pair && nqt - 1 - bx != bx) ? 2 : 1;
+  for (int pass = 0; pass < npass; ++pass) {
+  if (pass) __syncthreads();  // every wave is past its LDS reads of the first tile
+  const int mblk = (pass ? nqt - 1 - bx : bx) * (32 * NW);
+  const int qrow = mblk + wave * 32 + l32;
   const int hk = hq / (a.H / a.Hkv);
   const uint16_t* qb = a.q + b * a.q_sb + hq * a.q_sh;
   const uint16_t* kb = a.k + b * a.k_sb + hk * a.k_sh;
@@ -466,6 +475,7 @@ __global__ __launch_bounds__(64 * NW, 2) void flash2_fwd_kernel(FlashArgs a) {
         }
       }
   }
+  }  // pass
 }
 
 }  // namespace cake
@@ -473,6 +483,7 @@ __global__ __launch_bounds__(64 * NW, 2) void flash2_fwd_kernel(FlashArgs a) {
 using namespace cake;
 
 static int g_flash_impl = -1;  // -1: from CAKE_FLASH_IMPL (default 2)
+static long long g_flash_pair_min = 512;  // unpaired workgroups needed before pairing
 
 static int flash_impl() {
   if (g_flash_impl < 0) {
@@ -497,8 +508,13 @@ static int launch_flash(const FlashArgs& a, hipStream_t st) {
     int nw = 4;
     const int nw_min = a.D <= 64 ? 1 : 2;  // DP=128 staging registers need >= 2 waves
     while (nw > nw_min && (long long)((a.N + 32 * nw - 1) / (32 * nw)) * a.H * a.B < 32) nw >>= 1;
-    const dim3 g2((a.N + 32 * nw - 1) / (32 * nw), a.H, a.B);
-#define CAKE_FL2(P, W) hipLaunchKernelGGL((flash2_fwd_kernel<DT, P, W>), g2, dim3(64 * W), 0, st, a)
+    const int nqt = (a.N + 32 * nw - 1) / (32 * nw);
+    FlashArgs p = a;
+    // pair causal q tiles once the unpaired grid fills every CU twice (below that,
+    // halving the workgroups costs more parallelism than the balance gains)
+    p.pair = a.causal && nqt >= 2 && (long long)nqt * a.H * a.B >= g_flash_pair_min;
+    const dim3 g2(p.pair ? (nqt + 1) / 2 : nqt, a.H, a.B);
+#define CAKE_FL2(P, W) hipLaunchKernelGGL((flash2_fwd_kernel<DT, P, W>), g2, dim3(64 * W), 0, st, p)
     if (a.D <= 64) {
       if (nw == 4) CAKE_FL2(64, 4); else if (nw == 2) CAKE_FL2(64, 2); else CAKE_FL2(64, 1);
     } else {
@@ -527,6 +543,8 @@ static int launch_flash(const FlashArgs& a, hipStream_t st) {
 
 // 1 = the 16-row 16x16x32 kernel, 2 = the 32x32x16 swapped-QKᵀ kernel (when shapes allow)
 CAKE_API void cake_flash_set_impl(int v) { g_flash_impl = v; }
+// causal q-tile pairing threshold (unpaired workgroups); <= 0 never pairs
+CAKE_API void cake_flash_set_pair_min(long long n) { g_flash_pair_min = n > 0 ? n : (1ll << 62); }
 
 // strides in ELEMENTS: s[0]=batch, s[1]=head, s[2]=row for q, k, v, o (12 values)
 CAKE_API int cake_flash_attn(int dt, const void* q, const void* k, const void* v, void* o, int B,
@@ -538,7 +556,7 @@ CAKE_API int cake_flash_attn(int dt, const void* q, const void* k, const void* v
               B, H, Hkv, N, M, D,
               strides[0], strides[1], strides[2], strides[3], strides[4], strides[5],
               strides[6], strides[7], strides[8], strides[9], strides[10], strides[11],
-              scale * 1.4426950408889634f, causal, pos0};
+              scale * 1.4426950408889634f, causal, pos0, 0};
   if (dt == kBF16) return launch_flash<kBF16>(a, st);
   if (dt == kF16) return launch_flash<kF16>(a, st);
   return (int)hipErrorInvalidValue;

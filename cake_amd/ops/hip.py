@@ -416,6 +416,12 @@ def flash_set_impl(v: int) -> None:
     kernels().cake_flash_set_impl(int(v))
 
 
+def flash_set_pair_min(n: int) -> None:
+    """Causal flash (v2): pair q tiles x / n-1-x per workgroup once the unpaired grid has
+    at least n workgroups (default 512; <= 0 never pairs)."""
+    kernels().cake_flash_set_pair_min(int(n))
+
+
 def flash_attn(q, k, v, out, scale: float, causal: bool = False, pos0: int = 0):
     """out = softmax(q kᵀ * scale [+causal mask]) v on MFMA.
 

@@ -56,6 +56,29 @@ def test_flash_attn(cuda, dt, B, H, Hkv, N, M, D, causal, pos0, impl):
     torch.testing.assert_close(out.float(), _ref_attn(q, k, v, scale, causal, pos0), **_tol(dt))
 
 
+@pytest.mark.parametrize("N,pos0,D", [(1400, 0, 128), (2048, 0, 64), (300, 37, 128),
+                                       (128, 0, 128)])
+@pytest.mark.parametrize("pair_min", [1, 0])
+def test_flash_causal_pairing(cuda, N, pos0, D, pair_min):
+    """Causal q-tile pairing (workgroup x runs tiles x and n-1-x; odd tile counts leave
+    one unpaired middle tile) forced on / off gives the reference result."""
+    from cake_amd.ops import hip as K
+    torch.manual_seed(1)
+    dt, H, Hkv = torch.bfloat16, 8, 2
+    M = N + pos0
+    q = torch.randn(1, N, H, D, device=cuda).to(dt).transpose(1, 2)
+    k = torch.randn(1, M, Hkv, D, device=cuda).to(dt).transpose(1, 2)
+    v = torch.randn(1, M, Hkv, D, device=cuda).to(dt).transpose(1, 2)
+    out = torch.full((1, N, H, D), float("nan"), device=cuda, dtype=dt).transpose(1, 2)
+    K.flash_set_pair_min(pair_min)
+    try:
+        K.flash_attn(q, k, v, out, 1 / math.sqrt(D), True, pos0)
+    finally:
+        K.flash_set_pair_min(512)
+    torch.testing.assert_close(out.float(), _ref_attn(q, k, v, 1 / math.sqrt(D), True, pos0),
+                               **_tol(dt))
+
+
 @pytest.mark.parametrize("impl", [1, 2])
 def test_flash_attn_softmax_rescale_branch(cuda, impl):
     """A late key tile with a much larger score forces the online-softmax rescale."""
