@@ -484,6 +484,7 @@ using namespace cake;
 
 static int g_flash_impl = -1;  // -1: from CAKE_FLASH_IMPL (default 2)
 static long long g_flash_pair_min = 512;  // unpaired workgroups needed before pairing
+static int g_flash_nw = 0;                 // v2 waves per workgroup override (0 = auto)
 
 static int flash_impl() {
   if (g_flash_impl < 0) {
@@ -508,6 +509,7 @@ static int launch_flash(const FlashArgs& a, hipStream_t st) {
     int nw = 4;
     const int nw_min = a.D <= 64 ? 1 : 2;  // DP=128 staging registers need >= 2 waves
     while (nw > nw_min && (long long)((a.N + 32 * nw - 1) / (32 * nw)) * a.H * a.B < 32) nw >>= 1;
+    if (g_flash_nw >= nw_min && g_flash_nw <= 4) nw = g_flash_nw;
     const int nqt = (a.N + 32 * nw - 1) / (32 * nw);
     FlashArgs p = a;
     // pair causal q tiles once the unpaired grid fills every CU twice (below that,
@@ -543,6 +545,7 @@ static int launch_flash(const FlashArgs& a, hipStream_t st) {
 
 // 1 = the 16-row 16x16x32 kernel, 2 = the 32x32x16 swapped-QKᵀ kernel (when shapes allow)
 CAKE_API void cake_flash_set_impl(int v) { g_flash_impl = v; }
+CAKE_API void cake_flash_set_nw(int nw) { g_flash_nw = nw; }
 // causal q-tile pairing threshold (unpaired workgroups); <= 0 never pairs
 CAKE_API void cake_flash_set_pair_min(long long n) { g_flash_pair_min = n > 0 ? n : (1ll << 62); }
 

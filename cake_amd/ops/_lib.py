@@ -107,6 +107,7 @@ _SIGS.update({
     "cake_flash_attn": [I, P, P, P, P, I, I, I, I, I, I, P, F, I, I, P],
     "cake_flash_set_impl": [I],
     "cake_flash_set_pair_min": [C.c_longlong],
+    "cake_flash_set_nw": [I],
     "cake_groupnorm": [I, P, P, P, I, I, C.c_longlong, I, F, I, P, P, P],
     "cake_groupnorm_nhwc": [I, P, P, P, I, I, I, I, F, I, P, P, P, P, P],
     "cake_groupnorm_nhwc_splits": [I],
