@@ -139,6 +139,15 @@ __device__ __forceinline__ uint4 ld_nt16(const uint4* p) {
 
 __device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
 
+// tanh-approximated GELU (candle's gelu / diffusers "gelu-approximate"):
+// 0.5 x (1 + tanh(u)) == x * sigmoid(2u), u = sqrt(2/pi) (x + 0.044715 x^3) — one
+// v_exp + one v_rcp instead of libm tanhf (~50 instructions with a branch), which
+// made the GEGLU epilogue of SD's FF-in GEMM VALU-bound.
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float u2 = 1.5957691216057308f * fmaf(0.044715f * x, x * x, x);
+  return x * __builtin_amdgcn_rcpf(1.f + __expf(-u2));
+}
+
 // MFMA operand / accumulator vectors (16x16x32: 8 x 16-bit per lane, 4 f32 acc)
 typedef __bf16 cbf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 cf16x8 __attribute__((ext_vector_type(8)));

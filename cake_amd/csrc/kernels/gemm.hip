@@ -77,10 +77,6 @@ __device__ __forceinline__ int wrow(const GemmArgs& g, int v) {
   return w < 16 ? blk * 16 + w : g.half + blk * 16 + (w - 16);
 }
 
-__device__ __forceinline__ float gelu_tanh(float x) {
-  const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
-  return 0.5f * x * (1.f + tanhf(u));
-}
 
 // MFMA with the accumulator pinned to AGPRs (tied "+a" operand): for 128x128 wave
 // tiles (256 accumulator registers) hipcc's own allocation rotates the accumulators

@@ -139,11 +139,6 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const uint16_t* __restri
                          to_f32<DT>(beta[i]));
 }
 
-__device__ __forceinline__ float gelu_tanh(float x) {
-  const float k = 0.7978845608028654f;  // sqrt(2/pi)
-  return 0.5f * x * (1.f + tanhf(k * (x + 0.044715f * x * x * x)));
-}
-
 // h [rows, 2F] -> out [rows, F] = h[:, :F] * gelu_tanh(h[:, F:])
 template <int DT>
 __global__ void geglu_kernel(const uint16_t* __restrict__ h, long long rows, int F,
