@@ -23,11 +23,9 @@ __device__ __forceinline__ float bf16_to_f32(uint16_t h) {
   return __uint_as_float(((uint32_t)h) << 16);
 }
 
+// round to nearest even, NaN stays NaN: one v_cvt_pk_bf16_f32 on gfx950
 __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);  // NaN
-  u += 0x7fffu + ((u >> 16) & 1u);  // round to nearest even
-  return (uint16_t)(u >> 16);
+  return __builtin_bit_cast(uint16_t, (__bf16)f);
 }
 
 __device__ __forceinline__ float f16_to_f32(uint16_t h) {
@@ -137,7 +135,11 @@ __device__ __forceinline__ uint4 ld_nt16(const uint4* p) {
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
-__device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
+// x * sigmoid(x) with v_rcp (1 ulp) instead of the IEEE division sequence: the
+// SwiGLU / SiLU GEMM epilogues evaluate it once per output element
+__device__ __forceinline__ float silu(float x) {
+  return x * __builtin_amdgcn_rcpf(1.f + __expf(-x));
+}
 
 // tanh-approximated GELU (candle's gelu / diffusers "gelu-approximate"):
 // 0.5 x (1 + tanh(u)) == x * sigmoid(2u), u = sqrt(2/pi) (x + 0.044715 x^3) — one
