@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Headline benchmark: Llama-3 batch-1 greedy decode tokens/s (+ p50/p99 per-token latency).
+"""Headline benchmark: Llama-3 batch-1 decode tokens/s (+ p50/p99 per-token latency).
 
 BASELINE.json metric: "decode tokens/sec + p50 per-token latency, Llama-3-8B
 1-worker & 70B 8-worker".  The reference's formula (cake-core/src/cake/master.rs
@@ -9,23 +9,23 @@ timed region and exactly K decode steps are timed.
 * N = 1: all 32 layers local on one MI355X; the whole step (embedding, layers,
   lm_head, repeat penalty 1.1 over the last 128 tokens, argmax, next-token
   bookkeeping) is one hipGraph replay; the host reads each token back one step
-  behind the GPU.
+  behind the GPU.  ``llama3_70b.single`` is the same for Llama-3-70B (135 GB fits
+  one 288 GB MI355X).
 * N > 1 (one rank per GPU; launched by torchrun, or self-launched: with no
   WORLD_SIZE in the environment bench.py spawns the N ranks itself and only
-  relays rank 0's JSON line), default ``--parallel tp``: every rank holds 1/N
-  of every layer (heads, MLP rows, vocabulary) and streams 1/N of the weights
-  per token; the two per-layer all-reduces and the argmax max are device-side
-  one-shot kernels over xGMI inside each rank's decode graph
-  (parallel/tensor_parallel.py).  ``--parallel pp``: the reference's layer
-  sharding — the layers are sharded contiguously over the N
-  ranks as a cake topology would place them (rank 0 = master with
-  embedding/lm_head + the first shard); the hidden state hops rank→rank as
-  device-side peer stores over xGMI captured inside every rank's decode graph
-  (cake's TCP hop; --hop dist = host-issued RCCL p2p), the last
-  shard returns it to the master.  Batch-1 layer sharding does not add
-  throughput (one token walks the ranks in sequence): the curve is strong
-  scaling of ONE decode stream (--streams S > 1 keeps S sequences in flight and
-  reports their aggregate instead).
+  relays rank 0's JSON line): ``value`` is the reference's parallelism, layer
+  sharding (``--parallel pp``, cake-core/src/models/llama3/llama.rs:95-114): the
+  layers are sharded contiguously over the N ranks as a cake topology would
+  place them (rank 0 = master with embedding/lm_head + the first shard); the
+  hidden state hops rank->rank as device-side peer stores over xGMI (bf16
+  payload, as the reference ships the model dtype) captured inside every rank's
+  decode graph (--hop dist = host-issued RCCL p2p), the last shard returns it to
+  the master.  Batch-1 layer sharding does not add throughput (one token walks
+  the ranks in sequence): the curve is strong scaling of ONE decode stream.
+  Extra fields (``--no-extras`` skips them): ``tp`` = tensor parallelism
+  (beyond the reference: every rank streams 1/N of every layer, device-side
+  all-reduces over xGMI) and ``llama3_70b`` = the same two modes for 70B — the
+  BASELINE's "70B 8-worker" point is ``llama3_70b.pp`` at N = 8.
 
 Weights are random-init of the named architecture (no network, no checkpoints);
 EOS is ignored so exactly K tokens are generated.
@@ -62,9 +62,11 @@ def _args(argv=None):
     ap.add_argument("--streams", type=int, default=1,
                     help="N>1: concurrent sequences in the pipeline (1 = cake's single-sequence "
                          "pipeline, the headline; S > 1 = aggregate throughput of S sequences)")
-    ap.add_argument("--parallel", default="tp", choices=["tp", "pp"],
-                    help="N > 1: tp = tensor-parallel (every rank 1/N of every layer, default), "
-                         "pp = the reference's layer sharding (pipeline)")
+    ap.add_argument("--parallel", default="pp", choices=["tp", "pp"],
+                    help="N > 1 headline: pp = the reference's layer sharding (default), "
+                         "tp = tensor-parallel (every rank 1/N of every layer)")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="headline only: skip the tp / llama3_70b sub-records")
     ap.add_argument("--allreduce", default="ipc", choices=["ipc", "dist"],
                     help="tp all-reduce: device-side one-shot kernels over xGMI, or "
                          "torch.distributed")
@@ -148,7 +150,9 @@ def bench_cpu_single(a) -> None:
           1, {"device": "cpu"})
 
 
-def bench_single(a) -> None:
+def measure_single(a, model_name: str, steps: int, warmup: int, dump_tokens=None) -> dict:
+    """All layers local on cuda:0 (DeviceDecoder: one graph replay per token)."""
+    import gc
     from cake_amd.models.llama3.decode_loop import run_decode
     from cake_amd.models.llama3.factory import parse_dtype, random_model
     from cake_amd.models.llama3.model import DeviceDecoder
@@ -157,10 +161,10 @@ def bench_single(a) -> None:
     torch.cuda.set_device(0)
     dtype = parse_dtype(a.dtype)
     t0 = time.time()
-    model = random_model(a.model, "cuda:0", dtype, max_seq=a.max_seq)
+    model = random_model(model_name, "cuda:0", dtype, max_seq=a.max_seq)
     torch.cuda.synchronize()
     load_s = time.time() - t0
-    print(f"[bench] model {a.model} random-init in {load_s:.1f}s, "
+    print(f"[bench] model {model_name} random-init in {load_s:.1f}s, "
           f"HBM {torch.cuda.memory_allocated() / 2**30:.1f} GiB", file=sys.stderr, flush=True)
     dec = DeviceDecoder(model, repeat_penalty=a.repeat_penalty, repeat_last_n=a.repeat_last_n,
                         greedy=True, use_graph=not a.no_graph, steps_per_graph=a.steps_per_graph)
@@ -173,19 +177,94 @@ def bench_single(a) -> None:
     torch.cuda.synchronize()
     ttft = (time.perf_counter() - t0) * 1e3
     dec.capture()
-    if a.warmup:
-        run_decode(dec, a.warmup)
+    if warmup:
+        run_decode(dec, warmup)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    st = run_decode(dec, a.steps)
+    st = run_decode(dec, steps)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    if a.dump_tokens:
-        with open(a.dump_tokens, "w") as f:
+    if dump_tokens:
+        with open(dump_tokens, "w") as f:
             json.dump([dec.bufs.hist[:int(dec.bufs.hist_len.item())].tolist()], f)
-    _emit(a, a.steps / dt, dt * 1e3 / a.steps, st.percentile(50), st.percentile(99), 1,
-          {"ttft_ms_prefill": round(ttft, 3), "graph": not a.no_graph,
-           "steps_per_graph": dec.k, **hbm_mib()})
+    out = {"tokens_per_sec": round(steps / dt, 3), "ms_per_step": round(dt * 1e3 / steps, 4),
+           "p50_token_latency_ms": round(st.percentile(50), 4),
+           "p99_token_latency_ms": round(st.percentile(99), 4),
+           "ttft_ms_prefill": round(ttft, 3), "graph": not a.no_graph,
+           "steps_per_graph": dec.k, **hbm_mib()}
+    del dec, model, st
+    gc.collect()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    torch.cuda.reset_peak_memory_stats()
+    return out
+
+
+_MAIN_KEYS = ("tokens_per_sec", "ms_per_step", "p50_token_latency_ms", "p99_token_latency_ms")
+
+
+def _summary(r: dict | None) -> dict | None:
+    """Compact sub-record of one extra measurement."""
+    if r is None:
+        return None
+    keep = _MAIN_KEYS + ("hop", "hop_us", "hops_per_token", "allreduce", "allreduce_us",
+                         "layers_per_rank", "hbm_peak_mib_max_rank", "hbm_peak_mib",
+                         "ttft_ms_prefill")
+    return {k: r[k] for k in keep if k in r}
+
+
+def _extra_runs(a):
+    """(key path, model, mode) of the sub-records next to the headline."""
+    if a.no_extras or a.cpu or a.model != "llama3-8b":
+        return []
+    other = "tp" if a.parallel == "pp" else "pp"
+    return [((other,), "llama3-8b", other), (("llama3_70b", "pp"), "llama3-70b", "pp"),
+            (("llama3_70b", "tp"), "llama3-70b", "tp")]
+
+
+def bench_single(a) -> None:
+    r = measure_single(a, a.model, a.steps, a.warmup, a.dump_tokens)
+    extra = {k: v for k, v in r.items() if k not in _MAIN_KEYS}
+    if not a.no_extras and a.model == "llama3-8b":
+        # the 70B point on one GPU (135 GB of bf16 weights in 288 GB of HBM)
+        try:
+            extra["llama3_70b"] = {"single": _summary(measure_single(a, "llama3-70b", a.steps,
+                                                                     a.warmup))}
+        except Exception as e:  # noqa: BLE001  (the headline stands; the miss is reported)
+            extra["llama3_70b"] = {"single": None, "error": f"{type(e).__name__}: {e}"[:300]}
+    _emit(a, r["tokens_per_sec"], r["ms_per_step"], r["p50_token_latency_ms"],
+          r["p99_token_latency_ms"], 1, extra)
+
+
+def bench_multi(a) -> None:
+    """N ranks (torchrun or self-launched): the headline mode, then the extras."""
+    import torch.distributed as dist
+    from cake_amd.parallel.pipeline_bench import DistEnv, measure_pipeline
+    from cake_amd.parallel.tp_bench import measure_tp, tp_supported
+    env = DistEnv(a)
+    try:
+        measure = {"pp": measure_pipeline, "tp": measure_tp}
+        head = measure[a.parallel](a, env, a.model, a.steps, a.warmup, a.dump_tokens)
+        extra = {}
+        for path, model, mode in _extra_runs(a):
+            if mode == "tp" and not tp_supported(model, env.world):
+                r = {"skipped": f"tp{env.world} does not divide the KV heads"}
+            else:
+                r = _summary(measure[mode](a, env, model, a.steps, a.warmup))
+            if env.rank == 0:
+                d = extra
+                for k in path[:-1]:
+                    d = d.setdefault(k, {})
+                d[path[-1]] = r
+        if env.rank == 0:
+            rest = {k: v for k, v in head.items() if k not in _MAIN_KEYS}
+            if a.parallel == "pp":
+                rest["scaling"] = "weak" if head["streams"] == env.world else "strong"
+            _emit(a, head["tokens_per_sec"], head["ms_per_step"], head["p50_token_latency_ms"],
+                  head["p99_token_latency_ms"], env.world, {**rest, **extra})
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
 
 
 def _free_port() -> int:
@@ -252,12 +331,7 @@ def main(argv=None) -> int:
         return self_launch(a, argv)
     # under torchrun (WORLD_SIZE set) the distributed path runs even at N = 1
     if world > 1 or a.gpus > 1 or "WORLD_SIZE" in os.environ:
-        if a.parallel == "tp":
-            from cake_amd.parallel.tp_bench import bench_tp
-            bench_tp(a, _emit)
-        else:
-            from cake_amd.parallel.pipeline_bench import bench_pipeline
-            bench_pipeline(a, _emit)
+        bench_multi(a)
     elif a.cpu:
         bench_cpu_single(a)
     else:

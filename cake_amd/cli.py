@@ -82,6 +82,11 @@ def build_parser() -> argparse.ArgumentParser:
     a("--parallel", choices=["pp", "tp"], default="pp",
       help="with --transport rccl: pp = the topology's layer sharding (reference), "
            "tp = tensor parallel (every rank 1/N of every layer; topology layers ignored)")
+    a("--hop", choices=["ipc", "dist"], default="ipc",
+      help="--transport rccl pp: ipc = device-side hops captured in each rank's decode graph, "
+           "dist = host-issued RCCL p2p per hop")
+    a("--hop-dtype", choices=["f32", "bf16"], default="f32",
+      help="hidden-state payload of an ipc hop (bf16 = the reference's 16-bit transport)")
     a("--max-seq-len", type=int, default=4096)
     a("--no-graph", action="store_true", help="disable hipGraph capture of the decode step")
     a("--trace", default=None, help="write a chrome-trace JSON of each text generation")

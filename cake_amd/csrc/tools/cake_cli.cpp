@@ -88,6 +88,9 @@ const Flag kFlags[] = {
      "tcp, rccl (one rank per GPU) or loopback"},
     {"--parallel", "parallel", PyArg::kStr, "pp", "pp|tp", false,
      "rccl: pp = layer sharding (topology), tp = tensor parallel"},
+    {"--hop", "hop", PyArg::kStr, "ipc", "ipc|dist", false,
+     "rccl pp: device-side graph hops (ipc) or host-issued RCCL p2p (dist)"},
+    {"--hop-dtype", "hop_dtype", PyArg::kStr, "f32", "f32|bf16", false, "ipc hop payload"},
     {"--max-seq-len", "max_seq_len", PyArg::kInt, "4096", nullptr, false, "KV cache length"},
     {"--no-graph", "no_graph", PyArg::kBool, "0", nullptr, true, "disable hipGraph decode"},
     {"--trace", "trace", PyArg::kStr, nullptr, nullptr, false, "chrome-trace JSON per generation"},

@@ -25,6 +25,15 @@ tensor device→host→device on both ends, proto/message.rs:22-38).  Here:
   csrc/kernels/hop.hip), captured INSIDE each rank's decode graph, so a rank's
   whole token (receive -> its layers -> send) is one replay and no host is on
   the critical path.  Prefill always uses the dist path.
+* Every decode graph is captured once per attention split cap (position
+  buckets, as the single-GPU DeviceDecoder): all ranks track the live length
+  on the host (``_Stream.dev_pos``) and replay the smallest cap covering it.
+* Serving (:meth:`PipelineEngine.serve` / :meth:`PipelineEngine.generate`): the
+  master gates every unit of work with a host control message on a separate
+  gloo group (``prefill``, ``decode n``, ``stop``) — an idle worker blocks on
+  the host, never inside a device-side receive — and workers enqueue ``n``
+  token replays per ``decode`` message, so with ipc hops a chunk of tokens runs
+  with no host in the loop; the master reads tokens back one replay behind.
 """
 from __future__ import annotations
 
@@ -112,10 +121,11 @@ class _Stream:
         self.bufs = DecodeBuffers(eng.cfg, eng.stack.max_seq, eng.device, eng.stack.dtype,
                                   with_head=eng.is_master, resid=self.resid,
                                   pos=self.hdr[H_POS:H_POS + 1])
-        self.graphs: dict[str, torch.cuda.CUDAGraph] = {}
+        self.graphs: dict = {}     # body key -> {split cap: graph}
         self.send_work = None
         self.host_tokens: list[int] = []   # torch backend bookkeeping (master)
         self.host_pos = 0
+        self.dev_pos = 0   # position of the next decode token (host mirror, every rank)
 
 
 class PipelineEngine:
@@ -164,6 +174,15 @@ class PipelineEngine:
         self.k = max(1, int(steps_per_graph))
         self._skip_hops = False
         self._events: list = []
+        self.inbox, self.peer = {}, {}
+        # host control plane of serve()/generate(): its own gloo group, whose timeout
+        # bounds how long a worker may sit idle between requests
+        self.ctrl = None
+        if dist.is_initialized() and world > 1:
+            import datetime
+            idle = float(os.environ.get("CAKE_SERVE_IDLE_TIMEOUT", str(7 * 86400)))
+            self.ctrl = dist.new_group(list(range(world)), backend="gloo",
+                                       timeout=datetime.timedelta(seconds=idle))
         if hop == "ipc" and world > 1 and self.use_graph and dist.is_initialized():
             self._setup_ipc()  # (ipc hops need the hip backend with graphs: else dist)
 
@@ -330,6 +349,32 @@ class PipelineEngine:
     def _ipc_token_body(self, st: "_Stream") -> None:
         for k in self._ipc_stages():
             self._ipc_stage_body(st, k)
+
+    def hops_per_token(self) -> int:
+        return sum(1 for k in range(1, len(self.runs) + 2) if self._recv_point(k))
+
+    def close(self) -> None:
+        """Collective: unmap the peers' inboxes, free this rank's, drop the extra groups."""
+        if self.hip:
+            torch.cuda.synchronize(self.device)
+        if self.inbox or self.peer:
+            dist.barrier(group=self.group)
+            for t in self.peer.values():
+                t.close()
+            dist.barrier(group=self.group)
+            for t in self.inbox.values():
+                t.close()
+            self.inbox, self.peer = {}, {}
+        for st in self.streams:
+            st.graphs = {}
+        for g in (self.g_up, self.g_down, self.ctrl):
+            if g is not None and g is not self.group:
+                try:
+                    dist.destroy_process_group(g)
+                except Exception:  # noqa: BLE001  (best effort at teardown)
+                    pass
+        self.g_up = self.g_down = self.group
+        self.ctrl = None
 
     def check_hops(self) -> None:
         """Raise if any device-side receive timed out (a peer stopped sending)."""
@@ -507,6 +552,8 @@ class PipelineEngine:
         hdr = st.hdr
         if self.is_master:
             T = len(prompt)
+            if T == 0 or T + 1 > self.stack.max_seq:
+                raise ValueError(f"prompt of {T} tokens does not fit max_seq {self.stack.max_seq}")
             ids = torch.tensor(prompt, dtype=torch.int32, device=self.device)
             h = torch.empty((T, H), device=self.device, dtype=torch.float32)
             self._embed(ids, h)
@@ -538,6 +585,7 @@ class PipelineEngine:
             self._recv(h, self._final_src())
         hdr[H_FLAGS] = 0
         T = len(prompt)
+        st.dev_pos = T
         if self.hip:
             b = st.bufs
             b.hist[:T].copy_(ids)
@@ -565,45 +613,133 @@ class PipelineEngine:
         if int(st.hdr[H_FLAGS].item()) & FLAG_RESET:
             self.stack.reset(sid)
         self.stack.forward(h, self.runs[j].layers, pos0, session=sid)
+        st.dev_pos = pos0 + T
         nxt = self._next(j)
         if nxt != self.rank:
             self._wait(self._send(st.msg, nxt))
             self._wait(self._send(h, nxt))
         return h
 
-    # ------------------------------------------------------------------ serving (message-driven)
+    # ------------------------------------------------------------------ serving (control-gated)
+    def ctrl_send(self, cmd: dict) -> None:
+        """Master: one control message to every worker (host, gloo group)."""
+        if self.ctrl is not None:
+            dist.broadcast_object_list([cmd], src=0, group=self.ctrl)
+
+    def _ctrl_recv(self) -> dict:
+        box = [None]
+        dist.broadcast_object_list(box, src=0, group=self.ctrl)
+        return box[0]
+
     def serve(self) -> None:
-        """Worker loop for interactive use (CLI/API master on rank 0, one stream):
-        every hop starts with the stream's message; its header says PREFILL (a
-        [T, H] block follows), STOP (forward it and return) or decode."""
+        """Worker loop (CLI/API master on rank 0, stream 0): block on the host control
+        channel, then run what the master announced — ``prefill`` (the [T, H] hops
+        follow), ``decode n`` (n token replays: with ipc hops they are enqueued at
+        once and the device-side receives pace them), ``stop``.  A worker never
+        waits in a device-side receive for work that was not announced, so an idle
+        server cannot hit the hop timeout."""
         if self.is_master:
             raise RuntimeError("serve() is the worker loop")
         st = self.streams[0]
-        runs = [j for j in self.my_runs]
         while True:
-            stopped = False
-            for j in runs:
-                self._wait(st.send_work)
-                st.send_work = None
-                self._recv(st.msg, self._prev(j))
-                flags = int(st.hdr[H_FLAGS].item())
-                if flags & FLAG_STOP:
-                    self._wait(self._send(st.msg, self._next(j)))
-                    stopped = True
-                    continue
-                if flags & FLAG_PREFILL:
-                    self._prefill_run(st, j)
-                    continue
-                self._replay(st, f"run{j}", lambda j=j: self._body_run(st, j))
-                st.send_work = self._send(st.msg, self._next(j))
-            if stopped:
+            cmd = self._ctrl_recv()
+            op = cmd.get("op")
+            if op == "stop":
                 self.flush()
+                if self.hop == "ipc" and self.hip:
+                    torch.cuda.synchronize(self.device)
+                    self.check_hops()
                 return
+            if op == "prefill":
+                self.flush()
+                if self.hop == "ipc" and self.hip:
+                    torch.cuda.synchronize(self.device)
+                    self.check_hops()
+                self.prefill(0)
+            elif op == "decode":
+                st.dev_pos = int(cmd["pos"])
+                self.decode(int(cmd["n"]))
+            else:
+                raise RuntimeError(f"unknown control message {cmd!r}")
 
-    def step(self, sid: int = 0) -> int:
-        """Master: one decode step of one stream; returns the new token id."""
-        st = self.streams[sid]
+    def decode_budget(self, sid: int = 0) -> int:
+        """Decode steps that still fit the KV cache / token history of a stream."""
+        return max(0, self.stack.max_seq - 1 - self.streams[sid].dev_pos)
+
+    def generate(self, n: int, on_token=None, eos_ids=None, chunk: int | None = None) -> list[int]:
+        """Master, after prefill(0, prompt): up to n more tokens of stream 0 (clamped to
+        the cache), stopping at EOS.  Work is announced to the workers in chunks; the
+        next chunk is announced before the current one is read back, so the ranks
+        never idle between chunks.  Tokens are read back one replay behind (pinned
+        ring + events); the at most two chunks enqueued past an EOS are discarded
+        (the next prefill resets the stream)."""
+        import collections
+        if not self.is_master:
+            raise RuntimeError("generate() runs on the master")
+        st = self.streams[0]
+        n = min(int(n), self.decode_budget(0))
+        out: list[int] = []
+        if n <= 0:
+            return out
+        ipc = self.hop == "ipc" and self.use_graph
+        chunk = max(1, int(chunk or (16 if ipc else 1)))
         single = self.world == 1 or all(r.owner == 0 for r in self.runs)
+        base = int(st.bufs.hist_len.item()) if self.hip else 0
+        ring = torch.empty(max(1, n), dtype=torch.int32, pin_memory=self.hip and
+                           torch.cuda.is_available()) if self.hip else None
+        pending: collections.deque = collections.deque()
+        issued = 0
+        self._events = []
+        if self.hip:
+            ev0 = torch.cuda.Event(enable_timing=True)
+            ev0.record()
+            self._events.append(ev0)
+
+        def issue() -> None:
+            nonlocal issued
+            c = min(chunk, n - issued)
+            if not single:
+                self.ctrl_send({"op": "decode", "n": c, "pos": st.dev_pos})
+            for _ in range(c):
+                if ipc:
+                    self._replay_ipc_token(st)
+                else:
+                    self._step_host(st, single)
+                i = issued
+                issued += 1
+                if self.hip:
+                    ring[i:i + 1].copy_(st.bufs.hist[base + i:base + i + 1], non_blocking=True)
+                    ev = torch.cuda.Event(enable_timing=True)
+                    ev.record()
+                    self._events.append(ev)
+                    pending.append((i, ev))
+                else:
+                    pending.append((i, None))
+        issue()
+        stop = False
+        while pending:
+            if issued < n and len(pending) <= chunk and not stop:
+                issue()
+            i, ev = pending.popleft()
+            if stop:
+                continue
+            if ev is not None:
+                ev.synchronize()
+                tok = int(ring[i].item())
+            else:
+                tok = st.host_tokens[-(issued - i)]
+            out.append(tok)
+            if on_token is not None:
+                on_token(tok)
+            if eos_ids and tok in eos_ids:
+                stop = True
+        if self.hip:
+            torch.cuda.synchronize(self.device)
+        self.check_hops()
+        return out
+
+    def _step_host(self, st: "_Stream", single: bool) -> None:
+        """One master token with host-issued hops (dist transport / no graphs)."""
         self._wait(st.send_work)
         st.send_work = None
         st.hdr[H_FLAGS] = 0
@@ -615,6 +751,15 @@ class PipelineEngine:
             st.send_work = None
             self._recv(st.msg, self._final_src())
         self._replay(st, "last", lambda: self._body_last(st))
+        st.dev_pos += 1
+
+    def step(self, sid: int = 0) -> int:
+        """Master: one decode step of one stream with host-issued hops; returns the token
+        (tests and the dist transport; workers run decode(1) for it)."""
+        st = self.streams[sid]
+        if self.stack.max_seq - 1 - st.dev_pos <= 0:
+            raise ValueError("KV cache full (max_seq)")
+        self._step_host(st, self.world == 1 or all(r.owner == 0 for r in self.runs))
         if self.hip:
             if self.sampler is not None:
                 return self._host_sample_device(st)
@@ -622,20 +767,11 @@ class PipelineEngine:
         return st.host_tokens[-1]
 
     def shutdown(self) -> None:
-        """Master: send STOP along the chain and wait for it to come back."""
-        if not self.is_master or self.world == 1 or all(r.owner == 0 for r in self.runs):
+        """Master: tell every worker to leave serve()."""
+        if not self.is_master or self.world == 1:
             return
-        st = self.streams[0]
-        self._wait(st.send_work)
-        st.send_work = None
-        st.hdr[H_FLAGS] = FLAG_STOP
-        self._wait(self._send(st.msg, self._first_dst()))
-        for j in self.my_runs:   # master-owned middle runs see STOP too
-            if j in (0, len(self.runs) - 1):
-                continue
-            self._recv(st.msg, self._prev(j))
-            self._wait(self._send(st.msg, self._next(j)))
-        self._recv(st.msg, self._final_src())
+        self.flush()
+        self.ctrl_send({"op": "stop"})
 
     # ------------------------------------------------------------------ decode bodies
     def _body_first(self, st: _Stream) -> None:
@@ -677,51 +813,78 @@ class PipelineEngine:
             st.host_pos += 1
             st.hdr[H_POS] = st.host_pos
 
+    # ------------------------------------------------------------------ graphs
+    def _caps(self) -> list[int]:
+        from ..ops import hip as K
+        full = K.attn_max_split(self.stack.max_seq)
+        return sorted({min(c, full) for c in (8, 16, 32, 64)})
+
+    def _capture_caps(self, fn) -> dict:
+        """One graph of fn per attention split cap (position buckets)."""
+        from ..ops import hip as K
+        out = {}
+        for cap in self._caps():
+            g = torch.cuda.CUDAGraph()
+            with K.attn_split_cap(cap), torch.cuda.graph(g):
+                fn()
+            out[cap] = g
+        return out
+
+    @staticmethod
+    def _pick(graphs: dict, tk: int):
+        """Smallest-cap graph whose split count covers live length tk (any cap is
+        correct; a larger one only launches idle attention workgroups)."""
+        from ..ops import hip as K
+        need = K.attn_splits(tk)
+        for cap in sorted(graphs):
+            if cap >= need:
+                return graphs[cap]
+        return graphs[max(graphs)]
+
     def _replay(self, st: _Stream, key: str, fn) -> None:
         if not self.use_graph:
             fn()
             return
-        g = st.graphs.get(key)
-        if g is None:
+        gs = st.graphs.get(key)
+        if gs is None:
             raise RuntimeError("capture() first")
-        g.replay()
+        self._pick(gs, st.dev_pos + 2).replay()
+
+    def _warm(self, st: _Stream, fn) -> None:
+        """Run fn once outside capture on scratch state (the K/V row written is the
+        cache's last one), then restore the stream's message and token state."""
+        saved = st.msg.clone()
+        st.hdr[H_POS] = self.stack.max_seq - 1
+        keep = None
+        if self.is_master:
+            b = st.bufs
+            keep = [t.clone() for t in (b.tok, b.hist, b.hist_len, b.slot)]
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            fn()
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        st.msg.copy_(saved)
+        if keep is not None:
+            for t, v in zip((b.tok, b.hist, b.hist_len, b.slot), keep):
+                t.copy_(v)
 
     def capture(self) -> None:
-        """Capture one hipGraph per (stream, body) — RCCL hops stay outside.  With ipc
-        hops the receives/sends are inside the graphs: one graph per stream holding
-        this rank's stages of `k` consecutive tokens (streams = 1), or one per
-        (stream, stage) replayed stage-major so streams overlap (streams > 1)."""
+        """Capture the decode graphs (one per body and attention split cap) — RCCL hops
+        stay outside.  With ipc hops the receives/sends are inside the graphs: one
+        graph per stream holding this rank's stages of `k` consecutive tokens
+        (streams = 1), or one per (stream, stage) replayed stage-major so streams
+        overlap (streams > 1)."""
         if not self.use_graph:
             return
         if self.hop == "ipc":
             self._capture_ipc()
             return
         for st in self.streams:
-            bodies = self._bodies(st)
-            for key, fn in bodies.items():
-                # warm-up on a scratch copy of the state the body mutates; the
-                # warm-up writes K/V at a scratch position (last cache row) so
-                # the prefilled rows are untouched
-                saved = st.msg.clone()
-                st.hdr[H_POS] = self.stack.max_seq - 1
-                keep = None
-                if self.is_master:
-                    b = st.bufs
-                    keep = [t.clone() for t in (b.tok, b.hist, b.hist_len, b.slot)]
-                s = torch.cuda.Stream()
-                s.wait_stream(torch.cuda.current_stream())
-                with torch.cuda.stream(s):
-                    fn()
-                torch.cuda.current_stream().wait_stream(s)
-                torch.cuda.synchronize()
-                st.msg.copy_(saved)
-                if keep is not None:
-                    for t, v in zip((b.tok, b.hist, b.hist_len, b.slot), keep):
-                        t.copy_(v)
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
-                    fn()
-                st.graphs[key] = g
+            for key, fn in self._bodies(st).items():
+                self._warm(st, fn)
+                st.graphs[key] = self._capture_caps(fn)
         torch.cuda.synchronize()
 
     def _capture_ipc(self) -> None:
@@ -738,42 +901,26 @@ class PipelineEngine:
         self._skip_hops = True
         try:
             for key, (st, fn) in bodies.items():
-                saved = st.msg.clone()
-                st.hdr[H_POS] = self.stack.max_seq - 1
-                keep = None
-                if self.is_master:
-                    b = st.bufs
-                    keep = [t.clone() for t in (b.tok, b.hist, b.hist_len, b.slot)]
-                s = torch.cuda.Stream()
-                s.wait_stream(torch.cuda.current_stream())
-                with torch.cuda.stream(s):
-                    if len(self.streams) == 1:
-                        self._ipc_token_body(st)
-                    else:
-                        fn()
-                torch.cuda.current_stream().wait_stream(s)
-                torch.cuda.synchronize()
-                st.msg.copy_(saved)
-                if keep is not None:
-                    for t, v in zip((b.tok, b.hist, b.hist_len, b.slot), keep):
-                        t.copy_(v)
+                self._warm(st, (lambda st=st: self._ipc_token_body(st)) if len(self.streams) == 1
+                           else fn)
         finally:
             self._skip_hops = False
         for key, (st, fn) in bodies.items():
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                fn()
-            st.graphs[key] = g
+            st.graphs[key] = self._capture_caps(fn)
         torch.cuda.synchronize()
+
+    def _replay_ipc_token(self, st: _Stream) -> None:
+        """This rank's part of one token of stream st (streams = 1, k = 1 graphs)."""
+        self._pick(st.graphs[(st.sid, "tok")], st.dev_pos + self.k + 1).replay()
+        st.dev_pos += self.k
 
     def _decode_ipc(self, rounds: int) -> None:
         """Every rank enqueues its graphs for `rounds` tokens; the hops synchronise
         the ranks on the device.  The master records one event per replay."""
         if len(self.streams) == 1:
             st = self.streams[0]
-            g = st.graphs[(st.sid, "tok")]
-            for _ in range(-(-rounds // self.k)):
-                g.replay()
+            for _ in range(rounds // self.k):
+                self._replay_ipc_token(st)
                 if self.is_master:
                     ev = torch.cuda.Event(enable_timing=True)
                     ev.record()
@@ -783,7 +930,9 @@ class PipelineEngine:
         for _ in range(rounds):
             for k in stages:
                 for st in self.streams:
-                    st.graphs[(st.sid, k)].replay()
+                    self._pick(st.graphs[(st.sid, k)], st.dev_pos + 2).replay()
+            for st in self.streams:
+                st.dev_pos += 1
             if self.is_master:
                 ev = torch.cuda.Event(enable_timing=True)
                 ev.record()
@@ -808,8 +957,18 @@ class PipelineEngine:
 
     # ------------------------------------------------------------------ decode loop
     def decode(self, rounds: int) -> None:
-        """Every stream generates `rounds` tokens (ignoring EOS)."""
+        """Every stream generates `rounds` tokens (ignoring EOS); every rank calls it
+        with the same `rounds` (the bench; serve() for workers)."""
+        if rounds <= 0:
+            return
+        for st in self.streams:
+            if st.dev_pos + rounds > self.stack.max_seq - 1:
+                raise ValueError(f"decode of {rounds} tokens from position {st.dev_pos} "
+                                 f"overruns max_seq {self.stack.max_seq}")
         if self.hop == "ipc":
+            if len(self.streams) == 1 and rounds % self.k:
+                raise ValueError(f"rounds ({rounds}) must be a multiple of steps_per_graph "
+                                 f"({self.k})")
             self._events = []
             if self.is_master:
                 ev = torch.cuda.Event(enable_timing=True)
@@ -835,20 +994,25 @@ class PipelineEngine:
                     if single:
                         self._replay(st, "first", lambda: self._body_first(st))
                         self._replay(st, "last", lambda: self._body_last(st))
+                        st.dev_pos += 1
                         continue
                     self._wait(st.send_work)
                     if k > 0:
                         self._recv(st.msg, self._final_src())
                         self._replay(st, "last", lambda: self._body_last(st))
+                        st.dev_pos += 1
                     self._replay(st, "first", lambda: self._body_first(st))
                     st.send_work = self._send(st.msg, self._first_dst())
                 self._worker_runs(st)
+                if not self.is_master:
+                    st.dev_pos += 1
         if self.is_master and not single:
             for st in self.streams:
                 self._wait(st.send_work)
                 st.send_work = None
                 self._recv(st.msg, self._final_src())
                 self._replay(st, "last", lambda: self._body_last(st))
+                st.dev_pos += 1
         mark()
 
     def _worker_runs(self, st: _Stream) -> None:

@@ -3,8 +3,12 @@
 One process per GPU of a node: rank 0 is the master (tokenizer, embedding,
 ln_f, lm_head, sampling, CLI or REST API, plus every layer no worker owns);
 rank i >= 1 serves the i-th node of ``topology.yml`` (file order).  Hidden
-states hop device-to-device with RCCL p2p (``parallel/pipeline.py``) instead of
-cake's TCP frames; each rank loads only the tensors it owns from the
+states hop device-to-device (``parallel/pipeline.py``) instead of cake's TCP
+frames (cake-core/src/cake/client.rs:116-124, worker.rs:236-252): by default
+as device-side peer stores captured in every rank's decode graph (``--hop
+ipc``; host-issued RCCL p2p with ``--hop dist`` or when the IPC self-test
+fails), with every request announced to the workers on a host control channel
+(``PipelineEngine.serve``).  Each rank loads only the tensors it owns from the
 checkpoint (or a split-model bundle).
 
     torchrun --nproc-per-node 4 --master-addr 127.0.0.1 -m cake_amd.cli \\
@@ -88,26 +92,43 @@ class PipelineLLM(TextGenerator):
     def generated_tokens(self) -> int:
         return self.generated
 
-    def next_token(self, index: int) -> Token:
-        if self.generated == 0:
-            self.tokens = self.tokenizer.encode(self.history.encode_dialog_to_prompt(),
-                                                add_special_tokens=False).ids
-            tid = self.eng.prefill(0, self.tokens)
-        else:
-            tid = self.eng.step(0)
+    def _token(self, tid: int) -> Token:
         self.generated += 1
         self.tokens.append(tid)
-        text = self.tokenizer.decode([tid], skip_special_tokens=False)
-        return Token(tid, text, tid in self.eos_ids)
+        return Token(tid, self.tokenizer.decode([tid], skip_special_tokens=False),
+                     tid in self.eos_ids)
+
+    def _prefill(self) -> int:
+        self.tokens = self.tokenizer.encode(self.history.encode_dialog_to_prompt(),
+                                            add_special_tokens=False).ids
+        self.eng.ctrl_send({"op": "prefill"})
+        return self.eng.prefill(0, self.tokens)
+
+    def next_token(self, index: int) -> Token:
+        if self.generated == 0:
+            return self._token(self._prefill())
+        got = self.eng.generate(1)
+        if not got:
+            raise RuntimeError("KV cache full (--max-seq-len)")
+        return self._token(got[0])
 
     def stream(self, max_tokens, on_token, stop_at_eos=True):
+        """Prefill, then up to max_tokens - 1 decode tokens through the pipeline in
+        control-announced chunks (clamped to the KV cache), stopping at EOS."""
         out = []
-        for i in range(max_tokens):
-            t = self.next_token(i)
-            out.append(t)
-            on_token(t)
-            if t.is_end_of_stream and stop_at_eos:
-                break
+        if max_tokens <= 0:
+            return out
+        t = self._token(self._prefill())
+        out.append(t)
+        on_token(t)
+        if t.is_end_of_stream and stop_at_eos:
+            return out
+
+        def cb(tid: int) -> None:
+            tk = self._token(tid)
+            out.append(tk)
+            on_token(tk)
+        self.eng.generate(max_tokens - 1, cb, self.eos_ids if stop_at_eos else None)
         return out
 
 
@@ -209,6 +230,21 @@ def _tp_follow(eng) -> None:
         _tp_generate(eng, cmd)
 
 
+def _init_dist(ctx, rank: int, world: int) -> None:
+    """One rank per GPU (LOCAL_RANK); RCCL ("nccl") on GPUs, gloo on the CPU.
+    CAKE_DIST_BACKEND=gloo lets several ranks share one GPU (RCCL refuses duplicate
+    devices): tests and single-GPU rehearsals; decode hops stay device-side (ipc)."""
+    backend = os.environ.get("CAKE_DIST_BACKEND")
+    if ctx.device.type == "cuda":
+        local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(local)
+        ctx.device = torch.device("cuda", local)
+        backend = backend or "nccl"
+        init_process_group(backend, rank, world, ctx.device)
+    else:
+        init_process_group("gloo", rank, world)
+
+
 def run_tp(ctx) -> None:
     """``--transport rccl --parallel tp``: every rank loads 1/N of every layer (the
     topology's layer placement does not apply); rank 0 runs the master / API."""
@@ -216,13 +252,7 @@ def run_tp(ctx) -> None:
     from .tensor_parallel import AllReduce, TPEngine, check_tp, load_shards
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if ctx.device.type == "cuda":
-        local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
-        torch.cuda.set_device(local)
-        ctx.device = torch.device("cuda", local)
-        init_process_group("nccl", rank, world, ctx.device)
-    else:
-        init_process_group("gloo", rank, world)
+    _init_dist(ctx, rank, world)
     try:
         cfg = LlamaConfig.from_path(ctx.model_path)
         check_tp(cfg, world)
@@ -262,13 +292,7 @@ def run_rccl(ctx) -> None:
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if ctx.device.type == "cuda":
-        local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
-        torch.cuda.set_device(local)
-        ctx.device = torch.device("cuda", local)
-        init_process_group("nccl", rank, world, ctx.device)
-    else:
-        init_process_group("gloo", rank, world)
+    _init_dist(ctx, rank, world)
     try:
         cfg = LlamaConfig.from_path(ctx.model_path)
         owners = owners_from_topology(ctx.topology, cfg.num_hidden_layers, world)
@@ -278,19 +302,20 @@ def run_rccl(ctx) -> None:
         if rank == 0:
             head = HeadWeights.load(ShardedCheckpoint(ctx.model_path).get, cfg, ctx.device, ctx.dtype)
         s = ctx.sampling
+        a = ctx.args
         eng = PipelineEngine(cfg, stack, owners, rank, world, streams=1, head=head,
                              repeat_penalty=s.repeat_penalty, repeat_last_n=s.repeat_last_n,
-                             use_graph=not ctx.no_graph)
-        log.info("rank %d/%d owns layers %s", rank, world, mine[:3] + (["..."] if len(mine) > 3 else []))
+                             use_graph=not ctx.no_graph, hop=getattr(a, "hop", "ipc"),
+                             hop_bf16=getattr(a, "hop_dtype", "f32") == "bf16")
+        log.info("rank %d/%d owns layers %s (hops: %s)", rank, world,
+                 mine[:3] + (["..."] if len(mine) > 3 else []), eng.hop)
         if rank == 0 and eng.hip:
             eng.set_sampling(s)  # device-read parameters: per-request API sampling
         if eng.use_graph:
-            # the worker graphs read the position from the received header; a
-            # dummy prefill gives every graph valid state to capture against
-            if rank == 0:
-                eng.prefill(0, [cfg.bos_token_id or 0])
-            else:
-                _serve_one_prefill(eng)
+            # the graphs read the position from device state; a dummy prefill gives
+            # every graph valid state to capture against (collective, at start-up)
+            eng.prefill(0, [cfg.bos_token_id or 0] if rank == 0 else None)
+            eng.flush()
             eng.capture()
         _startup_metrics(eng, ctx, rank, world, len(mine))
         if rank == 0:
@@ -303,6 +328,7 @@ def run_rccl(ctx) -> None:
                 eng.shutdown()
         else:
             eng.serve()
+        eng.close()
     finally:
         dist.destroy_process_group()
 
@@ -316,17 +342,10 @@ def _startup_metrics(eng: PipelineEngine, ctx, rank: int, world: int, n_layers: 
             **(hbm_mib(ctx.device) if ctx.device.type == "cuda" else {})}
     ranks = [None] * world
     dist.all_gather_object(ranks, mine)
-    hops = sum(1 for k in range(1, len(eng.runs) + 2) if eng._recv_point(k))
+    hops = eng.hops_per_token()
     eng.metrics = {"hop_us": None if hop_us is None else round(hop_us, 2),
                    "hops_per_token": hops, "rank_hbm": ranks}
     if rank == 0:
         log.info("pipeline: %d hops/token, hop %s us; per-rank HBM %s", hops,
                  "n/a" if hop_us is None else f"{hop_us:.1f}",
                  [r.get("hbm_used_mib") for r in ranks])
-
-
-def _serve_one_prefill(eng: PipelineEngine) -> None:
-    st = eng.streams[0]
-    for j in eng.my_runs:
-        eng._recv(st.msg, eng._prev(j))
-        eng._prefill_run(st, j)

@@ -47,10 +47,20 @@ def test_self_launch_fails_fast_when_a_rank_dies():
     assert "stopping the others" in r.stderr
 
 
+def test_default_multi_rank_headline_is_layer_sharding():
+    """N > 1 without --parallel: the reference's layer sharding is the headline."""
+    r = _run(["--gpus", "2"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    j = _json(r)
+    assert j["n_gpus"] == 2 and j["config"]["parallelism"].startswith("pp2")
+    assert j["parallel"] == "pp" and j["hops_per_token"] == 2
+
+
 def test_self_launch_tensor_parallel(tmp_path):
-    """Default N > 1 mode: tensor-parallel ranks; same stream at TP 1 and TP 2 is covered
+    """--parallel tp: tensor-parallel ranks; same stream at TP 1 and TP 2 is covered
     by tests/test_tp_cpu.py (here: the launch / JSON contract)."""
-    r = _run(["--gpus", "2", "--model", "tiny-kv2", "--dump-tokens", str(tmp_path / "t.json")])
+    r = _run(["--gpus", "2", "--parallel", "tp", "--model", "tiny-kv2",
+              "--dump-tokens", str(tmp_path / "t.json")])
     assert r.returncode == 0, r.stderr[-2000:]
     j = _json(r)
     assert j["n_gpus"] == 2 and j["config"]["parallelism"].startswith("tp2")
