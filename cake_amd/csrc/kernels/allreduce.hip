@@ -23,9 +23,12 @@
 // (s_memrealtime) that sets an error word instead of hanging the GPU.
 //
 // Ops: SUM of f32 vectors (out = sum, or out += sum into the f32 residual
-// stream), and MAX of one 64-bit argmax key (vocab-sharded lm_head: the key is
+// stream), MAX of one 64-bit argmax key (vocab-sharded lm_head: the key is
 // (ordered logit << 32 | ~global index), so the max is the global argmax with
-// the smallest index on ties, exactly as the single-GPU argmax_kernel).
+// the smallest index on ties, exactly as the single-GPU argmax_kernel), and
+// GATHER of the vocab-sharded logits into a full vector on every rank (sampled
+// decoding: top-k / top-p need the global distribution; every rank then draws
+// the same token from the same full vector).
 #include "common.h"
 
 namespace cake {
@@ -139,6 +142,34 @@ __global__ __launch_bounds__(64) void ar_max_key_kernel(ArArgs a, unsigned long 
   ar_finish(a, tag);
 }
 
+// full[0, n) on every rank <- the ranks' contiguous shards: this rank owns
+// [off, off + n_local) = shard[0, n_local).  The inbox holds 2 banks x n granules;
+// every rank writes its shard at its global offset in every peer's bank.
+__global__ __launch_bounds__(kArThreads) void ar_gather_kernel(ArArgs a, const float* __restrict__ shard,
+                                                               int off, int n_local,
+                                                               float* __restrict__ full) {
+  const unsigned int tag = __hip_atomic_load(a.seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  const size_t bank = (size_t)(tag & 1u) * a.n;
+  const int i0 = blockIdx.x * kArThreads + threadIdx.x, stride = gridDim.x * kArThreads;
+  for (int i = i0; i < n_local; i += stride) {
+    const float v = shard[i];
+    const unsigned long long g = (unsigned long long)__float_as_uint(v) | ((unsigned long long)tag << 32);
+    for (int r = 0; r < a.world; ++r)
+      if (r != a.rank)
+        __hip_atomic_store(a.peer[r] + bank + off + i, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    full[off + i] = v;
+  }
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  bool late = false;
+  for (int i = i0; i < a.n; i += stride) {
+    if (i >= off && i < off + n_local) continue;
+    const unsigned long long g = ar_poll(a.inbox + bank + i, tag, t0, a.timeout_ticks, late);
+    full[i] = __uint_as_float((uint32_t)g);
+  }
+  if (late) atomicOr(a.err, 1);
+  ar_finish(a, tag);
+}
+
 }  // namespace cake
 
 using namespace cake;
@@ -189,5 +220,21 @@ CAKE_API int cake_ar_max_key(unsigned long long* slot, void* const* peers, const
   const int rc = ar_args(a, peers, inbox, seq, err, rank, world, 2, timeout_s);
   if (rc) return rc;
   hipLaunchKernelGGL(ar_max_key_kernel, dim3(1), dim3(64), 0, st, a, slot);
+  return (int)hipGetLastError();
+}
+
+// full (f32[n]) on every rank <- concatenation of the ranks' shards (shard = this
+// rank's [off, off + n_local)); the inbox must hold 2 x n granules.
+CAKE_API int cake_ar_gather(const float* shard, int off, int n_local, float* full, int n,
+                            void* const* peers, const void* inbox, unsigned int* seq, int* err,
+                            int rank, int world, double timeout_s, hipStream_t st) {
+  ArArgs a;
+  const int rc = ar_args(a, peers, inbox, seq, err, rank, world, n, timeout_s);
+  if (rc) return rc;
+  if (off < 0 || n_local < 0 || off + n_local > n) return (int)hipErrorInvalidValue;
+  int g = (n + kArThreads * 8 - 1) / (kArThreads * 8);
+  if (g > 64) g = 64;
+  if (g < 1) g = 1;
+  hipLaunchKernelGGL(ar_gather_kernel, dim3(g), dim3(kArThreads), 0, st, a, shard, off, n_local, full);
   return (int)hipGetLastError();
 }

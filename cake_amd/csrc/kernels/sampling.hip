@@ -187,7 +187,7 @@ __device__ __forceinline__ float sel_max(float v, float* red) {
 }
 
 // Threshold key: tokens with ordered(logit) >= *thr_out form the sampling set
-// (top-k, then top-p within it).  One workgroup; each radix level is one pass
+// (top-k, then the top-p cutoff over those tokens' full-vocabulary probabilities).  One workgroup; each radix level is one pass
 // over the logits (L2-resident right after the lm_head).
 __global__ __launch_bounds__(kSelThreads) void sample_threshold_kernel(
     const float* __restrict__ logits, int V, float inv_t, int top_k, float top_p,
@@ -238,17 +238,14 @@ __global__ __launch_bounds__(kSelThreads) void sample_threshold_kernel(
   }
   unsigned int pthr = 0u;
   if (top_p > 0.f && top_p < 1.f) {
+    // candle's TopKThenTopP / the host LogitsProcessor: the p cutoff applies to the
+    // FULL-vocabulary probabilities of the top-k tokens (no renormalisation inside
+    // top-k), so Z sums every token; when the top-k mass is below p all k are kept
     float m = -INFINITY;
-    for (int i = tid; i < V; i += kSelThreads) {
-      const float l = logits[i];
-      if (ordered(l) >= kthr) m = fmaxf(m, l);
-    }
+    for (int i = tid; i < V; i += kSelThreads) m = fmaxf(m, logits[i]);
     m = sel_max(m, red);
     float z = 0.f;
-    for (int i = tid; i < V; i += kSelThreads) {
-      const float l = logits[i];
-      if (ordered(l) >= kthr) z += __expf((l - m) * inv_t);
-    }
+    for (int i = tid; i < V; i += kSelThreads) z += __expf((logits[i] - m) * inv_t);
     z = wave_sum(z);
     __syncthreads();
     if ((tid & 63) == 0) red[tid >> 6] = z;

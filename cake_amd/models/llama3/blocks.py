@@ -173,18 +173,30 @@ class LayerStack:
     # ------------------------------------------------------------------ hip paths
     def _decode_graph(self, hidden, layers: list[int], pos0: int, session: int) -> None:
         """T = 1 over a run of layers as ONE graph replay (worker serving path): the
-        first request of a (session, run) runs eagerly and captures the step; later
-        ones copy the hidden state and position in, replay, copy the state out."""
-        key = (session, tuple(layers))
+        first request of a (session, run, attention split cap) runs eagerly and
+        captures the step; later ones copy the hidden state and position in, replay,
+        copy the state out.  The position is known on the host here, so the graph is
+        the one of the smallest split cap covering the live length (position
+        buckets, as DeviceDecoder.capture)."""
+        from ...ops import hip as K
+        full = K.attn_max_split(self.max_seq)
+        need = K.attn_splits(pos0 + 1)
+        cap = next((c for c in (8, 16, 32, 64) if c >= min(need, full)), 64)
+        cap = min(cap, full)
+        key = (session, tuple(layers), cap)
         ent = self._step_graph_cache.get(key)
         if ent is None:
-            bufs = DecodeBuffers(self.cfg, self.max_seq, self.device, self.dtype, with_head=False)
+            bufs = next((b for (s, l, _), (_, b) in self._step_graph_cache.items()
+                         if s == session and l == key[1]), None)
+            if bufs is None:
+                bufs = DecodeBuffers(self.cfg, self.max_seq, self.device, self.dtype,
+                                     with_head=False)
             bufs.pos.fill_(pos0)
             bufs.resid.copy_(hidden[0])
             self.decode_step(bufs, layers, session)
             hidden[0].copy_(bufs.resid)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):  # records only
+            with K.attn_split_cap(cap), torch.cuda.graph(g):  # records only
                 self.decode_step(bufs, layers, session)
             self._step_graph_cache[key] = (g, bufs)
             return

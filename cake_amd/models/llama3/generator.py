@@ -181,6 +181,8 @@ class LLamaGenerator(TextGenerator):
         on_token(first)
         if first.is_end_of_stream and stop_at_eos:
             return out
+        # every further token needs a KV-cache row: clamp to the cache (max_seq)
+        max_tokens = min(max_tokens, self.model.stack.max_seq - len(self.tokens) + 1)
         if not self._fast_path():
             for i in range(1, max_tokens):
                 t = self.next_token(i)

@@ -295,7 +295,11 @@ class DeviceDecoder:
         self.host_pos += 1
 
     def launch(self) -> None:
-        """Enqueue `self.k` decode steps (one graph replay; async)."""
+        """Enqueue `self.k` decode steps (one graph replay; async).  Raises instead of
+        writing past the KV cache / token history (max_seq)."""
+        if self.host_pos + self.k >= self.m.stack.max_seq:
+            raise ValueError(f"decode step at position {self.host_pos} (+{self.k}) overruns "
+                             f"max_seq {self.m.stack.max_seq}")
         if self.graph is not None:
             # live length of the last step of this replay (+1: sampled mode pushes)
             self._graph_for(self.host_pos + self.k + 1).replay()

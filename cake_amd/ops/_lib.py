@@ -58,6 +58,7 @@ _SIGS = {
     "cake_select_shard": [P, I, I, P, P, I, F, F, C.c_ulonglong, P, P],
     "cake_ar_sum": [P, P, I, I, P, P, P, P, I, I, C.c_double, P],
     "cake_ar_max_key": [P, P, P, P, P, I, I, C.c_double, P],
+    "cake_ar_gather": [P, I, I, P, I, P, P, P, P, I, I, C.c_double, P],
 }
 
 

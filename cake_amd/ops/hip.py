@@ -382,6 +382,19 @@ def ar_max_key(slot, peers, inbox: int, seq, err, rank: int, world: int, timeout
           "ar_max_key")
 
 
+def ar_gather(shard, off: int, full, peers, inbox: int, seq, err, rank: int, world: int,
+              timeout_s: float):
+    """full (f32[V], every rank) <- the TP ranks' contiguous vocabulary shards; this
+    rank's shard covers full[off:off + shard.numel()]."""
+    _req(shard, "shard", dtype=torch.float32)
+    _req(full, "full", dtype=torch.float32)
+    if off < 0 or off + shard.numel() > full.numel():
+        raise ValueError("shard outside the gathered vector")
+    check(kernels().cake_ar_gather(_p(shard), int(off), shard.numel(), _p(full), full.numel(),
+                                   peers, C.c_void_p(inbox), _p(seq), _p(err), int(rank),
+                                   int(world), float(timeout_s), _stream()), "ar_gather")
+
+
 def finalize_token(slot, tok, hist, hist_len, pos):
     for t, n in ((tok, "tok"), (hist, "hist"), (hist_len, "hist_len"), (pos, "pos")):
         _req(t, n, dtype=torch.int32)

@@ -165,14 +165,10 @@ class TPLLM(TextGenerator):
     def generated_tokens(self) -> int:
         return self.generated
 
-    @staticmethod
-    def check_sampling(sampling) -> None:
-        if sampling.top_k or (sampling.top_p is not None and sampling.top_p < 1.0):
-            raise ValueError("tensor-parallel serving supports greedy / temperature sampling "
-                             "(top_k / top_p need the whole vocabulary on one rank)")
-
     def set_sampling(self, sampling) -> None:
-        self.check_sampling(sampling)
+        """Per-request sampling: temperature / top_k / top_p / seed all travel in the
+        generate command; the ranks rewrite their device parameter blocks (no
+        recapture)."""
         self.sampling = sampling
 
     def next_token(self, index: int) -> Token:  # pragma: no cover - stream() drives it
@@ -184,7 +180,8 @@ class TPLLM(TextGenerator):
         s = self.sampling
         cmd = {"op": "generate", "prompt": prompt, "max_tokens": int(max_tokens),
                "eos": sorted(self.eos_ids) if stop_at_eos else [],
-               "temperature": 0.0 if s.greedy else float(s.temperature), "seed": int(s.seed)}
+               "temperature": 0.0 if s.greedy else float(s.temperature), "seed": int(s.seed),
+               "top_k": int(s.top_k or 0), "top_p": float(s.top_p) if s.top_p is not None else None}
         dist.broadcast_object_list([cmd], src=0)
         out = []
 
@@ -194,29 +191,80 @@ class TPLLM(TextGenerator):
                       tid in self.eos_ids)
             out.append(t)
             on_token(t)
-        _tp_generate(self.eng, cmd, emit)
+        self.last_stats = _tp_generate(self.eng, cmd, emit)
         return out
 
 
-def _tp_generate(eng, cmd, emit=None) -> None:
-    """One generation on every rank (same command, same tokens)."""
-    temp, seed = float(cmd["temperature"]), int(cmd["seed"])
-    if (temp, seed) != (eng.temperature, eng.seed):
-        eng.temperature, eng.seed = temp, seed
-        eng.graph = None  # the selection is baked into the graph: recapture (all ranks)
-    n, eos = int(cmd["max_tokens"]), set(cmd["eos"])
+def _tp_generate(eng, cmd, emit=None):
+    """One generation on every rank (same command, same tokens).  The sampling
+    configuration goes to the device parameter block (no recapture when only the
+    temperature / seed / top-k / top-p change); tokens are read back one step
+    behind the GPU (the next step is enqueued before the previous token is read),
+    and every rank stops after the same token."""
+    from ..models.llama3.decode_loop import DecodeStats
+    from ..models.sampling import SamplingConfig
+    temp = float(cmd["temperature"])
+    eng.set_sampling(None if temp <= 0 else SamplingConfig(
+        temperature=temp, top_k=int(cmd.get("top_k") or 0) or None, top_p=cmd.get("top_p"),
+        seed=int(cmd["seed"]), repeat_penalty=eng.penalty, repeat_last_n=eng.last_n))
+    # the first token comes from the prefill; every later one needs a cache row
+    n = min(int(cmd["max_tokens"]), eng.max_seq - len(cmd["prompt"]))
+    eos = set(cmd["eos"])
+    st = DecodeStats()
     if n <= 0:
-        return
+        return st
     tid = eng.prefill(cmd["prompt"])
     eng.capture()
-    for i in range(n):
-        if i > 0:
+    if emit is not None:
+        emit(tid)
+    if tid in eos or n == 1:
+        eng.check()
+        return st
+    if not eng.hip:
+        for _ in range(n - 1):
             tid = eng.step()
-        if emit is not None:
-            emit(tid)
-        if tid in eos:
+            if emit is not None:
+                emit(tid)
+            if tid in eos:
+                break
+        eng.check()
+        return st
+    b = eng.b
+    base = int(b.hist_len.item())
+    ring = torch.empty(n, dtype=torch.int32, pin_memory=True)
+    prev = torch.cuda.Event(enable_timing=True)
+    prev.record()
+    pending = None
+    for i in range(n - 1):
+        eng.launch()
+        ring[i:i + 1].copy_(b.hist[base + i:base + i + 1], non_blocking=True)
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        cur = (i, ev)
+        if pending is not None and _tp_take(eng, pending, ring, prev, st, emit, eos):
+            pending = None
             break
+        if pending is not None:
+            prev = pending[1]
+        pending = cur
+    if pending is not None:
+        _tp_take(eng, pending, ring, prev, st, emit, eos)
+    torch.cuda.synchronize(eng.device)
+    eng.tokens = b.hist[:int(b.hist_len.item())].tolist()
     eng.check()
+    return st
+
+
+def _tp_take(eng, pending, ring, prev, st, emit, eos) -> bool:
+    """Read one enqueued step's token; True at EOS."""
+    i, ev = pending
+    ev.synchronize()
+    tid = int(ring[i].item())
+    st.step_ms.append(prev.elapsed_time(ev))
+    st.tokens.append(tid)
+    if emit is not None:
+        emit(tid)
+    return tid in eos
 
 
 def _tp_follow(eng) -> None:
@@ -257,11 +305,10 @@ def run_tp(ctx) -> None:
         cfg = LlamaConfig.from_path(ctx.model_path)
         check_tp(cfg, world)
         blocks, head = load_shards(ctx.model_path, cfg, rank, world, ctx.device, ctx.dtype)
-        comm = AllReduce(rank, world, ctx.device, cfg.hidden_size)
+        comm = AllReduce(rank, world, ctx.device, cfg.hidden_size, n_gather=cfg.vocab_size)
         s = ctx.sampling
         eng = TPEngine(cfg, blocks, head, rank, world, ctx.device, ctx.dtype, ctx.max_seq_len,
                        comm, repeat_penalty=s.repeat_penalty, repeat_last_n=s.repeat_last_n,
-                       temperature=0.0 if s.greedy else s.temperature, seed=s.seed,
                        use_graph=not ctx.no_graph)
         log.info("rank %d/%d: tensor-parallel shard, all-reduce %s", rank, world, comm.mode)
         if rank == 0:

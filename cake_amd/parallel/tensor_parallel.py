@@ -14,10 +14,17 @@ vocabulary-sharded lm_head make the ranks agree; on the HIP path they are
 graph (RCCL / ``torch.distributed`` as the fallback and for prefill).
 
 Every rank keeps the full embedding table, so all ranks embed the selected
-token locally and stay in lock step with no broadcast.  Sampling: greedy (with
-the reference's repeat penalty) or temperature — the Gumbel-max draw uses the
-GLOBAL vocabulary index as its Philox counter, so the sharded draw equals the
-single-GPU one; top-k / top-p need the global distribution and are refused.
+token locally and stay in lock step with no broadcast.  Token selection:
+greedy (with the reference's repeat penalty) = shard argmax key + one 64-bit
+max all-reduce; sampled (temperature / top-k / top-p, the reference's
+LogitsProcessor, cake-core/src/models/llama3/llama.rs:34-48, 323-326) = the
+vocabulary shards are all-gathered into a full logits vector on every rank
+(allreduce.hip ar_gather, device-side), then every rank runs the single-GPU
+device selection (repeat penalty, top-k/top-p threshold, Philox Gumbel-max
+keyed by the GLOBAL index) on identical inputs and picks the same token — equal
+to the single-GPU draw.  The sampling configuration lives in a device
+parameter block, so a request with another temperature / seed / top-k / top-p
+replays the same graphs (one graph set per greedy/sampled mode).
 
 Shards: ``shard_block`` / ``shard_head`` cut a full checkpoint's tensors
 (heads and MLP rows split contiguously: rank r owns q heads
@@ -143,21 +150,28 @@ class AllReduce:
     IPC-exported) and tag counter; a start-up self-test must pass on every rank or
     the group falls back to "dist" (torch.distributed, RCCL on GPUs / gloo)."""
 
-    def __init__(self, rank: int, world: int, device, n: int, mode: str = "ipc", group=None):
+    def __init__(self, rank: int, world: int, device, n: int, mode: str = "ipc", group=None,
+                 n_gather: int = 0):
         self.rank, self.world, self.device, self.n = rank, world, torch.device(device), n
+        self.n_gather = int(n_gather)  # gather channel width (vocabulary; 0 = none)
         self.group = group
         self.mode = mode if (world > 1 and self.device.type == "cuda") else "dist"
         self.staged = (world > 1 and dist.is_initialized()
                        and dist.get_backend(group) == "gloo")
         self._inboxes, self._peers = [], []
+        self.gather_ch = None
         self.timeout_s = float(os.environ.get("CAKE_HOP_TIMEOUT", "60"))
         if self.mode == "ipc":
-            try:
-                self._setup_ipc()
-                ok = self._selftest()
-            except Exception as e:  # noqa: BLE001  (agree below, then fall back)
-                log.warning("tp all-reduce IPC setup failed on rank %d: %s", rank, e)
-                ok = False
+            # every rank runs the same collective sequence whatever fails locally
+            # (one handle exchange, one self-test, one agreement), so a failure on
+            # one rank falls back instead of leaving the others in a collective
+            ok = self._setup_ipc()
+            if ok:
+                try:
+                    ok = self._selftest()
+                except Exception as e:  # noqa: BLE001  (agreed on below)
+                    log.warning("tp all-reduce IPC self-test failed on rank %d: %s", rank, e)
+                    ok = False
             flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
             self._all_reduce_host(flag, dist.ReduceOp.MIN)
             if int(flag.item()) != 1:
@@ -188,25 +202,47 @@ class AllReduce:
             dist.all_reduce(t, group=self.group)
 
     # -- IPC channels
-    def _setup_ipc(self) -> None:
+    def _setup_ipc(self) -> bool:
+        """Both channels' inboxes, ONE handle exchange (joined even after a local
+        failure, with None handles), then the peer mappings.  The self-test runs only
+        if every rank mapped every peer (agreed with a MIN); returns that agreement."""
         from .hop import Inbox, PeerInbox
-        self.sum_ch = self._channel(self.n, Inbox, PeerInbox)
-        self.key_ch = self._channel(2, Inbox, PeerInbox)
-
-    def _channel(self, n: int, Inbox, PeerInbox) -> dict:
-        ib = Inbox(2 * self.world * n)
-        self._inboxes.append(ib)
+        sizes = {"sum": 2 * self.world * self.n, "key": 2 * self.world * 2}  # inbox granules
+        if self.n_gather:
+            sizes["gather"] = 2 * self.n_gather
+        mine = None
+        try:
+            ibs = {k: Inbox(n) for k, n in sizes.items()}
+            self._inboxes.extend(ibs.values())
+            mine = {k: ib.handle() for k, ib in ibs.items()}
+        except Exception as e:  # noqa: BLE001
+            log.warning("tp all-reduce inbox allocation failed on rank %d: %s", self.rank, e)
         handles = [None] * self.world
-        dist.all_gather_object(handles, ib.handle(), group=self.group)
-        peers = (C.c_void_p * 8)()
-        for r in range(self.world):
-            if r != self.rank:
-                p = PeerInbox(handles[r])
-                self._peers.append(p)
-                peers[r] = p.ptr
-        return {"inbox": ib, "peers": peers,
-                "seq": torch.zeros(2, dtype=torch.int32, device=self.device),
-                "err": torch.zeros(1, dtype=torch.int32, device=self.device)}
+        dist.all_gather_object(handles, mine, group=self.group)
+        ok = all(h is not None for h in handles)
+        chans = {}
+        if ok:
+            try:
+                for k in sizes:
+                    peers = (C.c_void_p * 8)()
+                    for r in range(self.world):
+                        if r != self.rank:
+                            p = PeerInbox(handles[r][k])
+                            self._peers.append(p)
+                            peers[r] = p.ptr
+                    chans[k] = {"inbox": ibs[k], "peers": peers,
+                                "seq": torch.zeros(2, dtype=torch.int32, device=self.device),
+                                "err": torch.zeros(1, dtype=torch.int32, device=self.device)}
+            except Exception as e:  # noqa: BLE001
+                log.warning("tp all-reduce IPC open failed on rank %d: %s", self.rank, e)
+                ok = False
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
+        self._all_reduce_host(flag, dist.ReduceOp.MIN)
+        if int(flag.item()) != 1:
+            return False
+        self.sum_ch, self.key_ch = chans["sum"], chans["key"]
+        self.gather_ch = chans.get("gather")
+        return True
 
     def _close_ipc(self) -> None:
         if self.device.type == "cuda":
@@ -281,10 +317,30 @@ class AllReduce:
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
         slot.copy_(torch.bitwise_xor(t, flip))
 
+    def gather_(self, shard: torch.Tensor, off: int, full: torch.Tensor) -> None:
+        """full <- the ranks' contiguous shards (this rank's at [off, off + len))."""
+        if self.world == 1:
+            full.copy_(shard)
+            return
+        if self.mode == "ipc":
+            if self.gather_ch is None:
+                raise RuntimeError("AllReduce built without a gather channel (n_gather)")
+            from ..ops import hip as K
+            ch = self.gather_ch
+            K.ar_gather(shard, off, full, ch["peers"], ch["inbox"].ptr, ch["seq"], ch["err"],
+                        self.rank, self.world, self.timeout_s)
+            return
+        full.zero_()
+        full[off:off + shard.numel()].copy_(shard)
+        self.dense_sum_(full)
+
     def errors(self) -> int:
         if self.mode != "ipc":
             return 0
-        return int(self.sum_ch["err"].item()) | int(self.key_ch["err"].item())
+        e = int(self.sum_ch["err"].item()) | int(self.key_ch["err"].item())
+        if self.gather_ch is not None:
+            e |= int(self.gather_ch["err"].item())
+        return e
 
     def measure_us(self, iters: int = 200) -> float | None:
         """Device time of one hidden-size all-reduce (graph of `iters` back to back)."""
@@ -345,6 +401,7 @@ class TPBuffers:
         self.hist = torch.zeros(max_seq, device=device, dtype=i32)
         self.hist_len = torch.zeros(1, device=device, dtype=i32)
         self.slot = torch.zeros(1, device=device, dtype=torch.int64)
+        self.thr = torch.zeros(1, device=device, dtype=i32)   # top-k/top-p threshold key
 
 
 class TPEngine:
@@ -361,7 +418,10 @@ class TPEngine:
         self.blocks = dict(sorted(blocks.items()))
         self.head, self.comm = head, comm
         self.penalty, self.last_n = float(repeat_penalty), int(repeat_last_n)
-        self.temperature, self.seed = float(temperature or 0.0), int(seed)
+        self.sampling = None         # SamplingConfig of the sampled mode (None = greedy)
+        self.params = None           # device SampleParams (hip)
+        self.full_logits = None      # gathered vocabulary (sampled mode)
+        self._host_sampler = None    # torch path: seeded LogitsProcessor over full logits
         self.hip = self.device.type == "cuda" and dtype in (torch.float16, torch.bfloat16)
         # the torch.distributed fallback issues host collectives: eager launches only
         self.use_graph = use_graph and self.hip and (world == 1 or comm.mode == "ipc")
@@ -377,9 +437,40 @@ class TPEngine:
         self.scale = 1.0 / math.sqrt(hd)
         self.b = TPBuffers(H, self.nq, self.nkv, hd, self.I_l, self.V_l, max_seq, self.device,
                            dtype)
-        self.graph = None
+        self.graphs: dict = {}       # mode ("greedy" / "sample") -> {split cap: graph}
         self.host_pos = 0
         self.tokens: list[int] = []
+        if temperature and temperature > 0:
+            from ..models.sampling import SamplingConfig
+            self.set_sampling(SamplingConfig(temperature=float(temperature), seed=int(seed),
+                                             repeat_penalty=self.penalty,
+                                             repeat_last_n=self.last_n))
+
+    # ------------------------------------------------------------------ sampling
+    @property
+    def mode(self) -> str:
+        return "greedy" if self.sampling is None else "sample"
+
+    def set_sampling(self, sampling) -> None:
+        """Sampling configuration of the next generation (every rank, same value; None or
+        temperature <= 0 = greedy).  hip: rewrites the device parameter block only —
+        the captured graphs of the mode are replayed as they are."""
+        from ..models.sampling import LogitsProcessor
+        self.sampling = sampling if sampling is not None and not sampling.greedy else None
+        if self.sampling is None:
+            self._host_sampler = None
+            return
+        if self.hip:
+            from ..ops import hip as K
+            if self.params is None:
+                self.params = torch.zeros(K.SAMPLE_PARAMS_WORDS, dtype=torch.int32,
+                                          device=self.device)
+            self.params.copy_(K.pack_sample_params(self.sampling))
+        else:
+            self._host_sampler = LogitsProcessor(self.sampling)
+        if self.full_logits is None:
+            self.full_logits = torch.zeros(self.cfg.vocab_size, device=self.device,
+                                           dtype=torch.float32)
 
     # ------------------------------------------------------------------ prefill
     def prefill(self, prompt: list[int]) -> int:
@@ -456,20 +547,35 @@ class TPEngine:
 
     # ------------------------------------------------------------------ head
     def _head_hip(self, row: torch.Tensor) -> None:
-        """ln_f + this rank's lm_head rows -> shard key -> global max -> next token."""
+        """ln_f + this rank's lm_head rows, then the token: greedy = shard argmax key ->
+        global max; sampled = gather the full vocabulary -> the single-GPU device
+        selection with the parameter block (identical on every rank)."""
         from ..ops import hip as K
         b = self.b
         K.norm_gemv_f32(row, self.head.norm, self.cfg.rms_norm_eps, self.head.lm, b.logits)
-        K.select_shard(b.logits, self.head.voff, b.hist, b.hist_len, self.last_n, self.penalty,
-                       self.temperature, self.seed, b.slot)
-        self.comm.max_key_(b.slot)
-        K.finalize_token(b.slot, b.tok, b.hist, b.hist_len, b.pos)
+        if self.sampling is None:
+            K.select_shard(b.logits, self.head.voff, b.hist, b.hist_len, self.last_n,
+                           self.penalty, 0.0, 0, b.slot)
+            self.comm.max_key_(b.slot)
+            K.finalize_token(b.slot, b.tok, b.hist, b.hist_len, b.pos)
+            return
+        full = self.full_logits
+        self.comm.gather_(b.logits, self.head.voff, full)
+        if self.penalty != 1.0:
+            K.repeat_penalty(full, b.hist, b.hist_len, self.last_n, self.penalty)
+        K.select_token(full, b.slot, b.hist, b.hist_len, b.tok, b.pos, thr=b.thr,
+                       params=self.params)
 
     def _head_torch(self, row: torch.Tensor) -> int:
-        if self.temperature > 0:
-            raise NotImplementedError("tensor-parallel sampling runs on the HIP path")
         x = R.rms_norm(row, self.head.norm, self.cfg.rms_norm_eps).to(self.dtype)
         logits = (x @ self.head.lm.t()).float()
+        if self.sampling is not None:   # every rank: same full logits, same seeded draw
+            full = self.full_logits
+            self.comm.gather_(logits, self.head.voff, full)
+            if self.penalty != 1.0:
+                full = R.apply_repeat_penalty(full.clone(), self.penalty,
+                                              self.tokens[-self.last_n:])
+            return int(self._host_sampler.sample(full))
         if self.penalty != 1.0:
             recent = [t - self.head.voff for t in self.tokens[-self.last_n:]]
             recent = [t for t in dict.fromkeys(recent) if 0 <= t < logits.numel()]
@@ -508,10 +614,11 @@ class TPEngine:
         self._head_hip(b.resid)
 
     def capture(self) -> None:
-        """Capture one decode step as a graph (after prefill; every rank together).  The
-        warm-up step's token state is restored afterwards; the K/V row it wrote is the
-        one the first real step rewrites with the same values."""
-        if not self.use_graph or self.graph is not None:
+        """Capture the decode step of the current mode (greedy / sampled) as graphs,
+        one per attention split cap (after prefill; every rank together, in the same
+        mode).  The warm-up step's token state is restored afterwards; the K/V row it
+        wrote is the one the first real step rewrites with the same values."""
+        if not self.use_graph or self.mode in self.graphs:
             return
         b = self.b
         saved = [t.clone() for t in (b.tok, b.pos, b.hist_len, b.hist, b.slot)]
@@ -523,24 +630,29 @@ class TPEngine:
         # every rank picks the same one from the same host position
         from ..ops import hip as K
         full = K.attn_max_split(self.max_seq)
-        self.graphs = {}
+        gs = {}
         for cap in sorted({min(c, full) for c in (8, 16, 32, 64)}):
             g = torch.cuda.CUDAGraph()
             with K.attn_split_cap(cap), torch.cuda.graph(g):
                 self._step_body()
-            self.graphs[cap] = g
-        self.graph = self.graphs[max(self.graphs)]
+            gs[cap] = g
+        self.graphs[self.mode] = gs
         torch.cuda.synchronize(self.device)
 
     def _graph_for(self, tk: int):
         from ..ops import hip as K
+        gs = self.graphs[self.mode]
         need = K.attn_splits(tk)
-        return next((self.graphs[c] for c in sorted(self.graphs) if c >= need), self.graph)
+        return next((gs[c] for c in sorted(gs) if c >= need), gs[max(gs)])
 
     def launch(self) -> None:
-        """Enqueue one decode step (async on the HIP path)."""
+        """Enqueue one decode step (async on the HIP path).  Raises instead of writing
+        past the KV cache / token history (max_seq)."""
+        if self.host_pos + 1 >= self.max_seq:
+            raise ValueError(f"decode step at position {self.host_pos} overruns max_seq "
+                             f"{self.max_seq}")
         if self.hip:
-            if self.graph is not None:
+            if self.use_graph and self.mode in self.graphs:
                 self._graph_for(self.host_pos + 2).replay()
             else:
                 self._step_body()

@@ -118,6 +118,10 @@ class Worker:
             raw = torch.frombuffer(data, dtype=torch.uint8) if len(data) else \
                 torch.empty(0, dtype=torch.uint8)
         x = raw.view(P.FROM_CANDLE[dtype]).reshape(list(shape))
+        if x.device == self.ctx.device or self.ctx.device.type == "cpu":
+            # a CPU worker would compute in place on the server's read-only receive
+            # buffer (x.to(cpu) aliases it): take the one copy explicitly instead
+            x = x.clone()
         y = self._run_ops(x, ops, session)
         name, shp, buf = P.tensor_payload(y)
         return name, shp, buf

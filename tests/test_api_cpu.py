@@ -82,3 +82,24 @@ def test_request_sampling_merge():
     s = request_sampling({"temperature": 0.7, "top_p": 1.0, "top_k": 0}, d)
     assert s.temperature == 0.7 and s.top_p is None and s.top_k is None and s.seed == 1
     assert request_sampling({}, d) == d
+
+
+def test_max_tokens_beyond_max_seq_is_clamped(tmp_path):
+    """A request for more tokens than the KV cache holds stops at the cache end instead
+    of writing past it (all-local generator; the TP and pipeline engines clamp the same
+    way: tests/test_tp_cpu.py, tests/test_pipeline_cpu.py)."""
+    from fastapi.testclient import TestClient
+    from cake_amd.api.server import create_app
+    write_checkpoint(tmp_path, tiny_config(), torch.float32)
+    (tmp_path / "topo.yml").write_text("{}\n")
+    args = build_parser().parse_args(["--model", str(tmp_path), "--topology",
+                                      str(tmp_path / "topo.yml"), "--cpu", "--temperature", "0",
+                                      "--max-seq-len", "48"])
+    master = Master(Context.from_args(args))
+    c = TestClient(create_app(master))
+    r = c.post("/api/v1/chat/completions",
+               json={"messages": [{"role": "user", "content": "hello"}], "max_tokens": 500})
+    assert r.status_code == 200
+    n_prompt = len(master.llm.tokens) - r.json()["usage"]["completion_tokens"]
+    assert 0 < r.json()["usage"]["completion_tokens"] <= 48 - n_prompt
+    assert len(master.llm.tokens) == 48   # generated up to the last cache row, no further

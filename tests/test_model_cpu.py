@@ -75,6 +75,10 @@ def test_sampling_rules():
     assert {lp.sample(logits) for _ in range(50)} <= {1, 3}
     lp = LogitsProcessor(SamplingConfig(temperature=1.0, top_p=0.4, seed=3))
     assert {lp.sample(logits) for _ in range(50)} == {1}  # first token alone reaches p
+    # top-k then top-p: p applies to full-vocabulary probabilities (no renormalisation
+    # inside top-k): the top-2 mass here is ~0.93 < 0.95, so both stay in the set
+    lp = LogitsProcessor(SamplingConfig(temperature=1.0, top_k=2, top_p=0.95, seed=5))
+    assert {lp.sample(logits) for _ in range(200)} == {1, 3}
     a = LogitsProcessor(SamplingConfig(temperature=0.8, seed=7))
     b = LogitsProcessor(SamplingConfig(temperature=0.8, seed=7))
     assert [a.sample(logits) for _ in range(20)] == [b.sample(logits) for _ in range(20)]

@@ -10,7 +10,9 @@ pytestmark = pytest.mark.gpu
 
 
 def _expected_set(logits, T, k, p):
-    """Token set of candle's LogitsProcessor: top-k, then top-p within it."""
+    """Token set of the host LogitsProcessor (models/sampling.py, candle's
+    TopKThenTopP): top-k, then the top-p cutoff on the top-k tokens' FULL-vocabulary
+    probabilities (not renormalised: a top-k mass below p keeps all k)."""
     probs = torch.softmax(logits.double() / T, 0)
     keep = torch.ones_like(probs, dtype=torch.bool)
     if k:
@@ -19,7 +21,6 @@ def _expected_set(logits, T, k, p):
         keep[idx] = True
     if p is not None and 0 < p < 1:
         pr = torch.where(keep, probs, torch.zeros_like(probs))
-        pr = pr / pr.sum()
         order = torch.argsort(pr, descending=True, stable=True)
         before = torch.cumsum(pr[order], 0) - pr[order]
         kp = torch.zeros_like(keep)
@@ -29,7 +30,8 @@ def _expected_set(logits, T, k, p):
 
 
 @pytest.mark.parametrize("V,k,p", [(128256, 40, None), (128256, None, 0.9), (128256, 50, 0.8),
-                                   (1000, 7, None), (1000, None, 0.5), (300, 300, 0.999)])
+                                   (1000, 7, None), (1000, None, 0.5), (300, 300, 0.999),
+                                   (128256, 5, 0.9), (1000, 20, 0.3)])
 def test_threshold_set(cuda, V, k, p):
     from cake_amd.ops import hip as K
     torch.manual_seed(V + (k or 0))

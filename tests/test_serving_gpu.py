@@ -86,9 +86,13 @@ def test_rccl_pp2_api_serving_matches_local(cuda, tmp_path):
             except OSError:
                 assert time.time() < deadline, (tmp_path / "serve.log").read_text()[-3000:]
                 time.sleep(1.0)
-        got = [_post(port, r) for r in REQS]
-        # a third request equal to the first: per-request state is reset
-        again = _post(port, REQS[0])
+        try:
+            got = [_post(port, r) for r in REQS]
+            # a third request equal to the first: per-request state is reset
+            again = _post(port, REQS[0])
+        except Exception as e:  # noqa: BLE001  (show what the server said)
+            time.sleep(2)
+            raise AssertionError(f"{e!r}\n" + (tmp_path / "serve.log").read_text()[-4000:])
     finally:
         os.killpg(p.pid, signal.SIGTERM)
         try:

@@ -91,3 +91,58 @@ def test_split_and_checks():
     check_tp(preset("llama3-70b"), 8)
     with pytest.raises(ValueError):
         check_tp(preset("llama3-8b"), 3)
+
+
+def _sample_worker(rank, world, port, q):
+    from cake_amd.models.sampling import SamplingConfig
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cfg = _cfg(world)
+        m = random_model(cfg, "cpu", torch.float32, max_seq=64, seed=3)
+        blocks = {li: shard_block(w, cfg, rank, world) for li, w in m.stack.weights.items()}
+        head = shard_head(m.head.embed, m.head.norm, m.head.lm_head, rank, world)
+        comm = AllReduce(rank, world, "cpu", cfg.hidden_size, n_gather=cfg.vocab_size)
+        eng = TPEngine(cfg, blocks, head, rank, world, "cpu", torch.float32, 64, comm,
+                       repeat_penalty=1.1, repeat_last_n=16)
+        out = []
+        for seed in (11, 12):
+            eng.set_sampling(SamplingConfig(temperature=0.9, top_k=40, top_p=0.9, seed=seed))
+            eng.prefill(PROMPT)
+            eng.decode(STEPS)
+            out.append(list(eng.tokens))
+        q.put((rank, out))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_tp_sampling_matches_all_local():
+    """temperature / top-k / top-p under TP: the gathered full logits give every rank
+    the reference's draw (host LogitsProcessor, same seed) -> the all-local stream."""
+    from cake_amd.models.sampling import LogitsProcessor, SamplingConfig
+    world = 2
+    cfg = _cfg(world)
+    m = random_model(cfg, "cpu", torch.float32, max_seq=64, seed=3)
+    ref = []
+    for seed in (11, 12):
+        lp = LogitsProcessor(SamplingConfig(temperature=0.9, top_k=40, top_p=0.9, seed=seed))
+        toks = list(PROMPT)
+        logits = m.forward(PROMPT, 0)
+        for _ in range(STEPS + 1):
+            t = lp.sample(R.apply_repeat_penalty(logits, 1.1, toks[-16:]))
+            toks.append(t)
+            logits = m.forward([t], len(toks) - 1)
+        ref.append(toks)
+    assert ref[0] != ref[1]   # the seed matters
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_sample_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=180) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got[0] == got[1] == ref

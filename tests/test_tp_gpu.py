@@ -129,3 +129,88 @@ def test_bench_under_torchrun_uses_rccl(cuda, tmp_path):
         j = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
         assert j["n_gpus"] == 1 and j["value"] > 0
         assert j["config"]["parallelism"].startswith(par + "1"), j["config"]
+
+
+SAMPLE = dict(temperature=0.9, top_k=40, top_p=0.9)
+
+
+def _sample_worker(rank, world, port, q):
+    import torch.distributed as dist
+    from cake_amd.models.llama3.factory import random_model
+    from cake_amd.models.sampling import SamplingConfig
+    from cake_amd.parallel.tensor_parallel import AllReduce, TPEngine, shard_block, shard_head
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      HSA_ENABLE_IPC_MODE_LEGACY="0", CAKE_HOP_TIMEOUT="20")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        cfg = _cfg(world)
+        m = random_model(cfg, "cuda:0", torch.bfloat16, max_seq=64, seed=5)
+        blocks = {li: shard_block(w, cfg, rank, world) for li, w in m.stack.weights.items()}
+        head = shard_head(m.head.embed, m.head.norm, m.head.lm_head, rank, world)
+        del m
+        comm = AllReduce(rank, world, "cuda:0", cfg.hidden_size, n_gather=cfg.vocab_size)
+        eng = TPEngine(cfg, blocks, head, rank, world, "cuda:0", torch.bfloat16, 64, comm,
+                       repeat_penalty=1.1, repeat_last_n=16)
+        out, graph_ids = [], []
+        for seed in (7, 8):
+            eng.set_sampling(SamplingConfig(seed=seed, **SAMPLE))
+            eng.prefill(PROMPT)
+            eng.capture()
+            graph_ids.append(sorted(id(g) for g in eng.graphs["sample"].values()))
+            for _ in range(STEPS):
+                eng.launch()
+            torch.cuda.synchronize()
+            eng.check()
+            out.append(eng.b.hist[:int(eng.b.hist_len.item())].tolist())
+        q.put((rank, comm.mode, out, graph_ids))
+        comm.close()
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_tp_sampling_matches_single_gpu_without_recapture(cuda):
+    """TP2 temperature/top-k/top-p draw (gathered vocabulary + the single-GPU device
+    selection) equals the single-GPU DeviceDecoder's draw for the same seed; a second
+    request with another seed replays the same graphs (parameter block only)."""
+    import torch.multiprocessing as mp
+    from cake_amd.models.llama3.decode_loop import run_decode
+    from cake_amd.models.llama3.factory import random_model
+    from cake_amd.models.llama3.model import DeviceDecoder
+    from cake_amd.models.sampling import SamplingConfig
+    world = 2
+    m = random_model(_cfg(world), "cuda:0", torch.bfloat16, max_seq=64, seed=5)
+    dec = DeviceDecoder(m, repeat_penalty=1.1, repeat_last_n=16)
+    ref = []
+    for seed in (7, 8):
+        dec.set_sampling(SamplingConfig(seed=seed, **SAMPLE))
+        first = dec.start(PROMPT)
+        dec.capture()
+        ref.append(PROMPT + [first] + run_decode(dec, STEPS).tokens)
+    del dec, m
+    assert ref[0] != ref[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_sample_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = {}
+    try:
+        for _ in range(world):
+            r, used, out, gids = q.get(timeout=150)
+            got[r] = (used, out, gids)
+        for p in ps:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+    finally:
+        for p in ps:
+            if p.is_alive():
+                p.kill()
+    assert got[0][0] == "ipc"
+    assert got[0][1] == got[1][1]                # ranks agree token for token
+    assert got[0][2][0] == got[0][2][1]          # same graphs for the second seed
+    n = len(PROMPT) + 4                          # bf16 sum order: first tokens exact
+    for toks, want in zip(got[0][1], ref):
+        assert toks[:n] == want[:n], (toks, want)
