@@ -56,6 +56,11 @@ static inline int attn_max_split(int S) {
 // a max_seq-sized grid cost ~3.7 us per layer at 4096; the kernel stays correct
 // for any cap — fewer, longer splits).
 static int g_attn_split_cap = 0;
+static unsigned long long* g_attn_stamps = nullptr;  // diagnostics only
+CAKE_API int cake_attn_set_stamps(void* p) {
+  g_attn_stamps = (unsigned long long*)p;
+  return 0;
+}
 CAKE_API int cake_attn_set_split_cap(int cap) {
   if (cap < 0 || cap > kMaxSplit) return (int)hipErrorInvalidValue;
   g_attn_split_cap = cap;
@@ -91,7 +96,7 @@ CAKE_API int cake_attn_decode(int dt, const float* q, const void* kc, const void
   const dim3 grid(nkv, g_attn_split_cap > 0 && g_attn_split_cap < ms ? g_attn_split_cap : ms);
   const AttnDecArgs a{q, (const uint16_t*)kc, (const uint16_t*)vc, pos, S,
                       scale * 1.4426950408889634f, part, tickets, (uint16_t*)out,
-                      g_attn_min_keys, (int)grid.y};
+                      g_attn_min_keys, (int)grid.y, g_attn_stamps};
   DISPATCH_DT_HD(dt, hd, return (launch_decode<DT, HD>(nh / nkv, grid, st, a)));
   return (int)hipErrorInvalidValue;
 }

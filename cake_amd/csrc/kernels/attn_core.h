@@ -101,7 +101,16 @@ struct AttnDecArgs {
   unsigned int* tickets;   // [nkv], zero between launches
   uint16_t* out;           // [nh*hd]
   int min_keys, maxsplit;
+  unsigned long long* stamps;  // diagnostics (nullptr in production): per-WG phase clocks
 };
+
+// Phase clock of workgroup (g, s) for the latency breakdown (scripts/attn_stamps.py):
+// slot k of 8, shader-clock ticks (s_memtime) from thread 0.
+#define ATTN_STAMP(k)                                                              \
+  do {                                                                             \
+    if (a.stamps != nullptr && threadIdx.x == 0)                                   \
+      stamp[k] = __builtin_amdgcn_s_memtime();                                     \
+  } while (0)
 
 template <int DT, int HD, int NREP>
 __device__ __forceinline__ void attn_decode_block(const AttnDecArgs& a, int g, int s,
@@ -118,6 +127,8 @@ __device__ __forceinline__ void attn_decode_block(const AttnDecArgs& a, int g, i
   unsigned int& last_flag = *reinterpret_cast<unsigned int*>(ps + NREP * kChunk);
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  unsigned long long stamp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  ATTN_STAMP(0);
   const uint16_t* kg = a.kc + (size_t)g * a.S * HD;
   const uint16_t* vg = a.vc + (size_t)g * a.S * HD;
   // The loads of the next chunk are issued before the current chunk is computed
@@ -139,6 +150,7 @@ __device__ __forceinline__ void attn_decode_block(const AttnDecArgs& a, int g, i
     }
   }
   const int Tk = *a.pos + 1;
+  ATTN_STAMP(1);
   // past 1024 keys two chunks per split: every extra chunk per split costs about
   // one load round trip (~1.8 us), every extra split ~0.05-0.1 us of merge
   // (profiles/r2_decode_attn_pv*.jsonl: 2048 keys 11.7 us in 17 splits vs 12.4 in 33)
@@ -176,6 +188,7 @@ __device__ __forceinline__ void attn_decode_block(const AttnDecArgs& a, int g, i
   }
   kv_store<HD, IPW>(rk, rv, smem, wave, lane, ke - 1 - kb);
   __syncthreads();
+  ATTN_STAMP(2);
   int buf = 0;
   for (int c0 = kb; c0 < ke; c0 += kChunk, buf ^= 1) {
     const int kn = min(kChunk, ke - c0);
@@ -260,14 +273,24 @@ __device__ __forceinline__ void attn_decode_block(const AttnDecArgs& a, int g, i
     __syncthreads();           // next chunk visible; this buffer free for reuse
   }
 
+  ATTN_STAMP(3);
   // combine the key groups: afterwards every lane of dim group dg holds its 8 sums
 #pragma unroll
   for (int d = 0; d < 8; ++d) {
     if constexpr (DG <= 8) o[d] = xor_add<8>(o[d]);
     o[d] = xor_add<32>(xor_add<16>(o[d]));
   }
+  ATTN_STAMP(4);
+  auto flush_stamps = [&](int n) {
+    if (a.stamps != nullptr && tid == 0) {
+      unsigned long long* d = a.stamps + ((size_t)s * gridDim.x + g) * 8;
+      for (int k = 0; k < 8; ++k) d[k] = k < n ? stamp[k] : 0ull;
+    }
+  };
   const int h = g * NREP + wave;
   if (ns == 1) {  // the whole context in this split: finish here
+    ATTN_STAMP(5);
+    flush_stamps(6);
     if (wave < NREP && kgi == 0) {
       const float inv = 1.f / l;
       uint16_t ob[8];
@@ -290,6 +313,7 @@ __device__ __forceinline__ void attn_decode_block(const AttnDecArgs& a, int g, i
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  ATTN_STAMP(5);
   if (tid == 0) {
     const unsigned int t =
         __hip_atomic_fetch_add(&a.tickets[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -298,6 +322,8 @@ __device__ __forceinline__ void attn_decode_block(const AttnDecArgs& a, int g, i
     last_flag = last;
   }
   __syncthreads();
+  ATTN_STAMP(6);
+  if (!last_flag) flush_stamps(7);
   if (!last_flag || wave >= NREP) return;
 
   // merge the ns <= 64 partials of this wave's head: lane t owns split t's (m, l)
@@ -336,6 +362,8 @@ __device__ __forceinline__ void attn_decode_block(const AttnDecArgs& a, int g, i
   uint16_t* dst = a.out + (size_t)h * HD + lane * DPL;
 #pragma unroll
   for (int d = 0; d < DPL; ++d) dst[d] = from_f32<DT>(acc[d] * inv);
+  ATTN_STAMP(7);
+  flush_stamps(8);
 }
 
 }  // namespace cake

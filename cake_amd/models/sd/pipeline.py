@@ -74,7 +74,10 @@ class SDGenerator(ImageGenerator):
         self.last_step_s: list[float] = []
 
     @classmethod
-    def load(cls, ctx) -> "SDGenerator":
+    def load(cls, ctx, remote=None) -> "SDGenerator":
+        """remote(name) -> a proxy for a component served by another rank of a
+        device-transport job (parallel/sd_rccl.py), or None; otherwise the topology
+        decides between a local unit and a TCP worker."""
         from tokenizers import Tokenizer
 
         from ...parallel.client import Client
@@ -96,6 +99,13 @@ class SDGenerator(ImageGenerator):
         clients: dict[str, Client] = {}
 
         def component(name):
+            if remote is not None:
+                proxy = remote(name)
+                if proxy is not None:
+                    log.info("%s is served by %s", name, proxy.ident())
+                    return proxy
+                log.info("%s will be served locally", name)
+                return load_unit(name, ctx, cfg)
             node = ctx.topology.get_node_for_layer(name)
             if node is not None:
                 if node.name not in clients:
@@ -134,11 +144,17 @@ class SDGenerator(ImageGenerator):
             emb = torch.cat([u.to(self.device), emb.to(self.device)], 0)
         return emb.to(device=self.device, dtype=self.dtype)
 
-    def _fused_steps(self) -> bool:
+    def _fused_steps(self, intermediary: bool = False) -> bool:
+        """Whole denoising loop as per-step graph replays: a local UNet, or one worker
+        rank holding the entire UNet (device transport; the host needs no latents
+        between steps unless intermediary images are requested)."""
         import os
 
         from .shardable import SDUnit
-        return (isinstance(self.unet, SDUnit) and torch.device(self.device).type == "cuda"
+        local = isinstance(self.unet, SDUnit)
+        if not (local or (getattr(self.unet, "can_denoise", False) and not intermediary)):
+            return False
+        return (torch.device(self.device).type == "cuda"
                 and self.dtype in (torch.float16, torch.bfloat16)
                 and os.environ.get("CAKE_SD_FUSED_STEP", "1") != "0")
 
@@ -211,7 +227,7 @@ class SDGenerator(ImageGenerator):
                 shape = (args.bsize, 4, cfg.height // 8, cfg.width // 8)
                 latents = torch.randn(shape, generator=gen).to(self.device) * sched.init_noise_sigma
             latents = latents.float()
-            if self._fused_steps() and t_start < len(ts):
+            if self._fused_steps(bool(args.intermediary_images)) and t_start < len(ts):
                 # local UNet on the GPU: each step is one graph replay (device timestep,
                 # UNet, CFG + scheduler update + next input; SDUnit.denoise)
                 steps = ts[t_start:]

@@ -28,6 +28,7 @@ class DDIMScheduler:
 
     def __init__(self, cfg: SchedulerConfig, steps: int):
         self.cfg = cfg
+        self.n_steps = steps
         self.acp = _alphas_cumprod(cfg)
         self.step_ratio = cfg.train_timesteps // steps
         self._timesteps = [s * self.step_ratio + cfg.steps_offset for s in range(steps)][::-1]
@@ -85,6 +86,7 @@ class EulerAncestralScheduler:
 
     def __init__(self, cfg: SchedulerConfig, steps: int):
         self.cfg = cfg
+        self.n_steps = steps
         acp = _alphas_cumprod(cfg)
         sig = ((1 - acp) / acp).sqrt()
         T = cfg.train_timesteps

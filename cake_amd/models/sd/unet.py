@@ -363,11 +363,26 @@ class UNet2DConditionModel(Module):
         with ops.layout_nhwc(ops.want_nhwc(sample)):
             return ops.to_external(self._body(W, ops.to_internal(sample), tbs, ctx, kv_cache))
 
-    def _body(self, W, sample, tbs, ctx, kv_cache):
+    # ------------------------------------------------------------------ stages
+    # The body as a chain of block-group stages ("down.0" .. "down.{n-1}", "mid",
+    # "up.0" .. "up.{n-1}"): the unit of UNet placement across ranks (beyond the
+    # reference, which places the UNet whole: sd.rs:200-300).  The state between
+    # stages is the running feature map plus the skip stack of the down path.
+    def stage_names(self) -> list[str]:
+        n = len(self.down)
+        return [f"down.{i}" for i in range(n)] + ["mid"] + [f"up.{i}" for i in range(n)]
+
+    def run_stage(self, W, name: str, x: torch.Tensor, skips: list, tbs, ctx, kv_cache):
+        """One stage over (x, skips) in the active layout; returns the new (x, skips).
+        down.0 takes the UNet input (conv_in); the last up stage ends in conv_out."""
         cfg = self.cfg
-        x = self.conv_in(W, sample)
-        skips = [x]
-        for res, att, ds in self.down:
+        kind, _, idx = name.partition(".")
+        if kind == "down":
+            i = int(idx)
+            if i == 0:
+                x = self.conv_in(W, x)
+                skips = [x]
+            res, att, ds = self.down[i]
             for j, r in enumerate(res):
                 x = r(W, x, tb=tbs[r.name])
                 if att:
@@ -376,16 +391,46 @@ class UNet2DConditionModel(Module):
             if ds is not None:
                 x = ds(W, x)
                 skips.append(x)
-        x = self.mid_res[0](W, x, tb=tbs[self.mid_res[0].name])
-        x = self.mid_att(W, x, ctx, kv_cache)
-        x = self.mid_res[1](W, x, tb=tbs[self.mid_res[1].name])
-        for res, att, us in self.up:
-            for j, r in enumerate(res):
-                x = r(W, torch.cat([x, skips.pop()], ops.cdim()), tb=tbs[r.name])
-                if att:
-                    x = att[j](W, x, ctx, kv_cache)
-            if us is not None:
-                x = us(W, x, up=True)  # nearest-2x upsample fused into the conv
-        x = ops.group_norm(x, W["conv_norm_out.weight"], W["conv_norm_out.bias"],
-                           cfg.norm_num_groups, cfg.norm_eps, silu=True)
-        return self.conv_out(W, x)
+            return x, skips
+        if kind == "mid":
+            x = self.mid_res[0](W, x, tb=tbs[self.mid_res[0].name])
+            x = self.mid_att(W, x, ctx, kv_cache)
+            x = self.mid_res[1](W, x, tb=tbs[self.mid_res[1].name])
+            return x, skips
+        i = int(idx)
+        res, att, us = self.up[i]
+        for j, r in enumerate(res):
+            x = r(W, torch.cat([x, skips.pop()], ops.cdim()), tb=tbs[r.name])
+            if att:
+                x = att[j](W, x, ctx, kv_cache)
+        if us is not None:
+            x = us(W, x, up=True)  # nearest-2x upsample fused into the conv
+        if i == len(self.up) - 1:
+            x = ops.group_norm(x, W["conv_norm_out.weight"], W["conv_norm_out.bias"],
+                               cfg.norm_num_groups, cfg.norm_eps, silu=True)
+            x = self.conv_out(W, x)
+        return x, skips
+
+    def forward_stages(self, W, names: list[str], x: torch.Tensor, skips: list, timestep, ctx,
+                       kv_cache: dict | None = None, t_index=None):
+        """Run consecutive stages: the building block of a UNet split over ranks.  The
+        UNet input (before down.0) and output (after the last up stage) are NCHW;
+        the (x, skips) handed between stages stay in the active internal layout (the
+        ranks of one job share it), so a hop moves them as they are."""
+        B = x.shape[0]
+        tbs = self.time_biases(W, timestep, B, x.dtype, x.device, t_index)
+        last = self.stage_names()[-1]
+        with ops.layout_nhwc(ops.want_nhwc(x)):
+            if names[0] == "down.0":
+                x = ops.to_internal(x)
+            for n in names:
+                x, skips = self.run_stage(W, n, x, skips, tbs, ctx, kv_cache)
+            if names[-1] == last:
+                x = ops.to_external(x)
+            return x, skips
+
+    def _body(self, W, sample, tbs, ctx, kv_cache):
+        x, skips = sample, []
+        for n in self.stage_names():
+            x, skips = self.run_stage(W, n, x, skips, tbs, ctx, kv_cache)
+        return x

@@ -328,6 +328,10 @@ def run_tp(ctx) -> None:
 
 
 def run_rccl(ctx) -> None:
+    if ctx.model_type == "image-model":
+        from .sd_rccl import run_sd_rccl
+        run_sd_rccl(ctx)
+        return
     if getattr(ctx.args, "parallel", "pp") == "tp":
         run_tp(ctx)
         return
