@@ -6,7 +6,9 @@ travel with the repository snapshot to the GPU box:
 * ``libcake_kernels.so`` — every ``csrc/kernels/*.hip`` file, ``hipcc
   --offload-arch=gfx950``; plain C ABI (``extern "C" cake_*``) driven from
   :mod:`cake_amd.ops.hip` through ctypes with torch's current HIP stream, so
-  the launches are capturable in hipGraphs.
+  the launches are capturable in hipGraphs.  Also ``csrc/driver/*.cpp``: the
+  native decode loop that replays the captured step graphs
+  (:mod:`cake_amd.runtime.graph_loop`).
 * ``libcake_runtime.so`` — ``csrc/runtime/*.cpp`` (topology parser, wire codec,
   safetensors mmap reader/writer, framed TCP transport), C ABI.
 * ``cake-split-model`` — native executable (``csrc/tools/split_model.cpp``).
@@ -95,7 +97,8 @@ def _py_ext_flags() -> tuple[list[str], str]:
 PY_EXT = LIB / "_cake_runtime"  # + EXT_SUFFIX
 
 def build_kernels(force: bool = False, jobs: int = 8) -> Path:
-    srcs = sorted((CSRC / "kernels").glob("*.hip"))
+    # HIP kernels + the native graph-replay decode driver (host code on the HIP runtime)
+    srcs = sorted((CSRC / "kernels").glob("*.hip")) + sorted((CSRC / "driver").glob("*.cpp"))
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         objs = list(ex.map(lambda s: _compile_hip(s, force), srcs))
     LIB.mkdir(parents=True, exist_ok=True)

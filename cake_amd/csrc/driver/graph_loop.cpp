@@ -1,0 +1,193 @@
+// Native decode driver: the per-token host loop of every serving mode.
+//
+// Replaces the reference master's token loop (cake-core/src/cake/master.rs:80-124:
+// `next_token` per step, tok/s timer restarted after the first token) and the
+// generator's per-step forward + sample (cake-core/src/models/llama3/llama.rs:277-341).
+// Here one decode step (every layer, the head and the token choice, plus the
+// device-side pipeline hops / all-reduces of a multi-rank engine) is ONE captured
+// hipGraph, and the chosen token never leaves the device except for reporting.
+// What is left for the host is this loop, in C++ with the Python GIL released:
+//
+//   * replay the step graph whose decode-attention split cap covers the live
+//     length (one graph per position bucket, chosen through a host table),
+//   * copy the replay's k tokens from the device history into a pinned ring and
+//     record an event — and only then wait for the PREVIOUS replay's event, so
+//     the GPU always has the next step queued while the host reads one back,
+//   * stop at EOS, at n tokens, or when the per-token callback asks (streaming
+//     API clients), and report per-token device time (p50/p99: BASELINE.md §2).
+//
+// A worker rank of a pipeline / tensor-parallel engine passes no history and no
+// callbacks: its replays are enqueued at once and paced by the device-side receives.
+// An optional `announce` callback runs one chunk of replays ahead of them (the
+// master's control message telling the workers how many replays to enqueue).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <chrono>
+#include <vector>
+
+#define CAKE_API extern "C" __attribute__((visibility("default")))
+
+extern "C" {
+typedef int32_t (*cake_token_cb)(void* ctx, int32_t token);
+typedef int32_t (*cake_announce_cb)(void* ctx, int32_t first, int32_t count);
+
+struct CakeLoopSpec {
+  void* const* execs;         // hipGraphExec_t per position bucket
+  int32_t n_execs;
+  const int32_t* bucket_of;   // [n_len]: bucket for the live length after a replay
+  int32_t n_len;
+  int32_t k;                  // decode steps per replay (tokens per graph)
+  const int32_t* hist;        // device token history, or null (worker: no read-back)
+  int32_t base;               // history index of the first token this run generates
+  int32_t pos;                // host mirror of the device position (last written row)
+  int32_t n;                  // tokens to generate (replays = ceil(n / k))
+  int32_t chunk;              // replays per announce (0: everything at once)
+  const int32_t* eos;         // EOS ids (host)
+  int32_t n_eos;
+  cake_token_cb on_token;     // optional; non-zero return = stop
+  void* token_ctx;
+  cake_announce_cb announce;  // optional; non-zero return = error
+  void* announce_ctx;
+  void* stream;               // hipStream_t
+  int32_t* out_tokens;        // host [out_cap]
+  float* out_ms;              // host [out_cap]: device time per token (ms)
+  int32_t out_cap;
+};
+
+struct CakeLoopResult {
+  int32_t n_tokens;   // tokens reported (stopped at EOS inclusive)
+  int32_t replays;    // graph replays enqueued
+  int32_t pos;        // host position after the last enqueued replay
+  int32_t stopped;    // 1 = EOS / callback stop, 0 = ran to n
+  double wall_s;
+};
+}
+
+namespace {
+
+struct Ring {
+  int32_t* host = nullptr;
+  std::vector<hipEvent_t> ev;
+  ~Ring() {
+    if (host) (void)hipHostFree(host);
+    for (auto e : ev) (void)hipEventDestroy(e);
+  }
+};
+
+inline int fail(hipError_t e) { return (int)e; }
+
+}  // namespace
+
+#define CAKE_TRY(x)                              \
+  do {                                           \
+    const hipError_t e_ = (x);                   \
+    if (e_ != hipSuccess) return fail(e_);       \
+  } while (0)
+
+CAKE_API int cake_graph_decode(const CakeLoopSpec* s, CakeLoopResult* r) {
+  if (!s || !r || s->n_execs <= 0 || !s->execs || s->k <= 0 || s->n < 0 || !s->bucket_of ||
+      s->n_len <= 0)
+    return (int)hipErrorInvalidValue;
+  *r = CakeLoopResult{0, 0, s->pos, 0, 0.0};
+  if (s->n == 0) return 0;
+  const auto t0 = std::chrono::steady_clock::now();
+  hipStream_t st = (hipStream_t)s->stream;
+  const int k = s->k;
+  const int replays = (s->n + k - 1) / k;
+  const bool readback = s->hist != nullptr;
+  if (readback && (!s->out_tokens || s->out_cap < s->n)) return (int)hipErrorInvalidValue;
+  const int chunk = s->chunk > 0 ? s->chunk : replays;
+  int pos = s->pos;
+  // one replay of the graph whose attention split cap covers the live length at its
+  // last step (+1: room for a pushed token)
+  auto launch = [&]() -> hipError_t {
+    int len = pos + k + 1;
+    if (len >= s->n_len) len = s->n_len - 1;
+    int b = s->bucket_of[len];
+    if (b < 0 || b >= s->n_execs) b = s->n_execs - 1;
+    pos += k;
+    return hipGraphLaunch((hipGraphExec_t)s->execs[b], st);
+  };
+  if (!readback && !s->on_token && !s->announce) {
+    // worker rank: enqueue every replay and return at once (the device-side
+    // receives pace them; the host goes back to its control channel)
+    for (int i = 0; i < replays; ++i) CAKE_TRY(launch());
+    r->replays = replays;
+    r->pos = pos;
+    return 0;
+  }
+
+  // two ring slots of k tokens (replay p+1 fills one while p is read from the
+  // other); three replay events (p+1 is recorded while p-1's still bounds p's
+  // interval) and a start event
+  Ring ring;
+  if (readback) CAKE_TRY(hipHostMalloc((void**)&ring.host, sizeof(int32_t) * 2 * k,
+                                       hipHostMallocDefault));
+  ring.ev.resize(4, nullptr);
+  for (auto& e : ring.ev) CAKE_TRY(hipEventCreate(&e));
+  CAKE_TRY(hipEventRecord(ring.ev[3], st));
+  hipEvent_t prev_done = ring.ev[3];
+
+  int issued = 0;          // replays enqueued
+  int announced = 0;       // replays announced to the workers
+  int pending = -1;        // replay index waiting for read-back
+  bool stop = false;
+  while (!stop) {
+    int cur = -1;
+    if (issued < replays) {
+      // keep the announcements one chunk ahead of the replays, so the workers have
+      // the next chunk enqueued before the master reaches it
+      while (s->announce && announced < replays && announced - issued <= chunk) {
+        const int c = chunk < replays - announced ? chunk : replays - announced;
+        if (s->announce(s->announce_ctx, announced, c) != 0) return (int)hipErrorUnknown;
+        announced += c;
+      }
+      CAKE_TRY(launch());
+      const int slot = issued & 1;
+      if (readback) {
+        const int lo = s->base + issued * k;
+        CAKE_TRY(hipMemcpyAsync(ring.host + slot * k, s->hist + lo, sizeof(int32_t) * k,
+                                hipMemcpyDeviceToHost, st));
+      }
+      CAKE_TRY(hipEventRecord(ring.ev[issued % 3], st));
+      cur = issued++;
+    }
+    if (pending >= 0) {
+      const int slot = pending & 1;
+      hipEvent_t done = ring.ev[pending % 3];
+      CAKE_TRY(hipEventSynchronize(done));
+      float ms = 0.f;
+      CAKE_TRY(hipEventElapsedTime(&ms, prev_done, done));
+      ms /= (float)k;
+      const int have = s->n - pending * k;
+      const int m = have < k ? have : k;
+      for (int i = 0; i < m && !stop; ++i) {
+        const int idx = r->n_tokens;
+        if (idx < s->out_cap && s->out_ms) s->out_ms[idx] = ms;
+        if (readback) {
+          const int32_t tok = ring.host[slot * k + i];
+          s->out_tokens[idx] = tok;
+          r->n_tokens = idx + 1;
+          if (s->on_token && s->on_token(s->token_ctx, tok) != 0) stop = true;
+          for (int e = 0; e < s->n_eos && !stop; ++e)
+            if (s->eos[e] == tok) stop = true;
+        } else {
+          r->n_tokens = idx + 1;
+        }
+      }
+      prev_done = done;  // the next replay's interval starts where this one ended
+    }
+    pending = cur;
+    if (pending < 0) break;
+  }
+  // replays announced to the workers but not yet issued (a stop inside an announced
+  // chunk) still run, unread: every rank must replay the same number of hops
+  for (; issued < announced; ++issued) CAKE_TRY(launch());
+  CAKE_TRY(hipStreamSynchronize(st));
+  r->replays = issued;
+  r->pos = pos;
+  r->stopped = stop ? 1 : 0;
+  r->wall_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  return 0;
+}

@@ -491,6 +491,59 @@ __global__ __launch_bounds__(256) void conv_splitk_finalize(ConvArgs a, int spli
   conv_epilogue<DT>(a, oc, p, v);
 }
 
+// Direct 3x3 convolution for the few-input-channel layers (UNet / VAE conv_in on
+// the 4 latent channels, the VAE encoder's RGB input): K = 9 * IC is too short
+// for the implicit GEMM's 64-wide K steps, and the work is small (P x OC x 36
+// FMAs), so it runs on the VALU.  The whole filter sits in LDS as f32
+// [9*IC][OC]; a thread owns 8 output channels of one pixel (channel group
+// fastest, so a wave's stores are contiguous), keeps its 9*IC input taps in
+// registers and reads the filter rows as LDS broadcasts / 32-byte vectors.
+// Bias, per-sample bias2 and the residual are fused as in conv_epilogue.
+constexpr int kSmallCMaxW = 18432;  // f32 filter elements in LDS (72 KB: OC <= 512 at IC = 4)
+
+template <int DT, int IC>
+__global__ __launch_bounds__(256) void conv_smallc_kernel(ConvArgs a) {
+  constexpr int KK = 9 * IC;
+  __shared__ __attribute__((aligned(16))) float wsm[kSmallCMaxW];
+  const int OC = a.OC;
+  for (int i = threadIdx.x; i < KK * OC; i += 256) {
+    const int k = i / OC, oc = i - k * OC;  // packed w [OC][3][3][IC]: k = (kh*3+kw)*IC + ic
+    wsm[i] = to_f32<DT>(a.w[(size_t)oc * KK + k]);
+  }
+  __syncthreads();
+  const int G = OC >> 3, ohw = a.OH * a.OW;
+  const long long total = (long long)a.P * G;
+  for (long long t = (long long)blockIdx.x * 256 + threadIdx.x; t < total;
+       t += (long long)gridDim.x * 256) {
+    const int p = (int)(t / G), og = (int)(t - (long long)p * G);
+    const int n = p / ohw, r = p - n * ohw, oh = r / a.OW, ow = r - oh * a.OW;
+    float xin[KK];
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int ih = oh * a.stride - a.pad + kh, iw = ow * a.stride - a.pad + kw;
+        const bool ok = ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
+        const uint16_t* src = a.x + (((size_t)n * a.H + (ok ? ih : 0)) * a.W + (ok ? iw : 0)) * IC;
+#pragma unroll
+        for (int c = 0; c < IC; ++c) xin[(kh * 3 + kw) * IC + c] = ok ? to_f32<DT>(src[c]) : 0.f;
+      }
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const float* wr = wsm + og * 8;
+#pragma unroll
+    for (int k = 0; k < KK; ++k) {
+      const float4 w0 = *reinterpret_cast<const float4*>(wr + k * OC);
+      const float4 w1 = *reinterpret_cast<const float4*>(wr + k * OC + 4);
+      acc[0] = fmaf(xin[k], w0.x, acc[0]); acc[1] = fmaf(xin[k], w0.y, acc[1]);
+      acc[2] = fmaf(xin[k], w0.z, acc[2]); acc[3] = fmaf(xin[k], w0.w, acc[3]);
+      acc[4] = fmaf(xin[k], w1.x, acc[4]); acc[5] = fmaf(xin[k], w1.y, acc[5]);
+      acc[6] = fmaf(xin[k], w1.z, acc[6]); acc[7] = fmaf(xin[k], w1.w, acc[7]);
+    }
+    conv_epilogue<DT>(a, og * 8, p, acc);
+    conv_epilogue<DT>(a, og * 8 + 4, p, acc + 4);
+  }
+}
+
 }  // namespace cake
 
 using namespace cake;
@@ -504,13 +557,34 @@ CAKE_API long long cake_conv2d_workspace(int P, int OC, int splits) {
 //      +4 = the same tiles with LDS-DMA staging (needs `zeros`);
 //      8/9 = halo kernel, 128/64 oc x (th x tw <= 128 pixels), 10/11 = 128/64 oc x
 //      (th x tw <= 64 pixels), 12/13 = 128/64 oc x (th x tw <= 256 pixels, 8 waves);
-//      stride 1 only, no split-K.
+//      stride 1 only, no split-K; 14 = direct 3x3 kernel for IC 3 / 4 (conv_in).
 CAKE_API int cake_conv2d_nhwc(int dt, const void* x, const void* w, const void* bias,
                               const float* bias2, const void* resid, void* out, float* ws,
                               const void* zeros,
                               int N, int H, int W, int IC, int OC, int KH, int KW, int stride,
                               int pad, int up, int cfg, int splits, int th, int tw,
                               int bias2_ld, hipStream_t st) {
+  if (cfg == 14) {  // direct small-IC 3x3 kernel
+    if ((IC != 3 && IC != 4) || KH != 3 || KW != 3 || OC % 8 || 9 * IC * OC > kSmallCMaxW ||
+        N <= 0 || stride <= 0 || up || (bias2 && bias2_ld > 0 && (bias2_ld % 4 || bias2_ld < OC)))
+      return (int)hipErrorInvalidValue;
+    const int OH = (H + 2 * pad - 3) / stride + 1, OW = (W + 2 * pad - 3) / stride + 1;
+    if (OH <= 0 || OW <= 0) return (int)hipErrorInvalidValue;
+    ConvArgs a{(const uint16_t*)x, (const uint16_t*)w, (const uint16_t*)bias, bias2,
+               (const uint16_t*)resid, (uint16_t*)out, nullptr, nullptr, N, H, W, IC, OC, OH, OW,
+               3, 3, stride, pad, 0, N * OH * OW, 0, 0, 0, 0};
+    a.bias2_ld = bias2_ld > 0 ? bias2_ld : OC;
+    const long long work = (long long)a.P * (OC / 8);
+    const unsigned grid = (unsigned)std::min<long long>((work + 255) / 256, 2048);
+#define CAKE_SMALLC(DTV)                                                                         \
+    if (IC == 3) hipLaunchKernelGGL((conv_smallc_kernel<DTV, 3>), dim3(grid), dim3(256), 0, st, a); \
+    else hipLaunchKernelGGL((conv_smallc_kernel<DTV, 4>), dim3(grid), dim3(256), 0, st, a);
+    if (dt == kBF16) { CAKE_SMALLC(kBF16); }
+    else if (dt == kF16) { CAKE_SMALLC(kF16); }
+    else return (int)hipErrorInvalidValue;
+#undef CAKE_SMALLC
+    return (int)hipGetLastError();
+  }
   if (IC % 64 || OC % 4 || N <= 0 || stride <= 0 || KH <= 0 || KW <= 0 || splits <= 0 ||
       (bias2 && bias2_ld > 0 && (bias2_ld % 4 || bias2_ld < OC)) ||
       (up && stride != 1) || cfg < 0 || cfg > 13 || (splits > 1 && !ws) || (cfg > 3 && !zeros))

@@ -240,8 +240,22 @@ __global__ __launch_bounds__(256) void geglu_vec_kernel(const uint16_t* __restri
 // ---------------------------------------------------------------------------
 constexpr int kGnMaxC = 4096;
 
+// Two-source input (the UNet up path's skip concatenation, never materialised
+// by a separate copy): channels [0, Cx) come from x [N, HW, Cx], channels
+// [Cx, C) from x2 [N, HW, C - Cx]; Cx == C is the plain one-source case.
+struct GnSrc {
+  const uint16_t* x;
+  const uint16_t* x2;
+  int Cx;
+  // 8 channels starting at c (c % 8 == 0, Cx % 8 == 0) of pixel p of image n
+  __device__ __forceinline__ const uint16_t* at(int n, int HW, int C, size_t p, int c) const {
+    return c < Cx ? x + ((size_t)n * HW + p) * Cx + c
+                  : x2 + ((size_t)n * HW + p) * (C - Cx) + (c - Cx);
+  }
+};
+
 template <int DT>
-__global__ __launch_bounds__(512) void gn_nhwc_stats_kernel(const uint16_t* __restrict__ x, int HW,
+__global__ __launch_bounds__(512) void gn_nhwc_stats_kernel(GnSrc src, int HW,
                                                             int C, int G, double* __restrict__ part,
                                                             unsigned int* __restrict__ tickets,
                                                             float* __restrict__ stats) {
@@ -253,10 +267,11 @@ __global__ __launch_bounds__(512) void gn_nhwc_stats_kernel(const uint16_t* __re
   const int per = (HW + S - 1) / S, p0 = sp * per, p1 = min(HW, p0 + per);
   double s0 = 0.0, q0 = 0.0, s1 = 0.0, q1 = 0.0;
   if (py < Ty) {
-    const uint16_t* base = x + ((size_t)n * HW) * C + cv * 8;
+    const uint16_t* base = src.at(n, HW, C, 0, cv * 8);
+    const int ld = cv * 8 < src.Cx ? src.Cx : C - src.Cx;
     for (int p = p0 + py; p < p1; p += Ty) {
       float f[8];
-      unpack8<DT>(*reinterpret_cast<const uint4*>(base + (size_t)p * C), f);
+      unpack8<DT>(*reinterpret_cast<const uint4*>(base + (size_t)p * ld), f);
       float a0 = 0.f, b0 = 0.f, a1 = 0.f, b1 = 0.f;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -332,13 +347,16 @@ __global__ __launch_bounds__(512) void gn_nhwc_stats_kernel(const uint16_t* __re
   }
 }
 
+// cat (optional): the raw two-source input written out as one [N, HW, C]
+// tensor for the consumers that need it unnormalised (the resnet's 1x1 shortcut)
 template <int DT, bool SILU>
-__global__ __launch_bounds__(256) void gn_nhwc_apply_kernel(const uint16_t* __restrict__ x,
+__global__ __launch_bounds__(256) void gn_nhwc_apply_kernel(GnSrc src,
                                                             const uint16_t* __restrict__ gamma,
                                                             const uint16_t* __restrict__ beta,
                                                             const float* __restrict__ stats,
                                                             int HW, int C, int G, float eps,
-                                                            uint16_t* __restrict__ y) {
+                                                            uint16_t* __restrict__ y,
+                                                            uint16_t* __restrict__ cat) {
   __shared__ float sc[kGnMaxC], sh[kGnMaxC];
   const int n = blockIdx.y, Cg = C / G;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
@@ -355,8 +373,10 @@ __global__ __launch_bounds__(256) void gn_nhwc_apply_kernel(const uint16_t* __re
   for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv;
        v += (size_t)gridDim.x * blockDim.x) {
     const int c0 = (int)(v % (C >> 3)) * 8;
+    const uint4 raw = *reinterpret_cast<const uint4*>(src.at(n, HW, C, v / (C >> 3), c0));
+    if (cat != nullptr) *reinterpret_cast<uint4*>(cat + base + v * 8) = raw;
     float f[8];
-    unpack8<DT>(*reinterpret_cast<const uint4*>(x + base + v * 8), f);
+    unpack8<DT>(raw, f);
     uint16_t o[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -453,11 +473,15 @@ CAKE_API int cake_groupnorm_nhwc_splits(int HW) {
   return s < 1 ? 1 : (s > 256 ? 256 : s);
 }
 
-CAKE_API int cake_groupnorm_nhwc(int dt, const void* x, const void* gamma, const void* beta, int N,
-                                 int HW, int C, int G, float eps, int silu_act, double* part,
-                                 unsigned int* tickets, float* stats, void* y, hipStream_t st) {
+// Two-source form: x [N, HW, Cx] ++ x2 [N, HW, C - Cx] along channels (x2 null
+// when Cx == C); cat (optional) receives the concatenated raw input.
+CAKE_API int cake_groupnorm_nhwc2(int dt, const void* x, const void* x2, int Cx, void* cat,
+                                  const void* gamma, const void* beta, int N, int HW, int C, int G,
+                                  float eps, int silu_act, double* part, unsigned int* tickets,
+                                  float* stats, void* y, hipStream_t st) {
   if (C % G || C % 8 || C > kGnMaxC || C / 8 > 512 || N <= 0 || HW <= 0 || (C / G) < 1 || G > 256)
     return (int)hipErrorInvalidValue;
+  if (Cx <= 0 || Cx > C || Cx % 8 || (Cx < C && x2 == nullptr)) return (int)hipErrorInvalidValue;
   // every 8-channel vector must span at most two groups
   if ((C / G) < 8 && 8 % (C / G)) return (int)hipErrorInvalidValue;
   if ((C / G) < 4) return (int)hipErrorInvalidValue;
@@ -465,17 +489,25 @@ CAKE_API int cake_groupnorm_nhwc(int dt, const void* x, const void* gamma, const
   const int S = cake_groupnorm_nhwc_splits(HW);
   const size_t nv = (size_t)HW * (C / 8);
   const unsigned ab = (unsigned)std::min<size_t>((nv + 255) / 256, 1024);
+  const GnSrc src{(const uint16_t*)x, (const uint16_t*)x2, Cx};
   DISPATCH_DT(dt, {
-    hipLaunchKernelGGL((gn_nhwc_stats_kernel<DT>), dim3(S, N), dim3(Tx * Ty), 0, st,
-                       (const uint16_t*)x, HW, C, G, part, tickets, stats);
+    hipLaunchKernelGGL((gn_nhwc_stats_kernel<DT>), dim3(S, N), dim3(Tx * Ty), 0, st, src, HW, C,
+                       G, part, tickets, stats);
     if (silu_act)
-      hipLaunchKernelGGL((gn_nhwc_apply_kernel<DT, true>), dim3(ab, N), dim3(256), 0, st,
-                         (const uint16_t*)x, (const uint16_t*)gamma, (const uint16_t*)beta, stats,
-                         HW, C, G, eps, (uint16_t*)y);
+      hipLaunchKernelGGL((gn_nhwc_apply_kernel<DT, true>), dim3(ab, N), dim3(256), 0, st, src,
+                         (const uint16_t*)gamma, (const uint16_t*)beta, stats, HW, C, G, eps,
+                         (uint16_t*)y, (uint16_t*)cat);
     else
-      hipLaunchKernelGGL((gn_nhwc_apply_kernel<DT, false>), dim3(ab, N), dim3(256), 0, st,
-                         (const uint16_t*)x, (const uint16_t*)gamma, (const uint16_t*)beta, stats,
-                         HW, C, G, eps, (uint16_t*)y);
+      hipLaunchKernelGGL((gn_nhwc_apply_kernel<DT, false>), dim3(ab, N), dim3(256), 0, st, src,
+                         (const uint16_t*)gamma, (const uint16_t*)beta, stats, HW, C, G, eps,
+                         (uint16_t*)y, (uint16_t*)cat);
   });
   return (int)hipGetLastError();
+}
+
+CAKE_API int cake_groupnorm_nhwc(int dt, const void* x, const void* gamma, const void* beta, int N,
+                                 int HW, int C, int G, float eps, int silu_act, double* part,
+                                 unsigned int* tickets, float* stats, void* y, hipStream_t st) {
+  return cake_groupnorm_nhwc2(dt, x, nullptr, C, nullptr, gamma, beta, N, HW, C, G, eps, silu_act,
+                              part, tickets, stats, y, st);
 }

@@ -62,8 +62,10 @@ def run_decode(dec: DeviceDecoder, n_steps: int, eos_ids: set[int] | None = None
         st.wall_s = time.perf_counter() - t0
         return st
 
-    # greedy: every launch runs dec.k steps; their tokens are the next k entries of
-    # the device history, copied to a pinned ring one launch behind
+    if dec.graph is not None:
+        return _run_native(dec, n_steps, eos_ids, on_token)
+    # eager (no graphs): every launch runs dec.k steps; their tokens are the next k
+    # entries of the device history, copied to a pinned ring one launch behind
     k = dec.k
     base = int(dec.bufs.hist_len.item())
     ring = torch.empty(2 * k, dtype=torch.int32, pin_memory=True)
@@ -106,4 +108,23 @@ def run_decode(dec: DeviceDecoder, n_steps: int, eos_ids: set[int] | None = None
         pending[1].synchronize()
     st.wall_s = time.perf_counter() - t0
     del dev
+    return st
+
+
+def _run_native(dec: DeviceDecoder, n_steps: int, eos_ids, on_token) -> DecodeStats:
+    """Greedy graph decode through the native driver (csrc/driver/graph_loop.cpp): the
+    replay / one-behind read-back / EOS loop runs in C++ without the GIL."""
+    from ...ops import graph_loop as GL
+    st = DecodeStats()
+    k = dec.k
+    base = int(dec.bufs.hist_len.item())
+    room = min(dec.bufs.hist.numel() - base, dec.m.stack.max_seq - 1 - dec.host_pos)
+    n = min(n_steps, room // k * k)
+    if n <= 0:
+        return st
+    res = GL.run(dec.graph_set(), k=k, n=n, pos=dec.host_pos, hist=dec.bufs.hist, base=base,
+                 eos_ids=eos_ids,
+                 on_token=(lambda t: bool(on_token(t))) if on_token is not None else None)
+    dec.host_pos = res.pos
+    st.tokens, st.step_ms, st.wall_s = res.tokens, res.step_ms, res.wall_s
     return st

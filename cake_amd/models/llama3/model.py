@@ -249,6 +249,19 @@ class DeviceDecoder:
         self.graph = self.graphs[max(self.graphs)]
         torch.cuda.synchronize()
 
+    def graph_set(self):
+        """The bucket graphs as the native decode loop's GraphSet (built once)."""
+        gs = getattr(self, "_graph_set", None)
+        if gs is None or gs.graphs[-1] is not self.graphs[max(self.graphs)]:
+            from ...ops import graph_loop as GL
+            caps = sorted(self.graphs)
+            index = {c: i for i, c in enumerate(caps)}
+            by_graph = {id(self.graphs[c]): index[c] for c in caps}
+            gs = self._graph_set = GL.GraphSet(
+                [self.graphs[c] for c in caps], lambda t: by_graph[id(self._graph_for(t))],
+                self.m.stack.max_seq)
+        return gs
+
     def _graph_for(self, tk: int) -> torch.cuda.CUDAGraph:
         from ...ops import hip as K
         need = K.attn_splits(tk)

@@ -103,6 +103,27 @@ def group_norm(x, w, b, groups: int, eps: float, silu: bool = False):
     return (F.silu(y) if silu else y).to(x.dtype)
 
 
+def group_norm_cat(x, skip, w, b, groups: int, eps: float, silu: bool = False,
+                   want_cat: bool = True):
+    """GroupNorm of the channel concatenation [x, skip] -> (normalised, raw concat or None).
+
+    Channels-last on the device: one two-source GroupNorm pass reads x and skip in
+    place and (want_cat) writes the raw concatenation alongside the normalised
+    output, so the UNet up path's skip concat is not a separate copy kernel."""
+    if nhwc():
+        from ...ops import hip as K
+        C = x.shape[-1] + skip.shape[-1]
+        if _hip(x) and K.group_norm_nhwc_supported(C, groups) and x.shape[-1] % 8 == 0:
+            x, skip = x.contiguous(), skip.contiguous()
+            shape = (*x.shape[:-1], C)
+            y = torch.empty(shape, device=x.device, dtype=x.dtype)
+            cat = torch.empty(shape, device=x.device, dtype=x.dtype) if want_cat else None
+            K.group_norm_nhwc(x, w, b, groups, eps, silu, y, skip=skip, cat_out=cat)
+            return y, cat
+    xc = torch.cat([x, skip], cdim())
+    return group_norm(xc, w, b, groups, eps, silu), xc
+
+
 def layer_norm(x, w, b, eps: float):
     if _hip(x):
         from ...ops import hip as K
@@ -207,7 +228,7 @@ def conv(W, name: str, x, stride: int = 1, padding: int = 1, up: bool = False, b
     if nhwc():
         from ...ops import hip as K
         OC, IC = w.shape[:2]
-        if _hip(x) and K.conv_supported(IC, OC, stride, up):
+        if _hip(x) and w.shape[2] == w.shape[3] and K.conv_supported(IC, OC, stride, up, w.shape[2]):
             from ...ops import conv as C
             key = f"{name}.weight@nhwc"
             wp = W.get(key)

@@ -84,12 +84,18 @@ class ResnetBlock2D(Module):
                 p.update(m.params())
         return p
 
-    def __call__(self, W, x, temb=None, tb=None):
+    def __call__(self, W, x, temb=None, tb=None, skip=None):
         """temb: the time embedding (the block projects silu(temb) itself), or tb: this
         block's precomputed time bias [B, C_out] f32 (the UNet batches every block's
-        projection into one GEMM)."""
-        h = ops.group_norm(x, W[f"{self.name}.norm1.weight"], W[f"{self.name}.norm1.bias"],
-                           self.groups, self.eps, silu=True)
+        projection into one GEMM).  skip: the up path's skip tensor; the block input
+        is then the channel concatenation [x, skip], formed inside norm1."""
+        if skip is not None:
+            h, x = ops.group_norm_cat(x, skip, W[f"{self.name}.norm1.weight"],
+                                      W[f"{self.name}.norm1.bias"], self.groups, self.eps,
+                                      silu=True, want_cat=True)
+        else:
+            h = ops.group_norm(x, W[f"{self.name}.norm1.weight"], W[f"{self.name}.norm1.bias"],
+                               self.groups, self.eps, silu=True)
         if tb is None and self.temb is not None and temb is not None:
             tb = self.temb(W, F.silu(temb))
         h = self.conv1(W, h, bias2=tb)  # time embedding fused as a per-sample bias
@@ -400,7 +406,7 @@ class UNet2DConditionModel(Module):
         i = int(idx)
         res, att, us = self.up[i]
         for j, r in enumerate(res):
-            x = r(W, torch.cat([x, skips.pop()], ops.cdim()), tb=tbs[r.name])
+            x = r(W, x, tb=tbs[r.name], skip=skips.pop())
             if att:
                 x = att[j](W, x, ctx, kv_cache)
         if us is not None:

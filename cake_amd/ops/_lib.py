@@ -111,6 +111,7 @@ _SIGS.update({
     "cake_flash_set_nw": [I],
     "cake_groupnorm": [I, P, P, P, I, I, C.c_longlong, I, F, I, P, P, P],
     "cake_groupnorm_nhwc": [I, P, P, P, I, I, I, I, F, I, P, P, P, P, P],
+    "cake_groupnorm_nhwc2": [I, P, P, I, P, P, P, I, I, I, I, F, I, P, P, P, P, P],
     "cake_groupnorm_nhwc_splits": [I],
     "cake_layernorm": [I, P, P, P, C.c_longlong, I, F, P, P],
     "cake_geglu": [I, P, C.c_longlong, I, P, P],

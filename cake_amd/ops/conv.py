@@ -19,7 +19,9 @@ _cache: dict[tuple, tuple[int, int]] = {}
 _AUTOTUNE = os.environ.get("CAKE_CONV_AUTOTUNE", "1") != "0"
 
 
-def _candidates(stride: int, k: int, splits_ok: bool):
+def _candidates(stride: int, k: int, splits_ok: bool, ic: int = 64):
+    if ic % 64:
+        return [(14, 1)]  # the direct small-IC kernel
     c = []
     if stride == 1 and k > 1:
         c += [(8, 1), (9, 1), (10, 1), (11, 1), (12, 1), (13, 1)]
@@ -52,7 +54,7 @@ def conv2d(x, w, bias=None, *, stride: int = 1, pad: int = 1, up: bool = False, 
         capturing = torch.cuda.is_current_stream_capturing()
         if _AUTOTUNE and not capturing:
             best = None
-            for cfg, sp in _candidates(stride, KH * KW, True):
+            for cfg, sp in _candidates(stride, KH * KW, True, IC):
                 f = (lambda c=cfg, s=sp: K.conv2d_nhwc(x, w, bias, stride=stride, pad=pad, up=up,
                                                        bias2=bias2, resid=resid, cfg=c, splits=s))
                 try:
@@ -65,7 +67,8 @@ def conv2d(x, w, bias=None, *, stride: int = 1, pad: int = 1, up: bool = False, 
         else:
             VH, VW = H << int(up), W << int(up)
             OH, OW = (VH + 2 * pad - KH) // stride + 1, (VW + 2 * pad - KW) // stride + 1
-            choice = K.conv_plan(N * OH * OW, OC, KH * KW * IC // 64)
+            choice = (K.conv_plan(N * OH * OW, OC, KH * KW * IC // 64) if IC % 64 == 0
+                      else (14, 1))
         _cache[key] = choice
     return K.conv2d_nhwc(x, w, bias, stride=stride, pad=pad, up=up, bias2=bias2, resid=resid,
                          cfg=choice[0], splits=choice[1])

@@ -510,25 +510,42 @@ def group_norm_nhwc_supported(C: int, groups: int) -> bool:
     return C % groups == 0 and C % 8 == 0 and C <= 4096 and cg >= 4 and (cg >= 8 or 8 % cg == 0)
 
 
-def group_norm_nhwc(x, gamma, beta, groups: int, eps: float, silu: bool, out):
-    """GroupNorm over channels-last x [N, ..., C] (contiguous) [+ fused SiLU]."""
-    N, C = x.shape[0], x.shape[-1]
-    HW = x.numel() // (N * C)
+def group_norm_nhwc(x, gamma, beta, groups: int, eps: float, silu: bool, out, skip=None,
+                    cat_out=None):
+    """GroupNorm over channels-last x [N, ..., C] (contiguous) [+ fused SiLU].
+
+    skip [N, ..., Cs]: normalise the channel concatenation x ++ skip without
+    materialising it first (the UNet up path); cat_out [N, ..., C + Cs] then
+    optionally receives the raw concatenation (written by the same pass)."""
+    N, Cx = x.shape[0], x.shape[-1]
+    HW = x.numel() // (N * Cx)
     _req(x, "x")
+    C = Cx
+    if skip is not None:
+        _req(skip, "skip", dtype=x.dtype)
+        if skip.shape[:-1] != x.shape[:-1]:
+            raise ValueError(f"group_norm_nhwc: skip {tuple(skip.shape)} vs x {tuple(x.shape)}")
+        C = Cx + skip.shape[-1]
+    oshape = (*x.shape[:-1], C)
     _req(gamma, "gamma", dtype=x.dtype, shape=(C,))
     _req(beta, "beta", dtype=x.dtype, shape=(C,))
-    _req(out, "out", dtype=x.dtype, shape=x.shape)
-    if not group_norm_nhwc_supported(C, groups):
-        raise ValueError(f"group_norm_nhwc: unsupported C={C} groups={groups}")
+    _req(out, "out", dtype=x.dtype, shape=oshape)
+    if cat_out is not None:
+        if skip is None:
+            raise ValueError("group_norm_nhwc: cat_out needs a skip source")
+        _req(cat_out, "cat_out", dtype=x.dtype, shape=oshape)
+    if not group_norm_nhwc_supported(C, groups) or Cx % 8:
+        raise ValueError(f"group_norm_nhwc: unsupported C={C} (x {Cx}) groups={groups}")
     S = kernels().cake_groupnorm_nhwc_splits(HW)
     t = _gn_tickets.get(x.device)
     if t is None or t.numel() < N:
         t = _gn_tickets[x.device] = torch.zeros(max(N, 64), device=x.device, dtype=torch.int32)
     part = torch.empty(N * S * groups * 2, device=x.device, dtype=torch.float64)
     stats = torch.empty(N * groups * 2, device=x.device, dtype=torch.float32)
-    check(kernels().cake_groupnorm_nhwc(_dt(x), _p(x), _p(gamma), _p(beta), N, HW, C, groups,
-                                        float(eps), int(silu), _p(part), _p(t), _p(stats),
-                                        _p(out), _stream()),
+    check(kernels().cake_groupnorm_nhwc2(_dt(x), _p(x), None if skip is None else _p(skip), Cx,
+                                         None if cat_out is None else _p(cat_out), _p(gamma),
+                                         _p(beta), N, HW, C, groups, float(eps), int(silu),
+                                         _p(part), _p(t), _p(stats), _p(out), _stream()),
           "groupnorm_nhwc")
 
 
@@ -570,7 +587,9 @@ def _zeros16(dev) -> torch.Tensor:
     return z
 
 
-def conv_supported(IC: int, OC: int, stride: int = 1, up: bool = False) -> bool:
+def conv_supported(IC: int, OC: int, stride: int = 1, up: bool = False, k: int = 3) -> bool:
+    if IC in (3, 4):  # direct small-IC kernel (conv_in)
+        return k == 3 and OC % 8 == 0 and 9 * IC * OC <= 18432 and not up
     return IC % 64 == 0 and OC % 4 == 0 and not (up and stride != 1)
 
 
@@ -611,7 +630,7 @@ def conv2d_nhwc(x, w, bias=None, *, stride: int = 1, pad: int = 1, up: bool = Fa
     """
     N, H, W, IC = x.shape
     OC, KH, KW, IC2 = w.shape
-    if IC2 != IC or not conv_supported(IC, OC, stride, up):
+    if IC2 != IC or KH != KW or not conv_supported(IC, OC, stride, up, KH):
         raise ValueError(f"conv2d_nhwc: unsupported IC={IC} OC={OC} w={tuple(w.shape)}")
     VH, VW = H << int(up), W << int(up)
     OH, OW = (VH + 2 * pad - KH) // stride + 1, (VW + 2 * pad - KW) // stride + 1
@@ -632,12 +651,14 @@ def conv2d_nhwc(x, w, bias=None, *, stride: int = 1, pad: int = 1, up: bool = Fa
         out = torch.empty(N, OH, OW, OC, device=x.device, dtype=x.dtype)
     _req(out, "out", dtype=x.dtype, shape=(N, OH, OW, OC))
     P, ksteps = N * OH * OW, KH * KW * IC // 64
+    if IC % 64:  # small-IC direct kernel: one variant
+        cfg, splits, ksteps = 14, 1, 1
     if cfg is None or splits is None:
         c0, s0 = conv_plan(P, OC, ksteps)
         cfg = c0 if cfg is None else cfg
         splits = s0 if splits is None else splits
     th = tw = 0
-    if cfg >= 8:  # halo kernels: stride 1, no split-K
+    if 8 <= cfg < 14:  # halo kernels: stride 1, no split-K
         if stride != 1:
             raise ValueError("conv2d_nhwc: halo tiles need stride 1")
         splits = 1

@@ -684,6 +684,8 @@ class PipelineEngine:
         ipc = self.hop == "ipc" and self.use_graph
         chunk = max(1, int(chunk or (16 if ipc else 1)))
         single = self.world == 1 or all(r.owner == 0 for r in self.runs)
+        if ipc and self.hip and self.k == 1 and (st.sid, "tok") in st.graphs:
+            return self._generate_native(st, n, on_token, eos_ids, chunk, single)
         base = int(st.bufs.hist_len.item()) if self.hip else 0
         ring = torch.empty(max(1, n), dtype=torch.int32, pin_memory=self.hip and
                            torch.cuda.is_available()) if self.hip else None
@@ -737,6 +739,41 @@ class PipelineEngine:
             torch.cuda.synchronize(self.device)
         self.check_hops()
         return out
+
+    def _graph_set(self, st: "_Stream"):
+        """This rank's token graphs of stream st as a native-loop GraphSet."""
+        gs = getattr(st, "graph_set", None)
+        graphs = st.graphs[(st.sid, "tok")]
+        if gs is None or gs.graphs[-1] is not graphs[max(graphs)]:
+            from ..ops import graph_loop as GL
+            caps = sorted(graphs)
+            idx = {id(graphs[c]): i for i, c in enumerate(caps)}
+            gs = st.graph_set = GL.GraphSet([graphs[c] for c in caps],
+                                            lambda t: idx[id(self._pick(graphs, t))],
+                                            self.stack.max_seq)
+        return gs
+
+    def _generate_native(self, st: "_Stream", n: int, on_token, eos_ids, chunk: int,
+                         single: bool) -> list[int]:
+        """generate() with ipc hops: the native loop (csrc/driver/graph_loop.cpp)
+        replays this rank's token graph, announces each chunk to the workers one chunk
+        ahead (the control callback) and reads tokens back one replay behind."""
+        from ..ops import graph_loop as GL
+        pos0 = st.dev_pos
+
+        def announce(first: int, count: int) -> None:
+            if not single:
+                self.ctrl_send({"op": "decode", "n": count, "pos": pos0 + first})
+
+        res = GL.run(self._graph_set(st), k=1, n=n, pos=pos0, hist=st.bufs.hist,
+                     base=int(st.bufs.hist_len.item()), eos_ids=eos_ids,
+                     on_token=(lambda t: bool(on_token(t))) if on_token is not None else None,
+                     announce=announce, chunk=chunk)
+        st.dev_pos = res.pos
+        self._native_step_ms = res.step_ms
+        torch.cuda.synchronize(self.device)
+        self.check_hops()
+        return res.tokens
 
     def _step_host(self, st: "_Stream", single: bool) -> None:
         """One master token with host-issued hops (dist transport / no graphs)."""
@@ -919,6 +956,10 @@ class PipelineEngine:
         the ranks on the device.  The master records one event per replay."""
         if len(self.streams) == 1:
             st = self.streams[0]
+            if not self.is_master:  # worker: native enqueue of every replay
+                from ..ops import graph_loop as GL
+                st.dev_pos = GL.run(self._graph_set(st), k=self.k, n=rounds, pos=st.dev_pos).pos
+                return
             for _ in range(rounds // self.k):
                 self._replay_ipc_token(st)
                 if self.is_master:

@@ -231,6 +231,18 @@ def _tp_generate(eng, cmd, emit=None):
         return st
     b = eng.b
     base = int(b.hist_len.item())
+    if eng.use_graph and eng.mode in eng.graphs:
+        # native decode driver (csrc/driver/graph_loop.cpp): every rank replays and
+        # reads back the same tokens, so all stop after the same one
+        from ..ops import graph_loop as GL
+        res = GL.run(eng.graph_set(), k=1, n=n - 1, pos=eng.host_pos, hist=b.hist, base=base,
+                     eos_ids=eos, on_token=(lambda t: bool(emit(t))) if emit is not None
+                     else None)
+        eng.host_pos = res.pos
+        st.tokens, st.step_ms, st.wall_s = res.tokens, res.step_ms, res.wall_s
+        eng.tokens = b.hist[:int(b.hist_len.item())].tolist()
+        eng.check()
+        return st
     ring = torch.empty(n, dtype=torch.int32, pin_memory=True)
     prev = torch.cuda.Event(enable_timing=True)
     prev.record()

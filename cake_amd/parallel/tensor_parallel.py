@@ -438,6 +438,7 @@ class TPEngine:
         self.b = TPBuffers(H, self.nq, self.nkv, hd, self.I_l, self.V_l, max_seq, self.device,
                            dtype)
         self.graphs: dict = {}       # mode ("greedy" / "sample") -> {split cap: graph}
+        self._graph_sets: dict = {}  # mode -> native-loop GraphSet of those graphs
         self.host_pos = 0
         self.tokens: list[int] = []
         if temperature and temperature > 0:
@@ -638,6 +639,18 @@ class TPEngine:
             gs[cap] = g
         self.graphs[self.mode] = gs
         torch.cuda.synchronize(self.device)
+
+    def graph_set(self):
+        """The current mode's bucket graphs as a native-loop GraphSet."""
+        gs = self.graphs[self.mode]
+        cur = self._graph_sets.get(self.mode)
+        if cur is None or cur.graphs[-1] is not gs[max(gs)]:
+            from ..ops import graph_loop as GL
+            caps = sorted(gs)
+            idx = {id(gs[c]): i for i, c in enumerate(caps)}
+            cur = self._graph_sets[self.mode] = GL.GraphSet(
+                [gs[c] for c in caps], lambda t: idx[id(self._graph_for(t))], self.max_seq)
+        return cur
 
     def _graph_for(self, tk: int):
         from ..ops import hip as K

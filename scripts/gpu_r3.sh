@@ -1,0 +1,30 @@
+#!/bin/bash
+# Round-3 GPU iteration: full GPU tests, the driver bench, decode attention phase clocks,
+# SDXL denoise seconds/step and its rocprofv3 kernel table.  Each GPU step has its own
+# time limit; the script stops at the first failure.
+set -u
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+step() {  # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  echo "== $name"
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  tail -4 "gpurun_out/$name.log"
+  if [[ $rc -ne 0 ]]; then echo "$name rc=$rc -> stop"; exit $rc; fi
+}
+[[ ${DO_TESTS:-1} == 1 ]] && step pytest 600 python -u -m pytest ${TESTS:-tests} -x -q -m gpu --timeout 120 --timeout-method thread
+[[ ${DO_BENCH:-1} == 1 ]] && step bench 400 python bench.py ${BENCH_ARGS:-}
+[[ ${DO_STAMPS:-0} == 1 ]] && step attn_stamps 120 python scripts/attn_stamps.py
+if [[ ${DO_SD:-0} == 1 ]]; then
+  step sd_xl 300 python scripts/bench_sd.py --version xl --denoise --graph --steps 8
+  step sd_15 200 python scripts/bench_sd.py --version v1-5 --denoise --graph --steps 8
+fi
+if [[ ${DO_SDPROF:-0} == 1 ]]; then
+  cd /tmp && export TMPDIR=/tmp
+  rm -rf "$GRAFT_REPO_ROOT/gpurun_out/sdprof"
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/sdprof" -o run -- python3 "$GRAFT_REPO_ROOT/scripts/bench_sd.py" --version xl --denoise --graph --steps 8 > "$GRAFT_REPO_ROOT/gpurun_out/sdprof.log" 2>&1 || { tail "$GRAFT_REPO_ROOT/gpurun_out/sdprof.log"; exit 1; }
+  cd "$GRAFT_REPO_ROOT"
+fi
+exit 0

@@ -106,7 +106,10 @@ def test_halo_tile_fits(OH, OW, bn):
 def test_conv_supported_rules():
     from cake_amd.ops import hip as K
     assert K.conv_supported(320, 320) and K.conv_supported(64, 4)
-    assert not K.conv_supported(4, 320)       # conv_in: IC not a multiple of 64
+    assert K.conv_supported(4, 320) and K.conv_supported(3, 128)  # conv_in: direct kernel
+    assert not K.conv_supported(4, 320, k=1) and not K.conv_supported(4, 4)  # 3x3, OC % 8
+    assert not K.conv_supported(4, 1024)      # filter exceeds the kernel's LDS copy
+    assert not K.conv_supported(8, 320)       # IC neither 3/4 nor a multiple of 64
     assert not K.conv_supported(320, 3)       # OC not a multiple of 4
     assert not K.conv_supported(64, 64, stride=2, up=True)
     assert K.group_norm_nhwc_supported(320, 32) and K.group_norm_nhwc_supported(128, 32)

@@ -65,6 +65,44 @@ def test_device_decoder_matches_host_loop(cuda, use_graph, k):
     assert len(st.step_ms) == 11 and all(x > 0 for x in st.step_ms)
 
 
+@pytest.mark.parametrize("k", [1, 3])
+def test_native_decode_loop_eos_and_callback(cuda, k):
+    """The C++ decode driver (graph_loop.cpp): tokens equal the eager loop's, it stops at
+    the first EOS (inclusive) and when the per-token callback asks, and the host position
+    mirror advances by whole replays."""
+    from cake_amd.models.llama3.decode_loop import run_decode
+    from cake_amd.models.llama3.model import DeviceDecoder
+
+    cfg = preset("llama3-8b", num_hidden_layers=2, vocab_size=2048, intermediate_size=1024,
+                 hidden_size=512, num_attention_heads=4, num_key_value_heads=1)
+    model = random_model(cfg, "cuda:0", torch.bfloat16, max_seq=256, seed=7)
+    prompt = [3, 1, 4, 1, 5, 9, 2, 6]
+
+    def fresh(use_graph):
+        dec = DeviceDecoder(model, repeat_penalty=1.1, repeat_last_n=16, greedy=True,
+                            use_graph=use_graph, steps_per_graph=k)
+        first = dec.start(prompt)
+        dec.capture()
+        return dec, first
+
+    dec, first = fresh(False)
+    ref = [first] + run_decode(dec, 14).tokens            # eager Python loop
+    dec, first = fresh(True)
+    pos0 = dec.host_pos
+    st = run_decode(dec, 14)                              # native loop
+    assert [first] + st.tokens == ref
+    assert dec.host_pos == pos0 + -(-14 // k) * k
+    assert len(st.step_ms) == 14 and all(x > 0 for x in st.step_ms)
+    eos = ref[6]
+    dec, first = fresh(True)
+    got = run_decode(dec, 14, eos_ids={eos}).tokens
+    assert got == ref[1:ref.index(eos, 1) + 1]
+    seen = []
+    dec, first = fresh(True)
+    got = run_decode(dec, 14, on_token=lambda t: (seen.append(t), len(seen) >= 4)[1]).tokens
+    assert got == seen == ref[1:5]
+
+
 def test_device_decoder_crosses_split_buckets(cuda):
     """Graphs captured per attention split cap: a generation whose live length crosses
     the 512-key bucket edge (cap 8 -> 16) matches the host loop token for token."""

@@ -123,24 +123,35 @@ def test_llama_hip_matches_transformers_gpu(cuda, tmp_path, shaped_8b):
     prompt = [1, 17, 99, 4, 250, 3, 77, 12, 5, 6, 7]
     ref = _hf_logits(hf, prompt)
     got = ours.forward(prompt, 0).cpu()
-    tol = 0.05 * float(ref[-1].abs().max())
-    torch.testing.assert_close(got, ref[-1], atol=tol, rtol=0.05)
-    # greedy decode through the whole-step graph == transformers' greedy continuation
+    # bf16 activations vs an f32 forward on the same bf16 weights: per-logit closeness
+    tol = 0.025 * float(ref[-1].abs().max())
+    torch.testing.assert_close(got, ref[-1], atol=tol, rtol=0.02)
+    # decode through the whole-step graph, one step per replay: every step's logits
+    # (the device buffer the token was selected from) against transformers' logits for
+    # the same prefix, and the greedy token equal to transformers' argmax unless the
+    # top two are a bf16-level near-tie
     dec = DeviceDecoder(ours, repeat_penalty=1.0, greedy=True)
-    toks = [dec.start(prompt)]
-    dec.capture()
-    toks += run_decode(dec, 5).tokens
     seq = list(prompt)
-    agree = 0
-    for t in toks:
+    first = dec.start(prompt)
+    lg0 = dec.logits().float().cpu()
+    torch.testing.assert_close(lg0, ref[-1], atol=tol, rtol=0.02)
+    dec.capture()
+    tok = first
+    for step in range(6):
         lg = _hf_logits(hf, seq)[-1]
+        if step > 0:
+            got_l = dec.logits().float().cpu()
+            t_tol = 0.025 * float(lg.abs().max())
+            torch.testing.assert_close(got_l, lg, atol=t_tol, rtol=0.02)
         top2 = torch.topk(lg, 2).values
-        if int(torch.argmax(lg)) == t:
-            agree += 1
-        else:  # only a near-tie may flip under bf16
-            assert float(top2[0] - top2[1]) < 0.05 * float(lg.abs().max()), (seq, t)
-        seq.append(t)
-    assert agree >= len(toks) - 1
+        if int(torch.argmax(lg)) != tok:
+            assert float(top2[0] - top2[1]) < 0.01 * float(lg.abs().max()), (seq, tok)
+        seq.append(tok)
+        if step == 5:
+            break
+        dec.launch()
+        torch.cuda.synchronize()
+        tok = int(dec.bufs.tok.item())
 
 
 @pytest.mark.gpu

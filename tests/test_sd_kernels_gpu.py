@@ -233,6 +233,57 @@ def test_group_norm_nhwc(cuda, dt, N, H, W, C, G, silu):
     torch.testing.assert_close(y.float(), ref.permute(0, 2, 3, 1), **_tol(dt))
 
 
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("N,H,W,Cx,Cs,G", [
+    (2, 16, 16, 1280, 640, 32),   # SDXL up path: x ++ skip with different widths
+    (2, 8, 8, 320, 320, 32),      # Cg = 20 straddles the x / skip boundary
+    (1, 5, 7, 640, 1280, 32),     # ragged spatial size
+])
+@pytest.mark.parametrize("want_cat", [False, True])
+def test_group_norm_nhwc_two_source(cuda, dt, N, H, W, Cx, Cs, G, want_cat):
+    """GroupNorm of the skip concatenation read in place (and the raw concat written)."""
+    from cake_amd.ops import hip as K
+    torch.manual_seed(12)
+    x = (torch.randn(N, H, W, Cx, device=cuda) * 2 + 1).to(dt)
+    s = (torch.randn(N, H, W, Cs, device=cuda) * 0.5 - 1).to(dt)
+    C = Cx + Cs
+    g = (1 + 0.1 * torch.randn(C, device=cuda)).to(dt)
+    b = (0.1 * torch.randn(C, device=cuda)).to(dt)
+    y = torch.empty(N, H, W, C, device=cuda, dtype=dt)
+    cat = torch.empty_like(y) if want_cat else None
+    for _ in range(2):
+        K.group_norm_nhwc(x, g, b, G, 1e-5, True, y, skip=s, cat_out=cat)
+    xc = torch.cat([x, s], -1)
+    ref = torch.nn.functional.group_norm(xc.float().permute(0, 3, 1, 2), G, g.float(), b.float(),
+                                         1e-5)
+    ref = torch.nn.functional.silu(ref)
+    torch.testing.assert_close(y.float(), ref.permute(0, 2, 3, 1), **_tol(dt))
+    if want_cat:
+        assert torch.equal(cat, xc)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("N,H,W,IC,OC,stride", [
+    (2, 32, 32, 4, 320, 1),     # UNet conv_in (SD1.5 / SDXL latents)
+    (1, 17, 13, 4, 512, 1),     # VAE decoder conv_in, ragged
+    (1, 16, 16, 3, 128, 1),     # VAE encoder RGB input
+    (1, 15, 16, 3, 64, 2),      # strided, odd size
+])
+@pytest.mark.parametrize("fused", [False, True])
+def test_conv2d_small_ic(cuda, dt, N, H, W, IC, OC, stride, fused):
+    """Direct 3x3 kernel for IC 3 / 4 (conv_in) vs the f32 reference, with fused epilogue."""
+    from cake_amd.ops import hip as K
+    torch.manual_seed(8)
+    x = torch.randn(N, H, W, IC, device=cuda).to(dt)
+    w = (torch.randn(OC, IC, 3, 3, device=cuda) / math.sqrt(IC * 9)).to(dt)
+    b = torch.randn(OC, device=cuda).to(dt)
+    OH, OW = (H + 2 - 3) // stride + 1, (W + 2 - 3) // stride + 1
+    b2 = torch.randn(N, OC, device=cuda) if fused else None
+    r = torch.randn(N, OH, OW, OC, device=cuda).to(dt) if fused else None
+    y = K.conv2d_nhwc(x, w.permute(0, 2, 3, 1).contiguous(), b, stride=stride, bias2=b2, resid=r)
+    torch.testing.assert_close(y.float(), _ref_conv(x, w, b, stride, 1, False, b2, r), **_tol(dt))
+
+
 @pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
 @pytest.mark.parametrize("B,N,M", [(1, 4096, 4096), (2, 1000, 777), (1, 16384, 16384), (1, 70, 33)])
 def test_attn512_vs_fp32(cuda, dt, B, N, M):
