@@ -65,6 +65,8 @@ def _args(argv=None):
     ap.add_argument("--parallel", default="pp", choices=["tp", "pp"],
                     help="N > 1 headline: pp = the reference's layer sharding (default), "
                          "tp = tensor-parallel (every rank 1/N of every layer)")
+    ap.add_argument("--no-sd", action="store_true",
+                    help="skip the N=1 Stable Diffusion seconds/step sub-record")
     ap.add_argument("--no-extras", action="store_true",
                     help="headline only: skip the tp / llama3_70b sub-records")
     ap.add_argument("--allreduce", default="ipc", choices=["ipc", "dist"],
@@ -232,6 +234,14 @@ def bench_single(a) -> None:
                                                                      a.warmup))}
         except Exception as e:  # noqa: BLE001  (the headline stands; the miss is reported)
             extra["llama3_70b"] = {"single": None, "error": f"{type(e).__name__}: {e}"[:300]}
+        # the reference's second metric: SD seconds per diffusion step (SDXL 1024^2,
+        # CFG batch 2, the UNet + scheduler step as one graph replay)
+        if not a.no_sd:
+            try:
+                from cake_amd.models.sd.bench import measure_denoise
+                extra["sd"] = {"sdxl_1024": measure_denoise("xl", 8)}
+            except Exception as e:  # noqa: BLE001
+                extra["sd"] = {"sdxl_1024": None, "error": f"{type(e).__name__}: {e}"[:300]}
     _emit(a, r["tokens_per_sec"], r["ms_per_step"], r["p50_token_latency_ms"],
           r["p99_token_latency_ms"], 1, extra)
 

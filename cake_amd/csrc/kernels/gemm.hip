@@ -51,8 +51,16 @@ enum GemmEpi : int {
   kEpiGeglu = 4,   // C16[:, f] = acc_h * gelu_tanh(acc_gate)
   kEpiPartial = 5, // W32[split] = acc (split-K slab, virtual column order)
   kEpiStore32 = 6, // R32 = acc (+ bias)              (f32 output, e.g. conv time biases)
-  kEpiSilu = 7,    // C16 = silu(acc (+ bias))        (time-embedding MLP)
+  kEpiSilu = 7,    // C16 = act(acc (+ bias)), act = GemmArgs::act: SiLU (time-embedding
+                   // MLP), quick_gelu / erf-GELU (CLIP MLP); host ids 7 / 8 / 9
 };
+
+// the activation of kEpiSilu (runtime-uniform: one kernel instance for all three)
+__device__ __forceinline__ float gemm_act(int act, float x) {
+  if (act == 1) return x * __frcp_rn(1.f + __expf(-1.702f * x));  // quick_gelu
+  if (act == 2) return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));  // GELU (erf)
+  return silu(x);
+}
 
 struct GemmArgs {
   const uint16_t* a;     // [M][lda]
@@ -68,6 +76,7 @@ struct GemmArgs {
   int Nv, half;          // gated: Nv = 2 * half, half = N
   int gated;             // B row order interleaves 16-row blocks of two halves
   int tiles_m, tiles_n, kps;  // k elements per split
+  int act;               // kEpiSilu activation: 0 SiLU, 1 quick_gelu, 2 GELU (erf)
 };
 
 // virtual B row -> weight row (gated: [16 gate rows | 16 up rows] per 32-row block)
@@ -234,7 +243,7 @@ __device__ __forceinline__ void epi_strip(const GemmArgs& g, const cf32x4 (&tile
           }
           if constexpr (EPI == kEpiSilu) {
 #pragma unroll
-            for (int c = 0; c < CPL; ++c) v[c] = silu(v[c]);
+            for (int c = 0; c < CPL; ++c) v[c] = gemm_act(g.act, v[c]);
           }
           uint16_t outv[CPL];
 #pragma unroll
@@ -545,7 +554,7 @@ __global__ __launch_bounds__(256) void gemm_splitk_finalize(GemmArgs g, int spli
     else {
       y = v[q] + (g.bias != nullptr ? to_f32<DT>(g.bias[fq]) : 0.f);
       if constexpr (EPI == kEpiAdd16) y += to_f32<DT>(g.r16[(size_t)m * g.ldr + fq]);
-      if constexpr (EPI == kEpiSilu) y = silu(y);
+      if constexpr (EPI == kEpiSilu) y = gemm_act(g.act, y);
     }
     if constexpr (EPI == kEpiResid32) g.r32[(size_t)m * g.ldr + fq] += y;
     else if constexpr (EPI == kEpiStore32) g.r32[(size_t)m * g.ldr + fq] = y;
@@ -640,6 +649,11 @@ CAKE_API int cake_gemm(int dt, int epi, int cfg, int splits, const void* a, long
                        const void* b, long long ldb, void* c, long long ldc, const void* bias,
                        void* resid, long long ldr, float* ws, const void* zeros, int M, int N,
                        int K, hipStream_t st) {
+  int act = 0;
+  if (epi == 8 || epi == 9) {  // quick_gelu / GELU: the activation epilogue, other act
+    act = epi - 7;
+    epi = kEpiSilu;
+  }
   int bm, bn;
   cfg_dims(cfg, bm, bn);
   if (bm == 0 || M <= 0 || N <= 0 || K <= 0 || K % 8 || lda % 8 || ldb % 8 || splits < 1)
@@ -655,6 +669,7 @@ CAKE_API int cake_gemm(int dt, int epi, int cfg, int splits, const void* a, long
   g.lda = lda; g.ldb = ldb; g.ldc = ldc; g.ldr = ldr;
   g.M = M; g.N = N; g.K = K;
   g.gated = gated ? 1 : 0;
+  g.act = act;
   g.half = N;
   g.Nv = gated ? 2 * N : N;
   g.tiles_m = (M + bm - 1) / bm;

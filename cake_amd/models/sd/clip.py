@@ -7,7 +7,6 @@ Weight names: HF ``CLIPTextModel`` (``text_model.*``).
 from __future__ import annotations
 
 import torch
-import torch.nn.functional as F
 
 from . import ops
 from .config import ClipConfig
@@ -37,6 +36,17 @@ class ClipTextTransformer:
     def __init__(self, cfg: ClipConfig, w: dict[str, torch.Tensor]):
         self.cfg = cfg
         self.w = w
+        self._fused: dict = {}
+
+    def _qkv(self, pre: str) -> tuple[torch.Tensor, torch.Tensor]:
+        """The layer's q|k|v weights and biases concatenated once (cached)."""
+        key = f"{pre}.self_attn.qkv@fused"
+        hit = self._fused.get(key)
+        if hit is None:
+            names = [f"{pre}.self_attn.{n}_proj" for n in ("q", "k", "v")]
+            hit = self._fused[key] = (torch.cat([self.w[f"{n}.weight"] for n in names], 0),
+                                      torch.cat([self.w[f"{n}.bias"] for n in names], 0))
+        return hit
 
     def forward(self, ids: torch.Tensor) -> torch.Tensor:
         cfg, w = self.cfg, self.w
@@ -44,23 +54,22 @@ class ClipTextTransformer:
         B, T = ids.shape
         x = w["text_model.embeddings.token_embedding.weight"][ids] + \
             w["text_model.embeddings.position_embedding.weight"][:T][None]
+        D = cfg.embed_dim
         for i in range(cfg.num_hidden_layers):
             pre = f"text_model.encoder.layers.{i}"
             h = ops.layer_norm(x, w[f"{pre}.layer_norm1.weight"], w[f"{pre}.layer_norm1.bias"],
                                cfg.layer_norm_eps)
-            q = ops.linear(h, w[f"{pre}.self_attn.q_proj.weight"], w[f"{pre}.self_attn.q_proj.bias"])
-            k = ops.linear(h, w[f"{pre}.self_attn.k_proj.weight"], w[f"{pre}.self_attn.k_proj.bias"])
-            v = ops.linear(h, w[f"{pre}.self_attn.v_proj.weight"], w[f"{pre}.self_attn.v_proj.bias"])
-            a = ops.attention(q, k, v, cfg.num_attention_heads, causal=True)
-            x = x + ops.linear(a, w[f"{pre}.self_attn.out_proj.weight"],
-                               w[f"{pre}.self_attn.out_proj.bias"])
+            # q|k|v as one GEMM; attention reads the three column slices in place
+            wqkv, bqkv = self._qkv(pre)
+            qkv = ops.linear(h, wqkv, bqkv)
+            a = ops.attention(qkv[..., :D], qkv[..., D:2 * D], qkv[..., 2 * D:],
+                              cfg.num_attention_heads, causal=True)
+            x = ops.linear(a, w[f"{pre}.self_attn.out_proj.weight"],
+                           w[f"{pre}.self_attn.out_proj.bias"], resid=x)  # residual fused
             h = ops.layer_norm(x, w[f"{pre}.layer_norm2.weight"], w[f"{pre}.layer_norm2.bias"],
                                cfg.layer_norm_eps)
-            h = ops.linear(h, w[f"{pre}.mlp.fc1.weight"], w[f"{pre}.mlp.fc1.bias"])
-            if cfg.activation == "quick_gelu":
-                h = h * torch.sigmoid(1.702 * h)
-            else:
-                h = F.gelu(h)
-            x = x + ops.linear(h, w[f"{pre}.mlp.fc2.weight"], w[f"{pre}.mlp.fc2.bias"])
+            act = "quick_gelu" if cfg.activation == "quick_gelu" else "gelu"
+            h = ops.linear(h, w[f"{pre}.mlp.fc1.weight"], w[f"{pre}.mlp.fc1.bias"], act=act)
+            x = ops.linear(h, w[f"{pre}.mlp.fc2.weight"], w[f"{pre}.mlp.fc2.bias"], resid=x)
         return ops.layer_norm(x, w["text_model.final_layer_norm.weight"],
                               w["text_model.final_layer_norm.bias"], cfg.layer_norm_eps)

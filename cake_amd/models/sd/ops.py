@@ -191,18 +191,29 @@ def _gemm_ok(x, w) -> bool:
         and w.stride(0) % 8 == 0
 
 
-def linear(x, w, b=None, resid=None, gated: str | None = None):
+def linear(x, w, b=None, resid=None, gated: str | None = None, act: str | None = None):
     """y = x w^T (+ b) on the MFMA GEMM (gemm.hip), with fused epilogues:
     resid -> y + resid (block residual); gated="geglu" -> GEGLU over the two halves
-    of w's rows (diffusers FeedForward proj, bias included)."""
+    of w's rows (diffusers FeedForward proj, bias included); act="quick_gelu" /
+    "gelu" -> the activation applied to y (+ b) (CLIP MLP)."""
+    if act is not None and (gated is not None or resid is not None):
+        raise ValueError("act combines with neither gated nor resid")
     if _gemm_ok(x, w):
         from ...ops import gemm as G
         if gated is not None:
             return G.linear(x, w, b, epi=gated)
         if resid is not None:
             return G.linear(x, w, b, epi="add16", resid=resid.contiguous())
+        if act is not None:
+            return G.linear(x, w, b, epi=act)
         return G.linear(x, w, b)
     y = F.linear(x, w, b)
+    if act == "quick_gelu":
+        return y * torch.sigmoid(1.702 * y)
+    if act == "gelu":
+        return F.gelu(y)
+    if act is not None:
+        raise ValueError(act)
     if gated == "geglu":
         a, g = y.float().chunk(2, -1)
         y = (a * F.gelu(g, approximate="tanh")).to(x.dtype)

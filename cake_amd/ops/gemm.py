@@ -18,7 +18,8 @@ import torch
 
 from ._lib import check, kernels
 
-EPI = {"store": 0, "resid32": 1, "add16": 2, "swiglu": 3, "geglu": 4, "store32": 6, "silu": 7}
+EPI = {"store": 0, "resid32": 1, "add16": 2, "swiglu": 3, "geglu": 4, "store32": 6, "silu": 7,
+       "quick_gelu": 8, "gelu": 9}
 _DT = {torch.bfloat16: 0, torch.float16: 1}
 # (BM, BN) of the kernel's tile configurations (gemm.hip CAKE_GEMM_CFGS)
 CFG_TILES = {0: (128, 128), 1: (64, 128), 2: (256, 128), 3: (128, 256), 4: (64, 64),
@@ -166,6 +167,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, *
       geglu   -> out [..., F] = (y_h + b_h) * gelu_tanh(y_gate + b_gate)
       store32 -> resid (f32 [..., N], any row stride) = y (+ bias); returns resid
       silu    -> out = silu(y (+ bias))
+      quick_gelu / gelu -> out = act(y (+ bias)) (CLIP MLP: x*sigmoid(1.702x) / erf GELU)
     """
     if epi not in EPI:
         raise ValueError(f"unknown epilogue {epi}")

@@ -34,13 +34,13 @@ def main():
     dev = torch.device("cuda:0")
     if a.vae:
         return bench_vae(a, cfg, dev, dt)
+    if a.denoise:
+        return bench_denoise(a, dev, dt)
     w = random_component("unet", cfg, dev, dt)
     unet = UNet2DConditionModel(cfg.unet)
     B = 2  # classifier-free guidance doubles the batch
     x = torch.randn(B, 4, cfg.height // 8, cfg.width // 8, device=dev, dtype=dt)
     ctx = torch.randn(B, 77, cfg.unet.cross_attention_dim, device=dev, dtype=dt)
-    if a.denoise:
-        return bench_denoise(a, cfg, w, dev, dt, ctx)
     tbuf = torch.zeros((), device=dev)
     kv = {} if a.kv_cache else None  # cross-attn k/v of the (fixed) text context, as the pipeline
     with torch.no_grad():
@@ -88,26 +88,14 @@ def bench_vae(a, cfg, dev, dt):
                       "value": round(dt_s, 4), "unit": "s"}))
 
 
-def bench_denoise(a, cfg, w, dev, dt, ctx):
-    from cake_amd.models.sd.schedulers import build_scheduler
-    from cake_amd.models.sd.shardable import SDUnit
-    unit = SDUnit("unet", cfg, w, dev, dt)
-    sched = build_scheduler(cfg.scheduler, a.steps + 2)
-    ts = sched.timesteps()
-    lat = torch.randn(1, 4, cfg.height // 8, cfg.width // 8, device=dev) * sched.init_noise_sigma
-    with torch.no_grad():
-        unit.denoise(lat, ctx, sched, ts, 7.5, True, 1)  # step 0 eager, capture, replays
-        unit.denoise(lat, ctx, sched, ts, 7.5, True, 3)  # first replay-only call (lazy init)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        _, per = unit.denoise(lat, ctx, sched, ts, 7.5, True, 2)
-        torch.cuda.synchronize()
-    wall = (time.perf_counter() - t0) / len(ts)
+def bench_denoise(a, dev, dt):
+    from cake_amd.models.sd.bench import measure_denoise
+    r = measure_denoise(a.version, a.steps, dt, dev)
     print(json.dumps({"metric": "sd_unet_seconds_per_step", "version": a.version,
-                      "resolution": f"{cfg.width}x{cfg.height}", "batch": 2, "dtype": a.dtype,
-                      "value": round(wall, 4), "unit": "s/step", "graph": True, "denoise": True,
-                      "scheduler": cfg.scheduler.kind, "steps": len(ts),
-                      "per_step_s": [round(x, 4) for x in per],
+                      "resolution": r["resolution"], "batch": 2, "dtype": a.dtype,
+                      "value": round(r["seconds_per_step"], 4), "unit": "s/step", "graph": True,
+                      "denoise": True, "scheduler": r["scheduler"], "steps": r["steps"],
+                      "per_step_s": [round(x, 4) for x in r["per_step_s"]],
                       "nhwc": os.environ.get("CAKE_SD_NHWC", "1") != "0"}))
 
 

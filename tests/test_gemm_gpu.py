@@ -56,6 +56,21 @@ def test_gemm_resid32_and_add16(cuda, dt, splits):
 
 
 @pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("epi", ["silu", "quick_gelu", "gelu"])
+@pytest.mark.parametrize("cfg,splits", [(None, 1), (0, 1), (4, 2)])
+def test_gemm_activation_epilogues(cuda, dt, epi, cfg, splits):
+    """Activation epilogue (time-embedding SiLU, CLIP quick_gelu / erf GELU) with bias,
+    direct and through the split-K finalize."""
+    from cake_amd.ops import gemm as G
+    torch.manual_seed(4)
+    M, N, K = 154, 3072, 768  # CLIP fc1 at batch 2 x 77 tokens
+    x, w, b = _r(M, K, dt=dt), _r(N, K, dt=dt, std=K ** -0.5), _r(N, dt=dt)
+    y = _ref(x, w, b)
+    ref = {"silu": F.silu(y), "quick_gelu": y * torch.sigmoid(1.702 * y), "gelu": F.gelu(y)}[epi]
+    _close(G.linear(x, w, b, epi=epi, cfg=cfg, splits=splits), ref, K)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
 @pytest.mark.parametrize("M,Fh,K,splits", [(37, 512, 512, 1), (130, 1024, 1024, 2),
                                           (257, 48, 320, 1)])
 def test_gemm_gated(cuda, dt, M, Fh, K, splits):
