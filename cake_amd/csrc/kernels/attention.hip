@@ -18,6 +18,7 @@
 //     (max, sum, o[hd]) partials (one launch per layer).
 //   * Prefill attention is the MFMA flash kernel (flash_attn.hip).
 #include "attn_core.h"
+#include "attn_core2.h"
 
 namespace cake {
 
@@ -37,9 +38,30 @@ __global__ __launch_bounds__(AttnGeom<NREP>::NT) void attn_decode_kernel(AttnDec
   attn_decode_block<DT, HD, NREP>(a, blockIdx.x, blockIdx.y, smem);
 }
 
+template <int DT, int HD, int NREP>
+__global__ __launch_bounds__(AttnGeom<NREP>::NT) void attn2_decode_kernel(AttnDecArgs a) {
+  __shared__ __attribute__((aligned(16)))
+      float lds[attn2_smem_floats<HD, NREP, AttnGeom<NREP>::NW>()];
+  if ((int)blockIdx.y >= a.maxsplit) {  // prefetch rows of the grid
+    attn_prefetch_block<AttnGeom<NREP>::NT>(
+        a, (blockIdx.y - a.maxsplit) * gridDim.x + blockIdx.x,
+        (gridDim.y - a.maxsplit) * gridDim.x);
+    return;
+  }
+  attn2_decode_block<DT, HD, NREP>(a, blockIdx.x, blockIdx.y, lds);
+}
+
 }  // namespace cake
 
 using namespace cake;
+
+// 1 = LDS-staged chunk core (attn_core.h), 2 = wave-stream MFMA core (attn_core2.h)
+static int g_attn_impl = 1;
+CAKE_API int cake_attn_set_impl(int impl) {
+  if (impl != 1 && impl != 2) return (int)hipErrorInvalidValue;
+  g_attn_impl = impl;
+  return 0;
+}
 
 #define DISPATCH_DT_HD(dt, hd, ...)                                              \
   do {                                                                           \
@@ -91,7 +113,10 @@ CAKE_API int cake_attn_set_min_keys(int min_keys) {
 template <int DT, int HD>
 static int launch_decode(int n_rep, dim3 grid, hipStream_t st, const AttnDecArgs& a) {
 #define CAKE_DEC(NR)                                                                          \
-  hipLaunchKernelGGL((attn_decode_kernel<DT, HD, NR>), grid, dim3(AttnGeom<NR>::NT), 0, st, a)
+  if (g_attn_impl == 2)                                                                       \
+    hipLaunchKernelGGL((attn2_decode_kernel<DT, HD, NR>), grid, dim3(AttnGeom<NR>::NT), 0, st, a); \
+  else                                                                                        \
+    hipLaunchKernelGGL((attn_decode_kernel<DT, HD, NR>), grid, dim3(AttnGeom<NR>::NT), 0, st, a)
   switch (n_rep) {
     case 1: CAKE_DEC(1); break;
     case 2: CAKE_DEC(2); break;

@@ -1,0 +1,338 @@
+// KV-cached GQA decode attention, v2: wave-independent key streams with MFMA scores.
+// Included by attention.hip (same arguments / partial layout / ticket combine as
+// attn_core.h, selected with cake_attn_set_impl(2)).
+//
+// Replaces the reference's attention core:
+//   cake-core/src/models/llama3/attention.rs:89-119 and cache.rs:93-122.
+//
+// Why a second core: v1 stages 64-key chunks global -> registers -> LDS and every
+// wave then re-reads q (f32, broadcast) and its K row / V columns from LDS, with a
+// workgroup barrier per chunk — about 2.2 µs per extra chunk of a split
+// (profiles/r2_decode_attn_pv*.jsonl: 1 split of 512 keys 20 µs vs 8 splits 8.7).
+// Here nothing of K/V goes through LDS and the waves never wait for each other
+// before the end of the split:
+//   * a wave owns 16-key blocks (w, w + NW, ...) of its split and keeps its own
+//     online-softmax state (m, l, o) for the NREP query heads of the group;
+//   * scores S^T[16 keys x 16 cols] = K_blk[16 x HD] . Q^T on v_mfma_f32_16x16x32
+//     (A = K rows straight from global memory: lane l holds row l&15, dims
+//     32 d + 8 (l>>4); B = q as bf16 / f16 in registers, columns >= NREP zero) —
+//     HD/32 MFMAs per block;
+//   * the block's p (and the per-head rescale) go to a 1 KB wave-private LDS tile,
+//     and P.V runs on the VALU from V rows also loaded straight from global
+//     (lane -> 8 dims x HD/32 keys): NREP x 8 f32 accumulators per lane;
+//   * the next block's K/V loads are issued before the current block is computed;
+//   * at the end: key-group sums across lanes (permlane swaps), the NW waves'
+//     states merged once through LDS, and the split's partial published to the
+//     ticket combine of attn_core.h (or written out directly when ns == 1).
+// Dead keys (past the live length, or speculative rows of split 0 loaded before
+// the position arrived) are masked in the scores and zeroed in V.
+#pragma once
+#include "attn_core.h"
+
+namespace cake {
+
+constexpr int kBlk = 16;  // keys per wave block (MFMA M dimension)
+
+template <int OFF> __device__ __forceinline__ float xor_max(float v) {
+  static_assert(OFF == 16 || OFF == 32, "xor_max offset");
+  const int b = __builtin_bit_cast(int, v);
+  const auto p = OFF == 16 ? __builtin_amdgcn_permlane16_swap(b, b, false, false)
+                           : __builtin_amdgcn_permlane32_swap(b, b, false, false);
+  return fmaxf(__builtin_bit_cast(float, (int)p[0]), __builtin_bit_cast(float, (int)p[1]));
+}
+
+// LDS floats of the v2 core: per wave a p tile [16 keys][16 cols] + alpha[16], then
+// the end-of-split wave states (m[16], l[16], o[NREP][HD]) of all NW waves.
+template <int HD, int NREP, int NW>
+constexpr int attn2_smem_floats() {
+  return NW * (kBlk * 16 + 16) + NW * (32 + NREP * HD) + 1;
+}
+
+// host/device split policy of the v2 core (mirrored by ops.hip.attn_splits)
+__device__ __forceinline__ void attn2_splits(int Tk, int min_keys, int maxsplit, int& ns,
+                                             int& kps) {
+  int keys = (Tk + kMaxSplit - 1) / kMaxSplit;
+  keys = (keys + kBlk - 1) / kBlk * kBlk;
+  if (keys < min_keys) keys = min_keys;
+  ns = (Tk + keys - 1) / keys;
+  if (ns > maxsplit) ns = maxsplit;
+  kps = (Tk + ns - 1) / ns;
+  kps = (kps + kBlk - 1) / kBlk * kBlk;
+  ns = (Tk + kps - 1) / kps;
+}
+
+template <int DT, int HD, int NREP>
+__device__ __forceinline__ void attn2_decode_block(const AttnDecArgs& a, int g, int s,
+                                                   float* lds) {
+  constexpr int NW = AttnGeom<NREP>::NW;
+  constexpr int DS = HD / 32;    // MFMA k-steps (A fragments) per key block
+  constexpr int NCH = HD / 8;    // 8-dim chunks per row
+  constexpr int KPL = NCH / 4;   // keys per lane in P.V (16 keys over 64 / NCH key groups)
+  static_assert(NCH == 8 || NCH == 16, "hd 64 or 128");
+  static_assert(NREP <= 16, "GQA group <= 16 heads");
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int col = lane & 15, rg = lane >> 4;       // MFMA column (head) / row group
+  const int ch = lane % NCH, kg = lane / NCH;      // P.V: dim chunk / key group
+  float* pt = lds + wave * (kBlk * 16 + 16);       // this wave's p tile + alpha row
+  float* alph = pt + kBlk * 16;
+  float* st = lds + NW * (kBlk * 16 + 16);         // end-of-split wave states
+  unsigned long long stamp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  ATTN_STAMP(0);
+  const uint16_t* kgp = a.kc + (size_t)g * a.S * HD;
+  const uint16_t* vgp = a.vc + (size_t)g * a.S * HD;
+
+  // one block's operands: K A-fragments and V rows of this lane
+  uint4 kf[DS], vf[KPL];
+  auto load_blk = [&](int key0, int last) {
+#pragma unroll
+    for (int d = 0; d < DS; ++d) {
+      const int r = min(key0 + col, last);
+      kf[d] = *reinterpret_cast<const uint4*>(kgp + (size_t)r * HD + d * 32 + rg * 8);
+    }
+#pragma unroll
+    for (int j = 0; j < KPL; ++j) {
+      const int r = min(key0 + kg * KPL + j, last);
+      vf[j] = *reinterpret_cast<const uint4*>(vgp + (size_t)r * HD + ch * 8);
+    }
+  };
+
+  // split 0 starts at key 0: its first blocks are requested with the position
+  // (rows clamped to the cache; dead rows are masked / zeroed below)
+  if (s == 0) load_blk(wave * kBlk, a.S - 1);
+  // q (f32, roped) -> pre-scaled 16-bit B fragments: column col = head g*NREP + col
+  uint4 qf[DS];
+  {
+    float qv[DS][8];
+#pragma unroll
+    for (int d = 0; d < DS; ++d) {
+      if (col < NREP) {
+        const float* qp = a.q + (size_t)(g * NREP + col) * HD + d * 32 + rg * 8;
+        const float4 x0 = *reinterpret_cast<const float4*>(qp);
+        const float4 x1 = *reinterpret_cast<const float4*>(qp + 4);
+        qv[d][0] = x0.x; qv[d][1] = x0.y; qv[d][2] = x0.z; qv[d][3] = x0.w;
+        qv[d][4] = x1.x; qv[d][5] = x1.y; qv[d][6] = x1.z; qv[d][7] = x1.w;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) qv[d][e] = 0.f;
+      }
+    }
+#pragma unroll
+    for (int d = 0; d < DS; ++d) {
+      uint16_t h[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) h[e] = from_f32<DT>(qv[d][e] * a.scale_log2);
+      qf[d] = *reinterpret_cast<const uint4*>(h);
+    }
+  }
+  const int Tk = *a.pos + 1;
+  ATTN_STAMP(1);
+  int ns, kps;
+  attn2_splits(Tk, a.min_keys, a.maxsplit, ns, kps);
+  if (s >= ns) return;
+  const int kb = s * kps, ke = min(Tk, kb + kps);
+  const int nblk = (ke - kb + kBlk - 1) / kBlk;
+
+  float m = -INFINITY, l = 0.f;   // of head `col` (identical across row groups)
+  float o[NREP][8];
+#pragma unroll
+  for (int h = 0; h < NREP; ++h)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[h][e] = 0.f;
+
+  int b = wave;
+  if (s != 0 && b < nblk) load_blk(kb + b * kBlk, ke - 1);
+  ATTN_STAMP(2);
+  for (; b < nblk; b += NW) {
+    const int key0 = kb + b * kBlk;
+    // this block's operands, then the next block's loads in flight
+    uint4 kc[DS], vc[KPL];
+#pragma unroll
+    for (int d = 0; d < DS; ++d) kc[d] = kf[d];
+#pragma unroll
+    for (int j = 0; j < KPL; ++j) vc[j] = vf[j];
+    if (b + NW < nblk) load_blk(key0 + NW * kBlk, ke - 1);
+    // scores: S[key 4 rg + e][col]
+    cf32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int d = 0; d < DS; ++d) acc = cmfma<DT>(kc[d], qf[d], acc);
+    float sc[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) sc[e] = key0 + 4 * rg + e < ke ? acc[e] : -INFINITY;
+    float bm = fmaxf(fmaxf(sc[0], sc[1]), fmaxf(sc[2], sc[3]));
+    bm = xor_max<32>(xor_max<16>(bm));
+    const float mn = fmaxf(m, bm);
+    const float alpha = exp2f(m - mn);  // 0 on the first block (m = -inf)
+    float p[4], ps = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { p[e] = exp2f(sc[e] - mn); ps += p[e]; }
+    ps = xor_add<32>(xor_add<16>(ps));
+    l = l * alpha + ps;
+    m = mn;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) pt[(4 * rg + e) * 16 + col] = p[e];
+    if (rg == 0) alph[col] = alpha;
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the tile is in LDS
+    __builtin_amdgcn_wave_barrier();
+    // P.V on this lane's KPL keys x 8 dims; dead keys' V rows are zero
+    float al[NREP];
+#pragma unroll
+    for (int h = 0; h < NREP; ++h) al[h] = alph[h];
+#pragma unroll
+    for (int h = 0; h < NREP; ++h)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[h][e] *= al[h];
+#pragma unroll
+    for (int j = 0; j < KPL; ++j) {
+      const int key = key0 + kg * KPL + j;
+      float vv[8];
+      unpack8<DT>(vc[j], vv);
+      if (key >= ke) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) vv[e] = 0.f;
+      }
+      const float* prow = pt + (kg * KPL + j) * 16;
+#pragma unroll
+      for (int h = 0; h < NREP; ++h) {
+        const float ph = prow[h];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[h][e] = fmaf(ph, vv[e], o[h][e]);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // tile reads done before the next block's writes
+  }
+  ATTN_STAMP(3);
+  // sum the key groups: lanes of one dim chunk (lane % NCH) end with the wave's o
+#pragma unroll
+  for (int h = 0; h < NREP; ++h)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float v = o[h][e];
+      if constexpr (NCH == 8) v = xor_add<8>(v);
+      o[h][e] = xor_add<32>(xor_add<16>(v));
+    }
+  // wave states -> LDS: m/l of head col (lanes 0..15), o[h][ch*8..] (lanes 0..NCH-1)
+  float* ws = st + wave * (32 + NREP * HD);
+  if (lane < 16) { ws[lane] = m; ws[16 + lane] = l; }
+  if (kg == 0) {
+#pragma unroll
+    for (int h = 0; h < NREP; ++h)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ws[32 + h * HD + ch * 8 + e] = o[h][e];
+  }
+  __syncthreads();
+  ATTN_STAMP(4);
+  // merge the NW waves: thread -> outputs (h, d) = tid, tid + NT, ...
+  constexpr int NT = NW * 64;
+  constexpr int NOUT = NREP * HD;
+  constexpr int OPT = (NOUT + NT - 1) / NT;
+  float mo[OPT], lo[OPT], ao[OPT];
+#pragma unroll
+  for (int i = 0; i < OPT; ++i) {
+    const int idx = tid + i * NT;
+    const int h = idx / HD, d = idx - h * HD;
+    float M = -INFINITY;
+    if (idx < NOUT) {
+#pragma unroll
+      for (int w = 0; w < NW; ++w) M = fmaxf(M, st[w * (32 + NREP * HD) + h]);
+    }
+    float L = 0.f, A = 0.f;
+    if (idx < NOUT) {
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        const float* wsw = st + w * (32 + NREP * HD);
+        const float wt = exp2f(wsw[h] - M);  // waves without keys: m = -inf -> 0
+        L = fmaf(wt, wsw[16 + h], L);
+        A = fmaf(wt, wsw[32 + h * HD + d], A);
+      }
+    }
+    mo[i] = M; lo[i] = L; ao[i] = A;
+  }
+  if (ns == 1) {  // the whole context in this split: finish here
+    ATTN_STAMP(5);
+#pragma unroll
+    for (int i = 0; i < OPT; ++i) {
+      const int idx = tid + i * NT;
+      if (idx < NOUT) a.out[(size_t)g * NOUT + idx] = from_f32<DT>(ao[i] / lo[i]);
+    }
+    if (a.stamps != nullptr && tid == 0) {
+      unsigned long long* dd = a.stamps + ((size_t)s * gridDim.x + g) * 8;
+      for (int k = 0; k < 8; ++k) dd[k] = k < 6 ? stamp[k] : 0ull;
+    }
+    return;
+  }
+  // publish the split's partial [h][s][m, l, o...] (layout of attn_core.h)
+#pragma unroll
+  for (int i = 0; i < OPT; ++i) {
+    const int idx = tid + i * NT;
+    if (idx < NOUT) {
+      const int h = idx / HD, d = idx - h * HD;
+      float* dst = a.part + ((size_t)(g * NREP + h) * kMaxSplit + s) * (HD + 2);
+      if (d == 0) { st_sc1(dst, mo[i]); st_sc1(dst + 1, lo[i]); }
+      st_sc1(dst + 2 + d, ao[i]);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  ATTN_STAMP(5);
+  unsigned int* last_flag = reinterpret_cast<unsigned int*>(lds + attn2_smem_floats<HD, NREP, NW>() - 1);
+  if (tid == 0) {
+    const unsigned int t =
+        __hip_atomic_fetch_add(&a.tickets[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned int last = (t == (unsigned int)(ns - 1)) ? 1u : 0u;
+    if (last) a.tickets[g] = 0u;  // re-arm for the next launch (kernel boundary orders it)
+    *last_flag = last;
+  }
+  __syncthreads();
+  ATTN_STAMP(6);
+  const bool is_last = *last_flag != 0;
+  if (!is_last || wave >= NREP) {
+    if (a.stamps != nullptr && tid == 0) {
+      unsigned long long* dd = a.stamps + ((size_t)s * gridDim.x + g) * 8;
+      for (int k = 0; k < 8; ++k) dd[k] = k < 7 ? stamp[k] : 0ull;
+    }
+    return;
+  }
+  // merge the ns <= 64 partials of this wave's head: lane t owns split t's (m, l)
+  constexpr int DPL = HD / 64;
+  const int h = g * NREP + wave;
+  const float* src = a.part + (size_t)h * kMaxSplit * (HD + 2);
+  const float mt = lane < ns ? ld_sc1(src + lane * (HD + 2)) : -INFINITY;
+  const float lt = lane < ns ? ld_sc1(src + lane * (HD + 2) + 1) : 0.f;
+  const float M = wave_max(mt);
+  const float wt = lane < ns ? exp2f(mt - M) : 0.f;
+  const float L = wave_sum(wt * lt);
+  pt[lane] = wt;  // (the wave's p tile is free now)
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+  float acc2[DPL];
+#pragma unroll
+  for (int d = 0; d < DPL; ++d) acc2[d] = 0.f;
+  constexpr int MR = 8;
+  for (int t0 = 0; t0 < ns; t0 += MR) {
+    float v[MR][DPL];
+#pragma unroll
+    for (int u = 0; u < MR; ++u) {
+      const int t = t0 + u < ns ? t0 + u : ns - 1;
+      const float* ptp = src + t * (HD + 2) + 2 + lane * DPL;
+#pragma unroll
+      for (int d = 0; d < DPL; ++d) v[u][d] = ld_sc1(ptp + d);
+    }
+#pragma unroll
+    for (int u = 0; u < MR; ++u) {
+      const float w = t0 + u < ns ? pt[t0 + u] : 0.f;
+#pragma unroll
+      for (int d = 0; d < DPL; ++d) acc2[d] = fmaf(w, v[u][d], acc2[d]);
+    }
+  }
+  const float inv = 1.f / L;
+  uint16_t* dst = a.out + (size_t)h * HD + lane * DPL;
+#pragma unroll
+  for (int d = 0; d < DPL; ++d) dst[d] = from_f32<DT>(acc2[d] * inv);
+  ATTN_STAMP(7);
+  if (a.stamps != nullptr && lane == 0 && wave == 0) {
+    unsigned long long* dd = a.stamps + ((size_t)s * gridDim.x + g) * 8;
+    for (int k = 0; k < 8; ++k) dd[k] = stamp[k];
+  }
+}
+
+}  // namespace cake

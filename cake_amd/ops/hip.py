@@ -136,6 +136,8 @@ def attn_decode(q, kcache, vcache, pos, scale, part, tickets, out, prefetch=None
     if hd not in (64, 128) or nh % nkv or (nh // nkv) not in (1, 2, 4, 8):
         raise ValueError(f"unsupported attention shape nh={nh} nkv={nkv} hd={hd}")
     pf, pfb = None, 0
+    if not _ATTN_IMPL_SET[0]:  # CAKE_ATTN_IMPL, applied once
+        attn_set_impl(_ATTN_IMPL[0])
     if _PF_ROWS_ENV[0] is not None:  # sweep override (CAKE_ATTN_PF_ROWS), applied once
         attn_set_prefetch_rows(int(_PF_ROWS_ENV[0]))
         _PF_ROWS_ENV[0] = None
@@ -181,8 +183,25 @@ def attn_max_split(S: int) -> int:
 def attn_splits(Tk: int) -> int:
     """Splits the decode-attention kernel uses at live length Tk with no cap (the
     device-side policy of attn_core.h, mirrored for choosing a capped graph)."""
+    if _ATTN_IMPL[0] == 2:  # attn_core2.h attn2_splits
+        keys = max(_ATTN_MIN_KEYS[0], -(-(-(-Tk // 64)) // 16) * 16)
+        ns = min(-(-Tk // keys), 64)
+        kps = -(-(-(-Tk // ns)) // 16) * 16
+        return -(-Tk // kps)
     keys = max(_ATTN_MIN_KEYS[0], 128 if Tk > 1024 else 64, -(-Tk // 64))
     return -(-Tk // keys)
+
+
+_ATTN_IMPL = [int(os.environ.get("CAKE_ATTN_IMPL", "1"))]
+_ATTN_IMPL_SET = [False]
+
+
+def attn_set_impl(impl: int) -> None:
+    """Decode-attention core: 1 = LDS-staged chunks (attn_core.h), 2 = wave-stream MFMA
+    (attn_core2.h).  Graphs captured before a change keep the core they recorded."""
+    check(kernels().cake_attn_set_impl(int(impl)), "attn_set_impl")
+    _ATTN_IMPL[0] = int(impl)
+    _ATTN_IMPL_SET[0] = True
 
 
 class attn_split_cap:

@@ -3,7 +3,8 @@ every workgroup; cake_attn_set_stamps).  Phases: 0 start, 1 position read issued
 2 first chunk in LDS, 3 chunk loop done, 4 key groups combined, 5 partial published /
 direct write issued, 6 ticket known, 7 merge done (last workgroup only).
 
-Each launch follows a 64 MiB streaming read, as in decode (K/V not L2-resident)."""
+Each launch follows a 64 MiB streaming read, as in decode (K/V not L2-resident).
+IMPLS=1,2 selects the decode-attention cores (attn_core.h / attn_core2.h)."""
 import ctypes as C
 import json
 import math
@@ -33,11 +34,15 @@ def main():
     lib = kernels()
     lib.cake_attn_set_stamps.argtypes = [C.c_void_p]
     lib.cake_attn_set_stamps.restype = C.c_int
-    for Tk in [int(x) for x in os.environ.get("TKS", "57,176,1024,2048,4000").split(",")]:
+    impls = [int(x) for x in os.environ.get("IMPLS", "1,2").split(",")]
+    cases = [(i, int(x)) for i in impls
+             for x in os.environ.get("TKS", "57,176,512,1024,2048,4000").split(",")]
+    for impl, Tk in cases:
+        K.attn_set_impl(impl)
         pos.fill_(Tk - 1)
         need = K.attn_splits(Tk)
         cap = next(c for c in (8, 16, 32, 64) if c >= need) if need <= 64 else 64
-        rec = {"Tk": Tk, "cap": cap}
+        rec = {"impl": impl, "Tk": Tk, "cap": cap, "splits": need}
         with K.attn_split_cap(cap):
             # plain timing: events around each launch after a streaming read
             ts = []

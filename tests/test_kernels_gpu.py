@@ -98,8 +98,18 @@ def test_qkv_rope(cuda, dt, H, nh, nkv, hd, pos):
                                              (32, 8, 128, 2047, 2048), (64, 8, 128, 300, 2048),
                                              (4, 1, 64, 17, 2048), (8, 8, 64, 200, 2048),
                                              (16, 4, 128, 70, 100), (32, 8, 128, 8190, 8192)])
+@pytest.fixture(params=[1, 2], ids=["core1", "core2"])
+def attn_impl(request, cuda):
+    """Both decode-attention cores (attn_core.h chunks / attn_core2.h wave-stream MFMA)."""
+    from cake_amd.ops import hip as K_
+    prev = K_._ATTN_IMPL[0]
+    K_.attn_set_impl(request.param)
+    yield request.param
+    K_.attn_set_impl(prev)
+
+
 @pytest.mark.parametrize("min_keys", [64, 256])
-def test_attn_decode(cuda, dt, nh, nkv, hd, pos, S, min_keys):
+def test_attn_decode(cuda, attn_impl, dt, nh, nkv, hd, pos, S, min_keys):
     """Split-K decode attention (split count derived on device from pos) vs f32 attention;
     S not a multiple of 64, more than 64 splits' worth of keys (S = 8192: 128-key splits)."""
     from cake_amd.ops import hip as K_
@@ -113,9 +123,11 @@ def test_attn_decode(cuda, dt, nh, nkv, hd, pos, S, min_keys):
     tickets = torch.zeros(nkv, dtype=torch.int32, device=cuda)
     K_.attn_set_min_keys(min_keys)
     try:
-        for _ in range(2):  # second call checks the tickets were re-armed
+        for it in range(2):  # second call checks the tickets were re-armed
             out.zero_()
-            K_.attn_decode(q, kc, vc, p, 1 / math.sqrt(hd), part, tickets, out)
+            # the second call also streams a buffer through the prefetch workgroups
+            K_.attn_decode(q, kc, vc, p, 1 / math.sqrt(hd), part, tickets, out,
+                           prefetch=vc if it else None)
             assert int(tickets.abs().sum()) == 0
     finally:
         K_.attn_set_min_keys(64)
@@ -143,7 +155,7 @@ def test_wave_reductions(cuda):
 
 
 @pytest.mark.parametrize("pos", [0, 5, 63, 64, 130])
-def test_attn_decode_dead_rows_nan(cuda, pos):
+def test_attn_decode_dead_rows_nan(cuda, attn_impl, pos):
     """Cache rows past the live length hold NaN: split 0 loads its first chunk before
     the length is known, so those rows must never reach the output."""
     from cake_amd.ops import hip as K_
