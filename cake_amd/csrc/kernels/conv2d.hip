@@ -44,6 +44,8 @@ struct ConvArgs {
   int N, H, W, IC, OC, OH, OW, KH, KW, stride, pad, up;
   int P, ksteps, ks_per_split, tiles_m, tiles_n;
   int bias2_ld;           // row stride of bias2 (elements; OC when packed)
+  int in_nchw;            // x is [N][IC][H][W] (direct small-IC kernel only: UNet conv_in)
+  int out_nchw;           // out is [N][OC][OH][OW] (no resid: UNet conv_out)
 };
 
 
@@ -62,6 +64,12 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, int oc, int p, 
     const int n = p / (a.OH * a.OW);
     const float4 b = *reinterpret_cast<const float4*>(a.bias2 + (size_t)n * a.bias2_ld + oc);
     r[0] += b.x; r[1] += b.y; r[2] += b.z; r[3] += b.w;
+  }
+  if (a.out_nchw) {  // planar output: the UNet's last conv writes the external layout
+    const int ohw = a.OH * a.OW, n = p / ohw, px = p - n * ohw;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a.out[((size_t)n * a.OC + oc + i) * ohw + px] = from_f32<DT>(r[i]);
+    return;
   }
   const size_t o = (size_t)p * a.OC + oc;
   if (a.resid) {
@@ -524,9 +532,18 @@ __global__ __launch_bounds__(256) void conv_smallc_kernel(ConvArgs a) {
       for (int kw = 0; kw < 3; ++kw) {
         const int ih = oh * a.stride - a.pad + kh, iw = ow * a.stride - a.pad + kw;
         const bool ok = ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
-        const uint16_t* src = a.x + (((size_t)n * a.H + (ok ? ih : 0)) * a.W + (ok ? iw : 0)) * IC;
+        const int ihc = ok ? ih : 0, iwc = ok ? iw : 0;
+        if (a.in_nchw) {  // planar input (the UNet's external layout)
+          const size_t plane = (size_t)a.H * a.W;
+          const uint16_t* src = a.x + (size_t)n * IC * plane + (size_t)ihc * a.W + iwc;
 #pragma unroll
-        for (int c = 0; c < IC; ++c) xin[(kh * 3 + kw) * IC + c] = ok ? to_f32<DT>(src[c]) : 0.f;
+          for (int c = 0; c < IC; ++c)
+            xin[(kh * 3 + kw) * IC + c] = ok ? to_f32<DT>(src[c * plane]) : 0.f;
+        } else {
+          const uint16_t* src = a.x + (((size_t)n * a.H + ihc) * a.W + iwc) * IC;
+#pragma unroll
+          for (int c = 0; c < IC; ++c) xin[(kh * 3 + kw) * IC + c] = ok ? to_f32<DT>(src[c]) : 0.f;
+        }
       }
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     const float* wr = wsm + og * 8;
@@ -558,12 +575,16 @@ CAKE_API long long cake_conv2d_workspace(int P, int OC, int splits) {
 //      8/9 = halo kernel, 128/64 oc x (th x tw <= 128 pixels), 10/11 = 128/64 oc x
 //      (th x tw <= 64 pixels), 12/13 = 128/64 oc x (th x tw <= 256 pixels, 8 waves);
 //      stride 1 only, no split-K; 14 = direct 3x3 kernel for IC 3 / 4 (conv_in).
-CAKE_API int cake_conv2d_nhwc(int dt, const void* x, const void* w, const void* bias,
-                              const float* bias2, const void* resid, void* out, float* ws,
-                              const void* zeros,
-                              int N, int H, int W, int IC, int OC, int KH, int KW, int stride,
-                              int pad, int up, int cfg, int splits, int th, int tw,
-                              int bias2_ld, hipStream_t st) {
+// layout: bit 0 = x NCHW (cfg 14 only), bit 1 = out NCHW (no resid)
+CAKE_API int cake_conv2d_nhwc2(int dt, const void* x, const void* w, const void* bias,
+                               const float* bias2, const void* resid, void* out, float* ws,
+                               const void* zeros,
+                               int N, int H, int W, int IC, int OC, int KH, int KW, int stride,
+                               int pad, int up, int cfg, int splits, int th, int tw,
+                               int bias2_ld, int layout, hipStream_t st) {
+  const int in_nchw = layout & 1, out_nchw = (layout >> 1) & 1;
+  if ((in_nchw && cfg != 14) || (out_nchw && resid) || layout < 0 || layout > 3)
+    return (int)hipErrorInvalidValue;
   if (cfg == 14) {  // direct small-IC 3x3 kernel
     if ((IC != 3 && IC != 4) || KH != 3 || KW != 3 || OC % 8 || 9 * IC * OC > kSmallCMaxW ||
         N <= 0 || stride <= 0 || up || (bias2 && bias2_ld > 0 && (bias2_ld % 4 || bias2_ld < OC)))
@@ -574,6 +595,8 @@ CAKE_API int cake_conv2d_nhwc(int dt, const void* x, const void* w, const void* 
                (const uint16_t*)resid, (uint16_t*)out, nullptr, nullptr, N, H, W, IC, OC, OH, OW,
                3, 3, stride, pad, 0, N * OH * OW, 0, 0, 0, 0};
     a.bias2_ld = bias2_ld > 0 ? bias2_ld : OC;
+    a.in_nchw = in_nchw;
+    a.out_nchw = out_nchw;
     const long long work = (long long)a.P * (OC / 8);
     const unsigned grid = (unsigned)std::min<long long>((work + 255) / 256, 2048);
 #define CAKE_SMALLC(DTV)                                                                         \
@@ -604,6 +627,8 @@ CAKE_API int cake_conv2d_nhwc(int dt, const void* x, const void* w, const void* 
                IC, OC, OH, OW, KH, KW, 1, pad, up, N * OH * OW, KH * KW * (IC / 64), 0,
                (OC + bm - 1) / bm, N * ty * tx};
     a.bias2_ld = bias2_ld > 0 ? bias2_ld : OC;
+    a.in_nchw = in_nchw;
+    a.out_nchw = out_nchw;
     const dim3 grid(a.tiles_m * a.tiles_n);
 #define CAKE_HALO(DTV)                                                                                     \
     switch (cfg) {                                                                                         \
@@ -626,6 +651,8 @@ CAKE_API int cake_conv2d_nhwc(int dt, const void* x, const void* w, const void* 
              (const uint16_t*)resid, (uint16_t*)out, ws, (const uint16_t*)zeros, N, H, W, IC, OC, OH, OW, KH, KW,
              stride, pad, up, N * OH * OW, KH * KW * (IC / 64), 0, 0, 0};
   a.bias2_ld = bias2_ld > 0 ? bias2_ld : OC;
+    a.in_nchw = in_nchw;
+    a.out_nchw = out_nchw;
   a.tiles_m = (OC + BMs[cfg] - 1) / BMs[cfg];
   a.tiles_n = (a.P + BNs[cfg] - 1) / BNs[cfg];
   splits = splits > a.ksteps ? a.ksteps : splits;
@@ -655,4 +682,14 @@ CAKE_API int cake_conv2d_nhwc(int dt, const void* x, const void* w, const void* 
   else return (int)hipErrorInvalidValue;
 #undef CAKE_CONV
   return (int)hipGetLastError();
+}
+
+CAKE_API int cake_conv2d_nhwc(int dt, const void* x, const void* w, const void* bias,
+                              const float* bias2, const void* resid, void* out, float* ws,
+                              const void* zeros,
+                              int N, int H, int W, int IC, int OC, int KH, int KW, int stride,
+                              int pad, int up, int cfg, int splits, int th, int tw,
+                              int bias2_ld, hipStream_t st) {
+  return cake_conv2d_nhwc2(dt, x, w, bias, bias2, resid, out, ws, zeros, N, H, W, IC, OC, KH, KW,
+                           stride, pad, up, cfg, splits, th, tw, bias2_ld, 0, st);
 }

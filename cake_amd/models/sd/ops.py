@@ -229,13 +229,18 @@ def conv2d(x, w, b=None, stride: int = 1, padding: int = 1):
 
 
 def conv(W, name: str, x, stride: int = 1, padding: int = 1, up: bool = False, bias2=None,
-         resid=None):
+         resid=None, in_nchw: bool = False, out_nchw: bool = False):
     """Convolution `name` of W on x in the active layout.
 
     up: nearest-2x upsample x first; bias2 [B, OC]: per-sample additive bias
     (ResnetBlock2D time embedding); resid: added to the output (block residual).
+    in_nchw / out_nchw (channels-last layout only): x arrives in / the output leaves in
+    the external NCHW layout — the UNet's conv_in / conv_out, so the layout change is
+    part of those kernels instead of two copy kernels per step.
     """
     w, b = W[f"{name}.weight"], W.get(f"{name}.bias")
+    if not nhwc():
+        in_nchw = out_nchw = False  # NCHW throughout
     if nhwc():
         from ...ops import hip as K
         OC, IC = w.shape[:2]
@@ -245,10 +250,20 @@ def conv(W, name: str, x, stride: int = 1, padding: int = 1, up: bool = False, b
             wp = W.get(key)
             if wp is None or wp.dtype != x.dtype:
                 wp = W[key] = w.to(x.dtype).permute(0, 2, 3, 1).contiguous()
+            if in_nchw and IC % 64 == 0:  # only the direct small-IC kernel reads planes
+                x, in_nchw = to_internal(x), False
+            if out_nchw and resid is not None:
+                y = conv(W, name, x, stride, padding, up, bias2, resid, in_nchw=in_nchw)
+                return to_external(y)
             return C.conv2d(x.contiguous(), wp, b, stride=stride, pad=padding, up=up,
                             bias2=None if bias2 is None else
                             (bias2 if bias2.dtype == torch.float32 else bias2.float()),
-                            resid=None if resid is None else resid.contiguous())
+                            resid=None if resid is None else resid.contiguous(),
+                            in_nchw=in_nchw, out_nchw=out_nchw)
+        if in_nchw:
+            x = to_internal(x)
+        if out_nchw:
+            return to_external(conv(W, name, x, stride, padding, up, bias2, resid))
         xn = x.permute(0, 3, 1, 2)  # channels_last view: MIOpen's NHWC kernels
         if up:
             xn = F.interpolate(xn, scale_factor=2.0, mode="nearest")

@@ -39,9 +39,9 @@ class Conv(Module):
             p[f"{self.name}.bias"] = (self.cout,)
         return p
 
-    def __call__(self, W, x, up=False, bias2=None, resid=None):
+    def __call__(self, W, x, up=False, bias2=None, resid=None, in_nchw=False, out_nchw=False):
         return ops.conv(W, self.name, x, self.stride, self.padding, up=up, bias2=bias2,
-                        resid=resid)
+                        resid=resid, in_nchw=in_nchw, out_nchw=out_nchw)
 
 
 class Linear(Module):
@@ -367,7 +367,8 @@ class UNet2DConditionModel(Module):
         tbs = self.time_biases(W, timestep, sample.shape[0], sample.dtype, sample.device,
                                t_index)
         with ops.layout_nhwc(ops.want_nhwc(sample)):
-            return ops.to_external(self._body(W, ops.to_internal(sample), tbs, ctx, kv_cache))
+            # NCHW in and out: conv_in reads the planes, conv_out writes them
+            return self._body(W, sample, tbs, ctx, kv_cache)
 
     # ------------------------------------------------------------------ stages
     # The body as a chain of block-group stages ("down.0" .. "down.{n-1}", "mid",
@@ -380,13 +381,14 @@ class UNet2DConditionModel(Module):
 
     def run_stage(self, W, name: str, x: torch.Tensor, skips: list, tbs, ctx, kv_cache):
         """One stage over (x, skips) in the active layout; returns the new (x, skips).
-        down.0 takes the UNet input (conv_in); the last up stage ends in conv_out."""
+        down.0 takes the NCHW UNet input (conv_in reads it in place); the last up stage
+        ends in conv_out, which writes the NCHW UNet output."""
         cfg = self.cfg
         kind, _, idx = name.partition(".")
         if kind == "down":
             i = int(idx)
             if i == 0:
-                x = self.conv_in(W, x)
+                x = self.conv_in(W, x, in_nchw=True)
                 skips = [x]
             res, att, ds = self.down[i]
             for j, r in enumerate(res):
@@ -414,7 +416,7 @@ class UNet2DConditionModel(Module):
         if i == len(self.up) - 1:
             x = ops.group_norm(x, W["conv_norm_out.weight"], W["conv_norm_out.bias"],
                                cfg.norm_num_groups, cfg.norm_eps, silu=True)
-            x = self.conv_out(W, x)
+            x = self.conv_out(W, x, out_nchw=True)
         return x, skips
 
     def forward_stages(self, W, names: list[str], x: torch.Tensor, skips: list, timestep, ctx,
@@ -425,14 +427,10 @@ class UNet2DConditionModel(Module):
         ranks of one job share it), so a hop moves them as they are."""
         B = x.shape[0]
         tbs = self.time_biases(W, timestep, B, x.dtype, x.device, t_index)
-        last = self.stage_names()[-1]
+        # (down.0 reads / the last up stage writes the NCHW layout itself)
         with ops.layout_nhwc(ops.want_nhwc(x)):
-            if names[0] == "down.0":
-                x = ops.to_internal(x)
             for n in names:
                 x, skips = self.run_stage(W, n, x, skips, tbs, ctx, kv_cache)
-            if names[-1] == last:
-                x = ops.to_external(x)
             return x, skips
 
     def _body(self, W, sample, tbs, ctx, kv_cache):

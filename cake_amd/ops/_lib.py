@@ -120,4 +120,5 @@ _SIGS.update({
     "cake_geglu": [I, P, C.c_longlong, I, P, P],
     "cake_stream_read": [P, Z, I, P, P],
     "cake_conv2d_nhwc": [I, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, P],
+    "cake_conv2d_nhwc2": [I, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, P],
 })

@@ -43,12 +43,17 @@ def _time(fn, iters=3) -> float:
 
 
 def conv2d(x, w, bias=None, *, stride: int = 1, pad: int = 1, up: bool = False, bias2=None,
-           resid=None):
-    """NHWC conv with the tuned kernel variant for this shape (see conv2d_nhwc)."""
-    N, H, W, IC = x.shape
+           resid=None, in_nchw: bool = False, out_nchw: bool = False):
+    """NHWC conv with the tuned kernel variant for this shape (see conv2d_nhwc; in_nchw /
+    out_nchw: planar input / output)."""
+    if in_nchw:
+        N, IC, H, W = x.shape
+    else:
+        N, H, W, IC = x.shape
     OC, KH, KW, _ = w.shape
+    lay = dict(in_nchw=in_nchw, out_nchw=out_nchw)
     key = (x.dtype, N, H, W, IC, OC, KH, KW, stride, pad, bool(up), bias2 is not None,
-           resid is not None)
+           resid is not None, in_nchw, out_nchw)
     choice = _cache.get(key)
     if choice is None:
         capturing = torch.cuda.is_current_stream_capturing()
@@ -56,7 +61,8 @@ def conv2d(x, w, bias=None, *, stride: int = 1, pad: int = 1, up: bool = False, 
             best = None
             for cfg, sp in _candidates(stride, KH * KW, True, IC):
                 f = (lambda c=cfg, s=sp: K.conv2d_nhwc(x, w, bias, stride=stride, pad=pad, up=up,
-                                                       bias2=bias2, resid=resid, cfg=c, splits=s))
+                                                       bias2=bias2, resid=resid, cfg=c, splits=s,
+                                                       **lay))
                 try:
                     t = _time(f)
                 except (ValueError, RuntimeError):
@@ -71,7 +77,7 @@ def conv2d(x, w, bias=None, *, stride: int = 1, pad: int = 1, up: bool = False, 
                       else (14, 1))
         _cache[key] = choice
     return K.conv2d_nhwc(x, w, bias, stride=stride, pad=pad, up=up, bias2=bias2, resid=resid,
-                         cfg=choice[0], splits=choice[1])
+                         cfg=choice[0], splits=choice[1], **lay)
 
 
 def tuned() -> dict:

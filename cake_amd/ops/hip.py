@@ -662,13 +662,19 @@ def conv_plan(P: int, OC: int, ksteps: int) -> tuple[int, int]:
 
 def conv2d_nhwc(x, w, bias=None, *, stride: int = 1, pad: int = 1, up: bool = False,
                 bias2=None, resid=None, out=None, cfg: int | None = None,
-                splits: int | None = None, tile: tuple[int, int] | None = None):
+                splits: int | None = None, tile: tuple[int, int] | None = None,
+                in_nchw: bool = False, out_nchw: bool = False):
     """NHWC conv: x [N,H,W,IC], w packed [OC,KH,KW,IC] -> [N,OH,OW,OC].
 
     bias [OC]; bias2 [N,OC] f32 (per-sample additive, e.g. time embedding);
     resid [N,OH,OW,OC] added in the epilogue; up = nearest-2x upsample of x first.
+    in_nchw: x is [N,IC,H,W] (the direct small-IC kernel only: UNet conv_in reads the
+    external layout); out_nchw: the output is written [N,OC,OH,OW] (no resid: conv_out).
     """
-    N, H, W, IC = x.shape
+    if in_nchw:
+        N, IC, H, W = x.shape
+    else:
+        N, H, W, IC = x.shape
     OC, KH, KW, IC2 = w.shape
     if IC2 != IC or KH != KW or not conv_supported(IC, OC, stride, up, KH):
         raise ValueError(f"conv2d_nhwc: unsupported IC={IC} OC={OC} w={tuple(w.shape)}")
@@ -686,13 +692,18 @@ def conv2d_nhwc(x, w, bias=None, *, stride: int = 1, pad: int = 1, up: bool = Fa
                              f"stride and 16-byte aligned rows")
         bias2_ld = bias2.stride(0) if N > 1 else OC
     if resid is not None:
+        if out_nchw:
+            raise ValueError("conv2d_nhwc: out_nchw takes no resid")
         _req(resid, "resid", dtype=x.dtype, shape=(N, OH, OW, OC))
+    oshape = (N, OC, OH, OW) if out_nchw else (N, OH, OW, OC)
     if out is None:
-        out = torch.empty(N, OH, OW, OC, device=x.device, dtype=x.dtype)
-    _req(out, "out", dtype=x.dtype, shape=(N, OH, OW, OC))
+        out = torch.empty(*oshape, device=x.device, dtype=x.dtype)
+    _req(out, "out", dtype=x.dtype, shape=oshape)
     P, ksteps = N * OH * OW, KH * KW * IC // 64
     if IC % 64:  # small-IC direct kernel: one variant
         cfg, splits, ksteps = 14, 1, 1
+    elif in_nchw:
+        raise ValueError("conv2d_nhwc: in_nchw needs the small-IC kernel (IC 3 / 4)")
     if cfg is None or splits is None:
         c0, s0 = conv_plan(P, OC, ksteps)
         cfg = c0 if cfg is None else cfg
@@ -707,13 +718,14 @@ def conv2d_nhwc(x, w, bias=None, *, stride: int = 1, pad: int = 1, up: bool = Fa
     kps = -(-ksteps // splits)
     splits = -(-ksteps // kps)
     ws = torch.empty(splits * P * OC, device=x.device, dtype=torch.float32) if splits > 1 else None
-    check(kernels().cake_conv2d_nhwc(_dt(x), _p(x), _p(w), None if bias is None else _p(bias),
-                                     None if bias2 is None else _p(bias2),
-                                     None if resid is None else _p(resid), _p(out),
-                                     None if ws is None else _p(ws), _p(_zeros16(x.device)),
-                                     N, H, W, IC, OC, KH, KW,
-                                     stride, pad, int(up), int(cfg), int(splits), th, tw,
-                                     int(bias2_ld), _stream()),
+    check(kernels().cake_conv2d_nhwc2(_dt(x), _p(x), _p(w), None if bias is None else _p(bias),
+                                      None if bias2 is None else _p(bias2),
+                                      None if resid is None else _p(resid), _p(out),
+                                      None if ws is None else _p(ws), _p(_zeros16(x.device)),
+                                      N, H, W, IC, OC, KH, KW,
+                                      stride, pad, int(up), int(cfg), int(splits), th, tw,
+                                      int(bias2_ld), int(in_nchw) | (int(out_nchw) << 1),
+                                      _stream()),
           "conv2d_nhwc")
     return out
 

@@ -17,6 +17,13 @@ step() {  # name timeout cmd...
 [[ ${DO_TESTS:-1} == 1 ]] && step pytest 600 python -u -m pytest ${TESTS:-tests} -x -q -m gpu --timeout 120 --timeout-method thread
 [[ ${DO_BENCH:-1} == 1 ]] && step bench 400 python bench.py ${BENCH_ARGS:-}
 [[ ${DO_STAMPS:-0} == 1 ]] && step attn_stamps 120 python scripts/attn_stamps.py
+if [[ ${DO_AB:-0} == 1 ]]; then  # decode A/B: attention core, MALL prefetch, long context
+  step ab_impl2 200 env CAKE_ATTN_IMPL=2 python bench.py --no-extras
+  step ab_nopf 200 env CAKE_ATTN_PREFETCH=0 python bench.py --no-extras
+  step ab_impl1 200 env CAKE_ATTN_IMPL=1 python bench.py --no-extras
+  step ab_p2048_impl1 200 env CAKE_ATTN_IMPL=1 python bench.py --no-extras --prompt-len 2048
+  step ab_p2048_impl2 200 env CAKE_ATTN_IMPL=2 python bench.py --no-extras --prompt-len 2048
+fi
 if [[ ${DO_SD:-0} == 1 ]]; then
   step sd_xl 300 python scripts/bench_sd.py --version xl --denoise --graph --steps 8
   step sd_15 200 python scripts/bench_sd.py --version v1-5 --denoise --graph --steps 8

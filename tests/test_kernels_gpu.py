@@ -92,12 +92,6 @@ def test_qkv_rope(cuda, dt, H, nh, nkv, hd, pos):
     assert kc[:, :pos].abs().sum() == 0 and kc[:, pos + 1:].abs().sum() == 0
 
 
-@pytest.mark.parametrize("dt", DTYPES)
-@pytest.mark.parametrize("nh,nkv,hd,pos,S", [(32, 8, 128, 0, 2048), (32, 8, 128, 63, 2048),
-                                             (32, 8, 128, 64, 2048), (32, 8, 128, 1000, 2048),
-                                             (32, 8, 128, 2047, 2048), (64, 8, 128, 300, 2048),
-                                             (4, 1, 64, 17, 2048), (8, 8, 64, 200, 2048),
-                                             (16, 4, 128, 70, 100), (32, 8, 128, 8190, 8192)])
 @pytest.fixture(params=[1, 2], ids=["core1", "core2"])
 def attn_impl(request, cuda):
     """Both decode-attention cores (attn_core.h chunks / attn_core2.h wave-stream MFMA)."""
@@ -108,6 +102,12 @@ def attn_impl(request, cuda):
     K_.attn_set_impl(prev)
 
 
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("nh,nkv,hd,pos,S", [(32, 8, 128, 0, 2048), (32, 8, 128, 63, 2048),
+                                             (32, 8, 128, 64, 2048), (32, 8, 128, 1000, 2048),
+                                             (32, 8, 128, 2047, 2048), (64, 8, 128, 300, 2048),
+                                             (4, 1, 64, 17, 2048), (8, 8, 64, 200, 2048),
+                                             (16, 4, 128, 70, 100), (32, 8, 128, 8190, 8192)])
 @pytest.mark.parametrize("min_keys", [64, 256])
 def test_attn_decode(cuda, attn_impl, dt, nh, nkv, hd, pos, S, min_keys):
     """Split-K decode attention (split count derived on device from pos) vs f32 attention;
