@@ -281,7 +281,28 @@ def test_conv2d_small_ic(cuda, dt, N, H, W, IC, OC, stride, fused):
     b2 = torch.randn(N, OC, device=cuda) if fused else None
     r = torch.randn(N, OH, OW, OC, device=cuda).to(dt) if fused else None
     y = K.conv2d_nhwc(x, w.permute(0, 2, 3, 1).contiguous(), b, stride=stride, bias2=b2, resid=r)
-    torch.testing.assert_close(y.float(), _ref_conv(x, w, b, stride, 1, False, b2, r), **_tol(dt))
+    ref = _ref_conv(x, w, b, stride, 1, False, b2, r)
+    torch.testing.assert_close(y.float(), ref, **_tol(dt))
+    if not fused:  # planar input and output (UNet conv_in from / conv_out to NCHW)
+        y2 = K.conv2d_nhwc(x.permute(0, 3, 1, 2).contiguous(), w.permute(0, 2, 3, 1).contiguous(),
+                           b, stride=stride, in_nchw=True, out_nchw=True)
+        assert y2.shape == (N, OC, OH, OW)
+        torch.testing.assert_close(y2.float(), ref.permute(0, 3, 1, 2), **_tol(dt))
+
+
+@pytest.mark.parametrize("cfg,splits", [(0, 1), (4, 2), (8, 1)])
+def test_conv2d_out_nchw(cuda, cfg, splits):
+    """conv_out-like (IC 320 -> OC 4) written straight into NCHW planes, incl. split-K."""
+    from cake_amd.ops import hip as K
+    torch.manual_seed(9)
+    dt = torch.float16
+    x = torch.randn(2, 12, 10, 320, device=cuda).to(dt)
+    w = (torch.randn(4, 320, 3, 3, device=cuda) / math.sqrt(320 * 9)).to(dt)
+    b = torch.randn(4, device=cuda).to(dt)
+    y = K.conv2d_nhwc(x, w.permute(0, 2, 3, 1).contiguous(), b, cfg=cfg, splits=splits,
+                      out_nchw=True)
+    torch.testing.assert_close(y.float(), _ref_conv(x, w, b, 1, 1, False).permute(0, 3, 1, 2),
+                               **_tol(dt))
 
 
 @pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
