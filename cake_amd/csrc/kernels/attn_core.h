@@ -138,6 +138,65 @@ __device__ __forceinline__ void attn_prefetch_block(const AttnDecArgs& a, int bl
       stamp[k] = __builtin_amdgcn_s_memtime();                                     \
   } while (0)
 
+// Merge the ns <= 64 split partials of head h (one wave; lane t owns split t's m, l)
+// into the head's output row.  The first round's loads — every split's (m, l) and the
+// o rows of the first kMergeRound splits — are all issued before any is used, so up
+// to kMergeRound splits cost one memory round trip (agent-scope loads go past the
+// XCD's L2: each round trip is a long one).  pw: 64 floats of scratch LDS.
+constexpr int kMergeRound = 16;
+
+template <int DT, int HD>
+__device__ __forceinline__ void attn_merge_head(const AttnDecArgs& a, int h, int ns, int lane,
+                                                float* pw) {
+  constexpr int DPL = HD / 64;  // output dims per lane
+  constexpr int MR = kMergeRound;
+  const float* src = a.part + (size_t)h * kMaxSplit * (HD + 2);
+  const float mt = lane < ns ? ld_sc1(src + lane * (HD + 2)) : -INFINITY;
+  const float lt = lane < ns ? ld_sc1(src + lane * (HD + 2) + 1) : 0.f;
+  float v[MR][DPL];
+#pragma unroll
+  for (int u = 0; u < MR; ++u) {
+    const int t = u < ns ? u : ns - 1;
+    const float* pt = src + t * (HD + 2) + 2 + lane * DPL;
+#pragma unroll
+    for (int d = 0; d < DPL; ++d) v[u][d] = ld_sc1(pt + d);
+  }
+  const float M = wave_max(mt);
+  const float wt = lane < ns ? exp2f(mt - M) : 0.f;
+  const float L = wave_sum(wt * lt);
+  pw[lane] = wt;
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the weights are in LDS
+  __builtin_amdgcn_wave_barrier();
+  float acc[DPL];
+#pragma unroll
+  for (int d = 0; d < DPL; ++d) acc[d] = 0.f;
+#pragma unroll
+  for (int u = 0; u < MR; ++u) {
+    const float w = u < ns ? pw[u] : 0.f;
+#pragma unroll
+    for (int d = 0; d < DPL; ++d) acc[d] = fmaf(w, v[u][d], acc[d]);
+  }
+  for (int t0 = MR; t0 < ns; t0 += MR) {  // ns > 16: further rounds
+#pragma unroll
+    for (int u = 0; u < MR; ++u) {
+      const int t = t0 + u < ns ? t0 + u : ns - 1;
+      const float* pt = src + t * (HD + 2) + 2 + lane * DPL;
+#pragma unroll
+      for (int d = 0; d < DPL; ++d) v[u][d] = ld_sc1(pt + d);
+    }
+#pragma unroll
+    for (int u = 0; u < MR; ++u) {
+      const float w = t0 + u < ns ? pw[t0 + u] : 0.f;
+#pragma unroll
+      for (int d = 0; d < DPL; ++d) acc[d] = fmaf(w, v[u][d], acc[d]);
+    }
+  }
+  const float inv = 1.f / L;
+  uint16_t* dst = a.out + (size_t)h * HD + lane * DPL;
+#pragma unroll
+  for (int d = 0; d < DPL; ++d) dst[d] = from_f32<DT>(acc[d] * inv);
+}
+
 template <int DT, int HD, int NREP>
 __device__ __forceinline__ void attn_decode_block(const AttnDecArgs& a, int g, int s,
                                                   uint16_t* smem) {
@@ -352,42 +411,7 @@ __device__ __forceinline__ void attn_decode_block(const AttnDecArgs& a, int g, i
   if (!last_flag) flush_stamps(7);
   if (!last_flag || wave >= NREP) return;
 
-  // merge the ns <= 64 partials of this wave's head: lane t owns split t's (m, l)
-  const float* src = a.part + (size_t)h * kMaxSplit * (HD + 2);
-  const float mt = lane < ns ? ld_sc1(src + lane * (HD + 2)) : -INFINITY;
-  const float lt = lane < ns ? ld_sc1(src + lane * (HD + 2) + 1) : 0.f;
-  const float M = wave_max(mt);
-  const float wt = lane < ns ? exp2f(mt - M) : 0.f;
-  const float L = wave_sum(wt * lt);
-  float* pw = ps + wave * kChunk;
-  pw[lane] = wt;
-  __builtin_amdgcn_s_waitcnt(0xc07f);
-  __builtin_amdgcn_wave_barrier();
-  float acc[DPL];
-#pragma unroll
-  for (int d = 0; d < DPL; ++d) acc[d] = 0.f;
-  // MR partials' loads in flight per round trip (ns <= 64)
-  constexpr int MR = 8;
-  for (int t0 = 0; t0 < ns; t0 += MR) {
-    float v[MR][DPL];
-#pragma unroll
-    for (int u = 0; u < MR; ++u) {
-      const int t = t0 + u < ns ? t0 + u : ns - 1;
-      const float* pt = src + t * (HD + 2) + 2 + lane * DPL;
-#pragma unroll
-      for (int d = 0; d < DPL; ++d) v[u][d] = ld_sc1(pt + d);
-    }
-#pragma unroll
-    for (int u = 0; u < MR; ++u) {
-      const float w = t0 + u < ns ? pw[t0 + u] : 0.f;
-#pragma unroll
-      for (int d = 0; d < DPL; ++d) acc[d] = fmaf(w, v[u][d], acc[d]);
-    }
-  }
-  const float inv = 1.f / L;
-  uint16_t* dst = a.out + (size_t)h * HD + lane * DPL;
-#pragma unroll
-  for (int d = 0; d < DPL; ++d) dst[d] = from_f32<DT>(acc[d] * inv);
+  attn_merge_head<DT, HD>(a, h, ns, lane, ps + wave * kChunk);
   ATTN_STAMP(7);
   flush_stamps(8);
 }

@@ -292,42 +292,7 @@ __device__ __forceinline__ void attn2_decode_block(const AttnDecArgs& a, int g, 
     }
     return;
   }
-  // merge the ns <= 64 partials of this wave's head: lane t owns split t's (m, l)
-  constexpr int DPL = HD / 64;
-  const int h = g * NREP + wave;
-  const float* src = a.part + (size_t)h * kMaxSplit * (HD + 2);
-  const float mt = lane < ns ? ld_sc1(src + lane * (HD + 2)) : -INFINITY;
-  const float lt = lane < ns ? ld_sc1(src + lane * (HD + 2) + 1) : 0.f;
-  const float M = wave_max(mt);
-  const float wt = lane < ns ? exp2f(mt - M) : 0.f;
-  const float L = wave_sum(wt * lt);
-  pt[lane] = wt;  // (the wave's p tile is free now)
-  __builtin_amdgcn_s_waitcnt(0xc07f);
-  __builtin_amdgcn_wave_barrier();
-  float acc2[DPL];
-#pragma unroll
-  for (int d = 0; d < DPL; ++d) acc2[d] = 0.f;
-  constexpr int MR = 8;
-  for (int t0 = 0; t0 < ns; t0 += MR) {
-    float v[MR][DPL];
-#pragma unroll
-    for (int u = 0; u < MR; ++u) {
-      const int t = t0 + u < ns ? t0 + u : ns - 1;
-      const float* ptp = src + t * (HD + 2) + 2 + lane * DPL;
-#pragma unroll
-      for (int d = 0; d < DPL; ++d) v[u][d] = ld_sc1(ptp + d);
-    }
-#pragma unroll
-    for (int u = 0; u < MR; ++u) {
-      const float w = t0 + u < ns ? pt[t0 + u] : 0.f;
-#pragma unroll
-      for (int d = 0; d < DPL; ++d) acc2[d] = fmaf(w, v[u][d], acc2[d]);
-    }
-  }
-  const float inv = 1.f / L;
-  uint16_t* dst = a.out + (size_t)h * HD + lane * DPL;
-#pragma unroll
-  for (int d = 0; d < DPL; ++d) dst[d] = from_f32<DT>(acc2[d] * inv);
+  attn_merge_head<DT, HD>(a, g * NREP + wave, ns, lane, pt);  // (the wave's p tile is free)
   ATTN_STAMP(7);
   if (a.stamps != nullptr && lane == 0 && wave == 0) {
     unsigned long long* dd = a.stamps + ((size_t)s * gridDim.x + g) * 8;

@@ -35,14 +35,16 @@ def main():
     lib.cake_attn_set_stamps.argtypes = [C.c_void_p]
     lib.cake_attn_set_stamps.restype = C.c_int
     impls = [int(x) for x in os.environ.get("IMPLS", "1,2").split(",")]
-    cases = [(i, int(x)) for i in impls
+    minks = [int(x) for x in os.environ.get("MINKS", "64").split(",")]
+    cases = [(i, mk, int(x)) for i in impls for mk in minks
              for x in os.environ.get("TKS", "57,176,512,1024,2048,4000").split(",")]
-    for impl, Tk in cases:
+    for impl, mk, Tk in cases:
         K.attn_set_impl(impl)
+        K.attn_set_min_keys(mk)
         pos.fill_(Tk - 1)
         need = K.attn_splits(Tk)
         cap = next(c for c in (8, 16, 32, 64) if c >= need) if need <= 64 else 64
-        rec = {"impl": impl, "Tk": Tk, "cap": cap, "splits": need}
+        rec = {"impl": impl, "min_keys": mk, "Tk": Tk, "cap": cap, "splits": need}
         with K.attn_split_cap(cap):
             # plain timing: events around each launch after a streaming read
             ts = []
