@@ -16,12 +16,19 @@ step() {  # name timeout cmd...
   if [[ $rc -eq 1 && $name == pytest* ]]; then grep -E "^FAILED|passed|failed" "gpurun_out/$name.log" | tail -8; return 0; fi
   if [[ $rc -ne 0 ]]; then echo "$name rc=$rc -> stop"; exit $rc; fi
 }
-if [[ ${DO_TESTS:-1} == 1 ]]; then
+if [[ ${DO_TESTS:-1} == 1 || ${DO_SDRCCL:-0} == 1 ]]; then
   step pytest_sdrccl 500 python -u -m pytest tests/test_sd_rccl_gpu.py -v -m gpu --timeout 420 --timeout-method thread
+fi
+if [[ ${DO_TESTS:-1} == 1 ]]; then
   step pytest 600 python -u -m pytest ${TESTS:-tests} -q -m gpu --timeout 120 --timeout-method thread --ignore=tests/test_sd_rccl_gpu.py
 fi
 [[ ${DO_BENCH:-1} == 1 ]] && step bench 400 python bench.py ${BENCH_ARGS:-}
-[[ ${DO_STAMPS:-0} == 1 ]] && step attn_stamps 120 python scripts/attn_stamps.py
+[[ ${DO_STAMPS:-0} == 1 ]] && step attn_stamps 240 env MINKS=${MINKS:-64} TKS=${TKS:-57,176,512,1024,2048,4000} python scripts/attn_stamps.py
+if [[ ${DO_AB2:-0} == 1 ]]; then  # attention core 2 after the one-round merge
+  step ab2_impl2 200 env CAKE_ATTN_IMPL=2 python bench.py --no-extras
+  step ab2_p2048_impl2 200 env CAKE_ATTN_IMPL=2 python bench.py --no-extras --prompt-len 2048
+  step ab2_p2048_impl1 200 env CAKE_ATTN_IMPL=1 python bench.py --no-extras --prompt-len 2048
+fi
 if [[ ${DO_AB:-0} == 1 ]]; then  # decode A/B: attention core, MALL prefetch, long context
   step ab_base 200 python bench.py --no-extras
   step ab_impl2 200 env CAKE_ATTN_IMPL=2 python bench.py --no-extras
