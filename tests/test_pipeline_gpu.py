@@ -57,3 +57,8 @@ def test_pipeline_ipc_hops_in_graph_match_single(cuda, tmp_path):
     assert m4["hop"] == "ipc" and pp4[0] == single[0] and len(pp4) == 2
     m5, pp5 = _bench(tmp_path, 2, 1, "ipc2bf", hop="ipc", hop_dtype="bf16")
     assert m5["hop"] == "ipc-bf16" and len(pp5[0]) == len(single[0])
+    # bf16 payloads round the residual stream once per hop (~2^-8 relative), so greedy
+    # tokens may part from the f32 run at a near-tie late in the sequence; a corrupted or
+    # misrouted hop changes them from the first token on.  Fixed seed: deterministic.
+    agree = next((i for i, (a, b) in enumerate(zip(pp5[0], single[0])) if a != b), len(single[0]))
+    assert agree >= min(8, len(single[0])), (agree, pp5[0], single[0])
