@@ -33,7 +33,8 @@ import torch.distributed as dist
 
 log = logging.getLogger("cake.sd.rccl")
 
-_DT = {"float32": torch.float32, "float16": torch.float16, "bfloat16": torch.bfloat16,
+_DT = {"float32": torch.float32, "float64": torch.float64, "float16": torch.float16,
+       "bfloat16": torch.bfloat16,
        "int32": torch.int32, "int64": torch.int64, "uint8": torch.uint8}
 
 
