@@ -29,12 +29,6 @@ template <int DT, int HD, int NREP>
 __global__ __launch_bounds__(AttnGeom<NREP>::NT) void attn_decode_kernel(AttnDecArgs a) {
   // one LDS array (LDS-DMA pipelines need it: MI355X guide, GEMM item 4a)
   __shared__ __attribute__((aligned(16))) uint16_t smem[attn_smem_elems<HD, NREP>()];
-  if ((int)blockIdx.y >= a.maxsplit) {  // prefetch rows of the grid
-    attn_prefetch_block<AttnGeom<NREP>::NT>(
-        a, (blockIdx.y - a.maxsplit) * gridDim.x + blockIdx.x,
-        (gridDim.y - a.maxsplit) * gridDim.x);
-    return;
-  }
   attn_decode_block<DT, HD, NREP>(a, blockIdx.x, blockIdx.y, smem);
 }
 
@@ -42,12 +36,6 @@ template <int DT, int HD, int NREP>
 __global__ __launch_bounds__(AttnGeom<NREP>::NT) void attn2_decode_kernel(AttnDecArgs a) {
   __shared__ __attribute__((aligned(16)))
       float lds[attn2_smem_floats<HD, NREP, AttnGeom<NREP>::NW>()];
-  if ((int)blockIdx.y >= a.maxsplit) {  // prefetch rows of the grid
-    attn_prefetch_block<AttnGeom<NREP>::NT>(
-        a, (blockIdx.y - a.maxsplit) * gridDim.x + blockIdx.x,
-        (gridDim.y - a.maxsplit) * gridDim.x);
-    return;
-  }
   attn2_decode_block<DT, HD, NREP>(a, blockIdx.x, blockIdx.y, lds);
 }
 
@@ -55,8 +43,10 @@ __global__ __launch_bounds__(AttnGeom<NREP>::NT) void attn2_decode_kernel(AttnDe
 
 using namespace cake;
 
-// 1 = LDS-staged chunk core (attn_core.h), 2 = wave-stream MFMA core (attn_core2.h)
-static int g_attn_impl = 1;
+// 1 = LDS-staged chunk core (attn_core.h), 2 = wave-stream MFMA core (attn_core2.h).
+// Core 2 is the default: equal at short context, 2 % more tok/s at a 2048-token one
+// (profiles/r3_decode_ab.jsonl).
+static int g_attn_impl = 2;
 CAKE_API int cake_attn_set_impl(int impl) {
   if (impl != 1 && impl != 2) return (int)hipErrorInvalidValue;
   g_attn_impl = impl;
@@ -95,15 +85,6 @@ CAKE_API int cake_attn_set_split_cap(int cap) {
   return 0;
 }
 
-// Workgroups (in rows of nkv) that prefetch the next kernel's weights while the
-// attention runs (0 = off; the prefetch pointer is passed per launch).
-static int g_attn_pf_rows = 24;
-CAKE_API int cake_attn_set_prefetch_rows(int rows) {
-  if (rows < 0 || rows > 256) return (int)hipErrorInvalidValue;
-  g_attn_pf_rows = rows;
-  return 0;
-}
-
 CAKE_API int cake_attn_set_min_keys(int min_keys) {
   if (min_keys < kChunk || min_keys % kChunk) return (int)hipErrorInvalidValue;
   g_attn_min_keys = min_keys;
@@ -128,27 +109,16 @@ static int launch_decode(int n_rep, dim3 grid, hipStream_t st, const AttnDecArgs
   return (int)hipGetLastError();
 }
 
-CAKE_API int cake_attn_decode_pf(int dt, const float* q, const void* kc, const void* vc,
-                                 const int* pos, int S, int nh, int nkv, int hd, float scale,
-                                 float* part, unsigned int* tickets, void* out,
-                                 const void* pf, long long pf_bytes, hipStream_t st) {
-  if (nkv <= 0 || nh % nkv || S <= 0 || pf_bytes < 0 || (pf && (uintptr_t)pf % 16))
-    return (int)hipErrorInvalidValue;
-  const int ms = attn_max_split(S);
-  const int splits = g_attn_split_cap > 0 && g_attn_split_cap < ms ? g_attn_split_cap : ms;
-  const bool prefetch = pf != nullptr && pf_bytes >= 16 && g_attn_pf_rows > 0;
-  const dim3 grid(nkv, splits + (prefetch ? g_attn_pf_rows : 0));
-  const AttnDecArgs a{q, (const uint16_t*)kc, (const uint16_t*)vc, pos, S,
-                      scale * 1.4426950408889634f, part, tickets, (uint16_t*)out,
-                      g_attn_min_keys, splits, g_attn_stamps,
-                      prefetch ? (const uint4*)pf : nullptr, prefetch ? pf_bytes / 16 : 0};
-  DISPATCH_DT_HD(dt, hd, return (launch_decode<DT, HD>(nh / nkv, grid, st, a)));
-  return (int)hipErrorInvalidValue;
-}
-
 CAKE_API int cake_attn_decode(int dt, const float* q, const void* kc, const void* vc,
                               const int* pos, int S, int nh, int nkv, int hd, float scale,
                               float* part, unsigned int* tickets, void* out, hipStream_t st) {
-  return cake_attn_decode_pf(dt, q, kc, vc, pos, S, nh, nkv, hd, scale, part, tickets, out,
-                             nullptr, 0, st);
+  if (nkv <= 0 || nh % nkv || S <= 0) return (int)hipErrorInvalidValue;
+  const int ms = attn_max_split(S);
+  const int splits = g_attn_split_cap > 0 && g_attn_split_cap < ms ? g_attn_split_cap : ms;
+  const dim3 grid(nkv, splits);
+  const AttnDecArgs a{q, (const uint16_t*)kc, (const uint16_t*)vc, pos, S,
+                      scale * 1.4426950408889634f, part, tickets, (uint16_t*)out,
+                      g_attn_min_keys, splits, g_attn_stamps};
+  DISPATCH_DT_HD(dt, hd, return (launch_decode<DT, HD>(nh / nkv, grid, st, a)));
+  return (int)hipErrorInvalidValue;
 }

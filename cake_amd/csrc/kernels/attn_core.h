@@ -102,33 +102,7 @@ struct AttnDecArgs {
   uint16_t* out;           // [nh*hd]
   int min_keys, maxsplit;
   unsigned long long* stamps;  // diagnostics (nullptr in production): per-WG phase clocks
-  const uint4* pf;             // MALL prefetch: the next kernel's weights (or nullptr)
-  long long pf_vec;            // their size in 16-byte vectors
 };
-
-// Prefetch role (workgroups past the attention grid): stream [pf, pf + pf_vec) once so
-// the bytes sit in the memory-side Infinity Cache when the next kernel (o_proj) reads
-// them.  Attention itself is latency-bound and leaves HBM idle for several µs; these
-// loads use that window.  Each workgroup reads one contiguous slice, 8 vectors per
-// thread in flight; the loaded words are folded and kept alive by an empty asm use.
-template <int NT>
-__device__ __forceinline__ void attn_prefetch_block(const AttnDecArgs& a, int blk, int nblk) {
-  const long long per = (a.pf_vec + nblk - 1) / nblk;
-  const long long lo = (long long)blk * per;
-  const long long hi = lo + per < a.pf_vec ? lo + per : a.pf_vec;
-  uint32_t acc = 0;
-  for (long long i = lo + threadIdx.x; i < hi; i += (long long)NT * 8) {
-    uint4 v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const long long j = i + (long long)u * NT;
-      v[u] = j < hi ? a.pf[j] : make_uint4(0u, 0u, 0u, 0u);
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) acc ^= v[u].x ^ v[u].w;
-  }
-  asm volatile("" ::"v"(acc));
-}
 
 // Phase clock of workgroup (g, s) for the latency breakdown (scripts/attn_stamps.py):
 // slot k of 8, shader-clock ticks (s_memtime) from thread 0.

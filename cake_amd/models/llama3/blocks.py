@@ -165,7 +165,7 @@ class LayerStack:
             K.qkv_rope(bufs.resid, w.ln1, cfg.rms_norm_eps, w.wq, w.wk, w.wv, self.inv_freq,
                        bufs.pos, bufs.q, kc, vc)
             K.attn_decode(bufs.q, kc, vc, bufs.pos, self.scale, bufs.part, bufs.tickets,
-                          bufs.attn_out, prefetch=w.wo)
+                          bufs.attn_out)
             K.gemv(bufs.attn_out, w.wo, bufs.resid, accumulate=True)
             K.swiglu(bufs.resid, w.ln2, cfg.rms_norm_eps, w.wg, w.wu, bufs.act)
             K.gemv(bufs.act, w.wd, bufs.resid, accumulate=True)

@@ -30,8 +30,6 @@ _SIGS = {
     "cake_gemv_x16": [I, P, P, I, I, P, I, P],
     "cake_gemv_norm_f32": [I, P, P, F, P, I, I, P, P],
     "cake_attn_decode": [I, P, P, P, P, I, I, I, I, F, P, P, P, P],
-    "cake_attn_decode_pf": [I, P, P, P, P, I, I, I, I, F, P, P, P, P, C.c_longlong, P],
-    "cake_attn_set_prefetch_rows": [I],
     "cake_attn_set_impl": [I],
     "cake_attn_set_min_keys": [I],
     "cake_attn_set_split_cap": [I],

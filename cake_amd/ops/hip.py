@@ -114,15 +114,13 @@ def norm_gemv_f32(resid, norm_w, eps, w, out):
                                        _p(out), _stream()), "gemv_norm_f32")
 
 
-def attn_decode(q, kcache, vcache, pos, scale, part, tickets, out, prefetch=None):
+def attn_decode(q, kcache, vcache, pos, scale, part, tickets, out):
     """Split-K GQA decode attention for the token at device position `pos`.
 
     The split count is derived on the device from the live length, so one
     captured launch serves every position.  part: f32 workspace
     (:func:`attn_workspace_numel`); tickets: int32 [nkv], zero-initialised once
-    and re-armed by the kernel itself.  prefetch: a device tensor (the next
-    kernel's weights) that extra workgroups of the launch stream into the
-    Infinity Cache while the latency-bound attention leaves HBM idle.
+    and re-armed by the kernel itself.
     """
     nkv, S, hd = kcache.shape
     nh = q.numel() // hd
@@ -135,30 +133,12 @@ def attn_decode(q, kcache, vcache, pos, scale, part, tickets, out, prefetch=None
     _req(tickets, "tickets", dtype=torch.int32, numel=nkv)
     if hd not in (64, 128) or nh % nkv or (nh // nkv) not in (1, 2, 4, 8):
         raise ValueError(f"unsupported attention shape nh={nh} nkv={nkv} hd={hd}")
-    pf, pfb = None, 0
     if not _ATTN_IMPL_SET[0]:  # CAKE_ATTN_IMPL, applied once
         attn_set_impl(_ATTN_IMPL[0])
-    if _PF_ROWS_ENV[0] is not None:  # sweep override (CAKE_ATTN_PF_ROWS), applied once
-        attn_set_prefetch_rows(int(_PF_ROWS_ENV[0]))
-        _PF_ROWS_ENV[0] = None
-    if prefetch is not None and _PF_ON[0]:
-        if not (prefetch.is_cuda and prefetch.is_contiguous() and prefetch.data_ptr() % 16 == 0):
-            raise ValueError("prefetch: contiguous 16-byte aligned device tensor expected")
-        pf, pfb = _p(prefetch), prefetch.numel() * prefetch.element_size()
-    check(kernels().cake_attn_decode_pf(_dt(kcache), _p(q), _p(kcache), _p(vcache), _p(pos), S,
-                                        nh, nkv, hd, float(scale), _p(part), _p(tickets),
-                                        _p(out), pf, pfb, _stream()),
+    check(kernels().cake_attn_decode(_dt(kcache), _p(q), _p(kcache), _p(vcache), _p(pos), S,
+                                     nh, nkv, hd, float(scale), _p(part), _p(tickets),
+                                     _p(out), _stream()),
           "attn_decode")
-
-
-# off by default until it measures faster (profiles/r3_decode_ab.jsonl)
-_PF_ON = [os.environ.get("CAKE_ATTN_PREFETCH", "0") != "0"]
-_PF_ROWS_ENV = [os.environ.get("CAKE_ATTN_PF_ROWS")]
-
-
-def attn_set_prefetch_rows(rows: int) -> None:
-    """Workgroup rows (x nkv) of the attention launch's weight prefetch (0 = off)."""
-    check(kernels().cake_attn_set_prefetch_rows(int(rows)), "attn_set_prefetch_rows")
 
 
 def attn_workspace_numel(nh: int, hd: int, S: int) -> int:
@@ -194,7 +174,7 @@ def attn_splits(Tk: int) -> int:
     return -(-Tk // keys)
 
 
-_ATTN_IMPL = [int(os.environ.get("CAKE_ATTN_IMPL", "1"))]
+_ATTN_IMPL = [int(os.environ.get("CAKE_ATTN_IMPL", "2"))]
 _ATTN_IMPL_SET = [False]
 
 

@@ -606,7 +606,7 @@ class TPEngine:
             K.qkv_rope(b.resid, w.ln1, eps, w.wq, w.wk, w.wv, self.inv_freq, b.pos, b.q,
                        self.kc[s], self.vc[s])
             K.attn_decode(b.q, self.kc[s], self.vc[s], b.pos, self.scale, b.part, b.tickets,
-                          b.attn_out, prefetch=w.wo)
+                          b.attn_out)
             K.gemv(b.attn_out, w.wo, b.partial, accumulate=False)
             comm.sum_(b.partial, b.resid, accumulate=True)
             K.swiglu(b.resid, w.ln2, eps, w.wg, w.wu, b.act)

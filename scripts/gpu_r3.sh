@@ -29,12 +29,9 @@ if [[ ${DO_AB2:-0} == 1 ]]; then  # attention core 2 after the one-round merge
   step ab2_p2048_impl2 200 env CAKE_ATTN_IMPL=2 python bench.py --no-extras --prompt-len 2048
   step ab2_p2048_impl1 200 env CAKE_ATTN_IMPL=1 python bench.py --no-extras --prompt-len 2048
 fi
-if [[ ${DO_AB:-0} == 1 ]]; then  # decode A/B: attention core, MALL prefetch, long context
+if [[ ${DO_AB:-0} == 1 ]]; then  # decode A/B: attention core, long context
   step ab_base 200 python bench.py --no-extras
   step ab_impl2 200 env CAKE_ATTN_IMPL=2 python bench.py --no-extras
-  step ab_pf 200 env CAKE_ATTN_PREFETCH=1 python bench.py --no-extras
-  step ab_pf8 200 env CAKE_ATTN_PREFETCH=1 CAKE_ATTN_PF_ROWS=8 python bench.py --no-extras
-  step ab_70b_pf 300 env CAKE_ATTN_PREFETCH=1 python bench.py --no-extras --model llama3-70b --steps 32
   step ab_p2048_impl1 200 env CAKE_ATTN_IMPL=1 python bench.py --no-extras --prompt-len 2048
   step ab_p2048_impl2 200 env CAKE_ATTN_IMPL=2 python bench.py --no-extras --prompt-len 2048
 fi

@@ -147,18 +147,30 @@ def test_sd_layout_ops_nhwc_matches_nchw():
     assert math.isclose(float(padded[..., -1, :].abs().sum()), 0.0)
 
 
-def test_attention_split_policy_and_buckets():
+@pytest.mark.parametrize("impl", [1, 2])
+def test_attention_split_policy_and_buckets(impl):
     """Host mirror of the decode-attention split policy (ops.hip.attn_splits, used to pick
-    a position-bucket graph): at most 64 splits, never more than a max_seq grid holds,
-    and the 8/16/32/64 buckets cover 512 / 2048 / 4096 / any keys.  (Not monotone: past
-    1024 keys a split takes two chunks, so 1025 keys use 9 splits where 1024 use 16.)"""
+    a position-bucket graph) for both cores: at most 64 splits, never more than a max_seq
+    grid holds, and the 8/16/32/64 buckets cover the live lengths the policy maps to them.
+    Core 1 is not monotone: past 1024 keys a split takes two chunks, so 1025 keys use 9
+    splits where 1024 use 16.  Core 2 splits in 16-key blocks, >= 64 keys per split."""
     from cake_amd.ops import hip as K
-    for tk in range(1, 20000, 7):
-        n = K.attn_splits(tk)
-        assert 1 <= n <= 64
-        assert n <= K.attn_max_split(tk)
-    assert K.attn_splits(1024) == 16 and K.attn_splits(1025) == 9
-    assert max(K.attn_splits(t) for t in range(1, 513)) <= 8
-    assert max(K.attn_splits(t) for t in range(1, 2049)) <= 16
-    assert max(K.attn_splits(t) for t in range(1, 4097)) <= 32
+    saved = K._ATTN_IMPL[0]
+    K._ATTN_IMPL[0] = impl
+    try:
+        for tk in range(1, 20000, 7):
+            n = K.attn_splits(tk)
+            assert 1 <= n <= 64
+            assert n <= K.attn_max_split(tk)
+        assert max(K.attn_splits(t) for t in range(1, 513)) <= 8
+        if impl == 1:
+            assert K.attn_splits(1024) == 16 and K.attn_splits(1025) == 9
+            assert max(K.attn_splits(t) for t in range(1, 2049)) <= 16
+            assert max(K.attn_splits(t) for t in range(1, 4097)) <= 32
+        else:
+            assert K.attn_splits(64) == 1 and K.attn_splits(65) == 2
+            assert K.attn_splits(1024) == 16 and K.attn_splits(4096) == 64
+            assert max(K.attn_splits(t) for t in range(1, 2049)) <= 32
+    finally:
+        K._ATTN_IMPL[0] = saved
     assert K.attn_max_split(4096) == 64 and K.attn_max_split(100) == 2
