@@ -24,6 +24,9 @@ namespace cake {
 
 // Grid (nkv, maxsplit): see attn_core.h for the split / chunk / combine scheme.
 static int g_attn_min_keys = 64;  // min keys per split (tunable)
+// core 2: number of splits aimed at past target * min_keys keys (fewer, longer splits
+// trade loop time for a cheaper ticket + merge tail; tunable)
+static int g_attn_target = 64;
 
 template <int DT, int HD, int NREP>
 __global__ __launch_bounds__(AttnGeom<NREP>::NT) void attn_decode_kernel(AttnDecArgs a) {
@@ -85,6 +88,12 @@ CAKE_API int cake_attn_set_split_cap(int cap) {
   return 0;
 }
 
+CAKE_API int cake_attn_set_target_splits(int target) {
+  if (target < 1 || target > kMaxSplit) return (int)hipErrorInvalidValue;
+  g_attn_target = target;
+  return 0;
+}
+
 CAKE_API int cake_attn_set_min_keys(int min_keys) {
   if (min_keys < kChunk || min_keys % kChunk) return (int)hipErrorInvalidValue;
   g_attn_min_keys = min_keys;
@@ -118,7 +127,7 @@ CAKE_API int cake_attn_decode(int dt, const float* q, const void* kc, const void
   const dim3 grid(nkv, splits);
   const AttnDecArgs a{q, (const uint16_t*)kc, (const uint16_t*)vc, pos, S,
                       scale * 1.4426950408889634f, part, tickets, (uint16_t*)out,
-                      g_attn_min_keys, splits, g_attn_stamps};
+                      g_attn_min_keys, splits, g_attn_stamps, g_attn_target};
   DISPATCH_DT_HD(dt, hd, return (launch_decode<DT, HD>(nh / nkv, grid, st, a)));
   return (int)hipErrorInvalidValue;
 }

@@ -102,6 +102,7 @@ struct AttnDecArgs {
   uint16_t* out;           // [nh*hd]
   int min_keys, maxsplit;
   unsigned long long* stamps;  // diagnostics (nullptr in production): per-WG phase clocks
+  int target;                  // core 2: splits aimed at (keys per split = Tk / target)
 };
 
 // Phase clock of workgroup (g, s) for the latency breakdown (scripts/attn_stamps.py):

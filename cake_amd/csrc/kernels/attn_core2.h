@@ -49,9 +49,9 @@ constexpr int attn2_smem_floats() {
 }
 
 // host/device split policy of the v2 core (mirrored by ops.hip.attn_splits)
-__device__ __forceinline__ void attn2_splits(int Tk, int min_keys, int maxsplit, int& ns,
-                                             int& kps) {
-  int keys = (Tk + kMaxSplit - 1) / kMaxSplit;
+__device__ __forceinline__ void attn2_splits(int Tk, int min_keys, int maxsplit, int target,
+                                             int& ns, int& kps) {
+  int keys = (Tk + target - 1) / target;
   keys = (keys + kBlk - 1) / kBlk * kBlk;
   if (keys < min_keys) keys = min_keys;
   ns = (Tk + keys - 1) / keys;
@@ -127,7 +127,7 @@ __device__ __forceinline__ void attn2_decode_block(const AttnDecArgs& a, int g, 
   const int Tk = *a.pos + 1;
   ATTN_STAMP(1);
   int ns, kps;
-  attn2_splits(Tk, a.min_keys, a.maxsplit, ns, kps);
+  attn2_splits(Tk, a.min_keys, a.maxsplit, a.target, ns, kps);
   if (s >= ns) return;
   const int kb = s * kps, ke = min(Tk, kb + kps);
   const int nblk = (ke - kb + kBlk - 1) / kBlk;

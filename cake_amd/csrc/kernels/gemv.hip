@@ -408,11 +408,34 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_x16_kernel(
   run_pairs<DT, false, U, PFC>(map, epi, xs, K, npairs, p0, gridDim.x * kGemvWaves, pre);
 }
 
-// RMSNorm(f32 row) then f32 output: the lm_head.
-template <int DT, int U, int PFC, int NX>
+// Greedy token selection fused into the lm_head (SEL): repeat penalty on the logits of
+// the last `last_n` history tokens, argmax (ties -> smallest index), and the step
+// finalizer (tok, history, pos) — what repeat_penalty_kernel + argmax_kernel +
+// finalize_kernel (sampling.hip) do in three more launches after the lm_head.
+struct HeadSel {
+  const int* hist;         // token history [max_hist]
+  const int* hist_len;     // device scalar
+  int last_n;              // <= 256 (4 window tokens per lane)
+  float penalty;           // 1 = none
+  unsigned long long* slot;  // best key (ordered(logit) << 32 | ~index), 0 between launches
+  unsigned int* ticket;      // finished workgroups, 0 between launches
+  int* tok;                // next input token
+  int* hist_w;             // history (written by the last workgroup)
+  int* hist_len_w;
+  int* pos;
+  int max_hist;
+};
+
+__device__ __forceinline__ unsigned int ordered_key(float f) {
+  const unsigned int u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+// RMSNorm(f32 row) then f32 output: the lm_head (SEL: + greedy selection, see HeadSel).
+template <int DT, int U, int PFC, int NX, bool SEL>
 __global__ __launch_bounds__(kGemvThreads) void gemv_norm_f32_kernel(
     const float* __restrict__ resid, const uint16_t* __restrict__ norm_w, float eps,
-    const uint16_t* __restrict__ w, int K, int N, float* __restrict__ out) {
+    const uint16_t* __restrict__ w, int K, int N, float* __restrict__ out, HeadSel hs) {
   extern __shared__ float xs[];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int npairs = (N + 1) >> 1;
@@ -421,6 +444,11 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_norm_f32_kernel(
     wa = w + (size_t)(2 * p) * K;
     wb = w + (size_t)min(2 * p + 1, N - 1) * K;
   };
+  // SEL: the history length is requested ahead of the x prologue (one load in front of
+  // it), the window itself after it (queued behind the first weight rows; first needed
+  // by the first pair's epilogue)
+  int hlen = 0;
+  if constexpr (SEL) hlen = hs.penalty != 1.f ? *hs.hist_len : 0;
   Regs<PFC> pre;
   NormPre<DT, NX> xp;
   const uint16_t *wa0, *wb0;
@@ -431,12 +459,71 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_norm_f32_kernel(
   __builtin_amdgcn_sched_barrier(0);
   if constexpr (NX > 0) xp.finish(eps, K, xs);
   else stage_rmsnorm<DT>(resid, norm_w, eps, K, xs);
+  int win[4] = {-1, -1, -1, -1};
+  if constexpr (SEL) {
+    const int n = min(hs.last_n, hlen), start = hlen - n;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (j * 64 + lane < n) win[j] = hs.hist[start + j * 64 + lane];
+  }
+  unsigned long long best = 0ull;
   auto epi = [&](int p, float da, float db) {
+    const int ra = 2 * p, rb = 2 * p + 1;
+    if constexpr (SEL) {
+      // penalty: the row is one of the window's tokens (each token once, like the
+      // unique-token loop of repeat_penalty_kernel)
+      if (hs.penalty != 1.f) {
+        const bool ia = win[0] == ra || win[1] == ra || win[2] == ra || win[3] == ra;
+        const bool ib = win[0] == rb || win[1] == rb || win[2] == rb || win[3] == rb;
+        if (__builtin_amdgcn_ballot_w64(ia) != 0ull) da = da >= 0.f ? da / hs.penalty : da * hs.penalty;
+        if (__builtin_amdgcn_ballot_w64(ib) != 0ull) db = db >= 0.f ? db / hs.penalty : db * hs.penalty;
+      }
+      const unsigned long long ka =
+          ((unsigned long long)ordered_key(da) << 32) | (0xffffffffu - (unsigned int)ra);
+      best = ka > best ? ka : best;
+      if (rb < N) {
+        const unsigned long long kb =
+            ((unsigned long long)ordered_key(db) << 32) | (0xffffffffu - (unsigned int)rb);
+        best = kb > best ? kb : best;
+      }
+    }
     if (lane != 0) return;
-    out[2 * p] = da;
-    if (2 * p + 1 < N) out[2 * p + 1] = db;
+    out[ra] = da;
+    if (rb < N) out[rb] = db;
   };
   run_pairs<DT, true, U, PFC>(map, epi, xs, K, npairs, p0, gridDim.x * kGemvWaves, pre);
+  if constexpr (SEL) {
+    // block max -> one returning 8-byte device atomic on the slot, drained before the
+    // ticket (atomics on both sides: the last workgroup reads the slot atomically)
+    __shared__ unsigned long long red[kGemvWaves];
+    __shared__ int is_last;
+    if (lane == 0) red[wave] = best;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned long long b = red[0];
+#pragma unroll
+      for (int i = 1; i < kGemvWaves; ++i) b = red[i] > b ? red[i] : b;
+      const unsigned long long old =
+          __hip_atomic_fetch_max(hs.slot, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::"v"((unsigned int)old) : "memory");
+      const unsigned int t =
+          __hip_atomic_fetch_add(hs.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      is_last = t == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (is_last && threadIdx.x == 0) {
+      const unsigned long long key =
+          __hip_atomic_fetch_max(hs.slot, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int t = (int)(0xffffffffu - (unsigned int)(key & 0xffffffffull));
+      *hs.tok = t;
+      const int len = *hs.hist_len_w;
+      if (len < hs.max_hist) { hs.hist_w[len] = t; *hs.hist_len_w = len + 1; }
+      *hs.pos += 1;
+      // re-arm for the next launch (the kernel boundary orders these for it)
+      __hip_atomic_store(hs.slot, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(hs.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
 // Launch geometry per kernel kind (tunable at run time; defaults from the
@@ -559,16 +646,36 @@ CAKE_API int cake_gemv_x16(int dt, const void* x, const void* w, int K, int N, f
   return (int)hipGetLastError();
 }
 
-CAKE_API int cake_gemv_norm_f32(int dt, const float* resid, const void* norm_w, float eps,
-                                const void* w, int K, int N, float* out, hipStream_t st) {
+template <bool SEL>
+static int launch_norm_f32(int dt, const float* resid, const void* norm_w, float eps,
+                           const void* w, int K, int N, float* out, const HeadSel& hs,
+                           hipStream_t st) {
   if (K % 8) return (int)hipErrorInvalidValue;
   const size_t lds = (size_t)K * sizeof(float);
   const GemvTune t = g_tune[kNormF32];
-  DISPATCH_DT(dt, DISPATCH_TUNE(t, K, CAKE_NX_NORM(K, hipLaunchKernelGGL((gemv_norm_f32_kernel<DT, U, PF, NX>),
+  DISPATCH_DT(dt, DISPATCH_TUNE(t, K, CAKE_NX_NORM(K, hipLaunchKernelGGL((gemv_norm_f32_kernel<DT, U, PF, NX, SEL>),
                                                       dim3(grid_for((N + 1) / 2, t.MB)),
                                                       dim3(kGemvThreads), lds, st, resid,
                                                       (const uint16_t*)norm_w, eps,
-                                                      (const uint16_t*)w, K, N, out))));
+                                                      (const uint16_t*)w, K, N, out, hs))));
   return (int)hipGetLastError();
 }
 
+CAKE_API int cake_gemv_norm_f32(int dt, const float* resid, const void* norm_w, float eps,
+                                const void* w, int K, int N, float* out, hipStream_t st) {
+  return launch_norm_f32<false>(dt, resid, norm_w, eps, w, K, N, out, HeadSel{}, st);
+}
+
+// lm_head + repeat penalty + argmax + step finalizer in one launch (greedy decode).
+// slot (u64) and ticket (u32) must be zero before the first launch; the kernel re-arms
+// them.  last_n <= 256.
+CAKE_API int cake_head_select(int dt, const float* resid, const void* norm_w, float eps,
+                              const void* w, int K, int N, float* out, int* hist, int* hist_len,
+                              int last_n, float penalty, unsigned long long* slot,
+                              unsigned int* ticket, int* tok, int* pos, int max_hist,
+                              hipStream_t st) {
+  if (last_n < 0 || last_n > 256 || !(penalty > 0.f) || slot == nullptr || ticket == nullptr)
+    return (int)hipErrorInvalidValue;
+  const HeadSel hs{hist, hist_len, last_n, penalty, slot, ticket, tok, hist, hist_len, pos, max_hist};
+  return launch_norm_f32<true>(dt, resid, norm_w, eps, w, K, N, out, hs, st);
+}

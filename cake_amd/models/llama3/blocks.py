@@ -65,6 +65,7 @@ class DecodeBuffers:
             self.hist_len = torch.zeros(1, device=device, dtype=i32)
             self.slot = torch.zeros(1, device=device, dtype=torch.int64)
             self.thr = torch.zeros(1, device=device, dtype=torch.int32)  # top-k/p threshold
+            self.sel_ticket = torch.zeros(1, device=device, dtype=i32)  # fused head_select
 
 
 class LayerStack:

@@ -14,6 +14,8 @@ one step behind the GPU.
 """
 from __future__ import annotations
 
+import os
+
 from dataclasses import dataclass, field
 
 import torch
@@ -159,6 +161,8 @@ class DeviceDecoder:
         self.graphs: dict[int, torch.cuda.CUDAGraph] = {}
         self.host_pos = 0  # device position of the next step (tracked on the host)
         self._layers = list(range(model.cfg.num_hidden_layers))
+        # CAKE_FUSED_HEAD=0 keeps the four-launch tail (A/B)
+        self._fuse_tail = os.environ.get("CAKE_FUSED_HEAD", "1") != "0"
 
     # the captured body
     def _step_body(self) -> None:
@@ -166,12 +170,24 @@ class DeviceDecoder:
         b, m = self.bufs, self.m
         K.embed(m.head.embed, b.tok, b.resid)
         m.stack.decode_step(b, self._layers, m.session)
+        if self._fused_select():
+            # greedy: lm_head + penalty + argmax + finalize in one launch
+            K.head_select(b.resid, m.head.norm, m.cfg.rms_norm_eps, m.head.lm_head, b.logits,
+                          b.hist, b.hist_len, self.last_n if self.penalty != 1.0 else 0,
+                          self.penalty, b.slot, b.sel_ticket, b.tok, b.pos)
+            return
         K.norm_gemv_f32(b.resid, m.head.norm, m.cfg.rms_norm_eps, m.head.lm_head, b.logits)
         if self.penalty != 1.0:
             K.repeat_penalty(b.logits, b.hist, b.hist_len, self.last_n, self.penalty)
         if self.greedy:
             K.select_token(b.logits, b.slot, b.hist, b.hist_len, b.tok, b.pos, self.sampling,
                            b.thr, params=self.params)
+
+    def _fused_select(self) -> bool:
+        """Greedy argmax with no device parameter block: the fused head_select tail."""
+        from ...ops import hip as K
+        return (self.greedy and self.sampling is None and self.params is None
+                and self.last_n <= K.HEAD_SELECT_MAX_LAST_N and self._fuse_tail)
 
     def set_sampling(self, sampling) -> None:
         """Per-request sampling configuration (None / temperature <= 0 = greedy).  The

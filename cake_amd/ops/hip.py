@@ -114,6 +114,32 @@ def norm_gemv_f32(resid, norm_w, eps, w, out):
                                        _p(out), _stream()), "gemv_norm_f32")
 
 
+HEAD_SELECT_MAX_LAST_N = 256
+
+
+def head_select(resid, norm_w, eps, w, logits, hist, hist_len, last_n: int, penalty: float,
+                slot, ticket, tok, pos) -> None:
+    """Greedy decode tail in ONE launch (gemv.hip cake_head_select): logits = lm_head(
+    rmsnorm(resid)), repeat penalty over the last `last_n` (<= 256) history tokens, argmax
+    (ties -> smallest id), then tok / history / pos advanced as finalize_token does.
+    slot (int64[1]) and ticket (int32[1]) start at zero; the kernel re-arms them."""
+    N, K = w.shape
+    _req(resid, "resid", dtype=torch.float32, numel=K)
+    _req(norm_w, "norm_w", dtype=w.dtype, shape=(K,))
+    _req(w, "w")
+    _req(logits, "logits", dtype=torch.float32, numel=N)
+    _req(slot, "slot", dtype=torch.int64, numel=1)
+    _req(ticket, "ticket", dtype=torch.int32, numel=1)
+    for t, n in ((tok, "tok"), (hist, "hist"), (hist_len, "hist_len"), (pos, "pos")):
+        _req(t, n, dtype=torch.int32)
+    if not 0 <= int(last_n) <= HEAD_SELECT_MAX_LAST_N:
+        raise ValueError(f"head_select: last_n {last_n} > {HEAD_SELECT_MAX_LAST_N}")
+    check(kernels().cake_head_select(_dt(w), _p(resid), _p(norm_w), float(eps), _p(w), K, N,
+                                     _p(logits), _p(hist), _p(hist_len), int(last_n),
+                                     float(penalty), _p(slot), _p(ticket), _p(tok), _p(pos),
+                                     hist.numel(), _stream()), "head_select")
+
+
 def attn_decode(q, kcache, vcache, pos, scale, part, tickets, out):
     """Split-K GQA decode attention for the token at device position `pos`.
 
@@ -133,8 +159,10 @@ def attn_decode(q, kcache, vcache, pos, scale, part, tickets, out):
     _req(tickets, "tickets", dtype=torch.int32, numel=nkv)
     if hd not in (64, 128) or nh % nkv or (nh // nkv) not in (1, 2, 4, 8):
         raise ValueError(f"unsupported attention shape nh={nh} nkv={nkv} hd={hd}")
-    if not _ATTN_IMPL_SET[0]:  # CAKE_ATTN_IMPL, applied once
+    if not _ATTN_IMPL_SET[0]:  # CAKE_ATTN_IMPL / CAKE_ATTN_TARGET, applied once
         attn_set_impl(_ATTN_IMPL[0])
+        if os.environ.get("CAKE_ATTN_TARGET"):
+            attn_set_target_splits(int(os.environ["CAKE_ATTN_TARGET"]))
     check(kernels().cake_attn_decode(_dt(kcache), _p(q), _p(kcache), _p(vcache), _p(pos), S,
                                      nh, nkv, hd, float(scale), _p(part), _p(tickets),
                                      _p(out), _stream()),
@@ -166,12 +194,21 @@ def attn_splits(Tk: int) -> int:
     device-side policy of attn_core.h, mirrored for choosing a capped graph)."""
     Tk = max(int(Tk), 1)
     if _ATTN_IMPL[0] == 2:  # attn_core2.h attn2_splits
-        keys = max(_ATTN_MIN_KEYS[0], -(-(-(-Tk // 64)) // 16) * 16)
+        keys = max(_ATTN_MIN_KEYS[0], -(-(-(-Tk // _ATTN_TARGET[0])) // 16) * 16)
         ns = min(-(-Tk // keys), 64)
         kps = -(-(-(-Tk // ns)) // 16) * 16
         return -(-Tk // kps)
     keys = max(_ATTN_MIN_KEYS[0], 128 if Tk > 1024 else 64, -(-Tk // 64))
     return -(-Tk // keys)
+
+
+_ATTN_TARGET = [64]
+
+
+def attn_set_target_splits(n: int) -> None:
+    """Core 2: splits per kv head aimed at (keys per split = ceil(Tk / n), >= min_keys)."""
+    check(kernels().cake_attn_set_target_splits(int(n)), "attn_set_target_splits")
+    _ATTN_TARGET[0] = int(n)
 
 
 _ATTN_IMPL = [int(os.environ.get("CAKE_ATTN_IMPL", "2"))]

@@ -4,7 +4,8 @@ every workgroup; cake_attn_set_stamps).  Phases: 0 start, 1 position read issued
 direct write issued, 6 ticket known, 7 merge done (last workgroup only).
 
 Each launch follows a 64 MiB streaming read, as in decode (K/V not L2-resident).
-IMPLS=1,2 selects the decode-attention cores (attn_core.h / attn_core2.h)."""
+IMPLS=1,2 selects the decode-attention cores (attn_core.h / attn_core2.h); TARGETS the
+core-2 split targets, MINKS the minimum keys per split."""
 import ctypes as C
 import json
 import math
@@ -21,7 +22,7 @@ from cake_amd.ops._lib import kernels  # noqa: E402
 def main():
     dev = torch.device("cuda:0")
     dt = torch.bfloat16
-    nh, nkv, hd, S = 32, 8, 128, 4096
+    nh, nkv, hd, S = 32, 8, 128, 8192
     kc = torch.randn(nkv, S, hd, device=dev).to(dt)
     vc = torch.randn(nkv, S, hd, device=dev).to(dt)
     q = torch.randn(nh * hd, device=dev)
@@ -36,15 +37,17 @@ def main():
     lib.cake_attn_set_stamps.restype = C.c_int
     impls = [int(x) for x in os.environ.get("IMPLS", "1,2").split(",")]
     minks = [int(x) for x in os.environ.get("MINKS", "64").split(",")]
-    cases = [(i, mk, int(x)) for i in impls for mk in minks
+    targets = [int(x) for x in os.environ.get("TARGETS", "64").split(",")]
+    cases = [(i, mk, tg, int(x)) for i in impls for mk in minks for tg in targets
              for x in os.environ.get("TKS", "57,176,512,1024,2048,4000").split(",")]
-    for impl, mk, Tk in cases:
+    for impl, mk, tg, Tk in cases:
         K.attn_set_impl(impl)
         K.attn_set_min_keys(mk)
+        K.attn_set_target_splits(tg)
         pos.fill_(Tk - 1)
         need = K.attn_splits(Tk)
         cap = next(c for c in (8, 16, 32, 64) if c >= need) if need <= 64 else 64
-        rec = {"impl": impl, "min_keys": mk, "Tk": Tk, "cap": cap, "splits": need}
+        rec = {"impl": impl, "min_keys": mk, "target": tg, "Tk": Tk, "cap": cap, "splits": need}
         with K.attn_split_cap(cap):
             # plain timing: events around each launch after a streaming read
             ts = []

@@ -35,6 +35,16 @@ if [[ ${DO_AB:-0} == 1 ]]; then  # decode A/B: attention core, long context
   step ab_p2048_impl1 200 env CAKE_ATTN_IMPL=1 python bench.py --no-extras --prompt-len 2048
   step ab_p2048_impl2 200 env CAKE_ATTN_IMPL=2 python bench.py --no-extras --prompt-len 2048
 fi
+if [[ ${DO_AB3:-0} == 1 ]]; then  # fused greedy head (lm_head+penalty+argmax+finalize), core-2 split target
+  step ab3_fused 200 python bench.py --no-extras
+  step ab3_unfused 200 env CAKE_FUSED_HEAD=0 python bench.py --no-extras
+  step ab3_drv_fused 200 python bench.py --no-extras --steps 20 --warmup 5
+  step ab3_drv_unfused 200 env CAKE_FUSED_HEAD=0 python bench.py --no-extras --steps 20 --warmup 5
+  for tg in ${AB3_TARGETS:-16 32 64}; do
+    step ab3_p2048_t$tg 200 env CAKE_ATTN_TARGET=$tg python bench.py --no-extras --prompt-len 2048
+    step ab3_p4000_t$tg 200 env CAKE_ATTN_TARGET=$tg python bench.py --no-extras --prompt-len 4000 --max-seq 8192
+  done
+fi
 if [[ ${DO_SD:-0} == 1 ]]; then
   step sd_xl 300 python scripts/bench_sd.py --version xl --denoise --graph --steps 8
   step sd_15 200 python scripts/bench_sd.py --version v1-5 --denoise --graph --steps 8
