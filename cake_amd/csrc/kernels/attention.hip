@@ -24,9 +24,10 @@ namespace cake {
 
 // Grid (nkv, maxsplit): see attn_core.h for the split / chunk / combine scheme.
 static int g_attn_min_keys = 64;  // min keys per split (tunable)
-// core 2: number of splits aimed at past target * min_keys keys (fewer, longer splits
-// trade loop time for a cheaper ticket + merge tail; tunable)
-static int g_attn_target = 64;
+// core 2: number of splits aimed at past target * min_keys keys: fewer, longer splits
+// trade loop time for a cheaper ticket + merge tail (16 splits: 8B decode +3.4 % tok/s at
+// 2048 keys, +5.7 % at 4000 vs 64; profiles/r3_decode_ab.jsonl); tunable
+static int g_attn_target = 16;
 
 template <int DT, int HD, int NREP>
 __global__ __launch_bounds__(AttnGeom<NREP>::NT) void attn_decode_kernel(AttnDecArgs a) {

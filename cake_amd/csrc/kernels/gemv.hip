@@ -424,6 +424,9 @@ struct HeadSel {
   int* hist_len_w;
   int* pos;
   int max_hist;
+  const uint16_t* embed;   // optional: the next step's input, resid = embed[tok] (f32)
+  float* emb_out;
+  int H;
 };
 
 __device__ __forceinline__ unsigned int ordered_key(float f) {
@@ -511,17 +514,33 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_norm_f32_kernel(
       is_last = t == gridDim.x - 1;
     }
     __syncthreads();
-    if (is_last && threadIdx.x == 0) {
-      const unsigned long long key =
-          __hip_atomic_fetch_max(hs.slot, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int t = (int)(0xffffffffu - (unsigned int)(key & 0xffffffffull));
-      *hs.tok = t;
-      const int len = *hs.hist_len_w;
-      if (len < hs.max_hist) { hs.hist_w[len] = t; *hs.hist_len_w = len + 1; }
-      *hs.pos += 1;
-      // re-arm for the next launch (the kernel boundary orders these for it)
-      __hip_atomic_store(hs.slot, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(hs.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (is_last) {  // block-uniform
+      __shared__ int sel_tok;
+      if (threadIdx.x == 0) {
+        const unsigned long long key =
+            __hip_atomic_fetch_max(hs.slot, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int t = (int)(0xffffffffu - (unsigned int)(key & 0xffffffffull));
+        *hs.tok = t;
+        const int len = *hs.hist_len_w;
+        if (len < hs.max_hist) { hs.hist_w[len] = t; *hs.hist_len_w = len + 1; }
+        *hs.pos += 1;
+        // re-arm for the next launch (the kernel boundary orders these for it)
+        __hip_atomic_store(hs.slot, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(hs.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sel_tok = t;
+      }
+      if (hs.embed != nullptr) {
+        // the next step's input row (what embed_kernel would launch for): every other
+        // workgroup has finished reading resid (their tickets preceded this one)
+        __syncthreads();
+        const uint16_t* row = hs.embed + (size_t)sel_tok * hs.H;
+        for (int i = threadIdx.x * 8; i < hs.H; i += kGemvThreads * 8) {
+          float f[8];
+          unpack8<DT>(*reinterpret_cast<const uint4*>(row + i), f);
+          *reinterpret_cast<float4*>(hs.emb_out + i) = make_float4(f[0], f[1], f[2], f[3]);
+          *reinterpret_cast<float4*>(hs.emb_out + i + 4) = make_float4(f[4], f[5], f[6], f[7]);
+        }
+      }
     }
   }
 }
@@ -666,16 +685,19 @@ CAKE_API int cake_gemv_norm_f32(int dt, const float* resid, const void* norm_w, 
   return launch_norm_f32<false>(dt, resid, norm_w, eps, w, K, N, out, HeadSel{}, st);
 }
 
-// lm_head + repeat penalty + argmax + step finalizer in one launch (greedy decode).
-// slot (u64) and ticket (u32) must be zero before the first launch; the kernel re-arms
-// them.  last_n <= 256.
+// lm_head + repeat penalty + argmax + step finalizer in one launch (greedy decode);
+// with `embed`, also the next step's input emb_out[K] = embed[tok] (f32).  slot (u64)
+// and ticket (u32) must be zero before the first launch; the kernel re-arms them.
+// last_n <= 256.
 CAKE_API int cake_head_select(int dt, const float* resid, const void* norm_w, float eps,
                               const void* w, int K, int N, float* out, int* hist, int* hist_len,
                               int last_n, float penalty, unsigned long long* slot,
                               unsigned int* ticket, int* tok, int* pos, int max_hist,
-                              hipStream_t st) {
-  if (last_n < 0 || last_n > 256 || !(penalty > 0.f) || slot == nullptr || ticket == nullptr)
+                              const void* embed, float* emb_out, hipStream_t st) {
+  if (last_n < 0 || last_n > 256 || !(penalty > 0.f) || slot == nullptr || ticket == nullptr ||
+      (embed != nullptr && (emb_out == nullptr || K % 8)))
     return (int)hipErrorInvalidValue;
-  const HeadSel hs{hist, hist_len, last_n, penalty, slot, ticket, tok, hist, hist_len, pos, max_hist};
+  const HeadSel hs{hist, hist_len, last_n, penalty, slot, ticket, tok, hist, hist_len, pos,
+                   max_hist, (const uint16_t*)embed, emb_out, K};
   return launch_norm_f32<true>(dt, resid, norm_w, eps, w, K, N, out, hs, st);
 }

@@ -168,13 +168,17 @@ class DeviceDecoder:
     def _step_body(self) -> None:
         from ...ops import hip as K
         b, m = self.bufs, self.m
-        K.embed(m.head.embed, b.tok, b.resid)
+        fused = self._fused_select()
+        if not fused:
+            K.embed(m.head.embed, b.tok, b.resid)
         m.stack.decode_step(b, self._layers, m.session)
-        if self._fused_select():
-            # greedy: lm_head + penalty + argmax + finalize in one launch
+        if fused:
+            # greedy: lm_head + penalty + argmax + finalize + the next step's embedding
+            # row in ONE launch (the step's input was embedded by the previous one, or
+            # by _select_first)
             K.head_select(b.resid, m.head.norm, m.cfg.rms_norm_eps, m.head.lm_head, b.logits,
                           b.hist, b.hist_len, self.last_n if self.penalty != 1.0 else 0,
-                          self.penalty, b.slot, b.sel_ticket, b.tok, b.pos)
+                          self.penalty, b.slot, b.sel_ticket, b.tok, b.pos, embed=m.head.embed)
             return
         K.norm_gemv_f32(b.resid, m.head.norm, m.cfg.rms_norm_eps, m.head.lm_head, b.logits)
         if self.penalty != 1.0:
@@ -239,13 +243,14 @@ class DeviceDecoder:
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         # warm the kernels once outside capture on scratch state, then restore
-        saved = [t.clone() for t in (self.bufs.tok, self.bufs.pos, self.bufs.hist_len)]
+        state = (self.bufs.tok, self.bufs.pos, self.bufs.hist_len, self.bufs.resid)
+        saved = [t.clone() for t in state]
         hist = self.bufs.hist.clone()
         with torch.cuda.stream(s):
             self._step_body()
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
-        for t, v in zip((self.bufs.tok, self.bufs.pos, self.bufs.hist_len), saved):
+        for t, v in zip(state, saved):
             t.copy_(v)
         self.bufs.hist.copy_(hist)
         self.bufs.slot.zero_()
@@ -312,6 +317,8 @@ class DeviceDecoder:
         if self.greedy:
             K.select_token(b.logits, b.slot, b.hist, b.hist_len, b.tok, b.pos, self.sampling,
                            b.thr, params=self.params)
+            if self._fused_select():  # the fused step body starts from the embedded token
+                K.embed(self.m.head.embed, b.tok, b.resid)
             self.host_pos += 1
             return int(b.tok.item())
         raise RuntimeError("sampled mode: caller pushes the first token")

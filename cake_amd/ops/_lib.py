@@ -29,7 +29,7 @@ _SIGS = {
     "cake_swiglu": [I, P, P, F, P, P, I, I, P, P],
     "cake_gemv_x16": [I, P, P, I, I, P, I, P],
     "cake_gemv_norm_f32": [I, P, P, F, P, I, I, P, P],
-    "cake_head_select": [I, P, P, F, P, I, I, P, P, P, I, F, P, P, P, P, I, P],
+    "cake_head_select": [I, P, P, F, P, I, I, P, P, P, I, F, P, P, P, P, I, P, P, P],
     "cake_attn_decode": [I, P, P, P, P, I, I, I, I, F, P, P, P, P],
     "cake_attn_set_impl": [I],
     "cake_attn_set_target_splits": [I],

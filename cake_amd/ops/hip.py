@@ -118,11 +118,13 @@ HEAD_SELECT_MAX_LAST_N = 256
 
 
 def head_select(resid, norm_w, eps, w, logits, hist, hist_len, last_n: int, penalty: float,
-                slot, ticket, tok, pos) -> None:
+                slot, ticket, tok, pos, embed=None) -> None:
     """Greedy decode tail in ONE launch (gemv.hip cake_head_select): logits = lm_head(
     rmsnorm(resid)), repeat penalty over the last `last_n` (<= 256) history tokens, argmax
     (ties -> smallest id), then tok / history / pos advanced as finalize_token does.
-    slot (int64[1]) and ticket (int32[1]) start at zero; the kernel re-arms them."""
+    With `embed` (the [V, H] table) the launch also writes the next step's input,
+    resid = embed[tok] (f32), as :func:`embed` would.  slot (int64[1]) and ticket
+    (int32[1]) start at zero; the kernel re-arms them."""
     N, K = w.shape
     _req(resid, "resid", dtype=torch.float32, numel=K)
     _req(norm_w, "norm_w", dtype=w.dtype, shape=(K,))
@@ -134,10 +136,16 @@ def head_select(resid, norm_w, eps, w, logits, hist, hist_len, last_n: int, pena
         _req(t, n, dtype=torch.int32)
     if not 0 <= int(last_n) <= HEAD_SELECT_MAX_LAST_N:
         raise ValueError(f"head_select: last_n {last_n} > {HEAD_SELECT_MAX_LAST_N}")
+    if embed is not None:
+        _req(embed, "embed", dtype=w.dtype)
+        if embed.dim() != 2 or embed.shape[1] != K:
+            raise ValueError(f"head_select: embed {tuple(embed.shape)} does not match H={K}")
     check(kernels().cake_head_select(_dt(w), _p(resid), _p(norm_w), float(eps), _p(w), K, N,
                                      _p(logits), _p(hist), _p(hist_len), int(last_n),
                                      float(penalty), _p(slot), _p(ticket), _p(tok), _p(pos),
-                                     hist.numel(), _stream()), "head_select")
+                                     hist.numel(), None if embed is None else _p(embed),
+                                     None if embed is None else _p(resid), _stream()),
+          "head_select")
 
 
 def attn_decode(q, kcache, vcache, pos, scale, part, tickets, out):
@@ -202,7 +210,7 @@ def attn_splits(Tk: int) -> int:
     return -(-Tk // keys)
 
 
-_ATTN_TARGET = [64]
+_ATTN_TARGET = [16]
 
 
 def attn_set_target_splits(n: int) -> None:

@@ -338,9 +338,19 @@ class PipelineEngine:
         if k == 0:
             K.embed(self.head.embed, st.bufs.tok, st.resid)
         elif k == R + 1:
-            K.norm_gemv_f32(st.resid, self.head.norm, self.cfg.rms_norm_eps, self.head.lm_head,
-                            st.bufs.logits)
-            self._select_device(st)
+            b = st.bufs
+            if (self.sampler is None and self.sampling is None and self.sample_params is None
+                    and self.last_n <= K.HEAD_SELECT_MAX_LAST_N
+                    and os.environ.get("CAKE_FUSED_HEAD", "1") != "0"):
+                # greedy: lm_head + penalty + argmax + finalize in one launch
+                K.head_select(st.resid, self.head.norm, self.cfg.rms_norm_eps,
+                              self.head.lm_head, b.logits, b.hist, b.hist_len,
+                              self.last_n if self.penalty != 1.0 else 0, self.penalty,
+                              b.slot, b.sel_ticket, b.tok, b.pos)
+            else:
+                K.norm_gemv_f32(st.resid, self.head.norm, self.cfg.rms_norm_eps,
+                                self.head.lm_head, b.logits)
+                self._select_device(st)
         else:
             self.stack.decode_step(st.bufs, self.runs[k - 1].layers, st.sid)
         if k < R + 1 and self._recv_point(k + 1) and not self._skip_hops:

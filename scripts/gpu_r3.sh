@@ -16,7 +16,7 @@ step() {  # name timeout cmd...
   if [[ $rc -eq 1 && $name == pytest* ]]; then grep -E "^FAILED|passed|failed" "gpurun_out/$name.log" | tail -8; return 0; fi
   if [[ $rc -ne 0 ]]; then echo "$name rc=$rc -> stop"; exit $rc; fi
 }
-if [[ ${DO_TESTS:-1} == 1 || ${DO_SDRCCL:-0} == 1 ]]; then
+if [[ ${DO_SDRCCL:-${DO_TESTS:-1}} == 1 ]]; then
   step pytest_sdrccl 500 python -u -m pytest tests/test_sd_rccl_gpu.py -v -m gpu --timeout 420 --timeout-method thread
 fi
 if [[ ${DO_TESTS:-1} == 1 ]]; then

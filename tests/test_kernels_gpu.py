@@ -264,15 +264,17 @@ def test_penalty_argmax_finalize(cuda):
 @pytest.mark.parametrize("K,N,last_n,penalty", [(4096, 128256, 128, 1.1), (256, 1001, 256, 1.3),
                                                 (512, 7, 0, 1.0), (512, 4097, 3, 2.0)])
 def test_head_select_matches_four_launches(cuda, dt, K, N, last_n, penalty):
-    """Fused lm_head + penalty + argmax + finalize (one launch) vs norm_gemv_f32 +
-    repeat_penalty + argmax + finalize_token on the same inputs; three steps in a row
-    (slot / ticket re-armed by the kernel; the history grows, so from step 2 on the
-    previous choice is itself penalised)."""
+    """Fused lm_head + penalty + argmax + finalize (+ the next step's embedding row) in one
+    launch vs norm_gemv_f32 + repeat_penalty + argmax + finalize_token + embed on the same
+    inputs; three steps in a row (slot / ticket re-armed by the kernel; the history grows,
+    so from step 2 on the previous choice is itself penalised; each step's input is the
+    previous step's embedded token)."""
     from cake_amd.ops import hip as K_
     torch.manual_seed(11)
-    resid = torch.randn(K, device=cuda) * 3
+    resid0 = torch.randn(K, device=cuda) * 3
     nw = (1 + 0.1 * torch.randn(K, device=cuda)).to(dt)
     w = _rand(N, K, dt=dt, std=0.02)
+    table = _rand(N, K, dt=dt, std=2.0)
     hist0 = torch.randint(0, N, (300,), dtype=torch.int32)
     hist0[:20] = hist0[0]  # repeated tokens: penalised once
     state = []
@@ -284,26 +286,32 @@ def test_head_select_matches_four_launches(cuda, dt, K, N, last_n, penalty):
                           pos=torch.tensor([299], dtype=torch.int32, device=cuda),
                           slot=torch.zeros(1, dtype=torch.int64, device=cuda),
                           ticket=torch.zeros(1, dtype=torch.int32, device=cuda),
-                          logits=torch.empty(N, device=cuda)))
+                          logits=torch.empty(N, device=cuda), resid=resid0.clone()))
     a, b = state
+    ref = w.float() @ R.rms_norm(resid0, nw, 1e-5)
     for step in range(3):
-        K_.head_select(resid, nw, 1e-5, w, a["logits"], a["hist"], a["hist_len"], last_n,
-                       penalty, a["slot"], a["ticket"], a["tok"], a["pos"])
-        K_.norm_gemv_f32(resid, nw, 1e-5, w, b["logits"])
+        K_.head_select(a["resid"], nw, 1e-5, w, a["logits"], a["hist"], a["hist_len"], last_n,
+                       penalty, a["slot"], a["ticket"], a["tok"], a["pos"],
+                       embed=table if step < 2 else None)
+        K_.norm_gemv_f32(b["resid"], nw, 1e-5, w, b["logits"])
         if penalty != 1.0:
             K_.repeat_penalty(b["logits"], b["hist"], b["hist_len"], last_n, penalty)
         K_.argmax(b["logits"], b["slot"])
         K_.finalize_token(b["slot"], b["tok"], b["hist"], b["hist_len"], b["pos"])
+        if step < 2:
+            K_.embed(table, b["tok"], b["resid"])
         torch.cuda.synchronize()
         torch.testing.assert_close(a["logits"], b["logits"])
-        for k in ("tok", "pos", "hist_len", "hist"):
+        for k in ("tok", "pos", "hist_len", "hist", "resid"):
             assert torch.equal(a[k], b[k]), (step, k)
         assert int(a["slot"]) == 0 and int(a["ticket"]) == 0
-    # reference check of the first step's choice (f32 torch math)
-    ref = w.float() @ R.rms_norm(resid, nw, 1e-5)
-    if penalty != 1.0 and last_n:
-        ref = R.apply_repeat_penalty(ref, penalty, hist0[300 - last_n:].tolist())
-    assert abs(float(ref[int(a["hist"][300])]) - float(ref.max())) <= 3e-3 * max(1.0, float(ref.abs().max()))
+        if step == 0:  # the first choice against f32 torch math
+            if penalty != 1.0 and last_n:
+                ref = R.apply_repeat_penalty(ref, penalty, hist0[300 - last_n:].tolist())
+            assert abs(float(ref[int(a["tok"])]) - float(ref.max())) <= \
+                3e-3 * max(1.0, float(ref.abs().max()))
+    # without embed the input row is left alone
+    assert torch.equal(a["resid"], b["resid"])
 
 
 @pytest.mark.parametrize("dt", DTYPES)

@@ -168,9 +168,17 @@ def test_attention_split_policy_and_buckets(impl):
             assert max(K.attn_splits(t) for t in range(1, 2049)) <= 16
             assert max(K.attn_splits(t) for t in range(1, 4097)) <= 32
         else:
+            # default split target 16: never more than 16 splits
             assert K.attn_splits(64) == 1 and K.attn_splits(65) == 2
-            assert K.attn_splits(1024) == 16 and K.attn_splits(4096) == 64
-            assert max(K.attn_splits(t) for t in range(1, 2049)) <= 32
+            assert K.attn_splits(1024) == 16 and K.attn_splits(4096) == 16
+            assert max(K.attn_splits(t) for t in range(1, 20000, 3)) <= 16
+            saved_t = K._ATTN_TARGET[0]
+            K._ATTN_TARGET[0] = 64
+            try:
+                assert K.attn_splits(4096) == 64
+                assert max(K.attn_splits(t) for t in range(1, 2049)) <= 32
+            finally:
+                K._ATTN_TARGET[0] = saved_t
     finally:
         K._ATTN_IMPL[0] = saved
     assert K.attn_max_split(4096) == 64 and K.attn_max_split(100) == 2

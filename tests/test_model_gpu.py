@@ -129,7 +129,7 @@ def test_device_decoder_crosses_split_buckets(cuda):
     dec.capture()
     assert sorted(dec.graphs) == [8, 16, 32, 64]
     assert dec._graph_for(500) is dec.graphs[8] and dec._graph_for(600) is dec.graphs[16]
-    assert K.attn_splits(4096) == (32 if K._ATTN_IMPL[0] == 1 else 64)
+    assert K.attn_splits(4096) == (32 if K._ATTN_IMPL[0] == 1 else 16)
     st = run_decode(dec, 15)
     assert [first] + st.tokens == host
 
