@@ -32,6 +32,9 @@
 namespace cake {
 
 constexpr int kBlk = 16;  // keys per wave block (MFMA M dimension)
+// bound on the merge's granule polls (s_sleep 1 apart): a producer that never publishes
+// ends the poll with a wrong output instead of a hung GPU
+constexpr int kAttnMaxPolls = 1 << 20;
 
 template <int OFF> __device__ __forceinline__ float xor_max(float v) {
   static_assert(OFF == 16 || OFF == 32, "xor_max offset");
@@ -125,6 +128,7 @@ __device__ __forceinline__ void attn2_decode_block(const AttnDecArgs& a, int g, 
     }
   }
   const int Tk = *a.pos + 1;
+  const unsigned int epoch = a.tickets[gridDim.x + g];  // this launch's granule tag - 1
   ATTN_STAMP(1);
   int ns, kps;
   attn2_splits(Tk, a.min_keys, a.maxsplit, a.target, ns, kps);
@@ -258,45 +262,118 @@ __device__ __forceinline__ void attn2_decode_block(const AttnDecArgs& a, int g, 
       unsigned long long* dd = a.stamps + ((size_t)s * gridDim.x + g) * 8;
       for (int k = 0; k < 8; ++k) dd[k] = k < 6 ? stamp[k] : 0ull;
     }
+    if (tid == 0) a.tickets[gridDim.x + g] = epoch + 1u;
     return;
   }
-  // publish the split's partial [h][s][m, l, o...] (layout of attn_core.h)
+  // Splits >= 1 publish their partial as 8-byte {value, tag} granules (one sc1 store
+  // each; a reader that sees the tag sees the value: no fence, no drain, no ticket) and
+  // exit.  Split 0 keeps its own partial in LDS and merges: one wave per head polls
+  // the other splits' granules until every tag is this launch's (tag = epoch + 1; the
+  // per-kv-head epoch lives in tickets[nkv + g] and is advanced by split 0 at the end,
+  // so stale granules of earlier launches never match).
+  const unsigned long long tagw = (unsigned long long)(epoch + 1u) << 32;
+  unsigned long long* gpart = reinterpret_cast<unsigned long long*>(a.part);
+  if (s != 0) {
+#pragma unroll
+    for (int i = 0; i < OPT; ++i) {
+      const int idx = tid + i * NT;
+      if (idx < NOUT) {
+        const int h = idx / HD, d = idx - h * HD;
+        unsigned long long* dst = gpart + ((size_t)(g * NREP + h) * kMaxSplit + s) * (HD + 2);
+        if (d == 0) {
+          __hip_atomic_store(dst, tagw | __float_as_uint(mo[i]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(dst + 1, tagw | __float_as_uint(lo[i]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __hip_atomic_store(dst + 2 + d, tagw | __float_as_uint(ao[i]), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    ATTN_STAMP(5);
+    if (a.stamps != nullptr && tid == 0) {
+      unsigned long long* dd = a.stamps + ((size_t)s * gridDim.x + g) * 8;
+      for (int k = 0; k < 8; ++k) dd[k] = k < 6 ? stamp[k] : 0ull;
+    }
+    return;
+  }
+  // split 0: own partial -> LDS (the p tiles are free now), then the per-head merge
+  float* own = lds;  // [NREP][HD + 2]: m, l, o[HD]
+  static_assert(NREP * (HD + 2) <= NW * (kBlk * 16 + 16), "own partial fits the p tiles");
+  __syncthreads();  // every wave is done with its p tile
 #pragma unroll
   for (int i = 0; i < OPT; ++i) {
     const int idx = tid + i * NT;
     if (idx < NOUT) {
       const int h = idx / HD, d = idx - h * HD;
-      float* dst = a.part + ((size_t)(g * NREP + h) * kMaxSplit + s) * (HD + 2);
-      if (d == 0) { st_sc1(dst, mo[i]); st_sc1(dst + 1, lo[i]); }
-      st_sc1(dst + 2 + d, ao[i]);
+      if (d == 0) { own[h * (HD + 2)] = mo[i]; own[h * (HD + 2) + 1] = lo[i]; }
+      own[h * (HD + 2) + 2 + d] = ao[i];
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   ATTN_STAMP(5);
-  unsigned int* last_flag = reinterpret_cast<unsigned int*>(lds + attn2_smem_floats<HD, NREP, NW>() - 1);
-  if (tid == 0) {
-    const unsigned int t =
-        __hip_atomic_fetch_add(&a.tickets[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned int last = (t == (unsigned int)(ns - 1)) ? 1u : 0u;
-    if (last) a.tickets[g] = 0u;  // re-arm for the next launch (kernel boundary orders it)
-    *last_flag = last;
-  }
-  __syncthreads();
-  ATTN_STAMP(6);
-  const bool is_last = *last_flag != 0;
-  if (!is_last || wave >= NREP) {
-    if (a.stamps != nullptr && tid == 0) {
-      unsigned long long* dd = a.stamps + ((size_t)s * gridDim.x + g) * 8;
-      for (int k = 0; k < 8; ++k) dd[k] = k < 7 ? stamp[k] : 0ull;
+  if (wave < NREP) {
+    constexpr int DPL = HD / 64;  // output dims per lane
+    const int h = wave;
+    const unsigned long long* src = gpart + (size_t)(g * NREP + h) * kMaxSplit * (HD + 2);
+    const float* ow = own + h * (HD + 2);
+    // (m, l) of split `lane` (lane 0: split 0's own, from LDS)
+    float mt = lane == 0 ? ow[0] : -INFINITY, lt = lane == 0 ? ow[1] : 0.f;
+    bool ok = true;
+    for (int tries = 0;; ++tries) {
+      ok = true;
+      if (lane >= 1 && lane < ns) {
+        const unsigned long long gm = __hip_atomic_load(src + lane * (HD + 2), __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long gl = __hip_atomic_load(src + lane * (HD + 2) + 1, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT);
+        ok = (gm >> 32) == (tagw >> 32) && (gl >> 32) == (tagw >> 32);
+        mt = __uint_as_float((unsigned int)gm);
+        lt = __uint_as_float((unsigned int)gl);
+      }
+      if (__builtin_amdgcn_ballot_w64(!ok) == 0ull || tries > kAttnMaxPolls) break;
+      __builtin_amdgcn_s_sleep(1);
     }
-    return;
+    const float M = wave_max(mt);
+    const float wt = lane < ns ? exp2f(mt - M) : 0.f;
+    const float L = wave_sum(wt * lt);
+    float acc[DPL];
+#pragma unroll
+    for (int d = 0; d < DPL; ++d) acc[d] = __shfl(wt, 0, 64) * ow[2 + lane * DPL + d];
+    // o rows of splits 1.., 16 per poll round
+    for (int t0 = 1; t0 < ns; t0 += 16) {
+      unsigned long long v[16][DPL];
+      for (int tries = 0;; ++tries) {
+        ok = true;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          const int t = t0 + u < ns ? t0 + u : ns - 1;
+#pragma unroll
+          for (int d = 0; d < DPL; ++d) {
+            v[u][d] = __hip_atomic_load(src + t * (HD + 2) + 2 + lane * DPL + d, __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+            ok = ok && (v[u][d] >> 32) == (tagw >> 32);
+          }
+        }
+        if (__builtin_amdgcn_ballot_w64(!ok) == 0ull || tries > kAttnMaxPolls) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const float w = __shfl(wt, t0 + u < ns ? t0 + u : 63, 64);
+        const float wu = t0 + u < ns ? w : 0.f;
+#pragma unroll
+        for (int d = 0; d < DPL; ++d) acc[d] = fmaf(wu, __uint_as_float((unsigned int)v[u][d]), acc[d]);
+      }
+    }
+    const float inv = 1.f / L;
+    uint16_t* dst = a.out + (size_t)(g * NREP + h) * HD + lane * DPL;
+#pragma unroll
+    for (int d = 0; d < DPL; ++d) dst[d] = from_f32<DT>(acc[d] * inv);
   }
-  attn_merge_head<DT, HD>(a, g * NREP + wave, ns, lane, pt);  // (the wave's p tile is free)
   ATTN_STAMP(7);
-  if (a.stamps != nullptr && lane == 0 && wave == 0) {
+  if (tid == 0) a.tickets[gridDim.x + g] = epoch + 1u;  // the next launch's tag
+  if (a.stamps != nullptr && tid == 0) {
     unsigned long long* dd = a.stamps + ((size_t)s * gridDim.x + g) * 8;
-    for (int k = 0; k < 8; ++k) dd[k] = stamp[k];
+    for (int k = 0; k < 8; ++k) dd[k] = (k == 6) ? stamp[5] : stamp[k];
   }
 }
 

@@ -55,8 +55,9 @@ class DecodeBuffers:
         self.q = torch.zeros(nh * hd, device=device, dtype=f32)
         self.attn_out = torch.zeros(nh * hd, device=device, dtype=dtype)
         self.act = torch.zeros(I, device=device, dtype=dtype)
-        self.part = torch.zeros(nh * 64 * (hd + 2), device=device, dtype=f32)  # <= 64 splits
-        self.tickets = torch.zeros(cfg.num_key_value_heads, device=device, dtype=i32)
+        # <= 64 splits per head, 8-byte granules (attention.hip); tickets: [2 nkv]
+        self.part = torch.zeros(2 * nh * 64 * (hd + 2), device=device, dtype=f32)
+        self.tickets = torch.zeros(2 * cfg.num_key_value_heads, device=device, dtype=i32)
         self.pos = torch.zeros(1, device=device, dtype=i32) if pos is None else pos
         if with_head:
             self.logits = torch.zeros(cfg.vocab_size, device=device, dtype=f32)

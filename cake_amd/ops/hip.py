@@ -153,8 +153,9 @@ def attn_decode(q, kcache, vcache, pos, scale, part, tickets, out):
 
     The split count is derived on the device from the live length, so one
     captured launch serves every position.  part: f32 workspace
-    (:func:`attn_workspace_numel`); tickets: int32 [nkv], zero-initialised once
-    and re-armed by the kernel itself.
+    (:func:`attn_workspace_numel`) and tickets: int32 [2 nkv], both zero-initialised
+    once, together, and maintained by the kernel itself (core 1: arrival tickets,
+    re-armed; core 2: per-kv-head epochs that tag the published partials).
     """
     nkv, S, hd = kcache.shape
     nh = q.numel() // hd
@@ -164,7 +165,7 @@ def attn_decode(q, kcache, vcache, pos, scale, part, tickets, out):
     _req(pos, "pos", dtype=torch.int32, numel=1)
     _req(part, "part", dtype=torch.float32, numel=attn_workspace_numel(nh, hd, S))
     _req(out, "out", dtype=kcache.dtype, numel=nh * hd)
-    _req(tickets, "tickets", dtype=torch.int32, numel=nkv)
+    _req(tickets, "tickets", dtype=torch.int32, numel=2 * nkv)
     if hd not in (64, 128) or nh % nkv or (nh // nkv) not in (1, 2, 4, 8):
         raise ValueError(f"unsupported attention shape nh={nh} nkv={nkv} hd={hd}")
     if not _ATTN_IMPL_SET[0]:  # CAKE_ATTN_IMPL / CAKE_ATTN_TARGET, applied once
@@ -178,9 +179,10 @@ def attn_decode(q, kcache, vcache, pos, scale, part, tickets, out):
 
 
 def attn_workspace_numel(nh: int, hd: int, S: int) -> int:
-    """Partials of at most 64 splits per head (attention.hip kMaxSplit)."""
+    """f32 elements of the partials of at most 64 splits per head (attention.hip
+    kMaxSplit): core 2 stores each value as an 8-byte {value, tag} granule."""
     del S
-    return nh * 64 * (hd + 2)
+    return 2 * nh * 64 * (hd + 2)
 
 
 _ATTN_MIN_KEYS = [64]

@@ -45,6 +45,14 @@ if [[ ${DO_AB3:-0} == 1 ]]; then  # fused greedy head (lm_head+penalty+argmax+fi
     step ab3_p4000_t$tg 200 env CAKE_ATTN_TARGET=$tg python bench.py --no-extras --prompt-len 4000 --max-seq 8192
   done
 fi
+if [[ ${DO_AB4:-0} == 1 ]]; then  # fused tail incl. embedding vs four launches + embed; PP2 rehearsal
+  step ab4_drv_fused 200 python bench.py --no-extras --steps 20 --warmup 5
+  step ab4_drv_unfused 200 env CAKE_FUSED_HEAD=0 python bench.py --no-extras --steps 20 --warmup 5
+  step ab4_fused 200 python bench.py --no-extras
+  step ab4_unfused 200 env CAKE_FUSED_HEAD=0 python bench.py --no-extras
+  step ab4_p2048 200 python bench.py --no-extras --prompt-len 2048
+  step ab4_pp2 400 python bench.py --gpus 2 --dist-backend gloo --steps 20 --warmup 5 --no-extras
+fi
 if [[ ${DO_SD:-0} == 1 ]]; then
   step sd_xl 300 python scripts/bench_sd.py --version xl --denoise --graph --steps 8
   step sd_15 200 python scripts/bench_sd.py --version v1-5 --denoise --graph --steps 8

@@ -118,15 +118,18 @@ def test_attn_decode(cuda, attn_impl, dt, nh, nkv, hd, pos, S, min_keys):
     vc = _rand(nkv, S, hd, dt=dt)
     q = torch.randn(nh * hd, device=cuda)
     p = torch.tensor([pos], dtype=torch.int32, device=cuda)
-    part = torch.empty(K_.attn_workspace_numel(nh, hd, S), device=cuda)
+    part = torch.zeros(K_.attn_workspace_numel(nh, hd, S), device=cuda)
     out = torch.empty(nh * hd, device=cuda, dtype=dt)
-    tickets = torch.zeros(nkv, dtype=torch.int32, device=cuda)
+    tickets = torch.zeros(2 * nkv, dtype=torch.int32, device=cuda)
     K_.attn_set_min_keys(min_keys)
     try:
-        for it in range(2):  # second call checks the tickets were re-armed
+        # the first call (another q) leaves its partials behind: the second must not
+        # merge them (core 1: tickets re-armed; core 2: epoch-tagged granules)
+        for it in range(2):
             out.zero_()
-            K_.attn_decode(q, kc, vc, p, 1 / math.sqrt(hd), part, tickets, out)
-            assert int(tickets.abs().sum()) == 0
+            K_.attn_decode(q if it else torch.randn_like(q), kc, vc, p, 1 / math.sqrt(hd), part,
+                           tickets, out)
+            assert int(tickets[:nkv].abs().sum()) == 0
     finally:
         K_.attn_set_min_keys(64)
     Tk = pos + 1
@@ -165,9 +168,9 @@ def test_attn_decode_dead_rows_nan(cuda, attn_impl, pos):
     vc[:, pos + 1:] = float("nan")
     q = torch.randn(nh * hd, device=cuda)
     p = torch.tensor([pos], dtype=torch.int32, device=cuda)
-    part = torch.empty(K_.attn_workspace_numel(nh, hd, S), device=cuda)
+    part = torch.zeros(K_.attn_workspace_numel(nh, hd, S), device=cuda)
     out = torch.empty(nh * hd, device=cuda, dtype=torch.bfloat16)
-    tickets = torch.zeros(nkv, dtype=torch.int32, device=cuda)
+    tickets = torch.zeros(2 * nkv, dtype=torch.int32, device=cuda)
     K_.attn_decode(q, kc, vc, p, 1 / math.sqrt(hd), part, tickets, out)
     Tk = pos + 1
     ref = R.attention(q.view(1, nh, hd), kc[:, :Tk].transpose(0, 1), vc[:, :Tk].transpose(0, 1),
