@@ -315,11 +315,14 @@ __device__ __forceinline__ void attn2_decode_block(const AttnDecArgs& a, int g, 
     const int h = wave;
     const unsigned long long* src = gpart + (size_t)(g * NREP + h) * kMaxSplit * (HD + 2);
     const float* ow = own + h * (HD + 2);
-    // (m, l) of split `lane` (lane 0: split 0's own, from LDS)
+    // One poll round covers (m, l) of split `lane` and the o rows of splits 1..16 (all
+    // of them at the default 16-split target): every granule requested at once, the
+    // round repeated until every tag is this launch's.
+    constexpr int RU = 16;  // o rows (splits) per round
     float mt = lane == 0 ? ow[0] : -INFINITY, lt = lane == 0 ? ow[1] : 0.f;
-    bool ok = true;
+    unsigned long long v[RU][DPL];
     for (int tries = 0;; ++tries) {
-      ok = true;
+      bool ok = true;
       if (lane >= 1 && lane < ns) {
         const unsigned long long gm = __hip_atomic_load(src + lane * (HD + 2), __ATOMIC_RELAXED,
                                                         __HIP_MEMORY_SCOPE_AGENT);
@@ -328,6 +331,16 @@ __device__ __forceinline__ void attn2_decode_block(const AttnDecArgs& a, int g, 
         ok = (gm >> 32) == (tagw >> 32) && (gl >> 32) == (tagw >> 32);
         mt = __uint_as_float((unsigned int)gm);
         lt = __uint_as_float((unsigned int)gl);
+      }
+#pragma unroll
+      for (int u = 0; u < RU; ++u) {
+        const int t = 1 + u < ns ? 1 + u : ns - 1;
+#pragma unroll
+        for (int d = 0; d < DPL; ++d) {
+          v[u][d] = __hip_atomic_load(src + t * (HD + 2) + 2 + lane * DPL + d, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+          ok = ok && (v[u][d] >> 32) == (tagw >> 32);
+        }
       }
       if (__builtin_amdgcn_ballot_w64(!ok) == 0ull || tries > kAttnMaxPolls) break;
       __builtin_amdgcn_s_sleep(1);
@@ -338,14 +351,21 @@ __device__ __forceinline__ void attn2_decode_block(const AttnDecArgs& a, int g, 
     float acc[DPL];
 #pragma unroll
     for (int d = 0; d < DPL; ++d) acc[d] = __shfl(wt, 0, 64) * ow[2 + lane * DPL + d];
-    // o rows of splits 1.., 16 per poll round
-    for (int t0 = 1; t0 < ns; t0 += 16) {
-      unsigned long long v[16][DPL];
-      for (int tries = 0;; ++tries) {
-        ok = true;
+    for (int t0 = 1;; t0 += RU) {
 #pragma unroll
-        for (int u = 0; u < 16; ++u) {
-          const int t = t0 + u < ns ? t0 + u : ns - 1;
+      for (int u = 0; u < RU; ++u) {
+        const float w = __shfl(wt, t0 + u < ns ? t0 + u : 63, 64);
+        const float wu = t0 + u < ns ? w : 0.f;
+#pragma unroll
+        for (int d = 0; d < DPL; ++d) acc[d] = fmaf(wu, __uint_as_float((unsigned int)v[u][d]), acc[d]);
+      }
+      if (t0 + RU >= ns) break;
+      // further rounds (more than 17 splits: a split target above 16)
+      for (int tries = 0;; ++tries) {
+        bool ok = true;
+#pragma unroll
+        for (int u = 0; u < RU; ++u) {
+          const int t = t0 + RU + u < ns ? t0 + RU + u : ns - 1;
 #pragma unroll
           for (int d = 0; d < DPL; ++d) {
             v[u][d] = __hip_atomic_load(src + t * (HD + 2) + 2 + lane * DPL + d, __ATOMIC_RELAXED,
@@ -355,13 +375,6 @@ __device__ __forceinline__ void attn2_decode_block(const AttnDecArgs& a, int g, 
         }
         if (__builtin_amdgcn_ballot_w64(!ok) == 0ull || tries > kAttnMaxPolls) break;
         __builtin_amdgcn_s_sleep(1);
-      }
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const float w = __shfl(wt, t0 + u < ns ? t0 + u : 63, 64);
-        const float wu = t0 + u < ns ? w : 0.f;
-#pragma unroll
-        for (int d = 0; d < DPL; ++d) acc[d] = fmaf(wu, __uint_as_float((unsigned int)v[u][d]), acc[d]);
       }
     }
     const float inv = 1.f / L;
