@@ -1,7 +1,8 @@
 """Per-kernel bytes / TB/s table for 8B batch-1 decode from a rocprofv3 kernel-trace db.
 
 Decode steps are the kernels between prefill and the end; gemv_x16 launches alternate
-o_proj / down_proj within a layer.  Bytes are the weight (and KV) bytes each kernel
+o_proj / down_proj within a layer.  The lm_head row is the fused greedy tail (lm_head +
+repeat penalty + argmax + finalize + the next step's embedding row) in greedy decode.  Bytes are the weight (and KV) bytes each kernel
 must stream; the speed-of-light column is scripts/decode_ceiling.py's pure-read probe
 for the same bytes and kernel structure (profiles/r2_decode_ceiling.jsonl).
 
@@ -18,6 +19,8 @@ PROBE_US = {"qkv_rope": 9.03, "attn_decode": 1.94, "o_proj": 6.59, "swiglu": 35.
 
 
 def kind(name):
+    if "attn2_decode" in name:  # decode-attention core 2 (the default)
+        return "attn_decode"
     for k in ("qkv_rope", "swiglu", "attn_decode", "gemv_norm_f32", "gemv_x16"):
         if k in name:
             return k
