@@ -28,6 +28,10 @@ static int g_attn_min_keys = 64;  // min keys per split (tunable)
 // trade loop time for a cheaper ticket + merge tail (16 splits: 8B decode +3.4 % tok/s at
 // 2048 keys, +5.7 % at 4000 vs 64; profiles/r3_decode_ab.jsonl); tunable
 static int g_attn_target = 16;
+// core 2: live lengths up to this many keys run as ONE split per kv head — its merge
+// tail (partials out, polled back in: ~6.5k cycles, profiles/r3_attn_stamps_granule_v2.jsonl)
+// costs what ~240 more keys of one split's loop cost (~27 cycles per key)
+static int g_attn_single = 320;
 
 template <int DT, int HD, int NREP>
 __global__ __launch_bounds__(AttnGeom<NREP>::NT) void attn_decode_kernel(AttnDecArgs a) {
@@ -95,6 +99,12 @@ CAKE_API int cake_attn_set_target_splits(int target) {
   return 0;
 }
 
+CAKE_API int cake_attn_set_single_max(int keys) {
+  if (keys < 0) return (int)hipErrorInvalidValue;
+  g_attn_single = keys;
+  return 0;
+}
+
 CAKE_API int cake_attn_set_min_keys(int min_keys) {
   if (min_keys < kChunk || min_keys % kChunk) return (int)hipErrorInvalidValue;
   g_attn_min_keys = min_keys;
@@ -128,7 +138,8 @@ CAKE_API int cake_attn_decode(int dt, const float* q, const void* kc, const void
   const dim3 grid(nkv, splits);
   const AttnDecArgs a{q, (const uint16_t*)kc, (const uint16_t*)vc, pos, S,
                       scale * 1.4426950408889634f, part, tickets, (uint16_t*)out,
-                      g_attn_min_keys, splits, g_attn_stamps, g_attn_target};
+                      g_attn_min_keys, splits, g_attn_stamps, g_attn_target,
+                      g_attn_single};
   DISPATCH_DT_HD(dt, hd, return (launch_decode<DT, HD>(nh / nkv, grid, st, a)));
   return (int)hipErrorInvalidValue;
 }

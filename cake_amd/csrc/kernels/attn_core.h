@@ -103,6 +103,7 @@ struct AttnDecArgs {
   int min_keys, maxsplit;
   unsigned long long* stamps;  // diagnostics (nullptr in production): per-WG phase clocks
   int target;                  // core 2: splits aimed at (keys per split = Tk / target)
+  int single;                  // core 2: live lengths up to this run as one split
 };
 
 // Phase clock of workgroup (g, s) for the latency breakdown (scripts/attn_stamps.py):

@@ -53,7 +53,12 @@ constexpr int attn2_smem_floats() {
 
 // host/device split policy of the v2 core (mirrored by ops.hip.attn_splits)
 __device__ __forceinline__ void attn2_splits(int Tk, int min_keys, int maxsplit, int target,
-                                             int& ns, int& kps) {
+                                             int single, int& ns, int& kps) {
+  if (Tk <= single) {  // one split: no partials, no merge (cheaper up to ~320 keys)
+    ns = 1;
+    kps = (Tk + kBlk - 1) / kBlk * kBlk;
+    return;
+  }
   int keys = (Tk + target - 1) / target;
   keys = (keys + kBlk - 1) / kBlk * kBlk;
   if (keys < min_keys) keys = min_keys;
@@ -131,7 +136,7 @@ __device__ __forceinline__ void attn2_decode_block(const AttnDecArgs& a, int g, 
   const unsigned int epoch = a.tickets[gridDim.x + g];  // this launch's granule tag - 1
   ATTN_STAMP(1);
   int ns, kps;
-  attn2_splits(Tk, a.min_keys, a.maxsplit, a.target, ns, kps);
+  attn2_splits(Tk, a.min_keys, a.maxsplit, a.target, a.single, ns, kps);
   if (s >= ns) return;
   const int kb = s * kps, ke = min(Tk, kb + kps);
   const int nblk = (ke - kb + kBlk - 1) / kBlk;

@@ -33,6 +33,7 @@ _SIGS = {
     "cake_attn_decode": [I, P, P, P, P, I, I, I, I, F, P, P, P, P],
     "cake_attn_set_impl": [I],
     "cake_attn_set_target_splits": [I],
+    "cake_attn_set_single_max": [I],
     "cake_attn_set_min_keys": [I],
     "cake_attn_set_split_cap": [I],
     "cake_wave_reduce_probe": [P, P, P],

@@ -172,6 +172,8 @@ def attn_decode(q, kcache, vcache, pos, scale, part, tickets, out):
         attn_set_impl(_ATTN_IMPL[0])
         if os.environ.get("CAKE_ATTN_TARGET"):
             attn_set_target_splits(int(os.environ["CAKE_ATTN_TARGET"]))
+        if os.environ.get("CAKE_ATTN_SINGLE"):
+            attn_set_single_max(int(os.environ["CAKE_ATTN_SINGLE"]))
     check(kernels().cake_attn_decode(_dt(kcache), _p(q), _p(kcache), _p(vcache), _p(pos), S,
                                      nh, nkv, hd, float(scale), _p(part), _p(tickets),
                                      _p(out), _stream()),
@@ -204,6 +206,8 @@ def attn_splits(Tk: int) -> int:
     device-side policy of attn_core.h, mirrored for choosing a capped graph)."""
     Tk = max(int(Tk), 1)
     if _ATTN_IMPL[0] == 2:  # attn_core2.h attn2_splits
+        if Tk <= _ATTN_SINGLE[0]:
+            return 1
         keys = max(_ATTN_MIN_KEYS[0], -(-(-(-Tk // _ATTN_TARGET[0])) // 16) * 16)
         ns = min(-(-Tk // keys), 64)
         kps = -(-(-(-Tk // ns)) // 16) * 16
@@ -213,6 +217,13 @@ def attn_splits(Tk: int) -> int:
 
 
 _ATTN_TARGET = [16]
+_ATTN_SINGLE = [320]
+
+
+def attn_set_single_max(keys: int) -> None:
+    """Core 2: live lengths up to `keys` run as one split per kv head (no merge)."""
+    check(kernels().cake_attn_set_single_max(int(keys)), "attn_set_single_max")
+    _ATTN_SINGLE[0] = int(keys)
 
 
 def attn_set_target_splits(n: int) -> None:

@@ -37,7 +37,8 @@ def main():
     lib.cake_attn_set_stamps.restype = C.c_int
     impls = [int(x) for x in os.environ.get("IMPLS", "1,2").split(",")]
     minks = [int(x) for x in os.environ.get("MINKS", "64").split(",")]
-    targets = [int(x) for x in os.environ.get("TARGETS", "64").split(",")]
+    targets = [int(x) for x in os.environ.get("TARGETS", "16").split(",")]
+    K.attn_set_single_max(int(os.environ.get("SINGLE", "320")))
     cases = [(i, mk, tg, int(x)) for i in impls for mk in minks for tg in targets
              for x in os.environ.get("TKS", "57,176,512,1024,2048,4000").split(",")]
     for impl, mk, tg, Tk in cases:

@@ -92,14 +92,19 @@ def test_qkv_rope(cuda, dt, H, nh, nkv, hd, pos):
     assert kc[:, :pos].abs().sum() == 0 and kc[:, pos + 1:].abs().sum() == 0
 
 
-@pytest.fixture(params=[1, 2], ids=["core1", "core2"])
+@pytest.fixture(params=[(1, 320), (2, 320), (2, 0)], ids=["core1", "core2", "core2-split"])
 def attn_impl(request, cuda):
-    """Both decode-attention cores (attn_core.h chunks / attn_core2.h wave-stream MFMA)."""
+    """Both decode-attention cores (attn_core.h chunks / attn_core2.h wave-stream MFMA);
+    core 2 also with its one-split range off, so short contexts take the split + merge
+    path too."""
     from cake_amd.ops import hip as K_
-    prev = K_._ATTN_IMPL[0]
-    K_.attn_set_impl(request.param)
-    yield request.param
+    impl, single = request.param
+    prev, prev_single = K_._ATTN_IMPL[0], K_._ATTN_SINGLE[0]
+    K_.attn_set_impl(impl)
+    K_.attn_set_single_max(single)
+    yield impl
     K_.attn_set_impl(prev)
+    K_.attn_set_single_max(prev_single)
 
 
 @pytest.mark.parametrize("dt", DTYPES)

@@ -169,7 +169,7 @@ def test_attention_split_policy_and_buckets(impl):
             assert max(K.attn_splits(t) for t in range(1, 4097)) <= 32
         else:
             # default split target 16: never more than 16 splits
-            assert K.attn_splits(64) == 1 and K.attn_splits(65) == 2
+            assert K.attn_splits(320) == 1 and K.attn_splits(321) == 6
             assert K.attn_splits(1024) == 16 and K.attn_splits(4096) == 16
             assert max(K.attn_splits(t) for t in range(1, 20000, 3)) <= 16
             saved_t = K._ATTN_TARGET[0]
