@@ -53,6 +53,10 @@ if [[ ${DO_AB4:-0} == 1 ]]; then  # fused tail incl. embedding vs four launches 
   step ab4_p2048 200 python bench.py --no-extras --prompt-len 2048
   step ab4_pp2 400 python bench.py --gpus 2 --dist-backend gloo --steps 20 --warmup 5 --no-extras
 fi
+if [[ ${DO_MULTI:-0} == 1 ]]; then  # multi-rank rehearsals, ranks sharing the one GPU (plumbing)
+  step multi_pp2 500 python bench.py --gpus 2 --dist-backend gloo --steps 20 --warmup 5
+  step multi_tp2 300 python bench.py --gpus 2 --dist-backend gloo --parallel tp --steps 20 --warmup 5 --no-extras
+fi
 if [[ ${DO_SD:-0} == 1 ]]; then
   step sd_xl 300 python scripts/bench_sd.py --version xl --denoise --graph --steps 8
   step sd_15 200 python scripts/bench_sd.py --version v1-5 --denoise --graph --steps 8
