@@ -180,6 +180,7 @@ __device__ __forceinline__ void attn2_decode_block(const AttnDecArgs& a, int g, 
 #pragma unroll
     for (int e = 0; e < 4; ++e) pt[(4 * rg + e) * 16 + col] = p[e];
     if (rg == 0) alph[col] = alpha;
+    if (b == wave) ATTN_STAMP(6);  // diagnostics: first block's scores done (one split only)
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the tile is in LDS
     __builtin_amdgcn_wave_barrier();
     // P.V on this lane's KPL keys x 8 dims; dead keys' V rows are zero
@@ -265,7 +266,7 @@ __device__ __forceinline__ void attn2_decode_block(const AttnDecArgs& a, int g, 
     }
     if (a.stamps != nullptr && tid == 0) {
       unsigned long long* dd = a.stamps + ((size_t)s * gridDim.x + g) * 8;
-      for (int k = 0; k < 8; ++k) dd[k] = k < 6 ? stamp[k] : 0ull;
+      for (int k = 0; k < 8; ++k) dd[k] = (k < 6 || k == 6) ? stamp[k] : 0ull;
     }
     if (tid == 0) a.tickets[gridDim.x + g] = epoch + 1u;
     return;
