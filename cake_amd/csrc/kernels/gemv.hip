@@ -551,8 +551,10 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_norm_f32_kernel(
 struct GemvTune { int U, PF, MB; };
 enum GemvKind { kQkv = 0, kSwiglu = 1, kX16 = 2, kNormF32 = 3, kNumKinds = 4 };
 // measured in the decode graph (8B, tok/s): profiles/r2_gemv_split_prologue_sweep*.jsonl —
-// prefetching the first weight rows behind the split x prologue is +10% (323 -> 357)
-static GemvTune g_tune[kNumKinds] = {{4, 8, 1024}, {2, 4, 512}, {4, 4, 1024}, {4, 4, 256}};
+// prefetching the first weight rows behind the split x prologue is +10% (323 -> 357); the
+// round-3 re-sweep (profiles/r3_decode_gemv_tuning_ingraph.jsonl) moved QKV to U 2 / PF 4
+// (+0.3 %, every round) and left the rest
+static GemvTune g_tune[kNumKinds] = {{2, 4, 1024}, {2, 4, 512}, {4, 4, 1024}, {4, 4, 256}};
 
 static inline int grid_for(int npairs, int max_blocks) {
   int g = (npairs + kGemvWaves - 1) / kGemvWaves;

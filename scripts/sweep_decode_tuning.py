@@ -15,9 +15,9 @@ from cake_amd.ops import hip as K  # noqa: E402
 
 # kind -> (U, prefetch, max_blocks); prefetch > 0 also selects the split x prologue
 # (gemv.hip NormPre / Plain16Pre) for the model's K
-DEFAULTS = {"qkv": (4, 8, 1024), "swiglu": (2, 4, 512), "x16": (4, 4, 1024),
+DEFAULTS = {"qkv": (2, 4, 1024), "swiglu": (2, 4, 512), "x16": (4, 4, 1024),
             "norm_f32": (4, 4, 256)}
-BEST = {"qkv": (4, 8, 1024), "swiglu": (2, 4, 512), "x16": (4, 4, 1024)}
+BEST = {"qkv": (2, 4, 1024), "swiglu": (2, 4, 512), "x16": (4, 4, 1024)}
 VARIANTS = {
     "default": {},
     "best": BEST,

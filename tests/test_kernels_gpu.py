@@ -349,7 +349,7 @@ def test_rope_kv_fused_qkv_and_silu_mul_rows(cuda, dt):
     ref = torch.nn.functional.silu(gu[:, :I].float()) * gu[:, I:].float()
     torch.testing.assert_close(act.float(), ref, **_tol(dt))
 
-GEMV_DEFAULTS = {"qkv": (4, 8, 1024), "swiglu": (2, 4, 512), "x16": (4, 4, 1024),
+GEMV_DEFAULTS = {"qkv": (2, 4, 1024), "swiglu": (2, 4, 512), "x16": (4, 4, 1024),
                  "norm_f32": (4, 4, 256)}
 
 
