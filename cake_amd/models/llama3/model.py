@@ -259,9 +259,8 @@ class DeviceDecoder:
         # 353 -> 368 tok/s at short context).  One graph per cap; launch() replays
         # the smallest whose cap covers the live length.
         from ...ops import hip as K
-        full = K.attn_max_split(self.m.stack.max_seq)
         self.graphs = {}
-        for cap in sorted({min(c, full) for c in (8, 16, 32, 64)}):
+        for cap in K.attn_split_caps(self.m.stack.max_seq):
             g = torch.cuda.CUDAGraph()
             with K.attn_split_cap(cap), torch.cuda.graph(g):
                 for _ in range(self.k):

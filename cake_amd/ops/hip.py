@@ -244,6 +244,21 @@ def attn_set_impl(impl: int) -> None:
     _ATTN_IMPL_SET[0] = True
 
 
+def attn_split_caps(max_seq: int) -> list[int]:
+    """Position-bucket split caps a decode graph set needs for live lengths up to max_seq:
+    the 8/16/32/64 caps (clamped to the max_seq grid) up to the first that covers every
+    live length's split count under the current policy (core 2 at a 16-split target
+    needs 8 and 16 only)."""
+    full = attn_max_split(max_seq)
+    need = max(attn_splits(t) for t in range(1, max_seq + 1))
+    caps = []
+    for c in (8, 16, 32, 64):
+        caps.append(min(c, full))
+        if c >= need:
+            break
+    return sorted(set(caps))
+
+
 class attn_split_cap:
     """Context manager: decode-attention launches (and graph captures) inside it use at
     most `cap` splits per kv head (correct at any live length; fastest where

@@ -863,8 +863,7 @@ class PipelineEngine:
     # ------------------------------------------------------------------ graphs
     def _caps(self) -> list[int]:
         from ..ops import hip as K
-        full = K.attn_max_split(self.stack.max_seq)
-        return sorted({min(c, full) for c in (8, 16, 32, 64)})
+        return K.attn_split_caps(self.stack.max_seq)
 
     def _capture_caps(self, fn) -> dict:
         """One graph of fn per attention split cap (position buckets)."""

@@ -630,9 +630,8 @@ class TPEngine:
         # one graph per attention split cap (position buckets, as DeviceDecoder.capture);
         # every rank picks the same one from the same host position
         from ..ops import hip as K
-        full = K.attn_max_split(self.max_seq)
         gs = {}
-        for cap in sorted({min(c, full) for c in (8, 16, 32, 64)}):
+        for cap in K.attn_split_caps(self.max_seq):
             g = torch.cuda.CUDAGraph()
             with K.attn_split_cap(cap), torch.cuda.graph(g):
                 self._step_body()

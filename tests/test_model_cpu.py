@@ -179,6 +179,8 @@ def test_attention_split_policy_and_buckets(impl):
                 assert max(K.attn_splits(t) for t in range(1, 2049)) <= 32
             finally:
                 K._ATTN_TARGET[0] = saved_t
+        assert K.attn_split_caps(4096) == ([8, 16, 32] if impl == 1 else [8, 16])
+        assert K.attn_split_caps(100) == [2]
     finally:
         K._ATTN_IMPL[0] = saved
     assert K.attn_max_split(4096) == 64 and K.attn_max_split(100) == 2
