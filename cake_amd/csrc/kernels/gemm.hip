@@ -145,12 +145,76 @@ __device__ __forceinline__ uint4 ds_read16(uint32_t addr) {
   return v;
 }
 
+// Epilogue operands that come from global memory — the bias columns and the residual
+// row segment of each strip — requested AHEAD of use: the bias once per wave, a strip's
+// residual before the previous strip is stored.  Loaded inside the strip (as before)
+// every strip waited one full memory round trip behind the previous strip's stores
+// (the compiler cannot hoist a load over stores that may alias it): +4.5-6.7 us per SD
+// add16 projection in isolation.
+// Measured per epilogue (profiles/r3_gemm_epilogue_ab.jsonl): the 16-bit residual add
+// (SD projections, +6-21 %) and the gated bias (+1-3 %) gain; the f32 residual / plain
+// stores did not (the extra live registers cost the 256-wide tiles a spill), so those keep
+// their in-strip loads (PRE = false).
+template <int DT, int EPI, int NF> struct EpiOps {
+  static constexpr int WTN = NF * 16;
+  static constexpr bool GATED = (EPI == kEpiSwiglu || EPI == kEpiGeglu);
+  static constexpr int OUTC = GATED ? WTN / 2 : WTN;
+  static constexpr int CPL = OUTC / 4;
+  static constexpr bool PRE = (EPI == kEpiAdd16 || GATED);
+  static constexpr bool RES = EPI == kEpiAdd16;
+  float bias[PRE ? (GATED ? 2 * CPL : CPL) : 1];
+  float res[2][RES ? CPL : 1];
+
+  // 16-bit values [n0, n0 + CPL) of row p (columns < n valid) as f32
+  __device__ __forceinline__ static void load16(const uint16_t* p, int n0, int n, bool vec,
+                                                float* o) {
+    if (vec) {
+#pragma unroll
+      for (int c = 0; c < CPL; c += 8) {
+        float f[8];
+        unpack8<DT>(*reinterpret_cast<const uint4*>(p + n0 + c), f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[c + e] = f[e];
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) o[c] = n0 + c < n ? to_f32<DT>(p[n0 + c]) : 0.f;
+    }
+  }
+
+  __device__ __forceinline__ void load_bias(const GemmArgs& g, int vcol0, int lane) {
+    if constexpr (PRE) {
+      const int ec = (lane & 3) * CPL;
+      if (g.bias == nullptr) {
+#pragma unroll
+        for (int c = 0; c < (GATED ? 2 * CPL : CPL); ++c) bias[c] = 0.f;
+        return;
+      }
+      const int n0 = GATED ? vcol0 / 2 + ec : vcol0 + ec;
+      const bool vec = CPL % 8 == 0 && n0 + CPL <= g.N && (n0 & 7) == 0 && (!GATED || (g.half & 7) == 0);
+      load16(g.bias, n0, g.N, vec, bias);
+      if constexpr (GATED) load16(g.bias + g.half, n0, g.N, vec, bias + CPL);
+    }
+  }
+
+  template <int B>
+  __device__ __forceinline__ void load_res(const GemmArgs& g, int m, int vcol0, int lane) {
+    if constexpr (RES) {
+      const int n0 = vcol0 + (lane & 3) * CPL;
+      if (m >= g.M) return;
+      const bool vec = CPL % 8 == 0 && n0 + CPL <= g.N && ((g.ldr | n0) & 7) == 0;
+      load16(g.r16 + (size_t)m * g.ldr, n0, g.N, vec, res[B]);
+    }
+  }
+};
+
 // One 16-row strip of a wave's output (NF 16x16 accumulator tiles = NF*16 virtual
 // columns starting at vcol0), staged through the wave's LDS slice stg and written
-// with the epilogue EPI.
-template <int DT, int EPI, int NF>
+// with the epilogue EPI (bias / residual from ops, buffer B).
+template <int DT, int EPI, int NF, int B>
 __device__ __forceinline__ void epi_strip(const GemmArgs& g, const cf32x4 (&tiles)[NF], float* stg,
-                                          int m_strip0, int vcol0, int split, int lane) {
+                                          int m_strip0, int vcol0, int split, int lane,
+                                          const EpiOps<DT, EPI, NF>& ops) {
   constexpr int WTN = NF * 16;
   constexpr int STG_LD = WTN + 4;
   constexpr bool GATED = (EPI == kEpiSwiglu || EPI == kEpiGeglu);
@@ -188,11 +252,7 @@ __device__ __forceinline__ void epi_strip(const GemmArgs& g, const cf32x4 (&tile
         for (int c = 0; c < CPL; ++c) {
           const int lc = ec + c;                           // output col within the wave
           const int vc = (lc >> 4) * 32 + (lc & 15);       // gate's staged column
-          float a = srow[vc], b = srow[vc + 16];
-          if (g.bias != nullptr && f0 + c < g.N) {
-            a += to_f32<DT>(g.bias[f0 + c]);
-            b += to_f32<DT>(g.bias[g.half + f0 + c]);
-          }
+          const float a = srow[vc] + ops.bias[c], b = srow[vc + 16] + ops.bias[CPL + c];
           float y;
           if constexpr (EPI == kEpiSwiglu) y = silu(a) * b;
           else y = a * gelu_tanh(b);
@@ -215,7 +275,10 @@ __device__ __forceinline__ void epi_strip(const GemmArgs& g, const cf32x4 (&tile
           v[c] = t4.x; v[c + 1] = t4.y; v[c + 2] = t4.z; v[c + 3] = t4.w;
         }
         const bool full = n0c + CPL <= g.N;
-        if (g.bias != nullptr) {
+        if constexpr (EpiOps<DT, EPI, NF>::PRE) {
+#pragma unroll
+          for (int c = 0; c < CPL; ++c) v[c] += ops.bias[c];
+        } else if (g.bias != nullptr) {
 #pragma unroll
           for (int c = 0; c < CPL; ++c)
             if (full || n0c + c < g.N) v[c] += to_f32<DT>(g.bias[n0c + c]);
@@ -236,10 +299,8 @@ __device__ __forceinline__ void epi_strip(const GemmArgs& g, const cf32x4 (&tile
           }
         } else {
           if constexpr (EPI == kEpiAdd16) {
-            const uint16_t* r = g.r16 + (size_t)m * g.ldr + n0c;
 #pragma unroll
-            for (int c = 0; c < CPL; ++c)
-              if (full || n0c + c < g.N) v[c] += to_f32<DT>(r[c]);
+            for (int c = 0; c < CPL; ++c) v[c] += ops.res[B][c];
           }
           if constexpr (EPI == kEpiSilu) {
 #pragma unroll
@@ -509,8 +570,15 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(GemmArgs g) {
   float* stg = reinterpret_cast<float*>(smem + wave * STG);
   const int row_m0 = m0 + wr * WTM;
   const int vcol0 = n0 + wc * WTN;  // first virtual column of this wave
-#pragma unroll
-  for (int i = 0; i < FM; ++i) epi_strip<DT, EPI, FN>(g, acc[i], stg, row_m0 + i * 16, vcol0, split, lane);
+  EpiOps<DT, EPI, FN> ops;
+  ops.load_bias(g, vcol0, lane);
+  ops.template load_res<0>(g, row_m0 + (lane >> 2), vcol0, lane);
+  static_for<0, FM>([&](auto ii) __attribute__((always_inline)) {
+    constexpr int i = decltype(ii)::value;
+    // the next strip's residual goes out before this strip's stores
+    if constexpr (i + 1 < FM) ops.template load_res<(i + 1) & 1>(g, row_m0 + (i + 1) * 16 + (lane >> 2), vcol0, lane);
+    epi_strip<DT, EPI, FN, i & 1>(g, acc[i], stg, row_m0 + i * 16, vcol0, split, lane, ops);
+  });
 }
 
 // Split-K finalize: out = epilogue(sum over splits of the slabs).  One thread
