@@ -281,6 +281,9 @@ __device__ __forceinline__ uint32_t cvt_pk(float lo, float hi) {
 
 constexpr int kVTS = 68;
 
+// deferred-max threshold of flash2 (log2 units): p <= 2^8 between rescales
+constexpr float kDefer = 8.f;
+
 template <int DT, int DP, int NW>
 __global__ __launch_bounds__(64 * NW, 2) void flash2_fwd_kernel(FlashArgs a) {
   constexpr int KS = DP / 16;   // QKᵀ k-steps
@@ -415,9 +418,12 @@ __global__ __launch_bounds__(64 * NW, 2) void flash2_fwd_kernel(FlashArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) mt = fmaxf(mt, s[t][r]);
     mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-    const float mn = fmaxf(m, mt);           // raw-score units
+    // Deferred max (FA-style threshold): the running max moves only when a tile's max
+    // exceeds it by more than 2^kDefer in probability units, so p stays <= 2^kDefer and
+    // most tiles skip the O rescale (skipped when no lane of the wave moved its max).
+    const bool grow = m == -INFINITY || (mt - m) * a.scale_log2 > kDefer;
+    const float mn = grow ? fmaxf(m, mt) : m;  // raw-score units
     const float mc = mn == -INFINITY ? 0.f : mn * a.scale_log2;
-    const float alpha = __builtin_amdgcn_exp2f(m * a.scale_log2 - mc);  // m = -inf -> 0
     float rs = 0.f;
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -427,11 +433,15 @@ __global__ __launch_bounds__(64 * NW, 2) void flash2_fwd_kernel(FlashArgs a) {
         s[t][r] = p;
         rs += p;
       }
-    l = l * alpha + rs;
+    if (__builtin_amdgcn_ballot_w64(grow) != 0ull) {
+      const float alpha = __builtin_amdgcn_exp2f(m * a.scale_log2 - mc);  // m = -inf -> 0
+      l *= alpha;
 #pragma unroll
-    for (int t = 0; t < DTL; ++t)
+      for (int t = 0; t < DTL; ++t)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
+        for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
+    }
+    l += rs;
     m = mn;
 
     // ---- Oᵀ += Vᵀ Pᵀ: k-step (t, s2) covers keys 32t + 16s2 + {8(j>>2) + 4h + (j&3)}
