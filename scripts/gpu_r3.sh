@@ -57,6 +57,13 @@ if [[ ${DO_MULTI:-0} == 1 ]]; then  # multi-rank rehearsals, ranks sharing the o
   step multi_pp2 500 python bench.py --gpus 2 --dist-backend gloo --steps 20 --warmup 5
   step multi_tp2 300 python bench.py --gpus 2 --dist-backend gloo --parallel tp --steps 20 --warmup 5 --no-extras
 fi
+if [[ ${DO_KAB:-0} == 1 ]]; then  # tokens per graph replay
+  step k1 200 python bench.py --no-extras --steps 20 --warmup 5
+  step k2 200 python bench.py --no-extras --steps 20 --warmup 4 --steps-per-graph 2
+  step k4 200 python bench.py --no-extras --steps 20 --warmup 4 --steps-per-graph 4
+  step k1b 200 python bench.py --no-extras --steps 128
+  step k4b 200 python bench.py --no-extras --steps 128 --steps-per-graph 4
+fi
 if [[ ${DO_SD:-0} == 1 ]]; then
   step sd_xl 300 python scripts/bench_sd.py --version xl --denoise --graph --steps 8
   step sd_15 200 python scripts/bench_sd.py --version v1-5 --denoise --graph --steps 8
