@@ -21,6 +21,16 @@ for P in ${PROMPTS:-32 2048}; do
   python3 "$ROOT/scripts/prof_window.py" "$(db_of "$ROOT/gpurun_out/prof_p$P")" 10 12 \
     > "$ROOT/gpurun_out/proftab/decode8b_p${P}_window.txt" || exit 1
 done
+if [[ ${DO_70B:-0} == 1 ]]; then
+  rm -rf "$ROOT/gpurun_out/prof_70b"
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$ROOT/gpurun_out/prof_70b" -o run -- \
+    python3 "$ROOT/bench.py" --no-extras --model llama3-70b --steps 24 --warmup 4 \
+    > "$ROOT/gpurun_out/prof_70b.log" 2>&1 || { tail -5 "$ROOT/gpurun_out/prof_70b.log"; exit 1; }
+  grep '^{' "$ROOT/gpurun_out/prof_70b.log" | cut -c1-160
+  python3 "$ROOT/scripts/prof_window.py" "$(db_of "$ROOT/gpurun_out/prof_70b")" 100 12 \
+    > "$ROOT/gpurun_out/proftab/decode70b_window.txt" || exit 1
+  cat "$ROOT/gpurun_out/proftab/decode70b_window.txt"
+fi
 if [[ ${DO_SDXL:-1} == 1 ]]; then
   rm -rf "$ROOT/gpurun_out/prof_sdxl"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$ROOT/gpurun_out/prof_sdxl" -o run -- \
