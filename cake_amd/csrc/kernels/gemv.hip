@@ -549,12 +549,14 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_norm_f32_kernel(
 // rocprofv3-measured sweep in profiles/): U = chunks in flight per row,
 // PF = prefetch the first weight batch before the x prologue, MB = grid cap.
 struct GemvTune { int U, PF, MB; };
-enum GemvKind { kQkv = 0, kSwiglu = 1, kX16 = 2, kNormF32 = 3, kNumKinds = 4 };
+// kX16 = 16-bit-input GEMVs with K > 8192 (down_proj), kX16S = K <= 8192 (o_proj)
+enum GemvKind { kQkv = 0, kSwiglu = 1, kX16 = 2, kNormF32 = 3, kX16S = 4, kNumKinds = 5 };
 // measured in the decode graph (8B, tok/s): profiles/r2_gemv_split_prologue_sweep*.jsonl —
 // prefetching the first weight rows behind the split x prologue is +10% (323 -> 357); the
 // round-3 re-sweep (profiles/r3_decode_gemv_tuning_ingraph.jsonl) moved QKV to U 2 / PF 4
 // (+0.3 %, every round) and left the rest
-static GemvTune g_tune[kNumKinds] = {{2, 4, 1024}, {2, 4, 512}, {4, 4, 1024}, {4, 4, 256}};
+static GemvTune g_tune[kNumKinds] = {{2, 4, 1024}, {2, 4, 512}, {4, 4, 1024}, {4, 4, 256},
+                                     {4, 4, 1024}};
 
 static inline int grid_for(int npairs, int max_blocks) {
   int g = (npairs + kGemvWaves - 1) / kGemvWaves;
@@ -651,7 +653,7 @@ CAKE_API int cake_gemv_x16(int dt, const void* x, const void* w, int K, int N, f
                            int accumulate, hipStream_t st) {
   if (K % 8) return (int)hipErrorInvalidValue;
   const size_t lds = (size_t)K * 2;
-  const GemvTune t = g_tune[kX16];
+  const GemvTune t = g_tune[K <= 8192 ? kX16S : kX16];
   const int g = grid_for((N + 1) / 2, t.MB);
   if (accumulate) {
     DISPATCH_DT(dt, DISPATCH_TUNE(t, K, CAKE_NX_X16(K, hipLaunchKernelGGL((gemv_x16_kernel<DT, U, PF, NX, true>),

@@ -505,7 +505,7 @@ def push_token(src, tok, hist, hist_len, pos):
                                     hist.numel(), _stream()), "push_token")
 
 
-GEMV_KINDS = {"qkv": 0, "swiglu": 1, "x16": 2, "norm_f32": 3}
+GEMV_KINDS = {"qkv": 0, "swiglu": 1, "x16": 2, "norm_f32": 3, "x16s": 4}  # x16s: K <= 8192
 
 
 def set_gemv_tuning(kind: str, U: int = 4, prefetch: int = 0, max_blocks: int = 1024) -> None:

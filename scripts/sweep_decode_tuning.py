@@ -16,10 +16,18 @@ from cake_amd.ops import hip as K  # noqa: E402
 # kind -> (U, prefetch, max_blocks); prefetch > 0 also selects the split x prologue
 # (gemv.hip NormPre / Plain16Pre) for the model's K
 DEFAULTS = {"qkv": (2, 4, 1024), "swiglu": (2, 4, 512), "x16": (4, 4, 1024),
-            "norm_f32": (4, 4, 256)}
+            "norm_f32": (4, 4, 256), "x16s": (4, 4, 1024)}
 BEST = {"qkv": (2, 4, 1024), "swiglu": (2, 4, 512), "x16": (4, 4, 1024)}
 VARIANTS = {
     "default": {},
+    # o_proj (x16s, K <= 8192) on its own
+    "o_u2pf4": {"x16s": (2, 4, 1024)},
+    "o_u2pf8": {"x16s": (2, 8, 1024)},
+    "o_u4pf8": {"x16s": (4, 8, 1024)},
+    "o_u8pf8": {"x16s": (8, 8, 1024)},
+    "o_u4pf4_256": {"x16s": (4, 4, 256)},
+    "o_u2pf8_256": {"x16s": (2, 8, 256)},
+    "o_u4pf4_384": {"x16s": (4, 4, 384)},
     "best": BEST,
     "best_head_pf4": {**BEST, "norm_f32": (4, 4, 256)},
     "best_q2pf8": {**BEST, "qkv": (2, 8, 1024)},

@@ -350,7 +350,7 @@ def test_rope_kv_fused_qkv_and_silu_mul_rows(cuda, dt):
     torch.testing.assert_close(act.float(), ref, **_tol(dt))
 
 GEMV_DEFAULTS = {"qkv": (2, 4, 1024), "swiglu": (2, 4, 512), "x16": (4, 4, 1024),
-                 "norm_f32": (4, 4, 256)}
+                 "norm_f32": (4, 4, 256), "x16s": (4, 4, 1024)}
 
 
 @pytest.fixture
