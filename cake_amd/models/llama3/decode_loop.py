@@ -117,7 +117,9 @@ def _run_native(dec: DeviceDecoder, n_steps: int, eos_ids, on_token) -> DecodeSt
     from ...ops import graph_loop as GL
     st = DecodeStats()
     k = dec.k
-    base = int(dec.bufs.hist_len.item())
+    # the device history holds one token per position up to the current one: its
+    # length is host_pos + 1 (no device read-back — a sync — inside the timed loop)
+    base = dec.host_pos + 1
     room = min(dec.bufs.hist.numel() - base, dec.m.stack.max_seq - 1 - dec.host_pos)
     n = min(n_steps, room // k * k)
     if n <= 0:
