@@ -24,8 +24,10 @@ timed region and exactly K decode steps are timed.
   the ranks in sequence): the curve is strong scaling of ONE decode stream.
   Extra fields (``--no-extras`` skips them): ``tp`` = tensor parallelism
   (beyond the reference: every rank streams 1/N of every layer, device-side
-  all-reduces over xGMI) and ``llama3_70b`` = the same two modes for 70B — the
-  BASELINE's "70B 8-worker" point is ``llama3_70b.pp`` at N = 8.
+  all-reduces over xGMI), ``pp_streams`` = the same layer-sharded pipeline with N
+  independent batch-1 sequences in flight (one per stage: the pipeline's aggregate
+  serving throughput) and ``llama3_70b`` = pp / tp for 70B — the BASELINE's "70B
+  8-worker" point is ``llama3_70b.pp`` at N = 8.
 
 Weights are random-init of the named architecture (no network, no checkpoints);
 EOS is ignored so exactly K tokens are generated.
@@ -209,9 +211,9 @@ def _summary(r: dict | None) -> dict | None:
     """Compact sub-record of one extra measurement."""
     if r is None:
         return None
-    keep = _MAIN_KEYS + ("hop", "hop_us", "hops_per_token", "allreduce", "allreduce_us",
-                         "layers_per_rank", "hbm_peak_mib_max_rank", "hbm_peak_mib",
-                         "ttft_ms_prefill")
+    keep = _MAIN_KEYS + ("streams", "per_stream_tokens_per_sec", "hop", "hop_us",
+                         "hops_per_token", "allreduce", "allreduce_us", "layers_per_rank",
+                         "hbm_peak_mib_max_rank", "hbm_peak_mib", "ttft_ms_prefill")
     return {k: r[k] for k in keep if k in r}
 
 
@@ -220,7 +222,10 @@ def _extra_runs(a):
     if a.no_extras or a.cpu or a.model != "llama3-8b":
         return []
     other = "tp" if a.parallel == "pp" else "pp"
-    return [((other,), "llama3-8b", other), (("llama3_70b", "pp"), "llama3-70b", "pp"),
+    # pp_streams: the same layer-sharded pipeline with one sequence in flight per stage
+    # (N independent batch-1 requests; aggregate tok/s — the pipeline's serving throughput)
+    return [((other,), "llama3-8b", other), (("pp_streams",), "llama3-8b", "pp_streams"),
+            (("llama3_70b", "pp"), "llama3-70b", "pp"),
             (("llama3_70b", "tp"), "llama3-70b", "tp")]
 
 
@@ -253,10 +258,17 @@ def bench_multi(a) -> None:
     from cake_amd.parallel.tp_bench import measure_tp, tp_supported
     env = DistEnv(a)
     try:
-        measure = {"pp": measure_pipeline, "tp": measure_tp}
+        def measure_streams(a_, env_, model, steps, warmup):
+            import copy
+            a2 = copy.copy(a_)
+            a2.streams = env_.world
+            return measure_pipeline(a2, env_, model, steps, warmup)
+        measure = {"pp": measure_pipeline, "tp": measure_tp, "pp_streams": measure_streams}
         head = measure[a.parallel](a, env, a.model, a.steps, a.warmup, a.dump_tokens)
         extra = {}
         for path, model, mode in _extra_runs(a):
+            if mode == "pp_streams" and (env.world == 1 or a.streams == env.world):
+                continue
             if mode == "tp" and not tp_supported(model, env.world):
                 r = {"skipped": f"tp{env.world} does not divide the KV heads"}
             else:
