@@ -89,29 +89,24 @@ __device__ __forceinline__ void attn2_decode_block(const AttnDecArgs& a, int g, 
   const uint16_t* kgp = a.kc + (size_t)g * a.S * HD;
   const uint16_t* vgp = a.vc + (size_t)g * a.S * HD;
 
-  // one block's operands: K A-fragments and V rows of this lane; two blocks in flight
-  // (kf/vf the next block of this wave, kf2/vf2 the one after)
-  uint4 kf[DS], vf[KPL], kf2[DS], vf2[KPL];
-  auto load_into = [&](int key0, int last, uint4 (&kd)[DS], uint4 (&vd)[KPL]) {
+  // one block's operands: K A-fragments and V rows of this lane
+  uint4 kf[DS], vf[KPL];
+  auto load_blk = [&](int key0, int last) {
 #pragma unroll
     for (int d = 0; d < DS; ++d) {
       const int r = min(key0 + col, last);
-      kd[d] = *reinterpret_cast<const uint4*>(kgp + (size_t)r * HD + d * 32 + rg * 8);
+      kf[d] = *reinterpret_cast<const uint4*>(kgp + (size_t)r * HD + d * 32 + rg * 8);
     }
 #pragma unroll
     for (int j = 0; j < KPL; ++j) {
       const int r = min(key0 + kg * KPL + j, last);
-      vd[j] = *reinterpret_cast<const uint4*>(vgp + (size_t)r * HD + ch * 8);
+      vf[j] = *reinterpret_cast<const uint4*>(vgp + (size_t)r * HD + ch * 8);
     }
   };
-  auto load_blk = [&](int key0, int last) { load_into(key0, last, kf, vf); };
 
   // split 0 starts at key 0: its first blocks are requested with the position
   // (rows clamped to the cache; dead rows are masked / zeroed below)
-  if (s == 0) {
-    load_blk(wave * kBlk, a.S - 1);
-    load_into((wave + NW) * kBlk, a.S - 1, kf2, vf2);
-  }
+  if (s == 0) load_blk(wave * kBlk, a.S - 1);
   // q (f32, roped) -> pre-scaled 16-bit B fragments: column col = head g*NREP + col
   uint4 qf[DS];
   {
@@ -154,21 +149,17 @@ __device__ __forceinline__ void attn2_decode_block(const AttnDecArgs& a, int g, 
     for (int e = 0; e < 8; ++e) o[h][e] = 0.f;
 
   int b = wave;
-  if (s != 0) {
-    if (b < nblk) load_blk(kb + b * kBlk, ke - 1);
-    if (b + NW < nblk) load_into(kb + (b + NW) * kBlk, ke - 1, kf2, vf2);
-  }
+  if (s != 0 && b < nblk) load_blk(kb + b * kBlk, ke - 1);
   ATTN_STAMP(2);
   for (; b < nblk; b += NW) {
     const int key0 = kb + b * kBlk;
-    // this block's operands; the next one moves up and the one after is requested, so
-    // two blocks' loads stay in flight behind this block's math
+    // this block's operands, then the next block's loads in flight
     uint4 kc[DS], vc[KPL];
 #pragma unroll
-    for (int d = 0; d < DS; ++d) { kc[d] = kf[d]; kf[d] = kf2[d]; }
+    for (int d = 0; d < DS; ++d) kc[d] = kf[d];
 #pragma unroll
-    for (int j = 0; j < KPL; ++j) { vc[j] = vf[j]; vf[j] = vf2[j]; }
-    if (b + 2 * NW < nblk) load_into(key0 + 2 * NW * kBlk, ke - 1, kf2, vf2);
+    for (int j = 0; j < KPL; ++j) vc[j] = vf[j];
+    if (b + NW < nblk) load_blk(key0 + NW * kBlk, ke - 1);
     // scores: S[key 4 rg + e][col]
     cf32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
