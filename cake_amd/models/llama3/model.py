@@ -191,7 +191,8 @@ class DeviceDecoder:
         """Greedy argmax with no device parameter block: the fused head_select tail."""
         from ...ops import hip as K
         return (self.greedy and self.sampling is None and self.params is None
-                and self.last_n <= K.HEAD_SELECT_MAX_LAST_N and self._fuse_tail)
+                and (self.penalty == 1.0 or self.last_n <= K.HEAD_SELECT_MAX_LAST_N)
+                and self._fuse_tail)
 
     def set_sampling(self, sampling) -> None:
         """Per-request sampling configuration (None / temperature <= 0 = greedy).  The

@@ -340,7 +340,7 @@ class PipelineEngine:
         elif k == R + 1:
             b = st.bufs
             if (self.sampler is None and self.sampling is None and self.sample_params is None
-                    and self.last_n <= K.HEAD_SELECT_MAX_LAST_N
+                    and (self.penalty == 1.0 or self.last_n <= K.HEAD_SELECT_MAX_LAST_N)
                     and os.environ.get("CAKE_FUSED_HEAD", "1") != "0"):
                 # greedy: lm_head + penalty + argmax + finalize in one launch
                 K.head_select(st.resid, self.head.norm, self.cfg.rms_norm_eps,
