@@ -13,9 +13,12 @@
 //     repeat_kv is never materialised.
 //   * Decode is flash-decoding with the split count chosen on device from the
 //     live length (so one captured launch serves every position): each
-//     workgroup streams its key range in 64-key chunks, computes a local
-//     softmax and P·V in f32, and the last-arriving split merges the
-//     (max, sum, o[hd]) partials (one launch per layer).
+//     workgroup streams its key range, computes a local softmax and P·V in f32,
+//     and the (max, sum, o[hd]) partials are merged inside the same launch —
+//     core 2 (default, attn_core2.h): 16-key blocks per wave, one split up to 320
+//     keys, else ~16 splits whose partials go out as epoch-tagged granules that
+//     split 0 polls and merges; core 1 (attn_core.h): 64-key LDS chunks, the
+//     last-arriving split merges behind a ticket.
 //   * Prefill attention is the MFMA flash kernel (flash_attn.hip).
 #include "attn_core.h"
 #include "attn_core2.h"
