@@ -167,7 +167,7 @@ def bench_pipeline(a, emit) -> None:
                  {k: v for k, v in r.items() if k not in ("tokens_per_sec", "ms_per_step",
                                                            "p50_token_latency_ms",
                                                            "p99_token_latency_ms")}
-                 | {"scaling": "weak" if r["streams"] == env.world else "strong"})
+                 | {"scaling": "weak" if env.world > 1 and r["streams"] == env.world else "strong"})
         dist.barrier()
     finally:
         dist.destroy_process_group()
