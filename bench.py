@@ -281,7 +281,8 @@ def bench_multi(a) -> None:
         if env.rank == 0:
             rest = {k: v for k, v in head.items() if k not in _MAIN_KEYS}
             if a.parallel == "pp":
-                rest["scaling"] = "weak" if env.world > 1 and head["streams"] == env.world else "strong"
+                weak = env.world > 1 and head["streams"] == env.world
+                rest["scaling"] = "weak" if weak else "strong"
             _emit(a, head["tokens_per_sec"], head["ms_per_step"], head["p50_token_latency_ms"],
                   head["p99_token_latency_ms"], env.world, {**rest, **extra})
         dist.barrier()
