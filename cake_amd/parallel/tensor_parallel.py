@@ -607,6 +607,11 @@ class TPEngine:
                        self.kc[s], self.vc[s])
             K.attn_decode(b.q, self.kc[s], self.vc[s], b.pos, self.scale, b.part, b.tickets,
                           b.attn_out)
+            if comm.world == 1:  # nothing to reduce: accumulate in place (no sum launch)
+                K.gemv(b.attn_out, w.wo, b.resid, accumulate=True)
+                K.swiglu(b.resid, w.ln2, eps, w.wg, w.wu, b.act)
+                K.gemv(b.act, w.wd, b.resid, accumulate=True)
+                continue
             K.gemv(b.attn_out, w.wo, b.partial, accumulate=False)
             comm.sum_(b.partial, b.resid, accumulate=True)
             K.swiglu(b.resid, w.ln2, eps, w.wg, w.wu, b.act)
