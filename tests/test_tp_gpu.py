@@ -73,10 +73,10 @@ def _reference(world):
     return PROMPT + [first] + run_decode(dec, STEPS).tokens
 
 
-@pytest.mark.parametrize("mode,world", [("ipc", 2), ("dist", 2), ("ipc", 4)])
+@pytest.mark.parametrize("mode,world", [("ipc", 2), ("dist", 2), ("ipc", 4), ("dist", 1)])
 def test_tp_matches_single_gpu(cuda, mode, world):
     """world ranks share cuda:0 (a 4-rank run exercises the all-reduce kernels' bank /
-    peer indexing beyond a pair)."""
+    peer indexing beyond a pair; one rank takes the in-place accumulate path)."""
     import torch.multiprocessing as mp
     ref = _reference(world)
     ctx = mp.get_context("spawn")
