@@ -23,6 +23,7 @@ concurrent masters on one worker (worker.rs:52-72) and are reset explicitly
 from __future__ import annotations
 
 import math
+import os
 from collections import OrderedDict
 
 import torch
@@ -91,6 +92,11 @@ class LayerStack:
         self._hostpos_bufs: DecodeBuffers | None = None
         self.step_graphs = False  # T = 1 forward() as graph replays (worker serving)
         self._step_graph_cache: dict = {}
+        # persistent decode (decode_mk.hip): one launch per token step instead of five
+        # per layer; CAKE_MK=0 keeps the per-layer launches
+        self.use_mk = os.environ.get("CAKE_MK", "0") != "0" and backend == "hip"
+        self._mk_ok: bool | None = None
+        self._mk_tables: dict = {}
 
     # ------------------------------------------------------------------ sessions
     def cache(self, session: int = 0) -> KVCache:
@@ -99,6 +105,8 @@ class LayerStack:
             while len(self._sessions) >= self.max_sessions:
                 old, _ = self._sessions.popitem(last=False)
                 self._drop_step_graphs(old)  # their graphs point at the evicted cache
+                for k in [k for k in self._mk_tables if k[0] == old]:
+                    del self._mk_tables[k]
             kv = KVCache(len(self.weights), self.cfg, self.max_seq, self.device, self.dtype)
             self._sessions[session] = kv
         else:
@@ -115,6 +123,8 @@ class LayerStack:
     def drop(self, session: int) -> None:
         self._sessions.pop(session, None)
         self._drop_step_graphs(session)
+        for k in [k for k in self._mk_tables if k[0] == session]:
+            del self._mk_tables[k]
 
     @property
     def layer_ids(self) -> list[int]:
@@ -153,13 +163,76 @@ class LayerStack:
         kv.length = max(kv.length, pos0 + T)
         return hidden
 
+    def mk_enabled(self) -> bool:
+        """Whether decode steps run as ONE persistent launch (decode_mk.hip)."""
+        if not self.use_mk:
+            return False
+        if self._mk_ok is None:
+            from ...ops import hip as K
+            cfg = self.cfg
+            self._mk_ok = bool(torch.cuda.is_available() and self.device.type == "cuda"
+                               and K.mk_supported(cfg.hidden_size, cfg.intermediate_size,
+                                                  cfg.num_attention_heads,
+                                                  cfg.num_key_value_heads, cfg.head_dim))
+        return self._mk_ok
+
+    def mk_table(self, layers: list[int], session: int = 0) -> torch.Tensor:
+        """int64 [len(layers), 8] device pointer table of the persistent decode:
+        ln1, wqkv, wo, ln2, wgu, wd and the session's K/V cache of each layer."""
+        key = (session, tuple(layers))
+        t = self._mk_tables.get(key)
+        if t is None:
+            kv = self.cache(session)
+            rows = []
+            for li in layers:
+                w, s = self.weights[li], self.slot_of[li]
+                rows.append([w.ln1.data_ptr(), w.wqkv.data_ptr(), w.wo.data_ptr(),
+                             w.ln2.data_ptr(), w.wgu.data_ptr(), w.wd.data_ptr(),
+                             kv.k[s].data_ptr(), kv.v[s].data_ptr()])
+            t = torch.tensor(rows, dtype=torch.int64).to(self.device)
+            self._mk_tables[key] = t
+        return t
+
+    def mk_workspace(self, bufs: DecodeBuffers) -> tuple[torch.Tensor, torch.Tensor]:
+        """The persistent decode's granule workspace and control words (zeroed once;
+        sized for every local layer, so any run of them can use it)."""
+        if getattr(bufs, "mk_gran", None) is None:
+            from ...ops import hip as K
+            cfg = self.cfg
+            words = len(self.weights) * K.mk_gstride(cfg.hidden_size, cfg.intermediate_size,
+                                                     cfg.num_attention_heads,
+                                                     cfg.num_key_value_heads, cfg.head_dim)
+            bufs.mk_gran = torch.zeros(words, dtype=torch.int64, device=self.device)
+            bufs.mk_ctl = torch.zeros(K.MK_CTL_WORDS, dtype=torch.int32, device=self.device)
+        return bufs.mk_gran, bufs.mk_ctl
+
+    def mk_check(self, bufs: DecodeBuffers) -> None:
+        """Raise if a persistent-decode launch gave up waiting (bounded spins)."""
+        ctl = getattr(bufs, "mk_ctl", None)
+        if ctl is None:
+            return
+        from ...ops import hip as K
+        site = K.mk_error(ctl)
+        if site:
+            ctl.zero_()
+            raise RuntimeError(f"persistent decode: a hand-off timed out (site {site}); "
+                               "outputs of that launch are invalid")
+
     def decode_step(self, bufs: DecodeBuffers, layers: list[int], session: int = 0) -> None:
         """Graph-capturable T=1 step over bufs.resid at device position bufs.pos (hip only):
-        five launches per layer (QKV+RoPE+KV write, attention, o_proj+residual,
+        ONE persistent launch for all `layers` when the shapes allow (decode_mk.hip),
+        else five launches per layer (QKV+RoPE+KV write, attention, o_proj+residual,
         norm+gate/up+SwiGLU, down_proj+residual)."""
         from ...ops import hip as K
-        kv = self.cache(session)
         cfg = self.cfg
+        if layers and self.mk_enabled():
+            gran, ctl = self.mk_workspace(bufs)
+            K.mk_decode(self.dtype, self.mk_table(layers, session), len(layers), cfg.hidden_size,
+                        cfg.intermediate_size, cfg.num_attention_heads, cfg.num_key_value_heads,
+                        cfg.head_dim, self.max_seq, cfg.rms_norm_eps, self.scale, self.inv_freq,
+                        bufs.pos, bufs.resid, gran, ctl)
+            return
+        kv = self.cache(session)
         for li in layers:
             w = self.weights[li]
             s = self.slot_of[li]

@@ -91,7 +91,7 @@ def kernels():
             for name, argtypes in _SIGS.items():
                 fn = getattr(lib, name)
                 fn.argtypes = argtypes
-                fn.restype = C.c_int
+                fn.restype = _RESTYPE.get(name, C.c_int)
             _lib = lib
     return _lib
 
@@ -123,3 +123,12 @@ _SIGS.update({
     "cake_conv2d_nhwc": [I, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, P],
     "cake_conv2d_nhwc2": [I, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, P],
 })
+
+_SIGS.update({
+    "cake_mk_gstride": [I, I, I, I, I],
+    "cake_mk_grid": [],
+    "cake_mk_supported": [I, I, I, I, I],
+    "cake_mk_decode": [I, P, I, I, I, I, I, I, I, F, F, P, P, P, P, P, C.c_double, P],
+})
+_RESTYPE = {"cake_mk_gstride": C.c_longlong}
+_SIGS["cake_mk_set_stamps"] = [P]

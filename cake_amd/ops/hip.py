@@ -180,6 +180,57 @@ def attn_decode(q, kcache, vcache, pos, scale, part, tickets, out):
           "attn_decode")
 
 
+# ---------------------------------------------------------------------------
+# persistent decode (decode_mk.hip): every layer of one token in one launch
+# ---------------------------------------------------------------------------
+
+MK_LAYER_PTRS = 8  # ln1, wqkv, wo, ln2, wgu, wd, kc, vc
+MK_CTL_WORDS = 4   # epoch, exit ticket, error flag, error site
+
+
+def mk_supported(H: int, I: int, nh: int, nkv: int, hd: int) -> bool:
+    """Shapes the persistent decode kernel handles on this device (H, I, nh*hd
+    multiples of 512; head_dim 128; GQA group 4 or 8)."""
+    return kernels().cake_mk_supported(int(H), int(I), int(nh), int(nkv), int(hd)) == 0
+
+
+def mk_gstride(H: int, I: int, nh: int, nkv: int, hd: int) -> int:
+    """Granule words (8 bytes) per layer of the persistent-decode workspace."""
+    return int(kernels().cake_mk_gstride(int(H), int(I), int(nh), int(nkv), int(hd)))
+
+
+def mk_decode(dtype, table, n_layers: int, H: int, I: int, nh: int, nkv: int, hd: int, S: int,
+              eps: float, scale: float, inv_freq, pos, resid, gran, ctl,
+              timeout_s: float = 2.0) -> None:
+    """One decode token through `n_layers` layers in ONE launch (decode_mk.hip).
+
+    table: int64 [n_layers, 8] device pointers (ln1, wqkv, wo, ln2, wgu, wd, kc, vc);
+    resid: f32 [H] — the layer-0 input, overwritten with the last layer's output;
+    gran: int64 [n_layers * mk_gstride(...)] and ctl: int32 [4], both zeroed once
+    (the kernel keeps them consistent across launches; a bounded spin that gives up
+    sets ctl[2] — see :func:`mk_error`)."""
+    _req(table, "table", dtype=torch.int64, shape=(n_layers, MK_LAYER_PTRS))
+    _req(inv_freq, "inv_freq", dtype=torch.float32, shape=(hd // 2,))
+    _req(pos, "pos", dtype=torch.int32, numel=1)
+    _req(resid, "resid", dtype=torch.float32, numel=H)
+    _req(gran, "gran", dtype=torch.int64, numel=n_layers * mk_gstride(H, I, nh, nkv, hd))
+    _req(ctl, "ctl", dtype=torch.int32, numel=MK_CTL_WORDS)
+    if not mk_supported(H, I, nh, nkv, hd):
+        raise ValueError(f"persistent decode does not support H={H} I={I} nh={nh} "
+                         f"nkv={nkv} hd={hd}")
+    check(kernels().cake_mk_decode(_DT[dtype], _p(table), int(n_layers), int(H), int(I), int(nh),
+                                   int(nkv), int(hd), int(S), float(eps), float(scale),
+                                   _p(inv_freq), _p(pos), _p(resid), _p(gran), _p(ctl),
+                                   float(timeout_s), _stream()),
+          "mk_decode")
+
+
+def mk_error(ctl) -> int:
+    """Nonzero site code when a persistent-decode spin gave up (host sync)."""
+    c = ctl.cpu()
+    return int(c[3]) if int(c[2]) != 0 else 0
+
+
 def attn_workspace_numel(nh: int, hd: int, S: int) -> int:
     """f32 elements of the partials of at most 64 splits per head (attention.hip
     kMaxSplit): core 2 stores each value as an 8-byte {value, tag} granule."""
