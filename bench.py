@@ -71,6 +71,12 @@ def _args(argv=None):
                     help="skip the N=1 Stable Diffusion seconds/step sub-record")
     ap.add_argument("--no-extras", action="store_true",
                     help="headline only: skip the tp / llama3_70b sub-records")
+    ap.add_argument("--tiny-extras", action="store_true",
+                    help="run every sub-record (tp, pp_streams, 70B pp/tp, split SD) on the "
+                         "tiny presets: the N-rank plumbing of the full default bench, cheap "
+                         "enough for CPU (gloo) tests")
+    ap.add_argument("--sd-steps", type=int, default=4,
+                    help="N>1: timed diffusion steps of the split-UNet sd sub-record")
     ap.add_argument("--allreduce", default="ipc", choices=["ipc", "dist"],
                     help="tp all-reduce: device-side one-shot kernels over xGMI, or "
                          "torch.distributed")
@@ -217,16 +223,25 @@ def _summary(r: dict | None) -> dict | None:
     return {k: r[k] for k in keep if k in r}
 
 
+def _extras_on(a) -> bool:
+    """Sub-records next to the headline: the full default bench (8B headline on the
+    GPU), or the tiny presets with --tiny-extras (CPU plumbing)."""
+    if a.no_extras:
+        return False
+    return bool(a.tiny_extras) or (not a.cpu and a.model == "llama3-8b")
+
+
 def _extra_runs(a):
     """(key path, model, mode) of the sub-records next to the headline."""
-    if a.no_extras or a.cpu or a.model != "llama3-8b":
+    if not _extras_on(a):
         return []
+    m8, m70 = ("tiny-kv2", "tiny") if a.tiny_extras else ("llama3-8b", "llama3-70b")
     other = "tp" if a.parallel == "pp" else "pp"
     # pp_streams: the same layer-sharded pipeline with one sequence in flight per stage
     # (N independent batch-1 requests; aggregate tok/s — the pipeline's serving throughput)
-    return [((other,), "llama3-8b", other), (("pp_streams",), "llama3-8b", "pp_streams"),
-            (("llama3_70b", "pp"), "llama3-70b", "pp"),
-            (("llama3_70b", "tp"), "llama3-70b", "tp")]
+    return [((other,), m8, other), (("pp_streams",), m8, "pp_streams"),
+            (("llama3_70b", "pp"), m70, "pp"),
+            (("llama3_70b", "tp"), m70, "tp")]
 
 
 def bench_single(a) -> None:
@@ -278,6 +293,17 @@ def bench_multi(a) -> None:
                 for k in path[:-1]:
                     d = d.setdefault(k, {})
                 d[path[-1]] = r
+        if _extras_on(a) and not a.no_sd:
+            # BASELINE config 5: SDXL 1024^2 (CFG) with the UNet's block groups split over
+            # the N ranks; seconds per diffusion step of one image (parallel/sd_split.py)
+            from cake_amd.parallel.sd_split import measure_sd_split
+            key = "sdxl_tiny_split" if a.tiny_extras else "sdxl_1024_split"
+            try:
+                r = measure_sd_split(env, steps=a.sd_steps, warmup=2, tiny=a.tiny_extras)
+            except Exception as e:  # noqa: BLE001  (setup failures are symmetric: all ranks)
+                r = {"error": f"{type(e).__name__}: {e}"[:300]}
+            if env.rank == 0:
+                extra["sd"] = {key: r}
         if env.rank == 0:
             rest = {k: v for k, v in head.items() if k not in _MAIN_KEYS}
             if a.parallel == "pp":

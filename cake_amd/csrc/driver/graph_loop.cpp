@@ -161,6 +161,15 @@ CAKE_API int cake_graph_decode(const CakeLoopSpec* s, CakeLoopResult* r) {
   int announced = 0;       // replays announced to the workers
   int pending = -1;        // replay index waiting for read-back
   bool stop = false;
+  hipError_t err = hipSuccess;  // first failure inside the loop (cleanup below)
+#define CAKE_LOOP_TRY(x)            \
+  do {                              \
+    const hipError_t e_ = (x);      \
+    if (e_ != hipSuccess) {         \
+      err = e_;                     \
+      goto loop_end;                \
+    }                               \
+  } while (0)
   while (!stop) {
     int cur = -1;
     if (issued < replays) {
@@ -168,25 +177,25 @@ CAKE_API int cake_graph_decode(const CakeLoopSpec* s, CakeLoopResult* r) {
       // the next chunk enqueued before the master reaches it
       while (s->announce && announced < replays && announced - issued <= chunk) {
         const int c = chunk < replays - announced ? chunk : replays - announced;
-        if (s->announce(s->announce_ctx, announced, c) != 0) return (int)hipErrorUnknown;
+        if (s->announce(s->announce_ctx, announced, c) != 0) CAKE_LOOP_TRY(hipErrorUnknown);
         announced += c;
       }
-      CAKE_TRY(launch());
+      CAKE_LOOP_TRY(launch());
       const int slot = issued & 1;
       if (readback) {
         const int lo = s->base + issued * k;
-        CAKE_TRY(hipMemcpyAsync(ring.host + slot * k, s->hist + lo, sizeof(int32_t) * k,
-                                hipMemcpyDeviceToHost, st));
+        CAKE_LOOP_TRY(hipMemcpyAsync(ring.host + slot * k, s->hist + lo, sizeof(int32_t) * k,
+                                     hipMemcpyDeviceToHost, st));
       }
-      CAKE_TRY(hipEventRecord(ring.ev[issued % 3], st));
+      CAKE_LOOP_TRY(hipEventRecord(ring.ev[issued % 3], st));
       cur = issued++;
     }
     if (pending >= 0) {
       const int slot = pending & 1;
       hipEvent_t done = ring.ev[pending % 3];
-      CAKE_TRY(hipEventSynchronize(done));
+      CAKE_LOOP_TRY(hipEventSynchronize(done));
       float ms = 0.f;
-      CAKE_TRY(hipEventElapsedTime(&ms, prev_done, done));
+      CAKE_LOOP_TRY(hipEventElapsedTime(&ms, prev_done, done));
       ms /= (float)k;
       const int have = s->n - pending * k;
       const int m = have < k ? have : k;
@@ -209,10 +218,25 @@ CAKE_API int cake_graph_decode(const CakeLoopSpec* s, CakeLoopResult* r) {
     pending = cur;
     if (pending < 0) break;
   }
+loop_end:
+#undef CAKE_LOOP_TRY
   // replays announced to the workers but not yet issued (a stop inside an announced
-  // chunk) still run, unread: every rank must replay the same number of hops
-  for (; issued < announced; ++issued) CAKE_TRY(launch());
-  CAKE_TRY(hipStreamSynchronize(st));
+  // chunk, or an error) still run, unread: every rank must replay the same number of
+  // hops, or the workers wait in device-side receives until their hop timeout.  Then
+  // drain the stream before returning, so no read-back into the thread-local pinned
+  // ring is still in flight when the next call reuses it.
+  for (; issued < announced; ++issued) {
+    const hipError_t e = launch();
+    if (e != hipSuccess) {
+      if (err == hipSuccess) err = e;
+      break;
+    }
+  }
+  {
+    const hipError_t e = hipStreamSynchronize(st);
+    if (err == hipSuccess) err = e;
+  }
+  if (err != hipSuccess) return fail(err);
   r->replays = issued;
   r->pos = pos;
   r->stopped = stop ? 1 : 0;

@@ -35,6 +35,7 @@ static int g_attn_target = 16;
 // tail (partials out, polled back in: ~6.5k cycles, profiles/r3_attn_stamps_granule_v2.jsonl)
 // costs what ~240 more keys of one split's loop cost (~27 cycles per key)
 static int g_attn_single = 320;
+static int g_attn_drop_partials = 0;  // test hook (cake_attn_debug_drop_partials)
 
 template <int DT, int HD, int NREP>
 __global__ __launch_bounds__(AttnGeom<NREP>::NT) void attn_decode_kernel(AttnDecArgs a) {
@@ -108,16 +109,44 @@ CAKE_API int cake_attn_set_single_max(int keys) {
   return 0;
 }
 
+// Test hook: core 2's splits >= 1 skip publishing their partials, so split 0's merge
+// runs into its poll bound and must raise the error word (tests/test_kernels_gpu.py).
+CAKE_API int cake_attn_debug_drop_partials(int on) {
+  g_attn_drop_partials = on != 0;
+  return 0;
+}
+
 CAKE_API int cake_attn_set_min_keys(int min_keys) {
   if (min_keys < kChunk || min_keys % kChunk) return (int)hipErrorInvalidValue;
   g_attn_min_keys = min_keys;
   return 0;
 }
 
+// Core 2's split 0 spins on the partials of the other splits of its head, so every
+// workgroup of the grid must be resident at once; a grid larger than the device can hold
+// (several waves per CU taken by other work would not be visible here, but a grid the
+// empty device cannot hold is refused) runs core 1's last-arriver merge instead.
+template <class K>
+static bool grid_resident(K kern, int threads, long long blocks) {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return false;
+  }
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, threads, 0) !=
+      hipSuccess)
+    return false;
+  return (long long)per_cu * cus >= blocks;
+}
+
 template <int DT, int HD>
 static int launch_decode(int n_rep, dim3 grid, hipStream_t st, const AttnDecArgs& a) {
 #define CAKE_DEC(NR)                                                                          \
-  if (g_attn_impl == 2)                                                                       \
+  if (g_attn_impl == 2 &&                                                                     \
+      grid_resident(attn2_decode_kernel<DT, HD, NR>, AttnGeom<NR>::NT, (long long)grid.x * grid.y)) \
     hipLaunchKernelGGL((attn2_decode_kernel<DT, HD, NR>), grid, dim3(AttnGeom<NR>::NT), 0, st, a); \
   else                                                                                        \
     hipLaunchKernelGGL((attn_decode_kernel<DT, HD, NR>), grid, dim3(AttnGeom<NR>::NT), 0, st, a)
@@ -142,7 +171,7 @@ CAKE_API int cake_attn_decode(int dt, const float* q, const void* kc, const void
   const AttnDecArgs a{q, (const uint16_t*)kc, (const uint16_t*)vc, pos, S,
                       scale * 1.4426950408889634f, part, tickets, (uint16_t*)out,
                       g_attn_min_keys, splits, g_attn_stamps, g_attn_target,
-                      g_attn_single};
+                      g_attn_single, g_attn_drop_partials};
   DISPATCH_DT_HD(dt, hd, return (launch_decode<DT, HD>(nh / nkv, grid, st, a)));
   return (int)hipErrorInvalidValue;
 }

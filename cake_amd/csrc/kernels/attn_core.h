@@ -98,12 +98,13 @@ struct AttnDecArgs {
   int S;
   float scale_log2;
   float* part;             // [nh][kMaxSplit][hd+2] f32
-  unsigned int* tickets;   // [nkv], zero between launches
+  unsigned int* tickets;   // [2 nkv + 2]: arrival tickets / epochs, then the error word
   uint16_t* out;           // [nh*hd]
   int min_keys, maxsplit;
   unsigned long long* stamps;  // diagnostics (nullptr in production): per-WG phase clocks
   int target;                  // core 2: splits aimed at (keys per split = Tk / target)
   int single;                  // core 2: live lengths up to this run as one split
+  int drop_partials;           // test hook: splits >= 1 never publish (forces a timeout)
 };
 
 // Phase clock of workgroup (g, s) for the latency breakdown (scripts/attn_stamps.py):

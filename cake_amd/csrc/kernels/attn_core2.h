@@ -33,8 +33,13 @@ namespace cake {
 
 constexpr int kBlk = 16;  // keys per wave block (MFMA M dimension)
 // bound on the merge's granule polls (s_sleep 1 apart): a producer that never publishes
-// ends the poll with a wrong output instead of a hung GPU
+// ends the poll instead of hanging the GPU, and sets the error word tickets[2 nkv]
+// (the output of that launch is invalid; the host raises on it: ops.hip.attn_error)
 constexpr int kAttnMaxPolls = 1 << 20;
+
+__device__ __noinline__ void attn_poll_timeout(unsigned int* err) {
+  __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 template <int OFF> __device__ __forceinline__ float xor_max(float v) {
   static_assert(OFF == 16 || OFF == 32, "xor_max offset");
@@ -283,7 +288,7 @@ __device__ __forceinline__ void attn2_decode_block(const AttnDecArgs& a, int g, 
 #pragma unroll
     for (int i = 0; i < OPT; ++i) {
       const int idx = tid + i * NT;
-      if (idx < NOUT) {
+      if (idx < NOUT && !a.drop_partials) {
         const int h = idx / HD, d = idx - h * HD;
         unsigned long long* dst = gpart + ((size_t)(g * NREP + h) * kMaxSplit + s) * (HD + 2);
         if (d == 0) {
@@ -348,7 +353,11 @@ __device__ __forceinline__ void attn2_decode_block(const AttnDecArgs& a, int g, 
           ok = ok && (v[u][d] >> 32) == (tagw >> 32);
         }
       }
-      if (__builtin_amdgcn_ballot_w64(!ok) == 0ull || tries > kAttnMaxPolls) break;
+      if (__builtin_amdgcn_ballot_w64(!ok) == 0ull) break;
+      if (tries > kAttnMaxPolls) {
+        if (lane == 0) attn_poll_timeout(a.tickets + 2 * gridDim.x);
+        break;
+      }
       __builtin_amdgcn_s_sleep(1);
     }
     const float M = wave_max(mt);
@@ -379,7 +388,11 @@ __device__ __forceinline__ void attn2_decode_block(const AttnDecArgs& a, int g, 
             ok = ok && (v[u][d] >> 32) == (tagw >> 32);
           }
         }
-        if (__builtin_amdgcn_ballot_w64(!ok) == 0ull || tries > kAttnMaxPolls) break;
+        if (__builtin_amdgcn_ballot_w64(!ok) == 0ull) break;
+        if (tries > kAttnMaxPolls) {
+          if (lane == 0) attn_poll_timeout(a.tickets + 2 * gridDim.x);
+          break;
+        }
         __builtin_amdgcn_s_sleep(1);
       }
     }

@@ -6,44 +6,56 @@
 //   append, GQA softmax(QK^T)V, o_proj), mlp.rs:13-33 (SwiGLU), cache.rs:93-122.
 //
 // Why one launch: the five-launch layer (gemv.hip + attention.hip) streams each
-// weight matrix near the HBM rate, but every kernel boundary drains the chip:
-// the next launch's first weight bytes are requested only after the previous
-// launch's last wave has retired (~1.2-1.9 us per boundary, 160 per 8B token;
-// MI355X_MICROARCH "boundary").  Here each workgroup (one per CU, all resident)
-// requests its FIRST weight block of the next op before it waits for that op's
-// input vector, so the HBM stream runs through every dependency edge.
+// weight matrix near the HBM rate, but every kernel boundary drains the chip: the
+// next launch's first weight bytes are requested only after the previous launch's
+// last wave has retired (MI355X_MICROARCH "boundary", ~1.2-1.9 us, 160 per 8B token).
 //
-// Structure (G = #CUs workgroups of NW waves, one per CU):
-//   * op = QKV+RoPE | attention | o_proj+residual | RMSNorm+gate/up+SwiGLU |
-//     down_proj+residual.  A GEMV op's row pairs are split into contiguous
-//     per-workgroup ranges; inside a workgroup the (pair x 512-element K block)
-//     space is split evenly over the waves, each wave keeps U blocks of both rows
-//     in flight (double-buffered registers), partial dot products go to LDS per
-//     (pair, wave) and are summed in a fixed order (deterministic).
-//   * edges (the all-to-all dependencies): every output word is published as an
-//     8-byte {tag, value} granule with one agent-scope (sc1, write-through) store;
-//     consumers sweep the granules with agent-scope loads until every tag is this
-//     launch's (MI355X_MICROARCH "Valid forms" R2: the data is its own flag, no
-//     fences).  Each (layer, edge) has its own granule array; the tag is a launch
-//     epoch kept in device memory and advanced by the last workgroup to exit, so
-//     graph replays never see a previous launch's words.
-//   * attention: nkv x ns units (ns splits of the live keys, chosen on device
-//     from the position) run on workgroups spread over the XCDs; the
-//     workgroups holding split 0 (the mergers) skip o_proj, so the attention
-//     chain overlaps everyone else's o_proj weight prefetch.  Old keys come from
-//     the cache (written by earlier launches), the current position's key/value
-//     from the QKV granules.
-//   * every spin is bounded (s_memrealtime); a timeout sets an error word the
-//     host checks, and stops every later spin of the launch instead of hanging.
+// Engine (one workgroup of 8 waves per CU, all resident):
+//   * wave 7 is the LOADER: it streams this CU's weight rows of every op of every
+//     layer, in order, into an LDS ring of 16 KB slots with LDS-DMA
+//     (global_load_lds, nt), keeping up to 4 slots in flight and publishing each
+//     landed slot with an LDS word.  It never waits for activations, so the HBM
+//     stream runs on through every dependency edge until the ring is full
+//     (MI355X_MICROARCH "prefetch-credit", "ldsdma-fill").
+//   * waves 0-6 are CONSUMERS: slot i goes to consumer i % 7; a consumer copies its
+//     slot to registers, frees it, and takes dot products (v_dot2 f32 <- 2 x 16-bit)
+//     with the op's input row, which is staged in LDS as 16-bit (the model dtype,
+//     as the reference's Linear sees it).  Partial sums go to LDS per (row pair,
+//     consumer) and are added in a fixed order (deterministic).
+//   * edges (all-to-all dependencies between ops): every output word is published as
+//     an 8-byte {tag, value} granule by one agent-scope (sc1, write-through) store;
+//     consumers load the granules of the next op's input and re-poll only the ones
+//     whose tag is not yet this launch's (MI355X_MICROARCH "Valid forms" R2: the data
+//     is its own flag, no fences).  While they gather, the loader keeps one slot in
+//     flight ("thinned"), so the gather's loads do not queue behind the ring fill.
+//     Each (layer, edge) has its own granule array; the tag is a launch epoch in
+//     device memory, advanced by the last workgroup to exit.
+//   * attention: nkv x ns units (ns splits of the live keys, chosen on device from
+//     the position) on workgroups spread over the XCDs; split 0 of each group merges
+//     and skips o_proj.  Old keys come from the cache, the current position's key /
+//     value from the QKV granules.
+//   * consumers synchronise among themselves with an LDS counter (the loader never
+//     joins a barrier); every global spin is bounded (s_memrealtime): a timeout sets
+//     an error word the host checks, and stops every later spin of the launch.
 #include "common.h"
 
 namespace cake {
 namespace mk {
 
 typedef unsigned long long u64;
-constexpr int kBlk = 512;    // K elements per weight block: 64 lanes x 8
-constexpr int kKeys = 16;    // keys per attention wave block (MFMA M)
+constexpr int kBlk = 512;       // K elements per row block (1 KB of 16-bit weights)
+constexpr int kKeys = 16;       // keys per attention wave block (MFMA M)
 constexpr int kMaxSplitMk = 16;
+constexpr int kMaxG = 512;
+constexpr int kNW = 8;          // waves per workgroup
+constexpr int kNL = 2;          // loader waves (the last kNL)
+constexpr int kNC = kNW - kNL;  // consumer waves 0 .. kNC-1
+constexpr int kNCT = kNC * 64;  // consumer threads
+constexpr int kJN = 22;         // residual-row words per consumer thread (H <= kJN * kNCT)
+constexpr int kSlot = 16384;    // ring slot bytes: 8 pair-blocks (row a + row b, 1 KB each)
+constexpr int kPB = 8;          // pair-blocks per slot
+constexpr int kFly = 3;         // slots the loader keeps in flight beyond the one it waits for
+constexpr int kMaxRing = 8;
 
 struct Layer {  // device-side pointer table, one entry per layer
   const uint16_t* ln1;
@@ -67,16 +79,15 @@ struct Args {
   long long gstride;
   unsigned* ctl;          // [0] epoch [1] exit ticket [2] error flag [3] error site
   int maxsplit, single, target, min_keys;
+  int ring;               // ring slots
+  int thin;               // loader keeps one slot in flight while consumers gather
   unsigned long long timeout;  // s_memrealtime ticks (100 MHz)
   unsigned long long* stamps;  // diagnostics (nullptr in production): per-WG phase clocks
 };
-constexpr int kStampsPerLayer = 10;
+constexpr int kStampsPerLayer = 14;  // 10 consumer + 4 loader phase clocks
 
 // granule offsets inside one layer's block (words)
-// sentinels: per edge one granule per producing workgroup (kMaxG slots)
-constexpr int kMaxG = 512;
-enum Edge { kERes = 0, kEQkv = 1, kEAtt = 2, kEMid = 3, kEAct = 4, kNumEdges = 5 };
-struct GOff { long long res, q, kv, att, mid, act, part, sent; };
+struct GOff { long long res, q, kv, att, mid, act, part; };
 __host__ __device__ inline GOff goff(int H, int I, int nh, int nkv, int hd, int maxsplit) {
   GOff o;
   o.res = 0;
@@ -86,37 +97,30 @@ __host__ __device__ inline GOff goff(int H, int I, int nh, int nkv, int hd, int 
   o.mid = o.att + (long long)nh * hd / 2;
   o.act = o.mid + H;
   o.part = o.act + I / 2;
-  o.sent = o.part + (long long)nh * maxsplit * (hd + 2);
   return o;
 }
 __host__ __device__ inline long long gstride_words(int H, int I, int nh, int nkv, int hd,
                                                    int maxsplit) {
   const GOff o = goff(H, I, nh, nkv, hd, maxsplit);
-  const long long n = o.sent + (long long)kNumEdges * kMaxG;
+  const long long n = o.part + (long long)nh * maxsplit * (hd + 2);
   return (n + 15) / 16 * 16;
 }
 
 // ---------------------------------------------------------------------------
 // global-address-space access: pointers read from the layer table are generic, and
-// generic (flat) loads count against lgkmcnt too, so every LDS wait would also wait
-// for the whole in-flight weight stream.  Every device-memory access below goes
+// generic (flat) loads count against lgkmcnt too.  Every device-memory access goes
 // through an address_space(1) pointer (global_load / global_store).
 // ---------------------------------------------------------------------------
 #define CAKE_G __attribute__((address_space(1)))
+#define CAKE_C __attribute__((address_space(4)))
 template <class T> __device__ __forceinline__ const CAKE_G T* gp(const T* p) {
   return (const CAKE_G T*)p;
 }
 template <class T> __device__ __forceinline__ CAKE_G T* gpw(T* p) { return (CAKE_G T*)p; }
-__device__ __forceinline__ uint4 ldg_nt16(const uint4* p) {
-  const u32x4 v = __builtin_nontemporal_load((const CAKE_G u32x4*)p);
-  return make_uint4(v.x, v.y, v.z, v.w);
-}
 __device__ __forceinline__ uint4 ldg16(const void* p) {
   const u32x4 v = *(const CAKE_G u32x4*)p;
   return make_uint4(v.x, v.y, v.z, v.w);
 }
-
-// granules
 __device__ __forceinline__ u64 gld(const u64* p) {
   return __hip_atomic_load(gp(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -133,6 +137,14 @@ __device__ __forceinline__ unsigned pack2(float a, float b, int dt) {
   const uint16_t x = dt == kBF16 ? f32_to_bf16(a) : f32_to_f16(a);
   const uint16_t y = dt == kBF16 ? f32_to_bf16(b) : f32_to_f16(b);
   return (unsigned)x | ((unsigned)y << 16);
+}
+// LDS words (ring control, consumer barrier): workgroup-scope atomics + LDS-only fences
+__device__ __forceinline__ unsigned lds_ld(const unsigned* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_st(unsigned* p, unsigned v) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 // threadIdx.x behind a volatile asm: lane-derived values are recomputed where used
@@ -161,7 +173,10 @@ __device__ __forceinline__ void poll(const u64* g, const int (&idx)[J], int n, u
                                      unsigned (&val)[J], const Args& a, Spin& sp, int site) {
   u64 v[J];
 #pragma unroll
-  for (int j = 0; j < J; ++j) v[j] = idx[j] < n ? gld(g + idx[j]) : ((u64)tag << 32);
+  for (int j = 0; j < J; ++j) v[j] = gld(g + (idx[j] < n ? idx[j] : 0));
+#pragma unroll
+  for (int j = 0; j < J; ++j)
+    if (idx[j] >= n) v[j] = (u64)tag << 32;
   if (!sp.dead) {
     for (unsigned it = 0;; ++it) {
       bool ok = true;
@@ -189,15 +204,29 @@ __device__ __forceinline__ void poll(const u64* g, const int (&idx)[J], int n, u
   for (int j = 0; j < J; ++j) val[j] = (unsigned)v[j];
 }
 
-// n granules of packed 16-bit pairs -> dst32[0..n) (LDS), all threads.
-template <int NT>
+// Consumer-only barrier: an LDS arrival counter (the loader wave never joins).
+struct CBar {
+  unsigned* cnt;
+  unsigned gen;
+};
+__device__ __forceinline__ void cbar(CBar& b) {
+  b.gen += kNC;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  if ((threadIdx.x & 63) == 0)
+    __hip_atomic_fetch_add(b.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  while (lds_ld(b.cnt) < b.gen) __builtin_amdgcn_s_sleep(0);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// n granules of packed 16-bit pairs -> dst32[0..n) (LDS), consumer threads.
 __device__ __forceinline__ void gather_u32(const u64* g, int n, unsigned tag, unsigned* dst,
                                            const Args& a, Spin& sp, int site) {
-  for (int base = 0; base < n; base += 8 * NT) {
+  const int ct = otid();
+  for (int base = 0; base < n; base += 8 * kNCT) {
     int idx[8];
     unsigned v[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) idx[j] = base + j * NT + otid();
+    for (int j = 0; j < 8; ++j) idx[j] = base + j * kNCT + ct;
     poll<8>(g, idx, n, tag, v, a, sp, site);
 #pragma unroll
     for (int j = 0; j < 8; ++j)
@@ -205,41 +234,29 @@ __device__ __forceinline__ void gather_u32(const u64* g, int n, unsigned tag, un
   }
 }
 
-// The poller wave: wait until the sentinels [0, n) of one edge carry `tag` (each
-// producing workgroup stores its sentinel after its data granules).  One wave polls
-// n words per pass instead of every thread polling every data granule — that storm of
-// agent-scope loads competed with the weight stream.  The data granules keep their
-// own tags, so a sentinel seen before some data (no store ordering is assumed) only
-// costs that thread a short re-poll in the sweep.
-__device__ __forceinline__ void wait_sent(const u64* sent, int n, unsigned tag, const Args& a,
-                                          Spin& sp, int site) {
-  const int lane = otid() & 63;
-  for (int base = 0; base < n; base += 4 * 64) {
-    int idx[4];
-    unsigned v[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) idx[j] = base + j * 64 + lane;
-    poll<4>(sent, idx, n, tag, v, a, sp, site);
-  }
-}
-
-// Residual row (H f32: granules, or plain memory written by an earlier launch)
-// -> raw[H] (LDS) and xs[H] = raw * rsqrt(mean(raw^2) + eps) * w (LDS).
-template <int DT, int NT, int J>
+// Residual row (H f32: granules, or plain memory written by an earlier launch) ->
+// xs[H] = model-dtype(raw * rsqrt(mean(raw^2) + eps) * w), and the f32 rows
+// [row_lo, row_lo + nrow) (the residual rows this workgroup's next epilogue adds to) into
+// rows[], consumer
+// threads; ends with a consumer barrier.
+template <int DT, int J>
 __device__ __forceinline__ void gather_norm(const u64* g, const float* plain, int H, unsigned tag,
-                                            const uint16_t* w, float eps, float* raw, float* xs,
-                                            float* red, const Args& a, Spin& sp, int site) {
+                                            const uint16_t* w, float eps, float* rows,
+                                            int row_lo, int nrow,
+                                            uint16_t* xs, float* red, CBar& cb, const Args& a,
+                                            Spin& sp, int site) {
+  const int ct = otid();
   int idx[J];
   unsigned v[J];
   float wv[J];
 #pragma unroll
   for (int j = 0; j < J; ++j) {
-    idx[j] = j * NT + otid();
-    wv[j] = idx[j] < H ? to_f32<DT>(gp(w)[idx[j]]) : 0.f;
+    idx[j] = j * kNCT + ct;
+    wv[j] = to_f32<DT>(gp(w)[idx[j] < H ? idx[j] : 0]);
   }
   if (plain != nullptr) {
 #pragma unroll
-    for (int j = 0; j < J; ++j) v[j] = idx[j] < H ? __float_as_uint(gp(plain)[idx[j]]) : 0u;
+    for (int j = 0; j < J; ++j) v[j] = __float_as_uint(gp(plain)[idx[j] < H ? idx[j] : 0]);
   } else {
     poll<J>(g, idx, H, tag, v, a, sp, site);
   }
@@ -247,157 +264,306 @@ __device__ __forceinline__ void gather_norm(const u64* g, const float* plain, in
 #pragma unroll
   for (int j = 0; j < J; ++j) {
     const float f = __uint_as_float(v[j]);
-    if (idx[j] < H) { raw[idx[j]] = f; ss = fmaf(f, f, ss); }
+    if (idx[j] < H) {
+      ss = fmaf(f, f, ss);
+      if ((unsigned)(idx[j] - row_lo) < (unsigned)nrow) rows[idx[j] - row_lo] = f;
+    }
   }
-  ss = block_sum(ss, red);
-  const float r = rsqrtf(ss / (float)H + eps);
+  ss = wave_sum(ss);
+  const int wave = ct >> 6;
+  if ((ct & 63) == 0) red[wave] = ss;
+  cbar(cb);
+  float tot = 0.f;
+#pragma unroll
+  for (int w2 = 0; w2 < kNC; ++w2) tot += red[w2];
+  const float r = rsqrtf(tot / (float)H + eps);
 #pragma unroll
   for (int j = 0; j < J; ++j)
-    if (idx[j] < H) xs[idx[j]] = __uint_as_float(v[j]) * r * wv[j];
+    if (idx[j] < H) xs[idx[j]] = from_f32<DT>(__uint_as_float(v[j]) * r * wv[j]);
+  cbar(cb);
 }
 
 // ---------------------------------------------------------------------------
-// weight-streaming GEMV core
+// ops: this CU's contiguous range of row pairs of one matrix
 // ---------------------------------------------------------------------------
-template <int U> struct Batch { uint4 a[U], b[U]; };
-
-// One op's share of a workgroup: pairs [pbeg, pbeg + npl); this wave's blocks [b0, b1)
-// of the flattened (pair, 512-element K block) space, bpp blocks per pair.
-struct Rng { int pbeg, npl, bpp, b0, b1; };
-
-__device__ __forceinline__ Rng make_rng(int P, int nparts, int ip, int K, int wave, int NW,
-                                        int align) {
-  Rng r;
+enum OpKind { kQKV = 0, kRows2 = 1, kGU = 2 };
+struct Op {
+  const uint16_t* base;
+  int kind, K, pbeg, npl, bpp;
+  unsigned up;  // kGU: byte distance gate row -> up row
+};
+__device__ __forceinline__ Op make_op(const uint16_t* base, int kind, int K, int P, int nparts,
+                                      int ip, int align, unsigned up) {
+  Op o;
+  o.base = base;
+  o.kind = kind;
+  o.K = K;
+  o.up = up;
   const int Pa = P / align;
   const int s = (int)((long long)ip * Pa / nparts) * align;
   const int e = (int)((long long)(ip + 1) * Pa / nparts) * align;
-  r.pbeg = s;
-  r.npl = ip < 0 ? 0 : e - s;
-  r.bpp = K / kBlk;
-  const int tot = r.npl * r.bpp;
-  r.b0 = wave * tot / NW;
-  r.b1 = (wave + 1) * tot / NW;
-  return r;
+  o.pbeg = s;
+  o.npl = ip < 0 ? 0 : e - s;
+  o.bpp = K / kBlk;
+  return o;
+}
+// byte offsets of local pair pl's two rows
+template <int HD>
+__device__ __forceinline__ void op_rows(const Op& o, int pl, unsigned long long& oa,
+                                        unsigned long long& ob) {
+  const int p = o.pbeg + pl;
+  const unsigned long long rb = (unsigned long long)o.K * 2u;
+  if (o.kind == kQKV) {
+    constexpr int half = HD / 2;
+    const int slot = p / half;
+    oa = (unsigned long long)(slot * HD + (p - slot * half)) * rb;
+    ob = oa + (unsigned long long)half * rb;
+  } else if (o.kind == kRows2) {
+    oa = (unsigned long long)(2 * p) * rb;
+    ob = oa + rb;
+  } else {
+    oa = (unsigned long long)p * rb;
+    ob = oa + o.up;
+  }
 }
 
-// Weight rows are read through a buffer resource over the whole matrix: a block past
-// the wave's range gets an out-of-range offset, which the hardware answers with zeros
-// and no memory traffic — so every load is unconditional (a load under a branch left
-// its result in a phi, and the compiler waited for it right there).
-// (the base pointer comes from the layer table through a vector load: readfirstlane
-// makes it provably uniform, else every buffer load became a waterfall loop)
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, long long bytes) {
-  const unsigned long long v = (unsigned long long)base;
-  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
-  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
-  void* b = (void*)(((unsigned long long)hi << 32) | lo);
-  return __builtin_amdgcn_make_buffer_rsrc(b, (short)0, (int)bytes, 0x00020000);
-}
-constexpr unsigned kOob = 0xFFFFFFF0u;
-__device__ __forceinline__ uint4 bload_nt(__amdgpu_buffer_rsrc_t rs, unsigned off) {
-  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 2);  // aux 2 = nt
-  return make_uint4(v.x, v.y, v.z, v.w);
+// The ops of layer l for this workgroup, in stream order: QKV, o_proj (npl 0 on a
+// merger), gate/up, down.
+template <int HD>
+__device__ __forceinline__ Op layer_op(const Args& a, const CAKE_C Layer* ly, int k, int G,
+                                       int wg, int o_ip) {
+  const int H = a.H, I = a.I, nh = a.nh, nkv = a.nkv;
+  if (k == 0) return make_op(ly->wqkv, kQKV, H, (nh + 2 * nkv) * (HD / 2), G, wg, 1, 0u);
+  if (k == 1) return make_op(ly->wo, kRows2, nh * HD, H / 2, G, wg, 1, 0u);
+  if (k == 2) return make_op(ly->wgu, kGU, H, I, G, wg, 2, (unsigned)I * (unsigned)H * 2u);
+  return make_op(ly->wd, kRows2, I, H / 2, G, wg, 1, 0u);
 }
 
-// map.offs(pair_local, oa, ob): byte offsets of the pair's two rows in map.rs
-template <int U, class Map>
-__device__ __forceinline__ void issue(const Map& map, int bpp, int b, int b1, Batch<U>& B) {
-  const unsigned lo = (unsigned)(otid() & 63) * 16u;
-  int pl = b / bpp, kb = b - pl * bpp;
-  unsigned oa, ob;
-  map.offs(pl, oa, ob);
+// ---------------------------------------------------------------------------
+// the loader wave
+// ---------------------------------------------------------------------------
+// One ring slot: 16 x 1 KB global -> LDS, lane l of load k landing at dst + 1024 k + 16 l,
+// non-temporal.  In ONE asm statement (M0 stepped between the loads) so hipcc neither
+// counts the loads nor inserts its conservative vmcnt(0) in front of the loader's own
+// LDS control accesses; completion is counted by hand (vmcnt below).
+__device__ __forceinline__ void glds_slot(const char* const (&p)[16], unsigned dst) {
+  unsigned keep;
+#define CAKE_GL(k) "global_load_lds_dwordx4 %[p" #k "], off nt\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
+  asm volatile("s_mov_b32 %[keep], m0\n\ts_mov_b32 m0, %[dst]\n\ts_nop 0\n\t"
+               CAKE_GL(0) CAKE_GL(1) CAKE_GL(2) CAKE_GL(3) CAKE_GL(4) CAKE_GL(5) CAKE_GL(6)
+               CAKE_GL(7) CAKE_GL(8) CAKE_GL(9) CAKE_GL(10) CAKE_GL(11) CAKE_GL(12) CAKE_GL(13)
+               CAKE_GL(14) CAKE_GL(15) "s_mov_b32 m0, %[keep]"
+               : [keep] "=&s"(keep)
+               : [dst] "s"(dst), [p0] "v"(p[0]), [p1] "v"(p[1]), [p2] "v"(p[2]), [p3] "v"(p[3]),
+                 [p4] "v"(p[4]), [p5] "v"(p[5]), [p6] "v"(p[6]), [p7] "v"(p[7]), [p8] "v"(p[8]),
+                 [p9] "v"(p[9]), [p10] "v"(p[10]), [p11] "v"(p[11]), [p12] "v"(p[12]),
+                 [p13] "v"(p[13]), [p14] "v"(p[14]), [p15] "v"(p[15])
+               : "memory", "scc");
+#undef CAKE_GL
+}
+
+struct RingCtl {
+  unsigned full[kMaxRing];  // slot sequence + 1 of the landed fill
+  unsigned free_[kMaxRing]; // slot sequence + 1 of the fill consumed
+  unsigned cb;              // consumer barrier counter
+  unsigned gath;            // consumers are gathering (loader thins)
+  unsigned pad[2];
+  float red[16];
+};
+
+// phase clock of this workgroup (s_memrealtime, 100 MHz, comparable across CUs):
+// [wg][layer * kStampsPerLayer + k], then kernel start / end
+#define MK_STAMP(idx)                                                                     \
+  do {                                                                                    \
+    if (a.stamps != nullptr && threadIdx.x == 0)                                          \
+      a.stamps[(size_t)blockIdx.x * (a.L * kStampsPerLayer + 2) + (idx)] =                \
+          __builtin_amdgcn_s_memrealtime();                                               \
+  } while (0)
+
+// Loader wave li (of kNL) fills the ring slots whose sequence number is li mod kNL.
+template <int HD>
+__device__ void loader_run(const Args& a, int G, int wg, int o_ip, unsigned ring_lds,
+                           RingCtl* rc, Spin& sp, int li) {
+  const int lane = otid() & 63;
+  const unsigned NS = (unsigned)a.ring;
+  const char* dummy = reinterpret_cast<const char*>(a.gran) + lane * 16;  // never-written words
+  unsigned seq = 0;   // slot sequence of the op being walked (all loaders count all slots)
+  unsigned fly = 0;   // this loader's slots in flight
+  unsigned last = 0;  // this loader's most recent slot
+  auto mark_all = [&]() {
+    for (unsigned k = 0; k < fly; ++k) {
+      const unsigned q = last - k * kNL;
+      lds_st(&rc->full[q % NS], q + 1u);
+    }
+    fly = 0;
+  };
+  for (int l = 0; l < a.L; ++l) {
+    const CAKE_C Layer* ly = (const CAKE_C Layer*)a.layers + l;
+    for (int k = 0; k < 4; ++k) {
+      const Op o = layer_op<HD>(a, ly, k, G, wg, o_ip);
+      const int tot = o.npl * o.bpp;
+      const int nsl = (tot + kPB - 1) / kPB;
+      const char* base = reinterpret_cast<const char*>(o.base);
+      for (int s = (int)(((unsigned)li + kNL - seq % kNL) % kNL); s < nsl; s += kNL) {
+        const unsigned i = seq + (unsigned)s;
+        const unsigned r = i % NS;
+        if (i >= NS && lds_ld(&rc->free_[r]) < i - NS + 1u) {
+          // ring full: publish everything in flight (consumers free a slot only after
+          // they have seen it land), then wait for the slot
+          __builtin_amdgcn_s_waitcnt(vm_wait(0));
+          mark_all();
+          for (unsigned it = 0; lds_ld(&rc->free_[r]) < i - NS + 1u; ++it) {
+            __builtin_amdgcn_s_sleep(1);
+            if ((it & 1023u) == 1023u && (sp.dead || ctl_ld(a.ctl + 2) != 0u ||
+                                          __builtin_amdgcn_s_memrealtime() - sp.t0 > a.timeout)) {
+              sp.dead = true;
+              break;
+            }
+          }
+        }
+        const char* pv[16];
+        const int q0 = s * kPB;
+        int pl = q0 / o.bpp, kb = q0 - pl * o.bpp;
+        unsigned long long oa, ob;
+        op_rows<HD>(o, pl, oa, ob);
 #pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const bool ok = b + u < b1;
-    const unsigned kbo = (unsigned)kb * (kBlk * 2) + lo;
-    B.a[u] = bload_nt(map.rs, ok ? oa + kbo : kOob);
-    B.b[u] = bload_nt(map.rs, ok ? ob + kbo : kOob);
-    if (++kb == bpp) {
-      kb = 0;
-      ++pl;
-      map.offs(pl, oa, ob);
+        for (int j = 0; j < kPB; ++j) {
+          const bool ok = q0 + j < tot;
+          const unsigned long long kbo = (unsigned long long)kb * (kBlk * 2) + lane * 16;
+          pv[2 * j] = ok ? base + oa + kbo : dummy;
+          pv[2 * j + 1] = ok ? base + ob + kbo : dummy;
+          if (++kb == o.bpp) {
+            kb = 0;
+            ++pl;
+            op_rows<HD>(o, pl, oa, ob);
+          }
+        }
+        glds_slot(pv, __builtin_amdgcn_readfirstlane(ring_lds + r * kSlot));
+        if (li == 0) {  // diagnostics: loader 0's first issue of o_proj / its last, gate/up, down
+          const int si = k == 1 && s == 0 ? 10 : k == 1 && s + kNL >= nsl ? 11
+                       : k == 2 && s == 0 ? 12 : k == 3 && s == 0 ? 13 : -1;
+          if (a.stamps != nullptr && si >= 0 && lane == 0)
+            a.stamps[(size_t)blockIdx.x * (a.L * kStampsPerLayer + 2) + l * kStampsPerLayer + si] =
+                __builtin_amdgcn_s_memrealtime();
+        }
+        ++fly;
+        last = i;
+        if (a.thin && lds_ld(&rc->gath) != 0u) {
+          __builtin_amdgcn_s_waitcnt(vm_wait(0));
+          mark_all();
+        } else if (fly > kFly) {
+          __builtin_amdgcn_s_waitcnt(vm_wait(2 * kPB * kFly));
+          const unsigned q = last - kFly * kNL;
+          lds_st(&rc->full[q % NS], q + 1u);
+          --fly;
+        }
+      }
+      seq += (unsigned)nsl;
     }
   }
+  __builtin_amdgcn_s_waitcnt(vm_wait(0));
+  mark_all();
 }
 
-template <int DT, bool XF32>
-__device__ __forceinline__ void fma8(const void* xs, int chunk, const uint4 va, const uint4 vb,
-                                     float& aa, float& ab) {
-  float xv[8], fa[8], fb[8];
-  if constexpr (XF32) {
-    const float4* p = reinterpret_cast<const float4*>(xs) + chunk * 2;
-    const float4 x0 = p[0], x1 = p[1];
-    xv[0] = x0.x; xv[1] = x0.y; xv[2] = x0.z; xv[3] = x0.w;
-    xv[4] = x1.x; xv[5] = x1.y; xv[6] = x1.z; xv[7] = x1.w;
-  } else {
-    unpack8<DT>(reinterpret_cast<const uint4*>(xs)[chunk], xv);
-  }
-  unpack8<DT>(va, fa);
-  unpack8<DT>(vb, fb);
+// ---------------------------------------------------------------------------
+// consumers: the slots of one op
+// ---------------------------------------------------------------------------
+template <int DT>
+__device__ __forceinline__ float dot8(const uint4 w, const uint4 x, float acc) {
+  typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+  typedef _Float16 hf2 __attribute__((ext_vector_type(2)));
+  const unsigned wv[4] = {w.x, w.y, w.z, w.w}, xv[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    aa = fmaf(fa[e], xv[e], aa);
-    ab = fmaf(fb[e], xv[e], ab);
+  for (int e = 0; e < 4; ++e) {
+    if constexpr (DT == kBF16)
+      acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2, wv[e]),
+                                            __builtin_bit_cast(bf2, xv[e]), acc, false);
+    else
+      acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(hf2, wv[e]), __builtin_bit_cast(hf2, xv[e]),
+                                   acc, false);
   }
+  return acc;
 }
 
-// Walk this wave's blocks [b0, b1) with `cur` = the already-issued first batch;
-// part[(pl * NW + wave) * 2 + {0,1}] = this wave's partial dot products of pair pl.
-template <int DT, bool XF32, int U, int NW, class Map>
-__device__ __forceinline__ void walk(const Map& map, const void* xs, const Rng& r, Batch<U>& cur,
-                                     float* part) {
-  const int lane = otid() & 63, wave = __builtin_amdgcn_readfirstlane(otid() >> 6);
-  if (r.b1 <= r.b0) return;
-  float aa = 0.f, ab = 0.f;
-  int pl_cur = r.b0 / r.bpp;
-  for (int b = r.b0; b < r.b1; b += U) {
-    Batch<U> nxt;
-    if (b + U < r.b1) issue<U>(map, r.bpp, b + U, r.b1, nxt);
-    int pl = b / r.bpp, kb = b - pl * r.bpp;
+// Consumer wave c: the op's slots seq0 + s (s % kNC == (c - seq0) mod kNC); partial dot
+// products accumulated into part[(pl * kNC + c) * 2 + {0, 1}] (column c: this wave only).
+template <int DT>
+__device__ __forceinline__ void consume_op(const Op& o, unsigned seq0, const uint8_t* ring,
+                                           RingCtl* rc, const uint16_t* xs, float* part, int NS,
+                                           const Args& a, Spin& sp) {
+  const int ct = otid();
+  const int c = __builtin_amdgcn_readfirstlane(ct >> 6), lane = ct & 63;
+  const int tot = o.npl * o.bpp;
+  const int nsl = (tot + kPB - 1) / kPB;
+  for (int t = lane; t < o.npl; t += 64) {
+    part[(t * kNC + c) * 2] = 0.f;
+    part[(t * kNC + c) * 2 + 1] = 0.f;
+  }
+  const int first = (int)(((unsigned)c + kNC - seq0 % kNC) % kNC);
+  for (int s = first; s < nsl; s += kNC) {
+    const unsigned i = seq0 + s;
+    const int r = (int)(i % (unsigned)NS);
+    for (unsigned it = 0; lds_ld(&rc->full[r]) < i + 1u; ++it) {
+      __builtin_amdgcn_s_sleep(0);
+      if ((it & 4095u) == 4095u && (sp.dead || ctl_ld(a.ctl + 2) != 0u ||
+                                    __builtin_amdgcn_s_memrealtime() - sp.t0 > a.timeout)) {
+        sp.dead = true;
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    const uint8_t* sl = ring + (size_t)r * kSlot + lane * 16;
+    uint4 wa[kPB], wb[kPB];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (b + u < r.b1) {
-        if (pl != pl_cur) {
+    for (int j = 0; j < kPB; ++j) {
+      wa[j] = *reinterpret_cast<const uint4*>(sl + (2 * j) * 1024);
+      wb[j] = *reinterpret_cast<const uint4*>(sl + (2 * j + 1) * 1024);
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the slot is in registers
+    lds_st(&rc->free_[r], i + 1u);
+    const int q0 = s * kPB;
+    int pl = q0 / o.bpp, kb = q0 - pl * o.bpp;
+    float aa = 0.f, ab = 0.f;
+    int pc = pl;
+#pragma unroll
+    for (int j = 0; j < kPB; ++j) {
+      if (q0 + j < tot) {
+        if (pl != pc) {
           const float sa = wave_sum(aa), sb = wave_sum(ab);
           if (lane == 0) {
-            part[(pl_cur * NW + wave) * 2] = sa;
-            part[(pl_cur * NW + wave) * 2 + 1] = sb;
+            part[(pc * kNC + c) * 2] += sa;
+            part[(pc * kNC + c) * 2 + 1] += sb;
           }
           aa = ab = 0.f;
-          pl_cur = pl;
+          pc = pl;
         }
-        fma8<DT, XF32>(xs, kb * 64 + lane, cur.a[u], cur.b[u], aa, ab);
+        const uint4 xv = *reinterpret_cast<const uint4*>(xs + kb * kBlk + lane * 8);
+        aa = dot8<DT>(wa[j], xv, aa);
+        ab = dot8<DT>(wb[j], xv, ab);
       }
-      if (++kb == r.bpp) { kb = 0; ++pl; }
+      if (++kb == o.bpp) { kb = 0; ++pl; }
     }
-    cur = nxt;
-  }
-  const float sa = wave_sum(aa), sb = wave_sum(ab);
-  if (lane == 0) {
-    part[(pl_cur * NW + wave) * 2] = sa;
-    part[(pl_cur * NW + wave) * 2 + 1] = sb;
+    const float sa = wave_sum(aa), sb = wave_sum(ab);
+    if (lane == 0) {
+      part[(pc * kNC + c) * 2] += sa;
+      part[(pc * kNC + c) * 2 + 1] += sb;
+    }
   }
 }
 
-// Sum of the partials of local pair t over the waves whose block range touches it.
-template <int NW>
-__device__ __forceinline__ void pair_sum(const float* part, const Rng& r, int t, float& da,
-                                         float& db) {
-  const int tot = r.npl * r.bpp, lo = t * r.bpp, hi = lo + r.bpp;
+__device__ __forceinline__ void pair_sum(const float* part, int t, float& da, float& db) {
   da = 0.f;
   db = 0.f;
 #pragma unroll
-  for (int w = 0; w < NW; ++w) {
-    const int b0 = w * tot / NW, b1 = (w + 1) * tot / NW;
-    if (b0 < hi && b1 > lo && b1 > b0) {
-      da += part[(t * NW + w) * 2];
-      db += part[(t * NW + w) * 2 + 1];
-    }
+  for (int c = 0; c < kNC; ++c) {
+    da += part[(t * kNC + c) * 2];
+    db += part[(t * kNC + c) * 2 + 1];
   }
 }
 
 // ---------------------------------------------------------------------------
-// attention unit (kv head g, split s): core2-style wave-independent key blocks
+// attention unit (kv head g, split s): core2-style wave-independent key blocks on the
+// consumer waves
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void splits_for(int Tk, int min_keys, int maxsplit, int target,
                                            int single, int& ns, int& kps) {
@@ -430,12 +596,14 @@ constexpr int attn_lds_floats() {
 }
 
 template <int DT, int HD, int NREP, int NW>
-__device__ __forceinline__ void attn_unit(const Args& a, const uint16_t* kcache, const uint16_t* vcache, const GOff& go, u64* gl, unsigned tag,
-                          int g, int s, int ns, int kps, int pos, float* lds, Spin& sp) {
+__device__ __forceinline__ void attn_unit(const Args& a, const uint16_t* kcache,
+                                          const uint16_t* vcache, const GOff& go, u64* gl,
+                                          unsigned tag,
+                          int g, int s, int ns, int kps, int pos, float* lds, Spin& sp, CBar& cb) {
   constexpr int NT = NW * 64;
   constexpr int DS = HD / 32, NCH = HD / 8, KPL = NCH / 4;
   static_assert(NCH == 8 || NCH == 16, "hd 64 or 128");
-  static_assert(NREP <= 16 && NREP <= NW, "GQA group");
+  static_assert(NREP <= 16, "GQA group");
   const int tid = otid(), wave = tid >> 6, lane = tid & 63;
   const int col = lane & 15, rg = lane >> 4;
   const int ch = lane % NCH, kg = lane / NCH;
@@ -516,7 +684,7 @@ __device__ __forceinline__ void attn_unit(const Args& a, const uint16_t* kcache,
       }
     }
   }
-  __syncthreads();
+  cbar(cb);
   uint4 qf[DS];
 #pragma unroll
   for (int d = 0; d < DS; ++d) {
@@ -617,7 +785,7 @@ __device__ __forceinline__ void attn_unit(const Args& a, const uint16_t* kcache,
 #pragma unroll
       for (int e = 0; e < 8; ++e) ws[32 + h * HD + ch * 8 + e] = o[h][e];
   }
-  __syncthreads();
+  cbar(cb);
   constexpr int NOUT = NREP * HD;
   constexpr int OPT = (NOUT + NT - 1) / NT;
   float mo[OPT], lo[OPT], ao[OPT];
@@ -662,13 +830,13 @@ __device__ __forceinline__ void attn_unit(const Args& a, const uint16_t* kcache,
         gst(dst + 2 + d, tag, __float_as_uint(ao[i]));
       }
     }
-    __syncthreads();  // LDS (st) reuse by the caller
+    cbar(cb);  // LDS (st) reuse by the caller
     return;
   } else {
     // split 0: own partial -> LDS (p tiles are free), one wave per head merges
     float* own = lds;
     static_assert(NREP * (HD + 2) <= NW * (kKeys * 16 + 16), "own partial fits the p tiles");
-    __syncthreads();
+    cbar(cb);
 #pragma unroll
     for (int i = 0; i < OPT; ++i) {
       const int idx = tid + i * NT;
@@ -678,10 +846,9 @@ __device__ __forceinline__ void attn_unit(const Args& a, const uint16_t* kcache,
         own[h * (HD + 2) + 2 + d] = ao[i];
       }
     }
-    __syncthreads();
-    if (wave < NREP) {
+    cbar(cb);
+    for (int h = wave; h < NREP; h += NW) {
       constexpr int DPL = HD / 64;
-      const int h = wave;
       const u64* src = gl + go.part + (size_t)(g * NREP + h) * a.maxsplit * (HD + 2);
       const float* ow = own + h * (HD + 2);
       // lane t < ns holds split t's (m, l); o rows of splits 1..ns-1, DPL dims per lane
@@ -726,14 +893,15 @@ __device__ __forceinline__ void attn_unit(const Args& a, const uint16_t* kcache,
       for (int d = 0; d < DPL; ++d) ob[h * HD + lane * DPL + d] = from_f32<DT>(acc[d] * inv);
     }
   }
-  __syncthreads();
+  cbar(cb);
   // publish the group's output: 2 x 16-bit per granule
   for (int i = tid; i < NOUT / 2; i += NT) {
     const unsigned w = (unsigned)ob[2 * i] | ((unsigned)ob[2 * i + 1] << 16);
     gst(att + i, tag, w);
   }
-  __syncthreads();
+  cbar(cb);
 }
+
 
 // ---------------------------------------------------------------------------
 // the persistent kernel
@@ -742,64 +910,46 @@ __device__ __forceinline__ int merger_wg(int g, int G, int nkv) {
   return g * (G / nkv) + (g & 7);
 }
 
-// Row maps: pair (local index pl) -> byte offsets of its two weight rows.
-template <int HD> struct MapQKV {  // rows (slot hd + i, slot hd + i + hd/2) of wqkv
-  __amdgpu_buffer_rsrc_t rs;
-  int pbeg, K;
-  __device__ __forceinline__ void offs(int pl, unsigned& oa, unsigned& ob) const {
-    constexpr int half = HD / 2;
-    const int p = pbeg + pl;
-    const int slot = p / half;
-    const unsigned ra = (unsigned)(slot * HD + (p - slot * half));
-    oa = ra * (unsigned)K * 2u;
-    ob = oa + (unsigned)(half * K * 2);
-  }
+// LDS layout (bytes): ring | RingCtl | rows f32[kMaxRows] | part f32[maxpl][kNC][2] | xs
+constexpr int kMaxRows = 64;  // residual rows of one workgroup's o_proj / down share
+struct Lds {
+  unsigned ring, ctl, raw, part, xs, total;
 };
-struct MapRows2 {  // rows 2p, 2p + 1
-  __amdgpu_buffer_rsrc_t rs;
-  int pbeg, K;
-  __device__ __forceinline__ void offs(int pl, unsigned& oa, unsigned& ob) const {
-    oa = (unsigned)(2 * (pbeg + pl)) * (unsigned)K * 2u;
-    ob = oa + (unsigned)K * 2u;
-  }
-};
-struct MapGU {  // gate row j and up row j (I rows further)
-  __amdgpu_buffer_rsrc_t rs;
-  int pbeg, K;
-  unsigned up;  // byte distance gate -> up
-  __device__ __forceinline__ void offs(int pl, unsigned& oa, unsigned& ob) const {
-    oa = (unsigned)(pbeg + pl) * (unsigned)K * 2u;
-    ob = oa + up;
-  }
-};
+__host__ __device__ inline Lds lds_layout(int H, int I, int nh, int hd, int nrep, int G, int ring) {
+  Lds o;
+  const int maxpl = (I + G - 1) / G + 2;
+  o.ring = 0;
+  o.ctl = o.ring + (unsigned)ring * kSlot;
+  o.raw = o.ctl + (unsigned)((sizeof(RingCtl) + 15) / 16 * 16);
+  o.part = o.raw + (unsigned)kMaxRows * 4u;
+  o.xs = o.part + (unsigned)(maxpl * kNC * 2 * 4 + 15) / 16 * 16;
+  unsigned xs = (unsigned)H * 2u;
+  const unsigned x16 = (unsigned)(nh * hd > I ? nh * hd : I) * 2u;
+  if (x16 > xs) xs = x16;
+  const unsigned at = 4u * (unsigned)(kNC * (kKeys * 16 + 16) + kNC * (32 + nrep * hd) + nrep * hd +
+                                      hd + nrep * hd / 2 + 16);
+  if (at > xs) xs = at;
+  o.total = o.xs + xs;
+  return o;
+}
 
-// phase clock of this workgroup (s_memrealtime, 100 MHz, comparable across CUs):
-// [wg][layer * kStampsPerLayer + k], then kernel start / end
-#define MK_STAMP(idx)                                                                     \
-  do {                                                                                    \
-    if (a.stamps != nullptr && threadIdx.x == 0)                                          \
-      a.stamps[(size_t)blockIdx.x * (a.L * kStampsPerLayer + 2) + (idx)] =                \
-          __builtin_amdgcn_s_memrealtime();                                               \
-  } while (0)
-
-template <int DT, int NW, int U, int HD, int NREP>
-__global__ __launch_bounds__(NW * 64) void mk_decode_kernel(Args a) {
-  constexpr int NT = NW * 64;
+template <int DT, int HD, int NREP>
+__global__ __launch_bounds__(kNW * 64) void mk_decode_kernel(Args a) {
   constexpr int half = HD / 2;
-  constexpr int POLL = NW - 1;  // the poller wave (issues its own prefetch after polling)
-  extern __shared__ float smem[];
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int G = gridDim.x, wg = blockIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-  const bool poller = wave == POLL;
   const int H = a.H, I = a.I, nh = a.nh, nkv = a.nkv, S = a.S;
   const int KO = nh * HD;
-  // LDS: rawA[H] rawB[H] part[maxpl][NW][2] red[32] xs[...]
-  const int maxpl = (I + G - 1) / G + 2;
-  float* rawA = smem;
-  float* rawB = rawA + H;
-  float* part = rawB + H;
-  float* red = part + maxpl * NW * 2;
-  float* xs = red + 32;
+  const Lds lay = lds_layout(H, I, nh, HD, NREP, G, a.ring);
+  uint8_t* ring = smem + lay.ring;
+  RingCtl* rc = reinterpret_cast<RingCtl*>(smem + lay.ctl);
+  float* rows = reinterpret_cast<float*>(smem + lay.raw);
+  float* part = reinterpret_cast<float*>(smem + lay.part);
+  uint16_t* xs = reinterpret_cast<uint16_t*>(smem + lay.xs);
+
+  if (threadIdx.x < sizeof(RingCtl) / 4) reinterpret_cast<unsigned*>(rc)[threadIdx.x] = 0u;
+  __syncthreads();
 
   Spin sp;
   sp.t0 = __builtin_amdgcn_s_memrealtime();
@@ -819,201 +969,150 @@ __global__ __launch_bounds__(NW * 64) void mk_decode_kernel(Args a) {
   const bool is_merger = is_attn && my_s == 0;
   const int o_ip = is_merger ? -1 : wg - n_merg_below;  // index among o_proj workgroups
   const GOff go = goff(H, I, nh, nkv, HD, a.maxsplit);
-  const int Pq = (nh + 2 * nkv) * half;
-  const long long bq = (long long)Pq * 2 * H * 2, bo = (long long)H * KO * 2;
-  const long long bgu = 2LL * I * H * 2, bd = (long long)H * I * 2;
-  const unsigned gu_off = (unsigned)I * (unsigned)H * 2u;
-
   MK_STAMP(a.L * kStampsPerLayer);
-  Batch<U> pre;
-  {
-    const CAKE_G Layer* ly = gp(a.layers);
-    const Rng r = make_rng(Pq, G, wg, H, wave, NW, 1);
-    issue<U>(MapQKV<HD>{rsrc(ly->wqkv, bq), r.pbeg, H}, r.bpp, r.b0, r.b1, pre);
-  }
 
-  for (int l = 0; l < a.L; ++l) {
-    const int tid = otid();
-    const CAKE_G Layer* ly = gp(a.layers + l);
-    u64* gl = a.gran + (size_t)l * a.gstride;
-    u64* sent = gl + go.sent;
-    // ---------------- QKV + RoPE + KV write ----------------
-    if (l > 0 && poller) {
-      wait_sent(sent + kERes * kMaxG, G, tag, a, sp, 21);
-      const Rng r = make_rng(Pq, G, wg, H, wave, NW, 1);
-      issue<U>(MapQKV<HD>{rsrc(ly->wqkv, bq), r.pbeg, H}, r.bpp, r.b0, r.b1, pre);
-    }
-    __syncthreads();
-    gather_norm<DT, NT, 16>(gl + go.res, l == 0 ? a.resid : nullptr, H, tag, ly->ln1, a.eps,
-                            rawA, xs, red, a, sp, 1);
-    __syncthreads();
-    const int sb = l * kStampsPerLayer;
-    MK_STAMP(sb + 0);
-    {
-      const Rng r = make_rng(Pq, G, wg, H, wave, NW, 1);
-      walk<DT, true, U, NW>(MapQKV<HD>{rsrc(ly->wqkv, bq), r.pbeg, H}, xs, r, pre, part);
-    }
-    if (!is_attn && o_ip >= 0 && !poller) {
-      const Rng r = make_rng(H / 2, G - nkv, o_ip, KO, wave, NW, 1);
-      issue<U>(MapRows2{rsrc(ly->wo, bo), r.pbeg, KO}, r.bpp, r.b0, r.b1, pre);
-    }
-    __syncthreads();
-    MK_STAMP(sb + 1);
-    {
-      const Rng r = make_rng(Pq, G, wg, H, wave, NW, 1);
-      uint16_t* kc = ly->kc;
-      uint16_t* vc = ly->vc;
-      for (int t = tid; t < r.npl; t += NT) {
-        float da, db;
-        pair_sum<NW>(part, r, t, da, db);
-        const int p = r.pbeg + t;
-        const int slot = p / half, i = p - slot * half;
-        const int kind = slot < nh ? 0 : (slot < nh + nkv ? 1 : 2);
-        const int head = slot - (kind == 0 ? 0 : (kind == 1 ? nh : nh + nkv));
-        float oa = da, ob = db;
-        if (kind < 2) {
-          float sn, cs;
-          sincosf((float)pos * gp(a.inv_freq)[i], &sn, &cs);
-          oa = da * cs - db * sn;
-          ob = da * sn + db * cs;
+  if (wave >= kNC) {
+    loader_run<HD>(a, G, wg, o_ip,
+                   (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)ring, rc,
+                   sp, wave - kNC);
+  } else {
+    CBar cb{&rc->cb, 0u};
+    unsigned seq = 0;
+    auto set_gath = [&](unsigned v) {
+      if (otid() == 0) lds_st(&rc->gath, v);
+    };
+    for (int l = 0; l < a.L; ++l) {
+      const int tid = otid();
+      const CAKE_C Layer* ly = (const CAKE_C Layer*)a.layers + l;
+      u64* gl = a.gran + (size_t)l * a.gstride;
+      const int sb = l * kStampsPerLayer;
+      // ---------------- QKV + RoPE + KV write ----------------
+      set_gath(1u);
+      const Op oo = layer_op<HD>(a, ly, 1, G, wg, o_ip);
+      gather_norm<DT, kJN>(gl + go.res, l == 0 ? a.resid : nullptr, H, tag, ly->ln1, a.eps, rows,
+                           2 * oo.pbeg, 2 * oo.npl, xs,
+                          rc->red, cb, a, sp, 1);
+      set_gath(0u);
+      MK_STAMP(sb + 0);
+      {
+        const Op o = layer_op<HD>(a, ly, 0, G, wg, o_ip);
+        consume_op<DT>(o, seq, ring, rc, xs, part, a.ring, a, sp);
+        seq += (o.npl * o.bpp + kPB - 1) / kPB;
+        cbar(cb);
+        MK_STAMP(sb + 1);
+        uint16_t* kc = ly->kc;
+        uint16_t* vc = ly->vc;
+        for (int t = tid; t < o.npl; t += kNCT) {
+          float da, db;
+          pair_sum(part, t, da, db);
+          const int p = o.pbeg + t;
+          const int slot = p / half, i = p - slot * half;
+          const int kind = slot < nh ? 0 : (slot < nh + nkv ? 1 : 2);
+          const int head = slot - (kind == 0 ? 0 : (kind == 1 ? nh : nh + nkv));
+          float oa = da, ob = db;
+          if (kind < 2) {
+            float sn, cs;
+            sincosf((float)pos * gp(a.inv_freq)[i], &sn, &cs);
+            oa = da * cs - db * sn;
+            ob = da * sn + db * cs;
+          }
+          if (kind == 0) {
+            gst(gl + go.q + (size_t)head * HD + i, tag, __float_as_uint(oa));
+            gst(gl + go.q + (size_t)head * HD + i + half, tag, __float_as_uint(ob));
+          } else {
+            uint16_t* cache = kind == 1 ? kc : vc;
+            const size_t off = ((size_t)head * S + pos) * HD + i;
+            const uint16_t ha = from_f32<DT>(oa), hb = from_f32<DT>(ob);
+            gpw(cache)[off] = ha;
+            gpw(cache)[off + half] = hb;
+            gst(gl + go.kv + (size_t)(kind - 1) * nkv * half + (size_t)head * half + i, tag,
+                (unsigned)ha | ((unsigned)hb << 16));
+          }
         }
-        if (kind == 0) {
-          gst(gl + go.q + (size_t)head * HD + i, tag, __float_as_uint(oa));
-          gst(gl + go.q + (size_t)head * HD + i + half, tag, __float_as_uint(ob));
-        } else {
-          uint16_t* cache = kind == 1 ? kc : vc;
-          const size_t off = ((size_t)head * S + pos) * HD + i;
-          const uint16_t ha = from_f32<DT>(oa), hb = from_f32<DT>(ob);
-          gpw(cache)[off] = ha;
-          gpw(cache)[off + half] = hb;
-          gst(gl + go.kv + (size_t)(kind - 1) * nkv * half + (size_t)head * half + i, tag,
-              (unsigned)ha | ((unsigned)hb << 16));
-        }
+        cbar(cb);
+        MK_STAMP(sb + 2);
       }
-    }
-    __syncthreads();
-    if (tid == 0) gst(sent + kEQkv * kMaxG + wg, tag, 1u);
-    MK_STAMP(sb + 2);
-    // ---------------- attention ----------------
-    if (is_attn) {
-      if (poller) wait_sent(sent + kEQkv * kMaxG, G, tag, a, sp, 22);
-      __syncthreads();
-      attn_unit<DT, HD, NREP, NW>(a, ly->kc, ly->vc, go, gl, tag, my_g, my_s, ns, kps, pos, xs, sp);
-      if (my_s == 0 && tid == 0) gst(sent + kEAtt * kMaxG + my_g, tag, 1u);
-      // o_proj prefetch, unconditional in this block so the batch is not live across the
-      // attention code (a merger's range is empty: every load is out of range, no traffic)
-      const Rng r = make_rng(H / 2, G - nkv, o_ip, KO, wave, NW, 1);
-      issue<U>(MapRows2{rsrc(ly->wo, bo), r.pbeg, KO}, r.bpp, r.b0, r.b1, pre);
-    }
-    if (is_merger && tid == 0) gst(sent + kEMid * kMaxG + wg, tag, 1u);  // no o_proj rows
-    // ---------------- o_proj + residual ----------------
-    if (o_ip >= 0) {
-      if (poller) wait_sent(sent + kEAtt * kMaxG, nkv, tag, a, sp, 23);
-      if (!is_attn && poller) {
-        const Rng r = make_rng(H / 2, G - nkv, o_ip, KO, wave, NW, 1);
-        issue<U>(MapRows2{rsrc(ly->wo, bo), r.pbeg, KO}, r.bpp, r.b0, r.b1, pre);
-      }
-      __syncthreads();
-      gather_u32<NT>(gl + go.att, KO / 2, tag, reinterpret_cast<unsigned*>(xs), a, sp, 2);
-      __syncthreads();
-      MK_STAMP(sb + 3);
-      const Rng r = make_rng(H / 2, G - nkv, o_ip, KO, wave, NW, 1);
-      walk<DT, false, U, NW>(MapRows2{rsrc(ly->wo, bo), r.pbeg, KO}, xs, r, pre, part);
-    }
-    if (!poller) {
-      const Rng r = make_rng(I, G, wg, H, wave, NW, 2);
-      issue<U>(MapGU{rsrc(ly->wgu, bgu), r.pbeg, H, gu_off}, r.bpp, r.b0, r.b1, pre);
-    }
-    __syncthreads();
-    MK_STAMP(sb + 4);
-    if (o_ip >= 0) {
-      const Rng r = make_rng(H / 2, G - nkv, o_ip, KO, wave, NW, 1);
-      for (int t = tid; t < r.npl; t += NT) {
-        float da, db;
-        pair_sum<NW>(part, r, t, da, db);
-        const int row = 2 * (r.pbeg + t);
-        gst(gl + go.mid + row, tag, __float_as_uint(rawA[row] + da));
-        gst(gl + go.mid + row + 1, tag, __float_as_uint(rawA[row + 1] + db));
-      }
-      __syncthreads();
-      if (tid == 0) gst(sent + kEMid * kMaxG + wg, tag, 1u);
-    }
-    // ---------------- RMSNorm + gate/up + SwiGLU ----------------
-    if (poller) {
-      wait_sent(sent + kEMid * kMaxG, G, tag, a, sp, 24);
-      const Rng r = make_rng(I, G, wg, H, wave, NW, 2);
-      issue<U>(MapGU{rsrc(ly->wgu, bgu), r.pbeg, H, gu_off}, r.bpp, r.b0, r.b1, pre);
-    }
-    __syncthreads();
-    gather_norm<DT, NT, 16>(gl + go.mid, nullptr, H, tag, ly->ln2, a.eps, rawB, xs, red, a, sp, 3);
-    __syncthreads();
-    MK_STAMP(sb + 5);
-    {
-      const Rng r = make_rng(I, G, wg, H, wave, NW, 2);
-      walk<DT, true, U, NW>(MapGU{rsrc(ly->wgu, bgu), r.pbeg, H, gu_off}, xs, r, pre, part);
-    }
-    if (!poller) {
-      const Rng r = make_rng(H / 2, G, wg, I, wave, NW, 1);
-      issue<U>(MapRows2{rsrc(ly->wd, bd), r.pbeg, I}, r.bpp, r.b0, r.b1, pre);
-    }
-    __syncthreads();
-    MK_STAMP(sb + 6);
-    {
-      const Rng r = make_rng(I, G, wg, H, wave, NW, 2);
-      for (int t = tid; 2 * t < r.npl; t += NT) {
-        float g0, u0, g1, u1;
-        pair_sum<NW>(part, r, 2 * t, g0, u0);
-        pair_sum<NW>(part, r, 2 * t + 1, g1, u1);
-        const int j = r.pbeg + 2 * t;
-        gst(gl + go.act + j / 2, tag, pack2(silu(g0) * u0, silu(g1) * u1, DT));
-      }
-    }
-    __syncthreads();
-    if (tid == 0) gst(sent + kEAct * kMaxG + wg, tag, 1u);
-    // ---------------- down_proj + residual ----------------
-    if (poller) {
-      wait_sent(sent + kEAct * kMaxG, G, tag, a, sp, 25);
-      const Rng r = make_rng(H / 2, G, wg, I, wave, NW, 1);
-      issue<U>(MapRows2{rsrc(ly->wd, bd), r.pbeg, I}, r.bpp, r.b0, r.b1, pre);
-    }
-    __syncthreads();
-    gather_u32<NT>(gl + go.act, I / 2, tag, reinterpret_cast<unsigned*>(xs), a, sp, 4);
-    __syncthreads();
-    MK_STAMP(sb + 7);
-    {
-      const Rng r = make_rng(H / 2, G, wg, I, wave, NW, 1);
-      walk<DT, false, U, NW>(MapRows2{rsrc(ly->wd, bd), r.pbeg, I}, xs, r, pre, part);
-    }
-    if (l + 1 < a.L && !poller) {
-      const CAKE_G Layer* ln = ly + 1;
-      const Rng r = make_rng(Pq, G, wg, H, wave, NW, 1);
-      issue<U>(MapQKV<HD>{rsrc(ln->wqkv, bq), r.pbeg, H}, r.bpp, r.b0, r.b1, pre);
-    }
-    __syncthreads();
-    MK_STAMP(sb + 8);
-    {
-      const Rng r = make_rng(H / 2, G, wg, I, wave, NW, 1);
-      u64* gn = gl + a.gstride;
-      const bool last = l + 1 == a.L;
-      for (int t = tid; t < r.npl; t += NT) {
-        float da, db;
-        pair_sum<NW>(part, r, t, da, db);
-        const int row = 2 * (r.pbeg + t);
-        const float va = rawB[row] + da, vb = rawB[row + 1] + db;
-        if (!last) {
-          gst(gn + go.res + row, tag, __float_as_uint(va));
-          gst(gn + go.res + row + 1, tag, __float_as_uint(vb));
-        } else {
-          gpw(a.resid)[row] = va;
-          gpw(a.resid)[row + 1] = vb;
+      // ---------------- attention ----------------
+      if (is_attn)
+        attn_unit<DT, HD, NREP, kNC>(a, ly->kc, ly->vc, go, gl, tag, my_g, my_s, ns, kps, pos,
+                                     reinterpret_cast<float*>(xs), sp, cb);
+      // ---------------- o_proj + residual ----------------
+      {
+        const Op o = layer_op<HD>(a, ly, 1, G, wg, o_ip);
+        if (o.npl > 0) {
+          set_gath(1u);
+          gather_u32(gl + go.att, KO / 2, tag, reinterpret_cast<unsigned*>(xs), a, sp, 2);
+          set_gath(0u);
+          cbar(cb);
+          MK_STAMP(sb + 3);
+          consume_op<DT>(o, seq, ring, rc, xs, part, a.ring, a, sp);
+          seq += (o.npl * o.bpp + kPB - 1) / kPB;
+          cbar(cb);
+          MK_STAMP(sb + 4);
+          for (int t = tid; t < o.npl; t += kNCT) {
+            float da, db;
+            pair_sum(part, t, da, db);
+            const int row = 2 * (o.pbeg + t);
+            gst(gl + go.mid + row, tag, __float_as_uint(rows[2 * t] + da));
+            gst(gl + go.mid + row + 1, tag, __float_as_uint(rows[2 * t + 1] + db));
+          }
+          cbar(cb);
         }
       }
-      if (!last) {
-        __syncthreads();
-        if (tid == 0) gst(gn + go.sent + kERes * kMaxG + wg, tag, 1u);
+      // ---------------- RMSNorm + gate/up + SwiGLU ----------------
+      set_gath(1u);
+      const Op od = layer_op<HD>(a, ly, 3, G, wg, o_ip);
+      gather_norm<DT, kJN>(gl + go.mid, nullptr, H, tag, ly->ln2, a.eps, rows, 2 * od.pbeg,
+                           2 * od.npl, xs, rc->red, cb, a,
+                          sp, 3);
+      set_gath(0u);
+      MK_STAMP(sb + 5);
+      {
+        const Op o = layer_op<HD>(a, ly, 2, G, wg, o_ip);
+        consume_op<DT>(o, seq, ring, rc, xs, part, a.ring, a, sp);
+        seq += (o.npl * o.bpp + kPB - 1) / kPB;
+        cbar(cb);
+        MK_STAMP(sb + 6);
+        for (int t = tid; 2 * t < o.npl; t += kNCT) {
+          float g0, u0, g1, u1;
+          pair_sum(part, 2 * t, g0, u0);
+          pair_sum(part, 2 * t + 1, g1, u1);
+          const int j = o.pbeg + 2 * t;
+          gst(gl + go.act + j / 2, tag, pack2(silu(g0) * u0, silu(g1) * u1, DT));
+        }
+        cbar(cb);
+      }
+      // ---------------- down_proj + residual ----------------
+      set_gath(1u);
+      gather_u32(gl + go.act, I / 2, tag, reinterpret_cast<unsigned*>(xs), a, sp, 4);
+      set_gath(0u);
+      cbar(cb);
+      MK_STAMP(sb + 7);
+      {
+        const Op o = layer_op<HD>(a, ly, 3, G, wg, o_ip);
+        consume_op<DT>(o, seq, ring, rc, xs, part, a.ring, a, sp);
+        seq += (o.npl * o.bpp + kPB - 1) / kPB;
+        cbar(cb);
+        MK_STAMP(sb + 8);
+        u64* gn = gl + a.gstride;
+        const bool last = l + 1 == a.L;
+        for (int t = tid; t < o.npl; t += kNCT) {
+          float da, db;
+          pair_sum(part, t, da, db);
+          const int row = 2 * (o.pbeg + t);
+          const float va = rows[2 * t] + da, vb = rows[2 * t + 1] + db;
+          if (!last) {
+            gst(gn + go.res + row, tag, __float_as_uint(va));
+            gst(gn + go.res + row + 1, tag, __float_as_uint(vb));
+          } else {
+            gpw(a.resid)[row] = va;
+            gpw(a.resid)[row + 1] = vb;
+          }
+        }
+        cbar(cb);
+        MK_STAMP(sb + 9);
       }
     }
-    MK_STAMP(sb + 9);
   }
   MK_STAMP(a.L * kStampsPerLayer + 1);
   // exit: the last workgroup advances the epoch (the next launch's tag)
@@ -1028,28 +1127,16 @@ __global__ __launch_bounds__(NW * 64) void mk_decode_kernel(Args a) {
   }
 }
 
-// LDS bytes of one workgroup
-inline size_t lds_bytes(int H, int I, int nh, int hd, int nrep, int G, int NW) {
-  const int maxpl = (I + G - 1) / G + 2;
-  size_t xs = (size_t)H;                       // f32 normalized row
-  const size_t x16 = (size_t)((nh * hd > I ? nh * hd : I) + 1) / 2;  // 16-bit rows as floats
-  if (x16 > xs) xs = x16;
-  const size_t at = (size_t)NW * (kKeys * 16 + 16) + (size_t)NW * (32 + nrep * hd) +
-                    (size_t)nrep * hd + hd + (size_t)nrep * hd / 2 + 16;
-  if (at > xs) xs = at;
-  return sizeof(float) * (2 * (size_t)H + (size_t)maxpl * NW * 2 + 32 + xs);
-}
-
 }  // namespace mk
 }  // namespace cake
 
 using namespace cake;
 
 namespace {
-constexpr int kMkNW = 8;
-constexpr int kMkU = 8;
 int g_mk_grid = 0;
 unsigned long long* g_mk_stamps = nullptr;  // diagnostics only
+int g_mk_thin = 1;
+int g_mk_ring = 0;  // 0 = as many slots as fit
 
 int mk_grid() {
   if (g_mk_grid > 0) return g_mk_grid;
@@ -1060,22 +1147,33 @@ int mk_grid() {
   return n;
 }
 
+constexpr unsigned kLdsMax = 160 * 1024;
+
+int ring_slots(int H, int I, int nh, int hd, int nrep, int G) {
+  const mk::Lds z = mk::lds_layout(H, I, nh, hd, nrep, G, 0);
+  if (z.total >= kLdsMax) return 0;
+  int n = (int)((kLdsMax - z.total) / mk::kSlot);
+  if (n > mk::kMaxRing) n = mk::kMaxRing;
+  if (g_mk_ring > 0 && g_mk_ring < n) n = g_mk_ring;
+  return n;
+}
+
 template <int DT, int HD, int NREP>
 int mk_launch(const mk::Args& a, int G, size_t lds, hipStream_t st) {
-  auto kern = mk::mk_decode_kernel<DT, kMkNW, kMkU, HD, NREP>;
+  auto kern = mk::mk_decode_kernel<DT, HD, NREP>;
   static bool attr_set = false;
   if (!attr_set) {
     if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            160 * 1024) != hipSuccess)
+                            (int)kLdsMax) != hipSuccess)
       return (int)hipErrorInvalidValue;
     attr_set = true;
   }
   int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, kMkNW * 64, lds) !=
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, mk::kNW * 64, lds) !=
           hipSuccess ||
       per_cu < 1)
     return (int)hipErrorLaunchOutOfResources;
-  hipLaunchKernelGGL(kern, dim3(G), dim3(kMkNW * 64), lds, st, a);
+  hipLaunchKernelGGL(kern, dim3(G), dim3(mk::kNW * 64), lds, st, a);
   return (int)hipGetLastError();
 }
 }  // namespace
@@ -1094,6 +1192,15 @@ CAKE_API int cake_mk_set_stamps(void* p) {
   return 0;
 }
 
+// Tuning / A-B: loader thinning during gathers (0/1) and a cap on the ring slots
+// (0 = as many as fit in LDS).
+CAKE_API int cake_mk_set_tuning(int thin, int ring) {
+  if (ring < 0 || ring > mk::kMaxRing) return (int)hipErrorInvalidValue;
+  g_mk_thin = thin != 0;
+  g_mk_ring = ring;
+  return 0;
+}
+
 // Shapes the persistent decode supports (0 = supported).
 CAKE_API int cake_mk_supported(int H, int I, int nh, int nkv, int hd) {
   const int G = mk_grid();
@@ -1102,14 +1209,15 @@ CAKE_API int cake_mk_supported(int H, int I, int nh, int nkv, int hd) {
   if (hd != 128 || nkv <= 0 || nh % nkv) return 3;
   const int nrep = nh / nkv;
   if (nrep != 4 && nrep != 8) return 4;
-  if (H > 16 * kMkNW * 64) return 5;
+  if (H > mk::kJN * mk::kNCT) return 5;
   if (G < nkv * (mk::kMaxSplitMk + 8) || G - nkv < 1 || G > mk::kMaxG) return 6;
-  if (mk::lds_bytes(H, I, nh, hd, nrep, G, kMkNW) > 160 * 1024) return 7;
+  if (ring_slots(H, I, nh, hd, nrep, G) < 2) return 7;
   if ((H / 2) < G || (nh + 2 * nkv) * hd / 2 < G) return 8;
+  if (2 * ((H / 2 + G - 1) / G) > mk::kMaxRows) return 9;
   return 0;
 }
 
-// layers: device array of L mk::Layer (11 pointers each); gran: L * gstride words;
+// layers: device array of L mk::Layer (8 pointers each); gran: L * gstride words;
 // ctl: 4 words; all zero-initialised before the first launch.
 CAKE_API int cake_mk_decode(int dt, const void* layers, int L, int H, int I, int nh, int nkv,
                             int hd, int S, float eps, float scale, const float* inv_freq,
@@ -1118,6 +1226,7 @@ CAKE_API int cake_mk_decode(int dt, const void* layers, int L, int H, int I, int
   if (cake_mk_supported(H, I, nh, nkv, hd) != 0 || L <= 0 || S <= 0 || !layers || !gran || !ctl)
     return (int)hipErrorInvalidValue;
   const int G = mk_grid();
+  const int nrep = nh / nkv;
   mk::Args a;
   a.layers = (const mk::Layer*)layers;
   a.L = L; a.H = H; a.I = I; a.nh = nh; a.nkv = nkv; a.hd = hd; a.S = S;
@@ -1133,10 +1242,11 @@ CAKE_API int cake_mk_decode(int dt, const void* layers, int L, int H, int I, int
   a.single = 320;
   a.target = 16;
   a.min_keys = 64;
+  a.ring = ring_slots(H, I, nh, hd, nrep, G);
+  a.thin = g_mk_thin;
   a.timeout = (unsigned long long)(timeout_s * 1e8);
   a.stamps = g_mk_stamps;
-  const int nrep = nh / nkv;
-  const size_t lds = mk::lds_bytes(H, I, nh, hd, nrep, G, kMkNW);
+  const size_t lds = mk::lds_layout(H, I, nh, hd, nrep, G, a.ring).total;
   if (dt == kBF16) {
     return nrep == 4 ? mk_launch<kBF16, 128, 4>(a, G, lds, st) : mk_launch<kBF16, 128, 8>(a, G, lds, st);
   } else if (dt == kF16) {

@@ -56,9 +56,10 @@ class DecodeBuffers:
         self.q = torch.zeros(nh * hd, device=device, dtype=f32)
         self.attn_out = torch.zeros(nh * hd, device=device, dtype=dtype)
         self.act = torch.zeros(I, device=device, dtype=dtype)
-        # <= 64 splits per head, 8-byte granules (attention.hip); tickets: [2 nkv]
+        # <= 64 splits per head, 8-byte granules (attention.hip); tickets: [2 nkv] + the
+        # merge's error word (+1 pad)
         self.part = torch.zeros(2 * nh * 64 * (hd + 2), device=device, dtype=f32)
-        self.tickets = torch.zeros(2 * cfg.num_key_value_heads, device=device, dtype=i32)
+        self.tickets = torch.zeros(2 * cfg.num_key_value_heads + 2, device=device, dtype=i32)
         self.pos = torch.zeros(1, device=device, dtype=i32) if pos is None else pos
         if with_head:
             self.logits = torch.zeros(cfg.vocab_size, device=device, dtype=f32)
@@ -207,11 +208,15 @@ class LayerStack:
         return bufs.mk_gran, bufs.mk_ctl
 
     def mk_check(self, bufs: DecodeBuffers) -> None:
-        """Raise if a persistent-decode launch gave up waiting (bounded spins)."""
+        """Raise if a decode launch gave up waiting in one of its bounded spins: the
+        persistent decode's hand-offs, or the split-K attention merge (host sync)."""
+        from ...ops import hip as K
+        if K.attn_error(bufs.tickets):
+            raise RuntimeError("decode attention: a split merge timed out waiting for its "
+                               "partials; outputs of that launch are invalid")
         ctl = getattr(bufs, "mk_ctl", None)
         if ctl is None:
             return
-        from ...ops import hip as K
         site = K.mk_error(ctl)
         if site:
             ctl.zero_()

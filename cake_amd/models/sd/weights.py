@@ -121,6 +121,55 @@ def random_component(name: str, cfg: SDConfig, device, dtype, seed: int = 0) -> 
     return out
 
 
+def unet_stage_keep(stages: list[str], n_stages: int):
+    """Predicate over UNet parameter names: the weights the block-group stages `stages`
+    run (UNet2DConditionModel.run_stage), plus what every stage needs (the time
+    embedding and every resnet's time projection: time_biases is one stacked GEMM)."""
+    pre = []
+    for s in stages:
+        kind, _, i = s.partition(".")
+        if kind == "down":
+            pre.append(f"down_blocks.{i}.")
+            if i == "0":
+                pre.append("conv_in.")
+        elif kind == "mid":
+            pre.append("mid_block.")
+        else:
+            pre.append(f"up_blocks.{i}.")
+            if int(i) == (n_stages - 1) // 2 - 1:
+                pre += ["conv_norm_out.", "conv_out."]
+
+    def keep(k: str) -> bool:
+        return (k.startswith("time_embedding.") or "time_emb_proj" in k
+                or any(k.startswith(p) for p in pre))
+    return keep
+
+
+def random_component_on_device(name: str, cfg: SDConfig, device, dtype, seed: int = 0,
+                               keep=None) -> dict[str, torch.Tensor]:
+    """random_component's distributions drawn on the device (seconds instead of minutes
+    for a full SDXL UNet on a busy host), restricted to the names `keep` accepts.  The
+    same seed gives the same tensors on every rank of one device type."""
+    import zlib
+    g = torch.Generator(device=device)
+    out = {}
+    for k, shp in component_shapes(name, cfg).items():
+        if keep is not None and not keep(k):
+            continue
+        # one seed per tensor: a rank keeping a subset draws the same values for it
+        g.manual_seed(seed * 1000003 + zlib.crc32(f"{name}/{k}".encode()))
+        if k.endswith(".bias"):
+            t = torch.zeros(shp, device=device, dtype=dtype)
+        elif len(shp) == 1:
+            t = torch.ones(shp, device=device, dtype=dtype)
+        else:
+            std = (0.02 if "token" in k else 0.01) if "embedding" in k else \
+                0.7 / math.sqrt(math.prod(shp[1:]))
+            t = torch.empty(shp, device=device, dtype=dtype).normal_(0.0, std, generator=g)
+        out[k] = t
+    return out
+
+
 # --------------------------------------------------------------------- synthetic files
 def write_clip_tokenizer(path: Path, vocab_size: int) -> None:
     """Byte-level BPE tokenizer with CLIP's <|startoftext|>/<|endoftext|> wrapping."""

@@ -84,7 +84,8 @@ class GraphSet:
 
 def run(gs: GraphSet, *, k: int, n: int, pos: int, hist: torch.Tensor | None = None,
         base: int = 0, eos_ids=None, on_token: Callable[[int], bool | None] | None = None,
-        announce: Callable[[int, int], None] | None = None, chunk: int = 0) -> LoopOut:
+        announce: Callable[[int, int], None] | None = None, chunk: int = 0,
+        callback_stops: bool = True) -> LoopOut:
     """Replay `ceil(n / k)` step graphs on the current stream.
 
     hist: the device int32 token history the graphs append to (the master); None on a
@@ -92,6 +93,9 @@ def run(gs: GraphSet, *, k: int, n: int, pos: int, hist: torch.Tensor | None = N
     pos: host mirror of the device position.  on_token(tok) -> True stops the loop
     (after EOS the at most one replay already enqueued past it is discarded by the
     caller's next prefill).  announce(first, count) runs before each chunk of replays.
+    callback_stops=False: on_token's return value and exceptions never stop the loop
+    (exceptions are re-raised after it) — for lock-step ranks (tensor parallel) where
+    only one rank has a callback and every rank must replay the same number of steps.
     """
     out = LoopOut(pos=pos)
     if n <= 0:
@@ -110,10 +114,11 @@ def run(gs: GraphSet, *, k: int, n: int, pos: int, hist: torch.Tensor | None = N
 
     def _tok(_ctx, t):
         try:
-            return 1 if on_token(int(t)) else 0
+            stop = bool(on_token(int(t)))
+            return 1 if stop and callback_stops else 0
         except BaseException as e:  # noqa: BLE001  (re-raised after the loop)
             errors.append(e)
-            return 1
+            return 1 if callback_stops else 0
 
     def _ann(_ctx, first, count):
         try:

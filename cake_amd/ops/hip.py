@@ -153,9 +153,10 @@ def attn_decode(q, kcache, vcache, pos, scale, part, tickets, out):
 
     The split count is derived on the device from the live length, so one
     captured launch serves every position.  part: f32 workspace
-    (:func:`attn_workspace_numel`) and tickets: int32 [2 nkv], both zero-initialised
+    (:func:`attn_workspace_numel`) and tickets: int32 [2 nkv + 2], both zero-initialised
     once, together, and maintained by the kernel itself (core 1: arrival tickets,
-    re-armed; core 2: per-kv-head epochs that tag the published partials).
+    re-armed; core 2: per-kv-head epochs that tag the published partials; word 2 nkv is
+    the error word a timed-out merge sets — :func:`attn_error`).
     """
     nkv, S, hd = kcache.shape
     nh = q.numel() // hd
@@ -165,7 +166,7 @@ def attn_decode(q, kcache, vcache, pos, scale, part, tickets, out):
     _req(pos, "pos", dtype=torch.int32, numel=1)
     _req(part, "part", dtype=torch.float32, numel=attn_workspace_numel(nh, hd, S))
     _req(out, "out", dtype=kcache.dtype, numel=nh * hd)
-    _req(tickets, "tickets", dtype=torch.int32, numel=2 * nkv)
+    _req(tickets, "tickets", dtype=torch.int32, numel=2 * nkv + 2)
     if hd not in (64, 128) or nh % nkv or (nh // nkv) not in (1, 2, 4, 8):
         raise ValueError(f"unsupported attention shape nh={nh} nkv={nkv} hd={hd}")
     if not _ATTN_IMPL_SET[0]:  # CAKE_ATTN_IMPL / CAKE_ATTN_TARGET, applied once
@@ -229,6 +230,17 @@ def mk_error(ctl) -> int:
     """Nonzero site code when a persistent-decode spin gave up (host sync)."""
     c = ctl.cpu()
     return int(c[3]) if int(c[2]) != 0 else 0
+
+
+def attn_error(tickets) -> bool:
+    """True when a split-K merge of :func:`attn_decode` gave up waiting for the
+    partials of its other splits (the error word after the 2 nkv tickets; host sync)."""
+    return int(tickets[-2].item()) != 0
+
+
+def attn_debug_drop_partials(on: bool) -> None:
+    """Test hook: core 2's splits >= 1 stop publishing, so the merges time out."""
+    check(kernels().cake_attn_debug_drop_partials(int(bool(on))), "attn_debug_drop_partials")
 
 
 def attn_workspace_numel(nh: int, hd: int, S: int) -> int:

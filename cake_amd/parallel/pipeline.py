@@ -696,6 +696,11 @@ class PipelineEngine:
         single = self.world == 1 or all(r.owner == 0 for r in self.runs)
         if ipc and self.hip and self.k == 1 and (st.sid, "tok") in st.graphs:
             return self._generate_native(st, n, on_token, eos_ids, chunk, single)
+        if ipc and self.k > 1:
+            # one ipc replay is k tokens: the announcements, hop counts and read-back
+            # below count replays as tokens, so the ranks would fall out of step
+            raise ValueError("generate() with ipc hops needs steps_per_graph == 1 "
+                             f"(got {self.k}); use run_rounds() for k-token replays")
         base = int(st.bufs.hist_len.item()) if self.hip else 0
         ring = torch.empty(max(1, n), dtype=torch.int32, pin_memory=self.hip and
                            torch.cuda.is_available()) if self.hip else None

@@ -235,9 +235,11 @@ def _tp_generate(eng, cmd, emit=None):
         # native decode driver (csrc/driver/graph_loop.cpp): every rank replays and
         # reads back the same tokens, so all stop after the same one
         from ..ops import graph_loop as GL
+        # the callback (rank 0 only) must not change this rank's replay count: every
+        # rank stops at the same EOS, whatever the callback returns or raises
         res = GL.run(eng.graph_set(), k=1, n=n - 1, pos=eng.host_pos, hist=b.hist, base=base,
                      eos_ids=eos, on_token=(lambda t: bool(emit(t))) if emit is not None
-                     else None)
+                     else None, callback_stops=False)
         eng.host_pos = res.pos
         st.tokens, st.step_ms, st.wall_s = res.tokens, res.step_ms, res.wall_s
         eng.tokens = b.hist[:int(b.hist_len.item())].tolist()

@@ -115,10 +115,16 @@ class SDEngine:
         from ..models.sd.unet import UNet2DConditionModel
         self.ctx, self.rank, self.world = ctx, rank, world
         self.device = ctx.device
+        # the long timeout only on the control broadcast a worker idles in (serve());
+        # a call's tensor metadata goes over a group with a normal timeout, so a master
+        # waiting on a stuck worker fails instead of blocking for days
         idle = float(os.environ.get("CAKE_SERVE_IDLE_TIMEOUT", str(7 * 86400)))
+        link_to = float(os.environ.get("CAKE_LINK_TIMEOUT", "600"))
         self.ctrl = dist.new_group(list(range(world)), backend="gloo",
                                    timeout=datetime.timedelta(seconds=idle))
-        self.link = TensorLink(self.device, self.ctrl)
+        self.meta = dist.new_group(list(range(world)), backend="gloo",
+                                   timeout=datetime.timedelta(seconds=link_to))
+        self.link = TensorLink(self.device, self.meta)
         self.cfg = sd_config_for(ctx)
         self.stages = UNet2DConditionModel(self.cfg.unet).stage_names()
         topo = ctx.topology

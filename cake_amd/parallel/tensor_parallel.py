@@ -394,7 +394,7 @@ class TPBuffers:
         self.attn_out = torch.zeros(nq * hd, device=device, dtype=dtype)
         self.act = torch.zeros(I_l, device=device, dtype=dtype)
         self.part = torch.zeros(2 * nq * 64 * (hd + 2), device=device, dtype=f32)
-        self.tickets = torch.zeros(2 * nkv_l, device=device, dtype=i32)
+        self.tickets = torch.zeros(2 * nkv_l + 2, device=device, dtype=i32)  # + error word
         self.pos = torch.zeros(1, device=device, dtype=i32)
         self.logits = torch.zeros(V_l, device=device, dtype=f32)
         self.tok = torch.zeros(1, device=device, dtype=i32)

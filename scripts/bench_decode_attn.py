@@ -20,7 +20,7 @@ def main():
         vc = torch.randn(nkv, S, hd, device=dev).to(dt)
         q = torch.randn(nh * hd, device=dev)
         part = torch.zeros(K.attn_workspace_numel(nh, hd, S), device=dev)
-        tickets = torch.zeros(2 * nkv, dtype=torch.int32, device=dev)
+        tickets = torch.zeros(2 * nkv + 2, dtype=torch.int32, device=dev)
         out = torch.empty(nh * hd, device=dev, dtype=dt)
         pos = torch.zeros(1, dtype=torch.int32, device=dev)
         for Tk in (55, 176, 512, 1024, 2048, 4096, 8192):

@@ -27,7 +27,11 @@ def main() -> None:
     ap.add_argument("--pos", type=int, nargs="+", default=[32])
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--max-seq", type=int, default=4096)
+    ap.add_argument("--thin", type=int, default=1)
+    ap.add_argument("--ring", type=int, default=0)
     a = ap.parse_args()
+    from cake_amd.ops._lib import kernels as _k
+    _k().cake_mk_set_tuning(a.thin, a.ring)
     over = {"num_hidden_layers": a.layers} if a.layers else {}
     cfg = preset(a.model, **over)
     layers = list(range(cfg.num_hidden_layers))
@@ -68,6 +72,7 @@ def main() -> None:
             e1.synchronize()
             us = e0.elapsed_time(e1) * 1e3 / a.reps
             rec = {"path": path, "model": a.model, "layers": len(layers), "pos": pos,
+                   "thin": a.thin, "ring": a.ring,
                    "us_per_step": round(us, 2), "us_per_layer": round(us / len(layers), 3),
                    "TBps": round(nbytes / us / 1e6, 3)}
             if path == "mk":

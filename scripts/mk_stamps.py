@@ -30,14 +30,20 @@ def main() -> None:
     ap.add_argument("--layers", type=int, default=0)
     ap.add_argument("--pos", type=int, default=32)
     ap.add_argument("--out", default="")
+    ap.add_argument("--thin", type=int, default=1)
+    ap.add_argument("--ring", type=int, default=0)
     a = ap.parse_args()
+    from cake_amd.ops._lib import kernels as _k
+    _k().cake_mk_set_tuning(a.thin, a.ring)
     cfg = preset(a.model, **({"num_hidden_layers": a.layers} if a.layers else {}))
     L = cfg.num_hidden_layers
     st = random_stack(cfg, list(range(L)), "cuda:0", torch.bfloat16, max_seq=4096)
+    st.use_mk = True
     bufs = st.decode_buffers()
     bufs.pos.fill_(a.pos)
     G = int(kernels().cake_mk_grid())
-    stamps = torch.zeros(G * (L * 10 + 2), dtype=torch.int64, device="cuda:0")
+    S = 14  # decode_mk.hip kStampsPerLayer
+    stamps = torch.zeros(G * (L * S + 2), dtype=torch.int64, device="cuda:0")
     for _ in range(3):
         st.decode_step(bufs, list(range(L)))
     torch.cuda.synchronize()
@@ -46,11 +52,11 @@ def main() -> None:
     torch.cuda.synchronize()
     kernels().cake_mk_set_stamps(None)
     st.mk_check(bufs)
-    t = stamps.view(G, L * 10 + 2).cpu().numpy().astype(np.float64)
-    t0 = t[:, L * 10].min()
+    t = stamps.view(G, L * S + 2).cpu().numpy().astype(np.float64)
+    t0 = t[:, L * S].min()
     rel = (t - t0) * 0.01  # us
     rel[t == 0] = np.nan
-    ph = rel[:, :L * 10].reshape(G, L, 10)
+    ph = rel[:, :L * S].reshape(G, L, S)
     mid = slice(1, L - 1) if L > 2 else slice(0, L)
 
     def med(x):
@@ -78,8 +84,16 @@ def main() -> None:
     rows["skew_down_done"] = med(np.nanmax(ph[:, mid, 8], 0) - np.nanmedian(ph[:, mid, 8], 0))
     lay = np.nanmedian(ph[:, 1:, 0], 0) - np.nanmedian(ph[:, :-1, 0], 0)
     rows["layer_us_median"] = float(np.median(lay))
-    rows["step_us"] = float(np.nanmax(rel[:, L * 10 + 1]))
-    out = {"model": a.model, "layers": L, "pos": a.pos, "grid": G,
+    # loader 0: o_proj first / last slot issued, gate/up and down first slot issued,
+    # relative to this layer's QKV x-ready of the same workgroup
+    x0 = ph[:, mid, 0]
+    for k, name in ((10, "ld_o_first"), (11, "ld_o_last"), (12, "ld_swi_first"), (13, "ld_down_first")):
+        rows[name] = med(ph[:, mid, k] - x0)
+    for k, name in ((1, "qkv_done"), (2, "qkv_pub"), (3, "o_xready"), (4, "o_done"), (5, "swi_xready"),
+                    (6, "swi_done"), (7, "down_xready"), (8, "down_done")):
+        rows["t_" + name] = med(ph[:, mid, k] - x0)
+    rows["step_us"] = float(np.nanmax(rel[:, L * S + 1]))
+    out = {"model": a.model, "layers": L, "pos": a.pos, "grid": G, "thin": a.thin, "ring": a.ring,
            **{k: round(v, 3) for k, v in rows.items()}}
     print(json.dumps(out))
     if a.out:

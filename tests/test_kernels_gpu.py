@@ -125,7 +125,7 @@ def test_attn_decode(cuda, attn_impl, dt, nh, nkv, hd, pos, S, min_keys):
     p = torch.tensor([pos], dtype=torch.int32, device=cuda)
     part = torch.zeros(K_.attn_workspace_numel(nh, hd, S), device=cuda)
     out = torch.empty(nh * hd, device=cuda, dtype=dt)
-    tickets = torch.zeros(2 * nkv, dtype=torch.int32, device=cuda)
+    tickets = torch.zeros(2 * nkv + 2, dtype=torch.int32, device=cuda)
     K_.attn_set_min_keys(min_keys)
     try:
         # the first call (another q) leaves its partials behind: the second must not
@@ -141,6 +141,31 @@ def test_attn_decode(cuda, attn_impl, dt, nh, nkv, hd, pos, S, min_keys):
     ref = R.attention(q.view(1, nh, hd), kc[:, :Tk].transpose(0, 1), vc[:, :Tk].transpose(0, 1),
                       pos).reshape(-1)
     torch.testing.assert_close(out.float(), ref, **_tol(dt))
+
+
+def test_attn_decode_merge_timeout_raises(cuda):
+    """Core 2's split 0 spins on the other splits' partials: if they never arrive, the
+    bounded poll must end the launch and raise the error word (not merge stale partials
+    silently)."""
+    from cake_amd.ops import hip as K_
+    nh, nkv, hd, S, pos = 32, 8, 128, 2048, 1500  # > 320 keys: several splits
+    kc = _rand(nkv, S, hd, dt=torch.bfloat16)
+    vc = _rand(nkv, S, hd, dt=torch.bfloat16)
+    q = torch.randn(nh * hd, device=cuda)
+    p = torch.tensor([pos], dtype=torch.int32, device=cuda)
+    part = torch.zeros(K_.attn_workspace_numel(nh, hd, S), device=cuda)
+    out = torch.empty(nh * hd, device=cuda, dtype=torch.bfloat16)
+    tickets = torch.zeros(2 * nkv + 2, dtype=torch.int32, device=cuda)
+    K_.attn_set_impl(2)
+    K_.attn_decode(q, kc, vc, p, 1 / math.sqrt(hd), part, tickets, out)
+    assert not K_.attn_error(tickets)
+    K_.attn_debug_drop_partials(True)
+    try:
+        K_.attn_decode(q, kc, vc, p, 1 / math.sqrt(hd), part, tickets, out)
+        torch.cuda.synchronize()
+    finally:
+        K_.attn_debug_drop_partials(False)
+    assert K_.attn_error(tickets)
 
 
 def test_wave_reductions(cuda):
@@ -175,7 +200,7 @@ def test_attn_decode_dead_rows_nan(cuda, attn_impl, pos):
     p = torch.tensor([pos], dtype=torch.int32, device=cuda)
     part = torch.zeros(K_.attn_workspace_numel(nh, hd, S), device=cuda)
     out = torch.empty(nh * hd, device=cuda, dtype=torch.bfloat16)
-    tickets = torch.zeros(2 * nkv, dtype=torch.int32, device=cuda)
+    tickets = torch.zeros(2 * nkv + 2, dtype=torch.int32, device=cuda)
     K_.attn_decode(q, kc, vc, p, 1 / math.sqrt(hd), part, tickets, out)
     Tk = pos + 1
     ref = R.attention(q.view(1, nh, hd), kc[:, :Tk].transpose(0, 1), vc[:, :Tk].transpose(0, 1),

