@@ -51,10 +51,9 @@ constexpr int kNW = 8;          // waves per workgroup
 constexpr int kNL = 2;          // loader waves (the last kNL)
 constexpr int kNC = kNW - kNL;  // consumer waves 0 .. kNC-1
 constexpr int kNCT = kNC * 64;  // consumer threads
-constexpr int kJN = 22;         // residual-row words per consumer thread (H <= kJN * kNCT)
 constexpr int kSlot = 16384;    // ring slot bytes: 8 pair-blocks (row a + row b, 1 KB each)
 constexpr int kPB = 8;          // pair-blocks per slot
-constexpr int kFly = 3;         // slots the loader keeps in flight beyond the one it waits for
+constexpr int kMaxFly = 3;      // slots a loader may keep in flight beyond the one it waits for
 constexpr int kMaxRing = 8;
 
 struct Layer {  // device-side pointer table, one entry per layer
@@ -81,6 +80,8 @@ struct Args {
   int maxsplit, single, target, min_keys;
   int ring;               // ring slots
   int thin;               // loader keeps one slot in flight while consumers gather
+  int fly;                // slots each loader keeps in flight beyond the one it waits for
+  int o_all;              // o_proj rows on every workgroup (1) or not on the mergers (0)
   unsigned long long timeout;  // s_memrealtime ticks (100 MHz)
   unsigned long long* stamps;  // diagnostics (nullptr in production): per-WG phase clocks
 };
@@ -235,51 +236,52 @@ __device__ __forceinline__ void gather_u32(const u64* g, int n, unsigned tag, un
 }
 
 // Residual row (H f32: granules, or plain memory written by an earlier launch) ->
-// xs[H] = model-dtype(raw * rsqrt(mean(raw^2) + eps) * w), and the f32 rows
-// [row_lo, row_lo + nrow) (the residual rows this workgroup's next epilogue adds to) into
-// rows[], consumer
-// threads; ends with a consumer barrier.
-template <int DT, int J>
+// xs[H] = model-dtype(raw * w * rsqrt(mean(raw^2) + eps)), and the f32 rows
+// [row_lo, row_lo + nrow) (the residual rows this workgroup's next epilogue adds to)
+// into rows[]; consumer threads, 8 words per thread in flight per pass (raw * w staged
+// in LDS at stage[H], so no per-thread arrays of H / threads entries are live); ends
+// with a consumer barrier.
+template <int DT>
 __device__ __forceinline__ void gather_norm(const u64* g, const float* plain, int H, unsigned tag,
                                             const uint16_t* w, float eps, float* rows,
-                                            int row_lo, int nrow,
-                                            uint16_t* xs, float* red, CBar& cb, const Args& a,
-                                            Spin& sp, int site) {
+                                            int row_lo, int nrow, uint16_t* xs, float* stage,
+                                            float* red, CBar& cb, const Args& a, Spin& sp,
+                                            int site) {
   const int ct = otid();
-  int idx[J];
-  unsigned v[J];
-  float wv[J];
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    idx[j] = j * kNCT + ct;
-    wv[j] = to_f32<DT>(gp(w)[idx[j] < H ? idx[j] : 0]);
-  }
-  if (plain != nullptr) {
-#pragma unroll
-    for (int j = 0; j < J; ++j) v[j] = __float_as_uint(gp(plain)[idx[j] < H ? idx[j] : 0]);
-  } else {
-    poll<J>(g, idx, H, tag, v, a, sp, site);
-  }
   float ss = 0.f;
+  for (int base = 0; base < H; base += 8 * kNCT) {
+    int idx[8];
+    unsigned v[8];
+    float wv[8];
 #pragma unroll
-  for (int j = 0; j < J; ++j) {
-    const float f = __uint_as_float(v[j]);
-    if (idx[j] < H) {
-      ss = fmaf(f, f, ss);
-      if ((unsigned)(idx[j] - row_lo) < (unsigned)nrow) rows[idx[j] - row_lo] = f;
+    for (int j = 0; j < 8; ++j) {
+      idx[j] = base + j * kNCT + ct;
+      wv[j] = to_f32<DT>(gp(w)[idx[j] < H ? idx[j] : 0]);
+    }
+    if (plain != nullptr) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = __float_as_uint(gp(plain)[idx[j] < H ? idx[j] : 0]);
+    } else {
+      poll<8>(g, idx, H, tag, v, a, sp, site);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float f = __uint_as_float(v[j]);
+      if (idx[j] < H) {
+        ss = fmaf(f, f, ss);
+        stage[idx[j]] = f * wv[j];
+        if ((unsigned)(idx[j] - row_lo) < (unsigned)nrow) rows[idx[j] - row_lo] = f;
+      }
     }
   }
   ss = wave_sum(ss);
-  const int wave = ct >> 6;
-  if ((ct & 63) == 0) red[wave] = ss;
+  if ((ct & 63) == 0) red[ct >> 6] = ss;
   cbar(cb);
   float tot = 0.f;
 #pragma unroll
   for (int w2 = 0; w2 < kNC; ++w2) tot += red[w2];
   const float r = rsqrtf(tot / (float)H + eps);
-#pragma unroll
-  for (int j = 0; j < J; ++j)
-    if (idx[j] < H) xs[idx[j]] = from_f32<DT>(__uint_as_float(v[j]) * r * wv[j]);
+  for (int i = ct; i < H; i += kNCT) xs[i] = from_f32<DT>(stage[i] * r);
   cbar(cb);
 }
 
@@ -334,7 +336,9 @@ __device__ __forceinline__ Op layer_op(const Args& a, const CAKE_C Layer* ly, in
                                        int wg, int o_ip) {
   const int H = a.H, I = a.I, nh = a.nh, nkv = a.nkv;
   if (k == 0) return make_op(ly->wqkv, kQKV, H, (nh + 2 * nkv) * (HD / 2), G, wg, 1, 0u);
-  if (k == 1) return make_op(ly->wo, kRows2, nh * HD, H / 2, G, wg, 1, 0u);
+  if (k == 1)
+    return a.o_all ? make_op(ly->wo, kRows2, nh * HD, H / 2, G, wg, 1, 0u)
+                   : make_op(ly->wo, kRows2, nh * HD, H / 2, G - nkv, o_ip, 1, 0u);
   if (k == 2) return make_op(ly->wgu, kGU, H, I, G, wg, 2, (unsigned)I * (unsigned)H * 2u);
   return make_op(ly->wd, kRows2, I, H / 2, G, wg, 1, 0u);
 }
@@ -451,9 +455,16 @@ __device__ void loader_run(const Args& a, int G, int wg, int o_ip, unsigned ring
         if (a.thin && lds_ld(&rc->gath) != 0u) {
           __builtin_amdgcn_s_waitcnt(vm_wait(0));
           mark_all();
-        } else if (fly > kFly) {
-          __builtin_amdgcn_s_waitcnt(vm_wait(2 * kPB * kFly));
-          const unsigned q = last - kFly * kNL;
+        } else if (fly > (unsigned)a.fly) {
+          // the oldest of this loader's slots has landed once at most a.fly newer ones
+          // (2 kPB loads each) are outstanding
+          switch (a.fly) {
+            case 0: __builtin_amdgcn_s_waitcnt(vm_wait(0)); break;
+            case 1: __builtin_amdgcn_s_waitcnt(vm_wait(2 * kPB)); break;
+            case 2: __builtin_amdgcn_s_waitcnt(vm_wait(4 * kPB)); break;
+            default: __builtin_amdgcn_s_waitcnt(vm_wait(6 * kPB)); break;
+          }
+          const unsigned q = last - (unsigned)a.fly * kNL;
           lds_st(&rc->full[q % NS], q + 1u);
           --fly;
         }
@@ -923,7 +934,7 @@ __host__ __device__ inline Lds lds_layout(int H, int I, int nh, int hd, int nrep
   o.raw = o.ctl + (unsigned)((sizeof(RingCtl) + 15) / 16 * 16);
   o.part = o.raw + (unsigned)kMaxRows * 4u;
   o.xs = o.part + (unsigned)(maxpl * kNC * 2 * 4 + 15) / 16 * 16;
-  unsigned xs = (unsigned)H * 2u;
+  unsigned xs = (unsigned)H * 6u;  // 16-bit normalised row + its f32 staging
   const unsigned x16 = (unsigned)(nh * hd > I ? nh * hd : I) * 2u;
   if (x16 > xs) xs = x16;
   const unsigned at = 4u * (unsigned)(kNC * (kKeys * 16 + 16) + kNC * (32 + nrep * hd) + nrep * hd +
@@ -989,8 +1000,8 @@ __global__ __launch_bounds__(kNW * 64) void mk_decode_kernel(Args a) {
       // ---------------- QKV + RoPE + KV write ----------------
       set_gath(1u);
       const Op oo = layer_op<HD>(a, ly, 1, G, wg, o_ip);
-      gather_norm<DT, kJN>(gl + go.res, l == 0 ? a.resid : nullptr, H, tag, ly->ln1, a.eps, rows,
-                           2 * oo.pbeg, 2 * oo.npl, xs,
+      gather_norm<DT>(gl + go.res, l == 0 ? a.resid : nullptr, H, tag, ly->ln1, a.eps, rows,
+                      2 * oo.pbeg, 2 * oo.npl, xs, reinterpret_cast<float*>(xs + H),
                           rc->red, cb, a, sp, 1);
       set_gath(0u);
       MK_STAMP(sb + 0);
@@ -1062,8 +1073,8 @@ __global__ __launch_bounds__(kNW * 64) void mk_decode_kernel(Args a) {
       // ---------------- RMSNorm + gate/up + SwiGLU ----------------
       set_gath(1u);
       const Op od = layer_op<HD>(a, ly, 3, G, wg, o_ip);
-      gather_norm<DT, kJN>(gl + go.mid, nullptr, H, tag, ly->ln2, a.eps, rows, 2 * od.pbeg,
-                           2 * od.npl, xs, rc->red, cb, a,
+      gather_norm<DT>(gl + go.mid, nullptr, H, tag, ly->ln2, a.eps, rows, 2 * od.pbeg,
+                      2 * od.npl, xs, reinterpret_cast<float*>(xs + H), rc->red, cb, a,
                           sp, 3);
       set_gath(0u);
       MK_STAMP(sb + 5);
@@ -1137,6 +1148,8 @@ int g_mk_grid = 0;
 unsigned long long* g_mk_stamps = nullptr;  // diagnostics only
 int g_mk_thin = 1;
 int g_mk_ring = 0;  // 0 = as many slots as fit
+int g_mk_fly = 1;
+int g_mk_o_all = 1;
 
 int mk_grid() {
   if (g_mk_grid > 0) return g_mk_grid;
@@ -1192,12 +1205,17 @@ CAKE_API int cake_mk_set_stamps(void* p) {
   return 0;
 }
 
-// Tuning / A-B: loader thinning during gathers (0/1) and a cap on the ring slots
-// (0 = as many as fit in LDS).
-CAKE_API int cake_mk_set_tuning(int thin, int ring) {
-  if (ring < 0 || ring > mk::kMaxRing) return (int)hipErrorInvalidValue;
+// Tuning / A-B: loader thinning during gathers (0/1), a cap on the ring slots (0 = as
+// many as fit in LDS) and the slots each loader keeps in flight beyond the one it waits
+// for (0..3): HBM saturates at a small in-flight depth per CU, and every slot in flight
+// is one not yet landed — ring space that banks no credit across an edge.
+CAKE_API int cake_mk_set_tuning(int thin, int ring, int fly, int o_all) {
+  if (ring < 0 || ring > mk::kMaxRing || fly < 0 || fly > mk::kMaxFly)
+    return (int)hipErrorInvalidValue;
   g_mk_thin = thin != 0;
   g_mk_ring = ring;
+  g_mk_fly = fly;
+  g_mk_o_all = o_all != 0;
   return 0;
 }
 
@@ -1209,11 +1227,11 @@ CAKE_API int cake_mk_supported(int H, int I, int nh, int nkv, int hd) {
   if (hd != 128 || nkv <= 0 || nh % nkv) return 3;
   const int nrep = nh / nkv;
   if (nrep != 4 && nrep != 8) return 4;
-  if (H > mk::kJN * mk::kNCT) return 5;
+  if (H % 8) return 5;
   if (G < nkv * (mk::kMaxSplitMk + 8) || G - nkv < 1 || G > mk::kMaxG) return 6;
   if (ring_slots(H, I, nh, hd, nrep, G) < 2) return 7;
   if ((H / 2) < G || (nh + 2 * nkv) * hd / 2 < G) return 8;
-  if (2 * ((H / 2 + G - 1) / G) > mk::kMaxRows) return 9;
+  if (2 * ((H / 2 + G - nkv - 1) / (G - nkv)) > mk::kMaxRows) return 9;
   return 0;
 }
 
@@ -1244,6 +1262,8 @@ CAKE_API int cake_mk_decode(int dt, const void* layers, int L, int H, int I, int
   a.min_keys = 64;
   a.ring = ring_slots(H, I, nh, hd, nrep, G);
   a.thin = g_mk_thin;
+  a.fly = g_mk_fly;
+  a.o_all = g_mk_o_all;
   a.timeout = (unsigned long long)(timeout_s * 1e8);
   a.stamps = g_mk_stamps;
   const size_t lds = mk::lds_layout(H, I, nh, hd, nrep, G, a.ring).total;

@@ -132,5 +132,5 @@ _SIGS.update({
 })
 _RESTYPE = {"cake_mk_gstride": C.c_longlong}
 _SIGS["cake_mk_set_stamps"] = [P]
-_SIGS["cake_mk_set_tuning"] = [I, I]
+_SIGS["cake_mk_set_tuning"] = [I, I, I, I]
 _SIGS["cake_attn_debug_drop_partials"] = [I]

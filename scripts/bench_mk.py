@@ -29,9 +29,11 @@ def main() -> None:
     ap.add_argument("--max-seq", type=int, default=4096)
     ap.add_argument("--thin", type=int, default=1)
     ap.add_argument("--ring", type=int, default=0)
+    ap.add_argument("--fly", type=int, default=1)
+    ap.add_argument("--o-all", type=int, default=1)
     a = ap.parse_args()
     from cake_amd.ops._lib import kernels as _k
-    _k().cake_mk_set_tuning(a.thin, a.ring)
+    _k().cake_mk_set_tuning(a.thin, a.ring, a.fly, a.o_all)
     over = {"num_hidden_layers": a.layers} if a.layers else {}
     cfg = preset(a.model, **over)
     layers = list(range(cfg.num_hidden_layers))
@@ -72,7 +74,7 @@ def main() -> None:
             e1.synchronize()
             us = e0.elapsed_time(e1) * 1e3 / a.reps
             rec = {"path": path, "model": a.model, "layers": len(layers), "pos": pos,
-                   "thin": a.thin, "ring": a.ring,
+                   "thin": a.thin, "ring": a.ring, "fly": a.fly, "o_all": a.o_all,
                    "us_per_step": round(us, 2), "us_per_layer": round(us / len(layers), 3),
                    "TBps": round(nbytes / us / 1e6, 3)}
             if path == "mk":

@@ -32,9 +32,11 @@ def main() -> None:
     ap.add_argument("--out", default="")
     ap.add_argument("--thin", type=int, default=1)
     ap.add_argument("--ring", type=int, default=0)
+    ap.add_argument("--fly", type=int, default=1)
+    ap.add_argument("--o-all", type=int, default=1)
     a = ap.parse_args()
     from cake_amd.ops._lib import kernels as _k
-    _k().cake_mk_set_tuning(a.thin, a.ring)
+    _k().cake_mk_set_tuning(a.thin, a.ring, a.fly, a.o_all)
     cfg = preset(a.model, **({"num_hidden_layers": a.layers} if a.layers else {}))
     L = cfg.num_hidden_layers
     st = random_stack(cfg, list(range(L)), "cuda:0", torch.bfloat16, max_seq=4096)
@@ -93,7 +95,7 @@ def main() -> None:
                     (6, "swi_done"), (7, "down_xready"), (8, "down_done")):
         rows["t_" + name] = med(ph[:, mid, k] - x0)
     rows["step_us"] = float(np.nanmax(rel[:, L * S + 1]))
-    out = {"model": a.model, "layers": L, "pos": a.pos, "grid": G, "thin": a.thin, "ring": a.ring,
+    out = {"model": a.model, "layers": L, "pos": a.pos, "grid": G, "thin": a.thin, "ring": a.ring, "fly": a.fly, "o_all": a.o_all,
            **{k: round(v, 3) for k, v in rows.items()}}
     print(json.dumps(out))
     if a.out:

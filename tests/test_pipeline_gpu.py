@@ -14,9 +14,9 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _bench(tmp_path, n, streams, name, hop="dist", hop_dtype="f32", k=1):
+def _bench(tmp_path, n, streams, name, hop="dist", hop_dtype="f32", k=1, steps=12):
     out = tmp_path / f"{name}.json"
-    args = ["bench.py", "--model", "tiny", "--steps", "12", "--warmup", "3", "--prompt-len", "9",
+    args = ["bench.py", "--model", "tiny", "--steps", str(steps), "--warmup", "3", "--prompt-len", "9",
             "--max-seq", "256", "--dump-tokens", str(out)]
     if n > 1:
         args += ["--gpus", str(n), "--parallel", "pp", "--dist-backend", "gloo",
@@ -55,10 +55,15 @@ def test_pipeline_ipc_hops_in_graph_match_single(cuda, tmp_path):
     assert m3["hop"] == "ipc" and pp3[0][:len(single[0])] == single[0]
     m4, pp4 = _bench(tmp_path, 2, 2, "ipc2s", hop="ipc")
     assert m4["hop"] == "ipc" and pp4[0] == single[0] and len(pp4) == 2
-    m5, pp5 = _bench(tmp_path, 2, 1, "ipc2bf", hop="ipc", hop_dtype="bf16")
-    assert m5["hop"] == "ipc-bf16" and len(pp5[0]) == len(single[0])
-    # bf16 payloads round the residual stream once per hop (~2^-8 relative), so greedy
-    # tokens may part from the f32 run at a near-tie late in the sequence; a corrupted or
-    # misrouted hop changes them from the first token on.  Fixed seed: deterministic.
-    agree = next((i for i, (a, b) in enumerate(zip(pp5[0], single[0])) if a != b), len(single[0]))
-    assert agree >= min(8, len(single[0])), (agree, pp5[0], single[0])
+    m5, pp5 = _bench(tmp_path, 2, 1, "ipc2bf", hop="ipc", hop_dtype="bf16", steps=40)
+    assert m5["hop"] == "ipc-bf16"
+    # bf16 payloads round the residual stream once per hop (~2^-8 relative): every step
+    # of the bf16-hop stream is checked against the single-GPU model teacher-forced on
+    # that stream — its pick is the reference argmax or within 0.1 of it
+    import torch
+    from _equiv import teacher_forced_check
+    from cake_amd.models.llama3.factory import random_model
+    model = random_model("tiny", "cuda:0", torch.bfloat16, max_seq=256)
+    chk = teacher_forced_check(model, pp5[0], 9, 1.1, 128, tol=0.1)
+    assert chk["steps"] >= 32 and not chk["bad"], chk
+    assert chk["near_ties"] <= chk["steps"] // 4, chk

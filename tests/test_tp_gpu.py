@@ -27,7 +27,7 @@ def _cfg(world=2):
 
 
 PROMPT = [3, 14, 15, 92, 65, 35, 89, 79]
-STEPS = 12
+STEPS = 40
 
 
 def _worker(rank, world, port, mode, q):
@@ -40,12 +40,12 @@ def _worker(rank, world, port, mode, q):
     try:
         torch.cuda.set_device(0)
         cfg = _cfg(world)
-        m = random_model(cfg, "cuda:0", torch.bfloat16, max_seq=64, seed=5)
+        m = random_model(cfg, "cuda:0", torch.bfloat16, max_seq=96, seed=5)
         blocks = {li: shard_block(w, cfg, rank, world) for li, w in m.stack.weights.items()}
         head = shard_head(m.head.embed, m.head.norm, m.head.lm_head, rank, world)
         del m
         comm = AllReduce(rank, world, "cuda:0", cfg.hidden_size, mode=mode)
-        eng = TPEngine(cfg, blocks, head, rank, world, "cuda:0", torch.bfloat16, 64, comm,
+        eng = TPEngine(cfg, blocks, head, rank, world, "cuda:0", torch.bfloat16, 96, comm,
                        repeat_penalty=1.1, repeat_last_n=16)
         eng.prefill(PROMPT)
         eng.capture()
@@ -66,11 +66,11 @@ def _reference(world):
     from cake_amd.models.llama3.decode_loop import run_decode
     from cake_amd.models.llama3.factory import random_model
     from cake_amd.models.llama3.model import DeviceDecoder
-    m = random_model(_cfg(world), "cuda:0", torch.bfloat16, max_seq=64, seed=5)
+    m = random_model(_cfg(world), "cuda:0", torch.bfloat16, max_seq=96, seed=5)
     dec = DeviceDecoder(m, repeat_penalty=1.1, repeat_last_n=16)
     first = dec.start(PROMPT)
     dec.capture()
-    return PROMPT + [first] + run_decode(dec, STEPS).tokens
+    return PROMPT + [first] + run_decode(dec, STEPS).tokens, m
 
 
 @pytest.mark.parametrize("mode,world", [("ipc", 2), ("dist", 2), ("ipc", 4), ("dist", 1)])
@@ -78,7 +78,8 @@ def test_tp_matches_single_gpu(cuda, mode, world):
     """world ranks share cuda:0 (a 4-rank run exercises the all-reduce kernels' bank /
     peer indexing beyond a pair; one rank takes the in-place accumulate path)."""
     import torch.multiprocessing as mp
-    ref = _reference(world)
+    from _equiv import teacher_forced_check
+    ref, model = _reference(world)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -101,10 +102,12 @@ def test_tp_matches_single_gpu(cuda, mode, world):
     assert got[0][0] == mode, got[0][0]    # the IPC self-test passed (no silent fallback)
     toks = got[0][1]
     assert len(toks) == len(ref)
-    # bf16 partial sums add in a different order than the single-GPU GEMVs: the first
-    # generated tokens must agree exactly
-    n = len(PROMPT) + 4
-    assert toks[:n] == ref[:n], (toks, ref)
+    # every one of the >= 32 generated steps against the single-GPU model teacher-forced
+    # on the TP stream: the TP pick is the reference argmax, or within 0.02 of it (the
+    # all-reduce sums the per-rank partial rows in another order than one GPU's GEMV)
+    chk = teacher_forced_check(model, toks, len(PROMPT), 1.1, 16, tol=0.02)
+    assert chk["steps"] >= 32 and not chk["bad"], chk
+    assert chk["near_ties"] <= chk["steps"] // 8, chk
     if mode == "ipc":
         assert got[0][2] is not None and got[0][2] > 0
 
@@ -145,12 +148,12 @@ def _sample_worker(rank, world, port, q):
     try:
         torch.cuda.set_device(0)
         cfg = _cfg(world)
-        m = random_model(cfg, "cuda:0", torch.bfloat16, max_seq=64, seed=5)
+        m = random_model(cfg, "cuda:0", torch.bfloat16, max_seq=96, seed=5)
         blocks = {li: shard_block(w, cfg, rank, world) for li, w in m.stack.weights.items()}
         head = shard_head(m.head.embed, m.head.norm, m.head.lm_head, rank, world)
         del m
         comm = AllReduce(rank, world, "cuda:0", cfg.hidden_size, n_gather=cfg.vocab_size)
-        eng = TPEngine(cfg, blocks, head, rank, world, "cuda:0", torch.bfloat16, 64, comm,
+        eng = TPEngine(cfg, blocks, head, rank, world, "cuda:0", torch.bfloat16, 96, comm,
                        repeat_penalty=1.1, repeat_last_n=16)
         out, graph_ids = [], []
         for seed in (7, 8):
