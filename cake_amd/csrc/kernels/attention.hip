@@ -45,10 +45,10 @@ __global__ __launch_bounds__(AttnGeom<NREP>::NT) void attn_decode_kernel(AttnDec
 }
 
 template <int DT, int HD, int NREP>
-__global__ __launch_bounds__(AttnGeom<NREP>::NT) void attn2_decode_kernel(AttnDecArgs a) {
+__global__ __launch_bounds__(AttnGeom2<NREP>::NT) void attn2_decode_kernel(AttnDecArgs a) {
   __shared__ __attribute__((aligned(16)))
-      float lds[attn2_smem_floats<HD, NREP, AttnGeom<NREP>::NW>()];
-  attn2_decode_block<DT, HD, NREP>(a, blockIdx.x, blockIdx.y, lds);
+      float lds[attn2_smem_floats<HD, NREP, AttnGeom2<NREP>::NW>()];
+  attn2_decode_block<DT, HD, NREP>(a, blockIdx.x, blockIdx.y, lds, gridDim.x);
 }
 
 }  // namespace cake
@@ -146,8 +146,8 @@ template <int DT, int HD>
 static int launch_decode(int n_rep, dim3 grid, hipStream_t st, const AttnDecArgs& a) {
 #define CAKE_DEC(NR)                                                                          \
   if (g_attn_impl == 2 &&                                                                     \
-      grid_resident(attn2_decode_kernel<DT, HD, NR>, AttnGeom<NR>::NT, (long long)grid.x * grid.y)) \
-    hipLaunchKernelGGL((attn2_decode_kernel<DT, HD, NR>), grid, dim3(AttnGeom<NR>::NT), 0, st, a); \
+      grid_resident(attn2_decode_kernel<DT, HD, NR>, AttnGeom2<NR>::NT, (long long)grid.x * grid.y)) \
+    hipLaunchKernelGGL((attn2_decode_kernel<DT, HD, NR>), grid, dim3(AttnGeom2<NR>::NT), 0, st, a); \
   else                                                                                        \
     hipLaunchKernelGGL((attn_decode_kernel<DT, HD, NR>), grid, dim3(AttnGeom<NR>::NT), 0, st, a)
   switch (n_rep) {

@@ -56,6 +56,16 @@ constexpr int attn2_smem_floats() {
   return NW * (kBlk * 16 + 16) + NW * (32 + NREP * HD) + 1;
 }
 
+// Core 2's workgroup: 12 waves (3 per SIMD: its ~156 VGPRs fit) for GQA groups of <= 4
+// heads, so up to 192 keys every wave owns ONE 16-key block whose loads were issued at
+// launch — the key loop is no longer a chain of dependent load round trips (4 waves:
+// ~1800 cycles per extra block, profiles/r3_attn_stamps_single_phases.jsonl); 8 waves
+// for 8-head groups (~200 VGPRs: 2 per SIMD).
+template <int NREP> struct AttnGeom2 {
+  static constexpr int NW = NREP >= 8 ? 8 : 12;
+  static constexpr int NT = 64 * NW;
+};
+
 // host/device split policy of the v2 core (mirrored by ops.hip.attn_splits)
 __device__ __forceinline__ void attn2_splits(int Tk, int min_keys, int maxsplit, int target,
                                              int single, int& ns, int& kps) {
@@ -74,10 +84,24 @@ __device__ __forceinline__ void attn2_splits(int Tk, int min_keys, int maxsplit,
   ns = (Tk + kps - 1) / kps;
 }
 
-template <int DT, int HD, int NREP>
+// Agent-coherent (sc1, L2-served, L1 bypassed) 16-byte buffer loads: the fused QKV ->
+// attention tail (gemv.hip qkv_attn_kernel) reads q and the new K/V row that other
+// workgroups of the same launch stored write-through (MI355X_MICROARCH "Valid forms").
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t sc1_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ uint4 ld16_sc1(__amdgpu_buffer_rsrc_t r, size_t byte_off) {
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)byte_off, 0, 16);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// FUSED: called by the last-arriving workgroup of kv group g inside the QKV launch —
+// q / K / V loads are sc1 and the whole context runs as one split (the host picks the
+// fused launch where attn2_splits gives one split; longer contexts stay correct, one
+// workgroup walking every key).  ng = number of kv heads (the standalone grid's x).
+template <int DT, int HD, int NREP, bool FUSED = false, int NW = AttnGeom2<NREP>::NW>
 __device__ __forceinline__ void attn2_decode_block(const AttnDecArgs& a, int g, int s,
-                                                   float* lds) {
-  constexpr int NW = AttnGeom<NREP>::NW;
+                                                   float* lds, int ng) {
   constexpr int DS = HD / 32;    // MFMA k-steps (A fragments) per key block
   constexpr int NCH = HD / 8;    // 8-dim chunks per row
   constexpr int KPL = NCH / 4;   // keys per lane in P.V (16 keys over 64 / NCH key groups)
@@ -96,16 +120,22 @@ __device__ __forceinline__ void attn2_decode_block(const AttnDecArgs& a, int g, 
 
   // one block's operands: K A-fragments and V rows of this lane
   uint4 kf[DS], vf[KPL];
+  __amdgpu_buffer_rsrc_t krs, vrs;
+  if constexpr (FUSED) { krs = sc1_rsrc(kgp); vrs = sc1_rsrc(vgp); }
   auto load_blk = [&](int key0, int last) {
 #pragma unroll
     for (int d = 0; d < DS; ++d) {
       const int r = min(key0 + col, last);
-      kf[d] = *reinterpret_cast<const uint4*>(kgp + (size_t)r * HD + d * 32 + rg * 8);
+      const size_t o = (size_t)r * HD + d * 32 + rg * 8;
+      if constexpr (FUSED) kf[d] = ld16_sc1(krs, o * 2);
+      else kf[d] = *reinterpret_cast<const uint4*>(kgp + o);
     }
 #pragma unroll
     for (int j = 0; j < KPL; ++j) {
       const int r = min(key0 + kg * KPL + j, last);
-      vf[j] = *reinterpret_cast<const uint4*>(vgp + (size_t)r * HD + ch * 8);
+      const size_t o = (size_t)r * HD + ch * 8;
+      if constexpr (FUSED) vf[j] = ld16_sc1(vrs, o * 2);
+      else vf[j] = *reinterpret_cast<const uint4*>(vgp + o);
     }
   };
 
@@ -119,9 +149,16 @@ __device__ __forceinline__ void attn2_decode_block(const AttnDecArgs& a, int g, 
 #pragma unroll
     for (int d = 0; d < DS; ++d) {
       if (col < NREP) {
-        const float* qp = a.q + (size_t)(g * NREP + col) * HD + d * 32 + rg * 8;
-        const float4 x0 = *reinterpret_cast<const float4*>(qp);
-        const float4 x1 = *reinterpret_cast<const float4*>(qp + 4);
+        const size_t qo = (size_t)(g * NREP + col) * HD + d * 32 + rg * 8;
+        float4 x0, x1;
+        if constexpr (FUSED) {
+          const __amdgpu_buffer_rsrc_t qr = sc1_rsrc(a.q);
+          x0 = __builtin_bit_cast(float4, ld16_sc1(qr, qo * 4));
+          x1 = __builtin_bit_cast(float4, ld16_sc1(qr, qo * 4 + 16));
+        } else {
+          x0 = *reinterpret_cast<const float4*>(a.q + qo);
+          x1 = *reinterpret_cast<const float4*>(a.q + qo + 4);
+        }
         qv[d][0] = x0.x; qv[d][1] = x0.y; qv[d][2] = x0.z; qv[d][3] = x0.w;
         qv[d][4] = x1.x; qv[d][5] = x1.y; qv[d][6] = x1.z; qv[d][7] = x1.w;
       } else {
@@ -138,10 +175,15 @@ __device__ __forceinline__ void attn2_decode_block(const AttnDecArgs& a, int g, 
     }
   }
   const int Tk = *a.pos + 1;
-  const unsigned int epoch = a.tickets[gridDim.x + g];  // this launch's granule tag - 1
+  const unsigned int epoch = a.tickets[ng + g];  // this launch's granule tag - 1
   ATTN_STAMP(1);
   int ns, kps;
-  attn2_splits(Tk, a.min_keys, a.maxsplit, a.target, a.single, ns, kps);
+  if constexpr (FUSED) {
+    ns = 1;
+    kps = (Tk + kBlk - 1) / kBlk * kBlk;
+  } else {
+    attn2_splits(Tk, a.min_keys, a.maxsplit, a.target, a.single, ns, kps);
+  }
   if (s >= ns) return;
   const int kb = s * kps, ke = min(Tk, kb + kps);
   const int nblk = (ke - kb + kBlk - 1) / kBlk;
@@ -270,10 +312,10 @@ __device__ __forceinline__ void attn2_decode_block(const AttnDecArgs& a, int g, 
       if (idx < NOUT) a.out[(size_t)g * NOUT + idx] = from_f32<DT>(ao[i] / lo[i]);
     }
     if (a.stamps != nullptr && tid == 0) {
-      unsigned long long* dd = a.stamps + ((size_t)s * gridDim.x + g) * 8;
+      unsigned long long* dd = a.stamps + ((size_t)s * ng + g) * 8;
       for (int k = 0; k < 8; ++k) dd[k] = (k < 6 || k == 6) ? stamp[k] : 0ull;
     }
-    if (tid == 0) a.tickets[gridDim.x + g] = epoch + 1u;
+    if (tid == 0) a.tickets[ng + g] = epoch + 1u;
     return;
   }
   // Splits >= 1 publish their partial as 8-byte {value, tag} granules (one sc1 store
@@ -301,7 +343,7 @@ __device__ __forceinline__ void attn2_decode_block(const AttnDecArgs& a, int g, 
     }
     ATTN_STAMP(5);
     if (a.stamps != nullptr && tid == 0) {
-      unsigned long long* dd = a.stamps + ((size_t)s * gridDim.x + g) * 8;
+      unsigned long long* dd = a.stamps + ((size_t)s * ng + g) * 8;
       for (int k = 0; k < 8; ++k) dd[k] = k < 6 ? stamp[k] : 0ull;
     }
     return;
@@ -355,7 +397,7 @@ __device__ __forceinline__ void attn2_decode_block(const AttnDecArgs& a, int g, 
       }
       if (__builtin_amdgcn_ballot_w64(!ok) == 0ull) break;
       if (tries > kAttnMaxPolls) {
-        if (lane == 0) attn_poll_timeout(a.tickets + 2 * gridDim.x);
+        if (lane == 0) attn_poll_timeout(a.tickets + 2 * ng);
         break;
       }
       __builtin_amdgcn_s_sleep(1);
@@ -390,7 +432,7 @@ __device__ __forceinline__ void attn2_decode_block(const AttnDecArgs& a, int g, 
         }
         if (__builtin_amdgcn_ballot_w64(!ok) == 0ull) break;
         if (tries > kAttnMaxPolls) {
-          if (lane == 0) attn_poll_timeout(a.tickets + 2 * gridDim.x);
+          if (lane == 0) attn_poll_timeout(a.tickets + 2 * ng);
           break;
         }
         __builtin_amdgcn_s_sleep(1);
@@ -402,9 +444,9 @@ __device__ __forceinline__ void attn2_decode_block(const AttnDecArgs& a, int g, 
     for (int d = 0; d < DPL; ++d) dst[d] = from_f32<DT>(acc[d] * inv);
   }
   ATTN_STAMP(7);
-  if (tid == 0) a.tickets[gridDim.x + g] = epoch + 1u;  // the next launch's tag
+  if (tid == 0) a.tickets[ng + g] = epoch + 1u;  // the next launch's tag
   if (a.stamps != nullptr && tid == 0) {
-    unsigned long long* dd = a.stamps + ((size_t)s * gridDim.x + g) * 8;
+    unsigned long long* dd = a.stamps + ((size_t)s * ng + g) * 8;
     for (int k = 0; k < 8; ++k) dd[k] = (k == 6) ? stamp[5] : stamp[k];
   }
 }

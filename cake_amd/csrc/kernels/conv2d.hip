@@ -561,9 +561,71 @@ __global__ __launch_bounds__(256) void conv_smallc_kernel(ConvArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// 1x1 convolution with few channels (IC, OC <= 16): the VAE's quant_conv (8 -> 8) and
+// post_quant_conv (4 -> 4) on the latent — a per-pixel 16x16 matrix-vector product,
+// bandwidth-bound, so one thread per pixel on the VALU with the filter in LDS (f32).
+// Either side may be planar (NCHW: the module's external layout, read / written here
+// instead of a layout-copy kernel) or channels-last.
+// ---------------------------------------------------------------------------
+constexpr int kPwMaxC = 16;
+
+template <int DT>
+__global__ __launch_bounds__(256) void conv1x1_small_kernel(const uint16_t* __restrict__ x,
+                                                            const uint16_t* __restrict__ w,
+                                                            const uint16_t* __restrict__ bias,
+                                                            uint16_t* __restrict__ out, int N,
+                                                            int HW, int IC, int OC, int in_nchw,
+                                                            int out_nchw) {
+  __shared__ float wsm[kPwMaxC * kPwMaxC + kPwMaxC];
+  for (int i = threadIdx.x; i < IC * OC; i += 256) wsm[i] = to_f32<DT>(w[i]);
+  if (threadIdx.x < OC) wsm[kPwMaxC * kPwMaxC + threadIdx.x] = bias ? to_f32<DT>(bias[threadIdx.x]) : 0.f;
+  __syncthreads();
+  const long long P = (long long)N * HW;
+  for (long long p = (long long)blockIdx.x * 256 + threadIdx.x; p < P; p += (long long)gridDim.x * 256) {
+    const int n = (int)(p / HW), r = (int)(p - (long long)n * HW);
+    float xin[kPwMaxC];
+#pragma unroll
+    for (int c = 0; c < kPwMaxC; ++c)
+      xin[c] = c < IC ? to_f32<DT>(in_nchw ? x[((size_t)n * IC + c) * HW + r] : x[(size_t)p * IC + c])
+                      : 0.f;
+#pragma unroll
+    for (int o = 0; o < kPwMaxC; ++o) {
+      if (o >= OC) break;
+      float acc = wsm[kPwMaxC * kPwMaxC + o];
+#pragma unroll
+      for (int c = 0; c < kPwMaxC; ++c)
+        if (c < IC) acc = fmaf(wsm[o * IC + c], xin[c], acc);
+      const uint16_t v = from_f32<DT>(acc);
+      if (out_nchw) out[((size_t)n * OC + o) * HW + r] = v;
+      else out[(size_t)p * OC + o] = v;
+    }
+  }
+}
+
 }  // namespace cake
 
 using namespace cake;
+
+// x [N, IC, HW] (layout bit 0) or [N, HW, IC]; w [OC, IC]; out [N, OC, HW] (bit 1) or
+// [N, HW, OC]; IC, OC in 1..16.
+CAKE_API int cake_conv1x1_small(int dt, const void* x, const void* w, const void* bias, void* out,
+                                int N, int HW, int IC, int OC, int layout, hipStream_t st) {
+  if (IC < 1 || IC > kPwMaxC || OC < 1 || OC > kPwMaxC || N <= 0 || HW <= 0 || layout < 0 ||
+      layout > 3)
+    return (int)hipErrorInvalidValue;
+  const long long P = (long long)N * HW;
+  const unsigned grid = (unsigned)std::min<long long>((P + 255) / 256, 4096);
+#define CAKE_PW(DTV)                                                                          \
+  hipLaunchKernelGGL((conv1x1_small_kernel<DTV>), dim3(grid), dim3(256), 0, st,              \
+                     (const uint16_t*)x, (const uint16_t*)w, (const uint16_t*)bias,          \
+                     (uint16_t*)out, N, HW, IC, OC, layout & 1, (layout >> 1) & 1)
+  if (dt == kBF16) CAKE_PW(kBF16);
+  else if (dt == kF16) CAKE_PW(kF16);
+  else return (int)hipErrorInvalidValue;
+#undef CAKE_PW
+  return (int)hipGetLastError();
+}
 
 // Workspace (f32 elements) the launcher needs for split-K with `splits` > 1.
 CAKE_API long long cake_conv2d_workspace(int P, int OC, int splits) {

@@ -24,6 +24,7 @@
 //   * The token position is read from device memory so the launches replay
 //     unchanged inside a hipGraph.
 #include "common.h"
+#include "attn_core2.h"
 
 namespace cake {
 
@@ -332,6 +333,115 @@ __global__ __launch_bounds__(kGemvThreads) void qkv_rope_kernel(QkvArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// QKV + RoPE + KV-cache write + short-context GQA attention, one launch
+//
+// The separate attention launch of a decode layer (attention.hip) costs a launch
+// boundary plus its cold start on top of its own ~8-block body at short context.  Here
+// the workgroup that finishes a kv group's q/k/v rows LAST runs that group's attention
+// (attn_core2.h, one split) in the same launch:
+//   * one pair per wave (grid = npairs / 4), so a workgroup's four pairs are four
+//     consecutive dims of one head: their roped outputs meet in LDS and leave as ONE
+//     16-byte (q, f32) or 8-byte (k/v row, 16-bit) write-through (sc1) store per half;
+//   * the storing wave drains (vmcnt 0), the workgroup barriers, one lane adds 1 to the
+//     group's arrival counter (agent scope); the add that returns blocks_per_group - 1
+//     marks the last arriver, which re-arms the counter and reads q and K/V with sc1
+//     loads (MI355X_MICROARCH "Valid forms", row 1);
+//   * the attention tail reuses the x staging LDS (K floats >= the core's 13 KB).
+// tickets: the attention launch's ticket array (arrivals in [0, nkv), the core-2 epochs
+// in [nkv, 2 nkv)); both re-armed in-kernel, so launches of either kind interleave.
+// ---------------------------------------------------------------------------
+struct QkvAttnTail {
+  unsigned int* tickets;
+  uint16_t* out;  // [nh*hd] attention output
+  float scale_log2;
+};
+
+template <int DT, int U, int PFC, int NX, int HD, int NREP>
+__global__ __launch_bounds__(kGemvThreads) void qkv_attn_kernel(QkvArgs a, QkvAttnTail t) {
+  static_assert(AttnGeom<NREP>::NT == kGemvThreads, "attention tail runs on the gemv block");
+  extern __shared__ float xs[];
+  __shared__ float ep[kGemvWaves][2];
+  __shared__ unsigned int last_flag;
+  constexpr int half = HD / 2;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int pb = blockIdx.x * kGemvWaves;  // the block's first pair (grid = npairs / 4)
+  const int p0 = pb + wave;
+  const uint16_t* wq = a.wq;
+  const ptrdiff_t dk = a.wk - a.wq, dv = a.wv - a.wq;
+  const int nh = a.nh, nkv = a.nkv, nqk = a.nh + a.nkv, K = a.K;
+  auto map = [=](int p, const uint16_t*& wa, const uint16_t*& wb) {
+    const int slot = p / half;
+    const bool isq = slot < nh, isk = !isq && slot < nqk;
+    const uint16_t* base = wq + (isq ? 0 : (isk ? dk : dv));
+    const int head = slot - (isq ? 0 : (isk ? nh : nqk));
+    const size_t ra = (size_t)head * HD + (p - slot * half);
+    wa = base + ra * K;
+    wb = base + (ra + half) * K;
+  };
+  Regs<PFC> pre;
+  NormPre<DT, NX> xp;
+  const uint16_t *wa0, *wb0;
+  map(p0, wa0, wb0);
+  if constexpr (NX > 0) xp.load(a.resid, a.norm_w, a.K);
+  __builtin_amdgcn_sched_barrier(0);
+  prefetch_rows<PFC>(wa0, wb0, pre);
+  const float f0 = a.inv_freq[p0 - (p0 / half) * half];
+  __builtin_amdgcn_sched_barrier(0);
+  if constexpr (NX > 0) xp.finish(a.eps, a.K, xs);
+  else stage_rmsnorm<DT>(a.resid, a.norm_w, a.eps, a.K, xs);
+  const int pos = *a.pos;
+  const int slot = pb / half;  // uniform over the block
+  auto epi = [&](int p, float da, float db) {
+    if (lane != 0) return;
+    float oa = da, ob = db;
+    if (slot < nqk) {  // q, k: RoPE
+      float s, c;
+      sincosf((float)pos * f0, &s, &c);
+      oa = da * c - db * s;
+      ob = da * s + db * c;
+    }
+    ep[wave][0] = oa;
+    ep[wave][1] = ob;
+  };
+  run_pairs<DT, true, U, PFC>(map, epi, xs, a.K, (nqk + nkv) * half, p0, 1 << 30, pre);
+  __syncthreads();
+  if (threadIdx.x < 2) {  // half 0: dims i0..i0+3, half 1: i0+half..
+    const int i0 = pb - slot * half + threadIdx.x * half;
+    const float v0 = ep[0][threadIdx.x], v1 = ep[1][threadIdx.x];
+    const float v2 = ep[2][threadIdx.x], v3 = ep[3][threadIdx.x];
+    if (slot < nh) {
+      float* q = a.q_out + (size_t)slot * HD + i0;
+      st_sc1(q, v0); st_sc1(q + 1, v1); st_sc1(q + 2, v2); st_sc1(q + 3, v3);
+    } else {
+      const bool isk = slot < nqk;
+      const int head = slot - (isk ? nh : nqk);
+      uint16_t* row = (isk ? a.kcache : a.vcache) + ((size_t)head * a.S + pos) * HD + i0;
+      const unsigned long long w =
+          (unsigned long long)from_f32<DT>(v0) | ((unsigned long long)from_f32<DT>(v1) << 16) |
+          ((unsigned long long)from_f32<DT>(v2) << 32) | ((unsigned long long)from_f32<DT>(v3) << 48);
+      __hip_atomic_store(reinterpret_cast<unsigned long long*>(row), w, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int g = slot < nh ? slot / NREP : (slot < nqk ? slot - nh : slot - nqk);
+  if (threadIdx.x == 0) {
+    constexpr int bpg = (NREP + 2) * half / kGemvWaves;  // workgroups per kv group
+    const unsigned int n =
+        __hip_atomic_fetch_add(&t.tickets[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned int last = n == (unsigned int)(bpg - 1) ? 1u : 0u;
+    if (last) __hip_atomic_store(&t.tickets[g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last_flag = last;
+  }
+  __syncthreads();
+  if (!last_flag) return;
+  const AttnDecArgs at{a.q_out, a.kcache, a.vcache, a.pos, a.S, t.scale_log2, nullptr, t.tickets,
+                       t.out, 0, 1, nullptr, 1, 0, 0};
+  attn2_decode_block<DT, HD, NREP, true, kGemvWaves>(at, g, 0, xs, nkv);
+}
+
+// ---------------------------------------------------------------------------
 // RMSNorm + gate/up + SiLU*mul
 // ---------------------------------------------------------------------------
 template <int DT, int U, int PFC, int NX>
@@ -629,6 +739,44 @@ CAKE_API int cake_qkv_rope(int dt, const float* resid, const void* norm_w, float
   DISPATCH_DT(dt, DISPATCH_TUNE(t, K, CAKE_NX_NORM(K, hipLaunchKernelGGL((qkv_rope_kernel<DT, U, PF, NX>),
                                                       dim3(grid_for(npairs, t.MB)),
                                                       dim3(kGemvThreads), lds, st, a))));
+  return (int)hipGetLastError();
+}
+
+// Fused QKV + RoPE + KV write + attention (qkv_attn_kernel): n_rep <= 4 (the attention
+// tail runs on the gemv block's 4 waves), hd 64 / 128; one pair per wave.
+CAKE_API int cake_qkv_attn_supported(int K, int nh, int nkv, int hd) {
+  if (K % 8 || nkv <= 0 || nh % nkv || (hd != 64 && hd != 128)) return 0;
+  const int nrep = nh / nkv;
+  return nrep == 1 || nrep == 2 || nrep == 4;
+}
+
+CAKE_API int cake_qkv_attn(int dt, const float* resid, const void* norm_w, float eps,
+                           const void* wq, const void* wk, const void* wv, int K, int nh,
+                           int nkv, int hd, const float* inv_freq, const int* pos,
+                           float* q_out, void* kcache, void* vcache, int S, float scale,
+                           unsigned int* tickets, void* out, hipStream_t st) {
+  if (!cake_qkv_attn_supported(K, nh, nkv, hd) || S <= 0) return (int)hipErrorInvalidValue;
+  QkvArgs a{resid, (const uint16_t*)norm_w, eps, (const uint16_t*)wq,
+            (const uint16_t*)wk, (const uint16_t*)wv, K, nh, nkv, hd, inv_freq, pos,
+            q_out, (uint16_t*)kcache, (uint16_t*)vcache, S};
+  const QkvAttnTail tl{tickets, (uint16_t*)out, scale * 1.4426950408889634f};
+  const int npairs = (nh + 2 * nkv) * (hd / 2);
+  const dim3 grid(npairs / kGemvWaves);  // one pair per wave: (hd / 2) % 4 == 0
+  const GemvTune t = g_tune[kQkv];
+#define CAKE_QA(HD, NR)                                                                     \
+  do {                                                                                      \
+    constexpr int nf = attn2_smem_floats<HD, NR, kGemvWaves>();                             \
+    const size_t lds = (size_t)(K > nf ? K : nf) * sizeof(float);                           \
+    DISPATCH_DT(dt, DISPATCH_TUNE(t, K, CAKE_NX_NORM(K, hipLaunchKernelGGL(                  \
+        (qkv_attn_kernel<DT, U, PF, NX, HD, NR>), grid, dim3(kGemvThreads), lds, st, a, tl)))); \
+  } while (0)
+  const int nrep = nh / nkv;
+  if (hd == 128) {
+    if (nrep == 4) CAKE_QA(128, 4); else if (nrep == 2) CAKE_QA(128, 2); else CAKE_QA(128, 1);
+  } else {
+    if (nrep == 4) CAKE_QA(64, 4); else if (nrep == 2) CAKE_QA(64, 2); else CAKE_QA(64, 1);
+  }
+#undef CAKE_QA
   return (int)hipGetLastError();
 }
 

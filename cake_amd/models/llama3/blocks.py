@@ -96,6 +96,9 @@ class LayerStack:
         # persistent decode (decode_mk.hip): one launch per token step instead of five
         # per layer; CAKE_MK=0 keeps the per-layer launches
         self.use_mk = os.environ.get("CAKE_MK", "0") != "0" and backend == "hip"
+        # one-split decode steps with QKV and attention as one launch (qkv_attn_kernel);
+        # off by default: measured slower than the two launches (profiles/r4_qkv_attn_ab.md)
+        self.use_qkv_attn = os.environ.get("CAKE_QKV_ATTN", "0") != "0" and backend == "hip"
         self._mk_ok: bool | None = None
         self._mk_tables: dict = {}
 
@@ -238,17 +241,32 @@ class LayerStack:
                         bufs.pos, bufs.resid, gran, ctl)
             return
         kv = self.cache(session)
+        fused = K.qkv_attn_active() and self.qkv_attn_ok()
         for li in layers:
             w = self.weights[li]
             s = self.slot_of[li]
             kc, vc = kv.k[s], kv.v[s]
-            K.qkv_rope(bufs.resid, w.ln1, cfg.rms_norm_eps, w.wq, w.wk, w.wv, self.inv_freq,
-                       bufs.pos, bufs.q, kc, vc)
-            K.attn_decode(bufs.q, kc, vc, bufs.pos, self.scale, bufs.part, bufs.tickets,
-                          bufs.attn_out)
+            if fused:  # QKV + RoPE + KV write + attention: one launch (short contexts)
+                K.qkv_attn(bufs.resid, w.ln1, cfg.rms_norm_eps, w.wq, w.wk, w.wv,
+                           self.inv_freq, bufs.pos, bufs.q, kc, vc, self.scale, bufs.tickets,
+                           bufs.attn_out)
+            else:
+                K.qkv_rope(bufs.resid, w.ln1, cfg.rms_norm_eps, w.wq, w.wk, w.wv,
+                           self.inv_freq, bufs.pos, bufs.q, kc, vc)
+                K.attn_decode(bufs.q, kc, vc, bufs.pos, self.scale, bufs.part, bufs.tickets,
+                              bufs.attn_out)
             K.gemv(bufs.attn_out, w.wo, bufs.resid, accumulate=True)
             K.swiglu(bufs.resid, w.ln2, cfg.rms_norm_eps, w.wg, w.wu, bufs.act)
             K.gemv(bufs.act, w.wd, bufs.resid, accumulate=True)
+
+    def qkv_attn_ok(self) -> bool:
+        """The fused QKV + attention launch covers this stack's shapes (hip, GQA <= 4)."""
+        if not self.use_qkv_attn:
+            return False
+        from ...ops import hip as K
+        c = self.cfg
+        return K.qkv_attn_supported(c.hidden_size, c.num_attention_heads,
+                                    c.num_key_value_heads, c.head_dim)
 
     # ------------------------------------------------------------------ hip paths
     def _decode_graph(self, hidden, layers: list[int], pos0: int, session: int) -> None:
@@ -263,6 +281,8 @@ class LayerStack:
         need = K.attn_splits(pos0 + 1)
         cap = next((c for c in (8, 16, 32, 64) if c >= min(need, full)), 64)
         cap = min(cap, full)
+        if need == 1 and self.qkv_attn_ok() and not self.mk_enabled():
+            cap = 1  # one split: QKV and attention as one launch per layer
         key = (session, tuple(layers), cap)
         ent = self._step_graph_cache.get(key)
         if ent is None:
@@ -276,7 +296,8 @@ class LayerStack:
             self.decode_step(bufs, layers, session)
             hidden[0].copy_(bufs.resid)
             g = torch.cuda.CUDAGraph()
-            with K.attn_split_cap(cap), torch.cuda.graph(g):  # records only
+            with K.attn_split_cap(cap if cap != 1 else full), K.qkv_attn_fused(cap == 1), \
+                    torch.cuda.graph(g):  # records only
                 self.decode_step(bufs, layers, session)
             self._step_graph_cache[key] = (g, bufs)
             return

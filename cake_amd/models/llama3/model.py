@@ -267,6 +267,15 @@ class DeviceDecoder:
                 for _ in range(self.k):
                     self._step_body()
             self.graphs[cap] = g
+        # bucket "1 split": QKV and attention as one launch per layer (the live lengths
+        # whose attention is one split per kv head; gemv.hip qkv_attn_kernel)
+        st = self.m.stack
+        if st.qkv_attn_ok() and not st.mk_enabled():
+            g = torch.cuda.CUDAGraph()
+            with K.qkv_attn_fused(), torch.cuda.graph(g):
+                for _ in range(self.k):
+                    self._step_body()
+            self.graphs[1] = g
         self.graph = self.graphs[max(self.graphs)]
         torch.cuda.synchronize()
 

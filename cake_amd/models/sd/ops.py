@@ -244,6 +244,37 @@ def conv(W, name: str, x, stride: int = 1, padding: int = 1, up: bool = False, b
     if nhwc():
         from ...ops import hip as K
         OC, IC = w.shape[:2]
+        if (_hip(x) and w.shape[2] == w.shape[3] == 1 and IC <= 16 and OC <= 16 and stride == 1
+                and padding == 0 and not up and bias2 is None and resid is None):
+            # few-channel 1x1 (VAE quant_conv / post_quant_conv): per-pixel kernel that
+            # reads / writes either layout itself
+            key = f"{name}.weight@1x1"
+            wp = W.get(key)
+            if wp is None or wp.dtype != x.dtype:
+                wp = W[key] = w.to(x.dtype).reshape(OC, IC).contiguous()
+            bb = None if b is None else b.to(x.dtype)
+            return K.conv1x1_small(x.contiguous(), wp, bb, in_nchw=in_nchw, out_nchw=out_nchw)
+        if (_hip(x) and OC < 4 and w.shape[2] == w.shape[3] and bias2 is None and resid is None
+                and K.conv_supported(IC, 4, stride, up, w.shape[2])):
+            # OC < 4 (VAE decoder.conv_out 128 -> 3): the MFMA conv on 4 output channels,
+            # the padded ones with zero filters, sliced off
+            from ...ops import conv as C
+            key = f"{name}.weight@nhwc4"
+            wp = W.get(key)
+            if wp is None or wp.dtype != x.dtype:
+                w4 = torch.zeros((4,) + tuple(w.shape[1:]), device=w.device, dtype=x.dtype)
+                w4[:OC] = w.to(x.dtype)
+                wp = W[key] = w4.permute(0, 2, 3, 1).contiguous()
+                b4 = torch.zeros(4, device=w.device, dtype=x.dtype)
+                if b is not None:
+                    b4[:OC] = b.to(x.dtype)
+                W[key + ".bias"] = b4
+            if in_nchw:
+                x = to_internal(x)
+            y = C.conv2d(x.contiguous(), wp, W[key + ".bias"], stride=stride, pad=padding, up=up,
+                         out_nchw=out_nchw)
+            y = y[:, :OC] if out_nchw else y[..., :OC]
+            return y if (out_nchw and y.shape[0] == 1) else y.contiguous()
         if _hip(x) and w.shape[2] == w.shape[3] and K.conv_supported(IC, OC, stride, up, w.shape[2]):
             from ...ops import conv as C
             key = f"{name}.weight@nhwc"

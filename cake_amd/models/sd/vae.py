@@ -120,15 +120,17 @@ class AutoencoderKL(Module):
     def encode(self, W, x: torch.Tensor, generator: torch.Generator | None = None) -> torch.Tensor:
         """image [B,3,H,W] in [-1,1] -> latent sample [B,4,H/8,W/8] (unscaled)."""
         with ops.layout_nhwc(ops.want_nhwc(x)):
-            moments = ops.to_external(self._encode(W, ops.to_internal(x))).float()
+            moments = self._encode(W, x).float()
         mean, logvar = moments.chunk(2, 1)
         logvar = logvar.clamp(-30.0, 20.0)
         eps = torch.randn(mean.shape, generator=generator, device="cpu").to(mean.device)
         return (mean + torch.exp(0.5 * logvar) * eps).to(x.dtype)
 
     def _encode(self, W, x):
+        """x: the external NCHW image; returns the NCHW moments (the first and last
+        convolutions read / write that layout themselves)."""
         G = self.cfg.norm_num_groups
-        h = self.e_in(W, x)
+        h = self.e_in(W, x, in_nchw=True)
         for res, ds in self.e_down:
             for r in res:
                 h = r(W, h)
@@ -139,15 +141,17 @@ class AutoencoderKL(Module):
         h = self.e_mid[1](W, h)
         h = ops.group_norm(h, W["encoder.conv_norm_out.weight"], W["encoder.conv_norm_out.bias"],
                            G, 1e-6, silu=True)
-        return self.quant(W, self.e_out(W, h))
+        return self.quant(W, self.e_out(W, h), out_nchw=True)
 
     def decode(self, W, z: torch.Tensor) -> torch.Tensor:
         with ops.layout_nhwc(ops.want_nhwc(z)):
-            return ops.to_external(self._decode(W, ops.to_internal(z)))
+            return self._decode(W, z)
 
     def _decode(self, W, z):
+        """z: the external NCHW latent; returns the NCHW image (post_quant_conv reads and
+        decoder.conv_out writes that layout themselves: no layout-copy kernels)."""
         G = self.cfg.norm_num_groups
-        h = self.d_in(W, self.post_quant(W, z))
+        h = self.d_in(W, self.post_quant(W, z, in_nchw=True))
         h = self.d_mid[0](W, h)
         h = self.d_att(W, h)
         h = self.d_mid[1](W, h)
@@ -158,4 +162,4 @@ class AutoencoderKL(Module):
                 h = us(W, h, up=True)
         h = ops.group_norm(h, W["decoder.conv_norm_out.weight"], W["decoder.conv_norm_out.bias"],
                            G, 1e-6, silu=True)
-        return self.d_out(W, h)
+        return self.d_out(W, h, out_nchw=True)

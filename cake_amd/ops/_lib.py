@@ -26,6 +26,8 @@ Z = C.c_size_t
 # name -> argtypes (all return int hipError_t)
 _SIGS = {
     "cake_qkv_rope": [I, P, P, F, P, P, P, I, I, I, I, P, P, P, P, P, I, P],
+    "cake_qkv_attn": [I, P, P, F, P, P, P, I, I, I, I, P, P, P, P, P, I, F, P, P, P],
+    "cake_qkv_attn_supported": [I, I, I, I],
     "cake_swiglu": [I, P, P, F, P, P, I, I, P, P],
     "cake_gemv_x16": [I, P, P, I, I, P, I, P],
     "cake_gemv_norm_f32": [I, P, P, F, P, I, I, P, P],
@@ -121,6 +123,7 @@ _SIGS.update({
     "cake_geglu": [I, P, C.c_longlong, I, P, P],
     "cake_stream_read": [P, Z, I, P, P],
     "cake_conv2d_nhwc": [I, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, P],
+    "cake_conv1x1_small": [I, P, P, P, P, I, I, I, I, I, P],
     "cake_conv2d_nhwc2": [I, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, P],
 })
 

@@ -77,6 +77,68 @@ def qkv_rope(resid, norm_w, eps, wq, wk, wv, inv_freq, pos, q_out, kcache, vcach
           "qkv_rope")
 
 
+
+def qkv_attn_supported(K: int, nh: int, nkv: int, hd: int) -> bool:
+    """Shapes the fused QKV + attention launch covers (GQA groups of <= 4 heads)."""
+    return bool(kernels().cake_qkv_attn_supported(int(K), int(nh), int(nkv), int(hd)))
+
+
+def qkv_attn(resid, norm_w, eps, wq, wk, wv, inv_freq, pos, q_out, kcache, vcache, scale,
+             tickets, out):
+    """:func:`qkv_rope` and :func:`attn_decode` as ONE launch (gemv.hip qkv_attn_kernel):
+    the workgroup that completes a kv group's q/k/v rows last runs that group's attention
+    over the whole live length as one split.  Fastest where attn_splits(Tk) == 1 (short
+    contexts); correct at any length.  tickets: the attention launch's [2 nkv + 2] array
+    (shared: both kernels re-arm what they use)."""
+    K = resid.numel()
+    nkv, S, hd = kcache.shape
+    nh = wq.shape[0] // hd
+    dt = wq.dtype
+    _req(resid, "resid", dtype=torch.float32)
+    _req(norm_w, "norm_w", dtype=dt, shape=(K,))
+    _req(wq, "wq", dtype=dt, shape=(nh * hd, K))
+    _req(wk, "wk", dtype=dt, shape=(nkv * hd, K))
+    _req(wv, "wv", dtype=dt, shape=(nkv * hd, K))
+    _req(inv_freq, "inv_freq", dtype=torch.float32, shape=(hd // 2,))
+    _req(pos, "pos", dtype=torch.int32, numel=1)
+    _req(q_out, "q_out", dtype=torch.float32, numel=nh * hd)
+    _req(kcache, "kcache", dtype=dt)
+    _req(vcache, "vcache", dtype=dt, shape=kcache.shape)
+    _req(tickets, "tickets", dtype=torch.int32, numel=2 * nkv + 2)
+    _req(out, "out", dtype=dt, numel=nh * hd)
+    if not qkv_attn_supported(K, nh, nkv, hd):
+        raise ValueError(f"qkv_attn: unsupported shape K={K} nh={nh} nkv={nkv} hd={hd}")
+    check(kernels().cake_qkv_attn(_dt(wq), _p(resid), _p(norm_w), float(eps), _p(wq), _p(wk),
+                                  _p(wv), K, nh, nkv, hd, _p(inv_freq), _p(pos), _p(q_out),
+                                  _p(kcache), _p(vcache), S, float(scale), _p(tickets), _p(out),
+                                  _stream()),
+          "qkv_attn")
+
+
+_QKV_ATTN = [False]
+
+
+class qkv_attn_fused:
+    """Context manager: decode steps issued (or captured) inside it run QKV + attention as
+    one launch where the shapes allow (LayerStack.decode_step); DeviceDecoder captures
+    one such graph for the live lengths that run one attention split."""
+
+    def __init__(self, on: bool = True):
+        self.on = bool(on)
+
+    def __enter__(self):
+        self.prev = _QKV_ATTN[0]
+        _QKV_ATTN[0] = self.on
+        return self
+
+    def __exit__(self, *exc):
+        _QKV_ATTN[0] = self.prev
+        return False
+
+
+def qkv_attn_active() -> bool:
+    return _QKV_ATTN[0]
+
 def swiglu(resid, norm_w, eps, wg, wu, act):
     """act = silu(rmsnorm(resid) @ wg.T) * (rmsnorm(resid) @ wu.T)   (batch 1)."""
     K = resid.numel()
@@ -749,6 +811,32 @@ def conv_supported(IC: int, OC: int, stride: int = 1, up: bool = False, k: int =
     if IC in (3, 4):  # direct small-IC kernel (conv_in)
         return k == 3 and OC % 8 == 0 and 9 * IC * OC <= 18432 and not up
     return IC % 64 == 0 and OC % 4 == 0 and not (up and stride != 1)
+
+
+def conv1x1_small(x, w, bias=None, out=None, *, in_nchw: bool = False, out_nchw: bool = False):
+    """1x1 convolution with IC, OC <= 16 (conv2d.hip conv1x1_small_kernel): x [N,H,W,IC]
+    (or [N,IC,H,W] with in_nchw), w [OC, IC] (or [OC, IC, 1, 1]) -> [N,H,W,OC] (or
+    [N,OC,H,W] with out_nchw)."""
+    if in_nchw:
+        N, IC, H, W = x.shape
+    else:
+        N, H, W, IC = x.shape
+    OC = w.shape[0]
+    if w.numel() != OC * IC or not (1 <= IC <= 16 and 1 <= OC <= 16):
+        raise ValueError(f"conv1x1_small: unsupported IC={IC} OC={OC} w={tuple(w.shape)}")
+    _req(x, "x")
+    _req(w, "w", dtype=x.dtype)
+    if bias is not None:
+        _req(bias, "bias", dtype=x.dtype, numel=OC)
+    oshape = (N, OC, H, W) if out_nchw else (N, H, W, OC)
+    if out is None:
+        out = torch.empty(*oshape, device=x.device, dtype=x.dtype)
+    _req(out, "out", dtype=x.dtype, shape=oshape)
+    check(kernels().cake_conv1x1_small(_dt(x), _p(x), _p(w), None if bias is None else _p(bias),
+                                       _p(out), N, H * W, IC, OC,
+                                       int(in_nchw) | (int(out_nchw) << 1), _stream()),
+          "conv1x1_small")
+    return out
 
 
 _HALO_TILES = {256: ((16, 16), (8, 32), (32, 8)),

@@ -127,12 +127,45 @@ def test_device_decoder_crosses_split_buckets(cuda):
     dec = DeviceDecoder(model, repeat_penalty=1.1, repeat_last_n=16, greedy=True)
     first = dec.start(prompt)
     dec.capture()
-    # caps up to the first covering every live length (core 2 at 16 splits: 8 and 16)
+    # caps up to the first covering every live length (core 2 at 16 splits: 8 and 16),
+    # below them the one-split bucket of fused QKV + attention launches (key 1)
     assert sorted(dec.graphs) == K.attn_split_caps(4096)
     assert sorted(dec.graphs)[:2] == [8, 16]
     assert dec._graph_for(500) is dec.graphs[8] and dec._graph_for(600) is dec.graphs[16]
     assert K.attn_splits(4096) == (32 if K._ATTN_IMPL[0] == 1 else 16)
     st = run_decode(dec, 15)
+    assert [first] + st.tokens == host
+
+
+@pytest.mark.parametrize("k", [1, 4])
+def test_device_decoder_crosses_fused_bucket(cuda, k):
+    """Live lengths crossing the one-split edge (320 keys): the fused QKV + attention
+    graph up to it, the two-launch graph (cap 8) after it — tokens equal the host loop."""
+    from cake_amd.models.llama3.decode_loop import run_decode
+    from cake_amd.models.llama3.model import DeviceDecoder
+    from cake_amd.ops import reference as R
+
+    cfg = preset("llama3-8b", num_hidden_layers=2, vocab_size=2048, intermediate_size=1024,
+                 hidden_size=512, num_attention_heads=8, num_key_value_heads=2)
+    model = random_model(cfg, "cuda:0", torch.bfloat16, max_seq=1024, seed=6)
+    model.stack.use_qkv_attn = True
+    g = torch.Generator().manual_seed(3)
+    prompt = torch.randint(0, 2048, (310,), generator=g).tolist()
+    toks = list(prompt)
+    logits = model.forward(prompt, 0)
+    host = []
+    for _ in range(20):
+        t = int(torch.argmax(R.apply_repeat_penalty(logits, 1.1, toks[-16:])))
+        host.append(t)
+        toks.append(t)
+        logits = model.forward([t], len(toks) - 1)
+    dec = DeviceDecoder(model, repeat_penalty=1.1, repeat_last_n=16, greedy=True,
+                        steps_per_graph=k)
+    first = dec.start(prompt)
+    dec.capture()
+    assert 1 in dec.graphs
+    assert dec._graph_for(320) is dec.graphs[1] and dec._graph_for(321) is dec.graphs[8]
+    st = run_decode(dec, 19)
     assert [first] + st.tokens == host
 
 

@@ -65,14 +65,28 @@ def test_unet_vae_channels_last_kernels_gpu_vs_cpu(cuda):
     vae = AutoencoderKL(cfg.vae)
     z = torch.randn(1, 4, 8, 8)
     ref = vae.decode(wv, z)
-    out = vae.decode({k: v.to(cuda, dt) for k, v in wv.items()}, z.to(cuda, dt))
+    gv = {k: v.to(cuda, dt) for k, v in wv.items()}
+    # every VAE convolution on the HIP kernels: no library (MIOpen) conv may run
+    import torch.nn.functional as F
+    real_conv = F.conv2d
+
+    def no_library_conv(*a, **k):
+        raise AssertionError("F.conv2d called on the channels-last GPU path")
+    F.conv2d = no_library_conv
+    try:
+        out = vae.decode(gv, z.to(cuda, dt))
+        img = torch.rand(1, 3, 64, 64) * 2 - 1
+        g = torch.Generator().manual_seed(0)
+        enc = vae.encode(gv, img.to(cuda, dt), g)
+    finally:
+        F.conv2d = real_conv
     torch.testing.assert_close(out.float().cpu(), ref, atol=6e-2, rtol=6e-2)
-    img = torch.rand(1, 3, 64, 64) * 2 - 1
+    # decoder.conv_out (64 -> 3) on padded output channels, the 1x1 quant convs direct
+    assert "decoder.conv_out.weight@nhwc4" in gv
+    assert "post_quant_conv.weight@1x1" in gv and "quant_conv.weight@1x1" in gv
     g = torch.Generator().manual_seed(0)
     ref = vae.encode(wv, img, g)
-    g = torch.Generator().manual_seed(0)
-    out = vae.encode({k: v.to(cuda, dt) for k, v in wv.items()}, img.to(cuda, dt), g)
-    torch.testing.assert_close(out.float().cpu(), ref, atol=6e-2, rtol=6e-2)
+    torch.testing.assert_close(enc.float().cpu(), ref, atol=6e-2, rtol=6e-2)
 
 
 def test_unet_unit_graph_replay_matches_eager(cuda):

@@ -290,6 +290,25 @@ def test_conv2d_small_ic(cuda, dt, N, H, W, IC, OC, stride, fused):
         torch.testing.assert_close(y2.float(), ref.permute(0, 3, 1, 2), **_tol(dt))
 
 
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("N,H,W,IC,OC", [(1, 128, 128, 4, 4), (2, 17, 9, 8, 8), (1, 5, 7, 3, 16),
+                                         (3, 8, 8, 16, 1)])
+@pytest.mark.parametrize("layout", [0, 1, 2, 3])
+def test_conv1x1_small(cuda, dt, N, H, W, IC, OC, layout):
+    """Few-channel 1x1 conv (VAE quant / post_quant) in every input / output layout vs
+    the f32 reference."""
+    from cake_amd.ops import hip as K
+    torch.manual_seed(11)
+    x = torch.randn(N, H, W, IC, device=cuda).to(dt)
+    w = (torch.randn(OC, IC, device=cuda) / math.sqrt(IC)).to(dt)
+    b = torch.randn(OC, device=cuda).to(dt)
+    ref = (x.float() @ w.float().t() + b.float())            # [N, H, W, OC]
+    in_nchw, out_nchw = bool(layout & 1), bool(layout & 2)
+    xi = x.permute(0, 3, 1, 2).contiguous() if in_nchw else x
+    y = K.conv1x1_small(xi, w, b, in_nchw=in_nchw, out_nchw=out_nchw)
+    torch.testing.assert_close(y.float(), ref.permute(0, 3, 1, 2) if out_nchw else ref, **_tol(dt))
+
+
 @pytest.mark.parametrize("cfg,splits", [(0, 1), (4, 2), (8, 1)])
 def test_conv2d_out_nchw(cuda, cfg, splits):
     """conv_out-like (IC 320 -> OC 4) written straight into NCHW planes, incl. split-K."""
