@@ -142,14 +142,38 @@ def build_runtime(force: bool = False, jobs: int = 8) -> Path:
         _run([CXX, "-O2", "-std=c++17", f"-I{rt}", str(tool), *map(str, core), "-o",
               str(SPLIT_TOOL), "-lpthread"])
     cli = CSRC / "tools" / "cake_cli.cpp"
-    if force or _newer(cli, [*core, emb, *sorted(rt.glob("*.h"))], CLI_TOOL):
+    if force or _newer(cli, [*core, emb, *sorted(rt.glob("*.h")), CSRC / "engine" / "llama_engine.h"],
+                       CLI_TOOL):
         _run([CXX, "-O2", "-std=c++17", f"-I{rt}", str(cli), *map(str, core), str(emb), "-o",
               str(CLI_TOOL), *elink])
     return pyext
 
 
+ENGINE_LIB = LIB / "libcake_engine.so"
+
+
+def build_engine(force: bool = False) -> Path:
+    """Native Llama engine (csrc/engine): host C++ on the HIP runtime over the kernel
+    library's C entry points, plus the runtime's JSON / safetensors readers."""
+    eng = CSRC / "engine" / "llama_engine.cpp"
+    rt = CSRC / "runtime"
+    objs = [_compile_cpp(rt / f"{n}.cpp", force) for n in ("json", "safetensors")]
+    out = BUILD / "engine" / "llama_engine.o"
+    out.parent.mkdir(parents=True, exist_ok=True)
+    deps = [*sorted((CSRC / "engine").glob("*.h")), *sorted(rt.glob("*.h")),
+            CSRC / "driver" / "graph_loop.h"]
+    if force or _newer(eng, deps, out):
+        _run([HIPCC, "-O2", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-Wall",
+              "-Wno-unused-function", "-c", str(eng), "-o", str(out)])
+    if force or any(_newer(o, [], ENGINE_LIB) for o in [out, *objs, KERNEL_LIB]):
+        _run([HIPCC, "-shared", "-fPIC", str(out), *map(str, objs), "-o", str(ENGINE_LIB),
+              f"-L{LIB}", "-lcake_kernels", "-Wl,-rpath,$ORIGIN"])
+    return ENGINE_LIB
+
+
 def build_all(force: bool = False, jobs: int = 8) -> None:
     build_kernels(force, jobs)
+    build_engine(force)
     build_runtime(force, jobs)
 
 
@@ -157,10 +181,12 @@ def main(argv: list[str] | None = None) -> int:
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=min(8, os.cpu_count() or 4))
-    ap.add_argument("--only", choices=["kernels", "runtime"], default=None)
+    ap.add_argument("--only", choices=["kernels", "engine", "runtime"], default=None)
     a = ap.parse_args(argv)
     if a.only in (None, "kernels"):
         print("built", build_kernels(a.force, a.jobs))
+    if a.only in (None, "engine"):
+        print("built", build_engine(a.force))
     if a.only in (None, "runtime"):
         print("built", build_runtime(a.force, a.jobs))
     return 0

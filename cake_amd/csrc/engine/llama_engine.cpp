@@ -1,0 +1,836 @@
+// Native Llama engine (see llama_engine.h): host orchestration in C++ over the gfx950
+// kernels' C entry points — what models/llama3/{blocks,model}.py + decode_loop.py do
+// through PyTorch, with no interpreter, no torch allocator and no torch graphs:
+//
+//   * weights: HF safetensors (mmap, csrc/runtime/safetensors.cpp) uploaded once into
+//     hipMalloc'd buffers in the model dtype (bf16 / f16; other checkpoint dtypes
+//     converted on the device by cake_cast16).  q|k|v rows and gate|up rows are packed
+//     into one matrix each: the prefill GEMMs read them as one operand, the decode
+//     GEMVs take the three / two row blocks as separate pointers.
+//   * prefill: embed -> per layer RMSNorm, q|k|v GEMM, RoPE + KV write, causal flash
+//     attention, o_proj GEMM (+residual epilogue), RMSNorm, gate|up GEMM (SwiGLU
+//     epilogue), down GEMM (+residual) -> final-norm lm_head GEMV on the last row
+//     (reference: llama.rs:72-138, transformer.rs:51-73).  GEMM tiles come from the
+//     same cost model + measured table (ops/gemm_tuned.json) as ops/gemm.py.
+//   * decode: one step = 5 launches per layer + the head; captured with
+//     hipStreamBeginCapture into one graph per attention split-cap bucket (the live
+//     length picks the bucket), replayed by the native loop (graph_loop.cpp).  Greedy
+//     steps end in the fused head_select launch (lm_head + penalty + argmax + the next
+//     step's embedding row); sampled steps in threshold + Gumbel-max draws keyed by
+//     (seed, step) — the same kernels and launch order as DeviceDecoder, so tokens match
+//     the Python engine exactly (tests/test_engine_gpu.py).
+#include "llama_engine.h"
+
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <memory>
+#include <sstream>
+#include <stdexcept>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "../driver/graph_loop.h"
+#include "../runtime/json.h"
+#include "../runtime/safetensors.h"
+
+#define CAKE_API extern "C" __attribute__((visibility("default")))
+
+// gfx950 kernel entry points (libcake_kernels.so)
+extern "C" {
+int cake_cast16(int src_kind, int dt, const void* src, void* dst, size_t n, hipStream_t st);
+int cake_embed(int dt, const void* table, const int* tok, int T, int H, float* out, hipStream_t st);
+int cake_rmsnorm(int dt, const float* x, const void* w, float eps, int T, int H, void* out,
+                 hipStream_t st);
+int cake_rope_kv(int dt, void* q, const void* k, const void* v, int ldq, int ld, int T, int nh,
+                 int nkv, int hd, const float* inv_freq, int pos0, int S, void* kc, void* vc,
+                 hipStream_t st);
+int cake_flash_attn(int dt, const void* q, const void* k, const void* v, void* o, int B, int H,
+                    int Hkv, int N, int M, int D, const long long* strides, float scale,
+                    int causal, int pos0, hipStream_t st);
+int cake_gemm(int dt, int epi, int cfg, int splits, const void* a, long long lda, const void* b,
+              long long ldb, void* c, long long ldc, const void* bias, void* resid,
+              long long ldr, float* ws, const void* zeros, int M, int N, int K, hipStream_t st);
+int cake_qkv_rope(int dt, const float* resid, const void* norm_w, float eps, const void* wq,
+                  const void* wk, const void* wv, int K, int nh, int nkv, int hd,
+                  const float* inv_freq, const int* pos, float* q_out, void* kcache,
+                  void* vcache, int S, hipStream_t st);
+int cake_attn_decode(int dt, const float* q, const void* kc, const void* vc, const int* pos,
+                     int S, int nh, int nkv, int hd, float scale, float* part,
+                     unsigned int* tickets, void* out, hipStream_t st);
+int cake_attn_set_split_cap(int cap);
+int cake_attn_splits(int Tk);
+int cake_attn_max_split(int S);
+int cake_gemv_x16(int dt, const void* x, const void* w, int K, int N, float* out, int accumulate,
+                  hipStream_t st);
+int cake_swiglu(int dt, const float* resid, const void* norm_w, float eps, const void* wg,
+                const void* wu, int K, int I, void* act, hipStream_t st);
+int cake_gemv_norm_f32(int dt, const float* resid, const void* norm_w, float eps, const void* w,
+                       int K, int N, float* out, hipStream_t st);
+int cake_head_select(int dt, const float* resid, const void* norm_w, float eps, const void* w,
+                     int K, int N, float* out, int* hist, int* hist_len, int last_n,
+                     float penalty, unsigned long long* slot, unsigned int* ticket, int* tok,
+                     int* pos, int max_hist, const void* embed, float* emb_out, hipStream_t st);
+int cake_repeat_penalty(float* logits, const int* hist, const int* hist_len, int last_n,
+                        float penalty, hipStream_t st);
+int cake_argmax(const float* logits, int V, unsigned long long* slot, hipStream_t st);
+int cake_sample_threshold(const float* logits, int V, float temperature, int top_k, float top_p,
+                          unsigned int* thr, hipStream_t st);
+int cake_gumbel_argmax(const float* logits, int V, float temperature, unsigned long long seed,
+                       const int* step, const unsigned int* thr, unsigned long long* slot,
+                       hipStream_t st);
+int cake_finalize_token(unsigned long long* slot, int* tok, int* hist, int* hist_len, int* pos,
+                        int max_hist, hipStream_t st);
+}
+
+namespace cake {
+namespace {
+
+constexpr int kHeadSelectMaxLastN = 256;  // gemv.hip head_select window bound
+constexpr int kAttnMaxSplit = 64;         // attention.hip kMaxSplit
+
+struct Error : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+void hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw Error(std::string(what) + ": " + hipGetErrorString(e));
+}
+void k_check(int rc, const char* what) {
+  if (rc != 0) throw Error(std::string(what) + ": " + hipGetErrorString((hipError_t)rc));
+}
+
+// <root>/cake_amd/lib/libcake_engine.so -> <root>/cake_amd
+std::string pkg_dir() {
+  Dl_info info{};
+  if (dladdr(reinterpret_cast<void*>(&pkg_dir), &info) && info.dli_fname) {
+    char buf[4096];
+    const char* p = realpath(info.dli_fname, buf);
+    std::string s = p ? p : info.dli_fname;
+    for (int i = 0; i < 2; ++i) {
+      const auto cut = s.find_last_of('/');
+      if (cut == std::string::npos) return ".";
+      s = s.substr(0, cut);
+    }
+    return s;
+  }
+  return ".";
+}
+
+std::string read_file(const std::string& path) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f) throw Error("cannot read " + path);
+  std::stringstream ss;
+  ss << f.rdbuf();
+  return ss.str();
+}
+
+// ---------------------------------------------------------------------------
+// model config (config.json; models/llama3/config.py from_dict)
+// ---------------------------------------------------------------------------
+struct Cfg {
+  int H = 0, I = 0, V = 0, L = 0, nh = 0, nkv = 0, hd = 0;
+  double eps = 1e-5, theta = 10000.0;
+  bool tie = false;
+  std::vector<int> eos;
+  Json rope_scaling;
+
+  static Cfg parse(const Json& d) {
+    auto num = [&](const char* k, double def) {
+      return d.has(k) && d.get(k).is_number() ? d.get(k).as_double() : def;
+    };
+    Cfg c;
+    c.H = (int)d.get("hidden_size").as_int();
+    c.I = (int)d.get("intermediate_size").as_int();
+    c.V = (int)d.get("vocab_size").as_int();
+    c.L = (int)d.get("num_hidden_layers").as_int();
+    c.nh = (int)d.get("num_attention_heads").as_int();
+    c.nkv = d.has("num_key_value_heads") && d.get("num_key_value_heads").is_number()
+                ? (int)d.get("num_key_value_heads").as_int() : c.nh;
+    c.hd = c.H / c.nh;
+    c.eps = num("rms_norm_eps", 1e-5);
+    c.theta = num("rope_theta", 10000.0);
+    c.tie = d.has("tie_word_embeddings") && d.get("tie_word_embeddings").type() == Json::Bool &&
+            d.get("tie_word_embeddings").as_bool();
+    if (d.has("eos_token_id")) {
+      const Json& e = d.get("eos_token_id");
+      if (e.is_array()) {
+        for (const auto& x : e.items()) c.eos.push_back((int)x.as_int());
+      } else if (e.is_number()) {
+        c.eos.push_back((int)e.as_int());
+      }
+    }
+    if (d.has("rope_scaling")) c.rope_scaling = d.get("rope_scaling");
+    return c;
+  }
+
+  // theta_i = 1 / theta^(2i/d) with optional Llama-3.1 "llama3" scaling (f64, as
+  // ops/reference.py inv_freq)
+  std::vector<float> inv_freq() const {
+    std::vector<float> out(hd / 2);
+    const bool l3 = rope_scaling.is_object() &&
+                    ((rope_scaling.has("rope_type") && rope_scaling.get("rope_type").is_string() &&
+                      rope_scaling.get("rope_type").as_string() == "llama3") ||
+                     (rope_scaling.has("type") && rope_scaling.get("type").is_string() &&
+                      rope_scaling.get("type").as_string() == "llama3"));
+    auto rs = [&](const char* k, double def) {
+      return rope_scaling.has(k) && rope_scaling.get(k).is_number() ? rope_scaling.get(k).as_double()
+                                                                    : def;
+    };
+    for (int i = 0; i < hd / 2; ++i) {
+      double f = 1.0 / std::pow(theta, (double)(2 * i) / (double)hd);
+      if (l3) {
+        const double factor = rs("factor", 8.0), lo = rs("low_freq_factor", 1.0),
+                     hi = rs("high_freq_factor", 4.0),
+                     old = rs("original_max_position_embeddings", 8192.0);
+        const double lo_wl = old / lo, hi_wl = old / hi, wl = 2.0 * M_PI / f;
+        const double o = wl > lo_wl ? f / factor : f;
+        const double smooth = (old / wl - lo) / (hi - lo);
+        const double mid = (1.0 - smooth) * o / factor + smooth * o;
+        f = (wl >= hi_wl && wl <= lo_wl) ? mid : o;
+      }
+      out[i] = (float)f;
+    }
+    return out;
+  }
+};
+
+// ---------------------------------------------------------------------------
+// GEMM tile plan (ops/gemm.py plan(): measured table, else the cost model)
+// ---------------------------------------------------------------------------
+struct GemmPlanner {
+  struct Tuned { long long M, Nv, K; std::string epi; int cfg, splits; };
+  std::vector<Tuned> tuned;
+
+  void load(const std::string& path) {
+    std::ifstream f(path);
+    if (!f) return;
+    try {
+      const Json j = Json::parse(read_file(path));
+      static const int known[] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 11, 12, 13};
+      for (const auto& e : j.get("entries").items()) {
+        const int cfg = (int)e.get("cfg").as_int();
+        if (std::find(std::begin(known), std::end(known), cfg) == std::end(known)) continue;
+        tuned.push_back({e.get("M").as_int(), e.get("Nv").as_int(), e.get("K").as_int(),
+                         e.get("epi").as_string(), cfg, (int)e.get("splits").as_int()});
+      }
+    } catch (const std::exception&) {
+      tuned.clear();  // a malformed table only loses the measured overrides
+    }
+  }
+
+  std::pair<int, int> plan(long long M, long long Nv, long long K, const std::string& epi) const {
+    const Tuned* near = nullptr;
+    double near_r = 0;
+    for (const auto& e : tuned) {
+      if (e.Nv != Nv || e.K != K || e.epi != epi) continue;
+      if (e.M == M) return {e.cfg, e.splits};
+      const double r = (double)std::max(M, e.M) / (double)std::min(M, e.M);
+      if (r <= 2 && (!near || r < near_r)) { near = &e; near_r = r; }
+    }
+    if (near) return {near->cfg, 1};
+    struct T { int cfg, bm, bn, slots; double eff; };
+    static const T tiles[] = {{0, 128, 128, 2, 1.0}, {1, 64, 128, 2, 0.8}, {4, 64, 64, 4, 0.7},
+                              {5, 256, 256, 1, 1.2}};
+    static const int small_c[] = {1, 4, 0}, big_c[] = {0, 1, 4, 5};
+    const int* cands = M <= 64 ? small_c : big_c;
+    const int nc = M <= 64 ? 3 : 4;
+    const long long ksteps = (K + 63) / 64;
+    double best = -1;
+    std::pair<int, int> out{0, 1};
+    for (int c = 0; c < nc; ++c) {
+      const T* t = nullptr;
+      for (const auto& x : tiles)
+        if (x.cfg == cands[c]) t = &x;
+      const long long tiles_n = ((M + t->bm - 1) / t->bm) * ((Nv + t->bn - 1) / t->bn);
+      for (int splits : {1, 2, 4, 8, 16}) {
+        if (splits > 1 && (ksteps / splits < 4 || tiles_n * splits > 2LL * 256 * t->slots)) continue;
+        const long long waves = (tiles_n * splits + 256LL * t->slots - 1) / (256LL * t->slots);
+        double cost = (double)waves * t->slots * t->bm * t->bn * (double)((ksteps + splits - 1) / splits) / t->eff;
+        if (splits > 1) cost += (double)M * Nv * splits * 0.1;
+        if (best < 0 || cost < best) { best = cost; out = {t->cfg, splits}; }
+      }
+    }
+    return out;
+  }
+};
+
+constexpr int kEpiStore = 0, kEpiResid32 = 1, kEpiSwiglu = 3;
+
+// ---------------------------------------------------------------------------
+// the engine
+// ---------------------------------------------------------------------------
+class Llama {
+ public:
+  Llama(const std::string& dir, const CakeEngineOpts& o) : dt_(o.dtype), dev_(o.device) {
+    if (dt_ != 0 && dt_ != 1) throw Error("dtype must be 0 (bf16) or 1 (f16)");
+    hip_check(hipSetDevice(dev_), "hipSetDevice");
+    hip_check(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking), "hipStreamCreate");
+    cfg_ = Cfg::parse(Json::parse(read_file(dir + "/config.json")));
+    S_ = o.max_seq > 0 ? o.max_seq : 4096;
+    k_ = std::max(1, o.steps_per_graph);
+    if (cfg_.H % 8 || cfg_.hd % 2 || cfg_.nh % cfg_.nkv) throw Error("unsupported model shape");
+    planner_.load(pkg_dir() + "/ops/gemm_tuned.json");
+    load_weights(dir);
+    alloc_state();
+  }
+
+  ~Llama() {
+    (void)hipSetDevice(dev_);
+    (void)hipStreamSynchronize(st_);
+    drop_graphs();
+    for (void* p : allocs_) (void)hipFree(p);
+    (void)hipStreamDestroy(st_);
+  }
+
+  const Cfg& cfg() const { return cfg_; }
+  int max_seq() const { return S_; }
+
+  void prefill_logits(const int32_t* prompt, int T, float* host_logits) {
+    hip_check(hipSetDevice(dev_), "hipSetDevice");
+    prefill(prompt, T);
+    hip_check(hipMemcpyAsync(host_logits, logits_, sizeof(float) * cfg_.V, hipMemcpyDeviceToHost,
+                             st_), "logits D2H");
+    hip_check(hipStreamSynchronize(st_), "sync");
+  }
+
+  void generate(const int32_t* prompt, int T, int max_new, const CakeEngineSampling& smp,
+                const int32_t* eos, int n_eos, cake_engine_token_cb cb, void* ctx, int32_t* out,
+                int out_cap, CakeEngineStats* stats) {
+    hip_check(hipSetDevice(dev_), "hipSetDevice");
+    if (T <= 0) throw Error("empty prompt");
+    if (max_new <= 0) return;
+    if (T + max_new + k_ + 1 > S_) throw Error("prompt + max_new exceeds max_seq");
+    if (out_cap < max_new) throw Error("output buffer smaller than max_new");
+    const auto t0 = std::chrono::steady_clock::now();
+    prefill(prompt, T);
+    // the prefill position bookkeeping of DeviceDecoder.start: history = prompt,
+    // pos = T - 1 (the last written row), slot cleared
+    std::vector<int32_t> h(prompt, prompt + T);
+    hip_check(hipMemcpyAsync(hist_, h.data(), sizeof(int32_t) * T, hipMemcpyHostToDevice, st_),
+              "hist H2D");
+    set_i32(hist_len_, T);
+    set_i32(pos_, T - 1);
+    hip_check(hipMemsetAsync(slot_, 0, sizeof(unsigned long long), st_), "slot");
+    Mode mode = mode_of(smp);
+    // first token from the prefill logits (DeviceDecoder._select_first)
+    select_tail(mode);
+    if (mode.fused) k_check(cake_embed(dt_, embed_, tok_, 1, cfg_.H, resid_, st_), "embed");
+    int32_t first = 0;
+    hip_check(hipMemcpyAsync(&first, tok_, sizeof(int32_t), hipMemcpyDeviceToHost, st_), "tok");
+    hip_check(hipStreamSynchronize(st_), "sync");
+    const auto t1 = std::chrono::steady_clock::now();
+    int n_out = 0;
+    out[n_out++] = first;
+    bool stop = cb && cb(ctx, first) != 0;
+    for (int e = 0; e < n_eos && !stop; ++e)
+      if (eos[e] == first) stop = true;
+    std::vector<float> ms;
+    if (!stop && max_new > 1) {
+      ensure_graphs(mode);
+      const int n = max_new - 1;
+      std::vector<int32_t> toks(n);
+      ms.assign(n, 0.f);
+      CakeLoopSpec spec{};
+      std::vector<void*> execs(execs_.begin(), execs_.end());
+      spec.execs = execs.data();
+      spec.n_execs = (int32_t)execs.size();
+      spec.bucket_of = bucket_of_.data();
+      spec.n_len = (int32_t)bucket_of_.size();
+      spec.k = k_;
+      spec.hist = hist_;
+      spec.base = T + 1;  // history index of the second generated token
+      spec.pos = T;       // device position after the first token
+      spec.n = n;
+      spec.chunk = 0;
+      spec.eos = eos;
+      spec.n_eos = n_eos;
+      spec.on_token = cb;
+      spec.token_ctx = ctx;
+      spec.stream = st_;
+      spec.out_tokens = toks.data();
+      spec.out_ms = ms.data();
+      spec.out_cap = n;
+      CakeLoopResult res{};
+      k_check(cake_graph_decode(&spec, &res), "graph_decode");
+      for (int i = 0; i < res.n_tokens && n_out < out_cap; ++i) out[n_out++] = toks[i];
+      ms.resize(res.n_tokens);
+    }
+    const auto t2 = std::chrono::steady_clock::now();
+    if (stats) {
+      stats->n_prompt = T;
+      stats->n_generated = n_out;
+      stats->prefill_s = std::chrono::duration<double>(t1 - t0).count();
+      stats->decode_s = std::chrono::duration<double>(t2 - t1).count();
+      stats->tokens_per_s = n_out > 1 && stats->decode_s > 0 ? (n_out - 1) / stats->decode_s : 0.0;
+      std::vector<float> s = ms;
+      std::sort(s.begin(), s.end());
+      auto pct = [&](double q) {
+        if (s.empty()) return 0.f;
+        const size_t i = std::min(s.size() - 1, (size_t)std::llround(q / 100.0 * (s.size() - 1)));
+        return s[i];
+      };
+      stats->p50_ms = pct(50);
+      stats->p99_ms = pct(99);
+    }
+  }
+
+ private:
+  struct LayerW { void *ln1, *wqkv, *wo, *ln2, *wgu, *wd; };
+  struct Mode {
+    bool fused = true;  // greedy with the fused head_select tail
+    bool greedy = true;
+    float temperature = 0.f, top_p = 0.f, penalty = 1.f;
+    int top_k = 0, last_n = 0;
+    unsigned long long seed = 0;
+    bool operator==(const Mode& o) const {
+      return std::tie(fused, greedy, temperature, top_p, penalty, top_k, last_n, seed) ==
+             std::tie(o.fused, o.greedy, o.temperature, o.top_p, o.penalty, o.top_k, o.last_n,
+                      o.seed);
+    }
+  };
+
+  int dt_, dev_;
+  hipStream_t st_ = nullptr;
+  Cfg cfg_;
+  int S_ = 0, k_ = 1;
+  GemmPlanner planner_;
+  std::vector<void*> allocs_;
+  void *embed_ = nullptr, *norm_ = nullptr, *lm_head_ = nullptr;
+  std::vector<LayerW> layers_;
+  uint16_t *kc_ = nullptr, *vc_ = nullptr;  // [L][nkv][S][hd]
+  float* inv_freq_ = nullptr;
+  // decode state (graph-stable addresses; DecodeBuffers)
+  float *resid_ = nullptr, *q_ = nullptr, *part_ = nullptr, *logits_ = nullptr;
+  void *attn_out_ = nullptr, *act_ = nullptr;
+  unsigned int *tickets_ = nullptr, *thr_ = nullptr, *sel_ticket_ = nullptr;
+  int *pos_ = nullptr, *tok_ = nullptr, *hist_ = nullptr, *hist_len_ = nullptr;
+  unsigned long long* slot_ = nullptr;
+  int* scratch_i32_ = nullptr;  // warm-up snapshot: tok, pos, hist_len
+  float* scratch_resid_ = nullptr;
+  int32_t* zeros_ = nullptr;    // 64 zero words (GEMM LDS-DMA padding source)
+  // prefill buffers (grown to the longest prompt)
+  int pre_T_ = 0;
+  float* hidden_ = nullptr;
+  void *x16_ = nullptr, *qkv_ = nullptr, *att_ = nullptr, *pact_ = nullptr;
+  int32_t* ptok_ = nullptr;
+  float* ws_ = nullptr;
+  size_t ws_n_ = 0;
+  // decode graphs
+  std::vector<hipGraphExec_t> execs_;
+  std::vector<hipGraph_t> graphs_;
+  std::vector<int32_t> bucket_of_;
+  Mode graph_mode_;
+  bool have_graphs_ = false;
+
+  template <class T> T* dalloc(size_t n) {
+    void* p = nullptr;
+    hip_check(hipMalloc(&p, std::max<size_t>(n * sizeof(T), 16)), "hipMalloc");
+    allocs_.push_back(p);
+    return reinterpret_cast<T*>(p);
+  }
+  void dfree(void* p) {
+    if (!p) return;
+    auto it = std::find(allocs_.begin(), allocs_.end(), p);
+    if (it != allocs_.end()) allocs_.erase(it);
+    (void)hipFree(p);
+  }
+
+  void set_i32(int* p, int v) {
+    hip_check(hipMemcpyAsync(p, &v, sizeof(int), hipMemcpyHostToDevice, st_), "i32 H2D");
+    hip_check(hipStreamSynchronize(st_), "sync");  // &v is a stack value
+  }
+
+  // ---- weights
+  void upload(Checkpoint& ck, const std::string& name, void* dst, size_t numel, void*& stage,
+              size_t& stage_bytes) {
+    const TensorView& t = ck.tensor(name);
+    size_t n = 1;
+    for (auto d : t.shape) n *= d;
+    if (n != numel) throw Error(name + ": " + std::to_string(n) + " elements, expected " +
+                                std::to_string(numel));
+    int kind;
+    if (t.dtype == "BF16") kind = 0;
+    else if (t.dtype == "F16") kind = 1;
+    else if (t.dtype == "F32") kind = 2;
+    else throw Error(name + ": unsupported dtype " + t.dtype);
+    if (kind == dt_) {
+      hip_check(hipMemcpy(dst, t.data, t.nbytes, hipMemcpyHostToDevice), "weight H2D");
+      return;
+    }
+    if (stage_bytes < t.nbytes) {
+      if (stage) (void)hipFree(stage);
+      hip_check(hipMalloc(&stage, t.nbytes), "hipMalloc stage");
+      stage_bytes = t.nbytes;
+    }
+    hip_check(hipMemcpy(stage, t.data, t.nbytes, hipMemcpyHostToDevice), "weight H2D");
+    k_check(cake_cast16(kind, dt_, stage, dst, n, st_), "cast16");
+    hip_check(hipStreamSynchronize(st_), "sync");
+  }
+
+  void load_weights(const std::string& dir) {
+    Checkpoint ck(dir);
+    const Cfg& c = cfg_;
+    const size_t H = c.H, I = c.I, V = c.V, nq = (size_t)c.nh * c.hd, nk = (size_t)c.nkv * c.hd;
+    void* stage = nullptr;
+    size_t stage_bytes = 0;
+    try {
+      embed_ = dalloc<uint16_t>(V * H);
+      upload(ck, "model.embed_tokens.weight", embed_, V * H, stage, stage_bytes);
+      norm_ = dalloc<uint16_t>(H);
+      upload(ck, "model.norm.weight", norm_, H, stage, stage_bytes);
+      if (ck.has("lm_head.weight") && !c.tie) {
+        lm_head_ = dalloc<uint16_t>(V * H);
+        upload(ck, "lm_head.weight", lm_head_, V * H, stage, stage_bytes);
+      } else {
+        lm_head_ = embed_;  // tied embeddings
+      }
+      layers_.resize(c.L);
+      for (int l = 0; l < c.L; ++l) {
+        const std::string p = "model.layers." + std::to_string(l) + ".";
+        LayerW& w = layers_[l];
+        w.ln1 = dalloc<uint16_t>(H);
+        upload(ck, p + "input_layernorm.weight", w.ln1, H, stage, stage_bytes);
+        w.wqkv = dalloc<uint16_t>((nq + 2 * nk) * H);
+        uint16_t* qkv = reinterpret_cast<uint16_t*>(w.wqkv);
+        upload(ck, p + "self_attn.q_proj.weight", qkv, nq * H, stage, stage_bytes);
+        upload(ck, p + "self_attn.k_proj.weight", qkv + nq * H, nk * H, stage, stage_bytes);
+        upload(ck, p + "self_attn.v_proj.weight", qkv + (nq + nk) * H, nk * H, stage, stage_bytes);
+        w.wo = dalloc<uint16_t>(H * nq);
+        upload(ck, p + "self_attn.o_proj.weight", w.wo, H * nq, stage, stage_bytes);
+        w.ln2 = dalloc<uint16_t>(H);
+        upload(ck, p + "post_attention_layernorm.weight", w.ln2, H, stage, stage_bytes);
+        w.wgu = dalloc<uint16_t>(2 * I * H);
+        uint16_t* gu = reinterpret_cast<uint16_t*>(w.wgu);
+        upload(ck, p + "mlp.gate_proj.weight", gu, I * H, stage, stage_bytes);
+        upload(ck, p + "mlp.up_proj.weight", gu + I * H, I * H, stage, stage_bytes);
+        w.wd = dalloc<uint16_t>(H * I);
+        upload(ck, p + "mlp.down_proj.weight", w.wd, H * I, stage, stage_bytes);
+      }
+    } catch (...) {
+      if (stage) (void)hipFree(stage);
+      throw;
+    }
+    if (stage) (void)hipFree(stage);
+  }
+
+  void alloc_state() {
+    const Cfg& c = cfg_;
+    const size_t kv = (size_t)c.L * c.nkv * S_ * c.hd;
+    kc_ = dalloc<uint16_t>(kv);
+    vc_ = dalloc<uint16_t>(kv);
+    const std::vector<float> f = c.inv_freq();
+    inv_freq_ = dalloc<float>(f.size());
+    hip_check(hipMemcpy(inv_freq_, f.data(), f.size() * sizeof(float), hipMemcpyHostToDevice),
+              "inv_freq");
+    const size_t nq = (size_t)c.nh * c.hd;
+    resid_ = dalloc<float>(c.H);
+    q_ = dalloc<float>(nq);
+    part_ = dalloc<float>(2 * (size_t)c.nh * kAttnMaxSplit * (c.hd + 2));
+    logits_ = dalloc<float>(c.V);
+    attn_out_ = dalloc<uint16_t>(nq);
+    act_ = dalloc<uint16_t>(c.I);
+    tickets_ = dalloc<unsigned int>(2 * c.nkv + 2);
+    thr_ = dalloc<unsigned int>(1);
+    sel_ticket_ = dalloc<unsigned int>(1);
+    pos_ = dalloc<int>(1);
+    tok_ = dalloc<int>(1);
+    hist_ = dalloc<int>(S_);
+    hist_len_ = dalloc<int>(1);
+    slot_ = dalloc<unsigned long long>(1);
+    scratch_i32_ = dalloc<int>(4);
+    scratch_resid_ = dalloc<float>(c.H);
+    zeros_ = dalloc<int32_t>(64);
+    hip_check(hipMemset(tickets_, 0, sizeof(unsigned int) * (2 * c.nkv + 2)), "memset");
+    hip_check(hipMemset(part_, 0, sizeof(float) * 2 * c.nh * kAttnMaxSplit * (c.hd + 2)), "memset");
+    hip_check(hipMemset(sel_ticket_, 0, sizeof(unsigned int)), "memset");
+    hip_check(hipMemset(slot_, 0, sizeof(unsigned long long)), "memset");
+    hip_check(hipMemset(zeros_, 0, sizeof(int32_t) * 64), "memset");
+    hip_check(hipMemset(hist_, 0, sizeof(int) * S_), "memset");
+    hip_check(hipDeviceSynchronize(), "sync");  // null-stream memsets before st_ work
+  }
+
+  uint16_t* kc(int l) const { return kc_ + (size_t)l * cfg_.nkv * S_ * cfg_.hd; }
+  uint16_t* vc(int l) const { return vc_ + (size_t)l * cfg_.nkv * S_ * cfg_.hd; }
+  float scale() const { return 1.0f / std::sqrt((float)cfg_.hd); }
+
+  // ---- prefill
+  void grow_prefill(int T) {
+    if (T <= pre_T_) return;
+    const Cfg& c = cfg_;
+    for (void* p : {(void*)hidden_, x16_, qkv_, att_, pact_, (void*)ptok_}) dfree(p);
+    const size_t nq = (size_t)c.nh * c.hd, nk = (size_t)c.nkv * c.hd;
+    hidden_ = dalloc<float>((size_t)T * c.H);
+    x16_ = dalloc<uint16_t>((size_t)T * c.H);
+    qkv_ = dalloc<uint16_t>((size_t)T * (nq + 2 * nk));
+    att_ = dalloc<uint16_t>((size_t)T * nq);
+    pact_ = dalloc<uint16_t>((size_t)T * c.I);
+    ptok_ = dalloc<int32_t>(T);
+    pre_T_ = T;
+  }
+
+  void gemm(int epi, const void* a, long long lda, const void* b, long long ldb, void* cptr,
+            long long ldc, float* resid, long long ldr, int M, int N, int K, const char* what) {
+    const bool gated = epi == kEpiSwiglu;
+    const long long Nv = gated ? 2LL * N : N;
+    static const char* names[] = {"store", "resid32", "add16", "swiglu"};
+    auto p = planner_.plan(M, Nv, K, names[epi]);
+    const int splits = p.second;
+    float* ws = nullptr;
+    if (splits > 1) {
+      const size_t need = (size_t)splits * M * Nv;
+      if (need > ws_n_) {
+        dfree(ws_);
+        ws_ = dalloc<float>(need);
+        ws_n_ = need;
+      }
+      ws = ws_;
+    }
+    k_check(cake_gemm(dt_, epi, p.first, splits, a, lda, b, ldb, cptr, ldc, nullptr, resid, ldr,
+                      ws, zeros_, M, N, K, st_), what);
+  }
+
+  void prefill(const int32_t* prompt, int T) {
+    const Cfg& c = cfg_;
+    if (T > S_) throw Error("prompt longer than max_seq");
+    grow_prefill(T);
+    const int nq = c.nh * c.hd, nk = c.nkv * c.hd, nqkv = nq + 2 * nk;
+    hip_check(hipMemcpyAsync(ptok_, prompt, sizeof(int32_t) * T, hipMemcpyHostToDevice, st_),
+              "prompt H2D");
+    k_check(cake_embed(dt_, embed_, ptok_, T, c.H, hidden_, st_), "embed");
+    const int pos0 = 0, Tk = T;
+    for (int l = 0; l < c.L; ++l) {
+      const LayerW& w = layers_[l];
+      k_check(cake_rmsnorm(dt_, hidden_, w.ln1, (float)c.eps, T, c.H, x16_, st_), "rmsnorm");
+      gemm(kEpiStore, x16_, c.H, w.wqkv, c.H, qkv_, nqkv, nullptr, 0, T, nqkv, c.H, "gemm qkv");
+      uint16_t* q = reinterpret_cast<uint16_t*>(qkv_);
+      k_check(cake_rope_kv(dt_, q, q + nq, q + nq + nk, nqkv, nqkv, T, c.nh, c.nkv, c.hd,
+                           inv_freq_, pos0, S_, kc(l), vc(l), st_), "rope_kv");
+      // [B, H, rows, D] strides of q (a column block of qkv), the layer's cache, the output
+      const long long Sh = (long long)S_ * c.hd;
+      const long long strides[12] = {(long long)T * nqkv, c.hd, nqkv,
+                                     (long long)c.nkv * Sh, Sh, c.hd,
+                                     (long long)c.nkv * Sh, Sh, c.hd,
+                                     (long long)T * nq, c.hd, nq};
+      k_check(cake_flash_attn(dt_, q, kc(l), vc(l), att_, 1, c.nh, c.nkv, T, Tk, c.hd, strides,
+                              scale(), 1, pos0, st_), "flash_attn");
+      gemm(kEpiResid32, att_, nq, w.wo, nq, nullptr, 0, hidden_, c.H, T, c.H, nq, "gemm o");
+      k_check(cake_rmsnorm(dt_, hidden_, w.ln2, (float)c.eps, T, c.H, x16_, st_), "rmsnorm");
+      gemm(kEpiSwiglu, x16_, c.H, w.wgu, c.H, pact_, c.I, nullptr, 0, T, c.I, c.H, "gemm gate|up");
+      gemm(kEpiResid32, pact_, c.I, w.wd, c.I, nullptr, 0, hidden_, c.H, T, c.H, c.I, "gemm down");
+    }
+    k_check(cake_gemv_norm_f32(dt_, hidden_ + (size_t)(T - 1) * c.H, norm_, (float)c.eps,
+                               lm_head_, c.H, c.V, logits_, st_), "lm_head");
+  }
+
+  // ---- token selection / decode step
+  Mode mode_of(const CakeEngineSampling& s) const {
+    Mode m;
+    m.greedy = s.temperature <= 0.f;
+    m.penalty = s.repeat_penalty;
+    m.last_n = s.repeat_last_n;
+    if (!m.greedy) {
+      m.temperature = s.temperature;
+      m.top_k = s.top_k > 0 ? s.top_k : 0;
+      m.top_p = (s.top_p > 0.f && s.top_p < 1.f) ? s.top_p : 0.f;
+      m.seed = s.seed;
+    }
+    m.fused = m.greedy && (m.penalty == 1.f || m.last_n <= kHeadSelectMaxLastN);
+    return m;
+  }
+
+  // logits -> penalty -> argmax / draw -> finalize (tok, history, pos)
+  void select_tail(const Mode& m) {
+    if (m.penalty != 1.f)
+      k_check(cake_repeat_penalty(logits_, hist_, hist_len_, m.last_n, m.penalty, st_), "penalty");
+    if (m.greedy) {
+      k_check(cake_argmax(logits_, cfg_.V, slot_, st_), "argmax");
+    } else {
+      const bool restrict = m.top_k > 0 || m.top_p > 0.f;
+      if (restrict)
+        k_check(cake_sample_threshold(logits_, cfg_.V, m.temperature, m.top_k, m.top_p, thr_, st_),
+                "sample_threshold");
+      k_check(cake_gumbel_argmax(logits_, cfg_.V, m.temperature, m.seed, hist_len_,
+                                 restrict ? thr_ : nullptr, slot_, st_), "gumbel_argmax");
+    }
+    k_check(cake_finalize_token(slot_, tok_, hist_, hist_len_, pos_, S_, st_), "finalize");
+  }
+
+  void step_body(const Mode& m) {
+    const Cfg& c = cfg_;
+    const int nq = c.nh * c.hd, nk = c.nkv * c.hd;
+    if (!m.fused) k_check(cake_embed(dt_, embed_, tok_, 1, c.H, resid_, st_), "embed");
+    for (int l = 0; l < c.L; ++l) {
+      const LayerW& w = layers_[l];
+      const uint16_t* wqkv = reinterpret_cast<const uint16_t*>(w.wqkv);
+      k_check(cake_qkv_rope(dt_, resid_, w.ln1, (float)c.eps, wqkv, wqkv + (size_t)nq * c.H,
+                            wqkv + (size_t)(nq + nk) * c.H, c.H, c.nh, c.nkv, c.hd, inv_freq_,
+                            pos_, q_, kc(l), vc(l), S_, st_), "qkv_rope");
+      k_check(cake_attn_decode(dt_, q_, kc(l), vc(l), pos_, S_, c.nh, c.nkv, c.hd, scale(), part_,
+                               tickets_, attn_out_, st_), "attn_decode");
+      k_check(cake_gemv_x16(dt_, attn_out_, w.wo, nq, c.H, resid_, 1, st_), "o_proj");
+      const uint16_t* wgu = reinterpret_cast<const uint16_t*>(w.wgu);
+      k_check(cake_swiglu(dt_, resid_, w.ln2, (float)c.eps, wgu, wgu + (size_t)c.I * c.H, c.H,
+                          c.I, act_, st_), "swiglu");
+      k_check(cake_gemv_x16(dt_, act_, w.wd, c.I, c.H, resid_, 1, st_), "down_proj");
+    }
+    if (m.fused) {
+      k_check(cake_head_select(dt_, resid_, norm_, (float)c.eps, lm_head_, c.H, c.V, logits_,
+                               hist_, hist_len_, m.penalty != 1.f ? m.last_n : 0, m.penalty,
+                               slot_, sel_ticket_, tok_, pos_, S_, embed_, resid_, st_),
+              "head_select");
+      return;
+    }
+    k_check(cake_gemv_norm_f32(dt_, resid_, norm_, (float)c.eps, lm_head_, c.H, c.V, logits_, st_),
+            "lm_head");
+    select_tail(m);
+  }
+
+  void drop_graphs() {
+    for (auto e : execs_) (void)hipGraphExecDestroy(e);
+    for (auto g : graphs_) (void)hipGraphDestroy(g);
+    execs_.clear();
+    graphs_.clear();
+    have_graphs_ = false;
+  }
+
+  // one graph per attention split cap (DeviceDecoder.capture position buckets)
+  void ensure_graphs(const Mode& m) {
+    if (have_graphs_ && graph_mode_ == m) return;
+    drop_graphs();
+    // warm every kernel once outside capture on the live state, then restore it (the
+    // K/V row this writes is the next step's, which that step rewrites)
+    hip_check(hipMemcpyAsync(scratch_i32_, tok_, sizeof(int), hipMemcpyDeviceToDevice, st_), "snap");
+    hip_check(hipMemcpyAsync(scratch_i32_ + 1, pos_, sizeof(int), hipMemcpyDeviceToDevice, st_), "snap");
+    hip_check(hipMemcpyAsync(scratch_i32_ + 2, hist_len_, sizeof(int), hipMemcpyDeviceToDevice, st_), "snap");
+    hip_check(hipMemcpyAsync(scratch_resid_, resid_, sizeof(float) * cfg_.H, hipMemcpyDeviceToDevice, st_), "snap");
+    step_body(m);
+    hip_check(hipMemcpyAsync(tok_, scratch_i32_, sizeof(int), hipMemcpyDeviceToDevice, st_), "restore");
+    hip_check(hipMemcpyAsync(pos_, scratch_i32_ + 1, sizeof(int), hipMemcpyDeviceToDevice, st_), "restore");
+    hip_check(hipMemcpyAsync(hist_len_, scratch_i32_ + 2, sizeof(int), hipMemcpyDeviceToDevice, st_), "restore");
+    hip_check(hipMemcpyAsync(resid_, scratch_resid_, sizeof(float) * cfg_.H, hipMemcpyDeviceToDevice, st_), "restore");
+    hip_check(hipMemsetAsync(slot_, 0, sizeof(unsigned long long), st_), "slot");
+    hip_check(hipStreamSynchronize(st_), "sync");
+    // caps: 8 / 16 / 32 / 64 (clamped to the max_seq grid) up to the first covering
+    // every live length (ops.hip.attn_split_caps)
+    const int full = cake_attn_max_split(S_);
+    int need = 1;
+    for (int t = 1; t <= S_; ++t) need = std::max(need, cake_attn_splits(t));
+    std::vector<int> caps;
+    for (int cap : {8, 16, 32, 64}) {
+      const int cc = std::min(cap, full);
+      if (std::find(caps.begin(), caps.end(), cc) == caps.end()) caps.push_back(cc);
+      if (cap >= need) break;
+    }
+    std::sort(caps.begin(), caps.end());
+    try {
+      for (int cap : caps) {
+        k_check(cake_attn_set_split_cap(cap), "attn_set_split_cap");
+        hipGraph_t g = nullptr;
+        hip_check(hipStreamBeginCapture(st_, hipStreamCaptureModeGlobal), "BeginCapture");
+        try {
+          for (int i = 0; i < k_; ++i) step_body(m);
+        } catch (...) {
+          (void)hipStreamEndCapture(st_, &g);
+          if (g) (void)hipGraphDestroy(g);
+          throw;
+        }
+        hip_check(hipStreamEndCapture(st_, &g), "EndCapture");
+        graphs_.push_back(g);
+        hipGraphExec_t e = nullptr;
+        hip_check(hipGraphInstantiate(&e, g, nullptr, nullptr, 0), "GraphInstantiate");
+        execs_.push_back(e);
+      }
+    } catch (...) {
+      (void)cake_attn_set_split_cap(0);
+      drop_graphs();
+      throw;
+    }
+    k_check(cake_attn_set_split_cap(0), "attn_set_split_cap");
+    bucket_of_.assign(S_ + 1, (int32_t)caps.size() - 1);
+    for (int t = 0; t <= S_; ++t) {
+      const int nd = cake_attn_splits(t);
+      for (size_t i = 0; i < caps.size(); ++i)
+        if (caps[i] >= nd) { bucket_of_[t] = (int32_t)i; break; }
+    }
+    graph_mode_ = m;
+    have_graphs_ = true;
+  }
+};
+
+void put_err(char* err, int errlen, const std::string& msg) {
+  if (err && errlen > 0) {
+    std::snprintf(err, (size_t)errlen, "%s", msg.c_str());
+  }
+}
+
+}  // namespace
+}  // namespace cake
+
+using cake::Llama;
+
+CAKE_API void* cake_engine_open(const char* model_dir, const CakeEngineOpts* opts, char* err,
+                                int32_t errlen) {
+  try {
+    if (!model_dir || !opts) throw cake::Error("null argument");
+    return new Llama(model_dir, *opts);
+  } catch (const std::exception& e) {
+    cake::put_err(err, errlen, e.what());
+    return nullptr;
+  }
+}
+
+CAKE_API int32_t cake_engine_info(void* h, int32_t* o) {
+  if (!h || !o) return (int32_t)hipErrorInvalidValue;
+  const Llama* m = static_cast<Llama*>(h);
+  const auto& c = m->cfg();
+  const int32_t v[8] = {c.V, c.H, c.L, c.nh, c.nkv, c.hd, c.I, m->max_seq()};
+  std::memcpy(o, v, sizeof(v));
+  return 0;
+}
+
+CAKE_API int32_t cake_engine_eos(void* h, int32_t* out, int32_t cap) {
+  if (!h) return 0;
+  const auto& e = static_cast<Llama*>(h)->cfg().eos;
+  for (int32_t i = 0; i < cap && i < (int32_t)e.size(); ++i) out[i] = e[i];
+  return (int32_t)e.size();
+}
+
+CAKE_API int32_t cake_engine_generate(void* h, const int32_t* prompt, int32_t n_prompt,
+                                      int32_t max_new, const CakeEngineSampling* sampling,
+                                      const int32_t* eos, int32_t n_eos,
+                                      cake_engine_token_cb cb, void* ctx, int32_t* out,
+                                      int32_t out_cap, CakeEngineStats* stats, char* err,
+                                      int32_t errlen) {
+  try {
+    if (!h || !prompt || !sampling || (!out && max_new > 0)) throw cake::Error("null argument");
+    static_cast<Llama*>(h)->generate(prompt, n_prompt, max_new, *sampling, eos, n_eos, cb, ctx,
+                                     out, out_cap, stats);
+    return 0;
+  } catch (const std::exception& e) {
+    cake::put_err(err, errlen, e.what());
+    return 1;
+  }
+}
+
+CAKE_API int32_t cake_engine_prefill_logits(void* h, const int32_t* prompt, int32_t n_prompt,
+                                            float* out, char* err, int32_t errlen) {
+  try {
+    if (!h || !prompt || !out) throw cake::Error("null argument");
+    static_cast<Llama*>(h)->prefill_logits(prompt, n_prompt, out);
+    return 0;
+  } catch (const std::exception& e) {
+    cake::put_err(err, errlen, e.what());
+    return 1;
+  }
+}
+
+CAKE_API void cake_engine_close(void* h) { delete static_cast<Llama*>(h); }

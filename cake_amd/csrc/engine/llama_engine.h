@@ -1,0 +1,65 @@
+// Native Llama text-generation engine: C ABI (libcake_engine.so).
+//
+// The whole text path of one all-local model without Python: checkpoint (safetensors,
+// HF names) -> device weights, MFMA-GEMM prefill, hipGraph-captured decode steps
+// (hipStreamBeginCapture over the gfx950 kernels' C entry points), device token
+// selection, and the per-token replay loop (graph_loop.cpp).  Reference: the master's
+// generation loop cake-core/src/cake/master.rs:80-124 and the Llama generator
+// cake-core/src/models/llama3/llama.rs:72-138, 277-341.
+#pragma once
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int32_t (*cake_engine_token_cb)(void* ctx, int32_t token);  // non-zero = stop
+
+struct CakeEngineOpts {
+  int32_t max_seq;          // KV-cache length (prompt + generated tokens)
+  int32_t dtype;            // 0 = bf16, 1 = f16
+  int32_t device;           // GPU ordinal
+  int32_t steps_per_graph;  // decode steps per graph replay (greedy only; >= 1)
+};
+
+struct CakeEngineSampling {
+  float temperature;        // <= 0: greedy
+  int32_t top_k;            // 0: off
+  float top_p;              // 0 or >= 1: off
+  uint64_t seed;
+  float repeat_penalty;     // 1: off
+  int32_t repeat_last_n;
+};
+
+struct CakeEngineStats {
+  int32_t n_prompt;
+  int32_t n_generated;
+  double prefill_s;         // embed + layers + head + first token (host wall)
+  double decode_s;          // generated tokens after the first (host wall)
+  double tokens_per_s;      // (n_generated - 1) / decode_s: the reference's rate
+  float p50_ms, p99_ms;     // device time per decode token
+};
+
+// config.json + safetensors of `model_dir`; null on failure (message in err).
+void* cake_engine_open(const char* model_dir, const struct CakeEngineOpts* opts, char* err,
+                       int32_t errlen);
+// [V, H, L, nh, nkv, hd, I, max_seq]
+int32_t cake_engine_info(void* engine, int32_t* out8);
+// EOS ids of the config (up to cap); returns the count
+int32_t cake_engine_eos(void* engine, int32_t* out, int32_t cap);
+// Prefill `prompt` from position 0, then generate up to max_new tokens (the first comes
+// from the prefill logits), stopping after an EOS id.  Tokens go to out[] (and cb).
+// Returns 0 or an error code (message in err).
+int32_t cake_engine_generate(void* engine, const int32_t* prompt, int32_t n_prompt,
+                             int32_t max_new, const struct CakeEngineSampling* sampling,
+                             const int32_t* eos, int32_t n_eos, cake_engine_token_cb cb,
+                             void* ctx, int32_t* out, int32_t out_cap,
+                             struct CakeEngineStats* stats, char* err, int32_t errlen);
+// Logits of the last prompt position after a prefill only (f32 [V] to host), for tests.
+int32_t cake_engine_prefill_logits(void* engine, const int32_t* prompt, int32_t n_prompt,
+                                   float* out, char* err, int32_t errlen);
+void cake_engine_close(void* engine);
+
+#ifdef __cplusplus
+}
+#endif

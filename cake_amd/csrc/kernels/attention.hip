@@ -116,6 +116,31 @@ CAKE_API int cake_attn_debug_drop_partials(int on) {
   return 0;
 }
 
+// Host mirror of the device split policy (attn2_splits / core 1's chunk rule) for a live
+// length Tk under the current settings: the native engine picks position-bucket graphs
+// with it (as ops.hip.attn_splits does for Python).
+CAKE_API int cake_attn_splits(int Tk) {
+  if (Tk < 1) Tk = 1;
+  if (g_attn_impl == 2) {
+    int ns, kps;
+    if (Tk <= g_attn_single) return 1;
+    int keys = (Tk + g_attn_target - 1) / g_attn_target;
+    keys = (keys + 15) / 16 * 16;
+    if (keys < g_attn_min_keys) keys = g_attn_min_keys;
+    ns = (Tk + keys - 1) / keys;
+    if (ns > kMaxSplit) ns = kMaxSplit;
+    kps = (Tk + ns - 1) / ns;
+    kps = (kps + 15) / 16 * 16;
+    return (Tk + kps - 1) / kps;
+  }
+  int keys = g_attn_min_keys;
+  if (Tk > 1024 && keys < 128) keys = 128;
+  if (keys < (Tk + 63) / 64) keys = (Tk + 63) / 64;
+  return (Tk + keys - 1) / keys;
+}
+
+CAKE_API int cake_attn_max_split(int S) { return S > 0 ? attn_max_split(S) : 0; }
+
 CAKE_API int cake_attn_set_min_keys(int min_keys) {
   if (min_keys < kChunk || min_keys % kChunk) return (int)hipErrorInvalidValue;
   g_attn_min_keys = min_keys;

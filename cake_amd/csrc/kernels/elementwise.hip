@@ -174,6 +174,19 @@ __global__ __launch_bounds__(256) void stream_read_kernel(const uint4* __restric
   if (acc == 0x9e3779b9u) sink[0] = acc;
 }
 
+// Weight upload conversion (native engine, csrc/engine/llama_engine.cpp): a checkpoint
+// tensor in bf16 / f16 / f32 (SK 0 / 1 / 2) -> the model's 16-bit dtype.
+template <int SK, int DT>
+__global__ __launch_bounds__(256) void cast16_kernel(const void* __restrict__ src,
+                                                     uint16_t* __restrict__ dst, size_t n) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+    float v;
+    if constexpr (SK == 2) v = reinterpret_cast<const float*>(src)[i];
+    else v = to_f32<SK>(reinterpret_cast<const uint16_t*>(src)[i]);
+    dst[i] = from_f32<DT>(v);
+  }
+}
+
 }  // namespace cake
 
 using namespace cake;
@@ -196,6 +209,19 @@ CAKE_API int cake_stream_read(const void* p, size_t bytes, int blocks, unsigned 
 static inline int ew_grid(size_t n) {
   size_t g = (n + 255) / 256;
   return (int)(g < 4096 ? g : 4096);
+}
+
+CAKE_API int cake_cast16(int src_kind, int dt, const void* src, void* dst, size_t n,
+                         hipStream_t st) {
+  if (src_kind < 0 || src_kind > 2) return (int)hipErrorInvalidValue;
+  const dim3 g(ew_grid(n)), b(256);
+#define CAKE_CAST(SKV)                                                                      \
+  DISPATCH_DT(dt, hipLaunchKernelGGL((cast16_kernel<SKV, DT>), g, b, 0, st, src, (uint16_t*)dst, n))
+  if (src_kind == 0) CAKE_CAST(0);
+  else if (src_kind == 1) CAKE_CAST(1);
+  else CAKE_CAST(2);
+#undef CAKE_CAST
+  return (int)hipGetLastError();
 }
 
 CAKE_API int cake_embed(int dt, const void* table, const int* tok, int T, int H, float* out,

@@ -6,6 +6,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <stdexcept>
 #include <string>
 
 namespace cake {
@@ -38,27 +39,66 @@ static PyObject* to_py(const PyArg& a) {
   Py_RETURN_NONE;
 }
 
-int run_embedded(const PyArgs& options) {
-  const bool owner = !Py_IsInitialized();
-  if (owner) {
-    PyConfig cfg;
-    PyConfig_InitPythonConfig(&cfg);
-    cfg.install_signal_handlers = 1;  // Ctrl-C -> KeyboardInterrupt, like the CLI
-    cfg.parse_argv = 0;
-    const PyStatus st = Py_InitializeFromConfig(&cfg);
-    PyConfig_Clear(&cfg);
-    if (PyStatus_Exception(st)) {
-      std::fprintf(stderr, "cake: cannot start the embedded Python runtime\n");
-      return 1;
-    }
-    PyEval_SaveThread();  // release the GIL: every call below takes it via PyGILState
+// Start the interpreter if this process has none (the GIL is released afterwards:
+// every call takes it through PyGILState).
+static bool ensure_interpreter() {
+  if (Py_IsInitialized()) return true;
+  PyConfig cfg;
+  PyConfig_InitPythonConfig(&cfg);
+  cfg.install_signal_handlers = 1;  // Ctrl-C -> KeyboardInterrupt, like the CLI
+  cfg.parse_argv = 0;
+  const PyStatus st = Py_InitializeFromConfig(&cfg);
+  PyConfig_Clear(&cfg);
+  if (PyStatus_Exception(st)) {
+    std::fprintf(stderr, "cake: cannot start the embedded Python runtime\n");
+    return false;
   }
-  const PyGILState_STATE gil = PyGILState_Ensure();
-  int rc = 1;
+  PyEval_SaveThread();
+  return true;
+}
+
+static void add_root_to_path() {
   PyObject* sys_path = PySys_GetObject("path");  // borrowed
   PyObject* root = PyUnicode_FromString(package_root().c_str());
   if (sys_path && root && !PySequence_Contains(sys_path, root)) PyList_Insert(sys_path, 0, root);
   Py_XDECREF(root);
+}
+
+std::string call_python(const std::string& module, const std::string& function,
+                        const std::string& arg) {
+  if (!ensure_interpreter()) throw std::runtime_error("no Python runtime");
+  const PyGILState_STATE gil = PyGILState_Ensure();
+  add_root_to_path();
+  PyObject* mod = PyImport_ImportModule(module.c_str());
+  PyObject* fn = mod ? PyObject_GetAttrString(mod, function.c_str()) : nullptr;
+  PyObject* a = PyUnicode_FromStringAndSize(arg.data(), (Py_ssize_t)arg.size());
+  PyObject* res = (fn && a) ? PyObject_CallOneArg(fn, a) : nullptr;
+  std::string out;
+  bool ok = false;
+  if (res && PyUnicode_Check(res)) {
+    Py_ssize_t n = 0;
+    const char* u = PyUnicode_AsUTF8AndSize(res, &n);
+    if (u) {
+      out.assign(u, (size_t)n);
+      ok = true;
+    }
+  }
+  if (!ok && PyErr_Occurred()) PyErr_Print();
+  Py_XDECREF(res);
+  Py_XDECREF(a);
+  Py_XDECREF(fn);
+  Py_XDECREF(mod);
+  PyGILState_Release(gil);
+  if (!ok) throw std::runtime_error(module + "." + function + " failed");
+  return out;
+}
+
+int run_embedded(const PyArgs& options) {
+  const bool owner = !Py_IsInitialized();
+  if (!ensure_interpreter()) return 1;
+  const PyGILState_STATE gil = PyGILState_Ensure();
+  int rc = 1;
+  add_root_to_path();
   PyObject* mod = PyImport_ImportModule("cake_amd.cli");
   PyObject* fn = mod ? PyObject_GetAttrString(mod, "run_parsed") : nullptr;
   PyObject* kw = PyDict_New();

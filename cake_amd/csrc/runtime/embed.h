@@ -25,6 +25,13 @@ using PyArgs = std::map<std::string, PyArg>;  // argparse dest -> typed value
 // (1 + a printed traceback on an uncaught exception).
 int run_embedded(const PyArgs& options);
 
+// Call `module.function(arg)` in the embedded interpreter (initialised on first use,
+// GIL taken for the call) with one str argument; returns the str result.  Throws
+// std::runtime_error (with the Python traceback printed) on failure.  The native text
+// path uses it for the tokenizer only (cake_amd/native_bridge.py).
+std::string call_python(const std::string& module, const std::string& function,
+                        const std::string& arg);
+
 // Directory that contains the cake_amd package (derived from the location of
 // the code object this function lives in), for sys.path.
 std::string package_root();

@@ -9,8 +9,10 @@
 // runs its role: the tensor compute (PyTorch-ROCm + the gfx950 HIP kernels) in
 // an interpreter embedded in THIS process (embed.cpp), the worker's TCP
 // control plane on the native WorkerServer.
+#include <dlfcn.h>
 #include <unistd.h>
 
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -19,7 +21,9 @@
 #include <string>
 #include <vector>
 
+#include "../engine/llama_engine.h"
 #include "embed.h"
+#include "json.h"
 #include "topology.h"
 
 using cake::PyArg;
@@ -135,6 +139,132 @@ bool in_choices(const std::string& v, const char* choices) {
   return false;
 }
 
+// ---------------------------------------------------------------------------
+// Native text generation: an all-local text model (no topology workers, no API server)
+// runs on the native engine (libcake_engine.so, dlopen'ed: worker / image / API runs
+// never load it) — checkpoint load, prefill, graph-replayed decode and token selection
+// in C++; the embedded interpreter only tokenizes (cake_amd/native_bridge.py).
+// CAKE_NATIVE=0 keeps the Python generator.  Output as Master.run: the streamed text,
+// then the reference's rate line (master.rs:93-121) on stderr.
+// ---------------------------------------------------------------------------
+struct EngineApi {
+  void* (*open)(const char*, const CakeEngineOpts*, char*, int32_t);
+  int32_t (*generate)(void*, const int32_t*, int32_t, int32_t, const CakeEngineSampling*,
+                      const int32_t*, int32_t, cake_engine_token_cb, void*, int32_t*, int32_t,
+                      CakeEngineStats*, char*, int32_t);
+  void (*close)(void*);
+};
+
+bool native_text_eligible(cake::PyArgs& o, bool text, bool worker, bool has_topology) {
+  const char* env = std::getenv("CAKE_NATIVE");
+  if (env && std::string(env) == "0") return false;
+  const auto is = [&](const char* k, const char* v) { return o[k].value == v; };
+  return text && !worker && !has_topology && o["api"].kind == PyArg::kNone &&
+         !is("cpu", "1") && is("transport", "tcp") && !is("no_graph", "1") &&
+         o["trace"].kind == PyArg::kNone && o["metrics"].kind == PyArg::kNone &&
+         (o["dtype"].kind == PyArg::kNone || is("dtype", "f16") || is("dtype", "bf16"));
+}
+
+struct StreamCtx {
+  std::string model;
+  std::vector<int32_t> eos;
+};
+
+int32_t stream_token(void* vctx, int32_t tok) {
+  auto* c = static_cast<StreamCtx*>(vctx);
+  for (int32_t e : c->eos)
+    if (e == tok) return 0;  // EOS: nothing printed (the loop stops on it)
+  cake::Json req = cake::Json::object();
+  req.set("model", cake::Json::string(c->model));
+  req.set("id", cake::Json::integer(tok));
+  try {
+    const std::string text = cake::call_python("cake_amd.native_bridge", "decode_token", req.dump());
+    std::fwrite(text.data(), 1, text.size(), stdout);
+    std::fflush(stdout);
+  } catch (const std::exception&) {
+  }
+  return 0;
+}
+
+int run_native_text(cake::PyArgs& o) {
+  const std::string lib = cake::package_root() + "/cake_amd/lib/libcake_engine.so";
+  void* h = dlopen(lib.c_str(), RTLD_NOW | RTLD_LOCAL);
+  if (!h) {
+    std::fprintf(stderr, "cake-cli: %s\n", dlerror());
+    return 1;
+  }
+  EngineApi api{};
+  api.open = reinterpret_cast<decltype(api.open)>(dlsym(h, "cake_engine_open"));
+  api.generate = reinterpret_cast<decltype(api.generate)>(dlsym(h, "cake_engine_generate"));
+  api.close = reinterpret_cast<decltype(api.close)>(dlsym(h, "cake_engine_close"));
+  if (!api.open || !api.generate || !api.close) {
+    std::fprintf(stderr, "cake-cli: engine symbols missing in %s\n", lib.c_str());
+    return 1;
+  }
+  StreamCtx ctx;
+  ctx.model = o["model"].value;
+  std::vector<int32_t> ids;
+  try {
+    cake::Json req = cake::Json::object();
+    req.set("model", cake::Json::string(ctx.model));
+    req.set("system", cake::Json::string(o["system_prompt"].value));
+    req.set("prompt", cake::Json::string(o["prompt"].value));
+    const cake::Json r = cake::Json::parse(
+        cake::call_python("cake_amd.native_bridge", "encode_chat", req.dump()));
+    for (const auto& x : r.get("ids").items()) ids.push_back((int32_t)x.as_int());
+    for (const auto& x : r.get("eos").items()) ctx.eos.push_back((int32_t)x.as_int());
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "cake-cli: tokenizer: %s\n", e.what());
+    return 1;
+  }
+  const auto num = [&](const char* k, double def) {
+    return o[k].kind == PyArg::kNone ? def : std::strtod(o[k].value.c_str(), nullptr);
+  };
+  CakeEngineOpts eo{};
+  eo.max_seq = (int32_t)num("max_seq_len", 4096);
+  eo.dtype = o["dtype"].value == "bf16" ? 0 : 1;  // reference default: f16
+  eo.device = (int32_t)num("device", 0);
+  eo.steps_per_graph = 1;
+  char err[1024] = {0};
+  const auto t0 = std::chrono::steady_clock::now();
+  void* eng = api.open(ctx.model.c_str(), &eo, err, sizeof(err));
+  if (!eng) {
+    std::fprintf(stderr, "cake-cli: native engine: %s\n", err);
+    return 1;
+  }
+  const double load_s =
+      std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  std::fprintf(stderr, "[cake-cli] native engine: model loaded in %.1f s (%zu prompt tokens)\n",
+               load_s, ids.size());
+  CakeEngineSampling smp{};
+  smp.temperature = (float)num("temperature", 1.0);
+  smp.top_k = (int32_t)num("top_k", 0);
+  smp.top_p = (float)num("top_p", 0.0);
+  smp.seed = (uint64_t)std::strtoull(o["seed"].value.c_str(), nullptr, 10);
+  smp.repeat_penalty = (float)num("repeat_penalty", 1.1);
+  smp.repeat_last_n = (int32_t)num("repeat_last_n", 128);
+  const int32_t n = (int32_t)num("sample_len", 100);
+  const int32_t room = eo.max_seq - (int32_t)ids.size() - 3;
+  const int32_t max_new = n < room ? n : room;
+  std::vector<int32_t> out((size_t)(max_new > 0 ? max_new : 1));
+  CakeEngineStats st{};
+  const int32_t rc = api.generate(eng, ids.data(), (int32_t)ids.size(), max_new, &smp,
+                                  ctx.eos.data(), (int32_t)ctx.eos.size(), stream_token, &ctx,
+                                  out.data(), (int32_t)out.size(), &st, err, sizeof(err));
+  std::fputc('\n', stdout);
+  std::fflush(stdout);
+  if (rc != 0) {
+    std::fprintf(stderr, "cake-cli: native engine: %s\n", err);
+    api.close(eng);
+    return 1;
+  }
+  std::fprintf(stderr, "[cake-cli] %d tokens generated (%.2f token/s) p50=%.2fms p99=%.2fms "
+               "ttft=%.1fms\n", st.n_generated, st.tokens_per_s, st.p50_ms, st.p99_ms,
+               st.prefill_s * 1e3);
+  api.close(eng);
+  return 0;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -187,6 +317,7 @@ int main(int argc, char** argv) {
   const bool text = opts["model_type"].value == "text-model";
   const std::string topo_path = opts["topology"].value;
   const bool worker = opts["mode"].value == "worker";
+  bool has_topology = false;
   if (access(topo_path.c_str(), R_OK) == 0) {
     try {
       const cake::Topology topo = cake::Topology::from_path(topo_path, text);
@@ -194,6 +325,7 @@ int main(int argc, char** argv) {
       for (const auto& n : topo.nodes) layers += n.layers.size();
       std::fprintf(stderr, "[cake-cli] topology %s: %zu node(s), %zu placed unit(s)\n",
                    topo_path.c_str(), topo.nodes.size(), layers);
+      has_topology = !topo.nodes.empty();
       if (worker) {
         if (topo.nodes.empty()) { std::fprintf(stderr, "cake-cli: topology has no workers\n"); return 2; }
         const PyArg& nm = opts["name"];
@@ -211,5 +343,6 @@ int main(int argc, char** argv) {
                  topo_path.c_str());
     return 2;
   }
+  if (native_text_eligible(opts, text, worker, has_topology)) return run_native_text(opts);
   return cake::run_embedded(opts);
 }

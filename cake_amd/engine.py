@@ -1,0 +1,156 @@
+"""ctypes front of the native Llama engine (csrc/engine/llama_engine.cpp, libcake_engine.so).
+
+The engine runs the whole text path of an all-local model in C++ — checkpoint load,
+MFMA prefill, hipGraph-captured decode steps and the token loop — with no PyTorch in
+the process's compute path.  This module only marshals arguments: the native CLI
+(cake-cli, csrc/tools/cake_cli.cpp) calls the same C ABI directly, and the tests pin it
+token-for-token to the Python DeviceDecoder (tests/test_engine_gpu.py).
+
+Reference: cake-core/src/cake/master.rs:80-124 (generation loop) and
+cake-core/src/models/llama3/llama.rs:72-138, 277-341 (the Llama generator).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+from pathlib import Path
+from typing import Callable
+
+LIB_PATH = Path(__file__).resolve().parent / "lib" / "libcake_engine.so"
+
+TOKEN_CB = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_int32)
+
+
+class EngineOpts(C.Structure):
+    _fields_ = [("max_seq", C.c_int32), ("dtype", C.c_int32), ("device", C.c_int32),
+                ("steps_per_graph", C.c_int32)]
+
+
+class EngineSampling(C.Structure):
+    _fields_ = [("temperature", C.c_float), ("top_k", C.c_int32), ("top_p", C.c_float),
+                ("seed", C.c_uint64), ("repeat_penalty", C.c_float),
+                ("repeat_last_n", C.c_int32)]
+
+
+class EngineStats(C.Structure):
+    _fields_ = [("n_prompt", C.c_int32), ("n_generated", C.c_int32), ("prefill_s", C.c_double),
+                ("decode_s", C.c_double), ("tokens_per_s", C.c_double), ("p50_ms", C.c_float),
+                ("p99_ms", C.c_float)]
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise RuntimeError(f"{LIB_PATH} missing: run `python -m cake_amd.build`")
+        L = C.CDLL(str(LIB_PATH))
+        P, I = C.c_void_p, C.c_int32
+        L.cake_engine_open.argtypes = [C.c_char_p, C.POINTER(EngineOpts), C.c_char_p, I]
+        L.cake_engine_open.restype = P
+        L.cake_engine_info.argtypes = [P, C.POINTER(C.c_int32)]
+        L.cake_engine_info.restype = I
+        L.cake_engine_eos.argtypes = [P, C.POINTER(C.c_int32), I]
+        L.cake_engine_eos.restype = I
+        L.cake_engine_generate.argtypes = [P, C.POINTER(C.c_int32), I, I, C.POINTER(EngineSampling),
+                                           C.POINTER(C.c_int32), I, TOKEN_CB, P,
+                                           C.POINTER(C.c_int32), I, C.POINTER(EngineStats),
+                                           C.c_char_p, I]
+        L.cake_engine_generate.restype = I
+        L.cake_engine_prefill_logits.argtypes = [P, C.POINTER(C.c_int32), I,
+                                                 C.POINTER(C.c_float), C.c_char_p, I]
+        L.cake_engine_prefill_logits.restype = I
+        L.cake_engine_close.argtypes = [P]
+        L.cake_engine_close.restype = None
+        _lib = L
+    return _lib
+
+
+@dataclass
+class GenResult:
+    tokens: list[int] = field(default_factory=list)
+    n_prompt: int = 0
+    prefill_s: float = 0.0
+    decode_s: float = 0.0
+    tokens_per_s: float = 0.0
+    p50_ms: float = 0.0
+    p99_ms: float = 0.0
+
+
+class NativeLlama:
+    """One model loaded by the native engine on one GPU."""
+
+    def __init__(self, model_dir: str | Path, *, max_seq: int = 4096, dtype: str = "bf16",
+                 device: int = 0, steps_per_graph: int = 1):
+        if dtype not in ("bf16", "f16"):
+            raise ValueError("native engine dtype: bf16 or f16")
+        opts = EngineOpts(int(max_seq), 0 if dtype == "bf16" else 1, int(device),
+                          max(1, int(steps_per_graph)))
+        err = C.create_string_buffer(1024)
+        self._h = lib().cake_engine_open(str(model_dir).encode(), C.byref(opts), err, len(err))
+        if not self._h:
+            raise RuntimeError(f"native engine: {err.value.decode(errors='replace')}")
+        info = (C.c_int32 * 8)()
+        lib().cake_engine_info(self._h, info)
+        (self.vocab_size, self.hidden_size, self.num_layers, self.num_heads, self.num_kv_heads,
+         self.head_dim, self.intermediate_size, self.max_seq) = list(info)
+        eos = (C.c_int32 * 16)()
+        n = lib().cake_engine_eos(self._h, eos, 16)
+        self.eos_ids = [int(eos[i]) for i in range(min(n, 16))]
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().cake_engine_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def prefill_logits(self, prompt: list[int]):
+        import numpy as np
+        arr = (C.c_int32 * len(prompt))(*prompt)
+        out = np.empty(self.vocab_size, dtype=np.float32)
+        err = C.create_string_buffer(1024)
+        rc = lib().cake_engine_prefill_logits(self._h, arr, len(prompt),
+                                              out.ctypes.data_as(C.POINTER(C.c_float)), err,
+                                              len(err))
+        if rc:
+            raise RuntimeError(f"native engine: {err.value.decode(errors='replace')}")
+        return out
+
+    def generate(self, prompt: list[int], max_new: int, *, temperature: float = 0.0,
+                 top_k: int | None = None, top_p: float | None = None, seed: int = 299792458,
+                 repeat_penalty: float = 1.1, repeat_last_n: int = 128,
+                 eos_ids: list[int] | None = None,
+                 on_token: Callable[[int], bool | None] | None = None) -> GenResult:
+        arr = (C.c_int32 * len(prompt))(*prompt)
+        smp = EngineSampling(float(temperature or 0.0), int(top_k or 0), float(top_p or 0.0),
+                             int(seed) & 0xFFFFFFFFFFFFFFFF, float(repeat_penalty),
+                             int(repeat_last_n))
+        eos = list(eos_ids or [])
+        eos_arr = (C.c_int32 * max(1, len(eos)))(*eos)
+        out = (C.c_int32 * max(1, max_new))()
+        stats = EngineStats()
+        err = C.create_string_buffer(1024)
+        errors: list[BaseException] = []
+
+        def _tok(_ctx, t):
+            try:
+                return 1 if on_token(int(t)) else 0
+            except BaseException as e:  # noqa: BLE001  (re-raised after the call)
+                errors.append(e)
+                return 1
+
+        cb = TOKEN_CB(_tok) if on_token is not None else TOKEN_CB()
+        rc = lib().cake_engine_generate(self._h, arr, len(prompt), int(max_new), C.byref(smp),
+                                        eos_arr, len(eos), cb, None, out, max(1, max_new),
+                                        C.byref(stats), err, len(err))
+        if errors:
+            raise errors[0]
+        if rc:
+            raise RuntimeError(f"native engine: {err.value.decode(errors='replace')}")
+        return GenResult([int(out[i]) for i in range(stats.n_generated)], stats.n_prompt,
+                         stats.prefill_s, stats.decode_s, stats.tokens_per_s, stats.p50_ms,
+                         stats.p99_ms)

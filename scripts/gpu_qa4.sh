@@ -4,7 +4,7 @@ set -o pipefail
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
 timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
-  tests/test_kernels_gpu.py tests/test_sd_kernels_gpu.py -k "attn or qkv or conv1x1 or small_ic or out_nchw" \
+  tests/test_kernels_gpu.py tests/test_sd_kernels_gpu.py tests/test_sampling_gpu.py -k "attn or qkv or conv1x1 or small_ic or out_nchw or full_mass" \
   > gpurun_out/qa4_k.log 2>&1 || { tail -30 gpurun_out/qa4_k.log; exit 1; }
 tail -1 gpurun_out/qa4_k.log
 timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread \

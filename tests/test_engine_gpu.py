@@ -1,0 +1,112 @@
+"""Native Llama engine (libcake_engine.so) vs the Python DeviceDecoder on the same
+checkpoint: same kernels in the same order, so prefill logits agree to rounding and the
+generated tokens are identical — greedy (fused head), greedy with a penalty window past
+the fused head's bound, several steps per replay, sampled (top-k / top-p / seed), a
+dtype conversion on load (bf16 checkpoint -> f16 engine), and a generation that crosses
+the attention split-cap buckets."""
+import pytest
+import torch
+
+from cake_amd.models.llama3.config import preset
+from cake_amd.utils.synth import write_checkpoint
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ckpt(tmp_path_factory):
+    d = tmp_path_factory.mktemp("native_ckpt")
+    cfg = preset("llama3-8b", num_hidden_layers=3, vocab_size=2048, intermediate_size=1024,
+                 hidden_size=512, num_attention_heads=8, num_key_value_heads=2,
+                 bos_token_id=1, eos_token_id=2)
+    write_checkpoint(d, cfg, torch.bfloat16, seed=3, single_file=True)
+    return d
+
+
+def _python(ckpt, dtype, max_seq, prompt, n, sampling=None, penalty=1.1, last_n=16, k=1):
+    from cake_amd.models.llama3.decode_loop import run_decode
+    from cake_amd.models.llama3.factory import load_model
+    from cake_amd.models.llama3.model import DeviceDecoder
+    model = load_model(ckpt, "cuda:0", dtype, max_seq=max_seq)
+    dec = DeviceDecoder(model, repeat_penalty=penalty, repeat_last_n=last_n, greedy=True,
+                        steps_per_graph=k, sampling=sampling)
+    first = dec.start(prompt)
+    dec.capture()
+    toks = [first] + run_decode(dec, n - 1).tokens
+    logits = model.forward(prompt, 0).float().cpu()
+    del dec, model
+    torch.cuda.empty_cache()
+    return toks, logits
+
+
+def test_native_engine_matches_python_decoder(cuda, ckpt):
+    from cake_amd.engine import NativeLlama
+    from cake_amd.models.sampling import SamplingConfig
+    prompt = [1, 17, 300, 5, 99, 1024, 7, 8]
+    n = 24
+    eng = NativeLlama(ckpt, max_seq=256, dtype="bf16")
+    assert (eng.num_layers, eng.num_kv_heads, eng.head_dim) == (3, 2, 64)
+    ref, ref_logits = _python(ckpt, torch.bfloat16, 256, prompt, n)
+    logits = torch.from_numpy(eng.prefill_logits(prompt))
+    torch.testing.assert_close(logits, ref_logits.reshape(-1)[-logits.numel():], atol=2e-2,
+                               rtol=2e-2)
+    got = eng.generate(prompt, n, repeat_penalty=1.1, repeat_last_n=16)
+    assert got.tokens == ref
+    assert got.n_prompt == len(prompt) and got.p50_ms > 0 and got.tokens_per_s > 0
+    # the same engine again (graphs reused, state reset by the prefill)
+    assert eng.generate(prompt, n, repeat_penalty=1.1, repeat_last_n=16).tokens == ref
+    # penalty window beyond the fused head's bound: embed + lm_head + penalty + argmax tail
+    ref2, _ = _python(ckpt, torch.bfloat16, 256, prompt, n, last_n=300)
+    assert eng.generate(prompt, n, repeat_penalty=1.1, repeat_last_n=300).tokens == ref2
+    # sampled: threshold + Gumbel-max draws keyed by (seed, step)
+    s = SamplingConfig(temperature=0.8, top_k=20, top_p=0.9, seed=5)
+    ref3, _ = _python(ckpt, torch.bfloat16, 256, prompt, n, sampling=s)
+    got3 = eng.generate(prompt, n, temperature=0.8, top_k=20, top_p=0.9, seed=5,
+                        repeat_penalty=1.1, repeat_last_n=16)
+    assert got3.tokens == ref3
+    # EOS stops the generation (inclusive) and the callback sees every token
+    seen = []
+    stop_at = ref[5]
+    got4 = eng.generate(prompt, n, repeat_penalty=1.1, repeat_last_n=16, eos_ids=[stop_at],
+                        on_token=lambda t: seen.append(t))
+    assert got4.tokens == ref[:ref.index(stop_at) + 1] == seen
+    eng.close()
+
+
+def test_native_engine_f16_multistep_and_buckets(cuda, ckpt):
+    """bf16 checkpoint converted to f16 on load, 4 steps per replay, and a live length
+    crossing the one-split (320 keys) and 512-key bucket edges."""
+    from cake_amd.engine import NativeLlama
+    g = torch.Generator().manual_seed(2)
+    prompt = torch.randint(3, 2048, (500,), generator=g).tolist()
+    n = 20
+    ref, _ = _python(ckpt, torch.float16, 1024, prompt, n, k=4)
+    eng = NativeLlama(ckpt, max_seq=1024, dtype="f16", steps_per_graph=4)
+    assert eng.generate(prompt, n, repeat_penalty=1.1, repeat_last_n=16).tokens == ref
+    short = prompt[:300]
+    ref2, _ = _python(ckpt, torch.float16, 1024, short, 40, k=4)
+    assert eng.generate(short, 40, repeat_penalty=1.1, repeat_last_n=16).tokens == ref2
+    eng.close()
+
+
+def test_cake_cli_native_text_matches_python_cli(cuda, ckpt, tmp_path):
+    """cake-cli on an all-local text model runs the native engine (the embedded
+    interpreter only tokenizes); its streamed text equals the Python CLI's
+    (CAKE_NATIVE=0) on the same flags."""
+    import os
+    import subprocess
+    import sys
+    from cake_amd.utils.synth import write_tokenizer  # noqa: F401  (ckpt has tokenizer.json)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cli = os.path.join(root, "cake_amd", "lib", "cake-cli")
+    args = ["--model", str(ckpt), "--topology", str(tmp_path / "none.yml"), "--temperature", "0",
+            "-n", "16", "--dtype", "bf16", "--prompt", "hello there", "--max-seq-len", "256"]
+    env = dict(os.environ, CAKE_LOG="warning")
+    nat = subprocess.run([cli, *args], capture_output=True, text=True, timeout=300, env=env,
+                         cwd=root)
+    assert nat.returncode == 0, nat.stderr[-3000:]
+    assert "native engine" in nat.stderr and "token/s" in nat.stderr
+    py = subprocess.run([sys.executable, "-m", "cake_amd.cli", *args], capture_output=True,
+                        text=True, timeout=300, env=dict(env, CAKE_NATIVE="0"), cwd=root)
+    assert py.returncode == 0, py.stderr[-3000:]
+    assert nat.stdout.strip() and nat.stdout == py.stdout

@@ -79,6 +79,14 @@ def test_sampling_rules():
     # inside top-k): the top-2 mass here is ~0.93 < 0.95, so both stay in the set
     lp = LogitsProcessor(SamplingConfig(temperature=1.0, top_k=2, top_p=0.95, seed=5))
     assert {lp.sample(logits) for _ in range(200)} == {1, 3}
+    # fixture where the two top-p readings give DIFFERENT sets: probabilities
+    # (0.30, 0.25, 0.20, 0.15, 0.10), top-k 3, top-p 0.6.  candle's sample_topk_topp
+    # (full-vocabulary probabilities of the top k, cutoff while the running sum is below
+    # p): 0 -> 0.30, 1 -> 0.55 < 0.6, so token 2 stays: {0, 1, 2}.  Renormalised inside
+    # top-k (0.40, 0.33, 0.27): 0.73 >= 0.6 after token 1: {0, 1}.
+    fx = torch.log(torch.tensor([0.30, 0.25, 0.20, 0.15, 0.10]))
+    lp = LogitsProcessor(SamplingConfig(temperature=1.0, top_k=3, top_p=0.6, seed=9))
+    assert {lp.sample(fx) for _ in range(400)} == {0, 1, 2}
     a = LogitsProcessor(SamplingConfig(temperature=0.8, seed=7))
     b = LogitsProcessor(SamplingConfig(temperature=0.8, seed=7))
     assert [a.sample(logits) for _ in range(20)] == [b.sample(logits) for _ in range(20)]

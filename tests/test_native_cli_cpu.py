@@ -101,3 +101,28 @@ def test_native_worker_serves_master(ckpt, tmp_path, host):
     finally:
         w.kill()
         w.wait()
+
+
+def test_native_bridge_tokenizer_matches_generator(ckpt):
+    """The tokenizer half of the native text path (cake_amd/native_bridge.py, called by
+    cake-cli through the embedded interpreter): the prompt ids and per-token text equal
+    what the Python generator uses."""
+    import json
+    from cake_amd import native_bridge as B
+    from cake_amd.models.chat import Message
+    from cake_amd.models.llama3.config import LlamaConfig
+    from cake_amd.models.llama3.generator import LLamaGenerator, load_tokenizer
+    r = json.loads(B.encode_chat(json.dumps({"model": str(ckpt), "system": "sys",
+                                             "prompt": "hello there"})))
+    cfg = LlamaConfig.from_path(ckpt)
+    tok, eos = load_tokenizer(ckpt, cfg.eos_token_id)
+    gen = LLamaGenerator.__new__(LLamaGenerator)
+    gen.tokenizer, gen.eos_ids = tok, eos
+    from cake_amd.models.chat import History
+    gen.history = History()
+    gen.add_message(Message.system("sys"))
+    gen.add_message(Message.user("hello there"))
+    ids = tok.encode(gen.history.encode_dialog_to_prompt(), add_special_tokens=False).ids
+    assert r["ids"] == list(ids) and r["eos"] == sorted(eos)
+    for t in (5, 72, 300, 259):
+        assert B.decode_token(json.dumps({"model": str(ckpt), "id": t})) == (gen._decode(t) or "")

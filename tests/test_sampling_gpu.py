@@ -46,6 +46,20 @@ def test_threshold_set(cuda, V, k, p):
     assert torch.equal(got, exp), (int(got.sum()), int(exp.sum()))
 
 
+def test_topk_topp_full_mass_fixture(cuda):
+    """Renormalised and full-mass top-p cutoffs differ on this fixture (see
+    test_model_cpu.test_sampling_rules): the device threshold keeps {0, 1, 2} as candle's
+    sample_topk_topp does, not the renormalised {0, 1}."""
+    from cake_amd.ops import hip as K
+    logits = torch.log(torch.tensor([0.30, 0.25, 0.20, 0.15, 0.10])).to(cuda)
+    thr = torch.zeros(1, dtype=torch.int32, device=cuda)
+    K.sample_threshold(logits, 1.0, 3, 0.6, thr)
+    u = logits.view(torch.int32).cpu().numpy().view("uint32").astype("int64")
+    key = torch.tensor(((u ^ 0x80000000) * ((u >> 31) == 0) + (0xFFFFFFFF - u) * ((u >> 31) == 1)))
+    got = (key >= (int(thr.item()) & 0xFFFFFFFF)).nonzero().flatten().tolist()
+    assert got == [0, 1, 2]
+
+
 @pytest.mark.parametrize("T,k,p", [(1.0, None, None), (0.7, 5, None), (1.3, None, 0.8)])
 def test_gumbel_draw_distribution(cuda, T, k, p):
     """chi^2 of 40k device draws against the renormalised softmax over the kept set."""
