@@ -23,6 +23,7 @@
 
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <chrono>
@@ -40,6 +41,7 @@
 
 #include "../driver/graph_loop.h"
 #include "../runtime/json.h"
+#include "../runtime/net.h"
 #include "../runtime/safetensors.h"
 
 #define CAKE_API extern "C" __attribute__((visibility("default")))
@@ -89,6 +91,13 @@ int cake_gumbel_argmax(const float* logits, int V, float temperature, unsigned l
                        hipStream_t st);
 int cake_finalize_token(unsigned long long* slot, int* tok, int* hist, int* hist_len, int* pos,
                         int max_hist, hipStream_t st);
+int cake_hop_alloc(size_t bytes, void** ptr);
+int cake_hop_free(void* ptr);
+int cake_hop_words(int H, int nhdr, int bf16);
+int cake_hop_send(const float* src, int H, int nhdr, int bf16, void* dst_inbox, unsigned int* seq,
+                  hipStream_t st);
+int cake_hop_recv(const void* inbox, int H, int nhdr, int bf16, float* dst, unsigned int* seq,
+                  int* err, double timeout_s, hipStream_t st);
 }
 
 namespace cake {
@@ -265,37 +274,120 @@ struct GemmPlanner {
 
 constexpr int kEpiStore = 0, kEpiResid32 = 1, kEpiSwiglu = 3;
 
+// Contiguous layer shards, rank 0 lighter by the head's weight in blocks
+// (parallel/pipeline.py shard_layers + head_cost_in_layers).
+std::vector<std::pair<int, int>> shard_layers(const Cfg& c, int world) {
+  std::vector<std::pair<int, int>> out;
+  if (world <= 1) {
+    out.push_back({0, c.L});
+    return out;
+  }
+  const double layer_bytes = 2.0 * ((double)c.H * (c.nh + 2 * c.nkv) * c.hd +
+                                    (double)c.nh * c.hd * c.H + 3.0 * c.H * c.I + 2.0 * c.H);
+  const double head = 2.0 * (double)c.V * c.H / layer_bytes;
+  const double total = c.L + head;
+  int start = 0;
+  for (int r = 0; r < world; ++r) {
+    int end = r < world - 1 ? (int)std::nearbyint((r + 1) * total / world - head) : c.L;
+    end = std::max(start + (c.L - start >= world - r ? 1 : 0), std::min(end, c.L - (world - 1 - r)));
+    out.push_back({start, end});
+    start = end;
+  }
+  return out;
+}
+
+std::string hex_of(const void* p, size_t n) {
+  static const char* d = "0123456789abcdef";
+  std::string s;
+  const uint8_t* b = static_cast<const uint8_t*>(p);
+  for (size_t i = 0; i < n; ++i) {
+    s.push_back(d[b[i] >> 4]);
+    s.push_back(d[b[i] & 15]);
+  }
+  return s;
+}
+
+void unhex(const std::string& s, void* out, size_t n) {
+  if (s.size() != 2 * n) throw Error("bad IPC handle");
+  auto v = [](char c) { return c <= '9' ? c - '0' : c - 'a' + 10; };
+  uint8_t* b = static_cast<uint8_t*>(out);
+  for (size_t i = 0; i < n; ++i) b[i] = (uint8_t)(v(s[2 * i]) << 4 | v(s[2 * i + 1]));
+}
+
+void send_json(int fd, const Json& j) {
+  const std::string t = j.dump();
+  send_frame(fd, reinterpret_cast<const uint8_t*>(t.data()), (uint32_t)t.size());
+}
+Json recv_json(int fd) { return Json::parse(recv_frame(fd)); }
+Json msg(const char* cmd) {
+  Json j = Json::object();
+  j.set("cmd", Json::string(cmd));
+  return j;
+}
+
 // ---------------------------------------------------------------------------
 // the engine
 // ---------------------------------------------------------------------------
 class Llama {
  public:
-  Llama(const std::string& dir, const CakeEngineOpts& o) : dt_(o.dtype), dev_(o.device) {
+  Llama(const std::string& dir, const CakeEngineOpts& o, const CakePipeOpts* pp = nullptr)
+      : dt_(o.dtype), dev_(o.device) {
     if (dt_ != 0 && dt_ != 1) throw Error("dtype must be 0 (bf16) or 1 (f16)");
+    if (pp) {
+      rank_ = pp->rank;
+      world_ = pp->world;
+      hop_bf16_ = pp->hop_bf16 != 0;
+      hop_timeout_ = pp->hop_timeout_s > 0 ? pp->hop_timeout_s : 30.0;
+      if (world_ < 1 || rank_ < 0 || rank_ >= world_) throw Error("bad rank / world");
+    }
     hip_check(hipSetDevice(dev_), "hipSetDevice");
     hip_check(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking), "hipStreamCreate");
     cfg_ = Cfg::parse(Json::parse(read_file(dir + "/config.json")));
     S_ = o.max_seq > 0 ? o.max_seq : 4096;
     k_ = std::max(1, o.steps_per_graph);
     if (cfg_.H % 8 || cfg_.hd % 2 || cfg_.nh % cfg_.nkv) throw Error("unsupported model shape");
+    if (world_ > cfg_.L) throw Error("more pipeline ranks than layers");
+    const auto sh = shard_layers(cfg_, world_);
+    lo_ = sh[rank_].first;
+    hi_ = sh[rank_].second;
+    head_ = rank_ == 0;
     planner_.load(pkg_dir() + "/ops/gemm_tuned.json");
     load_weights(dir);
     alloc_state();
+    if (world_ > 1) connect_pipeline(pp->master_addr ? pp->master_addr : "127.0.0.1:29517",
+                                     pp->connect_timeout_s > 0 ? pp->connect_timeout_s : 600.0);
   }
 
   ~Llama() {
     (void)hipSetDevice(dev_);
     (void)hipStreamSynchronize(st_);
+    if (rank_ == 0)
+      for (int fd : peers_) {
+        try {
+          send_json(fd, msg("exit"));
+        } catch (const std::exception&) {
+        }
+      }
+    for (int fd : peers_) tcp_close(fd);
+    if (ctl_fd_ >= 0) tcp_close(ctl_fd_);
     drop_graphs();
+    if (next_inbox_) (void)hipIpcCloseMemHandle(next_inbox_);
+    if (next_pbuf_) (void)hipIpcCloseMemHandle(next_pbuf_);
+    if (inbox_) (void)cake_hop_free(inbox_);
     for (void* p : allocs_) (void)hipFree(p);
     (void)hipStreamDestroy(st_);
   }
+
+  int rank() const { return rank_; }
+  int world() const { return world_; }
+  std::pair<int, int> layer_range() const { return {lo_, hi_}; }
 
   const Cfg& cfg() const { return cfg_; }
   int max_seq() const { return S_; }
 
   void prefill_logits(const int32_t* prompt, int T, float* host_logits) {
     hip_check(hipSetDevice(dev_), "hipSetDevice");
+    if (!head_) throw Error("prefill_logits() runs on pipeline rank 0");
     prefill(prompt, T);
     hip_check(hipMemcpyAsync(host_logits, logits_, sizeof(float) * cfg_.V, hipMemcpyDeviceToHost,
                              st_), "logits D2H");
@@ -306,6 +398,7 @@ class Llama {
                 const int32_t* eos, int n_eos, cake_engine_token_cb cb, void* ctx, int32_t* out,
                 int out_cap, CakeEngineStats* stats) {
     hip_check(hipSetDevice(dev_), "hipSetDevice");
+    if (!head_) throw Error("generate() runs on pipeline rank 0");
     if (T <= 0) throw Error("empty prompt");
     if (max_new <= 0) return;
     if (T + max_new + k_ + 1 > S_) throw Error("prompt + max_new exceeds max_seq");
@@ -351,6 +444,12 @@ class Llama {
       spec.pos = T;       // device position after the first token
       spec.n = n;
       spec.chunk = 0;
+      AnnounceCtx actx{this, T};
+      if (world_ > 1) {  // the workers enqueue each chunk of replays when told
+        spec.chunk = kAnnounceChunk;
+        spec.announce = &Llama::announce_cb;
+        spec.announce_ctx = &actx;
+      }
       spec.eos = eos;
       spec.n_eos = n_eos;
       spec.on_token = cb;
@@ -360,7 +459,9 @@ class Llama {
       spec.out_ms = ms.data();
       spec.out_cap = n;
       CakeLoopResult res{};
-      k_check(cake_graph_decode(&spec, &res), "graph_decode");
+      const int rc = cake_graph_decode(&spec, &res);
+      if (world_ > 1) sync_workers();
+      k_check(rc, "graph_decode");
       for (int i = 0; i < res.n_tokens && n_out < out_cap; ++i) out[n_out++] = toks[i];
       ms.resize(res.n_tokens);
     }
@@ -399,6 +500,14 @@ class Llama {
   };
 
   int dt_, dev_;
+  int rank_ = 0, world_ = 1, lo_ = 0, hi_ = 0;
+  bool head_ = true, hop_bf16_ = false;
+  double hop_timeout_ = 30.0;
+  void *inbox_ = nullptr, *next_inbox_ = nullptr, *next_pbuf_ = nullptr;
+  unsigned int* seq_ = nullptr;
+  int* hop_err_ = nullptr;
+  std::vector<int> peers_;  // rank 0: control sockets of ranks 1..world-1
+  int ctl_fd_ = -1;         // workers: control socket to rank 0
   hipStream_t st_ = nullptr;
   Cfg cfg_;
   int S_ = 0, k_ = 1;
@@ -483,20 +592,22 @@ class Llama {
     void* stage = nullptr;
     size_t stage_bytes = 0;
     try {
-      embed_ = dalloc<uint16_t>(V * H);
-      upload(ck, "model.embed_tokens.weight", embed_, V * H, stage, stage_bytes);
-      norm_ = dalloc<uint16_t>(H);
-      upload(ck, "model.norm.weight", norm_, H, stage, stage_bytes);
-      if (ck.has("lm_head.weight") && !c.tie) {
-        lm_head_ = dalloc<uint16_t>(V * H);
-        upload(ck, "lm_head.weight", lm_head_, V * H, stage, stage_bytes);
-      } else {
-        lm_head_ = embed_;  // tied embeddings
+      if (head_) {
+        embed_ = dalloc<uint16_t>(V * H);
+        upload(ck, "model.embed_tokens.weight", embed_, V * H, stage, stage_bytes);
+        norm_ = dalloc<uint16_t>(H);
+        upload(ck, "model.norm.weight", norm_, H, stage, stage_bytes);
+        if (ck.has("lm_head.weight") && !c.tie) {
+          lm_head_ = dalloc<uint16_t>(V * H);
+          upload(ck, "lm_head.weight", lm_head_, V * H, stage, stage_bytes);
+        } else {
+          lm_head_ = embed_;  // tied embeddings
+        }
       }
-      layers_.resize(c.L);
-      for (int l = 0; l < c.L; ++l) {
+      layers_.resize(hi_ - lo_);
+      for (int l = lo_; l < hi_; ++l) {
         const std::string p = "model.layers." + std::to_string(l) + ".";
-        LayerW& w = layers_[l];
+        LayerW& w = layers_[l - lo_];
         w.ln1 = dalloc<uint16_t>(H);
         upload(ck, p + "input_layernorm.weight", w.ln1, H, stage, stage_bytes);
         w.wqkv = dalloc<uint16_t>((nq + 2 * nk) * H);
@@ -524,7 +635,7 @@ class Llama {
 
   void alloc_state() {
     const Cfg& c = cfg_;
-    const size_t kv = (size_t)c.L * c.nkv * S_ * c.hd;
+    const size_t kv = (size_t)(hi_ - lo_) * c.nkv * S_ * c.hd;
     kc_ = dalloc<uint16_t>(kv);
     vc_ = dalloc<uint16_t>(kv);
     const std::vector<float> f = c.inv_freq();
@@ -532,7 +643,9 @@ class Llama {
     hip_check(hipMemcpy(inv_freq_, f.data(), f.size() * sizeof(float), hipMemcpyHostToDevice),
               "inv_freq");
     const size_t nq = (size_t)c.nh * c.hd;
-    resid_ = dalloc<float>(c.H);
+    // [H f32 | pos | pad]: a pipeline hop carries the position as its header word
+    resid_ = dalloc<float>(c.H + 4);
+    hidden_ = dalloc<float>((size_t)S_ * c.H);  // prefill hidden (peer-written in a pipeline)
     q_ = dalloc<float>(nq);
     part_ = dalloc<float>(2 * (size_t)c.nh * kAttnMaxSplit * (c.hd + 2));
     logits_ = dalloc<float>(c.V);
@@ -541,7 +654,7 @@ class Llama {
     tickets_ = dalloc<unsigned int>(2 * c.nkv + 2);
     thr_ = dalloc<unsigned int>(1);
     sel_ticket_ = dalloc<unsigned int>(1);
-    pos_ = dalloc<int>(1);
+    pos_ = reinterpret_cast<int*>(resid_ + c.H);
     tok_ = dalloc<int>(1);
     hist_ = dalloc<int>(S_);
     hist_len_ = dalloc<int>(1);
@@ -555,6 +668,11 @@ class Llama {
     hip_check(hipMemset(slot_, 0, sizeof(unsigned long long)), "memset");
     hip_check(hipMemset(zeros_, 0, sizeof(int32_t) * 64), "memset");
     hip_check(hipMemset(hist_, 0, sizeof(int) * S_), "memset");
+    hip_check(hipMemset(resid_, 0, sizeof(float) * (c.H + 4)), "memset");
+    seq_ = dalloc<unsigned int>(4);  // [0] send sequence, [1] receive sequence
+    hop_err_ = dalloc<int>(4);
+    hip_check(hipMemset(seq_, 0, sizeof(unsigned int) * 4), "memset");
+    hip_check(hipMemset(hop_err_, 0, sizeof(int) * 4), "memset");
     hip_check(hipDeviceSynchronize(), "sync");  // null-stream memsets before st_ work
   }
 
@@ -566,9 +684,8 @@ class Llama {
   void grow_prefill(int T) {
     if (T <= pre_T_) return;
     const Cfg& c = cfg_;
-    for (void* p : {(void*)hidden_, x16_, qkv_, att_, pact_, (void*)ptok_}) dfree(p);
+    for (void* p : {x16_, qkv_, att_, pact_, (void*)ptok_}) dfree(p);
     const size_t nq = (size_t)c.nh * c.hd, nk = (size_t)c.nkv * c.hd;
-    hidden_ = dalloc<float>((size_t)T * c.H);
     x16_ = dalloc<uint16_t>((size_t)T * c.H);
     qkv_ = dalloc<uint16_t>((size_t)T * (nq + 2 * nk));
     att_ = dalloc<uint16_t>((size_t)T * nq);
@@ -598,16 +715,51 @@ class Llama {
                       ws, zeros_, M, N, K, st_), what);
   }
 
+  // embed -> this rank's layers -> (pipeline: the other ranks' layers, hidden rows
+  // handed rank to rank through the peers' IPC-mapped prefill buffers) -> head
   void prefill(const int32_t* prompt, int T) {
     const Cfg& c = cfg_;
     if (T > S_) throw Error("prompt longer than max_seq");
-    grow_prefill(T);
-    const int nq = c.nh * c.hd, nk = c.nkv * c.hd, nqkv = nq + 2 * nk;
-    hip_check(hipMemcpyAsync(ptok_, prompt, sizeof(int32_t) * T, hipMemcpyHostToDevice, st_),
+    hip_check(hipMemcpyAsync(ptok_buf(T), prompt, sizeof(int32_t) * T, hipMemcpyHostToDevice, st_),
               "prompt H2D");
     k_check(cake_embed(dt_, embed_, ptok_, T, c.H, hidden_, st_), "embed");
+    prefill_layers(T);
+    if (world_ > 1) {
+      forward_hidden(T);
+      for (int r = 1; r < world_; ++r) {  // relay: rank r runs, then hands to r + 1
+        Json m = msg("prefill");
+        m.set("T", Json::integer(T));
+        send_json(peers_[r - 1], m);
+        const Json ack = recv_json(peers_[r - 1]);
+        if (!ack.has("ok") || !ack.get("ok").as_bool())
+          throw Error("pipeline rank " + std::to_string(r) + " prefill failed: " +
+                      (ack.has("error") ? ack.get("error").as_string() : std::string("?")));
+      }
+      // the last rank wrote its output rows into this rank's hidden_
+    }
+    k_check(cake_gemv_norm_f32(dt_, hidden_ + (size_t)(T - 1) * c.H, norm_, (float)c.eps,
+                               lm_head_, c.H, c.V, logits_, st_), "lm_head");
+  }
+
+  int32_t* ptok_buf(int T) {
+    grow_prefill(T);
+    return ptok_;
+  }
+
+  // hidden_ rows [0, T) -> the next rank's prefill buffer (device to device over the
+  // IPC mapping), complete before the control message that announces them
+  void forward_hidden(int T) {
+    hip_check(hipMemcpyAsync(next_pbuf_, hidden_, sizeof(float) * (size_t)T * cfg_.H,
+                             hipMemcpyDeviceToDevice, st_), "prefill hop");
+    hip_check(hipStreamSynchronize(st_), "sync");
+  }
+
+  void prefill_layers(int T) {
+    const Cfg& c = cfg_;
+    grow_prefill(T);
+    const int nq = c.nh * c.hd, nk = c.nkv * c.hd, nqkv = nq + 2 * nk;
     const int pos0 = 0, Tk = T;
-    for (int l = 0; l < c.L; ++l) {
+    for (int l = 0; l < hi_ - lo_; ++l) {
       const LayerW& w = layers_[l];
       k_check(cake_rmsnorm(dt_, hidden_, w.ln1, (float)c.eps, T, c.H, x16_, st_), "rmsnorm");
       gemm(kEpiStore, x16_, c.H, w.wqkv, c.H, qkv_, nqkv, nullptr, 0, T, nqkv, c.H, "gemm qkv");
@@ -627,8 +779,6 @@ class Llama {
       gemm(kEpiSwiglu, x16_, c.H, w.wgu, c.H, pact_, c.I, nullptr, 0, T, c.I, c.H, "gemm gate|up");
       gemm(kEpiResid32, pact_, c.I, w.wd, c.I, nullptr, 0, hidden_, c.H, T, c.H, c.I, "gemm down");
     }
-    k_check(cake_gemv_norm_f32(dt_, hidden_ + (size_t)(T - 1) * c.H, norm_, (float)c.eps,
-                               lm_head_, c.H, c.V, logits_, st_), "lm_head");
   }
 
   // ---- token selection / decode step
@@ -664,11 +814,37 @@ class Llama {
     k_check(cake_finalize_token(slot_, tok_, hist_, hist_len_, pos_, S_, st_), "finalize");
   }
 
+  // one decode step of this rank: [embed] layers [send, receive] head  (rank 0), or
+  // receive, layers, send (pipeline workers); the hop carries [hidden | position]
   void step_body(const Mode& m) {
     const Cfg& c = cfg_;
-    const int nq = c.nh * c.hd, nk = c.nkv * c.hd;
+    if (!head_) {
+      hop_recv();
+      step_layers();
+      hop_send();
+      return;
+    }
     if (!m.fused) k_check(cake_embed(dt_, embed_, tok_, 1, c.H, resid_, st_), "embed");
-    for (int l = 0; l < c.L; ++l) {
+    step_layers();
+    if (world_ > 1) {
+      hop_send();
+      hop_recv();
+    }
+    step_head(m);
+  }
+
+  void hop_send() {
+    k_check(cake_hop_send(resid_, cfg_.H, 1, hop_bf16_ ? 1 : 0, next_inbox_, seq_, st_), "hop_send");
+  }
+  void hop_recv() {
+    k_check(cake_hop_recv(inbox_, cfg_.H, 1, hop_bf16_ ? 1 : 0, resid_, seq_ + 1, hop_err_,
+                          hop_timeout_, st_), "hop_recv");
+  }
+
+  void step_layers() {
+    const Cfg& c = cfg_;
+    const int nq = c.nh * c.hd, nk = c.nkv * c.hd;
+    for (int l = 0; l < hi_ - lo_; ++l) {
       const LayerW& w = layers_[l];
       const uint16_t* wqkv = reinterpret_cast<const uint16_t*>(w.wqkv);
       k_check(cake_qkv_rope(dt_, resid_, w.ln1, (float)c.eps, wqkv, wqkv + (size_t)nq * c.H,
@@ -682,6 +858,10 @@ class Llama {
                           c.I, act_, st_), "swiglu");
       k_check(cake_gemv_x16(dt_, act_, w.wd, c.I, c.H, resid_, 1, st_), "down_proj");
     }
+  }
+
+  void step_head(const Mode& m) {
+    const Cfg& c = cfg_;
     if (m.fused) {
       k_check(cake_head_select(dt_, resid_, norm_, (float)c.eps, lm_head_, c.H, c.V, logits_,
                                hist_, hist_len_, m.penalty != 1.f ? m.last_n : 0, m.penalty,
@@ -692,6 +872,161 @@ class Llama {
     k_check(cake_gemv_norm_f32(dt_, resid_, norm_, (float)c.eps, lm_head_, c.H, c.V, logits_, st_),
             "lm_head");
     select_tail(m);
+  }
+
+  // ---- pipeline (one process per GPU, layer shards, device-side hops)
+  static constexpr int kAnnounceChunk = 8;  // replays per worker announcement
+  struct AnnounceCtx {
+    Llama* self;
+    int pos0;  // device position before the first replay of this run
+  };
+  static int32_t announce_cb(void* vctx, int32_t first, int32_t count) {
+    auto* a = static_cast<AnnounceCtx*>(vctx);
+    try {
+      Json m = msg("replays");
+      m.set("count", Json::integer(count));
+      m.set("pos", Json::integer(a->pos0 + (int64_t)first * a->self->k_));
+      for (int fd : a->self->peers_) send_json(fd, m);
+      return 0;
+    } catch (const std::exception&) {
+      return 1;
+    }
+  }
+
+  // every worker drained its stream; any hop that gave up waiting is an error
+  void sync_workers() {
+    std::string err;
+    for (size_t i = 0; i < peers_.size(); ++i) {
+      try {
+        send_json(peers_[i], msg("sync"));
+        const Json r = recv_json(peers_[i]);
+        if (r.has("hop_err") && r.get("hop_err").as_int() != 0)
+          err = "pipeline rank " + std::to_string(i + 1) + ": hop receive timed out";
+      } catch (const std::exception& e) {
+        err = e.what();
+      }
+    }
+    int own = 0;
+    hip_check(hipMemcpy(&own, hop_err_, sizeof(int), hipMemcpyDeviceToHost), "hop_err");
+    if (own) err = "pipeline rank 0: hop receive timed out";
+    if (!err.empty()) throw Error(err);
+  }
+
+ public:
+  // worker rank: serve the master's control messages until it says exit
+  void serve() {
+    hip_check(hipSetDevice(dev_), "hipSetDevice");
+    if (head_) throw Error("serve() runs on pipeline workers (rank > 0)");
+    ensure_graphs(Mode{});
+    std::vector<void*> execs(execs_.begin(), execs_.end());
+    for (;;) {
+      const Json m = recv_json(ctl_fd_);
+      const std::string cmd = m.get("cmd").as_string();
+      if (cmd == "exit") break;
+      if (cmd == "prefill") {
+        Json r = Json::object();
+        try {
+          const int T = (int)m.get("T").as_int();
+          if (T < 1 || T > S_) throw Error("bad prefill length");
+          prefill_layers(T);
+          forward_hidden(T);
+          r.set("ok", Json::boolean(true));
+        } catch (const std::exception& e) {
+          r.set("ok", Json::boolean(false));
+          r.set("error", Json::string(e.what()));
+        }
+        send_json(ctl_fd_, r);
+      } else if (cmd == "replays") {
+        CakeLoopSpec spec{};
+        spec.execs = execs.data();
+        spec.n_execs = (int32_t)execs.size();
+        spec.bucket_of = bucket_of_.data();
+        spec.n_len = (int32_t)bucket_of_.size();
+        spec.k = k_;
+        spec.pos = (int32_t)m.get("pos").as_int();
+        spec.n = (int32_t)m.get("count").as_int() * k_;
+        spec.stream = st_;
+        CakeLoopResult res{};
+        k_check(cake_graph_decode(&spec, &res), "graph_decode");  // enqueue only
+      } else if (cmd == "sync") {
+        Json r = Json::object();
+        const hipError_t e = hipStreamSynchronize(st_);
+        int herr = 0;
+        (void)hipMemcpy(&herr, hop_err_, sizeof(int), hipMemcpyDeviceToHost);
+        if (herr) (void)hipMemset(hop_err_, 0, sizeof(int));
+        r.set("ok", Json::boolean(e == hipSuccess));
+        r.set("hop_err", Json::integer(herr));
+        send_json(ctl_fd_, r);
+      } else {
+        throw Error("unknown control message " + cmd);
+      }
+    }
+  }
+
+ private:
+  // inboxes (uncached device memory, device-side hops) and prefill buffers exchanged as
+  // IPC handles over the TCP control plane; ring: rank r sends to (r + 1) % world
+  void connect_pipeline(const std::string& addr, double timeout_s) {
+    std::string host;
+    int port = 0;
+    split_host_port(addr, &host, &port);
+    const int words = cake_hop_words(cfg_.H, 1, hop_bf16_ ? 1 : 0);
+    k_check(cake_hop_alloc((size_t)words * 8, &inbox_), "hop_alloc");
+    hipIpcMemHandle_t hi, hp;
+    hip_check(hipIpcGetMemHandle(&hi, inbox_), "IpcGetMemHandle");
+    hip_check(hipIpcGetMemHandle(&hp, hidden_), "IpcGetMemHandle");
+    auto entry = [&](int r, const std::string& a, const std::string& b) {
+      Json j = Json::object();
+      j.set("rank", Json::integer(r));
+      j.set("inbox", Json::string(a));
+      j.set("pbuf", Json::string(b));
+      return j;
+    };
+    Json peer_next;
+    if (rank_ == 0) {
+      const int lfd = tcp_listen(host, port);
+      std::vector<Json> hs(world_);
+      hs[0] = entry(0, hex_of(&hi, sizeof(hi)), hex_of(&hp, sizeof(hp)));
+      peers_.assign(world_ - 1, -1);
+      try {
+        for (int i = 1; i < world_; ++i) {
+          std::string peer;
+          const int fd = tcp_accept(lfd, &peer);
+          tcp_set_timeout(fd, 0);
+          const Json j = recv_json(fd);
+          const int r = (int)j.get("rank").as_int();
+          if (r < 1 || r >= world_ || peers_[r - 1] >= 0) throw Error("bad pipeline rank hello");
+          peers_[r - 1] = fd;
+          hs[r] = j;
+        }
+      } catch (...) {
+        tcp_close(lfd);
+        throw;
+      }
+      tcp_close(lfd);
+      for (int r = 1; r < world_; ++r) send_json(peers_[r - 1], hs[(r + 1) % world_]);
+      peer_next = hs[1];
+    } else {
+      const auto deadline =
+          std::chrono::steady_clock::now() + std::chrono::duration<double>(timeout_s);
+      for (;;) {
+        try {
+          ctl_fd_ = tcp_connect(host, port, 2.0);
+          break;
+        } catch (const std::exception&) {
+          if (std::chrono::steady_clock::now() > deadline) throw;
+          usleep(200000);
+        }
+      }
+      tcp_set_timeout(ctl_fd_, 0);
+      send_json(ctl_fd_, entry(rank_, hex_of(&hi, sizeof(hi)), hex_of(&hp, sizeof(hp))));
+      peer_next = recv_json(ctl_fd_);
+    }
+    hipIpcMemHandle_t ni, np;
+    unhex(peer_next.get("inbox").as_string(), &ni, sizeof(ni));
+    unhex(peer_next.get("pbuf").as_string(), &np, sizeof(np));
+    hip_check(hipIpcOpenMemHandle(&next_inbox_, ni, hipIpcMemLazyEnablePeerAccess), "IpcOpen inbox");
+    hip_check(hipIpcOpenMemHandle(&next_pbuf_, np, hipIpcMemLazyEnablePeerAccess), "IpcOpen pbuf");
   }
 
   void drop_graphs() {
@@ -706,8 +1041,19 @@ class Llama {
   void ensure_graphs(const Mode& m) {
     if (have_graphs_ && graph_mode_ == m) return;
     drop_graphs();
-    // warm every kernel once outside capture on the live state, then restore it (the
-    // K/V row this writes is the next step's, which that step rewrites)
+    if (!head_) {  // pipeline worker: its layers once, eagerly, at position 0 (the row is
+                   // rewritten by every prefill), so no kernel's first launch is captured
+      hip_check(hipMemsetAsync(resid_, 0, sizeof(float) * (cfg_.H + 1), st_), "memset");
+      step_layers();
+      hip_check(hipStreamSynchronize(st_), "sync");
+    }
+    if (world_ == 1) warm_step(m);
+    capture_buckets(m);
+  }
+
+  // warm every kernel once outside capture on the live state, then restore it (the
+  // K/V row this writes is the next step's, which that step rewrites)
+  void warm_step(const Mode& m) {
     hip_check(hipMemcpyAsync(scratch_i32_, tok_, sizeof(int), hipMemcpyDeviceToDevice, st_), "snap");
     hip_check(hipMemcpyAsync(scratch_i32_ + 1, pos_, sizeof(int), hipMemcpyDeviceToDevice, st_), "snap");
     hip_check(hipMemcpyAsync(scratch_i32_ + 2, hist_len_, sizeof(int), hipMemcpyDeviceToDevice, st_), "snap");
@@ -719,6 +1065,9 @@ class Llama {
     hip_check(hipMemcpyAsync(resid_, scratch_resid_, sizeof(float) * cfg_.H, hipMemcpyDeviceToDevice, st_), "restore");
     hip_check(hipMemsetAsync(slot_, 0, sizeof(unsigned long long), st_), "slot");
     hip_check(hipStreamSynchronize(st_), "sync");
+  }
+
+  void capture_buckets(const Mode& m) {
     // caps: 8 / 16 / 32 / 64 (clamped to the max_seq grid) up to the first covering
     // every live length (ops.hip.attn_split_caps)
     const int full = cake_attn_max_split(S_);
@@ -786,6 +1135,39 @@ CAKE_API void* cake_engine_open(const char* model_dir, const CakeEngineOpts* opt
     cake::put_err(err, errlen, e.what());
     return nullptr;
   }
+}
+
+CAKE_API void* cake_engine_open_pp(const char* model_dir, const CakeEngineOpts* opts,
+                                   const CakePipeOpts* pipe, char* err, int32_t errlen) {
+  try {
+    if (!model_dir || !opts || !pipe) throw cake::Error("null argument");
+    return new Llama(model_dir, *opts, pipe);
+  } catch (const std::exception& e) {
+    cake::put_err(err, errlen, e.what());
+    return nullptr;
+  }
+}
+
+CAKE_API int32_t cake_engine_serve(void* h, char* err, int32_t errlen) {
+  try {
+    if (!h) throw cake::Error("null engine");
+    static_cast<Llama*>(h)->serve();
+    return 0;
+  } catch (const std::exception& e) {
+    cake::put_err(err, errlen, e.what());
+    return 1;
+  }
+}
+
+CAKE_API int32_t cake_engine_rank_info(void* h, int32_t* o) {
+  if (!h || !o) return (int32_t)hipErrorInvalidValue;
+  const Llama* m = static_cast<Llama*>(h);
+  const auto lr = m->layer_range();
+  o[0] = m->rank();
+  o[1] = m->world();
+  o[2] = lr.first;
+  o[3] = lr.second;
+  return 0;
 }
 
 CAKE_API int32_t cake_engine_info(void* h, int32_t* o) {

@@ -22,6 +22,19 @@ struct CakeEngineOpts {
   int32_t steps_per_graph;  // decode steps per graph replay (greedy only; >= 1)
 };
 
+// Layer-sharded pipeline over one process per GPU: rank r runs a contiguous layer
+// shard (rank 0 also the embedding and the head); each decode step's hidden state moves
+// rank to rank by device-side hops (hop.hip, IPC-mapped inboxes: no host in the step),
+// prefill rows through IPC-mapped buffers; the control plane (IPC handles, prefill
+// relay, replay announcements) is TCP to rank 0 at master_addr.
+struct CakePipeOpts {
+  int32_t rank, world;
+  const char* master_addr;   // "host:port" rank 0 listens on
+  int32_t hop_bf16;          // 1: bf16 hop payload (half the bytes)
+  double hop_timeout_s;      // a hop receive that waits longer sets the error word
+  double connect_timeout_s;  // workers: how long to retry reaching rank 0
+};
+
 struct CakeEngineSampling {
   float temperature;        // <= 0: greedy
   int32_t top_k;            // 0: off
@@ -43,6 +56,13 @@ struct CakeEngineStats {
 // config.json + safetensors of `model_dir`; null on failure (message in err).
 void* cake_engine_open(const char* model_dir, const struct CakeEngineOpts* opts, char* err,
                        int32_t errlen);
+// Pipeline rank (see CakePipeOpts): loads only its layer shard, joins the ring.
+void* cake_engine_open_pp(const char* model_dir, const struct CakeEngineOpts* opts,
+                          const struct CakePipeOpts* pipe, char* err, int32_t errlen);
+// Workers (rank > 0): serve rank 0's control messages until it closes; 0 or an error.
+int32_t cake_engine_serve(void* engine, char* err, int32_t errlen);
+// [rank, world, first layer, end layer]
+int32_t cake_engine_rank_info(void* engine, int32_t* out4);
 // [V, H, L, nh, nkv, hd, I, max_seq]
 int32_t cake_engine_info(void* engine, int32_t* out8);
 // EOS ids of the config (up to cap); returns the count

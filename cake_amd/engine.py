@@ -26,6 +26,12 @@ class EngineOpts(C.Structure):
                 ("steps_per_graph", C.c_int32)]
 
 
+class PipeOpts(C.Structure):
+    _fields_ = [("rank", C.c_int32), ("world", C.c_int32), ("master_addr", C.c_char_p),
+                ("hop_bf16", C.c_int32), ("hop_timeout_s", C.c_double),
+                ("connect_timeout_s", C.c_double)]
+
+
 class EngineSampling(C.Structure):
     _fields_ = [("temperature", C.c_float), ("top_k", C.c_int32), ("top_p", C.c_float),
                 ("seed", C.c_uint64), ("repeat_penalty", C.c_float),
@@ -50,6 +56,13 @@ def lib() -> C.CDLL:
         P, I = C.c_void_p, C.c_int32
         L.cake_engine_open.argtypes = [C.c_char_p, C.POINTER(EngineOpts), C.c_char_p, I]
         L.cake_engine_open.restype = P
+        L.cake_engine_open_pp.argtypes = [C.c_char_p, C.POINTER(EngineOpts), C.POINTER(PipeOpts),
+                                          C.c_char_p, I]
+        L.cake_engine_open_pp.restype = P
+        L.cake_engine_serve.argtypes = [P, C.c_char_p, I]
+        L.cake_engine_serve.restype = I
+        L.cake_engine_rank_info.argtypes = [P, C.POINTER(C.c_int32)]
+        L.cake_engine_rank_info.restype = I
         L.cake_engine_info.argtypes = [P, C.POINTER(C.c_int32)]
         L.cake_engine_info.restype = I
         L.cake_engine_eos.argtypes = [P, C.POINTER(C.c_int32), I]
@@ -83,15 +96,30 @@ class NativeLlama:
     """One model loaded by the native engine on one GPU."""
 
     def __init__(self, model_dir: str | Path, *, max_seq: int = 4096, dtype: str = "bf16",
-                 device: int = 0, steps_per_graph: int = 1):
+                 device: int = 0, steps_per_graph: int = 1, rank: int = 0, world: int = 1,
+                 master_addr: str = "127.0.0.1:29517", hop_bf16: bool = False,
+                 hop_timeout_s: float = 30.0, connect_timeout_s: float = 600.0):
+        """world > 1: one layer-sharded pipeline rank (rank 0 generates; the others call
+        :meth:`serve`).  Every rank of one pipeline must be constructed concurrently."""
         if dtype not in ("bf16", "f16"):
             raise ValueError("native engine dtype: bf16 or f16")
         opts = EngineOpts(int(max_seq), 0 if dtype == "bf16" else 1, int(device),
                           max(1, int(steps_per_graph)))
         err = C.create_string_buffer(1024)
-        self._h = lib().cake_engine_open(str(model_dir).encode(), C.byref(opts), err, len(err))
+        self._h = None
+        if world > 1:
+            self._addr = master_addr.encode()
+            pipe = PipeOpts(int(rank), int(world), self._addr, int(bool(hop_bf16)),
+                            float(hop_timeout_s), float(connect_timeout_s))
+            self._h = lib().cake_engine_open_pp(str(model_dir).encode(), C.byref(opts),
+                                                C.byref(pipe), err, len(err))
+        else:
+            self._h = lib().cake_engine_open(str(model_dir).encode(), C.byref(opts), err, len(err))
         if not self._h:
             raise RuntimeError(f"native engine: {err.value.decode(errors='replace')}")
+        ri = (C.c_int32 * 4)()
+        lib().cake_engine_rank_info(self._h, ri)
+        self.rank, self.world, self.first_layer, self.end_layer = list(ri)
         info = (C.c_int32 * 8)()
         lib().cake_engine_info(self._h, info)
         (self.vocab_size, self.hidden_size, self.num_layers, self.num_heads, self.num_kv_heads,
@@ -99,6 +127,13 @@ class NativeLlama:
         eos = (C.c_int32 * 16)()
         n = lib().cake_engine_eos(self._h, eos, 16)
         self.eos_ids = [int(eos[i]) for i in range(min(n, 16))]
+
+    def serve(self) -> None:
+        """Pipeline worker: run rank 0's prefill relays and replay announcements until it
+        closes the pipeline."""
+        err = C.create_string_buffer(1024)
+        if lib().cake_engine_serve(self._h, err, len(err)):
+            raise RuntimeError(f"native engine: {err.value.decode(errors='replace')}")
 
     def close(self) -> None:
         if getattr(self, "_h", None):

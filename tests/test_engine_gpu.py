@@ -110,3 +110,54 @@ def test_cake_cli_native_text_matches_python_cli(cuda, ckpt, tmp_path):
                         text=True, timeout=300, env=dict(env, CAKE_NATIVE="0"), cwd=root)
     assert py.returncode == 0, py.stderr[-3000:]
     assert nat.stdout.strip() and nat.stdout == py.stdout
+
+
+def test_native_pipeline_two_ranks_share_one_gpu(cuda, ckpt):
+    """Layer-sharded native pipeline: rank 1 is another process on the same GPU (device
+    hops through IPC-mapped inboxes, prefill rows through IPC-mapped buffers, TCP control
+    plane).  f32 hops are exact, so tokens equal the single-rank engine — greedy, sampled,
+    an EOS stop in the middle of an announced chunk, and a generation after it."""
+    import os
+    import socket
+    import subprocess
+    import sys
+    from cake_amd.engine import NativeLlama
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    addr = f"127.0.0.1:{port}"
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "from cake_amd.engine import NativeLlama\n"
+            "e = NativeLlama(%r, max_seq=256, dtype='bf16', rank=1, world=2, master_addr=%r)\n"
+            "print('layers', e.first_layer, e.end_layer, flush=True)\n"
+            "e.serve()\n"
+            "e.close()\n") % (root, str(ckpt), addr)
+    worker = subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.PIPE,
+                              stderr=subprocess.PIPE, text=True)
+    try:
+        prompt = [1, 17, 300, 5, 99, 1024, 7, 8]
+        single = NativeLlama(ckpt, max_seq=256, dtype="bf16")
+        ref = single.generate(prompt, 30, repeat_penalty=1.1, repeat_last_n=16).tokens
+        ref_s = single.generate(prompt, 30, temperature=0.7, top_k=40, seed=11,
+                                repeat_penalty=1.1, repeat_last_n=16).tokens
+        single.close()
+        eng = NativeLlama(ckpt, max_seq=256, dtype="bf16", rank=0, world=2, master_addr=addr)
+        assert (eng.rank, eng.world, eng.first_layer) == (0, 2, 0) and eng.end_layer < 3
+        assert eng.generate(prompt, 30, repeat_penalty=1.1, repeat_last_n=16).tokens == ref
+        got = eng.generate(prompt, 30, temperature=0.7, top_k=40, seed=11,
+                           repeat_penalty=1.1, repeat_last_n=16).tokens
+        assert got == ref_s
+        stop = ref[12]
+        got = eng.generate(prompt, 30, repeat_penalty=1.1, repeat_last_n=16, eos_ids=[stop])
+        assert got.tokens == ref[:ref.index(stop) + 1]
+        assert eng.generate(prompt, 30, repeat_penalty=1.1, repeat_last_n=16).tokens == ref
+        eng.close()
+        out, err = worker.communicate(timeout=60)
+        assert worker.returncode == 0, err[-3000:]
+        assert out.startswith("layers")
+    finally:
+        if worker.poll() is None:
+            worker.kill()
+            worker.wait()
