@@ -339,6 +339,11 @@ class Llama {
       hop_bf16_ = pp->hop_bf16 != 0;
       hop_timeout_ = pp->hop_timeout_s > 0 ? pp->hop_timeout_s : 30.0;
       if (world_ < 1 || rank_ < 0 || rank_ >= world_) throw Error("bad rank / world");
+      // one process per GPU; more ranks than GPUs share them round-robin (rehearsals on
+      // a one-GPU box, as parallel/pipeline_bench.py DistEnv)
+      int n = 0;
+      hip_check(hipGetDeviceCount(&n), "hipGetDeviceCount");
+      if (n > 0) dev_ %= n;
     }
     hip_check(hipSetDevice(dev_), "hipSetDevice");
     hip_check(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking), "hipStreamCreate");

@@ -149,6 +149,8 @@ bool in_choices(const std::string& v, const char* choices) {
 // ---------------------------------------------------------------------------
 struct EngineApi {
   void* (*open)(const char*, const CakeEngineOpts*, char*, int32_t);
+  void* (*open_pp)(const char*, const CakeEngineOpts*, const CakePipeOpts*, char*, int32_t);
+  int32_t (*serve)(void*, char*, int32_t);
   int32_t (*generate)(void*, const int32_t*, int32_t, int32_t, const CakeEngineSampling*,
                       const int32_t*, int32_t, cake_engine_token_cb, void*, int32_t*, int32_t,
                       CakeEngineStats*, char*, int32_t);
@@ -159,10 +161,18 @@ bool native_text_eligible(cake::PyArgs& o, bool text, bool worker, bool has_topo
   const char* env = std::getenv("CAKE_NATIVE");
   if (env && std::string(env) == "0") return false;
   const auto is = [&](const char* k, const char* v) { return o[k].value == v; };
-  return text && !worker && !has_topology && o["api"].kind == PyArg::kNone &&
-         !is("cpu", "1") && is("transport", "tcp") && !is("no_graph", "1") &&
-         o["trace"].kind == PyArg::kNone && o["metrics"].kind == PyArg::kNone &&
-         (o["dtype"].kind == PyArg::kNone || is("dtype", "f16") || is("dtype", "bf16"));
+  const bool common = text && o["api"].kind == PyArg::kNone && !is("cpu", "1") &&
+                      !is("no_graph", "1") && o["trace"].kind == PyArg::kNone &&
+                      o["metrics"].kind == PyArg::kNone &&
+                      (o["dtype"].kind == PyArg::kNone || is("dtype", "f16") || is("dtype", "bf16"));
+  if (is("transport", "rccl"))  // one process per GPU (torchrun env): layer-sharded pipeline
+    return common && is("parallel", "pp") && is("hop", "ipc") && std::getenv("WORLD_SIZE");
+  return common && !worker && !has_topology && is("transport", "tcp");
+}
+
+int env_int(const char* k, int def) {
+  const char* v = std::getenv(k);
+  return v ? std::atoi(v) : def;
 }
 
 struct StreamCtx {
@@ -197,13 +207,40 @@ int run_native_text(cake::PyArgs& o) {
   api.open = reinterpret_cast<decltype(api.open)>(dlsym(h, "cake_engine_open"));
   api.generate = reinterpret_cast<decltype(api.generate)>(dlsym(h, "cake_engine_generate"));
   api.close = reinterpret_cast<decltype(api.close)>(dlsym(h, "cake_engine_close"));
-  if (!api.open || !api.generate || !api.close) {
+  api.open_pp = reinterpret_cast<decltype(api.open_pp)>(dlsym(h, "cake_engine_open_pp"));
+  api.serve = reinterpret_cast<decltype(api.serve)>(dlsym(h, "cake_engine_serve"));
+  if (!api.open || !api.generate || !api.close || !api.open_pp || !api.serve) {
     std::fprintf(stderr, "cake-cli: engine symbols missing in %s\n", lib.c_str());
     return 1;
   }
+  // --transport rccl: this process is pipeline rank RANK of WORLD_SIZE (torchrun env);
+  // the engine's control plane listens on MASTER_PORT + 1 (torchrun's store owns the port)
+  const bool pipe = o["transport"].value == "rccl";
+  const int rank = pipe ? env_int("RANK", 0) : 0, world = pipe ? env_int("WORLD_SIZE", 1) : 1;
+  const char* maddr = std::getenv("MASTER_ADDR");
+  const std::string ctl = std::string(maddr ? maddr : "127.0.0.1") + ":" +
+                          std::to_string(env_int("MASTER_PORT", 29500) + 1);
   StreamCtx ctx;
   ctx.model = o["model"].value;
   std::vector<int32_t> ids;
+  if (rank != 0) {  // worker rank: its layer shard, then serve rank 0
+    const auto num = [&](const char* k, double def) {
+      return o[k].kind == PyArg::kNone ? def : std::strtod(o[k].value.c_str(), nullptr);
+    };
+    CakeEngineOpts eo{(int32_t)num("max_seq_len", 4096), o["dtype"].value == "bf16" ? 0 : 1,
+                      env_int("LOCAL_RANK", rank), 1};
+    CakePipeOpts po{rank, world, ctl.c_str(), o["hop_dtype"].value == "bf16" ? 1 : 0, 60.0, 600.0};
+    char err[1024] = {0};
+    void* eng = api.open_pp(ctx.model.c_str(), &eo, &po, err, sizeof(err));
+    if (!eng) {
+      std::fprintf(stderr, "cake-cli: rank %d: %s\n", rank, err);
+      return 1;
+    }
+    const int32_t rc = api.serve(eng, err, sizeof(err));
+    if (rc) std::fprintf(stderr, "cake-cli: rank %d: %s\n", rank, err);
+    api.close(eng);
+    return rc ? 1 : 0;
+  }
   try {
     cake::Json req = cake::Json::object();
     req.set("model", cake::Json::string(ctx.model));
@@ -223,11 +260,13 @@ int run_native_text(cake::PyArgs& o) {
   CakeEngineOpts eo{};
   eo.max_seq = (int32_t)num("max_seq_len", 4096);
   eo.dtype = o["dtype"].value == "bf16" ? 0 : 1;  // reference default: f16
-  eo.device = (int32_t)num("device", 0);
+  eo.device = pipe ? env_int("LOCAL_RANK", 0) : (int32_t)num("device", 0);
   eo.steps_per_graph = 1;
   char err[1024] = {0};
   const auto t0 = std::chrono::steady_clock::now();
-  void* eng = api.open(ctx.model.c_str(), &eo, err, sizeof(err));
+  CakePipeOpts po{0, world, ctl.c_str(), o["hop_dtype"].value == "bf16" ? 1 : 0, 60.0, 600.0};
+  void* eng = world > 1 ? api.open_pp(ctx.model.c_str(), &eo, &po, err, sizeof(err))
+                        : api.open(ctx.model.c_str(), &eo, err, sizeof(err));
   if (!eng) {
     std::fprintf(stderr, "cake-cli: native engine: %s\n", err);
     return 1;

@@ -161,3 +161,32 @@ def test_native_pipeline_two_ranks_share_one_gpu(cuda, ckpt):
         if worker.poll() is None:
             worker.kill()
             worker.wait()
+
+
+def test_cake_cli_native_pipeline_torchrun(cuda, ckpt, tmp_path):
+    """cake-cli --transport rccl --parallel pp under torchrun (2 ranks sharing the GPU):
+    the native pipeline prints the same text as the single-process native CLI."""
+    import os
+    import socket
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cli = os.path.join(root, "cake_amd", "lib", "cake-cli")
+    common = ["--model", str(ckpt), "--temperature", "0", "-n", "16", "--dtype", "bf16",
+              "--prompt", "hello there", "--max-seq-len", "256", "--topology",
+              str(tmp_path / "none.yml")]
+    env = dict(os.environ, CAKE_LOG="warning")
+    single = subprocess.run([cli, *common], capture_output=True, text=True, timeout=300, env=env,
+                            cwd=root)
+    assert single.returncode == 0, single.stderr[-3000:]
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    pp = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1",
+                         "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port",
+                         str(port), "--no-python", cli, *common, "--transport", "rccl",
+                         "--parallel", "pp", "--hop", "ipc", "--hop-dtype", "f32"],
+                        capture_output=True, text=True, timeout=300, env=env, cwd=root)
+    assert pp.returncode == 0, pp.stderr[-3000:]
+    assert single.stdout.strip() and pp.stdout == single.stdout
