@@ -31,6 +31,7 @@
 #include <cstdio>
 #include <cstring>
 #include <fstream>
+#include <list>
 #include <map>
 #include <memory>
 #include <sstream>
@@ -330,7 +331,8 @@ Json msg(const char* cmd) {
 // ---------------------------------------------------------------------------
 class Llama {
  public:
-  Llama(const std::string& dir, const CakeEngineOpts& o, const CakePipeOpts* pp = nullptr)
+  Llama(const std::string& dir, const CakeEngineOpts& o, const CakePipeOpts* pp = nullptr,
+        const std::vector<int>* layers = nullptr)
       : dt_(o.dtype), dev_(o.device) {
     if (dt_ != 0 && dt_ != 1) throw Error("dtype must be 0 (bf16) or 1 (f16)");
     if (pp) {
@@ -352,10 +354,22 @@ class Llama {
     k_ = std::max(1, o.steps_per_graph);
     if (cfg_.H % 8 || cfg_.hd % 2 || cfg_.nh % cfg_.nkv) throw Error("unsupported model shape");
     if (world_ > cfg_.L) throw Error("more pipeline ranks than layers");
-    const auto sh = shard_layers(cfg_, world_);
-    lo_ = sh[rank_].first;
-    hi_ = sh[rank_].second;
-    head_ = rank_ == 0;
+    if (layers) {  // a TCP worker: the topology node's layers, no embedding / head
+      owned_ = *layers;
+      std::sort(owned_.begin(), owned_.end());
+      owned_.erase(std::unique(owned_.begin(), owned_.end()), owned_.end());
+      if (owned_.empty() || owned_.front() < 0 || owned_.back() >= cfg_.L)
+        throw Error("worker layers outside the model");
+      head_ = false;
+    } else {
+      const auto sh = shard_layers(cfg_, world_);
+      for (int l = sh[rank_].first; l < sh[rank_].second; ++l) owned_.push_back(l);
+      head_ = rank_ == 0;
+    }
+    lo_ = owned_.front();
+    hi_ = owned_.back() + 1;
+    local_.assign(cfg_.L, -1);
+    for (size_t i = 0; i < owned_.size(); ++i) local_[owned_[i]] = (int)i;
     planner_.load(pkg_dir() + "/ops/gemm_tuned.json");
     load_weights(dir);
     alloc_state();
@@ -520,7 +534,11 @@ class Llama {
   std::vector<void*> allocs_;
   void *embed_ = nullptr, *norm_ = nullptr, *lm_head_ = nullptr;
   std::vector<LayerW> layers_;
-  uint16_t *kc_ = nullptr, *vc_ = nullptr;  // [L][nkv][S][hd]
+  struct KV { uint16_t *k, *v; };           // [local layers][nkv][S][hd]
+  std::map<uint64_t, KV> kv_;
+  std::list<uint64_t> lru_;
+  KV cur_{nullptr, nullptr};
+  std::vector<int> owned_, local_;          // global layer ids served here / inverse map
   float* inv_freq_ = nullptr;
   // decode state (graph-stable addresses; DecodeBuffers)
   float *resid_ = nullptr, *q_ = nullptr, *part_ = nullptr, *logits_ = nullptr;
@@ -609,10 +627,10 @@ class Llama {
           lm_head_ = embed_;  // tied embeddings
         }
       }
-      layers_.resize(hi_ - lo_);
-      for (int l = lo_; l < hi_; ++l) {
+      layers_.resize(owned_.size());
+      for (int l : owned_) {
         const std::string p = "model.layers." + std::to_string(l) + ".";
-        LayerW& w = layers_[l - lo_];
+        LayerW& w = layers_[local_[l]];
         w.ln1 = dalloc<uint16_t>(H);
         upload(ck, p + "input_layernorm.weight", w.ln1, H, stage, stage_bytes);
         w.wqkv = dalloc<uint16_t>((nq + 2 * nk) * H);
@@ -640,9 +658,7 @@ class Llama {
 
   void alloc_state() {
     const Cfg& c = cfg_;
-    const size_t kv = (size_t)(hi_ - lo_) * c.nkv * S_ * c.hd;
-    kc_ = dalloc<uint16_t>(kv);
-    vc_ = dalloc<uint16_t>(kv);
+    kv_session(0);  // session 0: generation / pipeline
     const std::vector<float> f = c.inv_freq();
     inv_freq_ = dalloc<float>(f.size());
     hip_check(hipMemcpy(inv_freq_, f.data(), f.size() * sizeof(float), hipMemcpyHostToDevice),
@@ -681,8 +697,72 @@ class Llama {
     hip_check(hipDeviceSynchronize(), "sync");  // null-stream memsets before st_ work
   }
 
-  uint16_t* kc(int l) const { return kc_ + (size_t)l * cfg_.nkv * S_ * cfg_.hd; }
-  uint16_t* vc(int l) const { return vc_ + (size_t)l * cfg_.nkv * S_ * cfg_.hd; }
+  uint16_t* kc(int l) const { return cur_.k + (size_t)l * cfg_.nkv * S_ * cfg_.hd; }
+  uint16_t* vc(int l) const { return cur_.v + (size_t)l * cfg_.nkv * S_ * cfg_.hd; }
+
+  // KV cache of one session (a master connection of a TCP worker; 0 = generation):
+  // allocated on first use, least recently used dropped past kMaxSessions (P4)
+  static constexpr size_t kMaxSessions = 8;
+  void kv_session(uint64_t id) {
+    auto it = kv_.find(id);
+    if (it == kv_.end()) {
+      if (kv_.size() >= kMaxSessions) {
+        uint64_t victim = lru_.front();
+        for (uint64_t x : lru_)
+          if (x != 0) { victim = x; break; }
+        drop_session(victim);
+      }
+      const size_t n = owned_.size() * (size_t)cfg_.nkv * S_ * cfg_.hd;
+      KV kv{dalloc<uint16_t>(n), dalloc<uint16_t>(n)};
+      it = kv_.emplace(id, kv).first;
+    }
+    lru_.remove(id);
+    lru_.push_back(id);
+    cur_ = it->second;
+  }
+
+ public:
+  void drop_session(uint64_t id) {
+    auto it = kv_.find(id);
+    if (it == kv_.end() || id == 0) return;
+    hip_check(hipStreamSynchronize(st_), "sync");
+    dfree(it->second.k);
+    dfree(it->second.v);
+    kv_.erase(it);
+    lru_.remove(id);
+    if (kv_.count(0)) cur_ = kv_[0];
+  }
+
+  // TCP worker compute: `layers` (global indices, this worker's) over hidden [T, H] f32
+  // (host, in place) at positions pos0.., with the session's KV cache (worker.rs:236-252;
+  // parallel/worker.py _run_ops)
+  void forward_host(uint64_t session, const std::vector<int>& layers, int pos0, float* h, int T) {
+    hip_check(hipSetDevice(dev_), "hipSetDevice");
+    const Cfg& c = cfg_;
+    if (T < 1 || pos0 < 0 || pos0 + T > S_) throw Error("positions exceed the KV cache");
+    std::vector<int> sel;
+    for (int l : layers) {
+      if (l < 0 || l >= c.L || local_[l] < 0)
+        throw Error("layer " + std::to_string(l) + " is not served here");
+      sel.push_back(local_[l]);
+    }
+    kv_session(session);
+    if (T == 1) {
+      hip_check(hipMemcpyAsync(resid_, h, sizeof(float) * c.H, hipMemcpyHostToDevice, st_), "H2D");
+      hip_check(hipMemcpyAsync(pos_, &pos0, sizeof(int), hipMemcpyHostToDevice, st_), "H2D");
+      step_layers(&sel);
+      hip_check(hipMemcpyAsync(h, resid_, sizeof(float) * c.H, hipMemcpyDeviceToHost, st_), "D2H");
+    } else {
+      const size_t bytes = sizeof(float) * (size_t)T * c.H;
+      hip_check(hipMemcpyAsync(hidden_, h, bytes, hipMemcpyHostToDevice, st_), "H2D");
+      prefill_layers(T, pos0, &sel);
+      hip_check(hipMemcpyAsync(h, hidden_, bytes, hipMemcpyDeviceToHost, st_), "D2H");
+    }
+    hip_check(hipStreamSynchronize(st_), "sync");
+    if (kv_.count(0)) cur_ = kv_[0];
+  }
+
+ private:
   float scale() const { return 1.0f / std::sqrt((float)cfg_.hd); }
 
   // ---- prefill
@@ -759,12 +839,14 @@ class Llama {
     hip_check(hipStreamSynchronize(st_), "sync");
   }
 
-  void prefill_layers(int T) {
+  void prefill_layers(int T, int pos0 = 0, const std::vector<int>* sel = nullptr) {
     const Cfg& c = cfg_;
     grow_prefill(T);
     const int nq = c.nh * c.hd, nk = c.nkv * c.hd, nqkv = nq + 2 * nk;
-    const int pos0 = 0, Tk = T;
-    for (int l = 0; l < hi_ - lo_; ++l) {
+    const int Tk = pos0 + T;
+    const int nl = sel ? (int)sel->size() : (int)layers_.size();
+    for (int i = 0; i < nl; ++i) {
+      const int l = sel ? (*sel)[i] : i;
       const LayerW& w = layers_[l];
       k_check(cake_rmsnorm(dt_, hidden_, w.ln1, (float)c.eps, T, c.H, x16_, st_), "rmsnorm");
       gemm(kEpiStore, x16_, c.H, w.wqkv, c.H, qkv_, nqkv, nullptr, 0, T, nqkv, c.H, "gemm qkv");
@@ -846,10 +928,12 @@ class Llama {
                           hop_timeout_, st_), "hop_recv");
   }
 
-  void step_layers() {
+  void step_layers(const std::vector<int>* sel = nullptr) {
     const Cfg& c = cfg_;
     const int nq = c.nh * c.hd, nk = c.nkv * c.hd;
-    for (int l = 0; l < hi_ - lo_; ++l) {
+    const int nl = sel ? (int)sel->size() : (int)layers_.size();
+    for (int i = 0; i < nl; ++i) {
+      const int l = sel ? (*sel)[i] : i;
       const LayerW& w = layers_[l];
       const uint16_t* wqkv = reinterpret_cast<const uint16_t*>(w.wqkv);
       k_check(cake_qkv_rope(dt_, resid_, w.ln1, (float)c.eps, wqkv, wqkv + (size_t)nq * c.H,
@@ -1150,6 +1234,40 @@ CAKE_API void* cake_engine_open_pp(const char* model_dir, const CakeEngineOpts* 
   } catch (const std::exception& e) {
     cake::put_err(err, errlen, e.what());
     return nullptr;
+  }
+}
+
+CAKE_API void* cake_engine_open_layers(const char* model_dir, const CakeEngineOpts* opts,
+                                       const int32_t* layers, int32_t n_layers, char* err,
+                                       int32_t errlen) {
+  try {
+    if (!model_dir || !opts || !layers || n_layers <= 0) throw cake::Error("bad arguments");
+    const std::vector<int> ls(layers, layers + n_layers);
+    return new Llama(model_dir, *opts, nullptr, &ls);
+  } catch (const std::exception& e) {
+    cake::put_err(err, errlen, e.what());
+    return nullptr;
+  }
+}
+
+CAKE_API int32_t cake_engine_forward(void* h, uint64_t session, const int32_t* layers,
+                                     int32_t n_layers, int32_t pos0, float* hidden, int32_t T,
+                                     char* err, int32_t errlen) {
+  try {
+    if (!h || !layers || !hidden) throw cake::Error("null argument");
+    static_cast<Llama*>(h)->forward_host(session, std::vector<int>(layers, layers + n_layers),
+                                         pos0, hidden, T);
+    return 0;
+  } catch (const std::exception& e) {
+    cake::put_err(err, errlen, e.what());
+    return 1;
+  }
+}
+
+CAKE_API void cake_engine_drop_session(void* h, uint64_t session) {
+  try {
+    if (h) static_cast<Llama*>(h)->drop_session(session);
+  } catch (const std::exception&) {
   }
 }
 

@@ -61,6 +61,16 @@ void* cake_engine_open_pp(const char* model_dir, const struct CakeEngineOpts* op
                           const struct CakePipeOpts* pipe, char* err, int32_t errlen);
 // Workers (rank > 0): serve rank 0's control messages until it closes; 0 or an error.
 int32_t cake_engine_serve(void* engine, char* err, int32_t errlen);
+// TCP worker (topology node): only `layers` (global indices), no embedding / head.
+void* cake_engine_open_layers(const char* model_dir, const struct CakeEngineOpts* opts,
+                              const int32_t* layers, int32_t n_layers, char* err,
+                              int32_t errlen);
+// Run `layers` over hidden [T, H] f32 (host memory, in place) at positions pos0.. with
+// the KV cache of `session` (created on first use); 0 or an error.
+int32_t cake_engine_forward(void* engine, uint64_t session, const int32_t* layers,
+                            int32_t n_layers, int32_t pos0, float* hidden, int32_t T, char* err,
+                            int32_t errlen);
+void cake_engine_drop_session(void* engine, uint64_t session);
 // [rank, world, first layer, end layer]
 int32_t cake_engine_rank_info(void* engine, int32_t* out4);
 // [V, H, L, nh, nkv, hd, I, max_seq]

@@ -190,3 +190,50 @@ def test_cake_cli_native_pipeline_torchrun(cuda, ckpt, tmp_path):
                         capture_output=True, text=True, timeout=300, env=env, cwd=root)
     assert pp.returncode == 0, pp.stderr[-3000:]
     assert single.stdout.strip() and pp.stdout == single.stdout
+
+
+def test_cake_cli_native_tcp_worker(cuda, ckpt, tmp_path):
+    """cake-cli --mode worker on the GPU serves its topology layers with the native engine
+    (no interpreter in the worker: KV cache per master connection); a master using it
+    prints the same text as the all-local native CLI."""
+    import os
+    import socket
+    import subprocess
+    import time
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cli = os.path.join(root, "cake_amd", "lib", "cake-cli")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    topo = tmp_path / "topology.yml"
+    topo.write_text(f"w1:\n  host: '127.0.0.1:{port}'\n  layers:\n    - 'model.layers.1-2'\n")
+    gen = ["--temperature", "0", "-n", "12", "--dtype", "bf16", "--prompt", "hello there",
+           "--max-seq-len", "256"]
+    env = dict(os.environ, CAKE_LOG="warning")
+    local = subprocess.run([cli, "--model", str(ckpt), "--topology", str(tmp_path / "none.yml"),
+                            *gen], capture_output=True, text=True, timeout=300, env=env, cwd=root)
+    assert local.returncode == 0, local.stderr[-3000:]
+    w = subprocess.Popen([cli, "--mode", "worker", "--name", "w1", "--model", str(ckpt),
+                          "--topology", str(topo), "--address", f"127.0.0.1:{port}", "--dtype",
+                          "bf16", "--max-seq-len", "256"], cwd=root, env=env,
+                         stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+    try:
+        t0 = time.time()
+        while True:
+            if w.poll() is not None:
+                raise AssertionError(f"worker exited: {w.stderr.read()[-3000:]}")
+            try:
+                socket.create_connection(("127.0.0.1", port), timeout=0.5).close()
+                break
+            except OSError:
+                assert time.time() - t0 < 180, "worker did not listen"
+                time.sleep(0.3)
+        dist = subprocess.run([cli, "--model", str(ckpt), "--topology", str(topo), *gen],
+                              capture_output=True, text=True, timeout=300, env=env, cwd=root)
+        assert dist.returncode == 0, dist.stderr[-3000:]
+        assert local.stdout.strip() and dist.stdout == local.stdout
+    finally:
+        w.kill()
+        err = w.communicate()[1]
+    assert "native worker" in err
