@@ -157,7 +157,7 @@ def build_engine(force: bool = False) -> Path:
     library's C entry points, plus the runtime's JSON / safetensors readers."""
     eng = CSRC / "engine" / "llama_engine.cpp"
     rt = CSRC / "runtime"
-    objs = [_compile_cpp(rt / f"{n}.cpp", force) for n in ("json", "safetensors")]
+    objs = [_compile_cpp(rt / f"{n}.cpp", force) for n in ("json", "safetensors", "net", "proto")]
     out = BUILD / "engine" / "llama_engine.o"
     out.parent.mkdir(parents=True, exist_ok=True)
     deps = [*sorted((CSRC / "engine").glob("*.h")), *sorted(rt.glob("*.h")),
@@ -167,7 +167,7 @@ def build_engine(force: bool = False) -> Path:
               "-Wno-unused-function", "-c", str(eng), "-o", str(out)])
     if force or any(_newer(o, [], ENGINE_LIB) for o in [out, *objs, KERNEL_LIB]):
         _run([HIPCC, "-shared", "-fPIC", str(out), *map(str, objs), "-o", str(ENGINE_LIB),
-              f"-L{LIB}", "-lcake_kernels", "-Wl,-rpath,$ORIGIN"])
+              f"-L{LIB}", "-lcake_kernels", "-Wl,-rpath,$ORIGIN", "-Wl,--no-undefined"])
     return ENGINE_LIB
 
 

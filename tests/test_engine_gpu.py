@@ -112,55 +112,70 @@ def test_cake_cli_native_text_matches_python_cli(cuda, ckpt, tmp_path):
     assert nat.stdout.strip() and nat.stdout == py.stdout
 
 
-def test_native_pipeline_two_ranks_share_one_gpu(cuda, ckpt):
-    """Layer-sharded native pipeline: rank 1 is another process on the same GPU (device
-    hops through IPC-mapped inboxes, prefill rows through IPC-mapped buffers, TCP control
+def test_native_pipeline_two_ranks_share_one_gpu(cuda, ckpt, tmp_path):
+    """Layer-sharded native pipeline: two rank processes on the same GPU (device hops
+    through IPC-mapped inboxes, prefill rows through IPC-mapped buffers, TCP control
     plane).  f32 hops are exact, so tokens equal the single-rank engine — greedy, sampled,
-    an EOS stop in the middle of an announced chunk, and a generation after it."""
+    an EOS stop in the middle of an announced chunk, and a generation after it.  Both
+    ranks are children of this process (siblings, as under torchrun: an IPC import reads
+    the exporter's dmabuf through its pid)."""
+    import json
     import os
     import socket
     import subprocess
     import sys
     from cake_amd.engine import NativeLlama
+    prompt = [1, 17, 300, 5, 99, 1024, 7, 8]
+    single = NativeLlama(ckpt, max_seq=256, dtype="bf16")
+    ref = single.generate(prompt, 30, repeat_penalty=1.1, repeat_last_n=16).tokens
+    ref_s = single.generate(prompt, 30, temperature=0.7, top_k=40, seed=11,
+                            repeat_penalty=1.1, repeat_last_n=16).tokens
+    single.close()
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
     addr = f"127.0.0.1:{port}"
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    code = ("import sys; sys.path.insert(0, %r)\n"
-            "from cake_amd.engine import NativeLlama\n"
-            "e = NativeLlama(%r, max_seq=256, dtype='bf16', rank=1, world=2, master_addr=%r)\n"
-            "print('layers', e.first_layer, e.end_layer, flush=True)\n"
-            "e.serve()\n"
-            "e.close()\n") % (root, str(ckpt), addr)
-    worker = subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.PIPE,
-                              stderr=subprocess.PIPE, text=True)
+    stop = ref[12]
+    rank0 = ("import sys, json; sys.path.insert(0, %r)\n"
+             "from cake_amd.engine import NativeLlama\n"
+             "e = NativeLlama(%r, max_seq=256, dtype='bf16', rank=0, world=2, master_addr=%r)\n"
+             "p = %r\n"
+             "out = {'layers': [e.first_layer, e.end_layer]}\n"
+             "out['greedy'] = e.generate(p, 30, repeat_penalty=1.1, repeat_last_n=16).tokens\n"
+             "out['sampled'] = e.generate(p, 30, temperature=0.7, top_k=40, seed=11,\n"
+             "                            repeat_penalty=1.1, repeat_last_n=16).tokens\n"
+             "out['eos'] = e.generate(p, 30, repeat_penalty=1.1, repeat_last_n=16,\n"
+             "                        eos_ids=[%d]).tokens\n"
+             "out['again'] = e.generate(p, 30, repeat_penalty=1.1, repeat_last_n=16).tokens\n"
+             "e.close()\n"
+             "print(json.dumps(out), flush=True)\n") % (root, str(ckpt), addr, prompt, stop)
+    rank1 = ("import sys; sys.path.insert(0, %r)\n"
+             "from cake_amd.engine import NativeLlama\n"
+             "e = NativeLlama(%r, max_seq=256, dtype='bf16', rank=1, world=2, master_addr=%r)\n"
+             "e.serve()\n"
+             "e.close()\n") % (root, str(ckpt), addr)
+    logs = [tmp_path / "rank0.log", tmp_path / "rank1.log"]
+    procs = [subprocess.Popen([sys.executable, "-c", c], stdout=subprocess.PIPE,
+                              stderr=open(lg, "w"), text=True)
+             for c, lg in ((rank0, logs[0]), (rank1, logs[1]))]
     try:
-        prompt = [1, 17, 300, 5, 99, 1024, 7, 8]
-        single = NativeLlama(ckpt, max_seq=256, dtype="bf16")
-        ref = single.generate(prompt, 30, repeat_penalty=1.1, repeat_last_n=16).tokens
-        ref_s = single.generate(prompt, 30, temperature=0.7, top_k=40, seed=11,
-                                repeat_penalty=1.1, repeat_last_n=16).tokens
-        single.close()
-        eng = NativeLlama(ckpt, max_seq=256, dtype="bf16", rank=0, world=2, master_addr=addr)
-        assert (eng.rank, eng.world, eng.first_layer) == (0, 2, 0) and eng.end_layer < 3
-        assert eng.generate(prompt, 30, repeat_penalty=1.1, repeat_last_n=16).tokens == ref
-        got = eng.generate(prompt, 30, temperature=0.7, top_k=40, seed=11,
-                           repeat_penalty=1.1, repeat_last_n=16).tokens
-        assert got == ref_s
-        stop = ref[12]
-        got = eng.generate(prompt, 30, repeat_penalty=1.1, repeat_last_n=16, eos_ids=[stop])
-        assert got.tokens == ref[:ref.index(stop) + 1]
-        assert eng.generate(prompt, 30, repeat_penalty=1.1, repeat_last_n=16).tokens == ref
-        eng.close()
-        out, err = worker.communicate(timeout=60)
-        assert worker.returncode == 0, err[-3000:]
-        assert out.startswith("layers")
+        out0, _ = procs[0].communicate(timeout=240)
+        procs[1].wait(timeout=60)
     finally:
-        if worker.poll() is None:
-            worker.kill()
-            worker.wait()
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    msg = "\n".join(f"---- {lg.name} ----\n" + lg.read_text()[-3000:] for lg in logs)
+    assert procs[0].returncode == 0 and procs[1].returncode == 0, msg
+    got = json.loads(out0.strip().splitlines()[-1])
+    assert got["layers"][0] == 0 and got["layers"][1] < 3
+    assert got["greedy"] == ref, msg
+    assert got["sampled"] == ref_s
+    assert got["eos"] == ref[:ref.index(stop) + 1]
+    assert got["again"] == ref
 
 
 def test_cake_cli_native_pipeline_torchrun(cuda, ckpt, tmp_path):
