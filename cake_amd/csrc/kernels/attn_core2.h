@@ -56,13 +56,13 @@ constexpr int attn2_smem_floats() {
   return NW * (kBlk * 16 + 16) + NW * (32 + NREP * HD) + 1;
 }
 
-// Core 2's workgroup: 12 waves (3 per SIMD: its ~156 VGPRs fit) for GQA groups of <= 4
-// heads, so up to 192 keys every wave owns ONE 16-key block whose loads were issued at
-// launch — the key loop is no longer a chain of dependent load round trips (4 waves:
-// ~1800 cycles per extra block, profiles/r3_attn_stamps_single_phases.jsonl); 8 waves
-// for 8-head groups (~200 VGPRs: 2 per SIMD).
+// Core 2's workgroup: 4 waves (8 for 8-head groups).  Rejected after measuring: 12
+// waves for <= 4-head groups (every wave one 16-key block up to 192 keys, so the key loop
+// is no longer a chain of load round trips) ran the 8B decode attention at 7.48 us vs
+// 5.48 (bench context, Tk <= 72): the wave-state merge and barrier scale with the wave
+// count while most waves hold no keys (profiles/r4_decode_attn_waves.md).
 template <int NREP> struct AttnGeom2 {
-  static constexpr int NW = NREP >= 8 ? 8 : 12;
+  static constexpr int NW = AttnGeom<NREP>::NW;
   static constexpr int NT = 64 * NW;
 };
 

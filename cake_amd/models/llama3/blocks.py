@@ -97,7 +97,7 @@ class LayerStack:
         # per layer; CAKE_MK=0 keeps the per-layer launches
         self.use_mk = os.environ.get("CAKE_MK", "0") != "0" and backend == "hip"
         # one-split decode steps with QKV and attention as one launch (qkv_attn_kernel);
-        # off by default: measured slower than the two launches (profiles/r4_qkv_attn_ab.md)
+        # off by default: measured slower than the two launches (profiles/r4_decode_attn_waves.md)
         self.use_qkv_attn = os.environ.get("CAKE_QKV_ATTN", "0") != "0" and backend == "hip"
         self._mk_ok: bool | None = None
         self._mk_tables: dict = {}
