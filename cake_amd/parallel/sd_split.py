@@ -237,4 +237,5 @@ def measure_sd_split(env, steps: int = 4, warmup: int = 2, version: str = "xl",
             "per_step_s": [round(s, 5) for s in step_s],
             # the final latents (equivalence across rank counts; tests)
             "latent_checksum": float(x.double().sum()), "latent_abs": float(x.double().abs().sum()),
-            "transport": "rccl p2p, packed buffer per hop" if hip else "gloo"}
+            "transport": ("gloo, host-staged packed buffer per hop" if link.staged else
+                          "rccl p2p, packed buffer per hop") if hip else "gloo"}
