@@ -101,16 +101,99 @@ class PackedLink:
         self._recv.pop((peer, key), None)
 
 
-def split_stages(stages: list[str], world: int) -> list[tuple[int, list[str]]]:
+def stage_costs(ucfg, h: int, w: int) -> dict[str, float]:
+    """Forward FLOPs of each UNet stage (down.i, mid, up.i) for an h x w latent, batch 1:
+    3x3 convolutions, the resnets' 1x1 shortcuts, and per transformer block the
+    projections (self q|k|v|o 4C^2, cross q|o 2C^2, GEGLU FF 12C^2, proj in/out 2C^2 per
+    model) plus the attention products (self HW^2 C, cross 77 HW C).  Only the ratios
+    matter: they balance the split."""
+    blocks = list(ucfg.blocks)
+    L = ucfg.layers_per_block
+
+    def conv(cin, cout, hw, k=3):
+        return 2.0 * k * k * cin * cout * hw
+
+    def resnet(cin, cout, hw):
+        return conv(cin, cout, hw) + conv(cout, cout, hw) + (conv(cin, cout, hw, 1) if cin != cout else 0)
+
+    def transformer(c, hw, depth):
+        per = 2.0 * hw * c * c * (4 + 2 + 12) + 4.0 * hw * hw * c + 4.0 * hw * 77 * c
+        return depth * per + 2 * 2.0 * hw * c * c
+
+    costs: dict[str, float] = {}
+    hw = h * w
+    chans = [b.out_channels for b in blocks]
+    cin = chans[0]
+    for i, b in enumerate(blocks):
+        c = conv(ucfg.in_channels, chans[0], hw) if i == 0 else 0.0
+        for j in range(L):
+            c += resnet(cin if j == 0 else b.out_channels, b.out_channels, hw)
+            if b.cross_attn:
+                c += transformer(b.out_channels, hw, b.transformer_layers)
+        cin = b.out_channels
+        if i < len(blocks) - 1:
+            hw //= 4
+            c += conv(b.out_channels, b.out_channels, hw)
+        costs[f"down.{i}"] = c
+    cm, mb = chans[-1], blocks[-1]
+    costs["mid"] = 2 * resnet(cm, cm, hw) + transformer(cm, hw, mb.transformer_layers)
+    rev = list(reversed(chans))
+    out = rev[0]
+    for i, b in enumerate(reversed(blocks)):
+        prev, out = out, rev[i]
+        skip_in = rev[min(i + 1, len(rev) - 1)]
+        c = 0.0
+        for j in range(L + 1):
+            skip = skip_in if j == L else out
+            c += resnet((prev if j == 0 else out) + skip, out, hw)
+            if b.cross_attn:
+                c += transformer(out, hw, b.transformer_layers)
+        if i < len(blocks) - 1:
+            hw *= 4
+            c += conv(out, out, hw)
+        else:
+            c += conv(out, ucfg.out_channels, hw)
+        costs[f"up.{i}"] = c
+    return costs
+
+
+def split_stages(stages: list[str], world: int,
+                 costs: dict[str, float] | None = None) -> list[tuple[int, list[str]]]:
     """Contiguous runs of UNet stages over min(world, len(stages)) ranks, rank 0 first
-    (the master owns the UNet input side); balanced by stage count."""
+    (the master owns the UNet input side).  With `costs` the split minimises the largest
+    rank's cost (the per-step critical path of the sequential pipeline); else it is
+    balanced by stage count."""
     n = min(world, len(stages))
-    runs, s = [], 0
-    for r in range(n):
-        e = s + (len(stages) - s) // (n - r)
-        runs.append((r, stages[s:e]))
-        s = e
-    return runs
+    if costs is None:
+        runs, s = [], 0
+        for r in range(n):
+            e = s + (len(stages) - s) // (n - r)
+            runs.append((r, stages[s:e]))
+            s = e
+        return runs
+    c = [float(costs[x]) for x in stages]
+    m = len(c)
+    pre = [0.0]
+    for x in c:
+        pre.append(pre[-1] + x)
+    INF = float("inf")
+    # best[k][j]: min over splits of stages[:j] into k non-empty runs of the largest run
+    best = [[INF] * (m + 1) for _ in range(n + 1)]
+    cut = [[0] * (m + 1) for _ in range(n + 1)]
+    best[0][0] = 0.0
+    for k in range(1, n + 1):
+        for j in range(k, m - (n - k) + 1):
+            for i in range(k - 1, j):
+                v = max(best[k - 1][i], pre[j] - pre[i])
+                if v < best[k][j]:
+                    best[k][j], cut[k][j] = v, i
+    bounds, j = [], m
+    for k in range(n, 0, -1):
+        i = cut[k][j]
+        bounds.append((i, j))
+        j = i
+    bounds.reverse()
+    return [(r, stages[a:b]) for r, (a, b) in enumerate(bounds)]
 
 
 def _sched_update(x, pred, coef_row, guidance: float):
@@ -138,7 +221,7 @@ def measure_sd_split(env, steps: int = 4, warmup: int = 2, version: str = "xl",
     cfg = tiny_config(version) if tiny else get_config(version)
     model = UNet2DConditionModel(cfg.unet)
     stages = model.stage_names()
-    runs = split_stages(stages, world)
+    runs = split_stages(stages, world, stage_costs(cfg.unet, cfg.height // 8, cfg.width // 8))
     mine = [names for r, names in runs if r == rank]
     names = mine[0] if mine else []
     hip = dev.type == "cuda"
