@@ -36,6 +36,12 @@ static int g_attn_target = 16;
 // costs what ~240 more keys of one split's loop cost (~27 cycles per key)
 static int g_attn_single = 320;
 static int g_attn_drop_partials = 0;  // test hook (cake_attn_debug_drop_partials)
+// core 2: key blocks per wave in flight (attn2_decode_block PFD); 0 = by the launch's
+// split cap: 1 for grids of <= 8 splits per kv head (the graph bucket of short contexts:
+// 5.47 vs 5.96 us per 8B layer at 33-177 keys, the deeper prefetch's larger code costs
+// more than it saves), 2 above (8B decode at 2048 keys +0.7 % tok/s;
+// profiles/r4_decode_attn_prefetch.md); tunable
+static int g_attn_prefetch = 0;
 
 template <int DT, int HD, int NREP>
 __global__ __launch_bounds__(AttnGeom<NREP>::NT) void attn_decode_kernel(AttnDecArgs a) {
@@ -44,11 +50,12 @@ __global__ __launch_bounds__(AttnGeom<NREP>::NT) void attn_decode_kernel(AttnDec
   attn_decode_block<DT, HD, NREP>(a, blockIdx.x, blockIdx.y, smem);
 }
 
-template <int DT, int HD, int NREP>
+template <int DT, int HD, int NREP, int PFD>
 __global__ __launch_bounds__(AttnGeom2<NREP>::NT) void attn2_decode_kernel(AttnDecArgs a) {
   __shared__ __attribute__((aligned(16)))
       float lds[attn2_smem_floats<HD, NREP, AttnGeom2<NREP>::NW>()];
-  attn2_decode_block<DT, HD, NREP>(a, blockIdx.x, blockIdx.y, lds, gridDim.x);
+  attn2_decode_block<DT, HD, NREP, false, AttnGeom2<NREP>::NW, PFD>(a, blockIdx.x, blockIdx.y,
+                                                                    lds, gridDim.x);
 }
 
 }  // namespace cake
@@ -100,6 +107,12 @@ CAKE_API int cake_attn_set_split_cap(int cap) {
 CAKE_API int cake_attn_set_target_splits(int target) {
   if (target < 1 || target > kMaxSplit) return (int)hipErrorInvalidValue;
   g_attn_target = target;
+  return 0;
+}
+
+CAKE_API int cake_attn_set_prefetch(int depth) {
+  if (depth < 0 || depth > 2) return (int)hipErrorInvalidValue;
+  g_attn_prefetch = depth;
   return 0;
 }
 
@@ -169,10 +182,17 @@ static bool grid_resident(K kern, int threads, long long blocks) {
 
 template <int DT, int HD>
 static int launch_decode(int n_rep, dim3 grid, hipStream_t st, const AttnDecArgs& a) {
+#define CAKE_DEC2(NR, PF)                                                                     \
+  if (grid_resident(attn2_decode_kernel<DT, HD, NR, PF>, AttnGeom2<NR>::NT,                   \
+                    (long long)grid.x * grid.y))                                              \
+    hipLaunchKernelGGL((attn2_decode_kernel<DT, HD, NR, PF>), grid, dim3(AttnGeom2<NR>::NT), 0, \
+                       st, a);                                                                \
+  else                                                                                        \
+    hipLaunchKernelGGL((attn_decode_kernel<DT, HD, NR>), grid, dim3(AttnGeom<NR>::NT), 0, st, a)
 #define CAKE_DEC(NR)                                                                          \
-  if (g_attn_impl == 2 &&                                                                     \
-      grid_resident(attn2_decode_kernel<DT, HD, NR>, AttnGeom2<NR>::NT, (long long)grid.x * grid.y)) \
-    hipLaunchKernelGGL((attn2_decode_kernel<DT, HD, NR>), grid, dim3(AttnGeom2<NR>::NT), 0, st, a); \
+  if (g_attn_impl == 2 && (g_attn_prefetch == 2 || (g_attn_prefetch == 0 && grid.y > 8)))    \
+    { CAKE_DEC2(NR, 2); }                                                                     \
+  else if (g_attn_impl == 2) { CAKE_DEC2(NR, 1); }                                            \
   else                                                                                        \
     hipLaunchKernelGGL((attn_decode_kernel<DT, HD, NR>), grid, dim3(AttnGeom<NR>::NT), 0, st, a)
   switch (n_rep) {
@@ -183,6 +203,7 @@ static int launch_decode(int n_rep, dim3 grid, hipStream_t st, const AttnDecArgs
     default: return (int)hipErrorInvalidValue;
   }
 #undef CAKE_DEC
+#undef CAKE_DEC2
   return (int)hipGetLastError();
 }
 

@@ -27,6 +27,8 @@
 // Dead keys (past the live length, or speculative rows of split 0 loaded before
 // the position arrived) are masked in the scores and zeroed in V.
 #pragma once
+#include <type_traits>
+
 #include "attn_core.h"
 
 namespace cake {
@@ -99,9 +101,14 @@ __device__ __forceinline__ uint4 ld16_sc1(__amdgpu_buffer_rsrc_t r, size_t byte_
 // q / K / V loads are sc1 and the whole context runs as one split (the host picks the
 // fused launch where attn2_splits gives one split; longer contexts stay correct, one
 // workgroup walking every key).  ng = number of kv heads (the standalone grid's x).
-template <int DT, int HD, int NREP, bool FUSED = false, int NW = AttnGeom2<NREP>::NW>
+// PFD: key blocks per wave in flight (1: the next block's loads issued with the current
+// block's compute; 2: two ahead, and split 0 requests its first TWO blocks per wave at
+// launch — up to 2 NW x 16 keys need no load round trip inside the loop).
+template <int DT, int HD, int NREP, bool FUSED = false, int NW = AttnGeom2<NREP>::NW,
+          int PFD = 2>
 __device__ __forceinline__ void attn2_decode_block(const AttnDecArgs& a, int g, int s,
                                                    float* lds, int ng) {
+  static_assert(PFD == 1 || PFD == 2, "prefetch depth 1 or 2");
   constexpr int DS = HD / 32;    // MFMA k-steps (A fragments) per key block
   constexpr int NCH = HD / 8;    // 8-dim chunks per row
   constexpr int KPL = NCH / 4;   // keys per lane in P.V (16 keys over 64 / NCH key groups)
@@ -119,52 +126,66 @@ __device__ __forceinline__ void attn2_decode_block(const AttnDecArgs& a, int g, 
   const uint16_t* vgp = a.vc + (size_t)g * a.S * HD;
 
   // one block's operands: K A-fragments and V rows of this lane
-  uint4 kf[DS], vf[KPL];
+  // PFD slots of one block's operands (slot index a compile-time constant everywhere)
+  uint4 kf[PFD][DS], vf[PFD][KPL];
   __amdgpu_buffer_rsrc_t krs, vrs;
   if constexpr (FUSED) { krs = sc1_rsrc(kgp); vrs = sc1_rsrc(vgp); }
-  auto load_blk = [&](int key0, int last) {
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, PFD - 1>;
+  auto load_blk = [&](auto slot, int key0, int last) {
+    constexpr int SL = decltype(slot)::value;
 #pragma unroll
     for (int d = 0; d < DS; ++d) {
       const int r = min(key0 + col, last);
       const size_t o = (size_t)r * HD + d * 32 + rg * 8;
-      if constexpr (FUSED) kf[d] = ld16_sc1(krs, o * 2);
-      else kf[d] = *reinterpret_cast<const uint4*>(kgp + o);
+      if constexpr (FUSED) kf[SL][d] = ld16_sc1(krs, o * 2);
+      else kf[SL][d] = *reinterpret_cast<const uint4*>(kgp + o);
     }
 #pragma unroll
     for (int j = 0; j < KPL; ++j) {
       const int r = min(key0 + kg * KPL + j, last);
       const size_t o = (size_t)r * HD + ch * 8;
-      if constexpr (FUSED) vf[j] = ld16_sc1(vrs, o * 2);
-      else vf[j] = *reinterpret_cast<const uint4*>(vgp + o);
+      if constexpr (FUSED) vf[SL][j] = ld16_sc1(vrs, o * 2);
+      else vf[SL][j] = *reinterpret_cast<const uint4*>(vgp + o);
     }
   };
 
   // split 0 starts at key 0: its first blocks are requested with the position
   // (rows clamped to the cache; dead rows are masked / zeroed below)
-  if (s == 0) load_blk(wave * kBlk, a.S - 1);
-  // q (f32, roped) -> pre-scaled 16-bit B fragments: column col = head g*NREP + col
+  if (s == 0) load_blk(I0{}, wave * kBlk, a.S - 1);
+  // q (f32, roped) -> pre-scaled 16-bit B fragments: column col = head g*NREP + col.
+  // The q loads go out right after the first block's, and split 0's second speculative
+  // block after q: loads retire in order, so q (needed by the first MFMA) never waits
+  // behind the second block.
   uint4 qf[DS];
   {
     float qv[DS][8];
+    float4 qx[DS][2];
 #pragma unroll
     for (int d = 0; d < DS; ++d) {
       if (col < NREP) {
         const size_t qo = (size_t)(g * NREP + col) * HD + d * 32 + rg * 8;
-        float4 x0, x1;
         if constexpr (FUSED) {
           const __amdgpu_buffer_rsrc_t qr = sc1_rsrc(a.q);
-          x0 = __builtin_bit_cast(float4, ld16_sc1(qr, qo * 4));
-          x1 = __builtin_bit_cast(float4, ld16_sc1(qr, qo * 4 + 16));
+          qx[d][0] = __builtin_bit_cast(float4, ld16_sc1(qr, qo * 4));
+          qx[d][1] = __builtin_bit_cast(float4, ld16_sc1(qr, qo * 4 + 16));
         } else {
-          x0 = *reinterpret_cast<const float4*>(a.q + qo);
-          x1 = *reinterpret_cast<const float4*>(a.q + qo + 4);
+          qx[d][0] = *reinterpret_cast<const float4*>(a.q + qo);
+          qx[d][1] = *reinterpret_cast<const float4*>(a.q + qo + 4);
         }
-        qv[d][0] = x0.x; qv[d][1] = x0.y; qv[d][2] = x0.z; qv[d][3] = x0.w;
-        qv[d][4] = x1.x; qv[d][5] = x1.y; qv[d][6] = x1.z; qv[d][7] = x1.w;
       } else {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) qv[d][e] = 0.f;
+        qx[d][0] = qx[d][1] = make_float4(0.f, 0.f, 0.f, 0.f);
       }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (PFD == 2)
+      if (s == 0) load_blk(I1{}, (wave + NW) * kBlk, a.S - 1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int d = 0; d < DS; ++d) {
+      const float4 x0 = qx[d][0], x1 = qx[d][1];
+      qv[d][0] = x0.x; qv[d][1] = x0.y; qv[d][2] = x0.z; qv[d][3] = x0.w;
+      qv[d][4] = x1.x; qv[d][5] = x1.y; qv[d][6] = x1.z; qv[d][7] = x1.w;
     }
 #pragma unroll
     for (int d = 0; d < DS; ++d) {
@@ -196,17 +217,23 @@ __device__ __forceinline__ void attn2_decode_block(const AttnDecArgs& a, int g, 
     for (int e = 0; e < 8; ++e) o[h][e] = 0.f;
 
   int b = wave;
-  if (s != 0 && b < nblk) load_blk(kb + b * kBlk, ke - 1);
+  if (s != 0) {
+    if (b < nblk) load_blk(I0{}, kb + b * kBlk, ke - 1);
+    if constexpr (PFD == 2)
+      if (b + NW < nblk) load_blk(I1{}, kb + (b + NW) * kBlk, ke - 1);
+  }
   ATTN_STAMP(2);
-  for (; b < nblk; b += NW) {
+  // one key block from slot `slot`; the block PFD x NW further on is requested into the
+  // freed slot before this one is computed
+  auto block = [&](auto slot, int b) {
+    constexpr int SL = decltype(slot)::value;
     const int key0 = kb + b * kBlk;
-    // this block's operands, then the next block's loads in flight
     uint4 kc[DS], vc[KPL];
 #pragma unroll
-    for (int d = 0; d < DS; ++d) kc[d] = kf[d];
+    for (int d = 0; d < DS; ++d) kc[d] = kf[SL][d];
 #pragma unroll
-    for (int j = 0; j < KPL; ++j) vc[j] = vf[j];
-    if (b + NW < nblk) load_blk(key0 + NW * kBlk, ke - 1);
+    for (int j = 0; j < KPL; ++j) vc[j] = vf[SL][j];
+    if (b + PFD * NW < nblk) load_blk(slot, key0 + PFD * NW * kBlk, ke - 1);
     // scores: S[key 4 rg + e][col]
     cf32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -256,6 +283,14 @@ __device__ __forceinline__ void attn2_decode_block(const AttnDecArgs& a, int g, 
       }
     }
     __builtin_amdgcn_wave_barrier();  // tile reads done before the next block's writes
+  };
+  if constexpr (PFD == 1) {
+    for (; b < nblk; b += NW) block(I0{}, b);
+  } else {
+    for (; b < nblk; b += 2 * NW) {
+      block(I0{}, b);
+      if (b + NW < nblk) block(I1{}, b + NW);
+    }
   }
   ATTN_STAMP(3);
   // sum the key groups: lanes of one dim chunk (lane % NCH) end with the wave's o

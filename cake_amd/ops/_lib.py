@@ -28,6 +28,7 @@ _SIGS = {
     "cake_qkv_rope": [I, P, P, F, P, P, P, I, I, I, I, P, P, P, P, P, I, P],
     "cake_qkv_attn": [I, P, P, F, P, P, P, I, I, I, I, P, P, P, P, P, I, F, P, P, P],
     "cake_qkv_attn_supported": [I, I, I, I],
+    "cake_attn_set_prefetch": [I],
     "cake_swiglu": [I, P, P, F, P, P, I, I, P, P],
     "cake_gemv_x16": [I, P, P, I, I, P, I, P],
     "cake_gemv_norm_f32": [I, P, P, F, P, I, I, P, P],

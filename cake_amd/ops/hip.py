@@ -237,6 +237,8 @@ def attn_decode(q, kcache, vcache, pos, scale, part, tickets, out):
             attn_set_target_splits(int(os.environ["CAKE_ATTN_TARGET"]))
         if os.environ.get("CAKE_ATTN_SINGLE"):
             attn_set_single_max(int(os.environ["CAKE_ATTN_SINGLE"]))
+        if os.environ.get("CAKE_ATTN_PREFETCH"):
+            attn_set_prefetch(int(os.environ["CAKE_ATTN_PREFETCH"]))
     check(kernels().cake_attn_decode(_dt(kcache), _p(q), _p(kcache), _p(vcache), _p(pos), S,
                                      nh, nkv, hd, float(scale), _p(part), _p(tickets),
                                      _p(out), _stream()),
@@ -349,6 +351,11 @@ def attn_set_single_max(keys: int) -> None:
     """Core 2: live lengths up to `keys` run as one split per kv head (no merge)."""
     check(kernels().cake_attn_set_single_max(int(keys)), "attn_set_single_max")
     _ATTN_SINGLE[0] = int(keys)
+
+
+def attn_set_prefetch(depth: int) -> None:
+    """Core 2: key blocks per wave in flight (1 or 2; 0 = by split cap, the default)."""
+    check(kernels().cake_attn_set_prefetch(int(depth)), "attn_set_prefetch")
 
 
 def attn_set_target_splits(n: int) -> None:
