@@ -93,6 +93,21 @@ int cake_gumbel_argmax(const float* logits, int V, float temperature, unsigned l
 int cake_finalize_token(unsigned long long* slot, int* tok, int* hist, int* hist_len, int* pos,
                         int max_hist, hipStream_t st);
 int cake_hop_alloc(size_t bytes, void** ptr);
+int cake_sum_slices(float* out, const float* src, int W, long long stride, long long n,
+                    int accumulate, hipStream_t st);
+long long cake_ar_inbox_words(int world, int n);
+int cake_ar_sum(const float* partial, float* out, int n, int accumulate, void* const* peers,
+                const void* inbox, unsigned int* seq, int* err, int rank, int world,
+                double timeout_s, hipStream_t st);
+int cake_ar_max_key(unsigned long long* slot, void* const* peers, const void* inbox,
+                    unsigned int* seq, int* err, int rank, int world, double timeout_s,
+                    hipStream_t st);
+int cake_ar_gather(const float* shard, int off, int n_local, float* full, int n,
+                   void* const* peers, const void* inbox, unsigned int* seq, int* err, int rank,
+                   int world, double timeout_s, hipStream_t st);
+int cake_select_shard(float* logits, int V, int off, const int* hist, const int* hist_len,
+                      int last_n, float penalty, float temperature, unsigned long long seed,
+                      unsigned long long* slot, hipStream_t st);
 int cake_hop_free(void* ptr);
 int cake_hop_words(int H, int nhdr, int bf16);
 int cake_hop_send(const float* src, int H, int nhdr, int bf16, void* dst_inbox, unsigned int* seq,
@@ -273,7 +288,7 @@ struct GemmPlanner {
   }
 };
 
-constexpr int kEpiStore = 0, kEpiResid32 = 1, kEpiSwiglu = 3;
+constexpr int kEpiStore = 0, kEpiResid32 = 1, kEpiSwiglu = 3, kEpiStore32 = 6;
 
 // Contiguous layer shards, rank 0 lighter by the head's weight in blocks
 // (parallel/pipeline.py shard_layers + head_cost_in_layers).
@@ -295,6 +310,13 @@ std::vector<std::pair<int, int>> shard_layers(const Cfg& c, int world) {
     start = end;
   }
   return out;
+}
+
+// [start, end) of rank's contiguous share of n items (parallel/tensor_parallel.py)
+std::pair<int, int> split_range(int n, int world, int rank) {
+  const int q = n / world, r = n % world;
+  const int a = rank * q + std::min(rank, r);
+  return {a, a + q + (rank < r ? 1 : 0)};
 }
 
 std::string hex_of(const void* p, size_t n) {
@@ -332,9 +354,18 @@ Json msg(const char* cmd) {
 class Llama {
  public:
   Llama(const std::string& dir, const CakeEngineOpts& o, const CakePipeOpts* pp = nullptr,
-        const std::vector<int>* layers = nullptr)
+        const std::vector<int>* layers = nullptr, const CakeTPOpts* tp = nullptr)
       : dt_(o.dtype), dev_(o.device) {
     if (dt_ != 0 && dt_ != 1) throw Error("dtype must be 0 (bf16) or 1 (f16)");
+    if (tp) {
+      tp_ = tp->world;
+      tp_rank_ = tp->rank;
+      hop_timeout_ = tp->timeout_s > 0 ? tp->timeout_s : 30.0;
+      if (tp_ < 1 || tp_ > 8 || tp_rank_ < 0 || tp_rank_ >= tp_) throw Error("bad TP rank / world");
+      int n = 0;
+      hip_check(hipGetDeviceCount(&n), "hipGetDeviceCount");
+      if (n > 0) dev_ %= n;
+    }
     if (pp) {
       rank_ = pp->rank;
       world_ = pp->world;
@@ -354,6 +385,21 @@ class Llama {
     k_ = std::max(1, o.steps_per_graph);
     if (cfg_.H % 8 || cfg_.hd % 2 || cfg_.nh % cfg_.nkv) throw Error("unsupported model shape");
     if (world_ > cfg_.L) throw Error("more pipeline ranks than layers");
+    // this rank's compute shapes: the whole model, or its tensor-parallel slice
+    lc_ = cfg_;
+    if (tp_ > 1) {
+      if (cfg_.nh % tp_ || cfg_.nkv % tp_)
+        throw Error("tensor-parallel degree must divide the query and KV heads");
+      lc_.nh = cfg_.nh / tp_;
+      lc_.nkv = cfg_.nkv / tp_;
+      const auto ir = split_range(cfg_.I, tp_, tp_rank_);
+      const auto vr = split_range(cfg_.V, tp_, tp_rank_);
+      i0_ = ir.first;
+      lc_.I = ir.second - ir.first;
+      voff_ = vr.first;
+      lc_.V = vr.second - vr.first;
+      if (lc_.I % 8 || (lc_.nh * cfg_.hd) % 8) throw Error("tensor-parallel slice not 8-aligned");
+    }
     if (layers) {  // a TCP worker: the topology node's layers, no embedding / head
       owned_ = *layers;
       std::sort(owned_.begin(), owned_.end());
@@ -375,12 +421,14 @@ class Llama {
     alloc_state();
     if (world_ > 1) connect_pipeline(pp->master_addr ? pp->master_addr : "127.0.0.1:29517",
                                      pp->connect_timeout_s > 0 ? pp->connect_timeout_s : 600.0);
+    if (tp_ > 1) connect_tp(tp->master_addr ? tp->master_addr : "127.0.0.1:29517",
+                            tp->connect_timeout_s > 0 ? tp->connect_timeout_s : 600.0);
   }
 
   ~Llama() {
     (void)hipSetDevice(dev_);
     (void)hipStreamSynchronize(st_);
-    if (rank_ == 0)
+    if (rank_ == 0 && tp_rank_ == 0)
       for (int fd : peers_) {
         try {
           send_json(fd, msg("exit"));
@@ -390,6 +438,8 @@ class Llama {
     for (int fd : peers_) tcp_close(fd);
     if (ctl_fd_ >= 0) tcp_close(ctl_fd_);
     drop_graphs();
+    for (void* p : tp_mapped_) (void)hipIpcCloseMemHandle(p);
+    for (void* p : tp_owned_) (void)cake_hop_free(p);
     if (next_inbox_) (void)hipIpcCloseMemHandle(next_inbox_);
     if (next_pbuf_) (void)hipIpcCloseMemHandle(next_pbuf_);
     if (inbox_) (void)cake_hop_free(inbox_);
@@ -397,8 +447,8 @@ class Llama {
     (void)hipStreamDestroy(st_);
   }
 
-  int rank() const { return rank_; }
-  int world() const { return world_; }
+  int rank() const { return tp_ > 1 ? tp_rank_ : rank_; }
+  int world() const { return tp_ > 1 ? tp_ : world_; }
   std::pair<int, int> layer_range() const { return {lo_, hi_}; }
 
   const Cfg& cfg() const { return cfg_; }
@@ -418,12 +468,53 @@ class Llama {
                 int out_cap, CakeEngineStats* stats) {
     hip_check(hipSetDevice(dev_), "hipSetDevice");
     if (!head_) throw Error("generate() runs on pipeline rank 0");
+    if (tp_ > 1 && tp_rank_ != 0) throw Error("generate() runs on tensor-parallel rank 0");
     if (T <= 0) throw Error("empty prompt");
     if (max_new <= 0) return;
     if (T + max_new + k_ + 1 > S_) throw Error("prompt + max_new exceeds max_seq");
     if (out_cap < max_new) throw Error("output buffer smaller than max_new");
+    if (tp_ > 1) {  // every tensor-parallel rank runs the same steps: tell them what
+      Json m = msg("generate");
+      Json pr = Json::array();
+      for (int i = 0; i < T; ++i) pr.push(Json::integer(prompt[i]));
+      m.set("prompt", pr);
+      m.set("max_new", Json::integer(max_new));
+      m.set("temperature", Json::number(smp.temperature));
+      m.set("top_k", Json::integer(smp.top_k));
+      m.set("top_p", Json::number(smp.top_p));
+      m.set("seed", Json::string(std::to_string(smp.seed)));
+      m.set("penalty", Json::number(smp.repeat_penalty));
+      m.set("last_n", Json::integer(smp.repeat_last_n));
+      for (int fd : peers_) send_json(fd, m);
+    }
+    run_generation(prompt, T, max_new, smp, eos, n_eos, cb, ctx, out, out_cap, stats, true);
+  }
+
+  // A tensor-parallel rank's generation never stops early (every rank replays the same
+  // steps; EOS / the callback only truncate the reported tokens on rank 0).
+  struct TpStop {
+    cake_engine_token_cb cb;
+    void* ctx;
+    const int32_t* eos;
+    int n_eos;
+    bool stopped;
+    int count;
+  };
+  static int32_t tp_token_cb(void* vctx, int32_t tok) {
+    auto* t = static_cast<TpStop*>(vctx);
+    if (t->stopped) return 0;
+    ++t->count;
+    if (t->cb && t->cb(t->ctx, tok) != 0) t->stopped = true;
+    for (int e = 0; e < t->n_eos; ++e)
+      if (t->eos[e] == tok) t->stopped = true;
+    return 0;
+  }
+
+  void run_generation(const int32_t* prompt, int T, int max_new, const CakeEngineSampling& smp,
+                      const int32_t* eos, int n_eos, cake_engine_token_cb cb, void* ctx,
+                      int32_t* out, int out_cap, CakeEngineStats* stats, bool lead) {
     const auto t0 = std::chrono::steady_clock::now();
-    prefill(prompt, T);
+    prefill_body(prompt, T);
     // the prefill position bookkeeping of DeviceDecoder.start: history = prompt,
     // pos = T - 1 (the last written row), slot cleared
     std::vector<int32_t> h(prompt, prompt + T);
@@ -434,19 +525,29 @@ class Llama {
     hip_check(hipMemsetAsync(slot_, 0, sizeof(unsigned long long), st_), "slot");
     Mode mode = mode_of(smp);
     // first token from the prefill logits (DeviceDecoder._select_first)
-    select_tail(mode);
+    if (tp_ > 1) {
+      head_tp(hidden_ + (size_t)(T - 1) * cfg_.H, mode);
+    } else {
+      k_check(cake_gemv_norm_f32(dt_, hidden_ + (size_t)(T - 1) * cfg_.H, norm_, (float)lc_.eps,
+                                 lm_head_, lc_.H, lc_.V, logits_, st_), "lm_head");
+      select_tail(mode);
+    }
     if (mode.fused) k_check(cake_embed(dt_, embed_, tok_, 1, cfg_.H, resid_, st_), "embed");
     int32_t first = 0;
     hip_check(hipMemcpyAsync(&first, tok_, sizeof(int32_t), hipMemcpyDeviceToHost, st_), "tok");
     hip_check(hipStreamSynchronize(st_), "sync");
     const auto t1 = std::chrono::steady_clock::now();
     int n_out = 0;
-    out[n_out++] = first;
-    bool stop = cb && cb(ctx, first) != 0;
-    for (int e = 0; e < n_eos && !stop; ++e)
-      if (eos[e] == first) stop = true;
+    bool stop = false;
+    if (lead) {
+      out[n_out++] = first;
+      stop = cb && cb(ctx, first) != 0;
+      for (int e = 0; e < n_eos && !stop; ++e)
+        if (eos[e] == first) stop = true;
+    }
+    TpStop tps{cb, ctx, eos, n_eos, stop, 0};
     std::vector<float> ms;
-    if (!stop && max_new > 1) {
+    if ((tp_ > 1 || !stop) && max_new > 1) {
       ensure_graphs(mode);
       const int n = max_new - 1;
       std::vector<int32_t> toks(n);
@@ -477,12 +578,27 @@ class Llama {
       spec.out_tokens = toks.data();
       spec.out_ms = ms.data();
       spec.out_cap = n;
+      if (tp_ > 1) {  // lock step: all n replays on every rank
+        spec.eos = nullptr;
+        spec.n_eos = 0;
+        spec.on_token = lead ? &Llama::tp_token_cb : nullptr;
+        spec.token_ctx = &tps;
+        if (!lead) {  // no read-back: enqueue every replay (device-paced by the all-reduces)
+          spec.hist = nullptr;
+          spec.out_tokens = nullptr;
+          spec.out_ms = nullptr;
+          spec.out_cap = 0;
+        }
+      }
       CakeLoopResult res{};
       const int rc = cake_graph_decode(&spec, &res);
       if (world_ > 1) sync_workers();
+      if (tp_ > 1 && lead) sync_tp_workers();
       k_check(rc, "graph_decode");
-      for (int i = 0; i < res.n_tokens && n_out < out_cap; ++i) out[n_out++] = toks[i];
-      ms.resize(res.n_tokens);
+      const int keep = tp_ > 1 ? tps.count : res.n_tokens;
+      if (lead)
+        for (int i = 0; i < keep && n_out < out_cap; ++i) out[n_out++] = toks[i];
+      ms.resize(lead ? std::min(keep, res.n_tokens) : 0);
     }
     const auto t2 = std::chrono::steady_clock::now();
     if (stats) {
@@ -526,6 +642,19 @@ class Llama {
   unsigned int* seq_ = nullptr;
   int* hop_err_ = nullptr;
   std::vector<int> peers_;  // rank 0: control sockets of ranks 1..world-1
+  // tensor parallel
+  struct ArChan {
+    void* inbox = nullptr;
+    std::vector<void*> peers;  // peer inboxes (IPC-mapped), own slot unused
+  };
+
+  int tp_ = 1, tp_rank_ = 0, i0_ = 0, voff_ = 0, slab_bank_ = 0;
+  Cfg lc_;                   // this rank's compute shapes (the whole model unless TP)
+  ArChan ch_sum_, ch_key_, ch_gat_;
+  float *partial_ = nullptr, *ppart_ = nullptr, *full_logits_ = nullptr, *slab_ = nullptr;
+  unsigned int* ar_seq_ = nullptr;
+  int* ar_err_ = nullptr;
+  std::vector<void*> peer_slab_, tp_mapped_, tp_owned_;
   int ctl_fd_ = -1;         // workers: control socket to rank 0
   hipStream_t st_ = nullptr;
   Cfg cfg_;
@@ -589,29 +718,58 @@ class Llama {
     for (auto d : t.shape) n *= d;
     if (n != numel) throw Error(name + ": " + std::to_string(n) + " elements, expected " +
                                 std::to_string(numel));
+    const size_t R = t.shape.empty() ? 1 : t.shape[0];
+    upload_slice(ck, name, dst, 0, R, 0, n / R, stage, stage_bytes);
+  }
+
+  // rows [r0, r0 + nr) x columns [c0, c0 + nc) of a 2-D tensor (1-D: one column) into
+  // dst as a dense [nr, nc] block in the model dtype (column slices gathered on the host)
+  void upload_slice(Checkpoint& ck, const std::string& name, void* dst, size_t r0, size_t nr,
+                    size_t c0, size_t nc, void*& stage, size_t& stage_bytes) {
+    const TensorView& t = ck.tensor(name);
     int kind;
     if (t.dtype == "BF16") kind = 0;
     else if (t.dtype == "F16") kind = 1;
     else if (t.dtype == "F32") kind = 2;
     else throw Error(name + ": unsupported dtype " + t.dtype);
+    const size_t es = kind == 2 ? 4 : 2;
+    const size_t R = t.shape.empty() ? 1 : t.shape[0];
+    const size_t C = R ? (t.nbytes / es) / R : 0;
+    if (r0 + nr > R || c0 + nc > C) throw Error(name + ": slice outside the tensor");
+    const uint8_t* src = t.data + (r0 * C + c0) * es;
+    std::vector<uint8_t> tmp;
+    if (nc != C) {
+      tmp.resize(nr * nc * es);
+      for (size_t r = 0; r < nr; ++r)
+        std::memcpy(tmp.data() + r * nc * es, t.data + ((r0 + r) * C + c0) * es, nc * es);
+      src = tmp.data();
+    }
+    const size_t bytes = nr * nc * es, n = nr * nc;
     if (kind == dt_) {
-      hip_check(hipMemcpy(dst, t.data, t.nbytes, hipMemcpyHostToDevice), "weight H2D");
+      hip_check(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice), "weight H2D");
       return;
     }
-    if (stage_bytes < t.nbytes) {
+    if (stage_bytes < bytes) {
       if (stage) (void)hipFree(stage);
-      hip_check(hipMalloc(&stage, t.nbytes), "hipMalloc stage");
-      stage_bytes = t.nbytes;
+      hip_check(hipMalloc(&stage, bytes), "hipMalloc stage");
+      stage_bytes = bytes;
     }
-    hip_check(hipMemcpy(stage, t.data, t.nbytes, hipMemcpyHostToDevice), "weight H2D");
+    hip_check(hipMemcpy(stage, src, bytes, hipMemcpyHostToDevice), "weight H2D");
     k_check(cake_cast16(kind, dt_, stage, dst, n, st_), "cast16");
     hip_check(hipStreamSynchronize(st_), "sync");
   }
 
+  // weights of this rank: all of the model, its pipeline layers, or (tensor parallel) its
+  // slices — q / k / v rows of its heads, o_proj columns of its heads, gate / up rows and
+  // down_proj columns of its intermediate range, lm_head rows of its vocabulary range
+  // (parallel/tensor_parallel.py shard_block / shard_head)
   void load_weights(const std::string& dir) {
     Checkpoint ck(dir);
     const Cfg& c = cfg_;
-    const size_t H = c.H, I = c.I, V = c.V, nq = (size_t)c.nh * c.hd, nk = (size_t)c.nkv * c.hd;
+    const size_t H = c.H, V = c.V, hd = c.hd;
+    const size_t nq = (size_t)lc_.nh * hd, nk = (size_t)lc_.nkv * hd, I = lc_.I;
+    const size_t q0 = (size_t)tp_rank_ * lc_.nh * hd, k0 = (size_t)tp_rank_ * lc_.nkv * hd;
+    const size_t i0 = i0_;
     void* stage = nullptr;
     size_t stage_bytes = 0;
     try {
@@ -620,9 +778,14 @@ class Llama {
         upload(ck, "model.embed_tokens.weight", embed_, V * H, stage, stage_bytes);
         norm_ = dalloc<uint16_t>(H);
         upload(ck, "model.norm.weight", norm_, H, stage, stage_bytes);
-        if (ck.has("lm_head.weight") && !c.tie) {
+        const bool own_head = ck.has("lm_head.weight") && !c.tie;
+        const char* hn = own_head ? "lm_head.weight" : "model.embed_tokens.weight";
+        if (tp_ > 1) {
+          lm_head_ = dalloc<uint16_t>((size_t)lc_.V * H);
+          upload_slice(ck, hn, lm_head_, voff_, lc_.V, 0, H, stage, stage_bytes);
+        } else if (own_head) {
           lm_head_ = dalloc<uint16_t>(V * H);
-          upload(ck, "lm_head.weight", lm_head_, V * H, stage, stage_bytes);
+          upload(ck, hn, lm_head_, V * H, stage, stage_bytes);
         } else {
           lm_head_ = embed_;  // tied embeddings
         }
@@ -635,19 +798,21 @@ class Llama {
         upload(ck, p + "input_layernorm.weight", w.ln1, H, stage, stage_bytes);
         w.wqkv = dalloc<uint16_t>((nq + 2 * nk) * H);
         uint16_t* qkv = reinterpret_cast<uint16_t*>(w.wqkv);
-        upload(ck, p + "self_attn.q_proj.weight", qkv, nq * H, stage, stage_bytes);
-        upload(ck, p + "self_attn.k_proj.weight", qkv + nq * H, nk * H, stage, stage_bytes);
-        upload(ck, p + "self_attn.v_proj.weight", qkv + (nq + nk) * H, nk * H, stage, stage_bytes);
+        upload_slice(ck, p + "self_attn.q_proj.weight", qkv, q0, nq, 0, H, stage, stage_bytes);
+        upload_slice(ck, p + "self_attn.k_proj.weight", qkv + nq * H, k0, nk, 0, H, stage,
+                     stage_bytes);
+        upload_slice(ck, p + "self_attn.v_proj.weight", qkv + (nq + nk) * H, k0, nk, 0, H, stage,
+                     stage_bytes);
         w.wo = dalloc<uint16_t>(H * nq);
-        upload(ck, p + "self_attn.o_proj.weight", w.wo, H * nq, stage, stage_bytes);
+        upload_slice(ck, p + "self_attn.o_proj.weight", w.wo, 0, H, q0, nq, stage, stage_bytes);
         w.ln2 = dalloc<uint16_t>(H);
         upload(ck, p + "post_attention_layernorm.weight", w.ln2, H, stage, stage_bytes);
         w.wgu = dalloc<uint16_t>(2 * I * H);
         uint16_t* gu = reinterpret_cast<uint16_t*>(w.wgu);
-        upload(ck, p + "mlp.gate_proj.weight", gu, I * H, stage, stage_bytes);
-        upload(ck, p + "mlp.up_proj.weight", gu + I * H, I * H, stage, stage_bytes);
+        upload_slice(ck, p + "mlp.gate_proj.weight", gu, i0, I, 0, H, stage, stage_bytes);
+        upload_slice(ck, p + "mlp.up_proj.weight", gu + I * H, i0, I, 0, H, stage, stage_bytes);
         w.wd = dalloc<uint16_t>(H * I);
-        upload(ck, p + "mlp.down_proj.weight", w.wd, H * I, stage, stage_bytes);
+        upload_slice(ck, p + "mlp.down_proj.weight", w.wd, 0, H, i0, I, stage, stage_bytes);
       }
     } catch (...) {
       if (stage) (void)hipFree(stage);
@@ -656,8 +821,9 @@ class Llama {
     if (stage) (void)hipFree(stage);
   }
 
+
   void alloc_state() {
-    const Cfg& c = cfg_;
+    const Cfg& c = lc_;
     kv_session(0);  // session 0: generation / pipeline
     const std::vector<float> f = c.inv_freq();
     inv_freq_ = dalloc<float>(f.size());
@@ -694,11 +860,20 @@ class Llama {
     hop_err_ = dalloc<int>(4);
     hip_check(hipMemset(seq_, 0, sizeof(unsigned int) * 4), "memset");
     hip_check(hipMemset(hop_err_, 0, sizeof(int) * 4), "memset");
+    if (tp_ > 1) {
+      partial_ = dalloc<float>(c.H);
+      ppart_ = dalloc<float>((size_t)S_ * c.H);
+      full_logits_ = dalloc<float>(cfg_.V);
+      ar_seq_ = dalloc<unsigned int>(8);  // [channel][tag, ticket]
+      ar_err_ = dalloc<int>(4);
+      hip_check(hipMemset(ar_seq_, 0, sizeof(unsigned int) * 8), "memset");
+      hip_check(hipMemset(ar_err_, 0, sizeof(int) * 4), "memset");
+    }
     hip_check(hipDeviceSynchronize(), "sync");  // null-stream memsets before st_ work
   }
 
-  uint16_t* kc(int l) const { return cur_.k + (size_t)l * cfg_.nkv * S_ * cfg_.hd; }
-  uint16_t* vc(int l) const { return cur_.v + (size_t)l * cfg_.nkv * S_ * cfg_.hd; }
+  uint16_t* kc(int l) const { return cur_.k + (size_t)l * lc_.nkv * S_ * lc_.hd; }
+  uint16_t* vc(int l) const { return cur_.v + (size_t)l * lc_.nkv * S_ * lc_.hd; }
 
   // KV cache of one session (a master connection of a TCP worker; 0 = generation):
   // allocated on first use, least recently used dropped past kMaxSessions (P4)
@@ -712,7 +887,7 @@ class Llama {
           if (x != 0) { victim = x; break; }
         drop_session(victim);
       }
-      const size_t n = owned_.size() * (size_t)cfg_.nkv * S_ * cfg_.hd;
+      const size_t n = owned_.size() * (size_t)lc_.nkv * S_ * lc_.hd;
       KV kv{dalloc<uint16_t>(n), dalloc<uint16_t>(n)};
       it = kv_.emplace(id, kv).first;
     }
@@ -738,7 +913,7 @@ class Llama {
   // parallel/worker.py _run_ops)
   void forward_host(uint64_t session, const std::vector<int>& layers, int pos0, float* h, int T) {
     hip_check(hipSetDevice(dev_), "hipSetDevice");
-    const Cfg& c = cfg_;
+    const Cfg& c = lc_;
     if (T < 1 || pos0 < 0 || pos0 + T > S_) throw Error("positions exceed the KV cache");
     std::vector<int> sel;
     for (int l : layers) {
@@ -768,7 +943,7 @@ class Llama {
   // ---- prefill
   void grow_prefill(int T) {
     if (T <= pre_T_) return;
-    const Cfg& c = cfg_;
+    const Cfg& c = lc_;
     for (void* p : {x16_, qkv_, att_, pact_, (void*)ptok_}) dfree(p);
     const size_t nq = (size_t)c.nh * c.hd, nk = (size_t)c.nkv * c.hd;
     x16_ = dalloc<uint16_t>((size_t)T * c.H);
@@ -783,7 +958,8 @@ class Llama {
             long long ldc, float* resid, long long ldr, int M, int N, int K, const char* what) {
     const bool gated = epi == kEpiSwiglu;
     const long long Nv = gated ? 2LL * N : N;
-    static const char* names[] = {"store", "resid32", "add16", "swiglu"};
+    static const char* names[] = {"store", "resid32", "add16", "swiglu", "geglu", "partial",
+                                  "store32"};
     auto p = planner_.plan(M, Nv, K, names[epi]);
     const int splits = p.second;
     float* ws = nullptr;
@@ -803,6 +979,13 @@ class Llama {
   // embed -> this rank's layers -> (pipeline: the other ranks' layers, hidden rows
   // handed rank to rank through the peers' IPC-mapped prefill buffers) -> head
   void prefill(const int32_t* prompt, int T) {
+    prefill_body(prompt, T);
+    const Cfg& c = lc_;
+    k_check(cake_gemv_norm_f32(dt_, hidden_ + (size_t)(T - 1) * c.H, norm_, (float)c.eps,
+                               lm_head_, c.H, c.V, logits_, st_), "lm_head");
+  }
+
+  void prefill_body(const int32_t* prompt, int T) {
     const Cfg& c = cfg_;
     if (T > S_) throw Error("prompt longer than max_seq");
     hip_check(hipMemcpyAsync(ptok_buf(T), prompt, sizeof(int32_t) * T, hipMemcpyHostToDevice, st_),
@@ -822,8 +1005,6 @@ class Llama {
       }
       // the last rank wrote its output rows into this rank's hidden_
     }
-    k_check(cake_gemv_norm_f32(dt_, hidden_ + (size_t)(T - 1) * c.H, norm_, (float)c.eps,
-                               lm_head_, c.H, c.V, logits_, st_), "lm_head");
   }
 
   int32_t* ptok_buf(int T) {
@@ -840,7 +1021,7 @@ class Llama {
   }
 
   void prefill_layers(int T, int pos0 = 0, const std::vector<int>* sel = nullptr) {
-    const Cfg& c = cfg_;
+    const Cfg& c = lc_;
     grow_prefill(T);
     const int nq = c.nh * c.hd, nk = c.nkv * c.hd, nqkv = nq + 2 * nk;
     const int Tk = pos0 + T;
@@ -861,10 +1042,20 @@ class Llama {
                                      (long long)T * nq, c.hd, nq};
       k_check(cake_flash_attn(dt_, q, kc(l), vc(l), att_, 1, c.nh, c.nkv, T, Tk, c.hd, strides,
                               scale(), 1, pos0, st_), "flash_attn");
-      gemm(kEpiResid32, att_, nq, w.wo, nq, nullptr, 0, hidden_, c.H, T, c.H, nq, "gemm o");
+      if (tp_ > 1) {  // partial o_proj over this rank's heads, summed over the ranks
+        gemm(kEpiStore32, att_, nq, w.wo, nq, nullptr, 0, ppart_, c.H, T, c.H, nq, "gemm o");
+        dense_allreduce(T);
+      } else {
+        gemm(kEpiResid32, att_, nq, w.wo, nq, nullptr, 0, hidden_, c.H, T, c.H, nq, "gemm o");
+      }
       k_check(cake_rmsnorm(dt_, hidden_, w.ln2, (float)c.eps, T, c.H, x16_, st_), "rmsnorm");
       gemm(kEpiSwiglu, x16_, c.H, w.wgu, c.H, pact_, c.I, nullptr, 0, T, c.I, c.H, "gemm gate|up");
-      gemm(kEpiResid32, pact_, c.I, w.wd, c.I, nullptr, 0, hidden_, c.H, T, c.H, c.I, "gemm down");
+      if (tp_ > 1) {
+        gemm(kEpiStore32, pact_, c.I, w.wd, c.I, nullptr, 0, ppart_, c.H, T, c.H, c.I, "gemm down");
+        dense_allreduce(T);
+      } else {
+        gemm(kEpiResid32, pact_, c.I, w.wd, c.I, nullptr, 0, hidden_, c.H, T, c.H, c.I, "gemm down");
+      }
     }
   }
 
@@ -880,7 +1071,7 @@ class Llama {
       m.top_p = (s.top_p > 0.f && s.top_p < 1.f) ? s.top_p : 0.f;
       m.seed = s.seed;
     }
-    m.fused = m.greedy && (m.penalty == 1.f || m.last_n <= kHeadSelectMaxLastN);
+    m.fused = m.greedy && (m.penalty == 1.f || m.last_n <= kHeadSelectMaxLastN) && tp_ == 1;
     return m;
   }
 
@@ -889,13 +1080,13 @@ class Llama {
     if (m.penalty != 1.f)
       k_check(cake_repeat_penalty(logits_, hist_, hist_len_, m.last_n, m.penalty, st_), "penalty");
     if (m.greedy) {
-      k_check(cake_argmax(logits_, cfg_.V, slot_, st_), "argmax");
+      k_check(cake_argmax(logits_, lc_.V, slot_, st_), "argmax");
     } else {
       const bool restrict = m.top_k > 0 || m.top_p > 0.f;
       if (restrict)
-        k_check(cake_sample_threshold(logits_, cfg_.V, m.temperature, m.top_k, m.top_p, thr_, st_),
+        k_check(cake_sample_threshold(logits_, lc_.V, m.temperature, m.top_k, m.top_p, thr_, st_),
                 "sample_threshold");
-      k_check(cake_gumbel_argmax(logits_, cfg_.V, m.temperature, m.seed, hist_len_,
+      k_check(cake_gumbel_argmax(logits_, lc_.V, m.temperature, m.seed, hist_len_,
                                  restrict ? thr_ : nullptr, slot_, st_), "gumbel_argmax");
     }
     k_check(cake_finalize_token(slot_, tok_, hist_, hist_len_, pos_, S_, st_), "finalize");
@@ -904,7 +1095,7 @@ class Llama {
   // one decode step of this rank: [embed] layers [send, receive] head  (rank 0), or
   // receive, layers, send (pipeline workers); the hop carries [hidden | position]
   void step_body(const Mode& m) {
-    const Cfg& c = cfg_;
+    const Cfg& c = lc_;
     if (!head_) {
       hop_recv();
       step_layers();
@@ -929,7 +1120,7 @@ class Llama {
   }
 
   void step_layers(const std::vector<int>* sel = nullptr) {
-    const Cfg& c = cfg_;
+    const Cfg& c = lc_;
     const int nq = c.nh * c.hd, nk = c.nkv * c.hd;
     const int nl = sel ? (int)sel->size() : (int)layers_.size();
     for (int i = 0; i < nl; ++i) {
@@ -941,16 +1132,30 @@ class Llama {
                             pos_, q_, kc(l), vc(l), S_, st_), "qkv_rope");
       k_check(cake_attn_decode(dt_, q_, kc(l), vc(l), pos_, S_, c.nh, c.nkv, c.hd, scale(), part_,
                                tickets_, attn_out_, st_), "attn_decode");
-      k_check(cake_gemv_x16(dt_, attn_out_, w.wo, nq, c.H, resid_, 1, st_), "o_proj");
+      if (tp_ > 1) {
+        k_check(cake_gemv_x16(dt_, attn_out_, w.wo, nq, c.H, partial_, 0, st_), "o_proj");
+        ar_sum();
+      } else {
+        k_check(cake_gemv_x16(dt_, attn_out_, w.wo, nq, c.H, resid_, 1, st_), "o_proj");
+      }
       const uint16_t* wgu = reinterpret_cast<const uint16_t*>(w.wgu);
       k_check(cake_swiglu(dt_, resid_, w.ln2, (float)c.eps, wgu, wgu + (size_t)c.I * c.H, c.H,
                           c.I, act_, st_), "swiglu");
-      k_check(cake_gemv_x16(dt_, act_, w.wd, c.I, c.H, resid_, 1, st_), "down_proj");
+      if (tp_ > 1) {
+        k_check(cake_gemv_x16(dt_, act_, w.wd, c.I, c.H, partial_, 0, st_), "down_proj");
+        ar_sum();
+      } else {
+        k_check(cake_gemv_x16(dt_, act_, w.wd, c.I, c.H, resid_, 1, st_), "down_proj");
+      }
     }
   }
 
   void step_head(const Mode& m) {
-    const Cfg& c = cfg_;
+    const Cfg& c = lc_;
+    if (tp_ > 1) {
+      head_tp(resid_, m);
+      return;
+    }
     if (m.fused) {
       k_check(cake_head_select(dt_, resid_, norm_, (float)c.eps, lm_head_, c.H, c.V, logits_,
                                hist_, hist_len_, m.penalty != 1.f ? m.last_n : 0, m.penalty,
@@ -1005,6 +1210,11 @@ class Llama {
   // worker rank: serve the master's control messages until it says exit
   void serve() {
     hip_check(hipSetDevice(dev_), "hipSetDevice");
+    if (tp_ > 1) {
+      if (tp_rank_ == 0) throw Error("serve() runs on tensor-parallel workers (rank > 0)");
+      serve_tp();
+      return;
+    }
     if (head_) throw Error("serve() runs on pipeline workers (rank > 0)");
     ensure_graphs(Mode{});
     std::vector<void*> execs(execs_.begin(), execs_.end());
@@ -1116,6 +1326,218 @@ class Llama {
     unhex(peer_next.get("pbuf").as_string(), &np, sizeof(np));
     hip_check(hipIpcOpenMemHandle(&next_inbox_, ni, hipIpcMemLazyEnablePeerAccess), "IpcOpen inbox");
     hip_check(hipIpcOpenMemHandle(&next_pbuf_, np, hipIpcMemLazyEnablePeerAccess), "IpcOpen pbuf");
+  }
+
+  // ---- tensor parallel (one process per GPU, every rank 1/W of every layer)
+  void ar_sum() {
+    k_check(cake_ar_sum(partial_, resid_, lc_.H, 1, ch_sum_.peers.data(), ch_sum_.inbox, ar_seq_,
+                        ar_err_, tp_rank_, tp_, hop_timeout_, st_), "ar_sum");
+  }
+
+  // this rank's lm_head rows -> the global token on every rank (greedy: shard argmax key,
+  // max over ranks; sampled: the full logits gathered, the single-GPU draw on each rank)
+  void head_tp(const float* row, const Mode& m) {
+    const Cfg& c = lc_;
+    k_check(cake_gemv_norm_f32(dt_, row, norm_, (float)c.eps, lm_head_, c.H, c.V, logits_, st_),
+            "lm_head");
+    if (m.greedy) {
+      k_check(cake_select_shard(logits_, c.V, voff_, hist_, hist_len_, m.last_n, m.penalty, 0.f,
+                                0, slot_, st_), "select_shard");
+      k_check(cake_ar_max_key(slot_, ch_key_.peers.data(), ch_key_.inbox, ar_seq_ + 2,
+                              ar_err_ + 1, tp_rank_, tp_, hop_timeout_, st_), "ar_max_key");
+    } else {
+      const int V = cfg_.V;
+      k_check(cake_ar_gather(logits_, voff_, c.V, full_logits_, V, ch_gat_.peers.data(),
+                             ch_gat_.inbox, ar_seq_ + 4, ar_err_ + 2, tp_rank_, tp_,
+                             hop_timeout_, st_), "ar_gather");
+      if (m.penalty != 1.f)
+        k_check(cake_repeat_penalty(full_logits_, hist_, hist_len_, m.last_n, m.penalty, st_),
+                "penalty");
+      const bool restrict = m.top_k > 0 || m.top_p > 0.f;
+      if (restrict)
+        k_check(cake_sample_threshold(full_logits_, V, m.temperature, m.top_k, m.top_p, thr_, st_),
+                "sample_threshold");
+      k_check(cake_gumbel_argmax(full_logits_, V, m.temperature, m.seed, hist_len_,
+                                 restrict ? thr_ : nullptr, slot_, st_), "gumbel_argmax");
+    }
+    k_check(cake_finalize_token(slot_, tok_, hist_, hist_len_, pos_, S_, st_), "finalize");
+  }
+
+  // prefill: partial rows ppart_ [T, H] summed over the ranks into hidden_ — every rank
+  // copies its rows into slot `rank` of every rank's slab (uncached device memory,
+  // IPC-mapped), a barrier, then each sums the W slots; two slab banks, alternating, so
+  // the next all-reduce never overwrites rows a slower rank still sums
+  void dense_allreduce(int T) {
+    const size_t SH = (size_t)S_ * cfg_.H, bytes = sizeof(float) * (size_t)T * cfg_.H;
+    const int bank = slab_bank_;
+    slab_bank_ ^= 1;
+    for (int p = 0; p < tp_; ++p) {
+      float* base = p == tp_rank_ ? slab_ : static_cast<float*>(peer_slab_[p]);
+      hip_check(hipMemcpyAsync(base + ((size_t)bank * tp_ + tp_rank_) * SH, ppart_, bytes,
+                               hipMemcpyDeviceToDevice, st_), "slab copy");
+    }
+    hip_check(hipStreamSynchronize(st_), "sync");
+    tp_barrier();
+    k_check(cake_sum_slices(hidden_, slab_ + (size_t)bank * tp_ * SH, tp_, (long long)SH,
+                            (long long)T * cfg_.H, 1, st_), "sum_slices");
+  }
+
+  // host barrier of the tensor-parallel ranks over the control sockets (star on rank 0)
+  void tp_barrier() {
+    if (tp_rank_ == 0) {
+      for (int fd : peers_) {
+        const Json j = recv_json(fd);
+        if (!j.has("cmd") || j.get("cmd").as_string() != "barrier") throw Error("TP barrier: bad message");
+      }
+      for (int fd : peers_) send_json(fd, msg("barrier"));
+    } else {
+      send_json(ctl_fd_, msg("barrier"));
+      const Json j = recv_json(ctl_fd_);
+      if (!j.has("cmd") || j.get("cmd").as_string() != "barrier") throw Error("TP barrier: bad message");
+    }
+  }
+
+  void sync_tp_workers() {
+    std::string err;
+    for (size_t i = 0; i < peers_.size(); ++i) {
+      try {
+        send_json(peers_[i], msg("sync"));
+        const Json r = recv_json(peers_[i]);
+        if (r.has("ar_err") && r.get("ar_err").as_int() != 0)
+          err = "tensor-parallel rank " + std::to_string(i + 1) + ": all-reduce timed out";
+        if (r.has("error")) err = r.get("error").as_string();
+      } catch (const std::exception& e) {
+        err = e.what();
+      }
+    }
+    int own[3] = {0, 0, 0};
+    hip_check(hipMemcpy(own, ar_err_, sizeof(own), hipMemcpyDeviceToHost), "ar_err");
+    if (own[0] | own[1] | own[2]) err = "tensor-parallel rank 0: all-reduce timed out";
+    if (!err.empty()) throw Error(err);
+  }
+
+  // worker rank: run the generations rank 0 announces, in lock step
+  void serve_tp() {
+    for (;;) {
+      const Json m = recv_json(ctl_fd_);
+      const std::string cmd = m.get("cmd").as_string();
+      if (cmd == "exit") break;
+      if (cmd == "generate") {
+        std::vector<int32_t> prompt;
+        for (const auto& x : m.get("prompt").items()) prompt.push_back((int32_t)x.as_int());
+        CakeEngineSampling smp{};
+        smp.temperature = (float)m.get("temperature").as_double();
+        smp.top_k = (int32_t)m.get("top_k").as_int();
+        smp.top_p = (float)m.get("top_p").as_double();
+        smp.seed = std::strtoull(m.get("seed").as_string().c_str(), nullptr, 10);
+        smp.repeat_penalty = (float)m.get("penalty").as_double();
+        smp.repeat_last_n = (int32_t)m.get("last_n").as_int();
+        const int max_new = (int)m.get("max_new").as_int();
+        run_generation(prompt.data(), (int)prompt.size(), max_new, smp, nullptr, 0, nullptr,
+                       nullptr, nullptr, 0, nullptr, false);
+      } else if (cmd == "sync") {
+        Json r = Json::object();
+        const hipError_t e = hipStreamSynchronize(st_);
+        int errs[3] = {0, 0, 0};
+        (void)hipMemcpy(errs, ar_err_, sizeof(errs), hipMemcpyDeviceToHost);
+        r.set("ok", Json::boolean(e == hipSuccess));
+        r.set("ar_err", Json::integer(errs[0] | errs[1] | errs[2]));
+        if (e != hipSuccess) r.set("error", Json::string(hipGetErrorString(e)));
+        send_json(ctl_fd_, r);
+      } else {
+        throw Error("unknown control message " + cmd);
+      }
+    }
+  }
+
+  // channel inboxes (uncached, hop.hip granules) and the prefill slab, exchanged as IPC
+  // handles through rank 0 (full mesh)
+  void connect_tp(const std::string& addr, double timeout_s) {
+    std::string host;
+    int port = 0;
+    split_host_port(addr, &host, &port);
+    auto alloc = [&](size_t words) {
+      void* p = nullptr;
+      k_check(cake_hop_alloc(words * 8, &p), "hop_alloc");
+      tp_owned_.push_back(p);
+      return p;
+    };
+    ch_sum_.inbox = alloc((size_t)cake_ar_inbox_words(tp_, cfg_.H));
+    ch_key_.inbox = alloc((size_t)cake_ar_inbox_words(tp_, 2));
+    ch_gat_.inbox = alloc(2 * (size_t)cfg_.V);
+    const size_t slab_bytes = sizeof(float) * 2 * (size_t)tp_ * S_ * cfg_.H;
+    void* sp = nullptr;
+    hip_check(hipExtMallocWithFlags(&sp, slab_bytes, hipDeviceMallocUncached), "slab alloc");
+    tp_owned_.push_back(sp);
+    slab_ = static_cast<float*>(sp);
+    void* mine[4] = {ch_sum_.inbox, ch_key_.inbox, ch_gat_.inbox, slab_};
+    Json me = Json::array();
+    for (void* p : mine) {
+      hipIpcMemHandle_t h;
+      hip_check(hipIpcGetMemHandle(&h, p), "IpcGetMemHandle");
+      me.push(Json::string(hex_of(&h, sizeof(h))));
+    }
+    std::vector<Json> table(tp_);
+    if (tp_rank_ == 0) {
+      table[0] = me;
+      const int lfd = tcp_listen(host, port);
+      peers_.assign(tp_ - 1, -1);
+      try {
+        for (int i = 1; i < tp_; ++i) {
+          std::string peer;
+          const int fd = tcp_accept(lfd, &peer);
+          tcp_set_timeout(fd, 0);
+          const Json j = recv_json(fd);
+          const int r = (int)j.get("rank").as_int();
+          if (r < 1 || r >= tp_ || peers_[r - 1] >= 0) throw Error("bad TP rank hello");
+          peers_[r - 1] = fd;
+          table[r] = j.get("h");
+        }
+      } catch (...) {
+        tcp_close(lfd);
+        throw;
+      }
+      tcp_close(lfd);
+      Json all = Json::array();
+      for (const auto& t : table) all.push(t);
+      Json m = Json::object();
+      m.set("table", all);
+      for (int fd : peers_) send_json(fd, m);
+    } else {
+      const auto deadline =
+          std::chrono::steady_clock::now() + std::chrono::duration<double>(timeout_s);
+      for (;;) {
+        try {
+          ctl_fd_ = tcp_connect(host, port, 2.0);
+          break;
+        } catch (const std::exception&) {
+          if (std::chrono::steady_clock::now() > deadline) throw;
+          usleep(200000);
+        }
+      }
+      tcp_set_timeout(ctl_fd_, 0);
+      Json hello = Json::object();
+      hello.set("rank", Json::integer(tp_rank_));
+      hello.set("h", me);
+      send_json(ctl_fd_, hello);
+      const Json m = recv_json(ctl_fd_);
+      for (int r = 0; r < tp_; ++r) table[r] = m.get("table").at(r);
+    }
+    ArChan* chans[3] = {&ch_sum_, &ch_key_, &ch_gat_};
+    for (auto* ch : chans) ch->peers.assign(tp_, nullptr);
+    peer_slab_.assign(tp_, nullptr);
+    for (int r = 0; r < tp_; ++r) {
+      if (r == tp_rank_) continue;
+      for (int k = 0; k < 4; ++k) {
+        hipIpcMemHandle_t h;
+        unhex(table[r].at(k).as_string(), &h, sizeof(h));
+        void* p = nullptr;
+        hip_check(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "IpcOpen");
+        tp_mapped_.push_back(p);
+        if (k < 3) chans[k]->peers[r] = p;
+        else peer_slab_[r] = p;
+      }
+    }
   }
 
   void drop_graphs() {
@@ -1268,6 +1690,17 @@ CAKE_API void cake_engine_drop_session(void* h, uint64_t session) {
   try {
     if (h) static_cast<Llama*>(h)->drop_session(session);
   } catch (const std::exception&) {
+  }
+}
+
+CAKE_API void* cake_engine_open_tp(const char* model_dir, const CakeEngineOpts* opts,
+                                   const CakeTPOpts* tp, char* err, int32_t errlen) {
+  try {
+    if (!model_dir || !opts || !tp) throw cake::Error("null argument");
+    return new Llama(model_dir, *opts, nullptr, nullptr, tp);
+  } catch (const std::exception& e) {
+    cake::put_err(err, errlen, e.what());
+    return nullptr;
   }
 }
 

@@ -35,6 +35,18 @@ struct CakePipeOpts {
   double connect_timeout_s;  // workers: how long to retry reaching rank 0
 };
 
+// Tensor parallel over one process per GPU: every rank holds 1/world of every layer (its
+// query / KV heads, its slice of the intermediate rows) and of the vocabulary; the
+// decode step's two all-reduces per layer and the token selection are device-side
+// (allreduce.hip, IPC-mapped inboxes) inside each rank's captured graph; prefill sums go
+// through IPC-mapped slabs.  Rank 0 generates; the others serve (cake_engine_serve).
+struct CakeTPOpts {
+  int32_t rank, world;       // world <= 8
+  const char* master_addr;   // "host:port" rank 0 listens on
+  double timeout_s;          // all-reduce wait bound (error word instead of a hang)
+  double connect_timeout_s;
+};
+
 struct CakeEngineSampling {
   float temperature;        // <= 0: greedy
   int32_t top_k;            // 0: off
@@ -59,6 +71,9 @@ void* cake_engine_open(const char* model_dir, const struct CakeEngineOpts* opts,
 // Pipeline rank (see CakePipeOpts): loads only its layer shard, joins the ring.
 void* cake_engine_open_pp(const char* model_dir, const struct CakeEngineOpts* opts,
                           const struct CakePipeOpts* pipe, char* err, int32_t errlen);
+// Tensor-parallel rank (see CakeTPOpts).
+void* cake_engine_open_tp(const char* model_dir, const struct CakeEngineOpts* opts,
+                          const struct CakeTPOpts* tp, char* err, int32_t errlen);
 // Workers (rank > 0): serve rank 0's control messages until it closes; 0 or an error.
 int32_t cake_engine_serve(void* engine, char* err, int32_t errlen);
 // TCP worker (topology node): only `layers` (global indices), no embedding / head.

@@ -187,9 +187,46 @@ __global__ __launch_bounds__(256) void cast16_kernel(const void* __restrict__ sr
   }
 }
 
+// Tensor-parallel prefill all-reduce (native engine): out (+)= sum of the W slices
+// src[w * stride .. + n) that the ranks wrote into this rank's (uncached) slab.
+__global__ __launch_bounds__(256) void sum_slices_kernel(float* __restrict__ out,
+                                                         const float* __restrict__ src, int W,
+                                                         long long stride, long long n,
+                                                         int accumulate) {
+  for (long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * 4; i < n;
+       i += (long long)gridDim.x * 256 * 4) {
+    if (i + 4 <= n) {
+      float4 a = accumulate ? *reinterpret_cast<const float4*>(out + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int w = 0; w < W; ++w) {
+        const float4 v = *reinterpret_cast<const float4*>(src + w * stride + i);
+        a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+      }
+      *reinterpret_cast<float4*>(out + i) = a;
+    } else {
+      for (long long j = i; j < n; ++j) {
+        float a = accumulate ? out[j] : 0.f;
+        for (int w = 0; w < W; ++w) a += src[w * stride + j];
+        out[j] = a;
+      }
+    }
+  }
+}
+
 }  // namespace cake
 
 using namespace cake;
+
+CAKE_API int cake_sum_slices(float* out, const float* src, int W, long long stride, long long n,
+                             int accumulate, hipStream_t st) {
+  if (W < 1 || n < 0 || stride < n || (stride % 4) || ((uintptr_t)out % 16) || ((uintptr_t)src % 16))
+    return (int)hipErrorInvalidValue;
+  if (n == 0) return 0;
+  long long g = (n / 4 + 255) / 256;
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(sum_slices_kernel, dim3((unsigned)g), dim3(256), 0, st, out, src, W, stride, n,
+                     accumulate);
+  return (int)hipGetLastError();
+}
 
 CAKE_API int cake_stream_read(const void* p, size_t bytes, int blocks, unsigned int* sink,
                               hipStream_t st) {

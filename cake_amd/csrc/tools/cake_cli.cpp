@@ -152,6 +152,7 @@ bool in_choices(const std::string& v, const char* choices) {
 struct EngineApi {
   void* (*open)(const char*, const CakeEngineOpts*, char*, int32_t);
   void* (*open_pp)(const char*, const CakeEngineOpts*, const CakePipeOpts*, char*, int32_t);
+  void* (*open_tp)(const char*, const CakeEngineOpts*, const CakeTPOpts*, char*, int32_t);
   int32_t (*serve)(void*, char*, int32_t);
   int32_t (*generate)(void*, const int32_t*, int32_t, int32_t, const CakeEngineSampling*,
                       const int32_t*, int32_t, cake_engine_token_cb, void*, int32_t*, int32_t,
@@ -168,7 +169,8 @@ bool native_text_eligible(cake::PyArgs& o, bool text, bool worker, bool has_topo
                       o["metrics"].kind == PyArg::kNone &&
                       (o["dtype"].kind == PyArg::kNone || is("dtype", "f16") || is("dtype", "bf16"));
   if (is("transport", "rccl"))  // one process per GPU (torchrun env): layer-sharded pipeline
-    return common && is("parallel", "pp") && is("hop", "ipc") && std::getenv("WORLD_SIZE");
+    return common && std::getenv("WORLD_SIZE") &&  // (pp, device hops) or tensor parallel
+           ((is("parallel", "pp") && is("hop", "ipc")) || is("parallel", "tp"));
   return common && !worker && !has_topology && is("transport", "tcp");
 }
 
@@ -211,13 +213,15 @@ int run_native_text(cake::PyArgs& o) {
   api.close = reinterpret_cast<decltype(api.close)>(dlsym(h, "cake_engine_close"));
   api.open_pp = reinterpret_cast<decltype(api.open_pp)>(dlsym(h, "cake_engine_open_pp"));
   api.serve = reinterpret_cast<decltype(api.serve)>(dlsym(h, "cake_engine_serve"));
-  if (!api.open || !api.generate || !api.close || !api.open_pp || !api.serve) {
+  api.open_tp = reinterpret_cast<decltype(api.open_tp)>(dlsym(h, "cake_engine_open_tp"));
+  if (!api.open || !api.generate || !api.close || !api.open_pp || !api.serve || !api.open_tp) {
     std::fprintf(stderr, "cake-cli: engine symbols missing in %s\n", lib.c_str());
     return 1;
   }
   // --transport rccl: this process is pipeline rank RANK of WORLD_SIZE (torchrun env);
   // the engine's control plane listens on MASTER_PORT + 1 (torchrun's store owns the port)
   const bool pipe = o["transport"].value == "rccl";
+  const bool tp = pipe && o["parallel"].value == "tp";
   const int rank = pipe ? env_int("RANK", 0) : 0, world = pipe ? env_int("WORLD_SIZE", 1) : 1;
   const char* maddr = std::getenv("MASTER_ADDR");
   const std::string ctl = std::string(maddr ? maddr : "127.0.0.1") + ":" +
@@ -232,8 +236,10 @@ int run_native_text(cake::PyArgs& o) {
     CakeEngineOpts eo{(int32_t)num("max_seq_len", 4096), o["dtype"].value == "bf16" ? 0 : 1,
                       env_int("LOCAL_RANK", rank), 1};
     CakePipeOpts po{rank, world, ctl.c_str(), o["hop_dtype"].value == "bf16" ? 1 : 0, 60.0, 600.0};
+    CakeTPOpts to{rank, world, ctl.c_str(), 60.0, 600.0};
     char err[1024] = {0};
-    void* eng = api.open_pp(ctx.model.c_str(), &eo, &po, err, sizeof(err));
+    void* eng = tp ? api.open_tp(ctx.model.c_str(), &eo, &to, err, sizeof(err))
+                   : api.open_pp(ctx.model.c_str(), &eo, &po, err, sizeof(err));
     if (!eng) {
       std::fprintf(stderr, "cake-cli: rank %d: %s\n", rank, err);
       return 1;
@@ -267,7 +273,9 @@ int run_native_text(cake::PyArgs& o) {
   char err[1024] = {0};
   const auto t0 = std::chrono::steady_clock::now();
   CakePipeOpts po{0, world, ctl.c_str(), o["hop_dtype"].value == "bf16" ? 1 : 0, 60.0, 600.0};
-  void* eng = world > 1 ? api.open_pp(ctx.model.c_str(), &eo, &po, err, sizeof(err))
+  CakeTPOpts to{0, world, ctl.c_str(), 60.0, 600.0};
+  void* eng = world > 1 ? (tp ? api.open_tp(ctx.model.c_str(), &eo, &to, err, sizeof(err))
+                              : api.open_pp(ctx.model.c_str(), &eo, &po, err, sizeof(err)))
                         : api.open(ctx.model.c_str(), &eo, err, sizeof(err));
   if (!eng) {
     std::fprintf(stderr, "cake-cli: native engine: %s\n", err);

@@ -32,6 +32,11 @@ class PipeOpts(C.Structure):
                 ("connect_timeout_s", C.c_double)]
 
 
+class TPOpts(C.Structure):
+    _fields_ = [("rank", C.c_int32), ("world", C.c_int32), ("master_addr", C.c_char_p),
+                ("timeout_s", C.c_double), ("connect_timeout_s", C.c_double)]
+
+
 class EngineSampling(C.Structure):
     _fields_ = [("temperature", C.c_float), ("top_k", C.c_int32), ("top_p", C.c_float),
                 ("seed", C.c_uint64), ("repeat_penalty", C.c_float),
@@ -59,6 +64,9 @@ def lib() -> C.CDLL:
         L.cake_engine_open_pp.argtypes = [C.c_char_p, C.POINTER(EngineOpts), C.POINTER(PipeOpts),
                                           C.c_char_p, I]
         L.cake_engine_open_pp.restype = P
+        L.cake_engine_open_tp.argtypes = [C.c_char_p, C.POINTER(EngineOpts), C.POINTER(TPOpts),
+                                          C.c_char_p, I]
+        L.cake_engine_open_tp.restype = P
         L.cake_engine_serve.argtypes = [P, C.c_char_p, I]
         L.cake_engine_serve.restype = I
         L.cake_engine_rank_info.argtypes = [P, C.POINTER(C.c_int32)]
@@ -98,16 +106,24 @@ class NativeLlama:
     def __init__(self, model_dir: str | Path, *, max_seq: int = 4096, dtype: str = "bf16",
                  device: int = 0, steps_per_graph: int = 1, rank: int = 0, world: int = 1,
                  master_addr: str = "127.0.0.1:29517", hop_bf16: bool = False,
-                 hop_timeout_s: float = 30.0, connect_timeout_s: float = 600.0):
-        """world > 1: one layer-sharded pipeline rank (rank 0 generates; the others call
-        :meth:`serve`).  Every rank of one pipeline must be constructed concurrently."""
+                 hop_timeout_s: float = 30.0, connect_timeout_s: float = 600.0,
+                 tp: bool = False):
+        """world > 1: one rank of a layer-sharded pipeline, or with tp=True of a tensor-
+        parallel group (rank 0 generates; the others call :meth:`serve`).  Every rank of
+        one group must be constructed concurrently."""
         if dtype not in ("bf16", "f16"):
             raise ValueError("native engine dtype: bf16 or f16")
         opts = EngineOpts(int(max_seq), 0 if dtype == "bf16" else 1, int(device),
                           max(1, int(steps_per_graph)))
         err = C.create_string_buffer(1024)
         self._h = None
-        if world > 1:
+        if world > 1 and tp:
+            self._addr = master_addr.encode()
+            o = TPOpts(int(rank), int(world), self._addr, float(hop_timeout_s),
+                       float(connect_timeout_s))
+            self._h = lib().cake_engine_open_tp(str(model_dir).encode(), C.byref(opts),
+                                                C.byref(o), err, len(err))
+        elif world > 1:
             self._addr = master_addr.encode()
             pipe = PipeOpts(int(rank), int(world), self._addr, int(bool(hop_bf16)),
                             float(hop_timeout_s), float(connect_timeout_s))
