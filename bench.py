@@ -171,7 +171,11 @@ def measure_single(a, model_name: str, steps: int, warmup: int, dump_tokens=None
     torch.cuda.set_device(0)
     dtype = parse_dtype(a.dtype)
     t0 = time.time()
-    model = random_model(model_name, "cuda:0", dtype, max_seq=a.max_seq)
+    # the KV cache holds the prompt and every warm-up / timed step (a longer run than
+    # --max-seq allows would stop early and time fewer steps than it reports)
+    need = a.prompt_len + warmup + steps + 16 * max(1, a.steps_per_graph)
+    max_seq = max(a.max_seq, -(-need // 64) * 64)
+    model = random_model(model_name, "cuda:0", dtype, max_seq=max_seq)
     torch.cuda.synchronize()
     load_s = time.time() - t0
     print(f"[bench] model {model_name} random-init in {load_s:.1f}s, "
@@ -194,6 +198,8 @@ def measure_single(a, model_name: str, steps: int, warmup: int, dump_tokens=None
     st = run_decode(dec, steps)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    if len(st.tokens) != steps:
+        raise RuntimeError(f"timed {len(st.tokens)} decode steps, expected {steps}")
     if dump_tokens:
         with open(dump_tokens, "w") as f:
             json.dump([dec.bufs.hist[:int(dec.bufs.hist_len.item())].tolist()], f)
