@@ -240,7 +240,7 @@ struct GemmPlanner {
     if (!f) return;
     try {
       const Json j = Json::parse(read_file(path));
-      static const int known[] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 11, 12, 13};
+      static const int known[] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 11, 12, 13, 14, 15, 16, 17, 18, 19};
       for (const auto& e : j.get("entries").items()) {
         const int cfg = (int)e.get("cfg").as_int();
         if (std::find(std::begin(known), std::end(known), cfg) == std::end(known)) continue;

@@ -165,16 +165,27 @@ template <int DT, int EPI, int NF> struct EpiOps {
   float bias[PRE ? (GATED ? 2 * CPL : CPL) : 1];
   float res[2][RES ? CPL : 1];
 
+  static constexpr int VW = CPL % 8 == 0 ? 8 : 4;  // vector width (16 / 8-byte accesses)
+
   // 16-bit values [n0, n0 + CPL) of row p (columns < n valid) as f32
   __device__ __forceinline__ static void load16(const uint16_t* p, int n0, int n, bool vec,
                                                 float* o) {
     if (vec) {
+      if constexpr (VW == 8) {
 #pragma unroll
-      for (int c = 0; c < CPL; c += 8) {
-        float f[8];
-        unpack8<DT>(*reinterpret_cast<const uint4*>(p + n0 + c), f);
+        for (int c = 0; c < CPL; c += 8) {
+          float f[8];
+          unpack8<DT>(*reinterpret_cast<const uint4*>(p + n0 + c), f);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o[c + e] = f[e];
+          for (int e = 0; e < 8; ++e) o[c + e] = f[e];
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < CPL; c += 4) {
+          const uint2 v = *reinterpret_cast<const uint2*>(p + n0 + c);
+          o[c] = to_f32<DT>((uint16_t)v.x); o[c + 1] = to_f32<DT>((uint16_t)(v.x >> 16));
+          o[c + 2] = to_f32<DT>((uint16_t)v.y); o[c + 3] = to_f32<DT>((uint16_t)(v.y >> 16));
+        }
       }
     } else {
 #pragma unroll
@@ -191,7 +202,7 @@ template <int DT, int EPI, int NF> struct EpiOps {
         return;
       }
       const int n0 = GATED ? vcol0 / 2 + ec : vcol0 + ec;
-      const bool vec = CPL % 8 == 0 && n0 + CPL <= g.N && (n0 & 7) == 0 && (!GATED || (g.half & 7) == 0);
+      const bool vec = n0 + CPL <= g.N && (n0 & (VW - 1)) == 0 && (!GATED || (g.half & (VW - 1)) == 0);
       load16(g.bias, n0, g.N, vec, bias);
       if constexpr (GATED) load16(g.bias + g.half, n0, g.N, vec, bias + CPL);
     }
@@ -202,11 +213,33 @@ template <int DT, int EPI, int NF> struct EpiOps {
     if constexpr (RES) {
       const int n0 = vcol0 + (lane & 3) * CPL;
       if (m >= g.M) return;
-      const bool vec = CPL % 8 == 0 && n0 + CPL <= g.N && ((g.ldr | n0) & 7) == 0;
+      const bool vec = n0 + CPL <= g.N && ((g.ldr | n0) & (VW - 1)) == 0;
       load16(g.r16 + (size_t)m * g.ldr, n0, g.N, vec, res[B]);
     }
   }
 };
+
+// CPL 16-bit outputs of one lane: 16-byte stores (8-byte when CPL % 8 != 0: the 80-column
+// wave tiles), element stores at the right edge (n valid columns) or misaligned rows
+// (align = row stride | first column, in elements)
+template <int CPL>
+__device__ __forceinline__ void store16(uint16_t* dst, const uint16_t* v, bool full,
+                                        long long align, int n) {
+  constexpr int VW = CPL % 8 == 0 ? 8 : 4;
+  if (full && (align & (VW - 1)) == 0) {
+    if constexpr (CPL % 8 == 0) {
+#pragma unroll
+      for (int c = 0; c < CPL; c += 8)
+        *reinterpret_cast<uint4*>(dst + c) = *reinterpret_cast<const uint4*>(v + c);
+    } else {
+#pragma unroll
+      for (int c = 0; c < CPL; c += 4)
+        *reinterpret_cast<uint2*>(dst + c) = *reinterpret_cast<const uint2*>(v + c);
+    }
+  } else {
+    for (int c = 0; c < CPL; ++c) if (c < n) dst[c] = v[c];
+  }
+}
 
 // One 16-row strip of a wave's output (NF 16x16 accumulator tiles = NF*16 virtual
 // columns starting at vcol0), staged through the wave's LDS slice stg and written
@@ -258,14 +291,7 @@ __device__ __forceinline__ void epi_strip(const GemmArgs& g, const cf32x4 (&tile
           else y = a * gelu_tanh(b);
           outv[c] = from_f32<DT>(y);
         }
-        uint16_t* dst = g.c + (size_t)m * g.ldc;
-        if (CPL % 8 == 0 && f0 + CPL <= g.N && ((g.ldc | f0) & 7) == 0) {
-#pragma unroll
-          for (int c = 0; c + 7 < CPL; c += 8)
-            *reinterpret_cast<uint4*>(dst + f0 + c) = *reinterpret_cast<const uint4*>(outv + c);
-        } else {
-          for (int c = 0; c < CPL; ++c) if (f0 + c < g.N) dst[f0 + c] = outv[c];
-        }
+        store16<CPL>(g.c + (size_t)m * g.ldc + f0, outv, f0 + CPL <= g.N, g.ldc | f0, g.N - f0);
       } else {
         const int n0c = vcol0 + ec;
         float v[CPL];
@@ -309,14 +335,7 @@ __device__ __forceinline__ void epi_strip(const GemmArgs& g, const cf32x4 (&tile
           uint16_t outv[CPL];
 #pragma unroll
           for (int c = 0; c < CPL; ++c) outv[c] = from_f32<DT>(v[c]);
-          uint16_t* dst = g.c + (size_t)m * g.ldc + n0c;
-          if (CPL % 8 == 0 && full && ((g.ldc | n0c) & 7) == 0) {
-#pragma unroll
-            for (int c = 0; c + 7 < CPL; c += 8)
-              *reinterpret_cast<uint4*>(dst + c) = *reinterpret_cast<const uint4*>(outv + c);
-          } else {
-            for (int c = 0; c < CPL; ++c) if (n0c + c < g.N) dst[c] = outv[c];
-          }
+          store16<CPL>(g.c + (size_t)m * g.ldc + n0c, outv, full, g.ldc | n0c, g.N - n0c);
         }
       }
     }
@@ -339,7 +358,9 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(GemmArgs g) {
   constexpr int IPW = ROWS / 8 / NWAVE;        // DMA wave-instructions per wave per k-step
   constexpr int BUF = ROWS * 128;              // bytes per LDS buffer
   static_assert(ROWS % (8 * NWAVE) == 0 && BM % 16 == 0 && BN % 32 == 0, "tile geometry");
-  static_assert(WTM % 16 == 0 && WTN % 32 == 0, "wave tile geometry");
+  static_assert(WTM % 16 == 0 && WTN % 16 == 0, "wave tile geometry");
+  static_assert(WTN % 32 == 0 || !(EPI == kEpiSwiglu || EPI == kEpiGeglu),
+                "gated epilogues pair 16-column blocks within a wave");
   constexpr int STG_LD = WTN + 4;              // epilogue staging row stride (floats)
   constexpr int STG = 16 * STG_LD * 4;         // bytes per wave
   constexpr int LDS_BYTES = (NS * BUF > NWAVE * STG) ? NS * BUF : NWAVE * STG;
@@ -641,7 +662,10 @@ using namespace cake;
 // are the non-interleaved forms kept for A/B; a 4-wave 256x256 tile (128x128
 // per wave; with or without the interleaved schedule: 0.5x of tile 5), an 8-phase
 // staggered-wave-group 256x256 tile (0.74x of tile 5, profiles/r2_gemm_8phase_rejected.jsonl)
-// and s_setprio measured slower / neutral and were dropped.
+// and s_setprio measured slower / neutral and were dropped.  14-19: 160-column tiles, whose
+// grids fill the 256 CUs exactly on the SD widths (640 / 1280 = 4 / 8 x 160: 2048 x 1280 at
+// 64 x 160 and 8192 x 640 at 128 x 160 are 256 tiles) at a higher operand reuse per tile
+// than 64 x 64 (45.7 / 71 FLOP per staged byte against 32).
 #define CAKE_GEMM_CFGS(X)    \
   X(0, 128, 128, 2, 2, 2, 6) \
   X(1, 64, 128, 1, 4, 2, 6)  \
@@ -654,7 +678,13 @@ using namespace cake;
   X(8, 128, 128, 2, 2, 2, 2) \
   X(11, 256, 256, 2, 4, 2, 0) \
   X(12, 64, 128, 1, 4, 3, 6) \
-  X(13, 64, 64, 2, 2, 4, 6)
+  X(13, 64, 64, 2, 2, 4, 6)  \
+  X(14, 64, 160, 2, 2, 2, 6) \
+  X(15, 64, 160, 4, 1, 2, 6) \
+  X(16, 128, 160, 4, 1, 2, 6) \
+  X(17, 128, 160, 2, 2, 2, 6) \
+  X(18, 64, 160, 2, 2, 3, 6) \
+  X(19, 128, 160, 2, 2, 3, 6)
 
 static inline void cfg_dims(int cfg, int& bm, int& bn) {
 #define X(id, BM, BN, WM, WN, NS, PR) if (cfg == id) { bm = BM; bn = BN; return; }
@@ -668,14 +698,24 @@ CAKE_API int cake_gemm_tile(int cfg, int* bm, int* bn) {
   return *bm > 0 ? 0 : (int)hipErrorInvalidValue;
 }
 
+// the gated epilogues pair 16-column gate / up blocks inside one wave: 32-column multiples
+template <int EPI>
+constexpr bool gated_ok(int wave_cols) {
+  return wave_cols % 32 == 0 || !(EPI == kEpiSwiglu || EPI == kEpiGeglu);
+}
+
 template <int DT, int EPI>
 static int launch_gemm(int cfg, dim3 grid, hipStream_t st, const GemmArgs& g) {
 
 #define X(id, BM, BN, WM, WN, NS, PR)                                                        \
   if (cfg == id) {                                                                           \
-    hipLaunchKernelGGL((gemm_kernel<DT, BM, BN, WM, WN, NS, EPI, PR>), grid, dim3(64 * WM * WN), \
-                       0, st, g);                                                            \
-    return (int)hipGetLastError();                                                          \
+    if constexpr (gated_ok<EPI>(BN / WN)) {                                                  \
+      hipLaunchKernelGGL((gemm_kernel<DT, BM, BN, WM, WN, NS, EPI, PR>), grid,               \
+                         dim3(64 * WM * WN), 0, st, g);                                      \
+      return (int)hipGetLastError();                                                        \
+    } else {                                                                                 \
+      return (int)hipErrorInvalidValue;                                                      \
+    }                                                                                        \
   }
   CAKE_GEMM_CFGS(X)
 #undef X

@@ -24,14 +24,18 @@ _DT = {torch.bfloat16: 0, torch.float16: 1}
 # (BM, BN) of the kernel's tile configurations (gemm.hip CAKE_GEMM_CFGS)
 CFG_TILES = {0: (128, 128), 1: (64, 128), 2: (256, 128), 3: (128, 256), 4: (64, 64),
              5: (256, 256), 6: (256, 128), 7: (128, 128), 8: (128, 128), 11: (256, 256),
-             12: (64, 128), 13: (64, 64)}
-_SLOTS = {0: 2, 1: 2, 2: 1, 3: 1, 4: 4, 5: 1, 6: 1, 7: 1, 8: 2, 11: 1, 12: 2, 13: 2}  # WGs/CU
+             12: (64, 128), 13: (64, 64), 14: (64, 160), 15: (64, 160), 16: (128, 160),
+             17: (128, 160), 18: (64, 160), 19: (128, 160)}
+_SLOTS = {0: 2, 1: 2, 2: 1, 3: 1, 4: 4, 5: 1, 6: 1, 7: 1, 8: 2, 11: 1, 12: 2, 13: 2,
+          14: 2, 15: 2, 16: 1, 17: 1, 18: 1, 19: 1}  # WGs/CU
+# 80-column wave tiles (two waves across the 160 columns): no gated epilogue
+NO_GATED = {14, 17, 18, 19}
 # relative per-tile throughput (measured per-config sweep,
 # profiles/r2_gemm_sweep_agpr.jsonl): the AGPR-accumulator 128x128 tile (0) for most
 # shapes, the 8-wave 256x256 tile (11) where its tiles fill the chip, 64-wide tiles
 # (1, 4) for short M
 _EFF = {0: 1.0, 1: 0.8, 2: 0.8, 3: 0.8, 4: 0.7, 5: 1.2, 6: 0.95, 7: 0.9, 8: 0.9, 11: 1.1,
-        12: 0.8, 13: 0.7}
+        12: 0.8, 13: 0.7, 14: 0.8, 15: 0.7, 16: 0.9, 17: 0.9, 18: 0.8, 19: 0.9}
 NUM_CUS = 256
 _bound = False
 _plans: dict = {}

@@ -21,25 +21,31 @@ SHAPES = [  # name, M, N (output features), K, epi
     ("8b_down_t512", 512, 4096, 14336, "resid32"),
     ("8b_qkv_t128", 128, 6144, 4096, "store"), ("8b_down_t32", 32, 4096, 14336, "resid32"),
     ("70b_qkv_t2048", 2048, 10240, 8192, "store"), ("70b_gateup_t2048", 2048, 28672, 8192, "swiglu"),
-    ("sdxl_qkv_4096tok", 8192, 1920, 640, "store"), ("sdxl_ff_in_4096tok", 8192, 5120, 640, "geglu"),
+    ("sdxl_qkv_4096tok", 8192, 1920, 640, "store"), ("sdxl_ff_in_4096tok", 8192, 2560, 640, "geglu"),
     ("sdxl_ff_out_4096tok", 8192, 640, 2560, "add16"), ("sdxl_qkv_1024tok", 2048, 3840, 1280, "store"),
-    ("sdxl_ff_in_1024tok", 2048, 10240, 1280, "geglu"), ("sd15_qkv_4096tok", 8192, 960, 320, "store"),
+    ("sdxl_ff_in_1024tok", 2048, 5120, 1280, "geglu"), ("sd15_qkv_4096tok", 8192, 960, 320, "store"),
     ("sdxl_attn_out_1024tok", 2048, 1280, 1280, "add16"), ("sdxl_ff_out_1024tok", 2048, 1280, 5120, "add16"),
     ("sdxl_attn_out_4096tok", 8192, 640, 640, "add16"), ("sdxl_q_1024tok", 2048, 1280, 1280, "store"),
-    ("sd15_ff_in_4096tok", 8192, 2560, 320, "geglu"), ("sd15_ff_out_4096tok", 8192, 320, 1280, "add16"),
+    ("sd15_ff_in_4096tok", 8192, 1280, 320, "geglu"), ("sd15_ff_out_4096tok", 8192, 320, 1280, "add16"),
     ("square_4096", 4096, 4096, 4096, "store"), ("square_8192", 8192, 8192, 8192, "store"),
 ]
 
 
+INNER = 1
+
+
 def timeit(fn, reps=20):
+    """Median over reps of (event time of INNER back-to-back calls) / INNER: INNER > 1
+    amortises the event / launch overhead that dominates a single ~20 us kernel."""
     ts = []
     for _ in range(reps):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
-        fn()
+        for _ in range(INNER):
+            fn()
         b.record()
         b.synchronize()
-        ts.append(a.elapsed_time(b))
+        ts.append(a.elapsed_time(b) / INNER)
     ts.sort()
     return ts[len(ts) // 2]
 
@@ -49,8 +55,12 @@ def main():
     ap.add_argument("--sweep", action="store_true")
     ap.add_argument("--only", default=None)
     ap.add_argument("--cfgs", default=None, help="comma list: time each cfg (splits 1)")
+    ap.add_argument("--inner", type=int, default=1, help="back-to-back calls per timing")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f16"])
     a = ap.parse_args()
-    dt = torch.bfloat16
+    global INNER
+    INNER = max(1, a.inner)
+    dt = torch.bfloat16 if a.dtype == "bf16" else torch.float16
     for name, M, N, K, epi in SHAPES:
         if a.only and a.only not in name:
             continue
@@ -108,6 +118,8 @@ def main():
             per = {}
             for _ in range(3):
                 for cfg in [int(c) for c in a.cfgs.split(",")]:
+                    if gated and cfg in G.NO_GATED:
+                        continue
                     t = timeit(lambda: ours(cfg, 1), reps=10)
                     per[cfg] = min(per.get(cfg, 1e9), t)
             rec["per_cfg_tflops"] = {c: round(flops / t / 1e9, 1) for c, t in per.items()}

@@ -1,0 +1,152 @@
+"""Measured GEMM plans for the exact linears of one UNet step (SDXL 1024^2 / SD 1.5 512^2, CFG
+batch 2): record every (M, weight rows, K, epilogue) that gemm.linear plans during one eager
+UNet forward, time every tile configuration (and split-K where the grid is small) on that
+shape, and merge the winners into cake_amd/ops/gemm_tuned.json.
+
+    python scripts/tune_sd_gemm.py [--versions xl,v1-5] [--write OUT.json] > profiles/...jsonl
+
+Timing: INNER launches captured in one hipGraph, median replay time / INNER (GPU time only: host
+launch overhead would otherwise hide the differences between tiles on ~15 us kernels).
+"""
+import argparse
+import collections
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from cake_amd.ops import gemm as G  # noqa: E402
+
+INNER, REPS = 10, 10
+TUNED = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "cake_amd",
+                     "ops", "gemm_tuned.json")
+
+
+def record_shapes(version, dt):
+    from cake_amd.models.sd.config import get_config
+    from cake_amd.models.sd.unet import UNet2DConditionModel
+    from cake_amd.models.sd.weights import random_component
+    cfg = get_config(version)
+    dev = torch.device("cuda:0")
+    w = random_component("unet", cfg, dev, dt)
+    unet = UNet2DConditionModel(cfg.unet)
+    x = torch.randn(2, 4, cfg.height // 8, cfg.width // 8, device=dev, dtype=dt)
+    ctx = torch.randn(2, 77, cfg.unet.cross_attention_dim, device=dev, dtype=dt)
+    tbuf = torch.full((), 999.0, device=dev)
+    kv = {}
+    with torch.no_grad():
+        unet.forward(w, x, tbuf, ctx, kv)  # first call: cross-attention k/v cache filled
+        torch.cuda.synchronize()
+        seen = collections.Counter()
+        orig = G.plan
+
+        def spy(M, Nv, K, epi="store"):
+            seen[(M, Nv, K, epi)] += 1
+            return orig(M, Nv, K, epi)
+        G.plan = spy
+        try:
+            unet.forward(w, x, tbuf, ctx, kv)
+        finally:
+            G.plan = orig
+        torch.cuda.synchronize()
+    del w, unet
+    torch.cuda.empty_cache()
+    return seen
+
+
+def timeit(fn):
+    """GPU time per call: INNER calls captured in one hipGraph, median replay / INNER (no
+    host launch cost in the number, as inside the UNet step's graph)."""
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(INNER):
+            fn()
+    g.replay()
+    ts = []
+    for _ in range(REPS):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        g.replay()
+        b.record()
+        b.synchronize()
+        ts.append(a.elapsed_time(b) / INNER)
+    del g
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
+def tune(M, Nv, K, epi, dt):
+    gated = epi in ("swiglu", "geglu")
+    N = Nv // 2 if gated else Nv
+    x = (torch.randn(M, K, device="cuda") * 0.5).to(dt)
+    w = (torch.randn(Nv, K, device="cuda") * K ** -0.5).to(dt)
+    b = (torch.randn(Nv, device="cuda") * 0.1).to(dt)
+    r = None
+    if epi in ("resid32", "store32"):
+        r = torch.zeros(M, N, device="cuda")
+    elif epi == "add16":
+        r = torch.randn(M, N, device="cuda").to(dt)
+
+    def run(cfg, splits):
+        return G.linear(x, w, b, epi=epi, resid=r, cfg=cfg, splits=splits)
+    cur = G.plan(M, Nv, K, epi)
+    res = {}
+    for cfg, (bm, bn) in G.CFG_TILES.items():
+        if gated and cfg in getattr(G, "NO_GATED", ()):
+            continue
+        tiles = -(-M // bm) * -(-Nv // bn)
+        for splits in (1, 2, 4):
+            if splits > 1 and (tiles * splits > 2 * G.NUM_CUS or K // splits < 256):
+                continue
+            try:
+                run(cfg, splits)
+                res[(cfg, splits)] = timeit(lambda: run(cfg, splits))
+            except Exception:  # noqa: BLE001  (a config the shape cannot take)
+                continue
+    if cur not in res:
+        run(*cur)
+        res[cur] = timeit(lambda: run(*cur))
+    best = min(res, key=res.get)
+    return cur, res[cur], best, res[best]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--versions", default="xl,v1-5")
+    ap.add_argument("--write", default=None,
+                    help="write gemm_tuned.json with the winners merged in to this path")
+    a = ap.parse_args()
+    dt = torch.float16
+    new = []
+    for version in a.versions.split(","):
+        shapes = record_shapes(version, dt)
+        tot_cur = tot_best = 0.0
+        for (M, Nv, K, epi), n in sorted(shapes.items(), key=lambda kv: -kv[1] * kv[0][0] * kv[0][1] * kv[0][2]):
+            cur, t_cur, best, t_best = tune(M, Nv, K, epi, dt)
+            fl = 2.0 * M * Nv * K
+            tot_cur += n * t_cur
+            tot_best += n * t_best
+            rec = {"version": version, "M": M, "Nv": Nv, "K": K, "epi": epi, "calls": n,
+                   "plan": list(cur), "plan_ms": round(t_cur, 4), "best": list(best),
+                   "best_ms": round(t_best, 4), "best_tflops": round(fl / t_best / 1e9, 1)}
+            print(json.dumps(rec), flush=True)
+            new.append({"M": M, "Nv": Nv, "K": K, "epi": epi, "cfg": best[0], "splits": best[1],
+                        "tflops": rec["best_tflops"], "shape": f"sd_{version}_unet"})
+        print(json.dumps({"version": version, "step_gemm_ms_plan": round(tot_cur, 3),
+                          "step_gemm_ms_best": round(tot_best, 3)}), flush=True)
+    if a.write:
+        with open(TUNED) as f:
+            table = json.load(f)
+        keys = {(e["M"], e["Nv"], e["K"], e["epi"]) for e in new}
+        old = [e for e in table["entries"] if (e["M"], e["Nv"], e["K"], e["epi"]) not in keys]
+        table["entries"] = old + new
+        table["sd_source"] = "scripts/tune_sd_gemm.py"
+        with open(a.write, "w") as f:
+            json.dump(table, f, indent=1)
+        print(f"# {len(new)} SD entries merged into {a.write}", file=sys.stderr)
+
+
+if __name__ == "__main__":
+    main()
