@@ -112,16 +112,33 @@ def tune(M, Nv, K, epi, dt):
     return cur, res[cur], best, res[best]
 
 
+def llama_shapes():
+    """Prefill linears of Llama-3-8B / 70B (q|k|v, o + residual, gate|up + SwiGLU, down +
+    residual) at the prompt lengths the engine and the bench run."""
+    out = collections.Counter()
+    for (H, I, nq, nkv), Ts in (((4096, 14336, 32, 8), (32, 128, 512, 1024, 2048, 4096)),
+                                ((8192, 28672, 64, 8), (512, 2048))):
+        hd = H // nq
+        for T in Ts:
+            out[(T, (nq + 2 * nkv) * hd, H, "store")] += 1
+            out[(T, H, H, "resid32")] += 1
+            out[(T, 2 * I, H, "swiglu")] += 1
+            out[(T, H, I, "resid32")] += 1
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--versions", default="xl,v1-5")
+    ap.add_argument("--versions", default="xl,v1-5",
+                    help="comma list of SD versions, and/or 'llama' for the prefill shapes")
     ap.add_argument("--write", default=None,
                     help="write gemm_tuned.json with the winners merged in to this path")
     a = ap.parse_args()
     dt = torch.float16
     new = []
     for version in a.versions.split(","):
-        shapes = record_shapes(version, dt)
+        dt = torch.bfloat16 if version == "llama" else torch.float16
+        shapes = llama_shapes() if version == "llama" else record_shapes(version, dt)
         tot_cur = tot_best = 0.0
         for (M, Nv, K, epi), n in sorted(shapes.items(), key=lambda kv: -kv[1] * kv[0][0] * kv[0][1] * kv[0][2]):
             cur, t_cur, best, t_best = tune(M, Nv, K, epi, dt)
@@ -133,7 +150,8 @@ def main():
                    "best_ms": round(t_best, 4), "best_tflops": round(fl / t_best / 1e9, 1)}
             print(json.dumps(rec), flush=True)
             new.append({"M": M, "Nv": Nv, "K": K, "epi": epi, "cfg": best[0], "splits": best[1],
-                        "tflops": rec["best_tflops"], "shape": f"sd_{version}_unet"})
+                        "tflops": rec["best_tflops"],
+                        "shape": "llama_prefill" if version == "llama" else f"sd_{version}_unet"})
         print(json.dumps({"version": version, "step_gemm_ms_plan": round(tot_cur, 3),
                           "step_gemm_ms_best": round(tot_best, 3)}), flush=True)
     if a.write:
