@@ -44,6 +44,13 @@ struct FlashArgs {
   int causal;
   int pos0;          // absolute position of query row 0 (keys start at 0)
   int pair;          // v2 causal: workgroup x runs q tiles x and n-1-x (equal work)
+  // v2 non-causal key split (grid.z = B * ksplit): split s walks keys [s*kchunk, (s+1)*kchunk)
+  // and writes its normalised f32 O rows to po and their log2-sum-exp to plse
+  // ([B * ksplit][H][N](D)); flash_merge_kernel combines the splits.
+  int ksplit = 1, kchunk = 0;
+  float* po = nullptr;
+  float* plse = nullptr;
+  long long ws_bytes = 0;  // host: bytes at po (ksplit * B * H * N * (D + 1) f32)
 };
 
 constexpr int kBM = 64, kBN = 64, kKP = 8;  // rows, keys, LDS row pad (elements)
@@ -298,7 +305,7 @@ __global__ __launch_bounds__(64 * NW, 2) void flash2_fwd_kernel(FlashArgs a) {
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int l32 = lane & 31, h = lane >> 5;
-  const int hq = blockIdx.y, b = blockIdx.z;
+  const int hq = blockIdx.y, b = blockIdx.z / a.ksplit, sk = blockIdx.z - b * a.ksplit;
   // Causal load balance: q tile x costs ~x key tiles, so with a grid that fills the
   // chip once, the last tiles' workgroups set the kernel time at ~2x the mean.
   // Paired, workgroup x runs tiles x and n-1-x back to back (n+1 tiles' work each).
@@ -335,6 +342,11 @@ __global__ __launch_bounds__(64 * NW, 2) void flash2_fwd_kernel(FlashArgs a) {
 
   int kend = a.M;
   if (a.causal) kend = min(kend, a.pos0 + mblk + 32 * NW);
+  int j0 = 0;
+  if (a.ksplit > 1) {  // non-causal only (host): this split's key tiles
+    j0 = sk * a.kchunk / 64;
+    kend = min(kend, (sk + 1) * a.kchunk);
+  }
   const int ntiles = (kend + 63) / 64;
 
   // staging: pair pi -> keys 2*(pi / NCH) + {0,1}, chunk pi % NCH
@@ -373,13 +385,13 @@ __global__ __launch_bounds__(64 * NW, 2) void flash2_fwd_kernel(FlashArgs a) {
     }
   };
 
-  if (ntiles > 0) {
-    gload(0);
+  if (ntiles > j0) {
+    gload(j0);
     sstore(0);
   }
   __syncthreads();
-  for (int j = 0; j < ntiles; ++j) {
-    const int buf = j & 1;
+  for (int j = j0; j < ntiles; ++j) {
+    const int buf = (j - j0) & 1;
     const bool more = j + 1 < ntiles;
     if (more) gload(j + 1);
     const uint16_t* Ks = Kb + buf * 64 * DP;
@@ -470,6 +482,24 @@ __global__ __launch_bounds__(64 * NW, 2) void flash2_fwd_kernel(FlashArgs a) {
   // ---- epilogue: O[q][d] = Oᵀ[d][q] / l  (d = 32dt + 8g + 4h + i)
   const float lt = l + __shfl_xor(l, 32, 64);
   const float inv = lt > 0.f ? 1.f / lt : 0.f;
+  if (a.ksplit > 1) {  // key split: f32 partial rows + log2-sum-exp for the merge
+    if (qrow < a.N) {
+      const size_t row = ((size_t)blockIdx.z * a.H + hq) * a.N + qrow;
+      float* prow = a.po + row * a.D;
+#pragma unroll
+      for (int dt = 0; dt < DTL; ++dt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int d = 32 * dt + 8 * g + 4 * h;
+          if (d < a.D)
+            *reinterpret_cast<float4*>(prow + d) =
+                make_float4(o[dt][4 * g] * inv, o[dt][4 * g + 1] * inv, o[dt][4 * g + 2] * inv,
+                            o[dt][4 * g + 3] * inv);
+        }
+      if (h == 0) a.plse[row] = lt > 0.f ? m * a.scale_log2 + __log2f(lt) : -INFINITY;
+    }
+    continue;
+  }
   if (qrow < a.N) {
     uint16_t* orow = a.o + b * a.o_sb + hq * a.o_sh + (long long)qrow * a.o_sn;
 #pragma unroll
@@ -488,10 +518,58 @@ __global__ __launch_bounds__(64 * NW, 2) void flash2_fwd_kernel(FlashArgs a) {
   }  // pass
 }
 
+// Merge of the key splits: O = sum_s 2^(lse_s - max) O_s / sum_s 2^(lse_s - max); one thread
+// per 4 head dims of one (b, h, q) row.
+template <int DT>
+__global__ __launch_bounds__(256) void flash_merge_kernel(FlashArgs a) {
+  const int dq = a.D / 4;
+  const size_t t = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const size_t rows = (size_t)a.B * a.H * a.N;
+  if (t >= rows * dq) return;
+  const size_t r = t / dq;
+  const int d = (int)(t - r * dq) * 4;
+  const int q = (int)(r % a.N), hq = (int)((r / a.N) % a.H), b = (int)(r / ((size_t)a.N * a.H));
+  const size_t hn = (size_t)a.H * a.N;
+  float lse[4], mx = -INFINITY;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    lse[s] = s < a.ksplit ? a.plse[(size_t)(b * a.ksplit + s) * hn + (size_t)hq * a.N + q]
+                          : -INFINITY;
+    mx = fmaxf(mx, lse[s]);
+  }
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  float wsum = 0.f;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    if (s >= a.ksplit || lse[s] == -INFINITY) continue;
+    const float w = __builtin_amdgcn_exp2f(lse[s] - mx);
+    const float4 v = *reinterpret_cast<const float4*>(
+        a.po + ((size_t)(b * a.ksplit + s) * hn + (size_t)hq * a.N + q) * a.D + d);
+    acc.x += w * v.x; acc.y += w * v.y; acc.z += w * v.z; acc.w += w * v.w;
+    wsum += w;
+  }
+  const float inv = wsum > 0.f ? 1.f / wsum : 0.f;
+  uint2 st;
+  st.x = pack2(from_f32<DT>(acc.x * inv), from_f32<DT>(acc.y * inv));
+  st.y = pack2(from_f32<DT>(acc.z * inv), from_f32<DT>(acc.w * inv));
+  *reinterpret_cast<uint2*>(a.o + b * a.o_sb + hq * a.o_sh + (long long)q * a.o_sn + d) = st;
+}
+
 }  // namespace cake
 
 using namespace cake;
 
+static int g_flash_ksplit = -1;  // v2 key splits: 0 = auto, 1 = off, 2 / 4 forced;
+                                 // -1: from CAKE_FLASH_KSPLIT (default auto)
+
+static int flash_ksplit() {
+  if (g_flash_ksplit < 0) {
+    const char* e = getenv("CAKE_FLASH_KSPLIT");
+    const int k = e ? atoi(e) : 0;
+    g_flash_ksplit = (k == 1 || k == 2 || k == 4) ? k : 0;
+  }
+  return g_flash_ksplit;
+}
 static int g_flash_impl = -1;  // -1: from CAKE_FLASH_IMPL (default 2)
 static long long g_flash_pair_min = 512;  // unpaired workgroups needed before pairing
 static int g_flash_nw = 0;                 // v2 waves per workgroup override (0 = auto)
@@ -525,7 +603,29 @@ static int launch_flash(const FlashArgs& a, hipStream_t st) {
     // pair causal q tiles once the unpaired grid fills every CU twice (below that,
     // halving the workgroups costs more parallelism than the balance gains)
     p.pair = a.causal && nqt >= 2 && (long long)nqt * a.H * a.B >= g_flash_pair_min;
-    const dim3 g2(p.pair ? (nqt + 1) / 2 : nqt, a.H, a.B);
+    // Non-causal grids with fewer workgroups than CUs (SD 1.5's 1024-token self-attention:
+    // 128) leave most of the chip idle: split the keys (>= 256 per split, up to two
+    // workgroups per CU) and merge the f32 partial rows in a second launch (44.8 -> 28.1 us
+    // there).  At >= 256 workgroups the split measured neutral (SDXL's 320: 35.4 us either
+    // way; profiles/r4_flash_key_split.jsonl), so it stays off.
+    p.ksplit = 1;
+    if (!a.causal && a.D % 4 == 0 && a.po != nullptr) {
+      const long long wgs = (long long)nqt * a.H * a.B;
+      int ks = 1;
+      if (flash_ksplit() == 0) {
+        if (wgs < 256)
+          while (ks < 4 && wgs * ks < 512 && a.M / (2 * ks) >= 256) ks *= 2;
+      } else {
+        ks = flash_ksplit();
+      }
+      const long long need = (long long)ks * a.B * a.H * a.N * (a.D + 1) * 4;
+      if (ks > 1 && need <= a.ws_bytes) {
+        p.ksplit = ks;
+        p.kchunk = ((a.M + ks - 1) / ks + 63) / 64 * 64;
+        p.plse = a.po + (size_t)ks * a.B * a.H * a.N * a.D;
+      }
+    }
+    const dim3 g2(p.pair ? (nqt + 1) / 2 : nqt, a.H, a.B * p.ksplit);
 #define CAKE_FL2(P, W) hipLaunchKernelGGL((flash2_fwd_kernel<DT, P, W>), g2, dim3(64 * W), 0, st, p)
     if (a.D <= 64) {
       if (nw == 4) CAKE_FL2(64, 4); else if (nw == 2) CAKE_FL2(64, 2); else CAKE_FL2(64, 1);
@@ -533,6 +633,11 @@ static int launch_flash(const FlashArgs& a, hipStream_t st) {
       if (nw == 4) CAKE_FL2(128, 4); else CAKE_FL2(128, 2);
     }
 #undef CAKE_FL2
+    if (p.ksplit > 1) {
+      const size_t n = (size_t)a.B * a.H * a.N * (a.D / 4);
+      hipLaunchKernelGGL((flash_merge_kernel<DT>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                         st, p);
+    }
     return (int)hipGetLastError();
   }
   const dim3 grid((a.N + kBM - 1) / kBM, a.H, a.B);
@@ -559,10 +664,15 @@ CAKE_API void cake_flash_set_nw(int nw) { g_flash_nw = nw; }
 // causal q-tile pairing threshold (unpaired workgroups); <= 0 never pairs
 CAKE_API void cake_flash_set_pair_min(long long n) { g_flash_pair_min = n > 0 ? n : (1ll << 62); }
 
-// strides in ELEMENTS: s[0]=batch, s[1]=head, s[2]=row for q, k, v, o (12 values)
-CAKE_API int cake_flash_attn(int dt, const void* q, const void* k, const void* v, void* o, int B,
-                             int H, int Hkv, int N, int M, int D, const long long* strides,
-                             float scale, int causal, int pos0, hipStream_t st) {
+// key splits of the non-causal v2 path: 0 = auto, 1 = never, 2 / 4 = forced (tests)
+CAKE_API void cake_flash_set_ksplit(int k) { g_flash_ksplit = (k == 1 || k == 2 || k == 4) ? k : 0; }
+
+// strides in ELEMENTS: s[0]=batch, s[1]=head, s[2]=row for q, k, v, o (12 values).
+// ws (optional, f32, ws_bytes): partial rows for the non-causal key split.
+CAKE_API int cake_flash_attn_ws(int dt, const void* q, const void* k, const void* v, void* o, int B,
+                                int H, int Hkv, int N, int M, int D, const long long* strides,
+                                float scale, int causal, int pos0, void* ws, long long ws_bytes,
+                                hipStream_t st) {
   if (H <= 0 || Hkv <= 0 || H % Hkv || D <= 0 || D > 256 || N <= 0 || M <= 0)
     return (int)hipErrorInvalidValue;
   FlashArgs a{(const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o,
@@ -570,7 +680,16 @@ CAKE_API int cake_flash_attn(int dt, const void* q, const void* k, const void* v
               strides[0], strides[1], strides[2], strides[3], strides[4], strides[5],
               strides[6], strides[7], strides[8], strides[9], strides[10], strides[11],
               scale * 1.4426950408889634f, causal, pos0, 0};
+  a.po = (float*)ws;
+  a.ws_bytes = ws ? ws_bytes : 0;
   if (dt == kBF16) return launch_flash<kBF16>(a, st);
   if (dt == kF16) return launch_flash<kF16>(a, st);
   return (int)hipErrorInvalidValue;
+}
+
+CAKE_API int cake_flash_attn(int dt, const void* q, const void* k, const void* v, void* o, int B,
+                             int H, int Hkv, int N, int M, int D, const long long* strides,
+                             float scale, int causal, int pos0, hipStream_t st) {
+  return cake_flash_attn_ws(dt, q, k, v, o, B, H, Hkv, N, M, D, strides, scale, causal, pos0,
+                            nullptr, 0, st);
 }

@@ -113,6 +113,8 @@ def check(rc: int, name: str) -> None:
 
 _SIGS.update({
     "cake_flash_attn": [I, P, P, P, P, I, I, I, I, I, I, P, F, I, I, P],
+    "cake_flash_attn_ws": [I, P, P, P, P, I, I, I, I, I, I, P, F, I, I, P, C.c_longlong, P],
+    "cake_flash_set_ksplit": [I],
     "cake_flash_set_impl": [I],
     "cake_flash_set_pair_min": [C.c_longlong],
     "cake_flash_set_nw": [I],

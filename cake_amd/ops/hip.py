@@ -685,9 +685,34 @@ def flash_attn(q, k, v, out, scale: float, causal: bool = False, pos0: int = 0):
             raise ValueError(f"flash_attn: {n} not 16-byte aligned for vector loads")
     st = [s for t in (q, k, v, out) for s in t.stride()[:3]]
     arr = (ctypes.c_longlong * 12)(*st)
-    check(kernels().cake_flash_attn(_dt(q), _p(q), _p(k), _p(v), _p(out), B, H, Hkv, N, M, D,
-                                    ctypes.cast(arr, ctypes.c_void_p), float(scale), int(causal),
-                                    int(pos0), _stream()), "flash_attn")
+    ws, nbytes = None, 0
+    if not causal:  # room for up to 4 key splits (the kernel picks; flash_attn.hip)
+        ws = _flash_ws(q.device, 4 * B * H * N * (D + 1))
+        nbytes = ws.numel() * 4
+    check(kernels().cake_flash_attn_ws(_dt(q), _p(q), _p(k), _p(v), _p(out), B, H, Hkv, N, M, D,
+                                       ctypes.cast(arr, ctypes.c_void_p), float(scale),
+                                       int(causal), int(pos0), _p(ws), nbytes, _stream()),
+          "flash_attn")
+
+
+_flash_wsd: dict = {}
+_flash_ws_keep: list = []
+
+
+def _flash_ws(dev, numel: int) -> torch.Tensor:
+    """f32 partial rows of the key-split flash path.  Superseded buffers stay alive: a
+    captured hipGraph may still point at them."""
+    w = _flash_wsd.get(dev)
+    if w is None or w.numel() < numel:
+        if w is not None:
+            _flash_ws_keep.append(w)
+        w = _flash_wsd[dev] = torch.empty(numel, dtype=torch.float32, device=dev)
+    return w
+
+
+def flash_set_ksplit(k: int) -> None:
+    """Key splits of non-causal flash attention: 0 auto, 1 off, 2 / 4 forced (tests / A-B)."""
+    kernels().cake_flash_set_ksplit(int(k))
 
 
 _zero16: dict = {}

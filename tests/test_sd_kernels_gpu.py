@@ -79,6 +79,32 @@ def test_flash_causal_pairing(cuda, N, pos0, D, pair_min):
                                **_tol(dt))
 
 
+@pytest.mark.parametrize("ksplit", [0, 2, 4])
+@pytest.mark.parametrize("B,H,N,M,D", [(2, 20, 1024, 1024, 64), (1, 3, 200, 1000, 64),
+                                       (2, 4, 77, 600, 128), (1, 2, 64, 513, 40)])
+def test_flash_key_split(cuda, ksplit, B, H, N, M, D):
+    """Non-causal key split (f32 partial rows per split + the merge launch), forced to 2 / 4
+    splits and automatic (SDXL's 1024-token self-attention splits by itself), including
+    ragged key counts whose last split is short; a spike in the second half makes the
+    splits' maxima differ."""
+    from cake_amd.ops import hip as K
+    torch.manual_seed(5)
+    dt = torch.bfloat16
+    q = torch.randn(B, N, H, D, device=cuda).to(dt).transpose(1, 2)
+    k = torch.randn(B, M, H, D, device=cuda)
+    k[:, M - 3, :, :] = q[:, :, 1, :].float() * 3  # row 1: its mass sits in the last split
+    k = k.to(dt).transpose(1, 2)
+    v = torch.randn(B, M, H, D, device=cuda).to(dt).transpose(1, 2)
+    out = torch.full((B, N, H, D), float("nan"), device=cuda, dtype=dt).transpose(1, 2)
+    K.flash_set_ksplit(ksplit)
+    try:
+        K.flash_attn(q, k, v, out, 1 / math.sqrt(D))
+    finally:
+        K.flash_set_ksplit(0)
+    torch.testing.assert_close(out.float(), _ref_attn(q, k, v, 1 / math.sqrt(D), False, 0),
+                               **_tol(dt))
+
+
 @pytest.mark.parametrize("impl", [1, 2])
 def test_flash_attn_softmax_rescale_branch(cuda, impl):
     """A late key tile with a much larger score forces the online-softmax rescale."""
