@@ -359,6 +359,17 @@ __global__ __launch_bounds__(256) void gn_nhwc_apply_kernel(GnSrc src,
                                                             uint16_t* __restrict__ cat) {
   __shared__ float sc[kGnMaxC], sh[kGnMaxC];
   const int n = blockIdx.y, Cg = C / G;
+  const size_t nv = (size_t)HW * (C >> 3);
+  const size_t base = (size_t)n * HW * C;
+  const size_t vstep = (size_t)gridDim.x * blockDim.x;
+  auto load = [&](size_t v) {
+    return *reinterpret_cast<const uint4*>(src.at(n, HW, C, v / (C >> 3), (int)(v % (C >> 3)) * 8));
+  };
+  // the first vector is requested before the scale / shift table is built (its stats /
+  // gamma / beta reads and the barrier overlap the load), then one vector ahead
+  size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint4 nxt = make_uint4(0, 0, 0, 0);
+  if (v < nv) nxt = load(v);
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     const int g = c / Cg;
     const float mean = stats[((size_t)n * G + g) * 2];
@@ -368,12 +379,10 @@ __global__ __launch_bounds__(256) void gn_nhwc_apply_kernel(GnSrc src,
     sh[c] = to_f32<DT>(beta[c]) - mean * a;
   }
   __syncthreads();
-  const size_t nv = (size_t)HW * (C >> 3);
-  const size_t base = (size_t)n * HW * C;
-  for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv;
-       v += (size_t)gridDim.x * blockDim.x) {
+  for (; v < nv; v += vstep) {
     const int c0 = (int)(v % (C >> 3)) * 8;
-    const uint4 raw = *reinterpret_cast<const uint4*>(src.at(n, HW, C, v / (C >> 3), c0));
+    const uint4 raw = nxt;
+    if (v + vstep < nv) nxt = load(v + vstep);
     if (cat != nullptr) *reinterpret_cast<uint4*>(cat + base + v * 8) = raw;
     float f[8];
     unpack8<DT>(raw, f);
