@@ -269,14 +269,27 @@ __global__ __launch_bounds__(512) void gn_nhwc_stats_kernel(GnSrc src, int HW,
   if (py < Ty) {
     const uint16_t* base = src.at(n, HW, C, 0, cv * 8);
     const int ld = cv * 8 < src.Cx ? src.Cx : C - src.Cx;
-    for (int p = p0 + py; p < p1; p += Ty) {
-      float f[8];
-      unpack8<DT>(*reinterpret_cast<const uint4*>(base + (size_t)p * ld), f);
+    // all (up to 8) of this thread's pixel vectors requested before any is consumed: one
+    // memory round trip per 8 pixels instead of per pixel
+    constexpr int U = 8;
+    for (int p = p0 + py; p < p1; p += U * Ty) {
+      uint4 raw[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int pp = p + u * Ty;
+        raw[u] = pp < p1 ? *reinterpret_cast<const uint4*>(base + (size_t)pp * ld)
+                         : make_uint4(0, 0, 0, 0);
+      }
       float a0 = 0.f, b0 = 0.f, a1 = 0.f, b1 = 0.f;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        if ((cv * 8 + e) / Cg == g0) { a0 += f[e]; b0 += f[e] * f[e]; }
-        else { a1 += f[e]; b1 += f[e] * f[e]; }
+      for (int u = 0; u < U; ++u) {
+        float f[8];
+        unpack8<DT>(raw[u], f);  // zero vectors past p1 add nothing
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          if ((cv * 8 + e) / Cg == g0) { a0 += f[e]; b0 += f[e] * f[e]; }
+          else { a1 += f[e]; b1 += f[e] * f[e]; }
+        }
       }
       s0 += a0; q0 += b0; s1 += a1; q1 += b1;
     }
@@ -322,12 +335,26 @@ __global__ __launch_bounds__(512) void gn_nhwc_stats_kernel(GnSrc src, int HW,
   {
     const int g = threadIdx.x % G, sl = threadIdx.x / G;
     double ts = 0.0, tq = 0.0;
-    if (sl < lpg)
-      for (int k = sl; k < S; k += lpg) {
-        const double* q = part + ((size_t)n * S + k) * G * 2;
-        ts += __builtin_nontemporal_load(q + 2 * g);
-        tq += __builtin_nontemporal_load(q + 2 * g + 1);
+    if (sl < lpg) {
+      // 8 partials requested per round trip (a serial chain of S / lpg loads was the
+      // tail of the whole launch)
+      constexpr int U = 8;
+      for (int k = sl; k < S; k += U * lpg) {
+        double ps[U], pq[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int kk = k + u * lpg;
+          const double* q = part + ((size_t)n * S + (kk < S ? kk : 0)) * G * 2 + 2 * g;
+          ps[u] = kk < S ? __builtin_nontemporal_load(q) : 0.0;
+          pq[u] = kk < S ? __builtin_nontemporal_load(q + 1) : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          ts += ps[u];
+          tq += pq[u];
+        }
       }
+    }
     red[threadIdx.x * 2] = ts;
     red[threadIdx.x * 2 + 1] = tq;
   }
