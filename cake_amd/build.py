@@ -62,7 +62,7 @@ def _run(cmd: list[str]) -> None:
 # per-file hipcc flags: the GEMM's compile-time-unrolled interleaved schedule needs its
 # lambdas fully inlined (below the default threshold the 128x128-per-wave tile keeps
 # closures in scratch memory)
-HIP_EXTRA = {"gemm": ["-mllvm", "-inline-threshold=100000"]}
+HIP_EXTRA = {"gemm": ["-mllvm", "-inline-threshold=100000"]}  # gemm.hip and gemm_inst_*.hip
 
 
 def _compile_hip(src: Path, force: bool) -> Path:
@@ -71,7 +71,8 @@ def _compile_hip(src: Path, force: bool) -> Path:
     headers = sorted((CSRC / "kernels").glob("*.h"))
     if force or _newer(src, headers, out):
         _run([HIPCC, "-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC",
-              "-Wno-unused-result", "-munsafe-fp-atomics", *HIP_EXTRA.get(src.stem, []),
+              "-Wno-unused-result", "-munsafe-fp-atomics",
+              *HIP_EXTRA.get(src.stem.split("_")[0], []),
               "-c", str(src), "-o", str(out)])
     return out
 
