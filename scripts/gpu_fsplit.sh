@@ -9,7 +9,7 @@ timeout -k 10 200 python scripts/bench_flash_split.py > $OUT/split.jsonl 2> $OUT
 cat $OUT/split.jsonl
 timeout -k 10 300 python scripts/bench_sd.py --version xl --denoise --graph --steps 8 > $OUT/xl.log 2>&1 || { tail $OUT/xl.log; exit 1; }
 grep '^{' $OUT/xl.log | tail -1 | cut -c1-150
-CAKE_FLASH_KSPLIT=1 timeout -k 10 300 python scripts/bench_sd.py --version xl --denoise --graph --steps 8 > $OUT/xl_off.log 2>&1 || { tail $OUT/xl_off.log; exit 1; }
-grep '^{' $OUT/xl_off.log | tail -1 | cut -c1-150
+true
+true
 timeout -k 10 300 python scripts/bench_sd.py --version v1-5 --denoise --graph --steps 8 > $OUT/v15.log 2>&1 || { tail $OUT/v15.log; exit 1; }
 grep '^{' $OUT/v15.log | tail -1 | cut -c1-150
