@@ -157,7 +157,11 @@ def main():
     if a.write:
         with open(TUNED) as f:
             table = json.load(f)
-        keys = {(e["M"], e["Nv"], e["K"], e["epi"]) for e in new}
+        uniq = {}
+        for e in new:  # a shape shared by two versions (time embedding) keeps one plan
+            uniq.setdefault((e["M"], e["Nv"], e["K"], e["epi"]), e)
+        new = list(uniq.values())
+        keys = set(uniq)
         old = [e for e in table["entries"] if (e["M"], e["Nv"], e["K"], e["epi"]) not in keys]
         table["entries"] = old + new
         table["sd_source"] = "scripts/tune_sd_gemm.py"

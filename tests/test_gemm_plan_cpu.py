@@ -1,0 +1,59 @@
+"""GEMM tile plans on the CPU: the measured table (ops/gemm_tuned.json) and the three places
+that name the tile configurations — the kernel table (csrc/kernels/gemm_kernel.h
+CAKE_GEMM_CFGS), the Python planner (ops/gemm.py CFG_TILES) and the native engine's planner
+(csrc/engine/llama_engine.cpp) — must agree, or a tuned plan launches a tile the library
+does not have."""
+import json
+import re
+from pathlib import Path
+
+from cake_amd.ops import gemm as G
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def _kernel_cfgs() -> dict:
+    src = (ROOT / "cake_amd/csrc/kernels/gemm_kernel.h").read_text()
+    body = src[src.index("#define CAKE_GEMM_CFGS(X)"):]
+    body = body[:body.index("\n\n")]
+    return {int(m[0]): (int(m[1]), int(m[2]), int(m[3]), int(m[4]))
+            for m in re.findall(r"X\((\d+),\s*(\d+),\s*(\d+),\s*(\d+),\s*(\d+),", body)}
+
+
+def test_tile_tables_agree():
+    kern = _kernel_cfgs()
+    assert set(kern) == set(G.CFG_TILES)
+    for cfg, (bm, bn, wm, wn) in kern.items():
+        assert G.CFG_TILES[cfg] == (bm, bn), cfg
+        # the gated epilogues need 32-column wave tiles; the others are refused up front
+        assert ((bn // wn) % 32 == 0) == (cfg not in G.NO_GATED), cfg
+    eng = (ROOT / "cake_amd/csrc/engine/llama_engine.cpp").read_text()
+    known = re.search(r"static const int known\[\] = \{([^}]*)\}", eng).group(1)
+    assert {int(x) for x in known.replace("\n", " ").split(",")} == set(G.CFG_TILES)
+    assert set(G._SLOTS) == set(G.CFG_TILES) and set(G._EFF) == set(G.CFG_TILES)
+
+
+def test_tuned_table_entries_are_launchable():
+    table = json.loads((ROOT / "cake_amd/ops/gemm_tuned.json").read_text())["entries"]
+    assert table
+    seen = set()
+    for e in table:
+        key = (e["M"], e["Nv"], e["K"], e["epi"])
+        assert key not in seen, f"duplicate plan {key}"
+        seen.add(key)
+        assert e["cfg"] in G.CFG_TILES and e["splits"] >= 1 and e["epi"] in G.EPI, e
+        if e["epi"] in ("swiglu", "geglu"):
+            assert e["cfg"] not in G.NO_GATED and e["Nv"] % 32 == 0, e
+        assert e["K"] % 8 == 0, e
+
+
+def test_plan_uses_measured_entries():
+    table = json.loads((ROOT / "cake_amd/ops/gemm_tuned.json").read_text())["entries"]
+    e = next(x for x in table if x["M"] >= 512)
+    assert G.plan(e["M"], e["Nv"], e["K"], e["epi"]) == (e["cfg"], e["splits"])
+    # a nearby M (within 2x) reuses the measured tile without split-K
+    cfg, splits = G.plan(e["M"] + 8, e["Nv"], e["K"], e["epi"])
+    assert cfg in G.CFG_TILES and splits == 1
+    # an unmeasured shape falls back to the cost model
+    cfg, splits = G.plan(333, 4448, 1024, "store")
+    assert cfg in G.CFG_TILES and splits >= 1
