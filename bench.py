@@ -6,11 +6,14 @@ BASELINE.json metric: "decode tokens/sec + p50 per-token latency, Llama-3-8B
 :93-121) excludes the first (prefill) token; here the prefill happens before the
 timed region and exactly K decode steps are timed.
 
+* Engine: the native engine (libcake_engine.so, ``--engine native``, default) —
+  the same C++ engine cake-cli, the REST API and the torchrun roles run; the
+  torch-hosted decoders (``--engine python``) remain as test oracles.
 * N = 1: all 32 layers local on one MI355X; the whole step (embedding, layers,
   lm_head, repeat penalty 1.1 over the last 128 tokens, argmax, next-token
-  bookkeeping) is one hipGraph replay; the host reads each token back one step
-  behind the GPU.  ``llama3_70b.single`` is the same for Llama-3-70B (135 GB fits
-  one 288 GB MI355X).
+  bookkeeping) is one hipGraph replay; the engine's C++ loop reads each token back
+  one step behind the GPU.  ``llama3_70b.single`` is the same for Llama-3-70B
+  (141 GB fits one 288 GB MI355X).
 * N > 1 (one rank per GPU; launched by torchrun, or self-launched: with no
   WORLD_SIZE in the environment bench.py spawns the N ranks itself and only
   relays rank 0's JSON line): ``value`` is the reference's parallelism, layer
@@ -19,15 +22,18 @@ timed region and exactly K decode steps are timed.
   place them (rank 0 = master with embedding/lm_head + the first shard); the
   hidden state hops rank->rank as device-side peer stores over xGMI (bf16
   payload, as the reference ships the model dtype) captured inside every rank's
-  decode graph (--hop dist = host-issued RCCL p2p), the last shard returns it to
-  the master.  Batch-1 layer sharding does not add throughput (one token walks
-  the ranks in sequence): the curve is strong scaling of ONE decode stream.
-  Extra fields (``--no-extras`` skips them): ``tp`` = tensor parallelism
-  (beyond the reference: every rank streams 1/N of every layer, device-side
-  all-reduces over xGMI), ``pp_streams`` = the same layer-sharded pipeline with N
-  independent batch-1 sequences in flight (one per stage: the pipeline's aggregate
-  serving throughput) and ``llama3_70b`` = pp / tp for 70B — the BASELINE's "70B
-  8-worker" point is ``llama3_70b.pp`` at N = 8.
+  decode graph, the last shard returns it to the master.  Batch-1 layer sharding
+  does not add throughput (one token walks the ranks in sequence): the curve is
+  strong scaling of ONE decode stream.  Extra fields (``--no-extras`` skips them):
+  ``tp`` = tensor parallelism (beyond the reference: every rank streams 1/N of
+  every layer, device-side all-reduces over xGMI), ``pp_streams`` = the layer-
+  sharded pipeline with N independent batch-1 sequences in flight (one per stage:
+  the pipeline's aggregate serving throughput; Python pipeline) and
+  ``llama3_70b`` = pp / tp for 70B — the BASELINE's "70B 8-worker" point is
+  ``llama3_70b.pp`` at N = 8.
+* Timing: W untimed warm-up steps, then exactly K decode steps bracketed by a
+  device synchronise on both sides on rank 0 (parallel/native_bench.py: in a
+  multi-rank run every token walks all ranks inside the replays rank 0 paces).
 
 Weights are random-init of the named architecture (no network, no checkpoints);
 EOS is ignored so exactly K tokens are generated.
@@ -87,6 +93,9 @@ def _args(argv=None):
                     help="hidden-state payload of an ipc hop (the reference ships the model dtype)")
     ap.add_argument("--cpu", action="store_true",
                     help="plumbing check without a GPU (torch reference math, f32, gloo)")
+    ap.add_argument("--engine", default="native", choices=["native", "python"],
+                    help="native = libcake_engine.so (the product path: cake-cli, the API, the "
+                         "torchrun roles); python = the torch-hosted decoders (test oracles)")
     ap.add_argument("--launch-timeout", type=float, default=1800.0,
                     help="self-launch (N>1 without torchrun): kill the ranks after this many s")
     return ap.parse_args(argv)
@@ -225,7 +234,8 @@ def _summary(r: dict | None) -> dict | None:
         return None
     keep = _MAIN_KEYS + ("streams", "per_stream_tokens_per_sec", "hop", "hop_us",
                          "hops_per_token", "allreduce", "allreduce_us", "layers_per_rank",
-                         "hbm_peak_mib_max_rank", "hbm_peak_mib", "ttft_ms_prefill")
+                         "hbm_peak_mib_max_rank", "hbm_peak_mib", "ttft_ms_prefill", "engine",
+                         "walk", "hbm_used_mib_max_rank", "hbm_used_mib")
     return {k: r[k] for k in keep if k in r}
 
 
@@ -250,14 +260,22 @@ def _extra_runs(a):
             (("llama3_70b", "tp"), m70, "tp")]
 
 
+def _native(a) -> bool:
+    return a.engine == "native" and not a.cpu and not a.no_graph and a.dtype in ("bf16", "f16")
+
+
 def bench_single(a) -> None:
-    r = measure_single(a, a.model, a.steps, a.warmup, a.dump_tokens)
+    if _native(a):
+        from cake_amd.parallel.native_bench import measure_native_single as measure
+    else:
+        measure = measure_single
+    r = measure(a, a.model, a.steps, a.warmup, a.dump_tokens)
     extra = {k: v for k, v in r.items() if k not in _MAIN_KEYS}
     if not a.no_extras and a.model == "llama3-8b":
         # the 70B point on one GPU (135 GB of bf16 weights in 288 GB of HBM)
         try:
-            extra["llama3_70b"] = {"single": _summary(measure_single(a, "llama3-70b", a.steps,
-                                                                     a.warmup))}
+            extra["llama3_70b"] = {"single": _summary(measure(a, "llama3-70b", a.steps,
+                                                              a.warmup))}
         except Exception as e:  # noqa: BLE001  (the headline stands; the miss is reported)
             extra["llama3_70b"] = {"single": None, "error": f"{type(e).__name__}: {e}"[:300]}
         # the reference's second metric: SD seconds per diffusion step (SDXL 1024^2,
@@ -285,7 +303,18 @@ def bench_multi(a) -> None:
             a2.streams = env_.world
             return measure_pipeline(a2, env_, model, steps, warmup)
         measure = {"pp": measure_pipeline, "tp": measure_tp, "pp_streams": measure_streams}
-        head = measure[a.parallel](a, env, a.model, a.steps, a.warmup, a.dump_tokens)
+        if _native(a):
+            from cake_amd.parallel.native_bench import measure_native_multi
+
+            def native_pp(a_, env_, model, steps, warmup, dump=None):
+                return measure_native_multi(a_, env_, model, steps, warmup, "pp", dump)
+
+            def native_tp(a_, env_, model, steps, warmup, dump=None):
+                return measure_native_multi(a_, env_, model, steps, warmup, "tp", dump)
+            # pp_streams (several sequences in flight) stays on the Python pipeline
+            measure.update(pp=native_pp, tp=native_tp)
+        head_fn = measure[a.parallel] if a.streams == 1 else measure_pipeline
+        head = head_fn(a, env, a.model, a.steps, a.warmup, a.dump_tokens)
         extra = {}
         for path, model, mode in _extra_runs(a):
             if mode == "pp_streams" and (env.world == 1 or a.streams == env.world):

@@ -50,6 +50,8 @@
 // gfx950 kernel entry points (libcake_kernels.so)
 extern "C" {
 int cake_cast16(int src_kind, int dt, const void* src, void* dst, size_t n, hipStream_t st);
+int cake_fill_normal(int dt, void* dst, size_t n, float mean, float std, unsigned long long key,
+                     hipStream_t st);
 int cake_embed(int dt, const void* table, const int* tok, int T, int H, float* out, hipStream_t st);
 int cake_rmsnorm(int dt, const float* x, const void* w, float eps, int T, int H, void* out,
                  hipStream_t st);
@@ -355,8 +357,9 @@ class Llama {
  public:
   Llama(const std::string& dir, const CakeEngineOpts& o, const CakePipeOpts* pp = nullptr,
         const std::vector<int>* layers = nullptr, const CakeTPOpts* tp = nullptr)
-      : dt_(o.dtype), dev_(o.device) {
+      : dt_(o.dtype), dev_(o.device), init_(o.init), seed_(o.seed) {
     if (dt_ != 0 && dt_ != 1) throw Error("dtype must be 0 (bf16) or 1 (f16)");
+    if (init_ != 0 && init_ != 1) throw Error("init must be 0 (checkpoint) or 1 (random)");
     if (tp) {
       tp_ = tp->world;
       tp_rank_ = tp->rank;
@@ -384,7 +387,8 @@ class Llama {
     S_ = o.max_seq > 0 ? o.max_seq : 4096;
     k_ = std::max(1, o.steps_per_graph);
     if (cfg_.H % 8 || cfg_.hd % 2 || cfg_.nh % cfg_.nkv) throw Error("unsupported model shape");
-    if (world_ > cfg_.L) throw Error("more pipeline ranks than layers");
+    const bool placed = pp && pp->owners && pp->n_owners > 0;
+    if (world_ > cfg_.L && !placed) throw Error("more pipeline ranks than layers");
     // this rank's compute shapes: the whole model, or its tensor-parallel slice
     lc_ = cfg_;
     if (tp_ > 1) {
@@ -408,21 +412,46 @@ class Llama {
         throw Error("worker layers outside the model");
       head_ = false;
     } else {
-      const auto sh = shard_layers(cfg_, world_);
-      for (int l = sh[rank_].first; l < sh[rank_].second; ++l) owned_.push_back(l);
+      // layer -> rank: the topology's owner map, or contiguous shards
+      owner_.assign(cfg_.L, 0);
+      if (placed) {
+        if (pp->n_owners != cfg_.L)
+          throw Error("owner map has " + std::to_string(pp->n_owners) + " entries for " +
+                      std::to_string(cfg_.L) + " layers");
+        for (int l = 0; l < cfg_.L; ++l) {
+          if (pp->owners[l] < 0 || pp->owners[l] >= world_)
+            throw Error("layer " + std::to_string(l) + " placed on rank " +
+                        std::to_string(pp->owners[l]) + " outside the world of " +
+                        std::to_string(world_));
+          owner_[l] = pp->owners[l];
+        }
+      } else {
+        const auto sh = shard_layers(cfg_, world_);
+        for (int r = 0; r < world_; ++r)
+          for (int l = sh[r].first; l < sh[r].second; ++l) owner_[l] = r;
+      }
+      for (int l = 0; l < cfg_.L; ++l)
+        if (owner_[l] == rank_) owned_.push_back(l);
       head_ = rank_ == 0;
     }
-    lo_ = owned_.front();
-    hi_ = owned_.back() + 1;
+    lo_ = owned_.empty() ? 0 : owned_.front();
+    hi_ = owned_.empty() ? 0 : owned_.back() + 1;
     local_.assign(cfg_.L, -1);
     for (size_t i = 0; i < owned_.size(); ++i) local_[owned_[i]] = (int)i;
+    if (!layers) plan_walk();
     planner_.load(pkg_dir() + "/ops/gemm_tuned.json");
     load_weights(dir);
     alloc_state();
-    if (world_ > 1) connect_pipeline(pp->master_addr ? pp->master_addr : "127.0.0.1:29517",
-                                     pp->connect_timeout_s > 0 ? pp->connect_timeout_s : 600.0);
-    if (tp_ > 1) connect_tp(tp->master_addr ? tp->master_addr : "127.0.0.1:29517",
-                            tp->connect_timeout_s > 0 ? tp->connect_timeout_s : 600.0);
+    if (world_ > 1) {
+      connect_pipeline(pp->master_addr ? pp->master_addr : "127.0.0.1:29517",
+                       pp->connect_timeout_s > 0 ? pp->connect_timeout_s : 600.0);
+      selftest_pipeline();
+    }
+    if (tp_ > 1) {
+      connect_tp(tp->master_addr ? tp->master_addr : "127.0.0.1:29517",
+                 tp->connect_timeout_s > 0 ? tp->connect_timeout_s : 600.0);
+      selftest_tp();
+    }
   }
 
   ~Llama() {
@@ -440,9 +469,9 @@ class Llama {
     drop_graphs();
     for (void* p : tp_mapped_) (void)hipIpcCloseMemHandle(p);
     for (void* p : tp_owned_) (void)cake_hop_free(p);
-    if (next_inbox_) (void)hipIpcCloseMemHandle(next_inbox_);
-    if (next_pbuf_) (void)hipIpcCloseMemHandle(next_pbuf_);
-    if (inbox_) (void)cake_hop_free(inbox_);
+    for (auto& kv : out_inbox_) (void)hipIpcCloseMemHandle(kv.second);
+    for (auto& kv : peer_pbuf_) (void)hipIpcCloseMemHandle(kv.second);
+    for (auto& kv : my_inbox_) (void)cake_hop_free(kv.second);
     for (void* p : allocs_) (void)hipFree(p);
     (void)hipStreamDestroy(st_);
   }
@@ -461,6 +490,13 @@ class Llama {
     hip_check(hipMemcpyAsync(host_logits, logits_, sizeof(float) * cfg_.V, hipMemcpyDeviceToHost,
                              st_), "logits D2H");
     hip_check(hipStreamSynchronize(st_), "sync");
+  }
+
+  void forced_logits(const int32_t* prompt, int T, const int32_t* forced, int n, float* out) {
+    hip_check(hipSetDevice(dev_), "hipSetDevice");
+    if (!head_ || tp_rank_ != 0) throw Error("forced_logits() runs on rank 0");
+    if (T <= 0 || n < 0 || T + n + 1 > S_) throw Error("prompt + forced tokens exceed max_seq");
+    forced_run(prompt, T, forced, n, out);
   }
 
   void generate(const int32_t* prompt, int T, int max_new, const CakeEngineSampling& smp,
@@ -485,29 +521,128 @@ class Llama {
       m.set("seed", Json::string(std::to_string(smp.seed)));
       m.set("penalty", Json::number(smp.repeat_penalty));
       m.set("last_n", Json::integer(smp.repeat_last_n));
+      m.set("eos", eos_json(eos, n_eos));
       for (int fd : peers_) send_json(fd, m);
     }
     run_generation(prompt, T, max_new, smp, eos, n_eos, cb, ctx, out, out_cap, stats, true);
   }
 
-  // A tensor-parallel rank's generation never stops early (every rank replays the same
-  // steps; EOS / the callback only truncate the reported tokens on rank 0).
+  // More tokens after the last generate / continue: the device history, position and
+  // graphs (same sampling mode) are where that call left them.
+  void continue_gen(int max_new, const int32_t* eos, int n_eos, cake_engine_token_cb cb,
+                    void* ctx, int32_t* out, int out_cap, CakeEngineStats* stats) {
+    hip_check(hipSetDevice(dev_), "hipSetDevice");
+    if (!head_) throw Error("continue() runs on pipeline rank 0");
+    if (tp_ > 1 && tp_rank_ != 0) throw Error("continue() runs on tensor-parallel rank 0");
+    if (!have_graphs_) throw Error("continue() needs a previous generate()");
+    if (max_new <= 0) return;
+    if (out_cap < max_new) throw Error("output buffer smaller than max_new");
+    const int L = read_i32(hist_len_);
+    if (L + max_new + k_ + 1 > S_) throw Error("context + max_new exceeds max_seq");
+    if (tp_ > 1) {
+      Json m = msg("continue");
+      m.set("max_new", Json::integer(max_new));
+      m.set("eos", eos_json(eos, n_eos));
+      for (int fd : peers_) send_json(fd, m);
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<float> ms;
+    const int n_out = decode_tokens(L, max_new, eos, n_eos, cb, ctx, out, out_cap, true, &ms);
+    const auto t1 = std::chrono::steady_clock::now();
+    if (stats) {
+      fill_stats(stats, L, n_out, 0.0, std::chrono::duration<double>(t1 - t0).count(), ms);
+      // every token of a continuation is a decode step: the rate counts all of them
+      stats->tokens_per_s = stats->decode_s > 0 ? n_out / stats->decode_s : 0.0;
+    }
+  }
+
+  // A tensor-parallel rank's callback never stops the generation (every rank must replay
+  // the same steps: they all stop at the same EOS token, which each reads back itself);
+  // the lead's callback only sees the tokens.
   struct TpStop {
     cake_engine_token_cb cb;
     void* ctx;
-    const int32_t* eos;
-    int n_eos;
     bool stopped;
-    int count;
   };
   static int32_t tp_token_cb(void* vctx, int32_t tok) {
     auto* t = static_cast<TpStop*>(vctx);
-    if (t->stopped) return 0;
-    ++t->count;
-    if (t->cb && t->cb(t->ctx, tok) != 0) t->stopped = true;
-    for (int e = 0; e < t->n_eos; ++e)
-      if (t->eos[e] == tok) t->stopped = true;
+    if (!t->stopped && t->cb && t->cb(t->ctx, tok) != 0) t->stopped = true;
     return 0;
+  }
+
+  static Json eos_json(const int32_t* eos, int n_eos) {
+    Json a = Json::array();
+    for (int i = 0; i < n_eos; ++i) a.push(Json::integer(eos[i]));
+    return a;
+  }
+
+  // n tokens of graph replays after history length L (device position L - 1); 0 or the
+  // tokens kept (lead: written to out, EOS inclusive); per-token device ms in *ms_out
+  int decode_tokens(int L, int n, const int32_t* eos, int n_eos, cake_engine_token_cb cb,
+                    void* ctx, int32_t* out, int out_cap, bool lead, std::vector<float>* ms_out) {
+    std::vector<int32_t> toks(n);
+    std::vector<float> ms(n, 0.f);
+    CakeLoopSpec spec{};
+    std::vector<void*> execs(execs_.begin(), execs_.end());
+    spec.execs = execs.data();
+    spec.n_execs = (int32_t)execs.size();
+    spec.bucket_of = bucket_of_.data();
+    spec.n_len = (int32_t)bucket_of_.size();
+    spec.k = k_;
+    spec.hist = hist_;
+    spec.base = L;      // history index of the first token of this run
+    spec.pos = L - 1;   // device position (last written row)
+    spec.n = n;
+    spec.chunk = 0;
+    AnnounceCtx actx{this, L - 1};
+    if (world_ > 1) {  // the workers enqueue each chunk of replays when told
+      spec.chunk = kAnnounceChunk;
+      spec.announce = &Llama::announce_cb;
+      spec.announce_ctx = &actx;
+    }
+    spec.eos = eos;
+    spec.n_eos = n_eos;
+    spec.on_token = cb;
+    spec.token_ctx = ctx;
+    spec.stream = st_;
+    spec.out_tokens = toks.data();
+    spec.out_ms = ms.data();
+    spec.out_cap = n;
+    TpStop tps{cb, ctx, false};
+    if (tp_ > 1) {  // lock step: every rank reads the tokens back and stops at EOS
+      spec.on_token = lead ? &Llama::tp_token_cb : nullptr;
+      spec.token_ctx = &tps;
+    }
+    CakeLoopResult res{};
+    const int rc = cake_graph_decode(&spec, &res);
+    if (world_ > 1) sync_workers();
+    if (tp_ > 1 && lead) sync_tp_workers();
+    k_check(rc, "graph_decode");
+    if (lead) check_attn_error("rank " + std::to_string(rank()));  // TP workers: in "sync"
+    int n_out = 0;
+    if (lead)
+      for (int i = 0; i < res.n_tokens && n_out < out_cap; ++i) out[n_out++] = toks[i];
+    ms.resize(lead ? res.n_tokens : 0);
+    if (ms_out) *ms_out = std::move(ms);
+    return n_out;
+  }
+
+  void fill_stats(CakeEngineStats* stats, int n_prompt, int n_out, double prefill_s,
+                  double decode_s, const std::vector<float>& ms) const {
+    stats->n_prompt = n_prompt;
+    stats->n_generated = n_out;
+    stats->prefill_s = prefill_s;
+    stats->decode_s = decode_s;
+    stats->tokens_per_s = n_out > 1 && decode_s > 0 ? (n_out - 1) / decode_s : 0.0;
+    std::vector<float> s = ms;
+    std::sort(s.begin(), s.end());
+    auto pct = [&](double q) {
+      if (s.empty()) return 0.f;
+      const size_t i = std::min(s.size() - 1, (size_t)std::llround(q / 100.0 * (s.size() - 1)));
+      return s[i];
+    };
+    stats->p50_ms = pct(50);
+    stats->p99_ms = pct(99);
   }
 
   void run_generation(const int32_t* prompt, int T, int max_new, const CakeEngineSampling& smp,
@@ -539,83 +674,44 @@ class Llama {
     const auto t1 = std::chrono::steady_clock::now();
     int n_out = 0;
     bool stop = false;
+    for (int e = 0; e < n_eos && !stop; ++e)
+      if (eos[e] == first) stop = true;
     if (lead) {
       out[n_out++] = first;
-      stop = cb && cb(ctx, first) != 0;
-      for (int e = 0; e < n_eos && !stop; ++e)
-        if (eos[e] == first) stop = true;
+      const bool cb_stop = cb && cb(ctx, first) != 0;
+      if (tp_ == 1) stop = stop || cb_stop;  // TP: only EOS stops (all ranks alike)
     }
-    TpStop tps{cb, ctx, eos, n_eos, stop, 0};
     std::vector<float> ms;
-    if ((tp_ > 1 || !stop) && max_new > 1) {
-      ensure_graphs(mode);
-      const int n = max_new - 1;
-      std::vector<int32_t> toks(n);
-      ms.assign(n, 0.f);
-      CakeLoopSpec spec{};
-      std::vector<void*> execs(execs_.begin(), execs_.end());
-      spec.execs = execs.data();
-      spec.n_execs = (int32_t)execs.size();
-      spec.bucket_of = bucket_of_.data();
-      spec.n_len = (int32_t)bucket_of_.size();
-      spec.k = k_;
-      spec.hist = hist_;
-      spec.base = T + 1;  // history index of the second generated token
-      spec.pos = T;       // device position after the first token
-      spec.n = n;
-      spec.chunk = 0;
-      AnnounceCtx actx{this, T};
-      if (world_ > 1) {  // the workers enqueue each chunk of replays when told
-        spec.chunk = kAnnounceChunk;
-        spec.announce = &Llama::announce_cb;
-        spec.announce_ctx = &actx;
-      }
-      spec.eos = eos;
-      spec.n_eos = n_eos;
-      spec.on_token = cb;
-      spec.token_ctx = ctx;
-      spec.stream = st_;
-      spec.out_tokens = toks.data();
-      spec.out_ms = ms.data();
-      spec.out_cap = n;
-      if (tp_ > 1) {  // lock step: all n replays on every rank
-        spec.eos = nullptr;
-        spec.n_eos = 0;
-        spec.on_token = lead ? &Llama::tp_token_cb : nullptr;
-        spec.token_ctx = &tps;
-        if (!lead) {  // no read-back: enqueue every replay (device-paced by the all-reduces)
-          spec.hist = nullptr;
-          spec.out_tokens = nullptr;
-          spec.out_ms = nullptr;
-          spec.out_cap = 0;
-        }
-      }
-      CakeLoopResult res{};
-      const int rc = cake_graph_decode(&spec, &res);
-      if (world_ > 1) sync_workers();
-      if (tp_ > 1 && lead) sync_tp_workers();
-      k_check(rc, "graph_decode");
-      const int keep = tp_ > 1 ? tps.count : res.n_tokens;
-      if (lead)
-        for (int i = 0; i < keep && n_out < out_cap; ++i) out[n_out++] = toks[i];
-      ms.resize(lead ? std::min(keep, res.n_tokens) : 0);
-    }
+    // graphs exist after every generation (continue() replays them), even a 1-token one
+    ensure_graphs(mode);
+    if (!stop && max_new > 1)
+      n_out += decode_tokens(T + 1, max_new - 1, eos, n_eos, cb, ctx, lead ? out + n_out : nullptr,
+                             lead ? out_cap - n_out : 0, lead, &ms);
     const auto t2 = std::chrono::steady_clock::now();
-    if (stats) {
-      stats->n_prompt = T;
-      stats->n_generated = n_out;
-      stats->prefill_s = std::chrono::duration<double>(t1 - t0).count();
-      stats->decode_s = std::chrono::duration<double>(t2 - t1).count();
-      stats->tokens_per_s = n_out > 1 && stats->decode_s > 0 ? (n_out - 1) / stats->decode_s : 0.0;
-      std::vector<float> s = ms;
-      std::sort(s.begin(), s.end());
-      auto pct = [&](double q) {
-        if (s.empty()) return 0.f;
-        const size_t i = std::min(s.size() - 1, (size_t)std::llround(q / 100.0 * (s.size() - 1)));
-        return s[i];
-      };
-      stats->p50_ms = pct(50);
-      stats->p99_ms = pct(99);
+    if (stats)
+      fill_stats(stats, T, n_out, std::chrono::duration<double>(t1 - t0).count(),
+                 std::chrono::duration<double>(t2 - t1).count(), ms);
+  }
+
+  int read_i32(const int* p) {
+    int v = 0;
+    hip_check(hipMemcpyAsync(&v, p, sizeof(int), hipMemcpyDeviceToHost, st_), "i32 D2H");
+    hip_check(hipStreamSynchronize(st_), "sync");
+    return v;
+  }
+
+  // the split-K attention merge's error word (tickets[2 nkv], attn_core2.h): a merge
+  // that gave up waiting for its partials left that launch's outputs invalid
+  void check_attn_error(const std::string& who) {
+    unsigned int w = 0;
+    hip_check(hipMemcpyAsync(&w, tickets_ + 2 * lc_.nkv, sizeof(w), hipMemcpyDeviceToHost, st_),
+              "attn err D2H");
+    hip_check(hipStreamSynchronize(st_), "sync");
+    if (w) {
+      hip_check(hipMemsetAsync(tickets_ + 2 * lc_.nkv, 0, sizeof(unsigned int), st_), "attn err");
+      hip_check(hipStreamSynchronize(st_), "sync");
+      throw Error(who + ": decode attention split merge timed out waiting for its partials; "
+                        "the tokens of that generation are invalid");
     }
   }
 
@@ -634,11 +730,30 @@ class Llama {
     }
   };
 
-  int dt_, dev_;
+  int dt_, dev_, init_ = 0;
+  bool forced_ = false;  // teacher-forcing steps: the head writes full logits
+  uint64_t seed_ = 0;
   int rank_ = 0, world_ = 1, lo_ = 0, hi_ = 0;
   bool head_ = true, hop_bf16_ = false;
   double hop_timeout_ = 30.0;
-  void *inbox_ = nullptr, *next_inbox_ = nullptr, *next_pbuf_ = nullptr;
+  // The token's walk (llama.rs:81-117): embedding on rank 0, then every maximal run of
+  // consecutive layers on one rank, then the head on rank 0.  An edge joins consecutive
+  // stops on different ranks; each edge has its own inbox on the receiving rank and its
+  // own sequence words (seq_[2e] send side, seq_[2e + 1] receive side).
+  enum StopKind { kEmbedStop, kRunStop, kHeadStop };
+  struct Stop {
+    StopKind kind;
+    int rank;
+    std::vector<int> layers;  // global ids (runs)
+    std::vector<int> sel;     // the same as this rank's local layer slots
+  };
+  std::vector<Stop> walk_;
+  std::vector<int> edge_in_;                // per stop: the edge feeding it, or -1
+  std::vector<std::pair<int, int>> edges_;  // (src rank, dst rank)
+  std::vector<int> owner_;                  // layer -> pipeline rank
+  std::map<int, void*> my_inbox_;           // edge -> own inbox (edges into this rank)
+  std::map<int, void*> out_inbox_;          // edge -> IPC-mapped inbox of the receiver
+  std::map<int, void*> peer_pbuf_;          // rank -> IPC-mapped prefill buffer
   unsigned int* seq_ = nullptr;
   int* hop_err_ = nullptr;
   std::vector<int> peers_;  // rank 0: control sockets of ranks 1..world-1
@@ -763,7 +878,55 @@ class Llama {
   // slices — q / k / v rows of its heads, o_proj columns of its heads, gate / up rows and
   // down_proj columns of its intermediate range, lm_head rows of its vocabulary range
   // (parallel/tensor_parallel.py shard_block / shard_head)
+  // init = 1: this rank's tensors (same shapes and packing as a checkpoint load) drawn
+  // on the device — N(0, 0.02) linears and lm_head, N(0, 1) embedding, N(1, 0.05) norms
+  // (models/llama3/weights.py random) — keyed by (seed, layer, tensor)
+  void load_random() {
+    const Cfg& c = cfg_;
+    const size_t H = c.H, V = c.V, hd = c.hd;
+    const size_t nq = (size_t)lc_.nh * hd, nk = (size_t)lc_.nkv * hd, I = lc_.I;
+    auto fill = [&](void* p, size_t n, float mean, float std, uint64_t tag) {
+      const uint64_t key = seed_ * 0x9e3779b97f4a7c15ULL + tag * 0xc2b2ae3d27d4eb4fULL +
+                           (uint64_t)tp_rank_ * 0x165667b19e3779f9ULL;
+      k_check(cake_fill_normal(dt_, p, n, mean, std, key, st_), "fill_normal");
+    };
+    if (head_) {
+      embed_ = dalloc<uint16_t>(V * H);
+      fill(embed_, V * H, 0.f, 1.f, 1);
+      norm_ = dalloc<uint16_t>(H);
+      fill(norm_, H, 1.f, 0.05f, 2);
+      if (c.tie && tp_ == 1) {
+        lm_head_ = embed_;
+      } else {
+        lm_head_ = dalloc<uint16_t>((size_t)lc_.V * H);
+        fill(lm_head_, (size_t)lc_.V * H, 0.f, 0.02f, 3);
+      }
+    }
+    layers_.resize(owned_.size());
+    for (int l : owned_) {
+      LayerW& w = layers_[local_[l]];
+      const uint64_t t = 16 + 16 * (uint64_t)l;
+      w.ln1 = dalloc<uint16_t>(H);
+      fill(w.ln1, H, 1.f, 0.05f, t);
+      w.wqkv = dalloc<uint16_t>((nq + 2 * nk) * H);
+      fill(w.wqkv, (nq + 2 * nk) * H, 0.f, 0.02f, t + 1);
+      w.wo = dalloc<uint16_t>(H * nq);
+      fill(w.wo, H * nq, 0.f, 0.02f, t + 2);
+      w.ln2 = dalloc<uint16_t>(H);
+      fill(w.ln2, H, 1.f, 0.05f, t + 3);
+      w.wgu = dalloc<uint16_t>(2 * I * H);
+      fill(w.wgu, 2 * I * H, 0.f, 0.02f, t + 4);
+      w.wd = dalloc<uint16_t>(H * I);
+      fill(w.wd, H * I, 0.f, 0.02f, t + 5);
+    }
+    hip_check(hipStreamSynchronize(st_), "sync");
+  }
+
   void load_weights(const std::string& dir) {
+    if (init_ == 1) {
+      load_random();
+      return;
+    }
     Checkpoint ck(dir);
     const Cfg& c = cfg_;
     const size_t H = c.H, V = c.V, hd = c.hd;
@@ -847,7 +1010,7 @@ class Llama {
     hist_len_ = dalloc<int>(1);
     slot_ = dalloc<unsigned long long>(1);
     scratch_i32_ = dalloc<int>(4);
-    scratch_resid_ = dalloc<float>(c.H);
+    scratch_resid_ = dalloc<float>(c.H + 4);  // + the hop header (self-tests)
     zeros_ = dalloc<int32_t>(64);
     hip_check(hipMemset(tickets_, 0, sizeof(unsigned int) * (2 * c.nkv + 2)), "memset");
     hip_check(hipMemset(part_, 0, sizeof(float) * 2 * c.nh * kAttnMaxSplit * (c.hd + 2)), "memset");
@@ -856,9 +1019,10 @@ class Llama {
     hip_check(hipMemset(zeros_, 0, sizeof(int32_t) * 64), "memset");
     hip_check(hipMemset(hist_, 0, sizeof(int) * S_), "memset");
     hip_check(hipMemset(resid_, 0, sizeof(float) * (c.H + 4)), "memset");
-    seq_ = dalloc<unsigned int>(4);  // [0] send sequence, [1] receive sequence
+    const size_t nseq = 2 * edges_.size() + 2;  // per edge: send, receive sequence
+    seq_ = dalloc<unsigned int>(nseq);
     hop_err_ = dalloc<int>(4);
-    hip_check(hipMemset(seq_, 0, sizeof(unsigned int) * 4), "memset");
+    hip_check(hipMemset(seq_, 0, sizeof(unsigned int) * nseq), "memset");
     hip_check(hipMemset(hop_err_, 0, sizeof(int) * 4), "memset");
     if (tp_ > 1) {
       partial_ = dalloc<float>(c.H);
@@ -935,6 +1099,7 @@ class Llama {
     }
     hip_check(hipStreamSynchronize(st_), "sync");
     if (kv_.count(0)) cur_ = kv_[0];
+    if (T == 1) check_attn_error("worker");
   }
 
  private:
@@ -991,19 +1156,23 @@ class Llama {
     hip_check(hipMemcpyAsync(ptok_buf(T), prompt, sizeof(int32_t) * T, hipMemcpyHostToDevice, st_),
               "prompt H2D");
     k_check(cake_embed(dt_, embed_, ptok_, T, c.H, hidden_, st_), "embed");
-    prefill_layers(T);
-    if (world_ > 1) {
-      forward_hidden(T);
-      for (int r = 1; r < world_; ++r) {  // relay: rank r runs, then hands to r + 1
-        Json m = msg("prefill");
-        m.set("T", Json::integer(T));
-        send_json(peers_[r - 1], m);
-        const Json ack = recv_json(peers_[r - 1]);
-        if (!ack.has("ok") || !ack.get("ok").as_bool())
-          throw Error("pipeline rank " + std::to_string(r) + " prefill failed: " +
-                      (ack.has("error") ? ack.get("error").as_string() : std::string("?")));
+    // the walk: rank 0 runs its stops, tells each worker when its stop is due; every
+    // stop hands its rows to the next stop's rank (the last one back to this rank)
+    for (size_t i = 0; i + 1 < walk_.size(); ++i) {
+      const Stop& s = walk_[i];
+      if (s.rank == 0) {
+        if (s.kind == kRunStop) prefill_layers(T, 0, &s.sel);
+        if (edge_in_[i + 1] >= 0) forward_hidden(T, walk_[i + 1].rank);
+        continue;
       }
-      // the last rank wrote its output rows into this rank's hidden_
+      Json m = msg("prefill");
+      m.set("T", Json::integer(T));
+      m.set("stop", Json::integer((int64_t)i));
+      send_json(peers_[s.rank - 1], m);
+      const Json ack = recv_json(peers_[s.rank - 1]);
+      if (!ack.has("ok") || !ack.get("ok").as_bool())
+        throw Error("pipeline rank " + std::to_string(s.rank) + " prefill failed: " +
+                    (ack.has("error") ? ack.get("error").as_string() : std::string("?")));
     }
   }
 
@@ -1012,10 +1181,12 @@ class Llama {
     return ptok_;
   }
 
-  // hidden_ rows [0, T) -> the next rank's prefill buffer (device to device over the
-  // IPC mapping), complete before the control message that announces them
-  void forward_hidden(int T) {
-    hip_check(hipMemcpyAsync(next_pbuf_, hidden_, sizeof(float) * (size_t)T * cfg_.H,
+  // hidden_ rows [0, T) -> rank dst's prefill buffer (device to device over the IPC
+  // mapping), complete before the control message that announces them
+  void forward_hidden(int T, int dst) {
+    auto it = peer_pbuf_.find(dst);
+    if (it == peer_pbuf_.end()) throw Error("no prefill mapping to rank " + std::to_string(dst));
+    hip_check(hipMemcpyAsync(it->second, hidden_, sizeof(float) * (size_t)T * cfg_.H,
                              hipMemcpyDeviceToDevice, st_), "prefill hop");
     hip_check(hipStreamSynchronize(st_), "sync");
   }
@@ -1092,32 +1263,76 @@ class Llama {
     k_check(cake_finalize_token(slot_, tok_, hist_, hist_len_, pos_, S_, st_), "finalize");
   }
 
-  // one decode step of this rank: [embed] layers [send, receive] head  (rank 0), or
-  // receive, layers, send (pipeline workers); the hop carries [hidden | position]
+  // one decode step of this rank: its stops of the walk in order — receive (when the
+  // previous stop is another rank's), the stop's work (embedding / layer run / head),
+  // send (when the next stop is another rank's); the hop carries [hidden | position]
   void step_body(const Mode& m) {
-    const Cfg& c = lc_;
-    if (!head_) {
-      hop_recv();
-      step_layers();
-      hop_send();
-      return;
+    for (size_t i = 0; i < walk_.size(); ++i) {
+      const Stop& s = walk_[i];
+      if (s.rank != rank_) continue;
+      if (edge_in_[i] >= 0) hop_recv(edge_in_[i]);
+      if (s.kind == kEmbedStop) {
+        if (!m.fused) k_check(cake_embed(dt_, embed_, tok_, 1, cfg_.H, resid_, st_), "embed");
+      } else if (s.kind == kRunStop) {
+        step_layers(&s.sel);
+      } else {
+        step_head(m);
+      }
+      if (i + 1 < walk_.size() && edge_in_[i + 1] >= 0) hop_send(edge_in_[i + 1]);
     }
-    if (!m.fused) k_check(cake_embed(dt_, embed_, tok_, 1, c.H, resid_, st_), "embed");
-    step_layers();
-    if (world_ > 1) {
-      hop_send();
-      hop_recv();
-    }
-    step_head(m);
   }
 
-  void hop_send() {
-    k_check(cake_hop_send(resid_, cfg_.H, 1, hop_bf16_ ? 1 : 0, next_inbox_, seq_, st_), "hop_send");
+  bool has_stops() const {
+    for (const Stop& s : walk_)
+      if (s.rank == rank_) return true;
+    return false;
   }
-  void hop_recv() {
-    k_check(cake_hop_recv(inbox_, cfg_.H, 1, hop_bf16_ ? 1 : 0, resid_, seq_ + 1, hop_err_,
-                          hop_timeout_, st_), "hop_recv");
+
+  void hop_send(int e) {
+    k_check(cake_hop_send(resid_, cfg_.H, 1, hop_bf16_ ? 1 : 0, out_inbox_.at(e), seq_ + 2 * e, st_),
+            "hop_send");
   }
+  void hop_recv(int e) {
+    k_check(cake_hop_recv(my_inbox_.at(e), cfg_.H, 1, hop_bf16_ ? 1 : 0, resid_, seq_ + 2 * e + 1,
+                          hop_err_, hop_timeout_, st_), "hop_recv");
+  }
+
+  // the walk of one token over the owner map (the placement loop llama.rs:205-220 and
+  // the contiguous-run coalescing of llama.rs:95-114)
+  void plan_walk() {
+    walk_.clear();
+    walk_.push_back({kEmbedStop, 0, {}, {}});
+    for (int l = 0; l < cfg_.L; ++l) {
+      const int r = owner_.empty() ? 0 : owner_[l];
+      if (walk_.back().kind != kRunStop || walk_.back().rank != r) walk_.push_back({kRunStop, r, {}, {}});
+      walk_.back().layers.push_back(l);
+      if (r == rank_) walk_.back().sel.push_back(local_[l]);
+    }
+    walk_.push_back({kHeadStop, 0, {}, {}});
+    edge_in_.assign(walk_.size(), -1);
+    edges_.clear();
+    for (size_t i = 1; i < walk_.size(); ++i)
+      if (walk_[i].rank != walk_[i - 1].rank) {
+        edge_in_[i] = (int)edges_.size();
+        edges_.push_back({walk_[i - 1].rank, walk_[i].rank});
+      }
+  }
+
+ public:
+  // "r:l0-l1,..." of the walk (logs / tests)
+  std::string walk_str() const {
+    std::string s;
+    for (const Stop& st : walk_)
+      if (st.kind == kRunStop) {
+        if (!s.empty()) s += ",";
+        s += std::to_string(st.rank) + ":" + std::to_string(st.layers.front()) + "-" +
+             std::to_string(st.layers.back());
+      }
+    return s;
+  }
+  int n_edges() const { return (int)edges_.size(); }
+
+ private:
 
   void step_layers(const std::vector<int>* sel = nullptr) {
     const Cfg& c = lc_;
@@ -1152,6 +1367,10 @@ class Llama {
 
   void step_head(const Mode& m) {
     const Cfg& c = lc_;
+    if (forced_) {  // teacher forcing: the full logits, no token choice
+      head_logits(resid_);
+      return;
+    }
     if (tp_ > 1) {
       head_tp(resid_, m);
       return;
@@ -1166,6 +1385,69 @@ class Llama {
     k_check(cake_gemv_norm_f32(dt_, resid_, norm_, (float)c.eps, lm_head_, c.H, c.V, logits_, st_),
             "lm_head");
     select_tail(m);
+  }
+
+  // f32 logits of the whole vocabulary for one hidden row: logits_ (one rank), or this
+  // rank's vocabulary shard gathered into full_logits_ on every tensor-parallel rank
+  float* head_logits(const float* row) {
+    const Cfg& c = lc_;
+    k_check(cake_gemv_norm_f32(dt_, row, norm_, (float)c.eps, lm_head_, c.H, c.V, logits_, st_),
+            "lm_head");
+    if (tp_ == 1) return logits_;
+    k_check(cake_ar_gather(logits_, voff_, c.V, full_logits_, cfg_.V, ch_gat_.peers.data(),
+                           ch_gat_.inbox, ar_seq_ + 4, ar_err_ + 2, tp_rank_, tp_, hop_timeout_,
+                           st_), "ar_gather");
+    return full_logits_;
+  }
+
+  // Teacher forcing: prefill `prompt`, then feed forced[0..n) one decode step each
+  // (eager launches of the same decode kernels, hops and all-reduces as the captured
+  // step); out[(n + 1) x V] = the logits after the prompt and after every forced token.
+  // Rank 0 drives; pipeline workers run their stops on "fstep", tensor-parallel workers
+  // the whole sequence on "forced".
+  void forced_run(const int32_t* prompt, int T, const int32_t* forced, int n, float* out) {
+    const bool lead = rank_ == 0 && tp_rank_ == 0;
+    grow_prefill(T);
+    if (tp_ > 1 && lead) {
+      Json m = msg("forced");
+      Json pr = Json::array(), fr = Json::array();
+      for (int i = 0; i < T; ++i) pr.push(Json::integer(prompt[i]));
+      for (int i = 0; i < n; ++i) fr.push(Json::integer(forced[i]));
+      m.set("prompt", pr);
+      m.set("forced", fr);
+      for (int fd : peers_) send_json(fd, m);
+    }
+    prefill_body(prompt, T);
+    const size_t V = cfg_.V;
+    float* lg = head_logits(hidden_ + (size_t)(T - 1) * cfg_.H);
+    if (out) hip_check(hipMemcpyAsync(out, lg, sizeof(float) * V, hipMemcpyDeviceToHost, st_), "D2H");
+    hip_check(hipStreamSynchronize(st_), "sync");
+    Mode m;
+    m.fused = false;
+    forced_ = true;
+    try {
+      for (int i = 0; i < n; ++i) {
+        if (world_ > 1)
+          for (int fd : peers_) {
+            Json st = msg("fstep");
+            send_json(fd, st);
+          }
+        set_i32(tok_, forced[i]);
+        set_i32(pos_, T + i);
+        step_body(m);
+        if (out)
+          hip_check(hipMemcpyAsync(out + (size_t)(i + 1) * V, tp_ > 1 ? full_logits_ : logits_,
+                                   sizeof(float) * V, hipMemcpyDeviceToHost, st_), "D2H");
+        hip_check(hipStreamSynchronize(st_), "sync");
+      }
+    } catch (...) {
+      forced_ = false;
+      throw;
+    }
+    forced_ = false;
+    if (world_ > 1) sync_workers();
+    if (tp_ > 1 && lead) sync_tp_workers();
+    if (lead) check_attn_error("rank " + std::to_string(rank()));
   }
 
   // ---- pipeline (one process per GPU, layer shards, device-side hops)
@@ -1196,13 +1478,18 @@ class Llama {
         const Json r = recv_json(peers_[i]);
         if (r.has("hop_err") && r.get("hop_err").as_int() != 0)
           err = "pipeline rank " + std::to_string(i + 1) + ": hop receive timed out";
+        if (r.has("error")) err = "pipeline rank " + std::to_string(i + 1) + ": " +
+                                  r.get("error").as_string();
       } catch (const std::exception& e) {
         err = e.what();
       }
     }
     int own = 0;
     hip_check(hipMemcpy(&own, hop_err_, sizeof(int), hipMemcpyDeviceToHost), "hop_err");
-    if (own) err = "pipeline rank 0: hop receive timed out";
+    if (own) {
+      (void)hipMemset(hop_err_, 0, sizeof(int));
+      err = "pipeline rank 0: hop receive timed out";
+    }
     if (!err.empty()) throw Error(err);
   }
 
@@ -1216,7 +1503,8 @@ class Llama {
       return;
     }
     if (head_) throw Error("serve() runs on pipeline workers (rank > 0)");
-    ensure_graphs(Mode{});
+    const bool active = has_stops();  // a rank the placement left idle only answers
+    if (active) ensure_graphs(Mode{});
     std::vector<void*> execs(execs_.begin(), execs_.end());
     for (;;) {
       const Json m = recv_json(ctl_fd_);
@@ -1226,16 +1514,25 @@ class Llama {
         Json r = Json::object();
         try {
           const int T = (int)m.get("T").as_int();
+          const int i = (int)m.get("stop").as_int();
           if (T < 1 || T > S_) throw Error("bad prefill length");
-          prefill_layers(T);
-          forward_hidden(T);
+          if (i < 1 || i + 1 >= (int)walk_.size() || walk_[i].rank != rank_)
+            throw Error("prefill stop " + std::to_string(i) + " is not this rank's");
+          prefill_layers(T, 0, &walk_[i].sel);
+          if (edge_in_[i + 1] >= 0) forward_hidden(T, walk_[i + 1].rank);
           r.set("ok", Json::boolean(true));
         } catch (const std::exception& e) {
           r.set("ok", Json::boolean(false));
           r.set("error", Json::string(e.what()));
         }
         send_json(ctl_fd_, r);
+      } else if (cmd == "fstep") {  // one eager teacher-forced step of this rank's stops
+        if (!active) continue;
+        Mode fm;
+        fm.fused = false;
+        step_body(fm);
       } else if (cmd == "replays") {
+        if (!active) continue;
         CakeLoopSpec spec{};
         spec.execs = execs.data();
         spec.n_execs = (int32_t)execs.size();
@@ -1255,6 +1552,12 @@ class Llama {
         if (herr) (void)hipMemset(hop_err_, 0, sizeof(int));
         r.set("ok", Json::boolean(e == hipSuccess));
         r.set("hop_err", Json::integer(herr));
+        if (e != hipSuccess) r.set("error", Json::string(hipGetErrorString(e)));
+        try {
+          check_attn_error("attention");
+        } catch (const std::exception& x) {
+          r.set("error", Json::string(x.what()));
+        }
         send_json(ctl_fd_, r);
       } else {
         throw Error("unknown control message " + cmd);
@@ -1270,22 +1573,32 @@ class Llama {
     int port = 0;
     split_host_port(addr, &host, &port);
     const int words = cake_hop_words(cfg_.H, 1, hop_bf16_ ? 1 : 0);
-    k_check(cake_hop_alloc((size_t)words * 8, &inbox_), "hop_alloc");
-    hipIpcMemHandle_t hi, hp;
-    hip_check(hipIpcGetMemHandle(&hi, inbox_), "IpcGetMemHandle");
-    hip_check(hipIpcGetMemHandle(&hp, hidden_), "IpcGetMemHandle");
-    auto entry = [&](int r, const std::string& a, const std::string& b) {
-      Json j = Json::object();
-      j.set("rank", Json::integer(r));
-      j.set("inbox", Json::string(a));
-      j.set("pbuf", Json::string(b));
-      return j;
-    };
-    Json peer_next;
+    // this rank's handles: its prefill buffer and one inbox per edge into it
+    Json me = Json::object();
+    me.set("rank", Json::integer(rank_));
+    {
+      hipIpcMemHandle_t hp;
+      hip_check(hipIpcGetMemHandle(&hp, hidden_), "IpcGetMemHandle");
+      me.set("pbuf", Json::string(hex_of(&hp, sizeof(hp))));
+      Json ib = Json::array();
+      for (size_t e = 0; e < edges_.size(); ++e) {
+        if (edges_[e].second != rank_) continue;
+        void* p = nullptr;
+        k_check(cake_hop_alloc((size_t)words * 8, &p), "hop_alloc");
+        my_inbox_[(int)e] = p;
+        hipIpcMemHandle_t hi;
+        hip_check(hipIpcGetMemHandle(&hi, p), "IpcGetMemHandle");
+        Json x = Json::array();
+        x.push(Json::integer((int64_t)e));
+        x.push(Json::string(hex_of(&hi, sizeof(hi))));
+        ib.push(x);
+      }
+      me.set("inboxes", ib);
+    }
+    std::vector<Json> table(world_);
     if (rank_ == 0) {
       const int lfd = tcp_listen(host, port);
-      std::vector<Json> hs(world_);
-      hs[0] = entry(0, hex_of(&hi, sizeof(hi)), hex_of(&hp, sizeof(hp)));
+      table[0] = me;
       peers_.assign(world_ - 1, -1);
       try {
         for (int i = 1; i < world_; ++i) {
@@ -1296,15 +1609,18 @@ class Llama {
           const int r = (int)j.get("rank").as_int();
           if (r < 1 || r >= world_ || peers_[r - 1] >= 0) throw Error("bad pipeline rank hello");
           peers_[r - 1] = fd;
-          hs[r] = j;
+          table[r] = j;
         }
       } catch (...) {
         tcp_close(lfd);
         throw;
       }
       tcp_close(lfd);
-      for (int r = 1; r < world_; ++r) send_json(peers_[r - 1], hs[(r + 1) % world_]);
-      peer_next = hs[1];
+      Json all = Json::array();
+      for (const auto& t : table) all.push(t);
+      Json m = Json::object();
+      m.set("table", all);
+      for (int fd : peers_) send_json(fd, m);
     } else {
       const auto deadline =
           std::chrono::steady_clock::now() + std::chrono::duration<double>(timeout_s);
@@ -1318,14 +1634,108 @@ class Llama {
         }
       }
       tcp_set_timeout(ctl_fd_, 0);
-      send_json(ctl_fd_, entry(rank_, hex_of(&hi, sizeof(hi)), hex_of(&hp, sizeof(hp))));
-      peer_next = recv_json(ctl_fd_);
+      send_json(ctl_fd_, me);
+      const Json m = recv_json(ctl_fd_);
+      for (int r = 0; r < world_; ++r) table[r] = m.get("table").at(r);
     }
-    hipIpcMemHandle_t ni, np;
-    unhex(peer_next.get("inbox").as_string(), &ni, sizeof(ni));
-    unhex(peer_next.get("pbuf").as_string(), &np, sizeof(np));
-    hip_check(hipIpcOpenMemHandle(&next_inbox_, ni, hipIpcMemLazyEnablePeerAccess), "IpcOpen inbox");
-    hip_check(hipIpcOpenMemHandle(&next_pbuf_, np, hipIpcMemLazyEnablePeerAccess), "IpcOpen pbuf");
+    // map the receivers of this rank's outgoing edges: their inbox, their prefill buffer
+    for (size_t e = 0; e < edges_.size(); ++e) {
+      if (edges_[e].first != rank_) continue;
+      const int dst = edges_[e].second;
+      const Json& t = table[dst];
+      bool found = false;
+      for (const auto& x : t.get("inboxes").items()) {
+        if ((int)x.at(0).as_int() != (int)e) continue;
+        hipIpcMemHandle_t h;
+        unhex(x.at(1).as_string(), &h, sizeof(h));
+        void* p = nullptr;
+        hip_check(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "IpcOpen inbox");
+        out_inbox_[(int)e] = p;
+        found = true;
+      }
+      if (!found) throw Error("rank " + std::to_string(dst) + " published no inbox for edge " +
+                              std::to_string(e));
+      if (!peer_pbuf_.count(dst)) {
+        hipIpcMemHandle_t h;
+        unhex(t.get("pbuf").as_string(), &h, sizeof(h));
+        void* p = nullptr;
+        hip_check(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "IpcOpen pbuf");
+        peer_pbuf_[dst] = p;
+      }
+    }
+  }
+
+  // Start-up self-test of every edge (before any graph exists): each rank pushes a
+  // tagged pattern through each outgoing edge (non-blocking peer stores), then receives
+  // on each incoming edge (bounded device wait) and checks every word; every rank's
+  // verdict goes to rank 0, which fails the start with the rank and peer named.  A
+  // mapping that does not carry stores across the devices fails here, not as a hop
+  // timeout in the middle of the first generation.
+  static float selftest_value(int e, int i) { return (float)(((i * 7 + e * 13) % 251) - 125); }
+
+  void selftest_pipeline() {
+    const int H = cfg_.H;
+    std::string bad;
+    std::vector<float> pat(H + 4, 0.f);
+    for (size_t e = 0; e < edges_.size(); ++e) {
+      if (edges_[e].first != rank_) continue;
+      for (int i = 0; i < H; ++i) pat[i] = selftest_value((int)e, i);
+      const uint32_t tag = 0xC0DE0000u + (uint32_t)e;
+      std::memcpy(&pat[H], &tag, 4);
+      hip_check(hipMemcpyAsync(scratch_resid_, pat.data(), sizeof(float) * (H + 1),
+                               hipMemcpyHostToDevice, st_), "selftest H2D");
+      k_check(cake_hop_send(scratch_resid_, H, 1, hop_bf16_ ? 1 : 0, out_inbox_.at((int)e),
+                            seq_ + 2 * e, st_), "selftest send");
+      hip_check(hipStreamSynchronize(st_), "selftest sync");
+    }
+    for (size_t e = 0; e < edges_.size(); ++e) {
+      if (edges_[e].second != rank_) continue;
+      hip_check(hipMemsetAsync(scratch_resid_, 0, sizeof(float) * (H + 1), st_), "memset");
+      k_check(cake_hop_recv(my_inbox_.at((int)e), H, 1, hop_bf16_ ? 1 : 0, scratch_resid_,
+                            seq_ + 2 * e + 1, hop_err_, hop_timeout_, st_), "selftest recv");
+      std::vector<float> got(H + 1);
+      hip_check(hipMemcpyAsync(got.data(), scratch_resid_, sizeof(float) * (H + 1),
+                               hipMemcpyDeviceToHost, st_), "selftest D2H");
+      int herr = 0;
+      hip_check(hipMemcpyAsync(&herr, hop_err_, sizeof(int), hipMemcpyDeviceToHost, st_), "err");
+      hip_check(hipStreamSynchronize(st_), "selftest sync");
+      const int src = edges_[e].first;
+      uint32_t tag = 0;
+      std::memcpy(&tag, &got[H], 4);
+      int wrong = 0;
+      for (int i = 0; i < H; ++i)
+        if (got[i] != selftest_value((int)e, i)) ++wrong;
+      if (herr) {
+        bad = "rank " + std::to_string(rank_) + ": hop from rank " + std::to_string(src) +
+              " (edge " + std::to_string(e) + ") timed out in the start-up self-test";
+        hip_check(hipMemset(hop_err_, 0, sizeof(int)), "memset");
+        break;
+      }
+      if (wrong || tag != 0xC0DE0000u + (uint32_t)e) {
+        bad = "rank " + std::to_string(rank_) + ": hop from rank " + std::to_string(src) +
+              " (edge " + std::to_string(e) + ") delivered " + std::to_string(wrong) +
+              " wrong words in the start-up self-test";
+        break;
+      }
+    }
+    // verdicts to rank 0 (which fails the start naming every bad edge)
+    if (rank_ == 0) {
+      for (size_t i = 0; i < peers_.size(); ++i) {
+        const Json r = recv_json(peers_[i]);
+        if (r.has("bad") && bad.empty()) bad = r.get("bad").as_string();
+      }
+      Json v = Json::object();
+      v.set("ok", Json::boolean(bad.empty()));
+      if (!bad.empty()) v.set("bad", Json::string(bad));
+      for (int fd : peers_) send_json(fd, v);
+    } else {
+      Json r = Json::object();
+      if (!bad.empty()) r.set("bad", Json::string(bad));
+      send_json(ctl_fd_, r);
+      const Json v = recv_json(ctl_fd_);
+      if (v.has("bad")) bad = v.get("bad").as_string();
+    }
+    if (!bad.empty()) throw Error("pipeline IPC self-test failed: " + bad);
   }
 
   // ---- tensor parallel (one process per GPU, every rank 1/W of every layer)
@@ -1412,8 +1822,18 @@ class Llama {
     }
     int own[3] = {0, 0, 0};
     hip_check(hipMemcpy(own, ar_err_, sizeof(own), hipMemcpyDeviceToHost), "ar_err");
-    if (own[0] | own[1] | own[2]) err = "tensor-parallel rank 0: all-reduce timed out";
+    if (own[0] | own[1] | own[2]) {
+      (void)hipMemset(ar_err_, 0, sizeof(own));
+      err = "tensor-parallel rank 0: all-reduce timed out";
+    }
     if (!err.empty()) throw Error(err);
+  }
+
+  static std::vector<int32_t> eos_of(const Json& m) {
+    std::vector<int32_t> v;
+    if (m.has("eos"))
+      for (const auto& x : m.get("eos").items()) v.push_back((int32_t)x.as_int());
+    return v;
   }
 
   // worker rank: run the generations rank 0 announces, in lock step
@@ -1433,21 +1853,120 @@ class Llama {
         smp.repeat_penalty = (float)m.get("penalty").as_double();
         smp.repeat_last_n = (int32_t)m.get("last_n").as_int();
         const int max_new = (int)m.get("max_new").as_int();
-        run_generation(prompt.data(), (int)prompt.size(), max_new, smp, nullptr, 0, nullptr,
-                       nullptr, nullptr, 0, nullptr, false);
+        const std::vector<int32_t> eos = eos_of(m);
+        run_generation(prompt.data(), (int)prompt.size(), max_new, smp, eos.data(),
+                       (int)eos.size(), nullptr, nullptr, nullptr, 0, nullptr, false);
+      } else if (cmd == "forced") {
+        std::vector<int32_t> prompt, forced;
+        for (const auto& x : m.get("prompt").items()) prompt.push_back((int32_t)x.as_int());
+        for (const auto& x : m.get("forced").items()) forced.push_back((int32_t)x.as_int());
+        forced_run(prompt.data(), (int)prompt.size(), forced.data(), (int)forced.size(), nullptr);
+      } else if (cmd == "continue") {
+        const std::vector<int32_t> eos = eos_of(m);
+        const int L = read_i32(hist_len_);
+        decode_tokens(L, (int)m.get("max_new").as_int(), eos.data(), (int)eos.size(), nullptr,
+                      nullptr, nullptr, 0, false, nullptr);
       } else if (cmd == "sync") {
         Json r = Json::object();
         const hipError_t e = hipStreamSynchronize(st_);
         int errs[3] = {0, 0, 0};
         (void)hipMemcpy(errs, ar_err_, sizeof(errs), hipMemcpyDeviceToHost);
+        if (errs[0] | errs[1] | errs[2]) (void)hipMemset(ar_err_, 0, sizeof(errs));
         r.set("ok", Json::boolean(e == hipSuccess));
         r.set("ar_err", Json::integer(errs[0] | errs[1] | errs[2]));
         if (e != hipSuccess) r.set("error", Json::string(hipGetErrorString(e)));
+        try {
+          check_attn_error("tensor-parallel rank " + std::to_string(tp_rank_));
+        } catch (const std::exception& x) {
+          r.set("error", Json::string(x.what()));
+        }
         send_json(ctl_fd_, r);
       } else {
         throw Error("unknown control message " + cmd);
       }
     }
+  }
+
+  // Start-up self-test of every tensor-parallel channel (before any graph exists): a
+  // sum all-reduce of a rank-scaled pattern, the argmax-key max, the vocabulary gather
+  // and the prefill slab all-reduce, each checked word for word; verdicts to rank 0.
+  void selftest_tp() {
+    const int H = cfg_.H, W = tp_;
+    std::string bad;
+    auto fail = [&](const std::string& what) {
+      if (bad.empty()) bad = "tensor-parallel rank " + std::to_string(tp_rank_) + ": " + what;
+    };
+    std::vector<float> pat(H);
+    for (int i = 0; i < H; ++i) pat[i] = (float)(tp_rank_ + 1) * (float)((i % 17) - 8);
+    const float tri = (float)(W * (W + 1) / 2);
+    // (1) decode sum channel
+    hip_check(hipMemcpyAsync(partial_, pat.data(), sizeof(float) * H, hipMemcpyHostToDevice, st_),
+              "selftest H2D");
+    k_check(cake_ar_sum(partial_, scratch_resid_, H, 0, ch_sum_.peers.data(), ch_sum_.inbox,
+                        ar_seq_, ar_err_, tp_rank_, tp_, hop_timeout_, st_), "selftest ar_sum");
+    std::vector<float> got(H);
+    hip_check(hipMemcpyAsync(got.data(), scratch_resid_, sizeof(float) * H, hipMemcpyDeviceToHost,
+                             st_), "selftest D2H");
+    hip_check(hipStreamSynchronize(st_), "sync");
+    for (int i = 0; i < H; ++i)
+      if (got[i] != tri * (float)((i % 17) - 8)) { fail("sum all-reduce delivered wrong words"); break; }
+    // (2) argmax-key max channel
+    const unsigned long long key = ((unsigned long long)(100 + tp_rank_) << 32) | (unsigned)tp_rank_;
+    hip_check(hipMemcpyAsync(slot_, &key, sizeof(key), hipMemcpyHostToDevice, st_), "H2D");
+    k_check(cake_ar_max_key(slot_, ch_key_.peers.data(), ch_key_.inbox, ar_seq_ + 2, ar_err_ + 1,
+                            tp_rank_, tp_, hop_timeout_, st_), "selftest ar_max_key");
+    unsigned long long mx = 0;
+    hip_check(hipMemcpyAsync(&mx, slot_, sizeof(mx), hipMemcpyDeviceToHost, st_), "D2H");
+    hip_check(hipStreamSynchronize(st_), "sync");
+    if (mx != (((unsigned long long)(100 + W - 1) << 32) | (unsigned)(W - 1)))
+      fail("argmax-key all-reduce returned a wrong key");
+    hip_check(hipMemsetAsync(slot_, 0, sizeof(unsigned long long), st_), "memset");
+    // (3) vocabulary gather channel
+    std::vector<float> shard(lc_.V);
+    for (int j = 0; j < lc_.V; ++j) shard[j] = (float)(voff_ + j);
+    hip_check(hipMemcpyAsync(logits_, shard.data(), sizeof(float) * lc_.V, hipMemcpyHostToDevice,
+                             st_), "H2D");
+    k_check(cake_ar_gather(logits_, voff_, lc_.V, full_logits_, cfg_.V, ch_gat_.peers.data(),
+                           ch_gat_.inbox, ar_seq_ + 4, ar_err_ + 2, tp_rank_, tp_, hop_timeout_,
+                           st_), "selftest ar_gather");
+    std::vector<float> full(cfg_.V);
+    hip_check(hipMemcpyAsync(full.data(), full_logits_, sizeof(float) * cfg_.V,
+                             hipMemcpyDeviceToHost, st_), "D2H");
+    hip_check(hipStreamSynchronize(st_), "sync");
+    for (int j = 0; j < cfg_.V; ++j)
+      if (full[j] != (float)j) { fail("vocabulary gather delivered wrong words"); break; }
+    // (4) prefill slab all-reduce (one row)
+    hip_check(hipMemcpyAsync(ppart_, pat.data(), sizeof(float) * H, hipMemcpyHostToDevice, st_),
+              "H2D");
+    hip_check(hipMemsetAsync(hidden_, 0, sizeof(float) * H, st_), "memset");
+    dense_allreduce(1);
+    hip_check(hipMemcpyAsync(got.data(), hidden_, sizeof(float) * H, hipMemcpyDeviceToHost, st_),
+              "D2H");
+    int errs[3] = {0, 0, 0};
+    hip_check(hipMemcpyAsync(errs, ar_err_, sizeof(errs), hipMemcpyDeviceToHost, st_), "D2H");
+    hip_check(hipStreamSynchronize(st_), "sync");
+    for (int i = 0; i < H; ++i)
+      if (got[i] != tri * (float)((i % 17) - 8)) { fail("prefill slab all-reduce delivered wrong words"); break; }
+    if (errs[0] | errs[1] | errs[2]) {
+      fail("an all-reduce channel timed out");
+      hip_check(hipMemset(ar_err_, 0, sizeof(errs)), "memset");
+    }
+    if (tp_rank_ == 0) {
+      for (int fd : peers_) {
+        const Json r = recv_json(fd);
+        if (r.has("bad") && bad.empty()) bad = r.get("bad").as_string();
+      }
+      Json v = Json::object();
+      if (!bad.empty()) v.set("bad", Json::string(bad));
+      for (int fd : peers_) send_json(fd, v);
+    } else {
+      Json r = Json::object();
+      if (!bad.empty()) r.set("bad", Json::string(bad));
+      send_json(ctl_fd_, r);
+      const Json v = recv_json(ctl_fd_);
+      if (v.has("bad")) bad = v.get("bad").as_string();
+    }
+    if (!bad.empty()) throw Error("tensor-parallel IPC self-test failed: " + bad);
   }
 
   // channel inboxes (uncached, hop.hip granules) and the prefill slab, exchanged as IPC
@@ -1757,6 +2276,43 @@ CAKE_API int32_t cake_engine_generate(void* h, const int32_t* prompt, int32_t n_
     cake::put_err(err, errlen, e.what());
     return 1;
   }
+}
+
+CAKE_API int32_t cake_engine_continue(void* h, int32_t max_new, const int32_t* eos, int32_t n_eos,
+                                      cake_engine_token_cb cb, void* ctx, int32_t* out,
+                                      int32_t out_cap, CakeEngineStats* stats, char* err,
+                                      int32_t errlen) {
+  try {
+    if (!h || (!out && max_new > 0)) throw cake::Error("null argument");
+    static_cast<Llama*>(h)->continue_gen(max_new, eos, n_eos, cb, ctx, out, out_cap, stats);
+    return 0;
+  } catch (const std::exception& e) {
+    cake::put_err(err, errlen, e.what());
+    return 1;
+  }
+}
+
+CAKE_API int32_t cake_engine_forced_logits(void* h, const int32_t* prompt, int32_t n_prompt,
+                                           const int32_t* forced, int32_t n_forced, float* out,
+                                           char* err, int32_t errlen) {
+  try {
+    if (!h || !prompt || (!forced && n_forced > 0) || !out) throw cake::Error("null argument");
+    static_cast<Llama*>(h)->forced_logits(prompt, n_prompt, forced, n_forced, out);
+    return 0;
+  } catch (const std::exception& e) {
+    cake::put_err(err, errlen, e.what());
+    return 1;
+  }
+}
+
+// "rank:first-last,..." runs of the token's walk (placement check), n = bytes written
+CAKE_API int32_t cake_engine_walk(void* h, char* out, int32_t cap) {
+  if (!h || !out || cap <= 0) return 0;
+  const std::string s = static_cast<Llama*>(h)->walk_str();
+  const int32_t n = (int32_t)std::min<size_t>(s.size(), (size_t)cap - 1);
+  std::memcpy(out, s.data(), (size_t)n);
+  out[n] = 0;
+  return n;
 }
 
 CAKE_API int32_t cake_engine_prefill_logits(void* h, const int32_t* prompt, int32_t n_prompt,

@@ -20,19 +20,29 @@ struct CakeEngineOpts {
   int32_t dtype;            // 0 = bf16, 1 = f16
   int32_t device;           // GPU ordinal
   int32_t steps_per_graph;  // decode steps per graph replay (greedy only; >= 1)
+  int32_t init;             // 0: the checkpoint's safetensors; 1: seeded random-normal
+                            // weights of the config.json architecture (benchmarks)
+  int32_t reserved;
+  uint64_t seed;            // init = 1: weight seed
 };
 
-// Layer-sharded pipeline over one process per GPU: rank r runs a contiguous layer
-// shard (rank 0 also the embedding and the head); each decode step's hidden state moves
-// rank to rank by device-side hops (hop.hip, IPC-mapped inboxes: no host in the step),
-// prefill rows through IPC-mapped buffers; the control plane (IPC handles, prefill
-// relay, replay announcements) is TCP to rank 0 at master_addr.
+// Layer-sharded pipeline over one process per GPU.  Placement: `owners[l]` is the rank
+// running layer l (a topology: node i -> rank i + 1, unplaced layers on rank 0), any
+// pattern — every maximal run of consecutive layers on one rank is one stop of the
+// token's walk (llama.rs:95-114); no owner map = contiguous shards, rank 0 lighter by
+// the head.  Rank 0 always holds the embedding and the head.  Each decode step's
+// hidden state moves between stops by device-side hops (hop.hip, one IPC-mapped inbox
+// per edge of the walk: no host in the step), prefill rows through IPC-mapped buffers;
+// the control plane (IPC handles, prefill relay, replay announcements) is TCP to rank 0
+// at master_addr.  Every edge is self-tested with a tagged pattern at start-up.
 struct CakePipeOpts {
   int32_t rank, world;
   const char* master_addr;   // "host:port" rank 0 listens on
   int32_t hop_bf16;          // 1: bf16 hop payload (half the bytes)
   double hop_timeout_s;      // a hop receive that waits longer sets the error word
   double connect_timeout_s;  // workers: how long to retry reaching rank 0
+  const int32_t* owners;     // [n_owners == num_hidden_layers] or null
+  int32_t n_owners;
 };
 
 // Tensor parallel over one process per GPU: every rank holds 1/world of every layer (its
@@ -100,6 +110,20 @@ int32_t cake_engine_generate(void* engine, const int32_t* prompt, int32_t n_prom
                              const int32_t* eos, int32_t n_eos, cake_engine_token_cb cb,
                              void* ctx, int32_t* out, int32_t out_cap,
                              struct CakeEngineStats* stats, char* err, int32_t errlen);
+// Continue the last generation for up to max_new more tokens (same sampling, the device
+// state where the previous generate / continue left it, EOS included): chat turns that
+// extend a context, and benchmarks that time exactly max_new decode steps.
+int32_t cake_engine_continue(void* engine, int32_t max_new, const int32_t* eos, int32_t n_eos,
+                             cake_engine_token_cb cb, void* ctx, int32_t* out, int32_t out_cap,
+                             struct CakeEngineStats* stats, char* err, int32_t errlen);
+// Teacher forcing (tests): prefill `prompt`, then one decode step per forced token (the
+// decode kernels, hops and all-reduces, launched eagerly); out[(n_forced + 1) x V] = the
+// f32 logits after the prompt and after each forced token.  Rank 0 of any mode.
+int32_t cake_engine_forced_logits(void* engine, const int32_t* prompt, int32_t n_prompt,
+                                  const int32_t* forced, int32_t n_forced, float* out, char* err,
+                                  int32_t errlen);
+// "rank:first-last,..." layer runs of the token's walk (placement check); bytes written.
+int32_t cake_engine_walk(void* engine, char* out, int32_t cap);
 // Logits of the last prompt position after a prefill only (f32 [V] to host), for tests.
 int32_t cake_engine_prefill_logits(void* engine, const int32_t* prompt, int32_t n_prompt,
                                    float* out, char* err, int32_t errlen);

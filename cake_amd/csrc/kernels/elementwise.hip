@@ -212,6 +212,49 @@ __global__ __launch_bounds__(256) void sum_slices_kernel(float* __restrict__ out
   }
 }
 
+// Seeded N(mean, std^2) fill of a 16-bit tensor, stateless: element i's value depends
+// only on (key, i) — a splitmix64 hash of the element pair index feeds one Box-Muller
+// draw per two elements — so any launch geometry (and any rank filling its own slice)
+// gives the same bits.  Random-init weights for the native engine's synthetic-checkpoint
+// mode (benchmarks: no network, no checkpoint; cake_engine_open with init = 1).
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ float2 normal_pair(uint64_t key, uint64_t pair) {
+  const uint64_t r = mix64(key ^ mix64(pair + 0x9e3779b97f4a7c15ULL));
+  const float u1 = (float)((uint32_t)(r >> 40) + 1u) * (1.0f / 16777216.f);  // (0, 1]
+  const float u2 = (float)(uint32_t)(r & 0xffffffu) * (1.0f / 16777216.f);  // [0, 1)
+  const float rad = sqrtf(-2.f * __logf(u1));
+  float s, c;
+  __sincosf(6.283185307179586f * u2, &s, &c);
+  return make_float2(rad * c, rad * s);
+}
+
+template <int DT>
+__global__ __launch_bounds__(256) void fill_normal_kernel(uint16_t* __restrict__ out, size_t n,
+                                                          float mean, float std, uint64_t key) {
+  const size_t n8 = n / 8;
+  for (size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x; g < n8;
+       g += (size_t)gridDim.x * blockDim.x) {
+    uint32_t w[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const float2 z = normal_pair(key, g * 4 + p);
+      w[p] = (uint32_t)from_f32<DT>(mean + std * z.x) | ((uint32_t)from_f32<DT>(mean + std * z.y) << 16);
+    }
+    reinterpret_cast<uint4*>(out)[g] = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+  // tail (n % 8 elements): the first threads of block 0
+  if (blockIdx.x == 0 && threadIdx.x < (n - n8 * 8)) {
+    const size_t i = n8 * 8 + threadIdx.x;
+    const float2 z = normal_pair(key, i / 2);
+    out[i] = from_f32<DT>(mean + std * ((i & 1) ? z.y : z.x));
+  }
+}
+
 }  // namespace cake
 
 using namespace cake;
@@ -258,6 +301,18 @@ CAKE_API int cake_cast16(int src_kind, int dt, const void* src, void* dst, size_
   else if (src_kind == 1) CAKE_CAST(1);
   else CAKE_CAST(2);
 #undef CAKE_CAST
+  return (int)hipGetLastError();
+}
+
+CAKE_API int cake_fill_normal(int dt, void* dst, size_t n, float mean, float std,
+                              unsigned long long key, hipStream_t st) {
+  if ((uintptr_t)dst % 16) return (int)hipErrorInvalidValue;
+  if (n == 0) return 0;
+  size_t g = (n / 8 + 255) / 256;
+  if (g > 16384) g = 16384;
+  if (g < 1) g = 1;
+  DISPATCH_DT(dt, hipLaunchKernelGGL((fill_normal_kernel<DT>), dim3((unsigned)g), dim3(256), 0, st,
+                                     (uint16_t*)dst, n, mean, std, (uint64_t)key));
   return (int)hipGetLastError();
 }
 

@@ -17,6 +17,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <iostream>
+#include <memory>
+#include <stdexcept>
 #include <mutex>
 #include <set>
 #include <string>
@@ -200,7 +202,44 @@ int32_t stream_token(void* vctx, int32_t tok) {
   return 0;
 }
 
-int run_native_text(cake::PyArgs& o) {
+// Layer -> pipeline rank of the topology: node i (file order) runs on rank i + 1, every
+// layer no node names stays on rank 0 (the master), as the reference's placement loop
+// (llama.rs:205-220 with topology.rs:81-92).  Empty when no node places a layer.
+std::vector<int32_t> owners_of(const cake::Topology* topo, int world, int num_layers) {
+  std::vector<int32_t> own;
+  if (!topo || topo->nodes.empty()) return own;
+  if ((int)topo->nodes.size() > world - 1)
+    throw std::runtime_error("topology has " + std::to_string(topo->nodes.size()) +
+                             " workers but only " + std::to_string(world - 1) +
+                             " worker ranks were launched");
+  own.assign((size_t)num_layers, 0);
+  bool any = false;
+  const std::string pre = "model.layers.";
+  for (size_t i = 0; i < topo->nodes.size(); ++i)
+    for (const auto& l : topo->nodes[i].layers)
+      if (l.rfind(pre, 0) == 0) {
+        const int li = std::atoi(l.c_str() + pre.size());
+        if (li >= 0 && li < num_layers) {
+          own[(size_t)li] = (int32_t)(i + 1);
+          any = true;
+        }
+      }
+  if (!any) own.clear();
+  return own;
+}
+
+int num_hidden_layers(const std::string& model_dir) {
+  std::FILE* f = std::fopen((model_dir + "/config.json").c_str(), "rb");
+  if (!f) throw std::runtime_error("cannot read " + model_dir + "/config.json");
+  std::string txt;
+  char buf[4096];
+  size_t n;
+  while ((n = std::fread(buf, 1, sizeof(buf), f)) > 0) txt.append(buf, n);
+  std::fclose(f);
+  return (int)cake::Json::parse(txt).get("num_hidden_layers").as_int();
+}
+
+int run_native_text(cake::PyArgs& o, const cake::Topology* topo) {
   const std::string lib = cake::package_root() + "/cake_amd/lib/libcake_engine.so";
   void* h = dlopen(lib.c_str(), RTLD_NOW | RTLD_LOCAL);
   if (!h) {
@@ -229,13 +268,24 @@ int run_native_text(cake::PyArgs& o) {
   StreamCtx ctx;
   ctx.model = o["model"].value;
   std::vector<int32_t> ids;
+  // pp: the topology's placement (every rank parses the same file)
+  std::vector<int32_t> owners;
+  if (pipe && !tp && world > 1) {
+    try {
+      owners = owners_of(topo, world, num_hidden_layers(ctx.model));
+    } catch (const std::exception& e) {
+      std::fprintf(stderr, "cake-cli: rank %d: %s\n", rank, e.what());
+      return 2;
+    }
+  }
   if (rank != 0) {  // worker rank: its layer shard, then serve rank 0
     const auto num = [&](const char* k, double def) {
       return o[k].kind == PyArg::kNone ? def : std::strtod(o[k].value.c_str(), nullptr);
     };
     CakeEngineOpts eo{(int32_t)num("max_seq_len", 4096), o["dtype"].value == "bf16" ? 0 : 1,
                       env_int("LOCAL_RANK", rank), 1};
-    CakePipeOpts po{rank, world, ctl.c_str(), o["hop_dtype"].value == "bf16" ? 1 : 0, 60.0, 600.0};
+    CakePipeOpts po{rank, world, ctl.c_str(), o["hop_dtype"].value == "bf16" ? 1 : 0, 60.0, 600.0,
+                    owners.empty() ? nullptr : owners.data(), (int32_t)owners.size()};
     CakeTPOpts to{rank, world, ctl.c_str(), 60.0, 600.0};
     char err[1024] = {0};
     void* eng = tp ? api.open_tp(ctx.model.c_str(), &eo, &to, err, sizeof(err))
@@ -272,7 +322,8 @@ int run_native_text(cake::PyArgs& o) {
   eo.steps_per_graph = 1;
   char err[1024] = {0};
   const auto t0 = std::chrono::steady_clock::now();
-  CakePipeOpts po{0, world, ctl.c_str(), o["hop_dtype"].value == "bf16" ? 1 : 0, 60.0, 600.0};
+  CakePipeOpts po{0, world, ctl.c_str(), o["hop_dtype"].value == "bf16" ? 1 : 0, 60.0, 600.0,
+                  owners.empty() ? nullptr : owners.data(), (int32_t)owners.size()};
   CakeTPOpts to{0, world, ctl.c_str(), 60.0, 600.0};
   void* eng = world > 1 ? (tp ? api.open_tp(ctx.model.c_str(), &eo, &to, err, sizeof(err))
                               : api.open_pp(ctx.model.c_str(), &eo, &po, err, sizeof(err)))
@@ -515,6 +566,7 @@ int main(int argc, char** argv) {
   const bool worker = opts["mode"].value == "worker";
   bool has_topology = false;
   cake::TopoNode worker_node;
+  std::unique_ptr<cake::Topology> topology;
   if (access(topo_path.c_str(), R_OK) == 0) {
     try {
       const cake::Topology topo = cake::Topology::from_path(topo_path, text);
@@ -523,6 +575,7 @@ int main(int argc, char** argv) {
       std::fprintf(stderr, "[cake-cli] topology %s: %zu node(s), %zu placed unit(s)\n",
                    topo_path.c_str(), topo.nodes.size(), layers);
       has_topology = !topo.nodes.empty();
+      topology.reset(new cake::Topology(topo));
       if (worker) {
         if (topo.nodes.empty()) { std::fprintf(stderr, "cake-cli: topology has no workers\n"); return 2; }
         const PyArg& nm = opts["name"];
@@ -542,7 +595,8 @@ int main(int argc, char** argv) {
                  topo_path.c_str());
     return 2;
   }
-  if (native_text_eligible(opts, text, worker, has_topology)) return run_native_text(opts);
+  if (native_text_eligible(opts, text, worker, has_topology))
+    return run_native_text(opts, topology.get());
   if (native_worker_eligible(opts, text, worker)) return run_native_worker(opts, worker_node);
   return cake::run_embedded(opts);
 }

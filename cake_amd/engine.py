@@ -23,13 +23,15 @@ TOKEN_CB = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_int32)
 
 class EngineOpts(C.Structure):
     _fields_ = [("max_seq", C.c_int32), ("dtype", C.c_int32), ("device", C.c_int32),
-                ("steps_per_graph", C.c_int32)]
+                ("steps_per_graph", C.c_int32), ("init", C.c_int32), ("reserved", C.c_int32),
+                ("seed", C.c_uint64)]
 
 
 class PipeOpts(C.Structure):
     _fields_ = [("rank", C.c_int32), ("world", C.c_int32), ("master_addr", C.c_char_p),
                 ("hop_bf16", C.c_int32), ("hop_timeout_s", C.c_double),
-                ("connect_timeout_s", C.c_double)]
+                ("connect_timeout_s", C.c_double), ("owners", C.POINTER(C.c_int32)),
+                ("n_owners", C.c_int32)]
 
 
 class TPOpts(C.Structure):
@@ -80,6 +82,15 @@ def lib() -> C.CDLL:
                                            C.POINTER(C.c_int32), I, C.POINTER(EngineStats),
                                            C.c_char_p, I]
         L.cake_engine_generate.restype = I
+        L.cake_engine_continue.argtypes = [P, I, C.POINTER(C.c_int32), I, TOKEN_CB, P,
+                                           C.POINTER(C.c_int32), I, C.POINTER(EngineStats),
+                                           C.c_char_p, I]
+        L.cake_engine_continue.restype = I
+        L.cake_engine_forced_logits.argtypes = [P, C.POINTER(C.c_int32), I, C.POINTER(C.c_int32),
+                                                I, C.POINTER(C.c_float), C.c_char_p, I]
+        L.cake_engine_forced_logits.restype = I
+        L.cake_engine_walk.argtypes = [P, C.c_char_p, I]
+        L.cake_engine_walk.restype = I
         L.cake_engine_prefill_logits.argtypes = [P, C.POINTER(C.c_int32), I,
                                                  C.POINTER(C.c_float), C.c_char_p, I]
         L.cake_engine_prefill_logits.restype = I
@@ -107,14 +118,19 @@ class NativeLlama:
                  device: int = 0, steps_per_graph: int = 1, rank: int = 0, world: int = 1,
                  master_addr: str = "127.0.0.1:29517", hop_bf16: bool = False,
                  hop_timeout_s: float = 30.0, connect_timeout_s: float = 600.0,
-                 tp: bool = False):
+                 tp: bool = False, owners: list[int] | None = None, random_init: bool = False,
+                 seed: int = 0):
         """world > 1: one rank of a layer-sharded pipeline, or with tp=True of a tensor-
         parallel group (rank 0 generates; the others call :meth:`serve`).  Every rank of
-        one group must be constructed concurrently."""
+        one group must be constructed concurrently.  ``owners`` (pipeline): the rank of
+        every layer (:func:`owners_from_topology`); None = contiguous shards.
+        ``random_init``: only ``config.json`` is read; the weights are seeded normal
+        draws on the device (benchmarks of a named architecture, no checkpoint)."""
         if dtype not in ("bf16", "f16"):
             raise ValueError("native engine dtype: bf16 or f16")
         opts = EngineOpts(int(max_seq), 0 if dtype == "bf16" else 1, int(device),
-                          max(1, int(steps_per_graph)))
+                          max(1, int(steps_per_graph)), 1 if random_init else 0, 0,
+                          int(seed) & 0xFFFFFFFFFFFFFFFF)
         err = C.create_string_buffer(1024)
         self._h = None
         if world > 1 and tp:
@@ -125,8 +141,14 @@ class NativeLlama:
                                                 C.byref(o), err, len(err))
         elif world > 1:
             self._addr = master_addr.encode()
+            own = None
+            if owners is not None:
+                own = (C.c_int32 * len(owners))(*[int(x) for x in owners])
+            self._owners = own  # kept alive for the call
             pipe = PipeOpts(int(rank), int(world), self._addr, int(bool(hop_bf16)),
-                            float(hop_timeout_s), float(connect_timeout_s))
+                            float(hop_timeout_s), float(connect_timeout_s),
+                            C.cast(own, C.POINTER(C.c_int32)) if own is not None else None,
+                            len(owners) if owners is not None else 0)
             self._h = lib().cake_engine_open_pp(str(model_dir).encode(), C.byref(opts),
                                                 C.byref(pipe), err, len(err))
         else:
@@ -143,6 +165,12 @@ class NativeLlama:
         eos = (C.c_int32 * 16)()
         n = lib().cake_engine_eos(self._h, eos, 16)
         self.eos_ids = [int(eos[i]) for i in range(min(n, 16))]
+
+    def walk(self) -> str:
+        """The token's walk as "rank:first-last" layer runs (comma separated)."""
+        buf = C.create_string_buffer(4096)
+        lib().cake_engine_walk(self._h, buf, len(buf))
+        return buf.value.decode()
 
     def serve(self) -> None:
         """Pipeline worker: run rank 0's prefill relays and replay announcements until it
@@ -171,6 +199,21 @@ class NativeLlama:
             raise RuntimeError(f"native engine: {err.value.decode(errors='replace')}")
         return out
 
+    def forced_logits(self, prompt: list[int], forced: list[int]):
+        """Teacher forcing: f32 logits [len(forced) + 1, V] after the prompt and after each
+        forced token (one eager decode step each, through every rank of the group)."""
+        import numpy as np
+        arr = (C.c_int32 * len(prompt))(*prompt)
+        fa = (C.c_int32 * max(1, len(forced)))(*forced)
+        out = np.empty((len(forced) + 1, self.vocab_size), dtype=np.float32)
+        err = C.create_string_buffer(1024)
+        rc = lib().cake_engine_forced_logits(self._h, arr, len(prompt), fa, len(forced),
+                                             out.ctypes.data_as(C.POINTER(C.c_float)), err,
+                                             len(err))
+        if rc:
+            raise RuntimeError(f"native engine: {err.value.decode(errors='replace')}")
+        return out
+
     def generate(self, prompt: list[int], max_new: int, *, temperature: float = 0.0,
                  top_k: int | None = None, top_p: float | None = None, seed: int = 299792458,
                  repeat_penalty: float = 1.1, repeat_last_n: int = 128,
@@ -180,6 +223,19 @@ class NativeLlama:
         smp = EngineSampling(float(temperature or 0.0), int(top_k or 0), float(top_p or 0.0),
                              int(seed) & 0xFFFFFFFFFFFFFFFF, float(repeat_penalty),
                              int(repeat_last_n))
+        return self._run(lambda eos_arr, n_eos, cb, out, stats, err: lib().cake_engine_generate(
+            self._h, arr, len(prompt), int(max_new), C.byref(smp), eos_arr, n_eos, cb, None, out,
+            max(1, max_new), stats, err, len(err)), max_new, eos_ids, on_token)
+
+    def continue_(self, max_new: int, *, eos_ids: list[int] | None = None,
+                  on_token: Callable[[int], bool | None] | None = None) -> GenResult:
+        """Up to max_new more tokens after the last generate / continue (same sampling;
+        the rate counts every token: all are decode steps)."""
+        return self._run(lambda eos_arr, n_eos, cb, out, stats, err: lib().cake_engine_continue(
+            self._h, int(max_new), eos_arr, n_eos, cb, None, out, max(1, max_new), stats, err,
+            len(err)), max_new, eos_ids, on_token)
+
+    def _run(self, call, max_new, eos_ids, on_token) -> GenResult:
         eos = list(eos_ids or [])
         eos_arr = (C.c_int32 * max(1, len(eos)))(*eos)
         out = (C.c_int32 * max(1, max_new))()
@@ -195,9 +251,7 @@ class NativeLlama:
                 return 1
 
         cb = TOKEN_CB(_tok) if on_token is not None else TOKEN_CB()
-        rc = lib().cake_engine_generate(self._h, arr, len(prompt), int(max_new), C.byref(smp),
-                                        eos_arr, len(eos), cb, None, out, max(1, max_new),
-                                        C.byref(stats), err, len(err))
+        rc = call(eos_arr, len(eos), cb, out, C.byref(stats), err)
         if errors:
             raise errors[0]
         if rc:
@@ -205,3 +259,20 @@ class NativeLlama:
         return GenResult([int(out[i]) for i in range(stats.n_generated)], stats.n_prompt,
                          stats.prefill_s, stats.decode_s, stats.tokens_per_s, stats.p50_ms,
                          stats.p99_ms)
+
+
+def owners_from_topology(topology, num_layers: int, world: int) -> list[int]:
+    """Layer -> pipeline rank of a topology: node i (file order) is rank i + 1, layers
+    no node names stay on rank 0 (the master), as the reference's placement loop
+    (cake-core/src/models/llama3/llama.rs:205-220, topology.rs:81-92)."""
+    from .parallel.rccl_roles import owners_from_topology as f
+    return f(topology, num_layers, world)
+
+
+def write_config(path: str | Path, cfg) -> Path:
+    """A model directory holding only ``config.json`` of ``cfg`` (random-init engines)."""
+    import json
+    p = Path(path)
+    p.mkdir(parents=True, exist_ok=True)
+    (p / "config.json").write_text(json.dumps(cfg.to_hf_dict()))
+    return p

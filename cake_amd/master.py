@@ -29,8 +29,7 @@ class Master:
         self.last_stats: dict = {}
         if llm is None and sd is None:
             if ctx.model_type == "text-model":
-                from .models.llama3.generator import LLamaGenerator
-                self.llm = LLamaGenerator.load(ctx)
+                self.llm = _load_text(ctx)
             else:
                 from .models.sd.pipeline import SDGenerator
                 self.sd = SDGenerator.load(ctx)
@@ -93,6 +92,10 @@ class Master:
                 lat = sorted(dev.step_ms)
             stats["p50_ms"] = lat[len(lat) // 2]
             stats["p99_ms"] = lat[min(len(lat) - 1, int(round(0.99 * (len(lat) - 1))))]
+            native = getattr(llm, "latency_ms", None)  # the native engine's device timing
+            pq = native() if callable(native) else None
+            if pq is not None:
+                stats["p50_ms"], stats["p99_ms"] = pq
         self._export(stats, t_start, times)
         log.info("%d tokens generated (%.2f token/s) p50=%.2fms p99=%.2fms ttft=%.1fms - mem=%.1f MiB",
                  generated, stats.get("tokens_per_sec", 0.0), stats.get("p50_ms", 0.0),
@@ -126,3 +129,16 @@ class Master:
 
     def generate_image(self, args, callback) -> None:
         self.sd.generate_image(args, callback)
+
+
+def _load_text(ctx):
+    """The native engine when it can serve this context (all-local on a GPU), else the
+    Python generator (CPU, f32, --no-graph, TCP workers in the placement, CAKE_NATIVE=0)."""
+    from .models.llama3.native_generator import NativeLLM, native_eligible
+    topo = getattr(ctx, "topology", None)
+    remote = bool(topo is not None and getattr(topo, "nodes", None))
+    if native_eligible(ctx, remote=remote):
+        log.info("text model on the native engine (libcake_engine.so)")
+        return NativeLLM.load(ctx)
+    from .models.llama3.generator import LLamaGenerator
+    return LLamaGenerator.load(ctx)

@@ -341,10 +341,66 @@ def run_tp(ctx) -> None:
         dist.destroy_process_group()
 
 
+def _native_rank_engine(ctx, rank: int, world: int, tp: bool):
+    """This rank's native engine of the group (pp: the topology's placement; tp: 1/N of
+    every layer).  Its control plane listens on MASTER_PORT + 1 (torchrun's store owns
+    MASTER_PORT); the decode hops / all-reduces are device-side inside every rank's graph."""
+    from ..engine import NativeLlama
+    from ..models.llama3.config import LlamaConfig
+    from ..models.llama3.native_generator import _dtype_name
+    a = ctx.args
+    cfg = LlamaConfig.from_path(ctx.model_path)
+    owners = None if tp else owners_from_topology(ctx.topology, cfg.num_hidden_layers, world)
+    if owners is not None and not any(owners):
+        owners = None  # no node places a layer: contiguous shards
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    addr = f"{os.environ.get('MASTER_ADDR', '127.0.0.1')}:{int(os.environ.get('MASTER_PORT', '29500')) + 1}"
+    timeout = float(os.environ.get("CAKE_HOP_TIMEOUT", "60"))
+    return NativeLlama(ctx.model_path, max_seq=ctx.max_seq_len, dtype=_dtype_name(ctx.dtype),
+                       device=local, rank=rank, world=world, master_addr=addr,
+                       hop_bf16=getattr(a, "hop_dtype", "f32") == "bf16", hop_timeout_s=timeout,
+                       tp=tp, owners=owners)
+
+
+def _native_group(ctx) -> bool:
+    """--transport rccl on the native engine: a GPU, 16-bit weights, graphs, device hops
+    (--hop ipc) or tensor parallel; CAKE_NATIVE=0 keeps the Python engines."""
+    from ..models.llama3.native_generator import native_eligible
+    a = ctx.args
+    tp = getattr(a, "parallel", "pp") == "tp"
+    return native_eligible(ctx) and (tp or getattr(a, "hop", "ipc") == "ipc")
+
+
+def run_native_rccl(ctx) -> None:
+    """Every rank runs the native engine; rank 0 is the master (CLI generation or the
+    REST API over :class:`NativeLLM`), the others serve it until it closes."""
+    from ..models.llama3.native_generator import NativeLLM
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    tp = getattr(ctx.args, "parallel", "pp") == "tp"
+    if ctx.device.type == "cuda":
+        local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(local)
+    eng = _native_rank_engine(ctx, rank, world, tp)
+    log.info("rank %d/%d: native engine, %s", rank, world,
+             "tensor parallel" if tp else f"walk {eng.walk()} (hops: ipc)")
+    try:
+        if rank == 0:
+            from ..master import Master
+            Master(ctx, llm=NativeLLM.load(ctx, engine=eng)).run()
+        else:
+            eng.serve()
+    finally:
+        eng.close()
+
+
 def run_rccl(ctx) -> None:
     if ctx.model_type == "image-model":
         from .sd_rccl import run_sd_rccl
         run_sd_rccl(ctx)
+        return
+    if _native_group(ctx):
+        run_native_rccl(ctx)
         return
     if getattr(ctx.args, "parallel", "pp") == "tp":
         run_tp(ctx)

@@ -178,11 +178,13 @@ def test_native_pipeline_two_ranks_share_one_gpu(cuda, ckpt, tmp_path):
     assert got["again"] == ref
 
 
-@pytest.mark.parametrize("par", ["pp", "tp"])
+@pytest.mark.parametrize("par", ["pp", "tp", "pp-topology"])
 def test_cake_cli_native_pipeline_torchrun(cuda, ckpt, tmp_path, par):
     """cake-cli --transport rccl --parallel pp|tp under torchrun (2 ranks sharing the GPU):
     the native pipeline prints the same text as the single-process native CLI (tensor
-    parallel: the same first tokens — partial sums change the rounding only)."""
+    parallel: the same first tokens — partial sums change the rounding only).  pp-topology:
+    topology.yml places layer 1 on the worker (node 1 -> rank 1): master 0, worker 1,
+    master 2, as the reference's placement loop."""
     import os
     import socket
     import subprocess
@@ -200,13 +202,18 @@ def test_cake_cli_native_pipeline_torchrun(cuda, ckpt, tmp_path, par):
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
+    extra = []
+    if par == "pp-topology":
+        topo = tmp_path / "t.yml"
+        topo.write_text("w1:\n  host: 'rank1'\n  layers:\n    - 'model.layers.1'\n")
+        extra = ["--topology", str(topo)]
     pp = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1",
                          "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port",
-                         str(port), "--no-python", cli, *common, "--transport", "rccl",
-                         "--parallel", par, "--hop", "ipc", "--hop-dtype", "f32"],
+                         str(port), "--no-python", cli, *common, *extra, "--transport", "rccl",
+                         "--parallel", par.split("-")[0], "--hop", "ipc", "--hop-dtype", "f32"],
                         capture_output=True, text=True, timeout=300, env=env, cwd=root)
     assert pp.returncode == 0, pp.stderr[-3000:]
-    if par == "pp":
+    if par.startswith("pp"):
         assert single.stdout.strip() and pp.stdout == single.stdout
     else:
         assert pp.stdout.strip() and pp.stdout[:8] == single.stdout[:8]
@@ -320,3 +327,195 @@ def test_native_tensor_parallel_two_ranks(cuda, ckpt, tmp_path):
     assert same >= 8, f"TP diverged from single-GPU at token {same}: {g} vs {ref}"
     assert got["again"] == g and len(got["sampled"]) == 16
     assert got["eos"] == g[:g.index(g[6]) + 1]
+
+
+# ---------------------------------------------------------------------------------------
+# multi-rank native groups: N rank processes (siblings, sharing the GPU on the 1-GPU pool)
+# ---------------------------------------------------------------------------------------
+def _port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _group(tmp_path, ckpt, world, rank0_body, kw="", timeout=240, tag="g"):
+    """Run rank 0 (``rank0_body`` with ``e`` the engine, printing ``out`` as JSON) and
+    world - 1 serving ranks; ``kw`` = extra NativeLlama keyword text.  Returns rank 0's
+    dict; on failure every rank's log is in the assertion message."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    addr = f"127.0.0.1:{_port()}"
+    head = ("import sys, json; sys.path.insert(0, %r)\n"
+            "from cake_amd.engine import NativeLlama\n"
+            "e = NativeLlama(%r, max_seq=1024, dtype='bf16', rank=%%d, world=%d, master_addr=%r, "
+            "hop_timeout_s=30.0%s)\n") % (root, str(ckpt), world, addr, kw)
+    r0 = head % 0 + "out = {'walk': e.walk()}\n" + rank0_body + \
+        "e.close()\nprint(json.dumps(out), flush=True)\n"
+    rw = head + "e.serve()\ne.close()\n"
+    logs = [tmp_path / f"{tag}{r}.log" for r in range(world)]
+    procs = [subprocess.Popen([sys.executable, "-c", r0 if r == 0 else rw % r],
+                              stdout=subprocess.PIPE, stderr=open(logs[r], "w"), text=True)
+             for r in range(world)]
+    try:
+        out0, _ = procs[0].communicate(timeout=timeout)
+        for p in procs[1:]:
+            p.wait(timeout=60)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    msg = "\n".join(f"---- {lg.name} ----\n" + lg.read_text()[-3000:] for lg in logs)
+    assert all(p.returncode == 0 for p in procs), msg
+    return json.loads(out0.strip().splitlines()[-1]), msg
+
+
+PROMPT = [1, 17, 300, 5, 99, 1024, 7, 8]
+
+
+@pytest.mark.parametrize("world,owners,walk", [
+    (2, [0, 1, 0], "0:0-0,1:1-1,0:2-2"),   # master, worker, master (llama.rs:95-114)
+    (2, [1, 0, 1], "1:0-0,0:1-1,1:2-2"),   # a worker visited twice per token
+    (3, [2, 1, 0], "2:0-0,1:1-1,0:2-2"),   # reversed ranks: edges 0->2->1->0
+    (3, [0, 0, 2], "0:0-1,2:2-2"),         # rank 1 idle (a topology node with no layers)
+])
+def test_native_pipeline_topology_placement(cuda, ckpt, tmp_path, world, owners, walk):
+    """cake_engine_open_pp with an owner map (topology.yml: node i -> rank i + 1): the walk
+    has one stop per maximal run and f32 hops are exact, so greedy and sampled tokens equal
+    the single-rank engine, and continue() extends a generation as one longer one."""
+    from cake_amd.engine import NativeLlama
+    single = NativeLlama(ckpt, max_seq=1024, dtype="bf16")
+    ref = single.generate(PROMPT, 30, repeat_penalty=1.1, repeat_last_n=16).tokens
+    ref_s = single.generate(PROMPT, 20, temperature=0.7, top_k=40, seed=11,
+                            repeat_penalty=1.1, repeat_last_n=16).tokens
+    single.close()
+    body = ("g = e.generate(%r, 18, repeat_penalty=1.1, repeat_last_n=16).tokens\n"
+            "out['greedy'] = g + e.continue_(12).tokens\n"
+            "out['sampled'] = e.generate(%r, 20, temperature=0.7, top_k=40, seed=11,\n"
+            "                            repeat_penalty=1.1, repeat_last_n=16).tokens\n"
+            ) % (PROMPT, PROMPT)
+    got, msg = _group(tmp_path, ckpt, world, body, kw=", owners=%r" % (owners,))
+    assert got["walk"] == walk, msg
+    assert got["greedy"] == ref, msg
+    assert got["sampled"] == ref_s, msg
+
+
+def _forced_ref(ckpt, n):
+    """Single-rank engine: its greedy tokens and the teacher-forced logits along them."""
+    from cake_amd.engine import NativeLlama
+    single = NativeLlama(ckpt, max_seq=1024, dtype="bf16")
+    toks = single.generate(PROMPT, n + 1, repeat_penalty=1.0).tokens
+    ref = single.forced_logits(PROMPT, toks[:n])
+    single.close()
+    return toks[:n], ref
+
+
+def _assert_forced_close(got, ref, rel, what):
+    """Every step's logits within rel x max|logit| of the single-rank engine's, and the
+    argmax equal wherever the single-rank top-2 margin exceeds that bound."""
+    import numpy as np
+    got, ref = np.asarray(got, dtype=np.float32), np.asarray(ref, dtype=np.float32)
+    assert got.shape == ref.shape
+    tol = rel * float(np.abs(ref).max())
+    err = float(np.abs(got - ref).max())
+    assert err <= tol, f"{what}: max |dlogit| {err:.4g} > {tol:.4g}"
+    top2 = np.sort(ref, axis=1)[:, -2:]
+    sure = (top2[:, 1] - top2[:, 0]) > 2 * tol
+    assert (got.argmax(1)[sure] == ref.argmax(1)[sure]).all(), f"{what}: argmax differs"
+
+
+def test_native_pipeline_bf16_hops_world3_teacher_forced(cuda, ckpt, tmp_path):
+    """bf16 hop payloads (half the bytes; the reference ships the model dtype) over a
+    3-rank walk: teacher-forced over 32 decode steps, every step's logits within 2 % of
+    the logit range of the single-rank engine's (f32 hops are exact; bf16 rounds the
+    residual stream at each of the 3 edges)."""
+    import numpy as np
+    forced, ref = _forced_ref(ckpt, 32)
+    body = "import numpy as np\nout['logits'] = e.forced_logits(%r, %r).tolist()\n" % (PROMPT, forced)
+    got, msg = _group(tmp_path, ckpt, 3, body, kw=", hop_bf16=True")
+    assert got["walk"] == "0:0-0,1:1-1,2:2-2", msg
+    _assert_forced_close(np.array(got["logits"]), ref, 0.02, "pp3 bf16 hops")
+    # f32 hops: exact
+    got2, msg = _group(tmp_path, ckpt, 3, body, tag="f")
+    assert np.array_equal(np.array(got2["logits"], dtype=np.float32), ref), msg
+
+
+@pytest.fixture(scope="module")
+def ckpt3(tmp_path_factory):
+    """3 KV heads (6 query heads, head_dim 64): tensor parallelism of degree 3."""
+    d = tmp_path_factory.mktemp("native_ckpt3")
+    cfg = preset("llama3-8b", num_hidden_layers=3, vocab_size=2048, intermediate_size=768,
+                 hidden_size=384, num_attention_heads=6, num_key_value_heads=3,
+                 bos_token_id=1, eos_token_id=2)
+    write_checkpoint(d, cfg, torch.bfloat16, seed=4, single_file=True)
+    return d
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_native_tensor_parallel_teacher_forced(cuda, ckpt, ckpt3, tmp_path, world):
+    """Native tensor parallelism teacher-forced over 32 decode steps (the decode kernels and
+    device all-reduces of the captured step, launched eagerly): every step's logits within
+    1 % of the logit range of the single-rank engine's (partial sums reorder f32 adds and
+    round each rank's bf16 attention / MLP activations), argmax equal wherever the margin
+    is larger; then greedy generate + continue in lock step."""
+    import numpy as np
+    ck = ckpt if world == 2 else ckpt3
+    forced, ref = _forced_ref(ck, 32)
+    body = ("out['logits'] = e.forced_logits(%r, %r).tolist()\n"
+            "g = e.generate(%r, 10, repeat_penalty=1.0).tokens\n"
+            "out['gen'] = g + e.continue_(6).tokens\n"
+            "out['eos'] = e.generate(%r, 16, repeat_penalty=1.0, eos_ids=[g[4]]).tokens\n"
+            ) % (PROMPT, forced, PROMPT, PROMPT)
+    got, msg = _group(tmp_path, ck, world, body, kw=", tp=True", tag=f"tp{world}_")
+    _assert_forced_close(np.array(got["logits"]), ref, 0.01, f"tp{world}")
+    g = got["gen"]
+    assert len(g) == 16 and g[0] == forced[0], msg
+    assert got["eos"] == g[:g.index(g[4]) + 1], msg
+
+
+def test_native_engine_attention_error_word(cuda, ckpt):
+    """A split-K attention merge that gives up waiting (test hook: the other splits never
+    publish) sets tickets[2 nkv]; the engine raises after the generation instead of
+    returning its tokens, clears the word, and the next generation is correct."""
+    from cake_amd.engine import NativeLlama
+    from cake_amd.ops import hip as K
+    g = torch.Generator().manual_seed(5)
+    prompt = torch.randint(3, 2048, (400,), generator=g).tolist()  # > 320 keys: split merge
+    eng = NativeLlama(ckpt, max_seq=1024, dtype="bf16")
+    ref = eng.generate(prompt, 4, repeat_penalty=1.0).tokens
+    K.attn_debug_drop_partials(True)
+    try:
+        with pytest.raises(RuntimeError, match="split merge timed out"):
+            eng.generate(prompt, 3, repeat_penalty=1.0)
+    finally:
+        K.attn_debug_drop_partials(False)
+    assert eng.generate(prompt, 4, repeat_penalty=1.0).tokens == ref
+    eng.close()
+
+
+def test_native_continue_equals_one_generation(cuda, ckpt):
+    from cake_amd.engine import NativeLlama
+    eng = NativeLlama(ckpt, max_seq=1024, dtype="bf16")
+    ref = eng.generate(PROMPT, 40, repeat_penalty=1.1, repeat_last_n=16).tokens
+    a = eng.generate(PROMPT, 15, repeat_penalty=1.1, repeat_last_n=16).tokens
+    b = eng.continue_(10).tokens
+    c = eng.continue_(15).tokens
+    assert a + b + c == ref
+    # random init: config.json only, seeded device draws (benchmarks); deterministic
+    from cake_amd.engine import write_config
+    from cake_amd.models.llama3.config import LlamaConfig
+    import tempfile
+    d = write_config(tempfile.mkdtemp(), LlamaConfig.from_path(ckpt))
+    r1 = NativeLlama(d, max_seq=256, dtype="bf16", random_init=True, seed=7)
+    t1 = r1.generate(PROMPT, 12, repeat_penalty=1.0).tokens
+    r1.close()
+    r2 = NativeLlama(d, max_seq=256, dtype="bf16", random_init=True, seed=7)
+    assert r2.generate(PROMPT, 12, repeat_penalty=1.0).tokens == t1
+    r2.close()
+    eng.close()
