@@ -20,6 +20,11 @@
 //     split 0 polls and merges; core 1 (attn_core.h): 64-key LDS chunks, the
 //     last-arriving split merges behind a ticket.
 //   * Prefill attention is the MFMA flash kernel (flash_attn.hip).
+#include <cstdio>
+#include <mutex>
+#include <utility>
+#include <vector>
+
 #include "attn_core.h"
 #include "attn_core2.h"
 
@@ -164,20 +169,38 @@ CAKE_API int cake_attn_set_min_keys(int min_keys) {
 // workgroup of the grid must be resident at once; a grid larger than the device can hold
 // (several waves per CU taken by other work would not be visible here, but a grid the
 // empty device cannot hold is refused) runs core 1's last-arriver merge instead.
+// The occupancy query is made once per kernel (a small table keyed by the kernel's
+// address: eager launches of the non-graph paths no longer pay a runtime call per layer),
+// and a fallback to core 1 is reported once.
 template <class K>
 static bool grid_resident(K kern, int threads, long long blocks) {
+  static std::mutex mu;
   static int cus = 0;
+  static std::vector<std::pair<const void*, int>> per_cu_of;
+  static bool warned = false;
+  std::lock_guard<std::mutex> g(mu);
   if (cus == 0) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       return false;
   }
-  int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, threads, 0) !=
-      hipSuccess)
-    return false;
-  return (long long)per_cu * cus >= blocks;
+  int per_cu = -1;
+  for (const auto& e : per_cu_of)
+    if (e.first == (const void*)kern) per_cu = e.second;
+  if (per_cu < 0) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, threads, 0) !=
+        hipSuccess)
+      return false;
+    per_cu_of.push_back({(const void*)kern, per_cu});
+  }
+  const bool ok = (long long)per_cu * cus >= blocks;
+  if (!ok && !warned) {
+    warned = true;
+    std::fprintf(stderr, "[cake] decode attention: a %lld-workgroup grid exceeds residency "
+                 "(%d per CU x %d CUs): core 1 merge for such grids\n", blocks, per_cu, cus);
+  }
+  return ok;
 }
 
 template <int DT, int HD>

@@ -215,6 +215,7 @@ class LayerStack:
         persistent decode's hand-offs, or the split-K attention merge (host sync)."""
         from ...ops import hip as K
         if K.attn_error(bufs.tickets):
+            K.attn_clear_error(bufs.tickets)
             raise RuntimeError("decode attention: a split merge timed out waiting for its "
                                "partials; outputs of that launch are invalid")
         ctl = getattr(bufs, "mk_ctl", None)

@@ -63,7 +63,9 @@ def run_decode(dec: DeviceDecoder, n_steps: int, eos_ids: set[int] | None = None
         return st
 
     if dec.graph is not None:
-        return _run_native(dec, n_steps, eos_ids, on_token)
+        st = _run_native(dec, n_steps, eos_ids, on_token)
+        _check(dec)
+        return st
     # eager (no graphs): every launch runs dec.k steps; their tokens are the next k
     # entries of the device history, copied to a pinned ring one launch behind
     k = dec.k
@@ -108,7 +110,17 @@ def run_decode(dec: DeviceDecoder, n_steps: int, eos_ids: set[int] | None = None
         pending[1].synchronize()
     st.wall_s = time.perf_counter() - t0
     del dev
+    _check(dec)
     return st
+
+
+def _check(dec: DeviceDecoder) -> None:
+    """Raise (and re-arm) when a decode launch of this run gave up in a bounded spin:
+    the split-K attention merge's error word (tickets[2 nkv]) or a persistent-decode
+    hand-off — its tokens are invalid (one host read, after the loop's final sync)."""
+    stack = getattr(dec.m, "stack", None)
+    if stack is not None and getattr(stack, "backend", "hip") == "hip":
+        stack.mk_check(dec.bufs)
 
 
 def _run_native(dec: DeviceDecoder, n_steps: int, eos_ids, on_token) -> DecodeStats:

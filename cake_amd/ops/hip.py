@@ -302,6 +302,11 @@ def attn_error(tickets) -> bool:
     return int(tickets[-2].item()) != 0
 
 
+def attn_clear_error(tickets) -> None:
+    """Re-arm the error word after it was reported (the kernels never clear it)."""
+    tickets[-2].zero_()
+
+
 def attn_debug_drop_partials(on: bool) -> None:
     """Test hook: core 2's splits >= 1 stop publishing, so the merges time out."""
     check(kernels().cake_attn_debug_drop_partials(int(bool(on))), "attn_debug_drop_partials")
@@ -700,13 +705,18 @@ _flash_ws_keep: list = []
 
 
 def _flash_ws(dev, numel: int) -> torch.Tensor:
-    """f32 partial rows of the key-split flash path.  Superseded buffers stay alive: a
-    captured hipGraph may still point at them."""
-    w = _flash_wsd.get(dev)
+    """f32 partial rows of the key-split flash path, one buffer per (device, stream): the
+    launches of one stream are serialized, so they may share it; work on another stream
+    (a graph captured on torch's capture stream, a side stream) gets its own.  A graph
+    replayed later must be replayed on the stream order it was captured in (the usual
+    single-stream replay).  Superseded buffers stay alive: a captured hipGraph may still
+    point at them."""
+    key = (dev, torch.cuda.current_stream(dev).cuda_stream)
+    w = _flash_wsd.get(key)
     if w is None or w.numel() < numel:
         if w is not None:
             _flash_ws_keep.append(w)
-        w = _flash_wsd[dev] = torch.empty(numel, dtype=torch.float32, device=dev)
+        w = _flash_wsd[key] = torch.empty(numel, dtype=torch.float32, device=dev)
     return w
 
 

@@ -391,6 +391,9 @@ class PipelineEngine:
         if self.hop == "ipc" and int(self._err.item()) != 0:
             raise RuntimeError(f"rank {self.rank}: a pipeline hop timed out "
                                f"(CAKE_HOP_TIMEOUT={os.environ.get('CAKE_HOP_TIMEOUT', '60')} s)")
+        if self.hip:
+            for st in self.streams:
+                self.stack.mk_check(st.bufs)
 
     def measure_hop_us(self, iters: int = 100) -> float | None:
         """One-way latency of a decode hop between ranks 0 and 1 (ping-pong; µs).

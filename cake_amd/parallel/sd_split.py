@@ -227,13 +227,24 @@ def measure_sd_split(env, steps: int = 4, warmup: int = 2, version: str = "xl",
     hip = dev.type == "cuda"
     if not hip:
         dtype = torch.float32
-    t_load = time.perf_counter()
-    W = random_component_on_device("unet", cfg, dev, dtype, seed=7,
-                                   keep=unet_stage_keep(names, len(stages)))
-    if hip:
-        torch.cuda.synchronize(dev)
-    load_s = time.perf_counter() - t_load
     meta = dist.new_group(list(range(world)), backend="gloo")
+    t_load = time.perf_counter()
+    err = None
+    try:
+        W = random_component_on_device("unet", cfg, dev, dtype, seed=7,
+                                       keep=unet_stage_keep(names, len(stages)))
+        if hip:
+            torch.cuda.synchronize(dev)
+    except Exception as e:  # noqa: BLE001  (reported to every rank below)
+        err = f"rank {rank}: {type(e).__name__}: {e}"[:300]
+    # a setup failure on ONE rank (e.g. an OOM drawing its stage weights) must stop every
+    # rank before the step loop, not leave the peers blocked in a hop receive
+    oks: list = [None] * world
+    dist.all_gather_object(oks, err, group=meta)
+    bad = [x for x in oks if x]
+    if bad:
+        raise RuntimeError("split-UNet setup failed: " + "; ".join(bad))
+    load_s = time.perf_counter() - t_load
     link = PackedLink(dev, meta, None)
     g = torch.Generator(device="cpu").manual_seed(11)
     emb = torch.randn(2, 77, cfg.unet.cross_attention_dim, generator=g).to(dev, dtype)

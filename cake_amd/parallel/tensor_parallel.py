@@ -722,6 +722,12 @@ class TPEngine:
     def check(self) -> None:
         if self.comm.errors():
             raise RuntimeError("tensor-parallel all-reduce timed out (a peer stopped?)")
+        if self.hip:
+            from ..ops import hip as K
+            if K.attn_error(self.b.tickets):
+                K.attn_clear_error(self.b.tickets)
+                raise RuntimeError(f"tensor-parallel rank {self.rank}: decode attention split "
+                                   "merge timed out; outputs of that launch are invalid")
 
     def close(self) -> None:
         self.comm.close()

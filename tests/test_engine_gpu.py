@@ -489,13 +489,14 @@ def test_native_engine_attention_error_word(cuda, ckpt):
     prompt = torch.randint(3, 2048, (400,), generator=g).tolist()  # > 320 keys: split merge
     eng = NativeLlama(ckpt, max_seq=1024, dtype="bf16")
     ref = eng.generate(prompt, 4, repeat_penalty=1.0).tokens
+    # the hook is a launch argument: a new sampling mode recaptures the graphs with it
     K.attn_debug_drop_partials(True)
     try:
         with pytest.raises(RuntimeError, match="split merge timed out"):
-            eng.generate(prompt, 3, repeat_penalty=1.0)
+            eng.generate(prompt, 3, repeat_penalty=1.05)
     finally:
         K.attn_debug_drop_partials(False)
-    assert eng.generate(prompt, 4, repeat_penalty=1.0).tokens == ref
+    assert eng.generate(prompt, 4, repeat_penalty=1.0).tokens == ref  # recaptured, clean
     eng.close()
 
 
