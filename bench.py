@@ -77,6 +77,9 @@ def _args(argv=None):
                     help="skip the N=1 Stable Diffusion seconds/step sub-record")
     ap.add_argument("--no-extras", action="store_true",
                     help="headline only: skip the tp / llama3_70b sub-records")
+    ap.add_argument("--extras", default="all",
+                    help="comma list of the sub-records to run: tp (or pp: the other mode), "
+                         "pp_streams, 70b_pp, 70b_tp, 70b_single, sd (default: all)")
     ap.add_argument("--tiny-extras", action="store_true",
                     help="run every sub-record (tp, pp_streams, 70B pp/tp, split SD) on the "
                          "tiny presets: the N-rank plumbing of the full default bench, cheap "
@@ -255,9 +258,18 @@ def _extra_runs(a):
     other = "tp" if a.parallel == "pp" else "pp"
     # pp_streams: the same layer-sharded pipeline with one sequence in flight per stage
     # (N independent batch-1 requests; aggregate tok/s — the pipeline's serving throughput)
-    return [((other,), m8, other), (("pp_streams",), m8, "pp_streams"),
-            (("llama3_70b", "pp"), m70, "pp"),
-            (("llama3_70b", "tp"), m70, "tp")]
+    # the Python pipeline (pp_streams) runs last: a speculative replay it leaves queued
+    # on a rank must not share a hardware queue with a later engine's replays
+    runs = [((other,), m8, other), (("llama3_70b", "pp"), m70, "pp"),
+            (("llama3_70b", "tp"), m70, "tp"), (("pp_streams",), m8, "pp_streams")]
+    return [r for r in runs if _want(a, "_".join(("70b",) + r[0][1:]) if r[0][0] == "llama3_70b"
+                                     else r[0][0])]
+
+
+def _want(a, name: str) -> bool:
+    """--extras selection (default all)."""
+    sel = {x.strip() for x in str(getattr(a, "extras", "all")).split(",") if x.strip()}
+    return "all" in sel or name in sel
 
 
 def _native(a) -> bool:
@@ -271,7 +283,7 @@ def bench_single(a) -> None:
         measure = measure_single
     r = measure(a, a.model, a.steps, a.warmup, a.dump_tokens)
     extra = {k: v for k, v in r.items() if k not in _MAIN_KEYS}
-    if not a.no_extras and a.model == "llama3-8b":
+    if not a.no_extras and a.model == "llama3-8b" and _want(a, "70b_single"):
         # the 70B point on one GPU (135 GB of bf16 weights in 288 GB of HBM)
         try:
             extra["llama3_70b"] = {"single": _summary(measure(a, "llama3-70b", a.steps,
@@ -280,7 +292,7 @@ def bench_single(a) -> None:
             extra["llama3_70b"] = {"single": None, "error": f"{type(e).__name__}: {e}"[:300]}
         # the reference's second metric: SD seconds per diffusion step (SDXL 1024^2,
         # CFG batch 2, the UNet + scheduler step as one graph replay)
-        if not a.no_sd:
+        if not a.no_sd and _want(a, "sd"):
             try:
                 from cake_amd.models.sd.bench import measure_denoise
                 extra["sd"] = {"sdxl_1024": measure_denoise("xl", 8)}
@@ -328,7 +340,7 @@ def bench_multi(a) -> None:
                 for k in path[:-1]:
                     d = d.setdefault(k, {})
                 d[path[-1]] = r
-        if _extras_on(a) and not a.no_sd:
+        if _extras_on(a) and not a.no_sd and _want(a, "sd"):
             # BASELINE config 5: SDXL 1024^2 (CFG) with the UNet's block groups split over
             # the N ranks; seconds per diffusion step of one image (parallel/sd_split.py)
             from cake_amd.parallel.sd_split import measure_sd_split

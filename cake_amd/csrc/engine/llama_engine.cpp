@@ -29,6 +29,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <list>
@@ -321,6 +322,23 @@ std::pair<int, int> split_range(int n, int world, int rank) {
   return {a, a + q + (rank < r ? 1 : 0)};
 }
 
+// CAKE_ENGINE_TRACE=1: control-plane progress on stderr (rank-tagged, seconds since the
+// process's first trace line) — where a multi-rank start or generation stands
+bool trace_on() {
+  static const bool on = [] {
+    const char* v = std::getenv("CAKE_ENGINE_TRACE");
+    return v && *v && std::string(v) != "0";
+  }();
+  return on;
+}
+void trace(int rank, const std::string& what) {
+  if (!trace_on()) return;
+  static const auto t0 = std::chrono::steady_clock::now();
+  const double t = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  std::fprintf(stderr, "[engine r%d +%.3fs] %s\n", rank, t, what.c_str());
+  std::fflush(stderr);
+}
+
 std::string hex_of(const void* p, size_t n) {
   static const char* d = "0123456789abcdef";
   std::string s;
@@ -442,10 +460,14 @@ class Llama {
     planner_.load(pkg_dir() + "/ops/gemm_tuned.json");
     load_weights(dir);
     alloc_state();
+    trace(rank(), "weights + state ready (" + std::to_string(owned_.size()) + " layers)");
     if (world_ > 1) {
       connect_pipeline(pp->master_addr ? pp->master_addr : "127.0.0.1:29517",
                        pp->connect_timeout_s > 0 ? pp->connect_timeout_s : 600.0);
+      trace(rank_, "pipeline connected: walk " + walk_str() + ", " +
+                       std::to_string(edges_.size()) + " edges");
       selftest_pipeline();
+      trace(rank_, "pipeline self-test passed");
     }
     if (tp_ > 1) {
       connect_tp(tp->master_addr ? tp->master_addr : "127.0.0.1:29517",
@@ -614,7 +636,10 @@ class Llama {
       spec.token_ctx = &tps;
     }
     CakeLoopResult res{};
+    trace(rank(), "decode " + std::to_string(n) + " tokens from length " + std::to_string(L));
     const int rc = cake_graph_decode(&spec, &res);
+    trace(rank(), "decode loop done: " + std::to_string(res.n_tokens) + " tokens, " +
+                      std::to_string(res.replays) + " replays, rc " + std::to_string(rc));
     if (world_ > 1) sync_workers();
     if (tp_ > 1 && lead) sync_tp_workers();
     k_check(rc, "graph_decode");
@@ -1168,6 +1193,7 @@ class Llama {
       Json m = msg("prefill");
       m.set("T", Json::integer(T));
       m.set("stop", Json::integer((int64_t)i));
+      trace(rank_, "prefill stop " + std::to_string(i) + " -> rank " + std::to_string(s.rank));
       send_json(peers_[s.rank - 1], m);
       const Json ack = recv_json(peers_[s.rank - 1]);
       if (!ack.has("ok") || !ack.get("ok").as_bool())
@@ -1509,6 +1535,7 @@ class Llama {
     for (;;) {
       const Json m = recv_json(ctl_fd_);
       const std::string cmd = m.get("cmd").as_string();
+      trace(rank_, "control: " + m.dump().substr(0, 120));
       if (cmd == "exit") break;
       if (cmd == "prefill") {
         Json r = Json::object();
@@ -2070,6 +2097,7 @@ class Llama {
   // one graph per attention split cap (DeviceDecoder.capture position buckets)
   void ensure_graphs(const Mode& m) {
     if (have_graphs_ && graph_mode_ == m) return;
+    trace(rank(), "capturing decode graphs");
     drop_graphs();
     if (!head_) {  // pipeline worker: its layers once, eagerly, at position 0 (the row is
                    // rewritten by every prefill), so no kernel's first launch is captured

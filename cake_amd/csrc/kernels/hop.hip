@@ -68,7 +68,10 @@ __global__ __launch_bounds__(kHopThreads) void hop_recv_kernel(
   const int nw = nh + nhdr;
   uint32_t* hw = reinterpret_cast<uint32_t*>(dst + H);
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  bool timed_out = false;
+  // fail fast: once a receive of this rank timed out (the error word is set until the
+  // host reads and clears it), later receives of the same run do not wait again — a
+  // dead peer costs one timeout, not one per queued replay
+  bool timed_out = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
   for (int i = threadIdx.x; i < nw; i += kHopThreads) {
     unsigned long long g;
     for (;;) {
