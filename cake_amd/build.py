@@ -80,7 +80,7 @@ def _compile_hip(src: Path, force: bool) -> Path:
 def _compile_cpp(src: Path, force: bool, extra: list[str] | None = None) -> Path:
     out = BUILD / "runtime" / (src.stem + ".o")
     out.parent.mkdir(parents=True, exist_ok=True)
-    headers = sorted((CSRC / "runtime").glob("*.h"))
+    headers = sorted((CSRC / "runtime").glob("*.h")) + [CSRC / "engine" / "llama_engine.h"]
     if force or _newer(src, headers, out):
         _run([CXX, "-O2", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
               "-fvisibility=hidden", *(extra or []), "-c", str(src), "-o", str(out)])
@@ -122,7 +122,7 @@ def build_runtime(force: bool = False, jobs: int = 8) -> Path:
     """C++ host runtime: pybind11 module, C-ABI library, split-model tool and cake-cli."""
     rt = CSRC / "runtime"
     core_srcs = [rt / f"{n}.cpp" for n in ("json", "topology", "proto", "net", "safetensors",
-                                            "server")]
+                                            "server", "native_worker")]
     inc, ext = _py_ext_flags()
     einc, elink = _embed_flags()
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
@@ -134,14 +134,15 @@ def build_runtime(force: bool = False, jobs: int = 8) -> Path:
     LIB.mkdir(parents=True, exist_ok=True)
     pyext = PY_EXT.with_name(PY_EXT.name + ext)
     if force or any(_newer(o, [], pyext) for o in [*core, bind]):
-        _run([CXX, "-shared", "-fPIC", *map(str, core), str(bind), "-o", str(pyext), "-lpthread"])
+        _run([CXX, "-shared", "-fPIC", *map(str, core), str(bind), "-o", str(pyext), "-lpthread",
+              "-ldl"])
     if force or any(_newer(o, [], RUNTIME_LIB) for o in [*core, capi, emb]):
         _run([CXX, "-shared", "-fPIC", *map(str, core), str(capi), str(emb), "-o",
               str(RUNTIME_LIB), *elink])
     tool = CSRC / "tools" / "split_model.cpp"
     if force or _newer(tool, [*core, *sorted(rt.glob("*.h"))], SPLIT_TOOL):
         _run([CXX, "-O2", "-std=c++17", f"-I{rt}", str(tool), *map(str, core), "-o",
-              str(SPLIT_TOOL), "-lpthread"])
+              str(SPLIT_TOOL), "-lpthread", "-ldl"])
     cli = CSRC / "tools" / "cake_cli.cpp"
     if force or _newer(cli, [*core, emb, *sorted(rt.glob("*.h")), CSRC / "engine" / "llama_engine.h"],
                        CLI_TOOL):

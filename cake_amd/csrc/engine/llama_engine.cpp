@@ -44,6 +44,7 @@
 #include "../driver/graph_loop.h"
 #include "../runtime/json.h"
 #include "../runtime/net.h"
+#include "../runtime/proto.h"
 #include "../runtime/safetensors.h"
 
 #define CAKE_API extern "C" __attribute__((visibility("default")))
@@ -374,7 +375,8 @@ Json msg(const char* cmd) {
 class Llama {
  public:
   Llama(const std::string& dir, const CakeEngineOpts& o, const CakePipeOpts* pp = nullptr,
-        const std::vector<int>* layers = nullptr, const CakeTPOpts* tp = nullptr)
+        const std::vector<int>* layers = nullptr, const CakeTPOpts* tp = nullptr,
+        const CakeRemoteOpts* remote = nullptr)
       : dt_(o.dtype), dev_(o.device), init_(o.init), seed_(o.seed) {
     if (dt_ != 0 && dt_ != 1) throw Error("dtype must be 0 (bf16) or 1 (f16)");
     if (init_ != 0 && init_ != 1) throw Error("init must be 0 (checkpoint) or 1 (random)");
@@ -448,8 +450,19 @@ class Llama {
         for (int r = 0; r < world_; ++r)
           for (int l = sh[r].first; l < sh[r].second; ++l) owner_[l] = r;
       }
+      if (remote) {  // TCP workers: layer -> worker index, -1 = local
+        if (remote->n_layers != cfg_.L || !remote->worker_of)
+          throw Error("remote placement must name every layer (-1 = local)");
+        remote_of_.assign(remote->worker_of, remote->worker_of + cfg_.L);
+        for (int l = 0; l < cfg_.L; ++l)
+          if (remote_of_[l] < -1 || remote_of_[l] >= remote->n_workers)
+            throw Error("layer " + std::to_string(l) + " placed on an unknown worker");
+        for (int w = 0; w < remote->n_workers; ++w)
+          remotes_.push_back({remote->workers[w] ? remote->workers[w] : "", -1});
+        remote_timeout_ = remote->timeout_s > 0 ? remote->timeout_s : 60.0;
+      }
       for (int l = 0; l < cfg_.L; ++l)
-        if (owner_[l] == rank_) owned_.push_back(l);
+        if (owner_[l] == rank_ && (remote_of_.empty() || remote_of_[l] < 0)) owned_.push_back(l);
       head_ = rank_ == 0;
     }
     lo_ = owned_.empty() ? 0 : owned_.front();
@@ -474,6 +487,7 @@ class Llama {
                  tp->connect_timeout_s > 0 ? tp->connect_timeout_s : 600.0);
       selftest_tp();
     }
+    if (!remotes_.empty()) connect_remotes();
   }
 
   ~Llama() {
@@ -488,6 +502,8 @@ class Llama {
       }
     for (int fd : peers_) tcp_close(fd);
     if (ctl_fd_ >= 0) tcp_close(ctl_fd_);
+    for (auto& r : remotes_)
+      if (r.fd >= 0) tcp_close(r.fd);
     drop_graphs();
     for (void* p : tp_mapped_) (void)hipIpcCloseMemHandle(p);
     for (void* p : tp_owned_) (void)cake_hop_free(p);
@@ -569,7 +585,9 @@ class Llama {
     }
     const auto t0 = std::chrono::steady_clock::now();
     std::vector<float> ms;
-    const int n_out = decode_tokens(L, max_new, eos, n_eos, cb, ctx, out, out_cap, true, &ms);
+    const int n_out = remote_mode()
+                          ? decode_eager(max_new, last_mode_, eos, n_eos, cb, ctx, out, out_cap, &ms)
+                          : decode_tokens(L, max_new, eos, n_eos, cb, ctx, out, out_cap, true, &ms);
     const auto t1 = std::chrono::steady_clock::now();
     if (stats) {
       fill_stats(stats, L, n_out, 0.0, std::chrono::duration<double>(t1 - t0).count(), ms);
@@ -707,11 +725,19 @@ class Llama {
       if (tp_ == 1) stop = stop || cb_stop;  // TP: only EOS stops (all ranks alike)
     }
     std::vector<float> ms;
-    // graphs exist after every generation (continue() replays them), even a 1-token one
-    ensure_graphs(mode);
-    if (!stop && max_new > 1)
-      n_out += decode_tokens(T + 1, max_new - 1, eos, n_eos, cb, ctx, lead ? out + n_out : nullptr,
-                             lead ? out_cap - n_out : 0, lead, &ms);
+    last_mode_ = mode;
+    if (remote_mode()) {  // host round trips inside the step: eager
+      have_graphs_ = true;  // continue() may follow
+      if (!stop && max_new > 1)
+        n_out += decode_eager(max_new - 1, mode, eos, n_eos, cb, ctx, out + n_out,
+                              out_cap - n_out, &ms);
+    } else {
+      // graphs exist after every generation (continue() replays them), even a 1-token one
+      ensure_graphs(mode);
+      if (!stop && max_new > 1)
+        n_out += decode_tokens(T + 1, max_new - 1, eos, n_eos, cb, ctx,
+                               lead ? out + n_out : nullptr, lead ? out_cap - n_out : 0, lead, &ms);
+    }
     const auto t2 = std::chrono::steady_clock::now();
     if (stats)
       fill_stats(stats, T, n_out, std::chrono::duration<double>(t1 - t0).count(),
@@ -765,13 +791,23 @@ class Llama {
   // consecutive layers on one rank, then the head on rank 0.  An edge joins consecutive
   // stops on different ranks; each edge has its own inbox on the receiving rank and its
   // own sequence words (seq_[2e] send side, seq_[2e + 1] receive side).
-  enum StopKind { kEmbedStop, kRunStop, kHeadStop };
+  enum StopKind { kEmbedStop, kRunStop, kHeadStop, kRemoteStop };
   struct Stop {
     StopKind kind;
     int rank;
     std::vector<int> layers;  // global ids (runs)
     std::vector<int> sel;     // the same as this rank's local layer slots
+    int remote = -1;          // kRemoteStop: index into remotes_
   };
+  // TCP workers (master side): one connection each, Hello -> WorkerInfo at open
+  struct RemoteWorker {
+    std::string addr;
+    int fd;
+  };
+  std::vector<RemoteWorker> remotes_;
+  std::vector<int> remote_of_;  // layer -> remote worker, -1 = local
+  double remote_timeout_ = 60.0;
+  std::vector<float> host_rows_;  // staging of the hidden rows a remote run transforms
   std::vector<Stop> walk_;
   std::vector<int> edge_in_;                // per stop: the edge feeding it, or -1
   std::vector<std::pair<int, int>> edges_;  // (src rank, dst rank)
@@ -829,7 +865,7 @@ class Llama {
   std::vector<hipGraphExec_t> execs_;
   std::vector<hipGraph_t> graphs_;
   std::vector<int32_t> bucket_of_;
-  Mode graph_mode_;
+  Mode graph_mode_, last_mode_;
   bool have_graphs_ = false;
 
   template <class T> T* dalloc(size_t n) {
@@ -1185,6 +1221,10 @@ class Llama {
     // stop hands its rows to the next stop's rank (the last one back to this rank)
     for (size_t i = 0; i + 1 < walk_.size(); ++i) {
       const Stop& s = walk_[i];
+      if (s.kind == kRemoteStop) {
+        remote_rows(s, 0, hidden_, T);
+        continue;
+      }
       if (s.rank == 0) {
         if (s.kind == kRunStop) prefill_layers(T, 0, &s.sel);
         if (edge_in_[i + 1] >= 0) forward_hidden(T, walk_[i + 1].rank);
@@ -1301,6 +1341,8 @@ class Llama {
         if (!m.fused) k_check(cake_embed(dt_, embed_, tok_, 1, cfg_.H, resid_, st_), "embed");
       } else if (s.kind == kRunStop) {
         step_layers(&s.sel);
+      } else if (s.kind == kRemoteStop) {
+        remote_step(s);
       } else {
         step_head(m);
       }
@@ -1329,6 +1371,13 @@ class Llama {
     walk_.clear();
     walk_.push_back({kEmbedStop, 0, {}, {}});
     for (int l = 0; l < cfg_.L; ++l) {
+      const int w = remote_of_.empty() ? -1 : remote_of_[l];
+      if (w >= 0) {  // a TCP worker's run: coalesced while the worker stays the same
+        if (walk_.back().kind != kRemoteStop || walk_.back().remote != w)
+          walk_.push_back({kRemoteStop, 0, {}, {}, w});
+        walk_.back().layers.push_back(l);
+        continue;
+      }
       const int r = owner_.empty() ? 0 : owner_[l];
       if (walk_.back().kind != kRunStop || walk_.back().rank != r) walk_.push_back({kRunStop, r, {}, {}});
       walk_.back().layers.push_back(l);
@@ -1349,10 +1398,10 @@ class Llama {
   std::string walk_str() const {
     std::string s;
     for (const Stop& st : walk_)
-      if (st.kind == kRunStop) {
+      if (st.kind == kRunStop || st.kind == kRemoteStop) {
         if (!s.empty()) s += ",";
-        s += std::to_string(st.rank) + ":" + std::to_string(st.layers.front()) + "-" +
-             std::to_string(st.layers.back());
+        s += (st.kind == kRemoteStop ? "w" + std::to_string(st.remote) : std::to_string(st.rank)) +
+             ":" + std::to_string(st.layers.front()) + "-" + std::to_string(st.layers.back());
       }
     return s;
   }
@@ -1475,6 +1524,144 @@ class Llama {
     if (tp_ > 1 && lead) sync_tp_workers();
     if (lead) check_attn_error("rank " + std::to_string(rank()));
   }
+
+  // ---- TCP workers (master side; the reference's Client, client.rs:23-133)
+  void connect_remotes() {
+    for (auto& w : remotes_) {
+      std::string host;
+      int port = 0;
+      split_host_port(w.addr, &host, &port);
+      w.fd = tcp_connect(host, port, remote_timeout_);
+      tcp_set_timeout(w.fd, remote_timeout_);
+      Message hello;
+      hello.type = MsgType::Hello;
+      const std::string body = encode_body(hello);
+      send_frame(w.fd, reinterpret_cast<const uint8_t*>(body.data()), (uint32_t)body.size());
+      const std::string rep = recv_frame(w.fd);
+      const Message info = decode_body(reinterpret_cast<const uint8_t*>(rep.data()), rep.size());
+      if (info.type != MsgType::WorkerInfo)
+        throw Error("worker " + w.addr + " did not answer Hello with WorkerInfo");
+      trace(0, "worker " + w.addr + ": " + info.info.device + " " + info.info.dtype + " (" +
+                   info.info.os + "/" + info.info.arch + "), handshake " +
+                   std::to_string(info.info.latency_lo) + " ms");
+    }
+  }
+
+  static float wire_to_f32(uint16_t h, bool bf16) {
+    uint32_t bits;
+    if (bf16) {
+      bits = (uint32_t)h << 16;
+    } else {
+      const uint32_t sg = (uint32_t)(h & 0x8000) << 16, e = (h >> 10) & 0x1f, m = h & 0x3ff;
+      if (e == 0) {
+        if (m == 0) {
+          bits = sg;
+        } else {
+          int ee = -1;
+          uint32_t mm = m;
+          do { ++ee; mm <<= 1; } while (!(mm & 0x400));
+          bits = sg | ((uint32_t)(127 - 15 - ee) << 23) | ((mm & 0x3ff) << 13);
+        }
+      } else if (e == 31) {
+        bits = sg | 0x7f800000u | (m << 13);
+      } else {
+        bits = sg | ((e + 127 - 15) << 23) | (m << 13);
+      }
+    }
+    float f;
+    std::memcpy(&f, &bits, 4);
+    return f;
+  }
+
+  // one Batch round trip: host_rows_ [T, H] f32 at positions pos0.. through the worker's
+  // run of layers (one (model.layers.l, pos0, l) item per layer), replaced by the reply
+  void remote_call(const Stop& s, int pos0, int T) {
+    RemoteWorker& w = remotes_.at(s.remote);
+    const size_t n = (size_t)T * cfg_.H;
+    Message m;
+    m.type = MsgType::Batch;
+    m.x.dtype = "f32";
+    m.x.shape = {1, (uint64_t)T, (uint64_t)cfg_.H};
+    m.x.data = reinterpret_cast<const uint8_t*>(host_rows_.data());
+    m.x.nbytes = n * 4;
+    for (int l : s.layers)
+      m.batch.push_back({"model.layers." + std::to_string(l), (uint64_t)pos0, (uint64_t)l});
+    const std::string body = encode_body(m);
+    send_frame(w.fd, reinterpret_cast<const uint8_t*>(body.data()), (uint32_t)body.size());
+    const std::string rep = recv_frame(w.fd);
+    const Message r = decode_body(reinterpret_cast<const uint8_t*>(rep.data()), rep.size());
+    if (r.type == MsgType::Error) throw Error("worker " + w.addr + ": " + r.error);
+    if (r.type != MsgType::Tensor) throw Error("worker " + w.addr + ": unexpected reply");
+    uint64_t cnt = 1;
+    for (auto d : r.x.shape) cnt *= d;
+    if (cnt != n) throw Error("worker " + w.addr + ": reply of " + std::to_string(cnt) +
+                              " values, expected " + std::to_string(n));
+    if (r.x.dtype == "f32" && r.x.nbytes == n * 4) {
+      std::memcpy(host_rows_.data(), r.x.data, n * 4);
+    } else if ((r.x.dtype == "f16" || r.x.dtype == "bf16") && r.x.nbytes == n * 2) {
+      const bool bf = r.x.dtype == "bf16";
+      for (size_t i = 0; i < n; ++i) {
+        uint16_t h;
+        std::memcpy(&h, r.x.data + 2 * i, 2);
+        host_rows_[i] = wire_to_f32(h, bf);
+      }
+    } else {
+      throw Error("worker " + w.addr + ": unsupported reply tensor " + r.x.dtype);
+    }
+  }
+
+  // prefill rows [T, H] (device) through a remote run
+  void remote_rows(const Stop& s, int pos0, float* rows, int T) {
+    const size_t n = (size_t)T * cfg_.H;
+    host_rows_.resize(n);
+    hip_check(hipMemcpyAsync(host_rows_.data(), rows, n * 4, hipMemcpyDeviceToHost, st_), "D2H");
+    hip_check(hipStreamSynchronize(st_), "sync");
+    remote_call(s, pos0, T);
+    hip_check(hipMemcpyAsync(rows, host_rows_.data(), n * 4, hipMemcpyHostToDevice, st_), "H2D");
+    hip_check(hipStreamSynchronize(st_), "sync");
+  }
+
+  // the decode row through a remote run; its position rides in resid_'s header word
+  void remote_step(const Stop& s) {
+    const int H = cfg_.H;
+    host_rows_.resize((size_t)H + 1);
+    hip_check(hipMemcpyAsync(host_rows_.data(), resid_, sizeof(float) * (H + 1),
+                             hipMemcpyDeviceToHost, st_), "D2H");
+    hip_check(hipStreamSynchronize(st_), "sync");
+    int pos = 0;
+    std::memcpy(&pos, &host_rows_[H], 4);
+    remote_call(s, pos, 1);
+    hip_check(hipMemcpyAsync(resid_, host_rows_.data(), sizeof(float) * H, hipMemcpyHostToDevice,
+                             st_), "H2D");
+    hip_check(hipStreamSynchronize(st_), "sync");
+  }
+
+  // decode with TCP workers in the walk: every step eagerly (host round trips inside it),
+  // the token read back after each; per-token host wall time
+  int decode_eager(int n, const Mode& m, const int32_t* eos, int n_eos, cake_engine_token_cb cb,
+                   void* ctx, int32_t* out, int out_cap, std::vector<float>* ms_out) {
+    std::vector<float> ms;
+    int n_out = 0;
+    for (int i = 0; i < n; ++i) {
+      const auto t0 = std::chrono::steady_clock::now();
+      step_body(m);
+      int32_t tok = 0;
+      hip_check(hipMemcpyAsync(&tok, tok_, sizeof(tok), hipMemcpyDeviceToHost, st_), "tok");
+      hip_check(hipStreamSynchronize(st_), "sync");
+      ms.push_back((float)(std::chrono::duration<double>(std::chrono::steady_clock::now() - t0)
+                               .count() * 1e3));
+      if (n_out < out_cap) out[n_out++] = tok;
+      bool stop = cb && cb(ctx, tok) != 0;
+      for (int e = 0; e < n_eos && !stop; ++e)
+        if (eos[e] == tok) stop = true;
+      if (stop) break;
+    }
+    check_attn_error("rank 0");
+    if (ms_out) *ms_out = std::move(ms);
+    return n_out;
+  }
+
+  bool remote_mode() const { return !remotes_.empty(); }
 
   // ---- pipeline (one process per GPU, layer shards, device-side hops)
   static constexpr int kAnnounceChunk = 8;  // replays per worker announcement
@@ -2200,6 +2387,17 @@ CAKE_API void* cake_engine_open_pp(const char* model_dir, const CakeEngineOpts* 
   try {
     if (!model_dir || !opts || !pipe) throw cake::Error("null argument");
     return new Llama(model_dir, *opts, pipe);
+  } catch (const std::exception& e) {
+    cake::put_err(err, errlen, e.what());
+    return nullptr;
+  }
+}
+
+CAKE_API void* cake_engine_open_remote(const char* model_dir, const CakeEngineOpts* opts,
+                                       const CakeRemoteOpts* remote, char* err, int32_t errlen) {
+  try {
+    if (!model_dir || !opts || !remote) throw cake::Error("null argument");
+    return new Llama(model_dir, *opts, nullptr, nullptr, nullptr, remote);
   } catch (const std::exception& e) {
     cake::put_err(err, errlen, e.what());
     return nullptr;

@@ -57,6 +57,20 @@ struct CakeTPOpts {
   double connect_timeout_s;
 };
 
+// Master over TCP workers (the reference's Client, cake-core/src/cake/client.rs:23-133):
+// layer l runs on worker worker_of[l] ("host:port", a topology node's host) or locally
+// (-1).  One connection per worker (Hello -> WorkerInfo at open); every contiguous run of
+// one worker's layers is one Batch round trip per token (llama.rs:95-114), the hidden
+// rows travel as f32 tensors.  The decode step runs eagerly (a host round trip sits
+// inside it); local runs, the head and the token choice are the same kernels.
+struct CakeRemoteOpts {
+  const int32_t* worker_of;     // [n_layers == num_hidden_layers]
+  int32_t n_layers;
+  const char* const* workers;   // [n_workers] "host:port"
+  int32_t n_workers;
+  double timeout_s;             // connect / reply wait bound
+};
+
 struct CakeEngineSampling {
   float temperature;        // <= 0: greedy
   int32_t top_k;            // 0: off
@@ -84,6 +98,9 @@ void* cake_engine_open_pp(const char* model_dir, const struct CakeEngineOpts* op
 // Tensor-parallel rank (see CakeTPOpts).
 void* cake_engine_open_tp(const char* model_dir, const struct CakeEngineOpts* opts,
                           const struct CakeTPOpts* tp, char* err, int32_t errlen);
+// Master with TCP workers (see CakeRemoteOpts): embedding, head and the local layers here.
+void* cake_engine_open_remote(const char* model_dir, const struct CakeEngineOpts* opts,
+                              const struct CakeRemoteOpts* remote, char* err, int32_t errlen);
 // Workers (rank > 0): serve rank 0's control messages until it closes; 0 or an error.
 int32_t cake_engine_serve(void* engine, char* err, int32_t errlen);
 // TCP worker (topology node): only `layers` (global indices), no embedding / head.

@@ -27,6 +27,7 @@
 #include "../engine/llama_engine.h"
 #include "embed.h"
 #include "json.h"
+#include "native_worker.h"
 #include "server.h"
 #include "topology.h"
 
@@ -155,6 +156,7 @@ struct EngineApi {
   void* (*open)(const char*, const CakeEngineOpts*, char*, int32_t);
   void* (*open_pp)(const char*, const CakeEngineOpts*, const CakePipeOpts*, char*, int32_t);
   void* (*open_tp)(const char*, const CakeEngineOpts*, const CakeTPOpts*, char*, int32_t);
+  void* (*open_remote)(const char*, const CakeEngineOpts*, const CakeRemoteOpts*, char*, int32_t);
   int32_t (*serve)(void*, char*, int32_t);
   int32_t (*generate)(void*, const int32_t*, int32_t, int32_t, const CakeEngineSampling*,
                       const int32_t*, int32_t, cake_engine_token_cb, void*, int32_t*, int32_t,
@@ -173,7 +175,8 @@ bool native_text_eligible(cake::PyArgs& o, bool text, bool worker, bool has_topo
   if (is("transport", "rccl"))  // one process per GPU (torchrun env): layer-sharded pipeline
     return common && std::getenv("WORLD_SIZE") &&  // (pp, device hops) or tensor parallel
            ((is("parallel", "pp") && is("hop", "ipc")) || is("parallel", "tp"));
-  return common && !worker && !has_topology && is("transport", "tcp");
+  (void)has_topology;  // topology workers: the engine's TCP client (native master)
+  return common && !worker && is("transport", "tcp");
 }
 
 int env_int(const char* k, int def) {
@@ -253,7 +256,9 @@ int run_native_text(cake::PyArgs& o, const cake::Topology* topo) {
   api.open_pp = reinterpret_cast<decltype(api.open_pp)>(dlsym(h, "cake_engine_open_pp"));
   api.serve = reinterpret_cast<decltype(api.serve)>(dlsym(h, "cake_engine_serve"));
   api.open_tp = reinterpret_cast<decltype(api.open_tp)>(dlsym(h, "cake_engine_open_tp"));
-  if (!api.open || !api.generate || !api.close || !api.open_pp || !api.serve || !api.open_tp) {
+  api.open_remote = reinterpret_cast<decltype(api.open_remote)>(dlsym(h, "cake_engine_open_remote"));
+  if (!api.open || !api.generate || !api.close || !api.open_pp || !api.serve || !api.open_tp ||
+      !api.open_remote) {
     std::fprintf(stderr, "cake-cli: engine symbols missing in %s\n", lib.c_str());
     return 1;
   }
@@ -325,17 +330,40 @@ int run_native_text(cake::PyArgs& o, const cake::Topology* topo) {
   CakePipeOpts po{0, world, ctl.c_str(), o["hop_dtype"].value == "bf16" ? 1 : 0, 60.0, 600.0,
                   owners.empty() ? nullptr : owners.data(), (int32_t)owners.size()};
   CakeTPOpts to{0, world, ctl.c_str(), 60.0, 600.0};
+  // --transport tcp with topology workers: the master's TCP client (llama.rs:205-220:
+  // each layer a node names runs on that node; contiguous runs go as one Batch)
+  std::vector<int32_t> worker_of;
+  std::vector<const char*> hosts;
+  if (!pipe && topo && !topo->nodes.empty()) {
+    int L = 0;
+    try {
+      L = num_hidden_layers(ctx.model);
+    } catch (const std::exception& e) {
+      std::fprintf(stderr, "cake-cli: %s\n", e.what());
+      return 1;
+    }
+    worker_of.assign((size_t)L, -1);
+    for (int l = 0; l < L; ++l) {
+      const cake::TopoNode* nd = topo->node_for_layer("model.layers." + std::to_string(l));
+      if (nd) worker_of[(size_t)l] = (int32_t)(nd - topo->nodes.data());
+    }
+    for (const auto& nd : topo->nodes) hosts.push_back(nd.host.c_str());
+  }
+  CakeRemoteOpts ro{worker_of.data(), (int32_t)worker_of.size(), hosts.data(),
+                    (int32_t)hosts.size(), 120.0};
   void* eng = world > 1 ? (tp ? api.open_tp(ctx.model.c_str(), &eo, &to, err, sizeof(err))
                               : api.open_pp(ctx.model.c_str(), &eo, &po, err, sizeof(err)))
-                        : api.open(ctx.model.c_str(), &eo, err, sizeof(err));
+              : !worker_of.empty() ? api.open_remote(ctx.model.c_str(), &eo, &ro, err, sizeof(err))
+                                   : api.open(ctx.model.c_str(), &eo, err, sizeof(err));
   if (!eng) {
     std::fprintf(stderr, "cake-cli: native engine: %s\n", err);
     return 1;
   }
   const double load_s =
       std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-  std::fprintf(stderr, "[cake-cli] native engine: model loaded in %.1f s (%zu prompt tokens)\n",
-               load_s, ids.size());
+  std::fprintf(stderr, "[cake-cli] native engine: model loaded in %.1f s (%zu prompt tokens)%s\n",
+               load_s, ids.size(),
+               worker_of.empty() ? "" : ", native master over TCP workers");
   CakeEngineSampling smp{};
   smp.temperature = (float)num("temperature", 1.0);
   smp.top_k = (int32_t)num("top_k", 0);
@@ -366,35 +394,8 @@ int run_native_text(cake::PyArgs& o, const cake::Topology* topo) {
 }
 
 // ---------------------------------------------------------------------------
-// Native TCP worker (--mode worker, text model): the native WorkerServer's compute is
-// the engine (only this node's layers, one KV cache per master connection), no
-// interpreter at all.  Reference: cake-core/src/cake/worker.rs:150-303.
+// Native TCP worker (--mode worker, text model): runtime/native_worker.cpp.
 // ---------------------------------------------------------------------------
-float half_to_f32(uint16_t h, bool bf16) {
-  uint32_t bits;
-  if (bf16) {
-    bits = (uint32_t)h << 16;
-  } else {
-    const uint32_t s = (uint32_t)(h & 0x8000) << 16, e = (h >> 10) & 0x1f, m = h & 0x3ff;
-    if (e == 0) {
-      if (m == 0) bits = s;
-      else {  // subnormal
-        int ee = -1;
-        uint32_t mm = m;
-        do { ++ee; mm <<= 1; } while (!(mm & 0x400));
-        bits = s | ((uint32_t)(127 - 15 - ee) << 23) | ((mm & 0x3ff) << 13);
-      }
-    } else if (e == 31) {
-      bits = s | 0x7f800000u | (m << 13);
-    } else {
-      bits = s | ((e + 127 - 15) << 23) | (m << 13);
-    }
-  }
-  float f;
-  std::memcpy(&f, &bits, 4);
-  return f;
-}
-
 bool native_worker_eligible(cake::PyArgs& o, bool text, bool worker) {
   const char* env = std::getenv("CAKE_NATIVE");
   if (env && std::string(env) == "0") return false;
@@ -404,112 +405,13 @@ bool native_worker_eligible(cake::PyArgs& o, bool text, bool worker) {
 }
 
 int run_native_worker(cake::PyArgs& o, const cake::TopoNode& node) {
-  const std::string lib = cake::package_root() + "/cake_amd/lib/libcake_engine.so";
-  void* h = dlopen(lib.c_str(), RTLD_NOW | RTLD_LOCAL);
-  if (!h) {
-    std::fprintf(stderr, "cake-cli: %s\n", dlerror());
-    return 1;
-  }
-  using OpenLayers = void* (*)(const char*, const CakeEngineOpts*, const int32_t*, int32_t, char*,
-                               int32_t);
-  using Forward = int32_t (*)(void*, uint64_t, const int32_t*, int32_t, int32_t, float*, int32_t,
-                              char*, int32_t);
-  using Drop = void (*)(void*, uint64_t);
-  auto open_layers = reinterpret_cast<OpenLayers>(dlsym(h, "cake_engine_open_layers"));
-  auto forward = reinterpret_cast<Forward>(dlsym(h, "cake_engine_forward"));
-  auto drop = reinterpret_cast<Drop>(dlsym(h, "cake_engine_drop_session"));
-  if (!open_layers || !forward || !drop) {
-    std::fprintf(stderr, "cake-cli: engine symbols missing in %s\n", lib.c_str());
-    return 1;
-  }
-  std::vector<int32_t> layers;
-  const std::string pre = "model.layers.";
-  for (const auto& l : node.layers)
-    if (l.rfind(pre, 0) == 0) layers.push_back((int32_t)std::atoi(l.c_str() + pre.size()));
-  if (layers.empty()) {
-    std::fprintf(stderr, "cake-cli: worker %s owns no model.layers.*\n", node.name.c_str());
-    return 2;
-  }
-  const auto num = [&](const char* k, double def) {
-    return o[k].kind == PyArg::kNone ? def : std::strtod(o[k].value.c_str(), nullptr);
-  };
-  const bool bf16 = o["dtype"].value == "bf16";
-  CakeEngineOpts eo{(int32_t)num("max_seq_len", 4096), bf16 ? 0 : 1, (int32_t)num("device", 0), 1};
-  char err[1024] = {0};
-  void* eng = open_layers(o["model"].value.c_str(), &eo, layers.data(), (int32_t)layers.size(),
-                          err, sizeof(err));
-  if (!eng) {
-    std::fprintf(stderr, "cake-cli: native worker: %s\n", err);
-    return 1;
-  }
-  cake::WorkerInfo info;
-  info.version = "0.1.0";
-  info.dtype = bf16 ? "bf16" : "f16";
-  info.os = "linux";
-  info.arch = "x86_64";
-  info.device = "rocm";
-  info.device_idx = (uint64_t)eo.device;
-  std::string host;
-  int port = 0;
-  {
-    const std::string a = o["address"].value;
-    const auto c = a.rfind(':');
-    host = c == std::string::npos ? a : a.substr(0, c);
-    port = c == std::string::npos ? 10128 : std::atoi(a.c_str() + c + 1);
-    if (host.empty()) host = "0.0.0.0";
-  }
-  cake::WorkerServer server(host, port, info, node.name);
-  std::mutex mu;  // one compute at a time (the GPU stream is shared)
-  server.set_compute([&](uint64_t session, const std::vector<cake::BatchItem>& ops,
-                         const cake::RawTensor& x) {
-    cake::OpResult r;
-    try {
-      const uint64_t H = x.shape.empty() ? 0 : x.shape.back();
-      uint64_t n = 1;
-      for (auto d : x.shape) n *= d;
-      std::vector<float> buf(n);
-      if (x.dtype == "f32" && x.nbytes == n * 4) {
-        std::memcpy(buf.data(), x.data, n * 4);
-      } else if ((x.dtype == "f16" || x.dtype == "bf16") && x.nbytes == n * 2) {
-        const uint16_t* p = reinterpret_cast<const uint16_t*>(x.data);
-        for (uint64_t i = 0; i < n; ++i) buf[i] = half_to_f32(p[i], x.dtype == "bf16");
-      } else {
-        throw std::runtime_error("unsupported tensor " + x.dtype);
-      }
-      const int T = H ? (int)(n / H) : 0;
-      std::lock_guard<std::mutex> g(mu);
-      size_t i = 0;
-      while (i < ops.size()) {  // consecutive ops at one position -> one engine call
-        const uint64_t pos = ops[i].index_pos;
-        std::vector<int32_t> ls;
-        for (; i < ops.size() && ops[i].index_pos == pos; ++i) {
-          const std::string& nm = ops[i].layer_name;
-          if (nm.rfind(pre, 0) != 0) throw std::runtime_error("not a layer: " + nm);
-          ls.push_back((int32_t)std::atoi(nm.c_str() + pre.size()));
-        }
-        char e2[512] = {0};
-        if (forward(eng, session, ls.data(), (int32_t)ls.size(), (int32_t)pos, buf.data(), T, e2,
-                    sizeof(e2)))
-          throw std::runtime_error(e2);
-      }
-      r.dtype = "f32";
-      r.shape = x.shape;
-      r.data.assign(reinterpret_cast<const char*>(buf.data()), n * 4);
-    } catch (const std::exception& e) {
-      r.error = e.what();
-    }
-    return r;
-  });
-  server.set_drop([&](uint64_t session) {
-    std::lock_guard<std::mutex> g(mu);
-    drop(eng, session);
-  });
-  server.set_reset([](uint64_t) {});  // positions are rewritten; nothing to clear
-  server.set_log([](const std::string& m) { std::fprintf(stderr, "[cake-cli] %s\n", m.c_str()); });
-  std::fprintf(stderr, "[cake-cli] native worker %s: %zu layers on device %d, listening on %s:%d\n",
-               node.name.c_str(), layers.size(), eo.device, host.c_str(), server.port());
-  server.serve();
-  return 0;
+  cake::NativeWorkerOpts w;
+  w.model_dir = o["model"].value;
+  w.address = o["address"].value;
+  w.device = o["device"].kind == PyArg::kNone ? 0 : std::atoi(o["device"].value.c_str());
+  w.max_seq = o["max_seq_len"].kind == PyArg::kNone ? 4096 : std::atoi(o["max_seq_len"].value.c_str());
+  w.bf16 = o["dtype"].value == "bf16";
+  return cake::run_native_worker(w, node);
 }
 
 }  // namespace

@@ -39,6 +39,12 @@ class TPOpts(C.Structure):
                 ("timeout_s", C.c_double), ("connect_timeout_s", C.c_double)]
 
 
+class RemoteOpts(C.Structure):
+    _fields_ = [("worker_of", C.POINTER(C.c_int32)), ("n_layers", C.c_int32),
+                ("workers", C.POINTER(C.c_char_p)), ("n_workers", C.c_int32),
+                ("timeout_s", C.c_double)]
+
+
 class EngineSampling(C.Structure):
     _fields_ = [("temperature", C.c_float), ("top_k", C.c_int32), ("top_p", C.c_float),
                 ("seed", C.c_uint64), ("repeat_penalty", C.c_float),
@@ -69,6 +75,9 @@ def lib() -> C.CDLL:
         L.cake_engine_open_tp.argtypes = [C.c_char_p, C.POINTER(EngineOpts), C.POINTER(TPOpts),
                                           C.c_char_p, I]
         L.cake_engine_open_tp.restype = P
+        L.cake_engine_open_remote.argtypes = [C.c_char_p, C.POINTER(EngineOpts),
+                                              C.POINTER(RemoteOpts), C.c_char_p, I]
+        L.cake_engine_open_remote.restype = P
         L.cake_engine_serve.argtypes = [P, C.c_char_p, I]
         L.cake_engine_serve.restype = I
         L.cake_engine_rank_info.argtypes = [P, C.POINTER(C.c_int32)]
@@ -119,13 +128,17 @@ class NativeLlama:
                  master_addr: str = "127.0.0.1:29517", hop_bf16: bool = False,
                  hop_timeout_s: float = 30.0, connect_timeout_s: float = 600.0,
                  tp: bool = False, owners: list[int] | None = None, random_init: bool = False,
-                 seed: int = 0):
+                 seed: int = 0, worker_of: list[int] | None = None,
+                 workers: list[str] | None = None, remote_timeout_s: float = 120.0):
         """world > 1: one rank of a layer-sharded pipeline, or with tp=True of a tensor-
         parallel group (rank 0 generates; the others call :meth:`serve`).  Every rank of
         one group must be constructed concurrently.  ``owners`` (pipeline): the rank of
         every layer (:func:`owners_from_topology`); None = contiguous shards.
         ``random_init``: only ``config.json`` is read; the weights are seeded normal
-        draws on the device (benchmarks of a named architecture, no checkpoint)."""
+        draws on the device (benchmarks of a named architecture, no checkpoint).
+        ``workers`` / ``worker_of`` (single process): TCP workers ("host:port") and the
+        worker index of every layer (-1 = local) — the master's Client
+        (cake-core/src/cake/client.rs:23-133), contiguous runs batched per round trip."""
         if dtype not in ("bf16", "f16"):
             raise ValueError("native engine dtype: bf16 or f16")
         opts = EngineOpts(int(max_seq), 0 if dtype == "bf16" else 1, int(device),
@@ -151,6 +164,15 @@ class NativeLlama:
                             len(owners) if owners is not None else 0)
             self._h = lib().cake_engine_open_pp(str(model_dir).encode(), C.byref(opts),
                                                 C.byref(pipe), err, len(err))
+        elif workers:
+            wo = (C.c_int32 * len(worker_of))(*[int(x) for x in worker_of])
+            hs = (C.c_char_p * len(workers))(*[w.encode() for w in workers])
+            self._remote = (wo, hs)  # kept alive for the call
+            ro = RemoteOpts(C.cast(wo, C.POINTER(C.c_int32)), len(worker_of),
+                            C.cast(hs, C.POINTER(C.c_char_p)), len(workers),
+                            float(remote_timeout_s))
+            self._h = lib().cake_engine_open_remote(str(model_dir).encode(), C.byref(opts),
+                                                    C.byref(ro), err, len(err))
         else:
             self._h = lib().cake_engine_open(str(model_dir).encode(), C.byref(opts), err, len(err))
         if not self._h:
@@ -267,6 +289,18 @@ def owners_from_topology(topology, num_layers: int, world: int) -> list[int]:
     (cake-core/src/models/llama3/llama.rs:205-220, topology.rs:81-92)."""
     from .parallel.rccl_roles import owners_from_topology as f
     return f(topology, num_layers, world)
+
+
+def remote_placement(topology, num_layers: int) -> tuple[list[int], list[str]]:
+    """(worker_of, workers) of a topology for the master's TCP client: node i serves the
+    layers it names (exact name lookup, topology.rs:81-92), the rest stay local."""
+    nodes = list(topology.nodes)
+    index = {id(n): i for i, n in enumerate(nodes)}
+    worker_of = []
+    for li in range(num_layers):
+        node = topology.get_node_for_layer(f"model.layers.{li}")
+        worker_of.append(-1 if node is None else index[id(node)])
+    return worker_of, [n.host for n in nodes]
 
 
 def write_config(path: str | Path, cfg) -> Path:

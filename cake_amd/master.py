@@ -132,13 +132,17 @@ class Master:
 
 
 def _load_text(ctx):
-    """The native engine when it can serve this context (all-local on a GPU), else the
-    Python generator (CPU, f32, --no-graph, TCP workers in the placement, CAKE_NATIVE=0)."""
+    """The native engine when it can serve this context (a GPU, 16-bit weights, graphs;
+    topology workers through its TCP client), else the Python generator (CPU, f32,
+    --no-graph, CAKE_NATIVE=0)."""
     from .models.llama3.native_generator import NativeLLM, native_eligible
-    topo = getattr(ctx, "topology", None)
-    remote = bool(topo is not None and getattr(topo, "nodes", None))
-    if native_eligible(ctx, remote=remote):
-        log.info("text model on the native engine (libcake_engine.so)")
+    if native_eligible(ctx):
+        topo = getattr(ctx, "topology", None)
+        if topo is not None and getattr(topo, "nodes", None):
+            log.info("text model on the native engine, TCP workers %s",
+                     [f"{n.name}@{n.host}" for n in topo.nodes])
+        else:
+            log.info("text model on the native engine (libcake_engine.so)")
         return NativeLLM.load(ctx)
     from .models.llama3.generator import LLamaGenerator
     return LLamaGenerator.load(ctx)

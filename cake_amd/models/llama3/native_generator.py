@@ -43,8 +43,17 @@ class NativeLLM(TextGenerator):
         from .generator import load_tokenizer
         from ...engine import NativeLlama
         if engine is None:
+            kw = {}
+            topo = getattr(ctx, "topology", None)
+            if topo is not None and getattr(topo, "nodes", None):
+                from ...engine import remote_placement
+                from .config import LlamaConfig
+                L = LlamaConfig.from_path(ctx.model_path).num_hidden_layers
+                worker_of, workers = remote_placement(topo, L)
+                if any(w >= 0 for w in worker_of):
+                    kw = dict(worker_of=worker_of, workers=workers)
             engine = NativeLlama(ctx.model_path, max_seq=ctx.max_seq_len,
-                                 dtype=_dtype_name(ctx.dtype), device=ctx.device.index or 0)
+                                 dtype=_dtype_name(ctx.dtype), device=ctx.device.index or 0, **kw)
         tok, eos = load_tokenizer(ctx.model_path, engine.eos_ids)
         return cls(engine, tok, eos, ctx.sampling)
 
@@ -143,8 +152,8 @@ def _dtype_name(dtype) -> str:
 
 
 def native_eligible(ctx, remote: bool = False) -> bool:
-    """The native engine serves this context: a GPU, a 16-bit dtype, graphs on, no TCP
-    workers in the master's placement, and CAKE_NATIVE != 0."""
+    """The native engine serves this context: a GPU, a 16-bit dtype, graphs on, and
+    CAKE_NATIVE != 0 (``remote`` = a placement it cannot serve)."""
     import os
 
     import torch

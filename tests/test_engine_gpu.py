@@ -260,6 +260,8 @@ def test_cake_cli_native_tcp_worker(cuda, ckpt, tmp_path):
                               capture_output=True, text=True, timeout=300, env=env, cwd=root)
         assert dist.returncode == 0, dist.stderr[-3000:]
         assert local.stdout.strip() and dist.stdout == local.stdout
+        # the master ran natively too (the engine's TCP client, no interpreter compute)
+        assert "native master over TCP workers" in dist.stderr, dist.stderr[-3000:]
     finally:
         w.kill()
         err = w.communicate()[1]
@@ -520,3 +522,111 @@ def test_native_continue_equals_one_generation(cuda, ckpt):
     assert r2.generate(PROMPT, 12, repeat_penalty=1.0).tokens == t1
     r2.close()
     eng.close()
+
+
+def _wait_listen(proc, port, what, t_max=180):
+    import socket
+    import time
+    t0 = time.time()
+    while True:
+        if proc.poll() is not None:
+            raise AssertionError(f"{what} exited: {proc.stderr.read()[-3000:]}")
+        try:
+            socket.create_connection(("127.0.0.1", port), timeout=0.5).close()
+            return
+        except OSError:
+            assert time.time() - t0 < t_max, f"{what} did not listen"
+            time.sleep(0.3)
+
+
+def test_native_master_two_tcp_workers_interleaved(cuda, ckpt, tmp_path):
+    """A topology with two native TCP workers, one of them visited twice per token
+    (w1: layers 0 and 2, w2: layer 1): the native master's walk is w0 -> w1 -> w0, each a
+    Batch round trip; the text equals the all-local engine's.  w2 is started through the
+    embeddable C ABI (cake_start_worker in libcake_runtime.so), which serves text natively."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cli = os.path.join(root, "cake_amd", "lib", "cake-cli")
+    p1, p2 = _port(), _port()
+    topo = tmp_path / "topology.yml"
+    topo.write_text(f"w1:\n  host: '127.0.0.1:{p1}'\n  layers:\n    - 'model.layers.0'\n"
+                    f"    - 'model.layers.2'\n"
+                    f"w2:\n  host: '127.0.0.1:{p2}'\n  layers:\n    - 'model.layers.1'\n")
+    gen = ["--temperature", "0", "-n", "14", "--prompt", "hello there", "--max-seq-len", "256"]
+    env = dict(os.environ, CAKE_LOG="warning")
+    local = subprocess.run([cli, "--model", str(ckpt), "--topology", str(tmp_path / "none.yml"),
+                            *gen], capture_output=True, text=True, timeout=300, env=env, cwd=root)
+    assert local.returncode == 0, local.stderr[-3000:]
+    w1 = subprocess.Popen([cli, "--mode", "worker", "--name", "w1", "--model", str(ckpt),
+                           "--topology", str(topo), "--address", f"127.0.0.1:{p1}",
+                           "--max-seq-len", "256"], cwd=root, env=env,
+                          stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+    capi = ("import ctypes, sys\n"
+            "L = ctypes.CDLL(%r)\n"
+            "L.cake_start_worker.argtypes = [ctypes.c_char_p] * 5\n"
+            "sys.exit(L.cake_start_worker(b'w2', %r, %r, b'text', b'127.0.0.1:%d'))\n") % (
+        os.path.join(root, "cake_amd", "lib", "libcake_runtime.so"), str(ckpt).encode(),
+        str(topo).encode(), p2)
+    w2 = subprocess.Popen([sys.executable, "-c", capi], cwd=root, env=env,
+                          stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+    try:
+        _wait_listen(w1, p1, "worker w1")
+        _wait_listen(w2, p2, "worker w2 (cake_start_worker)")
+        dist = subprocess.run([cli, "--model", str(ckpt), "--topology", str(topo), *gen],
+                              capture_output=True, text=True, timeout=300,
+                              env=dict(env, CAKE_ENGINE_TRACE="1"), cwd=root)
+        assert dist.returncode == 0, dist.stderr[-3000:]
+        assert "native master over TCP workers" in dist.stderr, dist.stderr[-3000:]
+        assert local.stdout.strip() and dist.stdout == local.stdout, (dist.stdout, local.stdout)
+    finally:
+        for w in (w1, w2):
+            w.kill()
+        e1, e2 = w1.communicate()[1], w2.communicate()[1]
+    assert "native worker w1" in e1
+    assert "[cake_start_worker] native worker w2" in e2, e2[-2000:]
+
+
+def test_native_api_serving_over_tcp_workers(cuda, ckpt, tmp_path):
+    """--api on the native engine with a TCP worker in the topology: the REST answer
+    equals the all-local native server's (greedy), and the master's text path is the
+    engine (NativeLLM over cake_engine_open_remote)."""
+    import os
+    import subprocess
+    from fastapi.testclient import TestClient
+    from cake_amd.api.server import create_app
+    from cake_amd.cli import build_parser
+    from cake_amd.context import Context
+    from cake_amd.master import Master
+    from cake_amd.models.llama3.native_generator import NativeLLM
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cli = os.path.join(root, "cake_amd", "lib", "cake-cli")
+    port = _port()
+    topo = tmp_path / "topology.yml"
+    topo.write_text(f"w1:\n  host: '127.0.0.1:{port}'\n  layers:\n    - 'model.layers.1-2'\n")
+    (tmp_path / "empty.yml").write_text("{}\n")
+    common = ["--model", str(ckpt), "--dtype", "bf16", "--temperature", "0", "--max-seq-len",
+              "256"]
+    req = {"messages": [{"role": "user", "content": "hello there"}], "max_tokens": 16}
+    m0 = Master(Context.from_args(build_parser().parse_args(
+        common + ["--topology", str(tmp_path / "empty.yml")])))
+    assert isinstance(m0.llm, NativeLLM)
+    want = TestClient(create_app(m0)).post("/api/v1/chat/completions", json=req).json()
+    m0.llm.eng.close()
+    w = subprocess.Popen([cli, "--mode", "worker", "--name", "w1", "--model", str(ckpt),
+                          "--topology", str(topo), "--address", f"127.0.0.1:{port}", "--dtype",
+                          "bf16", "--max-seq-len", "256"], cwd=root,
+                         env=dict(os.environ, CAKE_LOG="warning"), stdout=subprocess.DEVNULL,
+                         stderr=subprocess.PIPE, text=True)
+    try:
+        _wait_listen(w, port, "worker")
+        m1 = Master(Context.from_args(build_parser().parse_args(common + ["--topology", str(topo)])))
+        assert isinstance(m1.llm, NativeLLM) and m1.llm.eng.walk() == "0:0-0,w0:1-2"
+        got = TestClient(create_app(m1)).post("/api/v1/chat/completions", json=req).json()
+        m1.llm.eng.close()
+    finally:
+        w.kill()
+        w.communicate()
+    assert want["choices"][0]["message"]["content"]
+    assert got["choices"][0]["message"]["content"] == want["choices"][0]["message"]["content"]
