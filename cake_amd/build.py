@@ -97,13 +97,23 @@ def _py_ext_flags() -> tuple[list[str], str]:
 
 PY_EXT = LIB / "_cake_runtime"  # + EXT_SUFFIX
 
+EXPERIMENTAL = os.environ.get("CAKE_BUILD_EXPERIMENTAL", "0") != "0"
+
+
 def build_kernels(force: bool = False, jobs: int = 8) -> Path:
-    # HIP kernels + the native graph-replay decode driver (host code on the HIP runtime)
+    # HIP kernels + the native graph-replay decode driver (host code on the HIP runtime).
+    # csrc/experimental (the persistent decode engine, measured slower than the launch
+    # path: profiles/r4_mk_summary.md) only with CAKE_BUILD_EXPERIMENTAL=1.
     srcs = sorted((CSRC / "kernels").glob("*.hip")) + sorted((CSRC / "driver").glob("*.cpp"))
+    if EXPERIMENTAL:
+        srcs += sorted((CSRC / "experimental").glob("*.hip"))
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         objs = list(ex.map(lambda s: _compile_hip(s, force), srcs))
     LIB.mkdir(parents=True, exist_ok=True)
-    if force or any(_newer(o, [], KERNEL_LIB) for o in objs):
+    stale = [o for o in (BUILD / "kernels").glob("*.o") if o not in objs]
+    for o in stale:  # an object of a source no longer built (experimental off) must go
+        o.unlink()
+    if force or stale or any(_newer(o, [], KERNEL_LIB) for o in objs):
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs),
               "-o", str(KERNEL_LIB)])
     return KERNEL_LIB

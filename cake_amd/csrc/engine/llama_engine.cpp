@@ -74,6 +74,12 @@ int cake_attn_decode(int dt, const float* q, const void* kc, const void* vc, con
                      int S, int nh, int nkv, int hd, float scale, float* part,
                      unsigned int* tickets, void* out, hipStream_t st);
 int cake_attn_set_split_cap(int cap);
+int cake_attn_oproj_supported(int nh, int nkv, int hd, int H);
+long long cake_attn_oproj_ws_floats(int nkv, int H);
+long long cake_attn_oproj_ticket_words(int nkv, int H);
+int cake_attn_oproj(int dt, const float* q, const void* kc, const void* vc, const int* pos, int S,
+                    int nh, int nkv, int hd, float scale, const void* wo, int ldw, int H,
+                    float* out, int accumulate, float* ws, unsigned int* tickets, hipStream_t st);
 int cake_attn_splits(int Tk);
 int cake_attn_max_split(int S);
 int cake_gemv_x16(int dt, const void* x, const void* w, int K, int N, float* out, int accumulate,
@@ -586,7 +592,8 @@ class Llama {
     const auto t0 = std::chrono::steady_clock::now();
     std::vector<float> ms;
     const int n_out = remote_mode()
-                          ? decode_eager(max_new, last_mode_, eos, n_eos, cb, ctx, out, out_cap, &ms)
+                          ? decode_eager(L - 1, max_new, last_mode_, eos, n_eos, cb, ctx, out,
+                                         out_cap, &ms)
                           : decode_tokens(L, max_new, eos, n_eos, cb, ctx, out, out_cap, true, &ms);
     const auto t1 = std::chrono::steady_clock::now();
     if (stats) {
@@ -729,7 +736,7 @@ class Llama {
     if (remote_mode()) {  // host round trips inside the step: eager
       have_graphs_ = true;  // continue() may follow
       if (!stop && max_new > 1)
-        n_out += decode_eager(max_new - 1, mode, eos, n_eos, cb, ctx, out + n_out,
+        n_out += decode_eager(T, max_new - 1, mode, eos, n_eos, cb, ctx, out + n_out,
                               out_cap - n_out, &ms);
     } else {
       // graphs exist after every generation (continue() replays them), even a 1-token one
@@ -783,6 +790,11 @@ class Llama {
 
   int dt_, dev_, init_ = 0;
   bool forced_ = false;  // teacher-forcing steps: the head writes full logits
+  // fused decode attention + o_proj (attn_oproj.hip) for one-split live lengths: the
+  // short-context graph bucket and eager steps at such a position
+  bool ao_ok_ = false, short_step_ = false;
+  float* ao_ws_ = nullptr;
+  unsigned int* ao_tickets_ = nullptr;
   uint64_t seed_ = 0;
   int rank_ = 0, world_ = 1, lo_ = 0, hi_ = 0;
   bool head_ = true, hop_bf16_ = false;
@@ -1080,6 +1092,15 @@ class Llama {
     hip_check(hipMemset(zeros_, 0, sizeof(int32_t) * 64), "memset");
     hip_check(hipMemset(hist_, 0, sizeof(int) * S_), "memset");
     hip_check(hipMemset(resid_, 0, sizeof(float) * (c.H + 4)), "memset");
+    ao_ok_ = cake_attn_oproj_supported(c.nh, c.nkv, c.hd, c.H) != 0;
+    if (const char* e = std::getenv("CAKE_ATTN_OPROJ"))
+      if (std::string(e) == "0") ao_ok_ = false;
+    if (ao_ok_) {
+      ao_ws_ = dalloc<float>((size_t)cake_attn_oproj_ws_floats(c.nkv, c.H));
+      const size_t tw = (size_t)cake_attn_oproj_ticket_words(c.nkv, c.H);
+      ao_tickets_ = dalloc<unsigned int>(tw);
+      hip_check(hipMemset(ao_tickets_, 0, sizeof(unsigned int) * tw), "memset");
+    }
     const size_t nseq = 2 * edges_.size() + 2;  // per edge: send, receive sequence
     seq_ = dalloc<unsigned int>(nseq);
     hop_err_ = dalloc<int>(4);
@@ -1150,7 +1171,14 @@ class Llama {
     if (T == 1) {
       hip_check(hipMemcpyAsync(resid_, h, sizeof(float) * c.H, hipMemcpyHostToDevice, st_), "H2D");
       hip_check(hipMemcpyAsync(pos_, &pos0, sizeof(int), hipMemcpyHostToDevice, st_), "H2D");
-      step_layers(&sel);
+      short_step_ = short_at(pos0);
+      try {
+        step_layers(&sel);
+      } catch (...) {
+        short_step_ = false;
+        throw;
+      }
+      short_step_ = false;
       hip_check(hipMemcpyAsync(h, resid_, sizeof(float) * c.H, hipMemcpyDeviceToHost, st_), "D2H");
     } else {
       const size_t bytes = sizeof(float) * (size_t)T * c.H;
@@ -1165,6 +1193,10 @@ class Llama {
 
  private:
   float scale() const { return 1.0f / std::sqrt((float)cfg_.hd); }
+
+  // an eager step at device position `pos` takes the fused attention + o_proj launch
+  // exactly when a one-step graph replay there would (bucket of length pos + 2)
+  bool short_at(int pos) const { return ao_ok_ && cake_attn_splits(pos + 2) == 1; }
 
   // ---- prefill
   void grow_prefill(int T) {
@@ -1420,13 +1452,20 @@ class Llama {
       k_check(cake_qkv_rope(dt_, resid_, w.ln1, (float)c.eps, wqkv, wqkv + (size_t)nq * c.H,
                             wqkv + (size_t)(nq + nk) * c.H, c.H, c.nh, c.nkv, c.hd, inv_freq_,
                             pos_, q_, kc(l), vc(l), S_, st_), "qkv_rope");
-      k_check(cake_attn_decode(dt_, q_, kc(l), vc(l), pos_, S_, c.nh, c.nkv, c.hd, scale(), part_,
-                               tickets_, attn_out_, st_), "attn_decode");
-      if (tp_ > 1) {
-        k_check(cake_gemv_x16(dt_, attn_out_, w.wo, nq, c.H, partial_, 0, st_), "o_proj");
-        ar_sum();
+      if (short_step_ && ao_ok_) {  // one split: attention + o_proj in one launch
+        k_check(cake_attn_oproj(dt_, q_, kc(l), vc(l), pos_, S_, c.nh, c.nkv, c.hd, scale(), w.wo,
+                                nq, c.H, tp_ > 1 ? partial_ : resid_, tp_ > 1 ? 0 : 1, ao_ws_,
+                                ao_tickets_, st_), "attn_oproj");
+        if (tp_ > 1) ar_sum();
       } else {
-        k_check(cake_gemv_x16(dt_, attn_out_, w.wo, nq, c.H, resid_, 1, st_), "o_proj");
+        k_check(cake_attn_decode(dt_, q_, kc(l), vc(l), pos_, S_, c.nh, c.nkv, c.hd, scale(),
+                                 part_, tickets_, attn_out_, st_), "attn_decode");
+        if (tp_ > 1) {
+          k_check(cake_gemv_x16(dt_, attn_out_, w.wo, nq, c.H, partial_, 0, st_), "o_proj");
+          ar_sum();
+        } else {
+          k_check(cake_gemv_x16(dt_, attn_out_, w.wo, nq, c.H, resid_, 1, st_), "o_proj");
+        }
       }
       const uint16_t* wgu = reinterpret_cast<const uint16_t*>(w.wgu);
       k_check(cake_swiglu(dt_, resid_, w.ln2, (float)c.eps, wgu, wgu + (size_t)c.I * c.H, c.H,
@@ -1505,11 +1544,14 @@ class Llama {
         if (world_ > 1)
           for (int fd : peers_) {
             Json st = msg("fstep");
+            st.set("pos", Json::integer(T + i));
             send_json(fd, st);
           }
         set_i32(tok_, forced[i]);
         set_i32(pos_, T + i);
+        short_step_ = short_at(T + i);
         step_body(m);
+        short_step_ = false;
         if (out)
           hip_check(hipMemcpyAsync(out + (size_t)(i + 1) * V, tp_ > 1 ? full_logits_ : logits_,
                                    sizeof(float) * V, hipMemcpyDeviceToHost, st_), "D2H");
@@ -1517,6 +1559,7 @@ class Llama {
       }
     } catch (...) {
       forced_ = false;
+      short_step_ = false;
       throw;
     }
     forced_ = false;
@@ -1638,13 +1681,21 @@ class Llama {
 
   // decode with TCP workers in the walk: every step eagerly (host round trips inside it),
   // the token read back after each; per-token host wall time
-  int decode_eager(int n, const Mode& m, const int32_t* eos, int n_eos, cake_engine_token_cb cb,
-                   void* ctx, int32_t* out, int out_cap, std::vector<float>* ms_out) {
+  int decode_eager(int pos0, int n, const Mode& m, const int32_t* eos, int n_eos,
+                   cake_engine_token_cb cb, void* ctx, int32_t* out, int out_cap,
+                   std::vector<float>* ms_out) {
     std::vector<float> ms;
     int n_out = 0;
     for (int i = 0; i < n; ++i) {
       const auto t0 = std::chrono::steady_clock::now();
-      step_body(m);
+      short_step_ = short_at(pos0 + i);
+      try {
+        step_body(m);
+      } catch (...) {
+        short_step_ = false;
+        throw;
+      }
+      short_step_ = false;
       int32_t tok = 0;
       hip_check(hipMemcpyAsync(&tok, tok_, sizeof(tok), hipMemcpyDeviceToHost, st_), "tok");
       hip_check(hipStreamSynchronize(st_), "sync");
@@ -1744,7 +1795,9 @@ class Llama {
         if (!active) continue;
         Mode fm;
         fm.fused = false;
+        short_step_ = short_at((int)m.get("pos").as_int());
         step_body(fm);
+        short_step_ = false;
       } else if (cmd == "replays") {
         if (!active) continue;
         CakeLoopSpec spec{};
@@ -2324,19 +2377,24 @@ class Llama {
       if (std::find(caps.begin(), caps.end(), cc) == caps.end()) caps.push_back(cc);
       if (cap >= need) break;
     }
+    // cap 1: the one-split lengths with attention + o_proj fused (attn_oproj.hip)
+    if (ao_ok_) caps.push_back(1);
     std::sort(caps.begin(), caps.end());
     try {
       for (int cap : caps) {
-        k_check(cake_attn_set_split_cap(cap), "attn_set_split_cap");
+        k_check(cake_attn_set_split_cap(cap == 1 ? full : cap), "attn_set_split_cap");
         hipGraph_t g = nullptr;
+        short_step_ = cap == 1;
         hip_check(hipStreamBeginCapture(st_, hipStreamCaptureModeGlobal), "BeginCapture");
         try {
           for (int i = 0; i < k_; ++i) step_body(m);
         } catch (...) {
+          short_step_ = false;
           (void)hipStreamEndCapture(st_, &g);
           if (g) (void)hipGraphDestroy(g);
           throw;
         }
+        short_step_ = false;
         hip_check(hipStreamEndCapture(st_, &g), "EndCapture");
         graphs_.push_back(g);
         hipGraphExec_t e = nullptr;

@@ -37,7 +37,7 @@
 //   * consumers synchronise among themselves with an LDS counter (the loader never
 //     joins a barrier); every global spin is bounded (s_memrealtime): a timeout sets
 //     an error word the host checks, and stops every later spin of the launch.
-#include "common.h"
+#include "../kernels/common.h"
 
 namespace cake {
 namespace mk {

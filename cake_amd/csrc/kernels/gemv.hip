@@ -57,50 +57,4 @@ CAKE_API int cake_qkv_rope(int dt, const float* resid, const void* norm_w, float
   return (int)hipGetLastError();
 }
 
-// Fused QKV + RoPE + KV write + attention (qkv_attn_kernel): n_rep <= 4 (the attention
-// tail runs on the gemv block's 4 waves), hd 64 / 128; one pair per wave.
-CAKE_API int cake_qkv_attn_supported(int K, int nh, int nkv, int hd) {
-  if (K % 8 || nkv <= 0 || nh % nkv || (hd != 64 && hd != 128)) return 0;
-  const int nrep = nh / nkv;
-  return nrep == 1 || nrep == 2 || nrep == 4;
-}
-
-CAKE_API int cake_qkv_attn(int dt, const float* resid, const void* norm_w, float eps,
-                           const void* wq, const void* wk, const void* wv, int K, int nh,
-                           int nkv, int hd, const float* inv_freq, const int* pos,
-                           float* q_out, void* kcache, void* vcache, int S, float scale,
-                           unsigned int* tickets, void* out, hipStream_t st) {
-  if (!cake_qkv_attn_supported(K, nh, nkv, hd) || S <= 0) return (int)hipErrorInvalidValue;
-  QkvArgs a{resid, (const uint16_t*)norm_w, eps, (const uint16_t*)wq,
-            (const uint16_t*)wk, (const uint16_t*)wv, K, nh, nkv, hd, inv_freq, pos,
-            q_out, (uint16_t*)kcache, (uint16_t*)vcache, S};
-  const QkvAttnTail tl{tickets, (uint16_t*)out, scale * 1.4426950408889634f};
-  const int npairs = (nh + 2 * nkv) * (hd / 2);
-  const dim3 grid(npairs / kGemvWaves);  // one pair per wave: (hd / 2) % 4 == 0
-  // fixed tuning (U 2, 4-chunk prefetch: the QKV GEMV's default) instead of the run-time
-  // (U, prefetch) table: this opt-in path instantiated ~250 kernels that each inline the
-  // attention core, and made this file the build's long pole
-#define CAKE_QA(HD, NR)                                                                     \
-  do {                                                                                      \
-    constexpr int nf = attn2_smem_floats<HD, NR, kGemvWaves>();                             \
-    const size_t lds = (size_t)(K > nf ? K : nf) * sizeof(float);                           \
-    constexpr int U = 2;                                                                    \
-    if (K / 8 >= 64 * 4) {                                                                  \
-      constexpr int PF = 4;                                                                 \
-      DISPATCH_DT(dt, CAKE_NX_NORM(K, hipLaunchKernelGGL(                                   \
-          (qkv_attn_kernel<DT, U, PF, NX, HD, NR>), grid, dim3(kGemvThreads), lds, st, a, tl))); \
-    } else {                                                                                \
-      DISPATCH_DT(dt, hipLaunchKernelGGL((qkv_attn_kernel<DT, U, 0, 0, HD, NR>), grid,      \
-                                         dim3(kGemvThreads), lds, st, a, tl));              \
-    }                                                                                       \
-  } while (0)
-  const int nrep = nh / nkv;
-  if (hd == 128) {
-    if (nrep == 4) CAKE_QA(128, 4); else if (nrep == 2) CAKE_QA(128, 2); else CAKE_QA(128, 1);
-  } else {
-    if (nrep == 4) CAKE_QA(64, 4); else if (nrep == 2) CAKE_QA(64, 2); else CAKE_QA(64, 1);
-  }
-#undef CAKE_QA
-  return (int)hipGetLastError();
-}
 

@@ -3,7 +3,6 @@
 // instantiations compile in parallel).  Design notes: gemv.hip.
 #pragma once
 #include "common.h"
-#include "attn_core2.h"
 
 namespace cake {
 
@@ -309,115 +308,6 @@ __global__ __launch_bounds__(kGemvThreads) void qkv_rope_kernel(QkvArgs a) {
     }
   };
   run_pairs<DT, true, U, PFC>(map, epi, xs, a.K, npairs, p0, gridDim.x * kGemvWaves, pre);
-}
-
-// ---------------------------------------------------------------------------
-// QKV + RoPE + KV-cache write + short-context GQA attention, one launch
-//
-// The separate attention launch of a decode layer (attention.hip) costs a launch
-// boundary plus its cold start on top of its own ~8-block body at short context.  Here
-// the workgroup that finishes a kv group's q/k/v rows LAST runs that group's attention
-// (attn_core2.h, one split) in the same launch:
-//   * one pair per wave (grid = npairs / 4), so a workgroup's four pairs are four
-//     consecutive dims of one head: their roped outputs meet in LDS and leave as ONE
-//     16-byte (q, f32) or 8-byte (k/v row, 16-bit) write-through (sc1) store per half;
-//   * the storing wave drains (vmcnt 0), the workgroup barriers, one lane adds 1 to the
-//     group's arrival counter (agent scope); the add that returns blocks_per_group - 1
-//     marks the last arriver, which re-arms the counter and reads q and K/V with sc1
-//     loads (MI355X_MICROARCH "Valid forms", row 1);
-//   * the attention tail reuses the x staging LDS (K floats >= the core's 13 KB).
-// tickets: the attention launch's ticket array (arrivals in [0, nkv), the core-2 epochs
-// in [nkv, 2 nkv)); both re-armed in-kernel, so launches of either kind interleave.
-// ---------------------------------------------------------------------------
-struct QkvAttnTail {
-  unsigned int* tickets;
-  uint16_t* out;  // [nh*hd] attention output
-  float scale_log2;
-};
-
-template <int DT, int U, int PFC, int NX, int HD, int NREP>
-__global__ __launch_bounds__(kGemvThreads) void qkv_attn_kernel(QkvArgs a, QkvAttnTail t) {
-  static_assert(AttnGeom<NREP>::NT == kGemvThreads, "attention tail runs on the gemv block");
-  extern __shared__ float xs[];
-  __shared__ float ep[kGemvWaves][2];
-  __shared__ unsigned int last_flag;
-  constexpr int half = HD / 2;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int pb = blockIdx.x * kGemvWaves;  // the block's first pair (grid = npairs / 4)
-  const int p0 = pb + wave;
-  const uint16_t* wq = a.wq;
-  const ptrdiff_t dk = a.wk - a.wq, dv = a.wv - a.wq;
-  const int nh = a.nh, nkv = a.nkv, nqk = a.nh + a.nkv, K = a.K;
-  auto map = [=](int p, const uint16_t*& wa, const uint16_t*& wb) {
-    const int slot = p / half;
-    const bool isq = slot < nh, isk = !isq && slot < nqk;
-    const uint16_t* base = wq + (isq ? 0 : (isk ? dk : dv));
-    const int head = slot - (isq ? 0 : (isk ? nh : nqk));
-    const size_t ra = (size_t)head * HD + (p - slot * half);
-    wa = base + ra * K;
-    wb = base + (ra + half) * K;
-  };
-  Regs<PFC> pre;
-  NormPre<DT, NX> xp;
-  const uint16_t *wa0, *wb0;
-  map(p0, wa0, wb0);
-  if constexpr (NX > 0) xp.load(a.resid, a.norm_w, a.K);
-  __builtin_amdgcn_sched_barrier(0);
-  prefetch_rows<PFC>(wa0, wb0, pre);
-  const float f0 = a.inv_freq[p0 - (p0 / half) * half];
-  __builtin_amdgcn_sched_barrier(0);
-  if constexpr (NX > 0) xp.finish(a.eps, a.K, xs);
-  else stage_rmsnorm<DT>(a.resid, a.norm_w, a.eps, a.K, xs);
-  const int pos = *a.pos;
-  const int slot = pb / half;  // uniform over the block
-  auto epi = [&](int p, float da, float db) {
-    if (lane != 0) return;
-    float oa = da, ob = db;
-    if (slot < nqk) {  // q, k: RoPE
-      float s, c;
-      sincosf((float)pos * f0, &s, &c);
-      oa = da * c - db * s;
-      ob = da * s + db * c;
-    }
-    ep[wave][0] = oa;
-    ep[wave][1] = ob;
-  };
-  run_pairs<DT, true, U, PFC>(map, epi, xs, a.K, (nqk + nkv) * half, p0, 1 << 30, pre);
-  __syncthreads();
-  if (threadIdx.x < 2) {  // half 0: dims i0..i0+3, half 1: i0+half..
-    const int i0 = pb - slot * half + threadIdx.x * half;
-    const float v0 = ep[0][threadIdx.x], v1 = ep[1][threadIdx.x];
-    const float v2 = ep[2][threadIdx.x], v3 = ep[3][threadIdx.x];
-    if (slot < nh) {
-      float* q = a.q_out + (size_t)slot * HD + i0;
-      st_sc1(q, v0); st_sc1(q + 1, v1); st_sc1(q + 2, v2); st_sc1(q + 3, v3);
-    } else {
-      const bool isk = slot < nqk;
-      const int head = slot - (isk ? nh : nqk);
-      uint16_t* row = (isk ? a.kcache : a.vcache) + ((size_t)head * a.S + pos) * HD + i0;
-      const unsigned long long w =
-          (unsigned long long)from_f32<DT>(v0) | ((unsigned long long)from_f32<DT>(v1) << 16) |
-          ((unsigned long long)from_f32<DT>(v2) << 32) | ((unsigned long long)from_f32<DT>(v3) << 48);
-      __hip_atomic_store(reinterpret_cast<unsigned long long*>(row), w, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  const int g = slot < nh ? slot / NREP : (slot < nqk ? slot - nh : slot - nqk);
-  if (threadIdx.x == 0) {
-    constexpr int bpg = (NREP + 2) * half / kGemvWaves;  // workgroups per kv group
-    const unsigned int n =
-        __hip_atomic_fetch_add(&t.tickets[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned int last = n == (unsigned int)(bpg - 1) ? 1u : 0u;
-    if (last) __hip_atomic_store(&t.tickets[g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last_flag = last;
-  }
-  __syncthreads();
-  if (!last_flag) return;
-  const AttnDecArgs at{a.q_out, a.kcache, a.vcache, a.pos, a.S, t.scale_log2, nullptr, t.tickets,
-                       t.out, 0, 1, nullptr, 1, 0, 0};
-  attn2_decode_block<DT, HD, NREP, true, kGemvWaves>(at, g, 0, xs, nkv);
 }
 
 // ---------------------------------------------------------------------------

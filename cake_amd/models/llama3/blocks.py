@@ -60,6 +60,11 @@ class DecodeBuffers:
         # merge's error word (+1 pad)
         self.part = torch.zeros(2 * nh * 64 * (hd + 2), device=device, dtype=f32)
         self.tickets = torch.zeros(2 * cfg.num_key_value_heads + 2, device=device, dtype=i32)
+        # fused attention + o_proj (attn_oproj.hip): per-group partial rows, row-block
+        # arrival tickets (zeroed once, re-armed by the kernel)
+        nkv = cfg.num_key_value_heads
+        self.ao_ws = torch.zeros(nkv * H, device=device, dtype=f32)
+        self.ao_tickets = torch.zeros(H // 32 + 2 * nkv + 2, device=device, dtype=i32)
         self.pos = torch.zeros(1, device=device, dtype=i32) if pos is None else pos
         if with_head:
             self.logits = torch.zeros(cfg.vocab_size, device=device, dtype=f32)
@@ -96,9 +101,6 @@ class LayerStack:
         # persistent decode (decode_mk.hip): one launch per token step instead of five
         # per layer; CAKE_MK=0 keeps the per-layer launches
         self.use_mk = os.environ.get("CAKE_MK", "0") != "0" and backend == "hip"
-        # one-split decode steps with QKV and attention as one launch (qkv_attn_kernel);
-        # off by default: measured slower than the two launches (profiles/r4_decode_attn_waves.md)
-        self.use_qkv_attn = os.environ.get("CAKE_QKV_ATTN", "0") != "0" and backend == "hip"
         self._mk_ok: bool | None = None
         self._mk_tables: dict = {}
 
@@ -227,11 +229,23 @@ class LayerStack:
             raise RuntimeError(f"persistent decode: a hand-off timed out (site {site}); "
                                "outputs of that launch are invalid")
 
-    def decode_step(self, bufs: DecodeBuffers, layers: list[int], session: int = 0) -> None:
+    def attn_oproj_ok(self) -> bool:
+        """The fused decode attention + o_proj launch covers this stack's shapes."""
+        if self.backend != "hip" or os.environ.get("CAKE_ATTN_OPROJ", "1") == "0":
+            return False
+        from ...ops import hip as K
+        c = self.cfg
+        return K.attn_oproj_supported(c.num_attention_heads, c.num_key_value_heads,
+                                      c.head_dim, c.hidden_size)
+
+    def decode_step(self, bufs: DecodeBuffers, layers: list[int], session: int = 0,
+                    fused: bool | None = None) -> None:
         """Graph-capturable T=1 step over bufs.resid at device position bufs.pos (hip only):
-        ONE persistent launch for all `layers` when the shapes allow (decode_mk.hip),
-        else five launches per layer (QKV+RoPE+KV write, attention, o_proj+residual,
-        norm+gate/up+SwiGLU, down_proj+residual)."""
+        five launches per layer (QKV+RoPE+KV write, attention, o_proj+residual,
+        norm+gate/up+SwiGLU, down_proj+residual), or four with attention and o_proj as
+        one launch when `fused` (default: inside K.attn_oproj_fused(), i.e. the
+        short-context graph bucket; the caller guarantees one attention split); or the
+        experimental persistent launch (decode_mk.hip, CAKE_MK=1, if built)."""
         from ...ops import hip as K
         cfg = self.cfg
         if layers and self.mk_enabled():
@@ -242,32 +256,24 @@ class LayerStack:
                         bufs.pos, bufs.resid, gran, ctl)
             return
         kv = self.cache(session)
-        fused = K.qkv_attn_active() and self.qkv_attn_ok()
+        if fused is None:
+            fused = K.attn_oproj_active()
+        fused = fused and self.attn_oproj_ok()
         for li in layers:
             w = self.weights[li]
             s = self.slot_of[li]
             kc, vc = kv.k[s], kv.v[s]
-            if fused:  # QKV + RoPE + KV write + attention: one launch (short contexts)
-                K.qkv_attn(bufs.resid, w.ln1, cfg.rms_norm_eps, w.wq, w.wk, w.wv,
-                           self.inv_freq, bufs.pos, bufs.q, kc, vc, self.scale, bufs.tickets,
-                           bufs.attn_out)
+            K.qkv_rope(bufs.resid, w.ln1, cfg.rms_norm_eps, w.wq, w.wk, w.wv,
+                       self.inv_freq, bufs.pos, bufs.q, kc, vc)
+            if fused:
+                K.attn_oproj(bufs.q, kc, vc, bufs.pos, self.scale, w.wo, bufs.resid, True,
+                             bufs.ao_ws, bufs.ao_tickets)
             else:
-                K.qkv_rope(bufs.resid, w.ln1, cfg.rms_norm_eps, w.wq, w.wk, w.wv,
-                           self.inv_freq, bufs.pos, bufs.q, kc, vc)
                 K.attn_decode(bufs.q, kc, vc, bufs.pos, self.scale, bufs.part, bufs.tickets,
                               bufs.attn_out)
-            K.gemv(bufs.attn_out, w.wo, bufs.resid, accumulate=True)
+                K.gemv(bufs.attn_out, w.wo, bufs.resid, accumulate=True)
             K.swiglu(bufs.resid, w.ln2, cfg.rms_norm_eps, w.wg, w.wu, bufs.act)
             K.gemv(bufs.act, w.wd, bufs.resid, accumulate=True)
-
-    def qkv_attn_ok(self) -> bool:
-        """The fused QKV + attention launch covers this stack's shapes (hip, GQA <= 4)."""
-        if not self.use_qkv_attn:
-            return False
-        from ...ops import hip as K
-        c = self.cfg
-        return K.qkv_attn_supported(c.hidden_size, c.num_attention_heads,
-                                    c.num_key_value_heads, c.head_dim)
 
     # ------------------------------------------------------------------ hip paths
     def _decode_graph(self, hidden, layers: list[int], pos0: int, session: int) -> None:
@@ -282,8 +288,8 @@ class LayerStack:
         need = K.attn_splits(pos0 + 1)
         cap = next((c for c in (8, 16, 32, 64) if c >= min(need, full)), 64)
         cap = min(cap, full)
-        if need == 1 and self.qkv_attn_ok() and not self.mk_enabled():
-            cap = 1  # one split: QKV and attention as one launch per layer
+        if K.attn_oproj_short(pos0) and self.attn_oproj_ok():
+            cap = 1  # one split: attention and o_proj as one launch per layer
         key = (session, tuple(layers), cap)
         ent = self._step_graph_cache.get(key)
         if ent is None:
@@ -294,10 +300,10 @@ class LayerStack:
                                      with_head=False)
             bufs.pos.fill_(pos0)
             bufs.resid.copy_(hidden[0])
-            self.decode_step(bufs, layers, session)
+            self.decode_step(bufs, layers, session, fused=cap == 1)
             hidden[0].copy_(bufs.resid)
             g = torch.cuda.CUDAGraph()
-            with K.attn_split_cap(cap if cap != 1 else full), K.qkv_attn_fused(cap == 1), \
+            with K.attn_split_cap(cap if cap != 1 else full), K.attn_oproj_fused(cap == 1), \
                     torch.cuda.graph(g):  # records only
                 self.decode_step(bufs, layers, session)
             self._step_graph_cache[key] = (g, bufs)
@@ -323,9 +329,13 @@ class LayerStack:
         cfg = self.cfg
         K.qkv_rope(bufs.resid, w.ln1, cfg.rms_norm_eps, w.wq, w.wk, w.wv, self.inv_freq,
                    bufs.pos, bufs.q, kc, vc)
-        K.attn_decode(bufs.q, kc, vc, bufs.pos, self.scale, bufs.part, bufs.tickets,
-                      bufs.attn_out)
-        K.gemv(bufs.attn_out, w.wo, bufs.resid, accumulate=True)
+        if K.attn_oproj_short(pos0) and self.attn_oproj_ok():
+            K.attn_oproj(bufs.q, kc, vc, bufs.pos, self.scale, w.wo, bufs.resid, True,
+                         bufs.ao_ws, bufs.ao_tickets)
+        else:
+            K.attn_decode(bufs.q, kc, vc, bufs.pos, self.scale, bufs.part, bufs.tickets,
+                          bufs.attn_out)
+            K.gemv(bufs.attn_out, w.wo, bufs.resid, accumulate=True)
         K.swiglu(bufs.resid, w.ln2, cfg.rms_norm_eps, w.wg, w.wu, bufs.act)
         K.gemv(bufs.act, w.wd, bufs.resid, accumulate=True)
         hidden[0].copy_(bufs.resid)

@@ -267,12 +267,12 @@ class DeviceDecoder:
                 for _ in range(self.k):
                     self._step_body()
             self.graphs[cap] = g
-        # bucket "1 split": QKV and attention as one launch per layer (the live lengths
-        # whose attention is one split per kv head; gemv.hip qkv_attn_kernel)
+        # bucket "1 split": attention and o_proj as one launch per layer (attn_oproj.hip),
+        # for the live lengths whose attention is a single split
         st = self.m.stack
-        if st.qkv_attn_ok() and not st.mk_enabled():
+        if st.attn_oproj_ok() and not st.mk_enabled():
             g = torch.cuda.CUDAGraph()
-            with K.qkv_attn_fused(), torch.cuda.graph(g):
+            with K.attn_oproj_fused(), torch.cuda.graph(g):
                 for _ in range(self.k):
                     self._step_body()
             self.graphs[1] = g
@@ -349,7 +349,9 @@ class DeviceDecoder:
             # live length of the last step of this replay (+1: sampled mode pushes)
             self._graph_for(self.host_pos + self.k + 1).replay()
         else:
-            self._step_body()
+            from ...ops import hip as K
+            with K.attn_oproj_fused(K.attn_oproj_short(self.host_pos + self.k - 1)):
+                self._step_body()
         if self.greedy:  # greedy steps advance pos on the device; sampled ones via push()
             self.host_pos += self.k
 

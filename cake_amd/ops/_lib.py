@@ -25,9 +25,9 @@ Z = C.c_size_t
 
 # name -> argtypes (all return int hipError_t)
 _SIGS = {
+    "cake_attn_oproj": [I, P, P, P, P, I, I, I, I, F, P, I, I, P, I, P, P, P],
+    "cake_attn_oproj_supported": [I, I, I, I],
     "cake_qkv_rope": [I, P, P, F, P, P, P, I, I, I, I, P, P, P, P, P, I, P],
-    "cake_qkv_attn": [I, P, P, F, P, P, P, I, I, I, I, P, P, P, P, P, I, F, P, P, P],
-    "cake_qkv_attn_supported": [I, I, I, I],
     "cake_attn_set_prefetch": [I],
     "cake_swiglu": [I, P, P, F, P, P, I, I, P, P],
     "cake_gemv_x16": [I, P, P, I, I, P, I, P],
@@ -92,6 +92,8 @@ def kernels():
                     f"{path} not built; run `python -m cake_amd.build` (hipcc gfx950)")
             lib = C.CDLL(str(path), mode=C.RTLD_GLOBAL)
             for name, argtypes in _SIGS.items():
+                if name in _OPTIONAL and not hasattr(lib, name):
+                    continue  # csrc/experimental, built with CAKE_BUILD_EXPERIMENTAL=1
                 fn = getattr(lib, name)
                 fn.argtypes = argtypes
                 fn.restype = _RESTYPE.get(name, C.c_int)
@@ -137,6 +139,9 @@ _SIGS.update({
     "cake_mk_decode": [I, P, I, I, I, I, I, I, I, F, F, P, P, P, P, P, C.c_double, P],
 })
 _RESTYPE = {"cake_mk_gstride": C.c_longlong}
+# entry points of csrc/experimental (not in the default build)
+_OPTIONAL = {"cake_mk_gstride", "cake_mk_grid", "cake_mk_supported", "cake_mk_decode",
+             "cake_mk_set_stamps", "cake_mk_set_tuning"}
 _SIGS["cake_mk_set_stamps"] = [P]
 _SIGS["cake_mk_set_tuning"] = [I, I, I, I]
 _SIGS["cake_attn_debug_drop_partials"] = [I]

@@ -10,6 +10,7 @@ from __future__ import annotations
 import ctypes as C
 
 import os
+import threading
 
 import torch
 
@@ -77,67 +78,6 @@ def qkv_rope(resid, norm_w, eps, wq, wk, wv, inv_freq, pos, q_out, kcache, vcach
           "qkv_rope")
 
 
-
-def qkv_attn_supported(K: int, nh: int, nkv: int, hd: int) -> bool:
-    """Shapes the fused QKV + attention launch covers (GQA groups of <= 4 heads)."""
-    return bool(kernels().cake_qkv_attn_supported(int(K), int(nh), int(nkv), int(hd)))
-
-
-def qkv_attn(resid, norm_w, eps, wq, wk, wv, inv_freq, pos, q_out, kcache, vcache, scale,
-             tickets, out):
-    """:func:`qkv_rope` and :func:`attn_decode` as ONE launch (gemv.hip qkv_attn_kernel):
-    the workgroup that completes a kv group's q/k/v rows last runs that group's attention
-    over the whole live length as one split.  Fastest where attn_splits(Tk) == 1 (short
-    contexts); correct at any length.  tickets: the attention launch's [2 nkv + 2] array
-    (shared: both kernels re-arm what they use)."""
-    K = resid.numel()
-    nkv, S, hd = kcache.shape
-    nh = wq.shape[0] // hd
-    dt = wq.dtype
-    _req(resid, "resid", dtype=torch.float32)
-    _req(norm_w, "norm_w", dtype=dt, shape=(K,))
-    _req(wq, "wq", dtype=dt, shape=(nh * hd, K))
-    _req(wk, "wk", dtype=dt, shape=(nkv * hd, K))
-    _req(wv, "wv", dtype=dt, shape=(nkv * hd, K))
-    _req(inv_freq, "inv_freq", dtype=torch.float32, shape=(hd // 2,))
-    _req(pos, "pos", dtype=torch.int32, numel=1)
-    _req(q_out, "q_out", dtype=torch.float32, numel=nh * hd)
-    _req(kcache, "kcache", dtype=dt)
-    _req(vcache, "vcache", dtype=dt, shape=kcache.shape)
-    _req(tickets, "tickets", dtype=torch.int32, numel=2 * nkv + 2)
-    _req(out, "out", dtype=dt, numel=nh * hd)
-    if not qkv_attn_supported(K, nh, nkv, hd):
-        raise ValueError(f"qkv_attn: unsupported shape K={K} nh={nh} nkv={nkv} hd={hd}")
-    check(kernels().cake_qkv_attn(_dt(wq), _p(resid), _p(norm_w), float(eps), _p(wq), _p(wk),
-                                  _p(wv), K, nh, nkv, hd, _p(inv_freq), _p(pos), _p(q_out),
-                                  _p(kcache), _p(vcache), S, float(scale), _p(tickets), _p(out),
-                                  _stream()),
-          "qkv_attn")
-
-
-_QKV_ATTN = [False]
-
-
-class qkv_attn_fused:
-    """Context manager: decode steps issued (or captured) inside it run QKV + attention as
-    one launch where the shapes allow (LayerStack.decode_step); DeviceDecoder captures
-    one such graph for the live lengths that run one attention split."""
-
-    def __init__(self, on: bool = True):
-        self.on = bool(on)
-
-    def __enter__(self):
-        self.prev = _QKV_ATTN[0]
-        _QKV_ATTN[0] = self.on
-        return self
-
-    def __exit__(self, *exc):
-        _QKV_ATTN[0] = self.prev
-        return False
-
-
-def qkv_attn_active() -> bool:
-    return _QKV_ATTN[0]
 
 def swiglu(resid, norm_w, eps, wg, wu, act):
     """act = silu(rmsnorm(resid) @ wg.T) * (rmsnorm(resid) @ wu.T)   (batch 1)."""
@@ -210,6 +150,70 @@ def head_select(resid, norm_w, eps, w, logits, hist, hist_len, last_n: int, pena
           "head_select")
 
 
+def attn_oproj_supported(nh: int, nkv: int, hd: int, H: int) -> bool:
+    """Shapes of the fused decode attention + o_proj launch (attn_oproj.hip)."""
+    return bool(kernels().cake_attn_oproj_supported(int(nh), int(nkv), int(hd), int(H)))
+
+
+def attn_oproj_ws_sizes(nkv: int, H: int) -> tuple[int, int]:
+    """(f32 partial floats, int32 ticket words) of its workspace."""
+    return nkv * H, H // 32 + 2 * nkv + 2
+
+
+def attn_oproj(q, kcache, vcache, pos, scale, wo, out, accumulate: bool, ws, tickets):
+    """Decode attention + o_proj in ONE launch (short contexts: the attention runs as one
+    split): out (+)= W_o . attention(q, K, V).  wo [H, nh*hd] (this rank's columns);
+    ws f32 [nkv * H], tickets int32 (:func:`attn_oproj_ws_sizes`, zeroed once)."""
+    nkv, S, hd = kcache.shape
+    nh = q.numel() // hd
+    H = wo.shape[0]
+    _req(q, "q", dtype=torch.float32)
+    _req(kcache, "kcache")
+    _req(vcache, "vcache", dtype=kcache.dtype, shape=kcache.shape)
+    _req(pos, "pos", dtype=torch.int32, numel=1)
+    _req(wo, "wo", dtype=kcache.dtype, shape=(H, nh * hd))
+    _req(out, "out", dtype=torch.float32, numel=H)
+    nws, ntk = attn_oproj_ws_sizes(nkv, H)
+    _req(ws, "ws", dtype=torch.float32, numel=nws)
+    _req(tickets, "tickets", dtype=torch.int32, numel=ntk)
+    if not attn_oproj_supported(nh, nkv, hd, H):
+        raise ValueError(f"attn_oproj: unsupported shape nh={nh} nkv={nkv} hd={hd} H={H}")
+    check(kernels().cake_attn_oproj(_dt(kcache), _p(q), _p(kcache), _p(vcache), _p(pos), S, nh,
+                                    nkv, hd, float(scale), _p(wo), nh * hd, H, _p(out),
+                                    int(bool(accumulate)), _p(ws), _p(tickets), _stream()),
+          "attn_oproj")
+
+
+_AO_FUSED = threading.local()
+
+
+class attn_oproj_fused:
+    """Context: decode steps recorded / run inside use the fused attention + o_proj
+    launch (the short-context graph bucket; eager steps at a short live length)."""
+
+    def __init__(self, on: bool = True):
+        self.on = bool(on)
+
+    def __enter__(self):
+        self.prev = getattr(_AO_FUSED, "on", False)
+        _AO_FUSED.on = self.on
+        return self
+
+    def __exit__(self, *exc):
+        _AO_FUSED.on = self.prev
+        return False
+
+
+def attn_oproj_active() -> bool:
+    return getattr(_AO_FUSED, "on", False)
+
+
+def attn_oproj_short(pos: int) -> bool:
+    """An eager step at device position `pos` takes the fused launch exactly when a
+    one-step graph replay there would (its bucket: one attention split at pos + 2)."""
+    return attn_splits(int(pos) + 2) == 1
+
+
 def attn_decode(q, kcache, vcache, pos, scale, part, tickets, out):
     """Split-K GQA decode attention for the token at device position `pos`.
 
@@ -253,9 +257,16 @@ MK_LAYER_PTRS = 8  # ln1, wqkv, wo, ln2, wgu, wd, kc, vc
 MK_CTL_WORDS = 4   # epoch, exit ticket, error flag, error site
 
 
+def mk_available() -> bool:
+    """The persistent decode engine was built (csrc/experimental, CAKE_BUILD_EXPERIMENTAL=1)."""
+    return hasattr(kernels(), "cake_mk_decode")
+
+
 def mk_supported(H: int, I: int, nh: int, nkv: int, hd: int) -> bool:
     """Shapes the persistent decode kernel handles on this device (H, I, nh*hd
-    multiples of 512; head_dim 128; GQA group 4 or 8)."""
+    multiples of 512; head_dim 128; GQA group 4 or 8); False when it is not built."""
+    if not mk_available():
+        return False
     return kernels().cake_mk_supported(int(H), int(I), int(nh), int(nkv), int(hd)) == 0
 
 

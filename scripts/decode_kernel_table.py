@@ -19,6 +19,8 @@ PROBE_US = {"qkv_rope": 9.03, "attn_decode": 1.94, "o_proj": 6.59, "swiglu": 35.
 
 
 def kind(name):
+    if "attn_oproj" in name:  # fused attention + o_proj (one-split lengths)
+        return "attn_oproj"
     if "attn2_decode" in name:  # decode-attention core 2 (the default)
         return "attn_decode"
     for k in ("qkv_rope", "swiglu", "attn_decode", "gemv_norm_f32", "gemv_x16"):
@@ -37,20 +39,23 @@ def main():
     name_col = "kernel_name" if "kernel_name" in cols else "name"
     rows = c.execute(f"select {name_col}, start, end from kernels order by start").fetchall()
     agg, x16 = {}, 0
+    fused = any(kind(n) == "attn_oproj" for n, _, _ in rows)
     for n, s, e in rows:
         k = kind(n)
         if k is None:
             continue
-        if k == "gemv_x16":
-            k = "o_proj" if x16 % 2 == 0 else "down_proj"
+        if k == "gemv_x16":  # o_proj / down_proj alternate; only down_proj beside the fused
+            k = "down_proj" if fused else ("o_proj" if x16 % 2 == 0 else "down_proj")
             x16 += 1
         if k == "gemv_norm_f32":
             k = "lm_head"
         agg.setdefault(k, []).append((e - s) / 1e3)
     BYTES["attn_decode"] = 2 * NKV * a.ctx * HD * 2
+    BYTES["attn_oproj"] = BYTES["o_proj"] + BYTES["attn_decode"]
+    PROBE_US["attn_oproj"] = PROBE_US["o_proj"]
     print(f"{'kernel':<12} {'calls':>6} {'avg_us':>8} {'MB':>9} {'TB/s':>6} {'probe_us':>9} {'of_probe':>8}")
     per_tok = 0.0
-    for k in ("qkv_rope", "attn_decode", "o_proj", "swiglu", "down_proj", "lm_head"):
+    for k in ("qkv_rope", "attn_decode", "o_proj", "attn_oproj", "swiglu", "down_proj", "lm_head"):
         if k not in agg:
             continue
         d = sorted(agg[k])

@@ -112,12 +112,17 @@ def tune(M, Nv, K, epi, dt):
     return cur, res[cur], best, res[best]
 
 
-def llama_shapes():
+LLAMA_LENS = {"8b": (32, 128, 512, 1024, 2048, 4096), "70b": (512, 2048)}
+
+
+def llama_shapes(lens=None):
     """Prefill linears of Llama-3-8B / 70B (q|k|v, o + residual, gate|up + SwiGLU, down +
-    residual) at the prompt lengths the engine and the bench run."""
+    residual) at the prompt lengths the engine and the bench run (``lens``: model ->
+    prompt lengths, default LLAMA_LENS)."""
+    lens = lens or LLAMA_LENS
     out = collections.Counter()
-    for (H, I, nq, nkv), Ts in (((4096, 14336, 32, 8), (32, 128, 512, 1024, 2048, 4096)),
-                                ((8192, 28672, 64, 8), (512, 2048))):
+    for (H, I, nq, nkv), Ts in (((4096, 14336, 32, 8), lens.get("8b", ())),
+                                ((8192, 28672, 64, 8), lens.get("70b", ()))):
         hd = H // nq
         for T in Ts:
             out[(T, (nq + 2 * nkv) * hd, H, "store")] += 1
@@ -131,6 +136,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--versions", default="xl,v1-5",
                     help="comma list of SD versions, and/or 'llama' for the prefill shapes")
+    ap.add_argument("--llama-lens", default=None,
+                    help="prompt lengths of the llama shapes, e.g. '8b:256,384;70b:1024'")
     ap.add_argument("--write", default=None,
                     help="write gemm_tuned.json with the winners merged in to this path")
     a = ap.parse_args()
@@ -138,7 +145,11 @@ def main():
     new = []
     for version in a.versions.split(","):
         dt = torch.bfloat16 if version == "llama" else torch.float16
-        shapes = llama_shapes() if version == "llama" else record_shapes(version, dt)
+        lens = None
+        if a.llama_lens:
+            lens = {k: tuple(int(x) for x in v.split(",")) for k, v in
+                    (part.split(":") for part in a.llama_lens.split(";"))}
+        shapes = llama_shapes(lens) if version == "llama" else record_shapes(version, dt)
         tot_cur = tot_best = 0.0
         for (M, Nv, K, epi), n in sorted(shapes.items(), key=lambda kv: -kv[1] * kv[0][0] * kv[0][1] * kv[0][2]):
             cur, t_cur, best, t_best = tune(M, Nv, K, epi, dt)

@@ -92,58 +92,6 @@ def test_qkv_rope(cuda, dt, H, nh, nkv, hd, pos):
     assert kc[:, :pos].abs().sum() == 0 and kc[:, pos + 1:].abs().sum() == 0
 
 
-@pytest.mark.parametrize("dt", DTYPES)
-@pytest.mark.parametrize("H,nh,nkv,hd", [(4096, 32, 8, 128), (1024, 8, 2, 128), (512, 4, 2, 64),
-                                         (256, 4, 4, 64)])
-def test_qkv_attn_fused(cuda, dt, H, nh, nkv, hd):
-    """QKV + RoPE + KV write + attention as one launch (gemv.hip qkv_attn_kernel) vs the f32
-    reference and vs the two launches it replaces, over positions inside its one-split
-    range and past it (still correct: one workgroup walks every key), run back to back so
-    the in-kernel arrival counters must re-arm."""
-    from cake_amd.ops import hip as K_
-    if not K_.qkv_attn_supported(H, nh, nkv, hd):
-        pytest.fail("shape should be supported")
-    torch.manual_seed(9)
-    S = 1024
-    nw = (1 + 0.1 * torch.randn(H, device=cuda)).to(dt)
-    wq, wk, wv = (_rand(n * hd, H, dt=dt, std=0.05) for n in (nh, nkv, nkv))
-    invf = R.inv_freq(hd, 500000.0).to(cuda)
-    kc = _rand(nkv, S, hd, dt=dt)
-    vc = _rand(nkv, S, hd, dt=dt)
-    q = torch.empty(nh * hd, device=cuda)
-    out = torch.empty(nh * hd, device=cuda, dtype=dt)
-    tickets = torch.zeros(2 * nkv + 2, dtype=torch.int32, device=cuda)
-    part = torch.zeros(K_.attn_workspace_numel(nh, hd, S), device=cuda)
-    scale = 1 / math.sqrt(hd)
-    for pos in (0, 1, 15, 16, 200, 319, 320, 700, S - 1):
-        resid = torch.randn(H, device=cuda)
-        p = torch.tensor([pos], dtype=torch.int32, device=cuda)
-        # the two-launch path on a copy of the cache
-        kc2, vc2 = kc.clone(), vc.clone()
-        q2, out2 = torch.empty_like(q), torch.empty_like(out)
-        K_.qkv_rope(resid, nw, 1e-5, wq, wk, wv, invf, p, q2, kc2, vc2)
-        K_.attn_decode(q2, kc2, vc2, p, scale, part, tickets, out2)
-        out.fill_(float("nan"))
-        K_.qkv_attn(resid, nw, 1e-5, wq, wk, wv, invf, p, q, kc, vc, scale, tickets, out)
-        torch.cuda.synchronize()
-        assert int(tickets[:nkv].abs().sum()) == 0, "arrival counters not re-armed"
-        assert K_.attn_error(tickets) == 0
-        torch.testing.assert_close(q, q2, atol=1e-5, rtol=1e-5)
-        # (1 ulp: the RoPE rotation may contract to an FMA differently in the two kernels)
-        torch.testing.assert_close(kc[:, pos].float(), kc2[:, pos].float(), atol=1e-3, rtol=8e-3)
-        torch.testing.assert_close(vc[:, pos].float(), vc2[:, pos].float(), atol=1e-3, rtol=8e-3)
-        Tk = pos + 1
-        ref = R.attention(q.view(1, nh, hd), kc[:, :Tk].transpose(0, 1).float(),
-                          vc[:, :Tk].transpose(0, 1).float(), pos).reshape(-1)
-        # projected q (std ~3) makes the softmax sharp: the 16-bit q fragments of both
-        # paths drift from the f32 reference alike, so pin the fused launch to the
-        # two-launch path elementwise and both to the reference in norm
-        torch.testing.assert_close(out.float(), out2.float(), **_tol(dt))
-        err = float((out.float() - ref).norm() / ref.norm())
-        err2 = float((out2.float() - ref).norm() / ref.norm())
-        assert err < 1e-2 and err <= 1.5 * err2 + 1e-3, f"pos {pos}: {err:.3e} vs {err2:.3e}"
-
-
 @pytest.fixture(params=[(1, 320), (2, 320), (2, 0)], ids=["core1", "core2", "core2-split"])
 def attn_impl(request, cuda):
     """Both decode-attention cores (attn_core.h chunks / attn_core2.h wave-stream MFMA);
@@ -488,3 +436,52 @@ def test_gemv_split_prologue(cuda, gemv_tuning, U, pf, mb):
     kr = R.rope((wk.float() @ xn).view(1, nkv, hd), posv, invf).view(nkv, hd)
     torch.testing.assert_close(kc[:, pos].float(), kr, **_tol(dt))
     torch.testing.assert_close(vc[:, pos].float(), (wv.float() @ xn).view(nkv, hd), **_tol(dt))
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("H,nh,nkv,hd", [(4096, 32, 8, 128), (8192, 64, 8, 128), (512, 8, 2, 64),
+                                         (256, 4, 2, 64), (1024, 8, 8, 128), (512, 4, 1, 128)])
+def test_attn_oproj_fused(cuda, dt, H, nh, nkv, hd):
+    """Decode attention + o_proj as one launch (attn_oproj.hip) vs the two launches it
+    replaces (attn_decode, then the o_proj GEMV) and vs the f32 reference, over the
+    one-split lengths it serves, accumulating into the residual and plain (tensor-parallel
+    partial); back to back, so the row-block tickets must re-arm."""
+    from cake_amd.ops import hip as K_
+    assert K_.attn_oproj_supported(nh, nkv, hd, H)
+    torch.manual_seed(11)
+    S = 512
+    kc = _rand(nkv, S, hd, dt=dt)
+    vc = _rand(nkv, S, hd, dt=dt)
+    wo = _rand(H, nh * hd, dt=dt, std=(nh * hd) ** -0.5)
+    q = _rand(nh * hd)
+    nws, ntk = K_.attn_oproj_ws_sizes(nkv, H)
+    ws = torch.zeros(nws, device=cuda)
+    tk = torch.zeros(ntk, dtype=torch.int32, device=cuda)
+    part = torch.zeros(K_.attn_workspace_numel(nh, hd, S), device=cuda)
+    tickets = torch.zeros(2 * nkv + 2, dtype=torch.int32, device=cuda)
+    attn = torch.empty(nh * hd, device=cuda, dtype=dt)
+    scale = 1 / math.sqrt(hd)
+    for pos in (0, 1, 15, 16, 63, 200, 318):
+        p = torch.tensor([pos], dtype=torch.int32, device=cuda)
+        base = torch.randn(H, device=cuda)
+        # two launches
+        K_.attn_decode(q, kc, vc, p, scale, part, tickets, attn)
+        want = base.clone()
+        K_.gemv(attn, wo, want, accumulate=True)
+        # fused, accumulating
+        got = base.clone()
+        K_.attn_oproj(q, kc, vc, p, scale, wo, got, True, ws, tk)
+        # fused, plain (out = W_o . attn)
+        plain = torch.full((H,), float("nan"), device=cuda)
+        K_.attn_oproj(q, kc, vc, p, scale, wo, plain, False, ws, tk)
+        torch.cuda.synchronize()
+        assert int(tk[:H // 32].abs().sum()) == 0, "row-block tickets not re-armed"
+        torch.testing.assert_close(got, want, atol=2e-3, rtol=2e-3)
+        torch.testing.assert_close(plain, want - base, atol=2e-3, rtol=2e-3)
+        # f32 reference (16-bit attention output, as both paths round it)
+        Tk = pos + 1
+        ref = R.attention(q.view(1, nh, hd), kc[:, :Tk].transpose(0, 1).float(),
+                          vc[:, :Tk].transpose(0, 1).float(), pos).reshape(-1)
+        ref_out = base + wo.float() @ ref.to(dt).float()
+        err = (got - ref_out).abs().max().item()
+        assert err <= 2e-2 * max(1.0, ref_out.abs().max().item()), err

@@ -1,4 +1,7 @@
-"""Persistent decode (decode_mk.hip) against the five-launch layer path.
+"""Persistent decode (csrc/experimental/decode_mk.hip) against the five-launch layer path.
+
+Experimental: measured slower than the launch path (profiles/r4_mk_summary.md), so it is
+not in the default build; build with CAKE_BUILD_EXPERIMENTAL=1 to run these.
 
 Both paths run the same decode step (RMSNorm, QKV + RoPE + KV write, GQA attention
 over the cache, o_proj + residual, RMSNorm + SwiGLU, down_proj + residual) from the
@@ -19,6 +22,9 @@ def _stack(cfg, max_seq, seed=0):
     st = random_stack(cfg, list(range(cfg.num_hidden_layers)), "cuda:0", torch.bfloat16,
                       max_seq=max_seq, seed=seed)
     st.use_mk = True
+    from cake_amd.ops import hip as K
+    if not K.mk_available():
+        pytest.skip("persistent decode engine not built (CAKE_BUILD_EXPERIMENTAL=1)")
     if not st.mk_enabled():
         pytest.skip("persistent decode not supported here")
     return st

@@ -138,9 +138,9 @@ def test_device_decoder_crosses_split_buckets(cuda):
 
 
 @pytest.mark.parametrize("k", [1, 4])
-def test_device_decoder_crosses_fused_bucket(cuda, k):
-    """Live lengths crossing the one-split edge (320 keys): the fused QKV + attention
-    graph up to it, the two-launch graph (cap 8) after it — tokens equal the host loop."""
+def test_device_decoder_crosses_one_split_edge(cuda, k):
+    """Live lengths crossing the one-split edge (320 keys): the one-split attention graph
+    up to it, the split-K graph (cap 8) after it — tokens equal the host loop."""
     from cake_amd.models.llama3.decode_loop import run_decode
     from cake_amd.models.llama3.model import DeviceDecoder
     from cake_amd.ops import reference as R
@@ -148,7 +148,6 @@ def test_device_decoder_crosses_fused_bucket(cuda, k):
     cfg = preset("llama3-8b", num_hidden_layers=2, vocab_size=2048, intermediate_size=1024,
                  hidden_size=512, num_attention_heads=8, num_key_value_heads=2)
     model = random_model(cfg, "cuda:0", torch.bfloat16, max_seq=1024, seed=6)
-    model.stack.use_qkv_attn = True
     g = torch.Generator().manual_seed(3)
     prompt = torch.randint(0, 2048, (310,), generator=g).tolist()
     toks = list(prompt)
