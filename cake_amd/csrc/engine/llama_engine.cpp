@@ -79,7 +79,8 @@ long long cake_attn_oproj_ws_floats(int nkv, int H);
 long long cake_attn_oproj_ticket_words(int nkv, int H);
 int cake_attn_oproj(int dt, const float* q, const void* kc, const void* vc, const int* pos, int S,
                     int nh, int nkv, int hd, float scale, const void* wo, int ldw, int H,
-                    float* out, int accumulate, float* ws, unsigned int* tickets, hipStream_t st);
+                    float* out, int accumulate, float* ws, unsigned int* tickets,
+                    unsigned int* err, hipStream_t st);
 int cake_attn_splits(int Tk);
 int cake_attn_max_split(int S);
 int cake_gemv_x16(int dt, const void* x, const void* w, int K, int N, float* out, int accumulate,
@@ -1092,9 +1093,12 @@ class Llama {
     hip_check(hipMemset(zeros_, 0, sizeof(int32_t) * 64), "memset");
     hip_check(hipMemset(hist_, 0, sizeof(int) * S_), "memset");
     hip_check(hipMemset(resid_, 0, sizeof(float) * (c.H + 4)), "memset");
-    ao_ok_ = cake_attn_oproj_supported(c.nh, c.nkv, c.hd, c.H) != 0;
-    if (const char* e = std::getenv("CAKE_ATTN_OPROJ"))
-      if (std::string(e) == "0") ao_ok_ = false;
+    // opt-in (CAKE_ATTN_OPROJ=1): measured slower than the attention + o_proj pair on
+    // MI355X (profiles/r5_attn_oproj_ab.md), kept for the A/B
+    {
+      const char* e = std::getenv("CAKE_ATTN_OPROJ");
+      ao_ok_ = e && std::string(e) == "1" && cake_attn_oproj_supported(c.nh, c.nkv, c.hd, c.H) != 0;
+    }
     if (ao_ok_) {
       ao_ws_ = dalloc<float>((size_t)cake_attn_oproj_ws_floats(c.nkv, c.H));
       const size_t tw = (size_t)cake_attn_oproj_ticket_words(c.nkv, c.H);
@@ -1455,7 +1459,7 @@ class Llama {
       if (short_step_ && ao_ok_) {  // one split: attention + o_proj in one launch
         k_check(cake_attn_oproj(dt_, q_, kc(l), vc(l), pos_, S_, c.nh, c.nkv, c.hd, scale(), w.wo,
                                 nq, c.H, tp_ > 1 ? partial_ : resid_, tp_ > 1 ? 0 : 1, ao_ws_,
-                                ao_tickets_, st_), "attn_oproj");
+                                ao_tickets_, tickets_ + 2 * c.nkv, st_), "attn_oproj");
         if (tp_ > 1) ar_sum();
       } else {
         k_check(cake_attn_decode(dt_, q_, kc(l), vc(l), pos_, S_, c.nh, c.nkv, c.hd, scale(),

@@ -104,10 +104,18 @@ __device__ __forceinline__ uint4 ld16_sc1(__amdgpu_buffer_rsrc_t r, size_t byte_
 // PFD: key blocks per wave in flight (1: the next block's loads issued with the current
 // block's compute; 2: two ahead, and split 0 requests its first TWO blocks per wave at
 // launch — up to 2 NW x 16 keys need no load round trip inside the loop).
+struct NoHook {
+  __device__ __forceinline__ void operator()() const {}
+};
+
+// hook: called once per wave right after the block's first loads (K/V of the first one
+// or two key blocks, q) are issued and before anything waits on them — a caller's own
+// loads issued there queue BEHIND the attention's (vmcnt retires in order) instead of in
+// front of them (attn_oproj.hip: the o_proj weight tile)
 template <int DT, int HD, int NREP, bool FUSED = false, int NW = AttnGeom2<NREP>::NW,
-          int PFD = 2>
+          int PFD = 2, class Hook = NoHook>
 __device__ __forceinline__ void attn2_decode_block(const AttnDecArgs& a, int g, int s,
-                                                   float* lds, int ng) {
+                                                   float* lds, int ng, const Hook& hook = Hook()) {
   static_assert(PFD == 1 || PFD == 2, "prefetch depth 1 or 2");
   constexpr int DS = HD / 32;    // MFMA k-steps (A fragments) per key block
   constexpr int NCH = HD / 8;    // 8-dim chunks per row
@@ -180,6 +188,8 @@ __device__ __forceinline__ void attn2_decode_block(const AttnDecArgs& a, int g, 
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (PFD == 2)
       if (s == 0) load_blk(I1{}, (wave + NW) * kBlk, a.S - 1);
+    __builtin_amdgcn_sched_barrier(0);
+    hook();
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int d = 0; d < DS; ++d) {

@@ -20,7 +20,11 @@
 //     are read from HBM once and from that XCD's L2 after): a few KB per workgroup at
 //     the short lengths this kernel serves;
 //   * the nkv per-group partial rows of a row block are summed in a fixed order by the
-//     last-arriving workgroup (agent-scope ticket), so results are deterministic.
+//     last-arriving workgroup (relaxed agent-scope ticket), so results are deterministic.
+//     Partials travel as 8-byte {f32, tag} granules (one store each; the tag is the row
+//     block's launch epoch + 1): the last arriver polls for the tags instead of either
+//     side fencing — a release fence per workgroup writes back the L2 and cost ~50 us per
+//     launch here (MI355X_MICROARCH 'barrier-counter' / 'publish-large').
 //
 // Reference: cake-core/src/models/llama3/attention.rs:96-120 (scores, softmax, P.V,
 // o_proj); SURVEY K09-K13 + K03 (o_proj) + K14 (residual).
@@ -47,9 +51,10 @@ struct AttnOprojArgs {
   int H;                   // output rows
   float* out;              // [H] f32: out (+)= W_o . attn
   int accumulate;
-  float* ws;               // [nkv][H] f32 partial rows
-  unsigned int* tickets;   // [H / RB] arrival counters (zero between launches), then
-                           // [2 nkv + 2] scratch for the attention core's epoch words
+  unsigned long long* ws;  // [nkv][H] {f32 partial, tag} granules
+  unsigned int* tickets;   // [NRB] arrival counters (zero between launches), [NRB] epochs,
+                           // then [2 nkv + 2] scratch for the attention core's epoch words
+  unsigned int* err;       // error word (a poll that gave up), or null
   int nkv;
 };
 
@@ -87,16 +92,24 @@ __global__ __launch_bounds__(AttnGeom2<NREP>::NT) void attn_oproj_kernel(AttnOpr
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int sub = lane / LPR, cl = lane - sub * LPR;
   const int row0 = j * RB + wave * RPWV;
+  const int nrb = p.H / 32;  // ticket / epoch slots (the smallest row block)
+  const unsigned int epoch =
+      __hip_atomic_load(p.tickets + nrb + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
-  // (1) this workgroup's weight tile, in flight during the attention
+  // (1) this workgroup's weight tile, in flight during the attention: issued by the
+  // attention core's hook, right BEHIND its first K/V blocks and q (loads retire in
+  // order: issued in front, the weights would delay every attention step)
   uint4 w[IT][CPL];
   const uint16_t* wg = p.wo + (size_t)g * NCOL;
+  auto issue_weights = [&]() {
 #pragma unroll
-  for (int it = 0; it < IT; ++it) {
-    const uint4* wr = reinterpret_cast<const uint4*>(wg + (size_t)(row0 + it * RPW + sub) * p.ldw);
+    for (int it = 0; it < IT; ++it) {
+      const uint4* wr =
+          reinterpret_cast<const uint4*>(wg + (size_t)(row0 + it * RPW + sub) * p.ldw);
 #pragma unroll
-    for (int c = 0; c < CPL; ++c) w[it][c] = ld_nt16(wr + cl + c * LPR);
-  }
+      for (int c = 0; c < CPL; ++c) w[it][c] = ld_nt16(wr + cl + c * LPR);
+    }
+  };
 
   // (2) the group's attention, one split, output (16-bit, as the standalone kernel
   // writes it) into LDS: the core stores at out[g * NCOL + idx]
@@ -108,7 +121,7 @@ __global__ __launch_bounds__(AttnGeom2<NREP>::NT) void attn_oproj_kernel(AttnOpr
   at.S = p.S;
   at.scale_log2 = p.scale_log2;
   at.part = nullptr;
-  at.tickets = p.tickets + p.H / RB;  // scratch epoch words (never a tag in one split)
+  at.tickets = p.tickets + 2 * nrb;  // scratch epoch words (never a tag in one split)
   at.out = xs - (size_t)g * NCOL;
   at.min_keys = 64;
   at.maxsplit = 1;
@@ -116,7 +129,9 @@ __global__ __launch_bounds__(AttnGeom2<NREP>::NT) void attn_oproj_kernel(AttnOpr
   at.target = 16;
   at.single = p.S;  // every live length is one split here
   at.drop_partials = 0;
-  attn2_decode_block<DT, HD, NREP, false, NW, 1>(at, g, 0, lds, nkv);
+  // two key blocks per wave requested up front (PFD 2): up to 2 NW x 16 keys of the
+  // attention need no load issued behind the weights
+  attn2_decode_block<DT, HD, NREP, false, NW, 2>(at, g, 0, lds, nkv, issue_weights);
   __syncthreads();
 
   // (3) partial o_proj rows of this group: lanes of a row group sum their chunks
@@ -134,34 +149,46 @@ __global__ __launch_bounds__(AttnGeom2<NREP>::NT) void attn_oproj_kernel(AttnOpr
     }
     acc[it] = group_sum<LPR>(a);
   }
+  const unsigned long long tag = (unsigned long long)(epoch + 1u) << 32;
   if (cl == 0) {
 #pragma unroll
     for (int it = 0; it < IT; ++it)
-      __hip_atomic_store(reinterpret_cast<unsigned int*>(p.ws) + (size_t)g * p.H + row0 +
-                             it * RPW + sub,
-                         __float_as_uint(acc[it]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(p.ws + (size_t)g * p.H + row0 + it * RPW + sub,
+                         tag | __float_as_uint(acc[it]), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
   }
-  __threadfence();
   __syncthreads();
   // (4) the last of the nkv groups of row block j sums the partials (g order: fixed)
   if (threadIdx.x == 0) {
     const unsigned int t =
-        __hip_atomic_fetch_add(p.tickets + j, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(p.tickets + j, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     is_last = t == (unsigned int)(nkv - 1);
   }
   __syncthreads();
   if (!is_last) return;  // workgroup-uniform
-  __threadfence();
+  bool timed_out = false;
   for (int i = threadIdx.x; i < RB; i += NT) {
     const int r = j * RB + i;
     float s = 0.f;
-    for (int gg = 0; gg < nkv; ++gg)
-      s += __uint_as_float(__hip_atomic_load(reinterpret_cast<const unsigned int*>(p.ws) +
-                                                 (size_t)gg * p.H + r,
-                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    for (int gg = 0; gg < nkv; ++gg) {
+      unsigned long long v;
+      for (int tries = 0;; ++tries) {  // the granule of this launch (its tag) — bounded
+        v = __hip_atomic_load(p.ws + (size_t)gg * p.H + r, __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_AGENT);
+        if ((v >> 32) == (tag >> 32)) break;
+        if (tries > kAttnMaxPolls) { timed_out = true; break; }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      s += __uint_as_float((unsigned int)v);
+    }
     p.out[r] = p.accumulate ? p.out[r] + s : s;
   }
-  if (threadIdx.x == 0) __hip_atomic_store(p.tickets + j, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (timed_out && p.err) attn_poll_timeout(p.err);
+  __syncthreads();
+  if (threadIdx.x == 0) {  // re-arm for the next launch (the kernel boundary orders these)
+    __hip_atomic_store(p.tickets + j, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(p.tickets + nrb + j, epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 }  // namespace cake
@@ -178,21 +205,24 @@ CAKE_API int cake_attn_oproj_supported(int nh, int nkv, int hd, int H) {
   return ncol >= 128 && ncol <= 1024;
 }
 
-// workspace: f32 partial rows, then the ticket words (u32, zeroed once)
-CAKE_API long long cake_attn_oproj_ws_floats(int nkv, int H) { return (long long)nkv * H; }
+// workspace: {f32, tag} granules of the partial rows (as f32 words: 2 per granule), then
+// the ticket / epoch words (u32, zeroed once)
+CAKE_API long long cake_attn_oproj_ws_floats(int nkv, int H) { return 2ll * nkv * H; }
 CAKE_API long long cake_attn_oproj_ticket_words(int nkv, int H) {
-  return (long long)H / ao_rows(8) + 2 * nkv + 2;  // the smallest row block: room for both
+  return 2ll * (H / 32) + 2 * nkv + 2;  // slots for the smallest row block
 }
 
 CAKE_API int cake_attn_oproj(int dt, const float* q, const void* kc, const void* vc,
                              const int* pos, int S, int nh, int nkv, int hd, float scale,
                              const void* wo, int ldw, int H, float* out, int accumulate,
-                             float* ws, unsigned int* tickets, hipStream_t st) {
-  if (!cake_attn_oproj_supported(nh, nkv, hd, H) || S <= 0 || ldw < nh * hd || !ws || !tickets)
+                             float* ws, unsigned int* tickets, unsigned int* err,
+                             hipStream_t st) {
+  if (!cake_attn_oproj_supported(nh, nkv, hd, H) || S <= 0 || ldw < nh * hd || !ws || !tickets ||
+      ((uintptr_t)ws % 8))
     return (int)hipErrorInvalidValue;
   AttnOprojArgs p{q, (const uint16_t*)kc, (const uint16_t*)vc, pos, S,
-                  scale * 1.4426950408889634f, (const uint16_t*)wo, ldw, H, out, accumulate, ws,
-                  tickets, nkv};
+                  scale * 1.4426950408889634f, (const uint16_t*)wo, ldw, H, out, accumulate,
+                  reinterpret_cast<unsigned long long*>(ws), tickets, err, nkv};
   const int nrep = nh / nkv;
   const dim3 grid(nkv * (H / ao_rows(nrep)));
 #define CAKE_AO(DTV, HDV, NR)                                                                  \

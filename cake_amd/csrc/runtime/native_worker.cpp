@@ -61,7 +61,11 @@ float half_to_f32(uint16_t h, bool bf16) {
 
 }  // namespace
 
-bool native_engine_available() { return access(engine_path().c_str(), R_OK) == 0; }
+// the engine library is built and this machine exposes an AMD GPU (the KFD device node:
+// checked without initialising the HIP runtime in the host process)
+bool native_engine_available() {
+  return access(engine_path().c_str(), R_OK) == 0 && access("/dev/kfd", R_OK | W_OK) == 0;
+}
 
 int run_native_worker(const NativeWorkerOpts& o, const TopoNode& node) {
   const std::string tag = o.log_tag;

@@ -21,7 +21,7 @@ struct NativeWorkerOpts {
 
 // Serve `node` until the server stops; the exit code (1 = engine failure, 2 = no layers).
 int run_native_worker(const NativeWorkerOpts& o, const TopoNode& node);
-// libcake_engine.so next to this library / executable exists
+// libcake_engine.so next to this library / executable exists and a GPU is present
 bool native_engine_available();
 
 }  // namespace cake

@@ -63,8 +63,8 @@ class DecodeBuffers:
         # fused attention + o_proj (attn_oproj.hip): per-group partial rows, row-block
         # arrival tickets (zeroed once, re-armed by the kernel)
         nkv = cfg.num_key_value_heads
-        self.ao_ws = torch.zeros(nkv * H, device=device, dtype=f32)
-        self.ao_tickets = torch.zeros(H // 32 + 2 * nkv + 2, device=device, dtype=i32)
+        self.ao_ws = torch.zeros(2 * nkv * H, device=device, dtype=f32)
+        self.ao_tickets = torch.zeros(2 * (H // 32) + 2 * nkv + 2, device=device, dtype=i32)
         self.pos = torch.zeros(1, device=device, dtype=i32) if pos is None else pos
         if with_head:
             self.logits = torch.zeros(cfg.vocab_size, device=device, dtype=f32)
@@ -230,8 +230,10 @@ class LayerStack:
                                "outputs of that launch are invalid")
 
     def attn_oproj_ok(self) -> bool:
-        """The fused decode attention + o_proj launch covers this stack's shapes."""
-        if self.backend != "hip" or os.environ.get("CAKE_ATTN_OPROJ", "1") == "0":
+        """The fused decode attention + o_proj launch is enabled (opt-in, CAKE_ATTN_OPROJ=1:
+        slower than the unfused pair on MI355X, profiles/r5_attn_oproj_ab.md) and covers
+        this stack's shapes."""
+        if self.backend != "hip" or os.environ.get("CAKE_ATTN_OPROJ", "0") != "1":
             return False
         from ...ops import hip as K
         c = self.cfg
@@ -267,7 +269,7 @@ class LayerStack:
                        self.inv_freq, bufs.pos, bufs.q, kc, vc)
             if fused:
                 K.attn_oproj(bufs.q, kc, vc, bufs.pos, self.scale, w.wo, bufs.resid, True,
-                             bufs.ao_ws, bufs.ao_tickets)
+                             bufs.ao_ws, bufs.ao_tickets, bufs.tickets)
             else:
                 K.attn_decode(bufs.q, kc, vc, bufs.pos, self.scale, bufs.part, bufs.tickets,
                               bufs.attn_out)
@@ -331,7 +333,7 @@ class LayerStack:
                    bufs.pos, bufs.q, kc, vc)
         if K.attn_oproj_short(pos0) and self.attn_oproj_ok():
             K.attn_oproj(bufs.q, kc, vc, bufs.pos, self.scale, w.wo, bufs.resid, True,
-                         bufs.ao_ws, bufs.ao_tickets)
+                         bufs.ao_ws, bufs.ao_tickets, bufs.tickets)
         else:
             K.attn_decode(bufs.q, kc, vc, bufs.pos, self.scale, bufs.part, bufs.tickets,
                           bufs.attn_out)

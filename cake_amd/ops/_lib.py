@@ -25,7 +25,7 @@ Z = C.c_size_t
 
 # name -> argtypes (all return int hipError_t)
 _SIGS = {
-    "cake_attn_oproj": [I, P, P, P, P, I, I, I, I, F, P, I, I, P, I, P, P, P],
+    "cake_attn_oproj": [I, P, P, P, P, I, I, I, I, F, P, I, I, P, I, P, P, P, P],
     "cake_attn_oproj_supported": [I, I, I, I],
     "cake_qkv_rope": [I, P, P, F, P, P, P, I, I, I, I, P, P, P, P, P, I, P],
     "cake_attn_set_prefetch": [I],

@@ -156,14 +156,17 @@ def attn_oproj_supported(nh: int, nkv: int, hd: int, H: int) -> bool:
 
 
 def attn_oproj_ws_sizes(nkv: int, H: int) -> tuple[int, int]:
-    """(f32 partial floats, int32 ticket words) of its workspace."""
-    return nkv * H, H // 32 + 2 * nkv + 2
+    """(f32 words of the {partial, tag} granules, int32 ticket / epoch words) of its
+    workspace."""
+    return 2 * nkv * H, 2 * (H // 32) + 2 * nkv + 2
 
 
-def attn_oproj(q, kcache, vcache, pos, scale, wo, out, accumulate: bool, ws, tickets):
+def attn_oproj(q, kcache, vcache, pos, scale, wo, out, accumulate: bool, ws, tickets,
+               err_tickets=None):
     """Decode attention + o_proj in ONE launch (short contexts: the attention runs as one
     split): out (+)= W_o . attention(q, K, V).  wo [H, nh*hd] (this rank's columns);
-    ws f32 [nkv * H], tickets int32 (:func:`attn_oproj_ws_sizes`, zeroed once)."""
+    ws f32, tickets int32 (:func:`attn_oproj_ws_sizes`, zeroed once); err_tickets: the
+    attention tickets whose error word [2 nkv] a partial poll that gave up sets."""
     nkv, S, hd = kcache.shape
     nh = q.numel() // hd
     H = wo.shape[0]
@@ -180,7 +183,9 @@ def attn_oproj(q, kcache, vcache, pos, scale, wo, out, accumulate: bool, ws, tic
         raise ValueError(f"attn_oproj: unsupported shape nh={nh} nkv={nkv} hd={hd} H={H}")
     check(kernels().cake_attn_oproj(_dt(kcache), _p(q), _p(kcache), _p(vcache), _p(pos), S, nh,
                                     nkv, hd, float(scale), _p(wo), nh * hd, H, _p(out),
-                                    int(bool(accumulate)), _p(ws), _p(tickets), _stream()),
+                                    int(bool(accumulate)), _p(ws), _p(tickets),
+                                    None if err_tickets is None else
+                                    err_tickets.data_ptr() + 4 * 2 * nkv, _stream()),
           "attn_oproj")
 
 

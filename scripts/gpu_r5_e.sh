@@ -11,7 +11,7 @@ run bench_ao1 300 python bench.py --steps 64 --warmup 8 --no-extras --no-sd
 grep '^{' $OUT/bench_ao1.log | cut -c1-330
 CAKE_ATTN_OPROJ=0 run bench_ao0 300 python bench.py --steps 64 --warmup 8 --no-extras --no-sd
 grep '^{' $OUT/bench_ao0.log | cut -c1-330
-run mt 900 python -u -m pytest tests/test_model_gpu.py tests/test_engine_gpu.py tests/test_sampling_gpu.py -x -q --timeout 300 --timeout-method thread
+timeout -k 10 900 python -u -m pytest tests/test_model_gpu.py tests/test_engine_gpu.py tests/test_sampling_gpu.py -q --timeout 300 --timeout-method thread > $OUT/mt.log 2>&1; echo "== mt rc=$?" # python -u -m pytest tests/test_model_gpu.py tests/test_engine_gpu.py tests/test_sampling_gpu.py -q --timeout 300 --timeout-method thread
 tail -3 $OUT/mt.log
 cd /tmp && export TMPDIR=/tmp
 ROOT="$GRAFT_REPO_ROOT"

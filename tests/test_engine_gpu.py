@@ -73,10 +73,13 @@ def test_native_engine_matches_python_decoder(cuda, ckpt):
     eng.close()
 
 
-def test_native_engine_f16_multistep_and_buckets(cuda, ckpt):
+@pytest.mark.parametrize("fused", ["0", "1"])
+def test_native_engine_f16_multistep_and_buckets(cuda, ckpt, fused, monkeypatch):
     """bf16 checkpoint converted to f16 on load, 4 steps per replay, and a live length
-    crossing the one-split (320 keys) and 512-key bucket edges."""
+    crossing the one-split (320 keys) and 512-key bucket edges; with and without the
+    opt-in fused attention + o_proj bucket (CAKE_ATTN_OPROJ=1, engine and Python alike)."""
     from cake_amd.engine import NativeLlama
+    monkeypatch.setenv("CAKE_ATTN_OPROJ", fused)
     g = torch.Generator().manual_seed(2)
     prompt = torch.randint(3, 2048, (500,), generator=g).tolist()
     n = 20

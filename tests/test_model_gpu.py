@@ -128,9 +128,10 @@ def test_device_decoder_crosses_split_buckets(cuda):
     first = dec.start(prompt)
     dec.capture()
     # caps up to the first covering every live length (core 2 at 16 splits: 8 and 16),
-    # below them the one-split bucket of fused QKV + attention launches (key 1)
-    assert sorted(dec.graphs) == K.attn_split_caps(4096)
-    assert sorted(dec.graphs)[:2] == [8, 16]
+    # below them the one-split bucket of fused attention + o_proj launches (key 1)
+    assert sorted(dec.graphs) == ([1] if model.stack.attn_oproj_ok() else []) + \
+        K.attn_split_caps(4096)
+    assert [c for c in sorted(dec.graphs) if c > 1][:2] == [8, 16]
     assert dec._graph_for(500) is dec.graphs[8] and dec._graph_for(600) is dec.graphs[16]
     assert K.attn_splits(4096) == (32 if K._ATTN_IMPL[0] == 1 else 16)
     st = run_decode(dec, 15)
@@ -138,9 +139,11 @@ def test_device_decoder_crosses_split_buckets(cuda):
 
 
 @pytest.mark.parametrize("k", [1, 4])
-def test_device_decoder_crosses_one_split_edge(cuda, k):
-    """Live lengths crossing the one-split edge (320 keys): the one-split attention graph
-    up to it, the split-K graph (cap 8) after it — tokens equal the host loop."""
+def test_device_decoder_crosses_one_split_edge(cuda, k, monkeypatch):
+    """Live lengths crossing the one-split edge (320 keys): the one-split graph of fused
+    attention + o_proj launches (opt-in, CAKE_ATTN_OPROJ=1) up to it, the split-K graph
+    (cap 8) after it — tokens equal the host loop."""
+    monkeypatch.setenv("CAKE_ATTN_OPROJ", "1")
     from cake_amd.models.llama3.decode_loop import run_decode
     from cake_amd.models.llama3.model import DeviceDecoder
     from cake_amd.ops import reference as R
