@@ -30,6 +30,10 @@ _SIGS = {
     "cake_hop_send": [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p],
     "cake_hop_recv": [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
                       C.c_double, C.c_void_p],
+    "cake_bulk_send": [C.POINTER(C.c_void_p), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                       C.c_int, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p],
+    "cake_bulk_recv": [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_double,
+                       C.c_void_p],
 }
 _bound = False
 
@@ -126,3 +130,75 @@ def recv(inbox: Inbox, msg: torch.Tensor, H: int, nhdr: int, bf16: bool, seq: to
                                C.c_void_p(err.data_ptr()),
                                float(timeout_s or hop_timeout_s()), C.c_void_p(_stream())),
           "hop_recv")
+
+
+# ---------------------------------------------------------------------------
+# bulk hops: multi-megabyte messages (hop.hip bulk_send_kernel / bulk_recv_kernel)
+
+BULK_MAX_SEGMENTS = 32
+
+
+def _align16(n: int) -> int:
+    return (int(n) + 15) // 16 * 16
+
+
+class BulkInbox:
+    """Receiving end of a bulk channel on this rank's GPU: `nbytes` of message in
+    uncached device memory (+ one flag line), exported to the sender by IPC, and the
+    receive-side sequence / error words."""
+
+    def __init__(self, nbytes: int, device):
+        self.nbytes = _align16(nbytes)
+        self.box = Inbox((self.nbytes + 64) // 8)
+        z = lambda: torch.zeros(1, dtype=torch.int32, device=device)  # noqa: E731
+        self.seq, self.err = z(), z()
+
+    def handle(self) -> bytes:
+        return self.box.handle()
+
+    def recv(self, dst: torch.Tensor, timeout_s: float | None = None) -> None:
+        """Wait (on the device) for the next message and copy it into dst (a contiguous
+        device buffer of at least nbytes)."""
+        if not dst.is_cuda or not dst.is_contiguous() or \
+                dst.numel() * dst.element_size() < self.nbytes or dst.data_ptr() % 16:
+            raise ValueError("bulk recv: dst must be a 16-byte aligned contiguous device "
+                             f"buffer of >= {self.nbytes} bytes")
+        check(_lib().cake_bulk_recv(C.c_void_p(self.box.ptr), self.nbytes,
+                                    C.c_void_p(dst.data_ptr()), C.c_void_p(self.seq.data_ptr()),
+                                    C.c_void_p(self.err.data_ptr()),
+                                    float(timeout_s or hop_timeout_s()), C.c_void_p(_stream())),
+              "bulk_recv")
+
+    def error(self) -> bool:
+        return bool(int(self.err.item()))
+
+    def close(self) -> None:
+        self.box.close()
+
+
+class BulkPeer:
+    """Sending end of a bulk channel: the receiver's inbox mapped here, and the
+    send-side sequence / arrival counter words."""
+
+    def __init__(self, handle: bytes, nbytes: int, device):
+        self.nbytes = _align16(nbytes)
+        self.peer = PeerInbox(handle)
+        z = lambda: torch.zeros(1, dtype=torch.int32, device=device)  # noqa: E731
+        self.seq, self.count = z(), z()
+
+    def send(self, tensors: list, offsets: list[int]) -> None:
+        """Store each tensor's bytes (dense, 16-byte multiples) at its offset of the
+        peer's inbox, then raise the message flag (async, graph-capturable)."""
+        n = len(tensors)
+        if not 1 <= n <= BULK_MAX_SEGMENTS or len(offsets) != n:
+            raise ValueError(f"bulk send: 1..{BULK_MAX_SEGMENTS} segments")
+        ptrs = (C.c_void_p * n)(*[t.data_ptr() for t in tensors])
+        sizes = (C.c_uint64 * n)(*[t.numel() * t.element_size() for t in tensors])
+        offs = (C.c_uint64 * n)(*[int(o) for o in offsets])
+        check(_lib().cake_bulk_send(ptrs, sizes, offs, n, C.c_void_p(self.peer.ptr), self.nbytes,
+                                    C.c_void_p(self.seq.data_ptr()),
+                                    C.c_void_p(self.count.data_ptr()), C.c_void_p(_stream())),
+              "bulk_send")
+
+    def close(self) -> None:
+        self.peer.close()
