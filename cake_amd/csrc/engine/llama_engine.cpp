@@ -309,6 +309,11 @@ std::vector<std::pair<int, int>> shard_layers(const Cfg& c, int world) {
     out.push_back({0, c.L});
     return out;
   }
+  if (world > c.L) {  // one layer per rank, the ranks past the last layer idle
+    for (int r = 0; r < world; ++r) out.push_back(r < c.L ? std::make_pair(r, r + 1)
+                                                          : std::make_pair(c.L, c.L));
+    return out;
+  }
   const double layer_bytes = 2.0 * ((double)c.H * (c.nh + 2 * c.nkv) * c.hd +
                                     (double)c.nh * c.hd * c.H + 3.0 * c.H * c.I + 2.0 * c.H);
   const double head = 2.0 * (double)c.V * c.H / layer_bytes;
@@ -414,8 +419,6 @@ class Llama {
     S_ = o.max_seq > 0 ? o.max_seq : 4096;
     k_ = std::max(1, o.steps_per_graph);
     if (cfg_.H % 8 || cfg_.hd % 2 || cfg_.nh % cfg_.nkv) throw Error("unsupported model shape");
-    const bool placed = pp && pp->owners && pp->n_owners > 0;
-    if (world_ > cfg_.L && !placed) throw Error("more pipeline ranks than layers");
     // this rank's compute shapes: the whole model, or its tensor-parallel slice
     lc_ = cfg_;
     if (tp_ > 1) {
@@ -440,6 +443,7 @@ class Llama {
       head_ = false;
     } else {
       // layer -> rank: the topology's owner map, or contiguous shards
+      const bool placed = pp && pp->owners && pp->n_owners > 0;
       owner_.assign(cfg_.L, 0);
       if (placed) {
         if (pp->n_owners != cfg_.L)
