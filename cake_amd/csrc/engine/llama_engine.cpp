@@ -484,7 +484,13 @@ class Llama {
     planner_.load(pkg_dir() + "/ops/gemm_tuned.json");
     load_weights(dir);
     alloc_state();
-    trace(rank(), "weights + state ready (" + std::to_string(owned_.size()) + " layers)");
+    {
+      size_t fr = 0, tot = 0;
+      (void)hipMemGetInfo(&fr, &tot);
+      trace(rank(), "weights + state ready (" + std::to_string(owned_.size()) + " layers), " +
+                        std::to_string(fr >> 20) + " of " + std::to_string(tot >> 20) +
+                        " MiB free");
+    }
     if (world_ > 1) {
       connect_pipeline(pp->master_addr ? pp->master_addr : "127.0.0.1:29517",
                        pp->connect_timeout_s > 0 ? pp->connect_timeout_s : 600.0);
@@ -496,7 +502,9 @@ class Llama {
     if (tp_ > 1) {
       connect_tp(tp->master_addr ? tp->master_addr : "127.0.0.1:29517",
                  tp->connect_timeout_s > 0 ? tp->connect_timeout_s : 600.0);
+      trace(rank(), "tensor-parallel channels mapped");
       selftest_tp();
+      trace(rank(), "tensor-parallel self-test passed");
     }
     if (!remotes_.empty()) connect_remotes();
   }
@@ -842,6 +850,11 @@ class Llama {
   };
 
   int tp_ = 1, tp_rank_ = 0, i0_ = 0, voff_ = 0, slab_bank_ = 0;
+  // rows of one prefill all-reduce round: the slab (2 banks x tp slots x rows x H f32,
+  // uncached, IPC-mapped by every peer) is sized for this many rows, a longer prefill
+  // runs in rounds — a slab sized for max_seq (2 GB per rank at 70B tp8, 4096 keys) made
+  // the eight peer imports stall on one shared GPU
+  static constexpr int kSlabRows = 512;
   Cfg lc_;                   // this rank's compute shapes (the whole model unless TP)
   ArChan ch_sum_, ch_key_, ch_gat_;
   float *partial_ = nullptr, *ppart_ = nullptr, *full_logits_ = nullptr, *slab_ = nullptr;
@@ -2053,19 +2066,29 @@ class Llama {
   // IPC-mapped), a barrier, then each sums the W slots; two slab banks, alternating, so
   // the next all-reduce never overwrites rows a slower rank still sums
   void dense_allreduce(int T) {
-    const size_t SH = (size_t)S_ * cfg_.H, bytes = sizeof(float) * (size_t)T * cfg_.H;
-    const int bank = slab_bank_;
-    slab_bank_ ^= 1;
-    for (int p = 0; p < tp_; ++p) {
-      float* base = p == tp_rank_ ? slab_ : static_cast<float*>(peer_slab_[p]);
-      hip_check(hipMemcpyAsync(base + ((size_t)bank * tp_ + tp_rank_) * SH, ppart_, bytes,
-                               hipMemcpyDeviceToDevice, st_), "slab copy");
+    const int R = slab_rows();
+    const size_t SH = (size_t)R * cfg_.H;
+    // rounds of R rows; the two banks alternate, so a peer's copies of round k + 1 never
+    // land in the bank its sum of round k reads (each rank syncs its stream, sum
+    // included, before the barrier that releases the next round's copies)
+    for (int c0 = 0; c0 < T; c0 += R) {
+      const int rows = std::min(R, T - c0);
+      const size_t off = (size_t)c0 * cfg_.H, bytes = sizeof(float) * (size_t)rows * cfg_.H;
+      const int bank = slab_bank_;
+      slab_bank_ ^= 1;
+      for (int p = 0; p < tp_; ++p) {
+        float* base = p == tp_rank_ ? slab_ : static_cast<float*>(peer_slab_[p]);
+        hip_check(hipMemcpyAsync(base + ((size_t)bank * tp_ + tp_rank_) * SH, ppart_ + off, bytes,
+                                 hipMemcpyDeviceToDevice, st_), "slab copy");
+      }
+      hip_check(hipStreamSynchronize(st_), "sync");
+      tp_barrier();
+      k_check(cake_sum_slices(hidden_ + off, slab_ + (size_t)bank * tp_ * SH, tp_, (long long)SH,
+                              (long long)rows * cfg_.H, 1, st_), "sum_slices");
     }
-    hip_check(hipStreamSynchronize(st_), "sync");
-    tp_barrier();
-    k_check(cake_sum_slices(hidden_, slab_ + (size_t)bank * tp_ * SH, tp_, (long long)SH,
-                            (long long)T * cfg_.H, 1, st_), "sum_slices");
   }
+
+  int slab_rows() const { return std::min(S_, kSlabRows); }
 
   // host barrier of the tensor-parallel ranks over the control sockets (star on rank 0)
   void tp_barrier() {
@@ -2183,6 +2206,7 @@ class Llama {
     hip_check(hipMemcpyAsync(got.data(), scratch_resid_, sizeof(float) * H, hipMemcpyDeviceToHost,
                              st_), "selftest D2H");
     hip_check(hipStreamSynchronize(st_), "sync");
+    trace(rank(), "self-test: sum channel done");
     for (int i = 0; i < H; ++i)
       if (got[i] != tri * (float)((i % 17) - 8)) { fail("sum all-reduce delivered wrong words"); break; }
     // (2) argmax-key max channel
@@ -2195,6 +2219,7 @@ class Llama {
     hip_check(hipStreamSynchronize(st_), "sync");
     if (mx != (((unsigned long long)(100 + W - 1) << 32) | (unsigned)(W - 1)))
       fail("argmax-key all-reduce returned a wrong key");
+    trace(rank(), "self-test: key channel done");
     hip_check(hipMemsetAsync(slot_, 0, sizeof(unsigned long long), st_), "memset");
     // (3) vocabulary gather channel
     std::vector<float> shard(lc_.V);
@@ -2210,6 +2235,7 @@ class Llama {
     hip_check(hipStreamSynchronize(st_), "sync");
     for (int j = 0; j < cfg_.V; ++j)
       if (full[j] != (float)j) { fail("vocabulary gather delivered wrong words"); break; }
+    trace(rank(), "self-test: gather channel done");
     // (4) prefill slab all-reduce (one row)
     hip_check(hipMemcpyAsync(ppart_, pat.data(), sizeof(float) * H, hipMemcpyHostToDevice, st_),
               "H2D");
@@ -2259,11 +2285,13 @@ class Llama {
     ch_sum_.inbox = alloc((size_t)cake_ar_inbox_words(tp_, cfg_.H));
     ch_key_.inbox = alloc((size_t)cake_ar_inbox_words(tp_, 2));
     ch_gat_.inbox = alloc(2 * (size_t)cfg_.V);
-    const size_t slab_bytes = sizeof(float) * 2 * (size_t)tp_ * S_ * cfg_.H;
+    const size_t slab_bytes = sizeof(float) * 2 * (size_t)tp_ * slab_rows() * cfg_.H;
     void* sp = nullptr;
     hip_check(hipExtMallocWithFlags(&sp, slab_bytes, hipDeviceMallocUncached), "slab alloc");
     tp_owned_.push_back(sp);
     slab_ = static_cast<float*>(sp);
+    trace(rank(), "tensor-parallel inboxes + slab allocated (" +
+                      std::to_string(slab_bytes >> 20) + " MiB slab)");
     void* mine[4] = {ch_sum_.inbox, ch_key_.inbox, ch_gat_.inbox, slab_};
     Json me = Json::array();
     for (void* p : mine) {
@@ -2317,6 +2345,7 @@ class Llama {
       const Json m = recv_json(ctl_fd_);
       for (int r = 0; r < tp_; ++r) table[r] = m.get("table").at(r);
     }
+    trace(rank(), "tensor-parallel handle table exchanged");
     ArChan* chans[3] = {&ch_sum_, &ch_key_, &ch_gat_};
     for (auto* ch : chans) ch->peers.assign(tp_, nullptr);
     peer_slab_.assign(tp_, nullptr);
