@@ -165,21 +165,25 @@ ENGINE_LIB = LIB / "libcake_engine.so"
 
 
 def build_engine(force: bool = False) -> Path:
-    """Native Llama engine (csrc/engine): host C++ on the HIP runtime over the kernel
-    library's C entry points, plus the runtime's JSON / safetensors readers."""
-    eng = CSRC / "engine" / "llama_engine.cpp"
+    """Native engines (csrc/engine: Llama, Stable Diffusion): host C++ on the HIP runtime
+    over the kernel library's C entry points, plus the runtime's JSON / safetensors
+    readers."""
     rt = CSRC / "runtime"
     objs = [_compile_cpp(rt / f"{n}.cpp", force) for n in ("json", "safetensors", "net", "proto")]
-    out = BUILD / "engine" / "llama_engine.o"
-    out.parent.mkdir(parents=True, exist_ok=True)
     deps = [*sorted((CSRC / "engine").glob("*.h")), *sorted(rt.glob("*.h")),
             CSRC / "driver" / "graph_loop.h"]
-    if force or _newer(eng, deps, out):
-        _run([HIPCC, "-O2", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-Wall",
-              "-Wno-unused-function", "-c", str(eng), "-o", str(out)])
-    if force or any(_newer(o, [], ENGINE_LIB) for o in [out, *objs, KERNEL_LIB]):
-        _run([HIPCC, "-shared", "-fPIC", str(out), *map(str, objs), "-o", str(ENGINE_LIB),
-              f"-L{LIB}", "-lcake_kernels", "-Wl,-rpath,$ORIGIN", "-Wl,--no-undefined"])
+    eng_objs = []
+    for src in sorted((CSRC / "engine").glob("*.cpp")):  # llama_engine, sd_engine
+        out = BUILD / "engine" / (src.stem + ".o")
+        out.parent.mkdir(parents=True, exist_ok=True)
+        if force or _newer(src, deps, out):
+            _run([HIPCC, "-O2", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-Wall",
+                  "-Wno-unused-function", "-c", str(src), "-o", str(out)])
+        eng_objs.append(out)
+    if force or any(_newer(o, [], ENGINE_LIB) for o in [*eng_objs, *objs, KERNEL_LIB]):
+        _run([HIPCC, "-shared", "-fPIC", *map(str, eng_objs), *map(str, objs), "-o",
+              str(ENGINE_LIB), f"-L{LIB}", "-lcake_kernels", "-Wl,-rpath,$ORIGIN",
+              "-Wl,--no-undefined"])
     return ENGINE_LIB
 
 

@@ -1,0 +1,117 @@
+// Host helpers shared by the native engines (llama_engine.cpp, sd_engine.cpp): HIP error
+// checks, the package directory, file reads and the GEMM tile planner (ops/gemm.py plan()).
+#pragma once
+
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <fstream>
+#include <sstream>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../runtime/json.h"
+
+namespace cake {
+
+struct Error : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+inline void hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw Error(std::string(what) + ": " + hipGetErrorString(e));
+}
+inline void k_check(int rc, const char* what) {
+  if (rc != 0) throw Error(std::string(what) + ": " + hipGetErrorString((hipError_t)rc));
+}
+
+// <root>/cake_amd/lib/libcake_engine.so -> <root>/cake_amd
+inline std::string pkg_dir() {
+  Dl_info info{};
+  if (dladdr(reinterpret_cast<void*>(&pkg_dir), &info) && info.dli_fname) {
+    char buf[4096];
+    const char* p = realpath(info.dli_fname, buf);
+    std::string s = p ? p : info.dli_fname;
+    for (int i = 0; i < 2; ++i) {
+      const auto cut = s.find_last_of('/');
+      if (cut == std::string::npos) return ".";
+      s = s.substr(0, cut);
+    }
+    return s;
+  }
+  return ".";
+}
+
+inline std::string read_file(const std::string& path) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f) throw Error("cannot read " + path);
+  std::stringstream ss;
+  ss << f.rdbuf();
+  return ss.str();
+}
+
+// ---------------------------------------------------------------------------
+// GEMM tile plan (ops/gemm.py plan(): measured table, else the cost model)
+// ---------------------------------------------------------------------------
+struct GemmPlanner {
+  struct Tuned { long long M, Nv, K; std::string epi; int cfg, splits; };
+  std::vector<Tuned> tuned;
+
+  void load(const std::string& path) {
+    std::ifstream f(path);
+    if (!f) return;
+    try {
+      const Json j = Json::parse(read_file(path));
+      static const int known[] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 11, 12, 13, 14, 15, 16, 17, 18, 19};
+      for (const auto& e : j.get("entries").items()) {
+        const int cfg = (int)e.get("cfg").as_int();
+        if (std::find(std::begin(known), std::end(known), cfg) == std::end(known)) continue;
+        tuned.push_back({e.get("M").as_int(), e.get("Nv").as_int(), e.get("K").as_int(),
+                         e.get("epi").as_string(), cfg, (int)e.get("splits").as_int()});
+      }
+    } catch (const std::exception&) {
+      tuned.clear();  // a malformed table only loses the measured overrides
+    }
+  }
+
+  std::pair<int, int> plan(long long M, long long Nv, long long K, const std::string& epi) const {
+    const Tuned* near = nullptr;
+    double near_r = 0;
+    for (const auto& e : tuned) {
+      if (e.Nv != Nv || e.K != K || e.epi != epi) continue;
+      if (e.M == M) return {e.cfg, e.splits};
+      const double r = (double)std::max(M, e.M) / (double)std::min(M, e.M);
+      if (r <= 2 && (!near || r < near_r)) { near = &e; near_r = r; }
+    }
+    if (near) return {near->cfg, 1};
+    struct T { int cfg, bm, bn, slots; double eff; };
+    static const T tiles[] = {{0, 128, 128, 2, 1.0}, {1, 64, 128, 2, 0.8}, {4, 64, 64, 4, 0.7},
+                              {5, 256, 256, 1, 1.2}};
+    static const int small_c[] = {1, 4, 0}, big_c[] = {0, 1, 4, 5};
+    const int* cands = M <= 64 ? small_c : big_c;
+    const int nc = M <= 64 ? 3 : 4;
+    const long long ksteps = (K + 63) / 64;
+    double best = -1;
+    std::pair<int, int> out{0, 1};
+    for (int c = 0; c < nc; ++c) {
+      const T* t = nullptr;
+      for (const auto& x : tiles)
+        if (x.cfg == cands[c]) t = &x;
+      const long long tiles_n = ((M + t->bm - 1) / t->bm) * ((Nv + t->bn - 1) / t->bn);
+      for (int splits : {1, 2, 4, 8, 16}) {
+        if (splits > 1 && (ksteps / splits < 4 || tiles_n * splits > 2LL * 256 * t->slots)) continue;
+        const long long waves = (tiles_n * splits + 256LL * t->slots - 1) / (256LL * t->slots);
+        double cost = (double)waves * t->slots * t->bm * t->bn * (double)((ksteps + splits - 1) / splits) / t->eff;
+        if (splits > 1) cost += (double)M * Nv * splits * 0.1;
+        if (best < 0 || cost < best) { best = cost; out = {t->cfg, splits}; }
+      }
+    }
+    return out;
+  }
+};
+
+}  // namespace cake

@@ -1,0 +1,87 @@
+// Native Stable Diffusion engine (libcake_engine.so): the whole image generation —
+// text encoders, the classifier-free-guided denoising loop with its scheduler, the VAE
+// decode — as host C++ over the gfx950 kernels' C entry points, with no interpreter.
+//
+// What it replaces: the reference's native SD pipeline (cake-core/src/models/sd/sd.rs:
+// 320-532 generate_image, unet.rs:43-100, vae.rs:55-108, clip.rs:24-75 over candle) and
+// this repo's Python host loop (models/sd/pipeline.py, unet.py, vae.py, clip.py), whose
+// kernels and launch order it reproduces.  Tokenization stays with the caller (the HF
+// tokenizers library, as for the native Llama engine): the engine takes padded CLIP ids.
+//
+// Device path per generation:
+//   * text: CLIP-L (and OpenCLIP-bigG for xl / turbo) over the [uncond; cond] ids ->
+//     the [2, 77, D] context (both encoders concatenated on the feature axis);
+//     every cross-attention's k|v projection of it computed once into persistent buffers;
+//   * denoise: the first step eagerly (convolution autotuning, GEMM plans), every later
+//     step ONE hipGraph replay: time embedding from the device timestep table -> UNet
+//     (NHWC, fused epilogues) -> CFG combine + scheduler update + next input
+//     (sched_step) -> step += 1;
+//   * decode: latents / vae_scale -> VAE decoder -> RGB8 on the device.
+#pragma once
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct CakeSdOpts {
+  const char* version;   // "v1-5" | "v2-1" | "xl" | "turbo" (null: cake_sd.json / "v1-5")
+  int32_t width;         // 0: the version's default
+  int32_t height;
+  int32_t dtype;         // 0 bf16, 1 f16
+  int32_t device;
+  int32_t init;          // 1: seeded random weights (no component file is read)
+  int32_t autotune;      // 1: time the convolution variants on the first step (else planner)
+  int32_t tiny;          // 1: the small test architecture (models/sd/config.py tiny_config)
+  uint64_t seed;         // random-init seed
+  // component files (null: resolved under the model directory, weights.py COMPONENT_FILES)
+  const char* unet_path;
+  const char* vae_path;
+  const char* clip_path;
+  const char* clip2_path;
+} CakeSdOpts;
+
+typedef struct CakeSdGenArgs {
+  const int32_t* cond;      // [77] ids of the first tokenizer
+  const int32_t* uncond;    // [77] or null: no classifier-free guidance
+  const int32_t* cond2;     // [77] ids of the second tokenizer (xl / turbo)
+  const int32_t* uncond2;
+  int32_t n_steps;
+  float guidance;
+  uint64_t seed;            // the ancestral-noise key (sched_step), and the latent noise
+                            // when init_noise is null
+  const float* init_noise;  // optional [4 * (h/8) * (w/8)] standard-normal latent noise
+  int32_t use_graph;        // 1: every step after the first is one hipGraph replay
+} CakeSdGenArgs;
+
+typedef struct CakeSdResult {
+  int32_t width, height, n_steps;
+  double text_s, denoise_s, vae_s;
+} CakeSdResult;
+
+// Open (load or random-init) every component; null + err on failure.
+void* cake_sd_open(const char* model_dir, const CakeSdOpts* opts, char* err, int32_t errlen);
+// One image: rgb [height * width * 3] u8; latents_out (optional) [4 * h/8 * w/8] f32 (the
+// final latents); step_s (optional) [n_steps] seconds per step (device time).
+int32_t cake_sd_generate(void* engine, const CakeSdGenArgs* args, uint8_t* rgb,
+                         float* latents_out, double* step_s, CakeSdResult* result, char* err,
+                         int32_t errlen);
+void cake_sd_close(void* engine);
+// (width, height, context dim, model dtype, text dim 1, text dim 2 or 0) of an open engine
+void cake_sd_info(void* engine, int32_t* out6);
+
+// Component entry points (tests / parity checks; f32 host tensors in and out):
+// which = 0 CLIP (first encoder), 1 the second encoder; ids [B, 77] -> out [B, 77, D].
+int32_t cake_sd_text(void* engine, int32_t which, const int32_t* ids, int32_t B, float* out,
+                     char* err, int32_t errlen);
+// One eager UNet forward: sample [B, 4, h, w] (NCHW), timestep t, context [B, 77, Dctx]
+// -> out [B, 4, h, w].
+int32_t cake_sd_unet(void* engine, const float* sample, int32_t B, float t, const float* ctx,
+                     float* out, char* err, int32_t errlen);
+// VAE decode of z [1, 4, h, w] (already divided by vae_scale) -> image [1, 3, H, W] in [-1, 1].
+int32_t cake_sd_vae_decode(void* engine, const float* z, float* img, char* err, int32_t errlen);
+
+#ifdef __cplusplus
+}
+#endif

@@ -121,6 +121,32 @@ __global__ void to_rgb8_kernel(const uint16_t* __restrict__ img, int B, int H, i
   }
 }
 
+// CLIP text embedding: out[r, :] = tok[ids[r]] + pos[r % T] (the reference's token +
+// position embedding sum, clip.rs; one rounding of the f32 sum, as torch's 16-bit add)
+template <int DT>
+__global__ __launch_bounds__(256) void clip_embed_kernel(const uint16_t* __restrict__ tok,
+                                                         const uint16_t* __restrict__ pos,
+                                                         const int* __restrict__ ids, int rows,
+                                                         int T, int D, int V,
+                                                         uint16_t* __restrict__ out) {
+  const long long n = (long long)rows * D;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const int r = (int)(i / D), d = (int)(i - (long long)r * D);
+    int id = ids[r];
+    id = id < 0 ? 0 : (id >= V ? V - 1 : id);
+    const float v = to_f32<DT>(tok[(size_t)id * D + d]) + to_f32<DT>(pos[(size_t)(r % T) * D + d]);
+    out[i] = from_f32<DT>(v);
+  }
+}
+
+// 16-bit -> f32 (host read-back of component outputs)
+template <int DT>
+__global__ __launch_bounds__(256) void widen_kernel(const uint16_t* __restrict__ x, long long n,
+                                                    float* __restrict__ y) {
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
+    y[i] = to_f32<DT>(x[i]);
+}
+
 static inline int grid_for_n(long long n) {
   long long g = (n + 255) / 256;
   return (int)(g > 4096 ? 4096 : (g < 1 ? 1 : g));
@@ -190,6 +216,33 @@ CAKE_API int cake_to_rgb8(int dt, const void* img, int B, int H, int W, int nhwc
   else if (dt == kF16)
     hipLaunchKernelGGL((to_rgb8_kernel<kF16>), dim3(g), dim3(256), 0, st, (const uint16_t*)img,
                        B, H, W, nhwc, (uint8_t*)out);
+  else return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}
+
+CAKE_API int cake_clip_embed(int dt, const void* tok, const void* pos, const int* ids, int rows,
+                             int T, int D, int V, void* out, hipStream_t st) {
+  if (rows <= 0 || T <= 0 || D <= 0 || V <= 0) return (int)hipErrorInvalidValue;
+  const int g = grid_for_n((long long)rows * D);
+  if (dt == kBF16)
+    hipLaunchKernelGGL((clip_embed_kernel<kBF16>), dim3(g), dim3(256), 0, st,
+                       (const uint16_t*)tok, (const uint16_t*)pos, ids, rows, T, D, V,
+                       (uint16_t*)out);
+  else if (dt == kF16)
+    hipLaunchKernelGGL((clip_embed_kernel<kF16>), dim3(g), dim3(256), 0, st,
+                       (const uint16_t*)tok, (const uint16_t*)pos, ids, rows, T, D, V,
+                       (uint16_t*)out);
+  else return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}
+
+CAKE_API int cake_widen16(int dt, const void* x, long long n, float* y, hipStream_t st) {
+  if (n <= 0) return (int)hipErrorInvalidValue;
+  const int g = grid_for_n(n);
+  if (dt == kBF16)
+    hipLaunchKernelGGL((widen_kernel<kBF16>), dim3(g), dim3(256), 0, st, (const uint16_t*)x, n, y);
+  else if (dt == kF16)
+    hipLaunchKernelGGL((widen_kernel<kF16>), dim3(g), dim3(256), 0, st, (const uint16_t*)x, n, y);
   else return (int)hipErrorInvalidValue;
   return (int)hipGetLastError();
 }

@@ -155,3 +155,29 @@ def tiny_config(version: str = "v1-5") -> SDConfig:
     return SDConfig(version, 64, 64, unet, vae, clip, clip2, scheduler=base.scheduler,
                     vae_scale=base.vae_scale, default_guidance=base.default_guidance,
                     default_steps=base.default_steps)
+
+
+def mini_config(version: str = "v1-5") -> SDConfig:
+    """A small SD whose every shape takes the HIP kernel paths (channel counts multiples
+    of 64, GroupNorm groups of >= 4 channels; tiny_config's 32-channel convolutions fall
+    back to the library there): the native engine's parity tests
+    (csrc/engine/sd_engine.cpp reads the same architecture from cake_sd.json)."""
+    if version in ("xl", "turbo"):
+        unet = UNetConfig([UNetBlock(64, False, 2), UNetBlock(128, True, 2, 2)],
+                          cross_attention_dim=128, use_linear_projection=True, norm_num_groups=16)
+        clip = ClipConfig(vocab_size=512, embed_dim=64, intermediate_size=128, num_hidden_layers=2,
+                          num_attention_heads=2)
+        clip2 = ClipConfig(vocab_size=512, embed_dim=64, intermediate_size=128, num_hidden_layers=2,
+                           num_attention_heads=2, activation="gelu", pad_with="!")
+    else:
+        unet = UNetConfig([UNetBlock(64, True, 2), UNetBlock(128, True, 2),
+                           UNetBlock(128, False, 2)], cross_attention_dim=64, norm_num_groups=16,
+                          use_linear_projection=version == "v2-1")
+        clip = ClipConfig(vocab_size=512, embed_dim=64, intermediate_size=128, num_hidden_layers=2,
+                          num_attention_heads=2)
+        clip2 = None
+    vae = VAEConfig(block_out_channels=(64, 64, 128, 128), layers_per_block=1, norm_num_groups=16)
+    base = get_config(version)
+    return SDConfig(version, 64, 64, unet, vae, clip, clip2, scheduler=base.scheduler,
+                    vae_scale=base.vae_scale, default_guidance=base.default_guidance,
+                    default_steps=base.default_steps)

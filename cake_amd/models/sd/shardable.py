@@ -17,7 +17,7 @@ from pathlib import Path
 import torch
 
 from .clip import ClipTextTransformer
-from .config import SDConfig, get_config, tiny_config
+from .config import SDConfig, get_config, mini_config, tiny_config
 from .unet import UNet2DConditionModel
 from .util import pack_tensors, unpack_tensors
 from .vae import AutoencoderKL
@@ -30,9 +30,9 @@ SD_COMPONENTS = ("clip", "clip2", "vae", "unet")
 def sd_config_for(ctx) -> SDConfig:
     a = ctx.args
     meta = Path(ctx.model_path) / "cake_sd.json"
-    tiny = meta.exists() and json.loads(meta.read_text()).get("tiny", False)
-    if tiny:
-        cfg = tiny_config(a.sd_version)
+    info = json.loads(meta.read_text()) if meta.exists() else {}
+    if info.get("tiny", False) or info.get("mini", False):
+        cfg = (mini_config if info.get("mini", False) else tiny_config)(a.sd_version)
         if a.sd_height:
             cfg.height = a.sd_height
         if a.sd_width:

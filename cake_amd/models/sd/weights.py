@@ -194,7 +194,7 @@ def write_clip_tokenizer(path: Path, vocab_size: int) -> None:
 
 
 def write_sd_checkpoint(out_dir, cfg: SDConfig, dtype=torch.float16, seed: int = 0,
-                        tiny: bool = False) -> Path:
+                        tiny: bool = False, mini: bool = False) -> Path:
     out = Path(out_dir)
     suffix = ".fp16" if dtype == torch.float16 else ""
     names = ["unet", "vae", "clip"] + (["clip2"] if cfg.clip2 else [])
@@ -207,22 +207,25 @@ def write_sd_checkpoint(out_dir, cfg: SDConfig, dtype=torch.float16, seed: int =
     if cfg.clip2:
         write_clip_tokenizer(out / "tokenizer_2" / "tokenizer.json", cfg.clip2.vocab_size)
     (out / "cake_sd.json").write_text(json.dumps({"version": cfg.version, "synthetic": True,
-                                                     "tiny": tiny}))
+                                                     "tiny": tiny, "mini": mini}))
     return out
 
 
 def main(argv=None) -> int:
     import argparse
 
-    from .config import get_config, tiny_config
+    from .config import get_config, mini_config, tiny_config
     ap = argparse.ArgumentParser(description="write a random-init SD checkpoint (diffusers layout)")
     ap.add_argument("--version", default="v1-5", choices=["v1-5", "v2-1", "xl", "turbo"])
     ap.add_argument("--tiny", action="store_true")
+    ap.add_argument("--mini", action="store_true", help="the small all-HIP-shapes architecture")
     ap.add_argument("--out", required=True)
     ap.add_argument("--f32", action="store_true")
     a = ap.parse_args(argv)
-    cfg = tiny_config(a.version) if a.tiny else get_config(a.version)
-    write_sd_checkpoint(a.out, cfg, torch.float32 if a.f32 else torch.float16, tiny=a.tiny)
+    cfg = (mini_config(a.version) if a.mini else tiny_config(a.version) if a.tiny
+           else get_config(a.version))
+    write_sd_checkpoint(a.out, cfg, torch.float32 if a.f32 else torch.float16, tiny=a.tiny,
+                        mini=a.mini)
     print(a.out)
     return 0
 
