@@ -294,8 +294,10 @@ def bench_single(a) -> None:
         # CFG batch 2, the UNet + scheduler step as one graph replay)
         if not a.no_sd and _want(a, "sd"):
             try:
-                from cake_amd.models.sd.bench import measure_denoise
-                extra["sd"] = {"sdxl_1024": measure_denoise("xl", 8)}
+                from cake_amd.models.sd.bench import measure_denoise, measure_native
+                # native engine (the product path) unless --engine python
+                extra["sd"] = {"sdxl_1024": measure_native("xl", 8) if _native(a)
+                               else measure_denoise("xl", 8)}
             except Exception as e:  # noqa: BLE001
                 extra["sd"] = {"sdxl_1024": None, "error": f"{type(e).__name__}: {e}"[:300]}
     _emit(a, r["tokens_per_sec"], r["ms_per_step"], r["p50_token_latency_ms"],

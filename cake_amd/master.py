@@ -31,8 +31,7 @@ class Master:
             if ctx.model_type == "text-model":
                 self.llm = _load_text(ctx)
             else:
-                from .models.sd.pipeline import SDGenerator
-                self.sd = SDGenerator.load(ctx)
+                self.sd = _load_image(ctx)
         log.info("model loaded - mem=%.1f MiB", rss_mib())
 
     def run(self) -> None:
@@ -146,3 +145,19 @@ def _load_text(ctx):
         return NativeLLM.load(ctx)
     from .models.llama3.generator import LLamaGenerator
     return LLamaGenerator.load(ctx)
+
+
+def _load_image(ctx):
+    """The native SD engine when every component is local on a GPU (csrc/engine/
+    sd_engine.cpp), else the Python pipeline (also when the engine refuses the model,
+    e.g. the tiny test architecture's 32-channel convolutions)."""
+    from .models.sd.native_generator import NativeSDGenerator, native_sd_eligible
+    from .models.sd.pipeline import SDGenerator
+    if native_sd_eligible(ctx):
+        try:
+            gen = NativeSDGenerator.load(ctx)
+            log.info("image generation on the native SD engine")
+            return gen
+        except Exception as e:  # noqa: BLE001  (the Python pipeline serves what it refuses)
+            log.info("native SD engine unavailable (%s); using the Python pipeline", e)
+    return SDGenerator.load(ctx)

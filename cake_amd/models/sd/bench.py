@@ -40,3 +40,37 @@ def measure_denoise(version: str = "xl", steps: int = 8, dtype=torch.float16,
     del unit, w
     torch.cuda.empty_cache()
     return out
+
+
+def measure_native(version: str = "xl", steps: int = 8, dtype: str = "f16",
+                   device: int = 0) -> dict:
+    """The same metric on the native SD engine (csrc/engine/sd_engine.cpp): a full
+    generation per call — both text encoders, steps guided denoising steps (the first
+    eager, the rest hipGraph replays), the VAE decode — on random-init full-size weights;
+    seconds_per_step = the mean device time of the replayed steps of the second call (the
+    first autotunes the convolutions and captures the step)."""
+    import numpy as np
+
+    from ...sd_engine import NativeSD
+    eng = NativeSD(".", version=version, dtype=dtype, device=device, random_init=True, seed=7)
+    try:
+        ids = np.full(77, 49407, dtype=np.int32)
+        ids[0], ids[1:4] = 49406, (320, 1125, 539)
+        unc = np.full(77, 49407, dtype=np.int32)
+        unc[0] = 49406
+        kw = dict(cond=ids, uncond=unc)
+        if version in ("xl", "turbo"):
+            kw.update(cond2=ids, uncond2=unc)
+        n = steps + 1
+        eng.generate(n_steps=n, guidance=7.5, seed=1, **kw)
+        t0 = time.perf_counter()
+        out = eng.generate(n_steps=n, guidance=7.5, seed=2, **kw)
+        wall = time.perf_counter() - t0
+    finally:
+        eng.close()
+    per = out.step_s[1:]
+    return {"seconds_per_step": round(sum(per) / len(per), 5), "version": version,
+            "resolution": f"{eng.width}x{eng.height}", "batch": 2, "dtype": dtype,
+            "engine": "native", "steps": n, "per_step_s": [round(x, 5) for x in out.step_s],
+            "text_ms": round(out.text_s * 1e3, 2), "vae_decode_ms": round(out.vae_s * 1e3, 2),
+            "image_wall_s": round(wall, 4)}

@@ -1,0 +1,147 @@
+"""Stable Diffusion generator on the native engine (csrc/engine/sd_engine.cpp).
+
+The reference's generate_image (cake-core/src/models/sd/sd.rs:320-532) behind the
+ImageGenerator contract with the whole generation in C++ — both text encoders, the
+guided denoising loop (graph replays) and the VAE decode; the tokenizers (HF
+``tokenizers``), the seeded latent noise and the PNG writing stay here.  The noise and
+the ancestral-noise key are drawn from the request's generator in the same order as the
+Python pipeline (models/sd/pipeline.py), so a seed gives the same image on either path.
+
+Requests the engine does not cover — img2img, intermediary images, bsize > 1 — run on
+the Python pipeline, built on first use.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import time
+from typing import Callable
+
+import numpy as np
+import torch
+
+from ..base import ImageGenerator
+from .args import ImageGenerationArgs
+from .config import SDConfig
+from .weights import resolve
+
+log = logging.getLogger("cake.sd")
+
+
+class NativeSDGenerator(ImageGenerator):
+    MODEL_NAME = "stable-diffusion"
+
+    def __init__(self, cfg: SDConfig, engine, tok, pad_id, tok2=None, pad_id2=None,
+                 fallback: Callable[[], ImageGenerator] | None = None):
+        self.cfg, self.eng = cfg, engine
+        self.tok, self.pad_id, self.tok2, self.pad_id2 = tok, pad_id, tok2, pad_id2
+        self._fallback_factory = fallback
+        self._fallback = None
+        self.last_step_s: list[float] = []
+        self.last_result = None
+
+    @classmethod
+    def load(cls, ctx) -> "NativeSDGenerator":
+        from tokenizers import Tokenizer
+
+        from ...sd_engine import NativeSD
+        from .shardable import sd_config_for
+        a = ctx.args
+        cfg = sd_config_for(ctx)
+        xl = cfg.clip2 is not None
+
+        def pad_of(tok, clip_cfg):
+            pid = tok.token_to_id(clip_cfg.pad_with or "<|endoftext|>")
+            if pid is None:
+                raise ValueError(f"tokenizer has no pad token {clip_cfg.pad_with!r}")
+            return pid
+        tok = Tokenizer.from_file(str(resolve("tokenizer", a.sd_tokenizer, cfg.version, a.sd_use_f16,
+                                              ctx.model_path)))
+        tok2 = Tokenizer.from_file(str(resolve("tokenizer_2", a.sd_tokenizer_2, cfg.version,
+                                               a.sd_use_f16, ctx.model_path))) if xl else None
+        paths = {}
+        for comp, flag in (("unet", "sd_unet"), ("vae", "sd_vae"), ("clip", "sd_clip"),
+                           ("clip2", "sd_clip2")):
+            if comp == "clip2" and not xl:
+                continue
+            paths[comp] = str(resolve(comp, getattr(a, flag, None), cfg.version, a.sd_use_f16,
+                                      ctx.model_path))
+        eng = NativeSD(str(ctx.model_path), version=cfg.version, width=cfg.width,
+                       height=cfg.height, dtype="bf16" if ctx.dtype == torch.bfloat16 else "f16",
+                       device=ctx.device.index or 0, paths=paths)
+
+        def fallback():
+            from .pipeline import SDGenerator
+            return SDGenerator.load(ctx)
+        return cls(cfg, eng, tok, pad_of(tok, cfg.clip), tok2,
+                   pad_of(tok2, cfg.clip2) if xl else None, fallback)
+
+    def _ids(self, tok, pad, prompt: str) -> np.ndarray:
+        ids = tok.encode(prompt, add_special_tokens=True).ids
+        if len(ids) > 77:
+            raise ValueError(f"the prompt is too long, {len(ids)} > max-tokens (77)")
+        return np.asarray(ids + [pad] * (77 - len(ids)), dtype=np.int32)
+
+    def _python(self) -> ImageGenerator:
+        if self._fallback is None:
+            log.info("request needs the Python pipeline (img2img / intermediary images / bsize)")
+            self._fallback = self._fallback_factory()
+        return self._fallback
+
+    def generate_image(self, args: ImageGenerationArgs, callback: Callable[[list], None]) -> None:
+        if args.img2img or args.intermediary_images or args.bsize != 1 or args.tracing:
+            gen = self._python()
+            gen.generate_image(args, callback)
+            self.last_step_s = list(getattr(gen, "last_step_s", []))
+            return
+        from PIL import Image
+        cfg = self.cfg
+        guidance = args.guidance_scale if args.guidance_scale is not None else cfg.default_guidance
+        n_steps = args.n_steps if args.n_steps is not None else cfg.default_steps
+        gen = torch.Generator(device="cpu")
+        if args.image_seed is not None:
+            gen.manual_seed(int(args.image_seed))
+        else:
+            gen.seed()
+        use_guide = guidance > 1.0
+        kw = {"cond": self._ids(self.tok, self.pad_id, args.image_prompt)}
+        if use_guide:
+            kw["uncond"] = self._ids(self.tok, self.pad_id, args.uncond_prompt)
+        if self.tok2 is not None:
+            kw["cond2"] = self._ids(self.tok2, self.pad_id2, args.image_prompt)
+            if use_guide:
+                kw["uncond2"] = self._ids(self.tok2, self.pad_id2, args.uncond_prompt)
+        log.info('Running with prompt "%s".', args.image_prompt)
+        self.last_step_s = []
+        for idx in range(args.num_samples):
+            # the Python pipeline's draw order: latent noise, then the ancestral-noise key
+            noise = torch.randn((1, 4, cfg.height // 8, cfg.width // 8), generator=gen)
+            seed = int(torch.randint(0, 2 ** 62, (1,), generator=gen).item())
+            t0 = time.perf_counter()
+            out = self.eng.generate(n_steps=n_steps, guidance=guidance, seed=seed,
+                                    init_noise=noise.numpy(), **kw)
+            self.last_result = out
+            for k, dt in enumerate(out.step_s):
+                self.last_step_s.append(dt)
+                log.info("step %d/%d done, %.2fs", k + 1, n_steps, dt)
+            log.info("sample %d/%d: text %.1f ms, denoise %.1f ms, vae %.1f ms (%.1f ms total)",
+                     idx + 1, args.num_samples, out.text_s * 1e3, out.denoise_s * 1e3,
+                     out.vae_s * 1e3, (time.perf_counter() - t0) * 1e3)
+            callback([Image.fromarray(out.rgb, "RGB")])
+
+
+def native_sd_eligible(ctx) -> bool:
+    """Every SD component local on a GPU, a 16-bit dtype, CAKE_NATIVE != 0, engine built."""
+    if os.environ.get("CAKE_NATIVE", "1") == "0":
+        return False
+    if ctx.device.type != "cuda" or ctx.dtype not in (torch.float16, torch.bfloat16):
+        return False
+    topo = getattr(ctx, "topology", None)
+    if topo is not None:
+        for name in ("clip", "clip2", "vae", "unet"):
+            if topo.get_node_for_layer(name) is not None:
+                return False
+    if getattr(ctx.args, "sd_sliced_attention_size", None):
+        return True  # (flash attention has no score memory to slice)
+    from ...sd_engine import native_sd_available
+    return native_sd_available()

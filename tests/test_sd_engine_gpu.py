@@ -156,3 +156,39 @@ def test_generation_matches_python_denoise(cuda, mini):
                          use_graph=False, **kw)
     assert np.array_equal(eager.latents, out.latents)
     eng.close()
+
+
+def test_master_serves_images_from_the_native_engine(cuda, mini, tmp_path, monkeypatch):
+    """The CLI / API master picks the native engine for an all-local model; the same seed
+    and prompt give the same image as the Python pipeline (CAKE_NATIVE=0)."""
+    from cake_amd.cli import build_parser
+    from cake_amd.context import Context
+    from cake_amd.master import _load_image
+    from cake_amd.models.sd.args import ImageGenerationArgs
+    from cake_amd.models.sd.native_generator import NativeSDGenerator
+    v, cfg, d = mini
+    topo = tmp_path / "empty.yml"
+    topo.write_text("{}\n")
+    args = build_parser().parse_args(["--model", str(d), "--topology", str(topo), "--model-type",
+                                      "image-model", "--sd-version", v, "--dtype", "f16"])
+    ctx = Context.from_args(args)
+    monkeypatch.setenv("CAKE_CONV_AUTOTUNE", "0")
+    native = _load_image(ctx)
+    assert isinstance(native, NativeSDGenerator)
+    native.eng.close()
+    native.eng = __import__("cake_amd.sd_engine", fromlist=["NativeSD"]).NativeSD(
+        str(d), dtype="f16", autotune=False)  # static conv plans, as the Python side below
+    req = ImageGenerationArgs(image_prompt="a red cube", uncond_prompt="blurry", n_steps=3,
+                              image_seed=42)
+    got = []
+    native.generate_image(req, lambda imgs: got.append(imgs))
+    monkeypatch.setenv("CAKE_NATIVE", "0")
+    py = _load_image(ctx)
+    assert not isinstance(py, NativeSDGenerator)
+    ref = []
+    py.generate_image(req, lambda imgs: ref.append(imgs))
+    a = np.asarray(got[-1][0], dtype=np.int32)
+    b = np.asarray(ref[-1][0], dtype=np.int32)
+    assert a.shape == b.shape == (cfg.height, cfg.width, 3)
+    assert np.abs(a - b).mean() < 0.5 and np.abs(a - b).max() <= 8
+    assert len(native.last_step_s) == 3
