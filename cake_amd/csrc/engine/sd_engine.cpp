@@ -466,6 +466,8 @@ class SdEngine {
     paths_[1] = o.vae_path ? o.vae_path : "";
     paths_[2] = o.clip_path ? o.clip_path : "";
     paths_[3] = o.clip2_path ? o.clip2_path : "";
+    parts_ = o.parts ? o.parts : 15;
+    if (!cfg_.xl) parts_ &= 7;
     planner_.load(pkg_dir() + "/ops/gemm_tuned.json");
     zeros_ = dalloc(256);
     hip_check(hipMemset(zeros_, 0, 256), "memset");
@@ -494,6 +496,7 @@ class SdEngine {
   void generate(const CakeSdGenArgs& a, uint8_t* rgb, float* lat_out, double* step_s,
                 CakeSdResult* res) {
     hip_check(hipSetDevice(dev_), "hipSetDevice");
+    need(cfg_.xl ? 15 : 7, "every component (generate)");
     const bool guide = a.uncond != nullptr && a.guidance > 1.0f;
     if (cfg_.xl && (a.cond2 == nullptr || (guide && a.uncond2 == nullptr)))
       throw Error("xl / turbo need the second tokenizer's ids (cond2 / uncond2)");
@@ -503,6 +506,7 @@ class SdEngine {
     const auto t0 = std::chrono::steady_clock::now();
     // ---- text context [B2, 77, ctx]: rows [uncond; cond]
     text_context(a.cond, a.uncond, a.cond2, a.uncond2, guide);
+    hook_ctx_.clear();  // ctx_ / the k|v caches now hold this generation's context
     precompute_kv(B2);
     hip_check(hipStreamSynchronize(st_), "sync");
     const auto t1 = std::chrono::steady_clock::now();
@@ -580,6 +584,7 @@ class SdEngine {
   void text_component(int which, const int32_t* ids, int B, float* out) {
     hip_check(hipSetDevice(dev_), "hipSetDevice");
     if (which == 1 && !cfg_.xl) throw Error("this version has one text encoder");
+    need(which == 0 ? 4 : 8, which == 0 ? "clip" : "clip2");
     const ClipW& cw = which == 0 ? clip_ : clip2_;
     for (int b = 0; b < B; ++b) {
       text_a_.reset();
@@ -588,22 +593,55 @@ class SdEngine {
     }
   }
 
+  // one UNet forward (the TCP worker's unet component, tests): eager the first time for
+  // a batch size (convolution autotuning), captured the second, replayed after that; the
+  // cross-attention k|v are recomputed only when the context changes
   void unet_component(const float* sample, int B, float t, const float* ctx, float* out) {
     hip_check(hipSetDevice(dev_), "hipSetDevice");
+    need(1, "unet");
     if (B < 1 || B > 2) throw Error("unet hook: batch 1 or 2");
     const int h = cfg_.height / 8, w = cfg_.width / 8;
     const size_t n = (size_t)B * 4 * h * w, nc = (size_t)B * kTok * cfg_.ctx_dim();
     upload16(sample, n, inp_);
-    upload16(ctx, nc, ctx_);
-    precompute_kv(B);
+    if (hook_ctx_.size() != nc || std::memcmp(hook_ctx_.data(), ctx, nc * 4) != 0) {
+      hook_ctx_.assign(ctx, ctx + nc);
+      upload16(ctx, nc, ctx_);
+      precompute_kv(B);
+    }
     hip_check(hipMemcpyAsync(ttab_, &t, 4, hipMemcpyHostToDevice, st_), "H2D");
-    unet_a_.reset();
-    const uint16_t* y = unet_forward(inp_, B, ttab_, nullptr);
-    widen(y, n, out);
+    HookGraph& hg = hook_[B - 1];
+    if (hg.calls == 0 || hg.exec == nullptr) {
+      if (hg.calls == 0) {
+        unet_a_.reset();
+        hg.out = unet_forward(inp_, B, ttab_, nullptr);
+      } else {  // capture, then replay below
+        unet_a_.frozen = true;
+        hip_check(hipStreamBeginCapture(st_, hipStreamCaptureModeThreadLocal), "BeginCapture");
+        const uint16_t* y = nullptr;
+        try {
+          unet_a_.reset();
+          y = unet_forward(inp_, B, ttab_, nullptr);
+        } catch (...) {
+          hipGraph_t junk = nullptr;
+          (void)hipStreamEndCapture(st_, &junk);
+          if (junk) (void)hipGraphDestroy(junk);
+          unet_a_.frozen = false;
+          throw;
+        }
+        hip_check(hipStreamEndCapture(st_, &hg.g), "EndCapture");
+        unet_a_.frozen = false;
+        hip_check(hipGraphInstantiate(&hg.exec, hg.g, nullptr, nullptr, 0), "GraphInstantiate");
+        hg.out = y;
+      }
+    }
+    if (hg.exec) hip_check(hipGraphLaunch(hg.exec, st_), "hipGraphLaunch");
+    ++hg.calls;
+    widen(hg.out, n, out);
   }
 
   void vae_component(const float* zin, float* img) {
     hip_check(hipSetDevice(dev_), "hipSetDevice");
+    need(2, "vae");
     const int h = cfg_.height / 8, w = cfg_.width / 8;
     vae_a_.reset();
     uint16_t* z = new16(vae_a_, (size_t)4 * h * w);
@@ -860,9 +898,14 @@ class SdEngine {
     return t;
   }
 
+  void need(int mask, const char* what) const {
+    if ((parts_ & mask) != mask)
+      throw Error(std::string("this engine was opened without the ") + what);
+  }
+
   void build_and_load() {
     // ---------------- UNet (unet.py UNet2DConditionModel.__init__ / params)
-    {
+    if (parts_ & 1) {
       Loader L{this, nullptr, "unet", {}};
       if (init_ != 1) L.f = std::make_unique<SafeTensorsFile>(resolve(0));
       const UCfg& u = cfg_.unet;
@@ -941,7 +984,7 @@ class SdEngine {
       }
     }
     // ---------------- VAE decoder (vae.py AutoencoderKL decode half)
-    {
+    if (parts_ & 2) {
       Loader L{this, nullptr, "vae", {}};
       if (init_ != 1) L.f = std::make_unique<SafeTensorsFile>(resolve(1));
       const VCfg& v = cfg_.vae;
@@ -989,8 +1032,8 @@ class SdEngine {
       d_out_ = conv_param(L, "decoder.conv_out", v.out_ch, v.ch[0], 3);
     }
     // ---------------- text encoders (clip.py)
-    clip_ = clip_param(2, cfg_.clip);
-    if (cfg_.xl) clip2_ = clip_param(3, cfg_.clip2);
+    if (parts_ & 4) clip_ = clip_param(2, cfg_.clip);
+    if (cfg_.xl && (parts_ & 8)) clip2_ = clip_param(3, cfg_.clip2);
     hip_check(hipDeviceSynchronize(), "sync");
   }
 
@@ -1466,7 +1509,21 @@ class SdEngine {
     return gr;
   }
 
+  struct HookGraph {
+    hipGraph_t g = nullptr;
+    hipGraphExec_t exec = nullptr;
+    const uint16_t* out = nullptr;
+    long calls = 0;
+  };
+  HookGraph hook_[2];
+  std::vector<float> hook_ctx_;
+
   void drop_graphs() {
+    for (auto& hg : hook_) {
+      if (hg.exec) (void)hipGraphExecDestroy(hg.exec);
+      if (hg.g) (void)hipGraphDestroy(hg.g);
+      hg = HookGraph{};
+    }
     for (auto& kv : graphs_) {
       if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
       if (kv.second.g) (void)hipGraphDestroy(kv.second.g);
@@ -1574,7 +1631,7 @@ class SdEngine {
   std::string dir_;
   std::string paths_[4];
   SdCfg cfg_;
-  int dev_ = 0, dt_ = 1, init_ = 0;
+  int dev_ = 0, dt_ = 1, init_ = 0, parts_ = 15;
   uint64_t seed_ = 0;
   bool autotune_ = true;
   hipStream_t st_ = nullptr;

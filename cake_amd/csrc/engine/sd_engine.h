@@ -40,6 +40,7 @@ typedef struct CakeSdOpts {
   const char* vae_path;
   const char* clip_path;
   const char* clip2_path;
+  int32_t parts;         // components to load: 1 unet | 2 vae | 4 clip | 8 clip2 (0: all)
 } CakeSdOpts;
 
 typedef struct CakeSdGenArgs {

@@ -4,11 +4,11 @@
 // `start_worker(name, model_path, topology_path, model_type)`
 // (cake-ios/src/lib.rs:6-87), which runs a worker on 0.0.0.0:10128 with
 // default args inside the calling process.  Same here: the worker runs IN this
-// process and the call returns the worker's exit code when it stops.  A text worker
-// is the native one (WorkerServer over the native engine, native_worker.cpp; no
-// interpreter); image workers (and CAKE_NATIVE=0) run the compute runtime in the
-// embedded interpreter (embed.cpp; an interpreter the host process already runs is
-// reused).
+// process and the call returns the worker's exit code when it stops.  Text and image
+// workers are the native ones (WorkerServer over the native Llama / SD engines,
+// native_worker.cpp; no interpreter); CAKE_NATIVE=0 (and nodes with units the native
+// SD worker does not serve) run the compute runtime in the embedded interpreter
+// (embed.cpp; an interpreter the host process already runs is reused).
 #include <cstdio>
 #include <cstdlib>
 #include <stdexcept>
@@ -29,10 +29,10 @@ extern "C" __attribute__((visibility("default"))) int cake_start_worker(
   // text: the native worker in this process (engine over the WorkerServer), as
   // cake-cli --mode worker; the topology decides the layers (first node when the name
   // is not in it, worker.rs:90-104)
-  if (mt != "image" && !(nat && std::string(nat) == "0") && cake::native_engine_available()) {
+  if (!(nat && std::string(nat) == "0") && cake::native_engine_available()) {
     try {
       const cake::Topology topo = cake::Topology::from_path(
-          topology_path ? topology_path : "topology.yml", true);
+          topology_path ? topology_path : "topology.yml", mt != "image");
       if (topo.nodes.empty()) {
         std::fprintf(stderr, "cake_start_worker: topology has no workers\n");
         return 2;
@@ -45,7 +45,10 @@ extern "C" __attribute__((visibility("default"))) int cake_start_worker(
       w.model_dir = model_path ? model_path : ".";
       w.address = addr;
       w.log_tag = "cake_start_worker";
-      return cake::run_native_worker(w, nd ? *nd : topo.nodes[0]);
+      const cake::TopoNode& node = nd ? *nd : topo.nodes[0];
+      if (mt != "image") return cake::run_native_worker(w, node);
+      // image: the native SD worker for the components it serves (else the runtime below)
+      if (cake::native_sd_components(node)) return cake::run_native_sd_worker(w, node);
     } catch (const std::exception& e) {
       std::fprintf(stderr, "cake_start_worker: %s\n", e.what());
       return 2;

@@ -4,6 +4,7 @@
 #include <dlfcn.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -13,6 +14,7 @@
 #include <vector>
 
 #include "../engine/llama_engine.h"
+#include "../engine/sd_engine.h"
 #include "server.h"
 
 namespace cake {
@@ -179,5 +181,216 @@ int run_native_worker(const NativeWorkerOpts& o, const TopoNode& node) {
   return 0;
 }
 
+namespace {
+
+// any numeric wire tensor -> f32 values (ids arrive as integers, packs as f32)
+std::vector<float> as_f32(const RawTensor& x) {
+  uint64_t n = 1;
+  for (auto d : x.shape) n *= d;
+  std::vector<float> v(n);
+  const uint8_t* p = x.data;
+  auto need = [&](uint64_t es) {
+    if (x.nbytes != n * es) throw std::runtime_error("tensor byte size does not match its shape");
+  };
+  if (x.dtype == "f32") {
+    need(4);
+    std::memcpy(v.data(), p, n * 4);
+  } else if (x.dtype == "f16" || x.dtype == "bf16") {
+    need(2);
+    const uint16_t* h = reinterpret_cast<const uint16_t*>(p);
+    for (uint64_t i = 0; i < n; ++i) v[i] = half_to_f32(h[i], x.dtype == "bf16");
+  } else if (x.dtype == "i64") {
+    need(8);
+    for (uint64_t i = 0; i < n; ++i) { int64_t t; std::memcpy(&t, p + 8 * i, 8); v[i] = (float)t; }
+  } else if (x.dtype == "u32" || x.dtype == "i32") {
+    need(4);
+    for (uint64_t i = 0; i < n; ++i) {
+      uint32_t t;
+      std::memcpy(&t, p + 4 * i, 4);
+      v[i] = x.dtype == "u32" ? (float)t : (float)(int32_t)t;
+    }
+  } else if (x.dtype == "u8") {
+    need(1);
+    for (uint64_t i = 0; i < n; ++i) v[i] = (float)p[i];
+  } else {
+    throw std::runtime_error("unsupported tensor dtype " + x.dtype);
+  }
+  return v;
+}
+
+struct Packed {  // util.rs pack: [n, ndim, dims..., data..., ndim, ...]
+  std::vector<std::vector<uint64_t>> shapes;
+  std::vector<const float*> data;
+};
+
+Packed unpack(const std::vector<float>& f) {
+  Packed out;
+  if (f.empty()) throw std::runtime_error("empty packed tensor");
+  const size_t n = (size_t)f[0];
+  size_t i = 1;
+  for (size_t k = 0; k < n; ++k) {
+    if (i >= f.size()) throw std::runtime_error("truncated packed tensor");
+    const size_t nd = (size_t)f[i++];
+    std::vector<uint64_t> shp;
+    uint64_t numel = 1;
+    for (size_t d = 0; d < nd; ++d) {
+      if (i >= f.size()) throw std::runtime_error("truncated packed tensor");
+      shp.push_back((uint64_t)f[i++]);
+      numel *= shp.back();
+    }
+    if (i + numel > f.size()) throw std::runtime_error("truncated packed tensor");
+    out.shapes.push_back(shp);
+    out.data.push_back(f.data() + i);
+    i += numel;
+  }
+  return out;
+}
+
+const char* kSdParts[4] = {"unet", "vae", "clip", "clip2"};
+
+}  // namespace
+
+bool native_sd_components(const TopoNode& node) {
+  if (node.layers.empty()) return false;
+  for (const auto& l : node.layers)
+    if (std::find(std::begin(kSdParts), std::end(kSdParts), l) == std::end(kSdParts)) return false;
+  return true;
+}
+
+int run_native_sd_worker(const NativeWorkerOpts& o, const TopoNode& node) {
+  const std::string tag = o.log_tag;
+  const std::string lib = engine_path();
+  void* h = dlopen(lib.c_str(), RTLD_NOW | RTLD_LOCAL);
+  if (!h) {
+    std::fprintf(stderr, "%s: %s\n", tag.c_str(), dlerror());
+    return 1;
+  }
+  using Open = void* (*)(const char*, const CakeSdOpts*, char*, int32_t);
+  using Text = int32_t (*)(void*, int32_t, const int32_t*, int32_t, float*, char*, int32_t);
+  using Unet = int32_t (*)(void*, const float*, int32_t, float, const float*, float*, char*, int32_t);
+  using Vae = int32_t (*)(void*, const float*, float*, char*, int32_t);
+  using Info = void (*)(void*, int32_t*);
+  auto open = reinterpret_cast<Open>(dlsym(h, "cake_sd_open"));
+  auto text = reinterpret_cast<Text>(dlsym(h, "cake_sd_text"));
+  auto unet = reinterpret_cast<Unet>(dlsym(h, "cake_sd_unet"));
+  auto vae = reinterpret_cast<Vae>(dlsym(h, "cake_sd_vae_decode"));
+  auto info = reinterpret_cast<Info>(dlsym(h, "cake_sd_info"));
+  if (!open || !text || !unet || !vae || !info) {
+    std::fprintf(stderr, "%s: SD engine symbols missing in %s\n", tag.c_str(), lib.c_str());
+    return 1;
+  }
+  if (!native_sd_components(node)) {
+    std::fprintf(stderr, "%s: worker %s serves units the native SD worker does not\n",
+                 tag.c_str(), node.name.c_str());
+    return 2;
+  }
+  int parts = 0;
+  for (const auto& l : node.layers)
+    for (int k = 0; k < 4; ++k)
+      if (l == kSdParts[k]) parts |= 1 << k;
+  CakeSdOpts so{};
+  so.version = o.sd_version.empty() ? nullptr : o.sd_version.c_str();
+  so.width = o.sd_width;
+  so.height = o.sd_height;
+  so.dtype = o.bf16 ? 0 : 1;
+  so.device = o.device;
+  so.autotune = 1;
+  so.parts = parts;
+  const char** pp[4] = {&so.unet_path, &so.vae_path, &so.clip_path, &so.clip2_path};
+  for (int k = 0; k < 4; ++k) *pp[k] = o.sd_paths[k].empty() ? nullptr : o.sd_paths[k].c_str();
+  char err[1024] = {0};
+  void* eng = open(o.model_dir.c_str(), &so, err, sizeof(err));
+  if (!eng) {
+    std::fprintf(stderr, "%s: native SD worker: %s\n", tag.c_str(), err);
+    return 1;
+  }
+  int32_t inf[6];
+  info(eng, inf);
+  WorkerInfo wi;
+  wi.version = "0.1.0";
+  wi.dtype = o.bf16 ? "bf16" : "f16";
+  wi.os = "linux";
+  wi.arch = "x86_64";
+  wi.device = "rocm";
+  wi.device_idx = (uint64_t)o.device;
+  std::string host;
+  int port = 0;
+  {
+    const auto c = o.address.rfind(':');
+    host = c == std::string::npos ? o.address : o.address.substr(0, c);
+    port = c == std::string::npos ? 10128 : std::atoi(o.address.c_str() + c + 1);
+    if (host.empty()) host = "0.0.0.0";
+  }
+  WorkerServer server(host, port, wi, node.name);
+  std::mutex mu;
+  const int W = inf[0], H = inf[1], Dc = inf[2];
+  server.set_compute([&](uint64_t, const std::vector<BatchItem>& ops, const RawTensor& x) {
+    OpResult r;
+    try {
+      if (ops.size() != 1) throw std::runtime_error("one SD component per request");
+      const std::string& name = ops[0].layer_name;
+      const std::vector<float> f = as_f32(x);
+      std::lock_guard<std::mutex> g(mu);
+      char e2[512] = {0};
+      std::vector<float> out;
+      if (name == "clip" || name == "clip2") {
+        if (f.size() % 77) throw std::runtime_error("token ids must be [B, 77]");
+        const int B = (int)(f.size() / 77);
+        std::vector<int32_t> ids(f.size());
+        for (size_t i = 0; i < f.size(); ++i) ids[i] = (int32_t)f[i];
+        const int D = name == "clip" ? inf[4] : inf[5];
+        out.resize((size_t)B * 77 * D);
+        if (text(eng, name == "clip" ? 0 : 1, ids.data(), B, out.data(), e2, sizeof(e2)))
+          throw std::runtime_error(e2);
+        r.shape = {(uint64_t)B, 77, (uint64_t)D};
+      } else if (name == "unet") {
+        const Packed pk = unpack(f);
+        if (pk.shapes.size() != 3 || pk.shapes[0].size() != 4)
+          throw std::runtime_error("unet expects pack([latents, text_embeddings, timestep])");
+        const auto& ls = pk.shapes[0];
+        const int B = (int)ls[0];
+        if ((int)ls[1] != 4 || (int)ls[2] != H / 8 || (int)ls[3] != W / 8)
+          throw std::runtime_error("latents " + std::to_string(ls[2]) + "x" +
+                                   std::to_string(ls[3]) + " do not match the engine's " +
+                                   std::to_string(W) + "x" + std::to_string(H) + " (--sd-width/height)");
+        uint64_t ne = 1;
+        for (auto d : pk.shapes[1]) ne *= d;
+        if (ne != (uint64_t)B * 77 * Dc) throw std::runtime_error("text embedding shape mismatch");
+        out.resize((size_t)B * 4 * (H / 8) * (W / 8));
+        if (unet(eng, pk.data[0], B, pk.data[2][0], pk.data[1], out.data(), e2, sizeof(e2)))
+          throw std::runtime_error(e2);
+        r.shape = ls;
+      } else if (name == "vae") {
+        const Packed pk = unpack(f);
+        if (pk.shapes.size() != 2) throw std::runtime_error("vae expects pack([direction, x])");
+        if (pk.data[0][0] != 0.0f)
+          throw std::runtime_error("VAE encode (img2img) runs on the Python worker (CAKE_NATIVE=0)");
+        const auto& zs = pk.shapes[1];
+        if (zs.size() != 4 || zs[0] != 1 || (int)zs[2] != H / 8 || (int)zs[3] != W / 8)
+          throw std::runtime_error("vae decode expects [1, 4, h, w] at the engine's resolution");
+        out.resize((size_t)3 * H * W);
+        if (vae(eng, pk.data[1], out.data(), e2, sizeof(e2))) throw std::runtime_error(e2);
+        r.shape = {1, 3, (uint64_t)H, (uint64_t)W};
+      } else {
+        throw std::runtime_error("unknown SD component " + name);
+      }
+      r.dtype = "f32";
+      r.data.assign(reinterpret_cast<const char*>(out.data()), out.size() * 4);
+    } catch (const std::exception& e) {
+      r.error = e.what();
+    }
+    return r;
+  });
+  server.set_drop([](uint64_t) {});
+  server.set_reset([](uint64_t) {});
+  server.set_log([tag](const std::string& m) { std::fprintf(stderr, "[%s] %s\n", tag.c_str(), m.c_str()); });
+  std::string units;
+  for (const auto& l : node.layers) units += (units.empty() ? "" : ",") + l;
+  std::fprintf(stderr, "[%s] native SD worker %s: %s (%dx%d) on device %d, listening on %s:%d\n",
+               tag.c_str(), node.name.c_str(), units.c_str(), W, H, o.device, host.c_str(),
+               server.port());
+  server.serve();
+  return 0;
+}
 
 }  // namespace cake

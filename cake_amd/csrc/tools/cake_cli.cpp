@@ -404,6 +404,32 @@ bool native_worker_eligible(cake::PyArgs& o, bool text, bool worker) {
           o["dtype"].value == "bf16");
 }
 
+// image model: the native SD worker serves unet / clip / clip2 / vae (decode) components
+bool native_sd_worker_eligible(cake::PyArgs& o, bool text, bool worker,
+                               const cake::TopoNode& node) {
+  const char* env = std::getenv("CAKE_NATIVE");
+  if (env && std::string(env) == "0") return false;
+  return !text && worker && o["cpu"].value != "1" && o["transport"].value == "tcp" &&
+         (o["dtype"].kind == PyArg::kNone || o["dtype"].value == "f16" ||
+          o["dtype"].value == "bf16") &&
+         cake::native_sd_components(node) && cake::native_engine_available();
+}
+
+int run_native_sd_worker(cake::PyArgs& o, const cake::TopoNode& node) {
+  cake::NativeWorkerOpts w;
+  w.model_dir = o["model"].value;
+  w.address = o["address"].value;
+  w.device = o["device"].kind == PyArg::kNone ? 0 : std::atoi(o["device"].value.c_str());
+  w.bf16 = o["dtype"].value == "bf16";
+  w.sd_version = o["sd_version"].value;
+  if (o["sd_width"].kind != PyArg::kNone) w.sd_width = std::atoi(o["sd_width"].value.c_str());
+  if (o["sd_height"].kind != PyArg::kNone) w.sd_height = std::atoi(o["sd_height"].value.c_str());
+  const char* keys[4] = {"sd_unet", "sd_vae", "sd_clip", "sd_clip2"};
+  for (int k = 0; k < 4; ++k)
+    if (o[keys[k]].kind != PyArg::kNone) w.sd_paths[k] = o[keys[k]].value;
+  return cake::run_native_sd_worker(w, node);
+}
+
 int run_native_worker(cake::PyArgs& o, const cake::TopoNode& node) {
   cake::NativeWorkerOpts w;
   w.model_dir = o["model"].value;
@@ -500,5 +526,7 @@ int main(int argc, char** argv) {
   if (native_text_eligible(opts, text, worker, has_topology))
     return run_native_text(opts, topology.get());
   if (native_worker_eligible(opts, text, worker)) return run_native_worker(opts, worker_node);
+  if (native_sd_worker_eligible(opts, text, worker, worker_node))
+    return run_native_sd_worker(opts, worker_node);
   return cake::run_embedded(opts);
 }

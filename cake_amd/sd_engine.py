@@ -27,7 +27,10 @@ class SdOpts(C.Structure):
                 ("dtype", C.c_int32), ("device", C.c_int32), ("init", C.c_int32),
                 ("autotune", C.c_int32), ("tiny", C.c_int32), ("seed", C.c_uint64),
                 ("unet_path", C.c_char_p), ("vae_path", C.c_char_p), ("clip_path", C.c_char_p),
-                ("clip2_path", C.c_char_p)]
+                ("clip2_path", C.c_char_p), ("parts", C.c_int32)]
+
+
+PARTS = {"unet": 1, "vae": 2, "clip": 4, "clip2": 8}
 
 
 class SdGenArgs(C.Structure):
@@ -102,7 +105,7 @@ class NativeSD:
     def __init__(self, model_dir: str, version: str | None = None, width: int = 0,
                  height: int = 0, dtype: str = "f16", device: int = 0,
                  random_init: bool = False, seed: int = 0, autotune: bool = True,
-                 paths: dict | None = None):
+                 paths: dict | None = None, parts=None):
         if dtype not in ("f16", "bf16"):
             raise ValueError("native SD engine dtype: f16 or bf16")
         p = paths or {}
@@ -112,7 +115,8 @@ class NativeSD:
                    dtype=0 if dtype == "bf16" else 1, device=int(device),
                    init=1 if random_init else 0, autotune=1 if autotune else 0, tiny=0,
                    seed=int(seed), unet_path=self._keep[1], vae_path=self._keep[2],
-                   clip_path=self._keep[3], clip2_path=self._keep[4])
+                   clip_path=self._keep[3], clip2_path=self._keep[4],
+                   parts=0 if parts is None else sum(PARTS[p] for p in parts))
         err = C.create_string_buffer(1024)
         self._h = lib().cake_sd_open(str(model_dir).encode(), C.byref(o), err, 1024)
         if not self._h:

@@ -192,3 +192,70 @@ def test_master_serves_images_from_the_native_engine(cuda, mini, tmp_path, monke
     assert a.shape == b.shape == (cfg.height, cfg.width, 3)
     assert np.abs(a - b).mean() < 0.5 and np.abs(a - b).max() <= 8
     assert len(native.last_step_s) == 3
+
+
+def test_native_sd_tcp_worker_serves_the_unet(cuda, mini, tmp_path, monkeypatch):
+    """cake-cli --mode worker on an image model serves its topology components (here the
+    UNet) from the native SD engine — the reference's packed-tensor SingleOp interface,
+    no interpreter in the worker; the Python master's image over it matches its all-local
+    image (the master's host-side scheduler math vs the fused kernel: a few grey levels)."""
+    import os
+    import socket
+    import subprocess
+    import time
+
+    from cake_amd.cli import build_parser
+    from cake_amd.context import Context
+    from cake_amd.master import _load_image
+    from cake_amd.models.sd.args import ImageGenerationArgs
+    v, cfg, d = mini
+    if v != "v1-5":
+        pytest.skip("one version covers the worker plumbing")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cli = os.path.join(root, "cake_amd", "lib", "cake-cli")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    topo = tmp_path / "topology.yml"
+    topo.write_text(f"w1:\n  host: '127.0.0.1:{port}'\n  layers:\n    - 'unet'\n")
+    empty = tmp_path / "empty.yml"
+    empty.write_text("{}\n")
+    env = dict(os.environ, CAKE_LOG="warning")
+    w = subprocess.Popen([cli, "--mode", "worker", "--name", "w1", "--model", str(d),
+                          "--topology", str(topo), "--address", f"127.0.0.1:{port}",
+                          "--model-type", "image-model", "--sd-version", v, "--dtype", "f16"],
+                         cwd=root, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
+                         text=True)
+    monkeypatch.setenv("CAKE_NATIVE", "0")  # the master: the Python pipeline both times
+    req = ImageGenerationArgs(image_prompt="a red cube", uncond_prompt="", n_steps=3,
+                              image_seed=3)
+    try:
+        t0 = time.time()
+        while True:
+            if w.poll() is not None:
+                raise AssertionError(f"worker exited: {w.stderr.read()[-3000:]}")
+            try:
+                socket.create_connection(("127.0.0.1", port), timeout=0.5).close()
+                break
+            except OSError:
+                assert time.time() - t0 < 180, "worker did not listen"
+                time.sleep(0.3)
+
+        def image(topology):
+            args = build_parser().parse_args(["--model", str(d), "--topology", str(topology),
+                                              "--model-type", "image-model", "--sd-version", v,
+                                              "--dtype", "f16"])
+            gen = _load_image(Context.from_args(args))
+            out = []
+            gen.generate_image(req, lambda imgs: out.append(imgs))
+            return np.asarray(out[-1][0], dtype=np.int32)
+        remote = image(topo)
+        local = image(empty)
+    finally:
+        w.kill()
+        err = w.communicate()[1]
+    assert "native SD worker" in err, err[-2000:]
+    assert remote.shape == local.shape
+    diff = np.abs(remote - local)
+    assert diff.mean() < 2.0 and diff.max() <= 32, (diff.mean(), diff.max())
