@@ -8,14 +8,6 @@ timeout -k 10 300 python scripts/bench_sd.py --version xl --denoise --graph --st
 tail -3 $OUT/plain.log
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$ROOT/$OUT/prof" -o run -- python3 "$ROOT/scripts/bench_sd.py" --version xl --denoise --graph --steps 8 > "$ROOT/$OUT/prof.log" 2>&1 || { tail -20 "$ROOT/$OUT/prof.log"; exit 1; }
-f=$(find "$ROOT/$OUT/prof" -name '*kernel_stats.csv' | head -n 1)
-cp "$f" "$ROOT/$OUT/kernel_stats.csv"
-python3 - "$ROOT/$OUT/kernel_stats.csv" <<'PY'
-import csv, sys
-rows = list(csv.DictReader(open(sys.argv[1])))
-tot = sum(float(r["TotalDurationNs"]) for r in rows)
-print("total ms", round(tot / 1e6, 2))
-for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:28]:
-    print(f'{float(r["TotalDurationNs"])/1e6:9.2f} ms {int(r["Calls"]):6d} {float(r["AverageNs"])/1e3:9.2f} us  {r["Name"][:110]}')
-PY
+db=$(find "$ROOT/$OUT/prof" -name '*.db' | head -n 1)
+python3 "$ROOT/scripts/kernel_stats_db.py" "$db" --top 32 --per 8 --last-ms 240 > "$ROOT/$OUT/sdxl_step_kernels.txt" && cat "$ROOT/$OUT/sdxl_step_kernels.txt"
 find "$ROOT/$OUT/prof" -name '*.db' -delete

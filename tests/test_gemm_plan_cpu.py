@@ -1,7 +1,7 @@
 """GEMM tile plans on the CPU: the measured table (ops/gemm_tuned.json) and the three places
 that name the tile configurations — the kernel table (csrc/kernels/gemm_kernel.h
 CAKE_GEMM_CFGS), the Python planner (ops/gemm.py CFG_TILES) and the native engine's planner
-(csrc/engine/llama_engine.cpp) — must agree, or a tuned plan launches a tile the library
+(csrc/engine/engine_util.h, shared by the Llama and SD engines) — must agree, or a tuned plan launches a tile the library
 does not have."""
 import json
 import re
@@ -27,7 +27,7 @@ def test_tile_tables_agree():
         assert G.CFG_TILES[cfg] == (bm, bn), cfg
         # the gated epilogues need 32-column wave tiles; the others are refused up front
         assert ((bn // wn) % 32 == 0) == (cfg not in G.NO_GATED), cfg
-    eng = (ROOT / "cake_amd/csrc/engine/llama_engine.cpp").read_text()
+    eng = (ROOT / "cake_amd/csrc/engine/engine_util.h").read_text()
     known = re.search(r"static const int known\[\] = \{([^}]*)\}", eng).group(1)
     assert {int(x) for x in known.replace("\n", " ").split(",")} == set(G.CFG_TILES)
     assert set(G._SLOTS) == set(G.CFG_TILES) and set(G._EFF) == set(G.CFG_TILES)
