@@ -223,6 +223,7 @@ struct Schedule {
   std::vector<std::array<float, 4>> coef;  // (A, B, N, S_next) per step
   double init_sigma = 1.0;
   double first_scale = 1.0;                // input scale of step 0
+  std::vector<double> in_scale;            // input scale of every step (Euler-a; DDIM: 1)
 };
 
 Schedule build_schedule(const SchedCfg& c, int steps) {
@@ -283,6 +284,7 @@ Schedule build_schedule(const SchedCfg& c, int steps) {
   s.init_sigma = std::sqrt(mx * mx + 1.0);
   auto in_scale = [&](size_t i) { return 1.0 / std::sqrt(sigmas[i] * sigmas[i] + 1.0); };
   s.first_scale = in_scale(0);
+  for (size_t i = 0; i < s.ts.size(); ++i) s.in_scale.push_back(in_scale(i));
   for (size_t i = 0; i < s.ts.size(); ++i) {
     const double sf = sigmas[i], st = sigmas[i + 1];
     const double up = std::sqrt(std::max(0.0, st * st * (sf * sf - st * st) / (sf * sf)));
@@ -500,8 +502,15 @@ class SdEngine {
     const bool guide = a.uncond != nullptr && a.guidance > 1.0f;
     if (cfg_.xl && (a.cond2 == nullptr || (guide && a.uncond2 == nullptr)))
       throw Error("xl / turbo need the second tokenizer's ids (cond2 / uncond2)");
-    const int n = a.n_steps;
-    const Schedule s = build_schedule(cfg_.sched, n);
+    Schedule s = build_schedule(cfg_.sched, a.n_steps);
+    if (a.init_latents) {  // img2img: the steps from t_start on (pipeline.py t_start)
+      const int t0 = std::max(0, std::min(a.t_start, a.n_steps));
+      if (t0 >= a.n_steps) throw Error("img2img: no step left after t_start");
+      s.first_scale = s.in_scale.empty() ? 1.0 : s.in_scale[t0];
+      s.ts.erase(s.ts.begin(), s.ts.begin() + t0);
+      s.coef.erase(s.coef.begin(), s.coef.begin() + t0);
+    }
+    const int n = (int)s.ts.size();
     const int B2 = guide ? 2 : 1;
     const auto t0 = std::chrono::steady_clock::now();
     // ---- text context [B2, 77, ctx]: rows [uncond; cond]
@@ -514,7 +523,9 @@ class SdEngine {
     const int h = cfg_.height / 8, w = cfg_.width / 8;
     const size_t nl = (size_t)4 * h * w;
     std::vector<float> x(nl);
-    if (a.init_noise) {
+    if (a.init_latents) {
+      std::memcpy(x.data(), a.init_latents, nl * 4);
+    } else if (a.init_noise) {
       for (size_t i = 0; i < nl; ++i) x[i] = a.init_noise[i] * (float)s.init_sigma;
     } else {  // engine-side noise: seeded host normals (parity with torch's stream unpinned)
       std::mt19937_64 rng(a.seed);
@@ -637,6 +648,17 @@ class SdEngine {
     if (hg.exec) hip_check(hipGraphLaunch(hg.exec, st_), "hipGraphLaunch");
     ++hg.calls;
     widen(hg.out, n, out);
+  }
+
+  void vae_encode_component(const float* img, float* moments) {
+    hip_check(hipSetDevice(dev_), "hipSetDevice");
+    need(2, "vae");
+    vae_a_.reset();
+    const size_t n = (size_t)3 * cfg_.height * cfg_.width;
+    uint16_t* x = new16(vae_a_, n);
+    upload16(img, n, x);
+    const uint16_t* y = vae_encode(x);
+    widen(y, (size_t)2 * cfg_.vae.latent * (cfg_.height / 8) * (cfg_.width / 8), moments);
   }
 
   void vae_component(const float* zin, float* img) {
@@ -983,33 +1005,44 @@ class SdEngine {
         L.load(e.first + ".time_emb_proj.bias", {e.second}, tall_b_ + off);
       }
     }
-    // ---------------- VAE decoder (vae.py AutoencoderKL decode half)
+    // ---------------- VAE (vae.py AutoencoderKL: the decoder, and the encoder for img2img)
     if (parts_ & 2) {
       Loader L{this, nullptr, "vae", {}};
       if (init_ != 1) L.f = std::make_unique<SafeTensorsFile>(resolve(1));
       const VCfg& v = cfg_.vae;
+      {  // encoder
+        e_in_ = conv_param(L, "encoder.conv_in", v.ch[0], 3, 3);
+        int out = v.ch[0];
+        for (size_t i = 0; i < v.ch.size(); ++i) {
+          const int cin = out;
+          out = v.ch[i];
+          DownW d;
+          for (int j = 0; j < v.lpb; ++j)
+            d.res.push_back(resnet_param(L, "encoder.down_blocks." + std::to_string(i) +
+                                                ".resnets." + std::to_string(j),
+                                         j == 0 ? cin : out, out, 0));
+          if (i + 1 < v.ch.size()) {
+            d.has_ds = true;
+            d.ds = conv_param(L, "encoder.down_blocks." + std::to_string(i) + ".downsamplers.0.conv",
+                              out, out, 3);
+          }
+          e_down_.push_back(std::move(d));
+        }
+        for (int j = 0; j < 2; ++j)
+          e_mid_[j] = resnet_param(L, "encoder.mid_block.resnets." + std::to_string(j),
+                                   v.ch.back(), v.ch.back(), 0);
+        e_att_ = vae_attn_param(L, "encoder.mid_block.attentions.0", v.ch.back());
+        e_norm_w_ = param(L, "encoder.conv_norm_out.weight", {v.ch.back()});
+        e_norm_b_ = param(L, "encoder.conv_norm_out.bias", {v.ch.back()});
+        e_out_ = conv_param(L, "encoder.conv_out", 2 * v.latent, v.ch.back(), 3);
+        quant_ = conv_param(L, "quant_conv", 2 * v.latent, 2 * v.latent, 1);
+      }
       post_quant_ = conv_param(L, "post_quant_conv", v.latent, v.latent, 1);
       d_in_ = conv_param(L, "decoder.conv_in", v.ch.back(), v.latent, 3);
       for (int j = 0; j < 2; ++j)
         d_mid_[j] = resnet_param(L, "decoder.mid_block.resnets." + std::to_string(j), v.ch.back(),
                                  v.ch.back(), 0);
-      {
-        const std::string n = "decoder.mid_block.attentions.0";
-        const int C = v.ch.back();
-        d_att_.C = C;
-        d_att_.nw = param(L, n + ".group_norm.weight", {C});
-        d_att_.nb = param(L, n + ".group_norm.bias", {C});
-        d_att_.qkv = dalloc16((size_t)3 * C * C);
-        d_att_.qkv_b = dalloc16((size_t)3 * C);
-        const char* qkvn[3] = {".to_q", ".to_k", ".to_v"};
-        for (int k = 0; k < 3; ++k) {
-          load_linear_or_1x1(L, n + qkvn[k] + ".weight", C, C, d_att_.qkv + (size_t)k * C * C);
-          L.load(n + qkvn[k] + ".bias", {C}, d_att_.qkv_b + (size_t)k * C);
-        }
-        d_att_.ow = dalloc16((size_t)C * C);
-        load_linear_or_1x1(L, n + ".to_out.0.weight", C, C, d_att_.ow);
-        d_att_.ob = param(L, n + ".to_out.0.bias", {C});
-      }
+      d_att_ = vae_attn_param(L, "decoder.mid_block.attentions.0", v.ch.back());
       std::vector<int> rev(v.ch.rbegin(), v.ch.rend());
       int out = rev[0];
       for (size_t i = 0; i < rev.size(); ++i) {
@@ -1035,6 +1068,24 @@ class SdEngine {
     if (parts_ & 4) clip_ = clip_param(2, cfg_.clip);
     if (cfg_.xl && (parts_ & 8)) clip2_ = clip_param(3, cfg_.clip2);
     hip_check(hipDeviceSynchronize(), "sync");
+  }
+
+  VaeAttnW vae_attn_param(Loader& L, const std::string& n, int C) {
+    VaeAttnW a;
+    a.C = C;
+    a.nw = param(L, n + ".group_norm.weight", {C});
+    a.nb = param(L, n + ".group_norm.bias", {C});
+    a.qkv = dalloc16((size_t)3 * C * C);
+    a.qkv_b = dalloc16((size_t)3 * C);
+    const char* qkvn[3] = {".to_q", ".to_k", ".to_v"};
+    for (int k = 0; k < 3; ++k) {
+      load_linear_or_1x1(L, n + qkvn[k] + ".weight", C, C, a.qkv + (size_t)k * C * C);
+      L.load(n + qkvn[k] + ".bias", {C}, a.qkv_b + (size_t)k * C);
+    }
+    a.ow = dalloc16((size_t)C * C);
+    load_linear_or_1x1(L, n + ".to_out.0.weight", C, C, a.ow);
+    a.ob = param(L, n + ".to_out.0.bias", {C});
+    return a;
   }
 
   void load_linear_or_1x1(Loader& L, const std::string& name, int o, int i, uint16_t* dst) {
@@ -1592,6 +1643,52 @@ class SdEngine {
     return {conv(A, r.c2, h, 1, x.H, x.W, 1, 1, false, nullptr, 0, sc), x.H, x.W, r.cout};
   }
 
+  // mid-block attention: one head of dim C, residual in the output projection
+  Fm vae_attention(const VaeAttnW& at, Fm x) {
+    Arena& A = vae_a_;
+    const int C = at.C, T = x.H * x.W;
+    uint16_t* hn = group_norm(A, x.p, nullptr, C, 1, T, C, at.nw, at.nb, cfg_.vae.groups, 1e-6f,
+                              false);
+    uint16_t* qkv = new16(A, (size_t)T * 3 * C);
+    gemm(kStore, hn, C, T, C, at.qkv, 3 * C, at.qkv_b, qkv, 3 * C);
+    uint16_t* a = attention(A, qkv, 3 * C, qkv + C, 3 * C, qkv + 2 * C, 3 * C, 1, T, T, 1, C,
+                            false);
+    uint16_t* y = new16(A, (size_t)T * C);
+    gemm(kAdd16, a, C, T, C, at.ow, C, at.ob, y, C, x.p, C);
+    return {y, x.H, x.W, C};
+  }
+
+  // vae.py _encode: image [1, 3, H, W] (NCHW) -> moments [1, 8, h, w] (NCHW)
+  const uint16_t* vae_encode(const uint16_t* img) {
+    Arena& A = vae_a_;
+    const VCfg& v = cfg_.vae;
+    int H = cfg_.height, W = cfg_.width;
+    Fm x{conv(A, e_in_, img, 1, H, W, 1, 1, false, nullptr, 0, nullptr, true, false), H, W,
+         v.ch[0]};
+    for (const auto& d : e_down_) {
+      for (const auto& r : d.res) x = vae_resnet(r, x);
+      if (d.has_ds) {  // pad one zero row (bottom) and column (right), conv 3x3 stride 2
+        const int C = x.C;
+        uint16_t* pad = new16(A, (size_t)(x.H + 1) * (x.W + 1) * C);
+        hip_check(hipMemsetAsync(pad, 0, (size_t)(x.H + 1) * (x.W + 1) * C * 2, st_), "memset");
+        hip_check(hipMemcpy2DAsync(pad, (size_t)(x.W + 1) * C * 2, x.p, (size_t)x.W * C * 2,
+                                   (size_t)x.W * C * 2, x.H, hipMemcpyDeviceToDevice, st_),
+                  "pad copy");
+        int oh, ow;
+        uint16_t* y = conv(A, d.ds, pad, 1, x.H + 1, x.W + 1, 2, 0, false, nullptr, 0, nullptr,
+                           false, false, &oh, &ow);
+        x = {y, oh, ow, d.ds.OC};
+      }
+    }
+    x = vae_resnet(e_mid_[0], x);
+    x = vae_attention(e_att_, x);
+    x = vae_resnet(e_mid_[1], x);
+    uint16_t* hn = group_norm(A, x.p, nullptr, x.C, 1, x.H * x.W, x.C, e_norm_w_, e_norm_b_,
+                              v.groups, 1e-6f, true);
+    uint16_t* mo = conv(A, e_out_, hn, 1, x.H, x.W, 1, 1, false);
+    return conv(A, quant_, mo, 1, x.H, x.W, 1, 0, false, nullptr, 0, nullptr, false, true);
+  }
+
   const uint16_t* vae_decode(const uint16_t* z) {
     Arena& A = vae_a_;
     const VCfg& v = cfg_.vae;
@@ -1599,18 +1696,7 @@ class SdEngine {
     uint16_t* pq = conv(A, post_quant_, z, 1, h, w, 1, 0, false, nullptr, 0, nullptr, true, false);
     Fm x{conv(A, d_in_, pq, 1, h, w, 1, 1, false), h, w, v.ch.back()};
     x = vae_resnet(d_mid_[0], x);
-    {  // mid-block attention: one head of dim C
-      const int C = d_att_.C, T = x.H * x.W;
-      uint16_t* hn = group_norm(A, x.p, nullptr, C, 1, T, C, d_att_.nw, d_att_.nb, v.groups, 1e-6f,
-                                false);
-      uint16_t* qkv = new16(A, (size_t)T * 3 * C);
-      gemm(kStore, hn, C, T, C, d_att_.qkv, 3 * C, d_att_.qkv_b, qkv, 3 * C);
-      uint16_t* a = attention(A, qkv, 3 * C, qkv + C, 3 * C, qkv + 2 * C, 3 * C, 1, T, T, 1, C,
-                              false);
-      uint16_t* y = new16(A, (size_t)T * C);
-      gemm(kAdd16, a, C, T, C, d_att_.ow, C, d_att_.ob, y, C, x.p, C);
-      x.p = y;
-    }
+    x = vae_attention(d_att_, x);
     x = vae_resnet(d_mid_[1], x);
     for (const auto& up : d_up_) {
       for (const auto& r : up.res) x = vae_resnet(r, x);
@@ -1658,6 +1744,11 @@ class SdEngine {
   TransformerW mid_att_;
   std::vector<UpW> up_;
   // VAE
+  ConvW e_in_, e_out_, quant_;
+  std::vector<DownW> e_down_;
+  ResnetW e_mid_[2];
+  VaeAttnW e_att_;
+  uint16_t *e_norm_w_, *e_norm_b_;
   ConvW post_quant_, d_in_, d_out_;
   ResnetW d_mid_[2];
   VaeAttnW d_att_;
@@ -1746,6 +1837,17 @@ CAKE_API int32_t cake_sd_unet(void* eng, const float* sample, int32_t B, float t
 CAKE_API int32_t cake_sd_vae_decode(void* eng, const float* z, float* img, char* err, int32_t n) {
   try {
     static_cast<SdEngine*>(eng)->vae_component(z, img);
+    return 0;
+  } catch (const std::exception& e) {
+    cake::set_err(err, n, e.what());
+    return 1;
+  }
+}
+
+CAKE_API int32_t cake_sd_vae_encode(void* eng, const float* img, float* moments, char* err,
+                                    int32_t n) {
+  try {
+    static_cast<SdEngine*>(eng)->vae_encode_component(img, moments);
     return 0;
   } catch (const std::exception& e) {
     cake::set_err(err, n, e.what());

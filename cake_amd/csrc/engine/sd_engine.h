@@ -54,6 +54,10 @@ typedef struct CakeSdGenArgs {
                             // when init_noise is null
   const float* init_noise;  // optional [4 * (h/8) * (w/8)] standard-normal latent noise
   int32_t use_graph;        // 1: every step after the first is one hipGraph replay
+  // img2img: the schedule's steps from t_start on, starting from init_latents (the
+  // encoded image, scaled and noised to ts[t_start] by the caller); null = txt2img
+  int32_t t_start;
+  const float* init_latents;
 } CakeSdGenArgs;
 
 typedef struct CakeSdResult {
@@ -82,6 +86,10 @@ int32_t cake_sd_unet(void* engine, const float* sample, int32_t B, float t, cons
                      float* out, char* err, int32_t errlen);
 // VAE decode of z [1, 4, h, w] (already divided by vae_scale) -> image [1, 3, H, W] in [-1, 1].
 int32_t cake_sd_vae_decode(void* engine, const float* z, float* img, char* err, int32_t errlen);
+// VAE encode of an image [1, 3, H, W] in [-1, 1] -> the posterior moments [1, 8, h, w]
+// (mean | logvar; the caller samples, as vae.py AutoencoderKL.encode does).
+int32_t cake_sd_vae_encode(void* engine, const float* img, float* moments, char* err,
+                           int32_t errlen);
 
 #ifdef __cplusplus
 }

@@ -7,8 +7,11 @@ guided denoising loop (graph replays) and the VAE decode; the tokenizers (HF
 the ancestral-noise key are drawn from the request's generator in the same order as the
 Python pipeline (models/sd/pipeline.py), so a seed gives the same image on either path.
 
-Requests the engine does not cover — img2img, intermediary images, bsize > 1 — run on
-the Python pipeline, built on first use.
+img2img runs natively too: the engine encodes the image (VAE encoder), the posterior
+sample, the latent scaling and the noise to the start step are drawn here with the same
+generators and torch ops as the Python pipeline, and the engine denoises from that step.
+Requests the engine does not cover — intermediary images, bsize > 1, tracing — run on the
+Python pipeline, built on first use.
 """
 from __future__ import annotations
 
@@ -37,6 +40,8 @@ class NativeSDGenerator(ImageGenerator):
         self.tok, self.pad_id, self.tok2, self.pad_id2 = tok, pad_id, tok2, pad_id2
         self._fallback_factory = fallback
         self._fallback = None
+        # the VAE unit's own posterior-sampling generator (shardable.SDUnit.generator)
+        self.vae_generator = torch.Generator(device="cpu")
         self.last_step_s: list[float] = []
         self.last_result = None
 
@@ -88,8 +93,32 @@ class NativeSDGenerator(ImageGenerator):
             self._fallback = self._fallback_factory()
         return self._fallback
 
+    def _encode_image(self, path: str):
+        """pipeline.py image_preprocess + vae_encode on the engine: the latent sample
+        [1, 4, h, w] (model dtype, as the Python VAE unit returns it), or None when the
+        image does not have the engine's resolution."""
+        from .pipeline import image_preprocess
+        img = image_preprocess(path)
+        if tuple(img.shape[2:]) != (self.cfg.height, self.cfg.width):
+            return None
+        mo = torch.from_numpy(self.eng.vae_encode(img.numpy()))
+        dev = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
+        dt = torch.bfloat16 if self.eng._dt == 0 else torch.float16
+        moments = mo.to(dev).to(dt).float()
+        mean, logvar = moments.chunk(2, 1)
+        logvar = logvar.clamp(-30.0, 20.0)
+        eps = torch.randn(mean.shape, generator=self.vae_generator, device="cpu").to(mean.device)
+        return (mean + torch.exp(0.5 * logvar) * eps).to(dt)
+
     def generate_image(self, args: ImageGenerationArgs, callback: Callable[[list], None]) -> None:
-        if args.img2img or args.intermediary_images or args.bsize != 1 or args.tracing:
+        init = None
+        if args.img2img and not (args.intermediary_images or args.bsize != 1 or args.tracing):
+            if not 0.0 <= args.img2img_strength <= 1.0:
+                raise ValueError("img2img-strength should be between 0 and 1, got "
+                                 f"{args.img2img_strength}")
+            init = self._encode_image(args.img2img)
+        if (args.img2img and init is None) or args.intermediary_images or args.bsize != 1 \
+                or args.tracing:
             gen = self._python()
             gen.generate_image(args, callback)
             self.last_step_s = list(getattr(gen, "last_step_s", []))
@@ -113,17 +142,37 @@ class NativeSDGenerator(ImageGenerator):
                 kw["uncond2"] = self._ids(self.tok2, self.pad_id2, args.uncond_prompt)
         log.info('Running with prompt "%s".', args.image_prompt)
         self.last_step_s = []
+        t_start = n_steps - int(n_steps * args.img2img_strength) if init is not None else 0
         for idx in range(args.num_samples):
-            # the Python pipeline's draw order: latent noise, then the ancestral-noise key
-            noise = torch.randn((1, 4, cfg.height // 8, cfg.width // 8), generator=gen)
-            seed = int(torch.randint(0, 2 ** 62, (1,), generator=gen).item())
             t0 = time.perf_counter()
-            out = self.eng.generate(n_steps=n_steps, guidance=guidance, seed=seed,
-                                    init_noise=noise.numpy(), **kw)
+            if init is not None:  # pipeline.py's img2img latents, same draws and ops
+                from .schedulers import build_scheduler
+                sched = build_scheduler(cfg.scheduler, n_steps)
+                ts = sched.timesteps()
+                latents = init.float() * cfg.vae_scale
+                if t_start < len(ts):
+                    noise = torch.randn(latents.shape, generator=gen).to(latents.device)
+                    latents = sched.add_noise(latents, noise, ts[t_start])
+                latents = latents.float()
+                if t_start >= len(ts):  # strength 0: the encoded image itself
+                    img = self.eng.vae_decode((latents / cfg.vae_scale).cpu().numpy())
+                    rgb = ((np.clip(img[0] / 2 + 0.5, 0, 1) * 255).astype(np.uint8)
+                           .transpose(1, 2, 0).copy())
+                    callback([Image.fromarray(rgb, "RGB")])
+                    continue
+                seed = int(torch.randint(0, 2 ** 62, (1,), generator=gen).item())
+                out = self.eng.generate(n_steps=n_steps, guidance=guidance, seed=seed,
+                                        init_latents=latents.cpu().numpy(), t_start=t_start, **kw)
+            else:
+                # the Python pipeline's draw order: latent noise, then the ancestral-noise key
+                noise = torch.randn((1, 4, cfg.height // 8, cfg.width // 8), generator=gen)
+                seed = int(torch.randint(0, 2 ** 62, (1,), generator=gen).item())
+                out = self.eng.generate(n_steps=n_steps, guidance=guidance, seed=seed,
+                                        init_noise=noise.numpy(), **kw)
             self.last_result = out
             for k, dt in enumerate(out.step_s):
                 self.last_step_s.append(dt)
-                log.info("step %d/%d done, %.2fs", k + 1, n_steps, dt)
+                log.info("step %d/%d done, %.2fs", t_start + k + 1, n_steps, dt)
             log.info("sample %d/%d: text %.1f ms, denoise %.1f ms, vae %.1f ms (%.1f ms total)",
                      idx + 1, args.num_samples, out.text_s * 1e3, out.denoise_s * 1e3,
                      out.vae_s * 1e3, (time.perf_counter() - t0) * 1e3)

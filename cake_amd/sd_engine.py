@@ -37,7 +37,8 @@ class SdGenArgs(C.Structure):
     _fields_ = [("cond", C.POINTER(C.c_int32)), ("uncond", C.POINTER(C.c_int32)),
                 ("cond2", C.POINTER(C.c_int32)), ("uncond2", C.POINTER(C.c_int32)),
                 ("n_steps", C.c_int32), ("guidance", C.c_float), ("seed", C.c_uint64),
-                ("init_noise", C.POINTER(C.c_float)), ("use_graph", C.c_int32)]
+                ("init_noise", C.POINTER(C.c_float)), ("use_graph", C.c_int32),
+                ("t_start", C.c_int32), ("init_latents", C.POINTER(C.c_float))]
 
 
 class SdResult(C.Structure):
@@ -69,6 +70,8 @@ def lib() -> C.CDLL:
         L.cake_sd_unet.restype = I
         L.cake_sd_vae_decode.argtypes = [P, FP, FP, C.c_char_p, I]
         L.cake_sd_vae_decode.restype = I
+        L.cake_sd_vae_encode.argtypes = [P, FP, FP, C.c_char_p, I]
+        L.cake_sd_vae_encode.restype = I
         _bound = True
     return L
 
@@ -132,9 +135,11 @@ class NativeSD:
 
     def generate(self, cond, uncond=None, cond2=None, uncond2=None, n_steps: int = 30,
                  guidance: float = 7.5, seed: int = 0, init_noise=None,
-                 use_graph: bool = True) -> SdImage:
+                 use_graph: bool = True, init_latents=None, t_start: int = 0) -> SdImage:
         """One image from padded [77] id rows (uncond = None: no classifier-free
-        guidance; cond2 / uncond2: the second tokenizer's ids for xl / turbo)."""
+        guidance; cond2 / uncond2: the second tokenizer's ids for xl / turbo).  img2img:
+        init_latents [4, h, w] (the encoded image scaled and noised to the schedule's step
+        t_start) and the steps from t_start on."""
         ids = [None if x is None else _ids(x).reshape(-1) for x in (cond, uncond, cond2, uncond2)]
         for x in ids:
             if x is not None and x.size != N_TOK:
@@ -143,20 +148,25 @@ class NativeSD:
         h, w = self.height // 8, self.width // 8
         if noise is not None and noise.size != 4 * h * w:
             raise ValueError(f"init_noise must hold {4 * h * w} values")
+        lat0 = None if init_latents is None else _f32(init_latents).reshape(-1)
+        if lat0 is not None and lat0.size != 4 * h * w:
+            raise ValueError(f"init_latents must hold {4 * h * w} values")
         a = SdGenArgs(cond=_ip(ids[0]), uncond=_ip(ids[1]), cond2=_ip(ids[2]), uncond2=_ip(ids[3]),
                       n_steps=int(n_steps), guidance=float(guidance),
                       seed=int(seed) & 0xFFFFFFFFFFFFFFFF,
                       init_noise=None if noise is None else _fp(noise),
-                      use_graph=1 if use_graph else 0)
+                      use_graph=1 if use_graph else 0, t_start=int(t_start),
+                      init_latents=None if lat0 is None else _fp(lat0))
+        n_run = int(n_steps) - (max(0, int(t_start)) if lat0 is not None else 0)
         rgb = np.empty((self.height, self.width, 3), dtype=np.uint8)
         lat = np.empty((4, h, w), dtype=np.float32)
-        steps = (C.c_double * max(1, int(n_steps)))()
+        steps = (C.c_double * max(1, n_run))()
         res = SdResult()
         err = C.create_string_buffer(1024)
         rc = lib().cake_sd_generate(self._h, C.byref(a), rgb.ctypes.data_as(C.POINTER(C.c_uint8)),
                                     _fp(lat), steps, C.byref(res), err, 1024)
         self._check(rc, err)
-        return SdImage(rgb, lat, [float(steps[i]) for i in range(int(n_steps))], res.text_s,
+        return SdImage(rgb, lat, [float(steps[i]) for i in range(n_run)], res.text_s,
                        res.denoise_s, res.vae_s)
 
     def text(self, which: int, ids) -> np.ndarray:
@@ -188,6 +198,14 @@ class NativeSD:
         err = C.create_string_buffer(1024)
         self._check(lib().cake_sd_vae_decode(self._h, _fp(zz), _fp(img), err, 1024), err)
         return img
+
+    def vae_encode(self, img) -> np.ndarray:
+        """image [1, 3, H, W] in [-1, 1] -> posterior moments [1, 8, h, w] (mean | logvar)."""
+        x = _f32(img)
+        mo = np.empty((1, 8, self.height // 8, self.width // 8), dtype=np.float32)
+        err = C.create_string_buffer(1024)
+        self._check(lib().cake_sd_vae_encode(self._h, _fp(x), _fp(mo), err, 1024), err)
+        return mo
 
     def close(self) -> None:
         if getattr(self, "_h", None):

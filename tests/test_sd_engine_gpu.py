@@ -259,3 +259,43 @@ def test_native_sd_tcp_worker_serves_the_unet(cuda, mini, tmp_path, monkeypatch)
     assert remote.shape == local.shape
     diff = np.abs(remote - local)
     assert diff.mean() < 2.0 and diff.max() <= 32, (diff.mean(), diff.max())
+
+
+def test_img2img_on_the_native_engine_matches_python(cuda, mini, tmp_path, monkeypatch):
+    """img2img natively (the engine's VAE encoder, the pipeline's sampling and noise draws,
+    the denoise from t_start) gives the Python pipeline's image."""
+    from cake_amd.cli import build_parser
+    from cake_amd.context import Context
+    from cake_amd.master import _load_image
+    from cake_amd.models.sd.args import ImageGenerationArgs
+    from cake_amd.models.sd.native_generator import NativeSDGenerator
+    from cake_amd.sd_engine import NativeSD
+    v, cfg, d = mini
+    topo = tmp_path / "empty.yml"
+    topo.write_text("{}\n")
+    args = build_parser().parse_args(["--model", str(d), "--topology", str(topo), "--model-type",
+                                      "image-model", "--sd-version", v, "--dtype", "f16"])
+    ctx = Context.from_args(args)
+    native = _load_image(ctx)
+    assert isinstance(native, NativeSDGenerator)
+    native.eng.close()
+    native.eng = NativeSD(str(d), dtype="f16", autotune=False)
+    src = []
+    native.generate_image(ImageGenerationArgs(image_prompt="a blue sphere", n_steps=2,
+                                              image_seed=1), lambda imgs: src.append(imgs))
+    path = tmp_path / "src.png"
+    src[-1][0].save(path)
+    req = ImageGenerationArgs(image_prompt="a red cube", n_steps=4, img2img=str(path),
+                              img2img_strength=0.5, image_seed=8)
+    got = []
+    native.generate_image(req, lambda imgs: got.append(imgs))
+    assert native._fallback is None  # served natively
+    assert len(native.last_step_s) == 2  # t_start = 4 - int(4 * 0.5)
+    monkeypatch.setenv("CAKE_NATIVE", "0")
+    py = _load_image(ctx)
+    ref = []
+    py.generate_image(req, lambda imgs: ref.append(imgs))
+    a = np.asarray(got[-1][0], dtype=np.int32)
+    b = np.asarray(ref[-1][0], dtype=np.int32)
+    assert np.abs(a - b).mean() < 0.5 and np.abs(a - b).max() <= 8, (np.abs(a - b).mean(),
+                                                                     np.abs(a - b).max())
