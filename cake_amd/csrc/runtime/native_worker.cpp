@@ -5,7 +5,9 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
+#include <random>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -270,12 +272,13 @@ int run_native_sd_worker(const NativeWorkerOpts& o, const TopoNode& node) {
   using Unet = int32_t (*)(void*, const float*, int32_t, float, const float*, float*, char*, int32_t);
   using Vae = int32_t (*)(void*, const float*, float*, char*, int32_t);
   using Info = void (*)(void*, int32_t*);
+  auto vae_enc = reinterpret_cast<Vae>(dlsym(h, "cake_sd_vae_encode"));
   auto open = reinterpret_cast<Open>(dlsym(h, "cake_sd_open"));
   auto text = reinterpret_cast<Text>(dlsym(h, "cake_sd_text"));
   auto unet = reinterpret_cast<Unet>(dlsym(h, "cake_sd_unet"));
   auto vae = reinterpret_cast<Vae>(dlsym(h, "cake_sd_vae_decode"));
   auto info = reinterpret_cast<Info>(dlsym(h, "cake_sd_info"));
-  if (!open || !text || !unet || !vae || !info) {
+  if (!open || !text || !unet || !vae || !vae_enc || !info) {
     std::fprintf(stderr, "%s: SD engine symbols missing in %s\n", tag.c_str(), lib.c_str());
     return 1;
   }
@@ -323,6 +326,7 @@ int run_native_sd_worker(const NativeWorkerOpts& o, const TopoNode& node) {
   }
   WorkerServer server(host, port, wi, node.name);
   std::mutex mu;
+  std::mt19937 rng(0x5eedu);  // VAE posterior samples (parity with torch's stream unpinned)
   const int W = inf[0], H = inf[1], Dc = inf[2];
   server.set_compute([&](uint64_t, const std::vector<BatchItem>& ops, const RawTensor& x) {
     OpResult r;
@@ -363,8 +367,25 @@ int run_native_sd_worker(const NativeWorkerOpts& o, const TopoNode& node) {
       } else if (name == "vae") {
         const Packed pk = unpack(f);
         if (pk.shapes.size() != 2) throw std::runtime_error("vae expects pack([direction, x])");
-        if (pk.data[0][0] != 0.0f)
-          throw std::runtime_error("VAE encode (img2img) runs on the Python worker (CAKE_NATIVE=0)");
+        if (pk.data[0][0] == 1.0f) {  // encode: the posterior sample of the image
+          const auto& is = pk.shapes[1];
+          if (is.size() != 4 || is[0] != 1 || is[1] != 3 || (int)is[2] != H || (int)is[3] != W)
+            throw std::runtime_error("vae encode expects [1, 3, H, W] at the engine's resolution");
+          const size_t nl = (size_t)4 * (H / 8) * (W / 8);
+          std::vector<float> mo(2 * nl);
+          if (vae_enc(eng, pk.data[1], mo.data(), e2, sizeof(e2))) throw std::runtime_error(e2);
+          // mean + exp(logvar / 2) eps (vae.py encode; the worker's own seeded normals)
+          std::normal_distribution<float> nd(0.f, 1.f);
+          out.resize(nl);
+          for (size_t i = 0; i < nl; ++i) {
+            const float lv = std::min(20.f, std::max(-30.f, mo[nl + i]));
+            out[i] = mo[i] + std::exp(0.5f * lv) * nd(rng);
+          }
+          r.shape = {1, 4, (uint64_t)(H / 8), (uint64_t)(W / 8)};
+          r.dtype = "f32";
+          r.data.assign(reinterpret_cast<const char*>(out.data()), out.size() * 4);
+          return r;
+        }
         const auto& zs = pk.shapes[1];
         if (zs.size() != 4 || zs[0] != 1 || (int)zs[2] != H / 8 || (int)zs[3] != W / 8)
           throw std::runtime_error("vae decode expects [1, 4, h, w] at the engine's resolution");

@@ -26,10 +26,10 @@ struct NativeWorkerOpts {
 
 // Serve `node` until the server stops; the exit code (1 = engine failure, 2 = no layers).
 int run_native_worker(const NativeWorkerOpts& o, const TopoNode& node);
-// Native SD worker: serves the node's components (unet, clip, clip2, vae decode) from the
-// native SD engine (sd_engine.cpp) with the reference's packed-tensor SingleOp interface
-// (sd_shardable.rs:29-45, unet.rs:81-100, vae.rs:87-108).  VAE encode (img2img) stays on
-// the Python worker (CAKE_NATIVE=0).
+// Native SD worker: serves the node's components (unet, clip, clip2, vae encode / decode)
+// from the native SD engine (sd_engine.cpp) with the reference's packed-tensor SingleOp
+// interface (sd_shardable.rs:29-45, unet.rs:81-100, vae.rs:87-108); the VAE posterior
+// sample uses the worker's own seeded normals.
 int run_native_sd_worker(const NativeWorkerOpts& o, const TopoNode& node);
 // every unit of the node is an SD component the native worker serves
 bool native_sd_components(const TopoNode& node);

@@ -196,7 +196,7 @@ def test_master_serves_images_from_the_native_engine(cuda, mini, tmp_path, monke
 
 def test_native_sd_tcp_worker_serves_the_unet(cuda, mini, tmp_path, monkeypatch):
     """cake-cli --mode worker on an image model serves its topology components (here the
-    UNet) from the native SD engine — the reference's packed-tensor SingleOp interface,
+    UNet and the VAE, encode and decode) from the native SD engine — the reference's packed-tensor SingleOp interface,
     no interpreter in the worker; the Python master's image over it matches its all-local
     image (the master's host-side scheduler math vs the fused kernel: a few grey levels)."""
     import os
@@ -218,7 +218,7 @@ def test_native_sd_tcp_worker_serves_the_unet(cuda, mini, tmp_path, monkeypatch)
     port = s.getsockname()[1]
     s.close()
     topo = tmp_path / "topology.yml"
-    topo.write_text(f"w1:\n  host: '127.0.0.1:{port}'\n  layers:\n    - 'unet'\n")
+    topo.write_text(f"w1:\n  host: '127.0.0.1:{port}'\n  layers:\n    - 'unet'\n    - 'vae'\n")
     empty = tmp_path / "empty.yml"
     empty.write_text("{}\n")
     env = dict(os.environ, CAKE_LOG="warning")
@@ -242,16 +242,24 @@ def test_native_sd_tcp_worker_serves_the_unet(cuda, mini, tmp_path, monkeypatch)
                 assert time.time() - t0 < 180, "worker did not listen"
                 time.sleep(0.3)
 
-        def image(topology):
+        def image(topology, r=req):
             args = build_parser().parse_args(["--model", str(d), "--topology", str(topology),
                                               "--model-type", "image-model", "--sd-version", v,
                                               "--dtype", "f16"])
             gen = _load_image(Context.from_args(args))
             out = []
-            gen.generate_image(req, lambda imgs: out.append(imgs))
-            return np.asarray(out[-1][0], dtype=np.int32)
-        remote = image(topo)
-        local = image(empty)
+            gen.generate_image(r, lambda imgs: out.append(imgs))
+            return out[-1][0]
+        remote_img = image(topo)
+        remote = np.asarray(remote_img, dtype=np.int32)
+        local = np.asarray(image(empty), dtype=np.int32)
+        # img2img through the worker's VAE encoder (its own posterior normals: shape only)
+        src = tmp_path / "src.png"
+        remote_img.save(src)
+        i2i = image(topo, ImageGenerationArgs(image_prompt="a red cube", n_steps=4,
+                                              img2img=str(src), img2img_strength=0.5,
+                                              image_seed=4))
+        assert i2i.size == (cfg.width, cfg.height)
     finally:
         w.kill()
         err = w.communicate()[1]
