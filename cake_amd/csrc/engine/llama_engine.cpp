@@ -75,6 +75,9 @@ int cake_attn_decode(int dt, const float* q, const void* kc, const void* vc, con
                      int S, int nh, int nkv, int hd, float scale, float* part,
                      unsigned int* tickets, void* out, hipStream_t st);
 int cake_attn_set_split_cap(int cap);
+int cake_attn_set_heads(int max_keys, int waves);
+int cake_attn_decode_heads(int dt, const float* q, const void* kc, const void* vc, const int* pos,
+                           int S, int nh, int nkv, int hd, float scale, void* out, hipStream_t st);
 int cake_attn_oproj_supported(int nh, int nkv, int hd, int H);
 long long cake_attn_oproj_ws_floats(int nkv, int H);
 long long cake_attn_oproj_ticket_words(int nkv, int H);
@@ -713,6 +716,7 @@ class Llama {
   // fused decode attention + o_proj (attn_oproj.hip) for one-split live lengths: the
   // short-context graph bucket and eager steps at such a position
   bool ao_ok_ = false, short_step_ = false;
+  int heads_max_ = 0;  // live lengths <= this: head-parallel attention (attn_head_kernel)
   float* ao_ws_ = nullptr;
   unsigned int* ao_tickets_ = nullptr;
   uint64_t seed_ = 0;
@@ -1023,6 +1027,13 @@ class Llama {
       const char* e = std::getenv("CAKE_ATTN_OPROJ");
       ao_ok_ = e && std::string(e) == "1" && cake_attn_oproj_supported(c.nh, c.nkv, c.hd, c.H) != 0;
     }
+    // CAKE_ATTN_HEADS=<max keys>[:<waves>]: the head-parallel short-context attention
+    if (!ao_ok_) {
+      const char* e = std::getenv("CAKE_ATTN_HEADS");
+      int mx = 0, nw = 2;
+      if (e && *e) std::sscanf(e, "%d:%d", &mx, &nw);
+      if (mx > 0 && cake_attn_set_heads(mx, nw) == 0) heads_max_ = mx;
+    }
     if (ao_ok_) {
       ao_ws_ = dalloc<float>((size_t)cake_attn_oproj_ws_floats(c.nkv, c.H));
       const size_t tw = (size_t)cake_attn_oproj_ticket_words(c.nkv, c.H);
@@ -1124,7 +1135,13 @@ class Llama {
 
   // an eager step at device position `pos` takes the fused attention + o_proj launch
   // exactly when a one-step graph replay there would (bucket of length pos + 2)
-  bool short_at(int pos) const { return ao_ok_ && cake_attn_splits(pos + 2) == 1; }
+  bool short_at(int pos) const { return short_len(pos + 2); }
+  // live lengths served by the cap-1 graph bucket: one split with attention + o_proj fused,
+  // or up to heads_max_ keys on the head-parallel attention launch
+  bool short_len(int t) const {
+    if (ao_ok_) return cake_attn_splits(t) == 1;
+    return heads_max_ > 0 && t <= heads_max_;
+  }
 
   // ---- prefill
   void grow_prefill(int T) {
@@ -1386,7 +1403,11 @@ class Llama {
                                 ao_tickets_, tickets_ + 2 * c.nkv, st_), "attn_oproj");
         if (tp_ > 1) ar_sum();
       } else {
-        k_check(cake_attn_decode(dt_, q_, kc(l), vc(l), pos_, S_, c.nh, c.nkv, c.hd, scale(),
+        if (short_step_)  // head-parallel short-context attention
+          k_check(cake_attn_decode_heads(dt_, q_, kc(l), vc(l), pos_, S_, c.nh, c.nkv, c.hd,
+                                         scale(), attn_out_, st_), "attn_heads");
+        else
+          k_check(cake_attn_decode(dt_, q_, kc(l), vc(l), pos_, S_, c.nh, c.nkv, c.hd, scale(),
                                  part_, tickets_, attn_out_, st_), "attn_decode");
         if (tp_ > 1) {
           k_check(cake_gemv_x16(dt_, attn_out_, w.wo, nq, c.H, partial_, 0, st_), "o_proj");
@@ -2321,8 +2342,9 @@ class Llama {
       if (std::find(caps.begin(), caps.end(), cc) == caps.end()) caps.push_back(cc);
       if (cap >= need) break;
     }
-    // cap 1: the one-split lengths with attention + o_proj fused (attn_oproj.hip)
-    if (ao_ok_) caps.push_back(1);
+    // cap 1: the one-split lengths with attention + o_proj fused (attn_oproj.hip), or the
+    // short lengths on the head-parallel attention
+    if (ao_ok_ || heads_max_ > 0) caps.push_back(1);
     std::sort(caps.begin(), caps.end());
     try {
       for (int cap : caps) {
@@ -2354,8 +2376,9 @@ class Llama {
     bucket_of_.assign(S_ + 1, (int32_t)caps.size() - 1);
     for (int t = 0; t <= S_; ++t) {
       const int nd = cake_attn_splits(t);
+      const bool sh = short_len(t);
       for (size_t i = 0; i < caps.size(); ++i)
-        if (caps[i] >= nd) { bucket_of_[t] = (int32_t)i; break; }
+        if ((caps[i] == 1) == sh && caps[i] >= nd) { bucket_of_[t] = (int32_t)i; break; }
     }
     graph_mode_ = m;
     have_graphs_ = true;

@@ -63,6 +63,19 @@ __global__ __launch_bounds__(AttnGeom2<NREP>::NT) void attn2_decode_kernel(AttnD
                                                                     lds, gridDim.x);
 }
 
+// Head-parallel short-context decode: one workgroup per QUERY head (grid nh), NW waves
+// over the key blocks, the whole context as one split.  Against the per-kv-head launch
+// (nkv workgroups, each carrying its group's nrep heads) the same keys are read nrep
+// times (from L2), but P.V and the end merge carry one head instead of nrep and 4x more
+// workgroups issue the loads.  Engines launch it for live lengths up to g_attn_heads_max.
+template <int DT, int HD, int NW>
+__global__ __launch_bounds__(64 * NW) void attn_head_kernel(AttnDecArgs a, int nrep) {
+  __shared__ __attribute__((aligned(16))) float lds[attn2_smem_floats<HD, 1, NW>()];
+  const int h = blockIdx.x;
+  attn2_decode_block<DT, HD, 1, false, NW, 2, NoHook, true>(a, h, 0, lds, gridDim.x, NoHook(),
+                                                           h / nrep);
+}
+
 }  // namespace cake
 
 using namespace cake;
@@ -242,5 +255,40 @@ CAKE_API int cake_attn_decode(int dt, const float* q, const void* kc, const void
                       g_attn_min_keys, splits, g_attn_stamps, g_attn_target,
                       g_attn_single, g_attn_drop_partials};
   DISPATCH_DT_HD(dt, hd, return (launch_decode<DT, HD>(nh / nkv, grid, st, a)));
+  return (int)hipErrorInvalidValue;
+}
+
+// ---- head-parallel short-context launch (attn_head_kernel)
+static int g_attn_heads_max = 0;  // live lengths <= this take it (0: off)
+static int g_attn_head_waves = 2;
+
+CAKE_API int cake_attn_set_heads(int max_keys, int waves) {
+  if (max_keys < 0 || (waves != 1 && waves != 2 && waves != 4)) return (int)hipErrorInvalidValue;
+  g_attn_heads_max = max_keys;
+  g_attn_head_waves = waves;
+  return 0;
+}
+
+CAKE_API int cake_attn_heads_max() { return g_attn_heads_max; }
+
+// out [nh][hd] (16-bit) for the position *pos (live length *pos + 1); any length is
+// correct (one workgroup walks every key), short ones are what it is fast for.
+CAKE_API int cake_attn_decode_heads(int dt, const float* q, const void* kc, const void* vc,
+                                    const int* pos, int S, int nh, int nkv, int hd, float scale,
+                                    void* out, hipStream_t st) {
+  if (nkv <= 0 || nh % nkv || S <= 0) return (int)hipErrorInvalidValue;
+  const AttnDecArgs a{q, (const uint16_t*)kc, (const uint16_t*)vc, pos, S,
+                      scale * 1.4426950408889634f, nullptr, nullptr, (uint16_t*)out,
+                      g_attn_min_keys, 1, nullptr, g_attn_target, S, 0};
+  const int nrep = nh / nkv;
+#define CAKE_HEADS(NW) \
+  hipLaunchKernelGGL((attn_head_kernel<DT, HD, NW>), dim3(nh), dim3(64 * NW), 0, st, a, nrep)
+  DISPATCH_DT_HD(dt, hd, {
+    if (g_attn_head_waves == 1) CAKE_HEADS(1);
+    else if (g_attn_head_waves == 2) CAKE_HEADS(2);
+    else CAKE_HEADS(4);
+    return (int)hipGetLastError();
+  });
+#undef CAKE_HEADS
   return (int)hipErrorInvalidValue;
 }

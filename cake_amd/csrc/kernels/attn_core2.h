@@ -112,10 +112,13 @@ struct NoHook {
 // or two key blocks, q) are issued and before anything waits on them — a caller's own
 // loads issued there queue BEHIND the attention's (vmcnt retires in order) instead of in
 // front of them (attn_oproj.hip: the o_proj weight tile)
+// ONE: the head-parallel short-context launch (attn_head_kernel): one split, plain loads,
+// no epoch word (tickets untouched); g is then a QUERY head (NREP 1) and kvh its kv head.
 template <int DT, int HD, int NREP, bool FUSED = false, int NW = AttnGeom2<NREP>::NW,
-          int PFD = 2, class Hook = NoHook>
+          int PFD = 2, class Hook = NoHook, bool ONE = false>
 __device__ __forceinline__ void attn2_decode_block(const AttnDecArgs& a, int g, int s,
-                                                   float* lds, int ng, const Hook& hook = Hook()) {
+                                                   float* lds, int ng, const Hook& hook = Hook(),
+                                                   int kvh = -1) {
   static_assert(PFD == 1 || PFD == 2, "prefetch depth 1 or 2");
   constexpr int DS = HD / 32;    // MFMA k-steps (A fragments) per key block
   constexpr int NCH = HD / 8;    // 8-dim chunks per row
@@ -130,8 +133,9 @@ __device__ __forceinline__ void attn2_decode_block(const AttnDecArgs& a, int g, 
   float* st = lds + NW * (kBlk * 16 + 16);         // end-of-split wave states
   unsigned long long stamp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   ATTN_STAMP(0);
-  const uint16_t* kgp = a.kc + (size_t)g * a.S * HD;
-  const uint16_t* vgp = a.vc + (size_t)g * a.S * HD;
+  const int kv = kvh < 0 ? g : kvh;
+  const uint16_t* kgp = a.kc + (size_t)kv * a.S * HD;
+  const uint16_t* vgp = a.vc + (size_t)kv * a.S * HD;
 
   // one block's operands: K A-fragments and V rows of this lane
   // PFD slots of one block's operands (slot index a compile-time constant everywhere)
@@ -206,10 +210,11 @@ __device__ __forceinline__ void attn2_decode_block(const AttnDecArgs& a, int g, 
     }
   }
   const int Tk = *a.pos + 1;
-  const unsigned int epoch = a.tickets[ng + g];  // this launch's granule tag - 1
+  unsigned int epoch = 0;
+  if constexpr (!ONE) epoch = a.tickets[ng + g];  // this launch's granule tag - 1
   ATTN_STAMP(1);
   int ns, kps;
-  if constexpr (FUSED) {
+  if constexpr (FUSED || ONE) {
     ns = 1;
     kps = (Tk + kBlk - 1) / kBlk * kBlk;
   } else {
@@ -356,11 +361,13 @@ __device__ __forceinline__ void attn2_decode_block(const AttnDecArgs& a, int g, 
       const int idx = tid + i * NT;
       if (idx < NOUT) a.out[(size_t)g * NOUT + idx] = from_f32<DT>(ao[i] / lo[i]);
     }
-    if (a.stamps != nullptr && tid == 0) {
-      unsigned long long* dd = a.stamps + ((size_t)s * ng + g) * 8;
-      for (int k = 0; k < 8; ++k) dd[k] = (k < 6 || k == 6) ? stamp[k] : 0ull;
+    if constexpr (!ONE) {
+      if (a.stamps != nullptr && tid == 0) {
+        unsigned long long* dd = a.stamps + ((size_t)s * ng + g) * 8;
+        for (int k = 0; k < 8; ++k) dd[k] = (k < 6 || k == 6) ? stamp[k] : 0ull;
+      }
+      if (tid == 0) a.tickets[ng + g] = epoch + 1u;
     }
-    if (tid == 0) a.tickets[ng + g] = epoch + 1u;
     return;
   }
   // Splits >= 1 publish their partial as 8-byte {value, tag} granules (one sc1 store

@@ -35,6 +35,9 @@ _SIGS = {
     "cake_head_select": [I, P, P, F, P, I, I, P, P, P, I, F, P, P, P, P, I, P, P, P],
     "cake_attn_decode": [I, P, P, P, P, I, I, I, I, F, P, P, P, P],
     "cake_attn_set_impl": [I],
+    "cake_attn_decode_heads": [I, P, P, P, P, I, I, I, I, F, P, P],
+    "cake_attn_set_heads": [I, I],
+    "cake_attn_heads_max": [],
     "cake_attn_set_target_splits": [I],
     "cake_attn_set_single_max": [I],
     "cake_attn_set_min_keys": [I],

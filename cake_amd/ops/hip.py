@@ -254,6 +254,27 @@ def attn_decode(q, kcache, vcache, pos, scale, part, tickets, out):
           "attn_decode")
 
 
+def attn_decode_heads(q, kcache, vcache, pos, scale, out, waves: int = 2):
+    """Head-parallel short-context decode attention (attention.hip attn_head_kernel): one
+    workgroup per query head, the whole live length as one split; no workspace."""
+    nkv, S, hd = kcache.shape
+    nh = q.numel() // hd
+    _req(q, "q", dtype=torch.float32)
+    _req(kcache, "kcache")
+    _req(vcache, "vcache", dtype=kcache.dtype, shape=kcache.shape)
+    _req(pos, "pos", dtype=torch.int32, numel=1)
+    _req(out, "out", dtype=kcache.dtype, numel=nh * hd)
+    if hd not in (64, 128) or nh % nkv:
+        raise ValueError(f"unsupported attention shape nh={nh} nkv={nkv} hd={hd}")
+    L = kernels()
+    prev = int(L.cake_attn_heads_max())
+    check(L.cake_attn_set_heads(max(prev, 1), int(waves)), "attn_set_heads")
+    check(L.cake_attn_decode_heads(_dt(kcache), _p(q), _p(kcache), _p(vcache), _p(pos), S, nh,
+                                   nkv, hd, float(scale), _p(out), _stream()),
+          "attn_decode_heads")
+    check(L.cake_attn_set_heads(prev, 2), "attn_set_heads")
+
+
 # ---------------------------------------------------------------------------
 # persistent decode (decode_mk.hip): every layer of one token in one launch
 # ---------------------------------------------------------------------------

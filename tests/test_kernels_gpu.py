@@ -143,6 +143,29 @@ def test_attn_decode(cuda, attn_impl, dt, nh, nkv, hd, pos, S, min_keys):
     torch.testing.assert_close(out.float(), ref, **_tol(dt))
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("nh,nkv,hd", [(32, 8, 128), (16, 16, 64), (8, 1, 128)])
+@pytest.mark.parametrize("pos", [0, 15, 16, 70, 127, 600])
+@pytest.mark.parametrize("waves", [1, 2, 4])
+def test_attn_decode_heads(cuda, dt, nh, nkv, hd, pos, waves):
+    """Head-parallel short-context attention (one workgroup per query head, one split)
+    vs f32 attention: block edges (16 / 17 keys), a ragged tail, and a long context it is
+    still correct for (601 keys walked by one workgroup)."""
+    from cake_amd.ops import hip as K_
+    torch.manual_seed(5)
+    S = 1000
+    kc = _rand(nkv, S, hd, dt=dt)
+    vc = _rand(nkv, S, hd, dt=dt)
+    q = torch.randn(nh * hd, device=cuda)
+    p = torch.tensor([pos], dtype=torch.int32, device=cuda)
+    out = torch.full((nh * hd,), float("nan"), device=cuda, dtype=dt)
+    K_.attn_decode_heads(q, kc, vc, p, 1 / math.sqrt(hd), out, waves=waves)
+    Tk = pos + 1
+    ref = R.attention(q.view(1, nh, hd), kc[:, :Tk].transpose(0, 1), vc[:, :Tk].transpose(0, 1),
+                      pos).reshape(-1)
+    torch.testing.assert_close(out.float(), ref, **_tol(dt))
+
+
 def test_attn_decode_merge_timeout_raises(cuda):
     """Core 2's split 0 spins on the other splits' partials: if they never arrive, the
     bounded poll must end the launch and raise the error word (not merge stale partials
