@@ -281,8 +281,11 @@ __device__ __forceinline__ uint32_t cvt_pk(float lo, float hi) {
     const __bf16 a = (__bf16)lo, b = (__bf16)hi;
     return (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
   } else {
-    const _Float16 a = (_Float16)lo, b = (_Float16)hi;
-    return (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
+    // the two-element vector form lowers to one v_cvt_pk_f16_f32 (RNE); two scalar
+    // casts + shift/or took three instructions per pair
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    const h2 v = {(_Float16)lo, (_Float16)hi};
+    return __builtin_bit_cast(uint32_t, v);
   }
 }
 
@@ -349,19 +352,31 @@ __global__ __launch_bounds__(64 * NW, 2) void flash2_fwd_kernel(FlashArgs a) {
   }
   const int ntiles = (kend + 63) / 64;
 
-  // staging: pair pi -> keys 2*(pi / NCH) + {0,1}, chunk pi % NCH
+  // staging: pair pi -> keys 2*(pi / NCH) + {0,1}, chunk pi % NCH.  Per-thread element
+  // offsets of tile 0 are computed once; a tile adds the wave-uniform j * 64 rows.
   uint4 kr[NPR][2], vr[NPR][2];
+  long long koff[NPR], voff[NPR];
+  int krow[NPR];
+  bool cok[NPR];
+#pragma unroll
+  for (int i = 0; i < NPR; ++i) {
+    const int pi = tid + NT * i, kp = pi / NCH, c = pi - kp * NCH;
+    krow[i] = 2 * kp;
+    cok[i] = c * 8 < a.D;
+    koff[i] = (long long)(2 * kp) * a.k_sn + c * 8;
+    voff[i] = (long long)(2 * kp) * a.v_sn + c * 8;
+  }
   auto gload = [&](int j) {
+    const uint16_t* kj = kb + (long long)j * 64 * a.k_sn;
+    const uint16_t* vj = vb + (long long)j * 64 * a.v_sn;
 #pragma unroll
     for (int i = 0; i < NPR; ++i) {
-      const int pi = tid + NT * i, kp = pi / NCH, c = pi - kp * NCH;
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
-        const int key = j * 64 + 2 * kp + e;
-        const bool ok = key < a.M && c * 8 < a.D;
-        kr[i][e] = ok ? *reinterpret_cast<const uint4*>(kb + (long long)key * a.k_sn + c * 8)
+        const bool ok = j * 64 + krow[i] + e < a.M && cok[i];
+        kr[i][e] = ok ? *reinterpret_cast<const uint4*>(kj + koff[i] + e * a.k_sn)
                       : make_uint4(0, 0, 0, 0);
-        vr[i][e] = ok ? *reinterpret_cast<const uint4*>(vb + (long long)key * a.v_sn + c * 8)
+        vr[i][e] = ok ? *reinterpret_cast<const uint4*>(vj + voff[i] + e * a.v_sn)
                       : make_uint4(0, 0, 0, 0);
       }
     }
@@ -393,25 +408,39 @@ __global__ __launch_bounds__(64 * NW, 2) void flash2_fwd_kernel(FlashArgs a) {
   for (int j = j0; j < ntiles; ++j) {
     const int buf = (j - j0) & 1;
     const bool more = j + 1 < ntiles;
-    if (more) gload(j + 1);
     const uint16_t* Ks = Kb + buf * 64 * DP;
     const uint16_t* Vt = Vb + buf * DP * kVTS;
 
-    // ---- Sᵀ = K Qᵀ over two 32-key subtiles
+    // ---- Sᵀ = K Qᵀ over two 32-key subtiles.  A subtile's K fragments are all read
+    // before its MFMAs (DP 64: both subtiles' up front): read -> wait -> MFMA per fragment
+    // exposed the LDS latency KS times per subtile.
     f32x16 s[2];
+    constexpr int KT = DP == 64 ? 2 : 1;  // subtiles whose fragments are read together
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
+    for (int t0 = 0; t0 < 2; t0 += KT) {
+      uint4 kf[KT][KS];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) s[t][r] = 0.f;
-      const int row = 32 * t + l32;
+      for (int u = 0; u < KT; ++u) {
+        const int row = 32 * (t0 + u) + l32;
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        const uint4 kf =
-            *reinterpret_cast<const uint4*>(Ks + row * DP + k_swz<DP>(row, 2 * ks + h) * 8);
-        s[t] = mfma32<DT>(kf, qf[ks], s[t]);
+        for (int ks = 0; ks < KS; ++ks)
+          kf[u][ks] =
+              *reinterpret_cast<const uint4*>(Ks + row * DP + k_swz<DP>(row, 2 * ks + h) * 8);
+      }
+      if constexpr (DP == 64) __builtin_amdgcn_sched_barrier(0);  // reads before the MFMAs
+#pragma unroll
+      for (int u = 0; u < KT; ++u) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[t0 + u][r] = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) s[t0 + u] = mfma32<DT>(kf[u][ks], qf[ks], s[t0 + u]);
       }
     }
 
+    // the next tile's global loads go out AFTER the QKᵀ MFMAs: issued at the top of the
+    // iteration, the first MFMA's wait (vmcnt(0), emitted by the compiler for the q
+    // registers) drained them at once and the prefetch hid nothing
+    if (more) gload(j + 1);
     // ---- online softmax; the row spans lanes l, l^32.  Scores stay raw (the
     // scale is folded into one fma per exp2); masking only on boundary tiles.
     const bool edge = j * 64 + 64 > a.M || (a.causal && j * 64 + 63 > qmin);
@@ -424,27 +453,35 @@ __global__ __launch_bounds__(64 * NW, 2) void flash2_fwd_kernel(FlashArgs a) {
           if (key >= a.M || (a.causal && key > qpos)) s[t][r] = -INFINITY;
         }
     }
-    float mt = -INFINITY;
+    // row max: four independent max chains, then the lane l / l^32 exchange on
+    // permlane32_swap (no LDS round trip as with ds_bpermute)
+    float mq[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) mt = fmaxf(mt, s[t][r]);
-    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+      for (int r = 0; r < 16; ++r) mq[r & 3] = fmaxf(mq[r & 3], s[t][r]);
+    float mt = fmaxf(fmaxf(mq[0], mq[1]), fmaxf(mq[2], mq[3]));
+    {
+      const int bi = __builtin_bit_cast(int, mt);
+      const auto sw = __builtin_amdgcn_permlane32_swap(bi, bi, false, false);
+      mt = fmaxf(__builtin_bit_cast(float, (int)sw[0]), __builtin_bit_cast(float, (int)sw[1]));
+    }
     // Deferred max (FA-style threshold): the running max moves only when a tile's max
     // exceeds it by more than 2^kDefer in probability units, so p stays <= 2^kDefer and
     // most tiles skip the O rescale (skipped when no lane of the wave moved its max).
     const bool grow = m == -INFINITY || (mt - m) * a.scale_log2 > kDefer;
     const float mn = grow ? fmaxf(m, mt) : m;  // raw-score units
     const float mc = mn == -INFINITY ? 0.f : mn * a.scale_log2;
-    float rs = 0.f;
+    float rq[4] = {0.f, 0.f, 0.f, 0.f};  // four independent row-sum chains
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const float p = __builtin_amdgcn_exp2f(fmaf(s[t][r], a.scale_log2, -mc));
         s[t][r] = p;
-        rs += p;
+        rq[r & 3] += p;
       }
+    const float rs = (rq[0] + rq[1]) + (rq[2] + rq[3]);
     if (__builtin_amdgcn_ballot_w64(grow) != 0ull) {
       const float alpha = __builtin_amdgcn_exp2f(m * a.scale_log2 - mc);  // m = -inf -> 0
       l *= alpha;
