@@ -273,6 +273,10 @@ def _want(a, name: str) -> bool:
 
 
 def _native(a) -> bool:
+    # the native engine's hops / all-reduces are the in-graph device IPC ones: a run that
+    # asks for the host-staged torch.distributed transports stays on the Python engines
+    if getattr(a, "hop", "ipc") == "dist" or getattr(a, "allreduce", "ipc") == "dist":
+        return False
     return a.engine == "native" and not a.cpu and not a.no_graph and a.dtype in ("bf16", "f16")
 
 
