@@ -502,26 +502,32 @@ class SdEngine {
     const bool guide = a.uncond != nullptr && a.guidance > 1.0f;
     if (cfg_.xl && (a.cond2 == nullptr || (guide && a.uncond2 == nullptr)))
       throw Error("xl / turbo need the second tokenizer's ids (cond2 / uncond2)");
+    const int bsize = std::max(1, a.bsize);
+    if (bsize > 64) throw Error("bsize above 64");
+    if (a.init_latents && bsize != 1) throw Error("img2img takes bsize 1");
     Schedule s = build_schedule(cfg_.sched, a.n_steps);
+    int first = 0;  // index in the full schedule of the first step run
     if (a.init_latents) {  // img2img: the steps from t_start on (pipeline.py t_start)
       const int t0 = std::max(0, std::min(a.t_start, a.n_steps));
       if (t0 >= a.n_steps) throw Error("img2img: no step left after t_start");
       s.first_scale = s.in_scale.empty() ? 1.0 : s.in_scale[t0];
       s.ts.erase(s.ts.begin(), s.ts.begin() + t0);
       s.coef.erase(s.coef.begin(), s.coef.begin() + t0);
+      first = t0;
     }
     const int n = (int)s.ts.size();
-    const int B2 = guide ? 2 : 1;
+    const int B2 = (guide ? 2 : 1) * bsize;  // UNet rows
+    ensure_rows(B2);
     const auto t0 = std::chrono::steady_clock::now();
-    // ---- text context [B2, 77, ctx]: rows [uncond; cond]
-    text_context(a.cond, a.uncond, a.cond2, a.uncond2, guide);
+    // ---- text context [B2, 77, ctx]: rows [uncond; cond] x bsize
+    text_context(a.cond, a.uncond, a.cond2, a.uncond2, guide, bsize);
     hook_ctx_.clear();  // ctx_ / the k|v caches now hold this generation's context
     precompute_kv(B2);
     hip_check(hipStreamSynchronize(st_), "sync");
     const auto t1 = std::chrono::steady_clock::now();
     // ---- latents, tables
     const int h = cfg_.height / 8, w = cfg_.width / 8;
-    const size_t nl = (size_t)4 * h * w;
+    const size_t nl1 = (size_t)4 * h * w, nl = nl1 * bsize;
     std::vector<float> x(nl);
     if (a.init_latents) {
       std::memcpy(x.data(), a.init_latents, nl * 4);
@@ -547,19 +553,38 @@ class SdEngine {
     // ---- denoise: step 0 eager, then one graph replay per step
     std::vector<hipEvent_t> ev(2 * n);
     for (auto& e : ev) hip_check(hipEventCreate(&e), "event");
-    const auto key = std::make_tuple(guide, a.guidance);
-    for (int i = 0; i < n; ++i) {
-      hip_check(hipEventRecord(ev[2 * i], st_), "event");
-      if (i == 0 || !a.use_graph) {
-        step_body(B2, guide, a.guidance);
-      } else {
-        auto it = graphs_.find(key);
-        if (it == graphs_.end()) it = graphs_.emplace(key, capture_step(B2, guide, a.guidance)).first;
-        hip_check(hipGraphLaunch(it->second.exec, st_), "hipGraphLaunch");
+    const auto key = std::make_tuple(guide, a.guidance, B2);
+    const size_t img_bytes = (size_t)cfg_.height * cfg_.width * 3;
+    std::vector<uint8_t> mid;  // intermediary images (host)
+    double mid_s = 0.0;
+    try {
+      for (int i = 0; i < n; ++i) {
+        hip_check(hipEventRecord(ev[2 * i], st_), "event");
+        if (i == 0 || !a.use_graph) {
+          step_body(B2, guide, a.guidance);
+        } else {
+          auto it = graphs_.find(key);
+          if (it == graphs_.end())
+            it = graphs_.emplace(key, capture_step(B2, guide, a.guidance)).first;
+          hip_check(hipGraphLaunch(it->second.exec, st_), "hipGraphLaunch");
+        }
+        hip_check(hipEventRecord(ev[2 * i + 1], st_), "event");
+        // the reference decodes the latents after step i when i % intermediary == 0
+        // (sd.rs intermediary_images; pipeline.py _steps_eager / on_step)
+        if (a.intermediary > 0 && a.on_image && (first + i) % a.intermediary == 0) {
+          const auto m0 = std::chrono::steady_clock::now();
+          mid.resize(img_bytes * bsize);
+          decode_images(bsize, mid.data());
+          a.on_image(a.cb_ctx, first + i, bsize, mid.data());
+          mid_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - m0).count();
+        }
       }
-      hip_check(hipEventRecord(ev[2 * i + 1], st_), "event");
+      hip_check(hipStreamSynchronize(st_), "sync");
+    } catch (...) {
+      (void)hipStreamSynchronize(st_);
+      for (auto& e : ev) (void)hipEventDestroy(e);
+      throw;
     }
-    hip_check(hipStreamSynchronize(st_), "sync");
     const auto t2 = std::chrono::steady_clock::now();
     for (int i = 0; i < n; ++i) {
       float ms = 0;
@@ -569,25 +594,35 @@ class SdEngine {
     for (auto& e : ev) (void)hipEventDestroy(e);
     if (lat_out) hip_check(hipMemcpy(lat_out, x_, nl * 4, hipMemcpyDeviceToHost), "D2H latents");
     // ---- decode
-    vae_a_.reset();
-    uint16_t* z = new16(vae_a_, nl);
-    k_check(cake_scale_copy(dt_, x_, (long long)nl, (float)(1.0 / cfg_.vae_scale), 0, z, st_),
-            "scale_copy");
-    uint8_t* img8 = nullptr;
-    const uint16_t* img = vae_decode(z);
-    img8 = static_cast<uint8_t*>(vae_a_.alloc((size_t)cfg_.height * cfg_.width * 3));
-    k_check(cake_to_rgb8(dt_, img, 1, cfg_.height, cfg_.width, 0, img8, st_), "to_rgb8");
-    hip_check(hipMemcpyAsync(rgb, img8, (size_t)cfg_.height * cfg_.width * 3,
-                             hipMemcpyDeviceToHost, st_), "D2H image");
-    hip_check(hipStreamSynchronize(st_), "sync");
+    decode_images(bsize, rgb);
     const auto t3 = std::chrono::steady_clock::now();
     if (res) {
       res->width = cfg_.width;
       res->height = cfg_.height;
       res->n_steps = n;
       res->text_s = std::chrono::duration<double>(t1 - t0).count();
-      res->denoise_s = std::chrono::duration<double>(t2 - t1).count();
+      res->denoise_s = std::chrono::duration<double>(t2 - t1).count() - mid_s;
       res->vae_s = std::chrono::duration<double>(t3 - t2).count();
+    }
+  }
+
+  // the current latents x_ ([bsize, 4, h, w] f32) -> bsize RGB images on the host
+  // ([bsize, height, width, 3] u8), one VAE decode per image
+  void decode_images(int bsize, uint8_t* rgb) {
+    const int h = cfg_.height / 8, w = cfg_.width / 8;
+    const size_t nl1 = (size_t)4 * h * w;
+    const size_t img_bytes = (size_t)cfg_.height * cfg_.width * 3;
+    for (int b = 0; b < bsize; ++b) {
+      vae_a_.reset();
+      uint16_t* z = new16(vae_a_, nl1);
+      k_check(cake_scale_copy(dt_, x_ + b * nl1, (long long)nl1, (float)(1.0 / cfg_.vae_scale), 0,
+                              z, st_), "scale_copy");
+      const uint16_t* img = vae_decode(z);
+      uint8_t* img8 = static_cast<uint8_t*>(vae_a_.alloc(img_bytes));
+      k_check(cake_to_rgb8(dt_, img, 1, cfg_.height, cfg_.width, 0, img8, st_), "to_rgb8");
+      hip_check(hipMemcpyAsync(rgb + b * img_bytes, img8, img_bytes, hipMemcpyDeviceToHost, st_),
+                "D2H image");
+      hip_check(hipStreamSynchronize(st_), "sync");  // the VAE arena is reused next
     }
   }
 
@@ -610,7 +645,8 @@ class SdEngine {
   void unet_component(const float* sample, int B, float t, const float* ctx, float* out) {
     hip_check(hipSetDevice(dev_), "hipSetDevice");
     need(1, "unet");
-    if (B < 1 || B > 2) throw Error("unet hook: batch 1 or 2");
+    if (B < 1 || B > 128) throw Error("unet hook: batch 1..128");
+    ensure_rows(B);
     const int h = cfg_.height / 8, w = cfg_.width / 8;
     const size_t n = (size_t)B * 4 * h * w, nc = (size_t)B * kTok * cfg_.ctx_dim();
     upload16(sample, n, inp_);
@@ -620,7 +656,7 @@ class SdEngine {
       precompute_kv(B);
     }
     hip_check(hipMemcpyAsync(ttab_, &t, 4, hipMemcpyHostToDevice, st_), "H2D");
-    HookGraph& hg = hook_[B - 1];
+    HookGraph& hg = hook_[B];
     if (hg.calls == 0 || hg.exec == nullptr) {
       if (hg.calls == 0) {
         unet_a_.reset();
@@ -681,6 +717,12 @@ class SdEngine {
     return p;
   }
   uint16_t* dalloc16(size_t n) { return static_cast<uint16_t*>(dalloc(n * 2)); }
+  void dfree(void* p) {
+    if (!p) return;
+    auto it = std::find(owned_.begin(), owned_.end(), p);
+    if (it != owned_.end()) owned_.erase(it);
+    (void)hipFree(p);
+  }
   uint16_t* new16(Arena& a, size_t n) { return static_cast<uint16_t*>(a.alloc(n * 2)); }
   float* new32(Arena& a, size_t n) { return static_cast<float*>(a.alloc(n * 4)); }
 
@@ -1141,12 +1183,45 @@ class SdEngine {
   void alloc_state() {
     const int h = cfg_.height / 8, w = cfg_.width / 8;
     const size_t nl = (size_t)4 * h * w;
-    x_ = static_cast<float*>(dalloc(nl * 4));
+    x_ = static_cast<float*>(dalloc(2 * nl * 4));
     inp_ = dalloc16(2 * nl);
     ctx_ = dalloc16((size_t)2 * kTok * cfg_.ctx_dim());
     seed_dev_ = dalloc(8);
     step_ = static_cast<int*>(dalloc(64));
     ensure_tables(1024);
+  }
+
+  // UNet rows the per-generation buffers hold (latents, UNet input, text context and the
+  // cross-attention k|v of every transformer block): grown for bsize > 1 / larger hook
+  // batches; the captured graphs point at the old buffers and are dropped
+  int rows_cap_ = 2;
+  void ensure_rows(int rows) {
+    if (rows <= rows_cap_) return;
+    hip_check(hipStreamSynchronize(st_), "sync");
+    drop_graphs();
+    hook_ctx_.clear();
+    const int h = cfg_.height / 8, w = cfg_.width / 8;
+    const size_t nl = (size_t)4 * h * w;
+    dfree(x_);
+    dfree(inp_);
+    dfree(ctx_);
+    x_ = static_cast<float*>(dalloc((size_t)rows * nl * 4));
+    inp_ = dalloc16((size_t)rows * nl);
+    ctx_ = dalloc16((size_t)rows * kTok * cfg_.ctx_dim());
+    auto grow = [&](TransformerW& t) {
+      for (auto& blk : t.blocks) {
+        dfree(blk.kv_cache);
+        blk.kv_cache = dalloc16((size_t)rows * kTok * 2 * t.ch);
+      }
+    };
+    if (parts_ & 1) {
+      for (auto& d : down_)
+        for (auto& t : d.att) grow(t);
+      grow(mid_att_);
+      for (auto& u : up_)
+        for (auto& t : u.att) grow(t);
+    }
+    rows_cap_ = rows;
   }
 
   void ensure_tables(int n) {
@@ -1530,8 +1605,9 @@ class SdEngine {
     unet_a_.reset();
     const uint16_t* pred = unet_forward(inp_, B2, ttab_, step_);
     const int h = cfg_.height / 8, w = cfg_.width / 8;
-    k_check(cake_sched_step(dt_, x_, pred, (long long)4 * h * w, guide ? 1 : 0, guidance, coef_,
-                            step_, seed_dev_, inp_, st_), "sched_step");
+    const long long nl = (long long)4 * h * w * (guide ? B2 / 2 : B2);
+    k_check(cake_sched_step(dt_, x_, pred, nl, guide ? 1 : 0, guidance, coef_, step_, seed_dev_,
+                            inp_, st_), "sched_step");
     k_check(cake_step_advance(step_, st_), "step_advance");
   }
 
@@ -1539,7 +1615,7 @@ class SdEngine {
     hipGraph_t g = nullptr;
     hipGraphExec_t exec = nullptr;
   };
-  std::map<std::tuple<bool, float>, Graph> graphs_;
+  std::map<std::tuple<bool, float, int>, Graph> graphs_;  // (guidance on, scale, UNet rows)
 
   Graph capture_step(int B2, bool guide, float guidance) {
     Graph gr;
@@ -1566,15 +1642,15 @@ class SdEngine {
     const uint16_t* out = nullptr;
     long calls = 0;
   };
-  HookGraph hook_[2];
+  std::map<int, HookGraph> hook_;  // by batch
   std::vector<float> hook_ctx_;
 
   void drop_graphs() {
-    for (auto& hg : hook_) {
-      if (hg.exec) (void)hipGraphExecDestroy(hg.exec);
-      if (hg.g) (void)hipGraphDestroy(hg.g);
-      hg = HookGraph{};
+    for (auto& kv : hook_) {
+      if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
+      if (kv.second.g) (void)hipGraphDestroy(kv.second.g);
     }
+    hook_.clear();
     for (auto& kv : graphs_) {
       if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
       if (kv.second.g) (void)hipGraphDestroy(kv.second.g);
@@ -1609,17 +1685,20 @@ class SdEngine {
     return layer_norm(A, x, T, D, cw.fw, cw.fb, (float)c.eps);
   }
 
-  // ctx_ rows [uncond; cond] (or [cond]) of [77, D1 (+ D2)]
+  // ctx_ rows [uncond; cond] (or [cond]) of [77, D1 (+ D2)], repeated bsize times as the
+  // reference's text_embeddings.repeat((bsize, 1, 1)) (sd.rs; pipeline.py text_emb)
   void text_context(const int32_t* cond, const int32_t* uncond, const int32_t* cond2,
-                    const int32_t* uncond2, bool guide) {
+                    const int32_t* uncond2, bool guide, int bsize = 1) {
     const int D1 = cfg_.clip.D, Dc = cfg_.ctx_dim();
+    const int per = guide ? 2 : 1;
     auto put = [&](const ClipW& cw, const int32_t* ids, int row, int col) {
       text_a_.reset();
       const uint16_t* y = clip_forward(cw, ids);
       const int D = cw.cfg.D;
-      hip_check(hipMemcpy2DAsync(ctx_ + (size_t)row * kTok * Dc + col, (size_t)Dc * 2, y,
-                                 (size_t)D * 2, (size_t)D * 2, kTok, hipMemcpyDeviceToDevice, st_),
-                "ctx copy");
+      for (int b = 0; b < bsize; ++b)
+        hip_check(hipMemcpy2DAsync(ctx_ + (size_t)(b * per + row) * kTok * Dc + col,
+                                   (size_t)Dc * 2, y, (size_t)D * 2, (size_t)D * 2, kTok,
+                                   hipMemcpyDeviceToDevice, st_), "ctx copy");
       hip_check(hipStreamSynchronize(st_), "sync");  // the text arena is reused next
     };
     const int rc = guide ? 1 : 0;

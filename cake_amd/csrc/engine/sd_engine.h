@@ -58,6 +58,17 @@ typedef struct CakeSdGenArgs {
   // encoded image, scaled and noised to ts[t_start] by the caller); null = txt2img
   int32_t t_start;
   const float* init_latents;
+  // images per sample (the reference's bsize): the UNet runs 2 bsize rows under guidance,
+  // the text rows repeated [uncond, cond] x bsize as the reference's
+  // text_embeddings.repeat((bsize, 1, 1)); init_noise then holds bsize latents, rgb /
+  // latents_out bsize images.  0 = 1.  img2img takes bsize 1.
+  int32_t bsize;
+  // intermediary images: every step index i (of the full schedule) with i % intermediary
+  // == 0 is decoded and handed to on_image(cb_ctx, i, bsize, rgb [bsize, height, width, 3])
+  // before the next step runs (0 / null: none)
+  int32_t intermediary;
+  void (*on_image)(void* cb_ctx, int32_t step, int32_t n_images, const uint8_t* rgb);
+  void* cb_ctx;
 } CakeSdGenArgs;
 
 typedef struct CakeSdResult {
@@ -67,8 +78,9 @@ typedef struct CakeSdResult {
 
 // Open (load or random-init) every component; null + err on failure.
 void* cake_sd_open(const char* model_dir, const CakeSdOpts* opts, char* err, int32_t errlen);
-// One image: rgb [height * width * 3] u8; latents_out (optional) [4 * h/8 * w/8] f32 (the
-// final latents); step_s (optional) [n_steps] seconds per step (device time).
+// One sample of bsize images: rgb [bsize * height * width * 3] u8; latents_out (optional)
+// [bsize * 4 * h/8 * w/8] f32 (the final latents); step_s (optional) [n_steps] seconds per
+// step (device time).
 int32_t cake_sd_generate(void* engine, const CakeSdGenArgs* args, uint8_t* rgb,
                          float* latents_out, double* step_s, CakeSdResult* result, char* err,
                          int32_t errlen);

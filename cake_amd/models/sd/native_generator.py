@@ -10,8 +10,10 @@ Python pipeline (models/sd/pipeline.py), so a seed gives the same image on eithe
 img2img runs natively too: the engine encodes the image (VAE encoder), the posterior
 sample, the latent scaling and the noise to the start step are drawn here with the same
 generators and torch ops as the Python pipeline, and the engine denoises from that step.
-Requests the engine does not cover — intermediary images, bsize > 1, tracing — run on the
-Python pipeline, built on first use.
+bsize > 1 (the UNet over 2 bsize rows, the reference's repeated text rows) and intermediary
+images (decoded by the engine between steps, handed back through a callback) are native;
+tracing (Chrome trace spans of the Python loop) and img2img with bsize > 1 run on the Python
+pipeline, built on first use.
 """
 from __future__ import annotations
 
@@ -112,13 +114,12 @@ class NativeSDGenerator(ImageGenerator):
 
     def generate_image(self, args: ImageGenerationArgs, callback: Callable[[list], None]) -> None:
         init = None
-        if args.img2img and not (args.intermediary_images or args.bsize != 1 or args.tracing):
+        if args.img2img and not (args.bsize != 1 or args.tracing):
             if not 0.0 <= args.img2img_strength <= 1.0:
                 raise ValueError("img2img-strength should be between 0 and 1, got "
                                  f"{args.img2img_strength}")
             init = self._encode_image(args.img2img)
-        if (args.img2img and init is None) or args.intermediary_images or args.bsize != 1 \
-                or args.tracing:
+        if (args.img2img and init is None) or args.tracing:
             gen = self._python()
             gen.generate_image(args, callback)
             self.last_step_s = list(getattr(gen, "last_step_s", []))
@@ -142,6 +143,14 @@ class NativeSDGenerator(ImageGenerator):
                 kw["uncond2"] = self._ids(self.tok2, self.pad_id2, args.uncond_prompt)
         log.info('Running with prompt "%s".', args.image_prompt)
         self.last_step_s = []
+        bsize = max(1, int(args.bsize))
+
+        def pil(rgb: np.ndarray) -> list:
+            rgb = rgb.reshape(-1, cfg.height, cfg.width, 3)
+            return [Image.fromarray(np.ascontiguousarray(x), "RGB") for x in rgb]
+        every = int(args.intermediary_images or 0)
+        mid = {"intermediary": every, "on_image": (lambda _step, rgb: callback(pil(rgb)))} \
+            if every > 0 else {}
         t_start = n_steps - int(n_steps * args.img2img_strength) if init is not None else 0
         for idx in range(args.num_samples):
             t0 = time.perf_counter()
@@ -162,13 +171,14 @@ class NativeSDGenerator(ImageGenerator):
                     continue
                 seed = int(torch.randint(0, 2 ** 62, (1,), generator=gen).item())
                 out = self.eng.generate(n_steps=n_steps, guidance=guidance, seed=seed,
-                                        init_latents=latents.cpu().numpy(), t_start=t_start, **kw)
+                                        init_latents=latents.cpu().numpy(), t_start=t_start,
+                                        **kw, **mid)
             else:
                 # the Python pipeline's draw order: latent noise, then the ancestral-noise key
-                noise = torch.randn((1, 4, cfg.height // 8, cfg.width // 8), generator=gen)
+                noise = torch.randn((bsize, 4, cfg.height // 8, cfg.width // 8), generator=gen)
                 seed = int(torch.randint(0, 2 ** 62, (1,), generator=gen).item())
                 out = self.eng.generate(n_steps=n_steps, guidance=guidance, seed=seed,
-                                        init_noise=noise.numpy(), **kw)
+                                        init_noise=noise.numpy(), bsize=bsize, **kw, **mid)
             self.last_result = out
             for k, dt in enumerate(out.step_s):
                 self.last_step_s.append(dt)
@@ -176,7 +186,7 @@ class NativeSDGenerator(ImageGenerator):
             log.info("sample %d/%d: text %.1f ms, denoise %.1f ms, vae %.1f ms (%.1f ms total)",
                      idx + 1, args.num_samples, out.text_s * 1e3, out.denoise_s * 1e3,
                      out.vae_s * 1e3, (time.perf_counter() - t0) * 1e3)
-            callback([Image.fromarray(out.rgb, "RGB")])
+            callback(pil(out.rgb))
 
 
 def native_sd_eligible(ctx) -> bool:

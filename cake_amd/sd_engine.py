@@ -38,7 +38,13 @@ class SdGenArgs(C.Structure):
                 ("cond2", C.POINTER(C.c_int32)), ("uncond2", C.POINTER(C.c_int32)),
                 ("n_steps", C.c_int32), ("guidance", C.c_float), ("seed", C.c_uint64),
                 ("init_noise", C.POINTER(C.c_float)), ("use_graph", C.c_int32),
-                ("t_start", C.c_int32), ("init_latents", C.POINTER(C.c_float))]
+                ("t_start", C.c_int32), ("init_latents", C.POINTER(C.c_float)),
+                ("bsize", C.c_int32), ("intermediary", C.c_int32),
+                ("on_image", C.c_void_p), ("cb_ctx", C.c_void_p)]
+
+
+# on_image(cb_ctx, step, n_images, rgb [n_images, H, W, 3])
+IMAGE_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_int32, C.c_int32, C.POINTER(C.c_uint8))
 
 
 class SdResult(C.Structure):
@@ -94,8 +100,9 @@ def _ip(a: np.ndarray | None):
 
 @dataclass
 class SdImage:
-    rgb: np.ndarray                      # [H, W, 3] u8
-    latents: np.ndarray                  # [4, H/8, W/8] f32 (final, before the VAE)
+    rgb: np.ndarray                      # [H, W, 3] u8 ([bsize, H, W, 3] when bsize > 1)
+    latents: np.ndarray                  # [4, H/8, W/8] f32 (final, before the VAE; batched
+                                         # likewise)
     step_s: list[float] = field(default_factory=list)
     text_s: float = 0.0
     denoise_s: float = 0.0
@@ -135,37 +142,56 @@ class NativeSD:
 
     def generate(self, cond, uncond=None, cond2=None, uncond2=None, n_steps: int = 30,
                  guidance: float = 7.5, seed: int = 0, init_noise=None,
-                 use_graph: bool = True, init_latents=None, t_start: int = 0) -> SdImage:
-        """One image from padded [77] id rows (uncond = None: no classifier-free
+                 use_graph: bool = True, init_latents=None, t_start: int = 0,
+                 bsize: int = 1, intermediary: int = 0, on_image=None) -> SdImage:
+        """One sample from padded [77] id rows (uncond = None: no classifier-free
         guidance; cond2 / uncond2: the second tokenizer's ids for xl / turbo).  img2img:
         init_latents [4, h, w] (the encoded image scaled and noised to the schedule's step
-        t_start) and the steps from t_start on."""
+        t_start) and the steps from t_start on.  bsize images per sample (init_noise then
+        [bsize, 4, h, w]); intermediary > 0: on_image(step, rgb [n, H, W, 3]) after every
+        step index divisible by it."""
         ids = [None if x is None else _ids(x).reshape(-1) for x in (cond, uncond, cond2, uncond2)]
         for x in ids:
             if x is not None and x.size != N_TOK:
                 raise ValueError(f"id rows must be {N_TOK} long")
+        bsize = max(1, int(bsize))
         noise = None if init_noise is None else _f32(init_noise).reshape(-1)
         h, w = self.height // 8, self.width // 8
-        if noise is not None and noise.size != 4 * h * w:
-            raise ValueError(f"init_noise must hold {4 * h * w} values")
+        if noise is not None and noise.size != 4 * h * w * bsize:
+            raise ValueError(f"init_noise must hold {4 * h * w * bsize} values")
         lat0 = None if init_latents is None else _f32(init_latents).reshape(-1)
         if lat0 is not None and lat0.size != 4 * h * w:
             raise ValueError(f"init_latents must hold {4 * h * w} values")
+        err_cb: list = []
+
+        def _cb(_ctx, step, n, ptr):
+            try:
+                arr = np.ctypeslib.as_array(ptr, shape=(n, self.height, self.width, 3)).copy()
+                on_image(int(step), arr)
+            except Exception as e:  # noqa: BLE001 - re-raised after the engine returns
+                err_cb.append(e)
+        cb = IMAGE_FN(_cb) if (on_image is not None and intermediary > 0) else None
         a = SdGenArgs(cond=_ip(ids[0]), uncond=_ip(ids[1]), cond2=_ip(ids[2]), uncond2=_ip(ids[3]),
                       n_steps=int(n_steps), guidance=float(guidance),
                       seed=int(seed) & 0xFFFFFFFFFFFFFFFF,
                       init_noise=None if noise is None else _fp(noise),
                       use_graph=1 if use_graph else 0, t_start=int(t_start),
-                      init_latents=None if lat0 is None else _fp(lat0))
+                      init_latents=None if lat0 is None else _fp(lat0), bsize=bsize,
+                      intermediary=int(intermediary) if cb is not None else 0,
+                      on_image=C.cast(cb, C.c_void_p) if cb is not None else None, cb_ctx=None)
         n_run = int(n_steps) - (max(0, int(t_start)) if lat0 is not None else 0)
-        rgb = np.empty((self.height, self.width, 3), dtype=np.uint8)
-        lat = np.empty((4, h, w), dtype=np.float32)
+        rgb = np.empty((bsize, self.height, self.width, 3), dtype=np.uint8)
+        lat = np.empty((bsize, 4, h, w), dtype=np.float32)
         steps = (C.c_double * max(1, n_run))()
         res = SdResult()
         err = C.create_string_buffer(1024)
         rc = lib().cake_sd_generate(self._h, C.byref(a), rgb.ctypes.data_as(C.POINTER(C.c_uint8)),
                                     _fp(lat), steps, C.byref(res), err, 1024)
         self._check(rc, err)
+        if err_cb:
+            raise err_cb[0]
+        if bsize == 1:
+            rgb, lat = rgb[0], lat[0]
         return SdImage(rgb, lat, [float(steps[i]) for i in range(n_run)], res.text_s,
                        res.denoise_s, res.vae_s)
 

@@ -307,3 +307,43 @@ def test_img2img_on_the_native_engine_matches_python(cuda, mini, tmp_path, monke
     b = np.asarray(ref[-1][0], dtype=np.int32)
     assert np.abs(a - b).mean() < 0.5 and np.abs(a - b).max() <= 8, (np.abs(a - b).mean(),
                                                                      np.abs(a - b).max())
+
+
+def test_bsize_and_intermediary_images_on_the_native_engine(cuda, mini, tmp_path, monkeypatch):
+    """bsize 2 (the UNet over 4 rows with the reference's repeated text rows) and an
+    intermediary image every second step, natively: the same callbacks (count, image
+    count per call) and images as the Python pipeline."""
+    from cake_amd.cli import build_parser
+    from cake_amd.context import Context
+    from cake_amd.master import _load_image
+    from cake_amd.models.sd.args import ImageGenerationArgs
+    from cake_amd.models.sd.native_generator import NativeSDGenerator
+    from cake_amd.sd_engine import NativeSD
+    v, cfg, d = mini
+    topo = tmp_path / "empty.yml"
+    topo.write_text("{}\n")
+    args = build_parser().parse_args(["--model", str(d), "--topology", str(topo), "--model-type",
+                                      "image-model", "--sd-version", v, "--dtype", "f16"])
+    ctx = Context.from_args(args)
+    native = _load_image(ctx)
+    assert isinstance(native, NativeSDGenerator)
+    native.eng.close()
+    native.eng = NativeSD(str(d), dtype="f16", autotune=False)
+    req = ImageGenerationArgs(image_prompt="a red cube", uncond_prompt="blurry", n_steps=4,
+                              image_seed=5, bsize=2, intermediary_images=2)
+    got = []
+    native.generate_image(req, lambda imgs: got.append(imgs))
+    assert native._fallback is None  # served natively
+    assert len(native.last_step_s) == 4
+    monkeypatch.setenv("CAKE_NATIVE", "0")
+    py = _load_image(ctx)
+    ref = []
+    py.generate_image(req, lambda imgs: ref.append(imgs))
+    # steps 0 and 2 (i % 2 == 0), then the final images
+    assert len(got) == len(ref) == 3 and all(len(x) == 2 for x in got + ref)
+    for g, r in zip(got, ref):
+        for gi, ri in zip(g, r):
+            a, b = np.asarray(gi, dtype=np.int32), np.asarray(ri, dtype=np.int32)
+            assert a.shape == b.shape == (cfg.height, cfg.width, 3)
+            assert np.abs(a - b).mean() < 0.5 and np.abs(a - b).max() <= 8, (
+                np.abs(a - b).mean(), np.abs(a - b).max())
