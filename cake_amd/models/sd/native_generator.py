@@ -10,10 +10,11 @@ Python pipeline (models/sd/pipeline.py), so a seed gives the same image on eithe
 img2img runs natively too: the engine encodes the image (VAE encoder), the posterior
 sample, the latent scaling and the noise to the start step are drawn here with the same
 generators and torch ops as the Python pipeline, and the engine denoises from that step.
-bsize > 1 (the UNet over 2 bsize rows, the reference's repeated text rows) and intermediary
-images (decoded by the engine between steps, handed back through a callback) are native;
-tracing (Chrome trace spans of the Python loop) and img2img with bsize > 1 run on the Python
-pipeline, built on first use.
+bsize > 1 (the UNet over 2 bsize rows, the reference's repeated text rows), intermediary
+images (decoded by the engine between steps, handed back through a callback) and tracing
+(the Chrome trace spans — text embeddings, every step, VAE decode — rebuilt from the
+engine's own phase and per-step device timings) are native; img2img with bsize > 1 runs on
+the Python pipeline, built on first use.
 """
 from __future__ import annotations
 
@@ -91,7 +92,8 @@ class NativeSDGenerator(ImageGenerator):
 
     def _python(self) -> ImageGenerator:
         if self._fallback is None:
-            log.info("request needs the Python pipeline (img2img / intermediary images / bsize)")
+            log.info("request needs the Python pipeline (img2img at bsize > 1, or an image of "
+                     "another size)")
             self._fallback = self._fallback_factory()
         return self._fallback
 
@@ -114,12 +116,12 @@ class NativeSDGenerator(ImageGenerator):
 
     def generate_image(self, args: ImageGenerationArgs, callback: Callable[[list], None]) -> None:
         init = None
-        if args.img2img and not (args.bsize != 1 or args.tracing):
+        if args.img2img and args.bsize == 1:
             if not 0.0 <= args.img2img_strength <= 1.0:
                 raise ValueError("img2img-strength should be between 0 and 1, got "
                                  f"{args.img2img_strength}")
             init = self._encode_image(args.img2img)
-        if (args.img2img and init is None) or args.tracing:
+        if args.img2img and init is None:
             gen = self._python()
             gen.generate_image(args, callback)
             self.last_step_s = list(getattr(gen, "last_step_s", []))
@@ -152,6 +154,10 @@ class NativeSDGenerator(ImageGenerator):
         mid = {"intermediary": every, "on_image": (lambda _step, rgb: callback(pil(rgb)))} \
             if every > 0 else {}
         t_start = n_steps - int(n_steps * args.img2img_strength) if init is not None else 0
+        trace = None
+        if args.tracing:
+            from ...utils.trace import ChromeTrace
+            trace = ChromeTrace()
         for idx in range(args.num_samples):
             t0 = time.perf_counter()
             if init is not None:  # pipeline.py's img2img latents, same draws and ops
@@ -180,6 +186,16 @@ class NativeSDGenerator(ImageGenerator):
                 out = self.eng.generate(n_steps=n_steps, guidance=guidance, seed=seed,
                                         init_noise=noise.numpy(), bsize=bsize, **kw, **mid)
             self.last_result = out
+            if trace is not None:  # the pipeline's spans, from the engine's timings
+                t_end = time.perf_counter()
+                ts0 = t_end - (out.text_s + out.denoise_s + out.vae_s)
+                trace.add("text_embeddings", ts0, ts0 + out.text_s)
+                cur = ts0 + out.text_s
+                trace.add(f"denoise {len(out.step_s)} steps", cur, cur + out.denoise_s)
+                for k, dt in enumerate(out.step_s):
+                    trace.add(f"step {t_start + k + 1}", cur, cur + dt, device_s=dt)
+                    cur += dt
+                trace.add("vae_decode", t_end - out.vae_s, t_end, images=bsize)
             for k, dt in enumerate(out.step_s):
                 self.last_step_s.append(dt)
                 log.info("step %d/%d done, %.2fs", t_start + k + 1, n_steps, dt)
@@ -187,6 +203,11 @@ class NativeSDGenerator(ImageGenerator):
                      idx + 1, args.num_samples, out.text_s * 1e3, out.denoise_s * 1e3,
                      out.vae_s * 1e3, (time.perf_counter() - t0) * 1e3)
             callback(pil(out.rgb))
+        if trace is not None:
+            from pathlib import Path
+            path = Path(f"trace-{int(time.time() * 1000)}.json")
+            trace.save(path)
+            log.info("wrote chrome trace %s", path)
 
 
 def native_sd_eligible(ctx) -> bool:

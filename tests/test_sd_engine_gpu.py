@@ -347,3 +347,35 @@ def test_bsize_and_intermediary_images_on_the_native_engine(cuda, mini, tmp_path
             assert a.shape == b.shape == (cfg.height, cfg.width, 3)
             assert np.abs(a - b).mean() < 0.5 and np.abs(a - b).max() <= 8, (
                 np.abs(a - b).mean(), np.abs(a - b).max())
+
+
+def test_native_engine_writes_the_chrome_trace(cuda, mini, tmp_path, monkeypatch):
+    """--sd-tracing on the native engine: a Chrome trace with the pipeline's spans (text
+    embeddings, one per step, VAE decode) from the engine's timings, no Python fallback."""
+    import json
+
+    from cake_amd.cli import build_parser
+    from cake_amd.context import Context
+    from cake_amd.master import _load_image
+    from cake_amd.models.sd.args import ImageGenerationArgs
+    from cake_amd.models.sd.native_generator import NativeSDGenerator
+    v, cfg, d = mini
+    if v != "v1-5":
+        pytest.skip("one version covers the trace plumbing")
+    topo = tmp_path / "empty.yml"
+    topo.write_text("{}\n")
+    args = build_parser().parse_args(["--model", str(d), "--topology", str(topo), "--model-type",
+                                      "image-model", "--sd-version", v, "--dtype", "f16"])
+    native = _load_image(Context.from_args(args))
+    assert isinstance(native, NativeSDGenerator)
+    monkeypatch.chdir(tmp_path)
+    got = []
+    native.generate_image(ImageGenerationArgs(image_prompt="a red cube", n_steps=3, image_seed=2,
+                                              tracing=True), lambda imgs: got.append(imgs))
+    assert native._fallback is None and len(got) == 1
+    traces = list(tmp_path.glob("trace-*.json"))
+    assert len(traces) == 1
+    names = [e["name"] for e in json.loads(traces[0].read_text())["traceEvents"]]
+    assert "text_embeddings" in names and "vae_decode" in names
+    assert [n for n in names if n.startswith("step ")] == ["step 1", "step 2", "step 3"]
+    native.eng.close()
