@@ -168,6 +168,17 @@ __global__ __launch_bounds__(256) void layernorm_wave_kernel(const uint16_t* __r
   const uint16_t* xr = x + row * C;
   float v[CPL][8];
   float s = 0.f;
+  // gamma / beta requested with the row: loaded after the two reductions they put a
+  // further memory round trip on every row's critical path
+  uint4 gq[CPL], bq[CPL];
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nch) {
+      gq[i] = *reinterpret_cast<const uint4*>(gamma + c * 8);
+      bq[i] = *reinterpret_cast<const uint4*>(beta + c * 8);
+    }
+  }
 #pragma unroll
   for (int i = 0; i < CPL; ++i) {
     const int c = lane + 64 * i;
@@ -196,8 +207,8 @@ __global__ __launch_bounds__(256) void layernorm_wave_kernel(const uint16_t* __r
     const int c = lane + 64 * i;
     if (c >= nch) continue;
     float g[8], b[8];
-    unpack8<DT>(*reinterpret_cast<const uint4*>(gamma + c * 8), g);
-    unpack8<DT>(*reinterpret_cast<const uint4*>(beta + c * 8), b);
+    unpack8<DT>(gq[i], g);
+    unpack8<DT>(bq[i], b);
     uint16_t o[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = from_f32<DT>((v[i][e] - mean) * rstd * g[e] + b[e]);
