@@ -1,0 +1,25 @@
+#!/bin/bash
+# GPU box, round 5 (v): flash2 head dim 64 — V fragments read ahead of the softmax.
+# Flash tests, SD flash shapes and the SDXL step, previous commit (ab/) vs this tree.
+set -u
+cd "$GRAFT_REPO_ROOT"; OUT=gpurun_out/r5v; mkdir -p $OUT
+export HSA_ENABLE_IPC_MODE_LEGACY=0 PYTHONUNBUFFERED=1
+run() { local name=$1 t=$2; shift 2; timeout -k 10 $t "$@" > $OUT/$name.log 2>&1; local rc=$?; echo "== $name rc=$rc"; [[ $rc -eq 0 ]] || { tail -30 $OUT/$name.log; exit $rc; }; }
+run ft 300 python -u -m pytest tests/test_sd_kernels_gpu.py -k "flash" -x -q --timeout 200 --timeout-method thread
+tail -1 $OUT/ft.log
+for v in old new; do
+  if [[ $v == old ]]; then export CAKE_KERNEL_LIB=$PWD/ab/libcake_kernels_old.so; else unset CAKE_KERNEL_LIB; fi
+  run fl_$v 300 python scripts/bench_flash_split.py
+  cat $OUT/fl_$v.log | python -c "import sys,json
+for l in sys.stdin:
+    if l.startswith('{'):
+        r=json.loads(l); print(r['shape'], r['ks0_us'], r['ks0_tflops'])"
+done
+for v in old new old new; do
+  if [[ $v == old ]]; then export CAKE_KERNEL_LIB=$PWD/ab/libcake_kernels_old.so; else unset CAKE_KERNEL_LIB; fi
+  run sd_$v 300 python scripts/bench_sd.py --version xl --denoise --graph --steps 6
+  grep '^{' $OUT/sd_$v.log | python -c "import sys,json; r=json.loads(sys.stdin.read()); print('$v', r['value'], min(r['per_step_s']))"
+done
+unset CAKE_KERNEL_LIB
+run pf 300 python scripts/bench_prefill.py --lens 256,2048 --reps 3
+grep prompt_len $OUT/pf.log
