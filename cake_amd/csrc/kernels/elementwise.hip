@@ -95,6 +95,47 @@ __global__ void rope_kv_kernel(uint16_t* __restrict__ q, const uint16_t* __restr
   }
 }
 
+// Same, 8 elements per item with 16-byte accesses (hd % 16 == 0, 16-byte aligned rows and
+// bases): per token, nh + nkv rope items of half/8 vectors each (the a / b halves of a
+// head loaded and stored as whole 16-byte rows), then nkv * hd/8 V copies.  The scalar
+// form moved 2-byte elements one pair per thread per iteration (18 us per 2048-token
+// layer of 8B prefill).
+template <int DT>
+__global__ __launch_bounds__(256) void rope_kv_vec_kernel(
+    uint16_t* __restrict__ q, const uint16_t* __restrict__ k, const uint16_t* __restrict__ v,
+    int ldq, int ld, int nh, int nkv, int hd, const float* __restrict__ inv_freq, int pos0, int S,
+    uint16_t* __restrict__ kc, uint16_t* __restrict__ vc) {
+  const int t = blockIdx.x, pos = pos0 + t, half = hd >> 1, hv = half >> 3;
+  const int nrope = (nh + nkv) * hv, nv = nkv * (hd >> 3);
+  for (int p = threadIdx.x; p < nrope + nv; p += blockDim.x) {
+    if (p < nrope) {
+      const int head = p / hv, i0 = (p - head * hv) * 8;
+      const bool isq = head < nh;
+      const int hh = isq ? head : head - nh;
+      const uint16_t* src = isq ? q + (size_t)t * ldq + hh * hd : k + (size_t)t * ld + hh * hd;
+      float a[8], b[8];
+      unpack8<DT>(*reinterpret_cast<const uint4*>(src + i0), a);
+      unpack8<DT>(*reinterpret_cast<const uint4*>(src + i0 + half), b);
+      uint16_t oa[8], ob[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float sn, cs;
+        sincosf((float)pos * inv_freq[i0 + e], &sn, &cs);
+        oa[e] = from_f32<DT>(a[e] * cs - b[e] * sn);
+        ob[e] = from_f32<DT>(a[e] * sn + b[e] * cs);
+      }
+      uint16_t* dst = isq ? q + (size_t)t * ldq + hh * hd : kc + ((size_t)hh * S + pos) * hd;
+      *reinterpret_cast<uint4*>(dst + i0) = *reinterpret_cast<const uint4*>(oa);
+      *reinterpret_cast<uint4*>(dst + i0 + half) = *reinterpret_cast<const uint4*>(ob);
+    } else {
+      const int pp = p - nrope, per = hd >> 3;
+      const int head = pp / per, c = (pp - head * per) * 8;
+      *reinterpret_cast<uint4*>(vc + ((size_t)head * S + pos) * hd + c) =
+          *reinterpret_cast<const uint4*>(v + (size_t)t * ld + head * hd + c);
+    }
+  }
+}
+
 // act = silu(g) * u   (16-bit in/out), gu = [T, 2, I] packed or separate.
 template <int DT>
 __global__ void silu_mul_kernel(const uint16_t* __restrict__ g, const uint16_t* __restrict__ u,
@@ -337,6 +378,15 @@ CAKE_API int cake_rmsnorm(int dt, const float* x, const void* w, float eps, int 
 CAKE_API int cake_rope_kv(int dt, void* q, const void* k, const void* v, int ldq, int ld, int T, int nh,
                           int nkv, int hd, const float* inv_freq, int pos0, int S, void* kc,
                           void* vc, hipStream_t st) {
+  const bool vec = hd % 16 == 0 && ldq % 8 == 0 && ld % 8 == 0 &&
+                   ((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)kc | (uintptr_t)vc) % 16 == 0;
+  if (vec) {
+    DISPATCH_DT(dt, hipLaunchKernelGGL((rope_kv_vec_kernel<DT>), dim3(T), dim3(256), 0, st,
+                                       (uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, ldq,
+                                       ld, nh, nkv, hd, inv_freq, pos0, S, (uint16_t*)kc,
+                                       (uint16_t*)vc));
+    return (int)hipGetLastError();
+  }
   DISPATCH_DT(dt, hipLaunchKernelGGL((rope_kv_kernel<DT>), dim3(T), dim3(256), 0, st,
                                      (uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, ldq, ld, nh,
                                      nkv, hd, inv_freq, pos0, S, (uint16_t*)kc,

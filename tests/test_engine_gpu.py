@@ -633,3 +633,43 @@ def test_native_api_serving_over_tcp_workers(cuda, ckpt, tmp_path):
         w.communicate()
     assert want["choices"][0]["message"]["content"]
     assert got["choices"][0]["message"]["content"] == want["choices"][0]["message"]["content"]
+
+
+def test_native_master_fails_loudly_when_a_worker_dies(cuda, ckpt, tmp_path):
+    """Failure detection on the native master's TCP client: a generation through a live
+    worker succeeds; after the worker is killed the next generation raises (connection
+    error or the remote timeout) instead of hanging or emitting tokens."""
+    import os
+    import subprocess
+    import time
+
+    from cake_amd.engine import NativeLlama
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cli = os.path.join(root, "cake_amd", "lib", "cake-cli")
+    port = _port()
+    topo = tmp_path / "topology.yml"
+    topo.write_text(f"w1:\n  host: '127.0.0.1:{port}'\n  layers:\n    - 'model.layers.1'\n")
+    env = dict(os.environ, CAKE_LOG="warning")
+    w = subprocess.Popen([cli, "--mode", "worker", "--name", "w1", "--model", str(ckpt),
+                          "--topology", str(topo), "--address", f"127.0.0.1:{port}",
+                          "--max-seq-len", "256"], cwd=root, env=env,
+                         stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+    eng = None
+    try:
+        _wait_listen(w, port, "worker w1")
+        eng = NativeLlama(ckpt, max_seq=256, dtype="bf16", workers=[f"127.0.0.1:{port}"],
+                          worker_of=[-1, 0, -1], remote_timeout_s=10.0)
+        ok = eng.generate(PROMPT, 6, repeat_penalty=1.0).tokens
+        assert len(ok) == 6
+        w.kill()
+        w.wait(timeout=30)
+        t0 = time.time()
+        with pytest.raises(RuntimeError):
+            eng.generate(PROMPT, 6, repeat_penalty=1.0)
+        assert time.time() - t0 < 60
+    finally:
+        if eng is not None:
+            eng.close()
+        if w.poll() is None:
+            w.kill()
+        w.communicate()
