@@ -78,13 +78,6 @@ int cake_attn_set_split_cap(int cap);
 int cake_attn_set_heads(int max_keys, int waves);
 int cake_attn_decode_heads(int dt, const float* q, const void* kc, const void* vc, const int* pos,
                            int S, int nh, int nkv, int hd, float scale, void* out, hipStream_t st);
-int cake_attn_oproj_supported(int nh, int nkv, int hd, int H);
-long long cake_attn_oproj_ws_floats(int nkv, int H);
-long long cake_attn_oproj_ticket_words(int nkv, int H);
-int cake_attn_oproj(int dt, const float* q, const void* kc, const void* vc, const int* pos, int S,
-                    int nh, int nkv, int hd, float scale, const void* wo, int ldw, int H,
-                    float* out, int accumulate, float* ws, unsigned int* tickets,
-                    unsigned int* err, hipStream_t st);
 int cake_attn_splits(int Tk);
 int cake_attn_max_split(int S);
 int cake_gemv_x16(int dt, const void* x, const void* w, int K, int N, float* out, int accumulate,
@@ -133,6 +126,33 @@ int cake_hop_recv(const void* inbox, int H, int nhdr, int bf16, float* dst, unsi
 
 namespace cake {
 namespace {
+
+// Entry points of csrc/experimental/attn_oproj.hip, found in the loaded kernel library
+// (the one that holds cake_attn_decode) when it was built with CAKE_BUILD_EXPERIMENTAL=1;
+// all null otherwise.
+struct AoFns {
+  int (*supported)(int, int, int, int) = nullptr;
+  long long (*ws_floats)(int, int) = nullptr;
+  long long (*ticket_words)(int, int) = nullptr;
+  int (*run)(int, const float*, const void*, const void*, const int*, int, int, int, int, float,
+             const void*, int, int, float*, int, float*, unsigned int*, unsigned int*,
+             hipStream_t) = nullptr;
+};
+
+AoFns ao_fns() {
+  AoFns f;
+  Dl_info info;
+  if (!dladdr(reinterpret_cast<void*>(&cake_attn_decode), &info) || !info.dli_fname) return f;
+  void* h = dlopen(info.dli_fname, RTLD_LAZY | RTLD_NOLOAD);
+  if (!h) return f;
+  f.supported = reinterpret_cast<decltype(f.supported)>(dlsym(h, "cake_attn_oproj_supported"));
+  f.ws_floats = reinterpret_cast<decltype(f.ws_floats)>(dlsym(h, "cake_attn_oproj_ws_floats"));
+  f.ticket_words =
+      reinterpret_cast<decltype(f.ticket_words)>(dlsym(h, "cake_attn_oproj_ticket_words"));
+  f.run = reinterpret_cast<decltype(f.run)>(dlsym(h, "cake_attn_oproj"));
+  if (!f.supported || !f.ws_floats || !f.ticket_words || !f.run) f = AoFns{};
+  return f;
+}
 
 constexpr int kHeadSelectMaxLastN = 256;  // gemv.hip head_select window bound
 constexpr int kAttnMaxSplit = 64;         // attention.hip kMaxSplit
@@ -715,6 +735,9 @@ class Llama {
   bool forced_ = false;  // teacher-forcing steps: the head writes full logits
   // fused decode attention + o_proj (attn_oproj.hip) for one-split live lengths: the
   // short-context graph bucket and eager steps at such a position
+  // fused attention + o_proj (csrc/experimental/attn_oproj.hip, CAKE_BUILD_EXPERIMENTAL=1;
+  // measured slower than the pair: profiles/r5_attn_oproj_ab.md), looked up at run time
+  AoFns ao_;
   bool ao_ok_ = false, short_step_ = false;
   int heads_max_ = 0;  // live lengths <= this: head-parallel attention (attn_head_kernel)
   float* ao_ws_ = nullptr;
@@ -1025,7 +1048,8 @@ class Llama {
     // MI355X (profiles/r5_attn_oproj_ab.md), kept for the A/B
     {
       const char* e = std::getenv("CAKE_ATTN_OPROJ");
-      ao_ok_ = e && std::string(e) == "1" && cake_attn_oproj_supported(c.nh, c.nkv, c.hd, c.H) != 0;
+      if (e && std::string(e) == "1") ao_ = ao_fns();
+      ao_ok_ = ao_.run != nullptr && ao_.supported(c.nh, c.nkv, c.hd, c.H) != 0;
     }
     // CAKE_ATTN_HEADS=<max keys>[:<waves>]: the head-parallel short-context attention
     if (!ao_ok_) {
@@ -1035,8 +1059,8 @@ class Llama {
       if (mx > 0 && cake_attn_set_heads(mx, nw) == 0) heads_max_ = mx;
     }
     if (ao_ok_) {
-      ao_ws_ = dalloc<float>((size_t)cake_attn_oproj_ws_floats(c.nkv, c.H));
-      const size_t tw = (size_t)cake_attn_oproj_ticket_words(c.nkv, c.H);
+      ao_ws_ = dalloc<float>((size_t)ao_.ws_floats(c.nkv, c.H));
+      const size_t tw = (size_t)ao_.ticket_words(c.nkv, c.H);
       ao_tickets_ = dalloc<unsigned int>(tw);
       hip_check(hipMemset(ao_tickets_, 0, sizeof(unsigned int) * tw), "memset");
     }
@@ -1398,7 +1422,7 @@ class Llama {
                             wqkv + (size_t)(nq + nk) * c.H, c.H, c.nh, c.nkv, c.hd, inv_freq_,
                             pos_, q_, kc(l), vc(l), S_, st_), "qkv_rope");
       if (short_step_ && ao_ok_) {  // one split: attention + o_proj in one launch
-        k_check(cake_attn_oproj(dt_, q_, kc(l), vc(l), pos_, S_, c.nh, c.nkv, c.hd, scale(), w.wo,
+        k_check(ao_.run(dt_, q_, kc(l), vc(l), pos_, S_, c.nh, c.nkv, c.hd, scale(), w.wo,
                                 nq, c.H, tp_ > 1 ? partial_ : resid_, tp_ > 1 ? 0 : 1, ao_ws_,
                                 ao_tickets_, tickets_ + 2 * c.nkv, st_), "attn_oproj");
         if (tp_ > 1) ar_sum();

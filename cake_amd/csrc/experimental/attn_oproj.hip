@@ -30,7 +30,7 @@
 // o_proj); SURVEY K09-K13 + K03 (o_proj) + K14 (residual).
 #include <cstdio>
 
-#include "attn_core2.h"
+#include "../kernels/attn_core2.h"
 
 namespace cake {
 

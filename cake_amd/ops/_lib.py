@@ -144,7 +144,10 @@ _SIGS.update({
 _RESTYPE = {"cake_mk_gstride": C.c_longlong}
 # entry points of csrc/experimental (not in the default build)
 _OPTIONAL = {"cake_mk_gstride", "cake_mk_grid", "cake_mk_supported", "cake_mk_decode",
-             "cake_mk_set_stamps", "cake_mk_set_tuning"}
+             "cake_mk_set_stamps", "cake_mk_set_tuning",
+             # fused decode attention + o_proj (measured slower: profiles/r5_attn_oproj_ab.md)
+             "cake_attn_oproj", "cake_attn_oproj_supported", "cake_attn_oproj_ws_floats",
+             "cake_attn_oproj_ticket_words"}
 _SIGS["cake_mk_set_stamps"] = [P]
 _SIGS["cake_mk_set_tuning"] = [I, I, I, I]
 _SIGS["cake_attn_debug_drop_partials"] = [I]

@@ -151,8 +151,12 @@ def head_select(resid, norm_w, eps, w, logits, hist, hist_len, last_n: int, pena
 
 
 def attn_oproj_supported(nh: int, nkv: int, hd: int, H: int) -> bool:
-    """Shapes of the fused decode attention + o_proj launch (attn_oproj.hip)."""
-    return bool(kernels().cake_attn_oproj_supported(int(nh), int(nkv), int(hd), int(H)))
+    """Shapes of the fused decode attention + o_proj launch (csrc/experimental/attn_oproj.hip,
+    built with CAKE_BUILD_EXPERIMENTAL=1; False when the library was built without it)."""
+    L = kernels()
+    if not hasattr(L, "cake_attn_oproj_supported"):
+        return False
+    return bool(L.cake_attn_oproj_supported(int(nh), int(nkv), int(hd), int(H)))
 
 
 def attn_oproj_ws_sizes(nkv: int, H: int) -> tuple[int, int]:

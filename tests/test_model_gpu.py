@@ -146,7 +146,11 @@ def test_device_decoder_crosses_one_split_edge(cuda, k, monkeypatch):
     monkeypatch.setenv("CAKE_ATTN_OPROJ", "1")
     from cake_amd.models.llama3.decode_loop import run_decode
     from cake_amd.models.llama3.model import DeviceDecoder
+    from cake_amd.ops import hip as K
     from cake_amd.ops import reference as R
+    if not hasattr(K.kernels(), "cake_attn_oproj"):
+        pytest.skip("fused attention + o_proj not built (csrc/experimental: "
+                    "CAKE_BUILD_EXPERIMENTAL=1)")
 
     cfg = preset("llama3-8b", num_hidden_layers=2, vocab_size=2048, intermediate_size=1024,
                  hidden_size=512, num_attention_heads=8, num_key_value_heads=2)
