@@ -263,7 +263,8 @@ static int g_attn_heads_max = 0;  // live lengths <= this take it (0: off)
 static int g_attn_head_waves = 2;
 
 CAKE_API int cake_attn_set_heads(int max_keys, int waves) {
-  if (max_keys < 0 || (waves != 1 && waves != 2 && waves != 4)) return (int)hipErrorInvalidValue;
+  if (max_keys < 0 || (waves != 1 && waves != 2 && waves != 4 && waves != 8 && waves != 16))
+    return (int)hipErrorInvalidValue;
   g_attn_heads_max = max_keys;
   g_attn_head_waves = waves;
   return 0;
@@ -286,7 +287,9 @@ CAKE_API int cake_attn_decode_heads(int dt, const float* q, const void* kc, cons
   DISPATCH_DT_HD(dt, hd, {
     if (g_attn_head_waves == 1) CAKE_HEADS(1);
     else if (g_attn_head_waves == 2) CAKE_HEADS(2);
-    else CAKE_HEADS(4);
+    else if (g_attn_head_waves == 4) CAKE_HEADS(4);
+    else if (g_attn_head_waves == 8) CAKE_HEADS(8);
+    else CAKE_HEADS(16);
     return (int)hipGetLastError();
   });
 #undef CAKE_HEADS

@@ -146,7 +146,7 @@ def test_attn_decode(cuda, attn_impl, dt, nh, nkv, hd, pos, S, min_keys):
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("nh,nkv,hd", [(32, 8, 128), (16, 16, 64), (8, 1, 128)])
 @pytest.mark.parametrize("pos", [0, 15, 16, 70, 127, 600])
-@pytest.mark.parametrize("waves", [1, 2, 4])
+@pytest.mark.parametrize("waves", [1, 2, 4, 8, 16])
 def test_attn_decode_heads(cuda, dt, nh, nkv, hd, pos, waves):
     """Head-parallel short-context attention (one workgroup per query head, one split)
     vs f32 attention: block edges (16 / 17 keys), a ragged tail, and a long context it is
