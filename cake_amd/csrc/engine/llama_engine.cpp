@@ -76,6 +76,7 @@ int cake_attn_decode(int dt, const float* q, const void* kc, const void* vc, con
                      unsigned int* tickets, void* out, hipStream_t st);
 int cake_attn_set_split_cap(int cap);
 int cake_attn_set_heads(int max_keys, int waves);
+int cake_attn_set_head_prefetch(int pfd);
 int cake_attn_decode_heads(int dt, const float* q, const void* kc, const void* vc, const int* pos,
                            int S, int nh, int nkv, int hd, float scale, void* out, hipStream_t st);
 int cake_attn_splits(int Tk);
@@ -1054,9 +1055,10 @@ class Llama {
     // CAKE_ATTN_HEADS=<max keys>[:<waves>]: the head-parallel short-context attention
     if (!ao_ok_) {
       const char* e = std::getenv("CAKE_ATTN_HEADS");
-      int mx = 0, nw = 2;
-      if (e && *e) std::sscanf(e, "%d:%d", &mx, &nw);
-      if (mx > 0 && cake_attn_set_heads(mx, nw) == 0) heads_max_ = mx;
+      int mx = 0, nw = 2, pfd = 2;
+      if (e && *e) std::sscanf(e, "%d:%d:%d", &mx, &nw, &pfd);
+      if (mx > 0 && cake_attn_set_heads(mx, nw) == 0 && cake_attn_set_head_prefetch(pfd) == 0)
+        heads_max_ = mx;
     }
     if (ao_ok_) {
       ao_ws_ = dalloc<float>((size_t)ao_.ws_floats(c.nkv, c.H));

@@ -68,12 +68,12 @@ __global__ __launch_bounds__(AttnGeom2<NREP>::NT) void attn2_decode_kernel(AttnD
 // (nkv workgroups, each carrying its group's nrep heads) the same keys are read nrep
 // times (from L2), but P.V and the end merge carry one head instead of nrep and 4x more
 // workgroups issue the loads.  Engines launch it for live lengths up to g_attn_heads_max.
-template <int DT, int HD, int NW>
+template <int DT, int HD, int NW, int PFD>
 __global__ __launch_bounds__(64 * NW) void attn_head_kernel(AttnDecArgs a, int nrep) {
   __shared__ __attribute__((aligned(16))) float lds[attn2_smem_floats<HD, 1, NW>()];
   const int h = blockIdx.x;
-  attn2_decode_block<DT, HD, 1, false, NW, 2, NoHook, true>(a, h, 0, lds, gridDim.x, NoHook(),
-                                                           h / nrep);
+  attn2_decode_block<DT, HD, 1, false, NW, PFD, NoHook, true>(a, h, 0, lds, gridDim.x, NoHook(),
+                                                             h / nrep);
 }
 
 }  // namespace cake
@@ -261,6 +261,13 @@ CAKE_API int cake_attn_decode(int dt, const float* q, const void* kc, const void
 // ---- head-parallel short-context launch (attn_head_kernel)
 static int g_attn_heads_max = 0;  // live lengths <= this take it (0: off)
 static int g_attn_head_waves = 2;
+static int g_attn_head_pfd = 2;  // key blocks per wave in flight (2 or 4)
+
+CAKE_API int cake_attn_set_head_prefetch(int pfd) {
+  if (pfd != 2 && pfd != 4) return (int)hipErrorInvalidValue;
+  g_attn_head_pfd = pfd;
+  return 0;
+}
 
 CAKE_API int cake_attn_set_heads(int max_keys, int waves) {
   if (max_keys < 0 || (waves != 1 && waves != 2 && waves != 4 && waves != 8 && waves != 16))
@@ -282,8 +289,15 @@ CAKE_API int cake_attn_decode_heads(int dt, const float* q, const void* kc, cons
                       scale * 1.4426950408889634f, nullptr, nullptr, (uint16_t*)out,
                       g_attn_min_keys, 1, nullptr, g_attn_target, S, 0};
   const int nrep = nh / nkv;
-#define CAKE_HEADS(NW) \
-  hipLaunchKernelGGL((attn_head_kernel<DT, HD, NW>), dim3(nh), dim3(64 * NW), 0, st, a, nrep)
+#define CAKE_HEADS(NW)                                                                         \
+  do {                                                                                         \
+    if (g_attn_head_pfd == 4)                                                                  \
+      hipLaunchKernelGGL((attn_head_kernel<DT, HD, NW, 4>), dim3(nh), dim3(64 * NW), 0, st, a, \
+                         nrep);                                                                \
+    else                                                                                       \
+      hipLaunchKernelGGL((attn_head_kernel<DT, HD, NW, 2>), dim3(nh), dim3(64 * NW), 0, st, a, \
+                         nrep);                                                                \
+  } while (0)
   DISPATCH_DT_HD(dt, hd, {
     if (g_attn_head_waves == 1) CAKE_HEADS(1);
     else if (g_attn_head_waves == 2) CAKE_HEADS(2);

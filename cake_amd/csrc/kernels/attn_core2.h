@@ -119,7 +119,7 @@ template <int DT, int HD, int NREP, bool FUSED = false, int NW = AttnGeom2<NREP>
 __device__ __forceinline__ void attn2_decode_block(const AttnDecArgs& a, int g, int s,
                                                    float* lds, int ng, const Hook& hook = Hook(),
                                                    int kvh = -1) {
-  static_assert(PFD == 1 || PFD == 2, "prefetch depth 1 or 2");
+  static_assert(PFD == 1 || PFD == 2 || PFD == 4, "prefetch depth 1, 2 or 4");
   constexpr int DS = HD / 32;    // MFMA k-steps (A fragments) per key block
   constexpr int NCH = HD / 8;    // 8-dim chunks per row
   constexpr int KPL = NCH / 4;   // keys per lane in P.V (16 keys over 64 / NCH key groups)
@@ -190,8 +190,15 @@ __device__ __forceinline__ void attn2_decode_block(const AttnDecArgs& a, int g, 
       }
     }
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (PFD == 2)
+    if constexpr (PFD == 2) {
       if (s == 0) load_blk(I1{}, (wave + NW) * kBlk, a.S - 1);
+    } else if constexpr (PFD == 4) {
+      if (s == 0) {
+        load_blk(std::integral_constant<int, 1>{}, (wave + NW) * kBlk, a.S - 1);
+        load_blk(std::integral_constant<int, 2>{}, (wave + 2 * NW) * kBlk, a.S - 1);
+        load_blk(std::integral_constant<int, 3>{}, (wave + 3 * NW) * kBlk, a.S - 1);
+      }
+    }
     __builtin_amdgcn_sched_barrier(0);
     hook();
     __builtin_amdgcn_sched_barrier(0);
@@ -236,6 +243,13 @@ __device__ __forceinline__ void attn2_decode_block(const AttnDecArgs& a, int g, 
     if (b < nblk) load_blk(I0{}, kb + b * kBlk, ke - 1);
     if constexpr (PFD == 2)
       if (b + NW < nblk) load_blk(I1{}, kb + (b + NW) * kBlk, ke - 1);
+    if constexpr (PFD == 4) {
+      if (b + NW < nblk) load_blk(std::integral_constant<int, 1>{}, kb + (b + NW) * kBlk, ke - 1);
+      if (b + 2 * NW < nblk)
+        load_blk(std::integral_constant<int, 2>{}, kb + (b + 2 * NW) * kBlk, ke - 1);
+      if (b + 3 * NW < nblk)
+        load_blk(std::integral_constant<int, 3>{}, kb + (b + 3 * NW) * kBlk, ke - 1);
+    }
   }
   ATTN_STAMP(2);
   // one key block from slot `slot`; the block PFD x NW further on is requested into the
@@ -301,10 +315,17 @@ __device__ __forceinline__ void attn2_decode_block(const AttnDecArgs& a, int g, 
   };
   if constexpr (PFD == 1) {
     for (; b < nblk; b += NW) block(I0{}, b);
-  } else {
+  } else if constexpr (PFD == 2) {
     for (; b < nblk; b += 2 * NW) {
       block(I0{}, b);
       if (b + NW < nblk) block(I1{}, b + NW);
+    }
+  } else {
+    for (; b < nblk; b += 4 * NW) {
+      block(I0{}, b);
+      if (b + NW < nblk) block(std::integral_constant<int, 1>{}, b + NW);
+      if (b + 2 * NW < nblk) block(std::integral_constant<int, 2>{}, b + 2 * NW);
+      if (b + 3 * NW < nblk) block(std::integral_constant<int, 3>{}, b + 3 * NW);
     }
   }
   ATTN_STAMP(3);

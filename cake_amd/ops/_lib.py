@@ -37,6 +37,7 @@ _SIGS = {
     "cake_attn_set_impl": [I],
     "cake_attn_decode_heads": [I, P, P, P, P, I, I, I, I, F, P, P],
     "cake_attn_set_heads": [I, I],
+    "cake_attn_set_head_prefetch": [I],
     "cake_attn_heads_max": [],
     "cake_attn_set_target_splits": [I],
     "cake_attn_set_single_max": [I],

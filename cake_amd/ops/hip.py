@@ -258,7 +258,7 @@ def attn_decode(q, kcache, vcache, pos, scale, part, tickets, out):
           "attn_decode")
 
 
-def attn_decode_heads(q, kcache, vcache, pos, scale, out, waves: int = 2):
+def attn_decode_heads(q, kcache, vcache, pos, scale, out, waves: int = 2, prefetch: int = 2):
     """Head-parallel short-context decode attention (attention.hip attn_head_kernel): one
     workgroup per query head, the whole live length as one split; no workspace."""
     nkv, S, hd = kcache.shape
@@ -273,10 +273,12 @@ def attn_decode_heads(q, kcache, vcache, pos, scale, out, waves: int = 2):
     L = kernels()
     prev = int(L.cake_attn_heads_max())
     check(L.cake_attn_set_heads(max(prev, 1), int(waves)), "attn_set_heads")
+    check(L.cake_attn_set_head_prefetch(int(prefetch)), "attn_set_head_prefetch")
     check(L.cake_attn_decode_heads(_dt(kcache), _p(q), _p(kcache), _p(vcache), _p(pos), S, nh,
                                    nkv, hd, float(scale), _p(out), _stream()),
           "attn_decode_heads")
     check(L.cake_attn_set_heads(prev, 2), "attn_set_heads")
+    check(L.cake_attn_set_head_prefetch(2), "attn_set_head_prefetch")
 
 
 # ---------------------------------------------------------------------------

@@ -146,8 +146,9 @@ def test_attn_decode(cuda, attn_impl, dt, nh, nkv, hd, pos, S, min_keys):
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("nh,nkv,hd", [(32, 8, 128), (16, 16, 64), (8, 1, 128)])
 @pytest.mark.parametrize("pos", [0, 15, 16, 70, 127, 600])
-@pytest.mark.parametrize("waves", [1, 2, 4, 8, 16])
-def test_attn_decode_heads(cuda, dt, nh, nkv, hd, pos, waves):
+@pytest.mark.parametrize("waves,prefetch", [(1, 2), (2, 2), (4, 2), (8, 2), (16, 2), (4, 4),
+                                            (16, 4)])
+def test_attn_decode_heads(cuda, dt, nh, nkv, hd, pos, waves, prefetch):
     """Head-parallel short-context attention (one workgroup per query head, one split)
     vs f32 attention: block edges (16 / 17 keys), a ragged tail, and a long context it is
     still correct for (601 keys walked by one workgroup)."""
@@ -159,7 +160,7 @@ def test_attn_decode_heads(cuda, dt, nh, nkv, hd, pos, waves):
     q = torch.randn(nh * hd, device=cuda)
     p = torch.tensor([pos], dtype=torch.int32, device=cuda)
     out = torch.full((nh * hd,), float("nan"), device=cuda, dtype=dt)
-    K_.attn_decode_heads(q, kc, vc, p, 1 / math.sqrt(hd), out, waves=waves)
+    K_.attn_decode_heads(q, kc, vc, p, 1 / math.sqrt(hd), out, waves=waves, prefetch=prefetch)
     Tk = pos + 1
     ref = R.attention(q.view(1, nh, hd), kc[:, :Tk].transpose(0, 1), vc[:, :Tk].transpose(0, 1),
                       pos).reshape(-1)
