@@ -21,7 +21,7 @@ PROBE_US = {"qkv_rope": 9.03, "attn_decode": 1.94, "o_proj": 6.59, "swiglu": 35.
 def kind(name):
     if "attn_oproj" in name:  # fused attention + o_proj (one-split lengths)
         return "attn_oproj"
-    if "attn2_decode" in name:  # decode-attention core 2 (the default)
+    if "attn2_decode" in name or "attn_head_kernel" in name:  # core 2 / head-parallel
         return "attn_decode"
     for k in ("qkv_rope", "swiglu", "attn_decode", "gemv_norm_f32", "gemv_x16"):
         if k in name:
