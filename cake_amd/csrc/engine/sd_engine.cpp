@@ -36,6 +36,8 @@
 #include <vector>
 
 #include "../runtime/json.h"
+#include "../runtime/net.h"
+#include "../runtime/proto.h"
 #include "../runtime/safetensors.h"
 #include "engine_util.h"
 
@@ -366,6 +368,8 @@ float half_to_f32(uint16_t h, bool bf16) {
   return f;
 }
 
+const char* kPartNames[] = {"unet", "vae", "clip", "clip2"};
+
 const char* kEpiNames[] = {"store", "resid32", "add16", "swiglu", "geglu", "partial", "store32",
                            "silu", "quick_gelu", "gelu"};
 enum Epi { kStore = 0, kResid32 = 1, kAdd16 = 2, kGeglu = 4, kStore32 = 6, kSilu = 7,
@@ -470,6 +474,18 @@ class SdEngine {
     paths_[3] = o.clip2_path ? o.clip2_path : "";
     parts_ = o.parts ? o.parts : 15;
     if (!cfg_.xl) parts_ &= 7;
+    {
+      const char* ra[4] = {o.remote_unet, o.remote_vae, o.remote_clip, o.remote_clip2};
+      remote_timeout_ = o.remote_timeout_s > 0 ? o.remote_timeout_s : 120.0;
+      for (int k = 0; k < 4; ++k)
+        if (ra[k] && *ra[k]) {
+          if (!cfg_.xl && k == 3) continue;
+          remote_[k].addr = ra[k];
+          parts_ &= ~(1 << k);  // served remotely: not loaded here
+        }
+      for (auto& r : remote_)
+        if (!r.addr.empty()) connect_remote(r);
+    }
     planner_.load(pkg_dir() + "/ops/gemm_tuned.json");
     zeros_ = dalloc(256);
     hip_check(hipMemset(zeros_, 0, 256), "memset");
@@ -480,6 +496,8 @@ class SdEngine {
   }
 
   ~SdEngine() {
+    for (auto& r : remote_)
+      if (r.fd >= 0) tcp_close(r.fd);
     (void)hipSetDevice(dev_);
     (void)hipStreamSynchronize(st_);
     drop_graphs();
@@ -498,7 +516,10 @@ class SdEngine {
   void generate(const CakeSdGenArgs& a, uint8_t* rgb, float* lat_out, double* step_s,
                 CakeSdResult* res) {
     hip_check(hipSetDevice(dev_), "hipSetDevice");
-    need(cfg_.xl ? 15 : 7, "every component (generate)");
+    for (int k = 0; k < (cfg_.xl ? 4 : 3); ++k)
+      if (!(parts_ & (1 << k)) && remote_[k].addr.empty())
+        throw Error(std::string("generate: component ") + kPartNames[k] +
+                    " neither loaded nor served by a worker");
     const bool guide = a.uncond != nullptr && a.guidance > 1.0f;
     if (cfg_.xl && (a.cond2 == nullptr || (guide && a.uncond2 == nullptr)))
       throw Error("xl / turbo need the second tokenizer's ids (cond2 / uncond2)");
@@ -522,7 +543,8 @@ class SdEngine {
     // ---- text context [B2, 77, ctx]: rows [uncond; cond] x bsize
     text_context(a.cond, a.uncond, a.cond2, a.uncond2, guide, bsize);
     hook_ctx_.clear();  // ctx_ / the k|v caches now hold this generation's context
-    precompute_kv(B2);
+    const bool unet_remote = !remote_[0].addr.empty();
+    if (!unet_remote) precompute_kv(B2);
     hip_check(hipStreamSynchronize(st_), "sync");
     const auto t1 = std::chrono::steady_clock::now();
     // ---- latents, tables
@@ -560,7 +582,9 @@ class SdEngine {
     try {
       for (int i = 0; i < n; ++i) {
         hip_check(hipEventRecord(ev[2 * i], st_), "event");
-        if (i == 0 || !a.use_graph) {
+        if (unet_remote) {
+          remote_step(B2, guide, a.guidance, ttab[i]);
+        } else if (i == 0 || !a.use_graph) {
           step_body(B2, guide, a.guidance);
         } else {
           auto it = graphs_.find(key);
@@ -612,6 +636,28 @@ class SdEngine {
     const int h = cfg_.height / 8, w = cfg_.width / 8;
     const size_t nl1 = (size_t)4 * h * w;
     const size_t img_bytes = (size_t)cfg_.height * cfg_.width * 3;
+    if (!remote_[1].addr.empty()) {  // the worker's VAE: pack([0 (decode), z]) -> image
+      std::vector<float> z(nl1 * bsize);
+      hip_check(hipMemcpyAsync(z.data(), x_, z.size() * 4, hipMemcpyDeviceToHost, st_), "D2H");
+      hip_check(hipStreamSynchronize(st_), "sync");
+      for (int b = 0; b < bsize; ++b) {
+        std::vector<float> zb(z.begin() + b * nl1, z.begin() + (b + 1) * nl1);
+        for (auto& v : zb) v = (float)(v / cfg_.vae_scale);
+        const float dir = 0.f;
+        const std::vector<float> pk =
+            pack({{&dir, {1}}, {zb.data(), {1, 4, (uint64_t)h, (uint64_t)w}}});
+        const std::vector<float> img = remote_call(remote_[1], "vae", pk, {(uint64_t)pk.size()},
+                                                   (size_t)3 * cfg_.height * cfg_.width);
+        const size_t hw = (size_t)cfg_.height * cfg_.width;
+        uint8_t* dst = rgb + b * img_bytes;
+        for (size_t p = 0; p < hw; ++p)  // [3, H, W] in [-1, 1] -> HWC u8 (cake_to_rgb8)
+          for (int c = 0; c < 3; ++c) {
+            const float v = std::min(1.f, std::max(0.f, img[c * hw + p] * 0.5f + 0.5f));
+            dst[p * 3 + c] = (uint8_t)(v * 255.f);
+          }
+      }
+      return;
+    }
     for (int b = 0; b < bsize; ++b) {
       vae_a_.reset();
       uint16_t* z = new16(vae_a_, nl1);
@@ -625,6 +671,112 @@ class SdEngine {
       hip_check(hipStreamSynchronize(st_), "sync");  // the VAE arena is reused next
     }
   }
+
+  // ------------------------------------------------------------------ remote components
+  // The reference's Client (client.rs:23-133) for an image topology: one connection per
+  // worker, Hello -> WorkerInfo at open, a SingleOp per call with the component's name.
+  struct Remote {
+    std::string addr;
+    int fd = -1;
+  };
+
+  void connect_remote(Remote& r) {
+    std::string host;
+    int port = 0;
+    split_host_port(r.addr, &host, &port);
+    r.fd = tcp_connect(host, port, remote_timeout_);
+    tcp_set_timeout(r.fd, remote_timeout_);
+    Message hello;
+    hello.type = MsgType::Hello;
+    const std::string body = encode_body(hello);
+    send_frame(r.fd, reinterpret_cast<const uint8_t*>(body.data()), (uint32_t)body.size());
+    const std::string rep = recv_frame(r.fd);
+    const Message info = decode_body(reinterpret_cast<const uint8_t*>(rep.data()), rep.size());
+    if (info.type != MsgType::WorkerInfo)
+      throw Error("SD worker " + r.addr + " did not answer Hello with WorkerInfo");
+  }
+
+  // SingleOp `name` on f32 `x` of `shape`; the reply as f32 (16-bit replies widened)
+  std::vector<float> remote_call(Remote& r, const char* name, const std::vector<float>& x,
+                                 std::vector<uint64_t> shape, size_t expect) {
+    Message m;
+    m.type = MsgType::SingleOp;
+    m.layer_name = name;
+    m.x.dtype = "f32";
+    m.x.shape = std::move(shape);
+    m.x.data = reinterpret_cast<const uint8_t*>(x.data());
+    m.x.nbytes = x.size() * 4;
+    const std::string body = encode_body(m);
+    send_frame(r.fd, reinterpret_cast<const uint8_t*>(body.data()), (uint32_t)body.size());
+    const std::string rep = recv_frame(r.fd);
+    const Message t = decode_body(reinterpret_cast<const uint8_t*>(rep.data()), rep.size());
+    if (t.type == MsgType::Error) throw Error("SD worker " + r.addr + " (" + name + "): " + t.error);
+    if (t.type != MsgType::Tensor) throw Error("SD worker " + r.addr + ": unexpected reply");
+    uint64_t cnt = 1;
+    for (auto d : t.x.shape) cnt *= d;
+    if (cnt != expect)
+      throw Error("SD worker " + r.addr + " (" + name + "): " + std::to_string(cnt) +
+                  " values, expected " + std::to_string(expect));
+    std::vector<float> out(cnt);
+    if (t.x.dtype == "f32" && t.x.nbytes == cnt * 4) {
+      std::memcpy(out.data(), t.x.data, cnt * 4);
+    } else if ((t.x.dtype == "f16" || t.x.dtype == "bf16") && t.x.nbytes == cnt * 2) {
+      for (uint64_t i = 0; i < cnt; ++i) {
+        uint16_t hv;
+        std::memcpy(&hv, t.x.data + 2 * i, 2);
+        out[i] = half_to_f32(hv, t.x.dtype == "bf16");
+      }
+    } else {
+      throw Error("SD worker " + r.addr + ": unsupported reply tensor " + t.x.dtype);
+    }
+    return out;
+  }
+
+  // util.rs pack_tensors: [n, (ndim, dims..., values...) per tensor] as f32
+  struct PackItem {
+    const float* data;
+    std::vector<uint64_t> shape;
+  };
+  static std::vector<float> pack(const std::vector<PackItem>& items) {
+    std::vector<float> out{(float)items.size()};
+    for (const auto& it : items) {
+      out.push_back((float)it.shape.size());
+      uint64_t n = 1;
+      for (auto d : it.shape) {
+        out.push_back((float)d);
+        n *= d;
+      }
+      out.insert(out.end(), it.data, it.data + n);
+    }
+    return out;
+  }
+
+  // one denoising step through the worker's UNet: the model input and context down, the
+  // prediction up, then the same fused CFG + scheduler update as the local step
+  void remote_step(int B2, bool guide, float guidance, float t) {
+    const int h = cfg_.height / 8, w = cfg_.width / 8;
+    const size_t n = (size_t)B2 * 4 * h * w, nc = (size_t)B2 * kTok * cfg_.ctx_dim();
+    std::vector<float> inp(n), ctx(nc);
+    float* tmp = static_cast<float*>(text_scratch((n + nc) * 4));
+    k_check(cake_widen16(dt_, inp_, (long long)n, tmp, st_), "widen16");
+    k_check(cake_widen16(dt_, ctx_, (long long)nc, tmp + n, st_), "widen16");
+    hip_check(hipMemcpyAsync(inp.data(), tmp, n * 4, hipMemcpyDeviceToHost, st_), "D2H");
+    hip_check(hipMemcpyAsync(ctx.data(), tmp + n, nc * 4, hipMemcpyDeviceToHost, st_), "D2H");
+    hip_check(hipStreamSynchronize(st_), "sync");
+    const std::vector<float> pk = pack({{inp.data(), {(uint64_t)B2, 4, (uint64_t)h, (uint64_t)w}},
+                                        {ctx.data(), {(uint64_t)B2, kTok, (uint64_t)cfg_.ctx_dim()}},
+                                        {&t, {1}}});
+    const std::vector<float> pred = remote_call(remote_[0], "unet", pk, {(uint64_t)pk.size()}, n);
+    unet_a_.reset();
+    uint16_t* p16 = new16(unet_a_, n);
+    upload16(pred.data(), n, p16);
+    k_check(cake_sched_step(dt_, x_, p16, (long long)(n / (guide ? 2 : 1)), guide ? 1 : 0, guidance,
+                            coef_, step_, seed_dev_, inp_, st_), "sched_step");
+    k_check(cake_step_advance(step_, st_), "step_advance");
+  }
+
+  std::array<Remote, 4> remote_;  // unet, vae, clip, clip2
+  double remote_timeout_ = 120.0;
 
   // ------------------------------------------------------------------ component hooks
   void text_component(int which, const int32_t* ids, int B, float* out) {
@@ -1693,8 +1845,20 @@ class SdEngine {
     const int per = guide ? 2 : 1;
     auto put = [&](const ClipW& cw, const int32_t* ids, int row, int col) {
       text_a_.reset();
-      const uint16_t* y = clip_forward(cw, ids);
-      const int D = cw.cfg.D;
+      const int which = &cw == &clip_ ? 0 : 1;
+      const int D = which == 0 ? cfg_.clip.D : cfg_.clip2.D;
+      const uint16_t* y;
+      if (!remote_[2 + which].addr.empty()) {  // the worker's encoder: ids [1, 77] -> [1, 77, D]
+        std::vector<float> fid(kTok);
+        for (int t = 0; t < kTok; ++t) fid[t] = (float)ids[t];
+        const std::vector<float> e = remote_call(remote_[2 + which], which ? "clip2" : "clip", fid,
+                                                 {1, (uint64_t)kTok}, (size_t)kTok * D);
+        uint16_t* e16 = new16(text_a_, (size_t)kTok * D);
+        upload16(e.data(), e.size(), e16);
+        y = e16;
+      } else {
+        y = clip_forward(cw, ids);
+      }
       for (int b = 0; b < bsize; ++b)
         hip_check(hipMemcpy2DAsync(ctx_ + (size_t)(b * per + row) * kTok * Dc + col,
                                    (size_t)Dc * 2, y, (size_t)D * 2, (size_t)D * 2, kTok,

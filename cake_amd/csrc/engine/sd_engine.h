@@ -41,6 +41,15 @@ typedef struct CakeSdOpts {
   const char* clip_path;
   const char* clip2_path;
   int32_t parts;         // components to load: 1 unet | 2 vae | 4 clip | 8 clip2 (0: all)
+  // components served by TCP workers ("host:port", the reference's topology: a worker's
+  // SingleOp "unet" / "vae" / "clip" / "clip2"; null = local).  A remote UNet runs every
+  // step as one round trip (no step graph); generate() needs each component local or
+  // remote.
+  const char* remote_unet;
+  const char* remote_vae;
+  const char* remote_clip;
+  const char* remote_clip2;
+  double remote_timeout_s;  // per request (0: 120)
 } CakeSdOpts;
 
 typedef struct CakeSdGenArgs {

@@ -67,16 +67,21 @@ class NativeSDGenerator(ImageGenerator):
                                               ctx.model_path)))
         tok2 = Tokenizer.from_file(str(resolve("tokenizer_2", a.sd_tokenizer_2, cfg.version,
                                                a.sd_use_f16, ctx.model_path))) if xl else None
-        paths = {}
+        paths, remote = {}, {}
+        topo = getattr(ctx, "topology", None)
         for comp, flag in (("unet", "sd_unet"), ("vae", "sd_vae"), ("clip", "sd_clip"),
                            ("clip2", "sd_clip2")):
             if comp == "clip2" and not xl:
+                continue
+            node = topo.get_node_for_layer(comp) if topo is not None else None
+            if node is not None:  # served by a TCP worker (sd.rs: the topology's component)
+                remote[comp] = node.host
                 continue
             paths[comp] = str(resolve(comp, getattr(a, flag, None), cfg.version, a.sd_use_f16,
                                       ctx.model_path))
         eng = NativeSD(str(ctx.model_path), version=cfg.version, width=cfg.width,
                        height=cfg.height, dtype="bf16" if ctx.dtype == torch.bfloat16 else "f16",
-                       device=ctx.device.index or 0, paths=paths)
+                       device=ctx.device.index or 0, paths=paths, remote=remote)
 
         def fallback():
             from .pipeline import SDGenerator
@@ -116,7 +121,7 @@ class NativeSDGenerator(ImageGenerator):
 
     def generate_image(self, args: ImageGenerationArgs, callback: Callable[[list], None]) -> None:
         init = None
-        if args.img2img and args.bsize == 1:
+        if args.img2img and args.bsize == 1 and "vae" not in self.eng.remote:
             if not 0.0 <= args.img2img_strength <= 1.0:
                 raise ValueError("img2img-strength should be between 0 and 1, got "
                                  f"{args.img2img_strength}")
@@ -211,16 +216,14 @@ class NativeSDGenerator(ImageGenerator):
 
 
 def native_sd_eligible(ctx) -> bool:
-    """Every SD component local on a GPU, a 16-bit dtype, CAKE_NATIVE != 0, engine built."""
+    """A GPU master, a 16-bit dtype, CAKE_NATIVE != 0, engine built (components local or
+    served by the topology's workers)."""
     if os.environ.get("CAKE_NATIVE", "1") == "0":
         return False
     if ctx.device.type != "cuda" or ctx.dtype not in (torch.float16, torch.bfloat16):
         return False
-    topo = getattr(ctx, "topology", None)
-    if topo is not None:
-        for name in ("clip", "clip2", "vae", "unet"):
-            if topo.get_node_for_layer(name) is not None:
-                return False
+    # components in the topology are served by their TCP workers through the engine's
+    # client (remote_unet / _vae / _clip / _clip2)
     if getattr(ctx.args, "sd_sliced_attention_size", None):
         return True  # (flash attention has no score memory to slice)
     from ...sd_engine import native_sd_available

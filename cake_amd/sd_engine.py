@@ -27,7 +27,10 @@ class SdOpts(C.Structure):
                 ("dtype", C.c_int32), ("device", C.c_int32), ("init", C.c_int32),
                 ("autotune", C.c_int32), ("tiny", C.c_int32), ("seed", C.c_uint64),
                 ("unet_path", C.c_char_p), ("vae_path", C.c_char_p), ("clip_path", C.c_char_p),
-                ("clip2_path", C.c_char_p), ("parts", C.c_int32)]
+                ("clip2_path", C.c_char_p), ("parts", C.c_int32),
+                ("remote_unet", C.c_char_p), ("remote_vae", C.c_char_p),
+                ("remote_clip", C.c_char_p), ("remote_clip2", C.c_char_p),
+                ("remote_timeout_s", C.c_double)]
 
 
 PARTS = {"unet": 1, "vae": 2, "clip": 4, "clip2": 8}
@@ -115,18 +118,27 @@ class NativeSD:
     def __init__(self, model_dir: str, version: str | None = None, width: int = 0,
                  height: int = 0, dtype: str = "f16", device: int = 0,
                  random_init: bool = False, seed: int = 0, autotune: bool = True,
-                 paths: dict | None = None, parts=None):
+                 paths: dict | None = None, parts=None, remote: dict | None = None,
+                 remote_timeout_s: float = 120.0):
+        """remote: component -> "host:port" of the TCP worker serving it (the topology's
+        unet / vae / clip / clip2); those are not loaded here."""
         if dtype not in ("f16", "bf16"):
             raise ValueError("native SD engine dtype: f16 or bf16")
         p = paths or {}
+        rm = remote or {}
+        self.remote = dict(rm)
         self._keep = [x.encode() if x else None for x in
-                      (version, p.get("unet"), p.get("vae"), p.get("clip"), p.get("clip2"))]
+                      (version, p.get("unet"), p.get("vae"), p.get("clip"), p.get("clip2"),
+                       rm.get("unet"), rm.get("vae"), rm.get("clip"), rm.get("clip2"))]
         o = SdOpts(version=self._keep[0], width=int(width), height=int(height),
                    dtype=0 if dtype == "bf16" else 1, device=int(device),
                    init=1 if random_init else 0, autotune=1 if autotune else 0, tiny=0,
                    seed=int(seed), unet_path=self._keep[1], vae_path=self._keep[2],
                    clip_path=self._keep[3], clip2_path=self._keep[4],
-                   parts=0 if parts is None else sum(PARTS[p] for p in parts))
+                   parts=0 if parts is None else sum(PARTS[p] for p in parts),
+                   remote_unet=self._keep[5], remote_vae=self._keep[6],
+                   remote_clip=self._keep[7], remote_clip2=self._keep[8],
+                   remote_timeout_s=float(remote_timeout_s))
         err = C.create_string_buffer(1024)
         self._h = lib().cake_sd_open(str(model_dir).encode(), C.byref(o), err, 1024)
         if not self._h:

@@ -379,3 +379,83 @@ def test_native_engine_writes_the_chrome_trace(cuda, mini, tmp_path, monkeypatch
     assert "text_embeddings" in names and "vae_decode" in names
     assert [n for n in names if n.startswith("step ")] == ["step 1", "step 2", "step 3"]
     native.eng.close()
+
+
+@pytest.mark.parametrize("served", [("unet", "vae"), ("clip", "unet", "vae")])
+def test_native_master_with_remote_sd_components(cuda, mini, tmp_path, monkeypatch, served):
+    """The native SD engine as the master of an image topology: the UNet and the VAE on a
+    TCP worker (cake-cli --mode worker, the native SD worker), the text encoders local —
+    every step one SingleOp round trip through the engine's own client.  The image equals
+    the all-local native image (the same kernels; the worker's f32 wire round trip and the
+    host-side RGB8 conversion: a grey level)."""
+    import os
+    import socket
+    import subprocess
+    import time
+
+    from cake_amd.cli import build_parser
+    from cake_amd.context import Context
+    from cake_amd.master import _load_image
+    from cake_amd.models.sd.args import ImageGenerationArgs
+    from cake_amd.models.sd.native_generator import NativeSDGenerator
+    v, cfg, d = mini
+    if v != "v1-5":
+        pytest.skip("one version covers the remote plumbing")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cli = os.path.join(root, "cake_amd", "lib", "cake-cli")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    topo = tmp_path / "topology.yml"
+    topo.write_text(f"w1:\n  host: '127.0.0.1:{port}'\n  layers:\n" +
+                    "".join(f"    - '{c}'\n" for c in served))
+    empty = tmp_path / "empty.yml"
+    empty.write_text("{}\n")
+    env = dict(os.environ, CAKE_LOG="warning")
+    w = subprocess.Popen([cli, "--mode", "worker", "--name", "w1", "--model", str(d),
+                          "--topology", str(topo), "--address", f"127.0.0.1:{port}",
+                          "--model-type", "image-model", "--sd-version", v, "--dtype", "f16"],
+                         cwd=root, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
+                         text=True)
+    req = ImageGenerationArgs(image_prompt="a red cube", uncond_prompt="blurry", n_steps=3,
+                              image_seed=7)
+    gens = []
+    try:
+        t0 = time.time()
+        while True:
+            if w.poll() is not None:
+                raise AssertionError(f"worker exited: {w.stderr.read()[-3000:]}")
+            try:
+                socket.create_connection(("127.0.0.1", port), timeout=0.5).close()
+                break
+            except OSError:
+                assert time.time() - t0 < 180, "worker did not listen"
+                time.sleep(0.3)
+
+        def image(topology):
+            args = build_parser().parse_args(["--model", str(d), "--topology", str(topology),
+                                              "--model-type", "image-model", "--sd-version", v,
+                                              "--dtype", "f16"])
+            gen = _load_image(Context.from_args(args))
+            gens.append(gen)
+            out = []
+            gen.generate_image(req, lambda imgs: out.append(imgs))
+            return gen, out[-1][0]
+        rg, remote_img = image(topo)
+        assert isinstance(rg, NativeSDGenerator) and rg._fallback is None
+        assert sorted(rg.eng.remote) == sorted(served)
+        assert len(rg.last_step_s) == 3
+        lg, local_img = image(empty)
+        assert isinstance(lg, NativeSDGenerator) and not lg.eng.remote
+    finally:
+        for g in gens:
+            g.eng.close()
+        w.kill()
+        err = w.communicate()[1]
+    assert "native SD worker" in err, err[-2000:]
+    a = np.asarray(remote_img, dtype=np.int32)
+    b = np.asarray(local_img, dtype=np.int32)
+    assert a.shape == b.shape == (cfg.height, cfg.width, 3)
+    diff = np.abs(a - b)
+    assert diff.mean() < 0.5 and diff.max() <= 2, (diff.mean(), diff.max())
