@@ -114,8 +114,10 @@ def build_kernels(force: bool = False, jobs: int = 8) -> Path:
     for o in stale:  # an object of a source no longer built (experimental off) must go
         o.unlink()
     if force or stale or any(_newer(o, [], KERNEL_LIB) for o in objs):
+        # hipBLASLt for the plain prefill GEMMs it measured faster on (driver/blaslt.cpp);
+        # in a torch process the soname resolves to the copy torch already loaded
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs),
-              "-o", str(KERNEL_LIB)])
+              "-o", str(KERNEL_LIB), "-L/opt/rocm/lib", "-lhipblaslt"])
     return KERNEL_LIB
 
 

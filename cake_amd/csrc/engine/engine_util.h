@@ -57,11 +57,15 @@ inline std::string read_file(const std::string& path) {
 // ---------------------------------------------------------------------------
 // GEMM tile plan (ops/gemm.py plan(): measured table, else the cost model)
 // ---------------------------------------------------------------------------
+// plan cfg naming the library GEMM (hipBLASLt, driver/blaslt.cpp; ops/gemm.py LIB)
+constexpr int kGemmLib = -1;
+
 struct GemmPlanner {
   struct Tuned { long long M, Nv, K; std::string epi; int cfg, splits; };
   std::vector<Tuned> tuned;
 
-  void load(const std::string& path) {
+  void load(std::string path) {  // CAKE_GEMM_TABLE overrides (A/B of plan tables)
+    if (const char* e = std::getenv("CAKE_GEMM_TABLE"); e && *e) path = e;
     std::ifstream f(path);
     if (!f) return;
     try {
@@ -69,7 +73,10 @@ struct GemmPlanner {
       static const int known[] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 11, 12, 13, 14, 15, 16, 17, 18, 19};
       for (const auto& e : j.get("entries").items()) {
         const int cfg = (int)e.get("cfg").as_int();
-        if (std::find(std::begin(known), std::end(known), cfg) == std::end(known)) continue;
+        const std::string ep = e.get("epi").as_string();
+        const bool lib = cfg == kGemmLib && (ep == "store" || ep == "resid32" || ep == "store32" ||
+                                             ep == "swiglu");
+        if (!lib && std::find(std::begin(known), std::end(known), cfg) == std::end(known)) continue;
         tuned.push_back({e.get("M").as_int(), e.get("Nv").as_int(), e.get("K").as_int(),
                          e.get("epi").as_string(), cfg, (int)e.get("splits").as_int()});
       }

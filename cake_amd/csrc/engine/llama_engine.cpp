@@ -67,6 +67,10 @@ int cake_flash_attn(int dt, const void* q, const void* k, const void* v, void* o
 int cake_gemm(int dt, int epi, int cfg, int splits, const void* a, long long lda, const void* b,
               long long ldb, void* c, long long ldc, const void* bias, void* resid,
               long long ldr, float* ws, const void* zeros, int M, int N, int K, hipStream_t st);
+int cake_blaslt_gemm(int dt, int out, const void* a, long long lda, const void* w, long long ldw,
+                     void* c, long long ldc, int M, int N, int K, void* ws, size_t ws_bytes,
+                     hipStream_t st);
+int cake_silu_mul_rows(int dt, const void* gu, size_t T, int I, void* out, hipStream_t st);
 int cake_qkv_rope(int dt, const float* resid, const void* norm_w, float eps, const void* wq,
                   const void* wk, const void* wv, int K, int nh, int nkv, int hd,
                   const float* inv_freq, const int* pos, float* q_out, void* kcache,
@@ -826,6 +830,10 @@ class Llama {
   int32_t* ptok_ = nullptr;
   float* ws_ = nullptr;
   size_t ws_n_ = 0;
+  static constexpr size_t kLibWsBytes = 32u << 20;
+  uint8_t* lib_ws_ = nullptr;   // hipBLASLt workspace (first library GEMM)
+  uint16_t* pgu_ = nullptr;     // [T, 2I] gate|up product of a library SwiGLU GEMM
+  size_t pgu_n_ = 0;
   // decode graphs
   std::vector<hipGraphExec_t> execs_;
   std::vector<hipGraph_t> graphs_;
@@ -1190,6 +1198,10 @@ class Llama {
     static const char* names[] = {"store", "resid32", "add16", "swiglu", "geglu", "partial",
                                   "store32"};
     auto p = planner_.plan(M, Nv, K, names[epi]);
+    if (p.first == kGemmLib) {  // the measured table names the library GEMM (hipBLASLt)
+      lib_gemm(epi, a, lda, b, ldb, cptr, ldc, resid, ldr, M, N, K, what);
+      return;
+    }
     const int splits = p.second;
     float* ws = nullptr;
     if (splits > 1) {
@@ -1203,6 +1215,34 @@ class Llama {
     }
     k_check(cake_gemm(dt_, epi, p.first, splits, a, lda, b, ldb, cptr, ldc, nullptr, resid, ldr,
                       ws, zeros_, M, N, K, st_), what);
+  }
+
+  // store -> 16-bit C; store32 / resid32 -> f32 C with beta 0 / 1; swiglu -> the [M, 2N]
+  // product into pgu_, then silu(gate) * up into C
+  void lib_gemm(int epi, const void* a, long long lda, const void* b, long long ldb, void* cptr,
+                long long ldc, float* resid, long long ldr, int M, int N, int K,
+                const char* what) {
+    if (!lib_ws_) lib_ws_ = dalloc<uint8_t>(kLibWsBytes);
+    auto run = [&](int mode, void* c, long long ld, int n) {
+      k_check(cake_blaslt_gemm(dt_, mode, a, lda, b, ldb, c, ld, M, n, K, lib_ws_, kLibWsBytes,
+                               st_), what);
+    };
+    if (epi == kEpiStore) {
+      run(0, cptr, ldc, N);
+    } else if (epi == kEpiStore32 || epi == kEpiResid32) {
+      run(epi == kEpiStore32 ? 1 : 2, resid, ldr, N);
+    } else if (epi == kEpiSwiglu && ldc == N) {
+      const size_t need = (size_t)M * 2 * N;
+      if (need > pgu_n_) {
+        dfree(pgu_);
+        pgu_ = dalloc<uint16_t>(need);
+        pgu_n_ = need;
+      }
+      run(0, pgu_, 2LL * N, 2 * N);
+      k_check(cake_silu_mul_rows(dt_, pgu_, M, N, cptr, st_), what);
+    } else {
+      throw Error(std::string(what) + ": no library form of this epilogue");
+    }
   }
 
   // embed -> this rank's layers -> (pipeline: the other ranks' layers, hidden rows

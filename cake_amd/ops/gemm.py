@@ -37,6 +37,13 @@ NO_GATED = {14, 17, 18, 19}
 _EFF = {0: 1.0, 1: 0.8, 2: 0.8, 3: 0.8, 4: 0.7, 5: 1.2, 6: 0.95, 7: 0.9, 8: 0.9, 11: 1.1,
         12: 0.8, 13: 0.7, 14: 0.8, 15: 0.7, 16: 0.9, 17: 0.9, 18: 0.8, 19: 0.9}
 NUM_CUS = 256
+# plan cfg of the library GEMM (hipBLASLt, csrc/driver/blaslt.cpp): the measured table
+# names it for the plain prefill projections where it was faster on this chip
+# (profiles/r5_gemm_vs_hipblaslt.jsonl); epilogues it can carry: plain store, f32
+# store / accumulate (beta 1), and SwiGLU as library GEMM + silu_mul_rows
+LIB = -1
+LIB_EPIS = ("store", "resid32", "store32", "swiglu")
+_LIB_WS_BYTES = 32 << 20
 _bound = False
 _plans: dict = {}
 _ws: dict = {}
@@ -50,6 +57,8 @@ def _lib():
         P, I, L = C.c_void_p, C.c_int, C.c_longlong
         lib.cake_gemm.argtypes = [I, I, I, I, P, L, P, L, P, L, P, P, L, P, P, I, I, I, P]
         lib.cake_gemm.restype = I
+        lib.cake_blaslt_gemm.argtypes = [I, I, P, L, P, L, P, L, I, I, I, P, C.c_size_t, P]
+        lib.cake_blaslt_gemm.restype = I
         _bound = True
     return lib
 
@@ -80,10 +89,12 @@ def _load_tuned() -> list:
     scripts/gemm_tune_table.py from a bench_gemm.py --sweep on an MI355X)."""
     import json
     import os
-    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_tuned.json")
+    p = os.environ.get("CAKE_GEMM_TABLE") or os.path.join(
+        os.path.dirname(os.path.abspath(__file__)), "gemm_tuned.json")
     try:
         with open(p) as f:
-            return [e for e in json.load(f)["entries"] if e["cfg"] in CFG_TILES]
+            return [e for e in json.load(f)["entries"]
+                    if e["cfg"] in CFG_TILES or (e["cfg"] == LIB and e["epi"] in LIB_EPIS)]
     except (OSError, ValueError, KeyError):
         return []
 
@@ -120,6 +131,11 @@ def plan(M: int, Nv: int, K: int, epi: str = "store") -> tuple[int, int]:
     if p is not None:
         _plans[(M, Nv, K, epi)] = p
         return p
+    return _cost_plan(M, Nv, K)
+
+
+def _cost_plan(M: int, Nv: int, K: int) -> tuple[int, int]:
+    """The MFMA kernel's (cfg, splits) by the cost model."""
     best = None
     ksteps = -(-K // 64)
     cands = (1, 4, 0) if M <= 64 else (0, 1, 4, 5)
@@ -233,6 +249,11 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, *
         return resid if f32_out else out
     c0, s0 = plan(M, Nv, K, epi)
     cfg = c0 if cfg is None else cfg
+    if cfg == LIB and bias is None and epi in LIB_EPIS:
+        _lib_gemm(x2, lda, w, ldb, epi, out2, ldc, r2 if f32_out else None, ldr, M, N, K)
+        return resid if f32_out else out
+    if cfg == LIB:
+        cfg, s0 = _cost_plan(M, Nv, K)
     splits = s0 if splits is None else max(1, int(splits))
     ws = _workspace(x.device, splits * M * Nv) if splits > 1 else None
     check(_lib().cake_gemm(_DT[x.dtype], EPI[epi], int(cfg), int(splits), x2.data_ptr(), lda,
@@ -241,3 +262,31 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, *
                            None if ws is None else ws.data_ptr(), _zeros16(x.device).data_ptr(),
                            M, N, K, torch.cuda.current_stream().cuda_stream), "gemm")
     return resid if f32_out else out
+
+
+def _lib_gemm(x2, lda, w, ldb, epi, out2, ldc, r2, ldr, M, N, K) -> None:
+    """The library GEMM (hipBLASLt) for a plan that names it."""
+    dev = x2.device
+    ws = _lib_ws.get(dev)
+    if ws is None:
+        ws = _lib_ws[dev] = torch.empty(_LIB_WS_BYTES, dtype=torch.uint8, device=dev)
+    st = torch.cuda.current_stream().cuda_stream
+    dt = _DT[x2.dtype]
+
+    def run(mode, cptr, ld, n):
+        check(_lib().cake_blaslt_gemm(dt, mode, x2.data_ptr(), lda, w.data_ptr(), ldb, cptr, ld,
+                                      M, n, K, ws.data_ptr(), _LIB_WS_BYTES, st), "blaslt gemm")
+    if epi == "store":
+        run(0, out2.data_ptr(), ldc, N)
+    elif epi in ("store32", "resid32"):
+        run(1 if epi == "store32" else 2, r2.data_ptr(), ldr, N)
+    else:  # swiglu: [M, 2N] library product, then silu(gate) * up
+        if ldc != N:
+            raise ValueError("library swiglu needs a contiguous output")
+        gu = torch.empty(M, 2 * N, device=dev, dtype=x2.dtype)
+        run(0, gu.data_ptr(), 2 * N, 2 * N)
+        check(kernels().cake_silu_mul_rows(dt, gu.data_ptr(), M, N, out2.data_ptr(), st),
+              "silu_mul_rows")
+
+
+_lib_ws: dict = {}

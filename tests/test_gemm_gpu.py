@@ -159,3 +159,34 @@ def test_gemm_interleaved_all_epilogues(cuda, dt, cfg, M, N, K):
         return
     y = _ref(x, w2)
     _close(G.linear(x, w2, epi="swiglu", cfg=cfg, splits=1), F.silu(y[:, :Fh]) * y[:, Fh:], K)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("epi", ["store", "store32", "resid32", "swiglu"])
+@pytest.mark.parametrize("M,N,K", [(513, 1024, 4096), (64, 640, 1280), (2048, 4096, 4096)])
+def test_library_gemm_path(cuda, dt, epi, M, N, K):
+    """The plan cfg LIB (hipBLASLt, csrc/driver/blaslt.cpp): every epilogue it carries,
+    against the f32 reference; strided input rows and a strided f32 output."""
+    from cake_amd.ops import _lib
+    from cake_amd.ops import gemm as G
+    torch.manual_seed(M + N)
+    lib = _lib.kernels()
+    assert hasattr(lib, "cake_blaslt_gemm"), "library GEMM entry point missing"
+    xs = _r(M, K + 64, dt=dt)
+    x = xs[:, 16:16 + K]                     # row stride K + 64
+    Nv = 2 * N if epi == "swiglu" else N
+    w = _r(Nv, K, dt=dt, std=K ** -0.5)
+    y = _ref(x, w)
+    if epi == "store":
+        _close(G.linear(x, w, cfg=G.LIB), y, K)
+    elif epi == "swiglu":
+        ref = F.silu(y[:, :N]) * y[:, N:]
+        _close(G.linear(x, w, epi="swiglu", cfg=G.LIB), ref, K)
+    else:
+        big = torch.randn(M, N + 8, device="cuda")
+        r = big[:, :N]                       # f32 output with row stride N + 8
+        ref = (r + y) if epi == "resid32" else y
+        pad = big[:, N:].clone()
+        G.linear(x, w, epi=epi, resid=r, cfg=G.LIB)
+        torch.testing.assert_close(r, ref, atol=3e-2, rtol=1e-2)
+        assert torch.equal(big[:, N:], pad)  # the row padding is not written

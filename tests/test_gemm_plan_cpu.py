@@ -41,7 +41,11 @@ def test_tuned_table_entries_are_launchable():
         key = (e["M"], e["Nv"], e["K"], e["epi"])
         assert key not in seen, f"duplicate plan {key}"
         seen.add(key)
-        assert e["cfg"] in G.CFG_TILES and e["splits"] >= 1 and e["epi"] in G.EPI, e
+        assert e["splits"] >= 1 and e["epi"] in G.EPI, e
+        if e["cfg"] == G.LIB:  # the library GEMM: only the epilogues it carries
+            assert e["epi"] in G.LIB_EPIS and e["splits"] == 1, e
+            continue
+        assert e["cfg"] in G.CFG_TILES, e
         if e["epi"] in ("swiglu", "geglu"):
             assert e["cfg"] not in G.NO_GATED and e["Nv"] % 32 == 0, e
         assert e["K"] % 8 == 0, e
@@ -53,7 +57,22 @@ def test_plan_uses_measured_entries():
     assert G.plan(e["M"], e["Nv"], e["K"], e["epi"]) == (e["cfg"], e["splits"])
     # a nearby M (within 2x) reuses the measured tile without split-K
     cfg, splits = G.plan(e["M"] + 8, e["Nv"], e["K"], e["epi"])
-    assert cfg in G.CFG_TILES and splits == 1
+    assert (cfg in G.CFG_TILES or cfg == G.LIB) and splits == 1
     # an unmeasured shape falls back to the cost model
     cfg, splits = G.plan(333, 4448, 1024, "store")
     assert cfg in G.CFG_TILES and splits >= 1
+
+
+def test_library_gemm_plans_agree_with_the_engine():
+    """The measured table sends the large Llama prefill projections to the library GEMM
+    (profiles/r5_gemm_lib.jsonl); the engine planner accepts the same cfg for the same
+    epilogues, and the small-M shapes stay on the MFMA kernel where it measured faster."""
+    eng = (ROOT / "cake_amd/csrc/engine/engine_util.h").read_text()
+    assert re.search(r"constexpr int kGemmLib = (-?\d+);", eng).group(1) == str(G.LIB)
+    body = eng[eng.index("const bool lib = "):]
+    body = body[:body.index(";")]
+    assert set(re.findall(r'ep == "(\w+)"', body)) == set(G.LIB_EPIS)
+    assert G.plan(2048, 28672, 4096, "swiglu")[0] == G.LIB       # 8B gate|up, 2048 tokens
+    assert G.plan(2048, 6144, 4096, "store")[0] == G.LIB         # 8B q|k|v
+    assert G.plan(256, 6144, 4096, "store")[0] in G.CFG_TILES    # ours at 256 tokens
+    assert G.plan(2048, 1280, 5120, "add16")[0] in G.CFG_TILES   # SD shapes untouched
