@@ -849,10 +849,31 @@ class SdEngine {
     widen(y, (size_t)2 * cfg_.vae.latent * (cfg_.height / 8) * (cfg_.width / 8), moments);
   }
 
+  // img2img with the topology's VAE worker: pack([1 (encode), img]) -> the latent SAMPLE
+  // [1, 4, h, w] (the worker draws the posterior noise, as the Python client path does)
+  void vae_encode_remote(const float* img, float* sample) {
+    if (remote_[1].addr.empty()) throw Error("no remote VAE in this engine");
+    const float dir = 1.f;
+    const std::vector<float> pk = pack(
+        {{&dir, {1}}, {img, {1, 3, (uint64_t)cfg_.height, (uint64_t)cfg_.width}}});
+    const size_t nl = (size_t)4 * (cfg_.height / 8) * (cfg_.width / 8);
+    const std::vector<float> y = remote_call(remote_[1], "vae", pk, {(uint64_t)pk.size()}, nl);
+    std::copy(y.begin(), y.end(), sample);
+  }
+
   void vae_component(const float* zin, float* img) {
     hip_check(hipSetDevice(dev_), "hipSetDevice");
-    need(2, "vae");
     const int h = cfg_.height / 8, w = cfg_.width / 8;
+    if (!remote_[1].addr.empty()) {  // the topology's VAE worker: pack([0 (decode), z])
+      const float dir = 0.f;
+      const std::vector<float> pk =
+          pack({{&dir, {1}}, {zin, {1, 4, (uint64_t)h, (uint64_t)w}}});
+      const std::vector<float> y = remote_call(remote_[1], "vae", pk, {(uint64_t)pk.size()},
+                                               (size_t)3 * cfg_.height * cfg_.width);
+      std::copy(y.begin(), y.end(), img);
+      return;
+    }
+    need(2, "vae");
     vae_a_.reset();
     uint16_t* z = new16(vae_a_, (size_t)4 * h * w);
     upload16(zin, (size_t)4 * h * w, z);
@@ -2080,6 +2101,17 @@ CAKE_API int32_t cake_sd_unet(void* eng, const float* sample, int32_t B, float t
 CAKE_API int32_t cake_sd_vae_decode(void* eng, const float* z, float* img, char* err, int32_t n) {
   try {
     static_cast<SdEngine*>(eng)->vae_component(z, img);
+    return 0;
+  } catch (const std::exception& e) {
+    cake::set_err(err, n, e.what());
+    return 1;
+  }
+}
+
+CAKE_API int32_t cake_sd_vae_encode_remote(void* eng, const float* img, float* sample, char* err,
+                                           int32_t n) {
+  try {
+    static_cast<SdEngine*>(eng)->vae_encode_remote(img, sample);
     return 0;
   } catch (const std::exception& e) {
     cake::set_err(err, n, e.what());

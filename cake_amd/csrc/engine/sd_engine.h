@@ -111,6 +111,11 @@ int32_t cake_sd_vae_decode(void* engine, const float* z, float* img, char* err, 
 // (mean | logvar; the caller samples, as vae.py AutoencoderKL.encode does).
 int32_t cake_sd_vae_encode(void* engine, const float* img, float* moments, char* err,
                            int32_t errlen);
+// img2img with the topology's VAE worker: the image [1, 3, H, W] -> the latent sample
+// [1, 4, h, w] drawn by the worker (SingleOp "vae" on pack([1, img])).  With a remote VAE,
+// cake_sd_vae_decode goes to the worker as well.
+int32_t cake_sd_vae_encode_remote(void* engine, const float* img, float* sample, char* err,
+                                  int32_t errlen);
 
 #ifdef __cplusplus
 }

@@ -13,7 +13,8 @@ generators and torch ops as the Python pipeline, and the engine denoises from th
 bsize > 1 (the UNet over 2 bsize rows, the reference's repeated text rows), intermediary
 images (decoded by the engine between steps, handed back through a callback) and tracing
 (the Chrome trace spans — text embeddings, every step, VAE decode — rebuilt from the
-engine's own phase and per-step device timings) are native; img2img with bsize > 1 runs on
+engine's own phase and per-step device timings) are native (img2img with a remote VAE
+too: the worker encodes and draws the sample); img2img with bsize > 1 runs on
 the Python pipeline, built on first use.
 """
 from __future__ import annotations
@@ -110,9 +111,12 @@ class NativeSDGenerator(ImageGenerator):
         img = image_preprocess(path)
         if tuple(img.shape[2:]) != (self.cfg.height, self.cfg.width):
             return None
-        mo = torch.from_numpy(self.eng.vae_encode(img.numpy()))
         dev = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
         dt = torch.bfloat16 if self.eng._dt == 0 else torch.float16
+        if "vae" in self.eng.remote:  # the worker encodes and draws the sample
+            x = img.to(dt).float().numpy()  # the model-dtype image the client path sends
+            return torch.from_numpy(self.eng.vae_encode_remote(x)).to(dev).to(dt)
+        mo = torch.from_numpy(self.eng.vae_encode(img.numpy()))
         moments = mo.to(dev).to(dt).float()
         mean, logvar = moments.chunk(2, 1)
         logvar = logvar.clamp(-30.0, 20.0)
@@ -121,7 +125,7 @@ class NativeSDGenerator(ImageGenerator):
 
     def generate_image(self, args: ImageGenerationArgs, callback: Callable[[list], None]) -> None:
         init = None
-        if args.img2img and args.bsize == 1 and "vae" not in self.eng.remote:
+        if args.img2img and args.bsize == 1:
             if not 0.0 <= args.img2img_strength <= 1.0:
                 raise ValueError("img2img-strength should be between 0 and 1, got "
                                  f"{args.img2img_strength}")

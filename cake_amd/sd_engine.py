@@ -81,6 +81,8 @@ def lib() -> C.CDLL:
         L.cake_sd_vae_decode.restype = I
         L.cake_sd_vae_encode.argtypes = [P, FP, FP, C.c_char_p, I]
         L.cake_sd_vae_encode.restype = I
+        L.cake_sd_vae_encode_remote.argtypes = [P, FP, FP, C.c_char_p, I]
+        L.cake_sd_vae_encode_remote.restype = I
         _bound = True
     return L
 
@@ -244,6 +246,15 @@ class NativeSD:
         err = C.create_string_buffer(1024)
         self._check(lib().cake_sd_vae_encode(self._h, _fp(x), _fp(mo), err, 1024), err)
         return mo
+
+    def vae_encode_remote(self, img) -> np.ndarray:
+        """img2img with the topology's VAE worker: image [1, 3, H, W] -> the latent sample
+        [1, 4, h, w] the worker draws (the Python client path's semantics)."""
+        x = _f32(img)
+        out = np.empty((1, 4, self.height // 8, self.width // 8), dtype=np.float32)
+        err = C.create_string_buffer(1024)
+        self._check(lib().cake_sd_vae_encode_remote(self._h, _fp(x), _fp(out), err, 1024), err)
+        return out
 
     def close(self) -> None:
         if getattr(self, "_h", None):

@@ -448,6 +448,25 @@ def test_native_master_with_remote_sd_components(cuda, mini, tmp_path, monkeypat
         assert len(rg.last_step_s) == 3
         lg, local_img = image(empty)
         assert isinstance(lg, NativeSDGenerator) and not lg.eng.remote
+        if "vae" in served:  # img2img through the worker's VAE, natively
+            import torch
+
+            from cake_amd.models.sd.pipeline import image_preprocess
+            init = tmp_path / "init.png"
+            remote_img.save(init)
+            smp = rg._encode_image(str(init)).float().cpu()  # the worker's posterior sample
+            mo = torch.from_numpy(lg.eng.vae_encode(image_preprocess(str(init)).numpy()))
+            mean, logvar = mo.chunk(2, 1)
+            z = (smp - mean) / torch.exp(0.5 * logvar.clamp(-30.0, 20.0))
+            assert torch.isfinite(z).all() and z.abs().max() < 8, z.abs().max()
+            assert 0.7 < float(z.std()) < 1.3, float(z.std())   # mean + std * N(0, 1)
+            out2 = []
+            rg.generate_image(ImageGenerationArgs(image_prompt="a red cube", n_steps=4,
+                                                  image_seed=3, img2img=str(init),
+                                                  img2img_strength=0.5),
+                              lambda imgs: out2.append(imgs))
+            assert rg._fallback is None and len(rg.last_step_s) == 2
+            assert np.asarray(out2[-1][0]).shape == (cfg.height, cfg.width, 3)
     finally:
         for g in gens:
             g.eng.close()
