@@ -190,3 +190,52 @@ def test_library_gemm_path(cuda, dt, epi, M, N, K):
         G.linear(x, w, epi=epi, resid=r, cfg=G.LIB)
         torch.testing.assert_close(r, ref, atol=3e-2, rtol=1e-2)
         assert torch.equal(big[:, N:], pad)  # the row padding is not written
+
+
+_NO_TORCH_LIB_GEMM = r"""
+import ctypes as C, sys
+import numpy as np
+hip = C.CDLL("libamdhip64.so")
+lib = C.CDLL(sys.argv[1])
+assert "torch" not in sys.modules
+M, N, K = 300, 512, 1024
+rng = np.random.default_rng(0)
+def bf16(a):  # round-to-nearest-even f32 -> bf16 bits
+    u = a.astype(np.float32).view(np.uint32)
+    return ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
+x, w = rng.standard_normal((M, K)), rng.standard_normal((N, K)) / 32
+xb, wb = bf16(x), bf16(w)
+c0 = rng.standard_normal((M, N)).astype(np.float32)
+ptr = lambda: C.c_void_p()
+dx, dw, dc, ws = ptr(), ptr(), ptr(), ptr()
+for p, n in ((dx, xb.nbytes), (dw, wb.nbytes), (dc, c0.nbytes), (ws, 32 << 20)):
+    assert hip.hipMalloc(C.byref(p), C.c_size_t(n)) == 0
+H2D, D2H = 1, 2
+for p, a in ((dx, xb), (dw, wb), (dc, c0)):
+    assert hip.hipMemcpy(p, a.ctypes.data_as(C.c_void_p), C.c_size_t(a.nbytes), H2D) == 0
+L = C.c_longlong
+rc = lib.cake_blaslt_gemm(0, 2, dx, L(K), dw, L(K), dc, L(N), M, N, K, ws,
+                          C.c_size_t(32 << 20), C.c_void_p(0))
+assert rc == 0, rc
+assert hip.hipDeviceSynchronize() == 0
+out = np.empty_like(c0)
+assert hip.hipMemcpy(out.ctypes.data_as(C.c_void_p), dc, C.c_size_t(out.nbytes), D2H) == 0
+f = lambda b: (b.astype(np.uint32) << 16).view(np.float32).astype(np.float64)
+ref = c0 + f(xb) @ f(wb).T
+err = np.abs(out - ref).max()
+assert err < 1e-2 * np.abs(ref).max(), err
+maps = open("/proc/self/maps").read()
+print("ok", err, "libhipblaslt from", sorted({l.split()[-1] for l in maps.splitlines() if "libhipblaslt" in l}))
+"""
+
+
+def test_library_gemm_without_torch(cuda):
+    """The native engine / cake-cli / native worker processes load no torch: the kernel
+    library's hipBLASLt dependency resolves on its own (RUNPATH) and the f32-accumulate
+    GEMM is right there too."""
+    import subprocess
+    import sys
+    from cake_amd.ops import _lib
+    r = subprocess.run([sys.executable, "-c", _NO_TORCH_LIB_GEMM, str(_lib.lib_path())],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.startswith("ok"), r.stdout + r.stderr[-3000:]
