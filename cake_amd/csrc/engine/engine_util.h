@@ -94,7 +94,13 @@ struct GemmPlanner {
       const double r = (double)std::max(M, e.M) / (double)std::min(M, e.M);
       if (r <= 2 && (!near || r < near_r)) { near = &e; near_r = r; }
     }
-    if (near) return {near->cfg, 1};
+    if (near) {  // split-K scaled to this M (ops/gemm.py _near_splits)
+      if (near->cfg == kGemmLib) return {kGemmLib, 1};
+      long long sc = (long long)near->splits * near->M / std::max(M, 1LL);
+      int p = 1;
+      while ((long long)p * 2 <= sc) p *= 2;
+      return {near->cfg, p};
+    }
     struct T { int cfg, bm, bn, slots; double eff; };
     static const T tiles[] = {{0, 128, 128, 2, 1.0}, {1, 64, 128, 2, 0.8}, {4, 64, 64, 4, 0.7},
                               {5, 256, 256, 1, 1.2}};

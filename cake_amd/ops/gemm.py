@@ -102,19 +102,42 @@ def _load_tuned() -> list:
 _TUNED = _load_tuned()
 
 
-def _tuned(M: int, Nv: int, K: int, epi: str):
-    """Exact measured shape, else the same (Nv, K, epilogue) measured at an M within 2x
-    (its tile config, without split-K)."""
+def _near_splits(splits: int, m_near: int, M: int) -> int:
+    """Split-K of a measured neighbour scaled to this M (the split fills the grid the
+    neighbour's M left short: twice the rows, half the splits), a power of two >= 1."""
+    s = splits * m_near // max(M, 1)
+    p = 1
+    while p * 2 <= s:
+        p *= 2
+    return p
+
+
+def _tuned(M: int, Nv: int, K: int, epi: str, mfma_only: bool = False):
+    """Exact measured shape, else the same (Nv, K, epilogue) measured at the nearest M
+    within 2x (its tile config, split-K scaled to this M).  mfma_only skips the library
+    GEMM's entries."""
     near = None
     for e in _TUNED:
         if e["Nv"] != Nv or e["K"] != K or e["epi"] != epi:
+            continue
+        if mfma_only and e["cfg"] == LIB:
             continue
         if e["M"] == M:
             return e["cfg"], e["splits"]
         r = max(M, e["M"]) / min(M, e["M"])
         if r <= 2 and (near is None or r < near[0]):
-            near = (r, e["cfg"])
-    return (near[1], 1) if near else None
+            near = (r, e)
+    if near is None:
+        return None
+    e = near[1]
+    return e["cfg"], (1 if e["cfg"] == LIB else _near_splits(e["splits"], e["M"], M))
+
+
+def plan_mfma(M: int, Nv: int, K: int, epi: str = "store") -> tuple[int, int]:
+    """The MFMA kernel's (cfg, splits) for a shape: its measured entries, else the cost
+    model (the library GEMM's entries ignored)."""
+    p = _tuned(M, Nv, K, epi, mfma_only=True)
+    return p if p is not None else _cost_plan(M, Nv, K)
 
 
 def set_plan(M: int, N: int, K: int, epi: str, cfg: int, splits: int) -> None:
@@ -252,8 +275,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, *
     if cfg == LIB and bias is None and epi in LIB_EPIS:
         _lib_gemm(x2, lda, w, ldb, epi, out2, ldc, r2 if f32_out else None, ldr, M, N, K)
         return resid if f32_out else out
-    if cfg == LIB:
-        cfg, s0 = _cost_plan(M, Nv, K)
+    if cfg == LIB:  # an epilogue / bias the library form does not carry
+        cfg, s0 = plan_mfma(M, Nv, K, epi)
     splits = s0 if splits is None else max(1, int(splits))
     ws = _workspace(x.device, splits * M * Nv) if splits > 1 else None
     check(_lib().cake_gemm(_DT[x.dtype], EPI[epi], int(cfg), int(splits), x2.data_ptr(), lda,

@@ -44,6 +44,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--models", default="8b,70b")
     ap.add_argument("--ms", default="128,256,384,512,768,1024,1536,2048,3072,4096")
+    ap.add_argument("--sweep-splits", action="store_true",
+                    help="time the MFMA plan's tile at split-K 1/2/4/8 and keep the best")
     a = ap.parse_args()
     torch.manual_seed(0)
     for model in a.models.split(","):
@@ -53,9 +55,7 @@ def main():
             for M in [int(m) for m in a.ms.split(",")]:
                 x = (torch.randn(M, K, device="cuda") * 0.5).bfloat16()
                 r0 = torch.randn(M, N, device="cuda") if epi == "resid32" else None
-                cfg, spl = G.plan(M, Nv, K, epi)
-                if cfg == G.LIB:
-                    cfg, spl = G._cost_plan(M, Nv, K)
+                cfg, spl = G.plan_mfma(M, Nv, K, epi)
                 outs = {}
 
                 def run(kind):
@@ -85,6 +85,18 @@ def main():
 
                 def lib():
                     G.linear(x, w, epi=epi, resid=rr, out=out, cfg=G.LIB, splits=1)
+                if a.sweep_splits:
+                    best = None
+                    for sp in (1, 2, 4, 8):
+                        if sp > 1 and K // sp < 256:
+                            continue
+                        def f(sp=sp):
+                            G.linear(x, w, epi=epi, resid=rr, out=out, cfg=cfg, splits=sp)
+                        f()
+                        t = min(timeit(f, 10) for _ in range(2))
+                        if best is None or t < best[0]:
+                            best = (t, sp)
+                    spl = best[1]
                 ours(), lib()
                 torch.cuda.synchronize()
                 to = tl = 1e9

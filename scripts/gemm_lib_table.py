@@ -28,7 +28,9 @@ def main(path):
                      "tflops": r["lib_tflops"] if use_lib else r["ours_tflops"],
                      "shape": f"llama{r['model']}_{r['proj']}"})
     t["entries"] = kept
-    t["lib_source"] = os.path.basename(path) + " (cfg -1 = hipBLASLt where >= 3% faster)"
+    srcs = [x for x in t.get("lib_sources", []) if x != os.path.basename(path)]
+    t["lib_sources"] = srcs + [os.path.basename(path)]  # cfg -1 = hipBLASLt where >= 3% faster
+    t.pop("lib_source", None)
     with open(table, "w") as f:
         json.dump(t, f, indent=1)
     print(f"{len(rows)} shapes merged, {lib} on the library GEMM")

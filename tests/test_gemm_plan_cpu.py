@@ -76,3 +76,21 @@ def test_library_gemm_plans_agree_with_the_engine():
     assert G.plan(2048, 6144, 4096, "store")[0] == G.LIB         # 8B q|k|v
     assert G.plan(256, 6144, 4096, "store")[0] in G.CFG_TILES    # ours at 256 tokens
     assert G.plan(2048, 1280, 5120, "add16")[0] in G.CFG_TILES   # SD shapes untouched
+
+
+def test_nearest_measured_plan_scales_split_k(monkeypatch):
+    """A shape measured at M with split-K s, asked at M' within 2x: the same tile with
+    s * M / M' splits (a power of two >= 1) — the grid fill the split was chosen for —
+    and a library entry stays a library plan; the engine planner applies the same rule."""
+    monkeypatch.setattr(G, "_TUNED", [
+        {"M": 32, "Nv": 4096, "K": 14336, "epi": "resid32", "cfg": 13, "splits": 4},
+        {"M": 1024, "Nv": 4096, "K": 14336, "epi": "resid32", "cfg": G.LIB, "splits": 1}])
+    monkeypatch.setattr(G, "_plans", {})
+    assert G.plan(32, 4096, 14336, "resid32") == (13, 4)
+    assert G.plan(64, 4096, 14336, "resid32") == (13, 2)
+    assert G.plan(40, 4096, 14336, "resid32") == (13, 2)
+    assert G.plan(20, 4096, 14336, "resid32") == (13, 4)   # 6.4 -> 4
+    assert G.plan(1500, 4096, 14336, "resid32") == (G.LIB, 1)
+    assert G.plan_mfma(1500, 4096, 14336, "resid32")[0] in G.CFG_TILES
+    eng = (ROOT / "cake_amd/csrc/engine/engine_util.h").read_text()
+    assert "near->splits * near->M / std::max(M, 1LL)" in eng
