@@ -55,6 +55,49 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const float* __restrict__ 
   }
 }
 
+// The same for H <= 1024 * NV: the row's x and w slices are loaded once, all up front,
+// into registers (one round of load latency instead of a dependent chain per 1024
+// columns and a second pass over x)
+template <int DT, int NV>
+__global__ __launch_bounds__(256) void rmsnorm_reg_kernel(const float* __restrict__ x,
+                                                          const uint16_t* __restrict__ w,
+                                                          float eps, int H,
+                                                          uint16_t* __restrict__ out) {
+  __shared__ float red[16];
+  const float* xr = x + (size_t)blockIdx.x * H;
+  float4 v[NV];
+  uint2 wv[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int i = (threadIdx.x + j * 256) * 4;
+    if (i < H) {
+      v[j] = *reinterpret_cast<const float4*>(xr + i);
+      wv[j] = *reinterpret_cast<const uint2*>(w + i);
+    } else {
+      v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      wv[j] = make_uint2(0u, 0u);
+    }
+  }
+  float ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < NV; ++j)
+    ss += v[j].x * v[j].x + v[j].y * v[j].y + v[j].z * v[j].z + v[j].w * v[j].w;
+  ss = block_sum(ss, red);
+  const float r = rsqrtf(ss / (float)H + eps);
+  uint16_t* o = out + (size_t)blockIdx.x * H;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int i = (threadIdx.x + j * 256) * 4;
+    if (i >= H) continue;
+    uint2 ov;
+    ov.x = (uint32_t)from_f32<DT>(v[j].x * r * to_f32<DT>((uint16_t)(wv[j].x & 0xffff))) |
+           ((uint32_t)from_f32<DT>(v[j].y * r * to_f32<DT>((uint16_t)(wv[j].x >> 16))) << 16);
+    ov.y = (uint32_t)from_f32<DT>(v[j].z * r * to_f32<DT>((uint16_t)(wv[j].y & 0xffff))) |
+           ((uint32_t)from_f32<DT>(v[j].w * r * to_f32<DT>((uint16_t)(wv[j].y >> 16))) << 16);
+    *reinterpret_cast<uint2*>(o + i) = ov;
+  }
+}
+
 // Prefill RoPE: q [T, nh*hd] roped in place; k roped and v copied into the
 // cache rows pos0+t of [nkv][S][hd].
 template <int DT>
@@ -365,9 +408,20 @@ CAKE_API int cake_embed(int dt, const void* table, const int* tok, int T, int H,
   return (int)hipGetLastError();
 }
 
+static int g_rmsnorm_reg = 1;  // 0: the two-pass loop kernel (A/B, tests)
+CAKE_API void cake_rmsnorm_set_reg(int on) { g_rmsnorm_reg = on; }
+
 CAKE_API int cake_rmsnorm(int dt, const float* x, const void* w, float eps, int T, int H,
                           void* out, hipStream_t st) {
   if (H % 4) return (int)hipErrorInvalidValue;
+  // register-resident rows up to 8192 columns (every Llama hidden size); wider rows loop
+  if (H <= 8192 && g_rmsnorm_reg) {
+#define CAKE_RMS(NV) hipLaunchKernelGGL((rmsnorm_reg_kernel<DT, NV>), dim3(T), dim3(256), 0, st, x, \
+                                        (const uint16_t*)w, eps, H, (uint16_t*)out)
+    DISPATCH_DT(dt, if (H <= 2048) CAKE_RMS(2); else if (H <= 4096) CAKE_RMS(4); else CAKE_RMS(8));
+#undef CAKE_RMS
+    return (int)hipGetLastError();
+  }
   DISPATCH_DT(dt, hipLaunchKernelGGL((rmsnorm_kernel<DT>), dim3(T), dim3(256), 0, st, x,
                                      (const uint16_t*)w, eps, H, (uint16_t*)out));
   return (int)hipGetLastError();

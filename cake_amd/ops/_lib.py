@@ -46,6 +46,7 @@ _SIGS = {
     "cake_wave_reduce_probe": [P, P, P],
     "cake_embed": [I, P, P, I, I, P, P],
     "cake_rmsnorm": [I, P, P, F, I, I, P, P],
+    "cake_rmsnorm_set_reg": [I],
     "cake_rope_kv": [I, P, P, P, I, I, I, I, I, I, P, I, I, P, P, P],
     "cake_silu_mul": [I, P, P, Z, P, P],
     "cake_silu_mul_rows": [I, P, Z, I, P, P],
@@ -142,7 +143,7 @@ _SIGS.update({
     "cake_mk_supported": [I, I, I, I, I],
     "cake_mk_decode": [I, P, I, I, I, I, I, I, I, F, F, P, P, P, P, P, C.c_double, P],
 })
-_RESTYPE = {"cake_mk_gstride": C.c_longlong}
+_RESTYPE = {"cake_mk_gstride": C.c_longlong, "cake_rmsnorm_set_reg": None}
 # entry points of csrc/experimental (not in the default build)
 _OPTIONAL = {"cake_mk_gstride", "cake_mk_grid", "cake_mk_supported", "cake_mk_decode",
              "cake_mk_set_stamps", "cake_mk_set_tuning",

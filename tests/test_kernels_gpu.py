@@ -287,6 +287,28 @@ def test_embed_rmsnorm_silu_add(cuda, dt):
     torch.testing.assert_close(resid, ref)
 
 
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("H", [64, 1004, 2048, 3072, 4096, 5120, 8192, 12288])
+@pytest.mark.parametrize("reg", [1, 0])
+def test_rmsnorm_widths(cuda, dt, H, reg):
+    """Prefill RMSNorm: the register-resident row kernel (H <= 8192, partial last
+    vector group) and the two-pass loop kernel, against the f32 reference."""
+    from cake_amd.ops import _lib
+    from cake_amd.ops import hip as K_
+    torch.manual_seed(H)
+    T = 37
+    x = torch.randn(T, H, device=cuda) * 3
+    w = (1 + 0.1 * torch.randn(H, device=cuda)).to(dt)
+    out = torch.empty(T, H, device=cuda, dtype=dt)
+    lib = _lib.kernels()
+    lib.cake_rmsnorm_set_reg(reg)
+    try:
+        K_.rmsnorm(x, w, 1e-5, out)
+    finally:
+        lib.cake_rmsnorm_set_reg(1)
+    torch.testing.assert_close(out.float(), R.rms_norm(x, w, 1e-5), **_tol(dt))
+
+
 def test_penalty_argmax_finalize(cuda):
     from cake_amd.ops import hip as K_
     torch.manual_seed(7)
