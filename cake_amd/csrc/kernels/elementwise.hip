@@ -150,6 +150,10 @@ __global__ __launch_bounds__(256) void rope_kv_vec_kernel(
     uint16_t* __restrict__ kc, uint16_t* __restrict__ vc) {
   const int t = blockIdx.x, pos = pos0 + t, half = hd >> 1, hv = half >> 3;
   const int nrope = (nh + nkv) * hv, nv = nkv * (hd >> 3);
+  // the token's rotation angles once (shared by its nh + nkv heads), not per head
+  __shared__ float s_sn[128], s_cs[128];
+  for (int i = threadIdx.x; i < half; i += blockDim.x) sincosf((float)pos * inv_freq[i], &s_sn[i], &s_cs[i]);
+  __syncthreads();
   for (int p = threadIdx.x; p < nrope + nv; p += blockDim.x) {
     if (p < nrope) {
       const int head = p / hv, i0 = (p - head * hv) * 8;
@@ -162,8 +166,7 @@ __global__ __launch_bounds__(256) void rope_kv_vec_kernel(
       uint16_t oa[8], ob[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        float sn, cs;
-        sincosf((float)pos * inv_freq[i0 + e], &sn, &cs);
+        const float sn = s_sn[i0 + e], cs = s_cs[i0 + e];
         oa[e] = from_f32<DT>(a[e] * cs - b[e] * sn);
         ob[e] = from_f32<DT>(a[e] * sn + b[e] * cs);
       }
@@ -432,7 +435,7 @@ CAKE_API int cake_rmsnorm(int dt, const float* x, const void* w, float eps, int 
 CAKE_API int cake_rope_kv(int dt, void* q, const void* k, const void* v, int ldq, int ld, int T, int nh,
                           int nkv, int hd, const float* inv_freq, int pos0, int S, void* kc,
                           void* vc, hipStream_t st) {
-  const bool vec = hd % 16 == 0 && ldq % 8 == 0 && ld % 8 == 0 &&
+  const bool vec = hd % 16 == 0 && hd <= 256 && ldq % 8 == 0 && ld % 8 == 0 &&
                    ((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)kc | (uintptr_t)vc) % 16 == 0;
   if (vec) {
     DISPATCH_DT(dt, hipLaunchKernelGGL((rope_kv_vec_kernel<DT>), dim3(T), dim3(256), 0, st,
