@@ -85,11 +85,19 @@ struct GemmPlanner {
     }
   }
 
-  std::pair<int, int> plan(long long M, long long Nv, long long K, const std::string& epi) const {
+  // the MFMA kernel's plan: the measured entries other than the library GEMM's
+  std::pair<int, int> plan_mfma(long long M, long long Nv, long long K,
+                                const std::string& epi) const {
+    return plan(M, Nv, K, epi, true);
+  }
+
+  std::pair<int, int> plan(long long M, long long Nv, long long K, const std::string& epi,
+                           bool mfma_only = false) const {
     const Tuned* near = nullptr;
     double near_r = 0;
     for (const auto& e : tuned) {
       if (e.Nv != Nv || e.K != K || e.epi != epi) continue;
+      if (mfma_only && e.cfg == kGemmLib) continue;
       if (e.M == M) return {e.cfg, e.splits};
       const double r = (double)std::max(M, e.M) / (double)std::min(M, e.M);
       if (r <= 2 && (!near || r < near_r)) { near = &e; near_r = r; }

@@ -1199,8 +1199,11 @@ class Llama {
                                   "store32"};
     auto p = planner_.plan(M, Nv, K, names[epi]);
     if (p.first == kGemmLib) {  // the measured table names the library GEMM (hipBLASLt)
-      lib_gemm(epi, a, lda, b, ldb, cptr, ldc, resid, ldr, M, N, K, what);
-      return;
+      if (epi != kEpiSwiglu || ldc == N) {
+        lib_gemm(epi, a, lda, b, ldb, cptr, ldc, resid, ldr, M, N, K, what);
+        return;
+      }
+      p = planner_.plan_mfma(M, Nv, K, names[epi]);  // a strided SwiGLU output: the kernel
     }
     const int splits = p.second;
     float* ws = nullptr;

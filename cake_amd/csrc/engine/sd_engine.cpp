@@ -1421,7 +1421,7 @@ class SdEngine {
             long long ldr = 0) {
     const bool gated = epi == 3 || epi == kGeglu;
     const int N = gated ? Nv / 2 : Nv;
-    const auto pl = planner_.plan(M, Nv, K, kEpiNames[epi]);
+    const auto pl = planner_.plan_mfma(M, Nv, K, kEpiNames[epi]);  // no library path here
     float* ws = pl.second > 1 ? gemm_ws((size_t)pl.second * M * Nv) : nullptr;
     const bool f32out = epi == kResid32 || epi == kStore32;
     k_check(cake_gemm(dt_, epi, pl.first, pl.second, x, lda, w, K, f32out ? nullptr : out,

@@ -272,10 +272,10 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, *
         return resid if f32_out else out
     c0, s0 = plan(M, Nv, K, epi)
     cfg = c0 if cfg is None else cfg
-    if cfg == LIB and bias is None and epi in LIB_EPIS:
+    if cfg == LIB and bias is None and epi in LIB_EPIS and (epi != "swiglu" or ldc == N):
         _lib_gemm(x2, lda, w, ldb, epi, out2, ldc, r2 if f32_out else None, ldr, M, N, K)
         return resid if f32_out else out
-    if cfg == LIB:  # an epilogue / bias the library form does not carry
+    if cfg == LIB:  # an epilogue / bias / strided output the library form does not carry
         cfg, s0 = plan_mfma(M, Nv, K, epi)
     splits = s0 if splits is None else max(1, int(splits))
     ws = _workspace(x.device, splits * M * Nv) if splits > 1 else None
@@ -304,8 +304,6 @@ def _lib_gemm(x2, lda, w, ldb, epi, out2, ldc, r2, ldr, M, N, K) -> None:
     elif epi in ("store32", "resid32"):
         run(1 if epi == "store32" else 2, r2.data_ptr(), ldr, N)
     else:  # swiglu: [M, 2N] library product, then silu(gate) * up
-        if ldc != N:
-            raise ValueError("library swiglu needs a contiguous output")
         gu = torch.empty(M, 2 * N, device=dev, dtype=x2.dtype)
         run(0, gu.data_ptr(), 2 * N, 2 * N)
         check(kernels().cake_silu_mul_rows(dt, gu.data_ptr(), M, N, out2.data_ptr(), st),
