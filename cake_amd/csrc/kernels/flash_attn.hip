@@ -346,7 +346,7 @@ __global__ __launch_bounds__(64 * NW, 2) void flash2_fwd_kernel(FlashArgs a) {
   int kend = a.M;
   if (a.causal) kend = min(kend, a.pos0 + mblk + 32 * NW);
   int j0 = 0;
-  if (a.ksplit > 1) {  // non-causal only (host): this split's key tiles
+  if (a.ksplit > 1) {  // this split's key tiles (causal rows past the split: empty partials)
     j0 = sk * a.kchunk / 64;
     kend = min(kend, (sk + 1) * a.kchunk);
   }
@@ -646,7 +646,8 @@ static int launch_flash(const FlashArgs& a, hipStream_t st) {
     // there).  At >= 256 workgroups the split measured neutral (SDXL's 320: 35.4 us either
     // way; profiles/r4_flash_key_split.jsonl), so it stays off.
     p.ksplit = 1;
-    if (!a.causal && a.D % 4 == 0 && a.po != nullptr) {
+    // causal: only a forced split (cake_flash_set_ksplit 2 / 4; measured A/B)
+    if ((!a.causal || flash_ksplit() > 1) && a.D % 4 == 0 && a.po != nullptr) {
       const long long wgs = (long long)nqt * a.H * a.B;
       int ks = 1;
       if (flash_ksplit() == 0) {
