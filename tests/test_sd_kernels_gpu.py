@@ -105,6 +105,40 @@ def test_flash_key_split(cuda, ksplit, B, H, N, M, D):
                                **_tol(dt))
 
 
+@pytest.mark.parametrize("ksplit", [2, 4])
+@pytest.mark.parametrize("pair_min", [1, 0])
+@pytest.mark.parametrize("N,pos0", [(700, 0), (300, 90)])
+def test_flash_causal_forced_key_split(cuda, ksplit, pair_min, N, pos0):
+    """The forced causal key split (measured slower, kept opt-in): splits wholly past a
+    row's position write empty partials the merge skips; paired and unpaired tiles."""
+    import ctypes
+
+    from cake_amd.ops import hip as K
+    torch.manual_seed(9)
+    dt, H, Hkv, D = torch.bfloat16, 8, 2, 128
+    M = N + pos0
+    q = torch.randn(1, N, H, D, device=cuda).to(dt).transpose(1, 2)
+    k = torch.randn(1, M, Hkv, D, device=cuda).to(dt).transpose(1, 2)
+    v = torch.randn(1, M, Hkv, D, device=cuda).to(dt).transpose(1, 2)
+    out = torch.full((1, N, H, D), float("nan"), device=cuda, dtype=dt).transpose(1, 2)
+    ws = torch.empty(4 * H * N * (D + 1), device=cuda)
+    st = [x for t in (q, k, v, out) for x in t.stride()[:3]]
+    arr = (ctypes.c_longlong * 12)(*st)
+    lib = K.kernels()
+    K.flash_set_pair_min(pair_min)
+    lib.cake_flash_set_ksplit(ksplit)
+    try:
+        K.check(lib.cake_flash_attn_ws(0, K._p(q), K._p(k), K._p(v), K._p(out), 1, H, Hkv, N, M,
+                                       D, ctypes.cast(arr, ctypes.c_void_p), 1 / math.sqrt(D), 1,
+                                       pos0, K._p(ws), ws.numel() * 4, K._stream()), "flash")
+        torch.cuda.synchronize()
+    finally:
+        K.flash_set_pair_min(512)
+        lib.cake_flash_set_ksplit(0)
+    torch.testing.assert_close(out.float(), _ref_attn(q, k, v, 1 / math.sqrt(D), True, pos0),
+                               **_tol(dt))
+
+
 @pytest.mark.parametrize("impl", [1, 2])
 def test_flash_attn_softmax_rescale_branch(cuda, impl):
     """A late key tile with a much larger score forces the online-softmax rescale."""
