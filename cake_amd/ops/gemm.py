@@ -272,7 +272,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, *
         return resid if f32_out else out
     c0, s0 = plan(M, Nv, K, epi)
     cfg = c0 if cfg is None else cfg
-    if cfg == LIB and bias is None and epi in LIB_EPIS and (epi != "swiglu" or ldc == N):
+    lib_ok = epi != "swiglu" or (ldc == N and N % 8 == 0 and out2.data_ptr() % 16 == 0)
+    if cfg == LIB and bias is None and epi in LIB_EPIS and lib_ok:
         _lib_gemm(x2, lda, w, ldb, epi, out2, ldc, r2 if f32_out else None, ldr, M, N, K)
         return resid if f32_out else out
     if cfg == LIB:  # an epilogue / bias / strided output the library form does not carry
@@ -288,7 +289,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, *
 
 
 def _lib_gemm(x2, lda, w, ldb, epi, out2, ldc, r2, ldr, M, N, K) -> None:
-    """The library GEMM (hipBLASLt) for a plan that names it."""
+    """The library GEMM (hipBLASLt) for a plan that names it.  Its workspace is one buffer
+    per device: calls on one stream are serialized (as the MFMA kernel's split-K slabs)."""
     dev = x2.device
     ws = _lib_ws.get(dev)
     if ws is None:
