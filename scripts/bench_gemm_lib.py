@@ -21,10 +21,15 @@ MODELS = {  # name -> (H, I, nq, nkv*hd)
 }
 
 
-def shapes(model):
+def shapes(model, tp=1):
+    """The prefill projections of one rank: all layers (tp 1: o / down accumulate into the
+    residual) or a tensor-parallel rank's slices (o / down write f32 partials, store32)."""
     H, I, nq, nk = MODELS[model]
-    return [("qkv", nq + 2 * nk, H, "store"), ("o", H, nq, "resid32"),
-            ("gate_up", 2 * I, H, "swiglu"), ("down", H, I, "resid32")]
+    if tp == 1:
+        return [("qkv", nq + 2 * nk, H, "store"), ("o", H, nq, "resid32"),
+                ("gate_up", 2 * I, H, "swiglu"), ("down", H, I, "resid32")]
+    return [(f"tp{tp}_qkv", (nq + 2 * nk) // tp, H, "store"), (f"tp{tp}_o", H, nq // tp, "store32"),
+            (f"tp{tp}_gate_up", 2 * I // tp, H, "swiglu"), (f"tp{tp}_down", H, I // tp, "store32")]
 
 
 def timeit(fn, reps=15):
@@ -44,17 +49,18 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--models", default="8b,70b")
     ap.add_argument("--ms", default="128,256,384,512,768,1024,1536,2048,3072,4096")
+    ap.add_argument("--tp", default="1", help="comma list of tensor-parallel degrees")
     ap.add_argument("--sweep-splits", action="store_true",
                     help="time the MFMA plan's tile at split-K 1/2/4/8 and keep the best")
     a = ap.parse_args()
     torch.manual_seed(0)
-    for model in a.models.split(","):
-        for name, Nv, K, epi in shapes(model):
+    for model, tp in [(m, int(t)) for m in a.models.split(",") for t in a.tp.split(",")]:
+        for name, Nv, K, epi in shapes(model, tp):
             w = (torch.randn(Nv, K, device="cuda") * K ** -0.5).bfloat16()
             N = Nv // 2 if epi == "swiglu" else Nv
             for M in [int(m) for m in a.ms.split(",")]:
                 x = (torch.randn(M, K, device="cuda") * 0.5).bfloat16()
-                r0 = torch.randn(M, N, device="cuda") if epi == "resid32" else None
+                r0 = torch.randn(M, N, device="cuda") if epi in ("resid32", "store32") else None
                 cfg, spl = G.plan_mfma(M, Nv, K, epi)
                 outs = {}
 
@@ -71,14 +77,16 @@ def main():
                     ref = torch.nn.functional.silu(y[:, :N]) * y[:, N:]
                 elif epi == "resid32":
                     ref = r0 + y
+                elif epi == "store32":
+                    ref = y
                 else:
                     ref = y
                 scale = ref.abs().max().item()
                 err = {k: (v - ref).abs().max().item() / scale for k, v in outs.items()}
                 # timed forms write in place (resid32 accumulates: harmless for timing)
                 rr = r0.clone() if r0 is not None else None
-                out = None if epi == "resid32" else torch.empty(M, N, device="cuda",
-                                                                dtype=torch.bfloat16)
+                out = None if epi in ("resid32", "store32") else torch.empty(
+                    M, N, device="cuda", dtype=torch.bfloat16)
 
                 def ours():
                     G.linear(x, w, epi=epi, resid=rr, out=out, cfg=cfg, splits=spl)
