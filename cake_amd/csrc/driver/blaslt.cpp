@@ -40,6 +40,16 @@ std::mutex g_mu;
 std::map<int, hipblasLtHandle_t> g_handles;  // device -> handle
 std::map<std::pair<int, Key>, Plan> g_plans;
 
+constexpr size_t kMaxPlans = 4096;
+
+void destroy(Plan& p) {
+  if (p.la) hipblasLtMatrixLayoutDestroy(p.la);
+  if (p.lb) hipblasLtMatrixLayoutDestroy(p.lb);
+  if (p.lc) hipblasLtMatrixLayoutDestroy(p.lc);
+  if (p.desc) hipblasLtMatmulDescDestroy(p.desc);
+  p = Plan{};
+}
+
 hipDataType in_type(int dt) { return dt == 1 ? HIP_R_16F : HIP_R_16BF; }
 
 int build(hipblasLtHandle_t h, const Key& k, Plan& p) {
@@ -86,29 +96,32 @@ CAKE_API int cake_blaslt_gemm(int dt, int out, const void* a, long long lda, con
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 1000 + HIPBLAS_STATUS_INTERNAL_ERROR;
   const Key key{dt, out, M, N, K, lda, ldw, ldc, ws_bytes};
-  hipblasLtHandle_t h;
-  Plan* p;
-  {
-    std::lock_guard<std::mutex> g(g_mu);
-    auto hit = g_handles.find(dev);
-    if (hit == g_handles.end()) {
-      hipblasLtHandle_t nh = nullptr;
-      const hipblasStatus_t s = hipblasLtCreate(&nh);
-      if (s) return 1000 + s;
-      hit = g_handles.emplace(dev, nh).first;
-    }
-    h = hit->second;
-    auto it = g_plans.find({dev, key});
-    if (it == g_plans.end()) {
-      it = g_plans.emplace(std::make_pair(dev, key), Plan{}).first;
-      it->second.status = build(h, key, it->second);
-    }
-    p = &it->second;
+  // one lock over lookup and launch (an asynchronous enqueue): the cache may be emptied
+  // by another thread's call once it holds kMaxPlans shapes (a server seeing every prompt
+  // length), so no plan pointer outlives the lock
+  std::lock_guard<std::mutex> g(g_mu);
+  auto hit = g_handles.find(dev);
+  if (hit == g_handles.end()) {
+    hipblasLtHandle_t nh = nullptr;
+    const hipblasStatus_t s = hipblasLtCreate(&nh);
+    if (s) return 1000 + s;
+    hit = g_handles.emplace(dev, nh).first;
   }
-  if (p->status) return 1000 + p->status;
+  hipblasLtHandle_t h = hit->second;
+  auto it = g_plans.find({dev, key});
+  if (it == g_plans.end()) {
+    if (g_plans.size() >= kMaxPlans) {
+      for (auto& kv : g_plans) destroy(kv.second);
+      g_plans.clear();
+    }
+    it = g_plans.emplace(std::make_pair(dev, key), Plan{}).first;
+    it->second.status = build(h, key, it->second);
+  }
+  const Plan& p = it->second;
+  if (p.status) return 1000 + p.status;
   const float alpha = 1.f, beta = out == 2 ? 1.f : 0.f;
-  const hipblasStatus_t s = hipblasLtMatmul(h, p->desc, &alpha, w, p->la, a, p->lb, &beta, c, p->lc,
-                                            c, p->lc, &p->algo, p->ws ? ws : nullptr, p->ws, st);
+  const hipblasStatus_t s = hipblasLtMatmul(h, p.desc, &alpha, w, p.la, a, p.lb, &beta, c, p.lc, c,
+                                            p.lc, &p.algo, p.ws ? ws : nullptr, p.ws, st);
   return s ? 1000 + s : 0;
 }
 
