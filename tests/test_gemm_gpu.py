@@ -239,3 +239,19 @@ def test_library_gemm_without_torch(cuda):
     r = subprocess.run([sys.executable, "-c", _NO_TORCH_LIB_GEMM, str(_lib.lib_path())],
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and r.stdout.startswith("ok"), r.stdout + r.stderr[-3000:]
+
+
+def test_library_gemm_plan_cache_eviction(cuda):
+    """More distinct shapes than the library plan cache holds (4096): the cache empties and
+    rebuilds, and results stay right before and after (a server sees every prompt length)."""
+    from cake_amd.ops import gemm as G
+    torch.manual_seed(3)
+    w = _r(64, 64, dt=torch.bfloat16, std=0.125)
+    xs = _r(4200, 64, dt=torch.bfloat16)
+    out = torch.empty(4200, 64, device="cuda", dtype=torch.bfloat16)
+    for M in range(1, 4200, 1):
+        G.linear(xs[:M], w, cfg=G.LIB, out=out[:M])
+    torch.cuda.synchronize()
+    _close(out[:4199], _ref(xs[:4199], w), 64)
+    y = G.linear(xs[:5], w, cfg=G.LIB)  # an evicted shape, rebuilt
+    _close(y, _ref(xs[:5], w), 64)
