@@ -478,3 +478,60 @@ def test_native_master_with_remote_sd_components(cuda, mini, tmp_path, monkeypat
     assert a.shape == b.shape == (cfg.height, cfg.width, 3)
     diff = np.abs(a - b)
     assert diff.mean() < 0.5 and diff.max() <= 2, (diff.mean(), diff.max())
+
+
+def test_native_sd_master_fails_loudly_when_the_unet_worker_dies(cuda, mini, tmp_path):
+    """Failure detection on the native SD engine's TCP client: a generation through a live
+    UNet worker succeeds; after the worker is killed the next one raises (connection error
+    or the remote timeout) instead of hanging or returning an image."""
+    import os
+    import socket
+    import subprocess
+    import time
+
+    from cake_amd.sd_engine import NativeSD
+    v, cfg, d = mini
+    if v != "v1-5":
+        pytest.skip("one version covers the client's failure path")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cli = os.path.join(root, "cake_amd", "lib", "cake-cli")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    topo = tmp_path / "topology.yml"
+    topo.write_text(f"w1:\n  host: '127.0.0.1:{port}'\n  layers:\n    - 'unet'\n")
+    w = subprocess.Popen([cli, "--mode", "worker", "--name", "w1", "--model", str(d),
+                          "--topology", str(topo), "--address", f"127.0.0.1:{port}",
+                          "--model-type", "image-model", "--sd-version", v, "--dtype", "f16"],
+                         cwd=root, env=dict(os.environ, CAKE_LOG="warning"),
+                         stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+    eng = None
+    try:
+        t0 = time.time()
+        while True:
+            if w.poll() is not None:
+                raise AssertionError(f"worker exited: {w.stderr.read()[-3000:]}")
+            try:
+                socket.create_connection(("127.0.0.1", port), timeout=0.5).close()
+                break
+            except OSError:
+                assert time.time() - t0 < 180, "worker did not listen"
+                time.sleep(0.3)
+        eng = NativeSD(str(d), dtype="f16", autotune=False, remote={"unet": f"127.0.0.1:{port}"},
+                       remote_timeout_s=10.0)
+        ids = _ids(1, cfg.clip.vocab_size).numpy()
+        out = eng.generate(ids, ids, n_steps=2, guidance=7.5, seed=1)
+        assert out.rgb.shape[-1] == 3 and len(out.step_s) == 2
+        w.kill()
+        w.wait(timeout=30)
+        t0 = time.time()
+        with pytest.raises(RuntimeError):
+            eng.generate(ids, ids, n_steps=2, guidance=7.5, seed=1)
+        assert time.time() - t0 < 60
+    finally:
+        if eng is not None:
+            eng.close()
+        if w.poll() is None:
+            w.kill()
+        w.communicate()
