@@ -94,3 +94,20 @@ def test_nearest_measured_plan_scales_split_k(monkeypatch):
     assert G.plan_mfma(1500, 4096, 14336, "resid32")[0] in G.CFG_TILES
     eng = (ROOT / "cake_amd/csrc/engine/engine_util.h").read_text()
     assert "near->splits * near->M / std::max(M, 1LL)" in eng
+
+
+def test_kernel_library_exports_the_library_gemm():
+    """libcake_kernels.so carries the hipBLASLt entry point the plans name (and resolves
+    its hipBLASLt dependency: the load itself needs no GPU)."""
+    import ctypes
+
+    import pytest
+
+    import torch  # noqa: F401  (the HIP runtime as the package loads it)
+    from cake_amd.ops import _lib
+    path = _lib.lib_path()
+    if not path.exists():
+        pytest.skip("kernel library not built")
+    lib = ctypes.CDLL(str(path))
+    assert hasattr(lib, "cake_blaslt_gemm") and hasattr(lib, "cake_gemm")
+    assert hasattr(lib, "cake_rmsnorm_set_reg")
