@@ -85,6 +85,12 @@ struct GemmPlanner {
     }
   }
 
+  bool has_lib() const {
+    for (const auto& e : tuned)
+      if (e.cfg == kGemmLib) return true;
+    return false;
+  }
+
   // the MFMA kernel's plan: the measured entries other than the library GEMM's
   std::pair<int, int> plan_mfma(long long M, long long Nv, long long K,
                                 const std::string& epi) const {

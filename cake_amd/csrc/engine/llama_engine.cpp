@@ -419,6 +419,7 @@ class Llama {
     planner_.load(pkg_dir() + "/ops/gemm_tuned.json");
     load_weights(dir);
     alloc_state();
+    warm_library();
     {
       size_t fr = 0, tot = 0;
       (void)hipMemGetInfo(&fr, &tot);
@@ -1218,6 +1219,20 @@ class Llama {
     }
     k_check(cake_gemm(dt_, epi, p.first, splits, a, lda, b, ldb, cptr, ldc, nullptr, resid, ldr,
                       ws, zeros_, M, N, K, st_), what);
+  }
+
+  // hipBLASLt's first call in a process costs ~175 ms (library init; a new shape after it
+  // ~0.3 ms: scripts/gpu_r5_ax.sh): paid here at open, not by the first request's TTFT
+  void warm_library() {
+    if (!planner_.has_lib()) return;
+    if (!lib_ws_) lib_ws_ = dalloc<uint8_t>(kLibWsBytes);
+    const size_t n = 64 * 64 + 2 * 8 * 64;  // W [64, 64], A [8, 64], C [8, 64]
+    uint16_t* t = dalloc<uint16_t>(n);
+    hip_check(hipMemsetAsync(t, 0, n * 2, st_), "memset");
+    k_check(cake_blaslt_gemm(dt_, 0, t + 4096, 64, t, 64, t + 4096 + 512, 64, 8, 64, 64, lib_ws_,
+                             kLibWsBytes, st_), "hipBLASLt warm-up");
+    hip_check(hipStreamSynchronize(st_), "sync");
+    dfree(t);
   }
 
   // store -> 16-bit C; store32 / resid32 -> f32 C with beta 0 / 1; swiglu -> the [M, 2N]
