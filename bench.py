@@ -238,7 +238,7 @@ def _summary(r: dict | None) -> dict | None:
     keep = _MAIN_KEYS + ("streams", "per_stream_tokens_per_sec", "hop", "hop_us",
                          "hops_per_token", "allreduce", "allreduce_us", "layers_per_rank",
                          "hbm_peak_mib_max_rank", "hbm_peak_mib", "ttft_ms_prefill", "engine",
-                         "walk", "hbm_used_mib_max_rank", "hbm_used_mib")
+                         "walk", "hbm_used_mib_max_rank", "hbm_used_mib", "native_fallback")
     return {k: r[k] for k in keep if k in r}
 
 

@@ -26,7 +26,10 @@ inline void hip_check(hipError_t e, const char* what) {
   if (e != hipSuccess) throw Error(std::string(what) + ": " + hipGetErrorString(e));
 }
 inline void k_check(int rc, const char* what) {
-  if (rc != 0) throw Error(std::string(what) + ": " + hipGetErrorString((hipError_t)rc));
+  if (rc == 0) return;
+  if (rc >= 1000)  // driver/blaslt.cpp: 1000 + hipblasStatus_t
+    throw Error(std::string(what) + ": hipBLASLt status " + std::to_string(rc - 1000));
+  throw Error(std::string(what) + ": " + hipGetErrorString((hipError_t)rc));
 }
 
 // <root>/cake_amd/lib/libcake_engine.so -> <root>/cake_amd
@@ -57,8 +60,14 @@ inline std::string read_file(const std::string& path) {
 // ---------------------------------------------------------------------------
 // GEMM tile plan (ops/gemm.py plan(): measured table, else the cost model)
 // ---------------------------------------------------------------------------
-// plan cfg naming the library GEMM (hipBLASLt, driver/blaslt.cpp; ops/gemm.py LIB)
+// plan cfg naming the library GEMM (hipBLASLt, driver/blaslt.cpp; ops/gemm.py LIB).
+// Off the default path: table entries naming it are read only under CAKE_GEMM_LIB=1
+// (the A/B arm of scripts/bench_gemm_lib.py); otherwise every shape runs an MFMA plan.
 constexpr int kGemmLib = -1;
+inline bool gemm_lib_enabled() {
+  const char* e = std::getenv("CAKE_GEMM_LIB");
+  return e && *e == '1';
+}
 
 struct GemmPlanner {
   struct Tuned { long long M, Nv, K; std::string epi; int cfg, splits; };
@@ -68,13 +77,14 @@ struct GemmPlanner {
     if (const char* e = std::getenv("CAKE_GEMM_TABLE"); e && *e) path = e;
     std::ifstream f(path);
     if (!f) return;
+    const bool lib_ok = gemm_lib_enabled();
     try {
       const Json j = Json::parse(read_file(path));
-      static const int known[] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 11, 12, 13, 14, 15, 16, 17, 18, 19};
+      static const int known[] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20};
       for (const auto& e : j.get("entries").items()) {
         const int cfg = (int)e.get("cfg").as_int();
         const std::string ep = e.get("epi").as_string();
-        const bool lib = cfg == kGemmLib && (ep == "store" || ep == "resid32" || ep == "store32" ||
+        const bool lib = lib_ok && cfg == kGemmLib && (ep == "store" || ep == "resid32" || ep == "store32" ||
                                              ep == "swiglu");
         if (!lib && std::find(std::begin(known), std::end(known), cfg) == std::end(known)) continue;
         tuned.push_back({e.get("M").as_int(), e.get("Nv").as_int(), e.get("K").as_int(),

@@ -465,6 +465,7 @@ class Llama {
     for (auto& kv : out_inbox_) (void)hipIpcCloseMemHandle(kv.second);
     for (auto& kv : peer_pbuf_) (void)hipIpcCloseMemHandle(kv.second);
     for (auto& kv : my_inbox_) (void)cake_hop_free(kv.second);
+    if (relay_) (void)cake_hop_free(relay_);
     for (void* p : allocs_) (void)hipFree(p);
     (void)hipStreamDestroy(st_);
   }
@@ -779,7 +780,12 @@ class Llama {
   std::vector<int> owner_;                  // layer -> pipeline rank
   std::map<int, void*> my_inbox_;           // edge -> own inbox (edges into this rank)
   std::map<int, void*> out_inbox_;          // edge -> IPC-mapped inbox of the receiver
-  std::map<int, void*> peer_pbuf_;          // rank -> IPC-mapped prefill buffer
+  std::map<int, void*> peer_pbuf_;          // rank -> IPC-mapped prefill relay buffer
+  // prefill rows a peer hands to this rank land here (uncached device memory, IPC-exported,
+  // written over xGMI by the sender's copy), then one local copy moves them into hidden_:
+  // hidden_ itself stays ordinary cached memory for the GEMM epilogues, and no L2 line of
+  // this device can hold a stale copy of what the peer wrote
+  float* relay_ = nullptr;
   unsigned int* seq_ = nullptr;
   int* hop_err_ = nullptr;
   std::vector<int> peers_;  // rank 0: control sockets of ranks 1..world-1
@@ -1134,7 +1140,7 @@ class Llama {
   void forward_host(uint64_t session, const std::vector<int>& layers, int pos0, float* h, int T) {
     hip_check(hipSetDevice(dev_), "hipSetDevice");
     const Cfg& c = lc_;
-    if (T < 1 || pos0 < 0 || pos0 + T > S_) throw Error("positions exceed the KV cache");
+    if (T < 1 || pos0 < 0 || (int64_t)pos0 + T > S_) throw Error("positions exceed the KV cache");
     std::vector<int> sel;
     for (int l : layers) {
       if (l < 0 || l >= c.L || local_[l] < 0)
@@ -1199,12 +1205,12 @@ class Llama {
     static const char* names[] = {"store", "resid32", "add16", "swiglu", "geglu", "partial",
                                   "store32"};
     auto p = planner_.plan(M, Nv, K, names[epi]);
-    if (p.first == kGemmLib) {  // the measured table names the library GEMM (hipBLASLt)
-      if (epi != kEpiSwiglu || ldc == N) {
-        lib_gemm(epi, a, lda, b, ldb, cptr, ldc, resid, ldr, M, N, K, what);
+    if (p.first == kGemmLib) {  // the table names the library GEMM (CAKE_GEMM_LIB=1 only)
+      if ((epi != kEpiSwiglu || ldc == N) &&
+          lib_gemm(epi, a, lda, b, ldb, cptr, ldc, resid, ldr, M, N, K, what))
         return;
-      }
-      p = planner_.plan_mfma(M, Nv, K, names[epi]);  // a strided SwiGLU output: the kernel
+      // a strided SwiGLU output or a library failure: the MFMA kernel's plan
+      p = planner_.plan_mfma(M, Nv, K, names[epi]);
     }
     const int splits = p.second;
     float* ws = nullptr;
@@ -1229,26 +1235,29 @@ class Llama {
     const size_t n = 64 * 64 + 2 * 8 * 64;  // W [64, 64], A [8, 64], C [8, 64]
     uint16_t* t = dalloc<uint16_t>(n);
     hip_check(hipMemsetAsync(t, 0, n * 2, st_), "memset");
-    k_check(cake_blaslt_gemm(dt_, 0, t + 4096, 64, t, 64, t + 4096 + 512, 64, 8, 64, 64, lib_ws_,
-                             kLibWsBytes, st_), "hipBLASLt warm-up");
+    const int rc = cake_blaslt_gemm(dt_, 0, t + 4096, 64, t, 64, t + 4096 + 512, 64, 8, 64, 64,
+                                    lib_ws_, kLibWsBytes, st_);
     hip_check(hipStreamSynchronize(st_), "sync");
     dfree(t);
+    if (rc)  // best effort: a library that cannot start leaves every shape on the MFMA kernel
+      std::fprintf(stderr, "cake engine: hipBLASLt warm-up failed (rc %d); MFMA GEMMs only\n", rc);
   }
 
   // store -> 16-bit C; store32 / resid32 -> f32 C with beta 0 / 1; swiglu -> the [M, 2N]
-  // product into pgu_, then silu(gate) * up into C
-  void lib_gemm(int epi, const void* a, long long lda, const void* b, long long ldb, void* cptr,
+  // product into pgu_, then silu(gate) * up into C.  false (nothing written) when the
+  // library refuses the shape: the caller runs the MFMA kernel instead
+  bool lib_gemm(int epi, const void* a, long long lda, const void* b, long long ldb, void* cptr,
                 long long ldc, float* resid, long long ldr, int M, int N, int K,
                 const char* what) {
     if (!lib_ws_) lib_ws_ = dalloc<uint8_t>(kLibWsBytes);
     auto run = [&](int mode, void* c, long long ld, int n) {
-      k_check(cake_blaslt_gemm(dt_, mode, a, lda, b, ldb, c, ld, M, n, K, lib_ws_, kLibWsBytes,
-                               st_), what);
+      return cake_blaslt_gemm(dt_, mode, a, lda, b, ldb, c, ld, M, n, K, lib_ws_, kLibWsBytes,
+                              st_) == 0;
     };
     if (epi == kEpiStore) {
-      run(0, cptr, ldc, N);
+      return run(0, cptr, ldc, N);
     } else if (epi == kEpiStore32 || epi == kEpiResid32) {
-      run(epi == kEpiStore32 ? 1 : 2, resid, ldr, N);
+      return run(epi == kEpiStore32 ? 1 : 2, resid, ldr, N);
     } else if (epi == kEpiSwiglu && ldc == N) {
       const size_t need = (size_t)M * 2 * N;
       if (need > pgu_n_) {
@@ -1256,8 +1265,9 @@ class Llama {
         pgu_ = dalloc<uint16_t>(need);
         pgu_n_ = need;
       }
-      run(0, pgu_, 2LL * N, 2 * N);
+      if (!run(0, pgu_, 2LL * N, 2 * N)) return false;
       k_check(cake_silu_mul_rows(dt_, pgu_, M, N, cptr, st_), what);
+      return true;
     } else {
       throw Error(std::string(what) + ": no library form of this epilogue");
     }
@@ -1287,6 +1297,7 @@ class Llama {
         continue;
       }
       if (s.rank == 0) {
+        if (i > 0 && edge_in_[i] >= 0) take_relay(T);  // rows handed back by a worker rank
         if (s.kind == kRunStop) prefill_layers(T, 0, &s.sel);
         if (edge_in_[i + 1] >= 0) forward_hidden(T, walk_[i + 1].rank);
         continue;
@@ -1301,6 +1312,7 @@ class Llama {
         throw Error("pipeline rank " + std::to_string(s.rank) + " prefill failed: " +
                     (ack.has("error") ? ack.get("error").as_string() : std::string("?")));
     }
+    if (edge_in_.back() >= 0) take_relay(T);  // the last worker's rows, for the head
   }
 
   int32_t* ptok_buf(int T) {
@@ -1308,7 +1320,15 @@ class Llama {
     return ptok_;
   }
 
-  // hidden_ rows [0, T) -> rank dst's prefill buffer (device to device over the IPC
+  // rows [0, T) a peer wrote into this rank's relay buffer -> hidden_ (the copy reads the
+  // uncached relay from memory)
+  void take_relay(int T) {
+    if (!relay_) throw Error("no prefill relay buffer on this rank");
+    hip_check(hipMemcpyAsync(hidden_, relay_, sizeof(float) * (size_t)T * cfg_.H,
+                             hipMemcpyDeviceToDevice, st_), "prefill relay");
+  }
+
+  // hidden_ rows [0, T) -> rank dst's prefill relay buffer (device to device over the IPC
   // mapping), complete before the control message that announces them
   void forward_hidden(int T, int dst) {
     auto it = peer_pbuf_.find(dst);
@@ -1816,6 +1836,7 @@ class Llama {
           if (T < 1 || T > S_) throw Error("bad prefill length");
           if (i < 1 || i + 1 >= (int)walk_.size() || walk_[i].rank != rank_)
             throw Error("prefill stop " + std::to_string(i) + " is not this rank's");
+          if (edge_in_[i] >= 0) take_relay(T);
           prefill_layers(T, 0, &walk_[i].sel);
           if (edge_in_[i + 1] >= 0) forward_hidden(T, walk_[i + 1].rank);
           r.set("ok", Json::boolean(true));
@@ -1877,8 +1898,11 @@ class Llama {
     Json me = Json::object();
     me.set("rank", Json::integer(rank_));
     {
+      void* rp = nullptr;
+      k_check(cake_hop_alloc(sizeof(float) * (size_t)S_ * cfg_.H, &rp), "relay alloc");
+      relay_ = static_cast<float*>(rp);
       hipIpcMemHandle_t hp;
-      hip_check(hipIpcGetMemHandle(&hp, hidden_), "IpcGetMemHandle");
+      hip_check(hipIpcGetMemHandle(&hp, relay_), "IpcGetMemHandle");
       me.set("pbuf", Json::string(hex_of(&hp, sizeof(hp))));
       Json ib = Json::array();
       for (size_t e = 0; e < edges_.size(); ++e) {
@@ -1973,6 +1997,61 @@ class Llama {
   // timeout in the middle of the first generation.
   static float selftest_value(int e, int i) { return (float)(((i * 7 + e * 13) % 251) - 125); }
 
+  static bool selftest_forced_fail() {  // test hook: the fallback path of bench / cake-cli
+    const char* e = std::getenv("CAKE_IPC_SELFTEST_FAIL");
+    return e && *e == '1';
+  }
+
+  // every rank reaches this point, then every rank leaves it (rank 0 is the hub)
+  void ctl_barrier() {
+    if (rank_ == 0) {
+      for (int fd : peers_) (void)recv_json(fd);
+      for (int fd : peers_) send_json(fd, Json::object());
+    } else {
+      send_json(ctl_fd_, Json::object());
+      (void)recv_json(ctl_fd_);
+    }
+  }
+
+  // Each outgoing edge writes a pattern row into the receiver's relay buffer the way
+  // forward_hidden does (device copy over the IPC mapping, synchronized before the
+  // control message); after a barrier the receiver moves it out with take_relay's copy
+  // and checks every word.  Round 2 writes a new pattern over rows the receiver has
+  // already read, so a receiver that kept the old contents in a cache fails here.
+  void selftest_relay(std::string& bad) {
+    const int H = cfg_.H;
+    std::vector<float> pat(H), got(H);
+    for (int round = 1; round <= 2; ++round) {
+      for (size_t e = 0; e < edges_.size(); ++e) {
+        if (edges_[e].first != rank_ || (int)e >= S_) continue;
+        for (int i = 0; i < H; ++i) pat[i] = selftest_value((int)e + 64 * round, i);
+        hip_check(hipMemcpyAsync(hidden_, pat.data(), sizeof(float) * H, hipMemcpyHostToDevice,
+                                 st_), "selftest H2D");
+        float* dst = static_cast<float*>(peer_pbuf_.at(edges_[e].second)) + e * (size_t)H;
+        hip_check(hipMemcpyAsync(dst, hidden_, sizeof(float) * H, hipMemcpyDeviceToDevice, st_),
+                  "selftest relay");
+        hip_check(hipStreamSynchronize(st_), "selftest sync");
+      }
+      ctl_barrier();
+      for (size_t e = 0; e < edges_.size(); ++e) {
+        if (edges_[e].second != rank_ || (int)e >= S_) continue;
+        hip_check(hipMemcpyAsync(hidden_ + H, relay_ + e * (size_t)H, sizeof(float) * H,
+                                 hipMemcpyDeviceToDevice, st_), "selftest relay read");
+        hip_check(hipMemcpyAsync(got.data(), hidden_ + H, sizeof(float) * H,
+                                 hipMemcpyDeviceToHost, st_), "selftest D2H");
+        hip_check(hipStreamSynchronize(st_), "selftest sync");
+        int wrong = 0;
+        for (int i = 0; i < H; ++i)
+          if (got[i] != selftest_value((int)e + 64 * round, i)) ++wrong;
+        if (wrong && bad.empty())
+          bad = "rank " + std::to_string(rank_) + ": prefill relay from rank " +
+                std::to_string(edges_[e].first) + " (edge " + std::to_string(e) + ", round " +
+                std::to_string(round) + ") delivered " + std::to_string(wrong) + " wrong words";
+      }
+      ctl_barrier();
+    }
+  }
+
   void selftest_pipeline() {
     const int H = cfg_.H;
     std::string bad;
@@ -2018,6 +2097,11 @@ class Llama {
         break;
       }
     }
+    // the prefill relay buffers: every rank takes part whatever the hops found (the
+    // rounds are lock-stepped through rank 0)
+    selftest_relay(bad);
+    if (bad.empty() && selftest_forced_fail())
+      bad = "rank " + std::to_string(rank_) + ": failure forced by CAKE_IPC_SELFTEST_FAIL=1";
     // verdicts to rank 0 (which fails the start naming every bad edge)
     if (rank_ == 0) {
       for (size_t i = 0; i < peers_.size(); ++i) {
@@ -2260,10 +2344,33 @@ class Llama {
     hip_check(hipStreamSynchronize(st_), "sync");
     for (int i = 0; i < H; ++i)
       if (got[i] != tri * (float)((i % 17) - 8)) { fail("prefill slab all-reduce delivered wrong words"); break; }
+    // (5) two more rounds with new values (the banks alternate, so the second one
+    // rewrites the bank of (4)): every rank has already read that bank's contents, so a
+    // stale cached copy of a peer's slot fails here
+    for (int round = 1; round <= 2; ++round) {  // collective: every rank runs both
+      const float sc = -2.f - (float)round;
+      for (int i = 0; i < H; ++i) pat[i] = sc * (float)(tp_rank_ + 1) * (float)((i % 13) - 6);
+      hip_check(hipMemcpyAsync(ppart_, pat.data(), sizeof(float) * H, hipMemcpyHostToDevice,
+                               st_), "H2D");
+      hip_check(hipMemsetAsync(hidden_, 0, sizeof(float) * H, st_), "memset");
+      dense_allreduce(1);
+      hip_check(hipMemcpyAsync(got.data(), hidden_, sizeof(float) * H, hipMemcpyDeviceToHost,
+                               st_), "D2H");
+      hip_check(hipStreamSynchronize(st_), "sync");
+      for (int i = 0; i < H; ++i)
+        if (got[i] != sc * tri * (float)((i % 13) - 6)) {
+          fail("prefill slab all-reduce (round " + std::to_string(round + 1) +
+               ") delivered wrong words");
+          break;
+        }
+    }
+    hip_check(hipMemcpyAsync(errs, ar_err_, sizeof(errs), hipMemcpyDeviceToHost, st_), "D2H");
+    hip_check(hipStreamSynchronize(st_), "sync");
     if (errs[0] | errs[1] | errs[2]) {
       fail("an all-reduce channel timed out");
       hip_check(hipMemset(ar_err_, 0, sizeof(errs)), "memset");
     }
+    if (selftest_forced_fail()) fail("failure forced by CAKE_IPC_SELFTEST_FAIL=1");
     if (tp_rank_ == 0) {
       for (int fd : peers_) {
         const Json r = recv_json(fd);

@@ -51,6 +51,7 @@ CAKE_GEMM_EXTERN_ALL(kF16)
 
 using namespace cake;
 static inline void cfg_dims(int cfg, int& bm, int& bn) {
+  if (cfg == kPPCfg) { bm = bn = 256; return; }
 #define X(id, BM, BN, WM, WN, NS, PR) if (cfg == id) { bm = BM; bn = BN; return; }
   CAKE_GEMM_CFGS(X)
 #undef X

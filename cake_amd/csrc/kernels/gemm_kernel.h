@@ -652,6 +652,12 @@ __global__ __launch_bounds__(256) void gemm_splitk_finalize(GemmArgs g, int spli
   X(18, 64, 160, 2, 2, 3, 6) \
   X(19, 128, 160, 2, 2, 3, 6)
 
+}  // namespace cake
+
+#include "gemm_pp.h"
+
+namespace cake {
+
 template <int EPI>
 constexpr bool gated_ok(int wave_cols) {
   return wave_cols % 32 == 0 || !(EPI == kEpiSwiglu || EPI == kEpiGeglu);
@@ -659,6 +665,10 @@ constexpr bool gated_ok(int wave_cols) {
 
 template <int DT, int EPI>
 int launch_gemm(int cfg, dim3 grid, hipStream_t st, const GemmArgs& g) {
+  if (cfg == kPPCfg) {
+    hipLaunchKernelGGL((gemm_pp_kernel<DT, EPI>), grid, dim3(512), 0, st, g);
+    return (int)hipGetLastError();
+  }
 
 #define X(id, BM, BN, WM, WN, NS, PR)                                                        \
   if (cfg == id) {                                                                           \

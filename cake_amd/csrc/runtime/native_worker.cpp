@@ -84,10 +84,12 @@ int run_native_worker(const NativeWorkerOpts& o, const TopoNode& node) {
   using Forward = int32_t (*)(void*, uint64_t, const int32_t*, int32_t, int32_t, float*, int32_t,
                               char*, int32_t);
   using Drop = void (*)(void*, uint64_t);
+  using InfoFn = int32_t (*)(void*, int32_t*);
   auto open_layers = reinterpret_cast<OpenLayers>(dlsym(h, "cake_engine_open_layers"));
   auto forward = reinterpret_cast<Forward>(dlsym(h, "cake_engine_forward"));
   auto drop = reinterpret_cast<Drop>(dlsym(h, "cake_engine_drop_session"));
-  if (!open_layers || !forward || !drop) {
+  auto einfo = reinterpret_cast<InfoFn>(dlsym(h, "cake_engine_info"));
+  if (!open_layers || !forward || !drop || !einfo) {
     std::fprintf(stderr, "%s: engine symbols missing in %s\n", tag.c_str(), lib.c_str());
     return 1;
   }
@@ -113,6 +115,9 @@ int run_native_worker(const NativeWorkerOpts& o, const TopoNode& node) {
     std::fprintf(stderr, "%s: native worker: %s\n", tag.c_str(), err);
     return 1;
   }
+  int32_t einf[8] = {0};
+  einfo(eng, einf);
+  const uint64_t hidden = (uint64_t)einf[1];  // the model width every Batch row must have
   WorkerInfo info;
   info.version = "0.1.0";
   info.dtype = bf16 ? "bf16" : "f16";
@@ -135,9 +140,21 @@ int run_native_worker(const NativeWorkerOpts& o, const TopoNode& node) {
                          const RawTensor& x) {
     OpResult r;
     try {
+      // the engine reads and writes T rows of exactly `hidden` floats: a client tensor of
+      // another width (or a byte count that disagrees with its shape) is refused here,
+      // before any host buffer is sized from it
       const uint64_t H = x.shape.empty() ? 0 : x.shape.back();
+      if (H != hidden)
+        throw std::runtime_error("hidden width " + std::to_string(H) + " != the model's " +
+                                 std::to_string(hidden));
       uint64_t n = 1;
-      for (auto d : x.shape) n *= d;
+      for (auto d : x.shape) {
+        if (d != 0 && n > (uint64_t)INT32_MAX * hidden / d)
+          throw std::runtime_error("tensor too large");
+        n *= d;
+      }
+      if (n == 0 || n % H != 0 || n / H > (uint64_t)INT32_MAX)
+        throw std::runtime_error("tensor is not whole rows of the model width");
       std::vector<float> buf(n);
       if (x.dtype == "f32" && x.nbytes == n * 4) {
         std::memcpy(buf.data(), x.data, n * 4);
@@ -152,6 +169,7 @@ int run_native_worker(const NativeWorkerOpts& o, const TopoNode& node) {
       size_t i = 0;
       while (i < ops.size()) {  // consecutive ops at one position -> one engine call
         const uint64_t pos = ops[i].index_pos;
+        if (pos > (uint64_t)INT32_MAX) throw std::runtime_error("index_pos out of range");
         std::vector<int32_t> ls;
         for (; i < ops.size() && ops[i].index_pos == pos; ++i) {
           const std::string& nm = ops[i].layer_name;
@@ -225,27 +243,44 @@ struct Packed {  // util.rs pack: [n, ndim, dims..., data..., ndim, ...]
   std::vector<const float*> data;
 };
 
+// a pack header value: a finite, non-negative integer below 2^31 (anything else is a
+// malformed request, and casting it would be undefined behaviour)
+size_t pack_dim(float v) {
+  if (!(v >= 0.f) || v > 2147483647.f || v != std::floor(v))
+    throw std::runtime_error("malformed packed tensor header");
+  return (size_t)v;
+}
+
 Packed unpack(const std::vector<float>& f) {
   Packed out;
   if (f.empty()) throw std::runtime_error("empty packed tensor");
-  const size_t n = (size_t)f[0];
+  const size_t n = pack_dim(f[0]);
   size_t i = 1;
   for (size_t k = 0; k < n; ++k) {
     if (i >= f.size()) throw std::runtime_error("truncated packed tensor");
-    const size_t nd = (size_t)f[i++];
+    const size_t nd = pack_dim(f[i++]);
     std::vector<uint64_t> shp;
     uint64_t numel = 1;
     for (size_t d = 0; d < nd; ++d) {
       if (i >= f.size()) throw std::runtime_error("truncated packed tensor");
-      shp.push_back((uint64_t)f[i++]);
+      shp.push_back(pack_dim(f[i++]));
+      if (shp.back() != 0 && numel > f.size() / shp.back())
+        throw std::runtime_error("truncated packed tensor");
       numel *= shp.back();
     }
-    if (i + numel > f.size()) throw std::runtime_error("truncated packed tensor");
+    if (numel > f.size() - i) throw std::runtime_error("truncated packed tensor");
     out.shapes.push_back(shp);
     out.data.push_back(f.data() + i);
     i += numel;
   }
   return out;
+}
+
+// number of elements of one unpacked item
+uint64_t numel_of(const std::vector<uint64_t>& s) {
+  uint64_t n = 1;
+  for (auto d : s) n *= d;
+  return n;
 }
 
 const char* kSdParts[4] = {"unet", "vae", "clip", "clip2"};
@@ -349,7 +384,7 @@ int run_native_sd_worker(const NativeWorkerOpts& o, const TopoNode& node) {
         r.shape = {(uint64_t)B, 77, (uint64_t)D};
       } else if (name == "unet") {
         const Packed pk = unpack(f);
-        if (pk.shapes.size() != 3 || pk.shapes[0].size() != 4)
+        if (pk.shapes.size() != 3 || pk.shapes[0].size() != 4 || numel_of(pk.shapes[2]) < 1)
           throw std::runtime_error("unet expects pack([latents, text_embeddings, timestep])");
         const auto& ls = pk.shapes[0];
         const int B = (int)ls[0];
@@ -366,7 +401,8 @@ int run_native_sd_worker(const NativeWorkerOpts& o, const TopoNode& node) {
         r.shape = ls;
       } else if (name == "vae") {
         const Packed pk = unpack(f);
-        if (pk.shapes.size() != 2) throw std::runtime_error("vae expects pack([direction, x])");
+        if (pk.shapes.size() != 2 || numel_of(pk.shapes[0]) < 1)
+          throw std::runtime_error("vae expects pack([direction, x])");
         if (pk.data[0][0] == 1.0f) {  // encode: the posterior sample of the image
           const auto& is = pk.shapes[1];
           if (is.size() != 4 || is[0] != 1 || is[1] != 3 || (int)is[2] != H || (int)is[3] != W)
@@ -387,7 +423,7 @@ int run_native_sd_worker(const NativeWorkerOpts& o, const TopoNode& node) {
           return r;
         }
         const auto& zs = pk.shapes[1];
-        if (zs.size() != 4 || zs[0] != 1 || (int)zs[2] != H / 8 || (int)zs[3] != W / 8)
+        if (zs.size() != 4 || zs[0] != 1 || zs[1] != 4 || (int)zs[2] != H / 8 || (int)zs[3] != W / 8)
           throw std::runtime_error("vae decode expects [1, 4, h, w] at the engine's resolution");
         out.resize((size_t)3 * H * W);
         if (vae(eng, pk.data[1], out.data(), e2, sizeof(e2))) throw std::runtime_error(e2);

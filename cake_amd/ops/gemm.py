@@ -25,9 +25,9 @@ _DT = {torch.bfloat16: 0, torch.float16: 1}
 CFG_TILES = {0: (128, 128), 1: (64, 128), 2: (256, 128), 3: (128, 256), 4: (64, 64),
              5: (256, 256), 6: (256, 128), 7: (128, 128), 8: (128, 128), 11: (256, 256),
              12: (64, 128), 13: (64, 64), 14: (64, 160), 15: (64, 160), 16: (128, 160),
-             17: (128, 160), 18: (64, 160), 19: (128, 160)}
+             17: (128, 160), 18: (64, 160), 19: (128, 160), 20: (256, 256)}
 _SLOTS = {0: 2, 1: 2, 2: 1, 3: 1, 4: 4, 5: 1, 6: 1, 7: 1, 8: 2, 11: 1, 12: 2, 13: 2,
-          14: 2, 15: 2, 16: 1, 17: 1, 18: 1, 19: 1}  # WGs/CU
+          14: 2, 15: 2, 16: 1, 17: 1, 18: 1, 19: 1, 20: 1}  # WGs/CU
 # 80-column wave tiles (two waves across the 160 columns): no gated epilogue
 NO_GATED = {14, 17, 18, 19}
 # relative per-tile throughput (measured per-config sweep,
@@ -35,12 +35,12 @@ NO_GATED = {14, 17, 18, 19}
 # shapes, the 8-wave 256x256 tile (11) where its tiles fill the chip, 64-wide tiles
 # (1, 4) for short M
 _EFF = {0: 1.0, 1: 0.8, 2: 0.8, 3: 0.8, 4: 0.7, 5: 1.2, 6: 0.95, 7: 0.9, 8: 0.9, 11: 1.1,
-        12: 0.8, 13: 0.7, 14: 0.8, 15: 0.7, 16: 0.9, 17: 0.9, 18: 0.8, 19: 0.9}
+        12: 0.8, 13: 0.7, 14: 0.8, 15: 0.7, 16: 0.9, 17: 0.9, 18: 0.8, 19: 0.9, 20: 1.3}
 NUM_CUS = 256
-# plan cfg of the library GEMM (hipBLASLt, csrc/driver/blaslt.cpp): the measured table
-# names it for the plain prefill projections where it was faster on this chip
-# (profiles/r5_gemm_vs_hipblaslt.jsonl); epilogues it can carry: plain store, f32
-# store / accumulate (beta 1), and SwiGLU as library GEMM + silu_mul_rows
+# plan cfg of the library GEMM (hipBLASLt, csrc/driver/blaslt.cpp), kept as the A/B arm of
+# scripts/bench_gemm_lib.py: off the default path (table entries naming it are read only
+# under CAKE_GEMM_LIB=1, or when a caller passes cfg=LIB); epilogues it can carry: plain
+# store, f32 store / accumulate (beta 1), and SwiGLU as library GEMM + silu_mul_rows
 LIB = -1
 LIB_EPIS = ("store", "resid32", "store32", "swiglu")
 _LIB_WS_BYTES = 32 << 20
@@ -91,10 +91,12 @@ def _load_tuned() -> list:
     import os
     p = os.environ.get("CAKE_GEMM_TABLE") or os.path.join(
         os.path.dirname(os.path.abspath(__file__)), "gemm_tuned.json")
+    lib_ok = os.environ.get("CAKE_GEMM_LIB") == "1"
     try:
         with open(p) as f:
             return [e for e in json.load(f)["entries"]
-                    if e["cfg"] in CFG_TILES or (e["cfg"] == LIB and e["epi"] in LIB_EPIS)]
+                    if e["cfg"] in CFG_TILES
+                    or (lib_ok and e["cfg"] == LIB and e["epi"] in LIB_EPIS)]
     except (OSError, ValueError, KeyError):
         return []
 
@@ -290,12 +292,12 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, *
 
 def _lib_gemm(x2, lda, w, ldb, epi, out2, ldc, r2, ldr, M, N, K) -> None:
     """The library GEMM (hipBLASLt) for a plan that names it.  Its workspace is one buffer
-    per device: calls on one stream are serialized (as the MFMA kernel's split-K slabs)."""
+    per (device, stream), so library GEMMs on two streams never share one."""
     dev = x2.device
-    ws = _lib_ws.get(dev)
-    if ws is None:
-        ws = _lib_ws[dev] = torch.empty(_LIB_WS_BYTES, dtype=torch.uint8, device=dev)
     st = torch.cuda.current_stream().cuda_stream
+    ws = _lib_ws.get((dev, st))
+    if ws is None:
+        ws = _lib_ws[(dev, st)] = torch.empty(_LIB_WS_BYTES, dtype=torch.uint8, device=dev)
     dt = _DT[x2.dtype]
 
     def run(mode, cptr, ld, n):
@@ -305,11 +307,15 @@ def _lib_gemm(x2, lda, w, ldb, epi, out2, ldc, r2, ldr, M, N, K) -> None:
         run(0, out2.data_ptr(), ldc, N)
     elif epi in ("store32", "resid32"):
         run(1 if epi == "store32" else 2, r2.data_ptr(), ldr, N)
-    else:  # swiglu: [M, 2N] library product, then silu(gate) * up
-        gu = torch.empty(M, 2 * N, device=dev, dtype=x2.dtype)
+    else:  # swiglu: [M, 2N] library product (cached scratch), then silu(gate) * up
+        gu = _lib_gu.get((dev, st, x2.dtype))
+        if gu is None or gu.numel() < M * 2 * N:
+            gu = _lib_gu[(dev, st, x2.dtype)] = torch.empty(M * 2 * N, device=dev,
+                                                            dtype=x2.dtype)
         run(0, gu.data_ptr(), 2 * N, 2 * N)
         check(kernels().cake_silu_mul_rows(dt, gu.data_ptr(), M, N, out2.data_ptr(), st),
               "silu_mul_rows")
 
 
 _lib_ws: dict = {}
+_lib_gu: dict = {}

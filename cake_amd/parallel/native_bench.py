@@ -124,11 +124,22 @@ def measure_native_multi(a, env, model: str, steps: int, warmup: int, mode: str 
     t0 = time.time()
     out = None
     eng = None
+    err = None
     try:
         eng = NativeLlama(d, max_seq=_max_seq(a, steps, warmup), dtype=a.dtype,
                           device=env.dev.index or 0, steps_per_graph=1, rank=rank, world=world,
                           master_addr=addr, hop_bf16=a.hop_dtype == "bf16", hop_timeout_s=60.0,
                           connect_timeout_s=300.0, tp=mode == "tp", random_init=True, seed=1)
+    except RuntimeError as e:  # the start-up self-test (or the group's start) failed
+        err = str(e)
+    # every rank agrees: one failed start sends the whole group to the RCCL transport
+    if env.max_over_ranks(1.0 if err is not None else 0.0) > 0:
+        if eng is not None:
+            eng.close()
+        shutil.rmtree(d, ignore_errors=True)
+        env.release()
+        return _dist_fallback(a, env, model, steps, warmup, mode, dump_tokens, err)
+    try:
         hbm = _hbm_used_mib()
         if rank == 0:
             print(f"[bench] native {model} {mode}{world}: ranks joined in {time.time() - t0:.1f}s"
@@ -162,6 +173,30 @@ def measure_native_multi(a, env, model: str, steps: int, warmup: int, mode: str 
             out.update({"allreduce": "ipc", "allreduces_per_token": 2 * cfg.num_hidden_layers + 1})
     env.release()
     return out
+
+
+def _dist_fallback(a, env, model, steps, warmup, mode, dump_tokens, err):
+    """The record on the Python engines over torch.distributed (RCCL p2p hops / all-reduces)
+    after the native group could not start on its device IPC transport; the JSON names
+    the transport it ran on and the native start's error."""
+    import copy
+    from .pipeline_bench import measure_pipeline
+    from .tp_bench import measure_tp
+    if env.rank == 0:
+        print(f"[bench] native {model} {mode}{env.world} did not start ({err}); "
+              "falling back to the torch.distributed transport", file=sys.stderr, flush=True)
+    a2 = copy.copy(a)
+    a2.hop, a2.allreduce, a2.streams = "dist", "dist", 1
+    fn = measure_tp if mode == "tp" else measure_pipeline
+    r = fn(a2, env, model, steps, warmup, dump_tokens)
+    if env.rank == 0 and r is not None:
+        r = dict(r)
+        r.update({"engine": "python", "native_fallback": (err or "a peer rank failed")[:300]})
+        if mode == "pp":
+            r["hop"] = "dist"
+        else:
+            r["allreduce"] = "dist"
+    return r
 
 
 def _hops(walk: str | None) -> int:

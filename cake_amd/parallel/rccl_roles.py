@@ -319,7 +319,8 @@ def run_tp(ctx) -> None:
         cfg = LlamaConfig.from_path(ctx.model_path)
         check_tp(cfg, world)
         blocks, head = load_shards(ctx.model_path, cfg, rank, world, ctx.device, ctx.dtype)
-        comm = AllReduce(rank, world, ctx.device, cfg.hidden_size, n_gather=cfg.vocab_size)
+        comm = AllReduce(rank, world, ctx.device, cfg.hidden_size, n_gather=cfg.vocab_size,
+                         mode=getattr(ctx.args, "allreduce", "ipc"))
         s = ctx.sampling
         eng = TPEngine(cfg, blocks, head, rank, world, ctx.device, ctx.dtype, ctx.max_seq_len,
                        comm, repeat_penalty=s.repeat_penalty, repeat_last_n=s.repeat_last_n,
@@ -371,9 +372,10 @@ def _native_group(ctx) -> bool:
     return native_eligible(ctx) and (tp or getattr(a, "hop", "ipc") == "ipc")
 
 
-def run_native_rccl(ctx) -> None:
+def run_native_rccl(ctx) -> bool:
     """Every rank runs the native engine; rank 0 is the master (CLI generation or the
-    REST API over :class:`NativeLLM`), the others serve it until it closes."""
+    REST API over :class:`NativeLLM`), the others serve it until it closes.  False (and
+    nothing served) when the engine's start-up self-test refused the device transport."""
     from ..models.llama3.native_generator import NativeLLM
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -381,7 +383,16 @@ def run_native_rccl(ctx) -> None:
     if ctx.device.type == "cuda":
         local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
-    eng = _native_rank_engine(ctx, rank, world, tp)
+    try:
+        eng = _native_rank_engine(ctx, rank, world, tp)
+    except RuntimeError as e:
+        if "self-test failed" not in str(e):
+            raise
+        # the group's device IPC transport failed its start-up self-test (the verdict
+        # reaches every rank): all ranks run the Python engines over RCCL instead
+        log.warning("rank %d/%d: native engine refused the device transport (%s); "
+                    "serving over torch.distributed (RCCL) instead", rank, world, e)
+        return False
     log.info("rank %d/%d: native engine, %s", rank, world,
              "tensor parallel" if tp else f"walk {eng.walk()} (hops: ipc)")
     try:
@@ -392,6 +403,7 @@ def run_native_rccl(ctx) -> None:
             eng.serve()
     finally:
         eng.close()
+    return True
 
 
 def run_rccl(ctx) -> None:
@@ -400,8 +412,10 @@ def run_rccl(ctx) -> None:
         run_sd_rccl(ctx)
         return
     if _native_group(ctx):
-        run_native_rccl(ctx)
-        return
+        if run_native_rccl(ctx):
+            return
+        ctx.args.hop = "dist"  # the fallback transport: RCCL p2p / all-reduce
+        ctx.args.allreduce = "dist"
     if getattr(ctx.args, "parallel", "pp") == "tp":
         run_tp(ctx)
         return

@@ -25,7 +25,7 @@ def _close(got, ref, K):
 
 
 @pytest.mark.parametrize("dt", DTYPES)
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7, 8, 11, 12, 13, 14, 15, 16, 17, 18, 19])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7, 8, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20])
 @pytest.mark.parametrize("M,N,K,splits", [(128, 256, 256, 1), (77, 200, 320, 1),
                                           (300, 520, 1024, 3), (1, 64, 64, 1),
                                           (513, 136, 648, 2)])
@@ -135,8 +135,8 @@ def test_gemm_model_shapes(cuda, name, M, N, K, epi):
 
 
 @pytest.mark.parametrize("dt", DTYPES)
-@pytest.mark.parametrize("cfg", [5, 0, 13, 14, 15, 16, 17])
-@pytest.mark.parametrize("M,N,K", [(300, 700, 640), (257, 272, 2112)])
+@pytest.mark.parametrize("cfg", [5, 0, 13, 14, 15, 16, 17, 20])
+@pytest.mark.parametrize("M,N,K", [(300, 700, 640), (257, 272, 2112), (520, 776, 200)])
 def test_gemm_interleaved_all_epilogues(cuda, dt, cfg, M, N, K):
     """Interleaved-schedule tiles with ragged M/N and every epilogue."""
     from cake_amd.ops import gemm as G
@@ -255,3 +255,25 @@ def test_library_gemm_plan_cache_eviction(cuda):
     _close(out[:4199], _ref(xs[:4199], w), 64)
     y = G.linear(xs[:5], w, cfg=G.LIB)  # an evicted shape, rebuilt
     _close(y, _ref(xs[:5], w), 64)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("M,N,K,splits", [(2048, 6144, 4096, 1), (1000, 4096, 14336, 2),
+                                          (2048, 2 * 14336, 4096, 1)])
+def test_pingpong_gemm_llama_shapes(cuda, dt, M, N, K, splits):
+    """The ping-pong 256x256 kernel (cfg 20) on Llama prefill shapes: plain store,
+    f32 residual accumulate (split-K included) and the fused SwiGLU, random operands."""
+    from cake_amd.ops import gemm as G
+    torch.manual_seed(M + N + K)
+    x, w = _r(M, K, dt=dt), _r(N, K, dt=dt, std=K ** -0.5)
+    if N > 16384:  # the fused gate|up weight
+        Fh = N // 2
+        y = _ref(x, w)
+        _close(G.linear(x, w, epi="swiglu", cfg=20, splits=splits),
+               F.silu(y[:, :Fh]) * y[:, Fh:], K)
+        return
+    _close(G.linear(x, w, cfg=20, splits=splits), _ref(x, w), K)
+    r = torch.randn(M, N, device="cuda")
+    ref = r + _ref(x, w)
+    G.linear(x, w, epi="resid32", resid=r, cfg=20, splits=splits)
+    torch.testing.assert_close(r, ref, atol=3e-2, rtol=1e-2)

@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _bench(tmp_path, n, streams, name, hop="dist", hop_dtype="f32", k=1, steps=12,
-           engine="native"):
+           engine="native", extra_env=None):
     out = tmp_path / f"{name}.json"
     args = ["bench.py", "--model", "tiny", "--steps", str(steps), "--warmup", "3", "--prompt-len", "9",
             "--max-seq", "256", "--dump-tokens", str(out), "--engine", engine]
@@ -24,7 +24,8 @@ def _bench(tmp_path, n, streams, name, hop="dist", hop_dtype="f32", k=1, steps=1
                  "--streams", str(streams),
                  "--hop", hop, "--hop-dtype", hop_dtype, "--steps-per-graph", str(k),
                  "--launch-timeout", "200"]
-    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", CAKE_HOP_TIMEOUT="30")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", CAKE_HOP_TIMEOUT="30",
+               **(extra_env or {}))
     env.pop("WORLD_SIZE", None)
     r = subprocess.run([sys.executable] + args, cwd=ROOT, capture_output=True, text=True,
                        timeout=240, env=env)
@@ -99,3 +100,15 @@ def test_pipeline_ipc_hops_in_graph_match_single(cuda, tmp_path):
     steps = len(toks) - 9
     assert steps >= 32 and not bad, (bad, exact, near)
     assert near <= steps // 4, (exact, near)
+
+
+def test_failed_ipc_selftest_falls_back_to_dist(cuda, tmp_path):
+    """The native group's start-up self-test (hop inboxes and the uncached prefill relay
+    buffers, two rounds each) forced to fail on every rank: the N=2 bench still completes,
+    on the Python pipeline over torch.distributed, and says so."""
+    _, single = _bench(tmp_path, 1, 1, "single_py", engine="python")
+    m, pp = _bench(tmp_path, 2, 1, "forced", hop="ipc",
+                   extra_env={"CAKE_IPC_SELFTEST_FAIL": "1"})
+    assert m["hop"] == "dist" and m["engine"] == "python", m
+    assert "CAKE_IPC_SELFTEST_FAIL" in m["native_fallback"], m
+    assert pp[0] == single[0]

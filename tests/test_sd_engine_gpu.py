@@ -5,7 +5,8 @@ planner: the same variants):
 
   * each component — text encoder(s), one UNet forward, the VAE decode — agrees with
     the Python module to f16 rounding;
-  * a whole guided generation (DDIM for v1-5 / Euler-ancestral for turbo, graph replays
+  * a whole guided generation (DDIM for v1-5 and, with v-prediction, v2-1 /
+    Euler-ancestral for turbo, graph replays
     after the first step) ends in the same latents as SDUnit.denoise and the same image.
 """
 import numpy as np
@@ -17,7 +18,7 @@ pytestmark = pytest.mark.gpu
 DT = torch.float16
 
 
-@pytest.fixture(scope="module", params=["v1-5", "xl", "turbo"])
+@pytest.fixture(scope="module", params=["v1-5", "v2-1", "xl", "turbo"])
 def mini(request, tmp_path_factory):
     from cake_amd.models.sd.config import mini_config
     from cake_amd.models.sd.weights import write_sd_checkpoint
