@@ -51,7 +51,7 @@ CAKE_GEMM_EXTERN_ALL(kF16)
 
 using namespace cake;
 static inline void cfg_dims(int cfg, int& bm, int& bn) {
-  if (cfg == kPPCfg) { bm = bn = 256; return; }
+  if (cfg == kPPCfg || cfg == kRSCfg || cfg == k4WCfg) { bm = bn = 256; return; }
 #define X(id, BM, BN, WM, WN, NS, PR) if (cfg == id) { bm = BM; bn = BN; return; }
   CAKE_GEMM_CFGS(X)
 #undef X
@@ -110,6 +110,12 @@ CAKE_API int cake_gemm(int dt, int epi, int cfg, int splits, const void* a, long
     return (int)hipErrorInvalidValue;
   const bool gated = (epi == kEpiSwiglu || epi == kEpiGeglu);
   if (gated && N % 16) return (int)hipErrorInvalidValue;
+  if (cfg == kRSCfg || cfg == k4WCfg) {  // whole 64-element k steps; 31-bit offsets
+    const long long wrows = gated ? 2LL * N : N;
+    if (K % kGBK || ((long long)(M - 1) * lda + K) * 2 >= 0x7fffffffLL ||
+        ((wrows - 1) * ldb + K) * 2 >= 0x7fffffffLL)
+      return (int)hipErrorInvalidValue;
+  }
   GemmArgs g{};
   g.a = (const uint16_t*)a; g.b = (const uint16_t*)b; g.c = (uint16_t*)c;
   g.bias = (const uint16_t*)bias;

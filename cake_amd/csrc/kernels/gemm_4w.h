@@ -1,0 +1,191 @@
+// Four-wave 256x256 MFMA GEMM (plan cfg 22): the large Llama prefill projections.
+//
+// Included by gemm_kernel.h (launch_gemm dispatches cfg 22 here); same GemmArgs, tile
+// order, swizzled LDS image, fragment reads, interleaved schedule and epilogues as
+// gemm_kernel's IL path.
+//
+// The shape of the winning library kernel on this chip (hipBLASLt's 256x256x64 tile,
+// profiles/r6_gemm_pmc_8192.txt): one wave per SIMD, 128 x 128 outputs per wave, LDS-DMA
+// staging, 32 fragment reads per k-step.  gemm_kernel's 4-wave form of the same tile
+// measured 0.5x (round 2) because each of its 16 DMA issues per wave and k-step
+// recomputed a 64-bit source pointer and a zeros-page select in VALU; here a DMA is one
+// buffer_load_dwordx4 ... lds:
+//   * one per-lane byte offset VGPR per operand (the lane's row in its 32-row group and
+//     its swizzled 16-byte chunk), the group's row offset and the k step in the scalar
+//     soffset, the LDS destination in M0;
+//   * rows past the matrix read through the descriptor's range check (zeros, no fault),
+//     so no per-issue select and no zeros page; gated (SwiGLU / GEGLU) weights keep a
+//     constant row stride per group (16 gate + 16 up rows), so the same form covers them.
+//   Needs K and the split's k range in whole 64-element steps and operands under 2 GB
+//   (host-checked).
+#pragma once
+
+namespace cake {
+
+constexpr int k4WCfg = 22;  // plan cfg id of this kernel (BM = BN = 256)
+
+template <int DT, int EPI>
+__global__ __launch_bounds__(256) void gemm_4w_kernel(GemmArgs g) {
+  constexpr int BM = 256, BN = 256, WTM = 128, WTN = 128, FM = 8, FN = 8;
+  constexpr int BUF = (BM + BN) * 128;  // 64 KB per k-step buffer
+  constexpr int IPW = 16;               // DMA wave-instructions per wave per k-step
+  constexpr int STG_LD = WTN + 4, STG = 16 * STG_LD * 4;
+  static_assert(4 * STG <= 2 * BUF, "epilogue staging fits the operand buffers");
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * BUF];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+
+  // ---- XCD-aware grouped tile order (as gemm_kernel) ---------------------
+  const int ntiles = g.tiles_m * g.tiles_n;
+  int id;
+  {
+    const int bid = blockIdx.x;
+    const int q = ntiles / 8, r = ntiles % 8, x = bid % 8, i = bid / 8;
+    id = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+  }
+  constexpr int GROUP = 8;
+  const int per_group = GROUP * g.tiles_n;
+  const int first_m = (id / per_group) * GROUP;
+  const int gm = min(GROUP, g.tiles_m - first_m);
+  const int m0 = (first_m + (id % per_group) % gm) * BM;
+  const int n0 = ((id % per_group) / gm) * BN;
+  const int split = blockIdx.y;
+  const int kb = split * g.kps, ke = min(g.K, kb + g.kps);
+  const int nk = (ke - kb) / kGBK;
+
+  // ---- DMA: instruction i of this wave fills LDS rows i*32 + wave*8 + [0, 8) (A rows
+  // for i < 8, B rows after); lane l -> row + l/8, slot l%8 holding source chunk
+  // (l%8) ^ ((row >> 1) & 7), the same for every i
+  const int rA = wave * 8 + (lane >> 3);
+  const int chunk = (lane & 7) ^ ((rA >> 1) & 7);
+  const long long brows = g.gated ? 2LL * g.half : (long long)g.Nv;
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(g.a), (short)0, (int)(((long long)(g.M - 1) * g.lda + g.K) * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(g.b), (short)0, (int)(((brows - 1) * g.ldb + g.K) * 2), 0x00020000);
+  const uint32_t voff_a = (uint32_t)(((long long)(m0 + rA) * g.lda + chunk * 8) * 2);
+  long long brow0;  // weight row of this lane in B group 0
+  if (!g.gated) brow0 = n0 + rA;
+  else brow0 = (rA < 16 ? 0LL : (long long)g.half - 16) + n0 / 2 + rA;
+  const uint32_t voff_b = (uint32_t)((brow0 * g.ldb + chunk * 8) * 2);
+  // scalar byte offsets of each 32-row group (A: 32 rows; B: 32 virtual rows = 16
+  // weight rows of each half when gated)
+  const uint32_t gstride_a = (uint32_t)(32LL * g.lda * 2);
+  const uint32_t gstride_b = (uint32_t)((g.gated ? 16LL : 32LL) * g.ldb * 2);
+  const uint32_t kbase = (uint32_t)kb * 2;
+  // a step past the split's end: soffset 2^31 - 1 puts every lane out of range (zeros,
+  // no memory traffic; voffsets stay below 2^31, so the sum cannot wrap)
+  auto stage_one = [&](int step, int buf, int i) __attribute__((always_inline)) {
+    const uint32_t ks = kbase + (uint32_t)step * (kGBK * 2);
+    auto* dst = (__attribute__((address_space(3))) void*)(smem + buf * BUF + (i * 4 + wave) * 1024);
+    const bool live = step < nk;
+    if (i < 8)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          ra, dst, 16, voff_a, live ? (int)(ks + i * gstride_a) : 0x7fffffff, 0, 0);
+    else
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rb, dst, 16, voff_b, live ? (int)(ks + (i - 8) * gstride_b) : 0x7fffffff, 0, 0);
+  };
+  auto stage = [&](int step, int buf) {
+#pragma unroll
+    for (int i = 0; i < IPW; ++i) stage_one(step, buf, i);
+  };
+
+  // ---- fragment addresses (as gemm_kernel) ----------------------------------
+  const int swz = (lane & 15) >> 1;
+  const uint32_t lrow = (uint32_t)(lane & 15) * 128;
+  const uint32_t off0 = (uint32_t)(((lane >> 4) ^ swz) * 16);
+  const uint32_t off1 = (uint32_t)(((4 + (lane >> 4)) ^ swz) * 16);
+  const uint32_t lds0 = lds_off(smem);
+  const uint32_t a_base = lds0 + (uint32_t)(wr * WTM) * 128 + lrow;
+  const uint32_t b_base = lds0 + (uint32_t)(BM + wc * WTN) * 128 + lrow;
+
+  cf32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) azero(acc[i][j]);
+
+  // The interleaved two-stage schedule of gemm_kernel (IL, NS = 2):
+  //   [kk1 reads of t | kk0 MFMAs of t] wait | vmcnt(DMA t+1) barrier
+  //   [DMA t+2 into t's buffer + kk0 reads of t+1 | kk1 MFMAs of t] wait
+  // Every step issues all 16 DMAs (past the split's end: out of the descriptors' range,
+  // zeros) so the counted waits hold.
+  constexpr int NM = FM * FN, NR = FM + FN, NL = IPW + NR;
+  uint4 af0[FM], bf0[FN], af1[FM], bf1[FN];
+  stage(0, 0);
+  __builtin_amdgcn_s_waitcnt(vm_wait(0));
+  asm volatile("s_barrier" ::: "memory");
+  stage(1, 1);
+#pragma unroll
+  for (int i = 0; i < FM; ++i) af0[i] = ds_read16(a_base + i * 16 * 128 + off0);
+#pragma unroll
+  for (int j = 0; j < FN; ++j) bf0[j] = ds_read16(b_base + j * 16 * 128 + off0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  int buf = 0;
+  for (int t = 0; t < nk; ++t) {
+    const uint32_t ab = a_base + buf * BUF, bb = b_base + buf * BUF;
+    static_for<0, NM>([&](auto mi) __attribute__((always_inline)) {
+      constexpr int m = decltype(mi)::value;
+      amfma_v<DT>(acc[m / FN][m % FN], af0[m / FN], bf0[m % FN]);
+      static_for<(m * NR + NM - 1) / NM, ((m + 1) * NR + NM - 1) / NM>([&](auto ri)
+                                                                    __attribute__((always_inline)) {
+        constexpr int r = decltype(ri)::value;
+        if constexpr (r < FM) af1[r] = ds_read16_off<r * 16 * 128>(ab + off1);
+        else bf1[r - FM] = ds_read16_off<(r - FM) * 16 * 128>(bb + off1);
+      });
+    });
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    const int nbuf = buf ^ 1;
+    __builtin_amdgcn_s_waitcnt(vm_wait(0));  // DMA of step t+1 landed
+    asm volatile("s_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    const uint32_t na = a_base + nbuf * BUF, nb = b_base + nbuf * BUF;
+    const int s2 = t + 2;
+    static_for<0, NM>([&](auto mi) __attribute__((always_inline)) {
+      constexpr int m = decltype(mi)::value;
+      amfma_v<DT>(acc[m / FN][m % FN], af1[m / FN], bf1[m % FN]);
+      static_for<(m * NL + NM - 1) / NM, ((m + 1) * NL + NM - 1) / NM>([&](auto li)
+                                                                    __attribute__((always_inline)) {
+        constexpr int l = decltype(li)::value;
+        if constexpr (l % 2 == 0 && l / 2 < IPW) {  // DMAs and reads alternate
+          stage_one(s2, buf, l / 2);
+        } else {
+          constexpr int r = (l - 1) / 2;
+          if constexpr (r < FM) af0[r] = ds_read16_off<r * 16 * 128>(na + off0);
+          else bf0[r - FM] = ds_read16_off<(r - FM) * 16 * 128>(nb + off0);
+        }
+      });
+    });
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    buf = nbuf;
+  }
+
+  // ---- epilogue (as gemm_kernel) -----------------------------------------
+#pragma unroll
+  for (int j = 0; j < FN; ++j) asm volatile("" : "+a"(acc[FM - 1][j]));
+  asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+#pragma unroll
+  for (int j = 0; j < FN; ++j) asm volatile("" : "+a"(acc[FM - 1][j]));
+  __builtin_amdgcn_s_waitcnt(vm_wait(0));
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  float* stg = reinterpret_cast<float*>(smem + wave * STG);
+  const int row_m0 = m0 + wr * WTM;
+  const int vcol0 = n0 + wc * WTN;
+  EpiOps<DT, EPI, FN> ops;
+  ops.load_bias(g, vcol0, lane);
+  ops.template load_res<0>(g, row_m0 + (lane >> 2), vcol0, lane);
+  static_for<0, FM>([&](auto ii) __attribute__((always_inline)) {
+    constexpr int i = decltype(ii)::value;
+    if constexpr (i + 1 < FM)
+      ops.template load_res<(i + 1) & 1>(g, row_m0 + (i + 1) * 16 + (lane >> 2), vcol0, lane);
+    epi_strip<DT, EPI, FN, i & 1>(g, acc[i], stg, row_m0 + i * 16, vcol0, split, lane, ops);
+  });
+}
+
+}  // namespace cake

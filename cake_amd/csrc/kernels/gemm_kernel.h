@@ -655,6 +655,8 @@ __global__ __launch_bounds__(256) void gemm_splitk_finalize(GemmArgs g, int spli
 }  // namespace cake
 
 #include "gemm_pp.h"
+#include "gemm_rs.h"
+#include "gemm_4w.h"
 
 namespace cake {
 
@@ -667,6 +669,14 @@ template <int DT, int EPI>
 int launch_gemm(int cfg, dim3 grid, hipStream_t st, const GemmArgs& g) {
   if (cfg == kPPCfg) {
     hipLaunchKernelGGL((gemm_pp_kernel<DT, EPI>), grid, dim3(512), 0, st, g);
+    return (int)hipGetLastError();
+  }
+  if (cfg == kRSCfg) {
+    hipLaunchKernelGGL((gemm_rs_kernel<DT, EPI>), grid, dim3(256), 0, st, g);
+    return (int)hipGetLastError();
+  }
+  if (cfg == k4WCfg) {
+    hipLaunchKernelGGL((gemm_4w_kernel<DT, EPI>), grid, dim3(256), 0, st, g);
     return (int)hipGetLastError();
   }
 

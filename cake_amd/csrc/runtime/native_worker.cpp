@@ -10,6 +10,7 @@
 #include <random>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -23,7 +24,9 @@ namespace cake {
 namespace {
 
 // <root>/cake_amd/lib/libcake_engine.so: next to the library / executable holding this
+// (CAKE_ENGINE_LIB overrides: the host self-test's stub engine)
 std::string engine_path() {
+  if (const char* e = std::getenv("CAKE_ENGINE_LIB"); e && *e) return e;
   Dl_info info{};
   if (dladdr(reinterpret_cast<void*>(&engine_path), &info) && info.dli_fname) {
     char buf[4096];
@@ -85,11 +88,13 @@ int run_native_worker(const NativeWorkerOpts& o, const TopoNode& node) {
                               char*, int32_t);
   using Drop = void (*)(void*, uint64_t);
   using InfoFn = int32_t (*)(void*, int32_t*);
+  using CloseFn = void (*)(void*);
   auto open_layers = reinterpret_cast<OpenLayers>(dlsym(h, "cake_engine_open_layers"));
   auto forward = reinterpret_cast<Forward>(dlsym(h, "cake_engine_forward"));
   auto drop = reinterpret_cast<Drop>(dlsym(h, "cake_engine_drop_session"));
   auto einfo = reinterpret_cast<InfoFn>(dlsym(h, "cake_engine_info"));
-  if (!open_layers || !forward || !drop || !einfo) {
+  auto eclose = reinterpret_cast<CloseFn>(dlsym(h, "cake_engine_close"));
+  if (!open_layers || !forward || !drop || !einfo || !eclose) {
     std::fprintf(stderr, "%s: engine symbols missing in %s\n", tag.c_str(), lib.c_str());
     return 1;
   }
@@ -134,7 +139,8 @@ int run_native_worker(const NativeWorkerOpts& o, const TopoNode& node) {
     port = c == std::string::npos ? 10128 : std::atoi(a.c_str() + c + 1);
     if (host.empty()) host = "0.0.0.0";
   }
-  WorkerServer server(host, port, info, node.name);
+  auto srv = std::make_unique<WorkerServer>(host, port, info, node.name);
+  WorkerServer& server = *srv;
   std::mutex mu;  // one compute at a time (the GPU stream is shared)
   server.set_compute([&](uint64_t session, const std::vector<BatchItem>& ops,
                          const RawTensor& x) {
@@ -197,7 +203,10 @@ int run_native_worker(const NativeWorkerOpts& o, const TopoNode& node) {
   server.set_log([tag](const std::string& m) { std::fprintf(stderr, "[%s] %s\n", tag.c_str(), m.c_str()); });
   std::fprintf(stderr, "[%s] native worker %s: %zu layers on device %d, listening on %s:%d\n",
                tag.c_str(), node.name.c_str(), layers.size(), eo.device, host.c_str(), server.port());
+  if (o.on_serving) o.on_serving(server);
   server.serve();
+  srv.reset();  // stops and joins every connection thread: no compute left in flight
+  eclose(eng);
   return 0;
 }
 
@@ -307,13 +316,15 @@ int run_native_sd_worker(const NativeWorkerOpts& o, const TopoNode& node) {
   using Unet = int32_t (*)(void*, const float*, int32_t, float, const float*, float*, char*, int32_t);
   using Vae = int32_t (*)(void*, const float*, float*, char*, int32_t);
   using Info = void (*)(void*, int32_t*);
+  using Close = void (*)(void*);
   auto vae_enc = reinterpret_cast<Vae>(dlsym(h, "cake_sd_vae_encode"));
   auto open = reinterpret_cast<Open>(dlsym(h, "cake_sd_open"));
   auto text = reinterpret_cast<Text>(dlsym(h, "cake_sd_text"));
   auto unet = reinterpret_cast<Unet>(dlsym(h, "cake_sd_unet"));
   auto vae = reinterpret_cast<Vae>(dlsym(h, "cake_sd_vae_decode"));
   auto info = reinterpret_cast<Info>(dlsym(h, "cake_sd_info"));
-  if (!open || !text || !unet || !vae || !vae_enc || !info) {
+  auto sclose = reinterpret_cast<Close>(dlsym(h, "cake_sd_close"));
+  if (!open || !text || !unet || !vae || !vae_enc || !info || !sclose) {
     std::fprintf(stderr, "%s: SD engine symbols missing in %s\n", tag.c_str(), lib.c_str());
     return 1;
   }
@@ -359,7 +370,8 @@ int run_native_sd_worker(const NativeWorkerOpts& o, const TopoNode& node) {
     port = c == std::string::npos ? 10128 : std::atoi(o.address.c_str() + c + 1);
     if (host.empty()) host = "0.0.0.0";
   }
-  WorkerServer server(host, port, wi, node.name);
+  auto srv = std::make_unique<WorkerServer>(host, port, wi, node.name);
+  WorkerServer& server = *srv;
   std::mutex mu;
   std::mt19937 rng(0x5eedu);  // VAE posterior samples (parity with torch's stream unpinned)
   const int W = inf[0], H = inf[1], Dc = inf[2];
@@ -446,7 +458,10 @@ int run_native_sd_worker(const NativeWorkerOpts& o, const TopoNode& node) {
   std::fprintf(stderr, "[%s] native SD worker %s: %s (%dx%d) on device %d, listening on %s:%d\n",
                tag.c_str(), node.name.c_str(), units.c_str(), W, H, o.device, host.c_str(),
                server.port());
+  if (o.on_serving) o.on_serving(server);
   server.serve();
+  srv.reset();  // stops and joins every connection thread
+  sclose(eng);
   return 0;
 }
 

@@ -4,11 +4,14 @@
 // by cake-cli --mode worker and the embeddable cake_start_worker (capi.cpp).
 #pragma once
 
+#include <functional>
 #include <string>
 
 #include "topology.h"
 
 namespace cake {
+
+class WorkerServer;
 
 struct NativeWorkerOpts {
   std::string model_dir;
@@ -22,6 +25,9 @@ struct NativeWorkerOpts {
   std::string sd_version;
   int sd_width = 0, sd_height = 0;
   std::string sd_paths[4];
+  // called once the server listens, before it blocks in serve() (the host self-test
+  // takes the server here to stop it: csrc/tests/worker_selftest.cpp)
+  std::function<void(WorkerServer&)> on_serving;
 };
 
 // Serve `node` until the server stops; the exit code (1 = engine failure, 2 = no layers).

@@ -48,10 +48,13 @@ void WorkerServer::log(const std::string& s) {
   if (log_) log_(s);
 }
 
+// Everything under threads_mu_, which serve() also takes once before it returns: a
+// stop() from another thread has finished with this object by the time serve()'s
+// caller may destroy it (host self-test: csrc/tests/worker_selftest.cpp under TSan).
 void WorkerServer::stop() {
+  std::lock_guard<std::mutex> g(threads_mu_);
   if (stop_.exchange(true)) return;
   ::shutdown(listen_fd_, SHUT_RDWR);
-  std::lock_guard<std::mutex> g(threads_mu_);
   for (int fd : conn_fds_)
     if (fd >= 0) ::shutdown(fd, SHUT_RDWR);  // unblock readers; handle() closes
 }
@@ -72,6 +75,7 @@ void WorkerServer::serve() {
     conn_fds_.push_back(fd);
     threads_.emplace_back(&WorkerServer::handle, this, fd, peer, session);
   }
+  std::lock_guard<std::mutex> g(threads_mu_);  // a concurrent stop() has returned
 }
 
 void WorkerServer::handle(int fd, std::string peer, uint64_t session) {

@@ -50,7 +50,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shapes", default="sq,8b,70b")
     ap.add_argument("--ms", default="2048")
-    ap.add_argument("--arms", default="mfma,pp,pp2,lib")
+    ap.add_argument("--arms", default="mfma,rs,rs2,lib")
     ap.add_argument("--rounds", type=int, default=3)
     a = ap.parse_args()
     torch.manual_seed(0)
@@ -62,7 +62,8 @@ def main():
         r0 = torch.randn(M, N, device="cuda") if epi == "resid32" else None
         out = None if epi == "resid32" else torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         cfg5, s5 = G.plan_mfma(M, Nv, K, epi)
-        plans = {"mfma": (cfg5, s5), "pp": (20, 1), "pp2": (20, 2), "lib": (G.LIB, 1)}
+        plans = {"mfma": (cfg5, s5), "pp": (20, 1), "pp2": (20, 2), "rs": (21, 1), "rs2": (21, 2), "w4": (22, 1), "w42": (22, 2),
+                 "lib": (G.LIB, 1)}
         y = x.float() @ w.float().t()
         if epi == "swiglu":
             ref = torch.nn.functional.silu(y[:, :N]) * y[:, N:]

@@ -25,7 +25,7 @@ def _close(got, ref, K):
 
 
 @pytest.mark.parametrize("dt", DTYPES)
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7, 8, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7, 8, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22])
 @pytest.mark.parametrize("M,N,K,splits", [(128, 256, 256, 1), (77, 200, 320, 1),
                                           (300, 520, 1024, 3), (1, 64, 64, 1),
                                           (513, 136, 648, 2)])
@@ -33,6 +33,11 @@ def test_gemm_store_configs(cuda, dt, cfg, M, N, K, splits):
     from cake_amd.ops import gemm as G
     torch.manual_seed(M + N + K)
     x, w, b = _r(M, K, dt=dt), _r(N, K, dt=dt, std=K ** -0.5), _r(N, dt=dt)
+    if cfg in G.K64_ONLY and K % 64:  # refused, not wrong
+        from cake_amd.ops._lib import KernelError
+        with pytest.raises(KernelError):
+            G.linear(x, w, b, cfg=cfg, splits=splits)
+        return
     y = G.linear(x, w, b, cfg=cfg, splits=splits)
     _close(y, _ref(x, w, b), K)
     y2 = G.linear(x, w, cfg=cfg, splits=splits)
@@ -135,13 +140,18 @@ def test_gemm_model_shapes(cuda, name, M, N, K, epi):
 
 
 @pytest.mark.parametrize("dt", DTYPES)
-@pytest.mark.parametrize("cfg", [5, 0, 13, 14, 15, 16, 17, 20])
+@pytest.mark.parametrize("cfg", [5, 0, 13, 14, 15, 16, 17, 20, 21, 22])
 @pytest.mark.parametrize("M,N,K", [(300, 700, 640), (257, 272, 2112), (520, 776, 200)])
 def test_gemm_interleaved_all_epilogues(cuda, dt, cfg, M, N, K):
     """Interleaved-schedule tiles with ragged M/N and every epilogue."""
     from cake_amd.ops import gemm as G
     torch.manual_seed(M + N + K + cfg)
     x, w, b = _r(M, K, dt=dt), _r(N, K, dt=dt, std=K ** -0.5), _r(N, dt=dt)
+    if cfg in G.K64_ONLY and K % 64:
+        from cake_amd.ops._lib import KernelError
+        with pytest.raises(KernelError):
+            G.linear(x, w, b, cfg=cfg, splits=1)
+        return
     _close(G.linear(x, w, b, cfg=cfg, splits=1), _ref(x, w, b), K)
     r = torch.randn(M, N, device="cuda")
     ref = r + _ref(x, w)
@@ -260,20 +270,22 @@ def test_library_gemm_plan_cache_eviction(cuda):
 @pytest.mark.parametrize("dt", DTYPES)
 @pytest.mark.parametrize("M,N,K,splits", [(2048, 6144, 4096, 1), (1000, 4096, 14336, 2),
                                           (2048, 2 * 14336, 4096, 1)])
-def test_pingpong_gemm_llama_shapes(cuda, dt, M, N, K, splits):
-    """The ping-pong 256x256 kernel (cfg 20) on Llama prefill shapes: plain store,
-    f32 residual accumulate (split-K included) and the fused SwiGLU, random operands."""
+@pytest.mark.parametrize("cfg", [20, 21, 22])
+def test_big_tile_gemm_llama_shapes(cuda, dt, M, N, K, splits, cfg):
+    """The ping-pong (cfg 20) and register-staged (cfg 21) 256x256 kernels on Llama
+    prefill shapes: plain store, f32 residual accumulate (split-K included) and the fused
+    SwiGLU, random operands."""
     from cake_amd.ops import gemm as G
     torch.manual_seed(M + N + K)
     x, w = _r(M, K, dt=dt), _r(N, K, dt=dt, std=K ** -0.5)
     if N > 16384:  # the fused gate|up weight
         Fh = N // 2
         y = _ref(x, w)
-        _close(G.linear(x, w, epi="swiglu", cfg=20, splits=splits),
+        _close(G.linear(x, w, epi="swiglu", cfg=cfg, splits=splits),
                F.silu(y[:, :Fh]) * y[:, Fh:], K)
         return
-    _close(G.linear(x, w, cfg=20, splits=splits), _ref(x, w), K)
+    _close(G.linear(x, w, cfg=cfg, splits=splits), _ref(x, w), K)
     r = torch.randn(M, N, device="cuda")
     ref = r + _ref(x, w)
-    G.linear(x, w, epi="resid32", resid=r, cfg=20, splits=splits)
+    G.linear(x, w, epi="resid32", resid=r, cfg=cfg, splits=splits)
     torch.testing.assert_close(r, ref, atol=3e-2, rtol=1e-2)

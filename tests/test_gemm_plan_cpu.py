@@ -16,8 +16,16 @@ def _kernel_cfgs() -> dict:
     src = (ROOT / "cake_amd/csrc/kernels/gemm_kernel.h").read_text()
     body = src[src.index("#define CAKE_GEMM_CFGS(X)"):]
     body = body[:body.index("\n\n")]
-    return {int(m[0]): (int(m[1]), int(m[2]), int(m[3]), int(m[4]))
+    cfgs = {int(m[0]): (int(m[1]), int(m[2]), int(m[3]), int(m[4]))
             for m in re.findall(r"X\((\d+),\s*(\d+),\s*(\d+),\s*(\d+),\s*(\d+),", body)}
+    # the two 256x256 kernels of their own: ping-pong (8 waves, 2 x 4) and register-staged
+    # (4 waves, 2 x 2)
+    for hdr, name, waves in (("gemm_pp.h", "kPPCfg", (2, 4)), ("gemm_rs.h", "kRSCfg", (2, 2)),
+                             ("gemm_4w.h", "k4WCfg", (2, 2))):
+        t = (ROOT / "cake_amd/csrc/kernels" / hdr).read_text()
+        cid = int(re.search(name + r" = (\d+);", t).group(1))
+        cfgs[cid] = (256, 256) + waves
+    return cfgs
 
 
 def test_tile_tables_agree():
@@ -49,11 +57,14 @@ def test_tuned_table_entries_are_launchable():
         if e["epi"] in ("swiglu", "geglu"):
             assert e["cfg"] not in G.NO_GATED and e["Nv"] % 32 == 0, e
         assert e["K"] % 8 == 0, e
+        if e["cfg"] in G.K64_ONLY:
+            assert e["K"] % 64 == 0 and (e["K"] // e["splits"]) % 64 == 0, e
 
 
 def test_plan_uses_measured_entries():
     table = json.loads((ROOT / "cake_amd/ops/gemm_tuned.json").read_text())["entries"]
-    e = next(x for x in table if x["M"] >= 512)
+    # (entries naming the library GEMM are read only under CAKE_GEMM_LIB=1)
+    e = next(x for x in table if x["M"] >= 512 and x["cfg"] != G.LIB)
     assert G.plan(e["M"], e["Nv"], e["K"], e["epi"]) == (e["cfg"], e["splits"])
     # a nearby M (within 2x) reuses the measured tile without split-K
     cfg, splits = G.plan(e["M"] + 8, e["Nv"], e["K"], e["epi"])
@@ -63,19 +74,28 @@ def test_plan_uses_measured_entries():
     assert cfg in G.CFG_TILES and splits >= 1
 
 
-def test_library_gemm_plans_agree_with_the_engine():
-    """The measured table sends the large Llama prefill projections to the library GEMM
-    (profiles/r5_gemm_lib.jsonl); the engine planner accepts the same cfg for the same
-    epilogues, and the small-M shapes stay on the MFMA kernel where it measured faster."""
+def test_library_gemm_is_off_the_default_path(monkeypatch):
+    """No default plan names the library GEMM (hipBLASLt): every prefill projection runs an
+    MFMA kernel.  The measured library entries (profiles/r5_gemm_lib.jsonl) stay in the
+    table as the A/B arm, read only under CAKE_GEMM_LIB=1 — by both planners, for the same
+    epilogues."""
     eng = (ROOT / "cake_amd/csrc/engine/engine_util.h").read_text()
     assert re.search(r"constexpr int kGemmLib = (-?\d+);", eng).group(1) == str(G.LIB)
     body = eng[eng.index("const bool lib = "):]
     body = body[:body.index(";")]
+    assert "lib_ok &&" in body and 'getenv("CAKE_GEMM_LIB")' in eng
     assert set(re.findall(r'ep == "(\w+)"', body)) == set(G.LIB_EPIS)
-    assert G.plan(2048, 28672, 4096, "swiglu")[0] == G.LIB       # 8B gate|up, 2048 tokens
-    assert G.plan(2048, 6144, 4096, "store")[0] == G.LIB         # 8B q|k|v
-    assert G.plan(256, 6144, 4096, "store")[0] in G.CFG_TILES    # ours at 256 tokens
-    assert G.plan(2048, 1280, 5120, "add16")[0] in G.CFG_TILES   # SD shapes untouched
+    monkeypatch.setattr(G, "_plans", {})
+    assert all(e["cfg"] != G.LIB for e in G._TUNED)
+    assert G.plan(2048, 28672, 4096, "swiglu")[0] in G.CFG_TILES   # 8B gate|up, 2048 tokens
+    assert G.plan(2048, 6144, 4096, "store")[0] in G.CFG_TILES     # 8B q|k|v
+    assert G.plan(2048, 1280, 5120, "add16")[0] in G.CFG_TILES     # SD shapes
+    monkeypatch.setenv("CAKE_GEMM_LIB", "1")
+    lib_table = G._load_tuned()
+    assert any(e["cfg"] == G.LIB for e in lib_table)
+    monkeypatch.setattr(G, "_TUNED", lib_table)
+    monkeypatch.setattr(G, "_plans", {})
+    assert G.plan(2048, 28672, 4096, "swiglu")[0] == G.LIB
 
 
 def test_nearest_measured_plan_scales_split_k(monkeypatch):

@@ -1,5 +1,7 @@
-"""Native runtime self-test (topology, wire codec, safetensors, multi-threaded
-WorkerServer) built plain, with ASan+UBSan and with TSan -- host code only."""
+"""Native runtime self-tests built plain, with ASan+UBSan and with TSan -- host code only:
+topology, wire codec, safetensors, the multi-threaded WorkerServer, and the native text /
+SD workers (native_worker.cpp: concurrent masters, the compute lock, request
+validation, mid-request disconnects, stop) over a host stub of the engine library."""
 import os
 import shutil
 import subprocess
@@ -18,4 +20,4 @@ def test_runtime_selftest_under_sanitizers(variant, tmp_path):
                        capture_output=True, text=True, timeout=600)
     sys.stdout.write(r.stdout[-2000:])
     assert r.returncode == 0, r.stderr[-4000:]
-    assert r.stdout.count(" ok") == 4
+    assert r.stdout.count(" ok") == 6
