@@ -351,10 +351,25 @@ def bench_multi(a) -> None:
             # the N ranks; seconds per diffusion step of one image (parallel/sd_split.py)
             from cake_amd.parallel.sd_split import measure_sd_split
             key = "sdxl_tiny_split" if a.tiny_extras else "sdxl_1024_split"
-            try:
-                r = measure_sd_split(env, steps=a.sd_steps, warmup=2, tiny=a.tiny_extras)
-            except Exception as e:  # noqa: BLE001  (setup failures are symmetric: all ranks)
-                r = {"error": f"{type(e).__name__}: {e}"[:300]}
+            r, err = None, None
+            if _native(a) and not a.tiny_extras:  # the native engine's split UNet
+                from cake_amd.models.sd.bench import measure_native_split
+                try:
+                    r = measure_native_split(env, "xl", steps=a.sd_steps)
+                except Exception as e:  # noqa: BLE001  (falls back below, on every rank)
+                    err = f"{type(e).__name__}: {e}"[:300]
+                if env.max_over_ranks(1.0 if err else 0.0) == 0:
+                    err = None
+                else:
+                    r = None
+                    err = err or "a peer rank failed"
+            if r is None and (err is not None or not _native(a) or a.tiny_extras):
+                try:
+                    r = measure_sd_split(env, steps=a.sd_steps, warmup=2, tiny=a.tiny_extras)
+                    if err and r is not None:
+                        r = dict(r, native_fallback=err)
+                except Exception as e:  # noqa: BLE001  (setup failures are symmetric: all ranks)
+                    r = {"error": f"{type(e).__name__}: {e}"[:300]}
             if env.rank == 0:
                 extra["sd"] = {key: r}
         if env.rank == 0:

@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "../runtime/json.h"
+#include "../runtime/net.h"
 
 namespace cake {
 
@@ -31,6 +32,33 @@ inline void k_check(int rc, const char* what) {
     throw Error(std::string(what) + ": hipBLASLt status " + std::to_string(rc - 1000));
   throw Error(std::string(what) + ": " + hipGetErrorString((hipError_t)rc));
 }
+
+// ---------------------------------------------------------------------------
+// control plane of the multi-rank engines: IPC handles as hex, JSON frames over TCP
+// ---------------------------------------------------------------------------
+inline std::string hex_of(const void* p, size_t n) {
+  static const char* d = "0123456789abcdef";
+  std::string s;
+  const uint8_t* b = static_cast<const uint8_t*>(p);
+  for (size_t i = 0; i < n; ++i) {
+    s.push_back(d[b[i] >> 4]);
+    s.push_back(d[b[i] & 15]);
+  }
+  return s;
+}
+
+inline void unhex(const std::string& s, void* out, size_t n) {
+  if (s.size() != 2 * n) throw Error("bad IPC handle");
+  auto v = [](char c) { return c <= '9' ? c - '0' : c - 'a' + 10; };
+  uint8_t* b = static_cast<uint8_t*>(out);
+  for (size_t i = 0; i < n; ++i) b[i] = (uint8_t)(v(s[2 * i]) << 4 | v(s[2 * i + 1]));
+}
+
+inline void send_json(int fd, const Json& j) {
+  const std::string t = j.dump();
+  send_frame(fd, reinterpret_cast<const uint8_t*>(t.data()), (uint32_t)t.size());
+}
+inline Json recv_json(int fd) { return Json::parse(recv_frame(fd)); }
 
 // <root>/cake_amd/lib/libcake_engine.so -> <root>/cake_amd
 inline std::string pkg_dir() {

@@ -287,29 +287,6 @@ void trace(int rank, const std::string& what) {
   std::fflush(stderr);
 }
 
-std::string hex_of(const void* p, size_t n) {
-  static const char* d = "0123456789abcdef";
-  std::string s;
-  const uint8_t* b = static_cast<const uint8_t*>(p);
-  for (size_t i = 0; i < n; ++i) {
-    s.push_back(d[b[i] >> 4]);
-    s.push_back(d[b[i] & 15]);
-  }
-  return s;
-}
-
-void unhex(const std::string& s, void* out, size_t n) {
-  if (s.size() != 2 * n) throw Error("bad IPC handle");
-  auto v = [](char c) { return c <= '9' ? c - '0' : c - 'a' + 10; };
-  uint8_t* b = static_cast<uint8_t*>(out);
-  for (size_t i = 0; i < n; ++i) b[i] = (uint8_t)(v(s[2 * i]) << 4 | v(s[2 * i + 1]));
-}
-
-void send_json(int fd, const Json& j) {
-  const std::string t = j.dump();
-  send_frame(fd, reinterpret_cast<const uint8_t*>(t.data()), (uint32_t)t.size());
-}
-Json recv_json(int fd) { return Json::parse(recv_frame(fd)); }
 Json msg(const char* cmd) {
   Json j = Json::object();
   j.set("cmd", Json::string(cmd));

@@ -32,6 +32,7 @@
 #include <memory>
 #include <random>
 #include <string>
+#include <thread>
 #include <tuple>
 #include <vector>
 
@@ -84,6 +85,14 @@ int cake_to_rgb8(int dt, const void* img, int B, int H, int W, int nhwc, void* o
 int cake_clip_embed(int dt, const void* tok, const void* pos, const int* ids, int rows, int T,
                     int D, int V, void* out, hipStream_t st);
 int cake_widen16(int dt, const void* x, long long n, float* y, hipStream_t st);
+int cake_hop_alloc(size_t bytes, void** ptr);
+int cake_hop_free(void* ptr);
+int cake_bulk_send(const void* const* srcs, const unsigned long long* bytes,
+                   const unsigned long long* offs, int nseg, void* dst_rx,
+                   unsigned long long rx_bytes, unsigned int* seq, unsigned int* count,
+                   hipStream_t st);
+int cake_bulk_recv(const void* rx, unsigned long long bytes, void* dst, unsigned int* seq,
+                   int* err, double timeout_s, hipStream_t st);
 }
 
 namespace cake {
@@ -443,7 +452,8 @@ struct ClipW {
 // ---------------------------------------------------------------------------
 class SdEngine {
  public:
-  SdEngine(const std::string& dir, const CakeSdOpts& o) : dir_(dir) {
+  SdEngine(const std::string& dir, const CakeSdOpts& o, const CakeSdSplitOpts* sp = nullptr)
+      : dir_(dir) {
     dev_ = o.device;
     hip_check(hipSetDevice(dev_), "hipSetDevice");
     hip_check(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking), "hipStreamCreate");
@@ -474,6 +484,13 @@ class SdEngine {
     paths_[3] = o.clip2_path ? o.clip2_path : "";
     parts_ = o.parts ? o.parts : 15;
     if (!cfg_.xl) parts_ &= 7;
+    if (sp && sp->world > 1) {
+      srank_ = sp->rank;
+      sworld_ = sp->world;
+      if (srank_ < 0 || srank_ >= sworld_) throw Error("split UNet: bad rank");
+      if (srank_ > 0) parts_ = 1;  // the UNet runs only: text, scheduler and VAE on rank 0
+      else parts_ |= 1;
+    }
     {
       const char* ra[4] = {o.remote_unet, o.remote_vae, o.remote_clip, o.remote_clip2};
       remote_timeout_ = o.remote_timeout_s > 0 ? o.remote_timeout_s : 120.0;
@@ -493,11 +510,26 @@ class SdEngine {
     hip_check(hipMemset(gn_tickets_, 0, 256 * 4), "memset");
     build_and_load();
     alloc_state();
+    if (sworld_ > 1) connect_split(*sp);
   }
 
   ~SdEngine() {
     for (auto& r : remote_)
       if (r.fd >= 0) tcp_close(r.fd);
+    for (int fd : speers_) {
+      try {
+        Json m = Json::object();
+        m.set("cmd", Json::string("exit"));
+        send_json(fd, m);
+      } catch (const std::exception&) {
+      }
+      tcp_close(fd);
+    }
+    if (ctl_fd_ >= 0) tcp_close(ctl_fd_);
+    for (auto& c : chans_) {
+      if (c.inbox) (void)cake_hop_free(c.inbox);
+      if (c.peer) (void)hipIpcCloseMemHandle(c.peer);
+    }
     (void)hipSetDevice(dev_);
     (void)hipStreamSynchronize(st_);
     drop_graphs();
@@ -538,6 +570,12 @@ class SdEngine {
     }
     const int n = (int)s.ts.size();
     const int B2 = (guide ? 2 : 1) * bsize;  // UNet rows
+    if (sworld_ > 1 && srank_ != 0) throw Error("generate runs on split-UNet rank 0");
+    if (split_active() && B2 > rows_cap_)
+      throw Error("split UNet: bsize 1 (the device inboxes hold " + std::to_string(rows_cap_) +
+                  " UNet rows)");
+    if (split_active() && a.intermediary > 0)
+      throw Error("split UNet: intermediary images are decoded on the single-rank engine");
     ensure_rows(B2);
     const auto t0 = std::chrono::steady_clock::now();
     // ---- text context [B2, 77, ctx]: rows [uncond; cond] x bsize
@@ -572,6 +610,7 @@ class SdEngine {
     hip_check(hipMemcpyAsync(seed_dev_, &seed, 8, hipMemcpyHostToDevice, st_), "H2D");
     k_check(cake_scale_copy(dt_, x_, (long long)nl, (float)s.first_scale, guide ? 1 : 0, inp_, st_),
             "scale_copy");
+    if (split_active()) split_start(n, B2, ttab);  // the worker ranks' step loops
     // ---- denoise: step 0 eager, then one graph replay per step
     std::vector<hipEvent_t> ev(2 * n);
     for (auto& e : ev) hip_check(hipEventCreate(&e), "event");
@@ -604,6 +643,7 @@ class SdEngine {
         }
       }
       hip_check(hipStreamSynchronize(st_), "sync");
+      if (split_active()) split_finish();
     } catch (...) {
       (void)hipStreamSynchronize(st_);
       for (auto& e : ev) (void)hipEventDestroy(e);
@@ -1710,14 +1750,51 @@ class SdEngine {
       for (auto& t : u.att) run(t);
   }
 
-  // the UNet forward on inp [B, 4, h, w] (NCHW 16-bit): returns [B, 4, h, w] NCHW
-  const uint16_t* unet_forward(const uint16_t* inp, int B, const float* ttab, const int* tidx) {
+  // ---- the UNet as stages (the split UNet's units: parallel/sd_split.py stage_names):
+  // 0 .. nd-1 = down.i (down.0 also runs conv_in), nd = mid, nd+1 .. = up.i (the last one
+  // also norm_out + conv_out).  Skip tensors are numbered in push order; an up stage pops
+  // the highest live index first (the reference's LIFO skip stack), so every rank can
+  // hold just the skips it produces or receives.
+  int n_stages() const { return (int)down_.size() + 1 + (int)up_.size(); }
+  int stage_pushes(int k) const {
+    const int nd = (int)down_.size();
+    if (k >= nd) return 0;
+    return (k == 0 ? 1 : 0) + (int)down_[k].res.size() + (down_[k].has_ds ? 1 : 0);
+  }
+  int stage_pops(int k) const {
+    const int nd = (int)down_.size();
+    return k > nd ? (int)up_[k - nd - 1].res.size() : 0;
+  }
+  // live skips before stage k (the stack height)
+  int stack_before(int k) const {
+    int t = 0;
+    for (int i = 0; i < k; ++i) t += stage_pushes(i) - stage_pops(i);
+    return t;
+  }
+  int total_skips() const {
+    int t = 0;
+    for (int i = 0; i < n_stages(); ++i) t += stage_pushes(i);
+    return t;
+  }
+  std::string stage_name(int k) const {
+    const int nd = (int)down_.size();
+    if (k < nd) return "down." + std::to_string(k);
+    if (k == nd) return "mid";
+    return "up." + std::to_string(k - nd - 1);
+  }
+
+  struct UnetRun {  // per-forward context of the stages
+    float* tb;
+    int tb_ld;  // the row stride of tb (0: one shared row)
+  };
+
+  // time biases: sinusoidal embedding -> linear_1 (+SiLU) -> linear_2 (+SiLU) -> every
+  // resnet's projection as one GEMM (f32)
+  UnetRun unet_begin(int B, const float* ttab, const int* tidx) {
     Arena& A = unet_a_;
     const UCfg& u = cfg_.unet;
     B_ = B;
     const int C0 = u.blocks[0].ch;
-    // time biases: sinusoidal embedding -> linear_1 (+SiLU) -> linear_2 (+SiLU) -> every
-    // resnet's projection as one GEMM (f32)
     uint16_t* emb = new16(A, (size_t)B * C0);
     k_check(cake_timestep_embed(dt_, ttab, tidx, B, C0, u.flip ? 1 : 0, (float)u.shift, 1, emb, st_),
             "timestep_embed");
@@ -1727,56 +1804,452 @@ class SdEngine {
     gemm(kSilu, e1, temb_dim_, B, temb_dim_, t2w_, temb_dim_, t2b_, e2, temb_dim_);
     float* tb = new32(A, (size_t)B * temb_cols_);
     gemm(kStore32, e2, temb_dim_, B, temb_dim_, tall_w_, temb_cols_, tall_b_, tb, temb_cols_);
-    const int tb_ld = B > 1 ? temb_cols_ : 0;
-    auto tbias = [&](const ResnetW& r) { return tb + r.toff; };
-    auto tld = [&](const ResnetW& r) { return B > 1 ? tb_ld : r.cout; };
-    const int h = cfg_.height / 8, w = cfg_.width / 8;
+    return {tb, B > 1 ? temb_cols_ : 0};
+  }
+
+  // stage k: x in / out, pushes into / pops from sk at the stack height `top`; stage 0
+  // reads the NCHW input `inp`, the last stage leaves the NCHW prediction in x.p
+  void unet_stage(int k, const UnetRun& R, const uint16_t* inp, Fm& x, std::vector<Fm>& sk,
+                  int& top) {
+    Arena& A = unet_a_;
+    const UCfg& u = cfg_.unet;
     const int G = u.groups;
     const float eps = (float)u.eps;
-    // down.0: conv_in reads the NCHW input
-    Fm x{conv(A, conv_in_, inp, B, h, w, 1, 1, false, nullptr, 0, nullptr, true, false), h, w, C0};
-    std::vector<Fm> skips{x};
-    for (size_t i = 0; i < down_.size(); ++i) {
-      const DownW& d = down_[i];
+    auto tbias = [&](const ResnetW& r) { return R.tb + r.toff; };
+    auto tld = [&](const ResnetW& r) { return B_ > 1 ? R.tb_ld : r.cout; };
+    const int nd = (int)down_.size();
+    if (k < nd) {
+      if (k == 0) {  // down.0: conv_in reads the NCHW input
+        const int h = cfg_.height / 8, w = cfg_.width / 8;
+        x = Fm{conv(A, conv_in_, inp, B_, h, w, 1, 1, false, nullptr, 0, nullptr, true, false), h,
+               w, u.blocks[0].ch};
+        sk[top++] = x;
+      }
+      const DownW& d = down_[k];
       for (size_t j = 0; j < d.res.size(); ++j) {
         x = resnet(d.res[j], x, tbias(d.res[j]), tld(d.res[j]), nullptr, G, eps);
         if (!d.att.empty()) x = transformer(d.att[j], x);
-        skips.push_back(x);
+        sk[top++] = x;
       }
       if (d.has_ds) {
         int oh, ow;
-        uint16_t* y = conv(A, d.ds, x.p, B, x.H, x.W, 2, 1, false, nullptr, 0, nullptr, false,
+        uint16_t* y = conv(A, d.ds, x.p, B_, x.H, x.W, 2, 1, false, nullptr, 0, nullptr, false,
                            false, &oh, &ow);
         x = {y, oh, ow, d.ds.OC};
-        skips.push_back(x);
+        sk[top++] = x;
       }
+      return;
     }
-    x = resnet(mid_res_[0], x, tbias(mid_res_[0]), tld(mid_res_[0]), nullptr, G, eps);
-    x = transformer(mid_att_, x);
-    x = resnet(mid_res_[1], x, tbias(mid_res_[1]), tld(mid_res_[1]), nullptr, G, eps);
-    for (size_t i = 0; i < up_.size(); ++i) {
-      const UpW& up = up_[i];
-      for (size_t j = 0; j < up.res.size(); ++j) {
-        const Fm s = skips.back();
-        skips.pop_back();
-        x = resnet(up.res[j], x, tbias(up.res[j]), tld(up.res[j]), &s, G, eps);
-        if (!up.att.empty()) x = transformer(up.att[j], x);
-      }
-      if (up.has_us) {
-        int oh, ow;
-        uint16_t* y = conv(A, up.us, x.p, B, x.H, x.W, 1, 1, true, nullptr, 0, nullptr, false,
-                           false, &oh, &ow);
-        x = {y, oh, ow, up.us.OC};
-      }
+    if (k == nd) {
+      x = resnet(mid_res_[0], x, tbias(mid_res_[0]), tld(mid_res_[0]), nullptr, G, eps);
+      x = transformer(mid_att_, x);
+      x = resnet(mid_res_[1], x, tbias(mid_res_[1]), tld(mid_res_[1]), nullptr, G, eps);
+      return;
     }
-    uint16_t* hN = group_norm(A, x.p, nullptr, x.C, B, x.H * x.W, x.C, norm_out_w_, norm_out_b_,
-                              G, eps, true);
-    return conv(A, conv_out_, hN, B, x.H, x.W, 1, 1, false, nullptr, 0, nullptr, false, true);
+    const UpW& up = up_[k - nd - 1];
+    for (size_t j = 0; j < up.res.size(); ++j) {
+      const Fm s = sk[--top];
+      x = resnet(up.res[j], x, tbias(up.res[j]), tld(up.res[j]), &s, G, eps);
+      if (!up.att.empty()) x = transformer(up.att[j], x);
+    }
+    if (up.has_us) {
+      int oh, ow;
+      uint16_t* y = conv(A, up.us, x.p, B_, x.H, x.W, 1, 1, true, nullptr, 0, nullptr, false,
+                         false, &oh, &ow);
+      x = {y, oh, ow, up.us.OC};
+    }
+    if (k + 1 == n_stages()) {
+      uint16_t* hN = group_norm(A, x.p, nullptr, x.C, B_, x.H * x.W, x.C, norm_out_w_,
+                                norm_out_b_, G, eps, true);
+      x.p = conv(A, conv_out_, hN, B_, x.H, x.W, 1, 1, false, nullptr, 0, nullptr, false, true);
+      x.C = 4;
+    }
   }
 
+  // the UNet forward on inp [B, 4, h, w] (NCHW 16-bit): returns [B, 4, h, w] NCHW
+  const uint16_t* unet_forward(const uint16_t* inp, int B, const float* ttab, const int* tidx) {
+    const UnetRun R = unet_begin(B, ttab, tidx);
+    std::vector<Fm> sk(total_skips());
+    int top = 0;
+    Fm x{nullptr, 0, 0, 0};
+    for (int k = 0; k < n_stages(); ++k) unet_stage(k, R, inp, x, sk, top);
+    return x.p;
+  }
+
+  // ------------------------------------------------------------------ split UNet
+  // (sd_engine.h CakeSdSplitOpts).  Shapes of every stage output and skip tensor from the
+  // weights' channel counts, the producer / consumer stage of every skip, the runs of
+  // the ranks and the channels between them — the same on every rank.
+  struct Shp { int H, W, C; };
+  struct Chan {
+    int src = 0, dst = 0;
+    int x_after = -1;          // carries the feature map after this stage (-1: none)
+    std::vector<int> skips;    // skip indices, ascending
+    size_t cap = 0;            // inbox bytes (dst == this rank)
+    void* inbox = nullptr;     // dst == this rank: its uncached inbox
+    void* peer = nullptr;      // src == this rank: the receiver's inbox, IPC-mapped
+    unsigned* ctr = nullptr;   // device: send seq, send count, recv seq
+  };
+  size_t fm_bytes(const Shp& x, int B) const { return ((size_t)B * x.H * x.W * x.C * 2 + 15) / 16 * 16; }
+
+  void split_plan(const CakeSdSplitOpts& sp) {
+    const int n = n_stages(), nd = (int)down_.size();
+    // shapes (conv stride 2 pad 1: ceil(H / 2); the up blocks' nearest-2x conv: 2H)
+    int H = cfg_.height / 8, W = cfg_.width / 8, C = conv_in_.OC;
+    x_shp_.assign(n, Shp{0, 0, 0});
+    skip_shp_.clear();
+    skip_prod_.clear();
+    skip_cons_.assign(total_skips(), -1);
+    int top = 0;
+    std::vector<int> stack;
+    for (int k = 0; k < n; ++k) {
+      auto push = [&](Shp x) {
+        skip_shp_.push_back(x);
+        skip_prod_.push_back(k);
+        stack.push_back((int)skip_shp_.size() - 1);
+        ++top;
+      };
+      if (k < nd) {
+        if (k == 0) push({H, W, C});
+        const DownW& d = down_[k];
+        for (const auto& r : d.res) {
+          C = r.cout;
+          push({H, W, C});
+        }
+        if (d.has_ds) {
+          H = (H - 1) / 2 + 1;
+          W = (W - 1) / 2 + 1;
+          C = d.ds.OC;
+          push({H, W, C});
+        }
+      } else if (k == nd) {
+        C = mid_res_[1].cout;
+      } else {
+        const UpW& u = up_[k - nd - 1];
+        for (const auto& r : u.res) {
+          skip_cons_[stack.back()] = k;
+          stack.pop_back();
+          --top;
+          C = r.cout;
+        }
+        if (u.has_us) {
+          H *= 2;
+          W *= 2;
+          C = u.us.OC;
+        }
+        if (k + 1 == n) C = 4;  // conv_out: the NCHW prediction
+      }
+      x_shp_[k] = {H, W, C};
+    }
+    // owners: contiguous runs, rank 0 first
+    sused_ = std::min(sworld_, n);
+    sowner_.assign(n, 0);
+    if (sp.owners && sp.n_owners > 0) {
+      if (sp.n_owners != n) throw Error("split UNet: owners must name every one of the " +
+                                        std::to_string(n) + " stages");
+      for (int k = 0; k < n; ++k) sowner_[k] = sp.owners[k];
+      int used = 0;
+      for (int k = 0; k < n; ++k) {
+        if (sowner_[k] < 0 || sowner_[k] >= sworld_) throw Error("split UNet: owner out of range");
+        const int want = k == 0 ? 0 : (sowner_[k] == sowner_[k - 1] ? sowner_[k - 1] : sowner_[k - 1] + 1);
+        if (sowner_[k] != want) throw Error("split UNet: owners must be contiguous runs 0, 1, ...");
+        used = sowner_[k] + 1;
+      }
+      sused_ = used;
+    } else {
+      for (int k = 0; k < n; ++k) sowner_[k] = (int)((long long)k * sused_ / n);
+    }
+    s_first_ = n;
+    s_end_ = n;
+    for (int k = 0; k < n; ++k)
+      if (sowner_[k] == srank_) {
+        s_first_ = std::min(s_first_, k);
+        s_end_ = k + 1;
+      }
+    if (s_first_ >= s_end_) s_first_ = s_end_ = 0;
+    // channels: the feature map run -> next run (and the prediction back to rank 0), every
+    // skip producer -> consumer across ranks
+    chans_.clear();
+    auto chan = [&](int src, int dst) -> Chan& {
+      for (auto& c : chans_)
+        if (c.src == src && c.dst == dst) return c;
+      chans_.push_back(Chan{});
+      chans_.back().src = src;
+      chans_.back().dst = dst;
+      return chans_.back();
+    };
+    for (int k = 1; k < n; ++k)
+      if (sowner_[k] != sowner_[k - 1]) chan(sowner_[k - 1], sowner_[k]).x_after = k - 1;
+    if (sowner_[n - 1] != 0) chan(sowner_[n - 1], 0).x_after = n - 1;
+    for (size_t i = 0; i < skip_shp_.size(); ++i) {
+      const int src = sowner_[skip_prod_[i]], dst = sowner_[skip_cons_[i]];
+      if (src != dst) chan(src, dst).skips.push_back((int)i);
+    }
+    std::sort(chans_.begin(), chans_.end(), [](const Chan& a, const Chan& b) {
+      return a.src != b.src ? a.src < b.src : a.dst < b.dst;
+    });
+  }
+
+  // segment byte sizes of a channel's message at B rows: [feature map] + skips
+  std::vector<size_t> chan_segs(const Chan& c, int B) const {
+    std::vector<size_t> v;
+    if (c.x_after >= 0) v.push_back(fm_bytes(x_shp_[c.x_after], B));
+    for (int i : c.skips) v.push_back(fm_bytes(skip_shp_[i], B));
+    return v;
+  }
+  size_t chan_bytes(const Chan& c, int B) const {
+    size_t t = 0;
+    for (size_t b : chan_segs(c, B)) t += b;
+    return t;
+  }
+
+  // inboxes (uncached device memory, hop.hip bulk messages) for the channels into this
+  // rank, exchanged as IPC handles through rank 0; then every channel's sender maps its
+  // receiver's inbox
+  void connect_split(const CakeSdSplitOpts& sp) {
+    split_plan(sp);
+    stimeout_ = sp.timeout_s > 0 ? sp.timeout_s : 60.0;
+    std::string host;
+    int port = 0;
+    split_host_port(sp.master_addr ? sp.master_addr : "127.0.0.1:29533", &host, &port);
+    serr_ = static_cast<int*>(dalloc(64));
+    hip_check(hipMemset(serr_, 0, 64), "memset");
+    Json me = Json::object();
+    me.set("rank", Json::integer(srank_));
+    Json boxes = Json::array();
+    for (size_t i = 0; i < chans_.size(); ++i) {
+      Chan& c = chans_[i];
+      c.ctr = static_cast<unsigned*>(dalloc(64));  // send seq, send count, recv seq
+      hip_check(hipMemset(c.ctr, 0, 64), "memset");
+      if (c.dst != srank_) continue;
+      c.cap = chan_bytes(c, rows_cap_);
+      k_check(cake_hop_alloc(c.cap + 256, &c.inbox), "hop_alloc");
+      hip_check(hipMemset(c.inbox, 0, c.cap + 256), "memset inbox");
+      hipIpcMemHandle_t h;
+      hip_check(hipIpcGetMemHandle(&h, c.inbox), "IpcGetMemHandle");
+      Json e = Json::array();
+      e.push(Json::integer((int64_t)i));
+      e.push(Json::string(hex_of(&h, sizeof(h))));
+      boxes.push(e);
+    }
+    me.set("inboxes", boxes);
+    std::vector<Json> table(sworld_);
+    if (srank_ == 0) {
+      const int lfd = tcp_listen(host, port);
+      table[0] = me;
+      speers_.assign(sworld_ - 1, -1);
+      try {
+        for (int i = 1; i < sworld_; ++i) {
+          std::string peer;
+          const int fd = tcp_accept(lfd, &peer);
+          tcp_set_timeout(fd, 0);
+          const Json j = recv_json(fd);
+          const int r = (int)j.get("rank").as_int();
+          if (r < 1 || r >= sworld_ || speers_[r - 1] >= 0) throw Error("split UNet: bad rank hello");
+          speers_[r - 1] = fd;
+          table[r] = j;
+        }
+      } catch (...) {
+        tcp_close(lfd);
+        throw;
+      }
+      tcp_close(lfd);
+      Json all = Json::array();
+      for (const auto& t : table) all.push(t);
+      Json m = Json::object();
+      m.set("table", all);
+      for (int fd : speers_) send_json(fd, m);
+    } else {
+      const double ct = sp.connect_timeout_s > 0 ? sp.connect_timeout_s : 600.0;
+      const auto deadline = std::chrono::steady_clock::now() + std::chrono::duration<double>(ct);
+      for (;;) {
+        try {
+          ctl_fd_ = tcp_connect(host, port, 2.0);
+          break;
+        } catch (const std::exception&) {
+          if (std::chrono::steady_clock::now() > deadline) throw;
+          std::this_thread::sleep_for(std::chrono::milliseconds(200));
+        }
+      }
+      tcp_set_timeout(ctl_fd_, 0);
+      send_json(ctl_fd_, me);
+      const Json m = recv_json(ctl_fd_);
+      for (int r = 0; r < sworld_; ++r) table[r] = m.get("table").at(r);
+    }
+    for (size_t i = 0; i < chans_.size(); ++i) {
+      Chan& c = chans_[i];
+      if (c.src != srank_) continue;
+      bool found = false;
+      for (const auto& x : table[c.dst].get("inboxes").items()) {
+        if ((size_t)x.at(0).as_int() != i) continue;
+        hipIpcMemHandle_t h;
+        unhex(x.at(1).as_string(), &h, sizeof(h));
+        hip_check(hipIpcOpenMemHandle(&c.peer, h, hipIpcMemLazyEnablePeerAccess), "IpcOpen inbox");
+        found = true;
+      }
+      if (!found) throw Error("split UNet: rank " + std::to_string(c.dst) + " published no inbox");
+    }
+  }
+
+  // this rank's part of one denoise step of the split UNet on B rows: receive, its stages,
+  // send; rank 0 (stage 0 reads inp) then receives the prediction and returns it
+  const uint16_t* split_unet(int B, const uint16_t* inp) {
+    const UnetRun R = unet_begin(B, ttab_, step_);
+    std::vector<Fm> sk(total_skips());
+    Fm x{nullptr, 0, 0, 0};
+    auto recv = [&](const Chan& c) {
+      const std::vector<size_t> segs = chan_segs(c, B);
+      const size_t bytes = chan_bytes(c, B);
+      uint8_t* buf = static_cast<uint8_t*>(unet_a_.alloc(bytes));
+      k_check(cake_bulk_recv(c.inbox, bytes, buf, c.ctr + 2, serr_, stimeout_, st_), "bulk_recv");
+      size_t o = 0, si = 0;
+      if (c.x_after >= 0) {
+        const Shp& xs = x_shp_[c.x_after];
+        x = Fm{reinterpret_cast<uint16_t*>(buf), xs.H, xs.W, xs.C};
+        o += segs[si++];
+      }
+      for (int i : c.skips) {
+        const Shp& q = skip_shp_[i];
+        sk[i] = Fm{reinterpret_cast<uint16_t*>(buf + o), q.H, q.W, q.C};
+        o += segs[si++];
+      }
+    };
+    const bool pred_chan_rank0 = srank_ == 0;
+    for (const auto& c : chans_)
+      if (c.dst == srank_ && !(pred_chan_rank0 && c.x_after == n_stages() - 1)) recv(c);
+    int top = stack_before(s_first_);
+    for (int k = s_first_; k < s_end_; ++k) unet_stage(k, R, inp, x, sk, top);
+    for (const auto& c : chans_) {
+      if (c.src != srank_) continue;
+      const std::vector<size_t> segs = chan_segs(c, B);
+      std::vector<const void*> src;
+      std::vector<unsigned long long> nb, off;
+      size_t o = 0, si = 0;
+      auto add = [&](const void* p) {
+        src.push_back(p);
+        nb.push_back(segs[si]);
+        off.push_back(o);
+        o += segs[si++];
+      };
+      if (c.x_after >= 0) add(x.p);
+      for (int i : c.skips) add(sk[i].p);
+      k_check(cake_bulk_send(src.data(), nb.data(), off.data(), (int)src.size(), c.peer, o, c.ctr,
+                             c.ctr + 1, st_), "bulk_send");
+    }
+    if (srank_ != 0) return nullptr;
+    for (const auto& c : chans_)
+      if (c.dst == 0 && c.x_after == n_stages() - 1) recv(c);
+    return x.p;
+  }
+
+  // one step of a worker rank (graph-captured after the first): its stages, step += 1
+  void split_worker_step(int B) {
+    unet_a_.reset();
+    split_unet(B, nullptr);
+    k_check(cake_step_advance(step_, st_), "step_advance");
+  }
+
+  bool split_active() const { return sworld_ > 1 && sused_ > 1; }
+
+  // rank 0, at the start of a generation's denoise loop: each used worker rank gets the
+  // step count, the UNet rows, the timestep table and the text context
+  void split_start(int n_steps, int B2, const std::vector<float>& ttab) {
+    const size_t ctx_bytes = (size_t)B2 * kTok * cfg_.ctx_dim() * 2;
+    std::vector<uint8_t> ctx(ctx_bytes);
+    hip_check(hipMemcpyAsync(ctx.data(), ctx_, ctx_bytes, hipMemcpyDeviceToHost, st_), "D2H ctx");
+    hip_check(hipStreamSynchronize(st_), "sync");
+    Json m = Json::object();
+    m.set("cmd", Json::string("gen"));
+    m.set("n", Json::integer(n_steps));
+    m.set("B", Json::integer(B2));
+    Json tt = Json::array();
+    for (float t : ttab) tt.push(Json::number(t));
+    m.set("ttab", tt);
+    for (int r = 1; r < sused_; ++r) {
+      send_json(speers_[r - 1], m);
+      send_frame(speers_[r - 1], ctx.data(), (uint32_t)ctx.size());
+    }
+  }
+
+  // rank 0, after its denoise loop: every used worker's verdict
+  void split_finish() {
+    std::string bad;
+    for (int r = 1; r < sused_; ++r) {
+      const Json a = recv_json(speers_[r - 1]);
+      if (bad.empty() && a.has("error")) bad = "split UNet rank " + std::to_string(r) + ": " +
+                                                a.get("error").as_string();
+    }
+    int e = 0;
+    hip_check(hipMemcpy(&e, serr_, sizeof(int), hipMemcpyDeviceToHost), "D2H err");
+    if (e) {
+      hip_check(hipMemset(serr_, 0, sizeof(int)), "memset");
+      if (bad.empty()) bad = "split UNet: a hop into rank 0 timed out";
+    }
+    if (!bad.empty()) throw Error(bad);
+  }
+
+ public:
+  // ranks > 0: serve rank 0's generations (gen: the steps of one image) until it exits
+  void serve() {
+    hip_check(hipSetDevice(dev_), "hipSetDevice");
+    if (sworld_ < 2 || srank_ == 0) throw Error("serve() runs on split-UNet ranks > 0");
+    for (;;) {
+      const Json m = recv_json(ctl_fd_);
+      const std::string cmd = m.get("cmd").as_string();
+      if (cmd == "exit") return;
+      if (cmd != "gen") throw Error("split UNet: unknown control message " + cmd);
+      const int n = (int)m.get("n").as_int(), B = (int)m.get("B").as_int();
+      const std::string ctx = recv_frame(ctl_fd_);
+      Json ack = Json::object();
+      try {
+        if (B < 1 || B > rows_cap_) throw Error("split UNet: " + std::to_string(B) +
+                                               " UNet rows (the inboxes hold " +
+                                               std::to_string(rows_cap_) + ")");
+        if (ctx.size() != (size_t)B * kTok * cfg_.ctx_dim() * 2) throw Error("split UNet: context size");
+        std::vector<float> tt;
+        for (const auto& v : m.get("ttab").items()) tt.push_back((float)v.as_double());
+        ensure_tables((int)tt.size() + 1);
+        hip_check(hipMemcpyAsync(ttab_, tt.data(), tt.size() * 4, hipMemcpyHostToDevice, st_), "H2D");
+        hip_check(hipMemcpyAsync(ctx_, ctx.data(), ctx.size(), hipMemcpyHostToDevice, st_), "H2D");
+        hip_check(hipMemsetAsync(step_, 0, 4, st_), "memset");
+        precompute_kv(B);
+        for (int i = 0; i < n; ++i) {
+          if (i == 0) {
+            split_worker_step(B);
+          } else {
+            auto it = wgraphs_.find(B);
+            if (it == wgraphs_.end()) it = wgraphs_.emplace(B, capture_worker(B)).first;
+            hip_check(hipGraphLaunch(it->second.exec, st_), "hipGraphLaunch");
+          }
+        }
+        hip_check(hipStreamSynchronize(st_), "sync");
+        int e = 0;
+        hip_check(hipMemcpy(&e, serr_, sizeof(int), hipMemcpyDeviceToHost), "D2H err");
+        if (e) {
+          hip_check(hipMemset(serr_, 0, sizeof(int)), "memset");
+          throw Error("a hop into this rank timed out");
+        }
+      } catch (const std::exception& x) {
+        (void)hipStreamSynchronize(st_);
+        ack.set("error", Json::string(x.what()));
+      }
+      send_json(ctl_fd_, ack);
+    }
+  }
+
+  void split_info(int32_t* o) const {
+    o[0] = srank_;
+    o[1] = sworld_;
+    o[2] = n_stages();
+    o[3] = sused_;
+    o[4] = s_first_;
+    o[5] = s_end_;
+  }
+
+ private:
   void step_body(int B2, bool guide, float guidance) {
     unet_a_.reset();
-    const uint16_t* pred = unet_forward(inp_, B2, ttab_, step_);
+    const uint16_t* pred = split_active() ? split_unet(B2, inp_) : unet_forward(inp_, B2, ttab_, step_);
     const int h = cfg_.height / 8, w = cfg_.width / 8;
     const long long nl = (long long)4 * h * w * (guide ? B2 / 2 : B2);
     k_check(cake_sched_step(dt_, x_, pred, nl, guide ? 1 : 0, guidance, coef_, step_, seed_dev_,
@@ -1809,6 +2282,25 @@ class SdEngine {
     return gr;
   }
 
+  Graph capture_worker(int B) {
+    Graph gr;
+    unet_a_.frozen = true;
+    hip_check(hipStreamBeginCapture(st_, hipStreamCaptureModeThreadLocal), "BeginCapture");
+    try {
+      split_worker_step(B);
+    } catch (...) {
+      hipGraph_t junk = nullptr;
+      (void)hipStreamEndCapture(st_, &junk);
+      if (junk) (void)hipGraphDestroy(junk);
+      unet_a_.frozen = false;
+      throw;
+    }
+    hip_check(hipStreamEndCapture(st_, &gr.g), "EndCapture");
+    unet_a_.frozen = false;
+    hip_check(hipGraphInstantiate(&gr.exec, gr.g, nullptr, nullptr, 0), "GraphInstantiate");
+    return gr;
+  }
+
   struct HookGraph {
     hipGraph_t g = nullptr;
     hipGraphExec_t exec = nullptr;
@@ -1828,6 +2320,11 @@ class SdEngine {
       if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
       if (kv.second.g) (void)hipGraphDestroy(kv.second.g);
     }
+    for (auto& kv : wgraphs_) {
+      if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
+      if (kv.second.g) (void)hipGraphDestroy(kv.second.g);
+    }
+    wgraphs_.clear();
     graphs_.clear();
   }
 
@@ -2029,6 +2526,16 @@ class SdEngine {
   float* ttab_ = nullptr;
   float* coef_ = nullptr;
   int table_cap_ = 0;
+  // split UNet (connect_split): this rank, its stages, the channels
+  int srank_ = 0, sworld_ = 1, sused_ = 1, s_first_ = 0, s_end_ = 0;
+  double stimeout_ = 60.0;
+  int ctl_fd_ = -1;
+  std::vector<int> speers_;
+  std::vector<int> sowner_, skip_prod_, skip_cons_;
+  std::vector<Shp> x_shp_, skip_shp_;
+  std::vector<Chan> chans_;
+  int* serr_ = nullptr;
+  std::map<int, Graph> wgraphs_;  // worker step graphs by UNet rows
 };
 
 void set_err(char* err, int32_t n, const std::string& m) {
@@ -2050,6 +2557,35 @@ CAKE_API void* cake_sd_open(const char* model_dir, const CakeSdOpts* o, char* er
     cake::set_err(err, n, e.what());
     return nullptr;
   }
+}
+
+CAKE_API void* cake_sd_open_split(const char* model_dir, const CakeSdOpts* o,
+                                  const CakeSdSplitOpts* sp, char* err, int32_t n) {
+  try {
+    if (!sp) throw cake::Error("cake_sd_open_split: null split options");
+    CakeSdOpts d{};
+    d.dtype = 1;
+    d.autotune = 1;
+    return new SdEngine(model_dir ? model_dir : ".", o ? *o : d, sp);
+  } catch (const std::exception& e) {
+    cake::set_err(err, n, e.what());
+    return nullptr;
+  }
+}
+
+CAKE_API int32_t cake_sd_serve(void* eng, char* err, int32_t n) {
+  try {
+    if (!eng) throw cake::Error("cake_sd_serve: null engine");
+    static_cast<SdEngine*>(eng)->serve();
+    return 0;
+  } catch (const std::exception& e) {
+    cake::set_err(err, n, e.what());
+    return 1;
+  }
+}
+
+CAKE_API void cake_sd_split_info(void* eng, int32_t* out6) {
+  if (eng && out6) static_cast<SdEngine*>(eng)->split_info(out6);
 }
 
 CAKE_API int32_t cake_sd_generate(void* eng, const CakeSdGenArgs* a, uint8_t* rgb, float* lat,

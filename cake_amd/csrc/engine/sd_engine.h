@@ -87,6 +87,31 @@ typedef struct CakeSdResult {
 
 // Open (load or random-init) every component; null + err on failure.
 void* cake_sd_open(const char* model_dir, const CakeSdOpts* opts, char* err, int32_t errlen);
+
+// Split UNet over one process per GPU (BASELINE config 5; the reference reaches a remote
+// UNet once per step: cake-core/src/models/sd/sd.rs:464-513, unet.rs:81-100).  The UNet's
+// stages (down.i, mid, up.i) run in contiguous runs over ranks 0 .. used-1 (rank 0 first;
+// `owners`, if given, names the rank of every stage and must be such runs).  Each denoise
+// step is one graph replay per rank: bulk device hops (hop.hip, IPC-mapped uncached inboxes)
+// carry the feature map to the next run's rank, every skip tensor once from the rank that
+// pushes it straight to the rank whose up stage pops it, and the prediction back to rank
+// 0, which runs the text encoders, the scheduler and the VAE.  Control plane (IPC
+// handles, the generation's timesteps and text context) over TCP to rank 0 at
+// master_addr.  Rank 0 generates with cake_sd_generate; the others call cake_sd_serve.
+typedef struct CakeSdSplitOpts {
+  int32_t rank, world;
+  const char* master_addr;   // "host:port" rank 0 listens on
+  double timeout_s;          // a hop wait bound (the error word instead of a hang)
+  double connect_timeout_s;  // ranks > 0: how long to retry reaching rank 0
+  const int32_t* owners;     // [n_owners == the UNet's stage count] or null (even split)
+  int32_t n_owners;
+} CakeSdSplitOpts;
+void* cake_sd_open_split(const char* model_dir, const CakeSdOpts* opts,
+                         const CakeSdSplitOpts* split, char* err, int32_t errlen);
+// ranks > 0: serve rank 0's generations until it closes the group
+int32_t cake_sd_serve(void* engine, char* err, int32_t errlen);
+// (rank, world, stages, ranks used, first stage of this rank, end stage) of an engine
+void cake_sd_split_info(void* engine, int32_t* out6);
 // One sample of bsize images: rgb [bsize * height * width * 3] u8; latents_out (optional)
 // [bsize * 4 * h/8 * w/8] f32 (the final latents); step_s (optional) [n_steps] seconds per
 // step (device time).

@@ -179,24 +179,24 @@ CAKE_API int cake_attn_set_min_keys(int min_keys) {
 }
 
 // Core 2's split 0 spins on the partials of the other splits of its head, so every
-// workgroup of the grid must be resident at once; a grid larger than the device can hold
-// (several waves per CU taken by other work would not be visible here, but a grid the
-// empty device cannot hold is refused) runs core 1's last-arriver merge instead.
-// The occupancy query is made once per kernel (a small table keyed by the kernel's
-// address: eager launches of the non-graph paths no longer pay a runtime call per layer),
-// and a fallback to core 1 is reported once.
+// workgroup of the grid must be resident at once.  A grid larger than the empty device can
+// hold (70B: 8 KV heads x 64 splits = 512 workgroups at one per CU) is launched with fewer
+// splits — the device-side split policy reads its cap from the launch (maxsplit), so each
+// split covers more keys and the merge stays exact — and only a device that cannot hold
+// even one split per KV head runs core 1's last-arriver merge.  The occupancy query is
+// made once per kernel (a small table keyed by the kernel's address) and a trimmed grid is
+// reported once.
 template <class K>
-static bool grid_resident(K kern, int threads, long long blocks) {
+static long long resident_blocks(K kern, int threads) {
   static std::mutex mu;
   static int cus = 0;
   static std::vector<std::pair<const void*, int>> per_cu_of;
-  static bool warned = false;
   std::lock_guard<std::mutex> g(mu);
   if (cus == 0) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      return false;
+      return 0;
   }
   int per_cu = -1;
   for (const auto& e : per_cu_of)
@@ -204,26 +204,39 @@ static bool grid_resident(K kern, int threads, long long blocks) {
   if (per_cu < 0) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, threads, 0) !=
         hipSuccess)
-      return false;
+      return 0;
     per_cu_of.push_back({(const void*)kern, per_cu});
   }
-  const bool ok = (long long)per_cu * cus >= blocks;
-  if (!ok && !warned) {
+  return (long long)per_cu * cus;
+}
+
+// the splits of a core-2 grid of `heads` x `splits` workgroups that fit the device at once
+// (0: not even one per head)
+template <class K>
+static int resident_splits(K kern, int threads, int heads, int splits) {
+  static bool warned = false;
+  const long long cap = resident_blocks(kern, threads);
+  if (cap < heads) return 0;
+  if ((long long)heads * splits <= cap) return splits;
+  const int fit = (int)(cap / heads);
+  if (!warned) {
     warned = true;
-    std::fprintf(stderr, "[cake] decode attention: a %lld-workgroup grid exceeds residency "
-                 "(%d per CU x %d CUs): core 1 merge for such grids\n", blocks, per_cu, cus);
+    std::fprintf(stderr, "[cake] decode attention: %d x %d workgroups exceed residency (%lld); "
+                 "core 2 with %d splits per KV head\n", heads, splits, cap, fit);
   }
-  return ok;
+  return fit;
 }
 
 template <int DT, int HD>
 static int launch_decode(int n_rep, dim3 grid, hipStream_t st, const AttnDecArgs& a) {
 #define CAKE_DEC2(NR, PF)                                                                     \
-  if (grid_resident(attn2_decode_kernel<DT, HD, NR, PF>, AttnGeom2<NR>::NT,                   \
-                    (long long)grid.x * grid.y))                                              \
-    hipLaunchKernelGGL((attn2_decode_kernel<DT, HD, NR, PF>), grid, dim3(AttnGeom2<NR>::NT), 0, \
-                       st, a);                                                                \
-  else                                                                                        \
+  if (const int fit = resident_splits(attn2_decode_kernel<DT, HD, NR, PF>, AttnGeom2<NR>::NT,  \
+                                      (int)grid.x, (int)grid.y)) {                            \
+    AttnDecArgs a2 = a;                                                                       \
+    a2.maxsplit = fit;                                                                        \
+    hipLaunchKernelGGL((attn2_decode_kernel<DT, HD, NR, PF>), dim3(grid.x, fit),              \
+                       dim3(AttnGeom2<NR>::NT), 0, st, a2);                                   \
+  } else                                                                                      \
     hipLaunchKernelGGL((attn_decode_kernel<DT, HD, NR>), grid, dim3(AttnGeom<NR>::NT), 0, st, a)
 #define CAKE_DEC(NR)                                                                          \
   if (g_attn_impl == 2 && (g_attn_prefetch == 2 || (g_attn_prefetch == 0 && grid.y > 8)))    \

@@ -50,6 +50,19 @@ CAKE_GEMM_EXTERN_ALL(kF16)
 }  // namespace cake
 
 using namespace cake;
+
+// split-K pair tickets of gemm_4w (zero at load; every pair leaves its tile's zero)
+__device__ unsigned g_pair_tick[2 * kPairTiles];
+
+static unsigned* pair_ticks() {
+  static unsigned* p = nullptr;
+  if (!p) {
+    void* a = nullptr;
+    if (hipGetSymbolAddress(&a, HIP_SYMBOL(g_pair_tick)) == hipSuccess) p = static_cast<unsigned*>(a);
+  }
+  return p;
+}
+
 static inline void cfg_dims(int cfg, int& bm, int& bn) {
   if (cfg == kPPCfg || cfg == kRSCfg || cfg == k4WCfg) { bm = bn = 256; return; }
 #define X(id, BM, BN, WM, WN, NS, PR) if (cfg == id) { bm = BM; bn = BN; return; }
@@ -135,6 +148,16 @@ CAKE_API int cake_gemm(int dt, int epi, int cfg, int splits, const void* a, long
   splits = (K + kps - 1) / kps;
   g.kps = kps;
   const dim3 grid(g.tiles_m * g.tiles_n, splits);
+  // the four-wave tile's in-kernel pair: two splits, one slab per tile in ws (the caller's
+  // splits * M * Nv floats must cover it), no finalize launch
+  if (cfg == k4WCfg && splits == 2 && ws != nullptr && g.tiles_m * g.tiles_n <= kPairTiles &&
+      (long long)g.tiles_m * g.tiles_n * 65536 <= 2LL * M * g.Nv && pair_ticks()) {
+    g.pair = 1;
+    g.tick = pair_ticks();
+    return (dt == kBF16) ? dispatch_epi<kBF16>(epi, cfg, grid, st, g)
+           : (dt == kF16) ? dispatch_epi<kF16>(epi, cfg, grid, st, g)
+                          : (int)hipErrorInvalidValue;
+  }
   const int kernel_epi = splits > 1 ? (int)kEpiPartial : epi;
   if (splits > 1 && ws == nullptr) return (int)hipErrorInvalidValue;
   int rc = (dt == kBF16) ? dispatch_epi<kBF16>(kernel_epi, cfg, grid, st, g)

@@ -174,6 +174,48 @@ __global__ __launch_bounds__(256) void gemm_4w_kernel(GemmArgs g) {
   for (int j = 0; j < FN; ++j) asm volatile("" : "+a"(acc[FM - 1][j]));
   __builtin_amdgcn_s_waitcnt(vm_wait(0));
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  const float4* padd = nullptr;
+  if (g.pair) {
+    // split-K pair: ticket per tile (agent scope).  The first arrival stores its
+    // accumulators to the tile's slab ([i][j][thread] float4, coalesced), releases and
+    // raises the ready flag, and is done; the second waits for the flag (the first is
+    // already past its ticket, so it is running: no residency assumption), acquires,
+    // adds the slab and runs the epilogue, then clears the tile's counters for the next
+    // launch.  a + b in either order: the same bits whichever split arrives first.
+    unsigned* tk = g.tick + id;
+    unsigned* fl = g.tick + kPairTiles + id;
+    volatile uint32_t* bc = reinterpret_cast<volatile uint32_t*>(smem + 2 * BUF - 16);
+    if (tid == 0) bc[0] = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    const bool first = bc[0] == 0;
+    float4* slab = reinterpret_cast<float4*>(g.ws + (size_t)id * (BM * BN)) + tid;
+    if (first) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const cf32x4 v = acc[i][j];
+          slab[(i * FN + j) * 256] = make_float4(v[0], v[1], v[2], v[3]);
+        }
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(fl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      return;
+    }
+    if (tid == 0) {
+      while (__hip_atomic_load(fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+        __builtin_amdgcn_s_sleep(2);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(fl, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    padd = slab;  // the epilogue strips add the first split's accumulators
+  }
   float* stg = reinterpret_cast<float*>(smem + wave * STG);
   const int row_m0 = m0 + wr * WTM;
   const int vcol0 = n0 + wc * WTN;
@@ -184,7 +226,8 @@ __global__ __launch_bounds__(256) void gemm_4w_kernel(GemmArgs g) {
     constexpr int i = decltype(ii)::value;
     if constexpr (i + 1 < FM)
       ops.template load_res<(i + 1) & 1>(g, row_m0 + (i + 1) * 16 + (lane >> 2), vcol0, lane);
-    epi_strip<DT, EPI, FN, i & 1>(g, acc[i], stg, row_m0 + i * 16, vcol0, split, lane, ops);
+    epi_strip<DT, EPI, FN, i & 1>(g, acc[i], stg, row_m0 + i * 16, vcol0, split, lane, ops,
+                                  padd ? padd + i * FN * 256 : nullptr);
   });
 }
 

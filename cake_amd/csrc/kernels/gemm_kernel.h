@@ -46,7 +46,13 @@ struct GemmArgs {
   int gated;             // B row order interleaves 16-row blocks of two halves
   int tiles_m, tiles_n, kps;  // k elements per split
   int act;               // kEpiSilu activation: 0 SiLU, 1 quick_gelu, 2 GELU (erf)
+  // in-kernel split-K pair (gemm_4w.h, splits == 2): the first split of a tile to finish
+  // parks its accumulators in ws (one 256x256 f32 slab per tile), the second adds them and
+  // runs the epilogue; tick = [kPairTiles arrival counters | kPairTiles ready flags]
+  int pair;
+  unsigned* tick;
 };
+constexpr int kPairTiles = 16384;
 
 // virtual B row -> weight row (gated: [16 gate rows | 16 up rows] per 32-row block)
 __device__ __forceinline__ int wrow(const GemmArgs& g, int v) {
@@ -213,10 +219,13 @@ __device__ __forceinline__ void store16(uint16_t* dst, const uint16_t* v, bool f
 // One 16-row strip of a wave's output (NF 16x16 accumulator tiles = NF*16 virtual
 // columns starting at vcol0), staged through the wave's LDS slice stg and written
 // with the epilogue EPI (bias / residual from ops, buffer B).
+// add (split-K pair, gemm_4w.h): this thread's parked partner accumulators of the strip,
+// float4 j at add[j * 256], summed in before staging
 template <int DT, int EPI, int NF, int B>
 __device__ __forceinline__ void epi_strip(const GemmArgs& g, const cf32x4 (&tiles)[NF], float* stg,
                                           int m_strip0, int vcol0, int split, int lane,
-                                          const EpiOps<DT, EPI, NF>& ops) {
+                                          const EpiOps<DT, EPI, NF>& ops,
+                                          const float4* add = nullptr) {
   constexpr int WTN = NF * 16;
   constexpr int STG_LD = WTN + 4;
   constexpr bool GATED = (EPI == kEpiSwiglu || EPI == kEpiGeglu);
@@ -224,11 +233,22 @@ __device__ __forceinline__ void epi_strip(const GemmArgs& g, const cf32x4 (&tile
   constexpr int CPL = OUTC / 4;                // columns per lane (4 lanes per row)
   const int er = lane >> 2, ec = (lane & 3) * CPL;
   {
+    if (add) {
 #pragma unroll
-    for (int j = 0; j < NF; ++j)
+      for (int j = 0; j < NF; ++j) {
+        const float4 o = add[j * 256];
+        const float ov[4] = {o.x, o.y, o.z, o.w};
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
-        stg[((lane >> 4) * 4 + e) * STG_LD + j * 16 + (lane & 15)] = tiles[j][e];
+        for (int e = 0; e < 4; ++e)
+          stg[((lane >> 4) * 4 + e) * STG_LD + j * 16 + (lane & 15)] = tiles[j][e] + ov[e];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < NF; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          stg[((lane >> 4) * 4 + e) * STG_LD + j * 16 + (lane & 15)] = tiles[j][e];
+    }
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
     const int m = m_strip0 + er;

@@ -36,6 +36,12 @@ class SdOpts(C.Structure):
 PARTS = {"unet": 1, "vae": 2, "clip": 4, "clip2": 8}
 
 
+class SdSplitOpts(C.Structure):
+    _fields_ = [("rank", C.c_int32), ("world", C.c_int32), ("master_addr", C.c_char_p),
+                ("timeout_s", C.c_double), ("connect_timeout_s", C.c_double),
+                ("owners", C.POINTER(C.c_int32)), ("n_owners", C.c_int32)]
+
+
 class SdGenArgs(C.Structure):
     _fields_ = [("cond", C.POINTER(C.c_int32)), ("uncond", C.POINTER(C.c_int32)),
                 ("cond2", C.POINTER(C.c_int32)), ("uncond2", C.POINTER(C.c_int32)),
@@ -83,6 +89,13 @@ def lib() -> C.CDLL:
         L.cake_sd_vae_encode.restype = I
         L.cake_sd_vae_encode_remote.argtypes = [P, FP, FP, C.c_char_p, I]
         L.cake_sd_vae_encode_remote.restype = I
+        L.cake_sd_open_split.argtypes = [C.c_char_p, C.POINTER(SdOpts), C.POINTER(SdSplitOpts),
+                                         C.c_char_p, I]
+        L.cake_sd_open_split.restype = P
+        L.cake_sd_serve.argtypes = [P, C.c_char_p, I]
+        L.cake_sd_serve.restype = I
+        L.cake_sd_split_info.argtypes = [P, C.POINTER(C.c_int32)]
+        L.cake_sd_split_info.restype = None
         _bound = True
     return L
 
@@ -121,9 +134,14 @@ class NativeSD:
                  height: int = 0, dtype: str = "f16", device: int = 0,
                  random_init: bool = False, seed: int = 0, autotune: bool = True,
                  paths: dict | None = None, parts=None, remote: dict | None = None,
-                 remote_timeout_s: float = 120.0):
+                 remote_timeout_s: float = 120.0, rank: int = 0, world: int = 1,
+                 master_addr: str = "127.0.0.1:29533", hop_timeout_s: float = 60.0,
+                 connect_timeout_s: float = 600.0, owners: list[int] | None = None):
         """remote: component -> "host:port" of the TCP worker serving it (the topology's
-        unet / vae / clip / clip2); those are not loaded here."""
+        unet / vae / clip / clip2); those are not loaded here.  world > 1: one rank of a
+        split UNet over one process per GPU (sd_engine.h CakeSdSplitOpts): rank 0
+        generates, the others call :meth:`serve`; every rank of the group must be
+        constructed concurrently."""
         if dtype not in ("f16", "bf16"):
             raise ValueError("native SD engine dtype: f16 or bf16")
         p = paths or {}
@@ -142,13 +160,37 @@ class NativeSD:
                    remote_clip=self._keep[7], remote_clip2=self._keep[8],
                    remote_timeout_s=float(remote_timeout_s))
         err = C.create_string_buffer(1024)
-        self._h = lib().cake_sd_open(str(model_dir).encode(), C.byref(o), err, 1024)
+        if world > 1:
+            own = None
+            if owners is not None:
+                own = (C.c_int32 * len(owners))(*[int(x) for x in owners])
+            self._split_keep = (own, master_addr.encode())
+            sp = SdSplitOpts(int(rank), int(world), self._split_keep[1], float(hop_timeout_s),
+                             float(connect_timeout_s),
+                             C.cast(own, C.POINTER(C.c_int32)) if own is not None else None,
+                             len(owners) if owners is not None else 0)
+            self._h = lib().cake_sd_open_split(str(model_dir).encode(), C.byref(o), C.byref(sp),
+                                               err, 1024)
+        else:
+            self._h = lib().cake_sd_open(str(model_dir).encode(), C.byref(o), err, 1024)
         if not self._h:
             raise RuntimeError(f"native SD engine: {err.value.decode(errors='replace')}")
         info = (C.c_int32 * 6)()
         lib().cake_sd_info(self._h, info)
         self.width, self.height, self.context_dim, self._dt, d1, d2 = (int(x) for x in info)
         self.text_dims = (d1, d2)
+
+    def split_info(self) -> dict:
+        """rank, world, UNet stages, ranks used, and this rank's stage range."""
+        o = (C.c_int32 * 6)()
+        lib().cake_sd_split_info(self._h, o)
+        return dict(zip(("rank", "world", "stages", "ranks_used", "first", "end"),
+                        (int(x) for x in o)))
+
+    def serve(self) -> None:
+        """Split-UNet ranks > 0: run rank 0's generations until it closes the group."""
+        err = C.create_string_buffer(1024)
+        self._check(lib().cake_sd_serve(self._h, err, 1024), err)
 
     def _check(self, rc: int, err) -> None:
         if rc != 0:

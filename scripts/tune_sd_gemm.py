@@ -20,6 +20,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from cake_amd.ops import gemm as G  # noqa: E402
 
 INNER, REPS = 10, 10
+# A/B forms measured slower everywhere (the non-interleaved 8 / 11, ping-pong 20,
+# register-staged 21: profiles/r6_gemm_*): not timed unless --cfgs names them
+SKIP = {8, 11, 20, 21}
 TUNED = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "cake_amd",
                      "ops", "gemm_tuned.json")
 
@@ -77,7 +80,7 @@ def timeit(fn):
     return ts[len(ts) // 2]
 
 
-def tune(M, Nv, K, epi, dt):
+def tune(M, Nv, K, epi, dt, cfgs=None):
     gated = epi in ("swiglu", "geglu")
     N = Nv // 2 if gated else Nv
     x = (torch.randn(M, K, device="cuda") * 0.5).to(dt)
@@ -96,6 +99,12 @@ def tune(M, Nv, K, epi, dt):
     for cfg, (bm, bn) in G.CFG_TILES.items():
         if gated and cfg in getattr(G, "NO_GATED", ()):
             continue
+        if cfgs is not None and cfg not in cfgs:
+            continue
+        if cfgs is None and (cfg in SKIP or (M >= 1024 and bm <= 64)):
+            continue
+        if cfg in getattr(G, "K64_ONLY", ()) and K % 64:
+            continue
         tiles = -(-M // bm) * -(-Nv // bn)
         for splits in (1, 2, 4):
             if splits > 1 and (tiles * splits > 2 * G.NUM_CUS or K // splits < 256):
@@ -105,11 +114,11 @@ def tune(M, Nv, K, epi, dt):
                 res[(cfg, splits)] = timeit(lambda: run(cfg, splits))
             except Exception:  # noqa: BLE001  (a config the shape cannot take)
                 continue
-    if cur not in res:
+    if cur not in res and cur[0] != G.LIB:
         run(*cur)
         res[cur] = timeit(lambda: run(*cur))
     best = min(res, key=res.get)
-    return cur, res[cur], best, res[best]
+    return cur, res.get(cur, float("nan")), best, res[best]
 
 
 LLAMA_LENS = {"8b": (32, 128, 512, 1024, 2048, 4096), "70b": (512, 2048)}
@@ -138,12 +147,31 @@ def main():
                     help="comma list of SD versions, and/or 'llama' for the prefill shapes")
     ap.add_argument("--llama-lens", default=None,
                     help="prompt lengths of the llama shapes, e.g. '8b:256,384;70b:1024'")
+    ap.add_argument("--lib-shapes", action="store_true",
+                    help="re-tune (MFMA only) every table entry that names the library GEMM")
+    ap.add_argument("--cfgs", default=None, help="comma list of tile configs to time")
     ap.add_argument("--write", default=None,
                     help="write gemm_tuned.json with the winners merged in to this path")
     a = ap.parse_args()
     dt = torch.float16
     new = []
-    for version in a.versions.split(","):
+    cfgs = None if a.cfgs is None else {int(c) for c in a.cfgs.split(",")}
+    if a.lib_shapes:  # the library GEMM's measured shapes (CAKE_GEMM_LIB A/B arm)
+        with open(TUNED) as f:
+            lib = [e for e in json.load(f)["entries"] if e["cfg"] == G.LIB]
+        a.versions = ""
+        for e in lib:
+            M, Nv, K, epi = e["M"], e["Nv"], e["K"], e["epi"]
+            cur, t_cur, best, t_best = tune(M, Nv, K, epi, torch.bfloat16, cfgs)
+            fl = 2.0 * M * Nv * K
+            rec = {"version": "llama_lib", "M": M, "Nv": Nv, "K": K, "epi": epi,
+                   "lib_tflops": e.get("tflops"), "best": list(best),
+                   "best_ms": round(t_best, 4), "best_tflops": round(fl / t_best / 1e9, 1)}
+            print(json.dumps(rec), flush=True)
+            new.append({"M": M, "Nv": Nv, "K": K, "epi": epi, "cfg": best[0], "splits": best[1],
+                        "tflops": rec["best_tflops"], "shape": e.get("shape", "llama_prefill"),
+                        "lib_tflops": e.get("tflops")})
+    for version in [v for v in a.versions.split(",") if v]:
         dt = torch.bfloat16 if version == "llama" else torch.float16
         lens = None
         if a.llama_lens:
@@ -174,6 +202,9 @@ def main():
         new = list(uniq.values())
         keys = set(uniq)
         old = [e for e in table["entries"] if (e["M"], e["Nv"], e["K"], e["epi"]) not in keys]
+        if a.lib_shapes:  # the library arm stays, as its own entries (read under CAKE_GEMM_LIB=1)
+            old += [dict(e, shape="lib_ab") for e in table["entries"]
+                    if e["cfg"] == G.LIB and (e["M"], e["Nv"], e["K"], e["epi"]) in keys]
         table["entries"] = old + new
         table["sd_source"] = "scripts/tune_sd_gemm.py"
         with open(a.write, "w") as f:

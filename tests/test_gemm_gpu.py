@@ -289,3 +289,30 @@ def test_big_tile_gemm_llama_shapes(cuda, dt, M, N, K, splits, cfg):
     ref = r + _ref(x, w)
     G.linear(x, w, epi="resid32", resid=r, cfg=cfg, splits=splits)
     torch.testing.assert_close(r, ref, atol=3e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize("epi", ["store", "resid32", "swiglu"])
+def test_four_wave_split_pair(cuda, epi):
+    """cfg 22 with split-K 2 runs the in-kernel pair (the first split of a tile parks its
+    accumulators, the second adds them and runs the epilogue; gemm_4w.h): equal to the
+    f32 reference, bitwise repeatable whichever split arrives first, and the tile counters
+    left clean for the next launch (a third call still matches)."""
+    from cake_amd.ops import gemm as G
+    torch.manual_seed(3)
+    M, K = 2048, 4096
+    N = 4096 if epi != "swiglu" else 2 * 2048
+    x, w = _r(M, K, dt=torch.bfloat16), _r(N, K, dt=torch.bfloat16, std=K ** -0.5)
+    y = _ref(x, w)
+    outs = []
+    for _ in range(3):
+        if epi == "resid32":
+            r = torch.zeros(M, N, device="cuda")
+            G.linear(x, w, epi="resid32", resid=r, cfg=22, splits=2)
+            outs.append(r)
+        elif epi == "swiglu":
+            outs.append(G.linear(x, w, epi="swiglu", cfg=22, splits=2))
+        else:
+            outs.append(G.linear(x, w, cfg=22, splits=2))
+    ref = F.silu(y[:, :N // 2]) * y[:, N // 2:] if epi == "swiglu" else y
+    _close(outs[0], ref, K)
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])

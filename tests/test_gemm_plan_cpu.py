@@ -46,7 +46,8 @@ def test_tuned_table_entries_are_launchable():
     assert table
     seen = set()
     for e in table:
-        key = (e["M"], e["Nv"], e["K"], e["epi"])
+        # one MFMA plan per shape, and at most one library (A/B arm) entry beside it
+        key = (e["M"], e["Nv"], e["K"], e["epi"], e["cfg"] == G.LIB)
         assert key not in seen, f"duplicate plan {key}"
         seen.add(key)
         assert e["splits"] >= 1 and e["epi"] in G.EPI, e
