@@ -65,6 +65,8 @@ static unsigned* pair_ticks() {
 
 static inline void cfg_dims(int cfg, int& bm, int& bn) {
   if (cfg == kPPCfg || cfg == kRSCfg || cfg == k4WCfg) { bm = bn = 256; return; }
+  if (cfg == k4WCfg192) { bm = 256; bn = 192; return; }
+  if (cfg == k4WCfg128) { bm = 128; bn = 256; return; }
 #define X(id, BM, BN, WM, WN, NS, PR) if (cfg == id) { bm = BM; bn = BN; return; }
   CAKE_GEMM_CFGS(X)
 #undef X
@@ -123,7 +125,8 @@ CAKE_API int cake_gemm(int dt, int epi, int cfg, int splits, const void* a, long
     return (int)hipErrorInvalidValue;
   const bool gated = (epi == kEpiSwiglu || epi == kEpiGeglu);
   if (gated && N % 16) return (int)hipErrorInvalidValue;
-  if (cfg == kRSCfg || cfg == k4WCfg) {  // whole 64-element k steps; 31-bit offsets
+  const bool four = cfg == k4WCfg || cfg == k4WCfg192 || cfg == k4WCfg128;
+  if (cfg == kRSCfg || four) {  // whole 64-element k steps; 31-bit offsets
     const long long wrows = gated ? 2LL * N : N;
     if (K % kGBK || ((long long)(M - 1) * lda + K) * 2 >= 0x7fffffffLL ||
         ((wrows - 1) * ldb + K) * 2 >= 0x7fffffffLL)
@@ -150,12 +153,19 @@ CAKE_API int cake_gemm(int dt, int epi, int cfg, int splits, const void* a, long
   const dim3 grid(g.tiles_m * g.tiles_n, splits);
   // the four-wave tile's in-kernel pair: two splits, one slab per tile in ws (the caller's
   // splits * M * Nv floats must cover it), no finalize launch
-  if (cfg == k4WCfg && splits == 2 && ws != nullptr && g.tiles_m * g.tiles_n <= kPairTiles &&
-      (long long)g.tiles_m * g.tiles_n * 65536 <= 2LL * M * g.Nv && pair_ticks()) {
+  // splits == 2 on a four-wave tile: the tiles past the last whole wave (all of them when
+  // there are at most 128) run as in-kernel k-half pairs, the rest whole
+  const int ntiles = g.tiles_m * g.tiles_n;
+  const int npair = ntiles <= 256 ? ntiles : ntiles % 256;
+  if (four && splits == 2 && ws != nullptr && npair > 0 &&
+      npair <= 128 + (ntiles <= 256 ? 128 : 0) && ntiles <= kPairTiles &&
+      (long long)npair * bm * bn <= 2LL * M * g.Nv && pair_ticks()) {
     g.pair = 1;
     g.tick = pair_ticks();
-    return (dt == kBF16) ? dispatch_epi<kBF16>(epi, cfg, grid, st, g)
-           : (dt == kF16) ? dispatch_epi<kF16>(epi, cfg, grid, st, g)
+    g.dp_tiles = ntiles - npair;
+    const dim3 pgrid(g.dp_tiles + 2 * npair, 1);
+    return (dt == kBF16) ? dispatch_epi<kBF16>(epi, cfg, pgrid, st, g)
+           : (dt == kF16) ? dispatch_epi<kF16>(epi, cfg, pgrid, st, g)
                           : (int)hipErrorInvalidValue;
   }
   const int kernel_epi = splits > 1 ? (int)kEpiPartial : epi;

@@ -22,15 +22,22 @@
 
 namespace cake {
 
-constexpr int k4WCfg = 22;  // plan cfg id of this kernel (BM = BN = 256)
+constexpr int k4WCfg = 22;     // plan cfg id of the 256 x 256 tile
+constexpr int k4WCfg192 = 23;  // 256 x 192 (8B q|k|v: 6144 = 32 x 192 columns, 256 tiles at
+                               // 2048 tokens instead of 192)
+constexpr int k4WCfg128 = 24;  // 128 x 256 (8B o / down at 2048 tokens: 256 tiles, not 128)
 
-template <int DT, int EPI>
+template <int DT, int EPI, int BM, int BN>
 __global__ __launch_bounds__(256) void gemm_4w_kernel(GemmArgs g) {
-  constexpr int BM = 256, BN = 256, WTM = 128, WTN = 128, FM = 8, FN = 8;
-  constexpr int BUF = (BM + BN) * 128;  // 64 KB per k-step buffer
-  constexpr int IPW = 16;               // DMA wave-instructions per wave per k-step
+  static_assert((BM == 256 && (BN == 256 || BN == 192)) || (BM == 128 && BN == 256),
+                "four-wave tile shapes");
+  constexpr int WTM = BM / 2, WTN = BN / 2, FM = WTM / 16, FN = WTN / 16;
+  constexpr int BUF = (BM + BN) * 128;  // 64 / 56 / 48 KB per k-step buffer
+  constexpr int IPW = (BM + BN) / 32;   // DMA wave-instructions per wave per k-step
+  constexpr int NA = BM / 32;           // of which A
+  static_assert(IPW == FM + FN, "the second half alternates one DMA with one fragment read");
   constexpr int STG_LD = WTN + 4, STG = 16 * STG_LD * 4;
-  static_assert(4 * STG <= 2 * BUF, "epilogue staging fits the operand buffers");
+  static_assert(4 * STG <= 2 * BUF - 16, "epilogue staging fits the operand buffers");
   __shared__ __attribute__((aligned(16))) uint8_t smem[2 * BUF];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -38,12 +45,23 @@ __global__ __launch_bounds__(256) void gemm_4w_kernel(GemmArgs g) {
   const int wr = wave >> 1, wc = wave & 1;
 
   // ---- XCD-aware grouped tile order (as gemm_kernel) ---------------------
+  // Paired split-K (g.pair): workgroups [0, dp_tiles) run whole tiles, the rest run the
+  // remaining tiles as pairs of k halves (2 workgroups per tile) — the last partial wave
+  // of a grid at half length instead of full (8B gate|up at 2048 tokens: 896 tiles =
+  // 3 full waves + 128 paired tiles), or every tile paired when there are too few.
   const int ntiles = g.tiles_m * g.tiles_n;
-  int id;
+  int id, split = blockIdx.y;
   {
     const int bid = blockIdx.x;
-    const int q = ntiles / 8, r = ntiles % 8, x = bid % 8, i = bid / 8;
-    id = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+    const int dp = g.pair ? g.dp_tiles : ntiles;
+    if (bid < dp) {
+      const int q = dp / 8, r = dp % 8, x = bid % 8, i = bid / 8;
+      id = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+      if (g.pair) split = -1;  // a whole tile
+    } else {
+      id = dp + (bid - dp) / 2;
+      split = (bid - dp) & 1;
+    }
   }
   constexpr int GROUP = 8;
   const int per_group = GROUP * g.tiles_n;
@@ -51,12 +69,12 @@ __global__ __launch_bounds__(256) void gemm_4w_kernel(GemmArgs g) {
   const int gm = min(GROUP, g.tiles_m - first_m);
   const int m0 = (first_m + (id % per_group) % gm) * BM;
   const int n0 = ((id % per_group) / gm) * BN;
-  const int split = blockIdx.y;
-  const int kb = split * g.kps, ke = min(g.K, kb + g.kps);
+  const int kb = split < 0 ? 0 : split * g.kps;
+  const int ke = split < 0 ? g.K : min(g.K, kb + g.kps);
   const int nk = (ke - kb) / kGBK;
 
   // ---- DMA: instruction i of this wave fills LDS rows i*32 + wave*8 + [0, 8) (A rows
-  // for i < 8, B rows after); lane l -> row + l/8, slot l%8 holding source chunk
+  // for i < NA, B rows after); lane l -> row + l/8, slot l%8 holding source chunk
   // (l%8) ^ ((row >> 1) & 7), the same for every i
   const int rA = wave * 8 + (lane >> 3);
   const int chunk = (lane & 7) ^ ((rA >> 1) & 7);
@@ -81,12 +99,12 @@ __global__ __launch_bounds__(256) void gemm_4w_kernel(GemmArgs g) {
     const uint32_t ks = kbase + (uint32_t)step * (kGBK * 2);
     auto* dst = (__attribute__((address_space(3))) void*)(smem + buf * BUF + (i * 4 + wave) * 1024);
     const bool live = step < nk;
-    if (i < 8)
+    if (i < NA)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
           ra, dst, 16, voff_a, live ? (int)(ks + i * gstride_a) : 0x7fffffff, 0, 0);
     else
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rb, dst, 16, voff_b, live ? (int)(ks + (i - 8) * gstride_b) : 0x7fffffff, 0, 0);
+          rb, dst, 16, voff_b, live ? (int)(ks + (i - NA) * gstride_b) : 0x7fffffff, 0, 0);
   };
   auto stage = [&](int step, int buf) {
 #pragma unroll
@@ -175,20 +193,21 @@ __global__ __launch_bounds__(256) void gemm_4w_kernel(GemmArgs g) {
   __builtin_amdgcn_s_waitcnt(vm_wait(0));
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   const float4* padd = nullptr;
-  if (g.pair) {
+  if (g.pair && split >= 0) {
     // split-K pair: ticket per tile (agent scope).  The first arrival stores its
     // accumulators to the tile's slab ([i][j][thread] float4, coalesced), releases and
     // raises the ready flag, and is done; the second waits for the flag (the first is
     // already past its ticket, so it is running: no residency assumption), acquires,
     // adds the slab and runs the epilogue, then clears the tile's counters for the next
     // launch.  a + b in either order: the same bits whichever split arrives first.
-    unsigned* tk = g.tick + id;
-    unsigned* fl = g.tick + kPairTiles + id;
+    const int pid = id - g.dp_tiles;  // this pair's slot
+    unsigned* tk = g.tick + pid;
+    unsigned* fl = g.tick + kPairTiles + pid;
     volatile uint32_t* bc = reinterpret_cast<volatile uint32_t*>(smem + 2 * BUF - 16);
     if (tid == 0) bc[0] = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     const bool first = bc[0] == 0;
-    float4* slab = reinterpret_cast<float4*>(g.ws + (size_t)id * (BM * BN)) + tid;
+    float4* slab = reinterpret_cast<float4*>(g.ws + (size_t)pid * (BM * BN)) + tid;
     if (first) {
 #pragma unroll
       for (int i = 0; i < FM; ++i)

@@ -51,6 +51,7 @@ struct GemmArgs {
   // runs the epilogue; tick = [kPairTiles arrival counters | kPairTiles ready flags]
   int pair;
   unsigned* tick;
+  int dp_tiles;          // pair: tiles [0, dp_tiles) run whole, the rest as k-half pairs
 };
 constexpr int kPairTiles = 16384;
 
@@ -696,7 +697,15 @@ int launch_gemm(int cfg, dim3 grid, hipStream_t st, const GemmArgs& g) {
     return (int)hipGetLastError();
   }
   if (cfg == k4WCfg) {
-    hipLaunchKernelGGL((gemm_4w_kernel<DT, EPI>), grid, dim3(256), 0, st, g);
+    hipLaunchKernelGGL((gemm_4w_kernel<DT, EPI, 256, 256>), grid, dim3(256), 0, st, g);
+    return (int)hipGetLastError();
+  }
+  if (cfg == k4WCfg192) {
+    hipLaunchKernelGGL((gemm_4w_kernel<DT, EPI, 256, 192>), grid, dim3(256), 0, st, g);
+    return (int)hipGetLastError();
+  }
+  if (cfg == k4WCfg128) {
+    hipLaunchKernelGGL((gemm_4w_kernel<DT, EPI, 128, 256>), grid, dim3(256), 0, st, g);
     return (int)hipGetLastError();
   }
 

@@ -50,7 +50,9 @@ class NativeSDGenerator(ImageGenerator):
         self.last_result = None
 
     @classmethod
-    def load(cls, ctx) -> "NativeSDGenerator":
+    def load(cls, ctx, split: dict | None = None) -> "NativeSDGenerator":
+        """split: rank 0 of a native split UNet (NativeSD rank / world / master_addr /
+        owners keyword arguments; parallel/sd_rccl.py run_native_split)."""
         from tokenizers import Tokenizer
 
         from ...sd_engine import NativeSD
@@ -82,7 +84,7 @@ class NativeSDGenerator(ImageGenerator):
                                       ctx.model_path))
         eng = NativeSD(str(ctx.model_path), version=cfg.version, width=cfg.width,
                        height=cfg.height, dtype="bf16" if ctx.dtype == torch.bfloat16 else "f16",
-                       device=ctx.device.index or 0, paths=paths, remote=remote)
+                       device=ctx.device.index or 0, paths=paths, remote=remote, **(split or {}))
 
         def fallback():
             from .pipeline import SDGenerator

@@ -315,11 +315,66 @@ class DeviceUNet:
         return lat, times.cpu().tolist()
 
 
+def native_split_owners(topology, cfg, world: int) -> list[int] | None:
+    """Stage -> rank of the native engine's split UNet (csrc/engine/sd_engine.cpp
+    CakeSdSplitOpts) for a topology that places only UNet stages on ranks >= 1, in
+    contiguous runs 0, 1, 2, ... in stage order; None when the topology needs the Python
+    transport (a text encoder or the VAE on a worker rank, or another stage order) or
+    places nothing."""
+    n = len(cfg.unet.blocks)
+    stages = [f"down.{i}" for i in range(n)] + ["mid"] + [f"up.{i}" for i in range(n)]
+    for comp in ("clip", "clip2", "vae"):
+        if component_owner(topology, comp, world) != 0:
+            return None
+    own = unet_stage_owners(topology, stages, world)
+    owners = [own[s] for s in stages]
+    if max(owners) == 0 or owners[0] != 0:
+        return None
+    for a, b in zip(owners, owners[1:]):
+        if b not in (a, a + 1):
+            return None
+    return owners
+
+
+def run_native_split(ctx, owners: list[int]) -> None:
+    """Every rank opens the native SD engine's split UNet (one process per GPU, device bulk
+    hops, TCP control plane on MASTER_PORT + 2); rank 0 is the master (CLI images or the
+    REST API over NativeSDGenerator), the others serve its denoise steps."""
+    from ..models.sd.native_generator import NativeSDGenerator
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    addr = (f"{os.environ.get('MASTER_ADDR', '127.0.0.1')}:"
+            f"{int(os.environ.get('MASTER_PORT', '29500')) + 2}")
+    timeout = float(os.environ.get("CAKE_HOP_TIMEOUT", "60"))
+    split = dict(rank=rank, world=world, master_addr=addr, owners=owners,
+                 hop_timeout_s=timeout)
+    log.info("rank %d/%d: native split UNet, stage owners %s", rank, world, owners)
+    # the same model resolution on every rank; ranks > 0 load the UNet only (the engine)
+    gen = NativeSDGenerator.load(ctx, split=split)
+    try:
+        if rank == 0:
+            from ..master import Master
+            Master(ctx, sd=gen).run()
+        else:
+            gen.eng.serve()
+    finally:
+        gen.eng.close()
+
+
 def run_sd_rccl(ctx) -> None:
-    """Entry of ``--transport rccl --model-type image-model`` (every rank)."""
+    """Entry of ``--transport rccl --model-type image-model`` (every rank): the native
+    engine's split UNet when the topology places UNet stages only, in runs over ranks in
+    stage order (CAKE_NATIVE=0 or any other placement: the Python transport below)."""
     from .rccl_roles import _init_dist
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    from ..models.sd.native_generator import native_sd_eligible
+    if world > 1 and native_sd_eligible(ctx):
+        from ..models.sd.shardable import sd_config_for
+        owners = native_split_owners(ctx.topology, sd_config_for(ctx), world)
+        if owners is not None:
+            run_native_split(ctx, owners)
+            return
     _init_dist(ctx, rank, world)
     try:
         eng = SDEngine(ctx, rank, world)

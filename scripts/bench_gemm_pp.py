@@ -62,7 +62,7 @@ def main():
         r0 = torch.randn(M, N, device="cuda") if epi == "resid32" else None
         out = None if epi == "resid32" else torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         cfg5, s5 = G.plan_mfma(M, Nv, K, epi)
-        plans = {"mfma": (cfg5, s5), "pp": (20, 1), "pp2": (20, 2), "rs": (21, 1), "rs2": (21, 2), "w4": (22, 1), "w42": (22, 2),
+        plans = {"mfma": (cfg5, s5), "pp": (20, 1), "pp2": (20, 2), "rs": (21, 1), "rs2": (21, 2), "w4": (22, 1), "w42": (22, 2), "w3": (23, 1), "w32": (23, 2), "w1": (24, 1), "w12": (24, 2),
                  "lib": (G.LIB, 1)}
         y = x.float() @ w.float().t()
         if epi == "swiglu":

@@ -25,7 +25,7 @@ def _close(got, ref, K):
 
 
 @pytest.mark.parametrize("dt", DTYPES)
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7, 8, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7, 8, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24])
 @pytest.mark.parametrize("M,N,K,splits", [(128, 256, 256, 1), (77, 200, 320, 1),
                                           (300, 520, 1024, 3), (1, 64, 64, 1),
                                           (513, 136, 648, 2)])
@@ -140,7 +140,7 @@ def test_gemm_model_shapes(cuda, name, M, N, K, epi):
 
 
 @pytest.mark.parametrize("dt", DTYPES)
-@pytest.mark.parametrize("cfg", [5, 0, 13, 14, 15, 16, 17, 20, 21, 22])
+@pytest.mark.parametrize("cfg", [5, 0, 13, 14, 15, 16, 17, 20, 21, 22, 23, 24])
 @pytest.mark.parametrize("M,N,K", [(300, 700, 640), (257, 272, 2112), (520, 776, 200)])
 def test_gemm_interleaved_all_epilogues(cuda, dt, cfg, M, N, K):
     """Interleaved-schedule tiles with ragged M/N and every epilogue."""
@@ -269,8 +269,8 @@ def test_library_gemm_plan_cache_eviction(cuda):
 
 @pytest.mark.parametrize("dt", DTYPES)
 @pytest.mark.parametrize("M,N,K,splits", [(2048, 6144, 4096, 1), (1000, 4096, 14336, 2),
-                                          (2048, 2 * 14336, 4096, 1)])
-@pytest.mark.parametrize("cfg", [20, 21, 22])
+                                          (2048, 2 * 14336, 4096, 1), (2048, 2 * 14336, 4096, 2)])
+@pytest.mark.parametrize("cfg", [20, 21, 22, 23, 24])
 def test_big_tile_gemm_llama_shapes(cuda, dt, M, N, K, splits, cfg):
     """The ping-pong (cfg 20) and register-staged (cfg 21) 256x256 kernels on Llama
     prefill shapes: plain store, f32 residual accumulate (split-K included) and the fused
@@ -292,7 +292,8 @@ def test_big_tile_gemm_llama_shapes(cuda, dt, M, N, K, splits, cfg):
 
 
 @pytest.mark.parametrize("epi", ["store", "resid32", "swiglu"])
-def test_four_wave_split_pair(cuda, epi):
+@pytest.mark.parametrize("cfg", [22, 23, 24])
+def test_four_wave_split_pair(cuda, epi, cfg):
     """cfg 22 with split-K 2 runs the in-kernel pair (the first split of a tile parks its
     accumulators, the second adds them and runs the epilogue; gemm_4w.h): equal to the
     f32 reference, bitwise repeatable whichever split arrives first, and the tile counters
@@ -307,12 +308,12 @@ def test_four_wave_split_pair(cuda, epi):
     for _ in range(3):
         if epi == "resid32":
             r = torch.zeros(M, N, device="cuda")
-            G.linear(x, w, epi="resid32", resid=r, cfg=22, splits=2)
+            G.linear(x, w, epi="resid32", resid=r, cfg=cfg, splits=2)
             outs.append(r)
         elif epi == "swiglu":
-            outs.append(G.linear(x, w, epi="swiglu", cfg=22, splits=2))
+            outs.append(G.linear(x, w, epi="swiglu", cfg=cfg, splits=2))
         else:
-            outs.append(G.linear(x, w, cfg=22, splits=2))
+            outs.append(G.linear(x, w, cfg=cfg, splits=2))
     ref = F.silu(y[:, :N // 2]) * y[:, N // 2:] if epi == "swiglu" else y
     _close(outs[0], ref, K)
     assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])

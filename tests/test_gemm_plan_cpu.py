@@ -21,10 +21,12 @@ def _kernel_cfgs() -> dict:
     # the two 256x256 kernels of their own: ping-pong (8 waves, 2 x 4) and register-staged
     # (4 waves, 2 x 2)
     for hdr, name, waves in (("gemm_pp.h", "kPPCfg", (2, 4)), ("gemm_rs.h", "kRSCfg", (2, 2)),
-                             ("gemm_4w.h", "k4WCfg", (2, 2))):
+                             ("gemm_4w.h", "k4WCfg", (2, 2)), ("gemm_4w.h", "k4WCfg192", (2, 2)),
+                             ("gemm_4w.h", "k4WCfg128", (2, 2))):
         t = (ROOT / "cake_amd/csrc/kernels" / hdr).read_text()
         cid = int(re.search(name + r" = (\d+);", t).group(1))
-        cfgs[cid] = (256, 256) + waves
+        tile = {"k4WCfg192": (256, 192), "k4WCfg128": (128, 256)}.get(name, (256, 256))
+        cfgs[cid] = tile + waves
     return cfgs
 
 
