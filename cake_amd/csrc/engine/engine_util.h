@@ -108,7 +108,7 @@ struct GemmPlanner {
     const bool lib_ok = gemm_lib_enabled();
     try {
       const Json j = Json::parse(read_file(path));
-      static const int known[] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24};
+      static const int known[] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27};
       for (const auto& e : j.get("entries").items()) {
         const int cfg = (int)e.get("cfg").as_int();
         const std::string ep = e.get("epi").as_string();

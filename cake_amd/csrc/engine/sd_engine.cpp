@@ -557,7 +557,6 @@ class SdEngine {
       throw Error("xl / turbo need the second tokenizer's ids (cond2 / uncond2)");
     const int bsize = std::max(1, a.bsize);
     if (bsize > 64) throw Error("bsize above 64");
-    if (a.init_latents && bsize != 1) throw Error("img2img takes bsize 1");
     Schedule s = build_schedule(cfg_.sched, a.n_steps);
     int first = 0;  // index in the full schedule of the first step run
     if (a.init_latents) {  // img2img: the steps from t_start on (pipeline.py t_start)

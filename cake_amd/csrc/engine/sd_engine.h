@@ -63,14 +63,14 @@ typedef struct CakeSdGenArgs {
                             // when init_noise is null
   const float* init_noise;  // optional [4 * (h/8) * (w/8)] standard-normal latent noise
   int32_t use_graph;        // 1: every step after the first is one hipGraph replay
-  // img2img: the schedule's steps from t_start on, starting from init_latents (the
+  // img2img: the schedule's steps from t_start on, starting from init_latents ([bsize] x the
   // encoded image, scaled and noised to ts[t_start] by the caller); null = txt2img
   int32_t t_start;
   const float* init_latents;
   // images per sample (the reference's bsize): the UNet runs 2 bsize rows under guidance,
   // the text rows repeated [uncond, cond] x bsize as the reference's
   // text_embeddings.repeat((bsize, 1, 1)); init_noise then holds bsize latents, rgb /
-  // latents_out bsize images.  0 = 1.  img2img takes bsize 1.
+  // latents_out bsize images (img2img: init_latents bsize latents).  0 = 1.
   int32_t bsize;
   // intermediary images: every step index i (of the full schedule) with i % intermediary
   // == 0 is decoded and handed to on_image(cb_ctx, i, bsize, rgb [bsize, height, width, 3])

@@ -64,6 +64,7 @@ static unsigned* pair_ticks() {
 }
 
 static inline void cfg_dims(int cfg, int& bm, int& bn) {
+  if (cfg >= k4WCfg + k4WDeep && cfg <= k4WCfg128 + k4WDeep) cfg -= k4WDeep;  // DEEP twins
   if (cfg == kPPCfg || cfg == kRSCfg || cfg == k4WCfg) { bm = bn = 256; return; }
   if (cfg == k4WCfg192) { bm = 256; bn = 192; return; }
   if (cfg == k4WCfg128) { bm = 128; bn = 256; return; }
@@ -125,7 +126,7 @@ CAKE_API int cake_gemm(int dt, int epi, int cfg, int splits, const void* a, long
     return (int)hipErrorInvalidValue;
   const bool gated = (epi == kEpiSwiglu || epi == kEpiGeglu);
   if (gated && N % 16) return (int)hipErrorInvalidValue;
-  const bool four = cfg == k4WCfg || cfg == k4WCfg192 || cfg == k4WCfg128;
+  const bool four = four_wave_cfg(cfg);
   if (cfg == kRSCfg || four) {  // whole 64-element k steps; 31-bit offsets
     const long long wrows = gated ? 2LL * N : N;
     if (K % kGBK || ((long long)(M - 1) * lda + K) * 2 >= 0x7fffffffLL ||

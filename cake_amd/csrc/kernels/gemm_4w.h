@@ -26,8 +26,16 @@ constexpr int k4WCfg = 22;     // plan cfg id of the 256 x 256 tile
 constexpr int k4WCfg192 = 23;  // 256 x 192 (8B q|k|v: 6144 = 32 x 192 columns, 256 tiles at
                                // 2048 tokens instead of 192)
 constexpr int k4WCfg128 = 24;  // 128 x 256 (8B o / down at 2048 tokens: 256 tiles, not 128)
+constexpr int k4WDeep = 3;     // cfg + 3: the same tiles with DEEP staging (25, 26, 27)
+inline bool four_wave_cfg(int cfg) { return cfg >= k4WCfg && cfg <= k4WCfg128 + k4WDeep; }
 
-template <int DT, int EPI, int BM, int BN>
+// DEEP (cfg 25-27): the LDS image split by k half, so each half of step t+2 is staged as
+// soon as the half of step t it replaces has been read (kk0 half during the first MFMA
+// half of step t, kk1 half during the second), two barriers per step with vmcnt(2 x the
+// half's DMAs): a DMA has ~1.5 steps to land instead of ~0.5-1.  Half-rows are 64 bytes
+// (four 16-byte slots); slot s of row r holds chunk s ^ F[(r >> 2) & 3], F = {0, 2, 3, 1},
+// which spreads every ds_read_b128 lane group over 16 distinct bank quads.
+template <int DT, int EPI, int BM, int BN, bool DEEP = false>
 __global__ __launch_bounds__(256) void gemm_4w_kernel(GemmArgs g) {
   static_assert((BM == 256 && (BN == 256 || BN == 192)) || (BM == 128 && BN == 256),
                 "four-wave tile shapes");
@@ -111,6 +119,115 @@ __global__ __launch_bounds__(256) void gemm_4w_kernel(GemmArgs g) {
     for (int i = 0; i < IPW; ++i) stage_one(step, buf, i);
   };
 
+  cf32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) azero(acc[i][j]);
+  if constexpr (DEEP) {
+    constexpr int HB = (BM + BN) * 64;  // bytes per half-k region
+    constexpr int IPH = (BM + BN) / 64; // DMAs per wave per half (16 rows of 64 B each)
+    constexpr int NAH = BM / 64;        // of which A
+    static_assert(IPH * 2 == FM + FN, "a half's DMAs alternate with its fragment reads");
+    // DMA j of this wave fills half-rows (j * 4 + wave) * 16 + [0, 16); lane l -> row
+    // + l / 4, slot l % 4, holding chunk (l % 4) ^ F[(l >> 4) & 3] of the half
+    const int hrow = wave * 16 + (lane >> 2);
+    const int fsw = (0x78 >> (2 * ((lane >> 4) & 3))) & 3;
+    const int hch = (lane & 3) ^ fsw;
+    const uint32_t hvoff_a = (uint32_t)(((long long)(m0 + hrow) * g.lda + hch * 8) * 2);
+    long long hbrow;
+    if (!g.gated) hbrow = n0 + hrow;
+    else hbrow = ((wave & 1) ? (long long)g.half : 0LL) + (n0 / 32 + (wave >> 1)) * 16 + (lane >> 2);
+    const uint32_t hvoff_b = (uint32_t)((hbrow * g.ldb + hch * 8) * 2);
+    const uint32_t hstride_a = (uint32_t)(64LL * g.lda * 2);
+    const uint32_t hstride_b = (uint32_t)((g.gated ? 32LL : 64LL) * g.ldb * 2);
+    auto stage_half = [&](int step, int buf, int h, int j) __attribute__((always_inline)) {
+      const uint32_t ks = kbase + (uint32_t)step * (kGBK * 2) + (uint32_t)h * 64;
+      auto* dst = (__attribute__((address_space(3))) void*)(smem + (buf * 2 + h) * HB +
+                                                            (j * 4 + wave) * 1024);
+      const bool live = step < nk;
+      if (j < NAH)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            ra, dst, 16, hvoff_a, live ? (int)(ks + j * hstride_a) : 0x7fffffff, 0, 0);
+      else
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rb, dst, 16, hvoff_b, live ? (int)(ks + (j - NAH) * hstride_b) : 0x7fffffff, 0, 0);
+    };
+    // fragment (16 rows x 8 k) of tile row r0: row r0 + (l & 15), slot (l >> 4) ^ F[...]
+    const uint32_t lds0 = lds_off(smem);
+    const uint32_t foff = (uint32_t)(lane & 15) * 64 +
+                          (uint32_t)((((lane >> 4) & 3) ^ ((0x78 >> (2 * ((lane >> 2) & 3))) & 3)) * 16);
+    const uint32_t fa = lds0 + (uint32_t)(wr * WTM) * 64 + foff;
+    const uint32_t fb = lds0 + (uint32_t)(BM + wc * WTN) * 64 + foff;
+    constexpr int NM = FM * FN, NR = FM + FN;
+    uint4 af0[FM], bf0[FN], af1[FM], bf1[FN];
+    // prologue: both halves of steps 0 and 1, then step 0's k 0..31 fragments
+    for (int st = 0; st < 2; ++st)
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int j = 0; j < IPH; ++j) stage_half(st, st, h, j);
+    __builtin_amdgcn_s_waitcnt(vm_wait(2 * IPH));
+    asm volatile("s_barrier" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < FM; ++i) af0[i] = ds_read16(fa + i * 16 * 64);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) bf0[j] = ds_read16(fb + j * 16 * 64);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    auto half_step = [&](auto BI, int t) __attribute__((always_inline)) {
+      constexpr int b = decltype(BI)::value;
+      const uint32_t a1 = fa + (b * 2 + 1) * HB, b1 = fb + (b * 2 + 1) * HB;
+      const uint32_t a0n = fa + ((1 - b) * 2) * HB, b0n = fb + ((1 - b) * 2) * HB;
+      // MFMAs on k 0..31 of t | reads of t's k 32..63, the k 0..31 DMAs of t + 2
+      static_for<0, NM>([&](auto mi) __attribute__((always_inline)) {
+        constexpr int m = decltype(mi)::value;
+        amfma_v<DT>(acc[m / FN][m % FN], af0[m / FN], bf0[m % FN]);
+        static_for<(m * 2 * NR + NM - 1) / NM, ((m + 1) * 2 * NR + NM - 1) / NM>([&](auto li)
+                                                                        __attribute__((always_inline)) {
+          constexpr int l = decltype(li)::value;
+          if constexpr (l % 2 == 1) {
+            constexpr int r = l / 2;
+            if constexpr (r < FM) af1[r] = ds_read16_off<r * 16 * 64>(a1);
+            else bf1[r - FM] = ds_read16_off<(r - FM) * 16 * 64>(b1);
+          } else if constexpr ((l / 2) % 2 == 0) {  // DMAs spread over the phase
+            stage_half(t + 2, b, 0, l / 4);
+          }
+        });
+      });
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_waitcnt(vm_wait(2 * IPH));  // t + 1's k 0..31 landed
+      asm volatile("s_barrier" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      // MFMAs on k 32..63 of t | reads of t + 1's k 0..31, the k 32..63 DMAs of t + 2
+      static_for<0, NM>([&](auto mi) __attribute__((always_inline)) {
+        constexpr int m = decltype(mi)::value;
+        amfma_v<DT>(acc[m / FN][m % FN], af1[m / FN], bf1[m % FN]);
+        static_for<(m * 2 * NR + NM - 1) / NM, ((m + 1) * 2 * NR + NM - 1) / NM>([&](auto li)
+                                                                        __attribute__((always_inline)) {
+          constexpr int l = decltype(li)::value;
+          if constexpr (l % 2 == 1) {
+            constexpr int r = l / 2;
+            if constexpr (r < FM) af0[r] = ds_read16_off<r * 16 * 64>(a0n);
+            else bf0[r - FM] = ds_read16_off<(r - FM) * 16 * 64>(b0n);
+          } else if constexpr ((l / 2) % 2 == 0) {  // DMAs spread over the phase
+            stage_half(t + 2, b, 1, l / 4);
+          }
+        });
+      });
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_waitcnt(vm_wait(2 * IPH));  // t + 1's k 32..63 landed
+      asm volatile("s_barrier" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    using Z = std::integral_constant<int, 0>;
+    using O = std::integral_constant<int, 1>;
+    for (int t = 0; t < nk; t += 2) {
+      half_step(Z{}, t);
+      if (t + 1 < nk) half_step(O{}, t + 1);
+    }
+  } else {
   // ---- fragment addresses (as gemm_kernel) ----------------------------------
   const int swz = (lane & 15) >> 1;
   const uint32_t lrow = (uint32_t)(lane & 15) * 128;
@@ -120,11 +237,6 @@ __global__ __launch_bounds__(256) void gemm_4w_kernel(GemmArgs g) {
   const uint32_t a_base = lds0 + (uint32_t)(wr * WTM) * 128 + lrow;
   const uint32_t b_base = lds0 + (uint32_t)(BM + wc * WTN) * 128 + lrow;
 
-  cf32x4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) azero(acc[i][j]);
 
   // The interleaved two-stage schedule of gemm_kernel (IL, NS = 2):
   //   [kk1 reads of t | kk0 MFMAs of t] wait | vmcnt(DMA t+1) barrier
@@ -182,6 +294,8 @@ __global__ __launch_bounds__(256) void gemm_4w_kernel(GemmArgs g) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     buf = nbuf;
+  }
+
   }
 
   // ---- epilogue (as gemm_kernel) -----------------------------------------

@@ -14,8 +14,9 @@ bsize > 1 (the UNet over 2 bsize rows, the reference's repeated text rows), inte
 images (decoded by the engine between steps, handed back through a callback) and tracing
 (the Chrome trace spans — text embeddings, every step, VAE decode — rebuilt from the
 engine's own phase and per-step device timings) are native (img2img with a remote VAE
-too: the worker encodes and draws the sample); img2img with bsize > 1 runs on
-the Python pipeline, built on first use.
+too: the worker encodes and draws the sample; img2img at bsize > 1 starts every image from
+the encoded image with its own noise draw, as pipeline.py does).  Only an img2img image
+whose size is not the engine's runs on the Python pipeline, built on first use.
 """
 from __future__ import annotations
 
@@ -100,8 +101,7 @@ class NativeSDGenerator(ImageGenerator):
 
     def _python(self) -> ImageGenerator:
         if self._fallback is None:
-            log.info("request needs the Python pipeline (img2img at bsize > 1, or an image of "
-                     "another size)")
+            log.info("request needs the Python pipeline (an img2img image of another size)")
             self._fallback = self._fallback_factory()
         return self._fallback
 
@@ -127,7 +127,7 @@ class NativeSDGenerator(ImageGenerator):
 
     def generate_image(self, args: ImageGenerationArgs, callback: Callable[[list], None]) -> None:
         init = None
-        if args.img2img and args.bsize == 1:
+        if args.img2img:
             if not 0.0 <= args.img2img_strength <= 1.0:
                 raise ValueError("img2img-strength should be between 0 and 1, got "
                                  f"{args.img2img_strength}")
@@ -175,21 +175,23 @@ class NativeSDGenerator(ImageGenerator):
                 from .schedulers import build_scheduler
                 sched = build_scheduler(cfg.scheduler, n_steps)
                 ts = sched.timesteps()
-                latents = init.float() * cfg.vae_scale
+                # bsize > 1: every image starts from the encoded image, each with its own
+                # noise draw (pipeline.py repeats the latent the same way)
+                latents = init.float().repeat(bsize, 1, 1, 1) * cfg.vae_scale
                 if t_start < len(ts):
                     noise = torch.randn(latents.shape, generator=gen).to(latents.device)
                     latents = sched.add_noise(latents, noise, ts[t_start])
                 latents = latents.float()
                 if t_start >= len(ts):  # strength 0: the encoded image itself
-                    img = self.eng.vae_decode((latents / cfg.vae_scale).cpu().numpy())
+                    img = self.eng.vae_decode((latents[:1] / cfg.vae_scale).cpu().numpy())
                     rgb = ((np.clip(img[0] / 2 + 0.5, 0, 1) * 255).astype(np.uint8)
                            .transpose(1, 2, 0).copy())
-                    callback([Image.fromarray(rgb, "RGB")])
+                    callback([Image.fromarray(rgb, "RGB")] * bsize)
                     continue
                 seed = int(torch.randint(0, 2 ** 62, (1,), generator=gen).item())
                 out = self.eng.generate(n_steps=n_steps, guidance=guidance, seed=seed,
                                         init_latents=latents.cpu().numpy(), t_start=t_start,
-                                        **kw, **mid)
+                                        bsize=bsize, **kw, **mid)
             else:
                 # the Python pipeline's draw order: latent noise, then the ancestral-noise key
                 noise = torch.randn((bsize, 4, cfg.height // 8, cfg.width // 8), generator=gen)

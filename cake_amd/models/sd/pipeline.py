@@ -219,7 +219,9 @@ class SDGenerator(ImageGenerator):
         for idx in range(args.num_samples):
             ts = sched.timesteps()
             if init is not None:
-                latents = init * cfg.vae_scale
+                # bsize > 1: each image starts from the encoded image with its own noise
+                # (the reference's latent stays batch 1 against bsize text rows)
+                latents = init.repeat(args.bsize, 1, 1, 1) * cfg.vae_scale
                 if t_start < len(ts):
                     noise = torch.randn(latents.shape, generator=gen).to(self.device)
                     latents = sched.add_noise(latents, noise, ts[t_start])

@@ -27,19 +27,19 @@ CFG_TILES = {0: (128, 128), 1: (64, 128), 2: (256, 128), 3: (128, 256), 4: (64, 
              12: (64, 128), 13: (64, 64), 14: (64, 160), 15: (64, 160), 16: (128, 160),
              17: (128, 160), 18: (64, 160), 19: (128, 160), 20: (256, 256), 21: (256, 256),
              22: (256, 256), 23: (256, 192),
-             24: (128, 256)}
+             24: (128, 256), 25: (256, 256), 26: (256, 192), 27: (128, 256)}
 _SLOTS = {0: 2, 1: 2, 2: 1, 3: 1, 4: 4, 5: 1, 6: 1, 7: 1, 8: 2, 11: 1, 12: 2, 13: 2,
-          14: 2, 15: 2, 16: 1, 17: 1, 18: 1, 19: 1, 20: 1, 21: 1, 22: 1, 23: 1, 24: 1}  # WGs/CU
+          14: 2, 15: 2, 16: 1, 17: 1, 18: 1, 19: 1, 20: 1, 21: 1, 22: 1, 23: 1, 24: 1, 25: 1, 26: 1, 27: 1}  # WGs/CU
 # 80-column wave tiles (two waves across the 160 columns): no gated epilogue
 NO_GATED = {14, 17, 18, 19}
 # register-staged / four-wave 256x256 (gemm_rs.h, gemm_4w.h): whole 64-element k steps only
-K64_ONLY = {21, 22, 23, 24}
+K64_ONLY = {21, 22, 23, 24, 25, 26, 27}
 # relative per-tile throughput (measured per-config sweep,
 # profiles/r2_gemm_sweep_agpr.jsonl): the AGPR-accumulator 128x128 tile (0) for most
 # shapes, the 8-wave 256x256 tile (11) where its tiles fill the chip, 64-wide tiles
 # (1, 4) for short M
 _EFF = {0: 1.0, 1: 0.8, 2: 0.8, 3: 0.8, 4: 0.7, 5: 1.2, 6: 0.95, 7: 0.9, 8: 0.9, 11: 1.1,
-        12: 0.8, 13: 0.7, 14: 0.8, 15: 0.7, 16: 0.9, 17: 0.9, 18: 0.8, 19: 0.9, 20: 1.2, 21: 1.3, 22: 1.3, 23: 1.3, 24: 1.2}
+        12: 0.8, 13: 0.7, 14: 0.8, 15: 0.7, 16: 0.9, 17: 0.9, 18: 0.8, 19: 0.9, 20: 1.2, 21: 1.3, 22: 1.3, 23: 1.3, 24: 1.2, 25: 1.3, 26: 1.3, 27: 1.2}
 NUM_CUS = 256
 # plan cfg of the library GEMM (hipBLASLt, csrc/driver/blaslt.cpp), kept as the A/B arm of
 # scripts/bench_gemm_lib.py: off the default path (table entries naming it are read only

@@ -202,8 +202,8 @@ class NativeSD:
                  bsize: int = 1, intermediary: int = 0, on_image=None) -> SdImage:
         """One sample from padded [77] id rows (uncond = None: no classifier-free
         guidance; cond2 / uncond2: the second tokenizer's ids for xl / turbo).  img2img:
-        init_latents [4, h, w] (the encoded image scaled and noised to the schedule's step
-        t_start) and the steps from t_start on.  bsize images per sample (init_noise then
+        init_latents [bsize, 4, h, w] (the encoded image scaled and noised to the schedule's
+        step t_start, one noise draw per image) and the steps from t_start on.  bsize images per sample (init_noise then
         [bsize, 4, h, w]); intermediary > 0: on_image(step, rgb [n, H, W, 3]) after every
         step index divisible by it."""
         ids = [None if x is None else _ids(x).reshape(-1) for x in (cond, uncond, cond2, uncond2)]
@@ -216,8 +216,8 @@ class NativeSD:
         if noise is not None and noise.size != 4 * h * w * bsize:
             raise ValueError(f"init_noise must hold {4 * h * w * bsize} values")
         lat0 = None if init_latents is None else _f32(init_latents).reshape(-1)
-        if lat0 is not None and lat0.size != 4 * h * w:
-            raise ValueError(f"init_latents must hold {4 * h * w} values")
+        if lat0 is not None and lat0.size != 4 * h * w * bsize:
+            raise ValueError(f"init_latents must hold {4 * h * w * bsize} values")
         err_cb: list = []
 
         def _cb(_ctx, step, n, ptr):

@@ -25,7 +25,7 @@ def _close(got, ref, K):
 
 
 @pytest.mark.parametrize("dt", DTYPES)
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7, 8, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7, 8, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27])
 @pytest.mark.parametrize("M,N,K,splits", [(128, 256, 256, 1), (77, 200, 320, 1),
                                           (300, 520, 1024, 3), (1, 64, 64, 1),
                                           (513, 136, 648, 2)])
@@ -140,7 +140,7 @@ def test_gemm_model_shapes(cuda, name, M, N, K, epi):
 
 
 @pytest.mark.parametrize("dt", DTYPES)
-@pytest.mark.parametrize("cfg", [5, 0, 13, 14, 15, 16, 17, 20, 21, 22, 23, 24])
+@pytest.mark.parametrize("cfg", [5, 0, 13, 14, 15, 16, 17, 20, 21, 22, 23, 24, 25, 26, 27])
 @pytest.mark.parametrize("M,N,K", [(300, 700, 640), (257, 272, 2112), (520, 776, 200)])
 def test_gemm_interleaved_all_epilogues(cuda, dt, cfg, M, N, K):
     """Interleaved-schedule tiles with ragged M/N and every epilogue."""
@@ -270,7 +270,7 @@ def test_library_gemm_plan_cache_eviction(cuda):
 @pytest.mark.parametrize("dt", DTYPES)
 @pytest.mark.parametrize("M,N,K,splits", [(2048, 6144, 4096, 1), (1000, 4096, 14336, 2),
                                           (2048, 2 * 14336, 4096, 1), (2048, 2 * 14336, 4096, 2)])
-@pytest.mark.parametrize("cfg", [20, 21, 22, 23, 24])
+@pytest.mark.parametrize("cfg", [20, 21, 22, 23, 24, 25, 26, 27])
 def test_big_tile_gemm_llama_shapes(cuda, dt, M, N, K, splits, cfg):
     """The ping-pong (cfg 20) and register-staged (cfg 21) 256x256 kernels on Llama
     prefill shapes: plain store, f32 residual accumulate (split-K included) and the fused
@@ -292,7 +292,7 @@ def test_big_tile_gemm_llama_shapes(cuda, dt, M, N, K, splits, cfg):
 
 
 @pytest.mark.parametrize("epi", ["store", "resid32", "swiglu"])
-@pytest.mark.parametrize("cfg", [22, 23, 24])
+@pytest.mark.parametrize("cfg", [22, 23, 24, 25, 26, 27])
 def test_four_wave_split_pair(cuda, epi, cfg):
     """cfg 22 with split-K 2 runs the in-kernel pair (the first split of a tile parks its
     accumulators, the second adds them and runs the epilogue; gemm_4w.h): equal to the

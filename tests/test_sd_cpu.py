@@ -52,6 +52,11 @@ def test_generate_local(sd_dir, tmp_path):
     gen.generate_image(ImageGenerationArgs(n_steps=4, img2img=str(src), img2img_strength=0.5,
                                            image_seed=1), lambda imgs: out.append(imgs))
     assert out and out[-1][0].size == (64, 64)
+    # img2img at bsize 2: both images from the encoded image, each with its own noise
+    out2 = []
+    gen.generate_image(ImageGenerationArgs(n_steps=4, img2img=str(src), img2img_strength=0.5,
+                                           image_seed=1, bsize=2), lambda imgs: out2.append(imgs))
+    assert len(out2[-1]) == 2 and all(im.size == (64, 64) for im in out2[-1])
 
 
 def test_unet_on_worker_matches_local(tmp_path):

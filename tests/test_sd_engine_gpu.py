@@ -270,9 +270,11 @@ def test_native_sd_tcp_worker_serves_the_unet(cuda, mini, tmp_path, monkeypatch)
     assert diff.mean() < 2.0 and diff.max() <= 32, (diff.mean(), diff.max())
 
 
-def test_img2img_on_the_native_engine_matches_python(cuda, mini, tmp_path, monkeypatch):
+@pytest.mark.parametrize("bsize", [1, 2])
+def test_img2img_on_the_native_engine_matches_python(cuda, mini, tmp_path, monkeypatch, bsize):
     """img2img natively (the engine's VAE encoder, the pipeline's sampling and noise draws,
-    the denoise from t_start) gives the Python pipeline's image."""
+    the denoise from t_start) gives the Python pipeline's image; at bsize 2 both images
+    start from the encoded image with their own noise."""
     from cake_amd.cli import build_parser
     from cake_amd.context import Context
     from cake_amd.master import _load_image
@@ -295,7 +297,7 @@ def test_img2img_on_the_native_engine_matches_python(cuda, mini, tmp_path, monke
     path = tmp_path / "src.png"
     src[-1][0].save(path)
     req = ImageGenerationArgs(image_prompt="a red cube", n_steps=4, img2img=str(path),
-                              img2img_strength=0.5, image_seed=8)
+                              img2img_strength=0.5, image_seed=8, bsize=bsize)
     got = []
     native.generate_image(req, lambda imgs: got.append(imgs))
     assert native._fallback is None  # served natively
@@ -304,10 +306,14 @@ def test_img2img_on_the_native_engine_matches_python(cuda, mini, tmp_path, monke
     py = _load_image(ctx)
     ref = []
     py.generate_image(req, lambda imgs: ref.append(imgs))
-    a = np.asarray(got[-1][0], dtype=np.int32)
-    b = np.asarray(ref[-1][0], dtype=np.int32)
-    assert np.abs(a - b).mean() < 0.5 and np.abs(a - b).max() <= 8, (np.abs(a - b).mean(),
-                                                                     np.abs(a - b).max())
+    assert len(got[-1]) == len(ref[-1]) == bsize
+    for k in range(bsize):
+        a = np.asarray(got[-1][k], dtype=np.int32)
+        b = np.asarray(ref[-1][k], dtype=np.int32)
+        assert np.abs(a - b).mean() < 0.5 and np.abs(a - b).max() <= 8, (
+            k, np.abs(a - b).mean(), np.abs(a - b).max())
+    if bsize > 1:  # distinct noise per image
+        assert np.abs(np.asarray(got[-1][0], np.int32) - np.asarray(got[-1][1], np.int32)).max() > 0
 
 
 def test_bsize_and_intermediary_images_on_the_native_engine(cuda, mini, tmp_path, monkeypatch):
