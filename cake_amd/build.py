@@ -116,8 +116,10 @@ def build_kernels(force: bool = False, jobs: int = 8) -> Path:
     if force or stale or any(_newer(o, [], KERNEL_LIB) for o in objs):
         # hipBLASLt for the plain prefill GEMMs it measured faster on (driver/blaslt.cpp);
         # in a torch process the soname resolves to the copy torch already loaded
+        # --no-undefined: a kernel whose host stub the compiler dropped fails here, not at
+        # dlopen on the GPU box
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs),
-              "-o", str(KERNEL_LIB), "-L/opt/rocm/lib", "-lhipblaslt"])
+              "-o", str(KERNEL_LIB), "-L/opt/rocm/lib", "-lhipblaslt", "-Wl,--no-undefined"])
     return KERNEL_LIB
 
 

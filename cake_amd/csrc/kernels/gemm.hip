@@ -64,7 +64,7 @@ static unsigned* pair_ticks() {
 }
 
 static inline void cfg_dims(int cfg, int& bm, int& bn) {
-  if (cfg >= k4WCfg + k4WDeep && cfg <= k4WCfg128 + k4WDeep) cfg -= k4WDeep;  // DEEP twins
+  if (cfg >= k4WCfg + k4WSched && cfg <= k4WCfg128 + k4WSched) cfg -= k4WSched;  // three-barrier twins
   if (cfg == kPPCfg || cfg == kRSCfg || cfg == k4WCfg) { bm = bn = 256; return; }
   if (cfg == k4WCfg192) { bm = 256; bn = 192; return; }
   if (cfg == k4WCfg128) { bm = 128; bn = 256; return; }

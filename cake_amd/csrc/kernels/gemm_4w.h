@@ -20,22 +20,69 @@
 //   (host-checked).
 #pragma once
 
+// Diagnostic build only (scripts/gemm_stamp.hip defines CAKE_GEMM_STAMPS and the
+// g_gemm_stamps buffer): s_memtime at the k-loop's segment boundaries, summed per wave.
+#ifdef CAKE_GEMM_STAMPS
+#define CAKE_STAMP(v)                                                                   \
+  do {                                                                                  \
+    __builtin_amdgcn_sched_barrier(0);                                                  \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory");           \
+    __builtin_amdgcn_sched_barrier(0);                                                  \
+  } while (0)
+#else
+#define CAKE_STAMP(v) \
+  do {                \
+  } while (0)
+#endif
+
 namespace cake {
 
 constexpr int k4WCfg = 22;     // plan cfg id of the 256 x 256 tile
 constexpr int k4WCfg192 = 23;  // 256 x 192 (8B q|k|v: 6144 = 32 x 192 columns, 256 tiles at
                                // 2048 tokens instead of 192)
 constexpr int k4WCfg128 = 24;  // 128 x 256 (8B o / down at 2048 tokens: 256 tiles, not 128)
-constexpr int k4WDeep = 3;     // cfg + 3: the same tiles with DEEP staging (25, 26, 27)
-inline bool four_wave_cfg(int cfg) { return cfg >= k4WCfg && cfg <= k4WCfg128 + k4WDeep; }
+constexpr int k4WSched = 3;    // cfg + 3: the same tiles on the three-barrier schedule (25-27)
+inline bool four_wave_cfg(int cfg) { return cfg >= k4WCfg && cfg <= k4WCfg128 + k4WSched; }
+// op k of an alternating sequence of nr reads and nd DMAs (the longer list's tail last):
+// kind 0 = read, 1 = DMA, and its index within its list
+constexpr int alt_kind(int nr, int nd, int k) {
+  return k < 2 * (nr < nd ? nr : nd) ? k % 2 : (nr > nd ? 0 : 1);
+}
+constexpr int alt_idx(int nr, int nd, int k) {
+  const int mn = nr < nd ? nr : nd;
+  return k < 2 * mn ? k / 2 : mn + (k - 2 * mn);
+}
 
-// DEEP (cfg 25-27): the LDS image split by k half, so each half of step t+2 is staged as
-// soon as the half of step t it replaces has been read (kk0 half during the first MFMA
-// half of step t, kk1 half during the second), two barriers per step with vmcnt(2 x the
-// half's DMAs): a DMA has ~1.5 steps to land instead of ~0.5-1.  Half-rows are 64 bytes
-// (four 16-byte slots); slot s of row r holds chunk s ^ F[(r >> 2) & 3], F = {0, 2, 3, 1},
-// which spreads every ds_read_b128 lane group over 16 distinct bank quads.
-template <int DT, int EPI, int BM, int BN, bool DEEP = false>
+// LDS-DMA of one 1 KiB piece (buffer_load_dwordx4 ... offen lds) with the M0 write in the
+// same statement (M0 is not preserved around inline asm); d = the buffer descriptor as an
+// SGPR quad.  amfma_dma issues an MFMA between the M0 write and the DMA, which covers the
+// write's wait state (no s_nop) and keeps the DMA beside the MFMA it was scheduled with.
+template <int OFF>
+__device__ __forceinline__ void dma16(uint32_t mb, uint32_t voff, cu32x4 d, uint32_t soff) {
+  asm volatile("s_add_u32 m0, %0, %4\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+               :: "s"(mb), "v"(voff), "s"(d), "s"(soff), "i"(OFF) : "memory");
+}
+template <int DT, int OFF>
+__device__ __forceinline__ void amfma_dma(cf32x4& acc, const uint4& a, const uint4& b, uint32_t mb,
+                                          uint32_t voff, cu32x4 d, uint32_t soff) {
+  const cu32x4 av = __builtin_bit_cast(cu32x4, a), bv = __builtin_bit_cast(cu32x4, b);
+  if constexpr (DT == kBF16)
+    asm volatile("s_add_u32 m0, %3, %7\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0\n\t"
+                 "buffer_load_dwordx4 %4, %5, %6 offen lds"
+                 : "+a"(acc)
+                 : "v"(av), "v"(bv), "s"(mb), "v"(voff), "s"(d), "s"(soff), "i"(OFF)
+                 : "memory");
+  else
+    asm volatile("s_add_u32 m0, %3, %7\n\tv_mfma_f32_16x16x32_f16 %0, %1, %2, %0\n\t"
+                 "buffer_load_dwordx4 %4, %5, %6 offen lds"
+                 : "+a"(acc)
+                 : "v"(av), "v"(bv), "s"(mb), "v"(voff), "s"(d), "s"(soff), "i"(OFF)
+                 : "memory");
+}
+
+// SCHED 1 (cfg 25-27): the same tiles on a three-barrier schedule (the DMAs of step t+2
+// issued as soon as every wave has read the operand region they overwrite).
+template <int DT, int EPI, int BM, int BN, int SCHED = 0>
 __global__ __launch_bounds__(256) void gemm_4w_kernel(GemmArgs g) {
   static_assert((BM == 256 && (BN == 256 || BN == 192)) || (BM == 128 && BN == 256),
                 "four-wave tile shapes");
@@ -87,36 +134,58 @@ __global__ __launch_bounds__(256) void gemm_4w_kernel(GemmArgs g) {
   const int rA = wave * 8 + (lane >> 3);
   const int chunk = (lane & 7) ^ ((rA >> 1) & 7);
   const long long brows = g.gated ? 2LL * g.half : (long long)g.Nv;
-  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint16_t*>(g.a), (short)0, (int)(((long long)(g.M - 1) * g.lda + g.K) * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint16_t*>(g.b), (short)0, (int)(((brows - 1) * g.ldb + g.K) * 2), 0x00020000);
+  const int nrec_a = (int)(((long long)(g.M - 1) * g.lda + g.K) * 2);
+  const int nrec_b = (int)(((brows - 1) * g.ldb + g.K) * 2);
   const uint32_t voff_a = (uint32_t)(((long long)(m0 + rA) * g.lda + chunk * 8) * 2);
   long long brow0;  // weight row of this lane in B group 0
   if (!g.gated) brow0 = n0 + rA;
   else brow0 = (rA < 16 ? 0LL : (long long)g.half - 16) + n0 / 2 + rA;
   const uint32_t voff_b = (uint32_t)((brow0 * g.ldb + chunk * 8) * 2);
   // scalar byte offsets of each 32-row group (A: 32 rows; B: 32 virtual rows = 16
-  // weight rows of each half when gated)
+  // weight rows of each half when gated): loop-invariant SGPRs
   const uint32_t gstride_a = (uint32_t)(32LL * g.lda * 2);
   const uint32_t gstride_b = (uint32_t)((g.gated ? 16LL : 32LL) * g.ldb * 2);
-  const uint32_t kbase = (uint32_t)kb * 2;
-  // a step past the split's end: soffset 2^31 - 1 puts every lane out of range (zeros,
-  // no memory traffic; voffsets stay below 2^31, so the sum cannot wrap)
-  auto stage_one = [&](int step, int buf, int i) __attribute__((always_inline)) {
-    const uint32_t ks = kbase + (uint32_t)step * (kGBK * 2);
-    auto* dst = (__attribute__((address_space(3))) void*)(smem + buf * BUF + (i * 4 + wave) * 1024);
-    const bool live = step < nk;
-    if (i < NA)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          ra, dst, 16, voff_a, live ? (int)(ks + i * gstride_a) : 0x7fffffff, 0, 0);
-    else
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rb, dst, 16, voff_b, live ? (int)(ks + (i - NA) * gstride_b) : 0x7fffffff, 0, 0);
+  // The k step lives in the descriptors: base advanced to the step's first column and
+  // num_records shrunk by as much (a step past the split's end: 0 records, every lane out
+  // of range -> zeros, no memory traffic).  Per DMA that leaves the M0 write and the DMA
+  // itself in the MFMA stream, the rest is a handful of scalar ops per k-step.
+  // descriptor words: base (48 bits, stride 0), num_records, flags (raw, offen)
+  auto desc_at = [&](const uint16_t* base, int nrec, int step) __attribute__((always_inline)) {
+    const int k0 = kb + step * kGBK;
+    const unsigned long long p = (unsigned long long)(base + k0);
+    cu32x4 d;
+    d[0] = __builtin_amdgcn_readfirstlane((unsigned)p);
+    d[1] = __builtin_amdgcn_readfirstlane((unsigned)(p >> 32) & 0xFFFFu);
+    d[2] = __builtin_amdgcn_readfirstlane(step < nk ? (unsigned)(nrec - 2 * k0) : 0u);
+    d[3] = 0x00020000u;
+    return d;
+  };
+  auto src_a = [&](int step) __attribute__((always_inline)) { return desc_at(g.a, nrec_a, step); };
+  auto src_b = [&](int step) __attribute__((always_inline)) { return desc_at(g.b, nrec_b, step); };
+  const uint32_t m0_base = __builtin_amdgcn_readfirstlane(lds_off(smem) + (uint32_t)wave * 1024);
+  // M0 (= buffer base + 4 KiB per piece, the piece offset an immediate) / voffset / soffset
+  // of DMA I (A pieces for I < NA) into buffer buf
+  auto dma_mb = [&](int buf) __attribute__((always_inline)) {
+    return m0_base + (uint32_t)(buf * BUF);
+  };
+  auto dma_voff = [&](int i) __attribute__((always_inline)) { return i < NA ? voff_a : voff_b; };
+  auto dma_soff = [&](int i) __attribute__((always_inline)) {
+    return i < NA ? (uint32_t)i * gstride_a : (uint32_t)(i - NA) * gstride_b;
+  };
+  auto stage_one = [&](const cu32x4& sa, const cu32x4& sb, int buf, auto I)
+                       __attribute__((always_inline)) {
+    constexpr int i = decltype(I)::value;
+    dma16<i * 4096>(dma_mb(buf), dma_voff(i), i < NA ? sa : sb, dma_soff(i));
+  };
+  // MFMA with DMA I fused behind it
+  auto mfma_dma = [&](cf32x4& c, const uint4& a, const uint4& b, const cu32x4& sa,
+                      const cu32x4& sb, int buf, auto I) __attribute__((always_inline)) {
+    constexpr int i = decltype(I)::value;
+    amfma_dma<DT, i * 4096>(c, a, b, dma_mb(buf), dma_voff(i), i < NA ? sa : sb, dma_soff(i));
   };
   auto stage = [&](int step, int buf) {
-#pragma unroll
-    for (int i = 0; i < IPW; ++i) stage_one(step, buf, i);
+    const cu32x4 sa = src_a(step), sb = src_b(step);
+    static_for<0, IPW>([&](auto I) __attribute__((always_inline)) { stage_one(sa, sb, buf, I); });
   };
 
   cf32x4 acc[FM][FN];
@@ -124,110 +193,6 @@ __global__ __launch_bounds__(256) void gemm_4w_kernel(GemmArgs g) {
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < FN; ++j) azero(acc[i][j]);
-  if constexpr (DEEP) {
-    constexpr int HB = (BM + BN) * 64;  // bytes per half-k region
-    constexpr int IPH = (BM + BN) / 64; // DMAs per wave per half (16 rows of 64 B each)
-    constexpr int NAH = BM / 64;        // of which A
-    static_assert(IPH * 2 == FM + FN, "a half's DMAs alternate with its fragment reads");
-    // DMA j of this wave fills half-rows (j * 4 + wave) * 16 + [0, 16); lane l -> row
-    // + l / 4, slot l % 4, holding chunk (l % 4) ^ F[(l >> 4) & 3] of the half
-    const int hrow = wave * 16 + (lane >> 2);
-    const int fsw = (0x78 >> (2 * ((lane >> 4) & 3))) & 3;
-    const int hch = (lane & 3) ^ fsw;
-    const uint32_t hvoff_a = (uint32_t)(((long long)(m0 + hrow) * g.lda + hch * 8) * 2);
-    long long hbrow;
-    if (!g.gated) hbrow = n0 + hrow;
-    else hbrow = ((wave & 1) ? (long long)g.half : 0LL) + (n0 / 32 + (wave >> 1)) * 16 + (lane >> 2);
-    const uint32_t hvoff_b = (uint32_t)((hbrow * g.ldb + hch * 8) * 2);
-    const uint32_t hstride_a = (uint32_t)(64LL * g.lda * 2);
-    const uint32_t hstride_b = (uint32_t)((g.gated ? 32LL : 64LL) * g.ldb * 2);
-    auto stage_half = [&](int step, int buf, int h, int j) __attribute__((always_inline)) {
-      const uint32_t ks = kbase + (uint32_t)step * (kGBK * 2) + (uint32_t)h * 64;
-      auto* dst = (__attribute__((address_space(3))) void*)(smem + (buf * 2 + h) * HB +
-                                                            (j * 4 + wave) * 1024);
-      const bool live = step < nk;
-      if (j < NAH)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            ra, dst, 16, hvoff_a, live ? (int)(ks + j * hstride_a) : 0x7fffffff, 0, 0);
-      else
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            rb, dst, 16, hvoff_b, live ? (int)(ks + (j - NAH) * hstride_b) : 0x7fffffff, 0, 0);
-    };
-    // fragment (16 rows x 8 k) of tile row r0: row r0 + (l & 15), slot (l >> 4) ^ F[...]
-    const uint32_t lds0 = lds_off(smem);
-    const uint32_t foff = (uint32_t)(lane & 15) * 64 +
-                          (uint32_t)((((lane >> 4) & 3) ^ ((0x78 >> (2 * ((lane >> 2) & 3))) & 3)) * 16);
-    const uint32_t fa = lds0 + (uint32_t)(wr * WTM) * 64 + foff;
-    const uint32_t fb = lds0 + (uint32_t)(BM + wc * WTN) * 64 + foff;
-    constexpr int NM = FM * FN, NR = FM + FN;
-    uint4 af0[FM], bf0[FN], af1[FM], bf1[FN];
-    // prologue: both halves of steps 0 and 1, then step 0's k 0..31 fragments
-    for (int st = 0; st < 2; ++st)
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int j = 0; j < IPH; ++j) stage_half(st, st, h, j);
-    __builtin_amdgcn_s_waitcnt(vm_wait(2 * IPH));
-    asm volatile("s_barrier" ::: "memory");
-#pragma unroll
-    for (int i = 0; i < FM; ++i) af0[i] = ds_read16(fa + i * 16 * 64);
-#pragma unroll
-    for (int j = 0; j < FN; ++j) bf0[j] = ds_read16(fb + j * 16 * 64);
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    auto half_step = [&](auto BI, int t) __attribute__((always_inline)) {
-      constexpr int b = decltype(BI)::value;
-      const uint32_t a1 = fa + (b * 2 + 1) * HB, b1 = fb + (b * 2 + 1) * HB;
-      const uint32_t a0n = fa + ((1 - b) * 2) * HB, b0n = fb + ((1 - b) * 2) * HB;
-      // MFMAs on k 0..31 of t | reads of t's k 32..63, the k 0..31 DMAs of t + 2
-      static_for<0, NM>([&](auto mi) __attribute__((always_inline)) {
-        constexpr int m = decltype(mi)::value;
-        amfma_v<DT>(acc[m / FN][m % FN], af0[m / FN], bf0[m % FN]);
-        static_for<(m * 2 * NR + NM - 1) / NM, ((m + 1) * 2 * NR + NM - 1) / NM>([&](auto li)
-                                                                        __attribute__((always_inline)) {
-          constexpr int l = decltype(li)::value;
-          if constexpr (l % 2 == 1) {
-            constexpr int r = l / 2;
-            if constexpr (r < FM) af1[r] = ds_read16_off<r * 16 * 64>(a1);
-            else bf1[r - FM] = ds_read16_off<(r - FM) * 16 * 64>(b1);
-          } else if constexpr ((l / 2) % 2 == 0) {  // DMAs spread over the phase
-            stage_half(t + 2, b, 0, l / 4);
-          }
-        });
-      });
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_waitcnt(vm_wait(2 * IPH));  // t + 1's k 0..31 landed
-      asm volatile("s_barrier" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      // MFMAs on k 32..63 of t | reads of t + 1's k 0..31, the k 32..63 DMAs of t + 2
-      static_for<0, NM>([&](auto mi) __attribute__((always_inline)) {
-        constexpr int m = decltype(mi)::value;
-        amfma_v<DT>(acc[m / FN][m % FN], af1[m / FN], bf1[m % FN]);
-        static_for<(m * 2 * NR + NM - 1) / NM, ((m + 1) * 2 * NR + NM - 1) / NM>([&](auto li)
-                                                                        __attribute__((always_inline)) {
-          constexpr int l = decltype(li)::value;
-          if constexpr (l % 2 == 1) {
-            constexpr int r = l / 2;
-            if constexpr (r < FM) af0[r] = ds_read16_off<r * 16 * 64>(a0n);
-            else bf0[r - FM] = ds_read16_off<(r - FM) * 16 * 64>(b0n);
-          } else if constexpr ((l / 2) % 2 == 0) {  // DMAs spread over the phase
-            stage_half(t + 2, b, 1, l / 4);
-          }
-        });
-      });
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_waitcnt(vm_wait(2 * IPH));  // t + 1's k 32..63 landed
-      asm volatile("s_barrier" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-    };
-    using Z = std::integral_constant<int, 0>;
-    using O = std::integral_constant<int, 1>;
-    for (int t = 0; t < nk; t += 2) {
-      half_step(Z{}, t);
-      if (t + 1 < nk) half_step(O{}, t + 1);
-    }
-  } else {
   // ---- fragment addresses (as gemm_kernel) ----------------------------------
   const int swz = (lane & 15) >> 1;
   const uint32_t lrow = (uint32_t)(lane & 15) * 128;
@@ -236,15 +201,113 @@ __global__ __launch_bounds__(256) void gemm_4w_kernel(GemmArgs g) {
   const uint32_t lds0 = lds_off(smem);
   const uint32_t a_base = lds0 + (uint32_t)(wr * WTM) * 128 + lrow;
   const uint32_t b_base = lds0 + (uint32_t)(BM + wc * WTN) * 128 + lrow;
+  constexpr int NM = FM * FN, NR = FM + FN, NB = IPW - NA;
+  uint4 af0[FM], bf0[FN], af1[FM], bf1[FN];
 
+  if constexpr (SCHED == 1) {
+    // Three barriers per k-step; a step's operand regions are restaged as soon as every
+    // wave has read them, so the DMAs spread over two thirds of the step:
+    //   phase 1 (k 0..31 MFMAs of t): [B k 32..63 reads] lgkm+barrier (B of t free)
+    //     [A k 32..63 reads + B DMAs of t+2] lgkm+barrier (A of t free) [A DMAs]
+    //   phase 2 (k 32..63 MFMAs of t): [A DMAs] vmcnt(this step's) + barrier
+    //     (t+1 landed) [k 0..31 reads of t+1] lgkm
+    // Each wait + barrier follows an MFMA issue, so the pipe runs while the waves align.
+    // (placements measured: barriers at NM/8 and NM/2, or all A DMAs before phase 2 with its
+    // barrier at MFMA 1, ran within 3 % / 3-6 % slower, profiles/r6_gemm_three_barrier_ab.txt)
+    constexpr int Q1 = NM / 4, Q2 = (NM * 5) / 8, P1 = NM / 4;
+    constexpr int NA1 = NA / 2;  // A DMAs in phase 1's tail, the rest in phase 2's head
+    static_assert(Q1 >= FN / 2 && Q2 - Q1 - 1 >= (FM + NB) / 2, "op density");
+    stage(0, 0);
+    stage(1, 1);
+    __builtin_amdgcn_s_waitcnt(vm_wait(IPW));
+    asm volatile("s_barrier" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < FM; ++i) af0[i] = ds_read16(a_base + i * 16 * 128 + off0);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) bf0[j] = ds_read16(b_base + j * 16 * 128 + off0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    int buf = 0;
+    for (int t = 0; t < nk; ++t) {
+      const uint32_t ab = a_base + buf * BUF, bb = b_base + buf * BUF;
+      const int nbuf = buf ^ 1;
+      const uint32_t na = a_base + nbuf * BUF, nb = b_base + nbuf * BUF;
+      const cu32x4 sa = src_a(t + 2), sb = src_b(t + 2);
+      // ops k of n spread over MFMAs [lo, hi): op k after MFMA lo + floor(k (hi-lo) / n)
+      static_for<0, NM>([&](auto mi) __attribute__((always_inline)) {
+        constexpr int m = decltype(mi)::value;
+        // the first op placed after this MFMA, when it is a DMA, goes in the MFMA's statement
+        constexpr int L2 = Q2 - Q1 - 1, n2 = FM + NB, m2 = m - Q1 - 1;
+        constexpr int L3 = NM - Q2 - 1, m3 = m - Q2 - 1;
+        constexpr int k2 = (m2 * n2 + L2 - 1) / L2, k2e = ((m2 + 1) * n2 + L2 - 1) / L2;
+        constexpr int k3 = (m3 * NA1 + L3 - 1) / L3, k3e = ((m3 + 1) * NA1 + L3 - 1) / L3;
+        constexpr int fd = (m > Q1 && m < Q2 && k2 < k2e && alt_kind(FM, NB, k2) == 1)
+                               ? NA + alt_idx(FM, NB, k2)
+                               : (m > Q2 && k3 < k3e) ? k3 : -1;
+        if constexpr (fd >= 0) mfma_dma(acc[m / FN][m % FN], af0[m / FN], bf0[m % FN], sa, sb, buf, std::integral_constant<int, fd>{});
+        else amfma_v<DT>(acc[m / FN][m % FN], af0[m / FN], bf0[m % FN]);
+        if constexpr (m < Q1) {
+          static_for<(m * FN + Q1 - 1) / Q1, ((m + 1) * FN + Q1 - 1) / Q1>([&](auto ji)
+                                                                    __attribute__((always_inline)) {
+            constexpr int j = decltype(ji)::value;
+            bf1[j] = ds_read16_off<j * 16 * 128>(bb + off1);
+          });
+        } else if constexpr (m == Q1 || m == Q2) {
+          __builtin_amdgcn_sched_barrier(0);
+          asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+          __builtin_amdgcn_sched_barrier(0);
+        } else if constexpr (m < Q2) {
+          static_for<k2 + (fd >= 0 ? 1 : 0), k2e>([&](auto ki) __attribute__((always_inline)) {
+            constexpr int k = decltype(ki)::value;  // reads and DMAs alternate
+            if constexpr (alt_kind(FM, NB, k) == 0)
+              af1[alt_idx(FM, NB, k)] = ds_read16_off<alt_idx(FM, NB, k) * 16 * 128>(ab + off1);
+            else
+              stage_one(sa, sb, buf, std::integral_constant<int, NA + alt_idx(FM, NB, k)>{});
+          });
+        } else {
+          static_for<k3 + (fd >= 0 ? 1 : 0), k3e>([&](auto ki) __attribute__((always_inline)) {
+            stage_one(sa, sb, buf, ki);
+          });
+        }
+      });
+      static_for<0, NM>([&](auto mi) __attribute__((always_inline)) {
+        constexpr int m = decltype(mi)::value;
+        constexpr int n1 = NA - NA1;
+        constexpr int k1 = (m * n1 + P1 - 1) / P1, k1e = ((m + 1) * n1 + P1 - 1) / P1;
+        constexpr int fd = (m < P1 && k1 < k1e) ? NA1 + k1 : -1;
+        if constexpr (fd >= 0) mfma_dma(acc[m / FN][m % FN], af1[m / FN], bf1[m % FN], sa, sb, buf, std::integral_constant<int, fd>{});
+        else amfma_v<DT>(acc[m / FN][m % FN], af1[m / FN], bf1[m % FN]);
+        if constexpr (m < P1) {
+          static_for<k1 + (fd >= 0 ? 1 : 0), k1e>([&](auto ki) __attribute__((always_inline)) {
+            stage_one(sa, sb, buf, std::integral_constant<int, NA1 + decltype(ki)::value>{});
+          });
+        } else if constexpr (m == P1) {
+          __builtin_amdgcn_sched_barrier(0);
+          __builtin_amdgcn_s_waitcnt(vm_wait(IPW));  // step t+1's DMAs landed
+          asm volatile("s_barrier" ::: "memory");
+          __builtin_amdgcn_sched_barrier(0);
+        } else {
+          constexpr int L = NM - P1 - 1, mm = m - P1 - 1;
+          static_for<(mm * NR + L - 1) / L, ((mm + 1) * NR + L - 1) / L>([&](auto ri)
+                                                                   __attribute__((always_inline)) {
+            constexpr int r = decltype(ri)::value;
+            if constexpr (r < FM) af0[r] = ds_read16_off<r * 16 * 128>(na + off0);
+            else bf0[r - FM] = ds_read16_off<(r - FM) * 16 * 128>(nb + off0);
+          });
+        }
+      });
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      buf = nbuf;
+    }
+  } else {
 
   // The interleaved two-stage schedule of gemm_kernel (IL, NS = 2):
   //   [kk1 reads of t | kk0 MFMAs of t] wait | vmcnt(DMA t+1) barrier
   //   [DMA t+2 into t's buffer + kk0 reads of t+1 | kk1 MFMAs of t] wait
   // Every step issues all 16 DMAs (past the split's end: out of the descriptors' range,
   // zeros) so the counted waits hold.
-  constexpr int NM = FM * FN, NR = FM + FN, NL = IPW + NR;
-  uint4 af0[FM], bf0[FN], af1[FM], bf1[FN];
+  constexpr int NL = IPW + NR;
   stage(0, 0);
   __builtin_amdgcn_s_waitcnt(vm_wait(0));
   asm volatile("s_barrier" ::: "memory");
@@ -256,6 +319,8 @@ __global__ __launch_bounds__(256) void gemm_4w_kernel(GemmArgs g) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
   int buf = 0;
+  unsigned long long sg[4] = {0, 0, 0, 0}, tp = 0, t1 = 0, t2 = 0, t3 = 0;
+  CAKE_STAMP(tp);
   for (int t = 0; t < nk; ++t) {
     const uint32_t ab = a_base + buf * BUF, bb = b_base + buf * BUF;
     static_for<0, NM>([&](auto mi) __attribute__((always_inline)) {
@@ -268,22 +333,26 @@ __global__ __launch_bounds__(256) void gemm_4w_kernel(GemmArgs g) {
         else bf1[r - FM] = ds_read16_off<(r - FM) * 16 * 128>(bb + off1);
       });
     });
+    CAKE_STAMP(t1);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     const int nbuf = buf ^ 1;
     __builtin_amdgcn_s_waitcnt(vm_wait(0));  // DMA of step t+1 landed
     asm volatile("s_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
+    CAKE_STAMP(t2);
     const uint32_t na = a_base + nbuf * BUF, nb = b_base + nbuf * BUF;
-    const int s2 = t + 2;
+    const cu32x4 sa = src_a(t + 2), sb = src_b(t + 2);
     static_for<0, NM>([&](auto mi) __attribute__((always_inline)) {
       constexpr int m = decltype(mi)::value;
-      amfma_v<DT>(acc[m / FN][m % FN], af1[m / FN], bf1[m % FN]);
-      static_for<(m * NL + NM - 1) / NM, ((m + 1) * NL + NM - 1) / NM>([&](auto li)
-                                                                    __attribute__((always_inline)) {
+      constexpr int l0 = (m * NL + NM - 1) / NM, l1 = ((m + 1) * NL + NM - 1) / NM;
+      constexpr bool fuse = l0 < l1 && l0 % 2 == 0 && l0 / 2 < IPW;
+      if constexpr (fuse) mfma_dma(acc[m / FN][m % FN], af1[m / FN], bf1[m % FN], sa, sb, buf, std::integral_constant<int, l0 / 2>{});
+      else amfma_v<DT>(acc[m / FN][m % FN], af1[m / FN], bf1[m % FN]);
+      static_for<l0 + (fuse ? 1 : 0), l1>([&](auto li) __attribute__((always_inline)) {
         constexpr int l = decltype(li)::value;
         if constexpr (l % 2 == 0 && l / 2 < IPW) {  // DMAs and reads alternate
-          stage_one(s2, buf, l / 2);
+          stage_one(sa, sb, buf, std::integral_constant<int, l / 2>{});
         } else {
           constexpr int r = (l - 1) / 2;
           if constexpr (r < FM) af0[r] = ds_read16_off<r * 16 * 128>(na + off0);
@@ -291,10 +360,22 @@ __global__ __launch_bounds__(256) void gemm_4w_kernel(GemmArgs g) {
         }
       });
     });
+    CAKE_STAMP(t3);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     buf = nbuf;
+#ifdef CAKE_GEMM_STAMPS
+    unsigned long long t4;
+    CAKE_STAMP(t4);
+    sg[0] += t1 - tp; sg[1] += t2 - t1; sg[2] += t3 - t2; sg[3] += t4 - t3;
+    tp = t4;
+#endif
   }
+#ifdef CAKE_GEMM_STAMPS
+  if (lane == 0)
+    for (int i = 0; i < 4; ++i) g_gemm_stamps[((size_t)blockIdx.x * 4 + wave) * 4 + i] = sg[i];
+#endif
+  (void)sg; (void)tp; (void)t1; (void)t2; (void)t3;
 
   }
 

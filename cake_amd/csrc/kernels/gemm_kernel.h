@@ -708,16 +708,16 @@ int launch_gemm(int cfg, dim3 grid, hipStream_t st, const GemmArgs& g) {
     hipLaunchKernelGGL((gemm_4w_kernel<DT, EPI, 128, 256>), grid, dim3(256), 0, st, g);
     return (int)hipGetLastError();
   }
-  if (cfg == k4WCfg + k4WDeep) {
-    hipLaunchKernelGGL((gemm_4w_kernel<DT, EPI, 256, 256, true>), grid, dim3(256), 0, st, g);
+  if (cfg == k4WCfg + k4WSched) {
+    hipLaunchKernelGGL((gemm_4w_kernel<DT, EPI, 256, 256, 1>), grid, dim3(256), 0, st, g);
     return (int)hipGetLastError();
   }
-  if (cfg == k4WCfg192 + k4WDeep) {
-    hipLaunchKernelGGL((gemm_4w_kernel<DT, EPI, 256, 192, true>), grid, dim3(256), 0, st, g);
+  if (cfg == k4WCfg192 + k4WSched) {
+    hipLaunchKernelGGL((gemm_4w_kernel<DT, EPI, 256, 192, 1>), grid, dim3(256), 0, st, g);
     return (int)hipGetLastError();
   }
-  if (cfg == k4WCfg128 + k4WDeep) {
-    hipLaunchKernelGGL((gemm_4w_kernel<DT, EPI, 128, 256, true>), grid, dim3(256), 0, st, g);
+  if (cfg == k4WCfg128 + k4WSched) {
+    hipLaunchKernelGGL((gemm_4w_kernel<DT, EPI, 128, 256, 1>), grid, dim3(256), 0, st, g);
     return (int)hipGetLastError();
   }
 

@@ -63,7 +63,7 @@ def main():
         out = None if epi == "resid32" else torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         cfg5, s5 = G.plan_mfma(M, Nv, K, epi)
         plans = {"mfma": (cfg5, s5), "pp": (20, 1), "pp2": (20, 2), "rs": (21, 1), "rs2": (21, 2), "w4": (22, 1), "w42": (22, 2), "w3": (23, 1), "w32": (23, 2), "w1": (24, 1), "w12": (24, 2),
-                 "d4": (25, 1), "d42": (25, 2), "d3": (26, 1), "d32": (26, 2), "d1": (27, 1), "d12": (27, 2),
+                 "b4": (25, 1), "b42": (25, 2), "b3": (26, 1), "b32": (26, 2), "b1": (27, 1), "b12": (27, 2),
                  "lib": (G.LIB, 1)}
         y = x.float() @ w.float().t()
         if epi == "swiglu":

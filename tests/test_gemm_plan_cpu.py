@@ -27,12 +27,12 @@ def _kernel_cfgs() -> dict:
         cid = int(re.search(name + r" = (\d+);", t).group(1))
         tile = {"k4WCfg192": (256, 192), "k4WCfg128": (128, 256)}.get(name, (256, 256))
         cfgs[cid] = tile + waves
-    # the deep-staged twins of the four-wave tiles: cfg + k4WDeep, same tile
+    # the three-barrier twins of the four-wave tiles: cfg + k4WSched, same tile
     t = (ROOT / "cake_amd/csrc/kernels/gemm_4w.h").read_text()
-    deep = int(re.search(r"k4WDeep = (\d+);", t).group(1))
+    sched = int(re.search(r"k4WSched = (\d+);", t).group(1))
     for name in ("k4WCfg", "k4WCfg192", "k4WCfg128"):
         cid = int(re.search(name + r" = (\d+);", t).group(1))
-        cfgs[cid + deep] = cfgs[cid]
+        cfgs[cid + sched] = cfgs[cid]
     return cfgs
 
 
