@@ -1,21 +1,24 @@
-// Four-wave 256x256 MFMA GEMM (plan cfg 22): the large Llama prefill projections.
+// Four-wave MFMA GEMM tiles 256x256 / 256x192 / 128x256 (plan cfg 22-24, and 25-27 on the
+// three-barrier schedule): the large Llama prefill projections.
 //
-// Included by gemm_kernel.h (launch_gemm dispatches cfg 22 here); same GemmArgs, tile
-// order, swizzled LDS image, fragment reads, interleaved schedule and epilogues as
-// gemm_kernel's IL path.
+// Included by gemm_kernel.h (launch_gemm dispatches cfg 22-27 here); same GemmArgs, tile
+// order, swizzled LDS image, fragment reads and epilogues as gemm_kernel's IL path.
 //
 // The shape of the winning library kernel on this chip (hipBLASLt's 256x256x64 tile,
 // profiles/r6_gemm_pmc_8192.txt): one wave per SIMD, 128 x 128 outputs per wave, LDS-DMA
-// staging, 32 fragment reads per k-step.  gemm_kernel's 4-wave form of the same tile
-// measured 0.5x (round 2) because each of its 16 DMA issues per wave and k-step
-// recomputed a 64-bit source pointer and a zeros-page select in VALU; here a DMA is one
-// buffer_load_dwordx4 ... lds:
-//   * one per-lane byte offset VGPR per operand (the lane's row in its 32-row group and
-//     its swizzled 16-byte chunk), the group's row offset and the k step in the scalar
-//     soffset, the LDS destination in M0;
-//   * rows past the matrix read through the descriptor's range check (zeros, no fault),
-//     so no per-issue select and no zeros page; gated (SwiGLU / GEGLU) weights keep a
-//     constant row stride per group (16 gate + 16 up rows), so the same form covers them.
+// staging, 32 fragment reads per k-step.  At one wave per SIMD every instruction beside
+// the MFMAs is paid in MFMA gaps (16 cycles, 8 of them free), so a DMA piece is three
+// instructions and nothing else (k-loop stamps: profiles/r6_gemm_stamps.jsonl):
+//   * buffer_load_dwordx4 ... offen lds with one per-lane byte offset VGPR per operand (the
+//     lane's row in its 32-row group and its swizzled 16-byte chunk) and the group's row
+//     offset as a loop-invariant scalar soffset;
+//   * the k step in the descriptor: its base advanced and num_records shrunk per step (a
+//     handful of scalar ops per step, not per piece); rows past the matrix and steps past
+//     the split read through the range check as zeros (no per-issue select, no zeros
+//     page); gated (SwiGLU / GEGLU) weights keep a constant row stride per group (16 gate
+//     + 16 up rows), so the same form covers them;
+//   * the M0 write (buffer base + the piece's offset as an immediate) and the DMA in one
+//     asm statement with the MFMA it is scheduled behind, which also covers M0's wait state.
 //   Needs K and the split's k range in whole 64-element steps and operands under 2 GB
 //   (host-checked).
 #pragma once
