@@ -21,6 +21,7 @@
 //     last-arriving split merges behind a ticket.
 //   * Prefill attention is the MFMA flash kernel (flash_attn.hip).
 #include <cstdio>
+#include <cstdlib>
 #include <mutex>
 #include <utility>
 #include <vector>
@@ -219,10 +220,11 @@ static int resident_splits(K kern, int threads, int heads, int splits) {
   if (cap < heads) return 0;
   if ((long long)heads * splits <= cap) return splits;
   const int fit = (int)(cap / heads);
-  if (!warned) {
+  // the grid is trimmed to what fits (core 2's splits walk more keys each); logged on request
+  if (!warned && std::getenv("CAKE_ATTN_LOG") != nullptr) {
     warned = true;
-    std::fprintf(stderr, "[cake] decode attention: %d x %d workgroups exceed residency (%lld); "
-                 "core 2 with %d splits per KV head\n", heads, splits, cap, fit);
+    std::fprintf(stderr, "[cake] decode attention: %d x %d workgroups trimmed to residency "
+                 "(%lld): core 2 with %d splits per KV head\n", heads, splits, cap, fit);
   }
   return fit;
 }

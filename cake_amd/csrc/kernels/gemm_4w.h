@@ -99,6 +99,10 @@ __global__ __launch_bounds__(256) void gemm_4w_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[2 * BUF];
 
   const int tid = threadIdx.x, lane = tid & 63;
+#ifdef CAKE_GEMM_STAMPS
+  unsigned long long st_[6] = {0, 0, 0, 0, 0, 0}, t_entry;
+  CAKE_STAMP(t_entry);
+#endif
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 1, wc = wave & 1;
 
@@ -322,8 +326,11 @@ __global__ __launch_bounds__(256) void gemm_4w_kernel(GemmArgs g) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
   int buf = 0;
-  unsigned long long sg[4] = {0, 0, 0, 0}, tp = 0, t1 = 0, t2 = 0, t3 = 0;
+  unsigned long long tp = 0, t1 = 0, t2 = 0, t3 = 0;
   CAKE_STAMP(tp);
+#ifdef CAKE_GEMM_STAMPS
+  st_[4] = tp - t_entry;  // prologue: tile decode, descriptors, first two steps' DMAs
+#endif
   for (int t = 0; t < nk; ++t) {
     const uint32_t ab = a_base + buf * BUF, bb = b_base + buf * BUF;
     static_for<0, NM>([&](auto mi) __attribute__((always_inline)) {
@@ -370,15 +377,14 @@ __global__ __launch_bounds__(256) void gemm_4w_kernel(GemmArgs g) {
 #ifdef CAKE_GEMM_STAMPS
     unsigned long long t4;
     CAKE_STAMP(t4);
-    sg[0] += t1 - tp; sg[1] += t2 - t1; sg[2] += t3 - t2; sg[3] += t4 - t3;
+    st_[0] += t1 - tp; st_[1] += t2 - t1; st_[2] += t3 - t2; st_[3] += t4 - t3;
     tp = t4;
 #endif
   }
 #ifdef CAKE_GEMM_STAMPS
-  if (lane == 0)
-    for (int i = 0; i < 4; ++i) g_gemm_stamps[((size_t)blockIdx.x * 4 + wave) * 4 + i] = sg[i];
+  st_[5] = tp;  // loop end; the epilogue's length is taken at the kernel's end
 #endif
-  (void)sg; (void)tp; (void)t1; (void)t2; (void)t3;
+  (void)tp; (void)t1; (void)t2; (void)t3;
 
   }
 
@@ -446,6 +452,16 @@ __global__ __launch_bounds__(256) void gemm_4w_kernel(GemmArgs g) {
     epi_strip<DT, EPI, FN, i & 1>(g, acc[i], stg, row_m0 + i * 16, vcol0, split, lane, ops,
                                   padd ? padd + i * FN * 256 : nullptr);
   });
+#ifdef CAKE_GEMM_STAMPS
+  {
+    unsigned long long t_end;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tile's stores issued and done
+    CAKE_STAMP(t_end);
+    st_[5] = t_end - st_[5];
+    if (lane == 0)
+      for (int i = 0; i < 6; ++i) g_gemm_stamps[((size_t)blockIdx.x * 4 + wave) * 8 + i] = st_[i];
+  }
+#endif
 }
 
 }  // namespace cake

@@ -12,6 +12,7 @@
 //   B  LDS-read drain + vmcnt(0) (the next step's DMA) + barrier
 //   C  second half's 64 MFMAs + 16 DMAs + 16 fragment reads (issue stream)
 //   D  LDS-read drain at the step's end
+// and per tile: prologue (entry -> loop) and epilogue (loop end -> the tile's stores done).
 #define CAKE_GEMM_STAMPS 1
 #include <cstdio>
 #include <cstdlib>
@@ -19,7 +20,7 @@
 
 #include <hip/hip_runtime.h>
 
-__device__ unsigned long long g_gemm_stamps[4096 * 4 * 4];
+__device__ unsigned long long g_gemm_stamps[4096 * 4 * 8];
 
 #include "../cake_amd/csrc/kernels/gemm_kernel.h"
 
@@ -78,24 +79,24 @@ int main(int argc, char** argv) {
     if (ms < best) best = ms;
   }
   const size_t nw = (size_t)grid.x * 4;
-  std::vector<unsigned long long> st(nw * 4);
+  std::vector<unsigned long long> st(nw * 8);
   CK(hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(g_gemm_stamps), st.size() * 8));
   const double steps = (double)K / 64;
-  double seg[4] = {0, 0, 0, 0};
+  double seg[6] = {0, 0, 0, 0, 0, 0};
   for (size_t w = 0; w < nw; ++w)
-    for (int i = 0; i < 4; ++i) seg[i] += (double)st[w * 4 + i];
+    for (int i = 0; i < 6; ++i) seg[i] += (double)st[w * 8 + i];
   double tot = 0;
-  for (int i = 0; i < 4; ++i) {
-    seg[i] /= nw * steps;
-    tot += seg[i];
-  }
+  for (int i = 0; i < 6; ++i) seg[i] /= nw;
+  for (int i = 0; i < 4; ++i) tot += seg[i] / steps;
+  const double tile = seg[0] + seg[1] + seg[2] + seg[3] + seg[4] + seg[5];
   const char* names[4] = {"A mfma64+reads16", "B drain+vmcnt0+barrier", "C mfma64+dma16+reads16",
                           "D drain"};
   std::printf("{\"M\": %d, \"N\": %d, \"K\": %d, \"best_ms\": %.4f, \"tflops\": %.1f, "
               "\"cycles_per_kstep\": %.1f",
               M, N, K, best, 2.0 * M * N * K / best / 1e9, tot);
   for (int i = 0; i < 4; ++i)
-    std::printf(", \"%s\": [%.1f, %.3f]", names[i], seg[i], seg[i] / tot);
-  std::printf("}\n");
+    std::printf(", \"%s\": [%.1f, %.3f]", names[i], seg[i] / steps, seg[i] / steps / tot);
+  std::printf(", \"tile_cycles\": %.0f, \"prologue\": [%.0f, %.3f], \"epilogue\": [%.0f, %.3f]}\n",
+              tile, seg[4], seg[4] / tile, seg[5], seg[5] / tile);
   return 0;
 }
