@@ -82,11 +82,11 @@ int main(int argc, char** argv) {
   std::vector<unsigned long long> st(nw * 8);
   CK(hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(g_gemm_stamps), st.size() * 8));
   const double steps = (double)K / 64;
-  double seg[6] = {0, 0, 0, 0, 0, 0};
+  double seg[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   for (size_t w = 0; w < nw; ++w)
-    for (int i = 0; i < 6; ++i) seg[i] += (double)st[w * 8 + i];
+    for (int i = 0; i < 8; ++i) seg[i] += (double)st[w * 8 + i];
   double tot = 0;
-  for (int i = 0; i < 6; ++i) seg[i] /= nw;
+  for (int i = 0; i < 8; ++i) seg[i] /= nw;
   for (int i = 0; i < 4; ++i) tot += seg[i] / steps;
   const double tile = seg[0] + seg[1] + seg[2] + seg[3] + seg[4] + seg[5];
   const char* names[4] = {"A mfma64+reads16", "B drain+vmcnt0+barrier", "C mfma64+dma16+reads16",
@@ -96,7 +96,8 @@ int main(int argc, char** argv) {
               M, N, K, best, 2.0 * M * N * K / best / 1e9, tot);
   for (int i = 0; i < 4; ++i)
     std::printf(", \"%s\": [%.1f, %.3f]", names[i], seg[i] / steps, seg[i] / steps / tot);
-  std::printf(", \"tile_cycles\": %.0f, \"prologue\": [%.0f, %.3f], \"epilogue\": [%.0f, %.3f]}\n",
-              tile, seg[4], seg[4] / tile, seg[5], seg[5] / tile);
+  std::printf(", \"tile_cycles\": %.0f, \"prologue\": [%.0f, %.3f], \"epilogue\": [%.0f, %.3f], "
+              "\"epi_lead\": %.0f, \"epi_strips\": %.0f}\n",
+              tile, seg[4], seg[4] / tile, seg[5], seg[5] / tile, seg[7], seg[6]);
   return 0;
 }
