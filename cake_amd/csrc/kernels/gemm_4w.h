@@ -83,182 +83,6 @@ __device__ __forceinline__ void amfma_dma(cf32x4& acc, const uint4& a, const uin
                  : "memory");
 }
 
-// Epilogue of the four-wave tiles: a strip (16 rows x the wave's 128 columns) is staged
-// through LDS as in gemm_kernel, then read out 8 lanes per row, two rows per lane, and a
-// lane's 16-byte chunks interleaved with its row neighbours' (chunk c of lane q at output
-// column (8 c + q) x the chunk's elements), so each store instruction writes 8 whole
-// 128-byte lines.  gemm_kernel's read-out (4 lanes per row, 32 contiguous columns each)
-// wrote 32 bytes into each of 32 lines per instruction: the tile's stores took 12-24 % of
-// its time (profiles/r6_gemm_stamps.jsonl).
-template <int DT, int EPI, int NF> struct EpiW {
-  static constexpr int WTN = NF * 16;
-  static constexpr bool GATED = (EPI == kEpiSwiglu || EPI == kEpiGeglu);
-  static constexpr bool F32 = (EPI == kEpiResid32 || EPI == kEpiStore32 || EPI == kEpiPartial);
-  static constexpr int OUTC = GATED ? WTN / 2 : WTN;  // output columns of a strip
-  static constexpr int CE = F32 ? 4 : 8;              // output elements per 16-byte chunk
-  static constexpr int CPL = OUTC / 8;                // a lane's columns per row
-  static constexpr int NCH = CPL / CE;                // its chunks per row
-  static constexpr bool OK = OUTC % 8 == 0 && CPL % CE == 0;  // else: gemm_kernel's read-out
-  static constexpr bool RES = EPI == kEpiAdd16;
-  static constexpr bool PRE = (EPI == kEpiAdd16 || GATED);
-  float bias[PRE ? (GATED ? 2 * CPL : CPL) : 1];
-  float res[2][RES ? 2 * CPL : 1];  // [buffer][row pass x CPL]
-
-  __device__ __forceinline__ static int col(int lane, int c) { return (c * 8 + (lane & 7)) * CE; }
-
-  // 8 16-bit values at p + n (columns < lim valid) as f32
-  __device__ __forceinline__ static void load8(const uint16_t* p, int n, int lim, bool vec,
-                                               float* o) {
-    if (vec && n + 8 <= lim) {
-      unpack8<DT>(*reinterpret_cast<const uint4*>(p + n), o);
-    } else {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = n + e < lim ? to_f32<DT>(p[n + e]) : 0.f;
-    }
-  }
-
-  __device__ __forceinline__ void load_bias(const GemmArgs& g, int vcol0, int lane) {
-    if constexpr (PRE) {
-      if (g.bias == nullptr) {
-#pragma unroll
-        for (int c = 0; c < (GATED ? 2 * CPL : CPL); ++c) bias[c] = 0.f;
-        return;
-      }
-      const int base = GATED ? vcol0 / 2 : vcol0;
-      const bool vec = (base & 7) == 0 && (!GATED || (g.half & 7) == 0);
-#pragma unroll
-      for (int c = 0; c < NCH; ++c) {
-        load8(g.bias, base + col(lane, c), g.N, vec, bias + c * 8);
-        if constexpr (GATED) load8(g.bias + g.half, base + col(lane, c), g.N, vec, bias + CPL + c * 8);
-      }
-    }
-  }
-
-  // the add16 residual of this lane's two rows (m0 + lane/8 and + 8) of a strip
-  template <int B>
-  __device__ __forceinline__ void load_res(const GemmArgs& g, int m0, int vcol0, int lane) {
-    if constexpr (RES) {
-      const bool vec = ((g.ldr | vcol0) & 7) == 0;
-#pragma unroll
-      for (int rp = 0; rp < 2; ++rp) {
-        const int m = m0 + (lane >> 3) + 8 * rp;
-        if (m >= g.M) continue;
-#pragma unroll
-        for (int c = 0; c < NCH; ++c)
-          load8(g.r16 + (size_t)m * g.ldr, vcol0 + col(lane, c), g.N, vec, res[B] + rp * CPL + c * 8);
-      }
-    }
-  }
-};
-
-// a strip's accumulators (+ the split-K partner's, add) into the wave's staging slice
-template <int NF>
-__device__ __forceinline__ void stage_strip_w(const cf32x4 (&tiles)[NF], float* stg, int lane,
-                                              const float4* add) {
-  constexpr int STG_LD = NF * 16 + 4;
-  if (add) {
-#pragma unroll
-    for (int j = 0; j < NF; ++j) {
-      const float4 o = add[j * 256];
-      const float ov[4] = {o.x, o.y, o.z, o.w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        stg[((lane >> 4) * 4 + e) * STG_LD + j * 16 + (lane & 15)] = tiles[j][e] + ov[e];
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < NF; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        stg[((lane >> 4) * 4 + e) * STG_LD + j * 16 + (lane & 15)] = tiles[j][e];
-  }
-}
-
-// a staged strip read out 8 lanes per row and written with the epilogue EPI
-template <int DT, int EPI, int NF, int B>
-__device__ __forceinline__ void readout_strip_w(const GemmArgs& g, const float* stg, int m_strip0,
-                                                int vcol0, int split, int lane,
-                                                const EpiW<DT, EPI, NF>& ops) {
-  using W = EpiW<DT, EPI, NF>;
-  constexpr int STG_LD = NF * 16 + 4;
-#pragma unroll
-  for (int rp = 0; rp < 2; ++rp) {
-    const int row = (lane >> 3) + 8 * rp;
-    const int m = m_strip0 + row;
-    if (m >= g.M) continue;
-    const float* srow = stg + row * STG_LD;
-#pragma unroll
-    for (int c = 0; c < W::NCH; ++c) {
-      const int lc = W::col(lane, c);  // output column within the wave's strip
-      if constexpr (EPI == kEpiPartial) {
-        float* dst = g.ws + ((size_t)split * g.M + m) * g.Nv;
-        const int n = vcol0 + lc;
-        const float4 v = *reinterpret_cast<const float4*>(srow + lc);
-        if (n + 3 < g.Nv) *reinterpret_cast<float4*>(dst + n) = v;
-        else {
-          const float vv[4] = {v.x, v.y, v.z, v.w};
-          for (int q = 0; q < 4; ++q) if (n + q < g.Nv) dst[n + q] = vv[q];
-        }
-      } else if constexpr (W::GATED) {
-        const int f0 = vcol0 / 2 + lc;
-        const int vc = (lc >> 4) * 32 + (lc & 15);  // the gate's staged column
-        uint16_t outv[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float a = srow[vc + e] + ops.bias[c * 8 + e];
-          const float b = srow[vc + 16 + e] + ops.bias[W::CPL + c * 8 + e];
-          float y;
-          if constexpr (EPI == kEpiSwiglu) y = silu(a) * b;
-          else y = a * gelu_tanh(b);
-          outv[e] = from_f32<DT>(y);
-        }
-        store16<8>(g.c + (size_t)m * g.ldc + f0, outv, f0 + 8 <= g.N, g.ldc | f0, g.N - f0);
-      } else if constexpr (W::F32) {
-        const int n = vcol0 + lc;
-        const float4 t = *reinterpret_cast<const float4*>(srow + lc);
-        float v[4] = {t.x, t.y, t.z, t.w};
-        if (g.bias != nullptr)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) if (n + e < g.N) v[e] += to_f32<DT>(g.bias[n + e]);
-        constexpr bool ADD = EPI == kEpiResid32;
-        float* r = g.r32 + (size_t)m * g.ldr + n;
-        if (n + 4 <= g.N && ((g.ldr | n) & 3) == 0) {
-          float4 o = ADD ? *reinterpret_cast<float4*>(r) : make_float4(0.f, 0.f, 0.f, 0.f);
-          o.x += v[0]; o.y += v[1]; o.z += v[2]; o.w += v[3];
-          *reinterpret_cast<float4*>(r) = o;
-        } else {
-          for (int e = 0; e < 4; ++e)
-            if (n + e < g.N) r[e] = ADD ? r[e] + v[e] : v[e];
-        }
-      } else {
-        const int n = vcol0 + lc;
-        const float4 t0 = *reinterpret_cast<const float4*>(srow + lc);
-        const float4 t1 = *reinterpret_cast<const float4*>(srow + lc + 4);
-        float v[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
-        if constexpr (W::PRE) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] += ops.bias[c * 8 + e];
-        } else if (g.bias != nullptr) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) if (n + e < g.N) v[e] += to_f32<DT>(g.bias[n + e]);
-        }
-        if constexpr (EPI == kEpiAdd16) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] += ops.res[B][rp * W::CPL + c * 8 + e];
-        }
-        if constexpr (EPI == kEpiSilu) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = gemm_act(g.act, v[e]);
-        }
-        uint16_t outv[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) outv[e] = from_f32<DT>(v[e]);
-        store16<8>(g.c + (size_t)m * g.ldc + n, outv, n + 8 <= g.N, g.ldc | n, g.N - n);
-      }
-    }
-  }
-}
-
 // SCHED 1 (cfg 25-27): the same tiles on a three-barrier schedule (the DMAs of step t+2
 // issued as soon as every wave has read the operand region they overwrite).
 template <int DT, int EPI, int BM, int BN, int SCHED = 0>
