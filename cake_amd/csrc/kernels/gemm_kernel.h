@@ -333,37 +333,55 @@ __device__ __forceinline__ void epi_strip(const GemmArgs& g, const cf32x4 (&tile
   }
 }
 
-// Wide read-out (every wave tile 64 or 128 columns wide; gated: 128): a strip (16 rows x
-// the wave's columns) staged through LDS as above, then read out 8 lanes per row, two rows
-// per lane, a lane's 16-byte chunks interleaved with its row neighbours' (chunk c of lane q
-// at output column (8 c + q) x the chunk's elements), so each store instruction writes 8
-// whole 128-byte lines (64-column tiles: 8 rows x 128 B).  epi_strip's read-out (4 lanes per
-// row, CPL contiguous columns each) wrote 32 bytes into each of 32 lines per instruction:
-// the four-wave tile's stores took 12-24 % of its time (profiles/r6_gemm_stamps.jsonl).
+// Wide read-out: a strip (16 rows x the wave's columns) staged through LDS as above, then
+// read out LPR lanes per row (8 when an output row is whole 128-byte lines, else 4), a
+// lane's 16-byte (80-column tiles: 8-byte) chunks interleaved with its row neighbours'
+// (chunk c of lane q at output column (LPR c + q) x the chunk's elements), so a store
+// instruction covers each row it touches with one contiguous run (8 rows x 128 B on the
+// 64 / 128-column tiles).  epi_strip's read-out (4 lanes per row, CPL contiguous columns
+// each) wrote 16-32 bytes into each of up to 32 lines per instruction: the four-wave tile's
+// stores took 12-24 % of its time (profiles/r6_gemm_stamps.jsonl).
 template <int DT, int EPI, int NF> struct EpiW {
   static constexpr int WTN = NF * 16;
   static constexpr bool GATED = (EPI == kEpiSwiglu || EPI == kEpiGeglu);
   static constexpr bool F32 = (EPI == kEpiResid32 || EPI == kEpiStore32 || EPI == kEpiPartial);
   static constexpr int OUTC = GATED ? WTN / 2 : WTN;  // output columns of a strip
-  static constexpr int CE = F32 ? 4 : 8;              // output elements per 16-byte chunk
-  static constexpr int CPL = OUTC / 8;                // a lane's columns per row
-  static constexpr int NCH = CPL / CE;                // its chunks per row
-  static constexpr bool OK = OUTC % 8 == 0 && CPL % CE == 0;  // else: gemm_kernel's read-out
+  static constexpr int ESZ = F32 ? 4 : 2;
+  static constexpr int ROWB = OUTC * ESZ;             // bytes of one output row of a strip
+  // 8 lanes per row when the row is whole 128-byte lines, else 4; 16-byte chunks when a
+  // row splits into them evenly over its lanes, else 8-byte (the 80-column tiles)
+  static constexpr int LPR = ROWB % 128 == 0 ? 8 : 4;
+  static constexpr int CB = ROWB % (LPR * 16) == 0 ? 16 : 8;
+  static constexpr int CE = CB / ESZ;                 // output elements per chunk
+  static constexpr int NCH = ROWB / (LPR * CB);       // a lane's chunks per row
+  static constexpr int CPL = NCH * CE;                // a lane's columns per row
+  static constexpr int RPP = 64 / LPR;                // rows per read-out pass
+  static constexpr int NP = 16 / RPP;                 // passes per 16-row strip
+  static constexpr bool OK = ROWB % (LPR * CB) == 0 && CE >= 4 && (!F32 || CE == 4);
   static constexpr bool RES = EPI == kEpiAdd16;
   static constexpr bool PRE = (EPI == kEpiAdd16 || GATED);
   float bias[PRE ? (GATED ? 2 * CPL : CPL) : 1];
-  float res[2][RES ? 2 * CPL : 1];  // [buffer][row pass x CPL]
+  float res[2][RES ? NP * CPL : 1];  // [buffer][pass x CPL]
 
-  __device__ __forceinline__ static int col(int lane, int c) { return (c * 8 + (lane & 7)) * CE; }
+  __device__ __forceinline__ static int col(int lane, int c) {
+    return (c * LPR + lane % LPR) * CE;
+  }
+  __device__ __forceinline__ static int row(int lane, int p) { return lane / LPR + RPP * p; }
 
-  // 8 16-bit values at p + n (columns < lim valid) as f32
-  __device__ __forceinline__ static void load8(const uint16_t* p, int n, int lim, bool vec,
+  // CE (4 / 8) 16-bit values at p + n (columns < lim valid) as f32
+  __device__ __forceinline__ static void loadc(const uint16_t* p, int n, int lim, bool vec,
                                                float* o) {
-    if (vec && n + 8 <= lim) {
-      unpack8<DT>(*reinterpret_cast<const uint4*>(p + n), o);
+    if (vec && n + CE <= lim) {
+      if constexpr (CE == 8) {
+        unpack8<DT>(*reinterpret_cast<const uint4*>(p + n), o);
+      } else {
+        const uint2 v = *reinterpret_cast<const uint2*>(p + n);
+        o[0] = to_f32<DT>((uint16_t)v.x); o[1] = to_f32<DT>((uint16_t)(v.x >> 16));
+        o[2] = to_f32<DT>((uint16_t)v.y); o[3] = to_f32<DT>((uint16_t)(v.y >> 16));
+      }
     } else {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = n + e < lim ? to_f32<DT>(p[n + e]) : 0.f;
+      for (int e = 0; e < CE; ++e) o[e] = n + e < lim ? to_f32<DT>(p[n + e]) : 0.f;
     }
   }
 
@@ -375,27 +393,28 @@ template <int DT, int EPI, int NF> struct EpiW {
         return;
       }
       const int base = GATED ? vcol0 / 2 : vcol0;
-      const bool vec = (base & 7) == 0 && (!GATED || (g.half & 7) == 0);
+      const bool vec = (base & (CE - 1)) == 0 && (!GATED || (g.half & (CE - 1)) == 0);
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
-        load8(g.bias, base + col(lane, c), g.N, vec, bias + c * 8);
-        if constexpr (GATED) load8(g.bias + g.half, base + col(lane, c), g.N, vec, bias + CPL + c * 8);
+        loadc(g.bias, base + col(lane, c), g.N, vec, bias + c * CE);
+        if constexpr (GATED)
+          loadc(g.bias + g.half, base + col(lane, c), g.N, vec, bias + CPL + c * CE);
       }
     }
   }
 
-  // the add16 residual of this lane's two rows (m0 + lane/8 and + 8) of a strip
+  // the add16 residual of this lane's rows of a strip
   template <int B>
   __device__ __forceinline__ void load_res(const GemmArgs& g, int m0, int vcol0, int lane) {
     if constexpr (RES) {
-      const bool vec = ((g.ldr | vcol0) & 7) == 0;
+      const bool vec = ((g.ldr | vcol0) & (CE - 1)) == 0;
 #pragma unroll
-      for (int rp = 0; rp < 2; ++rp) {
-        const int m = m0 + (lane >> 3) + 8 * rp;
+      for (int p = 0; p < NP; ++p) {
+        const int m = m0 + row(lane, p);
         if (m >= g.M) continue;
 #pragma unroll
         for (int c = 0; c < NCH; ++c)
-          load8(g.r16 + (size_t)m * g.ldr, vcol0 + col(lane, c), g.N, vec, res[B] + rp * CPL + c * 8);
+          loadc(g.r16 + (size_t)m * g.ldr, vcol0 + col(lane, c), g.N, vec, res[B] + p * CPL + c * CE);
       }
     }
   }
@@ -431,9 +450,10 @@ __device__ __forceinline__ void readout_strip_w(const GemmArgs& g, const float* 
                                                 const EpiW<DT, EPI, NF>& ops) {
   using W = EpiW<DT, EPI, NF>;
   constexpr int STG_LD = NF * 16 + 4;
+  constexpr int CE = W::CE;
 #pragma unroll
-  for (int rp = 0; rp < 2; ++rp) {
-    const int row = (lane >> 3) + 8 * rp;
+  for (int p = 0; p < W::NP; ++p) {
+    const int row = W::row(lane, p);
     const int m = m_strip0 + row;
     if (m >= g.M) continue;
     const float* srow = stg + row * STG_LD;
@@ -452,17 +472,17 @@ __device__ __forceinline__ void readout_strip_w(const GemmArgs& g, const float* 
       } else if constexpr (W::GATED) {
         const int f0 = vcol0 / 2 + lc;
         const int vc = (lc >> 4) * 32 + (lc & 15);  // the gate's staged column
-        uint16_t outv[8];
+        uint16_t outv[CE];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float a = srow[vc + e] + ops.bias[c * 8 + e];
-          const float b = srow[vc + 16 + e] + ops.bias[W::CPL + c * 8 + e];
+        for (int e = 0; e < CE; ++e) {
+          const float a = srow[vc + e] + ops.bias[c * CE + e];
+          const float b = srow[vc + 16 + e] + ops.bias[W::CPL + c * CE + e];
           float y;
           if constexpr (EPI == kEpiSwiglu) y = silu(a) * b;
           else y = a * gelu_tanh(b);
           outv[e] = from_f32<DT>(y);
         }
-        store16<8>(g.c + (size_t)m * g.ldc + f0, outv, f0 + 8 <= g.N, g.ldc | f0, g.N - f0);
+        store16<CE>(g.c + (size_t)m * g.ldc + f0, outv, f0 + CE <= g.N, g.ldc | f0, g.N - f0);
       } else if constexpr (W::F32) {
         const int n = vcol0 + lc;
         const float4 t = *reinterpret_cast<const float4*>(srow + lc);
@@ -482,28 +502,31 @@ __device__ __forceinline__ void readout_strip_w(const GemmArgs& g, const float* 
         }
       } else {
         const int n = vcol0 + lc;
-        const float4 t0 = *reinterpret_cast<const float4*>(srow + lc);
-        const float4 t1 = *reinterpret_cast<const float4*>(srow + lc + 4);
-        float v[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+        float v[CE];
+#pragma unroll
+        for (int e = 0; e < CE; e += 4) {
+          const float4 t = *reinterpret_cast<const float4*>(srow + lc + e);
+          v[e] = t.x; v[e + 1] = t.y; v[e + 2] = t.z; v[e + 3] = t.w;
+        }
         if constexpr (W::PRE) {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] += ops.bias[c * 8 + e];
+          for (int e = 0; e < CE; ++e) v[e] += ops.bias[c * CE + e];
         } else if (g.bias != nullptr) {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) if (n + e < g.N) v[e] += to_f32<DT>(g.bias[n + e]);
+          for (int e = 0; e < CE; ++e) if (n + e < g.N) v[e] += to_f32<DT>(g.bias[n + e]);
         }
         if constexpr (EPI == kEpiAdd16) {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] += ops.res[B][rp * W::CPL + c * 8 + e];
+          for (int e = 0; e < CE; ++e) v[e] += ops.res[B][p * W::CPL + c * CE + e];
         }
         if constexpr (EPI == kEpiSilu) {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = gemm_act(g.act, v[e]);
+          for (int e = 0; e < CE; ++e) v[e] = gemm_act(g.act, v[e]);
         }
-        uint16_t outv[8];
+        uint16_t outv[CE];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) outv[e] = from_f32<DT>(v[e]);
-        store16<8>(g.c + (size_t)m * g.ldc + n, outv, n + 8 <= g.N, g.ldc | n, g.N - n);
+        for (int e = 0; e < CE; ++e) outv[e] = from_f32<DT>(v[e]);
+        store16<CE>(g.c + (size_t)m * g.ldc + n, outv, n + CE <= g.N, g.ldc | n, g.N - n);
       }
     }
   }
@@ -758,7 +781,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(GemmArgs g) {
   float* stg = reinterpret_cast<float*>(smem + wave * STG);
   const int row_m0 = m0 + wr * WTM;
   const int vcol0 = n0 + wc * WTN;  // first virtual column of this wave
-  if constexpr (EpiW<DT, EPI, FN>::OK) {  // 64 / 128-column wave tiles: whole-line stores
+  if constexpr (EpiW<DT, EPI, FN>::OK) {  // wide read-out (every tile shape in use)
     EpiW<DT, EPI, FN> ops;
     ops.load_bias(g, vcol0, lane);
     ops.template load_res<0>(g, row_m0, vcol0, lane);
