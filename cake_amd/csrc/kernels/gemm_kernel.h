@@ -451,6 +451,23 @@ __device__ __forceinline__ void readout_strip_w(const GemmArgs& g, const float* 
   using W = EpiW<DT, EPI, NF>;
   constexpr int STG_LD = NF * 16 + 4;
   constexpr int CE = W::CE;
+  // resid32: every chunk's residual requested before the first add / store (one memory
+  // round trip per strip, not one per chunk: the stores could alias later loads)
+  constexpr bool R32 = EPI == kEpiResid32;
+  float4 rold[R32 ? W::NP : 1][R32 ? W::NCH : 1];
+  if constexpr (R32) {
+#pragma unroll
+    for (int p = 0; p < W::NP; ++p) {
+      const int m = m_strip0 + W::row(lane, p);
+#pragma unroll
+      for (int c = 0; c < W::NCH; ++c) {
+        const int n = vcol0 + W::col(lane, c);
+        rold[p][c] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (m < g.M && n + 4 <= g.N && ((g.ldr | n) & 3) == 0)
+          rold[p][c] = *reinterpret_cast<const float4*>(g.r32 + (size_t)m * g.ldr + n);
+      }
+    }
+  }
 #pragma unroll
   for (int p = 0; p < W::NP; ++p) {
     const int row = W::row(lane, p);
@@ -490,13 +507,13 @@ __device__ __forceinline__ void readout_strip_w(const GemmArgs& g, const float* 
         if (g.bias != nullptr)
 #pragma unroll
           for (int e = 0; e < 4; ++e) if (n + e < g.N) v[e] += to_f32<DT>(g.bias[n + e]);
-        constexpr bool ADD = EPI == kEpiResid32;
         float* r = g.r32 + (size_t)m * g.ldr + n;
         if (n + 4 <= g.N && ((g.ldr | n) & 3) == 0) {
-          float4 o = ADD ? *reinterpret_cast<float4*>(r) : make_float4(0.f, 0.f, 0.f, 0.f);
+          float4 o = R32 ? rold[R32 ? p : 0][R32 ? c : 0] : make_float4(0.f, 0.f, 0.f, 0.f);
           o.x += v[0]; o.y += v[1]; o.z += v[2]; o.w += v[3];
           *reinterpret_cast<float4*>(r) = o;
         } else {
+          constexpr bool ADD = R32;
           for (int e = 0; e < 4; ++e)
             if (n + e < g.N) r[e] = ADD ? r[e] + v[e] : v[e];
         }
