@@ -107,7 +107,10 @@ def tune(M, Nv, K, epi, dt, cfgs=None):
             continue
         tiles = -(-M // bm) * -(-Nv // bn)
         for splits in (1, 2, 4):
-            if splits > 1 and (tiles * splits > 2 * G.NUM_CUS or K // splits < 256):
+            # four-wave tiles at splits 2 pair only the tiles past the last whole wave (the
+            # in-kernel pair, gemm.hip), whatever the tile count
+            pair = cfg in getattr(G, "K64_ONLY", ()) and cfg >= 22 and splits == 2
+            if splits > 1 and not pair and (tiles * splits > 2 * G.NUM_CUS or K // splits < 256):
                 continue
             try:
                 run(cfg, splits)
