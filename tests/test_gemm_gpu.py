@@ -317,3 +317,27 @@ def test_four_wave_split_pair(cuda, epi, cfg):
     ref = F.silu(y[:, :N // 2]) * y[:, N // 2:] if epi == "swiglu" else y
     _close(outs[0], ref, K)
     assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+
+
+@pytest.mark.parametrize("cfg,N,epi", [(22, 2 * 14336, "swiglu"), (22, 9216, "store"),
+                                       (25, 9216, "resid32"), (27, 4608, "store")])
+def test_four_wave_remainder_pair(cuda, cfg, N, epi):
+    """Split-K 2 on a grid of more than one wave: the tiles past the last whole wave run as
+    in-kernel k-half pairs, the rest whole (8B gate|up at 2048 tokens: 896 tiles = 3 waves
+    + 128 paired) -- equal to the f32 reference and repeatable."""
+    from cake_amd.ops import gemm as G
+    torch.manual_seed(5)
+    M, K = 2048, 4096
+    x, w = _r(M, K, dt=torch.bfloat16), _r(N, K, dt=torch.bfloat16, std=K ** -0.5)
+    y = _ref(x, w)
+    outs = []
+    for _ in range(2):
+        if epi == "resid32":
+            r = torch.zeros(M, N, device="cuda")
+            G.linear(x, w, epi="resid32", resid=r, cfg=cfg, splits=2)
+            outs.append(r)
+        else:
+            outs.append(G.linear(x, w, epi=epi, cfg=cfg, splits=2))
+    ref = F.silu(y[:, :N // 2]) * y[:, N // 2:] if epi == "swiglu" else y
+    _close(outs[0], ref, K)
+    assert torch.equal(outs[0], outs[1])
