@@ -2,7 +2,7 @@
 # round 6 final: the whole GPU suite as the driver runs it, smoke, the default bench, the
 # 8B prefill kernel table at 2048 tokens (no library GEMM), the N=2 shared-GPU rehearsal
 set -u
-cd "$GRAFT_REPO_ROOT"; OUT=gpurun_out/r6final3; mkdir -p $OUT
+cd "$GRAFT_REPO_ROOT"; OUT=gpurun_out/r6final4; mkdir -p $OUT
 export HSA_ENABLE_IPC_MODE_LEGACY=0 PYTHONUNBUFFERED=1
 ROOT="$GRAFT_REPO_ROOT"
 run() { local name=$1 t=$2; shift 2; timeout -k 10 $t "$@" > $OUT/$name.log 2>&1; local rc=$?; echo "== $name rc=$rc"; tail -3 $OUT/$name.log; [[ $rc -eq 0 ]] || { tail -60 $OUT/$name.log; exit $rc; }; }
