@@ -64,6 +64,7 @@ int cake_rope_kv(int dt, void* q, const void* k, const void* v, int ldq, int ld,
 int cake_flash_attn(int dt, const void* q, const void* k, const void* v, void* o, int B, int H,
                     int Hkv, int N, int M, int D, const long long* strides, float scale,
                     int causal, int pos0, hipStream_t st);
+long long cake_gemm_ws_floats(int cfg, int splits, int M, int N, int K, int gated);
 int cake_gemm(int dt, int epi, int cfg, int splits, const void* a, long long lda, const void* b,
               long long ldb, void* c, long long ldc, const void* bias, void* resid,
               long long ldr, float* ws, const void* zeros, int M, int N, int K, hipStream_t st);
@@ -1192,7 +1193,7 @@ class Llama {
     const int splits = p.second;
     float* ws = nullptr;
     if (splits > 1) {
-      const size_t need = (size_t)splits * M * Nv;
+      const size_t need = (size_t)cake_gemm_ws_floats(p.first, splits, M, N, K, gated ? 1 : 0);
       if (need > ws_n_) {
         dfree(ws_);
         ws_ = dalloc<float>(need);

@@ -49,6 +49,7 @@ extern "C" {
 int cake_cast16(int src_kind, int dt, const void* src, void* dst, size_t n, hipStream_t st);
 int cake_fill_normal(int dt, void* dst, size_t n, float mean, float std, unsigned long long key,
                      hipStream_t st);
+long long cake_gemm_ws_floats(int cfg, int splits, int M, int N, int K, int gated);
 int cake_gemm(int dt, int epi, int cfg, int splits, const void* a, long long lda, const void* b,
               long long ldb, void* c, long long ldc, const void* bias, void* resid,
               long long ldr, float* ws, const void* zeros, int M, int N, int K, hipStream_t st);
@@ -1461,7 +1462,9 @@ class SdEngine {
     const bool gated = epi == 3 || epi == kGeglu;
     const int N = gated ? Nv / 2 : Nv;
     const auto pl = planner_.plan_mfma(M, Nv, K, kEpiNames[epi]);  // no library path here
-    float* ws = pl.second > 1 ? gemm_ws((size_t)pl.second * M * Nv) : nullptr;
+    float* ws = pl.second > 1
+                    ? gemm_ws((size_t)cake_gemm_ws_floats(pl.first, pl.second, M, N, K, gated ? 1 : 0))
+                    : nullptr;
     const bool f32out = epi == kResid32 || epi == kStore32;
     k_check(cake_gemm(dt_, epi, pl.first, pl.second, x, lda, w, K, f32out ? nullptr : out,
                       f32out ? 0 : ldc,

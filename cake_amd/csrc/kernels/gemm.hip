@@ -107,6 +107,40 @@ static int dispatch_finalize(int epi, dim3 grid, hipStream_t st, const GemmArgs&
   return (int)hipGetLastError();
 }
 
+// Split plan of one call: the k split actually run (whole 64-element steps per split) and,
+// for a four-wave tile at splits 2, the in-kernel pair's tiles (0: the slab + finalize
+// form).  cake_gemm and cake_gemm_ws_floats both decide through this one function, so a
+// workspace sized by the query always covers the launch.
+struct SplitPlan {
+  int splits, kps, bm, bn, ntiles, npair;
+};
+static SplitPlan split_plan(int cfg, int splits, int M, long long Nv, int K) {
+  SplitPlan p{};
+  cfg_dims(cfg, p.bm, p.bn);
+  int kps = (K + splits - 1) / splits;
+  kps = (kps + kGBK - 1) / kGBK * kGBK;
+  p.kps = kps;
+  p.splits = (K + kps - 1) / kps;
+  if (p.bm == 0) return p;
+  p.ntiles = (int)(((M + p.bm - 1) / p.bm) * ((Nv + p.bn - 1) / p.bn));
+  const int npair = p.ntiles <= 256 ? p.ntiles : p.ntiles % 256;
+  if (four_wave_cfg(cfg) && p.splits == 2 && npair > 0 &&
+      npair <= 128 + (p.ntiles <= 256 ? 128 : 0) && p.ntiles <= kPairTiles &&
+      (long long)npair * p.bm * p.bn <= 2LL * M * Nv && pair_ticks())
+    p.npair = npair;
+  return p;
+}
+
+// f32 workspace (elements) a cake_gemm call with these arguments needs: the pair's slabs
+// (npair x BM x BN) or splits x M x Nv partial rows, 0 when it runs unsplit
+CAKE_API long long cake_gemm_ws_floats(int cfg, int splits, int M, int N, int K, int gated) {
+  if (splits < 1 || M <= 0 || N <= 0 || K <= 0) return 0;
+  const long long Nv = gated ? 2LL * N : N;
+  const SplitPlan p = split_plan(cfg, splits, M, Nv, K);
+  if (p.npair > 0) return (long long)p.npair * p.bm * p.bn;
+  return p.splits > 1 ? (long long)p.splits * M * Nv : 0;
+}
+
 // y = epilogue(x W^T).  N = output features (gated: W has 2N rows, gate rows
 // [0, N), up/gate-2 rows [N, 2N)).  splits > 1 needs ws = splits * M * Nv f32.
 // Requirements (host-checked in ops/gemm.py): K % 8 == 0, lda/ldb % 8 == 0,
@@ -147,20 +181,16 @@ CAKE_API int cake_gemm(int dt, int epi, int cfg, int splits, const void* a, long
   g.Nv = gated ? 2 * N : N;
   g.tiles_m = (M + bm - 1) / bm;
   g.tiles_n = (g.Nv + bn - 1) / bn;
-  int kps = (K + splits - 1) / splits;
-  kps = (kps + kGBK - 1) / kGBK * kGBK;
-  splits = (K + kps - 1) / kps;
-  g.kps = kps;
+  const SplitPlan sp = split_plan(cfg, splits, M, g.Nv, K);
+  splits = sp.splits;
+  g.kps = sp.kps;
   const dim3 grid(g.tiles_m * g.tiles_n, splits);
-  // the four-wave tile's in-kernel pair: two splits, one slab per tile in ws (the caller's
-  // splits * M * Nv floats must cover it), no finalize launch
   // splits == 2 on a four-wave tile: the tiles past the last whole wave (all of them when
-  // there are at most 128) run as in-kernel k-half pairs, the rest whole
+  // there are at most 256) run as in-kernel k-half pairs, the rest whole; one slab per
+  // paired tile in ws (cake_gemm_ws_floats), no finalize launch
   const int ntiles = g.tiles_m * g.tiles_n;
-  const int npair = ntiles <= 256 ? ntiles : ntiles % 256;
-  if (four && splits == 2 && ws != nullptr && npair > 0 &&
-      npair <= 128 + (ntiles <= 256 ? 128 : 0) && ntiles <= kPairTiles &&
-      (long long)npair * bm * bn <= 2LL * M * g.Nv && pair_ticks()) {
+  const int npair = sp.npair;
+  if (npair > 0 && ws != nullptr) {
     g.pair = 1;
     g.tick = pair_ticks();
     g.dp_tiles = ntiles - npair;

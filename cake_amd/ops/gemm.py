@@ -61,6 +61,8 @@ def _lib():
         P, I, L = C.c_void_p, C.c_int, C.c_longlong
         lib.cake_gemm.argtypes = [I, I, I, I, P, L, P, L, P, L, P, P, L, P, P, I, I, I, P]
         lib.cake_gemm.restype = I
+        lib.cake_gemm_ws_floats.argtypes = [I, I, I, I, I, I]
+        lib.cake_gemm_ws_floats.restype = L
         lib.cake_blaslt_gemm.argtypes = [I, I, P, L, P, L, P, L, I, I, I, P, C.c_size_t, P]
         lib.cake_blaslt_gemm.restype = I
         _bound = True
@@ -285,7 +287,9 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, *
     if cfg == LIB:  # an epilogue / bias / strided output the library form does not carry
         cfg, s0 = plan_mfma(M, Nv, K, epi)
     splits = s0 if splits is None else max(1, int(splits))
-    ws = _workspace(x.device, splits * M * Nv) if splits > 1 else None
+    # the kernel library sizes it (an in-kernel pair needs its slabs only)
+    ws = _workspace(x.device, int(_lib().cake_gemm_ws_floats(
+        int(cfg), int(splits), M, N, K, 1 if Nv != N else 0))) if splits > 1 else None
     check(_lib().cake_gemm(_DT[x.dtype], EPI[epi], int(cfg), int(splits), x2.data_ptr(), lda,
                            w.data_ptr(), ldb, cptr, ldc,
                            None if bias is None else bias.data_ptr(), rptr, ldr,
