@@ -155,10 +155,13 @@ struct GemmPlanner {
     }
     struct T { int cfg, bm, bn, slots; double eff; };
     static const T tiles[] = {{0, 128, 128, 2, 1.0}, {1, 64, 128, 2, 0.8}, {4, 64, 64, 4, 0.7},
-                              {5, 256, 256, 1, 1.2}};
-    static const int small_c[] = {1, 4, 0}, big_c[] = {0, 1, 4, 5};
+                              {5, 256, 256, 1, 1.2}, {22, 256, 256, 1, 1.3}};
+    static const int small_c[] = {1, 4, 0}, big_c[] = {0, 1, 4, 5, 22};
     const int* cands = M <= 64 ? small_c : big_c;
-    const int nc = M <= 64 ? 3 : 4;
+    // the four-wave 256x256 tile (cfg 22) where it can run: whole 64-element k steps,
+    // operands under 2 GB (ops/gemm.py _cost_plan); unsplit
+    const bool four = M > 64 && K % 64 == 0 && M * K * 2 < (1LL << 31) && Nv * K * 2 < (1LL << 31);
+    const int nc = M <= 64 ? 3 : (four ? 5 : 4);
     const long long ksteps = (K + 63) / 64;
     double best = -1;
     std::pair<int, int> out{0, 1};
@@ -168,7 +171,9 @@ struct GemmPlanner {
         if (x.cfg == cands[c]) t = &x;
       const long long tiles_n = ((M + t->bm - 1) / t->bm) * ((Nv + t->bn - 1) / t->bn);
       for (int splits : {1, 2, 4, 8, 16}) {
-        if (splits > 1 && (ksteps / splits < 4 || tiles_n * splits > 2LL * 256 * t->slots)) continue;
+        if (splits > 1 && (t->cfg == 22 || ksteps / splits < 4 ||
+                           tiles_n * splits > 2LL * 256 * t->slots))
+          continue;
         const long long waves = (tiles_n * splits + 256LL * t->slots - 1) / (256LL * t->slots);
         double cost = (double)waves * t->slots * t->bm * t->bn * (double)((ksteps + splits - 1) / splits) / t->eff;
         if (splits > 1) cost += (double)M * Nv * splits * 0.1;

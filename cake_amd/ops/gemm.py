@@ -170,11 +170,17 @@ def _cost_plan(M: int, Nv: int, K: int) -> tuple[int, int]:
     best = None
     ksteps = -(-K // 64)
     cands = (1, 4, 0) if M <= 64 else (0, 1, 4, 5)
+    # the four-wave 256x256 tile where it can run (whole 64-element k steps, operands under
+    # 2 GB); unsplit (its split-2 form is the shape-specific remainder pair)
+    four = M > 64 and K % 64 == 0 and M * K * 2 < 2 ** 31 and Nv * K * 2 < 2 ** 31
+    if four:
+        cands = cands + (22,)
     for cfg in cands:
         bm, bn = CFG_TILES[cfg]
         tiles = -(-M // bm) * -(-Nv // bn)
         for splits in (1, 2, 4, 8, 16):
-            if splits > 1 and (ksteps // splits < 4 or tiles * splits > 2 * NUM_CUS * _SLOTS[cfg]):
+            if splits > 1 and (cfg == 22 or ksteps // splits < 4 or
+                               tiles * splits > 2 * NUM_CUS * _SLOTS[cfg]):
                 continue
             waves = -(-tiles * splits // (NUM_CUS * _SLOTS[cfg]))
             cost = waves * _SLOTS[cfg] * bm * bn * (-(-ksteps // splits)) / _EFF[cfg]
