@@ -1206,7 +1206,7 @@ class Llama {
   }
 
   // hipBLASLt's first call in a process costs ~175 ms (library init; a new shape after it
-  // ~0.3 ms: scripts/gpu_r5_ax.sh): paid here at open, not by the first request's TTFT
+  // ~0.3 ms: scripts/gpu_runs/gpu_r5_ax.sh): paid here at open, not by the first request's TTFT
   void warm_library() {
     if (!planner_.has_lib()) return;
     if (!lib_ws_) lib_ws_ = dalloc<uint8_t>(kLibWsBytes);

@@ -1,6 +1,6 @@
 """Stall classes and LDS conflicts per kernel from one rocprofv3 --pmc pass:
 SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS
-SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES (scripts/gpu_sdpmc2.sh).
+SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES (scripts/gpu_runs/gpu_sdpmc2.sh).
 
     python scripts/prof_pmc_stalls.py COUNTERS.csv --last N [--title ...]
 
